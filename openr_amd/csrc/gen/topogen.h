@@ -1,0 +1,320 @@
+// topogen.h — deterministic synthetic LSDB generators (grid / fabric / WAN).
+//
+// Input generation only: no route computation lives here. Both the product
+// bindings (openr_amd/_decision) and the CPU oracle harness (oracle/_refcpu)
+// include this header so that the same seeded workloads feed both sides.
+//
+// Wiring follows the reference benchmark generators
+// (openr/decision/tests/RoutingBenchmarkUtils.cpp):
+//   grid   : createGrid / createGridAdjacencys / createAdjacencyEntry
+//            (RoutingBenchmarkUtils.cpp:131-291)
+//   fabric : createFabric + createSsws/Fsws/RswsAdjacencies + getId/getNodeName
+//            (RoutingBenchmarkUtils.cpp:15-30, 150-182, 298-473)
+// The reference draws prefixes from folly::Random::secureRandom
+// (openr/tests/mocks/PrefixGenerator.cpp:19), which is not reproducible; a
+// seeded splitmix64 stream replaces it (SURVEY.md §0 finding 5b).
+#pragma once
+
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <numeric>
+#include <string>
+#include <vector>
+
+namespace topogen {
+
+struct Adj {
+  std::string otherNodeName, ifName, otherIfName, nextHopV6, nextHopV4;
+  int32_t metric{1};
+  int32_t adjLabel{0};
+  bool isOverloaded{false};
+  int64_t weight{1};
+};
+
+struct AdjDb {
+  std::string thisNodeName;
+  bool isOverloaded{false};
+  int32_t nodeLabel{0};
+  int32_t nodeMetricIncrementVal{0};
+  std::vector<Adj> adjs;
+};
+
+struct Prefix {  // one advertisement (node, prefix) with PrefixMetrics
+  std::string node;
+  std::string prefix;
+  int32_t path_preference{0}, source_preference{0}, distance{0};
+};
+
+struct Lsdb {
+  std::string area{"test_area_name"};
+  std::vector<AdjDb> adjDbs;
+  std::vector<Prefix> prefixes;
+};
+
+inline uint64_t splitmix64(uint64_t& s) {
+  uint64_t z = (s += 0x9E3779B97F4A7C15ull);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+inline std::string hex2(unsigned v) {  // fmt "{:02x}"
+  char b[16];
+  std::snprintf(b, sizeof(b), "%02x", v);
+  return b;
+}
+
+// seeded replacement for PrefixGenerator::ipv6PrefixGenerator(n, 128)
+inline std::string seededV6Prefix(uint64_t& s) {
+  uint64_t a = splitmix64(s), b = splitmix64(s);
+  char buf[64];
+  std::snprintf(buf, sizeof(buf), "fc00:%x:%x:%x:%x:%x:%x:%x/128",
+                unsigned(a & 0xffff), unsigned((a >> 16) & 0xffff),
+                unsigned((a >> 32) & 0xffff), unsigned((a >> 48) & 0xffff),
+                unsigned(b & 0xffff), unsigned((b >> 16) & 0xffff),
+                unsigned((b >> 32) & 0xffff));
+  return buf;
+}
+
+// ---------------------------------------------------------------- grid ----
+// One adjacency toward grid node `nbr` (createAdjacencyEntry): address and
+// label describe the NEIGHBOR; metric 1 unless a metric stream is supplied.
+inline Adj gridAdj(uint32_t self, uint32_t nbr) {
+  Adj a;
+  a.otherNodeName = std::to_string(nbr);
+  a.ifName = "if_" + std::to_string(self) + "_" + std::to_string(nbr);
+  a.otherIfName = "if_" + std::to_string(nbr) + "_" + std::to_string(self);
+  a.nextHopV6 = "fe80:" + hex2(nbr >> 16) + "::" + hex2(nbr & 0xffff);
+  a.nextHopV4 = "10." + std::to_string(nbr >> 16) + "." +
+      std::to_string((nbr >> 8) & 0xff) + "." + std::to_string(nbr & 0xff);
+  a.metric = 1;
+  a.adjLabel = 100001 + int32_t(nbr);
+  return a;
+}
+
+struct GridOpts {
+  int n{10};
+  int prefixesPerNode{1};
+  uint64_t prefixSeed{0xC1};
+  // metricSeed != 0: per-direction metric U[1, metricMax] (config C2)
+  uint64_t metricSeed{0};
+  int metricMax{100};
+  // parity variant: fraction (per mille) of overloaded adjacencies / nodes
+  int adjOverloadPermille{0};
+  int nodeOverloadPermille{0};
+  uint64_t overloadSeed{0};
+};
+
+inline Lsdb grid(const GridOpts& o) {
+  Lsdb db;
+  const int n = o.n;
+  uint64_t ps = o.prefixSeed, ms = o.metricSeed, os = o.overloadSeed;
+  for (int row = 0; row < n; ++row) {
+    for (int col = 0; col < n; ++col) {
+      const uint32_t id = row * n + col;
+      AdjDb d;
+      d.thisNodeName = std::to_string(id);
+      d.nodeLabel = int32_t(id) + 1;
+      // createGridAdjacencys order: col+1, col-1, row-1, row+1
+      const int nb[4][2] = {{row, col + 1}, {row, col - 1}, {row - 1, col},
+                            {row + 1, col}};
+      for (auto& rc : nb) {
+        if (rc[0] < 0 || rc[0] >= n || rc[1] < 0 || rc[1] >= n) continue;
+        Adj a = gridAdj(id, rc[0] * n + rc[1]);
+        if (o.metricSeed) a.metric = 1 + int32_t(splitmix64(ms) % o.metricMax);
+        if (o.adjOverloadPermille &&
+            int(splitmix64(os) % 1000) < o.adjOverloadPermille) {
+          a.isOverloaded = true;
+        }
+        d.adjs.push_back(a);
+      }
+      if (o.nodeOverloadPermille &&
+          int(splitmix64(os) % 1000) < o.nodeOverloadPermille) {
+        d.isOverloaded = true;
+      }
+      db.adjDbs.push_back(std::move(d));
+      for (int k = 0; k < o.prefixesPerNode; ++k) {
+        db.prefixes.push_back({std::to_string(id), seededV6Prefix(ps)});
+      }
+    }
+  }
+  return db;
+}
+
+// -------------------------------------------------------------- fabric ----
+constexpr int kSswMarker = 1, kFswMarker = 2, kRswMarker = 3;
+
+inline std::string fabricName(int marker, int pod, int sw) {
+  return std::to_string(marker) + "-" + std::to_string(pod) + "-" +
+      std::to_string(sw);
+}
+
+inline Adj fabricAdj(const std::string& self, int marker, int pod, int sw) {
+  Adj a;
+  a.otherNodeName = fabricName(marker, pod, sw);
+  a.ifName = "if_" + self + "_" + a.otherNodeName;
+  a.otherIfName = "if_" + a.otherNodeName + "_" + self;
+  a.nextHopV6 = "fe80:" + hex2(marker) + ":" + hex2(pod) + "::" + hex2(sw);
+  a.nextHopV4 = std::to_string(marker) + "." + std::to_string(pod >> 8) + "." +
+      std::to_string(pod & 0xff) + "." + std::to_string(sw);
+  a.metric = 1;
+  a.adjLabel = marker * 100000 + pod * 100 + sw;  // getId
+  return a;
+}
+
+struct FabricOpts {
+  int pods{32}, planes{8}, sswPerPlane{36}, rswPerPod{48};
+  // full=true: every SSW advertises its plane FSW in EVERY pod (C3-full).
+  // full=false: the reference quirk -- the per-pod map::emplace keeps only
+  // the pod-0 adjacency (RoutingBenchmarkUtils.cpp:316-327, C3-ref).
+  bool full{true};
+  int prefixesPerNode{1};
+  uint64_t prefixSeed{0xC3};
+};
+
+inline Lsdb fabric(const FabricOpts& o) {
+  Lsdb db;
+  uint64_t ps = o.prefixSeed;
+  auto addPrefixes = [&](const std::string& node) {
+    for (int k = 0; k < o.prefixesPerNode; ++k) {
+      db.prefixes.push_back({node, seededV6Prefix(ps)});
+    }
+  };
+  const int fswPerPod = o.planes;
+  for (int plane = 0; plane < o.planes; ++plane) {
+    for (int s = 0; s < o.sswPerPlane; ++s) {
+      AdjDb d;
+      d.thisNodeName = fabricName(kSswMarker, plane, s);
+      d.nodeLabel = 1;  // createAdjValue(nodeName, 1, ...)
+      const int podsLinked = o.full ? o.pods : std::min(1, o.pods);
+      for (int pod = 0; pod < podsLinked; ++pod) {
+        d.adjs.push_back(fabricAdj(d.thisNodeName, kFswMarker, pod, plane));
+      }
+      addPrefixes(d.thisNodeName);
+      db.adjDbs.push_back(std::move(d));
+    }
+  }
+  for (int pod = 0; pod < o.pods; ++pod) {
+    for (int f = 0; f < fswPerPod; ++f) {
+      AdjDb d;
+      d.thisNodeName = fabricName(kFswMarker, pod, f);
+      d.nodeLabel = 1;
+      for (int s = 0; s < o.sswPerPlane; ++s) {
+        d.adjs.push_back(fabricAdj(d.thisNodeName, kSswMarker, f, s));
+      }
+      for (int r = 0; r < o.rswPerPod; ++r) {
+        d.adjs.push_back(fabricAdj(d.thisNodeName, kRswMarker, pod, r));
+      }
+      addPrefixes(d.thisNodeName);
+      db.adjDbs.push_back(std::move(d));
+    }
+  }
+  for (int pod = 0; pod < o.pods; ++pod) {
+    for (int r = 0; r < o.rswPerPod; ++r) {
+      AdjDb d;
+      d.thisNodeName = fabricName(kRswMarker, pod, r);
+      d.nodeLabel = 1;
+      for (int f = 0; f < fswPerPod; ++f) {
+        d.adjs.push_back(fabricAdj(d.thisNodeName, kFswMarker, pod, f));
+      }
+      addPrefixes(d.thisNodeName);
+      db.adjDbs.push_back(std::move(d));
+    }
+  }
+  return db;
+}
+
+// ----------------------------------------------------------------- WAN ----
+// Build-defined WAN: seeded points in the unit square,
+// Euclidean MST (Prim) ∪ k-nearest neighbours; per-direction metric
+// max(1, round(1000 d)) + U[0, 10].
+struct WanOpts {
+  int nodes{2000};
+  int k{3};
+  uint64_t seed{0xC4};
+  int prefixesPerNode{1};
+  std::string namePrefix{""};
+};
+
+inline Lsdb wan(const WanOpts& o) {
+  Lsdb db;
+  const int N = o.nodes;
+  uint64_t s = o.seed;
+  std::vector<double> x(N), y(N);
+  for (int i = 0; i < N; ++i) {
+    x[i] = double(splitmix64(s) >> 11) * 0x1.0p-53;
+    y[i] = double(splitmix64(s) >> 11) * 0x1.0p-53;
+  }
+  auto dist = [&](int a, int b) {
+    return std::sqrt((x[a] - x[b]) * (x[a] - x[b]) +
+                     (y[a] - y[b]) * (y[a] - y[b]));
+  };
+  std::vector<std::vector<int>> nbrs(N);
+  auto addEdge = [&](int a, int b) {
+    if (a == b) return;
+    if (std::find(nbrs[a].begin(), nbrs[a].end(), b) != nbrs[a].end()) return;
+    nbrs[a].push_back(b);
+    nbrs[b].push_back(a);
+  };
+  {  // Prim MST, O(N^2)
+    std::vector<double> best(N, 1e300);
+    std::vector<int> from(N, -1);
+    std::vector<char> in(N, 0);
+    best[0] = 0;
+    for (int it = 0; it < N; ++it) {
+      int u = -1;
+      for (int v = 0; v < N; ++v) {
+        if (!in[v] && (u < 0 || best[v] < best[u])) u = v;
+      }
+      in[u] = 1;
+      if (from[u] >= 0) addEdge(u, from[u]);
+      for (int v = 0; v < N; ++v) {
+        if (!in[v] && dist(u, v) < best[v]) {
+          best[v] = dist(u, v);
+          from[v] = u;
+        }
+      }
+    }
+  }
+  {  // k nearest neighbours
+    std::vector<int> idx(N);
+    for (int a = 0; a < N; ++a) {
+      std::iota(idx.begin(), idx.end(), 0);
+      const int kk = std::min(o.k + 1, N);
+      std::partial_sort(idx.begin(), idx.begin() + kk, idx.end(),
+                        [&](int p, int q) { return dist(a, p) < dist(a, q); });
+      for (int j = 0; j < kk; ++j) addEdge(a, idx[j]);
+    }
+  }
+  uint64_t ps = o.seed ^ 0x5eed;
+  uint64_t ms = o.seed ^ 0xfeed;
+  auto name = [&](int i) { return o.namePrefix + std::to_string(i); };
+  for (int a = 0; a < N; ++a) {
+    AdjDb d;
+    d.thisNodeName = name(a);
+    d.nodeLabel = a + 1;
+    std::sort(nbrs[a].begin(), nbrs[a].end());
+    for (int b : nbrs[a]) {
+      Adj ad;
+      ad.otherNodeName = name(b);
+      ad.ifName = "if_" + std::to_string(a) + "_" + std::to_string(b);
+      ad.otherIfName = "if_" + std::to_string(b) + "_" + std::to_string(a);
+      ad.nextHopV6 = "fe80::" + hex2(b >> 8) + hex2(b & 0xff);
+      ad.nextHopV4 = "10.0." + std::to_string(b >> 8) + "." +
+          std::to_string(b & 0xff);
+      ad.metric = std::max(1, int(std::lround(1000.0 * dist(a, b)))) +
+          int(splitmix64(ms) % 11);
+      ad.adjLabel = 100001 + b;
+      d.adjs.push_back(ad);
+    }
+    db.adjDbs.push_back(std::move(d));
+    for (int k = 0; k < o.prefixesPerNode; ++k) {
+      db.prefixes.push_back({name(a), seededV6Prefix(ps)});
+    }
+  }
+  return db;
+}
+
+}  // namespace topogen

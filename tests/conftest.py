@@ -1,0 +1,28 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (ROOT, os.path.join(ROOT, "tests"), os.path.join(ROOT, "oracle")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP device)")
+
+
+@pytest.fixture(scope="session")
+def oracle():
+    """CPU oracle (test infrastructure only)."""
+    import _refcpu
+    return _refcpu
+
+
+@pytest.fixture(scope="session")
+def product():
+    """The GPU product module; fails loudly if the HIP path is unavailable."""
+    import openr_amd
+    openr_amd.require_gpu()
+    return openr_amd.decision
