@@ -1,0 +1,38 @@
+# Builds the MI355X (gfx950) engine in-tree:
+#   openr_amd/lib/libopenr_gpu.so      HIP kernels + C-ABI (include/openr_gpu.h)
+#   openr_amd/_decision*.so            C++ drop-in (LinkState/SpfSolver/...) +
+#                                      pybind11 binding, linked to the above
+#   oracle/_refcpu*.so                 CPU oracle (test infrastructure only)
+HIPCC ?= /opt/rocm/bin/hipcc
+CXX ?= g++
+ARCH ?= gfx950
+PY_INC := $(shell python3 -c "import sysconfig;print(sysconfig.get_paths()['include'])")
+PYBIND_INC := $(shell python3 -c "import pybind11;print(pybind11.get_include())")
+EXT := $(shell python3 -c "import sysconfig;print(sysconfig.get_config_var('EXT_SUFFIX'))")
+
+LIB := openr_amd/lib/libopenr_gpu.so
+MOD := openr_amd/_decision$(EXT)
+KERNELS := $(wildcard openr_amd/csrc/kernels/*.hip)
+HOST := $(wildcard openr_amd/csrc/host/*.cpp)
+HOST_H := $(wildcard openr_amd/csrc/host/*.h) include/openr_gpu.h openr_amd/csrc/gen/topogen.h
+
+all: $(LIB) $(MOD) oracle
+
+$(LIB): $(KERNELS) include/openr_gpu.h
+	@mkdir -p openr_amd/lib
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -shared -Iinclude $(KERNELS) -o $@
+
+$(MOD): $(HOST) $(HOST_H) openr_amd/csrc/py/bindings.cpp $(LIB)
+	$(CXX) -O2 -std=c++17 -fPIC -shared -Wall -Wno-unused-function \
+	  -Iinclude -Iopenr_amd/csrc/host -I$(PY_INC) -I$(PYBIND_INC) \
+	  $(HOST) openr_amd/csrc/py/bindings.cpp -o $@ \
+	  -Lopenr_amd/lib -lopenr_gpu -Wl,-rpath,'$$ORIGIN/lib'
+
+oracle:
+	$(MAKE) -C oracle
+
+clean:
+	rm -f $(LIB) $(MOD)
+	$(MAKE) -C oracle clean
+
+.PHONY: all oracle clean

@@ -1,0 +1,224 @@
+#!/usr/bin/env python3
+"""bench.py — SPF+RouteDb builds/s on MI355X (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1], config C2): a batch of 4096 random-metric
+10x10 grid topologies (reference grid wiring, RoutingBenchmarkUtils.cpp:
+209-291; per-direction metric U[1,100] seeded 0xC2000000+i, one seeded /128
+prefix per node), ECMP SPF from node "1" + full RouteDb for every topology.
+One "step" = one launch of the fused SPF+RouteDb kernel over the whole
+batch; one "build" = one (topology, source) SPF + RouteDb. Inputs are
+HBM-resident (torch-owned device buffers) before timing starts.
+
+Multi-GPU (--gpus N via torch.distributed.run): weak scaling, each rank owns
+its own 4096-topology shard (topology indices rank*4096 ...), no data-path
+collective; RCCL only all-gathers per-rank digests/counts and max-reduces
+the elapsed time.
+"""
+import argparse
+import ctypes
+import hashlib
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+TOPOS_PER_GPU = 4096
+GRID_N = 10
+METRIC_SEED = 0xC2000000
+PREFIX_SEED = 0xC1
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def algorithmic_bytes_per_unit(N, E, T, P, W, Wl, S=1):
+    """bytes_inputs/S + 4N + 4*W*N + P*(4*Wl + 8),
+    bytes_inputs = 4(N+1) + 8E + ceil(N/8) + 16T."""
+    inputs = 4 * (N + 1) + 8 * E + (N + 7) // 8 + 16 * T
+    return inputs / S + 4 * N + 4 * W * N + P * (4 * Wl + 8)
+
+
+def cpu_baseline(units, reps=3):
+    """The oracle (refcpu, a faithful port of LinkState/SpfSolver) timed on
+    this host's cores over the same workload; ingestion excluded."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import _refcpu
+    threads = max(1, min(16, os.cpu_count() or 1))  # the box's CPU share
+    opts = dict(n=GRID_N, metricSeed=METRIC_SEED, prefixSeed=PREFIX_SEED)
+    rates = []
+    for _ in range(reps):
+        secs, n, routes = _refcpu.cpu_baseline_grid_batch(opts, units, threads, "1")
+        rates.append(n / secs)
+    rates.sort()
+    return {"value": round(rates[len(rates) // 2], 1), "unit": "builds/s",
+            "cores": threads, "kind": "port",
+            "sample": f"{units} C2 topologies x {reps} reps (median), "
+                      f"refcpu buildRouteDb('1'), {threads} threads, ingestion excluded"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--topos", type=int, default=TOPOS_PER_GPU)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    import openr_amd
+    import openr_amd.capi as capi
+    openr_amd.require_gpu()
+    M = openr_amd.decision
+    lib = capi.load()
+    lib.ogs_set_device(local_rank)
+
+    # ---- build this rank's shard on the host (outside the timed region) ----
+    T = args.topos
+    lo = rank * T
+    br = M.BatchRunner(True, False, False)
+    br.add_grid_batch(dict(n=GRID_N, metricSeed=METRIC_SEED, prefixSeed=PREFIX_SEED),
+                      lo, lo + T, "1")
+    h = br.host_arrays()
+    dev = torch.device("cuda", local_rank)
+
+    def up(key, dtype):
+        return torch.from_numpy(h[key].view(dtype)).to(dev)
+
+    node_base = up("node_base", "int32")
+    row_ptr = up("row_ptr", "int32")
+    edges = up("edges", "int64")
+    node_flags = up("node_flags", "uint8")
+    pfx_base = up("pfx_base", "int32")
+    adv_off = up("adv_off", "int32")
+    adv_node = up("adv_node", "int32")
+    adv_metrics = up("adv_metrics", "int32")
+    adv_min_nh = up("adv_min_nh", "int64")
+    pfx_flags = up("pfx_flags", "uint8")
+    units = up("units", "int32")
+    U = len(h["units"]) // 2
+    Sn, Sp, W = h["max_nodes"], h["max_prefixes"], h["nh_words"]
+    flags = h["flags"]
+    assert not (flags & capi.OGS_F_WIDE_METRIC)
+    o_dist = torch.empty(U * Sn, dtype=torch.int32, device=dev)
+    o_nh = torch.empty(U * W * Sn, dtype=torch.int32, device=dev)
+    o_meta = torch.empty(U * Sp, dtype=torch.int32, device=dev)
+    o_metric = torch.empty(U * Sp, dtype=torch.int32, device=dev)
+    o_mask = torch.empty(U * W * Sp, dtype=torch.int32, device=dev)
+    o_sel = torch.empty(U * Sp, dtype=torch.int32, device=dev)
+
+    g = capi.Graph(h["num_topos"], Sn, h["max_edges"], node_base.data_ptr(),
+                   row_ptr.data_ptr(), edges.data_ptr(), node_flags.data_ptr())
+    pt = capi.PrefixTable(Sp, pfx_base.data_ptr(), adv_off.data_ptr(),
+                          adv_node.data_ptr(), adv_metrics.data_ptr(),
+                          adv_min_nh.data_ptr(), pfx_flags.data_ptr())
+    out = capi.SpfOut(o_dist.data_ptr(), o_nh.data_ptr(), o_meta.data_ptr(),
+                      o_metric.data_ptr(), o_mask.data_ptr(), o_sel.data_ptr())
+    stream = torch.cuda.current_stream(dev)
+    sptr = ctypes.c_void_p(stream.cuda_stream)
+    gref, pref, oref = ctypes.byref(g), ctypes.byref(pt), ctypes.byref(out)
+
+    def step():
+        rc = lib.ogs_spf_routes(gref, pref, ctypes.c_void_p(units.data_ptr()),
+                                U, flags, W, oref, sptr)
+        if rc != 0:
+            capi.check(lib, rc, "ogs_spf_routes")
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        step()
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t0
+    kernel_ms = ev0.elapsed_time(ev1) / args.steps  # one launch per step
+
+    # ---- per-rank digest (result sanity) + cross-rank reduction -----------
+    meta = o_meta.cpu().numpy()
+    n_routes = int(((meta & 1) != 0).sum())
+    digest = hashlib.sha256(o_meta.cpu().numpy().tobytes() +
+                            o_metric.cpu().numpy().tobytes() +
+                            o_mask.cpu().numpy().tobytes()).digest()[:8]
+    local = torch.tensor([U, n_routes, int.from_bytes(digest, "little") >> 1, 0],
+                         dtype=torch.int64, device=dev)
+    elapsed = torch.tensor([wall], dtype=torch.float64, device=dev)
+    if dist:
+        gathered = [torch.zeros_like(local) for _ in range(world)]
+        dist.all_gather(gathered, local)
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+        total_units = int(sum(int(x[0]) for x in gathered))
+        total_routes = int(sum(int(x[1]) for x in gathered))
+    else:
+        total_units, total_routes = U, n_routes
+    tmax = float(elapsed.item())
+
+    if rank == 0:
+        N, E, P = GRID_N * GRID_N, 4 * GRID_N * (GRID_N - 1), GRID_N * GRID_N
+        bpu = algorithmic_bytes_per_unit(N, E, P, P, W, W)
+        achieved = bpu * U / (kernel_ms * 1e-3) / 1e9
+        value = total_units * args.steps / tmax
+        line = {
+            "metric": "SPF+RouteDb builds/sec (whole node)",
+            "value": round(value, 1),
+            "unit": "builds/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(tmax / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic",
+            "config": {
+                "workload": "C2: batch of 4096 random-metric (U[1,100]) 10x10 grid "
+                            "topologies per GPU, ECMP SPF from node '1' + RouteDb "
+                            "(100 prefixes/topology)",
+                "topologies_per_gpu": U,
+                "nodes": N, "directed_edges": E, "prefixes_per_topology": P,
+                "source": "1",
+                "parallelism": f"shard-by-topology x{world}",
+            },
+            "gteps": round(E * value / 1e9, 3),
+            "kernel_ms": round(kernel_ms, 5),
+            "routes_per_step": total_routes,
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": None,
+                "bytes_alg_per_unit": round(bpu, 1),
+            },
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(U)
+        print(json.dumps(line), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,178 @@
+/*
+ * openr_gpu.h — C-ABI of the MI355X (gfx950) SPF + RouteDb engine for Open/R
+ * Decision. This is the drop-in boundary: plain pointers and sizes, int
+ * status codes, no exceptions and no C++/torch types across the ABI.
+ *
+ * The reference has no FFI for this path; its C++ API is
+ *   LinkState::getSpfResult   (openr/decision/LinkState.h:358-359,
+ *                              LinkState.cpp:705-820)
+ *   LinkState::getKthPaths    (LinkState.h:383-384, LinkState.cpp:674-703)
+ *   SpfSolver::buildRouteDb   (openr/decision/SpfSolver.h:136-139,
+ *                              SpfSolver.cpp:160-453)
+ *   RibPolicy::applyPolicy    (openr/decision/RibPolicy.cpp:231-249)
+ *   DecisionRouteDb::calculateUpdate (SpfSolver.cpp:21-56)
+ * The C++ adapter in openr_amd/csrc/host keeps exactly those signatures and
+ * calls the entry points below; INTEGRATION.md shows the binding.
+ *
+ * Data layout (all arrays DEVICE-resident unless stated):
+ *   A "graph batch" holds T independent topologies in one CSR. Node ids are
+ *   local to their topology and equal the rank of the node name in byte-wise
+ *   sorted order, so id order == the reference's name tie-break order.
+ *   Each directed edge is one uint64:
+ *     bits  0..20  dst   local node id of the neighbour
+ *     bit  21      DST_OVERLOADED  neighbour is hard-drained: it is settled
+ *                  but never relaxes (LinkState.cpp:741-752) unless it is
+ *                  the SPF source itself
+ *     bits 22..30  rslot index of the reverse edge inside dst's CSR row
+ *     bit  31      DOWN  link not up (Link::isUp false, LinkState.h:118-121)
+ *     bits 32..63  metric (Link::getMaxMetric, LinkState.h:171-174)
+ *   Node flags (uint8): OGS_NODE_OVERLOADED (hard drain, no transit,
+ *   LinkState.cpp:741-752), OGS_NODE_SOFTDRAIN (int(metricInc) > 0,
+ *   SpfSolver.cpp:518-519), OGS_NODE_METRICINC (metricInc != 0,
+ *   SpfSolver.cpp:549-550).
+ *   Next-hop sets are bitsets over the SOURCE node's CSR row ("link slots"):
+ *   bit j of a node's set <=> the j-th link of the source is an ECMP first
+ *   hop toward it (the union rule of LinkState.cpp:795-811 composed with the
+ *   link filter of SpfSolver.cpp:705-743).
+ */
+#ifndef OPENR_GPU_H_
+#define OPENR_GPU_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ------------------------------------------------------ */
+#define OGS_OK 0
+#define OGS_E_INVALID (-1)     /* bad argument / inconsistent shapes         */
+#define OGS_E_NOMEM (-2)       /* device allocation failed                   */
+#define OGS_E_HIP (-3)         /* HIP runtime error, see ogs_last_error()    */
+#define OGS_E_UNSUPPORTED (-4) /* input outside the engine's exact domain:   */
+                               /* zero/negative metric, metric overflow,     */
+                               /* source degree > 256, ...                   */
+#define OGS_E_NODEVICE (-5)    /* no HIP device visible                      */
+
+/* ---- packed edge / node encodings -------------------------------------- */
+#define OGS_EDGE_DST_BITS 21
+#define OGS_EDGE_DST_MASK 0x1FFFFFu
+#define OGS_EDGE_DST_OVERLOADED (1u << 21)
+#define OGS_EDGE_RSLOT_SHIFT 22
+#define OGS_EDGE_RSLOT_MASK 0x1FFu
+#define OGS_EDGE_DOWN (1u << 31)
+#define OGS_MAX_NODES_PER_TOPO (1u << 21)
+#define OGS_MAX_DEGREE 512
+
+#define OGS_NODE_OVERLOADED 0x01u
+#define OGS_NODE_SOFTDRAIN 0x02u
+#define OGS_NODE_METRICINC 0x04u
+#define OGS_NODE_NONE 0xFFFFFFFFu /* advertiser with no adjacency database */
+
+/* ---- route record flags (ogs_route_out.meta) --------------------------- */
+#define OGS_ROUTE_VALID 0x01u       /* a unicast route exists              */
+#define OGS_ROUTE_DRAINED 0x02u     /* isBestNodeDrained -> drain_metric=1 */
+#define OGS_ROUTE_LOCAL 0x04u       /* localRouteConsidered                */
+#define OGS_ROUTE_SELECTED 0x08u    /* selection ran (bestRoutesCache set) */
+#define OGS_ROUTE_REASON_SHIFT 4    /* 4-bit reason when not VALID         */
+#define OGS_ROUTE_BEST_SHIFT 8      /* best advertiser index in segment    */
+#define OGS_REASON_NONE 0
+#define OGS_REASON_V4_DISABLED 1    /* SpfSolver.cpp:169-176 */
+#define OGS_REASON_UNREACHABLE 2    /* SpfSolver.cpp:217-223 */
+#define OGS_REASON_SELF 3           /* SpfSolver.cpp:253-258 */
+#define OGS_REASON_NO_NEXTHOP 4     /* SpfSolver.cpp:605-607 */
+#define OGS_REASON_MIN_NEXTHOP 5    /* SpfSolver.cpp:612-619 */
+
+/* ---- solver flags ------------------------------------------------------- */
+#define OGS_F_ENABLE_V4 0x01u          /* SpfSolver ctor enableV4          */
+#define OGS_F_V4_OVER_V6 0x02u         /* v4OverV6Nexthop                  */
+#define OGS_F_BEST_ROUTE_SELECTION 0x04u /* enableBestRouteSelection       */
+#define OGS_F_HOP_METRIC 0x08u         /* getSpfResult(useLinkMetric=false)*/
+#define OGS_F_WIDE_METRIC 0x10u        /* 64-bit distances (else 32-bit)   */
+
+/* CSR of T topologies. */
+typedef struct ogs_graph {
+  int32_t num_topos;
+  int32_t max_nodes;          /* max node count of any topology          */
+  int32_t max_edges;          /* max directed-edge count of any topology */
+  const uint32_t* node_base;  /* [T+1] first global node of topology t   */
+  const uint32_t* row_ptr;    /* [total_nodes+1] global edge offsets     */
+  const uint64_t* edges;      /* [E] packed as above                     */
+  const uint8_t* node_flags;  /* [total_nodes]                           */
+} ogs_graph;
+
+/* Prefix table: per topology a contiguous range of prefixes, each with a
+ * contiguous segment of advertisements (one (node, area) entry each). */
+typedef struct ogs_prefix_table {
+  int32_t max_prefixes;       /* max prefixes of any topology (P stride) */
+  const uint32_t* pfx_base;   /* [T+1] first global prefix of topology t */
+  const uint32_t* adv_off;    /* [P_total+1] advertiser segment offsets  */
+  const uint32_t* adv_node;   /* [A] local node id or OGS_NODE_NONE      */
+  const int32_t* adv_metrics; /* [A*4] drain_metric, path_preference,
+                                 source_preference, distance            */
+  const int64_t* adv_min_nh;  /* [A] minNexthop, INT64_MIN when unset    */
+  const uint8_t* pfx_flags;   /* [P_total] bit0: prefix is IPv4          */
+} ogs_prefix_table;
+
+/* One work unit = (topology, source node). */
+typedef struct ogs_unit {
+  uint32_t topo;
+  uint32_t src;
+} ogs_unit;
+
+/* Outputs (device). Any pointer may be NULL to skip that output. Layouts,
+ * with U = unit index, S_n = graph.max_nodes, S_p = prefixes.max_prefixes,
+ * W = nh_words:
+ *   dist   [U*S_n + v]            uint32 (uint64 with OGS_F_WIDE_METRIC);
+ *                                 all-ones = unreachable
+ *   nh     [(U*W + w)*S_n + v]    link-slot bitset of node v
+ *   meta   [U*S_p + p]            OGS_ROUTE_* flags | best << 8
+ *   metric [U*S_p + p]            shortest metric (dist width)
+ *   mask   [(U*W + w)*S_p + p]    next-hop link-slot bitset of the route
+ *   sel    [U*S_p + p]            selected-advertiser bitset (segments of
+ *                                 <= 32 entries; bestRoutesCache)        */
+typedef struct ogs_spf_out {
+  void* dist;
+  uint32_t* nh;
+  uint32_t* meta;
+  void* metric;
+  uint32_t* mask;
+  uint32_t* sel;
+} ogs_spf_out;
+
+/* ---- runtime ------------------------------------------------------------ */
+const char* ogs_version(void);
+const char* ogs_last_error(void); /* thread-local message of last failure */
+int ogs_device_count(int* count);
+int ogs_set_device(int device);
+int ogs_malloc(void** dptr, size_t bytes);
+int ogs_free(void* dptr);
+int ogs_memcpy_h2d(void* dst, const void* src, size_t bytes, void* stream);
+int ogs_memcpy_d2h(void* dst, const void* src, size_t bytes, void* stream);
+int ogs_memset(void* dst, int value, size_t bytes, void* stream);
+int ogs_stream_sync(void* stream);
+
+/* Smallest supported next-hop bitset width (words) for a source degree. */
+int ogs_nh_words_for_degree(int degree);
+
+/* ---- compute ------------------------------------------------------------ *
+ * Batched SPF (+ fused RouteDb when `prefixes` is non-NULL) for n_units
+ * (topology, source) units, launched asynchronously on `stream` (a
+ * hipStream_t; NULL = default stream). One wavefront per unit for small
+ * topologies, one workgroup per unit for large ones (chosen internally).
+ * 32-bit distances are exact only when max_metric * (max_nodes - 1) <
+ * 2^32 - 1; the caller sets OGS_F_WIDE_METRIC otherwise (the adapter does).
+ * Replaces: LinkState::runSpf/getSpfResult (LinkState.cpp:705-820) and the
+ * per-prefix loop of SpfSolver::buildRouteDb (SpfSolver.cpp:335-340,
+ * 160-311, 455-767), single area. */
+int ogs_spf_routes(const ogs_graph* graph, const ogs_prefix_table* prefixes,
+                   const ogs_unit* units /* device */, int32_t n_units,
+                   uint32_t flags, int32_t nh_words, ogs_spf_out* out,
+                   void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* OPENR_GPU_H_ */

@@ -1,0 +1,57 @@
+"""ctypes view of the C-ABI (include/openr_gpu.h) — what a Python consumer of
+the boundary binds. bench.py drives the kernel through it with torch-owned
+device memory and torch's current HIP stream."""
+import ctypes
+
+from . import LIB_PATH
+
+OGS_OK = 0
+OGS_F_ENABLE_V4 = 0x01
+OGS_F_V4_OVER_V6 = 0x02
+OGS_F_BEST_ROUTE_SELECTION = 0x04
+OGS_F_HOP_METRIC = 0x08
+OGS_F_WIDE_METRIC = 0x10
+
+# every extern "C" entry point declared in include/openr_gpu.h
+EXPORTS = [
+    "ogs_version", "ogs_last_error", "ogs_device_count", "ogs_set_device",
+    "ogs_malloc", "ogs_free", "ogs_memcpy_h2d", "ogs_memcpy_d2h", "ogs_memset",
+    "ogs_stream_sync", "ogs_nh_words_for_degree", "ogs_spf_routes",
+]
+
+
+class Graph(ctypes.Structure):
+    _fields_ = [("num_topos", ctypes.c_int32), ("max_nodes", ctypes.c_int32),
+                ("max_edges", ctypes.c_int32), ("node_base", ctypes.c_void_p),
+                ("row_ptr", ctypes.c_void_p), ("edges", ctypes.c_void_p),
+                ("node_flags", ctypes.c_void_p)]
+
+
+class PrefixTable(ctypes.Structure):
+    _fields_ = [("max_prefixes", ctypes.c_int32), ("pfx_base", ctypes.c_void_p),
+                ("adv_off", ctypes.c_void_p), ("adv_node", ctypes.c_void_p),
+                ("adv_metrics", ctypes.c_void_p), ("adv_min_nh", ctypes.c_void_p),
+                ("pfx_flags", ctypes.c_void_p)]
+
+
+class SpfOut(ctypes.Structure):
+    _fields_ = [("dist", ctypes.c_void_p), ("nh", ctypes.c_void_p),
+                ("meta", ctypes.c_void_p), ("metric", ctypes.c_void_p),
+                ("mask", ctypes.c_void_p), ("sel", ctypes.c_void_p)]
+
+
+def load():
+    lib = ctypes.CDLL(LIB_PATH)
+    lib.ogs_version.restype = ctypes.c_char_p
+    lib.ogs_last_error.restype = ctypes.c_char_p
+    lib.ogs_spf_routes.argtypes = [
+        ctypes.POINTER(Graph), ctypes.POINTER(PrefixTable), ctypes.c_void_p,
+        ctypes.c_int32, ctypes.c_uint32, ctypes.c_int32, ctypes.POINTER(SpfOut),
+        ctypes.c_void_p]
+    lib.ogs_spf_routes.restype = ctypes.c_int
+    return lib
+
+
+def check(lib, rc, what):
+    if rc != OGS_OK:
+        raise RuntimeError(f"{what} failed ({rc}): {lib.ogs_last_error().decode()}")

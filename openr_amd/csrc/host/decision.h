@@ -1,0 +1,496 @@
+// decision.h — MI355X drop-in for Open/R Decision's route computation.
+//
+// Same classes and method signatures as the reference (openr/decision):
+//   Link / LinkState        LinkState.h:64-583
+//   PrefixState             PrefixState.h:18-57
+//   SpfSolver               SpfSolver.h:112-277
+//   DecisionRouteDb         SpfSolver.h:68-109
+//   RibUnicastEntry / RibMplsEntry   RibEntry.h:22-196
+//   RibPolicy               RibPolicy.h:70-124
+// with plain structs in place of the thrift types. All SPF and route
+// computation runs on the GPU through the C-ABI in include/openr_gpu.h; this
+// layer owns ingestion (link formation and change detection, which define
+// LinkStateChange), flattening to the HBM CSR, and materialisation of the
+// compact GPU results back into API objects. There is no CPU route path: a
+// missing device or an input outside the GPU engine's domain throws.
+#pragma once
+
+#include <cstdint>
+#include <limits>
+#include <map>
+#include <memory>
+#include <optional>
+#include <set>
+#include <stdexcept>
+#include <string>
+#include <tuple>
+#include <unordered_map>
+#include <vector>
+
+#include "device.h"
+
+namespace openr_amd {
+
+using LinkStateMetric = uint64_t;  // LinkState.h:16
+
+enum MplsActionCode : int32_t {
+  PUSH = 0,
+  SWAP = 1,
+  PHP = 2,
+  POP_AND_LOOKUP = 3,
+  NOOP = 4
+};
+
+struct MplsAction {
+  int32_t action{SWAP};
+  std::optional<int32_t> swapLabel;
+  std::optional<std::vector<int32_t>> pushLabels;
+  auto tie() const { return std::tie(action, swapLabel, pushLabels); }
+  bool operator==(const MplsAction& o) const { return tie() == o.tie(); }
+  bool operator<(const MplsAction& o) const { return tie() < o.tie(); }
+};
+
+struct NextHopThrift {  // Network.thrift:61-92
+  std::string address;
+  std::optional<std::string> ifName;
+  int32_t weight{0};
+  std::optional<MplsAction> mplsAction;
+  int32_t metric{0};
+  std::optional<std::string> area;
+  std::optional<std::string> neighborNodeName;
+  auto tie() const {
+    return std::tie(address, ifName, weight, mplsAction, metric, area,
+                    neighborNodeName);
+  }
+  bool operator==(const NextHopThrift& o) const { return tie() == o.tie(); }
+  bool operator<(const NextHopThrift& o) const { return tie() < o.tie(); }
+};
+using NextHops = std::set<NextHopThrift>;
+
+struct Adjacency {  // Types.thrift:145-215
+  std::string otherNodeName, ifName, nextHopV6, nextHopV4;
+  int32_t metric{0};
+  int32_t adjLabel{0};
+  bool isOverloaded{false};
+  int32_t rtt{0};
+  int64_t timestamp{0};
+  int64_t weight{1};
+  std::string otherIfName;
+  bool adjOnlyUsedByOtherNode{false};
+};
+
+struct AdjacencyDatabase {  // Types.thrift:223-270
+  std::string thisNodeName;
+  bool isOverloaded{false};
+  std::vector<Adjacency> adjacencies;
+  int32_t nodeLabel{0};
+  std::string area;
+  int32_t nodeMetricIncrementVal{0};
+};
+
+struct PrefixMetrics {
+  int32_t version{1}, drain_metric{0}, path_preference{0},
+      source_preference{0}, distance{0};
+  auto tie() const {
+    return std::tie(version, drain_metric, path_preference, source_preference,
+                    distance);
+  }
+  bool operator==(const PrefixMetrics& o) const { return tie() == o.tie(); }
+};
+
+struct PrefixEntry {  // Types.thrift:349-408
+  std::string prefix;
+  int32_t type{0}, forwardingType{0}, forwardingAlgorithm{0};
+  std::optional<int64_t> minNexthop;
+  PrefixMetrics metrics;
+  std::set<std::string> tags;
+  std::vector<std::string> area_stack;
+  std::optional<int64_t> weight;
+  auto tie() const {
+    return std::tie(prefix, type, forwardingType, forwardingAlgorithm,
+                    minNexthop, metrics, tags, area_stack, weight);
+  }
+  bool operator==(const PrefixEntry& o) const { return tie() == o.tie(); }
+};
+
+inline bool isV4Prefix(const std::string& p) {
+  return p.find(':') == std::string::npos;
+}
+
+using NodeAndArea = std::pair<std::string, std::string>;
+
+// ------------------------------------------------------------------ Link --
+class Link {
+ public:
+  using Key = std::pair<std::pair<std::string, std::string>,
+                        std::pair<std::string, std::string>>;
+  Link(const std::string& area, const std::string& n1, const std::string& if1,
+       const std::string& n2, const std::string& if2, bool usable = true);
+  Link(const std::string& area, const std::string& n1, const Adjacency& a1,
+       const std::string& n2, const Adjacency& a2, bool usable = true);
+
+  bool isUp() const { return !overload_[0] && !overload_[1] && usable_; }
+  const std::string& getArea() const { return area_; }
+  const std::string& getOtherNodeName(const std::string& n) const {
+    return node_[1 - side(n)];
+  }
+  const std::string& firstNodeName() const { return key_.first.first; }
+  const std::string& secondNodeName() const { return key_.second.first; }
+  const std::string& getIfaceFromNode(const std::string& n) const {
+    return if_[side(n)];
+  }
+  LinkStateMetric getMetricFromNode(const std::string& n) const {
+    return metric_[side(n)];
+  }
+  LinkStateMetric getMaxMetric() const {
+    return std::max(metric_[0], metric_[1]);
+  }
+  int32_t getAdjLabelFromNode(const std::string& n) const {
+    return label_[side(n)];
+  }
+  int64_t getWeightFromNode(const std::string& n) const {
+    return weight_[side(n)];
+  }
+  bool getOverloadFromNode(const std::string& n) const {
+    return overload_[side(n)];
+  }
+  const std::string& getNhV4FromNode(const std::string& n) const {
+    return v4_[side(n)];
+  }
+  const std::string& getNhV6FromNode(const std::string& n) const {
+    return v6_[side(n)];
+  }
+  bool getUsability() const { return usable_; }
+
+  void setNhV4FromNode(const std::string& n, const std::string& v) {
+    v4_[side(n)] = v;
+  }
+  void setNhV6FromNode(const std::string& n, const std::string& v) {
+    v6_[side(n)] = v;
+  }
+  bool setMetricFromNode(const std::string& n, LinkStateMetric d) {
+    metric_[side(n)] = d;
+    return true;
+  }
+  void setAdjLabelFromNode(const std::string& n, int32_t l) {
+    label_[side(n)] = l;
+  }
+  void setWeightFromNode(const std::string& n, int64_t w) {
+    weight_[side(n)] = w;
+  }
+  bool setOverloadFromNode(const std::string& n, bool ov);
+  bool setLinkUsability(const Link& newLink);
+
+  const Key& key() const { return key_; }
+  bool operator<(const Link& o) const { return key_ < o.key_; }
+  bool operator==(const Link& o) const { return key_ == o.key_; }
+
+ private:
+  int side(const std::string& n) const {  // throws like LinkState.h:136
+    if (node_[0] == n) return 0;
+    if (node_[1] == n) return 1;
+    throw std::invalid_argument(n);
+  }
+  std::string area_;
+  std::string node_[2], if_[2], v4_[2], v6_[2];
+  LinkStateMetric metric_[2]{1, 1};
+  bool overload_[2]{false, false};
+  int32_t label_[2]{0, 0};
+  int64_t weight_[2]{1, 1};
+  bool usable_{true};
+  Key key_;
+};
+using LinkPtr = std::shared_ptr<Link>;
+
+// ---------------------------------------------------- flattened topology --
+// Host image of one LinkState in the C-ABI's CSR encoding + the device copy.
+struct FlatTopology {
+  std::vector<std::string> names;               // id -> node name (sorted)
+  std::unordered_map<std::string, uint32_t> id;  // node name -> id
+  std::vector<uint32_t> rowPtr;                  // [N+1]
+  std::vector<uint64_t> edges;                   // [E] packed
+  std::vector<uint8_t> nodeFlags;                // [N]
+  std::vector<Link*> edgeLink;                   // [E] link of each edge
+  uint64_t maxMetric{0};
+  int maxDegree{0};
+  bool hasZeroMetric{false};
+  bool hasWideMetric{false};  // metric >= 2^32 (negative i32)
+  uint64_t version{0};
+  DeviceBuffer dRow, dEdges, dFlags, dNodeBase;
+};
+
+// ------------------------------------------------------------- LinkState --
+class LinkState {
+ public:
+  LinkState(const std::string& area, const std::string& myNodeName);
+  LinkState(LinkState&&) noexcept;
+  ~LinkState();
+
+  class NodeSpfResult {  // LinkState.h:290-344 (pathLinks: via getKthPaths)
+   public:
+    explicit NodeSpfResult(LinkStateMetric m) : metric_(m) {}
+    LinkStateMetric metric() const { return metric_; }
+    const std::set<std::string>& nextHops() const { return nextHops_; }
+    void addNextHop(const std::string& n) { nextHops_.insert(n); }
+
+   private:
+    LinkStateMetric metric_;
+    std::set<std::string> nextHops_;
+  };
+  using SpfResult = std::unordered_map<std::string, NodeSpfResult>;
+  using Path = std::vector<LinkPtr>;
+
+  struct LinkStateChange {  // LinkState.h:396-421
+    bool topologyChanged{false};
+    std::vector<LinkPtr> addedLinks;
+    bool linkAttributesChanged{false};
+    bool nodeLabelChanged{false};
+  };
+
+  const SpfResult& getSpfResult(const std::string& nodeName,
+                                bool useLinkMetric = true) const;
+  const std::vector<Path>& getKthPaths(const std::string& src,
+                                       const std::string& dest,
+                                       size_t k) const;
+  LinkStateChange updateAdjacencyDatabase(const AdjacencyDatabase& db,
+                                          const std::string& area,
+                                          bool inInitialization = false);
+  LinkStateChange deleteAdjacencyDatabase(const std::string& nodeName);
+  std::optional<LinkStateMetric> getMetricFromAToB(
+      const std::string& a, const std::string& b,
+      bool useLinkMetric = true) const;
+
+  const std::string& getArea() const { return area_; }
+  bool hasNode(const std::string& n) const { return adjDbs_.count(n) != 0; }
+  std::vector<LinkPtr> linksFromNode(const std::string& n) const;
+  bool isNodeOverloaded(const std::string& n) const;
+  uint64_t getNodeMetricIncrement(const std::string& n) const;
+  size_t numLinks() const { return links_.size(); }
+  size_t numNodes() const;
+  const std::map<std::string, AdjacencyDatabase>& getAdjacencyDatabases()
+      const {
+    return adjDbs_;
+  }
+  static bool pathAInPathB(const Path& a, const Path& b);
+  uint64_t spfRuns() const { return spfRuns_; }
+
+  // GPU plumbing (used by SpfSolver and the batch builders)
+  const FlatTopology& flat() const;          // re-flattens when stale
+  const FlatTopology& flatOnDevice() const;  // + uploads when stale
+  void noteSpfRuns(uint64_t n) const { spfRuns_ += n; }
+
+ private:
+  LinkPtr makeLink(const std::string& node, const Adjacency& adj) const;
+  void invalidate(bool topologyChanged);
+
+  std::string area_, myNodeName_;
+  std::map<std::string, AdjacencyDatabase> adjDbs_;
+  std::map<Link::Key, LinkPtr> links_;                      // all links
+  std::unordered_map<std::string, std::set<Link::Key>> byNode_;
+  std::unordered_map<std::string, bool> overloaded_;
+  std::unordered_map<std::string, uint64_t> metricInc_;
+  mutable std::map<std::pair<std::string, bool>, SpfResult> spfMemo_;
+  mutable std::map<std::tuple<std::string, std::string, size_t>,
+                   std::vector<Path>>
+      kthMemo_;
+  mutable std::unique_ptr<FlatTopology> flat_;
+  mutable bool flatStale_{true};
+  mutable bool deviceStale_{true};
+  mutable uint64_t spfRuns_{0};
+  uint64_t mutation_{0};
+};
+
+// ----------------------------------------------------------- PrefixState --
+class PrefixState {
+ public:
+  using Entries = std::map<NodeAndArea, std::shared_ptr<PrefixEntry>>;
+  const std::map<std::string, Entries>& prefixes() const { return prefixes_; }
+  std::set<std::string> updatePrefix(const std::string& node,
+                                     const std::string& area,
+                                     const PrefixEntry& entry);
+  std::set<std::string> deletePrefix(const std::string& node,
+                                     const std::string& area,
+                                     const std::string& prefix);
+  uint64_t version() const { return version_; }
+
+ private:
+  std::map<std::string, Entries> prefixes_;
+  uint64_t version_{0};
+};
+
+// ------------------------------------------------------------ RIB types --
+struct RibUnicastEntry {  // RibEntry.h:45-113
+  std::string prefix;
+  NextHops nexthops;
+  unsigned int igpCost{0};
+  PrefixEntry bestPrefixEntry;
+  std::string bestArea;
+  bool doNotInstall{false};
+  std::optional<std::string> counterID;
+  bool localRouteConsidered{false};
+  bool operator==(const RibUnicastEntry& o) const {  // RibEntry.h:81-87
+    return prefix == o.prefix && bestPrefixEntry == o.bestPrefixEntry &&
+        doNotInstall == o.doNotInstall && counterID == o.counterID &&
+        localRouteConsidered == o.localRouteConsidered &&
+        nexthops == o.nexthops;
+  }
+  bool operator!=(const RibUnicastEntry& o) const { return !(*this == o); }
+};
+
+struct RibMplsEntry {  // RibEntry.h:115-197
+  int32_t label{0};
+  NextHops nexthops;
+  bool operator==(const RibMplsEntry& o) const {
+    return label == o.label && nexthops == o.nexthops;
+  }
+  bool operator!=(const RibMplsEntry& o) const { return !(*this == o); }
+};
+
+struct DecisionRouteUpdate {  // RouteUpdate.h:28-110
+  std::map<std::string, RibUnicastEntry> unicastRoutesToUpdate;
+  std::vector<std::string> unicastRoutesToDelete;
+  std::map<int32_t, RibMplsEntry> mplsRoutesToUpdate;
+  std::vector<int32_t> mplsRoutesToDelete;
+};
+
+struct DecisionRouteDb {  // SpfSolver.h:68-109
+  std::map<std::string, RibUnicastEntry> unicastRoutes;
+  std::map<int32_t, RibMplsEntry> mplsRoutes;
+  DecisionRouteUpdate calculateUpdate(const DecisionRouteDb& newDb) const;
+  void update(const DecisionRouteUpdate& u);
+};
+
+struct RouteSelectionResult {  // SpfSolver.h:37-66
+  std::set<NodeAndArea> allNodeAreas;
+  NodeAndArea bestNodeArea;
+  bool isBestNodeDrained{false};
+  bool hasNode(const std::string& n) const {
+    for (const auto& na : allNodeAreas) {
+      if (na.first == n) return true;
+    }
+    return false;
+  }
+};
+
+using AreaLinkStates = std::map<std::string, LinkState>;
+
+// ------------------------------------------------------------- SpfSolver --
+class SpfSolver {
+ public:
+  SpfSolver(const std::string& myNodeName, bool enableV4,
+            bool enableNodeSegmentLabel, bool enableBestRouteSelection = false,
+            bool v4OverV6Nexthop = false);
+  ~SpfSolver();
+
+  void updateStaticUnicastRoutes(
+      const std::map<std::string, RibUnicastEntry>& toUpdate,
+      const std::vector<std::string>& toDelete);
+  std::optional<DecisionRouteDb> buildRouteDb(
+      const std::string& myNodeName, const AreaLinkStates& areaLinkStates,
+      const PrefixState& prefixState);
+  std::optional<RibUnicastEntry> createRouteForPrefixOrGetStaticRoute(
+      const std::string& myNodeName, const AreaLinkStates& areaLinkStates,
+      const PrefixState& prefixState, const std::string& prefix);
+  const std::map<std::string, RouteSelectionResult>& getBestRoutesCache()
+      const {
+    return bestRoutesCache_;
+  }
+
+ private:
+  struct Impl;
+  std::unique_ptr<Impl> impl_;
+  std::map<std::string, RibUnicastEntry> staticUnicastRoutes_;
+  std::map<std::string, RouteSelectionResult> bestRoutesCache_;
+  std::string myNodeName_;
+  bool enableV4_, enableNodeSegmentLabel_, enableBestRouteSelection_,
+      v4OverV6Nexthop_;
+};
+
+// ------------------------------------------------------------- RibPolicy --
+struct RibRouteActionWeight {
+  int32_t default_weight{0};
+  std::map<std::string, int32_t> area_to_weight;
+  std::map<std::string, int32_t> neighbor_to_weight;
+};
+struct RibPolicyStatementSpec {
+  std::string name;
+  std::optional<std::vector<std::string>> prefixes;
+  std::optional<std::vector<std::string>> tags;
+  std::optional<RibRouteActionWeight> set_weight;
+  std::optional<std::string> counterID;
+};
+
+class RibPolicy {  // RibPolicy.h:70-124
+ public:
+  RibPolicy(const std::vector<RibPolicyStatementSpec>& statements,
+            int64_t ttlSecs);
+  bool isActive() const { return ttlSecs_ > 0; }
+  bool match(const RibUnicastEntry& route) const;
+  bool applyAction(RibUnicastEntry& route) const;
+  std::vector<std::string> applyPolicy(
+      std::map<std::string, RibUnicastEntry>& unicastEntries) const;
+
+ private:
+  struct Stmt {
+    std::string name;
+    std::set<std::string> prefixes, tags;
+    RibRouteActionWeight weight;
+    std::optional<std::string> counterID;
+  };
+  bool matchStmt(const Stmt& s, const RibUnicastEntry& r) const;
+  std::vector<Stmt> stmts_;
+  int64_t ttlSecs_;
+};
+
+// ---------------------------------------------------- batch flattening --
+// T independent single-area LSDBs flattened into one C-ABI graph batch +
+// prefix table (the bench and the batched parity tests use this).
+struct HostBatch {
+  std::vector<uint32_t> nodeBase{0}, rowPtr{0};
+  std::vector<uint64_t> edges;
+  std::vector<uint8_t> nodeFlags;
+  std::vector<uint32_t> pfxBase{0}, advOff{0}, advNode;
+  std::vector<int32_t> advMetrics;
+  std::vector<int64_t> advMinNh;
+  std::vector<uint8_t> pfxFlags;
+  int maxNodes{0}, maxEdges{0}, maxPrefixes{0}, maxDegree{0};
+  uint64_t maxMetric{0};
+  bool hasZeroMetric{false};
+  void append(const FlatTopology& t, const PrefixState& ps,
+              const std::string& area);
+};
+
+// ---------------------------------------------------- materialisation --
+// One unit's compact GPU results (host copies, distances widened to 64-bit,
+// all-ones = unreachable) and the host side of the prefix table.
+struct UnitView {
+  int W{1};
+  uint32_t N{0}, P{0};
+  const uint64_t* dist{nullptr};
+  const uint32_t* nh{nullptr};
+  size_t nhStride{0};  // nh[w * nhStride + v]
+  const uint32_t* meta{nullptr};
+  const uint64_t* metric{nullptr};
+  const uint32_t* mask{nullptr};
+  size_t maskStride{0};  // mask[w * maskStride + p]
+  const uint32_t* sel{nullptr};
+};
+
+struct PrefixHostTable {
+  std::vector<std::string> prefixes;
+  std::vector<const PrefixEntry*> advEntry;
+  std::vector<NodeAndArea> advKey;
+  std::vector<uint32_t> advOff;
+  void build(const PrefixState& ps);
+};
+
+bool wideDistancesNeeded(const FlatTopology& f);
+
+DecisionRouteDb materializeRouteDb(
+    const LinkState& ls, const FlatTopology& f, const std::string& area,
+    const std::string& me, const UnitView& r, const PrefixHostTable& pt,
+    bool v4OverV6Nexthop, bool enableNodeSegmentLabel,
+    const std::map<std::string, RibUnicastEntry>& statics,
+    std::map<std::string, RouteSelectionResult>* bestRoutesCache);
+
+}  // namespace openr_amd

@@ -1,0 +1,76 @@
+// device.h — RAII device memory over the C-ABI, and loud error mapping.
+#pragma once
+
+#include <cstddef>
+#include <stdexcept>
+#include <string>
+#include <utility>
+
+#include "openr_gpu.h"
+
+namespace openr_amd {
+
+// Every C-ABI failure becomes an exception: the product has no CPU path to
+// fall back to, so a missing device or an unsupported input must be loud.
+inline void ogsCheck(int rc, const char* what) {
+  if (rc == OGS_OK) return;
+  std::string msg = std::string(what) + " failed (" + std::to_string(rc) +
+      "): " + ogs_last_error();
+  if (rc == OGS_E_UNSUPPORTED) throw std::domain_error(msg);
+  if (rc == OGS_E_INVALID) throw std::invalid_argument(msg);
+  throw std::runtime_error(msg);
+}
+
+class DeviceBuffer {
+ public:
+  DeviceBuffer() = default;
+  explicit DeviceBuffer(size_t bytes) { resize(bytes); }
+  DeviceBuffer(const DeviceBuffer&) = delete;
+  DeviceBuffer& operator=(const DeviceBuffer&) = delete;
+  DeviceBuffer(DeviceBuffer&& o) noexcept { swap(o); }
+  DeviceBuffer& operator=(DeviceBuffer&& o) noexcept {
+    swap(o);
+    return *this;
+  }
+  ~DeviceBuffer() { ogs_free(ptr_); }
+
+  void resize(size_t bytes) {  // grow-only, contents not preserved
+    if (bytes <= cap_) {
+      size_ = bytes;
+      return;
+    }
+    ogs_free(ptr_);
+    ptr_ = nullptr;
+    cap_ = size_ = 0;
+    ogsCheck(ogs_malloc(&ptr_, bytes), "ogs_malloc");
+    cap_ = size_ = bytes;
+  }
+  template <typename T>
+  void upload(const T* host, size_t count, void* stream = nullptr) {
+    resize(count * sizeof(T));
+    ogsCheck(ogs_memcpy_h2d(ptr_, host, count * sizeof(T), stream),
+             "ogs_memcpy_h2d");
+  }
+  template <typename T>
+  void download(T* host, size_t count, void* stream = nullptr) const {
+    ogsCheck(ogs_memcpy_d2h(host, ptr_, count * sizeof(T), stream),
+             "ogs_memcpy_d2h");
+  }
+  void* get() const { return ptr_; }
+  template <typename T>
+  T* as() const {
+    return static_cast<T*>(ptr_);
+  }
+  size_t size() const { return size_; }
+
+ private:
+  void swap(DeviceBuffer& o) noexcept {
+    std::swap(ptr_, o.ptr_);
+    std::swap(size_, o.size_);
+    std::swap(cap_, o.cap_);
+  }
+  void* ptr_{nullptr};
+  size_t size_{0}, cap_{0};
+};
+
+}  // namespace openr_amd

@@ -1,0 +1,410 @@
+// link_state.cpp — ingestion, change detection and CSR flattening for the
+// GPU LinkState (reference: openr/decision/LinkState.cpp:50-715).
+#include <algorithm>
+#include <unordered_map>
+
+#include "decision.h"
+
+namespace openr_amd {
+
+// ------------------------------------------------------------------ Link --
+Link::Link(const std::string& area, const std::string& n1,
+           const std::string& if1, const std::string& n2,
+           const std::string& if2, bool usable)
+    : area_(area), usable_(usable) {
+  node_[0] = n1;
+  node_[1] = n2;
+  if_[0] = if1;
+  if_[1] = if2;
+  auto a = std::make_pair(n1, if1), b = std::make_pair(n2, if2);
+  key_ = a < b ? Key{a, b} : Key{b, a};  // unordered pair of (node, if)
+}
+
+Link::Link(const std::string& area, const std::string& n1, const Adjacency& a1,
+           const std::string& n2, const Adjacency& a2, bool usable)
+    : Link(area, n1, a1.ifName, n2, a2.ifName, usable) {
+  const Adjacency* a[2] = {&a1, &a2};
+  for (int i = 0; i < 2; ++i) {
+    // thrift i32 -> LinkStateMetric (LinkState.cpp:77-78)
+    metric_[i] = static_cast<LinkStateMetric>(static_cast<int64_t>(a[i]->metric));
+    overload_[i] = a[i]->isOverloaded;
+    label_[i] = a[i]->adjLabel;
+    weight_[i] = a[i]->weight;
+    v4_[i] = a[i]->nextHopV4;
+    v6_[i] = a[i]->nextHopV6;
+  }
+}
+
+bool Link::setOverloadFromNode(const std::string& n, bool ov) {
+  const bool wasUp = isUp();  // only up<->down is a topology change
+  overload_[side(n)] = ov;
+  return wasUp != isUp();
+}
+
+bool Link::setLinkUsability(const Link& newLink) {
+  if (!(*this == newLink)) throw std::logic_error("setLinkUsability: other link");
+  const bool wasUp = isUp();
+  usable_ = newLink.usable_;
+  return wasUp != isUp();
+}
+
+// ------------------------------------------------------------- LinkState --
+LinkState::LinkState(const std::string& area, const std::string& me)
+    : area_(area), myNodeName_(me) {}
+LinkState::LinkState(LinkState&&) noexcept = default;
+LinkState::~LinkState() = default;
+
+LinkPtr LinkState::makeLink(const std::string& node, const Adjacency& adj) const {
+  // bidirectional only (LinkState.cpp:406-423); usability judged by the
+  // LinkState owner (LinkState.h:18-40, 469-473)
+  auto it = adjDbs_.find(adj.otherNodeName);
+  if (it == adjDbs_.end()) return nullptr;
+  for (const auto& rev : it->second.adjacencies) {
+    if (rev.otherNodeName != node || rev.ifName != adj.otherIfName ||
+        rev.otherIfName != adj.ifName) {
+      continue;
+    }
+    auto usableBy = [&](const Adjacency& a) {
+      return !a.adjOnlyUsedByOtherNode || a.otherNodeName == myNodeName_;
+    };
+    return std::make_shared<Link>(area_, node, adj, adj.otherNodeName, rev,
+                                  usableBy(adj) && usableBy(rev));
+  }
+  return nullptr;
+}
+
+void LinkState::invalidate(bool topologyChanged) {
+  ++mutation_;
+  flatStale_ = true;
+  if (topologyChanged) {  // LinkState.cpp:635-638
+    spfMemo_.clear();
+    kthMemo_.clear();
+  }
+}
+
+LinkState::LinkStateChange LinkState::updateAdjacencyDatabase(
+    const AdjacencyDatabase& db, const std::string& /*area*/,
+    bool /*inInitialization*/) {
+  LinkStateChange ch;
+  const std::string name = db.thisNodeName;
+  AdjacencyDatabase prior;
+  if (auto it = adjDbs_.find(name); it != adjDbs_.end()) prior = it->second;
+  adjDbs_[name] = db;
+
+  std::map<Link::Key, LinkPtr> fresh;
+  for (const auto& adj : db.adjacencies) {
+    if (auto l = makeLink(name, adj)) fresh.emplace(l->key(), l);
+  }
+
+  // node hard-drain: a change (not a first sighting) moves the topology
+  {
+    auto it = overloaded_.find(name);
+    if (it == overloaded_.end()) {
+      overloaded_[name] = db.isOverloaded;
+    } else if (it->second != db.isOverloaded) {
+      it->second = db.isOverloaded;
+      ch.topologyChanged = true;
+    }
+  }
+  ch.topologyChanged |= prior.nodeMetricIncrementVal != db.nodeMetricIncrementVal;
+  metricInc_[name] =
+      static_cast<uint64_t>(static_cast<int64_t>(db.nodeMetricIncrementVal));
+  ch.nodeLabelChanged = prior.nodeLabel != db.nodeLabel;
+
+  // merge old vs new link sets, both in key order
+  std::vector<Link::Key> oldKeys;
+  if (auto it = byNode_.find(name); it != byNode_.end()) {
+    oldKeys.assign(it->second.begin(), it->second.end());
+  }
+  auto ni = fresh.begin();
+  size_t oi = 0;
+  while (ni != fresh.end() || oi < oldKeys.size()) {
+    if (ni != fresh.end() && (oi == oldKeys.size() || ni->first < oldKeys[oi])) {
+      const LinkPtr& l = ni->second;
+      ch.topologyChanged |= l->isUp();
+      links_[l->key()] = l;
+      byNode_[l->firstNodeName()].insert(l->key());
+      byNode_[l->secondNodeName()].insert(l->key());
+      ch.addedLinks.push_back(l);
+      ++ni;
+      continue;
+    }
+    if (oi < oldKeys.size() && (ni == fresh.end() || oldKeys[oi] < ni->first)) {
+      const LinkPtr l = links_.at(oldKeys[oi]);
+      ch.topologyChanged |= l->isUp();
+      byNode_.at(l->firstNodeName()).erase(l->key());
+      byNode_.at(l->secondNodeName()).erase(l->key());
+      links_.erase(l->key());
+      ++oi;
+      continue;
+    }
+    Link& nl = *ni->second;
+    Link& ol = *links_.at(oldKeys[oi]);
+    if (nl.getMetricFromNode(name) != ol.getMetricFromNode(name)) {
+      ch.topologyChanged |= ol.setMetricFromNode(name, nl.getMetricFromNode(name));
+    }
+    if (nl.isUp() != ol.isUp()) ch.topologyChanged |= ol.setLinkUsability(nl);
+    if (nl.getOverloadFromNode(name) != ol.getOverloadFromNode(name)) {
+      ch.topologyChanged |=
+          ol.setOverloadFromNode(name, nl.getOverloadFromNode(name));
+    }
+    if (nl.getAdjLabelFromNode(name) != ol.getAdjLabelFromNode(name)) {
+      ch.linkAttributesChanged = true;
+      ol.setAdjLabelFromNode(name, nl.getAdjLabelFromNode(name));
+    }
+    if (nl.getWeightFromNode(name) != ol.getWeightFromNode(name)) {
+      ch.linkAttributesChanged = true;
+      ol.setWeightFromNode(name, nl.getWeightFromNode(name));
+    }
+    if (nl.getNhV4FromNode(name) != ol.getNhV4FromNode(name)) {
+      ch.linkAttributesChanged = true;
+      ol.setNhV4FromNode(name, nl.getNhV4FromNode(name));
+    }
+    if (nl.getNhV6FromNode(name) != ol.getNhV6FromNode(name)) {
+      ch.linkAttributesChanged = true;
+      ol.setNhV6FromNode(name, nl.getNhV6FromNode(name));
+    }
+    ++ni;
+    ++oi;
+  }
+  invalidate(ch.topologyChanged);
+  return ch;
+}
+
+LinkState::LinkStateChange LinkState::deleteAdjacencyDatabase(
+    const std::string& name) {  // LinkState.cpp:642-659
+  LinkStateChange ch;
+  auto it = adjDbs_.find(name);
+  if (it == adjDbs_.end()) return ch;
+  if (auto bn = byNode_.find(name); bn != byNode_.end()) {
+    for (const auto& key : std::set<Link::Key>(bn->second)) {
+      const LinkPtr l = links_.at(key);
+      byNode_.at(l->getOtherNodeName(name)).erase(key);
+      links_.erase(key);
+    }
+    byNode_.erase(name);
+    overloaded_.erase(name);
+  }
+  adjDbs_.erase(it);
+  ch.topologyChanged = true;
+  invalidate(true);
+  return ch;
+}
+
+std::vector<LinkPtr> LinkState::linksFromNode(const std::string& n) const {
+  std::vector<LinkPtr> out;
+  if (auto it = byNode_.find(n); it != byNode_.end()) {
+    for (const auto& k : it->second) out.push_back(links_.at(k));
+  }
+  return out;
+}
+
+size_t LinkState::numNodes() const { return byNode_.size(); }
+
+bool LinkState::isNodeOverloaded(const std::string& n) const {
+  auto it = overloaded_.find(n);
+  return it != overloaded_.end() && it->second;
+}
+
+uint64_t LinkState::getNodeMetricIncrement(const std::string& n) const {
+  auto it = metricInc_.find(n);
+  return it == metricInc_.end() ? 0 : it->second;
+}
+
+bool LinkState::pathAInPathB(const Path& a, const Path& b) {
+  if (a.size() > b.size()) return false;  // LinkState.h:488-503
+  for (size_t i = 0; i + a.size() <= b.size(); ++i) {
+    size_t k = 0;
+    while (k < a.size() && *a[k] == *b[i + k]) ++k;
+    if (k == a.size()) return true;
+  }
+  return false;
+}
+
+// ------------------------------------------------------------ flattening --
+const FlatTopology& LinkState::flat() const {
+  if (flat_ && !flatStale_) return *flat_;
+  auto f = std::make_unique<FlatTopology>();
+  f->version = mutation_;
+  f->names.reserve(adjDbs_.size());
+  for (const auto& [n, _] : adjDbs_) {  // byte-wise name order == id order
+    f->id.emplace(n, uint32_t(f->names.size()));
+    f->names.push_back(n);
+  }
+  const uint32_t N = uint32_t(f->names.size());
+  if (N > OGS_MAX_NODES_PER_TOPO) throw std::domain_error("too many nodes");
+  // slot of every (link, endpoint) inside that endpoint's CSR row
+  std::unordered_map<const Link*, std::pair<uint32_t, uint32_t>> slot;
+  f->rowPtr.assign(N + 1, 0);
+  for (uint32_t u = 0; u < N; ++u) {
+    uint32_t j = 0;
+    if (auto it = byNode_.find(f->names[u]); it != byNode_.end()) {
+      for (const auto& key : it->second) {
+        const Link* l = links_.at(key).get();
+        auto& s = slot[l];
+        (l->firstNodeName() == f->names[u] ? s.first : s.second) = j++;
+      }
+    }
+    f->rowPtr[u + 1] = f->rowPtr[u] + j;
+    f->maxDegree = std::max<int>(f->maxDegree, int(j));
+  }
+  if (f->maxDegree >= OGS_MAX_DEGREE) throw std::domain_error("degree > 511");
+  f->edges.resize(f->rowPtr[N]);
+  f->edgeLink.resize(f->rowPtr[N]);
+  f->nodeFlags.assign(N, 0);
+  for (uint32_t u = 0; u < N; ++u) {
+    const std::string& un = f->names[u];
+    if (isNodeOverloaded(un)) f->nodeFlags[u] |= OGS_NODE_OVERLOADED;
+    const uint64_t inc = getNodeMetricIncrement(un);
+    if (static_cast<int>(inc) > 0) f->nodeFlags[u] |= OGS_NODE_SOFTDRAIN;
+    if (inc != 0) f->nodeFlags[u] |= OGS_NODE_METRICINC;
+    uint32_t e = f->rowPtr[u];
+    if (auto it = byNode_.find(un); it != byNode_.end()) {
+      for (const auto& key : it->second) {
+        Link* l = links_.at(key).get();
+        const std::string& vn = l->getOtherNodeName(un);
+        const uint32_t v = f->id.at(vn);
+        const auto& s = slot.at(l);
+        const uint32_t rslot = (l->firstNodeName() == vn) ? s.first : s.second;
+        const LinkStateMetric m = l->getMaxMetric();
+        uint32_t lo = v | (rslot << OGS_EDGE_RSLOT_SHIFT);
+        if (isNodeOverloaded(vn)) lo |= OGS_EDGE_DST_OVERLOADED;
+        if (!l->isUp()) lo |= OGS_EDGE_DOWN;
+        if (l->isUp()) {
+          f->maxMetric = std::max(f->maxMetric, m);
+          if (m == 0) f->hasZeroMetric = true;
+          if (m > 0xFFFFFFFFull) f->hasWideMetric = true;
+        }
+        f->edges[e] = uint64_t(lo) | (uint64_t(uint32_t(m)) << 32);
+        f->edgeLink[e] = l;
+        ++e;
+      }
+    }
+  }
+  flat_ = std::move(f);
+  flatStale_ = false;
+  deviceStale_ = true;
+  return *flat_;
+}
+
+const FlatTopology& LinkState::flatOnDevice() const {
+  const FlatTopology& f = flat();
+  if (!deviceStale_) return f;
+  FlatTopology& m = *flat_;
+  const uint32_t nodeBase[2] = {0, uint32_t(m.names.size())};
+  m.dNodeBase.upload(nodeBase, 2);
+  m.dRow.upload(m.rowPtr.data(), m.rowPtr.size());
+  m.dEdges.upload(m.edges.data(), std::max<size_t>(m.edges.size(), 1));
+  m.dFlags.upload(m.nodeFlags.data(), std::max<size_t>(m.nodeFlags.size(), 1));
+  deviceStale_ = false;
+  return f;
+}
+
+// ------------------------------------------------------------------- SPF --
+namespace {
+// Shared scratch for single-source launches made through the API surface.
+struct SpfScratch {
+  DeviceBuffer unit, dist, nh;
+};
+SpfScratch& scratch() {
+  static SpfScratch s;
+  return s;
+}
+
+bool needsWide(const FlatTopology& f, bool useLinkMetric) {
+  if (!useLinkMetric) return false;
+  const uint64_t n = f.names.empty() ? 0 : f.names.size() - 1;
+  return f.maxMetric != 0 && n != 0 &&
+      f.maxMetric > (0xFFFFFFFEull / n);
+}
+}  // namespace
+
+const LinkState::SpfResult& LinkState::getSpfResult(const std::string& node,
+                                                    bool useLinkMetric) const {
+  auto key = std::make_pair(node, useLinkMetric);
+  if (auto it = spfMemo_.find(key); it != spfMemo_.end()) return it->second;
+
+  SpfResult res;
+  const FlatTopology& f = flatOnDevice();
+  auto idIt = f.id.find(node);
+  ++spfRuns_;
+  if (idIt == f.id.end()) {
+    res.emplace(node, NodeSpfResult(0));  // unknown source settles only itself
+    return spfMemo_.emplace(key, std::move(res)).first->second;
+  }
+  if (useLinkMetric && (f.hasZeroMetric || f.hasWideMetric)) {
+    throw std::domain_error(
+        "getSpfResult: zero or negative link metric is outside the GPU "
+        "engine's exact domain");
+  }
+  const uint32_t s = idIt->second;
+  const uint32_t N = uint32_t(f.names.size());
+  const int degree = int(f.rowPtr[s + 1] - f.rowPtr[s]);
+  const int W = std::max(1, ogs_nh_words_for_degree(degree));
+  const bool wide = needsWide(f, useLinkMetric);
+  const size_t db = wide ? 8 : 4;
+
+  auto& sc = scratch();
+  const ogs_unit u{0, s};
+  sc.unit.upload(&u, 1);
+  sc.dist.resize(N * db);
+  sc.nh.resize(size_t(N) * W * 4);
+
+  ogs_graph g{};
+  g.num_topos = 1;
+  g.max_nodes = int32_t(N);
+  g.max_edges = int32_t(f.edges.size());
+  g.node_base = f.dNodeBase.as<uint32_t>();
+  g.row_ptr = f.dRow.as<uint32_t>();
+  g.edges = f.dEdges.as<uint64_t>();
+  g.node_flags = f.dFlags.as<uint8_t>();
+  ogs_spf_out out{};
+  out.dist = sc.dist.get();
+  out.nh = sc.nh.as<uint32_t>();
+  uint32_t flags = (useLinkMetric ? 0u : OGS_F_HOP_METRIC) |
+      (wide ? OGS_F_WIDE_METRIC : 0u);
+  ogsCheck(ogs_spf_routes(&g, nullptr, sc.unit.as<ogs_unit>(), 1, flags, W,
+                          &out, nullptr),
+           "ogs_spf_routes");
+  std::vector<uint64_t> dist(N);
+  std::vector<uint32_t> nh(size_t(N) * W);
+  if (wide) {
+    sc.dist.download(dist.data(), N);
+  } else {
+    std::vector<uint32_t> d32(N);
+    sc.dist.download(d32.data(), N);
+    for (uint32_t v = 0; v < N; ++v) {
+      dist[v] = d32[v] == 0xFFFFFFFFu ? ~0ull : d32[v];
+    }
+  }
+  sc.nh.download(nh.data(), nh.size());
+  ogsCheck(ogs_stream_sync(nullptr), "ogs_stream_sync");
+
+  const uint32_t rb = f.rowPtr[s];
+  for (uint32_t v = 0; v < N; ++v) {
+    if (dist[v] == ~0ull) continue;
+    NodeSpfResult r(dist[v]);
+    for (int w = 0; w < W; ++w) {
+      uint32_t bits = nh[size_t(w) * N + v];
+      while (bits) {
+        const int b = __builtin_ctz(bits);
+        bits &= bits - 1;
+        const Link* l = f.edgeLink[rb + w * 32 + b];
+        r.addNextHop(l->getOtherNodeName(node));
+      }
+    }
+    res.emplace(f.names[v], std::move(r));
+  }
+  return spfMemo_.emplace(key, std::move(res)).first->second;
+}
+
+std::optional<LinkStateMetric> LinkState::getMetricFromAToB(
+    const std::string& a, const std::string& b, bool useLinkMetric) const {
+  if (a == b) return 0;  // LinkState.cpp:661-672
+  const auto& r = getSpfResult(a, useLinkMetric);
+  auto it = r.find(b);
+  if (it == r.end()) return std::nullopt;
+  return it->second.metric();
+}
+
+}  // namespace openr_amd

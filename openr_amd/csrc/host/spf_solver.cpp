@@ -1,0 +1,512 @@
+// spf_solver.cpp — SpfSolver::buildRouteDb on the GPU (reference:
+// openr/decision/SpfSolver.cpp:139-767). The host flattens PrefixState into
+// the C-ABI prefix table, launches the fused SPF+RouteDb kernel for the
+// source and materialises the compact route records into RibUnicastEntry /
+// RibMplsEntry objects.
+#include <algorithm>
+
+#include "decision.h"
+
+namespace openr_amd {
+
+// ----------------------------------------------------------- PrefixState --
+std::set<std::string> PrefixState::updatePrefix(const std::string& node,
+                                                const std::string& area,
+                                                const PrefixEntry& entry) {
+  std::set<std::string> changed;  // PrefixState.cpp:15-38
+  auto& entries = prefixes_[entry.prefix];
+  auto key = std::make_pair(node, area);
+  auto it = entries.find(key);
+  if (it != entries.end() && *it->second == entry) return changed;
+  entries[key] = std::make_shared<PrefixEntry>(entry);
+  changed.insert(entry.prefix);
+  ++version_;
+  return changed;
+}
+
+std::set<std::string> PrefixState::deletePrefix(const std::string& node,
+                                                const std::string& area,
+                                                const std::string& prefix) {
+  std::set<std::string> changed;  // PrefixState.cpp:40-57
+  auto it = prefixes_.find(prefix);
+  if (it != prefixes_.end() && it->second.erase(std::make_pair(node, area))) {
+    changed.insert(prefix);
+    if (it->second.empty()) prefixes_.erase(it);
+    ++version_;
+  }
+  return changed;
+}
+
+// ------------------------------------------------------- DecisionRouteDb --
+DecisionRouteUpdate DecisionRouteDb::calculateUpdate(
+    const DecisionRouteDb& newDb) const {  // SpfSolver.cpp:21-56
+  DecisionRouteUpdate d;
+  for (const auto& [p, e] : newDb.unicastRoutes) {
+    auto it = unicastRoutes.find(p);
+    if (it == unicastRoutes.end() || it->second != e) d.unicastRoutesToUpdate[p] = e;
+  }
+  for (const auto& [p, _] : unicastRoutes) {
+    if (!newDb.unicastRoutes.count(p)) d.unicastRoutesToDelete.push_back(p);
+  }
+  for (const auto& [l, e] : newDb.mplsRoutes) {
+    auto it = mplsRoutes.find(l);
+    if (it == mplsRoutes.end() || it->second != e) d.mplsRoutesToUpdate[l] = e;
+  }
+  for (const auto& [l, _] : mplsRoutes) {
+    if (!newDb.mplsRoutes.count(l)) d.mplsRoutesToDelete.push_back(l);
+  }
+  return d;
+}
+
+void DecisionRouteDb::update(const DecisionRouteUpdate& u) {
+  for (const auto& p : u.unicastRoutesToDelete) unicastRoutes.erase(p);
+  for (const auto& [p, e] : u.unicastRoutesToUpdate) unicastRoutes[p] = e;
+  for (const auto& l : u.mplsRoutesToDelete) mplsRoutes.erase(l);
+  for (const auto& [l, e] : u.mplsRoutesToUpdate) mplsRoutes[l] = e;
+}
+
+// ------------------------------------------------------------ HostBatch --
+void HostBatch::append(const FlatTopology& t, const PrefixState& ps,
+                       const std::string& area) {
+  const uint32_t N = uint32_t(t.names.size());
+  const uint32_t e0 = rowPtr.back();
+  for (uint32_t v = 0; v < N; ++v) rowPtr.push_back(e0 + t.rowPtr[v + 1]);
+  edges.insert(edges.end(), t.edges.begin(), t.edges.end());
+  nodeFlags.insert(nodeFlags.end(), t.nodeFlags.begin(), t.nodeFlags.end());
+  nodeBase.push_back(nodeBase.back() + N);
+  maxNodes = std::max<int>(maxNodes, int(N));
+  maxEdges = std::max<int>(maxEdges, int(t.edges.size()));
+  maxDegree = std::max(maxDegree, t.maxDegree);
+  maxMetric = std::max(maxMetric, t.maxMetric);
+  hasZeroMetric |= t.hasZeroMetric;
+  uint32_t np = 0;
+  for (const auto& [prefix, entries] : ps.prefixes()) {
+    for (const auto& [na, e] : entries) {
+      if (na.second != area) {
+        throw std::out_of_range("prefix advertised in unknown area " + na.second);
+      }
+      auto it = t.id.find(na.first);
+      advNode.push_back(it == t.id.end() ? OGS_NODE_NONE : it->second);
+      advMetrics.insert(advMetrics.end(),
+                        {e->metrics.drain_metric, e->metrics.path_preference,
+                         e->metrics.source_preference, e->metrics.distance});
+      advMinNh.push_back(e->minNexthop ? *e->minNexthop : INT64_MIN);
+    }
+    advOff.push_back(uint32_t(advNode.size()));
+    pfxFlags.push_back(isV4Prefix(prefix) ? 1 : 0);
+    ++np;
+  }
+  pfxBase.push_back(pfxBase.back() + np);
+  maxPrefixes = std::max<int>(maxPrefixes, int(np));
+}
+
+// ------------------------------------------------------------- SpfSolver --
+struct SpfSolver::Impl {
+  DeviceBuffer pfxBase, advOff, advNode, advMetrics, advMinNh, pfxFlags;
+  DeviceBuffer unit, dist, nh, meta, metric, mask, sel;
+  const PrefixState* cachedPs{nullptr};
+  uint64_t cachedPsVersion{~0ull}, cachedTopoVersion{~0ull};
+  const FlatTopology* cachedTopo{nullptr};
+  PrefixHostTable table;
+};
+
+SpfSolver::SpfSolver(const std::string& me, bool enableV4, bool sr, bool brs,
+                     bool v4OverV6)
+    : impl_(std::make_unique<Impl>()),
+      myNodeName_(me),
+      enableV4_(enableV4),
+      enableNodeSegmentLabel_(sr),
+      enableBestRouteSelection_(brs),
+      v4OverV6Nexthop_(v4OverV6) {}
+SpfSolver::~SpfSolver() = default;
+
+void SpfSolver::updateStaticUnicastRoutes(
+    const std::map<std::string, RibUnicastEntry>& toUpdate,
+    const std::vector<std::string>& toDelete) {  // SpfSolver.cpp:109-137
+  for (const auto& [p, e] : toUpdate) staticUnicastRoutes_[p] = e;
+  for (const auto& p : toDelete) staticUnicastRoutes_.erase(p);
+}
+
+namespace {
+
+const LinkState& singleArea(const AreaLinkStates& als, std::string& area) {
+  if (als.size() != 1) {
+    throw std::domain_error(
+        "SpfSolver: multi-area route computation is not on the GPU path yet");
+  }
+  area = als.begin()->first;
+  return als.begin()->second;
+}
+
+NextHopThrift makeNh(const Link& l, const std::string& me, bool useV4,
+                     int32_t metric, std::optional<MplsAction> act) {
+  NextHopThrift nh;  // createNextHop (LsdbUtil.cpp:600-618)
+  nh.address = useV4 ? l.getNhV4FromNode(me) : l.getNhV6FromNode(me);
+  nh.ifName = l.getIfaceFromNode(me);
+  nh.metric = metric;
+  nh.mplsAction = std::move(act);
+  nh.area = l.getArea();
+  nh.neighborNodeName = l.getOtherNodeName(me);
+  nh.weight = 0;
+  return nh;
+}
+
+}  // namespace
+
+bool wideDistancesNeeded(const FlatTopology& f) {
+  const uint64_t n = f.names.empty() ? 0 : f.names.size() - 1;
+  return f.maxMetric != 0 && n != 0 && f.maxMetric > 0xFFFFFFFEull / n;
+}
+
+void PrefixHostTable::build(const PrefixState& ps) {
+  prefixes.clear();
+  advEntry.clear();
+  advKey.clear();
+  advOff.assign(1, 0);
+  for (const auto& [prefix, entries] : ps.prefixes()) {
+    prefixes.push_back(prefix);
+    for (const auto& [na, e] : entries) {
+      advEntry.push_back(e.get());
+      advKey.push_back(na);
+    }
+    advOff.push_back(uint32_t(advEntry.size()));
+  }
+}
+
+DecisionRouteDb materializeRouteDb(
+    const LinkState& ls, const FlatTopology& f, const std::string& area,
+    const std::string& me, const UnitView& r, const PrefixHostTable& pt,
+    bool v4OverV6Nexthop, bool enableNodeSegmentLabel,
+    const std::map<std::string, RibUnicastEntry>& statics,
+    std::map<std::string, RouteSelectionResult>* bestRoutesCache) {
+  DecisionRouteDb rdb;
+  if (bestRoutesCache) bestRoutesCache->clear();
+  const uint32_t s = f.id.at(me);
+  const uint32_t rb = f.rowPtr[s];
+  auto linksOf = [&](const uint32_t* words, size_t stride, auto&& fn) {
+    for (int w = 0; w < r.W; ++w) {
+      uint32_t bits = words[w * stride];
+      while (bits) {
+        const int b = __builtin_ctz(bits);
+        bits &= bits - 1;
+        fn(*f.edgeLink[rb + w * 32 + b]);
+      }
+    }
+  };
+  for (uint32_t p = 0; p < r.P; ++p) {
+    const uint32_t meta = r.meta[p];
+    const uint32_t a0 = pt.advOff[p];
+    const uint32_t best = a0 + (meta >> OGS_ROUTE_BEST_SHIFT);
+    if (bestRoutesCache && (meta & OGS_ROUTE_SELECTED)) {  // SpfSolver.cpp:247
+      RouteSelectionResult sel;
+      const uint32_t a1 = pt.advOff[p + 1];
+      for (uint32_t a = a0; a < std::min(a1, a0 + 32); ++a) {
+        if (r.sel[p] >> (a - a0) & 1u) sel.allNodeAreas.insert(pt.advKey[a]);
+      }
+      sel.bestNodeArea = pt.advKey[best];
+      sel.isBestNodeDrained = meta & OGS_ROUTE_DRAINED;
+      (*bestRoutesCache)[pt.prefixes[p]] = std::move(sel);
+    }
+    if (!(meta & OGS_ROUTE_VALID)) continue;
+    RibUnicastEntry e;
+    e.prefix = pt.prefixes[p];
+    const bool useV4 = isV4Prefix(e.prefix) && !v4OverV6Nexthop;
+    const int32_t m32 = static_cast<int32_t>(r.metric[p]);
+    linksOf(&r.mask[p], r.maskStride, [&](const Link& l) {
+      e.nexthops.insert(makeNh(l, me, useV4, m32, std::nullopt));
+    });
+    e.bestPrefixEntry = *pt.advEntry[best];
+    if (meta & OGS_ROUTE_DRAINED) e.bestPrefixEntry.metrics.drain_metric = 1;
+    e.bestPrefixEntry.weight = std::nullopt;  // RibEntry.h:77
+    e.bestArea = pt.advKey[best].second;
+    e.igpCost = static_cast<unsigned int>(r.metric[p]);
+    e.localRouteConsidered = meta & OGS_ROUTE_LOCAL;
+    rdb.unicastRoutes.emplace(e.prefix, std::move(e));
+  }
+  for (const auto& [prefix, e] : statics) {  // SpfSolver.cpp:343-349
+    if (!rdb.unicastRoutes.count(prefix)) rdb.unicastRoutes.emplace(prefix, e);
+  }
+
+  // node-label MPLS routes from the SPF result (SpfSolver.cpp:354-445)
+  if (enableNodeSegmentLabel) {
+    std::map<int32_t, std::pair<std::string, RibMplsEntry>> labelToNode;
+    for (const auto& [node, adjDb] : ls.getAdjacencyDatabases()) {
+      const int32_t label = adjDb.nodeLabel;
+      const bool valid =
+          (static_cast<uint32_t>(label) & 0xfff00000u) == 0 && label != 0;
+      if (!valid) continue;
+      auto it = labelToNode.find(label);
+      if (it != labelToNode.end() && it->second.first < node) continue;
+      if (node == me) {
+        NextHopThrift nh;
+        nh.address = "::";
+        nh.area = area;
+        nh.mplsAction = MplsAction{POP_AND_LOOKUP, std::nullopt, std::nullopt};
+        labelToNode.erase(label);
+        labelToNode.emplace(label, std::make_pair(me, RibMplsEntry{label, {nh}}));
+        continue;
+      }
+      const uint32_t v = f.id.at(node);
+      if (r.dist[v] == ~0ull) continue;  // no route to the label owner
+      RibMplsEntry entry{label, {}};
+      const int32_t m32 = static_cast<int32_t>(r.dist[v]);
+      linksOf(&r.nh[v], r.nhStride, [&](const Link& l) {
+        const bool php = l.getOtherNodeName(me) == node;
+        entry.nexthops.insert(makeNh(
+            l, me, false, m32,
+            php ? MplsAction{PHP, std::nullopt, std::nullopt}
+                : MplsAction{SWAP, label, std::nullopt}));
+      });
+      if (entry.nexthops.empty()) continue;
+      labelToNode.erase(label);
+      labelToNode.emplace(label, std::make_pair(node, std::move(entry)));
+    }
+    for (auto& [label, ne] : labelToNode) {
+      rdb.mplsRoutes.emplace(label, std::move(ne.second));
+    }
+  }
+  return rdb;
+}
+
+std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(
+    const std::string& me, const AreaLinkStates& als, const PrefixState& ps) {
+  bool exists = false;  // SpfSolver.cpp:318-324
+  for (const auto& [_, l] : als) exists |= l.hasNode(me);
+  if (!exists) return std::nullopt;
+  std::string area;
+  const LinkState& ls = singleArea(als, area);
+  const FlatTopology& f = ls.flatOnDevice();
+  if (f.hasZeroMetric || f.hasWideMetric) {
+    throw std::domain_error(
+        "buildRouteDb: zero or negative link metric is outside the GPU "
+        "engine's exact domain");
+  }
+  Impl& I = *impl_;
+
+  // ---- prefix table (cached on PrefixState / topology version) ------------
+  if (I.cachedPs != &ps || I.cachedPsVersion != ps.version() ||
+      I.cachedTopo != &f || I.cachedTopoVersion != f.version) {
+    HostBatch hb;
+    hb.append(f, ps, area);
+    I.table.build(ps);
+    I.pfxBase.upload(hb.pfxBase.data(), hb.pfxBase.size());
+    I.advOff.upload(hb.advOff.data(), hb.advOff.size());
+    I.advNode.upload(hb.advNode.data(), std::max<size_t>(hb.advNode.size(), 1));
+    I.advMetrics.upload(hb.advMetrics.data(), std::max<size_t>(hb.advMetrics.size(), 4));
+    I.advMinNh.upload(hb.advMinNh.data(), std::max<size_t>(hb.advMinNh.size(), 1));
+    I.pfxFlags.upload(hb.pfxFlags.data(), std::max<size_t>(hb.pfxFlags.size(), 1));
+    I.cachedPs = &ps;
+    I.cachedPsVersion = ps.version();
+    I.cachedTopo = &f;
+    I.cachedTopoVersion = f.version;
+  }
+
+  // ---- launch the fused kernel for (topology, me) -------------------------
+  const uint32_t s = f.id.at(me);
+  const uint32_t N = uint32_t(f.names.size());
+  const uint32_t P = uint32_t(I.table.prefixes.size());
+  const int degree = int(f.rowPtr[s + 1] - f.rowPtr[s]);
+  const int W = std::max(1, ogs_nh_words_for_degree(degree));
+  const bool wide = wideDistancesNeeded(f);
+  const size_t db = wide ? 8 : 4;
+  const ogs_unit u{0, s};
+  I.unit.upload(&u, 1);
+  I.dist.resize(N * db);
+  I.nh.resize(size_t(N) * W * 4);
+  const size_t P1 = std::max<uint32_t>(P, 1);
+  I.meta.resize(P1 * 4);
+  I.metric.resize(P1 * db);
+  I.mask.resize(P1 * W * 4);
+  I.sel.resize(P1 * 4);
+
+  ogs_graph g{};
+  g.num_topos = 1;
+  g.max_nodes = int32_t(N);
+  g.max_edges = int32_t(f.edges.size());
+  g.node_base = f.dNodeBase.as<uint32_t>();
+  g.row_ptr = f.dRow.as<uint32_t>();
+  g.edges = f.dEdges.as<uint64_t>();
+  g.node_flags = f.dFlags.as<uint8_t>();
+  ogs_prefix_table pt{};
+  pt.max_prefixes = int32_t(P);
+  pt.pfx_base = I.pfxBase.as<uint32_t>();
+  pt.adv_off = I.advOff.as<uint32_t>();
+  pt.adv_node = I.advNode.as<uint32_t>();
+  pt.adv_metrics = I.advMetrics.as<int32_t>();
+  pt.adv_min_nh = I.advMinNh.as<int64_t>();
+  pt.pfx_flags = I.pfxFlags.as<uint8_t>();
+  ogs_spf_out out{};
+  out.dist = I.dist.get();
+  out.nh = I.nh.as<uint32_t>();
+  out.meta = I.meta.as<uint32_t>();
+  out.metric = I.metric.get();
+  out.mask = I.mask.as<uint32_t>();
+  out.sel = I.sel.as<uint32_t>();
+  const uint32_t flags = (enableV4_ ? OGS_F_ENABLE_V4 : 0u) |
+      (v4OverV6Nexthop_ ? OGS_F_V4_OVER_V6 : 0u) |
+      (enableBestRouteSelection_ ? OGS_F_BEST_ROUTE_SELECTION : 0u) |
+      (wide ? OGS_F_WIDE_METRIC : 0u);
+  ogsCheck(ogs_spf_routes(&g, P ? &pt : nullptr, I.unit.as<ogs_unit>(), 1,
+                          flags, W, &out, nullptr),
+           "ogs_spf_routes");
+  ls.noteSpfRuns(1);
+
+  auto widen = [&](const DeviceBuffer& b, size_t n, std::vector<uint64_t>& v) {
+    v.resize(n);
+    if (wide) {
+      b.download(v.data(), n);
+    } else {
+      std::vector<uint32_t> t(n);
+      b.download(t.data(), n);
+      for (size_t i = 0; i < n; ++i) v[i] = t[i] == 0xFFFFFFFFu ? ~0ull : t[i];
+    }
+  };
+  std::vector<uint64_t> dist, metric;
+  std::vector<uint32_t> nh(size_t(N) * W), meta(P), mask(size_t(P) * W), sel(P);
+  widen(I.dist, N, dist);
+  I.nh.download(nh.data(), nh.size());
+  if (P) {
+    I.meta.download(meta.data(), P);
+    widen(I.metric, P, metric);
+    I.mask.download(mask.data(), mask.size());
+    I.sel.download(sel.data(), P);
+  }
+  ogsCheck(ogs_stream_sync(nullptr), "ogs_stream_sync");
+
+  UnitView view;
+  view.W = W;
+  view.N = N;
+  view.P = P;
+  view.dist = dist.data();
+  view.nh = nh.data();
+  view.nhStride = N;
+  view.meta = meta.data();
+  view.metric = metric.data();
+  view.mask = mask.data();
+  view.maskStride = P;
+  view.sel = sel.data();
+  return materializeRouteDb(ls, f, area, me, view, I.table, v4OverV6Nexthop_,
+                            enableNodeSegmentLabel_, staticUnicastRoutes_,
+                            &bestRoutesCache_);
+}
+
+std::optional<RibUnicastEntry> SpfSolver::createRouteForPrefixOrGetStaticRoute(
+    const std::string& me, const AreaLinkStates& als, const PrefixState& ps,
+    const std::string& prefix) {  // SpfSolver.cpp:139-158
+  std::optional<RibUnicastEntry> route;
+  bool exists = false;
+  for (const auto& [_, l] : als) exists |= l.hasNode(me);
+  auto pit = ps.prefixes().find(prefix);
+  const bool gated = isV4Prefix(prefix) && !enableV4_ && !v4OverV6Nexthop_;
+  if (exists && !gated && pit != ps.prefixes().end()) {
+    PrefixState one;  // a one-prefix table through the same GPU path
+    for (const auto& [na, e] : pit->second) one.updatePrefix(na.first, na.second, *e);
+    SpfSolver probe(myNodeName_, enableV4_, false, enableBestRouteSelection_,
+                    v4OverV6Nexthop_);
+    auto db = probe.buildRouteDb(me, als, one);
+    if (db) {
+      auto it = db->unicastRoutes.find(prefix);
+      if (it != db->unicastRoutes.end()) route = it->second;
+    }
+    auto bc = probe.getBestRoutesCache().find(prefix);
+    if (bc != probe.getBestRoutesCache().end()) {
+      bestRoutesCache_[prefix] = bc->second;
+    } else {
+      bestRoutesCache_.erase(prefix);
+    }
+  }
+  if (route) return route;
+  auto it = staticUnicastRoutes_.find(prefix);
+  if (it != staticUnicastRoutes_.end()) return it->second;
+  return std::nullopt;
+}
+
+// ------------------------------------------------------------- RibPolicy --
+RibPolicy::RibPolicy(const std::vector<RibPolicyStatementSpec>& statements,
+                     int64_t ttlSecs)
+    : ttlSecs_(ttlSecs) {  // RibPolicy.cpp:20-50, 167-182
+  if (statements.empty()) {
+    throw std::invalid_argument("Missing policy.statements attribute");
+  }
+  for (const auto& s : statements) {
+    if (!s.set_weight) {
+      throw std::invalid_argument(
+          "Missing policy_statement.action.set_weight attribute");
+    }
+    if (!s.prefixes && !s.tags) {
+      throw std::invalid_argument(
+          "Missing policy_statement.matcher.prefixes or "
+          "policy_statement.matcher.tags attribute");
+    }
+    Stmt st;
+    st.name = s.name;
+    if (s.prefixes) st.prefixes.insert(s.prefixes->begin(), s.prefixes->end());
+    if (s.tags) st.tags.insert(s.tags->begin(), s.tags->end());
+    st.weight = *s.set_weight;
+    st.counterID = s.counterID;
+    stmts_.push_back(std::move(st));
+  }
+}
+
+bool RibPolicy::matchStmt(const Stmt& s, const RibUnicastEntry& r) const {
+  if (s.tags.empty() && s.prefixes.empty()) return false;  // RibPolicy.cpp:74-107
+  bool tag = s.tags.empty();
+  for (const auto& t : s.tags) {
+    if (r.bestPrefixEntry.tags.count(t)) {
+      tag = true;
+      break;
+    }
+  }
+  return tag && (s.prefixes.empty() || s.prefixes.count(r.prefix));
+}
+
+bool RibPolicy::match(const RibUnicastEntry& r) const {
+  for (const auto& s : stmts_) {
+    if (matchStmt(s, r)) return true;
+  }
+  return false;
+}
+
+bool RibPolicy::applyAction(RibUnicastEntry& r) const {
+  for (const auto& s : stmts_) {  // first statement that transforms wins
+    if (!matchStmt(s, r)) continue;
+    r.counterID = s.counterID;
+    NextHops next;
+    for (const auto& nh : r.nexthops) {  // neighbor > area > default
+      int32_t w = s.weight.default_weight;
+      if (nh.area) {
+        if (auto it = s.weight.area_to_weight.find(*nh.area);
+            it != s.weight.area_to_weight.end()) {
+          w = it->second;
+        }
+      }
+      if (nh.neighborNodeName) {
+        if (auto it = s.weight.neighbor_to_weight.find(*nh.neighborNodeName);
+            it != s.weight.neighbor_to_weight.end()) {
+          w = it->second;
+        }
+      }
+      if (w > 0) {
+        NextHopThrift n = nh;
+        n.weight = w;
+        next.insert(std::move(n));
+      }
+    }
+    if (next.empty()) continue;  // keep the old next-hops (RibPolicy.cpp:148-158)
+    r.nexthops = std::move(next);
+    return true;
+  }
+  return false;
+}
+
+std::vector<std::string> RibPolicy::applyPolicy(
+    std::map<std::string, RibUnicastEntry>& entries) const {
+  std::vector<std::string> updated;  // RibPolicy.cpp:231-249
+  if (!isActive()) return updated;
+  for (auto& [p, e] : entries) {
+    if (applyAction(e)) updated.push_back(p);
+  }
+  return updated;
+}
+
+}  // namespace openr_amd

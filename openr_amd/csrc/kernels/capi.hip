@@ -1,0 +1,136 @@
+// capi.hip — extern "C" entry points of libopenr_gpu.so (include/openr_gpu.h).
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "openr_gpu.h"
+
+namespace ogs {
+hipError_t launch_spf_routes(const ogs_graph& g, const ogs_prefix_table* pt,
+                             const ogs_unit* units, int nUnits, uint32_t flags,
+                             int W, const ogs_spf_out& out, hipStream_t stream,
+                             int* unsupported);
+}
+
+namespace {
+thread_local std::string g_lastError;
+
+int fail(int code, const std::string& msg) {
+  g_lastError = msg;
+  return code;
+}
+
+int hipFail(hipError_t e, const char* what) {
+  return fail(OGS_E_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+}  // namespace
+
+extern "C" {
+
+const char* ogs_version(void) { return "openr-gpu-spf 0.1 (gfx950)"; }
+
+const char* ogs_last_error(void) { return g_lastError.c_str(); }
+
+int ogs_device_count(int* count) {
+  if (!count) return fail(OGS_E_INVALID, "count is NULL");
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess) {
+    *count = 0;
+    return fail(OGS_E_NODEVICE, std::string("hipGetDeviceCount: ") +
+                                    hipGetErrorString(e));
+  }
+  *count = n;
+  return n > 0 ? OGS_OK : fail(OGS_E_NODEVICE, "no HIP device visible");
+}
+
+int ogs_set_device(int device) {
+  hipError_t e = hipSetDevice(device);
+  return e == hipSuccess ? OGS_OK : hipFail(e, "hipSetDevice");
+}
+
+int ogs_malloc(void** dptr, size_t bytes) {
+  if (!dptr) return fail(OGS_E_INVALID, "dptr is NULL");
+  *dptr = nullptr;
+  if (bytes == 0) return OGS_OK;
+  hipError_t e = hipMalloc(dptr, bytes);
+  if (e == hipErrorOutOfMemory) return fail(OGS_E_NOMEM, "hipMalloc: out of memory");
+  return e == hipSuccess ? OGS_OK : hipFail(e, "hipMalloc");
+}
+
+int ogs_free(void* dptr) {
+  if (!dptr) return OGS_OK;
+  hipError_t e = hipFree(dptr);
+  return e == hipSuccess ? OGS_OK : hipFail(e, "hipFree");
+}
+
+int ogs_memcpy_h2d(void* dst, const void* src, size_t bytes, void* stream) {
+  if (bytes == 0) return OGS_OK;
+  hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice,
+                                static_cast<hipStream_t>(stream));
+  return e == hipSuccess ? OGS_OK : hipFail(e, "hipMemcpyAsync(H2D)");
+}
+
+int ogs_memcpy_d2h(void* dst, const void* src, size_t bytes, void* stream) {
+  if (bytes == 0) return OGS_OK;
+  hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost,
+                                static_cast<hipStream_t>(stream));
+  return e == hipSuccess ? OGS_OK : hipFail(e, "hipMemcpyAsync(D2H)");
+}
+
+int ogs_memset(void* dst, int value, size_t bytes, void* stream) {
+  if (bytes == 0) return OGS_OK;
+  hipError_t e =
+      hipMemsetAsync(dst, value, bytes, static_cast<hipStream_t>(stream));
+  return e == hipSuccess ? OGS_OK : hipFail(e, "hipMemsetAsync");
+}
+
+int ogs_stream_sync(void* stream) {
+  hipError_t e = hipStreamSynchronize(static_cast<hipStream_t>(stream));
+  return e == hipSuccess ? OGS_OK : hipFail(e, "hipStreamSynchronize");
+}
+
+int ogs_nh_words_for_degree(int degree) {
+  if (degree < 0 || degree > OGS_MAX_DEGREE) return OGS_E_UNSUPPORTED;
+  const int words = (degree + 31) / 32;
+  for (int w : {1, 2, 4, 8, 16}) {
+    if (words <= w) return w;
+  }
+  return OGS_E_UNSUPPORTED;
+}
+
+int ogs_spf_routes(const ogs_graph* graph, const ogs_prefix_table* prefixes,
+                   const ogs_unit* units, int32_t n_units, uint32_t flags,
+                   int32_t nh_words, ogs_spf_out* out, void* stream) {
+  if (!graph || !out) return fail(OGS_E_INVALID, "graph/out is NULL");
+  if (n_units < 0) return fail(OGS_E_INVALID, "n_units < 0");
+  if (n_units == 0) return OGS_OK;
+  if (!units || !graph->node_base || !graph->row_ptr || !graph->node_flags) {
+    return fail(OGS_E_INVALID, "graph arrays are NULL");
+  }
+  if (graph->max_nodes <= 0 ||
+      uint32_t(graph->max_nodes) > OGS_MAX_NODES_PER_TOPO) {
+    return fail(OGS_E_UNSUPPORTED, "max_nodes outside (0, 2^21]");
+  }
+  if (prefixes && (!prefixes->pfx_base || !prefixes->adv_off ||
+                   !prefixes->adv_node || !prefixes->adv_metrics ||
+                   !prefixes->adv_min_nh || !prefixes->pfx_flags)) {
+    return fail(OGS_E_INVALID, "prefix table arrays are NULL");
+  }
+  if (ogs_nh_words_for_degree(nh_words * 32) != nh_words) {
+    return fail(OGS_E_UNSUPPORTED, "nh_words must be 1, 2, 4, 8 or 16");
+  }
+  int unsupported = 0;
+  hipError_t e = ogs::launch_spf_routes(
+      *graph, prefixes, units, n_units, flags, nh_words, *out,
+      static_cast<hipStream_t>(stream), &unsupported);
+  if (unsupported) {
+    return fail(OGS_E_UNSUPPORTED,
+                "topology too large for the LDS-resident SPF path");
+  }
+  return e == hipSuccess ? OGS_OK : hipFail(e, "spf_route launch");
+}
+
+}  // extern "C"

@@ -1,0 +1,447 @@
+// spf_route.hip — batched ECMP SPF + fused per-prefix RouteDb for gfx950.
+//
+// One work unit = (topology, source). Small topologies (<= 256 nodes) run
+// one WAVEFRONT per unit (4 independent units per 256-thread workgroup, no
+// workgroup barriers); larger ones run one WORKGROUP per unit. The whole
+// per-unit working set (distances, next-hop link-slot bitsets and, when it
+// fits, the topology's CSR) lives in LDS.
+//
+// SPF (replaces LinkState::runSpf, LinkState.cpp:720-820). For metrics >= 1
+// the reference's Dijkstra result equals the unique fixpoint of
+//   dist(v) = min_{u in P(v)} dist(u) + w(u,v)
+//   NH(v)   = U_{u tight pred of v} ( u == src ? {links src->v with
+//             w == dist(v)} : NH(u) )
+// where P(v) are neighbours over up links that relax (u == src or u not
+// hard-drained, LinkState.cpp:741-752). Because only the source has an empty
+// next-hop set, the reference's "if empty add otherNode" (808-811) is exactly
+// "the predecessor is the source". Next-hop sets are kept over the SOURCE's
+// link slots, so they already include the link filter of getNextHopsThrift
+// (SpfSolver.cpp:705-743: up && maxMetric + (shortest - dist(nbr)) ==
+// shortest <=> maxMetric == dist(nbr)). The fixpoint is reached by
+// pull-style Bellman-Ford rounds over LDS with in-place (chaotic) updates;
+// distances only decrease, so the loop stops at the first round in which no
+// node of the unit changes (wave ballot / workgroup barrier-OR).
+//
+// RouteDb (replaces SpfSolver::createRouteForPrefix, SpfSolver.cpp:160-311,
+// 455-639, and LsdbUtil selectRoutes/selectBestNodeArea, LsdbUtil.cpp:
+// 700-823), single area: one lane per prefix walks the prefix's advertiser
+// segment a few times (reachability + hard-drain filter, best-route
+// selection, shortest distance, next-hop union, min-nexthop) and writes one
+// compact route record (flags|best, metric, link-slot mask).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "openr_gpu.h"
+
+namespace ogs {
+
+constexpr int kBlock = 256;
+
+template <typename D>
+struct DistInf {
+  static constexpr D value = ~D(0);
+};
+
+// ---- unit-scope synchronisation ------------------------------------------
+template <int UT>
+struct UnitScope;
+
+template <>
+struct UnitScope<64> {  // one wavefront per unit: lockstep, no s_barrier
+  static __device__ __forceinline__ void sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  static __device__ __forceinline__ bool any(bool x) {
+    sync();
+    return __ballot(x) != 0ull;
+  }
+};
+
+template <>
+struct UnitScope<kBlock> {  // one workgroup per unit
+  static __device__ __forceinline__ void sync() { __syncthreads(); }
+  static __device__ __forceinline__ bool any(bool x) {
+    return __syncthreads_or(x) != 0;
+  }
+};
+
+__device__ __forceinline__ uint32_t edge_dst(uint32_t lo) {
+  return lo & OGS_EDGE_DST_MASK;
+}
+__device__ __forceinline__ uint32_t edge_rslot(uint32_t lo) {
+  return (lo >> OGS_EDGE_RSLOT_SHIFT) & OGS_EDGE_RSLOT_MASK;
+}
+
+struct RouteCfg {
+  bool enableV4, v4OverV6, bestRouteSel;
+};
+
+// Route for one prefix from the unit's SPF state (dist/nh in LDS).
+template <typename D, int W>
+__device__ void route_one(const ogs_prefix_table& pt, uint32_t gp, uint32_t s,
+                          const uint8_t* __restrict__ nflags, const D* dist,
+                          const uint32_t* nh, const RouteCfg& cfg,
+                          uint32_t& meta, D& metric, uint32_t (&mask)[W],
+                          uint32_t& selBits) {
+  constexpr D kInf = DistInf<D>::value;
+  meta = 0;
+  metric = kInf;
+  selBits = 0;
+#pragma unroll
+  for (int w = 0; w < W; ++w) mask[w] = 0;
+
+  // v4 gate (SpfSolver.cpp:169-176)
+  const bool isV4 = pt.pfx_flags[gp] & 1u;
+  if (isV4 && !cfg.enableV4 && !cfg.v4OverV6) {
+    meta = OGS_REASON_V4_DISABLED << OGS_ROUTE_REASON_SHIFT;
+    return;
+  }
+  const uint32_t a0 = pt.adv_off[gp], a1 = pt.adv_off[gp + 1];
+
+  // pass 1: reachability in the advertiser's area (single area => this
+  // SPF), localPrefixConsidered, hard-drain census (SpfSolver.cpp:194-214,
+  // 526-541)
+  bool local = false;
+  uint32_t nReach = 0, nReachUp = 0;
+  for (uint32_t a = a0; a < a1; ++a) {
+    const uint32_t n = pt.adv_node[a];
+    if (n == s) local = true;
+    if (n != OGS_NODE_NONE && dist[n] != kInf) {
+      ++nReach;
+      nReachUp += (nflags[n] & OGS_NODE_OVERLOADED) ? 0u : 1u;
+    }
+  }
+  if (local) meta |= OGS_ROUTE_LOCAL;
+  if (nReach == 0) {
+    meta |= OGS_REASON_UNREACHABLE << OGS_ROUTE_REASON_SHIFT;
+    return;
+  }
+  const bool dropOverloaded = nReachUp != 0;
+  auto filtered = [&](uint32_t n) {
+    return n != OGS_NODE_NONE && dist[n] != kInf &&
+        !(dropOverloaded && (nflags[n] & OGS_NODE_OVERLOADED));
+  };
+
+  // best-route selection (LsdbUtil.cpp:760-823, SHORTEST_DISTANCE):
+  // max (-(drained), path_pref, source_pref), then min distance
+  int32_t bD = INT32_MIN, bP = INT32_MIN, bS = INT32_MIN, bDist = INT32_MAX;
+  if (cfg.bestRouteSel) {
+    for (uint32_t a = a0; a < a1; ++a) {
+      const uint32_t n = pt.adv_node[a];
+      if (!filtered(n)) continue;
+      const int4 m = reinterpret_cast<const int4*>(pt.adv_metrics)[a];
+      const int32_t d =
+          -((m.x != 0 || (nflags[n] & OGS_NODE_SOFTDRAIN)) ? 1 : 0);
+      if (d > bD || (d == bD && (m.y > bP || (m.y == bP && m.z > bS)))) {
+        bD = d;
+        bP = m.y;
+        bS = m.z;
+      }
+    }
+    for (uint32_t a = a0; a < a1; ++a) {
+      const uint32_t n = pt.adv_node[a];
+      if (!filtered(n)) continue;
+      const int4 m = reinterpret_cast<const int4*>(pt.adv_metrics)[a];
+      const int32_t d =
+          -((m.x != 0 || (nflags[n] & OGS_NODE_SOFTDRAIN)) ? 1 : 0);
+      if (d == bD && m.y == bP && m.z == bS && m.w < bDist) bDist = m.w;
+    }
+  }
+  auto selected = [&](uint32_t a, uint32_t n) {
+    if (!filtered(n)) return false;
+    if (!cfg.bestRouteSel) return true;
+    const int4 m = reinterpret_cast<const int4*>(pt.adv_metrics)[a];
+    const int32_t d = -((m.x != 0 || (nflags[n] & OGS_NODE_SOFTDRAIN)) ? 1 : 0);
+    return d == bD && m.y == bP && m.z == bS && m.w == bDist;
+  };
+
+  // selected set: self?, best = smallest (node, area) key (node ids are name
+  // ranks), shortest distance over all selected names (SpfSolver.cpp:664-677)
+  bool self = false;
+  uint32_t bestIdx = 0, bestNode = 0xFFFFFFFFu;
+  D shortest = kInf;
+  for (uint32_t a = a0; a < a1; ++a) {
+    const uint32_t n = pt.adv_node[a];
+    if (!selected(a, n)) continue;
+    if (a - a0 < 32) selBits |= 1u << (a - a0);
+    if (n == s) self = true;
+    if (n < bestNode) {
+      bestNode = n;
+      bestIdx = a - a0;
+    }
+    const D dn = dist[n];
+    if (dn < shortest) shortest = dn;
+  }
+  meta |= OGS_ROUTE_SELECTED | (bestIdx << OGS_ROUTE_BEST_SHIFT);
+  if (nflags[bestNode] & (OGS_NODE_OVERLOADED | OGS_NODE_METRICINC)) {
+    meta |= OGS_ROUTE_DRAINED;  // isNodeDrained (SpfSolver.cpp:543-551)
+  }
+  if (self) {
+    meta |= OGS_REASON_SELF << OGS_ROUTE_REASON_SHIFT;
+    return;
+  }
+  // next-hop union over the min-cost destinations + min-nexthop threshold
+  bool hasMinNh = false;
+  int64_t minNh = INT64_MIN;
+  for (uint32_t a = a0; a < a1; ++a) {
+    const uint32_t n = pt.adv_node[a];
+    if (!selected(a, n)) continue;
+    const int64_t t = pt.adv_min_nh[a];
+    if (t != INT64_MIN && (!hasMinNh || t > minNh)) {
+      hasMinNh = true;
+      minNh = t;
+    }
+    if (dist[n] != shortest) continue;
+#pragma unroll
+    for (int w = 0; w < W; ++w) mask[w] |= nh[n * W + w];
+  }
+  uint32_t cnt = 0;
+#pragma unroll
+  for (int w = 0; w < W; ++w) cnt += __popc(mask[w]);
+  metric = shortest;
+  if (cnt == 0) {
+    meta |= OGS_REASON_NO_NEXTHOP << OGS_ROUTE_REASON_SHIFT;
+    return;
+  }
+  if (hasMinNh && static_cast<uint64_t>(minNh) > cnt) {  // SpfSolver.cpp:612
+    meta |= OGS_REASON_MIN_NEXTHOP << OGS_ROUTE_REASON_SHIFT;
+    return;
+  }
+  meta |= OGS_ROUTE_VALID;
+}
+
+template <typename D, int W, int UT, bool STAGE>
+__global__ __launch_bounds__(kBlock) void spf_route_kernel(
+    ogs_graph g, ogs_prefix_table pt, int hasPrefixes,
+    const ogs_unit* __restrict__ units, int nUnits, uint32_t flags,
+    ogs_spf_out out, uint32_t ldsPerUnit) {
+  using Scope = UnitScope<UT>;
+  constexpr D kInf = DistInf<D>::value;
+  constexpr int kUnitsPerBlock = kBlock / UT;
+  const int uib = threadIdx.x / UT;
+  const int lane = threadIdx.x % UT;
+  const int uidx = blockIdx.x * kUnitsPerBlock + uib;
+  if (uidx >= nUnits) return;  // whole unit exits together
+
+  const ogs_unit unit = units[uidx];
+  const uint32_t nb = g.node_base[unit.topo];
+  const uint32_t N = g.node_base[unit.topo + 1] - nb;
+  const uint32_t s = unit.src;
+  const uint32_t* __restrict__ gRow = g.row_ptr + nb;
+  const uint8_t* __restrict__ nflags = g.node_flags + nb;
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* base = smem + uib * ldsPerUnit;
+  D* dist = reinterpret_cast<D*>(base);
+  const uint32_t distBytes = (N * sizeof(D) + 15u) & ~15u;
+  uint32_t* nh = reinterpret_cast<uint32_t*>(base + distBytes);
+  const uint32_t nhBytes = (N * W * 4u + 15u) & ~15u;
+
+  const uint32_t* rowp;
+  const uint64_t* edg;
+  if constexpr (STAGE) {
+    uint32_t* lrow = reinterpret_cast<uint32_t*>(base + distBytes + nhBytes);
+    const uint32_t rowBytes = ((N + 1) * 4u + 15u) & ~15u;
+    uint64_t* ledg =
+        reinterpret_cast<uint64_t*>(base + distBytes + nhBytes + rowBytes);
+    const uint32_t e0 = gRow[0];
+    const uint32_t E = gRow[N] - e0;
+    for (uint32_t i = lane; i <= N; i += UT) lrow[i] = gRow[i] - e0;
+    for (uint32_t i = lane; i < E; i += UT) ledg[i] = g.edges[e0 + i];
+    rowp = lrow;
+    edg = ledg;
+  } else {
+    rowp = gRow;
+    edg = g.edges;
+  }
+  for (uint32_t v = lane; v < N; v += UT) {
+    dist[v] = (v == s) ? D(0) : kInf;
+#pragma unroll
+    for (int w = 0; w < W; ++w) nh[v * W + w] = 0u;
+  }
+  Scope::sync();
+
+  const bool hop = flags & OGS_F_HOP_METRIC;
+  // ---- SPF: pull-style relaxation rounds to the fixpoint ------------------
+  for (;;) {
+    bool changed = false;
+    for (uint32_t v = lane; v < N; v += UT) {
+      if (v == s) continue;
+      D best = kInf;
+      uint32_t m[W];
+#pragma unroll
+      for (int w = 0; w < W; ++w) m[w] = 0u;
+      const uint32_t eb = rowp[v], ee = rowp[v + 1];
+      for (uint32_t e = eb; e < ee; ++e) {
+        const uint64_t ed = edg[e];
+        const uint32_t lo = static_cast<uint32_t>(ed);
+        if (lo & OGS_EDGE_DOWN) continue;
+        const uint32_t u = edge_dst(lo);
+        const bool fromSrc = (u == s);
+        if ((lo & OGS_EDGE_DST_OVERLOADED) && !fromSrc) continue;
+        const D du = dist[u];
+        if (du == kInf) continue;
+        const D cand = du + (hop ? D(1) : static_cast<D>(ed >> 32));
+        if (cand > best) continue;
+        uint32_t c[W];
+        if (fromSrc) {
+          const uint32_t slot = edge_rslot(lo);
+#pragma unroll
+          for (int w = 0; w < W; ++w) {
+            c[w] = (int(slot >> 5) == w) ? (1u << (slot & 31u)) : 0u;
+          }
+        } else {
+#pragma unroll
+          for (int w = 0; w < W; ++w) c[w] = nh[u * W + w];
+        }
+        if (cand < best) {
+          best = cand;
+#pragma unroll
+          for (int w = 0; w < W; ++w) m[w] = c[w];
+        } else {
+#pragma unroll
+          for (int w = 0; w < W; ++w) m[w] |= c[w];
+        }
+      }
+      bool diff = best != dist[v];
+#pragma unroll
+      for (int w = 0; w < W; ++w) diff |= (m[w] != nh[v * W + w]);
+      if (diff) {
+        dist[v] = best;
+#pragma unroll
+        for (int w = 0; w < W; ++w) nh[v * W + w] = m[w];
+        changed = true;
+      }
+    }
+    if (!Scope::any(changed)) break;
+  }
+
+  // ---- SPF outputs (coalesced) -------------------------------------------
+  const uint32_t Sn = g.max_nodes;
+  if (out.dist) {
+    D* od = reinterpret_cast<D*>(out.dist) + size_t(uidx) * Sn;
+    for (uint32_t v = lane; v < N; v += UT) od[v] = dist[v];
+  }
+  if (out.nh) {
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+      uint32_t* on = out.nh + (size_t(uidx) * W + w) * Sn;
+      for (uint32_t v = lane; v < N; v += UT) on[v] = nh[v * W + w];
+    }
+  }
+  if (!hasPrefixes) return;
+
+  // ---- fused RouteDb ------------------------------------------------------
+  const RouteCfg cfg{(flags & OGS_F_ENABLE_V4) != 0,
+                     (flags & OGS_F_V4_OVER_V6) != 0,
+                     (flags & OGS_F_BEST_ROUTE_SELECTION) != 0};
+  const uint32_t p0 = pt.pfx_base[unit.topo];
+  const uint32_t P = pt.pfx_base[unit.topo + 1] - p0;
+  const uint32_t Sp = pt.max_prefixes;
+  for (uint32_t p = lane; p < P; p += UT) {
+    uint32_t meta, selBits;
+    D metric;
+    uint32_t mask[W];
+    route_one<D, W>(pt, p0 + p, s, nflags, dist, nh, cfg, meta, metric, mask,
+                    selBits);
+    const size_t o = size_t(uidx) * Sp + p;
+    if (out.meta) out.meta[o] = meta;
+    if (out.metric) reinterpret_cast<D*>(out.metric)[o] = metric;
+    if (out.sel) out.sel[o] = selBits;
+    if (out.mask) {
+#pragma unroll
+      for (int w = 0; w < W; ++w) {
+        out.mask[(size_t(uidx) * W + w) * Sp + p] = mask[w];
+      }
+    }
+  }
+}
+
+// ---- host-side launch selection -------------------------------------------
+template <typename D, int W, int UT, bool STAGE>
+hipError_t launch_one(const ogs_graph& g, const ogs_prefix_table& pt,
+                      int hasPrefixes, const ogs_unit* units, int nUnits,
+                      uint32_t flags, const ogs_spf_out& out,
+                      uint32_t ldsPerUnit, hipStream_t stream) {
+  constexpr int upb = kBlock / UT;
+  const int grid = (nUnits + upb - 1) / upb;
+  const size_t lds = size_t(ldsPerUnit) * upb;
+  auto k = spf_route_kernel<D, W, UT, STAGE>;
+  if (lds > 64 * 1024) {
+    hipError_t e = hipFuncSetAttribute(
+        reinterpret_cast<const void*>(k),
+        hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), lds, stream, g, pt,
+                     hasPrefixes, units, nUnits, flags, out, ldsPerUnit);
+  return hipGetLastError();
+}
+
+uint32_t lds_per_unit(int maxNodes, int maxEdges, int W, int distBytes,
+                      bool stage) {
+  auto al = [](uint64_t x) { return (x + 15u) & ~uint64_t(15); };
+  uint64_t b = al(uint64_t(maxNodes) * distBytes) + al(uint64_t(maxNodes) * W * 4);
+  if (stage) b += al(uint64_t(maxNodes + 1) * 4) + al(uint64_t(maxEdges) * 8);
+  return static_cast<uint32_t>(b);
+}
+
+template <typename D, int W>
+hipError_t dispatch_w(const ogs_graph& g, const ogs_prefix_table& pt,
+                      int hasPrefixes, const ogs_unit* units, int nUnits,
+                      uint32_t flags, const ogs_spf_out& out,
+                      hipStream_t stream, int* unsupported) {
+  const int wave = g.max_nodes <= 256;
+  const uint32_t staged = lds_per_unit(g.max_nodes, g.max_edges, W, sizeof(D), true);
+  const uint32_t bare = lds_per_unit(g.max_nodes, g.max_edges, W, sizeof(D), false);
+  constexpr uint32_t kBudget = 160 * 1024;
+  if (wave && staged * 4 <= kBudget / 2) {
+    return launch_one<D, W, 64, true>(g, pt, hasPrefixes, units, nUnits, flags,
+                                      out, staged, stream);
+  }
+  if (staged <= kBudget / 2) {
+    return launch_one<D, W, kBlock, true>(g, pt, hasPrefixes, units, nUnits,
+                                          flags, out, staged, stream);
+  }
+  if (bare <= kBudget) {
+    return launch_one<D, W, kBlock, false>(g, pt, hasPrefixes, units, nUnits,
+                                           flags, out, bare, stream);
+  }
+  *unsupported = 1;  // > ~10k nodes per topology: needs the global path
+  return hipSuccess;
+}
+
+template <typename D>
+hipError_t dispatch_d(int W, const ogs_graph& g, const ogs_prefix_table& pt,
+                      int hasPrefixes, const ogs_unit* units, int nUnits,
+                      uint32_t flags, const ogs_spf_out& out,
+                      hipStream_t stream, int* unsupported) {
+  switch (W) {
+    case 1: return dispatch_w<D, 1>(g, pt, hasPrefixes, units, nUnits, flags, out, stream, unsupported);
+    case 2: return dispatch_w<D, 2>(g, pt, hasPrefixes, units, nUnits, flags, out, stream, unsupported);
+    case 4: return dispatch_w<D, 4>(g, pt, hasPrefixes, units, nUnits, flags, out, stream, unsupported);
+    case 8: return dispatch_w<D, 8>(g, pt, hasPrefixes, units, nUnits, flags, out, stream, unsupported);
+    case 16: return dispatch_w<D, 16>(g, pt, hasPrefixes, units, nUnits, flags, out, stream, unsupported);
+    default: *unsupported = 1; return hipSuccess;
+  }
+}
+
+hipError_t launch_spf_routes(const ogs_graph& g, const ogs_prefix_table* pt,
+                             const ogs_unit* units, int nUnits,
+                             uint32_t flags, int W, const ogs_spf_out& out,
+                             hipStream_t stream, int* unsupported) {
+  ogs_prefix_table empty{};
+  const ogs_prefix_table& p = pt ? *pt : empty;
+  const int hasPrefixes = pt ? 1 : 0;
+  if (flags & OGS_F_WIDE_METRIC) {
+    return dispatch_d<uint64_t>(W, g, p, hasPrefixes, units, nUnits, flags,
+                                out, stream, unsupported);
+  }
+  return dispatch_d<uint32_t>(W, g, p, hasPrefixes, units, nUnits, flags, out,
+                              stream, unsupported);
+}
+
+}  // namespace ogs

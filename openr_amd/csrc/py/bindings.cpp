@@ -1,0 +1,775 @@
+// openr_amd._decision — Python binding of the GPU drop-in (product path).
+// Exposes the same surface as the CPU oracle binding so tests can drive one
+// scenario through both. Every computation goes through libopenr_gpu.so.
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <sstream>
+
+#include "../gen/topogen.h"
+#include "../host/decision.h"
+
+namespace py = pybind11;
+using namespace openr_amd;
+
+PYBIND11_MAKE_OPAQUE(openr_amd::AreaLinkStates)
+
+namespace {
+
+template <typename T>
+T get(const py::dict& d, const char* k, T dflt) {
+  if (d.contains(k) && !d[k].is_none()) return d[k].cast<T>();
+  return dflt;
+}
+
+Adjacency toAdj(const py::dict& d) {
+  Adjacency a;
+  a.otherNodeName = get<std::string>(d, "otherNodeName", "");
+  a.ifName = get<std::string>(d, "ifName", "");
+  a.nextHopV6 = get<std::string>(d, "nextHopV6", "");
+  a.nextHopV4 = get<std::string>(d, "nextHopV4", "");
+  a.metric = get<int32_t>(d, "metric", 0);
+  a.adjLabel = get<int32_t>(d, "adjLabel", 0);
+  a.isOverloaded = get<bool>(d, "isOverloaded", false);
+  a.rtt = get<int32_t>(d, "rtt", 0);
+  a.timestamp = get<int64_t>(d, "timestamp", 0);
+  a.weight = get<int64_t>(d, "weight", 1);
+  a.otherIfName = get<std::string>(d, "otherIfName", "");
+  a.adjOnlyUsedByOtherNode = get<bool>(d, "adjOnlyUsedByOtherNode", false);
+  return a;
+}
+
+AdjacencyDatabase toAdjDb(const py::dict& d) {
+  AdjacencyDatabase db;
+  db.thisNodeName = get<std::string>(d, "thisNodeName", "");
+  db.isOverloaded = get<bool>(d, "isOverloaded", false);
+  db.nodeLabel = get<int32_t>(d, "nodeLabel", 0);
+  db.area = get<std::string>(d, "area", "");
+  db.nodeMetricIncrementVal = get<int32_t>(d, "nodeMetricIncrementVal", 0);
+  if (d.contains("adjacencies")) {
+    for (auto h : d["adjacencies"]) db.adjacencies.push_back(toAdj(h.cast<py::dict>()));
+  }
+  return db;
+}
+
+PrefixEntry toEntry(const py::dict& d) {
+  PrefixEntry e;
+  e.prefix = get<std::string>(d, "prefix", "");
+  e.type = get<int32_t>(d, "type", 0);
+  e.forwardingType = get<int32_t>(d, "forwardingType", 0);
+  e.forwardingAlgorithm = get<int32_t>(d, "forwardingAlgorithm", 0);
+  if (d.contains("minNexthop") && !d["minNexthop"].is_none()) {
+    e.minNexthop = d["minNexthop"].cast<int64_t>();
+  }
+  if (d.contains("metrics")) {
+    py::dict m = d["metrics"];
+    e.metrics.version = get<int32_t>(m, "version", 1);
+    e.metrics.drain_metric = get<int32_t>(m, "drain_metric", 0);
+    e.metrics.path_preference = get<int32_t>(m, "path_preference", 0);
+    e.metrics.source_preference = get<int32_t>(m, "source_preference", 0);
+    e.metrics.distance = get<int32_t>(m, "distance", 0);
+  }
+  if (d.contains("tags")) {
+    for (auto t : d["tags"]) e.tags.insert(t.cast<std::string>());
+  }
+  if (d.contains("area_stack")) {
+    for (auto t : d["area_stack"]) e.area_stack.push_back(t.cast<std::string>());
+  }
+  if (d.contains("weight") && !d["weight"].is_none()) e.weight = d["weight"].cast<int64_t>();
+  return e;
+}
+
+py::dict fromEntry(const PrefixEntry& e) {
+  py::dict d, m;
+  d["prefix"] = e.prefix;
+  d["type"] = e.type;
+  d["forwardingType"] = e.forwardingType;
+  d["forwardingAlgorithm"] = e.forwardingAlgorithm;
+  d["minNexthop"] = e.minNexthop ? py::cast(*e.minNexthop) : py::none();
+  m["version"] = e.metrics.version;
+  m["drain_metric"] = e.metrics.drain_metric;
+  m["path_preference"] = e.metrics.path_preference;
+  m["source_preference"] = e.metrics.source_preference;
+  m["distance"] = e.metrics.distance;
+  d["metrics"] = m;
+  d["tags"] = py::cast(std::vector<std::string>(e.tags.begin(), e.tags.end()));
+  d["area_stack"] = py::cast(e.area_stack);
+  d["weight"] = e.weight ? py::cast(*e.weight) : py::none();
+  return d;
+}
+
+py::object optStr(const std::optional<std::string>& s) {
+  return s ? py::cast(*s) : py::none();
+}
+
+py::tuple fromNh(const NextHopThrift& nh) {
+  py::object act = py::none();
+  if (nh.mplsAction) {
+    py::object push = py::none();
+    if (nh.mplsAction->pushLabels) push = py::tuple(py::cast(*nh.mplsAction->pushLabels));
+    act = py::make_tuple(nh.mplsAction->action,
+                         nh.mplsAction->swapLabel ? py::cast(*nh.mplsAction->swapLabel)
+                                                  : py::none(),
+                         push);
+  }
+  return py::make_tuple(nh.address, optStr(nh.ifName), nh.weight, act, nh.metric,
+                        optStr(nh.area), optStr(nh.neighborNodeName));
+}
+
+NextHopThrift toNh(const py::tuple& t) {
+  NextHopThrift nh;
+  nh.address = t[0].cast<std::string>();
+  if (!t[1].is_none()) nh.ifName = t[1].cast<std::string>();
+  nh.weight = t[2].cast<int32_t>();
+  if (!t[3].is_none()) {
+    py::tuple a = t[3];
+    MplsAction m;
+    m.action = a[0].cast<int32_t>();
+    if (!a[1].is_none()) m.swapLabel = a[1].cast<int32_t>();
+    if (!a[2].is_none()) m.pushLabels = a[2].cast<std::vector<int32_t>>();
+    nh.mplsAction = m;
+  }
+  nh.metric = t[4].cast<int32_t>();
+  if (!t[5].is_none()) nh.area = t[5].cast<std::string>();
+  if (!t[6].is_none()) nh.neighborNodeName = t[6].cast<std::string>();
+  return nh;
+}
+
+py::frozenset fromNhSet(const NextHops& s) {
+  py::set out;
+  for (const auto& nh : s) out.add(fromNh(nh));
+  return py::frozenset(out);
+}
+
+py::dict fromRoute(const RibUnicastEntry& r) {
+  py::dict d;
+  d["prefix"] = r.prefix;
+  d["nexthops"] = fromNhSet(r.nexthops);
+  d["igpCost"] = r.igpCost;
+  d["bestPrefixEntry"] = fromEntry(r.bestPrefixEntry);
+  d["bestArea"] = r.bestArea;
+  d["doNotInstall"] = r.doNotInstall;
+  d["counterID"] = optStr(r.counterID);
+  d["localRouteConsidered"] = r.localRouteConsidered;
+  return d;
+}
+
+RibUnicastEntry toRoute(const py::dict& d) {
+  RibUnicastEntry r;
+  r.prefix = d["prefix"].cast<std::string>();
+  for (auto h : d["nexthops"]) r.nexthops.insert(toNh(h.cast<py::tuple>()));
+  r.igpCost = get<unsigned>(d, "igpCost", 0);
+  if (d.contains("bestPrefixEntry")) r.bestPrefixEntry = toEntry(d["bestPrefixEntry"]);
+  r.bestArea = get<std::string>(d, "bestArea", "");
+  r.doNotInstall = get<bool>(d, "doNotInstall", false);
+  if (d.contains("counterID") && !d["counterID"].is_none()) {
+    r.counterID = d["counterID"].cast<std::string>();
+  }
+  r.localRouteConsidered = get<bool>(d, "localRouteConsidered", false);
+  return r;
+}
+
+py::dict fromChange(const LinkState::LinkStateChange& c) {
+  py::dict d;
+  d["topologyChanged"] = c.topologyChanged;
+  d["linkAttributesChanged"] = c.linkAttributesChanged;
+  d["nodeLabelChanged"] = c.nodeLabelChanged;
+  d["addedLinks"] = c.addedLinks.size();
+  return d;
+}
+
+py::dict fromLink(const Link& l) {
+  py::dict d;
+  const auto& k = l.key();
+  d["n1"] = k.first.first;
+  d["if1"] = k.first.second;
+  d["n2"] = k.second.first;
+  d["if2"] = k.second.second;
+  d["m1"] = l.getMetricFromNode(k.first.first);
+  d["m2"] = l.getMetricFromNode(k.second.first);
+  d["up"] = l.isUp();
+  d["usable"] = l.getUsability();
+  d["area"] = l.getArea();
+  return d;
+}
+
+py::dict fromUpdate(const DecisionRouteUpdate& u) {
+  py::dict d, uu, mu;
+  for (const auto& [p, e] : u.unicastRoutesToUpdate) uu[py::str(p)] = fromRoute(e);
+  for (const auto& [l, e] : u.mplsRoutesToUpdate) mu[py::int_(l)] = fromNhSet(e.nexthops);
+  d["unicastRoutesToUpdate"] = uu;
+  d["unicastRoutesToDelete"] = py::cast(u.unicastRoutesToDelete);
+  d["mplsRoutesToUpdate"] = mu;
+  d["mplsRoutesToDelete"] = py::cast(u.mplsRoutesToDelete);
+  return d;
+}
+
+// Canonical text of a route DB: byte-identical format to the oracle's.
+std::string canonical(const DecisionRouteDb& db) {
+  std::ostringstream os;
+  for (const auto& [p, r] : db.unicastRoutes) {
+    os << "U " << p << " c=" << r.igpCost << " a=" << r.bestArea
+       << " dm=" << r.bestPrefixEntry.metrics.drain_metric
+       << " bp=" << r.bestPrefixEntry.prefix << " l=" << r.localRouteConsidered
+       << "\n";
+    for (const auto& nh : r.nexthops) {
+      os << "  " << nh.address << "%" << nh.ifName.value_or("") << " m=" << nh.metric
+         << " w=" << nh.weight << " n=" << nh.neighborNodeName.value_or("")
+         << " ar=" << nh.area.value_or("");
+      if (nh.mplsAction) {
+        os << " act=" << nh.mplsAction->action << ":"
+           << nh.mplsAction->swapLabel.value_or(-1);
+      }
+      os << "\n";
+    }
+  }
+  for (const auto& [l, r] : db.mplsRoutes) {
+    os << "M " << l << "\n";
+    for (const auto& nh : r.nexthops) {
+      os << "  " << nh.address << "%" << nh.ifName.value_or("") << " m=" << nh.metric
+         << " n=" << nh.neighborNodeName.value_or("");
+      if (nh.mplsAction) {
+        os << " act=" << nh.mplsAction->action << ":"
+           << nh.mplsAction->swapLabel.value_or(-1);
+      }
+      os << "\n";
+    }
+  }
+  return os.str();
+}
+
+// ------------------------------------------------------ generated LSDBs ---
+void loadLsdb(const topogen::Lsdb& g, LinkState& ls, PrefixState& ps) {
+  for (const auto& d : g.adjDbs) {
+    AdjacencyDatabase db;
+    db.thisNodeName = d.thisNodeName;
+    db.isOverloaded = d.isOverloaded;
+    db.nodeLabel = d.nodeLabel;
+    db.area = g.area;
+    db.nodeMetricIncrementVal = d.nodeMetricIncrementVal;
+    for (const auto& a : d.adjs) {
+      Adjacency x;
+      x.otherNodeName = a.otherNodeName;
+      x.ifName = a.ifName;
+      x.otherIfName = a.otherIfName;
+      x.nextHopV6 = a.nextHopV6;
+      x.nextHopV4 = a.nextHopV4;
+      x.metric = a.metric;
+      x.adjLabel = a.adjLabel;
+      x.isOverloaded = a.isOverloaded;
+      x.weight = a.weight;
+      db.adjacencies.push_back(x);
+    }
+    ls.updateAdjacencyDatabase(db, g.area);
+  }
+  for (const auto& p : g.prefixes) {
+    PrefixEntry e;
+    e.prefix = p.prefix;
+    e.type = 1;  // LOOPBACK (RoutingBenchmarkUtils.cpp:281)
+    e.metrics.path_preference = p.path_preference;
+    e.metrics.source_preference = p.source_preference;
+    e.metrics.distance = p.distance;
+    ps.updatePrefix(p.node, g.area, e);
+  }
+}
+
+topogen::GridOpts gridOpts(const py::dict& d) {
+  topogen::GridOpts o;
+  o.n = get<int>(d, "n", 10);
+  o.prefixesPerNode = get<int>(d, "prefixesPerNode", 1);
+  o.prefixSeed = get<uint64_t>(d, "prefixSeed", 0xC1);
+  o.metricSeed = get<uint64_t>(d, "metricSeed", 0);
+  o.metricMax = get<int>(d, "metricMax", 100);
+  o.adjOverloadPermille = get<int>(d, "adjOverloadPermille", 0);
+  o.nodeOverloadPermille = get<int>(d, "nodeOverloadPermille", 0);
+  o.overloadSeed = get<uint64_t>(d, "overloadSeed", 0);
+  return o;
+}
+
+topogen::Lsdb genLsdb(const std::string& kind, const py::dict& d) {
+  if (kind == "grid") return topogen::grid(gridOpts(d));
+  if (kind == "fabric") {
+    topogen::FabricOpts o;
+    o.pods = get<int>(d, "pods", 32);
+    o.planes = get<int>(d, "planes", 8);
+    o.sswPerPlane = get<int>(d, "sswPerPlane", 36);
+    o.rswPerPod = get<int>(d, "rswPerPod", 48);
+    o.full = get<bool>(d, "full", true);
+    o.prefixesPerNode = get<int>(d, "prefixesPerNode", 1);
+    o.prefixSeed = get<uint64_t>(d, "prefixSeed", 0xC3);
+    return topogen::fabric(o);
+  }
+  if (kind == "wan") {
+    topogen::WanOpts o;
+    o.nodes = get<int>(d, "nodes", 2000);
+    o.k = get<int>(d, "k", 3);
+    o.seed = get<uint64_t>(d, "seed", 0xC4);
+    o.prefixesPerNode = get<int>(d, "prefixesPerNode", 1);
+    return topogen::wan(o);
+  }
+  throw std::invalid_argument("unknown generator " + kind);
+}
+
+// ---------------------------------------------------------- BatchRunner ---
+// Many (topology, source) units flattened into one graph batch and solved by
+// one launch of the fused kernel. Owns its device memory.
+class BatchRunner {
+ public:
+  BatchRunner(bool enableV4, bool sr, bool brs)
+      : enableV4_(enableV4), sr_(sr), brs_(brs) {}
+
+  void addLsdb(const topogen::Lsdb& g, const std::vector<std::string>& sources) {
+    auto w = std::make_unique<Topo>();
+    w->als.emplace(g.area, LinkState(g.area, "test_node"));
+    w->area = g.area;
+    LinkState& ls = w->als.at(g.area);
+    loadLsdb(g, ls, w->ps);
+    const FlatTopology& f = ls.flat();
+    w->table.build(w->ps);
+    const uint32_t t = uint32_t(topos_.size());
+    hb_.append(f, w->ps, g.area);
+    for (const auto& s : sources) {
+      units_.push_back({t, f.id.at(s)});
+      unitSrc_.push_back(s);
+      const int deg = int(f.rowPtr[f.id.at(s) + 1] - f.rowPtr[f.id.at(s)]);
+      W_ = std::max(W_, std::max(1, ogs_nh_words_for_degree(deg)));
+    }
+    wide_ |= wideDistancesNeeded(f);
+    topos_.push_back(std::move(w));
+  }
+
+  void upload() {
+    if (hb_.hasZeroMetric) throw std::domain_error("zero metric in batch");
+    dNodeBase_.upload(hb_.nodeBase.data(), hb_.nodeBase.size());
+    dRow_.upload(hb_.rowPtr.data(), hb_.rowPtr.size());
+    dEdges_.upload(hb_.edges.data(), std::max<size_t>(hb_.edges.size(), 1));
+    dFlags_.upload(hb_.nodeFlags.data(), std::max<size_t>(hb_.nodeFlags.size(), 1));
+    dPfxBase_.upload(hb_.pfxBase.data(), hb_.pfxBase.size());
+    dAdvOff_.upload(hb_.advOff.data(), hb_.advOff.size());
+    dAdvNode_.upload(hb_.advNode.data(), std::max<size_t>(hb_.advNode.size(), 1));
+    dAdvMetrics_.upload(hb_.advMetrics.data(), std::max<size_t>(hb_.advMetrics.size(), 4));
+    dAdvMinNh_.upload(hb_.advMinNh.data(), std::max<size_t>(hb_.advMinNh.size(), 1));
+    dPfxFlags_.upload(hb_.pfxFlags.data(), std::max<size_t>(hb_.pfxFlags.size(), 1));
+    dUnits_.upload(units_.data(), std::max<size_t>(units_.size(), 1));
+    const size_t U = units_.size(), db = wide_ ? 8 : 4;
+    const size_t Sn = hb_.maxNodes, Sp = std::max(hb_.maxPrefixes, 1);
+    dDist_.resize(U * Sn * db);
+    dNh_.resize(U * W_ * Sn * 4);
+    dMeta_.resize(U * Sp * 4);
+    dMetric_.resize(U * Sp * db);
+    dMask_.resize(U * W_ * Sp * 4);
+    dSel_.resize(U * Sp * 4);
+  }
+
+  void run() {
+    ogs_graph g = graph();
+    ogs_prefix_table pt = table();
+    ogs_spf_out out{dDist_.get(), dNh_.as<uint32_t>(), dMeta_.as<uint32_t>(),
+                    dMetric_.get(), dMask_.as<uint32_t>(), dSel_.as<uint32_t>()};
+    ogsCheck(ogs_spf_routes(&g, hb_.maxPrefixes ? &pt : nullptr,
+                            dUnits_.as<ogs_unit>(), int32_t(units_.size()),
+                            flags(), W_, &out, nullptr),
+             "ogs_spf_routes");
+    ogsCheck(ogs_stream_sync(nullptr), "ogs_stream_sync");
+  }
+
+  void download() {
+    const size_t U = units_.size(), Sn = hb_.maxNodes,
+                 Sp = std::max(hb_.maxPrefixes, 1);
+    auto widen = [&](const DeviceBuffer& b, size_t n, std::vector<uint64_t>& v) {
+      v.resize(n);
+      if (wide_) {
+        b.download(v.data(), n);
+      } else {
+        std::vector<uint32_t> t(n);
+        b.download(t.data(), n);
+        for (size_t i = 0; i < n; ++i) v[i] = t[i] == 0xFFFFFFFFu ? ~0ull : t[i];
+      }
+    };
+    widen(dDist_, U * Sn, dist_);
+    nh_.resize(U * W_ * Sn);
+    dNh_.download(nh_.data(), nh_.size());
+    meta_.resize(U * Sp);
+    dMeta_.download(meta_.data(), meta_.size());
+    widen(dMetric_, U * Sp, metric_);
+    mask_.resize(U * W_ * Sp);
+    dMask_.download(mask_.data(), mask_.size());
+    sel_.resize(U * Sp);
+    dSel_.download(sel_.data(), sel_.size());
+    ogsCheck(ogs_stream_sync(nullptr), "ogs_stream_sync");
+  }
+
+  DecisionRouteDb routeDb(size_t u) const {
+    const size_t Sn = hb_.maxNodes, Sp = std::max(hb_.maxPrefixes, 1);
+    const Topo& t = *topos_.at(units_.at(u).topo);
+    const LinkState& ls = t.als.at(t.area);
+    UnitView v;
+    v.W = W_;
+    v.N = uint32_t(ls.flat().names.size());
+    v.P = uint32_t(t.table.prefixes.size());
+    v.dist = &dist_[u * Sn];
+    v.nh = &nh_[u * W_ * Sn];
+    v.nhStride = Sn;
+    v.meta = &meta_[u * Sp];
+    v.metric = &metric_[u * Sp];
+    v.mask = &mask_[u * W_ * Sp];
+    v.maskStride = Sp;
+    v.sel = &sel_[u * Sp];
+    static const std::map<std::string, RibUnicastEntry> kNoStatics;
+    return materializeRouteDb(ls, ls.flat(), t.area, unitSrc_[u], v, t.table,
+                              false, sr_, kNoStatics, nullptr);
+  }
+
+  uint32_t flags() const {
+    return (enableV4_ ? OGS_F_ENABLE_V4 : 0u) |
+        (brs_ ? OGS_F_BEST_ROUTE_SELECTION : 0u) |
+        (wide_ ? OGS_F_WIDE_METRIC : 0u);
+  }
+  size_t numUnits() const { return units_.size(); }
+  const HostBatch& host() const { return hb_; }
+  const std::vector<ogs_unit>& units() const { return units_; }
+  int nhWords() const { return W_; }
+  bool wide() const { return wide_; }
+  const std::vector<uint64_t>& dist() const { return dist_; }
+  const std::vector<uint32_t>& meta() const { return meta_; }
+  const std::vector<uint64_t>& metric() const { return metric_; }
+
+ private:
+  ogs_graph graph() const {
+    ogs_graph g{};
+    g.num_topos = int32_t(topos_.size());
+    g.max_nodes = hb_.maxNodes;
+    g.max_edges = hb_.maxEdges;
+    g.node_base = dNodeBase_.as<uint32_t>();
+    g.row_ptr = dRow_.as<uint32_t>();
+    g.edges = dEdges_.as<uint64_t>();
+    g.node_flags = dFlags_.as<uint8_t>();
+    return g;
+  }
+  ogs_prefix_table table() const {
+    ogs_prefix_table pt{};
+    pt.max_prefixes = hb_.maxPrefixes;
+    pt.pfx_base = dPfxBase_.as<uint32_t>();
+    pt.adv_off = dAdvOff_.as<uint32_t>();
+    pt.adv_node = dAdvNode_.as<uint32_t>();
+    pt.adv_metrics = dAdvMetrics_.as<int32_t>();
+    pt.adv_min_nh = dAdvMinNh_.as<int64_t>();
+    pt.pfx_flags = dPfxFlags_.as<uint8_t>();
+    return pt;
+  }
+  struct Topo {
+    AreaLinkStates als;
+    std::string area;
+    PrefixState ps;
+    PrefixHostTable table;
+  };
+  bool enableV4_, sr_, brs_;
+  std::vector<std::unique_ptr<Topo>> topos_;
+  HostBatch hb_;
+  std::vector<ogs_unit> units_;
+  std::vector<std::string> unitSrc_;
+  int W_{1};
+  bool wide_{false};
+  DeviceBuffer dNodeBase_, dRow_, dEdges_, dFlags_, dPfxBase_, dAdvOff_,
+      dAdvNode_, dAdvMetrics_, dAdvMinNh_, dPfxFlags_, dUnits_, dDist_, dNh_,
+      dMeta_, dMetric_, dMask_, dSel_;
+  std::vector<uint64_t> dist_, metric_;
+  std::vector<uint32_t> nh_, meta_, mask_, sel_;
+};
+
+template <typename T>
+py::array_t<T> npcopy(const std::vector<T>& v) {
+  py::array_t<T> a(v.size());
+  std::copy(v.begin(), v.end(), a.mutable_data());
+  return a;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_decision, m) {
+  m.doc() = "MI355X (gfx950) SPF + RouteDb engine: Open/R Decision drop-in";
+
+  m.def("device_count", []() {
+    int n = 0;
+    ogs_device_count(&n);
+    return n;
+  });
+  m.def("version", []() { return std::string(ogs_version()); });
+
+  py::class_<LinkState>(m, "LinkState")
+      .def(py::init<const std::string&, const std::string&>())
+      .def("updateAdjacencyDatabase",
+           [](LinkState& s, py::dict db, const std::string& area, bool init) {
+             return fromChange(s.updateAdjacencyDatabase(toAdjDb(db), area, init));
+           },
+           py::arg("db"), py::arg("area"), py::arg("inInitialization") = false)
+      .def("deleteAdjacencyDatabase",
+           [](LinkState& s, const std::string& n) {
+             return fromChange(s.deleteAdjacencyDatabase(n));
+           })
+      .def("getSpfResult",
+           [](const LinkState& s, const std::string& n, bool ulm) {
+             py::dict out;
+             for (const auto& [name, r] : s.getSpfResult(n, ulm)) {
+               std::vector<std::string> nh(r.nextHops().begin(), r.nextHops().end());
+               out[py::str(name)] = py::make_tuple(r.metric(), nh);
+             }
+             return out;
+           },
+           py::arg("node"), py::arg("useLinkMetric") = true)
+      .def("getKthPaths",
+           [](const LinkState& s, const std::string& a, const std::string& b, size_t k) {
+             py::list out;
+             for (const auto& p : s.getKthPaths(a, b, k)) {
+               py::list path;
+               for (const auto& l : p) path.append(fromLink(*l));
+               out.append(path);
+             }
+             return out;
+           })
+      .def("getMetricFromAToB",
+           [](const LinkState& s, const std::string& a, const std::string& b) {
+             return s.getMetricFromAToB(a, b);
+           })
+      .def("hasNode", &LinkState::hasNode)
+      .def("isNodeOverloaded", &LinkState::isNodeOverloaded)
+      .def("getNodeMetricIncrement", &LinkState::getNodeMetricIncrement)
+      .def("numLinks", &LinkState::numLinks)
+      .def("numNodes", &LinkState::numNodes)
+      .def("spfRuns", &LinkState::spfRuns)
+      .def("getArea", &LinkState::getArea)
+      .def("linksFromNode", [](const LinkState& s, const std::string& n) {
+        py::list out;
+        for (const auto& l : s.linksFromNode(n)) out.append(fromLink(*l));
+        return out;
+      });
+
+  py::class_<AreaLinkStates>(m, "AreaLinkStates")
+      .def(py::init<>())
+      .def("add",
+           [](AreaLinkStates& a, const std::string& area, const std::string& me)
+               -> LinkState& {
+             return a.emplace(area, LinkState(area, me)).first->second;
+           },
+           py::return_value_policy::reference_internal)
+      .def("__getitem__",
+           [](AreaLinkStates& a, const std::string& area) -> LinkState& {
+             return a.at(area);
+           },
+           py::return_value_policy::reference_internal)
+      .def("areas", [](const AreaLinkStates& a) {
+        std::vector<std::string> v;
+        for (auto& [k, _] : a) v.push_back(k);
+        return v;
+      });
+
+  py::class_<PrefixState>(m, "PrefixState")
+      .def(py::init<>())
+      .def("updatePrefix",
+           [](PrefixState& s, const std::string& node, const std::string& area,
+              py::dict e) { return s.updatePrefix(node, area, toEntry(e)); })
+      .def("deletePrefix", &PrefixState::deletePrefix)
+      .def("prefixes", [](const PrefixState& s) {
+        py::dict out;
+        for (const auto& [p, es] : s.prefixes()) {
+          std::vector<NodeAndArea> keys;
+          for (const auto& [k, _] : es) keys.push_back(k);
+          out[py::str(p)] = keys;
+        }
+        return out;
+      });
+
+  py::class_<DecisionRouteDb>(m, "DecisionRouteDb")
+      .def(py::init<>())
+      .def("unicastRoutes",
+           [](const DecisionRouteDb& db) {
+             py::dict out;
+             for (const auto& [p, r] : db.unicastRoutes) out[py::str(p)] = fromRoute(r);
+             return out;
+           })
+      .def("mplsRoutes",
+           [](const DecisionRouteDb& db) {
+             py::dict out;
+             for (const auto& [l, r] : db.mplsRoutes) out[py::int_(l)] = fromNhSet(r.nexthops);
+             return out;
+           })
+      .def("calculateUpdate",
+           [](const DecisionRouteDb& a, const DecisionRouteDb& b) {
+             return fromUpdate(a.calculateUpdate(b));
+           })
+      .def("canonical", [](const DecisionRouteDb& db) { return py::bytes(canonical(db)); });
+
+  py::class_<SpfSolver>(m, "SpfSolver")
+      .def(py::init<const std::string&, bool, bool, bool, bool>(), py::arg("myNodeName"),
+           py::arg("enableV4"), py::arg("enableNodeSegmentLabel"),
+           py::arg("enableBestRouteSelection") = false, py::arg("v4OverV6Nexthop") = false)
+      .def("buildRouteDb",
+           [](SpfSolver& s, const std::string& me, const AreaLinkStates& a,
+              const PrefixState& ps) { return s.buildRouteDb(me, a, ps); })
+      .def("createRouteForPrefixOrGetStaticRoute",
+           [](SpfSolver& s, const std::string& me, const AreaLinkStates& a,
+              const PrefixState& ps, const std::string& prefix) -> py::object {
+             auto r = s.createRouteForPrefixOrGetStaticRoute(me, a, ps, prefix);
+             if (!r) return py::none();
+             return fromRoute(*r);
+           })
+      .def("updateStaticUnicastRoutes",
+           [](SpfSolver& s, py::dict upd, std::vector<std::string> del) {
+             std::map<std::string, RibUnicastEntry> u;
+             for (auto kv : upd) u[kv.first.cast<std::string>()] = toRoute(kv.second.cast<py::dict>());
+             s.updateStaticUnicastRoutes(u, del);
+           })
+      .def("getBestRoutesCache", [](const SpfSolver& s) {
+        py::dict out;
+        for (const auto& [p, r] : s.getBestRoutesCache()) {
+          py::dict d;
+          d["allNodeAreas"] = std::vector<NodeAndArea>(r.allNodeAreas.begin(), r.allNodeAreas.end());
+          d["bestNodeArea"] = r.bestNodeArea;
+          d["isBestNodeDrained"] = r.isBestNodeDrained;
+          out[py::str(p)] = d;
+        }
+        return out;
+      });
+
+  py::class_<RibPolicy>(m, "RibPolicy")
+      .def(py::init([](py::list stmts, int64_t ttl) {
+             std::vector<RibPolicyStatementSpec> v;
+             for (auto h : stmts) {
+               py::dict d = h.cast<py::dict>();
+               RibPolicyStatementSpec s;
+               s.name = get<std::string>(d, "name", "");
+               if (d.contains("prefixes") && !d["prefixes"].is_none())
+                 s.prefixes = d["prefixes"].cast<std::vector<std::string>>();
+               if (d.contains("tags") && !d["tags"].is_none())
+                 s.tags = d["tags"].cast<std::vector<std::string>>();
+               if (d.contains("set_weight") && !d["set_weight"].is_none()) {
+                 py::dict w = d["set_weight"];
+                 RibRouteActionWeight a;
+                 a.default_weight = get<int32_t>(w, "default_weight", 0);
+                 if (w.contains("area_to_weight"))
+                   a.area_to_weight = w["area_to_weight"].cast<std::map<std::string, int32_t>>();
+                 if (w.contains("neighbor_to_weight"))
+                   a.neighbor_to_weight =
+                       w["neighbor_to_weight"].cast<std::map<std::string, int32_t>>();
+                 s.set_weight = a;
+               }
+               if (d.contains("counterID") && !d["counterID"].is_none())
+                 s.counterID = d["counterID"].cast<std::string>();
+               v.push_back(s);
+             }
+             return RibPolicy(v, ttl);
+           }),
+           py::arg("statements"), py::arg("ttl_secs") = 3600)
+      .def("isActive", &RibPolicy::isActive)
+      .def("match", [](const RibPolicy& p, py::dict r) { return p.match(toRoute(r)); })
+      .def("applyAction",
+           [](const RibPolicy& p, py::dict r) {
+             auto e = toRoute(r);
+             bool ok = p.applyAction(e);
+             return py::make_tuple(ok, fromRoute(e));
+           })
+      .def("applyPolicy", [](const RibPolicy& p, DecisionRouteDb& db) {
+        return p.applyPolicy(db.unicastRoutes);
+      });
+
+  m.def("pathAInPathB", [](py::list a, py::list b) {
+    auto conv = [](py::list l) {
+      LinkState::Path p;
+      for (auto h : l) {
+        py::tuple t = h.cast<py::tuple>();
+        p.push_back(std::make_shared<Link>("", t[0].cast<std::string>(), t[1].cast<std::string>(),
+                                           t[2].cast<std::string>(), t[3].cast<std::string>()));
+      }
+      return p;
+    };
+    return LinkState::pathAInPathB(conv(a), conv(b));
+  });
+
+  // ---- bulk workloads ------------------------------------------------------
+  m.def("gen_route_dbs",
+        [](const std::string& kind, py::dict opts, std::vector<std::string> sources,
+           bool enableV4, bool sr, bool brs) {
+          auto g = genLsdb(kind, opts);
+          AreaLinkStates als;
+          auto& ls = als.emplace(g.area, LinkState(g.area, "test_node")).first->second;
+          PrefixState ps;
+          loadLsdb(g, ls, ps);
+          SpfSolver solver("test_node", enableV4, sr, brs);
+          std::vector<py::bytes> out;
+          for (const auto& s : sources) {
+            auto db = solver.buildRouteDb(s, als, ps);
+            out.push_back(py::bytes(db ? canonical(*db) : std::string("NONE")));
+          }
+          return out;
+        });
+
+  py::class_<BatchRunner>(m, "BatchRunner")
+      .def(py::init<bool, bool, bool>(), py::arg("enableV4") = true,
+           py::arg("enableNodeSegmentLabel") = false,
+           py::arg("enableBestRouteSelection") = false)
+      .def("add_generated",
+           [](BatchRunner& b, const std::string& kind, py::dict opts,
+              std::vector<std::string> sources) { b.addLsdb(genLsdb(kind, opts), sources); })
+      .def("add_grid_batch",
+           [](BatchRunner& b, py::dict opts, int lo, int hi, const std::string& source) {
+             // topology t: metric seed base+t, prefix seed base+t (config C2)
+             auto base = gridOpts(opts);
+             for (int t = lo; t < hi; ++t) {
+               auto o = base;
+               o.metricSeed = base.metricSeed + t;
+               o.prefixSeed = base.prefixSeed + t;
+               if (o.overloadSeed) o.overloadSeed = base.overloadSeed + t;
+               b.addLsdb(topogen::grid(o), {source});
+             }
+           })
+      .def("upload", &BatchRunner::upload)
+      .def("run", [](BatchRunner& b) {
+        py::gil_scoped_release nogil;
+        b.run();
+      })
+      .def("download", &BatchRunner::download)
+      .def("num_units", &BatchRunner::numUnits)
+      .def("canonical", [](const BatchRunner& b, size_t u) { return py::bytes(canonical(b.routeDb(u))); })
+      .def("route_counts",
+           [](const BatchRunner& b) {
+             std::vector<size_t> c;
+             for (size_t u = 0; u < b.numUnits(); ++u) c.push_back(b.routeDb(u).unicastRoutes.size());
+             return c;
+           })
+      .def("flags", &BatchRunner::flags)
+      .def("nh_words", &BatchRunner::nhWords)
+      .def("wide", &BatchRunner::wide)
+      .def("host_arrays", [](const BatchRunner& b) {
+        // the exact HBM image the kernel consumes (bench.py uploads it)
+        const HostBatch& h = b.host();
+        py::dict d;
+        d["node_base"] = npcopy(h.nodeBase);
+        d["row_ptr"] = npcopy(h.rowPtr);
+        d["edges"] = npcopy(h.edges);
+        d["node_flags"] = npcopy(h.nodeFlags);
+        d["pfx_base"] = npcopy(h.pfxBase);
+        d["adv_off"] = npcopy(h.advOff);
+        d["adv_node"] = npcopy(h.advNode);
+        d["adv_metrics"] = npcopy(h.advMetrics);
+        d["adv_min_nh"] = npcopy(h.advMinNh);
+        d["pfx_flags"] = npcopy(h.pfxFlags);
+        std::vector<uint32_t> u;
+        for (const auto& x : b.units()) {
+          u.push_back(x.topo);
+          u.push_back(x.src);
+        }
+        d["units"] = npcopy(u);
+        d["max_nodes"] = h.maxNodes;
+        d["max_edges"] = h.maxEdges;
+        d["max_prefixes"] = h.maxPrefixes;
+        d["max_degree"] = h.maxDegree;
+        d["num_topos"] = int(h.nodeBase.size() - 1);
+        d["nh_words"] = b.nhWords();
+        d["flags"] = b.flags();
+        return d;
+      })
+      .def("dist", [](const BatchRunner& b) { return npcopy(b.dist()); })
+      .def("meta", [](const BatchRunner& b) { return npcopy(b.meta()); })
+      .def("metric", [](const BatchRunner& b) { return npcopy(b.metric()); });
+}

@@ -790,7 +790,9 @@ std::optional<RibUnicastEntry> SpfSolver::addBestPaths(
   // SpfSolver.cpp:595-639
   if (nextHops.empty()) return std::nullopt;
   auto minNh = getMinNextHopThreshold(sel, entries);
-  if (minNh && *minNh > static_cast<int64_t>(nextHops.size())) {
+  // `int64 > size_t` compares as unsigned (SpfSolver.cpp:612): a negative
+  // minNexthop always drops the route.
+  if (minNh && static_cast<uint64_t>(*minNh) > nextHops.size()) {
     return std::nullopt;
   }
   PrefixEntry best = *entries.at(sel.bestNodeArea);

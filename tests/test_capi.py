@@ -1,0 +1,78 @@
+"""CPU-side checks of the drop-in boundary: the C-ABI library loads, exports
+every entry point include/openr_gpu.h declares, and the product fails loudly
+(no CPU fallback) when no HIP device is visible."""
+import ctypes
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_symbols():
+    src = open(os.path.join(ROOT, "include", "openr_gpu.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(ogs_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_declares_entry_points():
+    syms = declared_symbols()
+    assert "ogs_spf_routes" in syms and len(syms) >= 10
+
+
+def test_library_exports_every_declared_symbol():
+    import openr_amd
+    import openr_amd.capi as capi
+    lib = ctypes.CDLL(openr_amd.LIB_PATH)
+    missing = [s for s in declared_symbols() if not hasattr(lib, s)]
+    assert not missing, missing
+    assert sorted(capi.EXPORTS) == declared_symbols()
+
+
+def test_pure_entry_points_without_device():
+    import openr_amd.capi as capi
+    lib = capi.load()
+    assert b"gfx950" in lib.ogs_version()
+    assert [lib.ogs_nh_words_for_degree(d) for d in (0, 1, 32, 33, 65, 200, 511)] == \
+        [1, 1, 1, 2, 4, 8, 16]
+    assert lib.ogs_nh_words_for_degree(513) < 0
+
+
+def test_spf_routes_rejects_bad_arguments():
+    import openr_amd.capi as capi
+    lib = capi.load()
+    out = capi.SpfOut()
+    assert lib.ogs_spf_routes(None, None, None, 1, 0, 1, ctypes.byref(out), None) == -1
+    g = capi.Graph()
+    assert lib.ogs_spf_routes(ctypes.byref(g), None, None, 0, 0, 1, ctypes.byref(out), None) == 0
+    g.max_nodes = 10
+    assert lib.ogs_spf_routes(ctypes.byref(g), None, None, 4, 0, 1, ctypes.byref(out), None) == -1
+
+
+def test_product_fails_loudly_without_gpu():
+    import openr_amd
+    if openr_amd.decision.device_count() > 0:
+        pytest.skip("a GPU is visible")
+    with pytest.raises(RuntimeError):
+        openr_amd.require_gpu()
+    import lsdb as L
+    M = openr_amd.decision
+    als = M.AreaLinkStates()
+    ls = als.add(L.kTestingAreaName, "1")
+    ls.updateAdjacencyDatabase(L.createAdjDb("1", [L.adj12], 1), L.kTestingAreaName)
+    ls.updateAdjacencyDatabase(L.createAdjDb("2", [L.adj21], 2), L.kTestingAreaName)
+    with pytest.raises(RuntimeError):
+        ls.getSpfResult("1")
+    with pytest.raises(RuntimeError):
+        M.SpfSolver("1", False, False).buildRouteDb("1", als, M.PrefixState())
+
+
+def test_product_ingestion_matches_oracle_on_cpu(oracle):
+    """Link formation / LinkStateChange are host-side ingestion in the
+    product; they must agree with the oracle call-for-call."""
+    import openr_amd
+    import kat_cases
+    M = openr_amd.decision
+    kat_cases.kat_linkstate_basic(M)
+    kat_cases.kat_linkstate_link_usable(M)

@@ -1,0 +1,121 @@
+"""Bit-exact parity of the GPU product against the CPU oracle on seeded
+synthetic LSDBs (grid / fabric / WAN), including the full 4096-topology
+config-C2 batch the bench measures."""
+import random
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _cmp(a, b, label):
+    assert len(a) == len(b)
+    for i, (x, y) in enumerate(zip(a, b)):
+        if x != y:
+            xa, ya = x.decode().splitlines(), y.decode().splitlines()
+            diff = [(p, q) for p, q in zip(xa, ya) if p != q][:5]
+            pytest.fail(f"{label}[{i}] differs: {diff} (len {len(xa)} vs {len(ya)})")
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+@pytest.mark.parametrize("brs", [False, True])
+def test_grid_random_metrics_all_sources(product, oracle, seed, brs):
+    opts = dict(n=6, metricSeed=0xC2000000 + seed, prefixSeed=seed,
+                adjOverloadPermille=20, nodeOverloadPermille=10,
+                overloadSeed=0xABC + seed)
+    srcs = [str(i) for i in range(36)]
+    a = product.gen_route_dbs("grid", opts, srcs, True, True, brs)
+    b = oracle.gen_route_dbs("grid", opts, srcs, True, True, brs)
+    _cmp(a, b, "grid")
+
+
+def test_grid_unit_metric_ecmp(product, oracle):
+    opts = dict(n=10, prefixesPerNode=2)
+    srcs = [str(i) for i in range(0, 100, 7)]
+    _cmp(product.gen_route_dbs("grid", opts, srcs, True, True, False),
+         oracle.gen_route_dbs("grid", opts, srcs, True, True, False), "grid10")
+
+
+@pytest.mark.parametrize("full", [True, False])
+def test_fabric_small_all_sources(product, oracle, full):
+    opts = dict(pods=3, planes=2, sswPerPlane=3, rswPerPod=4, full=full)
+    n = 2 * 3 + 3 * 2 + 3 * 4
+    srcs = None
+    names = ([f"1-{p}-{s}" for p in range(2) for s in range(3)] +
+             [f"2-{p}-{f}" for p in range(3) for f in range(2)] +
+             [f"3-{p}-{r}" for p in range(3) for r in range(4)])
+    assert len(names) == n
+    srcs = names
+    _cmp(product.gen_route_dbs("fabric", opts, srcs, True, True, False),
+         oracle.gen_route_dbs("fabric", opts, srcs, True, True, False), "fabric")
+
+
+def test_wan_random_sources(product, oracle):
+    opts = dict(nodes=300, seed=0xC4)
+    rng = random.Random(7)
+    srcs = [str(rng.randrange(300)) for _ in range(12)]
+    _cmp(product.gen_route_dbs("wan", opts, srcs, True, True, True),
+         oracle.gen_route_dbs("wan", opts, srcs, True, True, True), "wan")
+
+
+def test_spf_result_matches_oracle(product, oracle):
+    import lsdb as L
+    rng = random.Random(11)
+    n = 7
+    for M in (product, oracle):
+        pass
+    def build(M):
+        als = M.AreaLinkStates()
+        ls = als.add(L.kTestingAreaName, "0")
+        r = random.Random(5)
+        for i in range(n):
+            for j in range(n):
+                node = i * n + j
+                adjs = []
+                for (ii, jj, a, b) in ((i, j + 1, "e", "w"), (i, j - 1, "w", "e"),
+                                       (i - 1, j, "n", "s"), (i + 1, j, "s", "n")):
+                    if 0 <= ii < n and 0 <= jj < n:
+                        nb = ii * n + jj
+                        adjs.append(L.createAdjacency(str(nb), f"{a}{node}", f"{b}{nb}",
+                                                      f"fe80::{nb}", f"10.0.0.{nb}",
+                                                      r.randint(1, 9), 100 + nb))
+                ls.updateAdjacencyDatabase(L.createAdjDb(str(node), adjs, node + 1),
+                                           L.kTestingAreaName)
+        return ls
+    pls, ols = build(product), build(oracle)
+    for src in [str(rng.randrange(n * n)) for _ in range(10)] + ["unknown"]:
+        for ulm in (True, False):
+            a = {k: (v[0], sorted(v[1])) for k, v in pls.getSpfResult(src, ulm).items()}
+            b = {k: (v[0], sorted(v[1])) for k, v in ols.getSpfResult(src, ulm).items()}
+            assert a == b, src
+
+
+def test_c2_full_batch_bit_exact(product, oracle):
+    """Config C2 at bench size: 4096 random-metric 10x10 grids, source "1",
+    one batched launch; every topology's RouteDb equals the oracle's."""
+    T = 4096
+    opts = dict(n=10, metricSeed=0xC2000000, prefixSeed=0xC1)
+    br = product.BatchRunner(True, False, False)
+    br.add_grid_batch(opts, 0, T, "1")
+    br.upload()
+    br.run()
+    br.download()
+    assert br.num_units() == T
+    gpu = [br.canonical(u) for u in range(T)]
+    cpu = oracle.grid_batch_route_dbs(opts, 0, T, "1")
+    _cmp(gpu, cpu, "c2")
+    assert all(c == 99 for c in br.route_counts())
+
+
+def test_c2_parity_variant_overloads(product, oracle):
+    """C2 parity variant: 2% adjacency overload + 1% node overload."""
+    T = 512
+    opts = dict(n=10, metricSeed=0xC2100000, prefixSeed=0xC1,
+                adjOverloadPermille=20, nodeOverloadPermille=10, overloadSeed=0xC20F)
+    br = product.BatchRunner(True, False, False)
+    br.add_grid_batch(opts, 0, T, "1")
+    br.upload()
+    br.run()
+    br.download()
+    _cmp([br.canonical(u) for u in range(T)],
+         oracle.grid_batch_route_dbs(opts, 0, T, "1"), "c2ovl")
