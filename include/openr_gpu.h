@@ -141,6 +141,27 @@ typedef struct ogs_spf_out {
   uint32_t* sel;
 } ogs_spf_out;
 
+/* KSP2 unit: edge-disjoint paths src -> dest avoiding an optional
+ * linksToIgnore mask. */
+typedef struct ogs_path_unit {
+  uint32_t topo;
+  uint32_t src;
+  uint32_t dest;
+  uint32_t reserved;
+} ogs_path_unit;
+
+/* Paths (device). Per unit U: path_count[U] = number of paths (bit 31 set
+ * if the output capacity was exceeded); path_len[U*max_paths + i] = links in
+ * path i; path_edges[U*max_edges + ...] = the paths' topology-local directed
+ * edge ids, concatenated, each path ordered source -> destination. */
+typedef struct ogs_path_out {
+  uint32_t* path_count;
+  uint32_t* path_len;
+  uint32_t* path_edges;
+  uint32_t max_paths;
+  uint32_t max_edges;
+} ogs_path_out;
+
 /* ---- runtime ------------------------------------------------------------ */
 const char* ogs_version(void);
 const char* ogs_last_error(void); /* thread-local message of last failure */
@@ -170,6 +191,17 @@ int ogs_spf_routes(const ogs_graph* graph, const ogs_prefix_table* prefixes,
                    const ogs_unit* units /* device */, int32_t n_units,
                    uint32_t flags, int32_t nh_words, ogs_spf_out* out,
                    void* stream);
+
+/* Batched edge-disjoint path tracing (KSP2). For each unit: SPF from src
+ * over the links not set in the unit's mask (`masks` + U*mask_words, bit l =
+ * topology-local link id l = min of the link's two directed edge ids; NULL =
+ * no mask), then the reference's greedy trace repeated until no path
+ * remains. Replaces LinkState::getKthPaths / traceOnePath
+ * (LinkState.cpp:226-247, 674-703): the k-th call is one launch whose masks
+ * hold the links of the paths for 1..k-1. */
+int ogs_ksp_paths(const ogs_graph* graph, const ogs_path_unit* units,
+                  int32_t n_units, const uint32_t* masks, uint32_t mask_words,
+                  uint32_t flags, ogs_path_out* out, void* stream);
 
 #ifdef __cplusplus
 }

@@ -47,6 +47,10 @@ class DeviceBuffer {
   }
   template <typename T>
   void upload(const T* host, size_t count, void* stream = nullptr) {
+    if (count == 0) {  // keep a valid (never read) allocation
+      resize(16);
+      return;
+    }
     resize(count * sizeof(T));
     ogsCheck(ogs_memcpy_h2d(ptr_, host, count * sizeof(T), stream),
              "ogs_memcpy_h2d");

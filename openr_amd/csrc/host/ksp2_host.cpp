@@ -1,12 +1,99 @@
-// ksp2_host.cpp — LinkState::getKthPaths (reference LinkState.cpp:674-703).
-// Placeholder until the KSP2 kernel lands: fails loudly.
+// ksp2_host.cpp — LinkState::getKthPaths on the GPU (reference
+// LinkState.cpp:674-703): the k-th call masks every link of the paths for
+// 1..k-1 and launches one KSP unit (masked SPF + greedy trace).
+#include <algorithm>
+#include <unordered_map>
+
 #include "decision.h"
 
 namespace openr_amd {
 
 const std::vector<LinkState::Path>& LinkState::getKthPaths(
-    const std::string&, const std::string&, size_t) const {
-  throw std::domain_error("getKthPaths: KSP2 GPU kernel not built yet");
+    const std::string& src, const std::string& dest, size_t k) const {
+  if (k < 1) throw std::invalid_argument("getKthPaths: k must be >= 1");
+  auto key = std::make_tuple(src, dest, k);
+  if (auto it = kthMemo_.find(key); it != kthMemo_.end()) return it->second;
+
+  std::vector<const Link*> ignore;
+  for (size_t i = 1; i < k; ++i) {
+    for (const auto& p : getKthPaths(src, dest, i)) {
+      for (const auto& l : p) ignore.push_back(l.get());
+    }
+  }
+  const FlatTopology& f = flatOnDevice();
+  std::vector<Path> paths;
+  auto sIt = f.id.find(src), dIt = f.id.find(dest);
+  if (sIt == f.id.end() || dIt == f.id.end() || src == dest) {
+    // unknown endpoints or src == dest: the reference finds no path
+    return kthMemo_.emplace(key, std::move(paths)).first->second;
+  }
+  if (f.hasZeroMetric || f.hasWideMetric) {
+    throw std::domain_error(
+        "getKthPaths: zero or negative link metric is outside the GPU "
+        "engine's exact domain");
+  }
+  const uint32_t E = uint32_t(f.edges.size());
+  const uint32_t maskWords = std::max<uint32_t>(1, (E + 31) / 32);
+  std::vector<uint32_t> mask;
+  if (!ignore.empty()) {
+    std::unordered_map<const Link*, uint32_t> canon;  // link -> min edge id
+    for (uint32_t e = 0; e < E; ++e) canon.emplace(f.edgeLink[e], e);
+    mask.assign(maskWords, 0u);
+    for (const Link* l : ignore) {
+      // links are re-flattened objects of this LinkState; match by key
+      const uint32_t e = canon.at(links_.at(l->key()).get());
+      mask[e >> 5] |= 1u << (e & 31u);
+    }
+  }
+  const uint32_t t = dIt->second;
+  const uint32_t maxPaths = f.rowPtr[t + 1] - f.rowPtr[t] + 1;
+  const uint32_t maxEdges = E / 2 + 1;
+
+  DeviceBuffer dUnit, dMask, dCount, dLen, dEdges;
+  const ogs_path_unit u{0, sIt->second, t, 0};
+  dUnit.upload(&u, 1);
+  if (!mask.empty()) dMask.upload(mask.data(), mask.size());
+  dCount.resize(4);
+  dLen.resize(maxPaths * 4);
+  dEdges.resize(maxEdges * 4);
+  ogs_graph g{};
+  g.num_topos = 1;
+  g.max_nodes = int32_t(f.names.size());
+  g.max_edges = int32_t(E);
+  g.node_base = f.dNodeBase.as<uint32_t>();
+  g.row_ptr = f.dRow.as<uint32_t>();
+  g.edges = f.dEdges.as<uint64_t>();
+  g.node_flags = f.dFlags.as<uint8_t>();
+  ogs_path_out out{dCount.as<uint32_t>(), dLen.as<uint32_t>(),
+                   dEdges.as<uint32_t>(), maxPaths, maxEdges};
+  const uint32_t flags = wideDistancesNeeded(f) ? OGS_F_WIDE_METRIC : 0u;
+  ogsCheck(ogs_ksp_paths(&g, dUnit.as<ogs_path_unit>(), 1,
+                         mask.empty() ? nullptr : dMask.as<uint32_t>(),
+                         maskWords, flags, &out, nullptr),
+           "ogs_ksp_paths");
+  ++spfRuns_;
+  uint32_t count = 0;
+  dCount.download(&count, 1);
+  ogsCheck(ogs_stream_sync(nullptr), "ogs_stream_sync");
+  if (count >> 31) throw std::runtime_error("getKthPaths: path buffer overflow");
+  std::vector<uint32_t> len(count), edges;
+  if (count) {
+    dLen.download(len.data(), count);
+    uint32_t total = 0;
+    for (auto x : len) total += x;
+    edges.resize(total);
+    dEdges.download(edges.data(), total);
+    ogsCheck(ogs_stream_sync(nullptr), "ogs_stream_sync");
+  }
+  size_t pos = 0;
+  for (uint32_t i = 0; i < count; ++i) {
+    Path p;
+    for (uint32_t j = 0; j < len[i]; ++j) {
+      p.push_back(links_.at(f.edgeLink[edges[pos++]]->key()));
+    }
+    paths.push_back(std::move(p));
+  }
+  return kthMemo_.emplace(key, std::move(paths)).first->second;
 }
 
 }  // namespace openr_amd

@@ -294,8 +294,8 @@ const FlatTopology& LinkState::flatOnDevice() const {
   const uint32_t nodeBase[2] = {0, uint32_t(m.names.size())};
   m.dNodeBase.upload(nodeBase, 2);
   m.dRow.upload(m.rowPtr.data(), m.rowPtr.size());
-  m.dEdges.upload(m.edges.data(), std::max<size_t>(m.edges.size(), 1));
-  m.dFlags.upload(m.nodeFlags.data(), std::max<size_t>(m.nodeFlags.size(), 1));
+  m.dEdges.upload(m.edges.data(), m.edges.size());
+  m.dFlags.upload(m.nodeFlags.data(), m.nodeFlags.size());
   deviceStale_ = false;
   return f;
 }

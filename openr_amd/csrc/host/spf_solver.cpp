@@ -291,10 +291,10 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(
     I.table.build(ps);
     I.pfxBase.upload(hb.pfxBase.data(), hb.pfxBase.size());
     I.advOff.upload(hb.advOff.data(), hb.advOff.size());
-    I.advNode.upload(hb.advNode.data(), std::max<size_t>(hb.advNode.size(), 1));
-    I.advMetrics.upload(hb.advMetrics.data(), std::max<size_t>(hb.advMetrics.size(), 4));
-    I.advMinNh.upload(hb.advMinNh.data(), std::max<size_t>(hb.advMinNh.size(), 1));
-    I.pfxFlags.upload(hb.pfxFlags.data(), std::max<size_t>(hb.pfxFlags.size(), 1));
+    I.advNode.upload(hb.advNode.data(), hb.advNode.size());
+    I.advMetrics.upload(hb.advMetrics.data(), hb.advMetrics.size());
+    I.advMinNh.upload(hb.advMinNh.data(), hb.advMinNh.size());
+    I.pfxFlags.upload(hb.pfxFlags.data(), hb.pfxFlags.size());
     I.cachedPs = &ps;
     I.cachedPsVersion = ps.version();
     I.cachedTopo = &f;

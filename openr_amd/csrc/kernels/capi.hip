@@ -12,6 +12,10 @@ hipError_t launch_spf_routes(const ogs_graph& g, const ogs_prefix_table* pt,
                              const ogs_unit* units, int nUnits, uint32_t flags,
                              int W, const ogs_spf_out& out, hipStream_t stream,
                              int* unsupported);
+hipError_t launch_ksp(const ogs_graph& g, const ogs_path_unit* units,
+                      int nUnits, const uint32_t* masks, uint32_t maskWords,
+                      uint32_t flags, const ogs_path_out& out,
+                      hipStream_t stream, int* unsupported);
 }
 
 namespace {
@@ -131,6 +135,33 @@ int ogs_spf_routes(const ogs_graph* graph, const ogs_prefix_table* prefixes,
                 "topology too large for the LDS-resident SPF path");
   }
   return e == hipSuccess ? OGS_OK : hipFail(e, "spf_route launch");
+}
+
+int ogs_ksp_paths(const ogs_graph* graph, const ogs_path_unit* units,
+                  int32_t n_units, const uint32_t* masks, uint32_t mask_words,
+                  uint32_t flags, ogs_path_out* out, void* stream) {
+  if (!graph || !out) return fail(OGS_E_INVALID, "graph/out is NULL");
+  if (n_units < 0) return fail(OGS_E_INVALID, "n_units < 0");
+  if (n_units == 0) return OGS_OK;
+  if (!units || !graph->node_base || !graph->row_ptr || !out->path_count ||
+      !out->path_len || !out->path_edges) {
+    return fail(OGS_E_INVALID, "graph/unit/output arrays are NULL");
+  }
+  if (graph->max_nodes <= 0 ||
+      uint32_t(graph->max_nodes) > OGS_MAX_NODES_PER_TOPO) {
+    return fail(OGS_E_UNSUPPORTED, "max_nodes outside (0, 2^21]");
+  }
+  if (masks && mask_words < uint32_t((graph->max_edges + 31) / 32)) {
+    return fail(OGS_E_INVALID, "mask_words too small for max_edges");
+  }
+  int unsupported = 0;
+  hipError_t e = ogs::launch_ksp(*graph, units, n_units, masks, mask_words,
+                                 flags, *out, static_cast<hipStream_t>(stream),
+                                 &unsupported);
+  if (unsupported) {
+    return fail(OGS_E_UNSUPPORTED, "topology too large for the LDS KSP path");
+  }
+  return e == hipSuccess ? OGS_OK : hipFail(e, "ksp launch");
 }
 
 }  // extern "C"

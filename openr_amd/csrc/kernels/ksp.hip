@@ -1,0 +1,227 @@
+// ksp.hip — edge-disjoint k-th shortest paths (KSP2) for gfx950.
+//
+// Replaces LinkState::getKthPaths + traceOnePath (LinkState.cpp:226-247,
+// 674-703). One work unit = (topology, source, destination, ignore-mask):
+//   1. SPF over the links NOT in the unit's linksToIgnore mask (the masked
+//      second pass; empty mask = the k = 1 SPF), wave/workgroup-parallel in
+//      LDS (spf_core.h);
+//   2. the reference's greedy trace, run by lane 0: repeatedly walk from the
+//      destination back to the source over NodeSpfResult::pathLinks in the
+//      reference order, marking every link visited (never unmarked), until
+//      no path remains. pathLinks(v) = tight links from relaxing
+//      predecessors in settlement order; with metrics >= 1 settlement order
+//      is (dist, name) (LinkState.h:618-626) = (dist, id), and a
+//      predecessor's parallel links follow its CSR row (canonical link
+//      order; the reference uses folly-hash order there, parity unpinned,
+//      see DESIGN.md). The recursion is an explicit stack in LDS; each frame
+//      resumes its scan from the last (dist, pred, slot) key it tried.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "openr_gpu.h"
+#include "spf_core.h"
+
+namespace ogs {
+
+struct Frame {
+  uint32_t node;
+  uint32_t edge;    // edge (node -> pred) chosen at this frame
+  uint32_t lastU;   // resume key: (dist[pred], pred, rslot)
+  uint32_t lastSlot;
+  uint64_t lastD;
+};
+
+template <typename D>
+__device__ bool key_less(D da, uint32_t ua, uint32_t sa, D db, uint32_t ub,
+                         uint32_t sb) {
+  if (da != db) return da < db;
+  if (ua != ub) return ua < ub;
+  return sa < sb;
+}
+
+template <typename D, int UT, bool STAGE, bool MASKED>
+__global__ __launch_bounds__(kBlock) void ksp_kernel(
+    ogs_graph g, const ogs_path_unit* __restrict__ units, int nUnits,
+    const uint32_t* __restrict__ masks, uint32_t maskWords,
+    ogs_path_out out, uint32_t ldsPerUnit) {
+  constexpr D kInf = DistInf<D>::value;
+  constexpr int kUnitsPerBlock = kBlock / UT;
+  const int uib = threadIdx.x / UT;
+  const int lane = threadIdx.x % UT;
+  const int uidx = blockIdx.x * kUnitsPerBlock + uib;
+  if (uidx >= nUnits) return;
+
+  const ogs_path_unit unit = units[uidx];
+  const uint32_t nb = g.node_base[unit.topo];
+  const uint32_t N = g.node_base[unit.topo + 1] - nb;
+  const uint32_t s = unit.src, t = unit.dest;
+  const uint32_t* __restrict__ gRow = g.row_ptr + nb;
+  const uint32_t e0 = gRow[0];
+  const uint32_t E = gRow[N] - e0;
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* base = smem + uib * ldsPerUnit;
+  D* dist = reinterpret_cast<D*>(base);
+  uint32_t off = align16(uint64_t(N) * sizeof(D));
+  uint32_t* visited = reinterpret_cast<uint32_t*>(base + off);
+  off += align16(uint64_t((E + 31) / 32) * 4);
+  Frame* stack = reinterpret_cast<Frame*>(base + off);
+  off += align16(uint64_t(N) * sizeof(Frame));
+  UnitCsr csr;
+  if constexpr (STAGE) {
+    uint32_t* lrow = reinterpret_cast<uint32_t*>(base + off);
+    off += align16(uint64_t(N + 1) * 4);
+    uint64_t* ledg = reinterpret_cast<uint64_t*>(base + off);
+    for (uint32_t i = lane; i <= N; i += UT) lrow[i] = gRow[i] - e0;
+    for (uint32_t i = lane; i < E; i += UT) ledg[i] = g.edges[e0 + i];
+    csr = UnitCsr{lrow, ledg, 0u};
+  } else {
+    csr = UnitCsr{gRow, g.edges, e0};
+  }
+  for (uint32_t i = lane; i < (E + 31) / 32; i += UT) visited[i] = 0u;
+  const uint32_t* ignore =
+      MASKED ? masks + size_t(uidx) * maskWords : nullptr;
+  spf_fixpoint<D, 1, UT, false, MASKED>(N, s, lane, csr, false, dist, nullptr,
+                                        ignore);
+
+  if (lane != 0) return;
+  // ---- greedy trace (lane 0) ----------------------------------------------
+  uint32_t* pathLen = out.path_len + size_t(uidx) * out.max_paths;
+  uint32_t* pathEdges = out.path_edges + size_t(uidx) * out.max_edges;
+  uint32_t nPaths = 0, nEdges = 0, status = 0;
+  const bool reachable = (s != t) && dist[t] != kInf;
+  while (reachable) {
+    // one traceOnePath(src, dest) call
+    int sp = 0;
+    // a frame without a resume key yet carries lastSlot's top bit
+    stack[0] = Frame{t, 0xFFFFFFFFu, 0u, 0x80000000u, 0ull};
+    bool found = false;
+    while (sp >= 0) {
+      Frame& f = stack[sp];
+      const uint32_t v = f.node;
+      const D dv = dist[v];
+      // next unvisited pathLink of v after the resume key
+      D bd = kInf;
+      uint32_t bu = 0xFFFFFFFFu, bs = 0xFFFFFFFFu, be = 0xFFFFFFFFu;
+      const bool fresh = (f.lastSlot & 0x80000000u) != 0;
+      const D ld = static_cast<D>(f.lastD);
+      for (uint32_t e = csr.rowp[v]; e < csr.rowp[v + 1]; ++e) {
+        const uint64_t ed = csr.edg[e];
+        const uint32_t lo = static_cast<uint32_t>(ed);
+        if (lo & OGS_EDGE_DOWN) continue;
+        const uint32_t u = edge_dst(lo);
+        if ((lo & OGS_EDGE_DST_OVERLOADED) && u != s) continue;
+        const uint32_t l = link_id(csr, e, lo);
+        if constexpr (MASKED) {
+          if ((ignore[l >> 5] >> (l & 31u)) & 1u) continue;
+        }
+        const D du = dist[u];
+        if (du == kInf || du + static_cast<D>(ed >> 32) != dv) continue;
+        const uint32_t slot = edge_rslot(lo);
+        if (!fresh && !key_less<D>(ld, f.lastU, f.lastSlot, du, u, slot)) continue;
+        if (key_less<D>(du, u, slot, bd, bu, bs)) {
+          bd = du;
+          bu = u;
+          bs = slot;
+          be = e;
+        }
+      }
+      if (be == 0xFFFFFFFFu) {  // exhausted: this recursion level fails
+        --sp;
+        continue;
+      }
+      f.lastD = static_cast<uint64_t>(bd);
+      f.lastU = bu;
+      f.lastSlot = bs;
+      const uint32_t l = link_id(csr, be, static_cast<uint32_t>(csr.edg[be]));
+      if ((visited[l >> 5] >> (l & 31u)) & 1u) continue;  // already used
+      visited[l >> 5] |= 1u << (l & 31u);
+      f.edge = be;
+      if (bu == s) {
+        found = true;
+        break;
+      }
+      ++sp;
+      stack[sp] = Frame{bu, 0xFFFFFFFFu, 0u, 0x80000000u, 0ull};
+    }
+    if (!found) break;
+    // path src -> dest = chosen edges from the top frame down to frame 0
+    if (nPaths >= out.max_paths || nEdges + uint32_t(sp + 1) > out.max_edges) {
+      status = 1;  // output capacity exceeded
+      break;
+    }
+    for (int i = sp; i >= 0; --i) pathEdges[nEdges++] = stack[i].edge - csr.eBase;
+    pathLen[nPaths++] = uint32_t(sp + 1);
+  }
+  out.path_count[uidx] = nPaths | (status << 31);
+}
+
+template <typename D, int UT, bool STAGE, bool MASKED>
+hipError_t ksp_launch(const ogs_graph& g, const ogs_path_unit* units,
+                      int nUnits, const uint32_t* masks, uint32_t maskWords,
+                      const ogs_path_out& out, uint32_t lds,
+                      hipStream_t stream) {
+  constexpr int upb = kBlock / UT;
+  const int grid = (nUnits + upb - 1) / upb;
+  const size_t bytes = size_t(lds) * upb;
+  auto k = ksp_kernel<D, UT, STAGE, MASKED>;
+  if (bytes > 64 * 1024) {
+    hipError_t e = hipFuncSetAttribute(
+        reinterpret_cast<const void*>(k),
+        hipFuncAttributeMaxDynamicSharedMemorySize, int(bytes));
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), bytes, stream, g, units,
+                     nUnits, masks, maskWords, out, lds);
+  return hipGetLastError();
+}
+
+template <typename D, bool MASKED>
+hipError_t ksp_dispatch(const ogs_graph& g, const ogs_path_unit* units,
+                        int nUnits, const uint32_t* masks, uint32_t maskWords,
+                        const ogs_path_out& out, hipStream_t stream,
+                        int* unsupported) {
+  const uint64_t N = g.max_nodes, E = g.max_edges;
+  const uint64_t core = align16(N * sizeof(D)) + align16((E + 31) / 32 * 4) +
+      align16(N * sizeof(Frame));
+  const uint64_t staged = core + align16((N + 1) * 4) + align16(E * 8);
+  constexpr uint64_t kBudget = 160 * 1024;
+  if (N <= 256 && staged * 4 <= kBudget / 2) {
+    return ksp_launch<D, 64, true, MASKED>(g, units, nUnits, masks, maskWords,
+                                           out, uint32_t(staged), stream);
+  }
+  if (staged <= kBudget / 2) {
+    return ksp_launch<D, kBlock, true, MASKED>(g, units, nUnits, masks,
+                                               maskWords, out, uint32_t(staged),
+                                               stream);
+  }
+  if (core <= kBudget) {
+    return ksp_launch<D, kBlock, false, MASKED>(g, units, nUnits, masks,
+                                                maskWords, out, uint32_t(core),
+                                                stream);
+  }
+  *unsupported = 1;
+  return hipSuccess;
+}
+
+hipError_t launch_ksp(const ogs_graph& g, const ogs_path_unit* units,
+                      int nUnits, const uint32_t* masks, uint32_t maskWords,
+                      uint32_t flags, const ogs_path_out& out,
+                      hipStream_t stream, int* unsupported) {
+  const bool wide = flags & OGS_F_WIDE_METRIC;
+  if (masks) {
+    return wide ? ksp_dispatch<uint64_t, true>(g, units, nUnits, masks,
+                                               maskWords, out, stream,
+                                               unsupported)
+                : ksp_dispatch<uint32_t, true>(g, units, nUnits, masks,
+                                               maskWords, out, stream,
+                                               unsupported);
+  }
+  return wide ? ksp_dispatch<uint64_t, false>(g, units, nUnits, nullptr, 0,
+                                              out, stream, unsupported)
+              : ksp_dispatch<uint32_t, false>(g, units, nUnits, nullptr, 0, out,
+                                              stream, unsupported);
+}
+
+}  // namespace ogs

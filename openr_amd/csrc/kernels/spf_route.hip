@@ -33,47 +33,9 @@
 #include <cstdint>
 
 #include "openr_gpu.h"
+#include "spf_core.h"
 
 namespace ogs {
-
-constexpr int kBlock = 256;
-
-template <typename D>
-struct DistInf {
-  static constexpr D value = ~D(0);
-};
-
-// ---- unit-scope synchronisation ------------------------------------------
-template <int UT>
-struct UnitScope;
-
-template <>
-struct UnitScope<64> {  // one wavefront per unit: lockstep, no s_barrier
-  static __device__ __forceinline__ void sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  }
-  static __device__ __forceinline__ bool any(bool x) {
-    sync();
-    return __ballot(x) != 0ull;
-  }
-};
-
-template <>
-struct UnitScope<kBlock> {  // one workgroup per unit
-  static __device__ __forceinline__ void sync() { __syncthreads(); }
-  static __device__ __forceinline__ bool any(bool x) {
-    return __syncthreads_or(x) != 0;
-  }
-};
-
-__device__ __forceinline__ uint32_t edge_dst(uint32_t lo) {
-  return lo & OGS_EDGE_DST_MASK;
-}
-__device__ __forceinline__ uint32_t edge_rslot(uint32_t lo) {
-  return (lo >> OGS_EDGE_RSLOT_SHIFT) & OGS_EDGE_RSLOT_MASK;
-}
 
 struct RouteCfg {
   bool enableV4, v4OverV6, bestRouteSel;
@@ -218,8 +180,6 @@ __global__ __launch_bounds__(kBlock) void spf_route_kernel(
     ogs_graph g, ogs_prefix_table pt, int hasPrefixes,
     const ogs_unit* __restrict__ units, int nUnits, uint32_t flags,
     ogs_spf_out out, uint32_t ldsPerUnit) {
-  using Scope = UnitScope<UT>;
-  constexpr D kInf = DistInf<D>::value;
   constexpr int kUnitsPerBlock = kBlock / UT;
   const int uib = threadIdx.x / UT;
   const int lane = threadIdx.x % UT;
@@ -240,8 +200,7 @@ __global__ __launch_bounds__(kBlock) void spf_route_kernel(
   uint32_t* nh = reinterpret_cast<uint32_t*>(base + distBytes);
   const uint32_t nhBytes = (N * W * 4u + 15u) & ~15u;
 
-  const uint32_t* rowp;
-  const uint64_t* edg;
+  UnitCsr csr;
   if constexpr (STAGE) {
     uint32_t* lrow = reinterpret_cast<uint32_t*>(base + distBytes + nhBytes);
     const uint32_t rowBytes = ((N + 1) * 4u + 15u) & ~15u;
@@ -251,73 +210,14 @@ __global__ __launch_bounds__(kBlock) void spf_route_kernel(
     const uint32_t E = gRow[N] - e0;
     for (uint32_t i = lane; i <= N; i += UT) lrow[i] = gRow[i] - e0;
     for (uint32_t i = lane; i < E; i += UT) ledg[i] = g.edges[e0 + i];
-    rowp = lrow;
-    edg = ledg;
+    csr = UnitCsr{lrow, ledg, 0u};
   } else {
-    rowp = gRow;
-    edg = g.edges;
+    csr = UnitCsr{gRow, g.edges, gRow[0]};
   }
-  for (uint32_t v = lane; v < N; v += UT) {
-    dist[v] = (v == s) ? D(0) : kInf;
-#pragma unroll
-    for (int w = 0; w < W; ++w) nh[v * W + w] = 0u;
-  }
-  Scope::sync();
-
-  const bool hop = flags & OGS_F_HOP_METRIC;
-  // ---- SPF: pull-style relaxation rounds to the fixpoint ------------------
-  for (;;) {
-    bool changed = false;
-    for (uint32_t v = lane; v < N; v += UT) {
-      if (v == s) continue;
-      D best = kInf;
-      uint32_t m[W];
-#pragma unroll
-      for (int w = 0; w < W; ++w) m[w] = 0u;
-      const uint32_t eb = rowp[v], ee = rowp[v + 1];
-      for (uint32_t e = eb; e < ee; ++e) {
-        const uint64_t ed = edg[e];
-        const uint32_t lo = static_cast<uint32_t>(ed);
-        if (lo & OGS_EDGE_DOWN) continue;
-        const uint32_t u = edge_dst(lo);
-        const bool fromSrc = (u == s);
-        if ((lo & OGS_EDGE_DST_OVERLOADED) && !fromSrc) continue;
-        const D du = dist[u];
-        if (du == kInf) continue;
-        const D cand = du + (hop ? D(1) : static_cast<D>(ed >> 32));
-        if (cand > best) continue;
-        uint32_t c[W];
-        if (fromSrc) {
-          const uint32_t slot = edge_rslot(lo);
-#pragma unroll
-          for (int w = 0; w < W; ++w) {
-            c[w] = (int(slot >> 5) == w) ? (1u << (slot & 31u)) : 0u;
-          }
-        } else {
-#pragma unroll
-          for (int w = 0; w < W; ++w) c[w] = nh[u * W + w];
-        }
-        if (cand < best) {
-          best = cand;
-#pragma unroll
-          for (int w = 0; w < W; ++w) m[w] = c[w];
-        } else {
-#pragma unroll
-          for (int w = 0; w < W; ++w) m[w] |= c[w];
-        }
-      }
-      bool diff = best != dist[v];
-#pragma unroll
-      for (int w = 0; w < W; ++w) diff |= (m[w] != nh[v * W + w]);
-      if (diff) {
-        dist[v] = best;
-#pragma unroll
-        for (int w = 0; w < W; ++w) nh[v * W + w] = m[w];
-        changed = true;
-      }
-    }
-    if (!Scope::any(changed)) break;
-  }
+  // staging writes are ordered before the first reads by the init sync
+  spf_fixpoint<D, W, UT, true, false>(N, s, lane, csr,
+                                      (flags & OGS_F_HOP_METRIC) != 0, dist,
+                                      nh, nullptr);
 
   // ---- SPF outputs (coalesced) -------------------------------------------
   const uint32_t Sn = g.max_nodes;
@@ -383,9 +283,9 @@ hipError_t launch_one(const ogs_graph& g, const ogs_prefix_table& pt,
 
 uint32_t lds_per_unit(int maxNodes, int maxEdges, int W, int distBytes,
                       bool stage) {
-  auto al = [](uint64_t x) { return (x + 15u) & ~uint64_t(15); };
-  uint64_t b = al(uint64_t(maxNodes) * distBytes) + al(uint64_t(maxNodes) * W * 4);
-  if (stage) b += al(uint64_t(maxNodes + 1) * 4) + al(uint64_t(maxEdges) * 8);
+  uint64_t b = align16(uint64_t(maxNodes) * distBytes) +
+      align16(uint64_t(maxNodes) * W * 4);
+  if (stage) b += align16(uint64_t(maxNodes + 1) * 4) + align16(uint64_t(maxEdges) * 8);
   return static_cast<uint32_t>(b);
 }
 

@@ -343,15 +343,15 @@ class BatchRunner {
     if (hb_.hasZeroMetric) throw std::domain_error("zero metric in batch");
     dNodeBase_.upload(hb_.nodeBase.data(), hb_.nodeBase.size());
     dRow_.upload(hb_.rowPtr.data(), hb_.rowPtr.size());
-    dEdges_.upload(hb_.edges.data(), std::max<size_t>(hb_.edges.size(), 1));
-    dFlags_.upload(hb_.nodeFlags.data(), std::max<size_t>(hb_.nodeFlags.size(), 1));
+    dEdges_.upload(hb_.edges.data(), hb_.edges.size());
+    dFlags_.upload(hb_.nodeFlags.data(), hb_.nodeFlags.size());
     dPfxBase_.upload(hb_.pfxBase.data(), hb_.pfxBase.size());
     dAdvOff_.upload(hb_.advOff.data(), hb_.advOff.size());
-    dAdvNode_.upload(hb_.advNode.data(), std::max<size_t>(hb_.advNode.size(), 1));
-    dAdvMetrics_.upload(hb_.advMetrics.data(), std::max<size_t>(hb_.advMetrics.size(), 4));
-    dAdvMinNh_.upload(hb_.advMinNh.data(), std::max<size_t>(hb_.advMinNh.size(), 1));
-    dPfxFlags_.upload(hb_.pfxFlags.data(), std::max<size_t>(hb_.pfxFlags.size(), 1));
-    dUnits_.upload(units_.data(), std::max<size_t>(units_.size(), 1));
+    dAdvNode_.upload(hb_.advNode.data(), hb_.advNode.size());
+    dAdvMetrics_.upload(hb_.advMetrics.data(), hb_.advMetrics.size());
+    dAdvMinNh_.upload(hb_.advMinNh.data(), hb_.advMinNh.size());
+    dPfxFlags_.upload(hb_.pfxFlags.data(), hb_.pfxFlags.size());
+    dUnits_.upload(units_.data(), units_.size());
     const size_t U = units_.size(), db = wide_ ? 8 : 4;
     const size_t Sn = hb_.maxNodes, Sp = std::max(hb_.maxPrefixes, 1);
     dDist_.resize(U * Sn * db);

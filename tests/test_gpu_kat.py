@@ -10,8 +10,6 @@ GPU_KATS = [k for k in kat_cases.ALL_KATS]
 
 @pytest.mark.parametrize("kat", GPU_KATS, ids=lambda f: f.__name__)
 def test_gpu_kat(product, kat):
-    if kat is kat_cases.kat_linkstate_kth_paths:
-        pytest.xfail("KSP2 kernel not built yet")
     kat(product)
 
 
