@@ -117,9 +117,9 @@ def main():
     o_mask = torch.empty(U * W * Sp, dtype=torch.int32, device=dev)
     o_sel = torch.empty(U * Sp, dtype=torch.int32, device=dev)
 
-    g = capi.Graph(h["num_topos"], Sn, h["max_edges"], node_base.data_ptr(),
+    g = capi.Graph(h["num_topos"], Sn, h["max_edges"], h["max_degree"], node_base.data_ptr(),
                    row_ptr.data_ptr(), edges.data_ptr(), node_flags.data_ptr())
-    pt = capi.PrefixTable(Sp, pfx_base.data_ptr(), adv_off.data_ptr(),
+    pt = capi.PrefixTable(Sp, h["max_advertisements"], pfx_base.data_ptr(), adv_off.data_ptr(),
                           adv_node.data_ptr(), adv_metrics.data_ptr(),
                           adv_min_nh.data_ptr(), pfx_flags.data_ptr())
     out = capi.SpfOut(o_dist.data_ptr(), o_nh.data_ptr(), o_meta.data_ptr(),

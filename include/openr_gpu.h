@@ -96,6 +96,7 @@ typedef struct ogs_graph {
   int32_t num_topos;
   int32_t max_nodes;          /* max node count of any topology          */
   int32_t max_edges;          /* max directed-edge count of any topology */
+  int32_t max_degree;         /* max CSR row length of any node          */
   const uint32_t* node_base;  /* [T+1] first global node of topology t   */
   const uint32_t* row_ptr;    /* [total_nodes+1] global edge offsets     */
   const uint64_t* edges;      /* [E] packed as above                     */
@@ -106,6 +107,7 @@ typedef struct ogs_graph {
  * contiguous segment of advertisements (one (node, area) entry each). */
 typedef struct ogs_prefix_table {
   int32_t max_prefixes;       /* max prefixes of any topology (P stride) */
+  int32_t max_advertisements; /* max advertisements of any topology      */
   const uint32_t* pfx_base;   /* [T+1] first global prefix of topology t */
   const uint32_t* adv_off;    /* [P_total+1] advertiser segment offsets  */
   const uint32_t* adv_node;   /* [A] local node id or OGS_NODE_NONE      */
@@ -173,6 +175,11 @@ int ogs_memcpy_h2d(void* dst, const void* src, size_t bytes, void* stream);
 int ogs_memcpy_d2h(void* dst, const void* src, size_t bytes, void* stream);
 int ogs_memset(void* dst, int value, size_t bytes, void* stream);
 int ogs_stream_sync(void* stream);
+
+/* Tuning knobs (process-wide; for A/B measurement):
+ *   "unit_width": small-topology path unit width, 64 / 128 / 256 threads per
+ *                 unit, -1 = automatic (default), 0 = generic kernel only. */
+int ogs_set_option(const char* name, int64_t value);
 
 /* Smallest supported next-hop bitset width (words) for a source degree. */
 int ogs_nh_words_for_degree(int degree);

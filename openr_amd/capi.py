@@ -17,19 +17,21 @@ EXPORTS = [
     "ogs_version", "ogs_last_error", "ogs_device_count", "ogs_set_device",
     "ogs_malloc", "ogs_free", "ogs_memcpy_h2d", "ogs_memcpy_d2h", "ogs_memset",
     "ogs_stream_sync", "ogs_nh_words_for_degree", "ogs_spf_routes",
-    "ogs_ksp_paths",
+    "ogs_ksp_paths", "ogs_set_option",
 ]
 
 
 class Graph(ctypes.Structure):
     _fields_ = [("num_topos", ctypes.c_int32), ("max_nodes", ctypes.c_int32),
-                ("max_edges", ctypes.c_int32), ("node_base", ctypes.c_void_p),
+                ("max_edges", ctypes.c_int32), ("max_degree", ctypes.c_int32),
+                ("node_base", ctypes.c_void_p),
                 ("row_ptr", ctypes.c_void_p), ("edges", ctypes.c_void_p),
                 ("node_flags", ctypes.c_void_p)]
 
 
 class PrefixTable(ctypes.Structure):
-    _fields_ = [("max_prefixes", ctypes.c_int32), ("pfx_base", ctypes.c_void_p),
+    _fields_ = [("max_prefixes", ctypes.c_int32), ("max_advertisements", ctypes.c_int32),
+                ("pfx_base", ctypes.c_void_p),
                 ("adv_off", ctypes.c_void_p), ("adv_node", ctypes.c_void_p),
                 ("adv_metrics", ctypes.c_void_p), ("adv_min_nh", ctypes.c_void_p),
                 ("pfx_flags", ctypes.c_void_p)]
@@ -50,6 +52,8 @@ def load():
         ctypes.c_int32, ctypes.c_uint32, ctypes.c_int32, ctypes.POINTER(SpfOut),
         ctypes.c_void_p]
     lib.ogs_spf_routes.restype = ctypes.c_int
+    lib.ogs_set_option.argtypes = [ctypes.c_char_p, ctypes.c_int64]
+    lib.ogs_set_option.restype = ctypes.c_int
     return lib
 
 

@@ -453,7 +453,7 @@ struct HostBatch {
   std::vector<int32_t> advMetrics;
   std::vector<int64_t> advMinNh;
   std::vector<uint8_t> pfxFlags;
-  int maxNodes{0}, maxEdges{0}, maxPrefixes{0}, maxDegree{0};
+  int maxNodes{0}, maxEdges{0}, maxPrefixes{0}, maxDegree{0}, maxAdvs{0};
   uint64_t maxMetric{0};
   bool hasZeroMetric{false};
   void append(const FlatTopology& t, const PrefixState& ps,

@@ -60,6 +60,7 @@ const std::vector<LinkState::Path>& LinkState::getKthPaths(
   g.num_topos = 1;
   g.max_nodes = int32_t(f.names.size());
   g.max_edges = int32_t(E);
+  g.max_degree = f.maxDegree;
   g.node_base = f.dNodeBase.as<uint32_t>();
   g.row_ptr = f.dRow.as<uint32_t>();
   g.edges = f.dEdges.as<uint64_t>();

@@ -354,6 +354,7 @@ const LinkState::SpfResult& LinkState::getSpfResult(const std::string& node,
   g.num_topos = 1;
   g.max_nodes = int32_t(N);
   g.max_edges = int32_t(f.edges.size());
+  g.max_degree = f.maxDegree;
   g.node_base = f.dNodeBase.as<uint32_t>();
   g.row_ptr = f.dRow.as<uint32_t>();
   g.edges = f.dEdges.as<uint64_t>();

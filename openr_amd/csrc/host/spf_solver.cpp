@@ -80,6 +80,7 @@ void HostBatch::append(const FlatTopology& t, const PrefixState& ps,
   maxMetric = std::max(maxMetric, t.maxMetric);
   hasZeroMetric |= t.hasZeroMetric;
   uint32_t np = 0;
+  const size_t a0 = advNode.size();
   for (const auto& [prefix, entries] : ps.prefixes()) {
     for (const auto& [na, e] : entries) {
       if (na.second != area) {
@@ -98,6 +99,7 @@ void HostBatch::append(const FlatTopology& t, const PrefixState& ps,
   }
   pfxBase.push_back(pfxBase.back() + np);
   maxPrefixes = std::max<int>(maxPrefixes, int(np));
+  maxAdvs = std::max<int>(maxAdvs, int(advNode.size() - a0));
 }
 
 // ------------------------------------------------------------- SpfSolver --
@@ -323,12 +325,14 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(
   g.num_topos = 1;
   g.max_nodes = int32_t(N);
   g.max_edges = int32_t(f.edges.size());
+  g.max_degree = f.maxDegree;
   g.node_base = f.dNodeBase.as<uint32_t>();
   g.row_ptr = f.dRow.as<uint32_t>();
   g.edges = f.dEdges.as<uint64_t>();
   g.node_flags = f.dFlags.as<uint8_t>();
   ogs_prefix_table pt{};
   pt.max_prefixes = int32_t(P);
+  pt.max_advertisements = int32_t(I.table.advEntry.size());
   pt.pfx_base = I.pfxBase.as<uint32_t>();
   pt.adv_off = I.advOff.as<uint32_t>();
   pt.adv_node = I.advNode.as<uint32_t>();

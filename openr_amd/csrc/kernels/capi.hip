@@ -8,6 +8,7 @@
 #include "openr_gpu.h"
 
 namespace ogs {
+extern int g_unitWidth;
 hipError_t launch_spf_routes(const ogs_graph& g, const ogs_prefix_table* pt,
                              const ogs_unit* units, int nUnits, uint32_t flags,
                              int W, const ogs_spf_out& out, hipStream_t stream,
@@ -94,6 +95,18 @@ int ogs_memset(void* dst, int value, size_t bytes, void* stream) {
 int ogs_stream_sync(void* stream) {
   hipError_t e = hipStreamSynchronize(static_cast<hipStream_t>(stream));
   return e == hipSuccess ? OGS_OK : hipFail(e, "hipStreamSynchronize");
+}
+
+int ogs_set_option(const char* name, int64_t value) {
+  if (!name) return fail(OGS_E_INVALID, "option name is NULL");
+  if (std::strcmp(name, "unit_width") == 0) {
+    if (value != -1 && value != 0 && value != 64 && value != 128 && value != 256) {
+      return fail(OGS_E_INVALID, "unit_width must be -1, 0, 64, 128 or 256");
+    }
+    ogs::g_unitWidth = int(value);
+    return OGS_OK;
+  }
+  return fail(OGS_E_INVALID, std::string("unknown option ") + name);
 }
 
 int ogs_nh_words_for_degree(int degree) {

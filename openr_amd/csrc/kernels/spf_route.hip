@@ -31,149 +31,13 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 
 #include "openr_gpu.h"
+#include "route_core.h"
 #include "spf_core.h"
 
 namespace ogs {
-
-struct RouteCfg {
-  bool enableV4, v4OverV6, bestRouteSel;
-};
-
-// Route for one prefix from the unit's SPF state (dist/nh in LDS).
-template <typename D, int W>
-__device__ void route_one(const ogs_prefix_table& pt, uint32_t gp, uint32_t s,
-                          const uint8_t* __restrict__ nflags, const D* dist,
-                          const uint32_t* nh, const RouteCfg& cfg,
-                          uint32_t& meta, D& metric, uint32_t (&mask)[W],
-                          uint32_t& selBits) {
-  constexpr D kInf = DistInf<D>::value;
-  meta = 0;
-  metric = kInf;
-  selBits = 0;
-#pragma unroll
-  for (int w = 0; w < W; ++w) mask[w] = 0;
-
-  // v4 gate (SpfSolver.cpp:169-176)
-  const bool isV4 = pt.pfx_flags[gp] & 1u;
-  if (isV4 && !cfg.enableV4 && !cfg.v4OverV6) {
-    meta = OGS_REASON_V4_DISABLED << OGS_ROUTE_REASON_SHIFT;
-    return;
-  }
-  const uint32_t a0 = pt.adv_off[gp], a1 = pt.adv_off[gp + 1];
-
-  // pass 1: reachability in the advertiser's area (single area => this
-  // SPF), localPrefixConsidered, hard-drain census (SpfSolver.cpp:194-214,
-  // 526-541)
-  bool local = false;
-  uint32_t nReach = 0, nReachUp = 0;
-  for (uint32_t a = a0; a < a1; ++a) {
-    const uint32_t n = pt.adv_node[a];
-    if (n == s) local = true;
-    if (n != OGS_NODE_NONE && dist[n] != kInf) {
-      ++nReach;
-      nReachUp += (nflags[n] & OGS_NODE_OVERLOADED) ? 0u : 1u;
-    }
-  }
-  if (local) meta |= OGS_ROUTE_LOCAL;
-  if (nReach == 0) {
-    meta |= OGS_REASON_UNREACHABLE << OGS_ROUTE_REASON_SHIFT;
-    return;
-  }
-  const bool dropOverloaded = nReachUp != 0;
-  auto filtered = [&](uint32_t n) {
-    return n != OGS_NODE_NONE && dist[n] != kInf &&
-        !(dropOverloaded && (nflags[n] & OGS_NODE_OVERLOADED));
-  };
-
-  // best-route selection (LsdbUtil.cpp:760-823, SHORTEST_DISTANCE):
-  // max (-(drained), path_pref, source_pref), then min distance
-  int32_t bD = INT32_MIN, bP = INT32_MIN, bS = INT32_MIN, bDist = INT32_MAX;
-  if (cfg.bestRouteSel) {
-    for (uint32_t a = a0; a < a1; ++a) {
-      const uint32_t n = pt.adv_node[a];
-      if (!filtered(n)) continue;
-      const int4 m = reinterpret_cast<const int4*>(pt.adv_metrics)[a];
-      const int32_t d =
-          -((m.x != 0 || (nflags[n] & OGS_NODE_SOFTDRAIN)) ? 1 : 0);
-      if (d > bD || (d == bD && (m.y > bP || (m.y == bP && m.z > bS)))) {
-        bD = d;
-        bP = m.y;
-        bS = m.z;
-      }
-    }
-    for (uint32_t a = a0; a < a1; ++a) {
-      const uint32_t n = pt.adv_node[a];
-      if (!filtered(n)) continue;
-      const int4 m = reinterpret_cast<const int4*>(pt.adv_metrics)[a];
-      const int32_t d =
-          -((m.x != 0 || (nflags[n] & OGS_NODE_SOFTDRAIN)) ? 1 : 0);
-      if (d == bD && m.y == bP && m.z == bS && m.w < bDist) bDist = m.w;
-    }
-  }
-  auto selected = [&](uint32_t a, uint32_t n) {
-    if (!filtered(n)) return false;
-    if (!cfg.bestRouteSel) return true;
-    const int4 m = reinterpret_cast<const int4*>(pt.adv_metrics)[a];
-    const int32_t d = -((m.x != 0 || (nflags[n] & OGS_NODE_SOFTDRAIN)) ? 1 : 0);
-    return d == bD && m.y == bP && m.z == bS && m.w == bDist;
-  };
-
-  // selected set: self?, best = smallest (node, area) key (node ids are name
-  // ranks), shortest distance over all selected names (SpfSolver.cpp:664-677)
-  bool self = false;
-  uint32_t bestIdx = 0, bestNode = 0xFFFFFFFFu;
-  D shortest = kInf;
-  for (uint32_t a = a0; a < a1; ++a) {
-    const uint32_t n = pt.adv_node[a];
-    if (!selected(a, n)) continue;
-    if (a - a0 < 32) selBits |= 1u << (a - a0);
-    if (n == s) self = true;
-    if (n < bestNode) {
-      bestNode = n;
-      bestIdx = a - a0;
-    }
-    const D dn = dist[n];
-    if (dn < shortest) shortest = dn;
-  }
-  meta |= OGS_ROUTE_SELECTED | (bestIdx << OGS_ROUTE_BEST_SHIFT);
-  if (nflags[bestNode] & (OGS_NODE_OVERLOADED | OGS_NODE_METRICINC)) {
-    meta |= OGS_ROUTE_DRAINED;  // isNodeDrained (SpfSolver.cpp:543-551)
-  }
-  if (self) {
-    meta |= OGS_REASON_SELF << OGS_ROUTE_REASON_SHIFT;
-    return;
-  }
-  // next-hop union over the min-cost destinations + min-nexthop threshold
-  bool hasMinNh = false;
-  int64_t minNh = INT64_MIN;
-  for (uint32_t a = a0; a < a1; ++a) {
-    const uint32_t n = pt.adv_node[a];
-    if (!selected(a, n)) continue;
-    const int64_t t = pt.adv_min_nh[a];
-    if (t != INT64_MIN && (!hasMinNh || t > minNh)) {
-      hasMinNh = true;
-      minNh = t;
-    }
-    if (dist[n] != shortest) continue;
-#pragma unroll
-    for (int w = 0; w < W; ++w) mask[w] |= nh[n * W + w];
-  }
-  uint32_t cnt = 0;
-#pragma unroll
-  for (int w = 0; w < W; ++w) cnt += __popc(mask[w]);
-  metric = shortest;
-  if (cnt == 0) {
-    meta |= OGS_REASON_NO_NEXTHOP << OGS_ROUTE_REASON_SHIFT;
-    return;
-  }
-  if (hasMinNh && static_cast<uint64_t>(minNh) > cnt) {  // SpfSolver.cpp:612
-    meta |= OGS_REASON_MIN_NEXTHOP << OGS_ROUTE_REASON_SHIFT;
-    return;
-  }
-  meta |= OGS_ROUTE_VALID;
-}
 
 template <typename D, int W, int UT, bool STAGE>
 __global__ __launch_bounds__(kBlock) void spf_route_kernel(
@@ -329,6 +193,20 @@ hipError_t dispatch_d(int W, const ogs_graph& g, const ogs_prefix_table& pt,
   }
 }
 
+template <typename D, int W>
+bool try_small(const ogs_graph& g, const ogs_prefix_table& pt, int hasPrefixes,
+               const ogs_unit* units, int nUnits, uint32_t flags,
+               const ogs_spf_out& out, int maxDegree, uint32_t maxA,
+               int unitWidth, hipStream_t stream, hipError_t* err);
+
+// OGS_UNIT_WIDTH (env) pins the small path's unit width (64/128/256) or
+// disables it (0 = generic kernel only); used for A/B measurements.
+int g_unitWidth = [] {
+  const char* e = getenv("OGS_UNIT_WIDTH");
+  return e ? atoi(e) : -1;
+}();
+int small_unit_width() { return g_unitWidth; }
+
 hipError_t launch_spf_routes(const ogs_graph& g, const ogs_prefix_table* pt,
                              const ogs_unit* units, int nUnits,
                              uint32_t flags, int W, const ogs_spf_out& out,
@@ -336,6 +214,18 @@ hipError_t launch_spf_routes(const ogs_graph& g, const ogs_prefix_table* pt,
   ogs_prefix_table empty{};
   const ogs_prefix_table& p = pt ? *pt : empty;
   const int hasPrefixes = pt ? 1 : 0;
+  const int uw = small_unit_width();
+  if (W == 1 && uw != 0) {
+    hipError_t err = hipSuccess;
+    const int width = uw > 0 ? uw : 0;
+    const uint32_t maxA = hasPrefixes ? uint32_t(p.max_advertisements) : 0u;
+    const bool done = (flags & OGS_F_WIDE_METRIC)
+        ? try_small<uint64_t, 1>(g, p, hasPrefixes, units, nUnits, flags, out,
+                                 g.max_degree, maxA, width, stream, &err)
+        : try_small<uint32_t, 1>(g, p, hasPrefixes, units, nUnits, flags, out,
+                                 g.max_degree, maxA, width, stream, &err);
+    if (done) return err;
+  }
   if (flags & OGS_F_WIDE_METRIC) {
     return dispatch_d<uint64_t>(W, g, p, hasPrefixes, units, nUnits, flags,
                                 out, stream, unsupported);

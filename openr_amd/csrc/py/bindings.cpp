@@ -441,6 +441,7 @@ class BatchRunner {
     g.num_topos = int32_t(topos_.size());
     g.max_nodes = hb_.maxNodes;
     g.max_edges = hb_.maxEdges;
+    g.max_degree = hb_.maxDegree;
     g.node_base = dNodeBase_.as<uint32_t>();
     g.row_ptr = dRow_.as<uint32_t>();
     g.edges = dEdges_.as<uint64_t>();
@@ -450,6 +451,7 @@ class BatchRunner {
   ogs_prefix_table table() const {
     ogs_prefix_table pt{};
     pt.max_prefixes = hb_.maxPrefixes;
+    pt.max_advertisements = hb_.maxAdvs;
     pt.pfx_base = dPfxBase_.as<uint32_t>();
     pt.adv_off = dAdvOff_.as<uint32_t>();
     pt.adv_node = dAdvNode_.as<uint32_t>();
@@ -763,6 +765,7 @@ PYBIND11_MODULE(_decision, m) {
         d["max_nodes"] = h.maxNodes;
         d["max_edges"] = h.maxEdges;
         d["max_prefixes"] = h.maxPrefixes;
+        d["max_advertisements"] = h.maxAdvs;
         d["max_degree"] = h.maxDegree;
         d["num_topos"] = int(h.nodeBase.size() - 1);
         d["nh_words"] = b.nhWords();
