@@ -95,6 +95,7 @@ def main():
     def up(key, dtype):
         return torch.from_numpy(h[key].view(dtype)).to(dev)
 
+    topo_desc = up("topo_desc", "int32")
     node_base = up("node_base", "int32")
     row_ptr = up("row_ptr", "int32")
     edges = up("edges", "int64")
@@ -118,7 +119,7 @@ def main():
     o_sel = torch.empty(U * Sp, dtype=torch.int32, device=dev)
 
     g = capi.Graph(h["num_topos"], Sn, h["max_edges"], h["max_degree"], node_base.data_ptr(),
-                   row_ptr.data_ptr(), edges.data_ptr(), node_flags.data_ptr())
+                   row_ptr.data_ptr(), edges.data_ptr(), node_flags.data_ptr(), topo_desc.data_ptr())
     pt = capi.PrefixTable(Sp, h["max_advertisements"], pfx_base.data_ptr(), adv_off.data_ptr(),
                           adv_node.data_ptr(), adv_metrics.data_ptr(),
                           adv_min_nh.data_ptr(), pfx_flags.data_ptr())

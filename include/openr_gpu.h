@@ -101,6 +101,11 @@ typedef struct ogs_graph {
   const uint32_t* row_ptr;    /* [total_nodes+1] global edge offsets     */
   const uint64_t* edges;      /* [E] packed as above                     */
   const uint8_t* node_flags;  /* [total_nodes]                           */
+  /* Optional [T*8] per-topology descriptor {node_base, nodes, edge_base,
+   * edges, pfx_base, prefixes, adv_base, advertisements} (prefix fields 0
+   * without a prefix table). Redundant with the arrays above; lets a unit
+   * fetch all its offsets with one load instead of a dependent chain. */
+  const uint32_t* topo_desc;
 } ogs_graph;
 
 /* Prefix table: per topology a contiguous range of prefixes, each with a
@@ -177,8 +182,9 @@ int ogs_memset(void* dst, int value, size_t bytes, void* stream);
 int ogs_stream_sync(void* stream);
 
 /* Tuning knobs (process-wide; for A/B measurement):
- *   "unit_width": small-topology path unit width, 64 / 128 / 256 threads per
- *                 unit, -1 = automatic (default), 0 = generic kernel only. */
+ *   "unit_width": small-topology kernel choice: -1 automatic (default),
+ *                 0 generic kernel only, 1 packed wave-per-unit kernel,
+ *                 64 / 128 / 256 split-state kernel at that unit width. */
 int ogs_set_option(const char* name, int64_t value);
 
 /* Smallest supported next-hop bitset width (words) for a source degree. */

@@ -9,7 +9,7 @@ extension raises.
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libopenr_gpu.so")
+LIB_PATH = os.environ.get("OGS_LIB") or os.path.join(_HERE, "lib", "libopenr_gpu.so")
 
 try:
     from . import _decision as decision  # noqa: F401

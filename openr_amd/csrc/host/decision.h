@@ -447,6 +447,7 @@ class RibPolicy {  // RibPolicy.h:70-124
 // prefix table (the bench and the batched parity tests use this).
 struct HostBatch {
   std::vector<uint32_t> nodeBase{0}, rowPtr{0};
+  std::vector<uint32_t> topoDesc;  // [T*8], see ogs_graph.topo_desc
   std::vector<uint64_t> edges;
   std::vector<uint8_t> nodeFlags;
   std::vector<uint32_t> pfxBase{0}, advOff{0}, advNode;

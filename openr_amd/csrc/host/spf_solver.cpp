@@ -70,6 +70,8 @@ void HostBatch::append(const FlatTopology& t, const PrefixState& ps,
                        const std::string& area) {
   const uint32_t N = uint32_t(t.names.size());
   const uint32_t e0 = rowPtr.back();
+  const uint32_t n0 = nodeBase.back(), pb0 = pfxBase.back();
+  const uint32_t ab0 = uint32_t(advNode.size());
   for (uint32_t v = 0; v < N; ++v) rowPtr.push_back(e0 + t.rowPtr[v + 1]);
   edges.insert(edges.end(), t.edges.begin(), t.edges.end());
   nodeFlags.insert(nodeFlags.end(), t.nodeFlags.begin(), t.nodeFlags.end());
@@ -100,11 +102,14 @@ void HostBatch::append(const FlatTopology& t, const PrefixState& ps,
   pfxBase.push_back(pfxBase.back() + np);
   maxPrefixes = std::max<int>(maxPrefixes, int(np));
   maxAdvs = std::max<int>(maxAdvs, int(advNode.size() - a0));
+  topoDesc.insert(topoDesc.end(),
+                  {n0, N, e0, uint32_t(t.edges.size()), pb0, np, ab0,
+                   uint32_t(advNode.size()) - ab0});
 }
 
 // ------------------------------------------------------------- SpfSolver --
 struct SpfSolver::Impl {
-  DeviceBuffer pfxBase, advOff, advNode, advMetrics, advMinNh, pfxFlags;
+  DeviceBuffer pfxBase, advOff, advNode, advMetrics, advMinNh, pfxFlags, desc;
   DeviceBuffer unit, dist, nh, meta, metric, mask, sel;
   const PrefixState* cachedPs{nullptr};
   uint64_t cachedPsVersion{~0ull}, cachedTopoVersion{~0ull};
@@ -292,6 +297,7 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(
     hb.append(f, ps, area);
     I.table.build(ps);
     I.pfxBase.upload(hb.pfxBase.data(), hb.pfxBase.size());
+    I.desc.upload(hb.topoDesc.data(), hb.topoDesc.size());
     I.advOff.upload(hb.advOff.data(), hb.advOff.size());
     I.advNode.upload(hb.advNode.data(), hb.advNode.size());
     I.advMetrics.upload(hb.advMetrics.data(), hb.advMetrics.size());
@@ -326,6 +332,7 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(
   g.max_nodes = int32_t(N);
   g.max_edges = int32_t(f.edges.size());
   g.max_degree = f.maxDegree;
+  g.topo_desc = I.desc.as<uint32_t>();
   g.node_base = f.dNodeBase.as<uint32_t>();
   g.row_ptr = f.dRow.as<uint32_t>();
   g.edges = f.dEdges.as<uint64_t>();

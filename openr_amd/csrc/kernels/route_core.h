@@ -21,13 +21,33 @@ struct RouteCfg {
   bool enableV4, v4OverV6, bestRouteSel;
 };
 
-// Route for one prefix from the unit's SPF state (dist/nh in LDS).
+// SPF state views: split arrays (dist[N], nh[N*W]) or one packed 64-bit
+// word per node (dist | nh << 32, 32-bit distances, W == 1).
 template <typename D, int W>
+struct SplitView {
+  const D* d;
+  const uint32_t* n;
+  __device__ __forceinline__ D dist(uint32_t v) const { return d[v]; }
+  __device__ __forceinline__ uint32_t nh(uint32_t v, int w) const {
+    return n[v * W + w];
+  }
+};
+struct PackedView {
+  const uint64_t* dn;
+  __device__ __forceinline__ uint32_t dist(uint32_t v) const {
+    return static_cast<uint32_t>(dn[v]);
+  }
+  __device__ __forceinline__ uint32_t nh(uint32_t v, int) const {
+    return static_cast<uint32_t>(dn[v] >> 32);
+  }
+};
+
+// Route for one prefix from the unit's SPF state.
+template <typename D, int W, typename View>
 __device__ void route_one(const ogs_prefix_table& pt, uint32_t gp, uint32_t s,
-                          const uint8_t* __restrict__ nflags, const D* dist,
-                          const uint32_t* nh, const RouteCfg& cfg,
-                          uint32_t& meta, D& metric, uint32_t (&mask)[W],
-                          uint32_t& selBits) {
+                          const uint8_t* __restrict__ nflags, const View& sv,
+                          const RouteCfg& cfg, uint32_t& meta, D& metric,
+                          uint32_t (&mask)[W], uint32_t& selBits) {
   constexpr D kInf = DistInf<D>::value;
   meta = 0;
   metric = kInf;
@@ -51,7 +71,7 @@ __device__ void route_one(const ogs_prefix_table& pt, uint32_t gp, uint32_t s,
   for (uint32_t a = a0; a < a1; ++a) {
     const uint32_t n = pt.adv_node[a];
     if (n == s) local = true;
-    if (n != OGS_NODE_NONE && dist[n] != kInf) {
+    if (n != OGS_NODE_NONE && sv.dist(n) != kInf) {
       ++nReach;
       nReachUp += (nflags[n] & OGS_NODE_OVERLOADED) ? 0u : 1u;
     }
@@ -63,7 +83,7 @@ __device__ void route_one(const ogs_prefix_table& pt, uint32_t gp, uint32_t s,
   }
   const bool dropOverloaded = nReachUp != 0;
   auto filtered = [&](uint32_t n) {
-    return n != OGS_NODE_NONE && dist[n] != kInf &&
+    return n != OGS_NODE_NONE && sv.dist(n) != kInf &&
         !(dropOverloaded && (nflags[n] & OGS_NODE_OVERLOADED));
   };
 
@@ -114,7 +134,7 @@ __device__ void route_one(const ogs_prefix_table& pt, uint32_t gp, uint32_t s,
       bestNode = n;
       bestIdx = a - a0;
     }
-    const D dn = dist[n];
+    const D dn = sv.dist(n);
     if (dn < shortest) shortest = dn;
   }
   meta |= OGS_ROUTE_SELECTED | (bestIdx << OGS_ROUTE_BEST_SHIFT);
@@ -136,9 +156,9 @@ __device__ void route_one(const ogs_prefix_table& pt, uint32_t gp, uint32_t s,
       hasMinNh = true;
       minNh = t;
     }
-    if (dist[n] != shortest) continue;
+    if (sv.dist(n) != shortest) continue;
 #pragma unroll
-    for (int w = 0; w < W; ++w) mask[w] |= nh[n * W + w];
+    for (int w = 0; w < W; ++w) mask[w] |= sv.nh(n, w);
   }
   uint32_t cnt = 0;
 #pragma unroll

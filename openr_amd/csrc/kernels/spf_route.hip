@@ -109,8 +109,8 @@ __global__ __launch_bounds__(kBlock) void spf_route_kernel(
     uint32_t meta, selBits;
     D metric;
     uint32_t mask[W];
-    route_one<D, W>(pt, p0 + p, s, nflags, dist, nh, cfg, meta, metric, mask,
-                    selBits);
+    route_one<D, W>(pt, p0 + p, s, nflags, SplitView<D, W>{dist, nh}, cfg,
+                    meta, metric, mask, selBits);
     const size_t o = size_t(uidx) * Sp + p;
     if (out.meta) out.meta[o] = meta;
     if (out.metric) reinterpret_cast<D*>(out.metric)[o] = metric;
@@ -199,8 +199,13 @@ bool try_small(const ogs_graph& g, const ogs_prefix_table& pt, int hasPrefixes,
                const ogs_spf_out& out, int maxDegree, uint32_t maxA,
                int unitWidth, hipStream_t stream, hipError_t* err);
 
-// OGS_UNIT_WIDTH (env) pins the small path's unit width (64/128/256) or
-// disables it (0 = generic kernel only); used for A/B measurements.
+bool try_wave(const ogs_graph& g, const ogs_prefix_table& pt, int hasPrefixes,
+              const ogs_unit* units, int nUnits, uint32_t flags,
+              const ogs_spf_out& out, uint32_t maxA, hipStream_t stream,
+              hipError_t* err);
+
+// unit_width option / OGS_UNIT_WIDTH env: -1 automatic, 0 generic kernel
+// only, 1 wave kernel, 64/128/256 small kernel at that unit width.
 int g_unitWidth = [] {
   const char* e = getenv("OGS_UNIT_WIDTH");
   return e ? atoi(e) : -1;
@@ -215,10 +220,17 @@ hipError_t launch_spf_routes(const ogs_graph& g, const ogs_prefix_table* pt,
   const ogs_prefix_table& p = pt ? *pt : empty;
   const int hasPrefixes = pt ? 1 : 0;
   const int uw = small_unit_width();
+  const uint32_t maxA = hasPrefixes ? uint32_t(p.max_advertisements) : 0u;
+  if (W == 1 && (uw == -1 || uw == 1)) {
+    hipError_t err = hipSuccess;
+    if (try_wave(g, p, hasPrefixes, units, nUnits, flags, out, maxA, stream,
+                 &err)) {
+      return err;
+    }
+  }
   if (W == 1 && uw != 0) {
     hipError_t err = hipSuccess;
-    const int width = uw > 0 ? uw : 0;
-    const uint32_t maxA = hasPrefixes ? uint32_t(p.max_advertisements) : 0u;
+    const int width = uw > 1 ? uw : 0;
     const bool done = (flags & OGS_F_WIDE_METRIC)
         ? try_small<uint64_t, 1>(g, p, hasPrefixes, units, nUnits, flags, out,
                                  g.max_degree, maxA, width, stream, &err)

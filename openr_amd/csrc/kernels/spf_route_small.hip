@@ -111,6 +111,11 @@ __global__ __launch_bounds__(UT == 64 ? 256 : UT) void spf_route_small_kernel(
   const int lane = threadIdx.x % UT;
   const int uidx = blockIdx.x * kUnitsPerBlock + uib;
   if (uidx >= nUnits) return;
+#ifdef OGS_STAMPS  // diagnostic build only: phase clocks into out.sel
+  const uint64_t tStart = __builtin_amdgcn_s_memtime();
+  uint64_t tStaged = 0, tSpf = 0;
+  uint32_t rounds = 0;
+#endif
 
   const ogs_unit unit = units[uidx];
   const uint32_t nb = g.node_base[unit.topo];
@@ -193,6 +198,9 @@ __global__ __launch_bounds__(UT == 64 ? 256 : UT) void spf_route_small_kernel(
   }
   Scope::sync();
 
+#ifdef OGS_STAMPS
+  tStaged = __builtin_amdgcn_s_memtime();
+#endif
   // ---- register-resident node slots --------------------------------------
   const bool hop = flags & OGS_F_HOP_METRIC;
   uint64_t ed[NPL][MAXD];
@@ -202,8 +210,9 @@ __global__ __launch_bounds__(UT == 64 ? 256 : UT) void spf_route_small_kernel(
   for (int k = 0; k < NPL; ++k) {
     const uint32_t v = lane + k * UT;
     const bool own = v < N;
-    const uint32_t eb = own ? lrow[v] : 0u;
-    const uint32_t deg = own ? lrow[v + 1] - eb : 0u;
+    // staged row offsets are global; the staged edges start at e0
+    const uint32_t eb = own ? lrow[v] - e0 : 0u;
+    const uint32_t deg = own ? lrow[v + 1] - lrow[v] : 0u;
 #pragma unroll
     for (int j = 0; j < MAXD; ++j) {
       ed[k][j] = (uint32_t(j) < deg) ? ledg[eb + j] : uint64_t(OGS_EDGE_DOWN);
@@ -279,8 +288,14 @@ __global__ __launch_bounds__(UT == 64 ? 256 : UT) void spf_route_small_kernel(
         changed = true;
       }
     }
+#ifdef OGS_STAMPS
+    ++rounds;
+#endif
     if (!Scope::any(changed)) break;
   }
+#ifdef OGS_STAMPS
+  tSpf = __builtin_amdgcn_s_memtime();
+#endif
 
   // ---- SPF outputs ---------------------------------------------------------
   const uint32_t Sn = g.max_nodes;
@@ -314,8 +329,8 @@ __global__ __launch_bounds__(UT == 64 ? 256 : UT) void spf_route_small_kernel(
     uint32_t meta, selBits;
     D metric;
     uint32_t mask[W];
-    route_one<D, W>(lp, p, s, lflags, dist, nh, cfg, meta, metric, mask,
-                    selBits);
+    route_one<D, W>(lp, p, s, lflags, SplitView<D, W>{dist, nh}, cfg, meta,
+                    metric, mask, selBits);
     const size_t o = size_t(uidx) * Sp + p;
     if (out.meta) out.meta[o] = meta;
     if (out.metric) reinterpret_cast<D*>(out.metric)[o] = metric;
@@ -325,6 +340,17 @@ __global__ __launch_bounds__(UT == 64 ? 256 : UT) void spf_route_small_kernel(
       for (int w = 0; w < W; ++w) out.mask[(size_t(uidx) * W + w) * Sp + p] = mask[w];
     }
   }
+#ifdef OGS_STAMPS
+  Scope::sync();
+  if (lane == 0 && out.sel) {
+    const uint64_t tEnd = __builtin_amdgcn_s_memtime();
+    uint32_t* d = out.sel + size_t(uidx) * Sp;
+    d[0] = uint32_t(tStaged - tStart);
+    d[1] = uint32_t(tSpf - tStaged);
+    d[2] = uint32_t(tEnd - tSpf);
+    d[3] = rounds;
+  }
+#endif
 }
 
 template <typename D, int W, int UT, int NPL, int MAXD>

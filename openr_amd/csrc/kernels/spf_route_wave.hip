@@ -1,0 +1,403 @@
+// spf_route_wave.hip — one WAVEFRONT per (topology, source) unit, 32-bit
+// distances, single-word next-hop sets: the C1/C2 hot path.
+//
+// Algorithm and outputs are those of spf_route.hip (reference mapping in its
+// header). Measured on MI355X, a C2 launch is 4096 units all resident at
+// once (16 waves/CU), and the relaxation rounds are LDS-throughput bound
+// (random-address reads into 16 units' working sets). This variant cuts LDS
+// instructions, not latency:
+//  * per node ONE 64-bit LDS word {dist, next-hop bits}: one ds_read_b64
+//    per edge instead of two ds_read_b32;
+//  * dirty tracking in scalar registers: the wave's ballots of "changed in
+//    this round" (one 64-bit mask per node slot) say which nodes moved; a
+//    node re-reads its neighbours only when one of them moved since its last
+//    evaluation (its value is a pure function of its neighbours', so a node
+//    whose neighbours are unchanged already holds its fixpoint value). The
+//    source starts as the only "moved" node;
+//  * edges (<= MAXD per node) and the node's own value stay in registers;
+//  * one dependent global load for the unit's offsets (ogs_graph.topo_desc)
+//    and one batch of staging loads for CSR + prefix table;
+//  * single-advertiser prefixes take a straight-line route path.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "openr_gpu.h"
+#include "route_core.h"
+#include "spf_core.h"
+
+namespace ogs {
+
+struct WaveLayout {
+  uint32_t dn, row, edges, flags, advOff, advNode, advMetrics, advMinNh,
+      pfxFlags, total;
+  __host__ __device__ static WaveLayout make(uint32_t N, uint32_t E, uint32_t P,
+                                             uint32_t A) {
+    WaveLayout L;
+    uint32_t o = 0;
+    L.dn = o;
+    o += align16(uint64_t(N) * 8);
+    L.row = o;
+    o += align16(uint64_t(N + 1) * 4);
+    L.edges = o;
+    o += align16(uint64_t(E) * 8);
+    L.flags = o;
+    o += align16(N);
+    L.advOff = o;
+    o += align16(uint64_t(P + 1) * 4);
+    L.advNode = o;
+    o += align16(uint64_t(A) * 4);
+    L.advMetrics = o;
+    o += align16(uint64_t(A) * 16);
+    L.advMinNh = o;
+    o += align16(uint64_t(A) * 8);
+    L.pfxFlags = o;
+    o += align16(P);
+    L.total = o;
+    return L;
+  }
+};
+
+template <int K, typename T>
+struct WStage {  // K elements per lane, all loads before any store
+  T v[K];
+  __device__ __forceinline__ void load(const T* __restrict__ src, uint32_t n,
+                                       int lane) {
+    if (n == 0) return;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const uint32_t i = uint32_t(k * 64 + lane);
+      v[k] = src[i < n ? i : n - 1];
+    }
+  }
+  __device__ __forceinline__ void store(T* dst, uint32_t n, int lane) const {
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const uint32_t i = uint32_t(k * 64 + lane);
+      if (i < n) dst[i] = v[k];
+    }
+  }
+};
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Straight-line route for a prefix with exactly one advertisement (same
+// result as route_one on a one-entry segment).
+__device__ __forceinline__ void route_single(uint32_t n, int64_t minNh,
+                                             uint32_t s, const uint8_t* nflags,
+                                             const uint64_t* dn, uint32_t& meta,
+                                             uint32_t& metric, uint32_t& mask) {
+  meta = (n == s) ? OGS_ROUTE_LOCAL : 0u;
+  metric = 0xFFFFFFFFu;
+  mask = 0u;
+  const uint64_t x = (n != OGS_NODE_NONE) ? dn[n] : ~0ull;
+  const uint32_t d = static_cast<uint32_t>(x);
+  if (n == OGS_NODE_NONE || d == 0xFFFFFFFFu) {
+    meta |= OGS_REASON_UNREACHABLE << OGS_ROUTE_REASON_SHIFT;
+    return;
+  }
+  meta |= OGS_ROUTE_SELECTED;  // best index 0
+  if (nflags[n] & (OGS_NODE_OVERLOADED | OGS_NODE_METRICINC)) {
+    meta |= OGS_ROUTE_DRAINED;
+  }
+  if (n == s) {
+    meta |= OGS_REASON_SELF << OGS_ROUTE_REASON_SHIFT;
+    return;
+  }
+  mask = static_cast<uint32_t>(x >> 32);
+  metric = d;
+  const uint32_t cnt = __popc(mask);
+  if (cnt == 0) {
+    meta |= OGS_REASON_NO_NEXTHOP << OGS_ROUTE_REASON_SHIFT;
+  } else if (minNh != INT64_MIN && static_cast<uint64_t>(minNh) > cnt) {
+    meta |= OGS_REASON_MIN_NEXTHOP << OGS_ROUTE_REASON_SHIFT;
+  } else {
+    meta |= OGS_ROUTE_VALID;
+  }
+}
+
+template <int NPL, int MAXD>
+__global__ __launch_bounds__(256) void spf_route_wave_kernel(
+    ogs_graph g, ogs_prefix_table pt, int hasPrefixes,
+    const ogs_unit* __restrict__ units, int nUnits, uint32_t flags,
+    ogs_spf_out out, uint32_t ldsPerUnit, uint32_t maxA) {
+  constexpr uint32_t kInf = 0xFFFFFFFFu;
+  const int uib = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int uidx = blockIdx.x * 4 + uib;
+  if (uidx >= nUnits) return;
+
+  // ---- unit offsets -------------------------------------------------------
+  const ogs_unit unit = units[uidx];
+  const uint32_t s = unit.src;
+  uint32_t nb, N, e0, E, p0 = 0, P = 0, a0 = 0, A = 0;
+  if (g.topo_desc) {
+    const uint4* d = reinterpret_cast<const uint4*>(g.topo_desc) + 2 * unit.topo;
+    const uint4 x = d[0], y = d[1];
+    nb = x.x;
+    N = x.y;
+    e0 = x.z;
+    E = x.w;
+    if (hasPrefixes) {
+      p0 = y.x;
+      P = y.y;
+      a0 = y.z;
+      A = y.w;
+    }
+  } else {
+    nb = g.node_base[unit.topo];
+    N = g.node_base[unit.topo + 1] - nb;
+    e0 = g.row_ptr[nb];
+    E = g.row_ptr[nb + N] - e0;
+    if (hasPrefixes) {
+      p0 = pt.pfx_base[unit.topo];
+      P = pt.pfx_base[unit.topo + 1] - p0;
+      a0 = pt.adv_off[p0];
+      A = pt.adv_off[p0 + P] - a0;
+    }
+  }
+  const WaveLayout L = WaveLayout::make(g.max_nodes, g.max_edges,
+                                        hasPrefixes ? pt.max_prefixes : 0,
+                                        hasPrefixes ? maxA : 0);
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* base = smem + uib * ldsPerUnit;
+  uint64_t* dn = reinterpret_cast<uint64_t*>(base + L.dn);
+  uint32_t* lrow = reinterpret_cast<uint32_t*>(base + L.row);
+  uint64_t* ledg = reinterpret_cast<uint64_t*>(base + L.edges);
+  uint8_t* lflags = reinterpret_cast<uint8_t*>(base + L.flags);
+  uint32_t* lAdvOff = reinterpret_cast<uint32_t*>(base + L.advOff);
+  uint32_t* lAdvNode = reinterpret_cast<uint32_t*>(base + L.advNode);
+  int4* lAdvMetrics = reinterpret_cast<int4*>(base + L.advMetrics);
+  int64_t* lAdvMinNh = reinterpret_cast<int64_t*>(base + L.advMinNh);
+  uint8_t* lPfxFlags = reinterpret_cast<uint8_t*>(base + L.pfxFlags);
+
+  // ---- staging: one batch of loads, then LDS writes -----------------------
+  {
+    WStage<NPL + 1, uint32_t> sRow;
+    WStage<NPL * MAXD, uint64_t> sEdge;  // E <= N * MAXD <= 64 * NPL * MAXD
+    WStage<NPL, uint8_t> sFlag;
+    sRow.load(g.row_ptr + nb, N + 1, lane);
+    sEdge.load(g.edges + e0, E, lane);
+    sFlag.load(g.node_flags + nb, N, lane);
+    constexpr int KP = NPL + 1;  // prefixes per lane per pass (P <= 64*KP)
+    WStage<KP, uint32_t> sOff, sNode;
+    WStage<KP, int4> sMet;
+    WStage<KP, int64_t> sMin;
+    WStage<KP, uint8_t> sPf;
+    const bool pfxFits = (P + 1 <= 64u * KP) && (A <= 64u * KP);
+    if (hasPrefixes && pfxFits) {
+      sOff.load(pt.adv_off + p0, P + 1, lane);
+      sNode.load(pt.adv_node + a0, A, lane);
+      sMet.load(reinterpret_cast<const int4*>(pt.adv_metrics) + a0, A, lane);
+      sMin.load(pt.adv_min_nh + a0, A, lane);
+      sPf.load(pt.pfx_flags + p0, P, lane);
+    }
+    sRow.store(lrow, N + 1, lane);
+    sEdge.store(ledg, E, lane);
+    sFlag.store(lflags, N, lane);
+    if (hasPrefixes && pfxFits) {
+      sOff.store(lAdvOff, P + 1, lane);
+      sNode.store(lAdvNode, A, lane);
+      sMet.store(lAdvMetrics, A, lane);
+      sMin.store(lAdvMinNh, A, lane);
+      sPf.store(lPfxFlags, P, lane);
+    } else if (hasPrefixes) {  // rare: long prefix tables, plain loop
+      for (uint32_t i = lane; i <= P; i += 64) lAdvOff[i] = pt.adv_off[p0 + i];
+      for (uint32_t i = lane; i < P; i += 64) lPfxFlags[i] = pt.pfx_flags[p0 + i];
+      for (uint32_t i = lane; i < A; i += 64) {
+        lAdvNode[i] = pt.adv_node[a0 + i];
+        lAdvMetrics[i] = reinterpret_cast<const int4*>(pt.adv_metrics)[a0 + i];
+        lAdvMinNh[i] = pt.adv_min_nh[a0 + i];
+      }
+    }
+  }
+  wave_sync();
+
+  // ---- registers: edges and own values of the lane's node slots -----------
+  const bool hop = flags & OGS_F_HOP_METRIC;
+  uint64_t ed[NPL][MAXD];
+  uint32_t dcur[NPL], ncur[NPL];
+#pragma unroll
+  for (int k = 0; k < NPL; ++k) {
+    const uint32_t v = lane + k * 64;
+    const bool own = v < N;
+    const uint32_t eb = own ? lrow[v] - e0 : 0u;
+    const uint32_t deg = own ? lrow[v + 1] - lrow[v] : 0u;
+#pragma unroll
+    for (int j = 0; j < MAXD; ++j) {
+      ed[k][j] = (uint32_t(j) < deg) ? ledg[eb + j] : uint64_t(OGS_EDGE_DOWN);
+    }
+    dcur[k] = (v == s) ? 0u : kInf;
+    ncur[k] = 0u;
+    if (own) dn[v] = dcur[k];
+  }
+  wave_sync();
+
+  // ---- SPF with dirty tracking ----------------------------------------------
+  uint64_t moved[NPL];  // nodes changed since the previous round (uniform)
+#pragma unroll
+  for (int k = 0; k < NPL; ++k) moved[k] = (s >> 6) == uint32_t(k) ? 1ull << (s & 63) : 0ull;
+  for (;;) {
+    uint64_t now[NPL];
+#pragma unroll
+    for (int k = 0; k < NPL; ++k) now[k] = 0ull;
+    bool any = false;
+#pragma unroll
+    for (int k = 0; k < NPL; ++k) {
+      const uint32_t v = lane + k * 64;
+      // a neighbour moved in the last round, or earlier in this one?
+      bool dirty = false;
+#pragma unroll
+      for (int j = 0; j < MAXD; ++j) {
+        const uint32_t lo = static_cast<uint32_t>(ed[k][j]);
+        const uint32_t u = edge_dst(lo);
+        uint64_t set = moved[0] | now[0];
+#pragma unroll
+        for (int kk = 1; kk < NPL; ++kk) {
+          set = (u >> 6) == uint32_t(kk) ? (moved[kk] | now[kk]) : set;
+        }
+        dirty |= !(lo & OGS_EDGE_DOWN) && ((set >> (u & 63)) & 1ull);
+      }
+      bool changed = false;
+      if (dirty && v < N && v != s) {
+        uint64_t x[MAXD];
+        bool ok[MAXD];
+#pragma unroll
+        for (int j = 0; j < MAXD; ++j) {
+          const uint32_t lo = static_cast<uint32_t>(ed[k][j]);
+          const uint32_t u = edge_dst(lo);
+          ok[j] = !(lo & OGS_EDGE_DOWN) &&
+              !((lo & OGS_EDGE_DST_OVERLOADED) && u != s);
+          x[j] = dn[ok[j] ? u : 0u];
+        }
+        uint32_t best = kInf;
+        uint32_t cand[MAXD];
+#pragma unroll
+        for (int j = 0; j < MAXD; ++j) {
+          const uint32_t du = static_cast<uint32_t>(x[j]);
+          const uint32_t w = hop ? 1u : static_cast<uint32_t>(ed[k][j] >> 32);
+          cand[j] = (ok[j] && du != kInf) ? du + w : kInf;
+          best = cand[j] < best ? cand[j] : best;
+        }
+        uint32_t m = 0u;
+#pragma unroll
+        for (int j = 0; j < MAXD; ++j) {
+          const uint32_t lo = static_cast<uint32_t>(ed[k][j]);
+          const uint32_t slot = edge_rslot(lo);
+          const uint32_t c = (edge_dst(lo) == s) ? (1u << (slot & 31u))
+                                                 : static_cast<uint32_t>(x[j] >> 32);
+          m |= (cand[j] == best && best != kInf) ? c : 0u;
+        }
+        if (best != dcur[k] || m != ncur[k]) {
+          dcur[k] = best;
+          ncur[k] = m;
+          dn[v] = uint64_t(best) | (uint64_t(m) << 32);
+          changed = true;
+        }
+      }
+      now[k] = __ballot(changed);
+      any |= now[k] != 0ull;
+    }
+#pragma unroll
+    for (int k = 0; k < NPL; ++k) moved[k] = now[k];
+    if (!any) break;
+    wave_sync();
+  }
+  wave_sync();
+
+  // ---- SPF outputs ----------------------------------------------------------
+  const uint32_t Sn = g.max_nodes;
+#pragma unroll
+  for (int k = 0; k < NPL; ++k) {
+    const uint32_t v = lane + k * 64;
+    if (v >= N) continue;
+    if (out.dist) static_cast<uint32_t*>(out.dist)[size_t(uidx) * Sn + v] = dcur[k];
+    if (out.nh) out.nh[size_t(uidx) * Sn + v] = ncur[k];
+  }
+  if (!hasPrefixes) return;
+
+  // ---- fused RouteDb --------------------------------------------------------
+  const RouteCfg cfg{(flags & OGS_F_ENABLE_V4) != 0,
+                     (flags & OGS_F_V4_OVER_V6) != 0,
+                     (flags & OGS_F_BEST_ROUTE_SELECTION) != 0};
+  ogs_prefix_table lp{};
+  lp.max_prefixes = pt.max_prefixes;
+  lp.adv_off = lAdvOff;
+  lp.adv_node = lAdvNode;
+  lp.adv_metrics = reinterpret_cast<const int32_t*>(lAdvMetrics);
+  lp.adv_min_nh = lAdvMinNh;
+  lp.pfx_flags = lPfxFlags;
+  const uint32_t Sp = pt.max_prefixes;
+  for (uint32_t p = lane; p < P; p += 64) {
+    uint32_t meta, metric, mask, selBits;
+    const uint32_t b0 = lAdvOff[p] - a0, b1 = lAdvOff[p + 1] - a0;
+    const bool gated = (lPfxFlags[p] & 1u) && !cfg.enableV4 && !cfg.v4OverV6;
+    if (b1 - b0 == 1 && !gated) {
+      route_single(lAdvNode[b0], lAdvMinNh[b0], s, lflags, dn, meta, metric,
+                   mask);
+      selBits = (meta & OGS_ROUTE_SELECTED) ? 1u : 0u;
+    } else {
+      uint32_t mk[1];
+      // route_one indexes the prefix table by prefix; rebase the segment
+      lp.adv_node = lAdvNode - a0;
+      lp.adv_metrics = reinterpret_cast<const int32_t*>(lAdvMetrics - a0);
+      lp.adv_min_nh = lAdvMinNh - a0;
+      route_one<uint32_t, 1>(lp, p, s, lflags, PackedView{dn}, cfg, meta,
+                             metric, mk, selBits);
+      mask = mk[0];
+    }
+    const size_t o = size_t(uidx) * Sp + p;
+    if (out.meta) out.meta[o] = meta;
+    if (out.metric) static_cast<uint32_t*>(out.metric)[o] = metric;
+    if (out.sel) out.sel[o] = selBits;
+    if (out.mask) out.mask[o] = mask;
+  }
+}
+
+template <int NPL, int MAXD>
+hipError_t launch_wave(const ogs_graph& g, const ogs_prefix_table& pt,
+                       int hasPrefixes, const ogs_unit* units, int nUnits,
+                       uint32_t flags, const ogs_spf_out& out, uint32_t lds,
+                       uint32_t maxA, hipStream_t stream) {
+  const int grid = (nUnits + 3) / 4;
+  const size_t bytes = size_t(lds) * 4;
+  auto k = spf_route_wave_kernel<NPL, MAXD>;
+  if (bytes > 64 * 1024) {
+    hipError_t e = hipFuncSetAttribute(
+        reinterpret_cast<const void*>(k),
+        hipFuncAttributeMaxDynamicSharedMemorySize, int(bytes));
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(k, dim3(grid), dim3(256), bytes, stream, g, pt,
+                     hasPrefixes, units, nUnits, flags, out, lds, maxA);
+  return hipGetLastError();
+}
+
+bool try_wave(const ogs_graph& g, const ogs_prefix_table& pt, int hasPrefixes,
+              const ogs_unit* units, int nUnits, uint32_t flags,
+              const ogs_spf_out& out, uint32_t maxA, hipStream_t stream,
+              hipError_t* err) {
+  if (flags & OGS_F_WIDE_METRIC) return false;
+  if (g.max_nodes > 256 || g.max_degree > 8 || g.max_degree < 0) return false;
+  const uint32_t P = hasPrefixes ? pt.max_prefixes : 0;
+  const uint32_t A = hasPrefixes ? maxA : 0;
+  const uint32_t lds = WaveLayout::make(g.max_nodes, g.max_edges, P, A).total;
+  if (uint64_t(lds) * 4 > 160 * 1024) return false;
+  const int N = g.max_nodes;
+  const bool d4 = g.max_degree <= 4;
+#define OGS_WAVE(NPL_, MAXD_)                                                 \
+  *err = launch_wave<NPL_, MAXD_>(g, pt, hasPrefixes, units, nUnits, flags,   \
+                                  out, lds, A, stream);                       \
+  return true;
+  if (N <= 64) { if (d4) { OGS_WAVE(1, 4) } OGS_WAVE(1, 8) }
+  if (N <= 128) { if (d4) { OGS_WAVE(2, 4) } OGS_WAVE(2, 8) }
+  if (d4) { OGS_WAVE(4, 4) }
+  OGS_WAVE(4, 8)
+#undef OGS_WAVE
+}
+
+}  // namespace ogs

@@ -342,6 +342,7 @@ class BatchRunner {
   void upload() {
     if (hb_.hasZeroMetric) throw std::domain_error("zero metric in batch");
     dNodeBase_.upload(hb_.nodeBase.data(), hb_.nodeBase.size());
+    dDesc_.upload(hb_.topoDesc.data(), hb_.topoDesc.size());
     dRow_.upload(hb_.rowPtr.data(), hb_.rowPtr.size());
     dEdges_.upload(hb_.edges.data(), hb_.edges.size());
     dFlags_.upload(hb_.nodeFlags.data(), hb_.nodeFlags.size());
@@ -442,6 +443,7 @@ class BatchRunner {
     g.max_nodes = hb_.maxNodes;
     g.max_edges = hb_.maxEdges;
     g.max_degree = hb_.maxDegree;
+    g.topo_desc = dDesc_.as<uint32_t>();
     g.node_base = dNodeBase_.as<uint32_t>();
     g.row_ptr = dRow_.as<uint32_t>();
     g.edges = dEdges_.as<uint64_t>();
@@ -473,7 +475,7 @@ class BatchRunner {
   std::vector<std::string> unitSrc_;
   int W_{1};
   bool wide_{false};
-  DeviceBuffer dNodeBase_, dRow_, dEdges_, dFlags_, dPfxBase_, dAdvOff_,
+  DeviceBuffer dDesc_, dNodeBase_, dRow_, dEdges_, dFlags_, dPfxBase_, dAdvOff_,
       dAdvNode_, dAdvMetrics_, dAdvMinNh_, dPfxFlags_, dUnits_, dDist_, dNh_,
       dMeta_, dMetric_, dMask_, dSel_;
   std::vector<uint64_t> dist_, metric_;
@@ -747,6 +749,7 @@ PYBIND11_MODULE(_decision, m) {
         const HostBatch& h = b.host();
         py::dict d;
         d["node_base"] = npcopy(h.nodeBase);
+        d["topo_desc"] = npcopy(h.topoDesc);
         d["row_ptr"] = npcopy(h.rowPtr);
         d["edges"] = npcopy(h.edges);
         d["node_flags"] = npcopy(h.nodeFlags);

@@ -22,19 +22,19 @@ def main():
     h = br.host_arrays()
     dev = torch.device("cuda", 0)
     t = {k: torch.from_numpy(h[k]).to(dev) for k in
-         ("node_base", "row_ptr", "edges", "node_flags", "pfx_base", "adv_off",
+         ("topo_desc", "node_base", "row_ptr", "edges", "node_flags", "pfx_base", "adv_off",
           "adv_node", "adv_metrics", "adv_min_nh", "pfx_flags", "units")}
     U = len(h["units"]) // 2
     Sn, Sp, W = h["max_nodes"], h["max_prefixes"], h["nh_words"]
     g = capi.Graph(h["num_topos"], Sn, h["max_edges"], h["max_degree"], t["node_base"].data_ptr(),
-                   t["row_ptr"].data_ptr(), t["edges"].data_ptr(), t["node_flags"].data_ptr())
+                   t["row_ptr"].data_ptr(), t["edges"].data_ptr(), t["node_flags"].data_ptr(), t["topo_desc"].data_ptr())
     pt = capi.PrefixTable(Sp, h["max_advertisements"], t["pfx_base"].data_ptr(),
                           t["adv_off"].data_ptr(), t["adv_node"].data_ptr(),
                           t["adv_metrics"].data_ptr(), t["adv_min_nh"].data_ptr(),
                           t["pfx_flags"].data_ptr())
     outs = {}
     stream = torch.cuda.current_stream(dev)
-    variants = [int(x) for x in os.environ.get("VARIANTS", "0,64,128,256").split(",")]
+    variants = [int(x) for x in os.environ.get("VARIANTS", "0,1,64,128").split(",")]
     times = {v: [] for v in variants}
     for v in variants:
         o = [torch.zeros(n, dtype=torch.int32, device=dev) for n in
