@@ -184,6 +184,7 @@ int ogs_stream_sync(void* stream);
 /* Tuning knobs (process-wide; for A/B measurement):
  *   "unit_width": small-topology kernel choice: -1 automatic (default),
  *                 0 generic kernel only, 1 packed wave-per-unit kernel,
+ *                 2 the same with dirty-node tracking,
  *                 64 / 128 / 256 split-state kernel at that unit width. */
 int ogs_set_option(const char* name, int64_t value);
 
@@ -196,7 +197,7 @@ int ogs_nh_words_for_degree(int degree);
  * hipStream_t; NULL = default stream). One wavefront per unit for small
  * topologies, one workgroup per unit for large ones (chosen internally).
  * 32-bit distances are exact only when max_metric * (max_nodes - 1) <
- * 2^32 - 1; the caller sets OGS_F_WIDE_METRIC otherwise (the adapter does).
+ * 2^31 - 1; the caller sets OGS_F_WIDE_METRIC otherwise (the adapter does).
  * Replaces: LinkState::runSpf/getSpfResult (LinkState.cpp:705-820) and the
  * per-prefix loop of SpfSolver::buildRouteDb (SpfSolver.cpp:335-340,
  * 160-311, 455-767), single area. */

@@ -315,7 +315,7 @@ bool needsWide(const FlatTopology& f, bool useLinkMetric) {
   if (!useLinkMetric) return false;
   const uint64_t n = f.names.empty() ? 0 : f.names.size() - 1;
   return f.maxMetric != 0 && n != 0 &&
-      f.maxMetric > (0xFFFFFFFEull / n);
+      f.maxMetric > (0x7FFFFFFEull / n);
 }
 }  // namespace
 

@@ -162,7 +162,8 @@ NextHopThrift makeNh(const Link& l, const std::string& me, bool useV4,
 
 bool wideDistancesNeeded(const FlatTopology& f) {
   const uint64_t n = f.names.empty() ? 0 : f.names.size() - 1;
-  return f.maxMetric != 0 && n != 0 && f.maxMetric > 0xFFFFFFFEull / n;
+  // 32-bit kernels cap "unreachable" at 2^31 - 1 inside their loops
+  return f.maxMetric != 0 && n != 0 && f.maxMetric > 0x7FFFFFFEull / n;
 }
 
 void PrefixHostTable::build(const PrefixState& ps) {

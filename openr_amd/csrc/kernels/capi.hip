@@ -100,7 +100,7 @@ int ogs_stream_sync(void* stream) {
 int ogs_set_option(const char* name, int64_t value) {
   if (!name) return fail(OGS_E_INVALID, "option name is NULL");
   if (std::strcmp(name, "unit_width") == 0) {
-    if (value != -1 && value != 0 && value != 1 && value != 64 &&
+    if (value != -1 && value != 0 && value != 1 && value != 2 && value != 64 &&
         value != 128 && value != 256) {
       return fail(OGS_E_INVALID, "unit_width must be -1, 0, 1, 64, 128 or 256");
     }

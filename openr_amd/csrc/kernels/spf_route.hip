@@ -201,8 +201,8 @@ bool try_small(const ogs_graph& g, const ogs_prefix_table& pt, int hasPrefixes,
 
 bool try_wave(const ogs_graph& g, const ogs_prefix_table& pt, int hasPrefixes,
               const ogs_unit* units, int nUnits, uint32_t flags,
-              const ogs_spf_out& out, uint32_t maxA, hipStream_t stream,
-              hipError_t* err);
+              const ogs_spf_out& out, uint32_t maxA, bool dirty,
+              hipStream_t stream, hipError_t* err);
 
 // unit_width option / OGS_UNIT_WIDTH env: -1 automatic, 0 generic kernel
 // only, 1 wave kernel, 64/128/256 small kernel at that unit width.
@@ -221,10 +221,10 @@ hipError_t launch_spf_routes(const ogs_graph& g, const ogs_prefix_table* pt,
   const int hasPrefixes = pt ? 1 : 0;
   const int uw = small_unit_width();
   const uint32_t maxA = hasPrefixes ? uint32_t(p.max_advertisements) : 0u;
-  if (W == 1 && (uw == -1 || uw == 1)) {
+  if (W == 1 && (uw == -1 || uw == 1 || uw == 2)) {
     hipError_t err = hipSuccess;
-    if (try_wave(g, p, hasPrefixes, units, nUnits, flags, out, maxA, stream,
-                 &err)) {
+    if (try_wave(g, p, hasPrefixes, units, nUnits, flags, out, maxA, uw == 2,
+                 stream, &err)) {
       return err;
     }
   }

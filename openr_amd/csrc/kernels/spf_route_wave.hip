@@ -120,7 +120,7 @@ __device__ __forceinline__ void route_single(uint32_t n, int64_t minNh,
   }
 }
 
-template <int NPL, int MAXD>
+template <int NPL, int MAXD, bool DIRTY>
 __global__ __launch_bounds__(256) void spf_route_wave_kernel(
     ogs_graph g, ogs_prefix_table pt, int hasPrefixes,
     const ogs_unit* __restrict__ units, int nUnits, uint32_t flags,
@@ -130,6 +130,11 @@ __global__ __launch_bounds__(256) void spf_route_wave_kernel(
   const int lane = threadIdx.x & 63;
   const int uidx = blockIdx.x * 4 + uib;
   if (uidx >= nUnits) return;
+#ifdef OGS_STAMPS  // diagnostic build only: phase clocks into out.sel
+  const uint64_t tStart = __builtin_amdgcn_s_memtime();
+  uint64_t tDesc = 0, tStaged = 0, tSpf = 0;
+  uint32_t rounds = 0, evals = 0;
+#endif
 
   // ---- unit offsets -------------------------------------------------------
   const ogs_unit unit = units[uidx];
@@ -160,6 +165,10 @@ __global__ __launch_bounds__(256) void spf_route_wave_kernel(
       A = pt.adv_off[p0 + P] - a0;
     }
   }
+#ifdef OGS_STAMPS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  tDesc = __builtin_amdgcn_s_memtime();
+#endif
   const WaveLayout L = WaveLayout::make(g.max_nodes, g.max_edges,
                                         hasPrefixes ? pt.max_prefixes : 0,
                                         hasPrefixes ? maxA : 0);
@@ -216,28 +225,46 @@ __global__ __launch_bounds__(256) void spf_route_wave_kernel(
     }
   }
   wave_sync();
+#ifdef OGS_STAMPS
+  tStaged = __builtin_amdgcn_s_memtime();
+#endif
 
-  // ---- registers: edges and own values of the lane's node slots -----------
+  // ---- registers: per-edge constants of the lane's node slots -------------
+  // Distances inside the loop are capped at kCap = 2^31 - 1 ("unreachable"),
+  // unusable edges carry weight kCap, so cand = du + w never wraps (the host
+  // guarantees every real path < 2^31 - 1 when it picks this kernel) and
+  // min() needs no predicate. The source's next-hop word is 0, so the tight
+  // contribution of edge j is nh(u) | srcBit_j with srcBit_j = the source
+  // link slot bit when u == src, else 0 (LinkState.cpp:808-811).
+  constexpr uint32_t kCap = 0x7FFFFFFFu;
   const bool hop = flags & OGS_F_HOP_METRIC;
-  uint64_t ed[NPL][MAXD];
+  uint32_t eu[NPL][MAXD], ew[NPL][MAXD], eb[NPL][MAXD];
   uint32_t dcur[NPL], ncur[NPL];
 #pragma unroll
   for (int k = 0; k < NPL; ++k) {
     const uint32_t v = lane + k * 64;
     const bool own = v < N;
-    const uint32_t eb = own ? lrow[v] - e0 : 0u;
+    const uint32_t e = own ? lrow[v] - e0 : 0u;
     const uint32_t deg = own ? lrow[v + 1] - lrow[v] : 0u;
 #pragma unroll
     for (int j = 0; j < MAXD; ++j) {
-      ed[k][j] = (uint32_t(j) < deg) ? ledg[eb + j] : uint64_t(OGS_EDGE_DOWN);
+      const uint64_t x = (uint32_t(j) < deg) ? ledg[e + j] : uint64_t(OGS_EDGE_DOWN);
+      const uint32_t lo = static_cast<uint32_t>(x);
+      const uint32_t u = edge_dst(lo);
+      const bool ok = !(lo & OGS_EDGE_DOWN) &&
+          !((lo & OGS_EDGE_DST_OVERLOADED) && u != s);
+      const uint32_t w = hop ? 1u : static_cast<uint32_t>(x >> 32);
+      eu[k][j] = ok ? u : 0u;
+      ew[k][j] = ok ? (w < kCap ? w : kCap) : kCap;
+      eb[k][j] = (ok && u == s) ? (1u << (edge_rslot(lo) & 31u)) : 0u;
     }
-    dcur[k] = (v == s) ? 0u : kInf;
+    dcur[k] = (v == s) ? 0u : kCap;
     ncur[k] = 0u;
     if (own) dn[v] = dcur[k];
   }
   wave_sync();
 
-  // ---- SPF with dirty tracking ----------------------------------------------
+  // ---- SPF: pull rounds (optionally only for nodes with a moved neighbour) --
   uint64_t moved[NPL];  // nodes changed since the previous round (uniform)
 #pragma unroll
   for (int k = 0; k < NPL; ++k) moved[k] = (s >> 6) == uint32_t(k) ? 1ull << (s & 63) : 0ull;
@@ -249,48 +276,43 @@ __global__ __launch_bounds__(256) void spf_route_wave_kernel(
 #pragma unroll
     for (int k = 0; k < NPL; ++k) {
       const uint32_t v = lane + k * 64;
-      // a neighbour moved in the last round, or earlier in this one?
-      bool dirty = false;
-#pragma unroll
-      for (int j = 0; j < MAXD; ++j) {
-        const uint32_t lo = static_cast<uint32_t>(ed[k][j]);
-        const uint32_t u = edge_dst(lo);
-        uint64_t set = moved[0] | now[0];
-#pragma unroll
-        for (int kk = 1; kk < NPL; ++kk) {
-          set = (u >> 6) == uint32_t(kk) ? (moved[kk] | now[kk]) : set;
-        }
-        dirty |= !(lo & OGS_EDGE_DOWN) && ((set >> (u & 63)) & 1ull);
-      }
-      bool changed = false;
-      if (dirty && v < N && v != s) {
-        uint64_t x[MAXD];
-        bool ok[MAXD];
+      bool dirty = true;
+      if constexpr (DIRTY) {
+        dirty = false;
 #pragma unroll
         for (int j = 0; j < MAXD; ++j) {
-          const uint32_t lo = static_cast<uint32_t>(ed[k][j]);
-          const uint32_t u = edge_dst(lo);
-          ok[j] = !(lo & OGS_EDGE_DOWN) &&
-              !((lo & OGS_EDGE_DST_OVERLOADED) && u != s);
-          x[j] = dn[ok[j] ? u : 0u];
+          const uint32_t u = eu[k][j];
+          uint64_t set = moved[0] | now[0];
+#pragma unroll
+          for (int kk = 1; kk < NPL; ++kk) {
+            set = (u >> 6) == uint32_t(kk) ? (moved[kk] | now[kk]) : set;
+          }
+          dirty |= ew[k][j] != kCap && ((set >> (u & 63)) & 1ull);
         }
-        uint32_t best = kInf;
+      }
+      bool changed = false;
+#ifdef OGS_STAMPS
+      evals += __popcll(__ballot(dirty && v < N && v != s));
+#endif
+      if (dirty && v < N && v != s) {
+        uint64_t x[MAXD];
+#pragma unroll
+        for (int j = 0; j < MAXD; ++j) x[j] = dn[eu[k][j]];
+        uint32_t best = kCap;
         uint32_t cand[MAXD];
 #pragma unroll
         for (int j = 0; j < MAXD; ++j) {
-          const uint32_t du = static_cast<uint32_t>(x[j]);
-          const uint32_t w = hop ? 1u : static_cast<uint32_t>(ed[k][j] >> 32);
-          cand[j] = (ok[j] && du != kInf) ? du + w : kInf;
+          cand[j] = static_cast<uint32_t>(x[j]) + ew[k][j];
           best = cand[j] < best ? cand[j] : best;
         }
         uint32_t m = 0u;
 #pragma unroll
         for (int j = 0; j < MAXD; ++j) {
-          const uint32_t lo = static_cast<uint32_t>(ed[k][j]);
-          const uint32_t slot = edge_rslot(lo);
-          const uint32_t c = (edge_dst(lo) == s) ? (1u << (slot & 31u))
-                                                 : static_cast<uint32_t>(x[j] >> 32);
-          m |= (cand[j] == best && best != kInf) ? c : 0u;
+          m |= (cand[j] == best) ? (static_cast<uint32_t>(x[j] >> 32) | eb[k][j]) : 0u;
+        }
+        if (best >= kCap) {
+          best = kCap;
+          m = 0u;
         }
         if (best != dcur[k] || m != ncur[k]) {
           dcur[k] = best;
@@ -304,10 +326,23 @@ __global__ __launch_bounds__(256) void spf_route_wave_kernel(
     }
 #pragma unroll
     for (int k = 0; k < NPL; ++k) moved[k] = now[k];
+#ifdef OGS_STAMPS
+    ++rounds;
+#endif
     if (!any) break;
     wave_sync();
   }
+  // back to the ABI's "unreachable" (all ones) for outputs and routes
+#pragma unroll
+  for (int k = 0; k < NPL; ++k) {
+    const uint32_t v = lane + k * 64;
+    if (dcur[k] >= kCap) dcur[k] = kInf;
+    if (v < N && dcur[k] == kInf) dn[v] = uint64_t(kInf);
+  }
   wave_sync();
+#ifdef OGS_STAMPS
+  tSpf = __builtin_amdgcn_s_memtime();
+#endif
 
   // ---- SPF outputs ----------------------------------------------------------
   const uint32_t Sn = g.max_nodes;
@@ -356,16 +391,29 @@ __global__ __launch_bounds__(256) void spf_route_wave_kernel(
     if (out.sel) out.sel[o] = selBits;
     if (out.mask) out.mask[o] = mask;
   }
+#ifdef OGS_STAMPS
+  wave_sync();
+  if (lane == 0 && out.sel) {
+    const uint64_t tEnd = __builtin_amdgcn_s_memtime();
+    uint32_t* d = out.sel + size_t(uidx) * Sp;
+    d[0] = uint32_t(tStaged - tStart);
+    d[1] = uint32_t(tSpf - tStaged);
+    d[2] = uint32_t(tEnd - tSpf);
+    d[3] = rounds;
+    d[4] = uint32_t(tDesc - tStart);
+    d[5] = evals;
+  }
+#endif
 }
 
-template <int NPL, int MAXD>
+template <int NPL, int MAXD, bool DIRTY>
 hipError_t launch_wave(const ogs_graph& g, const ogs_prefix_table& pt,
                        int hasPrefixes, const ogs_unit* units, int nUnits,
                        uint32_t flags, const ogs_spf_out& out, uint32_t lds,
                        uint32_t maxA, hipStream_t stream) {
   const int grid = (nUnits + 3) / 4;
   const size_t bytes = size_t(lds) * 4;
-  auto k = spf_route_wave_kernel<NPL, MAXD>;
+  auto k = spf_route_wave_kernel<NPL, MAXD, DIRTY>;
   if (bytes > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute(
         reinterpret_cast<const void*>(k),
@@ -379,8 +427,8 @@ hipError_t launch_wave(const ogs_graph& g, const ogs_prefix_table& pt,
 
 bool try_wave(const ogs_graph& g, const ogs_prefix_table& pt, int hasPrefixes,
               const ogs_unit* units, int nUnits, uint32_t flags,
-              const ogs_spf_out& out, uint32_t maxA, hipStream_t stream,
-              hipError_t* err) {
+              const ogs_spf_out& out, uint32_t maxA, bool dirty,
+              hipStream_t stream, hipError_t* err) {
   if (flags & OGS_F_WIDE_METRIC) return false;
   if (g.max_nodes > 256 || g.max_degree > 8 || g.max_degree < 0) return false;
   const uint32_t P = hasPrefixes ? pt.max_prefixes : 0;
@@ -390,8 +438,12 @@ bool try_wave(const ogs_graph& g, const ogs_prefix_table& pt, int hasPrefixes,
   const int N = g.max_nodes;
   const bool d4 = g.max_degree <= 4;
 #define OGS_WAVE(NPL_, MAXD_)                                                 \
-  *err = launch_wave<NPL_, MAXD_>(g, pt, hasPrefixes, units, nUnits, flags,   \
-                                  out, lds, A, stream);                       \
+  *err = dirty ? launch_wave<NPL_, MAXD_, true>(g, pt, hasPrefixes, units,    \
+                                               nUnits, flags, out, lds, A,    \
+                                               stream)                        \
+               : launch_wave<NPL_, MAXD_, false>(g, pt, hasPrefixes, units,   \
+                                                nUnits, flags, out, lds, A,   \
+                                                stream);                      \
   return true;
   if (N <= 64) { if (d4) { OGS_WAVE(1, 4) } OGS_WAVE(1, 8) }
   if (N <= 128) { if (d4) { OGS_WAVE(2, 4) } OGS_WAVE(2, 8) }

@@ -35,15 +35,15 @@ def main():
     o = [torch.zeros(n, dtype=torch.int32, device=dev) for n in
          (U * Sn, U * W * Sn, U * Sp, U * Sp, U * W * Sp, U * Sp)]
     so = capi.SpfOut(*[x.data_ptr() for x in o])
-    for uw in [int(x) for x in os.environ.get("VARIANTS", "64,128").split(",")]:
+    for uw in [int(x) for x in os.environ.get("VARIANTS", "1,64").split(",")]:
         capi.check(lib, lib.ogs_set_option(b"unit_width", uw), "opt")
         for _ in range(3):
             capi.check(lib, lib.ogs_spf_routes(ctypes.byref(g), ctypes.byref(pt),
                                                ctypes.c_void_p(t["units"].data_ptr()), U,
                                                h["flags"], W, ctypes.byref(so), None), "run")
         torch.cuda.synchronize()
-        st = o[5].cpu().numpy().reshape(U, Sp)[:, :4].astype(np.float64)
-        names = ["stage", "spf", "routes", "rounds"]
+        st = o[5].cpu().numpy().reshape(U, Sp)[:, :6].astype(np.float64)
+        names = ["stage", "spf", "routes", "rounds", "desc", "evals"]
         print(f"unit_width={uw}: " + "  ".join(
             f"{n}: med={np.median(st[:, i]):.0f} p90={np.percentile(st[:, i], 90):.0f} "
             f"max={st[:, i].max():.0f}" for i, n in enumerate(names)))
