@@ -31,8 +31,16 @@ $(MOD): $(HOST) $(HOST_H) openr_amd/csrc/py/bindings.cpp $(LIB)
 oracle:
 	$(MAKE) -C oracle
 
+# diagnostic build: per-unit phase clocks written into ogs_spf_out.sel
+# (tools/stamps.py); never loaded by the product
+STAMPS := openr_amd/lib/libopenr_gpu_stamps.so
+stamps: $(STAMPS)
+$(STAMPS): $(KERNELS) include/openr_gpu.h
+	@mkdir -p openr_amd/lib
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -shared -DOGS_STAMPS -Iinclude $(KERNELS) -o $@
+
 clean:
-	rm -f $(LIB) $(MOD)
+	rm -f $(LIB) $(MOD) $(STAMPS)
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle clean
+.PHONY: all oracle clean stamps

@@ -106,6 +106,7 @@ def main():
     adv_metrics = up("adv_metrics", "int32")
     adv_min_nh = up("adv_min_nh", "int64")
     pfx_flags = up("pfx_flags", "uint8")
+    slot_node = up("slot_node", "uint16")
     units = up("units", "int32")
     U = len(h["units"]) // 2
     Sn, Sp, W = h["max_nodes"], h["max_prefixes"], h["nh_words"]
@@ -119,7 +120,8 @@ def main():
     o_sel = torch.empty(U * Sp, dtype=torch.int32, device=dev)
 
     g = capi.Graph(h["num_topos"], Sn, h["max_edges"], h["max_degree"], node_base.data_ptr(),
-                   row_ptr.data_ptr(), edges.data_ptr(), node_flags.data_ptr(), topo_desc.data_ptr())
+                   row_ptr.data_ptr(), edges.data_ptr(), node_flags.data_ptr(), topo_desc.data_ptr(),
+                   slot_node.data_ptr(), h["slot_stride"])
     pt = capi.PrefixTable(Sp, h["max_advertisements"], pfx_base.data_ptr(), adv_off.data_ptr(),
                           adv_node.data_ptr(), adv_metrics.data_ptr(),
                           adv_min_nh.data_ptr(), pfx_flags.data_ptr())

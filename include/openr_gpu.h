@@ -70,6 +70,9 @@ extern "C" {
 #define OGS_NODE_METRICINC 0x04u
 #define OGS_NODE_NONE 0xFFFFFFFFu /* advertiser with no adjacency database */
 
+#define OGS_PFX_V4 0x01u
+#define OGS_PFX_HAS_MIN_NH 0x02u
+
 /* ---- route record flags (ogs_route_out.meta) --------------------------- */
 #define OGS_ROUTE_VALID 0x01u       /* a unicast route exists              */
 #define OGS_ROUTE_DRAINED 0x02u     /* isBestNodeDrained -> drain_metric=1 */
@@ -106,6 +109,14 @@ typedef struct ogs_graph {
    * without a prefix table). Redundant with the arrays above; lets a unit
    * fetch all its offsets with one load instead of a dependent chain. */
   const uint32_t* topo_desc;
+  /* Optional [T*slot_stride] relaxation order for the wave-per-unit path:
+   * position i of topology t holds a node id (0xFFFF = empty); position i
+   * is processed in slot i/64 by lane i%64. Any permutation is exact; the
+   * adapter 2-colours the topology so consecutive slots alternate colour
+   * classes and one round propagates two hops on bipartite graphs.
+   * slot_stride is 64, 128 or 256 (0 with slot_node NULL). */
+  const uint16_t* slot_node;
+  int32_t slot_stride;
 } ogs_graph;
 
 /* Prefix table: per topology a contiguous range of prefixes, each with a
@@ -119,7 +130,8 @@ typedef struct ogs_prefix_table {
   const int32_t* adv_metrics; /* [A*4] drain_metric, path_preference,
                                  source_preference, distance            */
   const int64_t* adv_min_nh;  /* [A] minNexthop, INT64_MIN when unset    */
-  const uint8_t* pfx_flags;   /* [P_total] bit0: prefix is IPv4          */
+  const uint8_t* pfx_flags;   /* [P_total] bit0: prefix is IPv4; bit1: an
+                                 advertisement sets minNexthop           */
 } ogs_prefix_table;
 
 /* One work unit = (topology, source node). */

@@ -26,7 +26,8 @@ class Graph(ctypes.Structure):
                 ("max_edges", ctypes.c_int32), ("max_degree", ctypes.c_int32),
                 ("node_base", ctypes.c_void_p),
                 ("row_ptr", ctypes.c_void_p), ("edges", ctypes.c_void_p),
-                ("node_flags", ctypes.c_void_p), ("topo_desc", ctypes.c_void_p)]
+                ("node_flags", ctypes.c_void_p), ("topo_desc", ctypes.c_void_p),
+                ("slot_node", ctypes.c_void_p), ("slot_stride", ctypes.c_int32)]
 
 
 class PrefixTable(ctypes.Structure):

@@ -216,7 +216,8 @@ struct FlatTopology {
   bool hasZeroMetric{false};
   bool hasWideMetric{false};  // metric >= 2^32 (negative i32)
   uint64_t version{0};
-  DeviceBuffer dRow, dEdges, dFlags, dNodeBase;
+  int slotStride{0};  // ogs_graph.slot_stride of dSlot (0: none)
+  DeviceBuffer dRow, dEdges, dFlags, dNodeBase, dSlot;
 };
 
 // ------------------------------------------------------------- LinkState --
@@ -454,11 +455,14 @@ struct HostBatch {
   std::vector<int32_t> advMetrics;
   std::vector<int64_t> advMinNh;
   std::vector<uint8_t> pfxFlags;
+  std::vector<uint8_t> color;  // [N_total] BFS 2-colouring (slot_order.h)
   int maxNodes{0}, maxEdges{0}, maxPrefixes{0}, maxDegree{0}, maxAdvs{0};
   uint64_t maxMetric{0};
   bool hasZeroMetric{false};
   void append(const FlatTopology& t, const PrefixState& ps,
               const std::string& area);
+  // ogs_graph.slot_node image ([T*stride]); returns the stride, 0 if none
+  int slotOrder(std::vector<uint16_t>& out) const;
 };
 
 // ---------------------------------------------------- materialisation --

@@ -4,6 +4,7 @@
 #include <unordered_map>
 
 #include "decision.h"
+#include "slot_order.h"
 
 namespace openr_amd {
 
@@ -296,6 +297,14 @@ const FlatTopology& LinkState::flatOnDevice() const {
   m.dRow.upload(m.rowPtr.data(), m.rowPtr.size());
   m.dEdges.upload(m.edges.data(), m.edges.size());
   m.dFlags.upload(m.nodeFlags.data(), m.nodeFlags.size());
+  m.slotStride = slotStrideFor(int(m.names.size()));
+  if (m.slotStride) {
+    std::vector<uint16_t> slots(m.slotStride);
+    placeSlots(colorNodes(m.rowPtr.data(), m.edges.data(),
+                          uint32_t(m.names.size())),
+               m.slotStride, slots.data());
+    m.dSlot.upload(slots.data(), slots.size());
+  }
   deviceStale_ = false;
   return f;
 }
@@ -359,6 +368,8 @@ const LinkState::SpfResult& LinkState::getSpfResult(const std::string& node,
   g.row_ptr = f.dRow.as<uint32_t>();
   g.edges = f.dEdges.as<uint64_t>();
   g.node_flags = f.dFlags.as<uint8_t>();
+  g.slot_node = f.slotStride ? f.dSlot.as<uint16_t>() : nullptr;
+  g.slot_stride = f.slotStride;
   ogs_spf_out out{};
   out.dist = sc.dist.get();
   out.nh = sc.nh.as<uint32_t>();

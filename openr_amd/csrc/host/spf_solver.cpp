@@ -6,6 +6,7 @@
 #include <algorithm>
 
 #include "decision.h"
+#include "slot_order.h"
 
 namespace openr_amd {
 
@@ -76,6 +77,8 @@ void HostBatch::append(const FlatTopology& t, const PrefixState& ps,
   edges.insert(edges.end(), t.edges.begin(), t.edges.end());
   nodeFlags.insert(nodeFlags.end(), t.nodeFlags.begin(), t.nodeFlags.end());
   nodeBase.push_back(nodeBase.back() + N);
+  const auto c = colorNodes(t.rowPtr.data(), t.edges.data(), N);
+  color.insert(color.end(), c.begin(), c.end());
   maxNodes = std::max<int>(maxNodes, int(N));
   maxEdges = std::max<int>(maxEdges, int(t.edges.size()));
   maxDegree = std::max(maxDegree, t.maxDegree);
@@ -96,7 +99,10 @@ void HostBatch::append(const FlatTopology& t, const PrefixState& ps,
       advMinNh.push_back(e->minNexthop ? *e->minNexthop : INT64_MIN);
     }
     advOff.push_back(uint32_t(advNode.size()));
-    pfxFlags.push_back(isV4Prefix(prefix) ? 1 : 0);
+    bool anyMinNh = false;
+    for (const auto& [na, e] : entries) anyMinNh |= e->minNexthop.has_value();
+    pfxFlags.push_back((isV4Prefix(prefix) ? OGS_PFX_V4 : 0u) |
+                       (anyMinNh ? OGS_PFX_HAS_MIN_NH : 0u));
     ++np;
   }
   pfxBase.push_back(pfxBase.back() + np);
@@ -105,6 +111,20 @@ void HostBatch::append(const FlatTopology& t, const PrefixState& ps,
   topoDesc.insert(topoDesc.end(),
                   {n0, N, e0, uint32_t(t.edges.size()), pb0, np, ab0,
                    uint32_t(advNode.size()) - ab0});
+}
+
+int HostBatch::slotOrder(std::vector<uint16_t>& out) const {
+  const int stride = slotStrideFor(maxNodes);
+  out.clear();
+  if (!stride) return 0;
+  const size_t T = nodeBase.size() - 1;
+  out.resize(T * stride);
+  for (size_t t = 0; t < T; ++t) {
+    const std::vector<uint8_t> c(color.begin() + nodeBase[t],
+                                 color.begin() + nodeBase[t + 1]);
+    placeSlots(c, stride, &out[t * stride]);
+  }
+  return stride;
 }
 
 // ------------------------------------------------------------- SpfSolver --
@@ -338,6 +358,8 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(
   g.row_ptr = f.dRow.as<uint32_t>();
   g.edges = f.dEdges.as<uint64_t>();
   g.node_flags = f.dFlags.as<uint8_t>();
+  g.slot_node = f.slotStride ? f.dSlot.as<uint16_t>() : nullptr;
+  g.slot_stride = f.slotStride;
   ogs_prefix_table pt{};
   pt.max_prefixes = int32_t(P);
   pt.max_advertisements = int32_t(I.table.advEntry.size());

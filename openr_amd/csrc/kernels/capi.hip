@@ -132,6 +132,13 @@ int ogs_spf_routes(const ogs_graph* graph, const ogs_prefix_table* prefixes,
       uint32_t(graph->max_nodes) > OGS_MAX_NODES_PER_TOPO) {
     return fail(OGS_E_UNSUPPORTED, "max_nodes outside (0, 2^21]");
   }
+  if (graph->slot_node && graph->slot_stride != 64 &&
+      graph->slot_stride != 128 && graph->slot_stride != 256) {
+    return fail(OGS_E_INVALID, "slot_stride must be 64, 128 or 256");
+  }
+  if (graph->slot_node && graph->slot_stride < graph->max_nodes) {
+    return fail(OGS_E_INVALID, "slot_stride < max_nodes");
+  }
   if (prefixes && (!prefixes->pfx_base || !prefixes->adv_off ||
                    !prefixes->adv_node || !prefixes->adv_metrics ||
                    !prefixes->adv_min_nh || !prefixes->pfx_flags)) {

@@ -56,7 +56,9 @@ __device__ void route_one(const ogs_prefix_table& pt, uint32_t gp, uint32_t s,
   for (int w = 0; w < W; ++w) mask[w] = 0;
 
   // v4 gate (SpfSolver.cpp:169-176)
-  const bool isV4 = pt.pfx_flags[gp] & 1u;
+  const uint8_t pflags = pt.pfx_flags[gp];
+  const bool isV4 = pflags & OGS_PFX_V4;
+  const bool hasMinNh = pflags & OGS_PFX_HAS_MIN_NH;
   if (isV4 && !cfg.enableV4 && !cfg.v4OverV6) {
     meta = OGS_REASON_V4_DISABLED << OGS_ROUTE_REASON_SHIFT;
     return;
@@ -146,14 +148,14 @@ __device__ void route_one(const ogs_prefix_table& pt, uint32_t gp, uint32_t s,
     return;
   }
   // next-hop union over the min-cost destinations + min-nexthop threshold
-  bool hasMinNh = false;
+  bool anyMinNh = false;
   int64_t minNh = INT64_MIN;
   for (uint32_t a = a0; a < a1; ++a) {
     const uint32_t n = pt.adv_node[a];
     if (!selected(a, n)) continue;
-    const int64_t t = pt.adv_min_nh[a];
-    if (t != INT64_MIN && (!hasMinNh || t > minNh)) {
-      hasMinNh = true;
+    const int64_t t = hasMinNh ? pt.adv_min_nh[a] : INT64_MIN;
+    if (t != INT64_MIN && (!anyMinNh || t > minNh)) {
+      anyMinNh = true;
       minNh = t;
     }
     if (sv.dist(n) != shortest) continue;
@@ -168,7 +170,7 @@ __device__ void route_one(const ogs_prefix_table& pt, uint32_t gp, uint32_t s,
     meta |= OGS_REASON_NO_NEXTHOP << OGS_ROUTE_REASON_SHIFT;
     return;
   }
-  if (hasMinNh && static_cast<uint64_t>(minNh) > cnt) {  // SpfSolver.cpp:612
+  if (anyMinNh && static_cast<uint64_t>(minNh) > cnt) {  // SpfSolver.cpp:612
     meta |= OGS_REASON_MIN_NEXTHOP << OGS_ROUTE_REASON_SHIFT;
     return;
   }

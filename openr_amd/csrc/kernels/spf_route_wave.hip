@@ -28,11 +28,13 @@
 
 namespace ogs {
 
+// LDS image of one unit. Advertisement metrics are staged only when best
+// route selection reads them; minNexthop is read from HBM on demand (only
+// for prefixes flagged OGS_PFX_HAS_MIN_NH).
 struct WaveLayout {
-  uint32_t dn, row, edges, flags, advOff, advNode, advMetrics, advMinNh,
-      pfxFlags, total;
+  uint32_t dn, row, edges, flags, advOff, advNode, advMetrics, pfxFlags, total;
   __host__ __device__ static WaveLayout make(uint32_t N, uint32_t E, uint32_t P,
-                                             uint32_t A) {
+                                             uint32_t A, bool brs) {
     WaveLayout L;
     uint32_t o = 0;
     L.dn = o;
@@ -48,9 +50,7 @@ struct WaveLayout {
     L.advNode = o;
     o += align16(uint64_t(A) * 4);
     L.advMetrics = o;
-    o += align16(uint64_t(A) * 16);
-    L.advMinNh = o;
-    o += align16(uint64_t(A) * 8);
+    o += brs ? align16(uint64_t(A) * 16) : 0u;
     L.pfxFlags = o;
     o += align16(P);
     L.total = o;
@@ -139,6 +139,20 @@ __global__ __launch_bounds__(256) void spf_route_wave_kernel(
   // ---- unit offsets -------------------------------------------------------
   const ogs_unit unit = units[uidx];
   const uint32_t s = unit.src;
+  // relaxation order (slot_order.h): position k*64+lane -> node id
+  const bool perm = !DIRTY && g.slot_node && g.slot_stride == NPL * 64;
+  uint32_t vk[NPL];
+  if (perm) {
+    const uint16_t* so = g.slot_node + size_t(unit.topo) * (NPL * 64);
+#pragma unroll
+    for (int k = 0; k < NPL; ++k) {
+      const uint32_t x = so[k * 64 + lane];
+      vk[k] = x == 0xFFFFu ? 0xFFFFFFFFu : x;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < NPL; ++k) vk[k] = uint32_t(k * 64 + lane);
+  }
   uint32_t nb, N, e0, E, p0 = 0, P = 0, a0 = 0, A = 0;
   if (g.topo_desc) {
     const uint4* d = reinterpret_cast<const uint4*>(g.topo_desc) + 2 * unit.topo;
@@ -169,9 +183,10 @@ __global__ __launch_bounds__(256) void spf_route_wave_kernel(
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   tDesc = __builtin_amdgcn_s_memtime();
 #endif
+  const bool brs = flags & OGS_F_BEST_ROUTE_SELECTION;
   const WaveLayout L = WaveLayout::make(g.max_nodes, g.max_edges,
                                         hasPrefixes ? pt.max_prefixes : 0,
-                                        hasPrefixes ? maxA : 0);
+                                        hasPrefixes ? maxA : 0, brs);
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* base = smem + uib * ldsPerUnit;
   uint64_t* dn = reinterpret_cast<uint64_t*>(base + L.dn);
@@ -181,7 +196,6 @@ __global__ __launch_bounds__(256) void spf_route_wave_kernel(
   uint32_t* lAdvOff = reinterpret_cast<uint32_t*>(base + L.advOff);
   uint32_t* lAdvNode = reinterpret_cast<uint32_t*>(base + L.advNode);
   int4* lAdvMetrics = reinterpret_cast<int4*>(base + L.advMetrics);
-  int64_t* lAdvMinNh = reinterpret_cast<int64_t*>(base + L.advMinNh);
   uint8_t* lPfxFlags = reinterpret_cast<uint8_t*>(base + L.pfxFlags);
 
   // ---- staging: one batch of loads, then LDS writes -----------------------
@@ -195,14 +209,12 @@ __global__ __launch_bounds__(256) void spf_route_wave_kernel(
     constexpr int KP = NPL + 1;  // prefixes per lane per pass (P <= 64*KP)
     WStage<KP, uint32_t> sOff, sNode;
     WStage<KP, int4> sMet;
-    WStage<KP, int64_t> sMin;
     WStage<KP, uint8_t> sPf;
     const bool pfxFits = (P + 1 <= 64u * KP) && (A <= 64u * KP);
     if (hasPrefixes && pfxFits) {
       sOff.load(pt.adv_off + p0, P + 1, lane);
       sNode.load(pt.adv_node + a0, A, lane);
-      sMet.load(reinterpret_cast<const int4*>(pt.adv_metrics) + a0, A, lane);
-      sMin.load(pt.adv_min_nh + a0, A, lane);
+      if (brs) sMet.load(reinterpret_cast<const int4*>(pt.adv_metrics) + a0, A, lane);
       sPf.load(pt.pfx_flags + p0, P, lane);
     }
     sRow.store(lrow, N + 1, lane);
@@ -211,16 +223,14 @@ __global__ __launch_bounds__(256) void spf_route_wave_kernel(
     if (hasPrefixes && pfxFits) {
       sOff.store(lAdvOff, P + 1, lane);
       sNode.store(lAdvNode, A, lane);
-      sMet.store(lAdvMetrics, A, lane);
-      sMin.store(lAdvMinNh, A, lane);
+      if (brs) sMet.store(lAdvMetrics, A, lane);
       sPf.store(lPfxFlags, P, lane);
     } else if (hasPrefixes) {  // rare: long prefix tables, plain loop
       for (uint32_t i = lane; i <= P; i += 64) lAdvOff[i] = pt.adv_off[p0 + i];
       for (uint32_t i = lane; i < P; i += 64) lPfxFlags[i] = pt.pfx_flags[p0 + i];
       for (uint32_t i = lane; i < A; i += 64) {
         lAdvNode[i] = pt.adv_node[a0 + i];
-        lAdvMetrics[i] = reinterpret_cast<const int4*>(pt.adv_metrics)[a0 + i];
-        lAdvMinNh[i] = pt.adv_min_nh[a0 + i];
+        if (brs) lAdvMetrics[i] = reinterpret_cast<const int4*>(pt.adv_metrics)[a0 + i];
       }
     }
   }
@@ -242,7 +252,7 @@ __global__ __launch_bounds__(256) void spf_route_wave_kernel(
   uint32_t dcur[NPL], ncur[NPL];
 #pragma unroll
   for (int k = 0; k < NPL; ++k) {
-    const uint32_t v = lane + k * 64;
+    const uint32_t v = vk[k];
     const bool own = v < N;
     const uint32_t e = own ? lrow[v] - e0 : 0u;
     const uint32_t deg = own ? lrow[v + 1] - lrow[v] : 0u;
@@ -275,7 +285,7 @@ __global__ __launch_bounds__(256) void spf_route_wave_kernel(
     bool any = false;
 #pragma unroll
     for (int k = 0; k < NPL; ++k) {
-      const uint32_t v = lane + k * 64;
+      const uint32_t v = vk[k];
       bool dirty = true;
       if constexpr (DIRTY) {
         dirty = false;
@@ -335,7 +345,7 @@ __global__ __launch_bounds__(256) void spf_route_wave_kernel(
   // back to the ABI's "unreachable" (all ones) for outputs and routes
 #pragma unroll
   for (int k = 0; k < NPL; ++k) {
-    const uint32_t v = lane + k * 64;
+    const uint32_t v = vk[k];
     if (dcur[k] >= kCap) dcur[k] = kInf;
     if (v < N && dcur[k] == kInf) dn[v] = uint64_t(kInf);
   }
@@ -348,7 +358,7 @@ __global__ __launch_bounds__(256) void spf_route_wave_kernel(
   const uint32_t Sn = g.max_nodes;
 #pragma unroll
   for (int k = 0; k < NPL; ++k) {
-    const uint32_t v = lane + k * 64;
+    const uint32_t v = vk[k];
     if (v >= N) continue;
     if (out.dist) static_cast<uint32_t*>(out.dist)[size_t(uidx) * Sn + v] = dcur[k];
     if (out.nh) out.nh[size_t(uidx) * Sn + v] = ncur[k];
@@ -364,23 +374,24 @@ __global__ __launch_bounds__(256) void spf_route_wave_kernel(
   lp.adv_off = lAdvOff;
   lp.adv_node = lAdvNode;
   lp.adv_metrics = reinterpret_cast<const int32_t*>(lAdvMetrics);
-  lp.adv_min_nh = lAdvMinNh;
+  lp.adv_min_nh = pt.adv_min_nh;  // HBM, absolute advertisement index
   lp.pfx_flags = lPfxFlags;
   const uint32_t Sp = pt.max_prefixes;
   for (uint32_t p = lane; p < P; p += 64) {
     uint32_t meta, metric, mask, selBits;
     const uint32_t b0 = lAdvOff[p] - a0, b1 = lAdvOff[p + 1] - a0;
-    const bool gated = (lPfxFlags[p] & 1u) && !cfg.enableV4 && !cfg.v4OverV6;
+    const uint8_t pf = lPfxFlags[p];
+    const bool gated = (pf & OGS_PFX_V4) && !cfg.enableV4 && !cfg.v4OverV6;
     if (b1 - b0 == 1 && !gated) {
-      route_single(lAdvNode[b0], lAdvMinNh[b0], s, lflags, dn, meta, metric,
-                   mask);
+      const int64_t minNh = (pf & OGS_PFX_HAS_MIN_NH) ? pt.adv_min_nh[a0 + b0]
+                                                      : INT64_MIN;
+      route_single(lAdvNode[b0], minNh, s, lflags, dn, meta, metric, mask);
       selBits = (meta & OGS_ROUTE_SELECTED) ? 1u : 0u;
     } else {
       uint32_t mk[1];
       // route_one indexes the prefix table by prefix; rebase the segment
       lp.adv_node = lAdvNode - a0;
       lp.adv_metrics = reinterpret_cast<const int32_t*>(lAdvMetrics - a0);
-      lp.adv_min_nh = lAdvMinNh - a0;
       route_one<uint32_t, 1>(lp, p, s, lflags, PackedView{dn}, cfg, meta,
                              metric, mk, selBits);
       mask = mk[0];
@@ -433,7 +444,8 @@ bool try_wave(const ogs_graph& g, const ogs_prefix_table& pt, int hasPrefixes,
   if (g.max_nodes > 256 || g.max_degree > 8 || g.max_degree < 0) return false;
   const uint32_t P = hasPrefixes ? pt.max_prefixes : 0;
   const uint32_t A = hasPrefixes ? maxA : 0;
-  const uint32_t lds = WaveLayout::make(g.max_nodes, g.max_edges, P, A).total;
+  const uint32_t lds = WaveLayout::make(g.max_nodes, g.max_edges, P, A,
+                                        flags & OGS_F_BEST_ROUTE_SELECTION).total;
   if (uint64_t(lds) * 4 > 160 * 1024) return false;
   const int N = g.max_nodes;
   const bool d4 = g.max_degree <= 4;

@@ -352,6 +352,9 @@ class BatchRunner {
     dAdvMetrics_.upload(hb_.advMetrics.data(), hb_.advMetrics.size());
     dAdvMinNh_.upload(hb_.advMinNh.data(), hb_.advMinNh.size());
     dPfxFlags_.upload(hb_.pfxFlags.data(), hb_.pfxFlags.size());
+    std::vector<uint16_t> slots;
+    slotStride_ = slotOrder_ ? hb_.slotOrder(slots) : 0;
+    dSlot_.upload(slots.data(), slots.size());
     dUnits_.upload(units_.data(), units_.size());
     const size_t U = units_.size(), db = wide_ ? 8 : 4;
     const size_t Sn = hb_.maxNodes, Sp = std::max(hb_.maxPrefixes, 1);
@@ -428,6 +431,7 @@ class BatchRunner {
         (wide_ ? OGS_F_WIDE_METRIC : 0u);
   }
   size_t numUnits() const { return units_.size(); }
+  void setSlotOrder(bool on) { slotOrder_ = on; }
   const HostBatch& host() const { return hb_; }
   const std::vector<ogs_unit>& units() const { return units_; }
   int nhWords() const { return W_; }
@@ -448,6 +452,8 @@ class BatchRunner {
     g.row_ptr = dRow_.as<uint32_t>();
     g.edges = dEdges_.as<uint64_t>();
     g.node_flags = dFlags_.as<uint8_t>();
+    g.slot_node = slotStride_ ? dSlot_.as<uint16_t>() : nullptr;
+    g.slot_stride = slotStride_;
     return g;
   }
   ogs_prefix_table table() const {
@@ -469,6 +475,9 @@ class BatchRunner {
     PrefixHostTable table;
   };
   bool enableV4_, sr_, brs_;
+  bool slotOrder_{true};
+  int slotStride_{0};
+  DeviceBuffer dSlot_;
   std::vector<std::unique_ptr<Topo>> topos_;
   HostBatch hb_;
   std::vector<ogs_unit> units_;
@@ -742,6 +751,8 @@ PYBIND11_MODULE(_decision, m) {
              return c;
            })
       .def("flags", &BatchRunner::flags)
+      .def("set_slot_order", &BatchRunner::setSlotOrder,
+           "use the 2-colour relaxation order (default on; takes effect at upload)")
       .def("nh_words", &BatchRunner::nhWords)
       .def("wide", &BatchRunner::wide)
       .def("host_arrays", [](const BatchRunner& b) {
@@ -759,6 +770,9 @@ PYBIND11_MODULE(_decision, m) {
         d["adv_metrics"] = npcopy(h.advMetrics);
         d["adv_min_nh"] = npcopy(h.advMinNh);
         d["pfx_flags"] = npcopy(h.pfxFlags);
+        std::vector<uint16_t> slots;
+        d["slot_stride"] = h.slotOrder(slots);
+        d["slot_node"] = npcopy(slots);
         std::vector<uint32_t> u;
         for (const auto& x : b.units()) {
           u.push_back(x.topo);

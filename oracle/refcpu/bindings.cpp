@@ -540,7 +540,7 @@ PYBIND11_MODULE(_refcpu, m) {
   // Grid batch (config C2): topology i uses metric seed base+i and prefix
   // seed pbase+i. Returns canonical DBs for topologies [lo, hi).
   m.def("grid_batch_route_dbs",
-        [](py::dict opts, int lo, int hi, const std::string& source) {
+        [](py::dict opts, int lo, int hi, const std::string& source, bool brs) {
           std::vector<py::bytes> out;
           auto base = gridOpts(opts);
           for (int t = lo; t < hi; ++t) {
@@ -552,12 +552,14 @@ PYBIND11_MODULE(_refcpu, m) {
             Workspace w;
             auto& ls = w.als.emplace(g.area, LinkState(g.area, "test_node")).first->second;
             loadLsdb(g, ls, w.ps);
-            SpfSolver solver("test_node", true, false, false);
+            SpfSolver solver("test_node", true, false, brs);
             auto db = solver.buildRouteDb(source, w.als, w.ps);
             out.push_back(py::bytes(db ? canonical(*db) : std::string("NONE")));
           }
           return out;
-        });
+        },
+        py::arg("opts"), py::arg("lo"), py::arg("hi"), py::arg("source"),
+        py::arg("brs") = false);
 
   // CPU baseline for the grid batch: T threads, each owns private replicas
   // (LinkState memo maps are not thread-safe). Ingestion is

@@ -176,3 +176,31 @@ def test_ksp2_on_multigraphs(product, oracle):
             assert a == b, (s, d, k)
             links = [l for p in a for l in p]
             assert len(links) == len(set(links))
+
+
+@pytest.mark.parametrize("brs", [False, True])
+def test_c2_kernel_variants_identical(product, oracle, brs):
+    """Every SPF+RouteDb kernel variant (generic workgroup, small, wave; with
+    and without the 2-colour slot order) gives the oracle's RouteDbs."""
+    import openr_amd.capi as capi
+    lib = capi.load()
+    T = 256
+    opts = dict(n=10, metricSeed=0xC2200000, prefixSeed=0xC1,
+                adjOverloadPermille=10, overloadSeed=0xC22F)
+    cpu = None
+    try:
+        for uw in (0, 1, 2, 64):
+            for order in (True, False):
+                capi.check(lib, lib.ogs_set_option(b"unit_width", uw), "unit_width")
+                br = product.BatchRunner(True, False, brs)
+                br.set_slot_order(order)
+                br.add_grid_batch(opts, 0, T, "1")
+                br.upload()
+                br.run()
+                br.download()
+                gpu = [br.canonical(u) for u in range(T)]
+                if cpu is None:
+                    cpu = oracle.grid_batch_route_dbs(opts, 0, T, "1", brs)
+                _cmp(gpu, cpu, f"c2 uw={uw} order={order}")
+    finally:
+        lib.ogs_set_option(b"unit_width", -1)
