@@ -107,6 +107,7 @@ def main():
     adv_min_nh = up("adv_min_nh", "int64")
     pfx_flags = up("pfx_flags", "uint8")
     slot_node = up("slot_node", "uint16")
+    slot_edges = up("slot_edges", "uint32")
     units = up("units", "int32")
     U = len(h["units"]) // 2
     Sn, Sp, W = h["max_nodes"], h["max_prefixes"], h["nh_words"]
@@ -121,7 +122,8 @@ def main():
 
     g = capi.Graph(h["num_topos"], Sn, h["max_edges"], h["max_degree"], node_base.data_ptr(),
                    row_ptr.data_ptr(), edges.data_ptr(), node_flags.data_ptr(), topo_desc.data_ptr(),
-                   slot_node.data_ptr(), h["slot_stride"])
+                   slot_node.data_ptr(), h["slot_stride"],
+                   slot_edges.data_ptr() if h["slot_degree"] else None, h["slot_degree"])
     pt = capi.PrefixTable(Sp, h["max_advertisements"], pfx_base.data_ptr(), adv_off.data_ptr(),
                           adv_node.data_ptr(), adv_metrics.data_ptr(),
                           adv_min_nh.data_ptr(), pfx_flags.data_ptr())

@@ -117,7 +117,22 @@ typedef struct ogs_graph {
    * slot_stride is 64, 128 or 256 (0 with slot_node NULL). */
   const uint16_t* slot_node;
   int32_t slot_stride;
+  /* Optional [T][slot_degree][slot_stride] per-position edge image for the
+   * wave path (requires slot_node; all metrics <= 65535, degree <= 8):
+   * entry j of position i is the i-th ordered node's j-th CSR edge,
+   *   bits 0-8   neighbour POSITION, bit 9 OGS_SLOT_EDGE_DOWN (also for
+   *              missing edges), bit 10 neighbour overloaded, bits 11-13
+   *              rslot (reverse edge index in the neighbour's row),
+   *   bits 16-31 metric.
+   * Lets each lane load its edges coalesced straight into registers.
+   * slot_degree is 4 or 8 (0 with slot_edges NULL). */
+  const uint32_t* slot_edges;
+  int32_t slot_degree;
 } ogs_graph;
+
+#define OGS_SLOT_EDGE_DOWN (1u << 9)
+#define OGS_SLOT_EDGE_DST_OVERLOADED (1u << 10)
+#define OGS_SLOT_EDGE_RSLOT_SHIFT 11
 
 /* Prefix table: per topology a contiguous range of prefixes, each with a
  * contiguous segment of advertisements (one (node, area) entry each). */
@@ -196,8 +211,10 @@ int ogs_stream_sync(void* stream);
 /* Tuning knobs (process-wide; for A/B measurement):
  *   "unit_width": small-topology kernel choice: -1 automatic (default),
  *                 0 generic kernel only, 1 packed wave-per-unit kernel,
- *                 2 the same with dirty-node tracking,
- *                 64 / 128 / 256 split-state kernel at that unit width. */
+ *                 2 split-state kernel at its automatic unit width,
+ *                 64 / 128 / 256 split-state kernel at that unit width.
+ *   "wave_wg_lds": minimum LDS bytes per wave-kernel workgroup (occupancy
+ *                 probe; 0 default). */
 int ogs_set_option(const char* name, int64_t value);
 
 /* Smallest supported next-hop bitset width (words) for a source degree. */

@@ -27,7 +27,8 @@ class Graph(ctypes.Structure):
                 ("node_base", ctypes.c_void_p),
                 ("row_ptr", ctypes.c_void_p), ("edges", ctypes.c_void_p),
                 ("node_flags", ctypes.c_void_p), ("topo_desc", ctypes.c_void_p),
-                ("slot_node", ctypes.c_void_p), ("slot_stride", ctypes.c_int32)]
+                ("slot_node", ctypes.c_void_p), ("slot_stride", ctypes.c_int32),
+                ("slot_edges", ctypes.c_void_p), ("slot_degree", ctypes.c_int32)]
 
 
 class PrefixTable(ctypes.Structure):
@@ -44,8 +45,8 @@ class SpfOut(ctypes.Structure):
                 ("mask", ctypes.c_void_p), ("sel", ctypes.c_void_p)]
 
 
-def load():
-    lib = ctypes.CDLL(LIB_PATH)
+def load(path=None):
+    lib = ctypes.CDLL(path or LIB_PATH)
     lib.ogs_version.restype = ctypes.c_char_p
     lib.ogs_last_error.restype = ctypes.c_char_p
     lib.ogs_spf_routes.argtypes = [

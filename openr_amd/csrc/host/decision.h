@@ -217,7 +217,8 @@ struct FlatTopology {
   bool hasWideMetric{false};  // metric >= 2^32 (negative i32)
   uint64_t version{0};
   int slotStride{0};  // ogs_graph.slot_stride of dSlot (0: none)
-  DeviceBuffer dRow, dEdges, dFlags, dNodeBase, dSlot;
+  int slotDegree{0};  // ogs_graph.slot_degree of dSlotEdges (0: none)
+  DeviceBuffer dRow, dEdges, dFlags, dNodeBase, dSlot, dSlotEdges;
 };
 
 // ------------------------------------------------------------- LinkState --
@@ -461,8 +462,12 @@ struct HostBatch {
   bool hasZeroMetric{false};
   void append(const FlatTopology& t, const PrefixState& ps,
               const std::string& area);
-  // ogs_graph.slot_node image ([T*stride]); returns the stride, 0 if none
-  int slotOrder(std::vector<uint16_t>& out) const;
+  // ogs_graph.slot_node image ([T*stride]); returns the stride, 0 if none.
+  // With `edgesOut`, also the slot_edges image and its degree (0 if the
+  // batch does not qualify).
+  int slotOrder(std::vector<uint16_t>& out,
+                std::vector<uint32_t>* edgesOut = nullptr,
+                int* degreeOut = nullptr) const;
 };
 
 // ---------------------------------------------------- materialisation --

@@ -304,6 +304,16 @@ const FlatTopology& LinkState::flatOnDevice() const {
                           uint32_t(m.names.size())),
                m.slotStride, slots.data());
     m.dSlot.upload(slots.data(), slots.size());
+    m.slotDegree = slotDegreeFor(m.maxDegree, m.maxMetric, m.slotStride);
+    if (m.slotDegree) {
+      std::vector<uint32_t> img(size_t(m.slotDegree) * m.slotStride);
+      placeSlotEdges(slots.data(), m.slotStride, m.rowPtr.data(),
+                     m.edges.data(), uint32_t(m.names.size()), m.slotDegree,
+                     img.data());
+      m.dSlotEdges.upload(img.data(), img.size());
+    }
+  } else {
+    m.slotDegree = 0;
   }
   deviceStale_ = false;
   return f;
@@ -370,6 +380,8 @@ const LinkState::SpfResult& LinkState::getSpfResult(const std::string& node,
   g.node_flags = f.dFlags.as<uint8_t>();
   g.slot_node = f.slotStride ? f.dSlot.as<uint16_t>() : nullptr;
   g.slot_stride = f.slotStride;
+  g.slot_edges = f.slotDegree ? f.dSlotEdges.as<uint32_t>() : nullptr;
+  g.slot_degree = f.slotDegree;
   ogs_spf_out out{};
   out.dist = sc.dist.get();
   out.nh = sc.nh.as<uint32_t>();

@@ -68,4 +68,38 @@ inline void placeSlots(const std::vector<uint8_t>& color, int stride,
   for (uint32_t v = 0; v < N; ++v) out[color[v] ? i1++ : i0++] = uint16_t(v);
 }
 
+// Degree of the per-position edge image (ogs_graph.slot_edges), or 0 when
+// the batch does not qualify (degree > 8 or a metric > 65535).
+inline int slotDegreeFor(int maxDegree, uint64_t maxMetric, int stride) {
+  if (!stride || maxDegree > 8 || maxMetric > 0xFFFFu) return 0;
+  return maxDegree <= 4 ? 4 : 8;
+}
+
+// Per-position edge image of one topology: out[j * stride + p] describes
+// edge j of the node at position p (layout in include/openr_gpu.h).
+// rowPtr[v] indexes `edges` directly (global or topology-local offsets).
+inline void placeSlotEdges(const uint16_t* slots, int stride,
+                           const uint32_t* rowPtr, const uint64_t* edges,
+                           uint32_t N, int degree, uint32_t* out) {
+  std::vector<uint16_t> pos(N, 0);
+  for (int p = 0; p < stride; ++p) {
+    if (slots[p] != 0xFFFF) pos[slots[p]] = uint16_t(p);
+  }
+  std::fill(out, out + size_t(degree) * stride, OGS_SLOT_EDGE_DOWN);
+  for (int p = 0; p < stride; ++p) {
+    const uint32_t v = slots[p];
+    if (v == 0xFFFF) continue;
+    for (uint32_t e = rowPtr[v], j = 0; e < rowPtr[v + 1]; ++e, ++j) {
+      const uint32_t lo = uint32_t(edges[e]);
+      const uint32_t w = uint32_t(edges[e] >> 32);
+      const uint32_t u = lo & OGS_EDGE_DST_MASK;
+      const uint32_t rslot = (lo >> OGS_EDGE_RSLOT_SHIFT) & OGS_EDGE_RSLOT_MASK;
+      out[size_t(j) * stride + p] = uint32_t(pos[u]) |
+          ((lo & OGS_EDGE_DOWN) ? OGS_SLOT_EDGE_DOWN : 0u) |
+          ((lo & OGS_EDGE_DST_OVERLOADED) ? OGS_SLOT_EDGE_DST_OVERLOADED : 0u) |
+          (rslot << OGS_SLOT_EDGE_RSLOT_SHIFT) | (w << 16);
+    }
+  }
+}
+
 }  // namespace openr_amd

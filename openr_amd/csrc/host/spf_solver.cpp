@@ -113,16 +113,27 @@ void HostBatch::append(const FlatTopology& t, const PrefixState& ps,
                    uint32_t(advNode.size()) - ab0});
 }
 
-int HostBatch::slotOrder(std::vector<uint16_t>& out) const {
+int HostBatch::slotOrder(std::vector<uint16_t>& out,
+                         std::vector<uint32_t>* edgesOut,
+                         int* degreeOut) const {
   const int stride = slotStrideFor(maxNodes);
+  const int degree = slotDegreeFor(maxDegree, maxMetric, stride);
   out.clear();
+  if (edgesOut) edgesOut->clear();
+  if (degreeOut) *degreeOut = edgesOut ? degree : 0;
   if (!stride) return 0;
   const size_t T = nodeBase.size() - 1;
   out.resize(T * stride);
+  if (edgesOut && degree) edgesOut->resize(T * size_t(degree) * stride);
   for (size_t t = 0; t < T; ++t) {
     const std::vector<uint8_t> c(color.begin() + nodeBase[t],
                                  color.begin() + nodeBase[t + 1]);
     placeSlots(c, stride, &out[t * stride]);
+    if (edgesOut && degree) {
+      placeSlotEdges(&out[t * stride], stride, &rowPtr[nodeBase[t]],
+                     edges.data(), nodeBase[t + 1] - nodeBase[t], degree,
+                     &(*edgesOut)[t * size_t(degree) * stride]);
+    }
   }
   return stride;
 }
@@ -360,6 +371,8 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(
   g.node_flags = f.dFlags.as<uint8_t>();
   g.slot_node = f.slotStride ? f.dSlot.as<uint16_t>() : nullptr;
   g.slot_stride = f.slotStride;
+  g.slot_edges = f.slotDegree ? f.dSlotEdges.as<uint32_t>() : nullptr;
+  g.slot_degree = f.slotDegree;
   ogs_prefix_table pt{};
   pt.max_prefixes = int32_t(P);
   pt.max_advertisements = int32_t(I.table.advEntry.size());

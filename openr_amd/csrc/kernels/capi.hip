@@ -9,6 +9,7 @@
 
 namespace ogs {
 extern int g_unitWidth;
+extern int g_waveWgLds;
 hipError_t launch_spf_routes(const ogs_graph& g, const ogs_prefix_table* pt,
                              const ogs_unit* units, int nUnits, uint32_t flags,
                              int W, const ogs_spf_out& out, hipStream_t stream,
@@ -102,9 +103,16 @@ int ogs_set_option(const char* name, int64_t value) {
   if (std::strcmp(name, "unit_width") == 0) {
     if (value != -1 && value != 0 && value != 1 && value != 2 && value != 64 &&
         value != 128 && value != 256) {
-      return fail(OGS_E_INVALID, "unit_width must be -1, 0, 1, 64, 128 or 256");
+      return fail(OGS_E_INVALID, "unit_width must be -1, 0, 1, 2, 64, 128 or 256");
     }
     ogs::g_unitWidth = int(value);
+    return OGS_OK;
+  }
+  if (std::strcmp(name, "wave_wg_lds") == 0) {
+    if (value < 0 || value > 160 * 1024) {
+      return fail(OGS_E_INVALID, "wave_wg_lds must be in [0, 163840]");
+    }
+    ogs::g_waveWgLds = int(value);
     return OGS_OK;
   }
   return fail(OGS_E_INVALID, std::string("unknown option ") + name);
@@ -138,6 +146,10 @@ int ogs_spf_routes(const ogs_graph* graph, const ogs_prefix_table* prefixes,
   }
   if (graph->slot_node && graph->slot_stride < graph->max_nodes) {
     return fail(OGS_E_INVALID, "slot_stride < max_nodes");
+  }
+  if (graph->slot_edges &&
+      (!graph->slot_node || (graph->slot_degree != 4 && graph->slot_degree != 8))) {
+    return fail(OGS_E_INVALID, "slot_edges needs slot_node and slot_degree 4 or 8");
   }
   if (prefixes && (!prefixes->pfx_base || !prefixes->adv_off ||
                    !prefixes->adv_node || !prefixes->adv_metrics ||

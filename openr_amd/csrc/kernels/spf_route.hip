@@ -201,11 +201,12 @@ bool try_small(const ogs_graph& g, const ogs_prefix_table& pt, int hasPrefixes,
 
 bool try_wave(const ogs_graph& g, const ogs_prefix_table& pt, int hasPrefixes,
               const ogs_unit* units, int nUnits, uint32_t flags,
-              const ogs_spf_out& out, uint32_t maxA, bool dirty,
-              hipStream_t stream, hipError_t* err);
+              const ogs_spf_out& out, uint32_t maxA, hipStream_t stream,
+              hipError_t* err);
 
 // unit_width option / OGS_UNIT_WIDTH env: -1 automatic, 0 generic kernel
-// only, 1 wave kernel, 64/128/256 small kernel at that unit width.
+// only, 1 wave kernel, 2 small kernel (automatic width), 64/128/256 small
+// kernel at that unit width.
 int g_unitWidth = [] {
   const char* e = getenv("OGS_UNIT_WIDTH");
   return e ? atoi(e) : -1;
@@ -221,16 +222,16 @@ hipError_t launch_spf_routes(const ogs_graph& g, const ogs_prefix_table* pt,
   const int hasPrefixes = pt ? 1 : 0;
   const int uw = small_unit_width();
   const uint32_t maxA = hasPrefixes ? uint32_t(p.max_advertisements) : 0u;
-  if (W == 1 && (uw == -1 || uw == 1 || uw == 2)) {
+  if (W == 1 && (uw == -1 || uw == 1)) {
     hipError_t err = hipSuccess;
-    if (try_wave(g, p, hasPrefixes, units, nUnits, flags, out, maxA, uw == 2,
-                 stream, &err)) {
+    if (try_wave(g, p, hasPrefixes, units, nUnits, flags, out, maxA, stream,
+                 &err)) {
       return err;
     }
   }
   if (W == 1 && uw != 0) {
     hipError_t err = hipSuccess;
-    const int width = uw > 1 ? uw : 0;
+    const int width = uw >= 64 ? uw : 0;
     const bool done = (flags & OGS_F_WIDE_METRIC)
         ? try_small<uint64_t, 1>(g, p, hasPrefixes, units, nUnits, flags, out,
                                  g.max_degree, maxA, width, stream, &err)

@@ -8,12 +8,12 @@
 // instructions, not latency:
 //  * per node ONE 64-bit LDS word {dist, next-hop bits}: one ds_read_b64
 //    per edge instead of two ds_read_b32;
-//  * dirty tracking in scalar registers: the wave's ballots of "changed in
-//    this round" (one 64-bit mask per node slot) say which nodes moved; a
-//    node re-reads its neighbours only when one of them moved since its last
-//    evaluation (its value is a pure function of its neighbours', so a node
-//    whose neighbours are unchanged already holds its fixpoint value). The
-//    source starts as the only "moved" node;
+//  * branch-free relaxation: unusable edges read a dummy word, edges into
+//    the source read a per-link-slot word, so a round is add/min/compare/or
+//    only (VALU issue is the bound: 4 waves per SIMD, 4 cycles per op);
+//  * nodes are relaxed in a host-chosen order (ogs_graph.slot_node): the
+//    two BFS colour classes go to different 64-lane slots, so one round
+//    advances two hops on bipartite topologies;
 //  * edges (<= MAXD per node) and the node's own value stay in registers;
 //  * one dependent global load for the unit's offsets (ogs_graph.topo_desc)
 //    and one batch of staging loads for CSR + prefix table;
@@ -32,13 +32,17 @@ namespace ogs {
 // route selection reads them; minNexthop is read from HBM on demand (only
 // for prefixes flagged OGS_PFX_HAS_MIN_NH).
 struct WaveLayout {
-  uint32_t dn, row, edges, flags, advOff, advNode, advMetrics, pfxFlags, total;
+  uint32_t dn, dn32, row, edges, flags, advOff, advNode, advMetrics, pfxFlags,
+      total;
   __host__ __device__ static WaveLayout make(uint32_t N, uint32_t E, uint32_t P,
                                              uint32_t A, bool brs) {
     WaveLayout L;
     uint32_t o = 0;
-    L.dn = o;
-    o += align16(uint64_t(N) * 8);
+    const uint32_t P0 = N <= 64 ? 64 : N <= 128 ? 128 : 256;  // = 64 * NPL
+    L.dn = o;  // P0 positions (later: N node words) + dummy + 8 source words
+    o += align16(uint64_t(P0 + 9) * 8);
+    L.dn32 = o;  // narrow-form words, same positions (first: posOf scratch)
+    o += align16(uint64_t(P0 + 9) * 4);
     L.row = o;
     o += align16(uint64_t(N + 1) * 4);
     L.edges = o;
@@ -58,12 +62,24 @@ struct WaveLayout {
   }
 };
 
+struct IdentitySlots {
+  uint16_t v[256];
+  constexpr IdentitySlots() : v() {
+    for (int i = 0; i < 256; ++i) v[i] = uint16_t(i);
+  }
+};
+__device__ IdentitySlots kIdentitySlots;
+
 template <int K, typename T>
 struct WStage {  // K elements per lane, all loads before any store
   T v[K];
   __device__ __forceinline__ void load(const T* __restrict__ src, uint32_t n,
                                        int lane) {
-    if (n == 0) return;
+    if (n == 0) {  // keep v[] defined on every path (no stack copy)
+#pragma unroll
+      for (int k = 0; k < K; ++k) v[k] = T{};
+      return;
+    }
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       const uint32_t i = uint32_t(k * 64 + lane);
@@ -120,43 +136,37 @@ __device__ __forceinline__ void route_single(uint32_t n, int64_t minNh,
   }
 }
 
-template <int NPL, int MAXD, bool DIRTY>
+template <int NPL, int MAXD>
 __global__ __launch_bounds__(256) void spf_route_wave_kernel(
     ogs_graph g, ogs_prefix_table pt, int hasPrefixes,
     const ogs_unit* __restrict__ units, int nUnits, uint32_t flags,
     ogs_spf_out out, uint32_t ldsPerUnit, uint32_t maxA) {
   constexpr uint32_t kInf = 0xFFFFFFFFu;
-  const int uib = threadIdx.x >> 6;
+  // wave-uniform by construction; readfirstlane lets the compiler prove it,
+  // so the unit record and its descriptor come through scalar loads
+  const int uib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const int uidx = blockIdx.x * 4 + uib;
   if (uidx >= nUnits) return;
 #ifdef OGS_STAMPS  // diagnostic build only: phase clocks into out.sel
   const uint64_t tStart = __builtin_amdgcn_s_memtime();
+  const uint64_t rtStart = __builtin_amdgcn_s_memrealtime();  // 100 MHz
   uint64_t tDesc = 0, tStaged = 0, tSpf = 0;
-  uint32_t rounds = 0, evals = 0;
+  uint32_t rounds = 0;
 #endif
 
   // ---- unit offsets -------------------------------------------------------
   const ogs_unit unit = units[uidx];
   const uint32_t s = unit.src;
-  // relaxation order (slot_order.h): position k*64+lane -> node id
-  const bool perm = !DIRTY && g.slot_node && g.slot_stride == NPL * 64;
+  // relaxation order (slot_order.h): position k*64+lane -> node id; loaded
+  // with the staging batch below
+  const bool perm = g.slot_node && g.slot_stride == NPL * 64;
   uint32_t vk[NPL];
-  if (perm) {
-    const uint16_t* so = g.slot_node + size_t(unit.topo) * (NPL * 64);
-#pragma unroll
-    for (int k = 0; k < NPL; ++k) {
-      const uint32_t x = so[k * 64 + lane];
-      vk[k] = x == 0xFFFFu ? 0xFFFFFFFFu : x;
-    }
-  } else {
-#pragma unroll
-    for (int k = 0; k < NPL; ++k) vk[k] = uint32_t(k * 64 + lane);
-  }
   uint32_t nb, N, e0, E, p0 = 0, P = 0, a0 = 0, A = 0;
   if (g.topo_desc) {
     const uint4* d = reinterpret_cast<const uint4*>(g.topo_desc) + 2 * unit.topo;
-    const uint4 x = d[0], y = d[1];
+    const uint4 x = d[0];
+    const uint4 y = d[1];
     nb = x.x;
     N = x.y;
     e0 = x.z;
@@ -199,13 +209,40 @@ __global__ __launch_bounds__(256) void spf_route_wave_kernel(
   uint8_t* lPfxFlags = reinterpret_cast<uint8_t*>(base + L.pfxFlags);
 
   // ---- staging: one batch of loads, then LDS writes -----------------------
+  // With the per-position edge image (ogs_graph.slot_edges) each lane loads
+  // its nodes' edges coalesced straight into registers and the CSR is not
+  // staged at all.
+  constexpr uint32_t P0 = NPL * 64;
+  const bool img = perm && g.slot_edges && g.slot_degree == MAXD;
+  uint32_t ie[NPL][MAXD];
   {
     WStage<NPL + 1, uint32_t> sRow;
     WStage<NPL * MAXD, uint64_t> sEdge;  // E <= N * MAXD <= 64 * NPL * MAXD
     WStage<NPL, uint8_t> sFlag;
-    sRow.load(g.row_ptr + nb, N + 1, lane);
-    sEdge.load(g.edges + e0, E, lane);
+    sRow.load(g.row_ptr + nb, img ? 0u : N + 1, lane);
+    sEdge.load(g.edges + e0, img ? 0u : E, lane);
+    if (img) {
+      const uint32_t* ib = g.slot_edges + size_t(unit.topo) * (MAXD * P0);
+#pragma unroll
+      for (int j = 0; j < MAXD; ++j) {
+#pragma unroll
+        for (int k = 0; k < NPL; ++k) ie[k][j] = ib[j * P0 + k * 64 + lane];
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < MAXD; ++j) {
+#pragma unroll
+        for (int k = 0; k < NPL; ++k) ie[k][j] = 0u;
+      }
+    }
     sFlag.load(g.node_flags + nb, N, lane);
+    // unconditional (identity table without slot_node): no branch, so
+    // nothing waits on these loads before the whole batch is issued
+    const uint16_t* so = perm ? g.slot_node + size_t(unit.topo) * (NPL * 64)
+                              : kIdentitySlots.v;
+    uint32_t rawSlot[NPL];
+#pragma unroll
+    for (int k = 0; k < NPL; ++k) rawSlot[k] = so[k * 64 + lane];
     constexpr int KP = NPL + 1;  // prefixes per lane per pass (P <= 64*KP)
     WStage<KP, uint32_t> sOff, sNode;
     WStage<KP, int4> sMet;
@@ -214,16 +251,20 @@ __global__ __launch_bounds__(256) void spf_route_wave_kernel(
     if (hasPrefixes && pfxFits) {
       sOff.load(pt.adv_off + p0, P + 1, lane);
       sNode.load(pt.adv_node + a0, A, lane);
-      if (brs) sMet.load(reinterpret_cast<const int4*>(pt.adv_metrics) + a0, A, lane);
+      sMet.load(reinterpret_cast<const int4*>(pt.adv_metrics) + a0, brs ? A : 0u, lane);
       sPf.load(pt.pfx_flags + p0, P, lane);
     }
-    sRow.store(lrow, N + 1, lane);
-    sEdge.store(ledg, E, lane);
+#pragma unroll
+    for (int k = 0; k < NPL; ++k) {
+      vk[k] = rawSlot[k] == 0xFFFFu ? 0xFFFFFFFFu : rawSlot[k];
+    }
+    sRow.store(lrow, img ? 0u : N + 1, lane);
+    sEdge.store(ledg, img ? 0u : E, lane);
     sFlag.store(lflags, N, lane);
     if (hasPrefixes && pfxFits) {
       sOff.store(lAdvOff, P + 1, lane);
       sNode.store(lAdvNode, A, lane);
-      if (brs) sMet.store(lAdvMetrics, A, lane);
+      sMet.store(lAdvMetrics, brs ? A : 0u, lane);
       sPf.store(lPfxFlags, P, lane);
     } else if (hasPrefixes) {  // rare: long prefix tables, plain loop
       for (uint32_t i = lane; i <= P; i += 64) lAdvOff[i] = pt.adv_off[p0 + i];
@@ -240,114 +281,239 @@ __global__ __launch_bounds__(256) void spf_route_wave_kernel(
 #endif
 
   // ---- registers: per-edge constants of the lane's node slots -------------
-  // Distances inside the loop are capped at kCap = 2^31 - 1 ("unreachable"),
-  // unusable edges carry weight kCap, so cand = du + w never wraps (the host
-  // guarantees every real path < 2^31 - 1 when it picks this kernel) and
-  // min() needs no predicate. The source's next-hop word is 0, so the tight
-  // contribution of edge j is nh(u) | srcBit_j with srcBit_j = the source
-  // link slot bit when u == src, else 0 (LinkState.cpp:808-811).
-  constexpr uint32_t kCap = 0x7FFFFFFFu;
+  // During SPF the LDS words are indexed by POSITION (slot*64 + lane), not
+  // by node id: under the 2-colour order the neighbours of consecutive lanes
+  // sit at consecutive positions of the other slot, so the gathers are
+  // (nearly) bank-conflict free. Extra words after the P0 = 64*NPL
+  // positions remove every branch and special case from the relaxation:
+  //  * word P0 (dummy) = "unreachable": target of unusable edges;
+  //  * word P0+1+r = {dist 0, next hops {r}}: the source seen through its
+  //    link slot r. An edge v -> src reads the word of its own slot instead
+  //    of the source's, so the tight contribution of every edge is just the
+  //    word's next-hop part (LinkState.cpp:808-811: NH(v) gets the source's
+  //    link to v).
   const bool hop = flags & OGS_F_HOP_METRIC;
-  uint32_t eu[NPL][MAXD], ew[NPL][MAXD], eb[NPL][MAXD];
-  uint32_t dcur[NPL], ncur[NPL];
+  uint32_t ea[NPL][MAXD], ew[NPL][MAXD];  // word position, weight (0 if unusable)
+  uint32_t wmax = 0;
+  if (img) {
+    uint32_t posS = 0;  // the source's position (uniform)
 #pragma unroll
-  for (int k = 0; k < NPL; ++k) {
-    const uint32_t v = vk[k];
-    const bool own = v < N;
-    const uint32_t e = own ? lrow[v] - e0 : 0u;
-    const uint32_t deg = own ? lrow[v + 1] - lrow[v] : 0u;
-#pragma unroll
-    for (int j = 0; j < MAXD; ++j) {
-      const uint64_t x = (uint32_t(j) < deg) ? ledg[e + j] : uint64_t(OGS_EDGE_DOWN);
-      const uint32_t lo = static_cast<uint32_t>(x);
-      const uint32_t u = edge_dst(lo);
-      const bool ok = !(lo & OGS_EDGE_DOWN) &&
-          !((lo & OGS_EDGE_DST_OVERLOADED) && u != s);
-      const uint32_t w = hop ? 1u : static_cast<uint32_t>(x >> 32);
-      eu[k][j] = ok ? u : 0u;
-      ew[k][j] = ok ? (w < kCap ? w : kCap) : kCap;
-      eb[k][j] = (ok && u == s) ? (1u << (edge_rslot(lo) & 31u)) : 0u;
+    for (int k = 0; k < NPL; ++k) {
+      const uint64_t m = __builtin_amdgcn_ballot_w64(vk[k] == s);
+      if (m) posS = uint32_t(k * 64) + uint32_t(__builtin_ctzll(m));
     }
-    dcur[k] = (v == s) ? 0u : kCap;
-    ncur[k] = 0u;
-    if (own) dn[v] = dcur[k];
-  }
-  wave_sync();
-
-  // ---- SPF: pull rounds (optionally only for nodes with a moved neighbour) --
-  uint64_t moved[NPL];  // nodes changed since the previous round (uniform)
 #pragma unroll
-  for (int k = 0; k < NPL; ++k) moved[k] = (s >> 6) == uint32_t(k) ? 1ull << (s & 63) : 0ull;
-  for (;;) {
-    uint64_t now[NPL];
+    for (int k = 0; k < NPL; ++k) {
 #pragma unroll
-    for (int k = 0; k < NPL; ++k) now[k] = 0ull;
-    bool any = false;
+      for (int j = 0; j < MAXD; ++j) {
+        const uint32_t x = ie[k][j];
+        const uint32_t nbr = x & 0x1FFu;
+        const bool ok = !(x & OGS_SLOT_EDGE_DOWN) &&
+            !((x & OGS_SLOT_EDGE_DST_OVERLOADED) && nbr != posS);
+        const uint32_t w = hop ? 1u : x >> 16;
+        ea[k][j] = !ok ? P0
+                       : (nbr == posS ? P0 + 1 + ((x >> OGS_SLOT_EDGE_RSLOT_SHIFT) & 7u)
+                                      : nbr);
+        ew[k][j] = ok ? w : 0u;
+        wmax = ew[k][j] > wmax ? ew[k][j] : wmax;
+      }
+    }
+  } else {
+    {
+      uint32_t* posOf = reinterpret_cast<uint32_t*>(base + L.dn32);  // scratch
+#pragma unroll
+      for (int k = 0; k < NPL; ++k) {
+        if (vk[k] < N) posOf[vk[k]] = uint32_t(k * 64 + lane);
+      }
+    }
+    wave_sync();
+    const uint32_t* posOf = reinterpret_cast<const uint32_t*>(base + L.dn32);
 #pragma unroll
     for (int k = 0; k < NPL; ++k) {
       const uint32_t v = vk[k];
-      bool dirty = true;
-      if constexpr (DIRTY) {
-        dirty = false;
+      const bool own = v < N;
+      const uint32_t e = own ? lrow[v] - e0 : 0u;
+      const uint32_t deg = own ? lrow[v + 1] - lrow[v] : 0u;
+#pragma unroll
+      for (int j = 0; j < MAXD; ++j) {
+        const uint64_t x = (uint32_t(j) < deg) ? ledg[e + j] : uint64_t(OGS_EDGE_DOWN);
+        const uint32_t lo = static_cast<uint32_t>(x);
+        const uint32_t u = edge_dst(lo);
+        const bool ok = !(lo & OGS_EDGE_DOWN) &&
+            !((lo & OGS_EDGE_DST_OVERLOADED) && u != s);
+        const uint32_t w = hop ? 1u : static_cast<uint32_t>(x >> 32);
+        ea[k][j] = !ok ? P0 : (u == s ? P0 + 1 + edge_rslot(lo) : posOf[u]);
+        ew[k][j] = ok ? w : 0u;
+        wmax = ew[k][j] > wmax ? ew[k][j] : wmax;
+      }
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint32_t t = __shfl_xor(wmax, o);
+    wmax = t > wmax ? t : wmax;
+  }
+  wmax = __builtin_amdgcn_readfirstlane(wmax);
+  uint64_t actMask[NPL];  // lanes holding a non-source node (uniform)
+  uint32_t dcur[NPL], ncur[NPL];
+#pragma unroll
+  for (int k = 0; k < NPL; ++k) {
+    actMask[k] = __builtin_amdgcn_ballot_w64(vk[k] < N && vk[k] != s);
+  }
+  // Two-slot units whose slots are separated (every edge between two nodes
+  // joins slot 0 and slot 1, true for the 2-colour order on bipartite
+  // graphs) converge at the first slot evaluation after the first one that
+  // changes nothing: slot X unchanged means slot Y's inputs are those of its
+  // previous evaluation. Others stop after a full unchanged round.
+  bool sep = false;
+  if (NPL == 2) {
+    bool bad = false;
+#pragma unroll
+    for (int k = 0; k < NPL; ++k) {
+#pragma unroll
+      for (int j = 0; j < MAXD; ++j) {
+        bad |= ((actMask[k] >> lane) & 1ull) && ea[k][j] < P0 &&
+            (ea[k][j] >> 6) == uint32_t(k);
+      }
+    }
+    sep = __builtin_amdgcn_ballot_w64(bad) == 0ull;
+  }
+  wave_sync();  // posOf scratch is overwritten below
+
+  // ---- SPF: pull rounds to the fixpoint -------------------------------------
+  // Narrow form (every path < 2^23, the common case, decided per unit): one
+  // 32-bit word per node, dist << 8 | next-hop bits (source degree <= 8).
+  // Adding w << 8 carries the next-hop bits along, all candidates tied with
+  // the minimum share its distance bits, so the new word is simply the OR of
+  // the candidates <= (min | 0xFF). Unreachable = 2^31 (dist field 2^23):
+  // unreachable candidates are > 2^31 and never tie with a reachable one.
+  // Wide form (paths < 2^31 - 1, host-guaranteed): 64-bit {dist, nh} words,
+  // tie test by equality.
+  const bool narrow = uint64_t(wmax) * (N > 0 ? N - 1 : 0) < 0x7FFFFFull;
+  if (narrow) {
+    constexpr uint32_t kUnr = 0x80000000u;
+    uint32_t* d32 = reinterpret_cast<uint32_t*>(base + L.dn32);
+    uint32_t ws[NPL][MAXD], cur[NPL];
+#pragma unroll
+    for (int k = 0; k < NPL; ++k) {
+#pragma unroll
+      for (int j = 0; j < MAXD; ++j) ws[k][j] = ew[k][j] << 8;
+      cur[k] = vk[k] == s ? 0u : kUnr;
+      d32[k * 64 + lane] = cur[k];
+    }
+    if (lane == 0) d32[P0] = kUnr;
+    if (lane < 8) d32[P0 + 1 + lane] = 1u << lane;
+    wave_sync();
+    for (int step = 0;; ) {
+      uint64_t now = 0ull;
+      bool done = false;
+#pragma unroll
+      for (int k = 0; k < NPL; ++k) {
+        uint32_t cand[MAXD];
+        uint32_t best = kUnr;
 #pragma unroll
         for (int j = 0; j < MAXD; ++j) {
-          const uint32_t u = eu[k][j];
-          uint64_t set = moved[0] | now[0];
+          cand[j] = d32[ea[k][j]] + ws[k][j];
+          best = cand[j] < best ? cand[j] : best;
+        }
+        const uint32_t hiB = best | 0xFFu;
+        uint32_t word = best & kUnr;
 #pragma unroll
-          for (int kk = 1; kk < NPL; ++kk) {
-            set = (u >> 6) == uint32_t(kk) ? (moved[kk] | now[kk]) : set;
-          }
-          dirty |= ew[k][j] != kCap && ((set >> (u & 63)) & 1ull);
+        for (int j = 0; j < MAXD; ++j) word |= cand[j] <= hiB ? cand[j] : 0u;
+        const uint64_t diff = __builtin_amdgcn_ballot_w64(word != cur[k]);
+        cur[k] = word;
+        d32[k * 64 + lane] = word;
+        now |= diff & actMask[k];
+        if (sep && ++step >= 2 && !(diff & actMask[k])) {
+          done = true;
+          break;
         }
       }
-      bool changed = false;
 #ifdef OGS_STAMPS
-      evals += __popcll(__ballot(dirty && v < N && v != s));
+      ++rounds;
 #endif
-      if (dirty && v < N && v != s) {
+      if (done || !now) break;
+      wave_sync();
+    }
+#pragma unroll
+    for (int k = 0; k < NPL; ++k) {
+      dcur[k] = cur[k] >= kUnr ? kInf : cur[k] >> 8;
+      ncur[k] = cur[k] >= kUnr ? 0u : cur[k] & 0xFFu;
+    }
+  } else {
+    constexpr uint32_t kUnr = 0x80000000u;
+    uint32_t we[NPL][MAXD];
+#pragma unroll
+    for (int k = 0; k < NPL; ++k) {
+#pragma unroll
+      for (int j = 0; j < MAXD; ++j) {
+        // unusable: dummy {kUnr} + 2^31-1 = 2^32-1, never wins, never wraps
+        we[k][j] = ea[k][j] == P0 ? kUnr - 1 : ew[k][j];
+      }
+      dcur[k] = vk[k] == s ? 0u : kUnr;
+      ncur[k] = 0u;
+      dn[k * 64 + lane] = dcur[k];
+    }
+    if (lane == 0) dn[P0] = uint64_t(kUnr);
+    if (lane < 8) dn[P0 + 1 + lane] = uint64_t(1u << lane) << 32;
+    wave_sync();
+    for (int step = 0;; ) {
+      uint64_t now = 0ull;
+      bool done = false;
+#pragma unroll
+      for (int k = 0; k < NPL; ++k) {
         uint64_t x[MAXD];
 #pragma unroll
-        for (int j = 0; j < MAXD; ++j) x[j] = dn[eu[k][j]];
-        uint32_t best = kCap;
+        for (int j = 0; j < MAXD; ++j) x[j] = dn[ea[k][j]];
+        uint32_t best = kUnr;
         uint32_t cand[MAXD];
 #pragma unroll
         for (int j = 0; j < MAXD; ++j) {
-          cand[j] = static_cast<uint32_t>(x[j]) + ew[k][j];
+          cand[j] = static_cast<uint32_t>(x[j]) + we[k][j];
           best = cand[j] < best ? cand[j] : best;
         }
         uint32_t m = 0u;
 #pragma unroll
         for (int j = 0; j < MAXD; ++j) {
-          m |= (cand[j] == best) ? (static_cast<uint32_t>(x[j] >> 32) | eb[k][j]) : 0u;
+          m |= (cand[j] == best) ? static_cast<uint32_t>(x[j] >> 32) : 0u;
         }
-        if (best >= kCap) {
-          best = kCap;
-          m = 0u;
-        }
-        if (best != dcur[k] || m != ncur[k]) {
-          dcur[k] = best;
-          ncur[k] = m;
-          dn[v] = uint64_t(best) | (uint64_t(m) << 32);
-          changed = true;
+        const uint64_t diff = __builtin_amdgcn_ballot_w64(best != dcur[k]) |
+            __builtin_amdgcn_ballot_w64(m != ncur[k]);
+        dcur[k] = best;
+        ncur[k] = m;
+        dn[k * 64 + lane] = uint64_t(best) | (uint64_t(m) << 32);
+        now |= diff & actMask[k];
+        if (sep && ++step >= 2 && !(diff & actMask[k])) {
+          done = true;
+          break;
         }
       }
-      now[k] = __ballot(changed);
-      any |= now[k] != 0ull;
+#ifdef OGS_STAMPS
+      ++rounds;
+#endif
+      if (done || !now) break;
+      wave_sync();
     }
 #pragma unroll
-    for (int k = 0; k < NPL; ++k) moved[k] = now[k];
-#ifdef OGS_STAMPS
-    ++rounds;
-#endif
-    if (!any) break;
-    wave_sync();
+    for (int k = 0; k < NPL; ++k) {
+      if (dcur[k] >= kUnr) {
+        dcur[k] = kInf;
+        ncur[k] = 0u;
+      }
+    }
   }
-  // back to the ABI's "unreachable" (all ones) for outputs and routes
+  // final {dist, nh} words, now by NODE ID, for the route phase (ABI
+  // "unreachable" = all ones); the source lane's registers hold its unused
+  // evaluation. All position-indexed reads precede these writes in program
+  // order.
 #pragma unroll
   for (int k = 0; k < NPL; ++k) {
     const uint32_t v = vk[k];
-    if (dcur[k] >= kCap) dcur[k] = kInf;
-    if (v < N && dcur[k] == kInf) dn[v] = uint64_t(kInf);
+    if (v == s) {
+      dcur[k] = 0u;
+      ncur[k] = 0u;
+    }
+    if (v < N) dn[v] = uint64_t(dcur[k]) | (uint64_t(ncur[k]) << 32);
   }
   wave_sync();
 #ifdef OGS_STAMPS
@@ -412,19 +578,25 @@ __global__ __launch_bounds__(256) void spf_route_wave_kernel(
     d[2] = uint32_t(tEnd - tSpf);
     d[3] = rounds;
     d[4] = uint32_t(tDesc - tStart);
-    d[5] = evals;
+    d[5] = uint32_t(rtStart);
+    d[6] = uint32_t(__builtin_amdgcn_s_memrealtime());
   }
 #endif
 }
 
-template <int NPL, int MAXD, bool DIRTY>
+// "wave_wg_lds" option: minimum LDS bytes per workgroup (occupancy probe for
+// A/B measurements; 0 = just what the units need)
+int g_waveWgLds = 0;
+
+template <int NPL, int MAXD>
 hipError_t launch_wave(const ogs_graph& g, const ogs_prefix_table& pt,
                        int hasPrefixes, const ogs_unit* units, int nUnits,
                        uint32_t flags, const ogs_spf_out& out, uint32_t lds,
                        uint32_t maxA, hipStream_t stream) {
   const int grid = (nUnits + 3) / 4;
-  const size_t bytes = size_t(lds) * 4;
-  auto k = spf_route_wave_kernel<NPL, MAXD, DIRTY>;
+  size_t bytes = size_t(lds) * 4;
+  if (bytes < size_t(g_waveWgLds)) bytes = size_t(g_waveWgLds);
+  auto k = spf_route_wave_kernel<NPL, MAXD>;
   if (bytes > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute(
         reinterpret_cast<const void*>(k),
@@ -438,8 +610,8 @@ hipError_t launch_wave(const ogs_graph& g, const ogs_prefix_table& pt,
 
 bool try_wave(const ogs_graph& g, const ogs_prefix_table& pt, int hasPrefixes,
               const ogs_unit* units, int nUnits, uint32_t flags,
-              const ogs_spf_out& out, uint32_t maxA, bool dirty,
-              hipStream_t stream, hipError_t* err) {
+              const ogs_spf_out& out, uint32_t maxA, hipStream_t stream,
+              hipError_t* err) {
   if (flags & OGS_F_WIDE_METRIC) return false;
   if (g.max_nodes > 256 || g.max_degree > 8 || g.max_degree < 0) return false;
   const uint32_t P = hasPrefixes ? pt.max_prefixes : 0;
@@ -449,13 +621,9 @@ bool try_wave(const ogs_graph& g, const ogs_prefix_table& pt, int hasPrefixes,
   if (uint64_t(lds) * 4 > 160 * 1024) return false;
   const int N = g.max_nodes;
   const bool d4 = g.max_degree <= 4;
-#define OGS_WAVE(NPL_, MAXD_)                                                 \
-  *err = dirty ? launch_wave<NPL_, MAXD_, true>(g, pt, hasPrefixes, units,    \
-                                               nUnits, flags, out, lds, A,    \
-                                               stream)                        \
-               : launch_wave<NPL_, MAXD_, false>(g, pt, hasPrefixes, units,   \
-                                                nUnits, flags, out, lds, A,   \
-                                                stream);                      \
+#define OGS_WAVE(NPL_, MAXD_)                                             \
+  *err = launch_wave<NPL_, MAXD_>(g, pt, hasPrefixes, units, nUnits, flags, \
+                                  out, lds, A, stream);                   \
   return true;
   if (N <= 64) { if (d4) { OGS_WAVE(1, 4) } OGS_WAVE(1, 8) }
   if (N <= 128) { if (d4) { OGS_WAVE(2, 4) } OGS_WAVE(2, 8) }

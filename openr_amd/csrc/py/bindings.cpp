@@ -353,8 +353,11 @@ class BatchRunner {
     dAdvMinNh_.upload(hb_.advMinNh.data(), hb_.advMinNh.size());
     dPfxFlags_.upload(hb_.pfxFlags.data(), hb_.pfxFlags.size());
     std::vector<uint16_t> slots;
-    slotStride_ = slotOrder_ ? hb_.slotOrder(slots) : 0;
+    std::vector<uint32_t> slotEdges;
+    slotStride_ = slotOrder_ ? hb_.slotOrder(slots, &slotEdges, &slotDegree_) : 0;
+    if (!slotStride_ || !slotEdgeImage_) slotDegree_ = 0;
     dSlot_.upload(slots.data(), slots.size());
+    dSlotEdges_.upload(slotEdges.data(), slotEdges.size());
     dUnits_.upload(units_.data(), units_.size());
     const size_t U = units_.size(), db = wide_ ? 8 : 4;
     const size_t Sn = hb_.maxNodes, Sp = std::max(hb_.maxPrefixes, 1);
@@ -432,6 +435,7 @@ class BatchRunner {
   }
   size_t numUnits() const { return units_.size(); }
   void setSlotOrder(bool on) { slotOrder_ = on; }
+  void setSlotEdgeImage(bool on) { slotEdgeImage_ = on; }
   const HostBatch& host() const { return hb_; }
   const std::vector<ogs_unit>& units() const { return units_; }
   int nhWords() const { return W_; }
@@ -454,6 +458,8 @@ class BatchRunner {
     g.node_flags = dFlags_.as<uint8_t>();
     g.slot_node = slotStride_ ? dSlot_.as<uint16_t>() : nullptr;
     g.slot_stride = slotStride_;
+    g.slot_edges = slotDegree_ ? dSlotEdges_.as<uint32_t>() : nullptr;
+    g.slot_degree = slotDegree_;
     return g;
   }
   ogs_prefix_table table() const {
@@ -475,9 +481,9 @@ class BatchRunner {
     PrefixHostTable table;
   };
   bool enableV4_, sr_, brs_;
-  bool slotOrder_{true};
-  int slotStride_{0};
-  DeviceBuffer dSlot_;
+  bool slotOrder_{true}, slotEdgeImage_{true};
+  int slotStride_{0}, slotDegree_{0};
+  DeviceBuffer dSlot_, dSlotEdges_;
   std::vector<std::unique_ptr<Topo>> topos_;
   HostBatch hb_;
   std::vector<ogs_unit> units_;
@@ -753,6 +759,8 @@ PYBIND11_MODULE(_decision, m) {
       .def("flags", &BatchRunner::flags)
       .def("set_slot_order", &BatchRunner::setSlotOrder,
            "use the 2-colour relaxation order (default on; takes effect at upload)")
+      .def("set_slot_edge_image", &BatchRunner::setSlotEdgeImage,
+           "hand the wave kernel the per-position edge image (default on)")
       .def("nh_words", &BatchRunner::nhWords)
       .def("wide", &BatchRunner::wide)
       .def("host_arrays", [](const BatchRunner& b) {
@@ -771,8 +779,12 @@ PYBIND11_MODULE(_decision, m) {
         d["adv_min_nh"] = npcopy(h.advMinNh);
         d["pfx_flags"] = npcopy(h.pfxFlags);
         std::vector<uint16_t> slots;
-        d["slot_stride"] = h.slotOrder(slots);
+        std::vector<uint32_t> slotEdges;
+        int slotDegree = 0;
+        d["slot_stride"] = h.slotOrder(slots, &slotEdges, &slotDegree);
         d["slot_node"] = npcopy(slots);
+        d["slot_edges"] = npcopy(slotEdges);
+        d["slot_degree"] = slotDegree;
         std::vector<uint32_t> u;
         for (const auto& x : b.units()) {
           u.push_back(x.topo);

@@ -189,11 +189,12 @@ def test_c2_kernel_variants_identical(product, oracle, brs):
                 adjOverloadPermille=10, overloadSeed=0xC22F)
     cpu = None
     try:
-        for uw in (0, 1, 2, 64):
-            for order in (True, False):
+        for uw in (0, 1, 2, 128):
+            for order, image in ((True, True), (True, False), (False, False)):
                 capi.check(lib, lib.ogs_set_option(b"unit_width", uw), "unit_width")
                 br = product.BatchRunner(True, False, brs)
                 br.set_slot_order(order)
+                br.set_slot_edge_image(image)
                 br.add_grid_batch(opts, 0, T, "1")
                 br.upload()
                 br.run()
@@ -201,6 +202,65 @@ def test_c2_kernel_variants_identical(product, oracle, brs):
                 gpu = [br.canonical(u) for u in range(T)]
                 if cpu is None:
                     cpu = oracle.grid_batch_route_dbs(opts, 0, T, "1", brs)
-                _cmp(gpu, cpu, f"c2 uw={uw} order={order}")
+                _cmp(gpu, cpu, f"c2 uw={uw} order={order} image={image}")
     finally:
         lib.ogs_set_option(b"unit_width", -1)
+
+
+@pytest.mark.parametrize("metric_max", [85000, 200000, 20000000])
+def test_wave_kernel_distance_forms(product, oracle, metric_max):
+    """The wave kernel relaxes in a 32-bit packed form when every path is
+    < 2^23 and in 64-bit words otherwise (decided per unit from the largest
+    usable weight); both forms and the boundary between them are exact.
+    metric_max 85000 * 99 straddles 2^23 across topologies; 2e7 * 99 needs
+    the host's wide (u64) path."""
+    T = 128
+    opts = dict(n=10, metricSeed=0xC2300000, prefixSeed=0xC1, metricMax=metric_max)
+    br = product.BatchRunner(True, False, False)
+    br.add_grid_batch(opts, 0, T, "1")
+    br.upload()
+    br.run()
+    br.download()
+    _cmp([br.canonical(u) for u in range(T)],
+         oracle.grid_batch_route_dbs(opts, 0, T, "1"), f"c2 metricMax={metric_max}")
+
+
+def _tri_grid(M, n, seed):
+    """n x n grid plus one diagonal per cell: odd cycles (not bipartite), so
+    the 2-colour slot order leaves same-slot edges and the wave kernel must
+    fall back to the full-round convergence test."""
+    import lsdb as L
+    als = M.AreaLinkStates()
+    ls = als.add(L.kTestingAreaName, "0")
+    ps = M.PrefixState()
+    r = random.Random(seed)
+    metric, nbrs = {}, {}
+    for i in range(n):
+        for j in range(n):
+            for (di, dj) in ((0, 1), (1, 0), (1, 1)):
+                ii, jj = i + di, j + dj
+                if ii < n and jj < n:
+                    a, b = i * n + j, ii * n + jj
+                    metric[(a, b)] = metric[(b, a)] = r.randint(1, 20)
+                    nbrs.setdefault(a, []).append(b)
+                    nbrs.setdefault(b, []).append(a)
+    for v in range(n * n):
+        adjs = [L.createAdjacency(str(u), f"if{v}-{u}", f"if{u}-{v}", f"fe80::{u}",
+                                  f"10.0.{u // 250}.{u % 250}", metric[(v, u)], 100 + u)
+                for u in sorted(nbrs[v])]
+        ls.updateAdjacencyDatabase(L.createAdjDb(str(v), adjs, v + 1), L.kTestingAreaName)
+        L.updatePrefixDatabase(ps, L.createPrefixDb(
+            str(v), [L.createPrefixEntry(f"fc00::{v:x}/128")]))
+    return als, ps
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_non_bipartite_small_topology(product, oracle, seed):
+    n = 10
+    (pa, pp), (oa, op) = _tri_grid(product, n, seed), _tri_grid(oracle, n, seed)
+    ps_ = product.SpfSolver("0", True, False)
+    os_ = oracle.SpfSolver("0", True, False)
+    for src in ("0", "37", "99"):
+        a = ps_.buildRouteDb(src, pa, pp)
+        b = os_.buildRouteDb(src, oa, op)
+        assert a.canonical() == b.canonical(), src

@@ -12,8 +12,10 @@ def _batch(kind="grid", **kw):
     M = openr_amd.decision
     br = M.BatchRunner(True, False, False)
     if kind == "grid":
-        br.add_grid_batch(dict(n=kw.get("n", 10), metricSeed=0xC2000000,
-                               prefixSeed=0xC1), 0, kw.get("topos", 8), "1")
+        opts = dict(n=kw.get("n", 10), metricSeed=0xC2000000, prefixSeed=0xC1)
+        if kw.get("ovl"):
+            opts.update(adjOverloadPermille=50, nodeOverloadPermille=30, overloadSeed=7)
+        br.add_grid_batch(opts, 0, kw.get("topos", 8), "1")
     else:
         br.add_generated(kind, kw["opts"], kw["sources"])
     return br.host_arrays()
@@ -82,3 +84,35 @@ def test_spf_routes_rejects_bad_slot_stride():
         rc = lib.ogs_spf_routes(ctypes.byref(g), None, units, 1, 0, 1,
                                 ctypes.byref(out), None)
         assert rc == -1, stride
+
+
+@pytest.mark.parametrize("n", [7, 10, 16])
+def test_slot_edge_image_matches_csr(n):
+    """ogs_graph.slot_edges restates each ordered node's CSR row: neighbour
+    position, down / overloaded bits, reverse slot and metric."""
+    h = _batch(n=n, topos=3, ovl=True)
+    T, S, D = h["num_topos"], h["slot_stride"], h["slot_degree"]
+    assert D in (4, 8)
+    slots = h["slot_node"].reshape(T, S)
+    img = h["slot_edges"].reshape(T, D, S)
+    rp, edges, nb = h["row_ptr"], h["edges"], h["node_base"]
+    for t in range(T):
+        for p in range(S):
+            v = int(slots[t, p])
+            if v == 0xFFFF:
+                assert (img[t, :, p] & 0x200).all()
+                continue
+            row = range(int(rp[nb[t] + v]), int(rp[nb[t] + v + 1]))
+            for j in range(D):
+                x = int(img[t, j, p])
+                if j >= len(row):
+                    assert x & 0x200
+                    continue
+                e = int(edges[row[j]])
+                lo, w = e & 0xFFFFFFFF, e >> 32
+                u = lo & 0x1FFFFF
+                assert int(slots[t, x & 0x1FF]) == u
+                assert bool(x & 0x200) == bool(lo >> 31)
+                assert bool(x & 0x400) == bool(lo & (1 << 21))
+                assert (x >> 11) & 7 == (lo >> 22) & 0x1FF
+                assert x >> 16 == w

@@ -7,7 +7,7 @@ import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-from c2dev import C2, variants  # noqa: E402
+from c2dev import C2, apply, variants  # noqa: E402
 
 
 def main():
@@ -18,12 +18,12 @@ def main():
     pt = c.table()
     stream = torch.cuda.current_stream(c.dev)
     vs = variants("0,1,1p,64")
-    outs = {name: c.outputs() for name, _, _ in vs}
-    times = {name: [] for name, _, _ in vs}
-    graphs = {True: c.graph(True), False: c.graph(False)}
+    outs = {name: c.outputs() for name, *_ in vs}
+    times = {name: [] for name, *_ in vs}
+    graphs = {o: c.graph(o) for o in (None, "p", "pi")}
     for rnd in range(12):
-        for name, uw, order in vs:
-            c.capi.check(c.lib, c.lib.ogs_set_option(b"unit_width", uw), "set_option")
+        for name, uw, order, lds, use_b in vs:
+            apply(c, uw, lds, use_b)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
             for _ in range(10):
@@ -33,7 +33,7 @@ def main():
             if rnd >= 2:
                 times[name].append(e0.elapsed_time(e1) / 10)
     ref = outs[vs[0][0]]
-    for name, _, _ in vs:
+    for name, *_ in vs:
         same = all(torch.equal(a, b) for a, b in zip(ref, outs[name]))
         ts = sorted(times[name])
         print(f"variant={name:>5} median={ts[len(ts)//2]*1e3:8.2f} us "

@@ -9,7 +9,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 KEYS = ("topo_desc", "node_base", "row_ptr", "edges", "node_flags", "pfx_base", "adv_off",
-        "adv_node", "adv_metrics", "adv_min_nh", "pfx_flags", "units", "slot_node")
+        "adv_node", "adv_metrics", "adv_min_nh", "pfx_flags", "units", "slot_node",
+        "slot_edges")
 
 
 class C2:
@@ -18,7 +19,11 @@ class C2:
         import openr_amd
         import openr_amd.capi as capi
         self.capi = capi
-        self.lib = capi.load()
+        self.lib = self.liba = capi.load()
+        # optional second build of the C-ABI (OGS_LIB_B) for same-process A/B
+        self.libb = None
+        if os.environ.get("OGS_LIB_B"):
+            self.libb = capi.load(os.environ["OGS_LIB_B"])
         br = openr_amd.decision.BatchRunner(True, False, brs)
         br.add_grid_batch(dict(n=10, metricSeed=0xC2000000, prefixSeed=0xC1), 0, topos, "1")
         h = self.h = br.host_arrays()
@@ -28,7 +33,8 @@ class C2:
         self.Sn, self.Sp, self.W = h["max_nodes"], h["max_prefixes"], h["nh_words"]
         self.flags = h["flags"]
 
-    def graph(self, order=True):
+    def graph(self, order="pi"):
+        image = order == "pi"
         h, t = self.h, self.t
         g = self.capi.Graph(h["num_topos"], self.Sn, h["max_edges"], h["max_degree"],
                             t["node_base"].data_ptr(), t["row_ptr"].data_ptr(),
@@ -37,6 +43,9 @@ class C2:
         if order:
             g.slot_node = t["slot_node"].data_ptr()
             g.slot_stride = h["slot_stride"]
+            if image and h["slot_degree"]:
+                g.slot_edges = t["slot_edges"].data_ptr()
+                g.slot_degree = h["slot_degree"]
         return g
 
     def table(self):
@@ -62,8 +71,24 @@ class C2:
 
 
 def variants(default):
-    """VARIANTS="1,1p,64": unit_width, suffix p = with slot order."""
+    """VARIANTS="1,1p,1pi,1p@81920,1p#b,64": unit_width, suffix p = with
+    slot order, pi = slot order + per-position edge image, @B = wave_wg_lds
+    option (minimum LDS bytes per workgroup), #b = run through the OGS_LIB_B
+    build."""
     out = []
     for x in os.environ.get("VARIANTS", default).split(","):
-        out.append((x, int(x.rstrip("p")), x.endswith("p")))
+        spec, _, which = x.partition("#")
+        base, _, lds = spec.partition("@")
+        uw = int(base.rstrip("pi"))
+        flags = base[len(str(uw)):]
+        # order: "p" = slot order only, "pi" = slot order + edge image
+        order = {"": None, "p": "p", "pi": "pi"}[flags]
+        out.append((x, uw, order, int(lds or 0), which == "b"))
     return out
+
+
+def apply(c, uw, lds, use_b=False):
+    c.lib = c.libb if use_b else c.liba
+    c.capi.check(c.lib, c.lib.ogs_set_option(b"unit_width", uw), "unit_width")
+    if lds or not use_b:
+        c.capi.check(c.lib, c.lib.ogs_set_option(b"wave_wg_lds", lds), "wave_wg_lds")

@@ -8,7 +8,7 @@ import sys
 import numpy as np
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-from c2dev import C2, variants  # noqa: E402
+from c2dev import C2, apply, variants  # noqa: E402
 
 
 def main():
@@ -16,14 +16,21 @@ def main():
     c = C2()
     pt = c.table()
     o = c.outputs()
-    for name, uw, order in variants("1,1p"):
-        c.capi.check(c.lib, c.lib.ogs_set_option(b"unit_width", uw), "opt")
+    for name, uw, order, lds, use_b in variants("1,1p"):
+        apply(c, uw, lds, use_b)
         g = c.graph(order)
         for _ in range(3):
             c.run(g, pt, o)
         torch.cuda.synchronize()
-        st = o[5].cpu().numpy().reshape(c.U, c.Sp)[:, :6].astype(np.float64)
-        names = ["stage", "spf", "routes", "rounds", "desc", "evals"]
+        raw = o[5].cpu().numpy().reshape(c.U, c.Sp)[:, :7].astype(np.int64)
+        st = raw[:, :5].astype(np.float64)
+        names = ["stage", "spf", "routes", "rounds", "desc"]
+        rt0 = raw[:, 5] - raw[:, 5].min()  # 100 MHz realtime, 10 ns ticks
+        rt1 = raw[:, 6] - raw[:, 5].min()
+        print(f"variant={name}: wave start (us after first) med={np.median(rt0)/100:.2f} "
+              f"p90={np.percentile(rt0, 90)/100:.2f} max={rt0.max()/100:.2f}; "
+              f"wave end med={np.median(rt1)/100:.2f} max={rt1.max()/100:.2f}; "
+              f"wave life med={np.median(rt1 - rt0)/100:.2f}")
         print(f"variant={name}: " + "  ".join(
             f"{n}: med={np.median(st[:, i]):.0f} p90={np.percentile(st[:, i], 90):.0f} "
             f"max={st[:, i].max():.0f}" for i, n in enumerate(names)))
