@@ -57,8 +57,155 @@ def cpu_baseline(units, reps=3):
                       f"refcpu buildRouteDb('1'), {threads} threads, ingestion excluded"}
 
 
+def fabric_names(pods, planes, ssw, rsw):
+    """Node names of topogen::fabric (RoutingBenchmarkUtils.cpp:421-473)."""
+    return ([f"1-{p}-{s}" for p in range(planes) for s in range(ssw)],
+            [f"2-{p}-{f}" for p in range(pods) for f in range(planes)],
+            [f"3-{p}-{r}" for p in range(pods) for r in range(rsw)])
+
+
+def run_c3(args, torch, dist, rank, world, local_rank):
+    """Config C3-full: fabric pods=32 planes=8 ssw/plane=36 rsw/pod=48
+    (N=2080, E=43,008), `--prefixes-per-node` prefixes per node, every node a
+    source. One step = this rank's share of the 2080 sources; one build = the
+    RouteDbs of all 2080 sources. Sources are grouped by next-hop bitset
+    width (SSW+RSW: 1 word, FSW: 3 words -> 4) so each launch writes masks
+    of its own width."""
+    import openr_amd
+    import openr_amd.capi as capi
+    openr_amd.require_gpu()
+    M = openr_amd.decision
+    lib = capi.load()
+    lib.ogs_set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    opts = dict(pods=32, planes=8, sswPerPlane=36, rswPerPod=48, full=True,
+                prefixesPerNode=args.prefixes_per_node)
+    ssw, fsw, rsw = fabric_names(32, 8, 36, 48)
+    groups = [ssw + rsw, fsw]
+    launches = []
+    N = len(ssw) + len(fsw) + len(rsw)
+    for names in groups:
+        mine = names[rank::world]
+        br = M.BatchRunner(True, False, False)
+        br.add_generated("fabric", opts, mine)
+        h = br.host_arrays()
+        up = lambda key, dt: torch.from_numpy(h[key].view(dt)).to(dev)  # noqa: E731
+        t = {k: up(k, dt) for k, dt in (
+            ("node_base", "int32"), ("row_ptr", "int32"), ("edges", "int64"),
+            ("node_flags", "uint8"), ("topo_desc", "int32"), ("pfx_base", "int32"),
+            ("adv_off", "int32"), ("adv_node", "int32"), ("adv_metrics", "int32"),
+            ("adv_min_nh", "int64"), ("pfx_flags", "uint8"), ("units", "int32"),
+            ("edge_src", "int32"))}
+        U = len(h["units"]) // 2
+        Sn, Sp, W = h["max_nodes"], h["max_prefixes"], h["nh_words"]
+        o = dict(dist=torch.empty(U * Sn, dtype=torch.int32, device=dev),
+                 nh=torch.empty(U * W * Sn, dtype=torch.int32, device=dev),
+                 meta=torch.empty(U * Sp, dtype=torch.int32, device=dev),
+                 metric=torch.empty(U * Sp, dtype=torch.int32, device=dev),
+                 mask=torch.empty(U * W * Sp, dtype=torch.int32, device=dev))
+        g = capi.Graph(h["num_topos"], Sn, h["max_edges"], h["max_degree"],
+                       t["node_base"].data_ptr(), t["row_ptr"].data_ptr(),
+                       t["edges"].data_ptr(), t["node_flags"].data_ptr(),
+                       t["topo_desc"].data_ptr())
+        g.edge_src = t["edge_src"].data_ptr()
+        pt = capi.PrefixTable(Sp, h["max_advertisements"], t["pfx_base"].data_ptr(),
+                              t["adv_off"].data_ptr(), t["adv_node"].data_ptr(),
+                              t["adv_metrics"].data_ptr(), t["adv_min_nh"].data_ptr(),
+                              t["pfx_flags"].data_ptr())
+        so = capi.SpfOut(o["dist"].data_ptr(), o["nh"].data_ptr(), o["meta"].data_ptr(),
+                         o["metric"].data_ptr(), o["mask"].data_ptr(), None)
+        # algorithmic bytes (SURVEY §8(d)), inputs shared by all N sources
+        E = h["max_edges"]
+        P = Sp
+        T = h["max_advertisements"]
+        inputs = 4 * (N + 1) + 8 * E + (N + 7) // 8 + 16 * T
+        rp = h["row_ptr"]
+        srcs = h["units"].reshape(-1, 2)[:, 1]
+        deg = rp[srcs + 1] - rp[srcs]
+        wl = (deg + 31) // 32
+        bpu = float((inputs / N + 4 * N + 4 * wl * N + P * (4 * wl + 8)).sum())
+        launches.append(dict(br=br, h=h, t=t, o=o, g=g, pt=pt, so=so, U=U, W=W,
+                             flags=h["flags"], bytes=bpu))
+    stream = torch.cuda.current_stream(dev)
+    sptr = ctypes.c_void_p(stream.cuda_stream)
+    evs = []
+
+    def step(timed=False):
+        for L in launches:
+            if timed:
+                e0 = torch.cuda.Event(enable_timing=True)
+                e1 = torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+            rc = lib.ogs_spf_routes(ctypes.byref(L["g"]), ctypes.byref(L["pt"]),
+                                    ctypes.c_void_p(L["t"]["units"].data_ptr()), L["U"],
+                                    L["flags"], L["W"], ctypes.byref(L["so"]), sptr)
+            if rc != 0:
+                capi.check(lib, rc, "ogs_spf_routes")
+            if timed:
+                e1.record(stream)
+                evs.append((L, e0, e1))
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(timed=True)
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t0
+    kern = {}
+    for L, e0, e1 in evs:
+        kern[id(L)] = kern.get(id(L), 0.0) + e0.elapsed_time(e1) / args.steps
+    kernel_ms = sum(kern.values())
+    units = sum(L["U"] for L in launches)
+    nbytes = sum(L["bytes"] for L in launches)
+    routes = sum(int(((L["o"]["meta"] & 1) != 0).sum().item()) for L in launches)
+    local = torch.tensor([units, routes], dtype=torch.int64, device=dev)
+    elapsed = torch.tensor([wall], dtype=torch.float64, device=dev)
+    if dist:
+        dist.all_reduce(local)
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    tmax = float(elapsed.item())
+    if rank == 0:
+        total_units = int(local[0].item())
+        achieved = nbytes / (kernel_ms * 1e-3) / 1e9
+        value = total_units * args.steps / tmax / N
+        line = {
+            "metric": "SPF+RouteDb builds/sec (whole node)",
+            "value": round(value, 4), "unit": "builds/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(tmax / args.steps * 1e3, 4),
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+            "dtype": "u32", "data": "synthetic",
+            "config": {"workload": f"C3-full: fabric all-sources (N=2080, E=43008, "
+                                   f"{args.prefixes_per_node} prefixes/node), one build = "
+                                   "RouteDb of every node",
+                       "sources": N, "prefixes": N * args.prefixes_per_node,
+                       "parallelism": f"shard-by-source x{world}"},
+            "route_dbs_per_s": round(total_units * args.steps / tmax, 1),
+            "routes_per_step": int(local[1].item()),
+            "gteps": round(43008 * total_units * args.steps / tmax / 1e9, 3),
+            "kernel_ms": round(kernel_ms, 4),
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "bytes_alg_per_step_rank0": round(nbytes, 1)},
+        }
+        print(json.dumps(line), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="c2", choices=["c2", "c3"])
+    ap.add_argument("--prefixes-per-node", type=int, default=100)
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
@@ -78,6 +225,8 @@ def main():
 
     import openr_amd
     import openr_amd.capi as capi
+    if args.config == "c3":
+        return run_c3(args, torch, dist, rank, world, local_rank)
     openr_amd.require_gpu()
     M = openr_amd.decision
     lib = capi.load()

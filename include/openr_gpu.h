@@ -128,6 +128,10 @@ typedef struct ogs_graph {
    * slot_degree is 4 or 8 (0 with slot_edges NULL). */
   const uint32_t* slot_edges;
   int32_t slot_degree;
+  /* Optional [E_total] topology-local row (owner node) of every directed
+   * edge: enables the edge-parallel multi-source path for topologies too
+   * large for the wave kernel (all-sources batches, C3/C4/C5). */
+  const uint32_t* edge_src;
 } ogs_graph;
 
 #define OGS_SLOT_EDGE_DOWN (1u << 9)
@@ -212,9 +216,12 @@ int ogs_stream_sync(void* stream);
  *   "unit_width": small-topology kernel choice: -1 automatic (default),
  *                 0 generic kernel only, 1 packed wave-per-unit kernel,
  *                 2 split-state kernel at its automatic unit width,
+ *                 3 multi-source edge-parallel kernel (needs edge_src),
  *                 64 / 128 / 256 split-state kernel at that unit width.
  *   "wave_wg_lds": minimum LDS bytes per wave-kernel workgroup (occupancy
- *                 probe; 0 default). */
+ *                 probe; 0 default).
+ *   "ms_group":   sources per workgroup of the multi-source kernel (0 auto,
+ *                 1, 2, 4). */
 int ogs_set_option(const char* name, int64_t value);
 
 /* Smallest supported next-hop bitset width (words) for a source degree. */

@@ -143,6 +143,24 @@ inline Lsdb grid(const GridOpts& o) {
   return db;
 }
 
+// Parity variants for any generator: mark a seeded fraction (per mille) of
+// adjacencies / nodes overloaded (drained).
+inline void applyOverloads(Lsdb& db, int adjPermille, int nodePermille,
+                           uint64_t seed) {
+  if (!adjPermille && !nodePermille) return;
+  uint64_t os = seed;
+  for (auto& d : db.adjDbs) {
+    for (auto& a : d.adjs) {
+      if (adjPermille && int(splitmix64(os) % 1000) < adjPermille) {
+        a.isOverloaded = true;
+      }
+    }
+    if (nodePermille && int(splitmix64(os) % 1000) < nodePermille) {
+      d.isOverloaded = true;
+    }
+  }
+}
+
 // -------------------------------------------------------------- fabric ----
 constexpr int kSswMarker = 1, kFswMarker = 2, kRswMarker = 3;
 

@@ -218,7 +218,7 @@ struct FlatTopology {
   uint64_t version{0};
   int slotStride{0};  // ogs_graph.slot_stride of dSlot (0: none)
   int slotDegree{0};  // ogs_graph.slot_degree of dSlotEdges (0: none)
-  DeviceBuffer dRow, dEdges, dFlags, dNodeBase, dSlot, dSlotEdges;
+  DeviceBuffer dRow, dEdges, dFlags, dNodeBase, dSlot, dSlotEdges, dEdgeSrc;
 };
 
 // ------------------------------------------------------------- LinkState --
@@ -457,6 +457,7 @@ struct HostBatch {
   std::vector<int64_t> advMinNh;
   std::vector<uint8_t> pfxFlags;
   std::vector<uint8_t> color;  // [N_total] BFS 2-colouring (slot_order.h)
+  std::vector<uint32_t> edgeSrc;  // [E_total] topology-local row of each edge
   int maxNodes{0}, maxEdges{0}, maxPrefixes{0}, maxDegree{0}, maxAdvs{0};
   uint64_t maxMetric{0};
   bool hasZeroMetric{false};

@@ -297,6 +297,14 @@ const FlatTopology& LinkState::flatOnDevice() const {
   m.dRow.upload(m.rowPtr.data(), m.rowPtr.size());
   m.dEdges.upload(m.edges.data(), m.edges.size());
   m.dFlags.upload(m.nodeFlags.data(), m.nodeFlags.size());
+  {
+    std::vector<uint32_t> esrc;
+    esrc.reserve(m.edges.size());
+    for (uint32_t v = 0; v + 1 < m.rowPtr.size(); ++v) {
+      esrc.insert(esrc.end(), m.rowPtr[v + 1] - m.rowPtr[v], v);
+    }
+    m.dEdgeSrc.upload(esrc.data(), esrc.size());
+  }
   m.slotStride = slotStrideFor(int(m.names.size()));
   if (m.slotStride) {
     std::vector<uint16_t> slots(m.slotStride);
@@ -382,6 +390,7 @@ const LinkState::SpfResult& LinkState::getSpfResult(const std::string& node,
   g.slot_stride = f.slotStride;
   g.slot_edges = f.slotDegree ? f.dSlotEdges.as<uint32_t>() : nullptr;
   g.slot_degree = f.slotDegree;
+  g.edge_src = f.dEdgeSrc.as<uint32_t>();
   ogs_spf_out out{};
   out.dist = sc.dist.get();
   out.nh = sc.nh.as<uint32_t>();

@@ -73,7 +73,10 @@ void HostBatch::append(const FlatTopology& t, const PrefixState& ps,
   const uint32_t e0 = rowPtr.back();
   const uint32_t n0 = nodeBase.back(), pb0 = pfxBase.back();
   const uint32_t ab0 = uint32_t(advNode.size());
-  for (uint32_t v = 0; v < N; ++v) rowPtr.push_back(e0 + t.rowPtr[v + 1]);
+  for (uint32_t v = 0; v < N; ++v) {
+    rowPtr.push_back(e0 + t.rowPtr[v + 1]);
+    edgeSrc.insert(edgeSrc.end(), t.rowPtr[v + 1] - t.rowPtr[v], v);
+  }
   edges.insert(edges.end(), t.edges.begin(), t.edges.end());
   nodeFlags.insert(nodeFlags.end(), t.nodeFlags.begin(), t.nodeFlags.end());
   nodeBase.push_back(nodeBase.back() + N);
@@ -373,6 +376,7 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(
   g.slot_stride = f.slotStride;
   g.slot_edges = f.slotDegree ? f.dSlotEdges.as<uint32_t>() : nullptr;
   g.slot_degree = f.slotDegree;
+  g.edge_src = f.dEdgeSrc.as<uint32_t>();
   ogs_prefix_table pt{};
   pt.max_prefixes = int32_t(P);
   pt.max_advertisements = int32_t(I.table.advEntry.size());

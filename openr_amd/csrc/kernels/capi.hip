@@ -10,6 +10,7 @@
 namespace ogs {
 extern int g_unitWidth;
 extern int g_waveWgLds;
+extern int g_msGroup;
 hipError_t launch_spf_routes(const ogs_graph& g, const ogs_prefix_table* pt,
                              const ogs_unit* units, int nUnits, uint32_t flags,
                              int W, const ogs_spf_out& out, hipStream_t stream,
@@ -101,11 +102,18 @@ int ogs_stream_sync(void* stream) {
 int ogs_set_option(const char* name, int64_t value) {
   if (!name) return fail(OGS_E_INVALID, "option name is NULL");
   if (std::strcmp(name, "unit_width") == 0) {
-    if (value != -1 && value != 0 && value != 1 && value != 2 && value != 64 &&
-        value != 128 && value != 256) {
-      return fail(OGS_E_INVALID, "unit_width must be -1, 0, 1, 2, 64, 128 or 256");
+    if (value != -1 && value != 0 && value != 1 && value != 2 && value != 3 &&
+        value != 64 && value != 128 && value != 256) {
+      return fail(OGS_E_INVALID, "unit_width must be -1, 0, 1, 2, 3, 64, 128 or 256");
     }
     ogs::g_unitWidth = int(value);
+    return OGS_OK;
+  }
+  if (std::strcmp(name, "ms_group") == 0) {
+    if (value != 0 && value != 1 && value != 2 && value != 4) {
+      return fail(OGS_E_INVALID, "ms_group must be 0, 1, 2 or 4");
+    }
+    ogs::g_msGroup = int(value);
     return OGS_OK;
   }
   if (std::strcmp(name, "wave_wg_lds") == 0) {

@@ -204,9 +204,13 @@ bool try_wave(const ogs_graph& g, const ogs_prefix_table& pt, int hasPrefixes,
               const ogs_spf_out& out, uint32_t maxA, hipStream_t stream,
               hipError_t* err);
 
+bool try_ms(const ogs_graph& g, const ogs_prefix_table& pt, int hasPrefixes,
+            const ogs_unit* units, int nUnits, uint32_t flags, int W,
+            const ogs_spf_out& out, hipStream_t stream, hipError_t* err);
+
 // unit_width option / OGS_UNIT_WIDTH env: -1 automatic, 0 generic kernel
-// only, 1 wave kernel, 2 small kernel (automatic width), 64/128/256 small
-// kernel at that unit width.
+// only, 1 wave kernel, 2 small kernel (automatic width), 3 multi-source
+// edge-parallel kernel, 64/128/256 small kernel at that unit width.
 int g_unitWidth = [] {
   const char* e = getenv("OGS_UNIT_WIDTH");
   return e ? atoi(e) : -1;
@@ -229,7 +233,14 @@ hipError_t launch_spf_routes(const ogs_graph& g, const ogs_prefix_table* pt,
       return err;
     }
   }
-  if (W == 1 && uw != 0) {
+  // large shared topologies: multi-source edge-parallel kernel
+  if ((uw == -1 && g.max_nodes > 256) || uw == 3) {
+    hipError_t err = hipSuccess;
+    if (try_ms(g, p, hasPrefixes, units, nUnits, flags, W, out, stream, &err)) {
+      return err;
+    }
+  }
+  if (W == 1 && uw != 0 && uw != 3) {
     hipError_t err = hipSuccess;
     const int width = uw >= 64 ? uw : 0;
     const bool done = (flags & OGS_F_WIDE_METRIC)

@@ -298,7 +298,11 @@ topogen::Lsdb genLsdb(const std::string& kind, const py::dict& d) {
     o.full = get<bool>(d, "full", true);
     o.prefixesPerNode = get<int>(d, "prefixesPerNode", 1);
     o.prefixSeed = get<uint64_t>(d, "prefixSeed", 0xC3);
-    return topogen::fabric(o);
+    auto db = topogen::fabric(o);
+    topogen::applyOverloads(db, get<int>(d, "adjOverloadPermille", 0),
+                            get<int>(d, "nodeOverloadPermille", 0),
+                            get<uint64_t>(d, "overloadSeed", 0x0F));
+    return db;
   }
   if (kind == "wan") {
     topogen::WanOpts o;
@@ -306,7 +310,11 @@ topogen::Lsdb genLsdb(const std::string& kind, const py::dict& d) {
     o.k = get<int>(d, "k", 3);
     o.seed = get<uint64_t>(d, "seed", 0xC4);
     o.prefixesPerNode = get<int>(d, "prefixesPerNode", 1);
-    return topogen::wan(o);
+    auto db = topogen::wan(o);
+    topogen::applyOverloads(db, get<int>(d, "adjOverloadPermille", 0),
+                            get<int>(d, "nodeOverloadPermille", 0),
+                            get<uint64_t>(d, "overloadSeed", 0x0F));
+    return db;
   }
   throw std::invalid_argument("unknown generator " + kind);
 }
@@ -345,6 +353,7 @@ class BatchRunner {
     dDesc_.upload(hb_.topoDesc.data(), hb_.topoDesc.size());
     dRow_.upload(hb_.rowPtr.data(), hb_.rowPtr.size());
     dEdges_.upload(hb_.edges.data(), hb_.edges.size());
+    dEdgeSrc_.upload(hb_.edgeSrc.data(), hb_.edgeSrc.size());
     dFlags_.upload(hb_.nodeFlags.data(), hb_.nodeFlags.size());
     dPfxBase_.upload(hb_.pfxBase.data(), hb_.pfxBase.size());
     dAdvOff_.upload(hb_.advOff.data(), hb_.advOff.size());
@@ -460,6 +469,7 @@ class BatchRunner {
     g.slot_stride = slotStride_;
     g.slot_edges = slotDegree_ ? dSlotEdges_.as<uint32_t>() : nullptr;
     g.slot_degree = slotDegree_;
+    g.edge_src = dEdgeSrc_.as<uint32_t>();
     return g;
   }
   ogs_prefix_table table() const {
@@ -483,7 +493,7 @@ class BatchRunner {
   bool enableV4_, sr_, brs_;
   bool slotOrder_{true}, slotEdgeImage_{true};
   int slotStride_{0}, slotDegree_{0};
-  DeviceBuffer dSlot_, dSlotEdges_;
+  DeviceBuffer dSlot_, dSlotEdges_, dEdgeSrc_;
   std::vector<std::unique_ptr<Topo>> topos_;
   HostBatch hb_;
   std::vector<ogs_unit> units_;
@@ -771,6 +781,7 @@ PYBIND11_MODULE(_decision, m) {
         d["topo_desc"] = npcopy(h.topoDesc);
         d["row_ptr"] = npcopy(h.rowPtr);
         d["edges"] = npcopy(h.edges);
+        d["edge_src"] = npcopy(h.edgeSrc);
         d["node_flags"] = npcopy(h.nodeFlags);
         d["pfx_base"] = npcopy(h.pfxBase);
         d["adv_off"] = npcopy(h.advOff);

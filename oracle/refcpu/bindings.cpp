@@ -305,7 +305,11 @@ topogen::Lsdb genLsdb(const std::string& kind, const py::dict& d) {
     o.full = get<bool>(d, "full", true);
     o.prefixesPerNode = get<int>(d, "prefixesPerNode", 1);
     o.prefixSeed = get<uint64_t>(d, "prefixSeed", 0xC3);
-    return topogen::fabric(o);
+    auto db = topogen::fabric(o);
+    topogen::applyOverloads(db, get<int>(d, "adjOverloadPermille", 0),
+                            get<int>(d, "nodeOverloadPermille", 0),
+                            get<uint64_t>(d, "overloadSeed", 0x0F));
+    return db;
   }
   if (kind == "wan") {
     topogen::WanOpts o;
@@ -313,7 +317,11 @@ topogen::Lsdb genLsdb(const std::string& kind, const py::dict& d) {
     o.k = get<int>(d, "k", 3);
     o.seed = get<uint64_t>(d, "seed", 0xC4);
     o.prefixesPerNode = get<int>(d, "prefixesPerNode", 1);
-    return topogen::wan(o);
+    auto db = topogen::wan(o);
+    topogen::applyOverloads(db, get<int>(d, "adjOverloadPermille", 0),
+                            get<int>(d, "nodeOverloadPermille", 0),
+                            get<uint64_t>(d, "overloadSeed", 0x0F));
+    return db;
   }
   throw std::invalid_argument("unknown generator " + kind);
 }
