@@ -13,12 +13,13 @@ EXT := $(shell python3 -c "import sysconfig;print(sysconfig.get_config_var('EXT_
 LIB := openr_amd/lib/libopenr_gpu.so
 MOD := openr_amd/_decision$(EXT)
 KERNELS := $(wildcard openr_amd/csrc/kernels/*.hip)
+KERNEL_H := $(wildcard openr_amd/csrc/kernels/*.h)
 HOST := $(wildcard openr_amd/csrc/host/*.cpp)
 HOST_H := $(wildcard openr_amd/csrc/host/*.h) include/openr_gpu.h openr_amd/csrc/gen/topogen.h
 
 all: $(LIB) $(MOD) oracle
 
-$(LIB): $(KERNELS) include/openr_gpu.h
+$(LIB): $(KERNELS) $(KERNEL_H) include/openr_gpu.h
 	@mkdir -p openr_amd/lib
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -shared -Iinclude $(KERNELS) -o $@
 
@@ -35,7 +36,7 @@ oracle:
 # (tools/stamps.py); never loaded by the product
 STAMPS := openr_amd/lib/libopenr_gpu_stamps.so
 stamps: $(STAMPS)
-$(STAMPS): $(KERNELS) include/openr_gpu.h
+$(STAMPS): $(KERNELS) $(KERNEL_H) include/openr_gpu.h
 	@mkdir -p openr_amd/lib
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -shared -DOGS_STAMPS -Iinclude $(KERNELS) -o $@
 

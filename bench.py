@@ -64,27 +64,16 @@ def fabric_names(pods, planes, ssw, rsw):
             [f"3-{p}-{r}" for p in range(pods) for r in range(rsw)])
 
 
-def run_c3(args, torch, dist, rank, world, local_rank):
-    """Config C3-full: fabric pods=32 planes=8 ssw/plane=36 rsw/pod=48
-    (N=2080, E=43,008), `--prefixes-per-node` prefixes per node, every node a
-    source. One step = this rank's share of the 2080 sources; one build = the
-    RouteDbs of all 2080 sources. Sources are grouped by next-hop bitset
-    width (SSW+RSW: 1 word, FSW: 3 words -> 4) so each launch writes masks
-    of its own width."""
-    import openr_amd
-    import openr_amd.capi as capi
-    openr_amd.require_gpu()
-    M = openr_amd.decision
-    lib = capi.load()
-    lib.ogs_set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+def c3_launches(torch, M, capi, dev, rank, world, ppn, with_sel=False):
+    """Host build + device upload of this rank's C3 launches: sources grouped
+    by next-hop bitset width (SSW+RSW: 1 word, FSW: 3 words -> 4) so each
+    launch writes masks of its own width."""
     opts = dict(pods=32, planes=8, sswPerPlane=36, rswPerPod=48, full=True,
-                prefixesPerNode=args.prefixes_per_node)
+                prefixesPerNode=ppn)
     ssw, fsw, rsw = fabric_names(32, 8, 36, 48)
-    groups = [ssw + rsw, fsw]
-    launches = []
     N = len(ssw) + len(fsw) + len(rsw)
-    for names in groups:
+    launches = []
+    for names in (ssw + rsw, fsw):
         mine = names[rank::world]
         br = M.BatchRunner(True, False, False)
         br.add_generated("fabric", opts, mine)
@@ -103,6 +92,8 @@ def run_c3(args, torch, dist, rank, world, local_rank):
                  meta=torch.empty(U * Sp, dtype=torch.int32, device=dev),
                  metric=torch.empty(U * Sp, dtype=torch.int32, device=dev),
                  mask=torch.empty(U * W * Sp, dtype=torch.int32, device=dev))
+        if with_sel:
+            o["sel"] = torch.empty(U * Sp, dtype=torch.int32, device=dev)
         g = capi.Graph(h["num_topos"], Sn, h["max_edges"], h["max_degree"],
                        t["node_base"].data_ptr(), t["row_ptr"].data_ptr(),
                        t["edges"].data_ptr(), t["node_flags"].data_ptr(),
@@ -113,7 +104,8 @@ def run_c3(args, torch, dist, rank, world, local_rank):
                               t["adv_metrics"].data_ptr(), t["adv_min_nh"].data_ptr(),
                               t["pfx_flags"].data_ptr())
         so = capi.SpfOut(o["dist"].data_ptr(), o["nh"].data_ptr(), o["meta"].data_ptr(),
-                         o["metric"].data_ptr(), o["mask"].data_ptr(), None)
+                         o["metric"].data_ptr(), o["mask"].data_ptr(),
+                         o["sel"].data_ptr() if with_sel else None)
         # algorithmic bytes, inputs shared by all N sources
         E = h["max_edges"]
         P = Sp
@@ -125,25 +117,43 @@ def run_c3(args, torch, dist, rank, world, local_rank):
         wl = (deg + 31) // 32
         bpu = float((inputs / N + 4 * N + 4 * wl * N + P * (4 * wl + 8)).sum())
         launches.append(dict(br=br, h=h, t=t, o=o, g=g, pt=pt, so=so, U=U, W=W,
-                             flags=h["flags"], bytes=bpu))
-    stream = torch.cuda.current_stream(dev)
-    sptr = ctypes.c_void_p(stream.cuda_stream)
-    evs = []
+                             flags=h["flags"], bytes=bpu, names=mine))
+    return launches, N
 
-    def step(timed=False):
-        for L in launches:
-            if timed:
-                e0 = torch.cuda.Event(enable_timing=True)
-                e1 = torch.cuda.Event(enable_timing=True)
-                e0.record(stream)
+
+def run_c3(args, torch, dist, rank, world, local_rank):
+    """Config C3-full: fabric pods=32 planes=8 ssw/plane=36 rsw/pod=48
+    (N=2080, E=43,008), `--prefixes-per-node` prefixes per node, every node a
+    source. One step = this rank's share of the 2080 sources; one build = the
+    RouteDbs of all 2080 sources."""
+    import openr_amd
+    import openr_amd.capi as capi
+    openr_amd.require_gpu()
+    M = openr_amd.decision
+    lib = capi.load()
+    lib.ogs_set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    launches, N = c3_launches(torch, M, capi, dev, rank, world, args.prefixes_per_node)
+    # the width groups are independent: with --c3-streams 2 the second group
+    # runs on its own HIP stream, overlapped with the first
+    main = torch.cuda.current_stream(dev)
+    side = torch.cuda.Stream(dev) if args.c3_streams > 1 else main
+    streams = [main, side] + [main] * max(0, len(launches) - 2)
+
+    def step():
+        fork = torch.cuda.Event()
+        fork.record(main)
+        side.wait_event(fork)
+        for L, st in zip(launches, streams):
             rc = lib.ogs_spf_routes(ctypes.byref(L["g"]), ctypes.byref(L["pt"]),
                                     ctypes.c_void_p(L["t"]["units"].data_ptr()), L["U"],
-                                    L["flags"], L["W"], ctypes.byref(L["so"]), sptr)
+                                    L["flags"], L["W"], ctypes.byref(L["so"]),
+                                    ctypes.c_void_p(st.cuda_stream))
             if rc != 0:
                 capi.check(lib, rc, "ogs_spf_routes")
-            if timed:
-                e1.record(stream)
-                evs.append((L, e0, e1))
+        join = torch.cuda.Event()
+        join.record(side)
+        main.wait_event(join)
 
     for _ in range(args.warmup):
         step()
@@ -151,18 +161,20 @@ def run_c3(args, torch, dist, rank, world, local_rank):
     if dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
+    e0.record(main)
     for _ in range(args.steps):
-        step(timed=True)
+        step()
+    e1.record(main)
     torch.cuda.synchronize(dev)
     if dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t0
-    kern = {}
-    for L, e0, e1 in evs:
-        kern[id(L)] = kern.get(id(L), 0.0) + e0.elapsed_time(e1) / args.steps
-    kernel_ms = sum(kern.values())
+    # device time of one whole build on this rank (all launches of a step)
+    kernel_ms = e0.elapsed_time(e1) / args.steps
     units = sum(L["U"] for L in launches)
     nbytes = sum(L["bytes"] for L in launches)
     routes = sum(int(((L["o"]["meta"] & 1) != 0).sum().item()) for L in launches)
@@ -206,11 +218,15 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="c2", choices=["c2", "c3"])
     ap.add_argument("--prefixes-per-node", type=int, default=100)
+    ap.add_argument("--c3-streams", type=int, default=2, choices=[1, 2],
+                    help="C3: HIP streams for the two source groups")
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--topos", type=int, default=TOPOS_PER_GPU)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--opt", action="append", default=[],
+                    help="engine option name=value (ogs_set_option), for A/B runs")
     args = ap.parse_args()
 
     import torch
@@ -225,6 +241,10 @@ def main():
 
     import openr_amd
     import openr_amd.capi as capi
+    for o in args.opt:
+        name, val = o.split("=", 1)
+        lib0 = capi.load()
+        capi.check(lib0, lib0.ogs_set_option(name.encode(), int(val)), name)
     if args.config == "c3":
         return run_c3(args, torch, dist, rank, world, local_rank)
     openr_amd.require_gpu()

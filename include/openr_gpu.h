@@ -221,7 +221,17 @@ int ogs_stream_sync(void* stream);
  *   "wave_wg_lds": minimum LDS bytes per wave-kernel workgroup (occupancy
  *                 probe; 0 default).
  *   "ms_group":   sources per workgroup of the multi-source kernel (0 auto,
- *                 1, 2, 4). */
+ *                 1, 2, 4).
+ *   "route_stream": RouteDb form for large shared topologies: 2 (default)
+ *                 one launch per unit set, SPF then the unit's RouteDb write
+ *                 stream from LDS; 1 an SPF launch then a route-stream launch
+ *                 (dist/next-hop sets through HBM); 0 the fused multi-source
+ *                 kernel. Scratch (prefix keys, dist/next-hop sets when
+ *                 out->dist / out->nh are NULL) comes from a grow-only
+ *                 per-device workspace.
+ *   "spf_frontier": 1 (default) large topologies (edge_src given) solve
+ *                 SPF with the frontier kernel (one workgroup per unit,
+ *                 only changed rows pushed); 0 the multi-source edge sweep. */
 int ogs_set_option(const char* name, int64_t value);
 
 /* Smallest supported next-hop bitset width (words) for a source degree. */

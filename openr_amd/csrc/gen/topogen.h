@@ -45,6 +45,8 @@ struct Prefix {  // one advertisement (node, prefix) with PrefixMetrics
   std::string node;
   std::string prefix;
   int32_t path_preference{0}, source_preference{0}, distance{0};
+  int32_t drain_metric{0};
+  int64_t minNexthop{-1};  // < 0: unset
 };
 
 struct Lsdb {
@@ -157,6 +159,63 @@ inline void applyOverloads(Lsdb& db, int adjPermille, int nodePermille,
     }
     if (nodePermille && int(splitmix64(os) % 1000) < nodePermille) {
       d.isOverloaded = true;
+    }
+  }
+}
+
+// Prefix-table variants for any generator (parity cases for the RouteDb
+// paths beyond one plain advertisement per prefix): per mille of the
+// generated prefixes become IPv4 (v4 gate, SpfSolver.cpp:169-176), anycast
+// (1-3 extra advertisers, sometimes a node without adjacency DB;
+// PrefixMetrics path/source preference in {100, 200}, distance U[0, 10]),
+// carry minNexthop in [0, 3] (SpfSolver.cpp:496-509, 612-619), or are
+// drained (drain_metric = 1, LsdbUtil.cpp:760-823).
+struct PrefixMix {
+  int v4Permille{0}, anycastPermille{0}, minNhPermille{0}, drainPermille{0};
+  uint64_t seed{0x3F};
+};
+
+inline void applyPrefixMix(Lsdb& db, const PrefixMix& m) {
+  if (!m.v4Permille && !m.anycastPermille && !m.minNhPermille &&
+      !m.drainPermille) {
+    return;
+  }
+  uint64_t s = m.seed;
+  auto hit = [&](int permille) {
+    return permille && int(splitmix64(s) % 1000) < permille;
+  };
+  auto metrics = [&](Prefix& p) {
+    p.path_preference = (splitmix64(s) & 1) ? 200 : 100;
+    p.source_preference = (splitmix64(s) & 1) ? 200 : 100;
+    p.distance = int32_t(splitmix64(s) % 11);
+    if (hit(m.drainPermille)) p.drain_metric = 1;
+    if (hit(m.minNhPermille)) p.minNexthop = int64_t(splitmix64(s) % 4);
+  };
+  const size_t n0 = db.prefixes.size();
+  const size_t nodes = db.adjDbs.size();
+  for (size_t i = 0; i < n0; ++i) {
+    if (hit(m.v4Permille)) {
+      const uint64_t a = splitmix64(s);
+      db.prefixes[i].prefix = "10." + std::to_string((a >> 16) & 0xff) + "." +
+          std::to_string((a >> 8) & 0xff) + "." + std::to_string(a & 0xff) +
+          "/32";
+    }
+    if (hit(m.drainPermille)) db.prefixes[i].drain_metric = 1;
+    if (hit(m.minNhPermille)) {
+      db.prefixes[i].minNexthop = int64_t(splitmix64(s) % 4);
+    }
+    if (hit(m.anycastPermille) && nodes > 1) {
+      metrics(db.prefixes[i]);
+      const int extra = 1 + int(splitmix64(s) % 3);
+      for (int k = 0; k < extra; ++k) {
+        Prefix q;
+        q.prefix = db.prefixes[i].prefix;
+        q.node = (splitmix64(s) % 16 == 0)
+            ? "ghost-" + std::to_string(splitmix64(s) % 4)
+            : db.adjDbs[splitmix64(s) % nodes].thisNodeName;
+        metrics(q);
+        db.prefixes.push_back(q);
+      }
     }
   }
 }

@@ -11,6 +11,8 @@ namespace ogs {
 extern int g_unitWidth;
 extern int g_waveWgLds;
 extern int g_msGroup;
+extern int g_routeStream;
+extern int g_spfFrontier;
 hipError_t launch_spf_routes(const ogs_graph& g, const ogs_prefix_table* pt,
                              const ogs_unit* units, int nUnits, uint32_t flags,
                              int W, const ogs_spf_out& out, hipStream_t stream,
@@ -114,6 +116,20 @@ int ogs_set_option(const char* name, int64_t value) {
       return fail(OGS_E_INVALID, "ms_group must be 0, 1, 2 or 4");
     }
     ogs::g_msGroup = int(value);
+    return OGS_OK;
+  }
+  if (std::strcmp(name, "route_stream") == 0) {
+    if (value != 0 && value != 1 && value != 2) {
+      return fail(OGS_E_INVALID, "route_stream must be 0, 1 or 2");
+    }
+    ogs::g_routeStream = int(value);
+    return OGS_OK;
+  }
+  if (std::strcmp(name, "spf_frontier") == 0) {
+    if (value != 0 && value != 1) {
+      return fail(OGS_E_INVALID, "spf_frontier must be 0 or 1");
+    }
+    ogs::g_spfFrontier = int(value);
     return OGS_OK;
   }
   if (std::strcmp(name, "wave_wg_lds") == 0) {

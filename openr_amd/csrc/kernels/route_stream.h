@@ -1,0 +1,135 @@
+// route_stream.h — the RouteDb write stream of one unit (device code),
+// shared by route_stream_kernel (SPF state read back from HBM) and the fused
+// frontier SPF + RouteDb kernel (SPF state still in LDS).
+//
+// A single-advertiser prefix's route depends only on its advertiser v
+// (SpfSolver::createRouteForPrefix, SpfSolver.cpp:160-311, on a one-entry
+// segment; selectBestRoutes 455-551 and addBestPaths 595-639 degenerate):
+//   unreachable v         -> reason UNREACHABLE          (217-223)
+//   v == source           -> SELECTED, reason SELF        (253-258)
+//   no next hop           -> reason NO_NEXTHOP            (605-607)
+//   else                  -> VALID, metric dist(v), mask NH(v)
+// plus DRAINED when v is hard-drained or has a metric increment
+// (isNodeDrained, 543-551) and LOCAL when v is the source. So the stream
+// keeps one record per NODE and gathers it per prefix; every other prefix
+// (several advertisements, minNexthop, advertiser without adjacency DB) runs
+// the full route_one (route_core.h). The per-prefix choice is precomputed
+// once per call into a u32 key (pfx_key_kernel).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "openr_gpu.h"
+#include "route_core.h"
+#include "spf_core.h"
+
+namespace ogs {
+
+constexpr uint32_t kKeySlow = 0x80000000u;  // run route_one
+constexpr uint32_t kKeyV4 = 0x40000000u;    // prefix is IPv4 (run-time gate)
+constexpr uint32_t kKeyNode = OGS_EDGE_DST_MASK;
+
+// Record flags of a single-advertiser prefix advertised by v.
+__device__ __forceinline__ uint32_t node_route_meta(uint32_t v, uint32_t s,
+                                                    bool reachable,
+                                                    uint32_t nhCount,
+                                                    uint8_t nflag) {
+  uint32_t meta = (v == s) ? OGS_ROUTE_LOCAL : 0u;
+  if (!reachable) return meta | (OGS_REASON_UNREACHABLE << OGS_ROUTE_REASON_SHIFT);
+  meta |= OGS_ROUTE_SELECTED;
+  if (nflag & (OGS_NODE_OVERLOADED | OGS_NODE_METRICINC)) meta |= OGS_ROUTE_DRAINED;
+  if (v == s) return meta | (OGS_REASON_SELF << OGS_ROUTE_REASON_SHIFT);
+  return meta | (nhCount ? OGS_ROUTE_VALID
+                         : (OGS_REASON_NO_NEXTHOP << OGS_ROUTE_REASON_SHIFT));
+}
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void nt_store4(uint32_t* p, uint32_t a, uint32_t b,
+                                          uint32_t c, uint32_t d) {
+  u32x4 v = {a, b, c, d};
+  __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
+}
+
+template <int W>
+struct Rec {
+  uint32_t meta, metric, mask[W], sel;
+};
+
+// Streams unit u's P route records (rows of stride Sp). rec(v, r) fills
+// meta / metric / mask of node v's record; sv is the unit's SPF state for
+// route_one. Four consecutive prefixes per lane: one 16-B key load and one
+// 16-B non-temporal store per output array.
+template <int W, typename View, typename RecFn>
+__device__ __forceinline__ void stream_routes(
+    const ogs_prefix_table& pt, const uint32_t* __restrict__ tkey, uint32_t p0,
+    uint32_t P, uint32_t Sp, size_t u, uint32_t s,
+    const uint8_t* __restrict__ nflags, const View& sv, const RouteCfg& cfg,
+    const ogs_spf_out& out, RecFn rec) {
+  constexpr uint32_t kInf = 0xFFFFFFFFu;
+  const int tid = threadIdx.x;
+  const bool v4Gated = !cfg.enableV4 && !cfg.v4OverV6;
+  uint32_t* oMeta = out.meta ? out.meta + u * Sp : nullptr;
+  uint32_t* oMetric =
+      out.metric ? static_cast<uint32_t*>(out.metric) + u * Sp : nullptr;
+  uint32_t* oSel = out.sel ? out.sel + u * Sp : nullptr;
+  uint32_t* oMask = out.mask ? out.mask + u * W * Sp : nullptr;
+
+  auto one = [&](uint32_t p, uint32_t k, Rec<W>& r) {
+    if (!(k & kKeySlow)) {
+      if ((k & kKeyV4) && v4Gated) {
+        r.meta = OGS_REASON_V4_DISABLED << OGS_ROUTE_REASON_SHIFT;
+        r.metric = kInf;
+        r.sel = 0u;
+#pragma unroll
+        for (int w = 0; w < W; ++w) r.mask[w] = 0u;
+        return;
+      }
+      rec(k & kKeyNode, r);
+      r.sel = (r.meta & OGS_ROUTE_SELECTED) ? 1u : 0u;
+    } else {
+      route_one<uint32_t, W>(pt, p0 + p, s, nflags, sv, cfg, r.meta, r.metric,
+                             r.mask, r.sel);
+    }
+  };
+
+  // 16-B accesses need 16-B aligned rows: Sp % 4 == 0 and aligned bases
+  const uintptr_t align = reinterpret_cast<uintptr_t>(out.meta) |
+      reinterpret_cast<uintptr_t>(out.metric) |
+      reinterpret_cast<uintptr_t>(out.sel) | reinterpret_cast<uintptr_t>(out.mask);
+  const bool vec = (Sp & 3u) == 0u && (align & 15u) == 0u;
+  const uint32_t Pv = vec ? (P & ~3u) : 0u;
+  for (uint32_t q = uint32_t(tid) * 4u; q < Pv; q += kBlock * 4u) {
+    const uint4 k4 = *reinterpret_cast<const uint4*>(tkey + q);
+    Rec<W> r0, r1, r2, r3;
+    one(q + 0, k4.x, r0);
+    one(q + 1, k4.y, r1);
+    one(q + 2, k4.z, r2);
+    one(q + 3, k4.w, r3);
+    if (oMeta) nt_store4(oMeta + q, r0.meta, r1.meta, r2.meta, r3.meta);
+    if (oMetric) nt_store4(oMetric + q, r0.metric, r1.metric, r2.metric, r3.metric);
+    if (oSel) nt_store4(oSel + q, r0.sel, r1.sel, r2.sel, r3.sel);
+    if (oMask) {
+#pragma unroll
+      for (int w = 0; w < W; ++w) {
+        nt_store4(oMask + size_t(w) * Sp + q, r0.mask[w], r1.mask[w], r2.mask[w],
+                  r3.mask[w]);
+      }
+    }
+  }
+  for (uint32_t p = Pv + tid; p < P; p += kBlock) {  // tail / unaligned rows
+    Rec<W> r;
+    one(p, tkey[p], r);
+    if (oMeta) oMeta[p] = r.meta;
+    if (oMetric) oMetric[p] = r.metric;
+    if (oSel) oSel[p] = r.sel;
+    if (oMask) {
+#pragma unroll
+      for (int w = 0; w < W; ++w) oMask[size_t(w) * Sp + p] = r.mask[w];
+    }
+  }
+}
+
+}  // namespace ogs

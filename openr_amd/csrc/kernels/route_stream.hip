@@ -1,0 +1,268 @@
+// route_stream.hip — RouteDb streaming for large shared topologies (C3
+// fabric all-sources: 2,080 sources x 208,000 prefixes = 432 M routes, 5.7 GB
+// of route records per whole-node build; C4/C5 WAN batches).
+//
+// The route phase of an all-sources build is a pure HBM write stream: every
+// (source, prefix) pair gets a compact record (flags|best, metric, link-slot
+// mask). Doing it inside the SPF workgroup (spf_route_ms.hip's fused form)
+// leaves it latency-bound: a few resident waves per CU, each walking the
+// prefix table through a chain of dependent loads. Here it is its own
+// launch, after the SPF launch has left dist / next-hop sets in HBM:
+//
+//  1. pfx_key_kernel — once per call, one thread per (topology, prefix):
+//     folds the advertiser segment into one u32 key:
+//       bits 0..20  the single advertiser's node id,
+//       bit  30     prefix is IPv4 (the v4 gate is applied at run time),
+//       bit  31     SLOW: several advertisements, minNexthop set, or an
+//                   advertiser without adjacency DB -> full route_one.
+//  2. route_stream_kernel — one workgroup per unit: turns the unit's SPF
+//     state into one record per NODE in LDS (a single-advertiser prefix's
+//     route depends only on its advertiser: SpfSolver.cpp:160-311 with a
+//     one-entry segment), then streams the unit's prefix rows: per lane four
+//     consecutive prefixes = one 16-B key load, LDS gathers, and one 16-B
+//     non-temporal store per output array. SLOW prefixes run route_one
+//     (route_core.h) against the unit's SPF state in HBM/L2.
+// Results are identical to the fused kernels' (same route_core semantics;
+// tests/test_gpu_parity.py compares both against the oracle).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <map>
+#include <mutex>
+#include <utility>
+
+#include "openr_gpu.h"
+#include "route_core.h"
+#include "route_stream.h"
+#include "spf_core.h"
+
+namespace ogs {
+
+__global__ __launch_bounds__(kBlock) void pfx_key_kernel(
+    ogs_prefix_table pt, int numTopos, uint32_t* __restrict__ key) {
+  const uint32_t Sp = uint32_t(pt.max_prefixes);
+  const uint32_t t = blockIdx.y;
+  const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
+  if (t >= uint32_t(numTopos) || p >= Sp) return;
+  const uint32_t p0 = pt.pfx_base[t];
+  const uint32_t P = pt.pfx_base[t + 1] - p0;
+  uint32_t k = kKeySlow;
+  if (p < P) {
+    const uint32_t gp = p0 + p;
+    const uint32_t a0 = pt.adv_off[gp], a1 = pt.adv_off[gp + 1];
+    const uint8_t f = pt.pfx_flags[gp];
+    if (a1 - a0 == 1 && !(f & OGS_PFX_HAS_MIN_NH)) {
+      const uint32_t n = pt.adv_node[a0];
+      if (n != OGS_NODE_NONE) k = n | ((f & OGS_PFX_V4) ? kKeyV4 : 0u);
+    }
+  }
+  key[size_t(t) * Sp + p] = k;
+}
+
+// Unit's SPF state as left in HBM by the SPF launch (ogs_spf_out layout).
+template <int W>
+struct HbmView {
+  const uint32_t* d;  // dist + u*Sn
+  const uint32_t* n;  // nh + u*W*Sn
+  uint32_t Sn;
+  __device__ __forceinline__ uint32_t dist(uint32_t v) const { return d[v]; }
+  __device__ __forceinline__ uint32_t nh(uint32_t v, int w) const {
+    return n[size_t(w) * Sn + v];
+  }
+};
+
+template <int W>
+__global__ __launch_bounds__(kBlock) void route_stream_kernel(
+    ogs_graph g, ogs_prefix_table pt, const uint32_t* __restrict__ key,
+    const ogs_unit* __restrict__ units, uint32_t flags,
+    const uint32_t* __restrict__ sDist, const uint32_t* __restrict__ sNh,
+    ogs_spf_out out) {
+  constexpr uint32_t kInf = 0xFFFFFFFFu;
+  const int tid = threadIdx.x;
+  const uint32_t u = blockIdx.x;
+  const ogs_unit unit = units[u];
+  const uint32_t t = unit.topo, s = unit.src;
+  const uint32_t nb = g.node_base[t];
+  const uint32_t N = g.node_base[t + 1] - nb;
+  const uint32_t Sn = uint32_t(g.max_nodes);
+  const uint32_t Sp = uint32_t(pt.max_prefixes);
+  const uint8_t* __restrict__ nflags = g.node_flags + nb;
+  const HbmView<W> sv{sDist + size_t(u) * Sn, sNh + size_t(u) * W * Sn, Sn};
+  const RouteCfg cfg{(flags & OGS_F_ENABLE_V4) != 0,
+                     (flags & OGS_F_V4_OVER_V6) != 0,
+                     (flags & OGS_F_BEST_ROUTE_SELECTION) != 0};
+
+  // per-node records in LDS
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint32_t* rMeta = reinterpret_cast<uint32_t*>(smem);
+  uint32_t* rMetric = rMeta + Sn;
+  uint32_t* rMask = rMetric + Sn;  // [W][Sn]
+  for (uint32_t v = tid; v < N; v += kBlock) {
+    const uint32_t d = sv.dist(v);
+    uint32_t m[W], cnt = 0;
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+      m[w] = sv.nh(v, w);  // 0 for the source and unreachable nodes
+      cnt += __popc(m[w]);
+    }
+    rMeta[v] = node_route_meta(v, s, d != kInf, cnt, nflags[v]);
+    rMetric[v] = (v == s) ? kInf : d;
+#pragma unroll
+    for (int w = 0; w < W; ++w) rMask[w * Sn + v] = m[w];
+  }
+  __syncthreads();
+
+  const uint32_t p0 = pt.pfx_base[t];
+  const uint32_t P = pt.pfx_base[t + 1] - p0;
+  stream_routes<W>(pt, key + size_t(t) * Sp, p0, P, Sp, u, s, nflags, sv, cfg, out,
+                   [&](uint32_t v, Rec<W>& r) {
+                     r.meta = rMeta[v];
+                     r.metric = rMetric[v];
+#pragma unroll
+                     for (int w = 0; w < W; ++w) r.mask[w] = rMask[w * Sn + v];
+                   });
+}
+
+// ---- per-(device, stream) workspace (grow-only; freed at process exit) ----
+// Calls on one stream run in order, so its scratch is reused safely; calls
+// on different streams (e.g. two unit groups overlapped) get separate ones.
+namespace {
+struct Workspace {
+  void* ptr = nullptr;
+  size_t bytes = 0;
+};
+std::mutex g_wsMutex;
+std::map<std::pair<int, hipStream_t>, Workspace> g_ws;
+}  // namespace
+
+hipError_t workspace(size_t bytes, hipStream_t stream, void** out) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  std::lock_guard<std::mutex> lock(g_wsMutex);
+  Workspace& w = g_ws[{dev, stream}];
+  if (w.bytes < bytes) {
+    if (w.ptr) {
+      e = hipFree(w.ptr);  // implicit device sync: no launch still reads it
+      if (e != hipSuccess) return e;
+      w.ptr = nullptr;
+      w.bytes = 0;
+    }
+    e = hipMalloc(&w.ptr, bytes);
+    if (e != hipSuccess) return e;
+    w.bytes = bytes;
+  }
+  *out = w.ptr;
+  return hipSuccess;
+}
+
+// "route_stream" option for large shared topologies: 2 (default) fused
+// frontier SPF + route stream, one launch; 1 SPF launch then route-stream
+// launch (dist / next-hop sets through HBM); 0 the fused multi-source kernel.
+int g_routeStream = 2;
+
+bool try_ms(const ogs_graph& g, const ogs_prefix_table& pt, int hasPrefixes,
+            const ogs_unit* units, int nUnits, uint32_t flags, int W,
+            const ogs_spf_out& out, hipStream_t stream, hipError_t* err);
+bool frontier_fits(const ogs_graph& g, uint32_t flags, int W);
+size_t chunk_scratch_bytes(const ogs_graph& g);
+hipError_t launch_frontier_spf(const ogs_graph& g, const ogs_unit* units,
+                               int nUnits, uint32_t flags, int W,
+                               uint32_t* dist, uint32_t* nh, void* scratch,
+                               hipStream_t stream);
+hipError_t launch_frontier_routes(const ogs_graph& g, const ogs_prefix_table& pt,
+                                  const uint32_t* key, const ogs_unit* units,
+                                  int nUnits, uint32_t flags, int W,
+                                  const ogs_spf_out& out, void* scratch,
+                                  hipStream_t stream);
+
+template <int W>
+hipError_t launch_route_stream(const ogs_graph& g, const ogs_prefix_table& pt,
+                               const uint32_t* key, const ogs_unit* units,
+                               int nUnits, uint32_t flags, const uint32_t* dist,
+                               const uint32_t* nh, const ogs_spf_out& out,
+                               hipStream_t stream) {
+  const size_t lds = size_t(g.max_nodes) * (2 + W) * 4;
+  auto k = route_stream_kernel<W>;
+  if (lds > 64 * 1024) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       int(lds));
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(k, dim3(nUnits), dim3(kBlock), lds, stream, g, pt, key,
+                     units, flags, dist, nh, out);
+  return hipGetLastError();
+}
+
+static size_t round256(size_t x) { return (x + 255) & ~size_t(255); }
+
+// SPF only through the frontier kernel (callers without a prefix table).
+bool try_frontier(const ogs_graph& g, const ogs_unit* units, int nUnits,
+                  uint32_t flags, int W, uint32_t* dist, uint32_t* nh,
+                  hipStream_t stream, hipError_t* err) {
+  if (!dist || !nh || !g.edge_src || !frontier_fits(g, flags, W)) return false;
+  if (W != 1 && W != 2 && W != 4 && W != 8) return false;
+  void* ws = nullptr;
+  *err = workspace(chunk_scratch_bytes(g), stream, &ws);
+  if (*err != hipSuccess) return true;
+  *err = launch_frontier_spf(g, units, nUnits, flags, W, dist, nh, ws, stream);
+  return true;
+}
+
+// Large shared topologies with a prefix table: key fold, then either the
+// fused frontier SPF + stream launch (route_stream 2), or an SPF launch
+// (frontier / multi-source sweep) and a route-stream launch (route_stream 1).
+bool try_ms_stream(const ogs_graph& g, const ogs_prefix_table& pt,
+                   const ogs_unit* units, int nUnits, uint32_t flags, int W,
+                   const ogs_spf_out& out, hipStream_t stream, hipError_t* err) {
+  if (!g_routeStream || !g.edge_src || (flags & OGS_F_WIDE_METRIC)) return false;
+  if (W != 1 && W != 2 && W != 4) return false;
+  if (size_t(g.max_nodes) * (2 + W) * 4 > 160 * 1024) return false;
+  const size_t Sn = size_t(g.max_nodes), Sp = size_t(pt.max_prefixes);
+  const bool fused = g_routeStream == 2 && frontier_fits(g, flags, W);
+  const bool frontier = frontier_fits(g, flags, W);
+  const size_t keyBytes = round256(size_t(g.num_topos) * Sp * 4);
+  const size_t chunkBytes = frontier ? chunk_scratch_bytes(g) : 0;
+  const size_t distBytes = (fused || out.dist) ? 0 : round256(size_t(nUnits) * Sn * 4);
+  const size_t nhBytes = (fused || out.nh) ? 0 : round256(size_t(nUnits) * W * Sn * 4);
+  void* ws = nullptr;
+  *err = workspace(keyBytes + chunkBytes + distBytes + nhBytes, stream, &ws);
+  if (*err != hipSuccess) return true;
+  char* base = static_cast<char*>(ws);
+  uint32_t* key = reinterpret_cast<uint32_t*>(base);
+  void* chunkScratch = base + keyBytes;
+  if (Sp > 0) {
+    hipLaunchKernelGGL(pfx_key_kernel, dim3(unsigned((Sp + kBlock - 1) / kBlock),
+                                            unsigned(g.num_topos)),
+                       dim3(kBlock), 0, stream, pt, g.num_topos, key);
+    *err = hipGetLastError();
+    if (*err != hipSuccess) return true;
+  }
+  if (fused) {
+    *err = launch_frontier_routes(g, pt, key, units, nUnits, flags, W, out,
+                                  chunkScratch, stream);
+    return true;
+  }
+  ogs_spf_out spf{};
+  spf.dist = out.dist ? out.dist : base + keyBytes + chunkBytes;
+  spf.nh = out.nh ? out.nh
+                  : reinterpret_cast<uint32_t*>(base + keyBytes + chunkBytes + distBytes);
+  if (frontier) {
+    *err = launch_frontier_spf(g, units, nUnits, flags, W,
+                               static_cast<uint32_t*>(spf.dist), spf.nh,
+                               chunkScratch, stream);
+  } else if (!try_ms(g, pt, 0, units, nUnits, flags, W, spf, stream, err)) {
+    return false;
+  }
+  if (*err != hipSuccess || Sp == 0) return true;
+  const uint32_t* d = static_cast<const uint32_t*>(spf.dist);
+  switch (W) {
+    case 1: *err = launch_route_stream<1>(g, pt, key, units, nUnits, flags, d, spf.nh, out, stream); break;
+    case 2: *err = launch_route_stream<2>(g, pt, key, units, nUnits, flags, d, spf.nh, out, stream); break;
+    default: *err = launch_route_stream<4>(g, pt, key, units, nUnits, flags, d, spf.nh, out, stream); break;
+  }
+  return true;
+}
+
+}  // namespace ogs

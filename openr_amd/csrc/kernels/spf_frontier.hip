@@ -1,0 +1,416 @@
+// spf_frontier.hip — frontier SPF for large topologies, one workgroup per
+// (topology, source) unit: C3 fabric all-sources (N = 2,080, E = 43,008),
+// C4 link-failure variants and C5 areas of WAN graphs.
+//
+// Same fixpoint as spf_core.h / spf_route_ms.hip (reference mapping there:
+// LinkState::runSpf, LinkState.cpp:720-820): distances are the least
+// solution of dist(v) = min over usable u of dist(u) + w(u, v), next-hop
+// sets the least solution of NH(v) = U over tight u of (u == src ?
+// {slot(src->v)} : NH(u)), where u relaxes iff u == src or u is not
+// hard-drained (741-752). What differs is the work schedule: the pull
+// sweeps of the other kernels touch every edge in every round; here only the
+// rows of nodes that CHANGED in the previous round are pushed (Bellman-Ford
+// with a frontier), so each phase costs about one pass over the edges:
+//  * chunk_prep_kernel cuts every topology's rows into chunks of <= 8
+//    directed edges, once per call, into a workspace list (u64: node | count
+//    | hard-drained bit, local edge begin), so a round's work is balanced
+//    over the workgroup however skewed the degrees (fabric: RSW 8, SSW 32,
+//    FSW 84 links) and the list costs no LDS;
+//  * stamp[v] = the round in which v must be pushed (set when its distance /
+//    next-hop set changes; a node changed again mid-round is simply pushed
+//    once more in the next round, which is exact for a monotone fixpoint);
+//  * dist phase: push dist[v] + w into dist[u] with LDS atomicMin;
+//    next-hop phase: the source's row seeds link-slot bits on tight edges,
+//    then changed nodes push NH(v) into tight neighbours with atomicOr;
+//  * edges and chunks stay in HBM/L2 (shared by every source of the batch);
+//    LDS holds only dist / next-hop sets / stamps (10 B per node at W = 1),
+//    so up to 7 units share a CU and hide each other's L2 latency.
+// Outputs: dist[u*Sn + v], nh[(u*W + w)*Sn + v] (ogs_spf_out layout); the
+// fused form then streams the unit's RouteDb (route_stream.h) from LDS.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "openr_gpu.h"
+#include "route_core.h"
+#include "route_stream.h"
+#include "spf_core.h"
+
+namespace ogs {
+
+constexpr uint32_t kChunk = 8;
+constexpr uint32_t kChunkCntShift = 21;  // bits 21..24: edge count - 1
+constexpr uint32_t kChunkDrained = 1u << 25;
+
+// Exclusive prefix sum of x over the workgroup's current tile; returns the
+// sum's base for this thread and adds the tile total to *base (LDS).
+__device__ __forceinline__ uint32_t tile_scan(uint32_t x, uint32_t* wsum,
+                                              uint32_t* base) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint32_t inc = x;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(inc, d, 64);
+    if (lane >= d) inc += y;
+  }
+  if (lane == 63) wsum[wave] = inc;
+  __syncthreads();
+  uint32_t off = *base;
+  for (int w = 0; w < wave; ++w) off += wsum[w];
+  __syncthreads();
+  if (threadIdx.x == kBlock - 1) *base = off + inc;
+  return off + inc - x;
+}
+
+// Upper bound of sum_v ceil(deg(v)/8) over a topology.
+__host__ __device__ inline uint32_t chunk_cap(const ogs_graph& g) {
+  return uint32_t(g.max_edges) / kChunk + uint32_t(g.max_nodes);
+}
+
+// One workgroup per topology: chunks[t*cap + i], count nChunk[t].
+__global__ __launch_bounds__(kBlock) void chunk_prep_kernel(
+    ogs_graph g, uint32_t cap, uint64_t* __restrict__ chunks,
+    uint32_t* __restrict__ nChunk) {
+  __shared__ uint32_t wsum[kBlock / 64];
+  __shared__ uint32_t base;
+  const uint32_t t = blockIdx.x;
+  const uint32_t nb = g.node_base[t];
+  const uint32_t N = g.node_base[t + 1] - nb;
+  const uint32_t* __restrict__ row = g.row_ptr + nb;
+  const uint32_t e0 = row[0];
+  uint64_t* out = chunks + size_t(t) * cap;
+  if (threadIdx.x == 0) base = 0;
+  __syncthreads();
+  for (uint32_t t0 = 0; t0 < N; t0 += kBlock) {
+    const uint32_t v = t0 + threadIdx.x;
+    uint32_t b = 0, deg = 0;
+    if (v < N) {
+      b = row[v] - e0;
+      deg = row[v + 1] - e0 - b;
+    }
+    const uint32_t n = (deg + kChunk - 1) / kChunk;
+    const uint32_t at = tile_scan(n, wsum, &base);
+    const uint32_t drained =
+        (v < N && (g.node_flags[nb + v] & OGS_NODE_OVERLOADED)) ? kChunkDrained : 0u;
+    for (uint32_t k = 0; k < n; ++k) {
+      const uint32_t cnt = min(kChunk, deg - k * kChunk);
+      out[at + k] = uint64_t(v | ((cnt - 1) << kChunkCntShift) | drained) |
+          (uint64_t(b + k * kChunk) << 32);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) nChunk[t] = base;
+}
+
+// Loads chunk ch's edges into registers: past the chunk's count an edge
+// reads as DOWN (dst 0, never relaxes).
+__device__ __forceinline__ void load_chunk(const uint64_t* __restrict__ edges,
+                                           uint64_t ch, uint64_t (&x)[kChunk]) {
+  const uint32_t b = uint32_t(ch >> 32);
+  const uint32_t n = ((uint32_t(ch) >> kChunkCntShift) & 15u) + 1u;
+#pragma unroll
+  for (uint32_t i = 0; i < kChunk; ++i) {
+    x[i] = i < n ? edges[b + i] : uint64_t(OGS_EDGE_DOWN);
+  }
+}
+
+// One unit's SPF into LDS (dist[v], nh[v*W + w]); returns after the final
+// workgroup barrier. stamp[] is scratch.
+template <int W>
+__device__ __forceinline__ void frontier_spf(
+    uint32_t N, uint32_t s, const uint64_t* __restrict__ edges,
+    const uint64_t* __restrict__ chunks, uint32_t C, bool hop,
+    const uint32_t* __restrict__ gRow, uint32_t e0, uint32_t* dist,
+    uint32_t* nh, uint16_t* stamp, uint64_t* tp) {
+  constexpr uint32_t kInf = 0xFFFFFFFFu;
+  const int tid = threadIdx.x;
+  for (uint32_t v = tid; v < N; v += kBlock) {
+    dist[v] = (v == s) ? 0u : kInf;
+    stamp[v] = (v == s) ? 1 : 0;
+#pragma unroll
+    for (int w = 0; w < W; ++w) nh[v * W + w] = 0u;
+  }
+  __syncthreads();
+#ifdef OGS_STAMPS
+  tp[0] = __builtin_amdgcn_s_memtime();
+#endif
+
+  // ---- dist phase: push dist(v) + w from the nodes changed last round ------
+  uint32_t r = 1;
+  for (;; ++r) {
+    bool changed = false;
+    for (uint32_t c = tid; c < C; c += kBlock) {
+      const uint64_t ch = chunks[c];
+      const uint32_t v = uint32_t(ch) & OGS_EDGE_DST_MASK;
+      if (stamp[v] != r) continue;
+      if ((uint32_t(ch) & kChunkDrained) && v != s) continue;
+      const uint32_t dv = dist[v];
+      uint64_t x[kChunk];
+      load_chunk(edges, ch, x);
+      uint32_t t[kChunk], cand[kChunk], dt[kChunk];
+#pragma unroll
+      for (uint32_t i = 0; i < kChunk; ++i) {
+        const uint32_t lo = static_cast<uint32_t>(x[i]);
+        t[i] = edge_dst(lo);
+        cand[i] = (lo & OGS_EDGE_DOWN)
+            ? kInf : dv + (hop ? 1u : static_cast<uint32_t>(x[i] >> 32));
+      }
+#pragma unroll
+      for (uint32_t i = 0; i < kChunk; ++i) dt[i] = dist[t[i]];
+#pragma unroll
+      for (uint32_t i = 0; i < kChunk; ++i) {
+        if (cand[i] < dt[i]) {
+          atomicMin(&dist[t[i]], cand[i]);
+          stamp[t[i]] = uint16_t(r + 1);
+          changed = true;
+        }
+      }
+    }
+    if (!__syncthreads_or(changed)) break;
+  }
+#ifdef OGS_STAMPS
+  tp[1] = __builtin_amdgcn_s_memtime();
+  tp[3] = r;
+#endif
+
+  // ---- next-hop phase --------------------------------------------------------
+  // seed: the source's own row (slot j = j-th edge of the source's row)
+  const uint32_t r0 = r + 1;
+  {
+    const uint32_t b = gRow[s] - e0, n = gRow[s + 1] - e0 - b;
+    for (uint32_t j = tid; j < n && j < 32u * W; j += kBlock) {
+      const uint64_t x = edges[b + j];
+      const uint32_t lo = static_cast<uint32_t>(x);
+      if (lo & OGS_EDGE_DOWN) continue;
+      const uint32_t t = edge_dst(lo);
+      const uint32_t w = hop ? 1u : static_cast<uint32_t>(x >> 32);
+      if (w == dist[t]) {
+        atomicOr(&nh[t * W + (j >> 5)], 1u << (j & 31u));
+        stamp[t] = uint16_t(r0);
+      }
+    }
+  }
+  __syncthreads();
+  // then changed nodes push NH(v) into tight neighbours
+  for (r = r0;; ++r) {
+    bool changed = false;
+    for (uint32_t c = tid; c < C; c += kBlock) {
+      const uint64_t ch = chunks[c];
+      const uint32_t v = uint32_t(ch) & OGS_EDGE_DST_MASK;
+      if (stamp[v] != r || v == s || (uint32_t(ch) & kChunkDrained)) continue;
+      const uint32_t dv = dist[v];
+      uint32_t nv[W];
+#pragma unroll
+      for (int w = 0; w < W; ++w) nv[w] = nh[v * W + w];
+      uint64_t x[kChunk];
+      load_chunk(edges, ch, x);
+      uint32_t t[kChunk], cand[kChunk], dt[kChunk];
+#pragma unroll
+      for (uint32_t i = 0; i < kChunk; ++i) {
+        const uint32_t lo = static_cast<uint32_t>(x[i]);
+        t[i] = edge_dst(lo);
+        cand[i] = (lo & OGS_EDGE_DOWN)
+            ? kInf : dv + (hop ? 1u : static_cast<uint32_t>(x[i] >> 32));
+      }
+#pragma unroll
+      for (uint32_t i = 0; i < kChunk; ++i) dt[i] = dist[t[i]];
+#pragma unroll
+      for (uint32_t i = 0; i < kChunk; ++i) {
+        if (cand[i] != dt[i]) continue;  // not a tight edge (or down)
+        bool add = false;
+#pragma unroll
+        for (int k = 0; k < W; ++k) {
+          const uint32_t a = nv[k] & ~nh[t[i] * W + k];
+          if (a) {
+            atomicOr(&nh[t[i] * W + k], a);
+            add = true;
+          }
+        }
+        if (add) {
+          stamp[t[i]] = uint16_t(r + 1);
+          changed = true;
+        }
+      }
+    }
+    if (!__syncthreads_or(changed)) break;
+  }
+#ifdef OGS_STAMPS
+  tp[2] = __builtin_amdgcn_s_memtime();
+  tp[4] = r - r0 + 1;
+#endif
+}
+
+uint32_t frontier_lds_bytes(uint32_t Sn, int W) {
+  return 4u * (((Sn + 3u) & ~3u) + ((Sn * W + 3u) & ~3u)) + 2u * ((Sn + 1u) & ~1u);
+}
+
+// ROUTES = false: SPF only, dist / nh to HBM.
+// ROUTES = true: SPF + the unit's RouteDb stream (route_stream.h) from LDS;
+// dist / nh go to HBM only when requested.
+template <int W, bool ROUTES>
+__global__ __launch_bounds__(kBlock) void spf_frontier_kernel(
+    ogs_graph g, ogs_prefix_table pt, const uint32_t* __restrict__ key,
+    const uint64_t* __restrict__ chunks, const uint32_t* __restrict__ nChunk,
+    uint32_t cap, const ogs_unit* __restrict__ units, uint32_t flags,
+    uint32_t* __restrict__ oDist, uint32_t* __restrict__ oNh, ogs_spf_out out) {
+  constexpr uint32_t kInf = 0xFFFFFFFFu;
+  const int tid = threadIdx.x;
+  const uint32_t u0 = blockIdx.x;
+  const ogs_unit unit = units[u0];
+  const uint32_t s = unit.src;
+  const uint32_t nb = g.node_base[unit.topo];
+  const uint32_t N = g.node_base[unit.topo + 1] - nb;
+  const uint32_t* __restrict__ gRow = g.row_ptr + nb;
+  const uint32_t e0 = gRow[0];
+  const uint8_t* __restrict__ nflags = g.node_flags + nb;
+  const uint32_t Sn = uint32_t(g.max_nodes);
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint32_t* dist = reinterpret_cast<uint32_t*>(smem);              // [Sn]
+  uint32_t* nh = dist + ((Sn + 3u) & ~3u);                           // [Sn*W]
+  uint16_t* stamp = reinterpret_cast<uint16_t*>(nh + ((Sn * W + 3u) & ~3u));  // [Sn]
+
+  uint64_t tp[5] = {0, 0, 0, 0, 0};
+#ifdef OGS_STAMPS
+  const uint64_t t0 = __builtin_amdgcn_s_memtime();
+  const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
+#endif
+  frontier_spf<W>(N, s, g.edges + e0, chunks + size_t(unit.topo) * cap,
+                  nChunk[unit.topo], (flags & OGS_F_HOP_METRIC) != 0, gRow, e0,
+                  dist, nh, stamp, tp);
+
+  for (uint32_t v = tid; v < N; v += kBlock) {
+    if (oDist) oDist[size_t(u0) * Sn + v] = dist[v];
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+      if (oNh) oNh[(size_t(u0) * W + w) * Sn + v] = nh[v * W + w];
+    }
+  }
+  if constexpr (ROUTES) {
+    // per-node record flags (8 bits) over the dead stamps
+    uint16_t* rMeta = stamp;
+    for (uint32_t v = tid; v < N; v += kBlock) {
+      uint32_t cnt = 0;
+#pragma unroll
+      for (int w = 0; w < W; ++w) cnt += __popc(nh[v * W + w]);
+      rMeta[v] = uint16_t(node_route_meta(v, s, dist[v] != kInf, cnt, nflags[v]));
+    }
+    __syncthreads();
+    const uint32_t Sp = uint32_t(pt.max_prefixes);
+    const uint32_t p0 = pt.pfx_base[unit.topo];
+    const uint32_t P = pt.pfx_base[unit.topo + 1] - p0;
+    const RouteCfg cfg{(flags & OGS_F_ENABLE_V4) != 0,
+                       (flags & OGS_F_V4_OVER_V6) != 0,
+                       (flags & OGS_F_BEST_ROUTE_SELECTION) != 0};
+    const SplitView<uint32_t, W> sv{dist, nh};
+    stream_routes<W>(pt, key + size_t(unit.topo) * Sp, p0, P, Sp, u0, s, nflags, sv,
+                     cfg, out, [&](uint32_t v, Rec<W>& r) {
+                       r.meta = rMeta[v];
+                       r.metric = (v == s) ? kInf : dist[v];
+#pragma unroll
+                       for (int w = 0; w < W; ++w) r.mask[w] = nh[v * W + w];
+                     });
+  }
+#ifdef OGS_STAMPS  // diagnostic build only: phase clocks into out.sel row u0
+  __syncthreads();
+  if (tid == 0 && out.sel) {
+    uint32_t* st = out.sel + size_t(u0) * uint32_t(pt.max_prefixes);
+    st[0] = uint32_t(tp[0] - t0);       // setup
+    st[1] = uint32_t(tp[1] - tp[0]);    // dist phase
+    st[2] = uint32_t(tp[2] - tp[1]);    // next-hop phase
+    st[3] = uint32_t(__builtin_amdgcn_s_memtime() - tp[2]);  // outputs + routes
+    st[4] = uint32_t(tp[3]);            // dist rounds
+    st[5] = uint32_t(tp[4]);            // next-hop rounds
+    st[6] = uint32_t(rt0);
+    st[7] = uint32_t(__builtin_amdgcn_s_memrealtime());
+  }
+#endif
+}
+
+template <int W, bool ROUTES>
+hipError_t launch_frontier(const ogs_graph& g, const ogs_prefix_table& pt,
+                           const uint32_t* key, const uint64_t* chunks,
+                           const uint32_t* nChunk, const ogs_unit* units,
+                           int nUnits, uint32_t flags, uint32_t* dist,
+                           uint32_t* nh, const ogs_spf_out& out,
+                           hipStream_t stream) {
+  const uint32_t lds = frontier_lds_bytes(uint32_t(g.max_nodes), W);
+  auto k = spf_frontier_kernel<W, ROUTES>;
+  if (lds > 64 * 1024) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       int(lds));
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(k, dim3(nUnits), dim3(kBlock), lds, stream, g, pt, key,
+                     chunks, nChunk, chunk_cap(g), units, flags, dist, nh, out);
+  return hipGetLastError();
+}
+
+// "spf_frontier" option: 1 (default) large topologies use this kernel for
+// their SPF, 0 the multi-source edge sweep (spf_route_ms.hip).
+int g_spfFrontier = 1;
+
+bool frontier_fits(const ogs_graph& g, uint32_t flags, int W) {
+  if (!g_spfFrontier || (flags & OGS_F_WIDE_METRIC)) return false;
+  if (g.max_nodes > 30000 || g.max_degree > OGS_MAX_DEGREE) return false;  // u16 stamps
+  return frontier_lds_bytes(uint32_t(g.max_nodes), W) <= 160u * 1024u;
+}
+
+// Scratch of the chunk lists of every topology of the batch.
+size_t chunk_scratch_bytes(const ogs_graph& g) {
+  return (size_t(g.num_topos) * chunk_cap(g) * 8 + size_t(g.num_topos) * 4 + 255) &
+      ~size_t(255);
+}
+
+hipError_t prep_chunks(const ogs_graph& g, void* scratch, hipStream_t stream,
+                       uint64_t** chunks, uint32_t** nChunk) {
+  *chunks = static_cast<uint64_t*>(scratch);
+  *nChunk = reinterpret_cast<uint32_t*>(*chunks + size_t(g.num_topos) * chunk_cap(g));
+  hipLaunchKernelGGL(chunk_prep_kernel, dim3(g.num_topos), dim3(kBlock), 0, stream,
+                     g, chunk_cap(g), *chunks, *nChunk);
+  return hipGetLastError();
+}
+
+// SPF only (dist / next-hop sets to HBM); `scratch` holds
+// chunk_scratch_bytes(g). Call only when frontier_fits().
+hipError_t launch_frontier_spf(const ogs_graph& g, const ogs_unit* units,
+                               int nUnits, uint32_t flags, int W,
+                               uint32_t* dist, uint32_t* nh, void* scratch,
+                               hipStream_t stream) {
+  uint64_t* chunks = nullptr;
+  uint32_t* nChunk = nullptr;
+  hipError_t e = prep_chunks(g, scratch, stream, &chunks, &nChunk);
+  if (e != hipSuccess) return e;
+  const ogs_prefix_table pt{};
+  const ogs_spf_out none{};
+  switch (W) {
+    case 1: return launch_frontier<1, false>(g, pt, nullptr, chunks, nChunk, units, nUnits, flags, dist, nh, none, stream);
+    case 2: return launch_frontier<2, false>(g, pt, nullptr, chunks, nChunk, units, nUnits, flags, dist, nh, none, stream);
+    case 4: return launch_frontier<4, false>(g, pt, nullptr, chunks, nChunk, units, nUnits, flags, dist, nh, none, stream);
+    case 8: return launch_frontier<8, false>(g, pt, nullptr, chunks, nChunk, units, nUnits, flags, dist, nh, none, stream);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+// Fused frontier SPF + RouteDb stream (key = pfx_key_kernel output). W is
+// 1, 2 or 4.
+hipError_t launch_frontier_routes(const ogs_graph& g, const ogs_prefix_table& pt,
+                                  const uint32_t* key, const ogs_unit* units,
+                                  int nUnits, uint32_t flags, int W,
+                                  const ogs_spf_out& out, void* scratch,
+                                  hipStream_t stream) {
+  uint64_t* chunks = nullptr;
+  uint32_t* nChunk = nullptr;
+  hipError_t e = prep_chunks(g, scratch, stream, &chunks, &nChunk);
+  if (e != hipSuccess) return e;
+  uint32_t* dist = static_cast<uint32_t*>(out.dist);
+  switch (W) {
+    case 1: return launch_frontier<1, true>(g, pt, key, chunks, nChunk, units, nUnits, flags, dist, out.nh, out, stream);
+    case 2: return launch_frontier<2, true>(g, pt, key, chunks, nChunk, units, nUnits, flags, dist, out.nh, out, stream);
+    case 4: return launch_frontier<4, true>(g, pt, key, chunks, nChunk, units, nUnits, flags, dist, out.nh, out, stream);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace ogs

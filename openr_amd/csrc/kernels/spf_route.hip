@@ -204,6 +204,12 @@ bool try_wave(const ogs_graph& g, const ogs_prefix_table& pt, int hasPrefixes,
               const ogs_spf_out& out, uint32_t maxA, hipStream_t stream,
               hipError_t* err);
 
+bool try_frontier(const ogs_graph& g, const ogs_unit* units, int nUnits,
+                  uint32_t flags, int W, uint32_t* dist, uint32_t* nh,
+                  hipStream_t stream, hipError_t* err);
+bool try_ms_stream(const ogs_graph& g, const ogs_prefix_table& pt,
+                   const ogs_unit* units, int nUnits, uint32_t flags, int W,
+                   const ogs_spf_out& out, hipStream_t stream, hipError_t* err);
 bool try_ms(const ogs_graph& g, const ogs_prefix_table& pt, int hasPrefixes,
             const ogs_unit* units, int nUnits, uint32_t flags, int W,
             const ogs_spf_out& out, hipStream_t stream, hipError_t* err);
@@ -236,6 +242,15 @@ hipError_t launch_spf_routes(const ogs_graph& g, const ogs_prefix_table* pt,
   // large shared topologies: multi-source edge-parallel kernel
   if ((uw == -1 && g.max_nodes > 256) || uw == 3) {
     hipError_t err = hipSuccess;
+    if (hasPrefixes &&
+        try_ms_stream(g, p, units, nUnits, flags, W, out, stream, &err)) {
+      return err;
+    }
+    if (!hasPrefixes && !out.meta && !out.metric && !out.mask && !out.sel &&
+        try_frontier(g, units, nUnits, flags, W, static_cast<uint32_t*>(out.dist),
+                     out.nh, stream, &err)) {
+      return err;
+    }
     if (try_ms(g, p, hasPrefixes, units, nUnits, flags, W, out, stream, &err)) {
       return err;
     }

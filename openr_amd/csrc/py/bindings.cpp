@@ -270,6 +270,8 @@ void loadLsdb(const topogen::Lsdb& g, LinkState& ls, PrefixState& ps) {
     e.metrics.path_preference = p.path_preference;
     e.metrics.source_preference = p.source_preference;
     e.metrics.distance = p.distance;
+    e.metrics.drain_metric = p.drain_metric;
+    if (p.minNexthop >= 0) e.minNexthop = p.minNexthop;
     ps.updatePrefix(p.node, g.area, e);
   }
 }
@@ -287,7 +289,21 @@ topogen::GridOpts gridOpts(const py::dict& d) {
   return o;
 }
 
+topogen::Lsdb genLsdbRaw(const std::string& kind, const py::dict& d);
+
 topogen::Lsdb genLsdb(const std::string& kind, const py::dict& d) {
+  auto db = genLsdbRaw(kind, d);
+  topogen::PrefixMix m;
+  m.v4Permille = get<int>(d, "v4Permille", 0);
+  m.anycastPermille = get<int>(d, "anycastPermille", 0);
+  m.minNhPermille = get<int>(d, "minNhPermille", 0);
+  m.drainPermille = get<int>(d, "drainPermille", 0);
+  m.seed = get<uint64_t>(d, "mixSeed", 0x3F);
+  topogen::applyPrefixMix(db, m);
+  return db;
+}
+
+topogen::Lsdb genLsdbRaw(const std::string& kind, const py::dict& d) {
   if (kind == "grid") return topogen::grid(gridOpts(d));
   if (kind == "fabric") {
     topogen::FabricOpts o;

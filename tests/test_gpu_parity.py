@@ -303,3 +303,70 @@ def test_multi_source_kernel_wan_overloads(product, oracle, seed):
     srcs = [str(rng.randrange(700)) for _ in range(9)]
     _cmp(product.gen_route_dbs("wan", opts, srcs, True, True, True),
          oracle.gen_route_dbs("wan", opts, srcs, True, True, True), "wan700")
+
+
+def _batch_dbs(product, kind, opts, srcs, enable_v4, brs, **options):
+    """All sources of one generated topology in ONE BatchRunner launch, with
+    engine options set for the duration of the call."""
+    import openr_amd.capi as capi
+    lib = capi.load()
+    try:
+        for k, v in options.items():
+            capi.check(lib, lib.ogs_set_option(k.encode(), v), k)
+        br = product.BatchRunner(enable_v4, False, brs)
+        br.add_generated(kind, opts, srcs)
+        br.upload()
+        br.run()
+        br.download()
+        return [br.canonical(u) for u in range(len(srcs))]
+    finally:
+        lib.ogs_set_option(b"route_stream", 2)
+        lib.ogs_set_option(b"spf_frontier", 1)
+        lib.ogs_set_option(b"ms_group", 0)
+
+
+MIX = dict(v4Permille=150, anycastPermille=120, minNhPermille=60, drainPermille=50)
+
+
+@pytest.mark.parametrize("stream,frontier", [(0, 0), (1, 0), (1, 1), (2, 1)])
+@pytest.mark.parametrize("enable_v4,brs", [(True, False), (False, True), (True, True)])
+def test_route_stream_fabric_prefix_mix(product, oracle, stream, frontier, enable_v4, brs):
+    """Split SPF / route-stream launches vs the fused multi-source kernel on a
+    352-node fabric whose prefix table mixes v4 (gated when v4 is off),
+    anycast (several advertisers, ghost advertisers), minNexthop and drained
+    advertisements, plus drained nodes/links: bit-exact vs the oracle."""
+    opts = dict(pods=8, planes=4, sswPerPlane=16, rswPerPod=32, full=True,
+                prefixesPerNode=3, nodeOverloadPermille=20, adjOverloadPermille=10,
+                **MIX)
+    names = ([f"1-{p}-{s}" for p in range(4) for s in range(16)] +
+             [f"2-{p}-{f}" for p in range(8) for f in range(4)] +
+             [f"3-{p}-{r}" for p in range(8) for r in range(32)])
+    srcs = names[::5] + ["2-5-1", "1-3-15"]
+    a = _batch_dbs(product, "fabric", opts, srcs, enable_v4, brs, route_stream=stream,
+                   spf_frontier=frontier)
+    _cmp(a, oracle.gen_route_dbs("fabric", opts, srcs, enable_v4, False, brs), "fabricmix")
+
+
+@pytest.mark.parametrize("stream,frontier", [(0, 0), (1, 0), (1, 1), (2, 1)])
+def test_route_stream_wan_prefix_mix(product, oracle, stream, frontier):
+    """700-node WAN, random metrics, overloads and the prefix mix, best-route
+    selection on, through every large-topology SPF / RouteDb form."""
+    opts = dict(nodes=700, seed=0xC5, prefixesPerNode=2, nodeOverloadPermille=30,
+                adjOverloadPermille=20, **MIX)
+    rng = random.Random(11)
+    srcs = [str(rng.randrange(700)) for _ in range(10)]
+    a = _batch_dbs(product, "wan", opts, srcs, True, True, route_stream=stream,
+                   spf_frontier=frontier)
+    _cmp(a, oracle.gen_route_dbs("wan", opts, srcs, True, False, True), "wanmix")
+
+
+def test_route_stream_unaligned_prefix_rows(product, oracle):
+    """Prefix count not a multiple of 4 (scalar tail path of the stream)."""
+    opts = dict(pods=4, planes=4, sswPerPlane=20, rswPerPod=60, full=True,
+                prefixesPerNode=1, **MIX)
+    names = ([f"1-{p}-{s}" for p in range(4) for s in range(20)] +
+             [f"2-{p}-{f}" for p in range(4) for f in range(4)] +
+             [f"3-{p}-{r}" for p in range(4) for r in range(60)])
+    srcs = names[::7]
+    a = _batch_dbs(product, "fabric", opts, srcs, True, False)
+    _cmp(a, oracle.gen_route_dbs("fabric", opts, srcs, True, False, False), "fabric_tail")
