@@ -16,7 +16,6 @@ the elapsed time.
 """
 import argparse
 import ctypes
-import hashlib
 import json
 import os
 import sys
@@ -24,6 +23,12 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+
+# torch first: its HIP runtime must be the one libopenr_gpu.so binds to (one
+# HIP runtime per process); openr_amd's import loads the engine library
+import torch  # noqa: E402,F401
+
+from openr_amd import shard  # noqa: E402
 
 TOPOS_PER_GPU = 4096
 GRID_N = 10
@@ -74,7 +79,7 @@ def c3_launches(torch, M, capi, dev, rank, world, ppn, with_sel=False):
     N = len(ssw) + len(fsw) + len(rsw)
     launches = []
     for names in (ssw + rsw, fsw):
-        mine = names[rank::world]
+        mine = shard.interleave(names, rank, world)
         br = M.BatchRunner(True, False, False)
         br.add_generated("fabric", opts, mine)
         h = br.host_arrays()
@@ -121,6 +126,25 @@ def c3_launches(torch, M, capi, dev, rank, world, ppn, with_sel=False):
     return launches, N
 
 
+def pmc_traffic(tag, match):
+    """HBM bytes per launch of the kernels whose name contains `match`, from
+    the newest committed PMC summary profiles/r*_pmc_<tag>.json
+    (tools/gpu_pmc.sh: FETCH_SIZE and WRITE_SIZE passes, gfx950 FETCH_SIZE
+    x2 correction). Returns (bytes summed over matching kernels, file) or
+    (None, None)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_pmc_{tag}.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    hits = [v["hbm_bytes_per_launch"] for k, v in d.items()
+            if match in k and v.get("hbm_bytes_per_launch") is not None]
+    if not hits:
+        return None, None
+    return float(sum(hits)), os.path.relpath(files[-1], ROOT)
+
+
 def run_c3(args, torch, dist, rank, world, local_rank):
     """Config C3-full: fabric pods=32 planes=8 ssw/plane=36 rsw/pod=48
     (N=2080, E=43,008), `--prefixes-per-node` prefixes per node, every node a
@@ -133,6 +157,8 @@ def run_c3(args, torch, dist, rank, world, local_rank):
     lib = capi.load()
     lib.ogs_set_device(local_rank)
     dev = torch.device("cuda", local_rank)
+    steps = args.steps if args.config == "c3" else args.c3_steps
+    warmup = args.warmup if args.config == "c3" else 2
     launches, N = c3_launches(torch, M, capi, dev, rank, world, args.prefixes_per_node)
     # the width groups are independent: with --c3-streams 2 the second group
     # runs on its own HIP stream, overlapped with the first
@@ -155,7 +181,7 @@ def run_c3(args, torch, dist, rank, world, local_rank):
         join.record(side)
         main.wait_event(join)
 
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         step()
     torch.cuda.synchronize(dev)
     if dist:
@@ -165,7 +191,7 @@ def run_c3(args, torch, dist, rank, world, local_rank):
     e1 = torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     e0.record(main)
-    for _ in range(args.steps):
+    for _ in range(steps):
         step()
     e1.record(main)
     torch.cuda.synchronize(dev)
@@ -174,25 +200,23 @@ def run_c3(args, torch, dist, rank, world, local_rank):
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t0
     # device time of one whole build on this rank (all launches of a step)
-    kernel_ms = e0.elapsed_time(e1) / args.steps
+    kernel_ms = e0.elapsed_time(e1) / steps
     units = sum(L["U"] for L in launches)
     nbytes = sum(L["bytes"] for L in launches)
     routes = sum(int(((L["o"]["meta"] & 1) != 0).sum().item()) for L in launches)
-    local = torch.tensor([units, routes], dtype=torch.int64, device=dev)
-    elapsed = torch.tensor([wall], dtype=torch.float64, device=dev)
-    if dist:
-        dist.all_reduce(local)
-        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
-    tmax = float(elapsed.item())
+    digest = shard.combine_digests(
+        shard.route_digest(L["o"]["meta"].cpu().numpy(), L["o"]["metric"].cpu().numpy())
+        for L in launches)
+    total_units, total_routes, job_digest, tmax, _ = shard.reduce_stats(
+        dist, torch, dev, units, routes, digest, wall)
     if rank == 0:
-        total_units = int(local[0].item())
         achieved = nbytes / (kernel_ms * 1e-3) / 1e9
-        value = total_units * args.steps / tmax / N
+        value = total_units * steps / tmax / N
         line = {
             "metric": "SPF+RouteDb builds/sec (whole node)",
             "value": round(value, 4), "unit": "builds/s",
-            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": round(tmax / args.steps * 1e3, 4),
+            "n_gpus": world, "steps": steps, "warmup": warmup,
+            "ms_per_step": round(tmax / steps * 1e3, 4),
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
             "dtype": "u32", "data": "synthetic",
             "config": {"workload": f"C3-full: fabric all-sources (N=2080, E=43008, "
@@ -200,18 +224,22 @@ def run_c3(args, torch, dist, rank, world, local_rank):
                                    "RouteDb of every node",
                        "sources": N, "prefixes": N * args.prefixes_per_node,
                        "parallelism": f"shard-by-source x{world}"},
-            "route_dbs_per_s": round(total_units * args.steps / tmax, 1),
-            "routes_per_step": int(local[1].item()),
-            "gteps": round(43008 * total_units * args.steps / tmax / 1e9, 3),
+            "route_dbs_per_s": round(total_units * steps / tmax, 1),
+            "routes_per_step": total_routes,
+            "route_digest": f"{job_digest:016x}",
+            "gteps": round(43008 * total_units * steps / tmax / 1e9, 3),
             "kernel_ms": round(kernel_ms, 4),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
                          "bytes_alg_per_step_rank0": round(nbytes, 1)},
         }
-        print(json.dumps(line), flush=True)
-    if dist:
-        dist.destroy_process_group()
+        traffic, src = pmc_traffic("c3", "spf_frontier_kernel")
+        if traffic is not None and world == 1:
+            line["roofline"]["traffic"] = round(traffic, 1)
+            line["roofline"]["traffic_source"] = src
+        return line
+    return None
 
 
 def main():
@@ -225,6 +253,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--topos", type=int, default=TOPOS_PER_GPU)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-c3", action="store_true",
+                    help="skip the C3 fabric all-sources line embedded in the C2 result")
+    ap.add_argument("--c3-steps", type=int, default=10)
     ap.add_argument("--opt", action="append", default=[],
                     help="engine option name=value (ogs_set_option), for A/B runs")
     args = ap.parse_args()
@@ -246,18 +277,23 @@ def main():
         lib0 = capi.load()
         capi.check(lib0, lib0.ogs_set_option(name.encode(), int(val)), name)
     if args.config == "c3":
-        return run_c3(args, torch, dist, rank, world, local_rank)
+        line = run_c3(args, torch, dist, rank, world, local_rank)
+        if line is not None:
+            print(json.dumps(line), flush=True)
+        if dist:
+            dist.destroy_process_group()
+        return
     openr_amd.require_gpu()
     M = openr_amd.decision
     lib = capi.load()
     lib.ogs_set_device(local_rank)
 
     # ---- build this rank's shard on the host (outside the timed region) ----
-    T = args.topos
-    lo = rank * T
+    # weak scaling: the job is world x --topos topologies, rank r owns block r
+    lo, hi = shard.block_range(world * args.topos, rank, world)
     br = M.BatchRunner(True, False, False)
     br.add_grid_batch(dict(n=GRID_N, metricSeed=METRIC_SEED, prefixSeed=PREFIX_SEED),
-                      lo, lo + T, "1")
+                      lo, hi, "1")
     h = br.host_arrays()
     dev = torch.device("cuda", local_rank)
 
@@ -331,21 +367,9 @@ def main():
     # ---- per-rank digest (result sanity) + cross-rank reduction -----------
     meta = o_meta.cpu().numpy()
     n_routes = int(((meta & 1) != 0).sum())
-    digest = hashlib.sha256(o_meta.cpu().numpy().tobytes() +
-                            o_metric.cpu().numpy().tobytes() +
-                            o_mask.cpu().numpy().tobytes()).digest()[:8]
-    local = torch.tensor([U, n_routes, int.from_bytes(digest, "little") >> 1, 0],
-                         dtype=torch.int64, device=dev)
-    elapsed = torch.tensor([wall], dtype=torch.float64, device=dev)
-    if dist:
-        gathered = [torch.zeros_like(local) for _ in range(world)]
-        dist.all_gather(gathered, local)
-        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
-        total_units = int(sum(int(x[0]) for x in gathered))
-        total_routes = int(sum(int(x[1]) for x in gathered))
-    else:
-        total_units, total_routes = U, n_routes
-    tmax = float(elapsed.item())
+    digest = shard.route_digest(meta, o_metric.cpu().numpy(), o_mask.cpu().numpy())
+    total_units, total_routes, job_digest, tmax, _ = shard.reduce_stats(
+        dist, torch, dev, U, n_routes, digest, wall)
 
     if rank == 0:
         N, E, P = GRID_N * GRID_N, 4 * GRID_N * (GRID_N - 1), GRID_N * GRID_N
@@ -377,6 +401,7 @@ def main():
             "gteps": round(E * value / 1e9, 3),
             "kernel_ms": round(kernel_ms, 5),
             "routes_per_step": total_routes,
+            "route_digest": f"{job_digest:016x}",
             "roofline": {
                 "bound": "hbm",
                 "achieved": round(achieved, 1),
@@ -387,8 +412,22 @@ def main():
                 "bytes_alg_per_unit": round(bpu, 1),
             },
         }
+        traffic, src = pmc_traffic("c2", "spf_route_wave_kernel")
+        if traffic is not None:
+            line["roofline"]["traffic"] = round(traffic, 1)
+            line["roofline"]["traffic_source"] = src
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(U)
+    if not args.no_c3:
+        # the north-star headline config, sharded by source over the ranks
+        c3 = run_c3(args, torch, dist, rank, world, local_rank)
+        if rank == 0:
+            line["c3_fabric_all_sources"] = {
+                k: c3[k] for k in ("value", "unit", "ms_per_step", "kernel_ms",
+                                   "route_dbs_per_s", "gteps", "routes_per_step",
+                                   "route_digest", "roofline", "config")}
+            line["c3_fabric_all_sources"]["steps"] = c3["steps"]
+    if rank == 0:
         print(json.dumps(line), flush=True)
     if dist:
         dist.destroy_process_group()

@@ -1,0 +1,65 @@
+"""Multi-GPU sharding of SPF + RouteDb batches.
+
+The batch shards embarrassingly: topologies (C2), sources (C3), link-failure
+variants (C4) and destinations (C5) are independent units, so every rank
+solves its own block with NO data-path collective. The only collectives are
+one all-gather of per-rank {units, routes, digest} records and one MAX
+all-reduce of the elapsed time (RCCL over xGMI on the GPU box; gloo in the
+CPU tests). Nothing here touches a device: the helpers take whatever
+process group `torch.distributed` was initialised with.
+"""
+import hashlib
+
+DIGEST_FIELDS = 4  # units, routes, digest (63-bit), reserved
+
+
+def block_range(total, rank, world):
+    """Contiguous block [lo, hi) of ceil(total / world) units for `rank`."""
+    if world <= 0 or not 0 <= rank < world:
+        raise ValueError(f"bad rank {rank} / world {world}")
+    per = -(-total // world)
+    lo = min(total, rank * per)
+    return lo, min(total, lo + per)
+
+
+def interleave(items, rank, world):
+    """Round-robin share of `items` (C3: balances RSW/FSW/SSW degree classes
+    over ranks)."""
+    if world <= 0 or not 0 <= rank < world:
+        raise ValueError(f"bad rank {rank} / world {world}")
+    return list(items)[rank::world]
+
+
+def route_digest(*arrays):
+    """63-bit digest of a rank's route records (numpy arrays, in order)."""
+    h = hashlib.sha256()
+    for a in arrays:
+        h.update(memoryview(a).cast("B"))
+    return int.from_bytes(h.digest()[:8], "little") >> 1
+
+
+def combine_digests(digests):
+    """Order-independent combination of per-rank digests: XOR (each rank's
+    block is fixed by its rank, so XOR of the blocks is the whole job's)."""
+    out = 0
+    for d in digests:
+        out ^= int(d)
+    return out
+
+
+def reduce_stats(dist, torch, device, units, routes, digest, elapsed_s):
+    """All-gather per-rank {units, routes, digest}, MAX-reduce elapsed.
+    Returns (total_units, total_routes, combined_digest, max_elapsed_s,
+    per_rank list). With dist None (single process) it returns the inputs."""
+    local = torch.tensor([int(units), int(routes), int(digest), 0],
+                         dtype=torch.int64, device=device)
+    elapsed = torch.tensor([float(elapsed_s)], dtype=torch.float64, device=device)
+    if dist is None:
+        rows = [local.tolist()]
+    else:
+        gathered = [torch.zeros_like(local) for _ in range(dist.get_world_size())]
+        dist.all_gather(gathered, local)
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+        rows = [g.tolist() for g in gathered]
+    return (sum(r[0] for r in rows), sum(r[1] for r in rows),
+            combine_digests(r[2] for r in rows), float(elapsed.item()), rows)

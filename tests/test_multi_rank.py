@@ -1,0 +1,98 @@
+"""World-size-2 gloo tests of the multi-GPU path on CPU:
+every unit is solved by exactly one rank, and the all-gathered per-rank
+{units, routes, digest} records reproduce the single-process job. Route
+databases come from the CPU oracle here (the GPU product is covered by the
+-m gpu parity tests); what is under test is the sharding + reduction code
+bench.py runs on the GPU box."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from openr_amd import shard
+
+GRID = dict(n=6, metricSeed=0xC2000000, prefixSeed=0xC1)
+TOPOS = 10  # whole job
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _route_counts(dbs):
+    return sum(db.count(b"\n") for db in dbs)
+
+
+def _job_stats(oracle, lo, hi):
+    dbs = oracle.grid_batch_route_dbs(GRID, lo, hi, "1", False)
+    return hi - lo, _route_counts(dbs), shard.route_digest(*[bytearray(d) for d in dbs])
+
+
+def _worker(rank, world, port, out_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import _refcpu
+        lo, hi = shard.block_range(TOPOS, rank, world)
+        units, routes, digest = _job_stats(_refcpu, lo, hi)
+        res = shard.reduce_stats(dist, torch, torch.device("cpu"), units, routes, digest,
+                                 0.5 + rank)
+        fabric = shard.interleave([f"n{i}" for i in range(11)], rank, world)
+        gathered = [None] * world
+        dist.all_gather_object(gathered, fabric)
+        out_q.put((rank, res, gathered, (lo, hi)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_two_rank_gloo_matches_single_process(oracle):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    results.sort(key=lambda x: x[0])
+    # every rank sees the same reduced record
+    assert results[0][1][:4] == results[1][1][:4]
+    total_units, total_routes, digest, tmax, rows = results[0][1]
+    assert tmax == 1.5  # MAX over ranks
+    # blocks tile the job exactly once
+    assert [r[3] for r in results] == [(0, 5), (5, 10)]
+    # the gathered job equals the single-process job, rank by rank
+    expect = [_job_stats(oracle, lo, hi) for lo, hi in [(0, 5), (5, 10)]]
+    assert total_units == TOPOS
+    assert total_routes == sum(e[1] for e in expect)
+    assert digest == shard.combine_digests(e[2] for e in expect)
+    assert [tuple(r[:3]) for r in rows] == [tuple(e) for e in expect]
+    # C3-style interleave covers every source exactly once
+    got = sorted(x for part in results[0][2] for x in part)
+    assert got == sorted(f"n{i}" for i in range(11))
+
+
+@pytest.mark.parametrize("total,world", [(4096, 1), (4096, 8), (10, 3), (2, 4), (0, 2)])
+def test_block_range_tiles(total, world):
+    seen = []
+    for r in range(world):
+        lo, hi = shard.block_range(total, r, world)
+        assert 0 <= lo <= hi <= total
+        seen.extend(range(lo, hi))
+    assert seen == list(range(total))
+
+
+def test_bad_rank_rejected():
+    with pytest.raises(ValueError):
+        shard.block_range(10, 2, 2)
+    with pytest.raises(ValueError):
+        shard.interleave([1, 2], -1, 2)
