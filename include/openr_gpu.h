@@ -200,6 +200,24 @@ typedef struct ogs_path_out {
   uint32_t max_edges;
 } ogs_path_out;
 
+/* Multi-area routing domain (SpfSolver over several LinkStates, one per
+ * area: SpfSolver.cpp:160-311). The areas are the
+ * num_areas topologies of an ogs_graph batch; the domain has ONE prefix
+ * table (ogs_prefix_table with num_topos = 1: pfx_base[0..1]) whose
+ * advertisement segments list (node, area) entries in (node name, area
+ * name) order, adv_node holding the node's id in ITS OWN area. Node names
+ * are numbered across areas ("name ids") so the reference's by-name lookups
+ * of selected advertisers in every area (SpfSolver.cpp:664-665) are one
+ * table read. */
+typedef struct ogs_area_table {
+  int32_t num_areas;          /* A <= 32                                  */
+  int32_t num_names;          /* G distinct node names of the domain      */
+  const uint32_t* name_local; /* [G*A] id of name g in area a, or
+                                 OGS_NODE_NONE if a has no such node     */
+  const uint32_t* adv_area;   /* [A_total] area index of each entry       */
+  const uint32_t* adv_name;   /* [A_total] name id of each entry's node   */
+} ogs_area_table;
+
 /* ---- runtime ------------------------------------------------------------ */
 const char* ogs_version(void);
 const char* ogs_last_error(void); /* thread-local message of last failure */
@@ -262,6 +280,28 @@ int ogs_spf_routes(const ogs_graph* graph, const ogs_prefix_table* prefixes,
 int ogs_ksp_paths(const ogs_graph* graph, const ogs_path_unit* units,
                   int32_t n_units, const uint32_t* masks, uint32_t mask_words,
                   uint32_t flags, ogs_path_out* out, void* stream);
+
+/* Multi-area RouteDb for n_units sources from their per-area SPF results
+ * (a prior ogs_spf_routes launch over the area batch without a prefix
+ * table): units[u] = the source's name id; spf_row[u*A + a] = the row of
+ * (source, area a) in spf_dist / spf_nh (layouts of ogs_spf_out with
+ * S_n = graph->max_nodes and the same nh_words), OGS_NODE_NONE when the
+ * source has no adjacency database in area a (its SPF there is the source
+ * alone, LinkState.cpp:730-734). Outputs per unit as ogs_spf_out (meta,
+ * metric, sel over S_p = prefixes->max_prefixes) with one next-hop mask per
+ * area: mask[((U*A + a)*W + w)*S_p + p] over the source's links in area a.
+ * 32-bit distances only. Replaces createRouteForPrefix across areas
+ * (SpfSolver.cpp:160-311: per-area reachability, selectBestRoutes 455-486,
+ * areas with best routes, getNextHopsWithMetric per area 648-688, minimum
+ * metric union over areas, addBestPaths 595-639). */
+int ogs_routes_multiarea(const ogs_graph* graph,
+                         const ogs_prefix_table* prefixes,
+                         const ogs_area_table* areas,
+                         const uint32_t* units /* device, [n_units] */,
+                         int32_t n_units, const uint32_t* spf_row /* device */,
+                         const uint32_t* spf_dist, const uint32_t* spf_nh,
+                         uint32_t flags, int32_t nh_words, ogs_spf_out* out,
+                         void* stream);
 
 #ifdef __cplusplus
 }

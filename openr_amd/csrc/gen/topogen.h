@@ -394,4 +394,116 @@ inline Lsdb wan(const WanOpts& o) {
   return db;
 }
 
+// --------------------------------------------------------- multi-area ----
+// Build-defined multi-area WAN: `areas` WAN areas of
+// `nodesPerArea` nodes (the WAN generator, seed + a, node names "a<a>-<i>",
+// area names "area<a>"), plus `abrs` border routers "abr-<k>" present in two
+// areas under the same name, each linked to two nodes of both areas.
+// `prefixesPerNode` prefixes per node in its (first) area; a seeded per
+// mille of them anycast with 1-3 extra advertisers in random areas
+// (sometimes an ABR, which then advertises the prefix in that area).
+// PrefixMetrics path/source preference in {100, 200}, distance U[0, 10].
+struct MultiAreaOpts {
+  int areas{8}, nodesPerArea{1250}, abrs{64}, k{3};
+  uint64_t seed{0xC5A0};
+  int prefixesPerNode{10};
+  int anycastPermille{50};
+};
+
+inline std::vector<Lsdb> multiArea(const MultiAreaOpts& o) {
+  std::vector<Lsdb> out;
+  const int A = std::max(1, o.areas);
+  for (int a = 0; a < A; ++a) {
+    WanOpts w;
+    w.nodes = o.nodesPerArea;
+    w.k = o.k;
+    w.seed = o.seed + uint64_t(a);
+    w.prefixesPerNode = o.prefixesPerNode;
+    w.namePrefix = "a" + std::to_string(a) + "-";
+    out.push_back(wan(w));
+    out.back().area = "area" + std::to_string(a);
+  }
+  uint64_t s = o.seed ^ 0xab5eed;
+  auto metrics = [&](Prefix& p) {
+    p.path_preference = (splitmix64(s) & 1) ? 200 : 100;
+    p.source_preference = (splitmix64(s) & 1) ? 200 : 100;
+    p.distance = int32_t(splitmix64(s) % 11);
+  };
+  for (auto& db : out) {
+    for (auto& p : db.prefixes) metrics(p);
+  }
+  std::vector<std::vector<int>> abrAreas(o.abrs);
+  for (int k = 0; k < o.abrs; ++k) {
+    const int a1 = k % A;
+    const int a2 = A > 1 ? (a1 + 1 + (k / A) % (A - 1)) % A : a1;
+    abrAreas[k] = a1 == a2 ? std::vector<int>{a1} : std::vector<int>{a1, a2};
+    const std::string name = "abr-" + std::to_string(k);
+    for (int a : abrAreas[k]) {
+      Lsdb& db = out[a];
+      AdjDb d;
+      d.thisNodeName = name;
+      d.nodeLabel = 900000 + k;
+      const int n = int(db.adjDbs.size());
+      const int t1 = int(splitmix64(s) % uint64_t(n));
+      const int t2 = (t1 + 1 + int(splitmix64(s) % uint64_t(std::max(1, n - 1)))) % n;
+      for (int t : {t1, t2}) {
+        if (t == t1 && t == t2 && !d.adjs.empty()) continue;
+        AdjDb& nb = db.adjDbs[t];
+        if (!d.adjs.empty() && d.adjs.back().otherNodeName == nb.thisNodeName) continue;
+        const int32_t metric = 100 + int32_t(splitmix64(s) % 50);
+        Adj x;  // abr -> t
+        x.otherNodeName = nb.thisNodeName;
+        x.ifName = "if_" + name + "_" + nb.thisNodeName;
+        x.otherIfName = "if_" + nb.thisNodeName + "_" + name;
+        x.nextHopV6 = "fe80::ab:" + hex2(unsigned(t >> 8)) + hex2(unsigned(t & 0xff));
+        x.nextHopV4 = "10.200." + std::to_string(t >> 8) + "." + std::to_string(t & 0xff);
+        x.metric = metric;
+        x.adjLabel = 200001 + t;
+        d.adjs.push_back(x);
+        Adj y;  // t -> abr
+        y.otherNodeName = name;
+        y.ifName = x.otherIfName;
+        y.otherIfName = x.ifName;
+        y.nextHopV6 = "fe80::ab:ff" + hex2(unsigned(k & 0xff));
+        y.nextHopV4 = "10.201.0." + std::to_string(k & 0xff);
+        y.metric = metric;
+        y.adjLabel = 300001 + k;
+        nb.adjs.push_back(y);
+      }
+      db.adjDbs.push_back(std::move(d));
+    }
+    for (int i = 0; i < o.prefixesPerNode; ++i) {
+      Prefix p{name, seededV6Prefix(s)};
+      metrics(p);
+      out[abrAreas[k][0]].prefixes.push_back(p);
+    }
+  }
+  // anycast: extra advertisers of existing prefixes in random areas
+  std::vector<std::pair<int, size_t>> all;
+  for (int a = 0; a < A; ++a) {
+    for (size_t i = 0; i < out[a].prefixes.size(); ++i) all.emplace_back(a, i);
+  }
+  for (const auto& [a, i] : all) {
+    if (int(splitmix64(s) % 1000) >= o.anycastPermille) continue;
+    const std::string prefix = out[a].prefixes[i].prefix;
+    const int extra = 1 + int(splitmix64(s) % 3);
+    for (int e = 0; e < extra; ++e) {
+      Prefix q;
+      q.prefix = prefix;
+      int b = int(splitmix64(s) % uint64_t(A));
+      if (o.abrs > 0 && splitmix64(s) % 8 == 0) {
+        const int k = int(splitmix64(s) % uint64_t(o.abrs));
+        b = abrAreas[k][splitmix64(s) % abrAreas[k].size()];
+        q.node = "abr-" + std::to_string(k);
+      } else {
+        const auto& dbs = out[b].adjDbs;
+        q.node = dbs[splitmix64(s) % dbs.size()].thisNodeName;
+      }
+      metrics(q);
+      out[b].prefixes.push_back(q);
+    }
+  }
+  return out;
+}
+
 }  // namespace topogen

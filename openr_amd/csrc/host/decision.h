@@ -399,6 +399,21 @@ class SpfSolver {
   }
 
  private:
+  // several areas (SpfSolver.cpp:160-311 across LinkStates)
+  std::optional<DecisionRouteDb> buildRouteDbMultiArea(
+      const std::string& myNodeName, const AreaLinkStates& areaLinkStates,
+      const PrefixState& prefixState);
+  void prepareMultiArea(const AreaLinkStates& areaLinkStates,
+                        const PrefixState& prefixState);
+  struct MultiAreaResult {  // host copies of one source's GPU results
+    std::vector<uint32_t> row;  // [A] SPF row of each area or OGS_NODE_NONE
+    std::vector<uint32_t> dist32, nh, meta, metric, mask, sel;
+    int W{1};
+    size_t Sn{0}, P{0};
+  };
+  DecisionRouteDb materializeMultiArea(const std::string& myNodeName,
+                                       const AreaLinkStates& areaLinkStates,
+                                       const MultiAreaResult& r);
   struct Impl;
   std::unique_ptr<Impl> impl_;
   std::map<std::string, RibUnicastEntry> staticUnicastRoutes_;
@@ -496,6 +511,16 @@ struct PrefixHostTable {
 };
 
 bool wideDistancesNeeded(const FlatTopology& f);
+
+// label -> (owner node, route), the reference's labelToNode
+// (SpfSolver.cpp:356-358, duplicate labels: smallest owner name wins)
+using LabelRoutes = std::map<int32_t, std::pair<std::string, RibMplsEntry>>;
+// Node-label routes of one area from the source's SPF there (dist/nh as in
+// UnitView; dist == nullptr when the source has no SPF in that area).
+void addNodeLabelRoutes(const LinkState& ls, const FlatTopology& f,
+                        const std::string& area, const std::string& me,
+                        const uint64_t* dist, const uint32_t* nhWords,
+                        size_t nhStride, int W, LabelRoutes& labelToNode);
 
 DecisionRouteDb materializeRouteDb(
     const LinkState& ls, const FlatTopology& f, const std::string& area,

@@ -149,6 +149,24 @@ struct SpfSolver::Impl {
   uint64_t cachedPsVersion{~0ull}, cachedTopoVersion{~0ull};
   const FlatTopology* cachedTopo{nullptr};
   PrefixHostTable table;
+
+  // multi-area domain (buildRouteDbMultiArea): the areas' CSR as one graph
+  // batch + the domain prefix table with per-entry area / node-name ids
+  struct MultiArea {
+    std::vector<std::pair<const FlatTopology*, uint64_t>> topoKey;
+    const PrefixState* ps{nullptr};
+    uint64_t psVersion{~0ull};
+    std::vector<std::string> areas;  // area index -> name (map order)
+    std::vector<const FlatTopology*> flats;
+    HostBatch hb;
+    std::unordered_map<std::string, uint32_t> nameId;
+    uint32_t maxPrefixes{0}, numNames{0};
+    PrefixHostTable table;
+    DeviceBuffer nodeBase, rowPtr, edges, flags, edgeSrc, desc;
+    DeviceBuffer pfxBase, advOff, advNode, advMetrics, advMinNh, pfxFlags,
+        advArea, advName, nameLocal;
+    DeviceBuffer units, srcName, spfRow, dist, nh, meta, metric, mask, sel;
+  } ma;
 };
 
 SpfSolver::SpfSolver(const std::string& me, bool enableV4, bool sr, bool brs,
@@ -271,38 +289,9 @@ DecisionRouteDb materializeRouteDb(
 
   // node-label MPLS routes from the SPF result (SpfSolver.cpp:354-445)
   if (enableNodeSegmentLabel) {
-    std::map<int32_t, std::pair<std::string, RibMplsEntry>> labelToNode;
-    for (const auto& [node, adjDb] : ls.getAdjacencyDatabases()) {
-      const int32_t label = adjDb.nodeLabel;
-      const bool valid =
-          (static_cast<uint32_t>(label) & 0xfff00000u) == 0 && label != 0;
-      if (!valid) continue;
-      auto it = labelToNode.find(label);
-      if (it != labelToNode.end() && it->second.first < node) continue;
-      if (node == me) {
-        NextHopThrift nh;
-        nh.address = "::";
-        nh.area = area;
-        nh.mplsAction = MplsAction{POP_AND_LOOKUP, std::nullopt, std::nullopt};
-        labelToNode.erase(label);
-        labelToNode.emplace(label, std::make_pair(me, RibMplsEntry{label, {nh}}));
-        continue;
-      }
-      const uint32_t v = f.id.at(node);
-      if (r.dist[v] == ~0ull) continue;  // no route to the label owner
-      RibMplsEntry entry{label, {}};
-      const int32_t m32 = static_cast<int32_t>(r.dist[v]);
-      linksOf(&r.nh[v], r.nhStride, [&](const Link& l) {
-        const bool php = l.getOtherNodeName(me) == node;
-        entry.nexthops.insert(makeNh(
-            l, me, false, m32,
-            php ? MplsAction{PHP, std::nullopt, std::nullopt}
-                : MplsAction{SWAP, label, std::nullopt}));
-      });
-      if (entry.nexthops.empty()) continue;
-      labelToNode.erase(label);
-      labelToNode.emplace(label, std::make_pair(node, std::move(entry)));
-    }
+    LabelRoutes labelToNode;
+    addNodeLabelRoutes(ls, f, area, me, r.dist, r.nh, r.nhStride, r.W,
+                       labelToNode);
     for (auto& [label, ne] : labelToNode) {
       rdb.mplsRoutes.emplace(label, std::move(ne.second));
     }
@@ -310,11 +299,60 @@ DecisionRouteDb materializeRouteDb(
   return rdb;
 }
 
+void addNodeLabelRoutes(const LinkState& ls, const FlatTopology& f,
+                        const std::string& area, const std::string& me,
+                        const uint64_t* dist, const uint32_t* nhWords,
+                        size_t nhStride, int W, LabelRoutes& labelToNode) {
+  // SpfSolver.cpp:357-437, one area; dist == nullptr: the source has no
+  // SPF in this area (no adjacency database), every other owner unreachable
+  const auto sIt = f.id.find(me);
+  for (const auto& [node, adjDb] : ls.getAdjacencyDatabases()) {
+    const int32_t label = adjDb.nodeLabel;
+    const bool valid =
+        (static_cast<uint32_t>(label) & 0xfff00000u) == 0 && label != 0;
+    if (!valid) continue;
+    auto it = labelToNode.find(label);
+    if (it != labelToNode.end() && it->second.first < node) continue;
+    if (node == me) {
+      NextHopThrift nh;
+      nh.address = "::";
+      nh.area = area;
+      nh.mplsAction = MplsAction{POP_AND_LOOKUP, std::nullopt, std::nullopt};
+      labelToNode.erase(label);
+      labelToNode.emplace(label, std::make_pair(me, RibMplsEntry{label, {nh}}));
+      continue;
+    }
+    if (!dist || sIt == f.id.end()) continue;
+    const uint32_t v = f.id.at(node);
+    if (dist[v] == ~0ull) continue;  // no route to the label owner
+    RibMplsEntry entry{label, {}};
+    const int32_t m32 = static_cast<int32_t>(dist[v]);
+    const uint32_t rb = f.rowPtr[sIt->second];
+    for (int w = 0; w < W; ++w) {
+      uint32_t bits = nhWords[w * nhStride + v];
+      while (bits) {
+        const int b = __builtin_ctz(bits);
+        bits &= bits - 1;
+        const Link& l = *f.edgeLink[rb + w * 32 + b];
+        const bool php = l.getOtherNodeName(me) == node;
+        entry.nexthops.insert(makeNh(
+            l, me, false, m32,
+            php ? MplsAction{PHP, std::nullopt, std::nullopt}
+                : MplsAction{SWAP, label, std::nullopt}));
+      }
+    }
+    if (entry.nexthops.empty()) continue;
+    labelToNode.erase(label);
+    labelToNode.emplace(label, std::make_pair(node, std::move(entry)));
+  }
+}
+
 std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(
     const std::string& me, const AreaLinkStates& als, const PrefixState& ps) {
   bool exists = false;  // SpfSolver.cpp:318-324
   for (const auto& [_, l] : als) exists |= l.hasNode(me);
   if (!exists) return std::nullopt;
+  if (als.size() > 1) return buildRouteDbMultiArea(me, als, ps);
   std::string area;
   const LinkState& ls = singleArea(als, area);
   const FlatTopology& f = ls.flatOnDevice();
@@ -439,6 +477,281 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(
   return materializeRouteDb(ls, f, area, me, view, I.table, v4OverV6Nexthop_,
                             enableNodeSegmentLabel_, staticUnicastRoutes_,
                             &bestRoutesCache_);
+}
+
+// Domain tables of a multi-area buildRouteDb: the areas' CSR as one graph
+// batch (cached on the areas' topology versions) and the domain prefix table
+// with per-entry area and node-name ids (cached on the PrefixState version).
+void SpfSolver::prepareMultiArea(const AreaLinkStates& als, const PrefixState& ps) {
+  Impl::MultiArea& M = impl_->ma;
+  const uint32_t A = uint32_t(als.size());
+  std::vector<std::pair<const FlatTopology*, uint64_t>> key;
+  for (const auto& [area, ls] : als) {
+    const FlatTopology& f = ls.flat();
+    if (f.hasZeroMetric || f.hasWideMetric || wideDistancesNeeded(f)) {
+      throw std::domain_error(
+          "buildRouteDb: zero, negative or > 2^31 path metric is outside the "
+          "multi-area GPU path's exact domain");
+    }
+    key.emplace_back(&f, f.version);
+  }
+  const bool topoChanged = key != M.topoKey;
+  if (topoChanged) {
+    static const PrefixState kNoPrefixes;
+    M.areas.clear();
+    M.flats.clear();
+    M.hb = HostBatch();
+    for (const auto& [area, ls] : als) {
+      M.areas.push_back(area);
+      M.flats.push_back(&ls.flat());
+      M.hb.append(ls.flat(), kNoPrefixes, area);
+    }
+    M.nodeBase.upload(M.hb.nodeBase.data(), M.hb.nodeBase.size());
+    M.rowPtr.upload(M.hb.rowPtr.data(), M.hb.rowPtr.size());
+    M.edges.upload(M.hb.edges.data(), M.hb.edges.size());
+    M.flags.upload(M.hb.nodeFlags.data(), M.hb.nodeFlags.size());
+    M.edgeSrc.upload(M.hb.edgeSrc.data(), M.hb.edgeSrc.size());
+    M.desc.upload(M.hb.topoDesc.data(), M.hb.topoDesc.size());
+    M.topoKey = key;
+  }
+  if (!topoChanged && M.ps == &ps && M.psVersion == ps.version()) return;
+  M.nameId.clear();
+  std::vector<std::string> names;
+  auto nid = [&](const std::string& n) {
+    auto [it, fresh] = M.nameId.emplace(n, uint32_t(names.size()));
+    if (fresh) names.push_back(n);
+    return it->second;
+  };
+  for (const FlatTopology* f : M.flats) {
+    for (const auto& n : f->names) nid(n);
+  }
+  M.table.build(ps);
+  std::vector<uint32_t> advOff{0}, advNode, advArea, advName;
+  std::vector<int32_t> advMetrics;
+  std::vector<int64_t> advMinNh;
+  std::vector<uint8_t> pfxFlags;
+  for (const auto& [prefix, entries] : ps.prefixes()) {
+    bool anyMinNh = false;
+    for (const auto& [na, e] : entries) {
+      auto ait = std::find(M.areas.begin(), M.areas.end(), na.second);
+      if (ait == M.areas.end()) {  // areaLinkStates.at(area) throws there
+        throw std::out_of_range("prefix advertised in unknown area " + na.second);
+      }
+      const uint32_t a = uint32_t(ait - M.areas.begin());
+      const auto lit = M.flats[a]->id.find(na.first);
+      advNode.push_back(lit == M.flats[a]->id.end() ? OGS_NODE_NONE : lit->second);
+      advArea.push_back(a);
+      advName.push_back(nid(na.first));
+      advMetrics.insert(advMetrics.end(),
+                        {e->metrics.drain_metric, e->metrics.path_preference,
+                         e->metrics.source_preference, e->metrics.distance});
+      advMinNh.push_back(e->minNexthop ? *e->minNexthop : INT64_MIN);
+      anyMinNh |= e->minNexthop.has_value();
+    }
+    advOff.push_back(uint32_t(advNode.size()));
+    pfxFlags.push_back((isV4Prefix(prefix) ? OGS_PFX_V4 : 0u) |
+                       (anyMinNh ? OGS_PFX_HAS_MIN_NH : 0u));
+  }
+  M.numNames = uint32_t(names.size());
+  std::vector<uint32_t> nameLocal(size_t(M.numNames) * A, OGS_NODE_NONE);
+  for (uint32_t g = 0; g < M.numNames; ++g) {
+    for (uint32_t a = 0; a < A; ++a) {
+      auto it = M.flats[a]->id.find(names[g]);
+      if (it != M.flats[a]->id.end()) nameLocal[size_t(g) * A + a] = it->second;
+    }
+  }
+  M.maxPrefixes = uint32_t(pfxFlags.size());
+  const uint32_t pfxBase[2] = {0, M.maxPrefixes};
+  M.pfxBase.upload(pfxBase, 2);
+  M.advOff.upload(advOff.data(), advOff.size());
+  M.advNode.upload(advNode.data(), advNode.size());
+  M.advArea.upload(advArea.data(), advArea.size());
+  M.advName.upload(advName.data(), advName.size());
+  M.advMetrics.upload(advMetrics.data(), advMetrics.size());
+  M.advMinNh.upload(advMinNh.data(), advMinNh.size());
+  M.pfxFlags.upload(pfxFlags.data(), pfxFlags.size());
+  M.nameLocal.upload(nameLocal.data(), nameLocal.size());
+  M.ps = &ps;
+  M.psVersion = ps.version();
+}
+
+// Per-area masks -> next hops over that area's links; MPLS node labels of
+// every area in map order (SpfSolver.cpp:354-445).
+DecisionRouteDb SpfSolver::materializeMultiArea(const std::string& me,
+                                                const AreaLinkStates& als,
+                                                const MultiAreaResult& R) {
+  Impl::MultiArea& M = impl_->ma;
+  const uint32_t A = uint32_t(als.size());
+  const int W = R.W;
+  const size_t Sn = R.Sn, P = R.P;
+  DecisionRouteDb rdb;
+  bestRoutesCache_.clear();
+  const PrefixHostTable& pt = M.table;
+  for (uint32_t p = 0; p < P; ++p) {
+    const uint32_t m = R.meta[p];
+    const uint32_t a0 = pt.advOff[p];
+    const uint32_t best = a0 + (m >> OGS_ROUTE_BEST_SHIFT);
+    if (m & OGS_ROUTE_SELECTED) {  // SpfSolver.cpp:247
+      RouteSelectionResult rs;
+      for (uint32_t a = a0; a < std::min(pt.advOff[p + 1], a0 + 32); ++a) {
+        if (R.sel[p] >> (a - a0) & 1u) rs.allNodeAreas.insert(pt.advKey[a]);
+      }
+      rs.bestNodeArea = pt.advKey[best];
+      rs.isBestNodeDrained = m & OGS_ROUTE_DRAINED;
+      bestRoutesCache_[pt.prefixes[p]] = std::move(rs);
+    }
+    if (!(m & OGS_ROUTE_VALID)) continue;
+    RibUnicastEntry e;
+    e.prefix = pt.prefixes[p];
+    const bool useV4 = isV4Prefix(e.prefix) && !v4OverV6Nexthop_;
+    const int32_t m32 = static_cast<int32_t>(R.metric[p]);
+    for (uint32_t a = 0; a < A; ++a) {
+      if (R.row[a] == OGS_NODE_NONE) continue;
+      const FlatTopology& f = *M.flats[a];
+      const uint32_t rb = f.rowPtr[f.id.at(me)];
+      for (int w = 0; w < W; ++w) {
+        uint32_t bits = R.mask[(size_t(a) * W + w) * P + p];
+        while (bits) {
+          const int b = __builtin_ctz(bits);
+          bits &= bits - 1;
+          e.nexthops.insert(makeNh(*f.edgeLink[rb + w * 32 + b], me, useV4, m32,
+                                   std::nullopt));
+        }
+      }
+    }
+    e.bestPrefixEntry = *pt.advEntry[best];
+    if (m & OGS_ROUTE_DRAINED) e.bestPrefixEntry.metrics.drain_metric = 1;
+    e.bestPrefixEntry.weight = std::nullopt;  // RibEntry.h:77
+    e.bestArea = pt.advKey[best].second;
+    e.igpCost = static_cast<unsigned int>(R.metric[p]);
+    e.localRouteConsidered = m & OGS_ROUTE_LOCAL;
+    rdb.unicastRoutes.emplace(e.prefix, std::move(e));
+  }
+  for (const auto& [prefix, e] : staticUnicastRoutes_) {  // SpfSolver.cpp:343-349
+    if (!rdb.unicastRoutes.count(prefix)) rdb.unicastRoutes.emplace(prefix, e);
+  }
+  if (enableNodeSegmentLabel_) {
+    LabelRoutes labelToNode;
+    std::vector<uint64_t> d64(Sn);
+    uint32_t a = 0;
+    for (const auto& [area, ls] : als) {
+      const uint64_t* dist = nullptr;
+      const uint32_t* nhw = nullptr;
+      if (R.row[a] != OGS_NODE_NONE) {
+        for (size_t v = 0; v < Sn; ++v) {
+          const uint32_t d = R.dist32[R.row[a] * Sn + v];
+          d64[v] = d == 0xFFFFFFFFu ? ~0ull : d;
+        }
+        dist = d64.data();
+        nhw = &R.nh[size_t(R.row[a]) * W * Sn];
+      }
+      addNodeLabelRoutes(ls, *M.flats[a], area, me, dist, nhw, Sn, W, labelToNode);
+      ++a;
+    }
+    for (auto& [label, ne] : labelToNode) {
+      rdb.mplsRoutes.emplace(label, std::move(ne.second));
+    }
+  }
+  return rdb;
+}
+
+std::optional<DecisionRouteDb> SpfSolver::buildRouteDbMultiArea(
+    const std::string& me, const AreaLinkStates& als, const PrefixState& ps) {
+  if (als.size() > 32) throw std::domain_error("buildRouteDb: more than 32 areas");
+  prepareMultiArea(als, ps);
+  Impl::MultiArea& M = impl_->ma;
+  const uint32_t A = uint32_t(als.size());
+  MultiAreaResult R;
+
+  // ---- SPF of the source in every area holding it (one launch) -----------
+  std::vector<ogs_unit> su;
+  R.row.assign(A, OGS_NODE_NONE);
+  for (uint32_t a = 0; a < A; ++a) {
+    const FlatTopology& f = *M.flats[a];
+    auto it = f.id.find(me);
+    if (it == f.id.end()) continue;
+    R.row[a] = uint32_t(su.size());
+    su.push_back({a, it->second});
+    const int deg = int(f.rowPtr[it->second + 1] - f.rowPtr[it->second]);
+    R.W = std::max(R.W, std::max(1, ogs_nh_words_for_degree(deg)));
+  }
+  const int W = R.W;
+  R.Sn = size_t(std::max(M.hb.maxNodes, 1));
+  R.P = M.maxPrefixes;
+  const size_t Sn = R.Sn, P = R.P, P1 = std::max<size_t>(P, 1);
+  const uint32_t S = M.nameId.at(me);
+  M.units.upload(su.data(), su.size());
+  M.spfRow.upload(R.row.data(), R.row.size());
+  M.srcName.upload(&S, 1);
+  M.dist.resize(su.size() * Sn * 4);
+  M.nh.resize(su.size() * W * Sn * 4);
+  M.meta.resize(P1 * 4);
+  M.metric.resize(P1 * 4);
+  M.mask.resize(P1 * A * W * 4);
+  M.sel.resize(P1 * 4);
+  ogs_graph g{};
+  g.num_topos = int32_t(A);
+  g.max_nodes = int32_t(Sn);
+  g.max_edges = M.hb.maxEdges;
+  g.max_degree = M.hb.maxDegree;
+  g.node_base = M.nodeBase.as<uint32_t>();
+  g.row_ptr = M.rowPtr.as<uint32_t>();
+  g.edges = M.edges.as<uint64_t>();
+  g.node_flags = M.flags.as<uint8_t>();
+  g.topo_desc = M.desc.as<uint32_t>();
+  g.edge_src = M.edgeSrc.as<uint32_t>();
+  const uint32_t flags = (enableV4_ ? OGS_F_ENABLE_V4 : 0u) |
+      (v4OverV6Nexthop_ ? OGS_F_V4_OVER_V6 : 0u) |
+      (enableBestRouteSelection_ ? OGS_F_BEST_ROUTE_SELECTION : 0u);
+  ogs_spf_out spf{};
+  spf.dist = M.dist.get();
+  spf.nh = M.nh.as<uint32_t>();
+  ogsCheck(ogs_spf_routes(&g, nullptr, M.units.as<ogs_unit>(), int32_t(su.size()),
+                          flags, W, &spf, nullptr),
+           "ogs_spf_routes");
+  for (const auto& [area, ls] : als) {
+    if (ls.flat().id.count(me)) ls.noteSpfRuns(1);
+  }
+
+  // ---- multi-area RouteDb --------------------------------------------------
+  if (P) {
+    ogs_prefix_table pt{};
+    pt.max_prefixes = int32_t(P);
+    pt.max_advertisements = int32_t(M.table.advEntry.size());
+    pt.pfx_base = M.pfxBase.as<uint32_t>();
+    pt.adv_off = M.advOff.as<uint32_t>();
+    pt.adv_node = M.advNode.as<uint32_t>();
+    pt.adv_metrics = M.advMetrics.as<int32_t>();
+    pt.adv_min_nh = M.advMinNh.as<int64_t>();
+    pt.pfx_flags = M.pfxFlags.as<uint8_t>();
+    ogs_area_table at{int32_t(A), int32_t(M.numNames), M.nameLocal.as<uint32_t>(),
+                      M.advArea.as<uint32_t>(), M.advName.as<uint32_t>()};
+    ogs_spf_out out{};
+    out.meta = M.meta.as<uint32_t>();
+    out.metric = M.metric.get();
+    out.mask = M.mask.as<uint32_t>();
+    out.sel = M.sel.as<uint32_t>();
+    ogsCheck(ogs_routes_multiarea(&g, &pt, &at, M.srcName.as<uint32_t>(), 1,
+                                  M.spfRow.as<uint32_t>(), M.dist.as<uint32_t>(),
+                                  M.nh.as<uint32_t>(), flags, W, &out, nullptr),
+             "ogs_routes_multiarea");
+  }
+  R.dist32.resize(su.size() * Sn);
+  R.nh.resize(su.size() * W * Sn);
+  R.meta.resize(P);
+  R.metric.resize(P);
+  R.mask.resize(P * A * W);
+  R.sel.resize(P);
+  M.dist.download(R.dist32.data(), R.dist32.size());
+  M.nh.download(R.nh.data(), R.nh.size());
+  if (P) {
+    M.meta.download(R.meta.data(), P);
+    M.metric.download(R.metric.data(), P);
+    M.mask.download(R.mask.data(), R.mask.size());
+    M.sel.download(R.sel.data(), P);
+  }
+  ogsCheck(ogs_stream_sync(nullptr), "ogs_stream_sync");
+  return materializeMultiArea(me, als, R);
 }
 
 std::optional<RibUnicastEntry> SpfSolver::createRouteForPrefixOrGetStaticRoute(

@@ -17,6 +17,12 @@ hipError_t launch_spf_routes(const ogs_graph& g, const ogs_prefix_table* pt,
                              const ogs_unit* units, int nUnits, uint32_t flags,
                              int W, const ogs_spf_out& out, hipStream_t stream,
                              int* unsupported);
+hipError_t launch_routes_multiarea(const ogs_graph& g, const ogs_prefix_table& pt,
+                                   const ogs_area_table& at,
+                                   const uint32_t* units, int n,
+                                   const uint32_t* spfRow, const uint32_t* dist,
+                                   const uint32_t* nh, uint32_t flags, int W,
+                                   const ogs_spf_out& out, hipStream_t stream);
 hipError_t launch_ksp(const ogs_graph& g, const ogs_path_unit* units,
                       int nUnits, const uint32_t* masks, uint32_t maskWords,
                       uint32_t flags, const ogs_path_out& out,
@@ -219,6 +225,41 @@ int ogs_ksp_paths(const ogs_graph* graph, const ogs_path_unit* units,
     return fail(OGS_E_UNSUPPORTED, "topology too large for the LDS KSP path");
   }
   return e == hipSuccess ? OGS_OK : hipFail(e, "ksp launch");
+}
+
+int ogs_routes_multiarea(const ogs_graph* graph,
+                         const ogs_prefix_table* prefixes,
+                         const ogs_area_table* areas, const uint32_t* units,
+                         int32_t n_units, const uint32_t* spf_row,
+                         const uint32_t* spf_dist, const uint32_t* spf_nh,
+                         uint32_t flags, int32_t nh_words, ogs_spf_out* out,
+                         void* stream) {
+  if (!graph || !prefixes || !areas || !out) {
+    return fail(OGS_E_INVALID, "graph/prefixes/areas/out is NULL");
+  }
+  if (n_units < 0) return fail(OGS_E_INVALID, "n_units < 0");
+  if (n_units == 0) return OGS_OK;
+  if (!units || !spf_row || !spf_dist || !spf_nh || !graph->node_base ||
+      !graph->node_flags || !areas->name_local || !areas->adv_area ||
+      !areas->adv_name || !prefixes->pfx_base || !prefixes->adv_off ||
+      !prefixes->adv_node || !prefixes->adv_metrics || !prefixes->adv_min_nh ||
+      !prefixes->pfx_flags) {
+    return fail(OGS_E_INVALID, "multi-area input arrays are NULL");
+  }
+  if (areas->num_areas <= 0 || areas->num_areas > 32 ||
+      areas->num_areas > graph->num_topos) {
+    return fail(OGS_E_INVALID, "num_areas outside [1, min(32, num_topos)]");
+  }
+  if (flags & OGS_F_WIDE_METRIC) {
+    return fail(OGS_E_UNSUPPORTED, "multi-area RouteDb uses 32-bit distances");
+  }
+  if (ogs_nh_words_for_degree(nh_words * 32) != nh_words) {
+    return fail(OGS_E_UNSUPPORTED, "nh_words must be 1, 2, 4, 8 or 16");
+  }
+  hipError_t e = ogs::launch_routes_multiarea(
+      *graph, *prefixes, *areas, units, n_units, spf_row, spf_dist, spf_nh,
+      flags, nh_words, *out, static_cast<hipStream_t>(stream));
+  return e == hipSuccess ? OGS_OK : hipFail(e, "multi-area route launch");
 }
 
 }  // extern "C"

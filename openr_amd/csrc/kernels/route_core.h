@@ -125,19 +125,26 @@ __device__ void route_one(const ogs_prefix_table& pt, uint32_t gp, uint32_t s,
   // selected set: self?, best = smallest (node, area) key (node ids are name
   // ranks), shortest distance over all selected names (SpfSolver.cpp:664-677)
   bool self = false;
-  uint32_t bestIdx = 0, bestNode = 0xFFFFFFFFu;
+  uint32_t bestIdx = 0, bestNode = 0xFFFFFFFFu, selfIdx = 0;
   D shortest = kInf;
   for (uint32_t a = a0; a < a1; ++a) {
     const uint32_t n = pt.adv_node[a];
     if (!selected(a, n)) continue;
     if (a - a0 < 32) selBits |= 1u << (a - a0);
-    if (n == s) self = true;
+    if (n == s && !self) {
+      self = true;
+      selfIdx = a - a0;
+    }
     if (n < bestNode) {
       bestNode = n;
       bestIdx = a - a0;
     }
     const D dn = sv.dist(n);
     if (dn < shortest) shortest = dn;
+  }
+  if (cfg.bestRouteSel && self) {  // selectBestNodeArea (LsdbUtil.cpp:700-711)
+    bestNode = s;
+    bestIdx = selfIdx;
   }
   meta |= OGS_ROUTE_SELECTED | (bestIdx << OGS_ROUTE_BEST_SHIFT);
   if (nflags[bestNode] & (OGS_NODE_OVERLOADED | OGS_NODE_METRICINC)) {

@@ -545,6 +545,46 @@ PYBIND11_MODULE(_refcpu, m) {
 
   // ---- bulk workloads ------------------------------------------------------
   // Build one generated LSDB and return canonical route DBs for `sources`.
+  // Multi-area domain (topogen::multiArea): canonical RouteDbs per source.
+  m.def("gen_route_dbs_multiarea",
+        [](py::dict d, std::vector<std::string> sources, bool enableV4, bool sr,
+           bool brs) {
+          topogen::MultiAreaOpts o;
+          o.areas = get<int>(d, "areas", 8);
+          o.nodesPerArea = get<int>(d, "nodesPerArea", 1250);
+          o.abrs = get<int>(d, "abrs", 64);
+          o.k = get<int>(d, "k", 3);
+          o.seed = get<uint64_t>(d, "seed", 0xC5A0);
+          o.prefixesPerNode = get<int>(d, "prefixesPerNode", 10);
+          o.anycastPermille = get<int>(d, "anycastPermille", 50);
+          auto lsdbs = topogen::multiArea(o);
+          AreaLinkStates als;
+          PrefixState ps;
+          for (size_t a = 0; a < lsdbs.size(); ++a) {
+            topogen::applyOverloads(lsdbs[a], get<int>(d, "adjOverloadPermille", 0),
+                                    get<int>(d, "nodeOverloadPermille", 0),
+                                    get<uint64_t>(d, "overloadSeed", 0x0F) + a);
+            topogen::PrefixMix m;
+            m.v4Permille = get<int>(d, "v4Permille", 0);
+            m.minNhPermille = get<int>(d, "minNhPermille", 0);
+            m.drainPermille = get<int>(d, "drainPermille", 0);
+            m.seed = get<uint64_t>(d, "mixSeed", 0x3F) + a;
+            topogen::applyPrefixMix(lsdbs[a], m);
+            auto& ls = als.emplace(lsdbs[a].area, LinkState(lsdbs[a].area, "test_node"))
+                           .first->second;
+            loadLsdb(lsdbs[a], ls, ps);
+          }
+          SpfSolver solver("test_node", enableV4, sr, brs);
+          std::vector<py::bytes> out;
+          for (const auto& s : sources) {
+            auto db = solver.buildRouteDb(s, als, ps);
+            out.push_back(py::bytes(db ? canonical(*db) : std::string("NONE")));
+          }
+          return out;
+        },
+        py::arg("opts"), py::arg("sources"), py::arg("enableV4") = true,
+        py::arg("sr") = false, py::arg("brs") = false);
+
   m.def("gen_route_dbs",
         [](const std::string& kind, py::dict opts, std::vector<std::string> sources,
            bool enableV4, bool sr, bool bestRouteSel) {

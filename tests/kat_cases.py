@@ -683,3 +683,7 @@ ALL_KATS = [
     kat_interface_soft_drain, kat_simple_ring, kat_parallel_adj_ring, kat_grid,
     kat_rib_policy,
 ]
+
+# multi-area known-answer tests (tests/kat_multiarea.py)
+from kat_multiarea import MULTI_AREA_KATS  # noqa: E402
+ALL_KATS += MULTI_AREA_KATS

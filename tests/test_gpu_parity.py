@@ -370,3 +370,28 @@ def test_route_stream_unaligned_prefix_rows(product, oracle):
     srcs = names[::7]
     a = _batch_dbs(product, "fabric", opts, srcs, True, False)
     _cmp(a, oracle.gen_route_dbs("fabric", opts, srcs, True, False, False), "fabric_tail")
+
+
+MA = dict(areas=3, nodesPerArea=60, abrs=6, prefixesPerNode=2, anycastPermille=200)
+
+
+@pytest.mark.parametrize("enable_v4,sr,brs", [(True, False, False), (True, True, True),
+                                              (False, False, True)])
+def test_multi_area_domain(product, oracle, enable_v4, sr, brs):
+    """Multi-area domain (3 WAN areas + 6 ABRs in two areas each, anycast
+    across areas, overloads, v4 / minNexthop / drain prefix mix): per-source
+    RouteDbs through SPF-per-area + the multi-area route kernel, bit-exact
+    vs the oracle (incl. node-label MPLS routes with SR on)."""
+    opts = dict(MA, nodeOverloadPermille=20, adjOverloadPermille=20, v4Permille=100,
+                minNhPermille=50, drainPermille=50)
+    srcs = ["abr-0", "abr-3", "abr-5", "a0-7", "a1-33", "a2-59", "a2-0"]
+    _cmp(product.gen_route_dbs_multiarea(opts, srcs, enable_v4, sr, brs),
+         oracle.gen_route_dbs_multiarea(opts, srcs, enable_v4, sr, brs), "multiarea")
+
+
+def test_multi_area_large_areas(product, oracle):
+    """Areas above the wave kernel's size (frontier SPF per area)."""
+    opts = dict(areas=2, nodesPerArea=400, abrs=4, prefixesPerNode=1, anycastPermille=100)
+    srcs = ["abr-1", "a1-399", "a0-5"]
+    _cmp(product.gen_route_dbs_multiarea(opts, srcs, True, False, True),
+         oracle.gen_route_dbs_multiarea(opts, srcs, True, False, True), "multiarea400")

@@ -44,3 +44,14 @@ def test_oracle_spf_runs_counter(oracle):
     solver = oracle.SpfSolver("1", False, True)
     L.getRouteMap(solver, ["1", "2", "3", "4"], als, ps)
     assert ls.spfRuns() == 4
+
+
+def test_oracle_multi_area_generator(oracle):
+    """The multi-area generator builds a connected domain: an ABR reaches
+    prefixes in both of its areas, a plain node only its own area + anycast."""
+    opts = dict(areas=3, nodesPerArea=40, abrs=6, prefixesPerNode=1, anycastPermille=0)
+    abr, plain = oracle.gen_route_dbs_multiarea(opts, ["abr-0", "a2-3"], True, False, False)
+    n_abr = abr.count(b"\nU ") + abr.startswith(b"U ")
+    n_plain = plain.count(b"\nU ") + plain.startswith(b"U ")
+    assert n_abr >= 2 * 40 - 2  # two areas' worth of routes
+    assert 30 <= n_plain < n_abr
