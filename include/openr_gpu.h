@@ -281,6 +281,47 @@ int ogs_ksp_paths(const ogs_graph* graph, const ogs_path_unit* units,
                   int32_t n_units, const uint32_t* masks, uint32_t mask_words,
                   uint32_t flags, ogs_path_out* out, void* stream);
 
+/* Link-failure variants (config C4, the SURVEY §5 "link-flap variant"):
+ * per unit, topology-local DIRECTED edge ids that are treated as removed --
+ * the links an adjacency-database update deleted at both ends
+ * (LinkState::updateAdjacencyDatabase, LinkState.cpp:491-634; list both
+ * directions of each link). OGS_NODE_NONE pads a unit's list. Next-hop
+ * link slots stay those of the unmodified CSR row, so a variant's records
+ * compare slot for slot with the base's. */
+typedef struct ogs_unit_mods {
+  const uint32_t* dead_edges; /* [n_units * dead_per_unit]            */
+  int32_t dead_per_unit;      /* 1..8                                  */
+} ogs_unit_mods;
+
+/* Route diff of every unit against ONE base unit's route records (same
+ * topology, source and prefix table): DecisionRouteDb::calculateUpdate
+ * (SpfSolver.cpp:21-56) with RibUnicastEntry::operator== (RibEntry.h:81-87):
+ * a route is updated when it is new or its best entry (+ drain override),
+ * local flag or next-hop set (metric and link mask) differ; igpCost and
+ * bestArea are not compared. */
+typedef struct ogs_route_diff {
+  const uint32_t* base_meta;   /* [S_p]                                 */
+  const uint32_t* base_metric; /* [S_p]                                 */
+  const uint32_t* base_mask;   /* [W * S_p]                             */
+  uint32_t* changed;           /* [n_units * ceil(S_p/32)] bit p set iff
+                                  prefix p's route is added, updated or
+                                  deleted (zeroed by the call)          */
+  uint32_t* counts;            /* [n_units * 2] {routes to update,
+                                  routes to delete}                     */
+} ogs_route_diff;
+
+/* Batched SPF + RouteDb of link-failure variants with an optional route
+ * diff (mods / diff may be NULL). Large-topology path only (graph->edge_src
+ * required, nh_words 1, 2 or 4, 32-bit distances); OGS_E_UNSUPPORTED
+ * otherwise. Replaces, per variant, the reference's adjacency-DB update +
+ * buildRouteDb + calculateUpdate. */
+int ogs_spf_routes_variants(const ogs_graph* graph,
+                            const ogs_prefix_table* prefixes,
+                            const ogs_unit* units /* device */, int32_t n_units,
+                            const ogs_unit_mods* mods,
+                            const ogs_route_diff* diff, uint32_t flags,
+                            int32_t nh_words, ogs_spf_out* out, void* stream);
+
 /* Multi-area RouteDb for n_units sources from their per-area SPF results
  * (a prior ogs_spf_routes launch over the area batch without a prefix
  * table): units[u] = the source's name id; spf_row[u*A + a] = the row of

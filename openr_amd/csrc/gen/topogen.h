@@ -19,6 +19,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
+#include <map>
 #include <numeric>
 #include <string>
 #include <vector>
@@ -392,6 +393,76 @@ inline Lsdb wan(const WanOpts& o) {
     }
   }
   return db;
+}
+
+// ------------------------------------------------ link-failure variants ----
+// Config C4: each variant removes 1 or 2 distinct links
+// (dualPermille of them 2), i.e. the adjacency on BOTH ends, seeded.
+struct LinkRef {
+  std::string a, ifA, b, ifB;  // adjacency (a, ifA) <-> (b, ifB)
+};
+
+inline std::vector<LinkRef> bidirectionalLinks(const Lsdb& db) {
+  std::vector<LinkRef> out;
+  std::map<std::string, const AdjDb*> byName;
+  for (const auto& d : db.adjDbs) byName[d.thisNodeName] = &d;
+  for (const auto& d : db.adjDbs) {
+    for (const auto& x : d.adjs) {
+      if (!(d.thisNodeName < x.otherNodeName)) continue;
+      auto it = byName.find(x.otherNodeName);
+      if (it == byName.end()) continue;
+      for (const auto& y : it->second->adjs) {
+        if (y.otherNodeName == d.thisNodeName && y.ifName == x.otherIfName &&
+            y.otherIfName == x.ifName) {
+          out.push_back({d.thisNodeName, x.ifName, x.otherNodeName, y.ifName});
+          break;
+        }
+      }
+    }
+  }
+  return out;
+}
+
+inline std::vector<std::vector<LinkRef>> linkFailureVariants(const Lsdb& db,
+                                                             int count,
+                                                             uint64_t seed,
+                                                             int dualPermille) {
+  const auto links = bidirectionalLinks(db);
+  std::vector<std::vector<LinkRef>> out;
+  if (links.empty()) return out;
+  uint64_t s = seed;
+  for (int v = 0; v < count; ++v) {
+    std::vector<LinkRef> fail{links[splitmix64(s) % links.size()]};
+    if (links.size() > 1 && int(splitmix64(s) % 1000) < dualPermille) {
+      size_t j = splitmix64(s) % links.size();
+      while (links[j].a == fail[0].a && links[j].ifA == fail[0].ifA) {
+        j = (j + 1) % links.size();
+      }
+      fail.push_back(links[j]);
+    }
+    out.push_back(std::move(fail));
+  }
+  return out;
+}
+
+// The LSDB with the variant's adjacencies removed at both ends.
+inline Lsdb withoutLinks(const Lsdb& db, const std::vector<LinkRef>& fail) {
+  Lsdb out = db;
+  for (auto& d : out.adjDbs) {
+    auto& v = d.adjs;
+    v.erase(std::remove_if(v.begin(), v.end(),
+                           [&](const Adj& x) {
+                             for (const auto& f : fail) {
+                               if ((d.thisNodeName == f.a && x.ifName == f.ifA) ||
+                                   (d.thisNodeName == f.b && x.ifName == f.ifB)) {
+                                 return true;
+                               }
+                             }
+                             return false;
+                           }),
+            v.end());
+  }
+  return out;
 }
 
 // --------------------------------------------------------- multi-area ----

@@ -23,6 +23,11 @@ hipError_t launch_routes_multiarea(const ogs_graph& g, const ogs_prefix_table& p
                                    const uint32_t* spfRow, const uint32_t* dist,
                                    const uint32_t* nh, uint32_t flags, int W,
                                    const ogs_spf_out& out, hipStream_t stream);
+hipError_t launch_variants(const ogs_graph& g, const ogs_prefix_table& pt,
+                           const ogs_unit* units, int nUnits,
+                           const ogs_unit_mods* mods, const ogs_route_diff* diff,
+                           uint32_t flags, int W, const ogs_spf_out& out,
+                           hipStream_t stream, int* unsupported);
 hipError_t launch_ksp(const ogs_graph& g, const ogs_path_unit* units,
                       int nUnits, const uint32_t* masks, uint32_t maskWords,
                       uint32_t flags, const ogs_path_out& out,
@@ -225,6 +230,46 @@ int ogs_ksp_paths(const ogs_graph* graph, const ogs_path_unit* units,
     return fail(OGS_E_UNSUPPORTED, "topology too large for the LDS KSP path");
   }
   return e == hipSuccess ? OGS_OK : hipFail(e, "ksp launch");
+}
+
+int ogs_spf_routes_variants(const ogs_graph* graph,
+                            const ogs_prefix_table* prefixes,
+                            const ogs_unit* units, int32_t n_units,
+                            const ogs_unit_mods* mods,
+                            const ogs_route_diff* diff, uint32_t flags,
+                            int32_t nh_words, ogs_spf_out* out, void* stream) {
+  if (!graph || !prefixes || !out) return fail(OGS_E_INVALID, "graph/prefixes/out is NULL");
+  if (n_units < 0) return fail(OGS_E_INVALID, "n_units < 0");
+  if (n_units == 0) return OGS_OK;
+  if (!units || !graph->node_base || !graph->row_ptr || !graph->edges ||
+      !graph->node_flags || !prefixes->pfx_base || !prefixes->adv_off ||
+      !prefixes->adv_node || !prefixes->adv_metrics || !prefixes->adv_min_nh ||
+      !prefixes->pfx_flags) {
+    return fail(OGS_E_INVALID, "graph / prefix table arrays are NULL");
+  }
+  if (mods && (!mods->dead_edges || mods->dead_per_unit < 1 || mods->dead_per_unit > 8)) {
+    return fail(OGS_E_INVALID, "mods: dead_edges NULL or dead_per_unit outside [1, 8]");
+  }
+  if (diff && (!diff->base_meta || !diff->base_metric || !diff->base_mask ||
+               !diff->changed || !diff->counts)) {
+    return fail(OGS_E_INVALID, "diff arrays are NULL");
+  }
+  if (graph->max_nodes <= 0 || uint32_t(graph->max_nodes) > OGS_MAX_NODES_PER_TOPO) {
+    return fail(OGS_E_UNSUPPORTED, "max_nodes outside (0, 2^21]");
+  }
+  if (ogs_nh_words_for_degree(nh_words * 32) != nh_words) {
+    return fail(OGS_E_UNSUPPORTED, "nh_words must be 1, 2, 4, 8 or 16");
+  }
+  int unsupported = 0;
+  hipError_t e = ogs::launch_variants(*graph, *prefixes, units, n_units, mods, diff,
+                                      flags, nh_words, *out,
+                                      static_cast<hipStream_t>(stream), &unsupported);
+  if (unsupported) {
+    return fail(OGS_E_UNSUPPORTED,
+                "variants need the large-topology path (edge_src, nh_words <= 4, "
+                "32-bit distances)");
+  }
+  return e == hipSuccess ? OGS_OK : hipFail(e, "variant launch");
 }
 
 int ogs_routes_multiarea(const ogs_graph* graph,

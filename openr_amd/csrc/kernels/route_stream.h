@@ -58,16 +58,46 @@ struct Rec {
   uint32_t meta, metric, mask[W], sel;
 };
 
+// Route diff against a base unit (ogs_route_diff; calculateUpdate,
+// SpfSolver.cpp:21-56, RibUnicastEntry::operator==, RibEntry.h:81-87).
+struct DiffCtx {
+  const uint32_t* bMeta;    // [Sp]
+  const uint32_t* bMetric;  // [Sp]
+  const uint32_t* bMask;    // [W][Sp]
+  uint32_t* changed;        // this unit's bitmap row (zeroed)
+  uint32_t* counts;         // LDS {update, delete} accumulators
+};
+
+template <int W>
+__device__ __forceinline__ bool route_changed(const Rec<W>& r, const DiffCtx& d,
+                                              uint32_t Sp, uint32_t p,
+                                              uint32_t& upd, uint32_t& del) {
+  constexpr uint32_t kEq = OGS_ROUTE_DRAINED | OGS_ROUTE_LOCAL |
+      (0xFFFFFFu << OGS_ROUTE_BEST_SHIFT);
+  const uint32_t bm = d.bMeta[p];
+  const bool va = r.meta & OGS_ROUTE_VALID, vb = bm & OGS_ROUTE_VALID;
+  bool ch = va != vb;
+  if (va && vb) {
+    ch = ((r.meta ^ bm) & kEq) != 0u || r.metric != d.bMetric[p];
+#pragma unroll
+    for (int w = 0; w < W; ++w) ch |= r.mask[w] != d.bMask[size_t(w) * Sp + p];
+  }
+  upd += (va && ch) ? 1u : 0u;
+  del += (vb && !va) ? 1u : 0u;
+  return ch;
+}
+
 // Streams unit u's P route records (rows of stride Sp). rec(v, r) fills
 // meta / metric / mask of node v's record; sv is the unit's SPF state for
 // route_one. Four consecutive prefixes per lane: one 16-B key load and one
 // 16-B non-temporal store per output array.
-template <int W, typename View, typename RecFn>
+template <int W, bool DIFF = false, typename View, typename RecFn>
 __device__ __forceinline__ void stream_routes(
     const ogs_prefix_table& pt, const uint32_t* __restrict__ tkey, uint32_t p0,
     uint32_t P, uint32_t Sp, size_t u, uint32_t s,
     const uint8_t* __restrict__ nflags, const View& sv, const RouteCfg& cfg,
-    const ogs_spf_out& out, RecFn rec) {
+    const ogs_spf_out& out, RecFn rec, const DiffCtx* diff = nullptr) {
+  uint32_t upd = 0, del = 0;
   constexpr uint32_t kInf = 0xFFFFFFFFu;
   const int tid = threadIdx.x;
   const bool v4Gated = !cfg.enableV4 && !cfg.v4OverV6;
@@ -118,6 +148,29 @@ __device__ __forceinline__ void stream_routes(
                   r3.mask[w]);
       }
     }
+    if constexpr (DIFF) {
+      // lane l holds prefixes q..q+3; the wave's 256 prefixes are 8 words:
+      // word l (lanes 8l..8l+7) bit 4k+j = prefix 32l + 4k + j
+      const uint64_t b0 = __ballot(route_changed<W>(r0, *diff, Sp, q + 0, upd, del));
+      const uint64_t b1 = __ballot(route_changed<W>(r1, *diff, Sp, q + 1, upd, del));
+      const uint64_t b2 = __ballot(route_changed<W>(r2, *diff, Sp, q + 2, upd, del));
+      const uint64_t b3 = __ballot(route_changed<W>(r3, *diff, Sp, q + 3, upd, del));
+      const int lane = threadIdx.x & 63;
+      if (lane < 8) {
+        uint32_t word = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int l = lane * 8 + k;
+          word |= uint32_t((b0 >> l) & 1u) << (4 * k);
+          word |= uint32_t((b1 >> l) & 1u) << (4 * k + 1);
+          word |= uint32_t((b2 >> l) & 1u) << (4 * k + 2);
+          word |= uint32_t((b3 >> l) & 1u) << (4 * k + 3);
+        }
+        // the wave's first prefix is q - 4 * lane (lane 0's q)
+        const uint32_t w0 = (q - 4u * uint32_t(lane)) / 32u + uint32_t(lane);
+        if (word) atomicOr(diff->changed + w0, word);
+      }
+    }
   }
   for (uint32_t p = Pv + tid; p < P; p += kBlock) {  // tail / unaligned rows
     Rec<W> r;
@@ -129,6 +182,15 @@ __device__ __forceinline__ void stream_routes(
 #pragma unroll
       for (int w = 0; w < W; ++w) oMask[size_t(w) * Sp + p] = r.mask[w];
     }
+    if constexpr (DIFF) {
+      if (route_changed<W>(r, *diff, Sp, p, upd, del)) {
+        atomicOr(diff->changed + p / 32u, 1u << (p % 32u));
+      }
+    }
+  }
+  if constexpr (DIFF) {
+    if (upd) atomicAdd(diff->counts, upd);
+    if (del) atomicAdd(diff->counts + 1, del);
   }
 }
 

@@ -210,6 +210,47 @@ bool try_frontier(const ogs_graph& g, const ogs_unit* units, int nUnits,
   return true;
 }
 
+hipError_t launch_frontier_variants(const ogs_graph& g, const ogs_prefix_table& pt,
+                                    const uint32_t* key, const ogs_unit* units,
+                                    int n, uint32_t flags, int W,
+                                    const ogs_spf_out& out,
+                                    const ogs_unit_mods* mods,
+                                    const ogs_route_diff* diff, void* scratch,
+                                    hipStream_t stream);
+
+// ogs_spf_routes_variants: key fold + zeroed diff bitmap + fused frontier
+// SPF / RouteDb / diff launch. *unsupported when outside the frontier path.
+hipError_t launch_variants(const ogs_graph& g, const ogs_prefix_table& pt,
+                           const ogs_unit* units, int nUnits,
+                           const ogs_unit_mods* mods, const ogs_route_diff* diff,
+                           uint32_t flags, int W, const ogs_spf_out& out,
+                           hipStream_t stream, int* unsupported) {
+  if (!g.edge_src || (flags & OGS_F_WIDE_METRIC) || !frontier_fits(g, flags, W) ||
+      (W != 1 && W != 2 && W != 4)) {
+    *unsupported = 1;
+    return hipSuccess;
+  }
+  const size_t Sp = size_t(pt.max_prefixes);
+  const size_t keyBytes = round256(size_t(g.num_topos) * Sp * 4);
+  void* ws = nullptr;
+  hipError_t e = workspace(keyBytes + chunk_scratch_bytes(g), stream, &ws);
+  if (e != hipSuccess) return e;
+  uint32_t* key = static_cast<uint32_t*>(ws);
+  if (diff) {
+    e = hipMemsetAsync(diff->changed, 0, size_t(nUnits) * ((Sp + 31) / 32) * 4, stream);
+    if (e != hipSuccess) return e;
+  }
+  if (Sp > 0) {
+    hipLaunchKernelGGL(pfx_key_kernel, dim3(unsigned((Sp + kBlock - 1) / kBlock),
+                                            unsigned(g.num_topos)),
+                       dim3(kBlock), 0, stream, pt, g.num_topos, key);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return launch_frontier_variants(g, pt, key, units, nUnits, flags, W, out, mods,
+                                  diff, static_cast<char*>(ws) + keyBytes, stream);
+}
+
 // Large shared topologies with a prefix table: key fold, then either the
 // fused frontier SPF + stream launch (route_stream 2), or an SPF launch
 // (frontier / multi-source sweep) and a route-stream launch (route_stream 1).

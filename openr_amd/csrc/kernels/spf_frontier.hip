@@ -41,6 +41,7 @@ namespace ogs {
 constexpr uint32_t kChunk = 8;
 constexpr uint32_t kChunkCntShift = 21;  // bits 21..24: edge count - 1
 constexpr uint32_t kChunkDrained = 1u << 25;
+constexpr int kMaxDead = 8;  // ogs_unit_mods.dead_per_unit limit
 
 // Exclusive prefix sum of x over the workgroup's current tile; returns the
 // sum's base for this thread and adds the tile total to *base (LDS).
@@ -104,24 +105,40 @@ __global__ __launch_bounds__(kBlock) void chunk_prep_kernel(
 
 // Loads chunk ch's edges into registers: past the chunk's count an edge
 // reads as DOWN (dst 0, never relaxes).
+// Dead edges of a link-failure variant (ogs_unit_mods), unit-uniform.
+struct DeadEdges {
+  uint32_t e[kMaxDead];
+  __device__ __forceinline__ bool has(uint32_t x) const {
+    bool d = false;
+#pragma unroll
+    for (int k = 0; k < kMaxDead; ++k) d |= x == e[k];
+    return d;
+  }
+};
+
+template <bool MODS>
 __device__ __forceinline__ void load_chunk(const uint64_t* __restrict__ edges,
-                                           uint64_t ch, uint64_t (&x)[kChunk]) {
+                                           uint64_t ch, uint64_t (&x)[kChunk],
+                                           const DeadEdges& dead) {
   const uint32_t b = uint32_t(ch >> 32);
   const uint32_t n = ((uint32_t(ch) >> kChunkCntShift) & 15u) + 1u;
 #pragma unroll
   for (uint32_t i = 0; i < kChunk; ++i) {
     x[i] = i < n ? edges[b + i] : uint64_t(OGS_EDGE_DOWN);
+    if constexpr (MODS) {
+      if (dead.has(b + i)) x[i] |= uint64_t(OGS_EDGE_DOWN);
+    }
   }
 }
 
 // One unit's SPF into LDS (dist[v], nh[v*W + w]); returns after the final
 // workgroup barrier. stamp[] is scratch.
-template <int W>
+template <int W, bool MODS>
 __device__ __forceinline__ void frontier_spf(
     uint32_t N, uint32_t s, const uint64_t* __restrict__ edges,
     const uint64_t* __restrict__ chunks, uint32_t C, bool hop,
     const uint32_t* __restrict__ gRow, uint32_t e0, uint32_t* dist,
-    uint32_t* nh, uint16_t* stamp, uint64_t* tp) {
+    uint32_t* nh, uint16_t* stamp, uint64_t* tp, const DeadEdges& dead) {
   constexpr uint32_t kInf = 0xFFFFFFFFu;
   const int tid = threadIdx.x;
   for (uint32_t v = tid; v < N; v += kBlock) {
@@ -146,7 +163,7 @@ __device__ __forceinline__ void frontier_spf(
       if ((uint32_t(ch) & kChunkDrained) && v != s) continue;
       const uint32_t dv = dist[v];
       uint64_t x[kChunk];
-      load_chunk(edges, ch, x);
+      load_chunk<MODS>(edges, ch, x, dead);
       uint32_t t[kChunk], cand[kChunk], dt[kChunk];
 #pragma unroll
       for (uint32_t i = 0; i < kChunk; ++i) {
@@ -182,6 +199,9 @@ __device__ __forceinline__ void frontier_spf(
       const uint64_t x = edges[b + j];
       const uint32_t lo = static_cast<uint32_t>(x);
       if (lo & OGS_EDGE_DOWN) continue;
+      if constexpr (MODS) {
+        if (dead.has(b + j)) continue;
+      }
       const uint32_t t = edge_dst(lo);
       const uint32_t w = hop ? 1u : static_cast<uint32_t>(x >> 32);
       if (w == dist[t]) {
@@ -203,7 +223,7 @@ __device__ __forceinline__ void frontier_spf(
 #pragma unroll
       for (int w = 0; w < W; ++w) nv[w] = nh[v * W + w];
       uint64_t x[kChunk];
-      load_chunk(edges, ch, x);
+      load_chunk<MODS>(edges, ch, x, dead);
       uint32_t t[kChunk], cand[kChunk], dt[kChunk];
 #pragma unroll
       for (uint32_t i = 0; i < kChunk; ++i) {
@@ -247,12 +267,13 @@ uint32_t frontier_lds_bytes(uint32_t Sn, int W) {
 // ROUTES = false: SPF only, dist / nh to HBM.
 // ROUTES = true: SPF + the unit's RouteDb stream (route_stream.h) from LDS;
 // dist / nh go to HBM only when requested.
-template <int W, bool ROUTES>
+template <int W, bool ROUTES, bool MODS = false, bool DIFF = false>
 __global__ __launch_bounds__(kBlock) void spf_frontier_kernel(
     ogs_graph g, ogs_prefix_table pt, const uint32_t* __restrict__ key,
     const uint64_t* __restrict__ chunks, const uint32_t* __restrict__ nChunk,
     uint32_t cap, const ogs_unit* __restrict__ units, uint32_t flags,
-    uint32_t* __restrict__ oDist, uint32_t* __restrict__ oNh, ogs_spf_out out) {
+    uint32_t* __restrict__ oDist, uint32_t* __restrict__ oNh, ogs_spf_out out,
+    ogs_unit_mods mods, ogs_route_diff diff) {
   constexpr uint32_t kInf = 0xFFFFFFFFu;
   const int tid = threadIdx.x;
   const uint32_t u0 = blockIdx.x;
@@ -270,14 +291,21 @@ __global__ __launch_bounds__(kBlock) void spf_frontier_kernel(
   uint32_t* nh = dist + ((Sn + 3u) & ~3u);                           // [Sn*W]
   uint16_t* stamp = reinterpret_cast<uint16_t*>(nh + ((Sn * W + 3u) & ~3u));  // [Sn]
 
+  DeadEdges dead;
+#pragma unroll
+  for (int k = 0; k < kMaxDead; ++k) {
+    dead.e[k] = (MODS && k < mods.dead_per_unit)
+        ? mods.dead_edges[size_t(u0) * mods.dead_per_unit + k]
+        : OGS_NODE_NONE;
+  }
   uint64_t tp[5] = {0, 0, 0, 0, 0};
 #ifdef OGS_STAMPS
   const uint64_t t0 = __builtin_amdgcn_s_memtime();
   const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
 #endif
-  frontier_spf<W>(N, s, g.edges + e0, chunks + size_t(unit.topo) * cap,
-                  nChunk[unit.topo], (flags & OGS_F_HOP_METRIC) != 0, gRow, e0,
-                  dist, nh, stamp, tp);
+  frontier_spf<W, MODS>(N, s, g.edges + e0, chunks + size_t(unit.topo) * cap,
+                        nChunk[unit.topo], (flags & OGS_F_HOP_METRIC) != 0, gRow,
+                        e0, dist, nh, stamp, tp, dead);
 
   for (uint32_t v = tid; v < N; v += kBlock) {
     if (oDist) oDist[size_t(u0) * Sn + v] = dist[v];
@@ -303,13 +331,24 @@ __global__ __launch_bounds__(kBlock) void spf_frontier_kernel(
                        (flags & OGS_F_V4_OVER_V6) != 0,
                        (flags & OGS_F_BEST_ROUTE_SELECTION) != 0};
     const SplitView<uint32_t, W> sv{dist, nh};
-    stream_routes<W>(pt, key + size_t(unit.topo) * Sp, p0, P, Sp, u0, s, nflags, sv,
-                     cfg, out, [&](uint32_t v, Rec<W>& r) {
-                       r.meta = rMeta[v];
-                       r.metric = (v == s) ? kInf : dist[v];
+    __shared__ uint32_t cnt[2];
+    if constexpr (DIFF) {
+      if (tid < 2) cnt[tid] = 0u;
+      __syncthreads();
+    }
+    const DiffCtx dc{diff.base_meta, diff.base_metric, diff.base_mask,
+                     diff.changed + size_t(u0) * ((Sp + 31u) / 32u), cnt};
+    stream_routes<W, DIFF>(pt, key + size_t(unit.topo) * Sp, p0, P, Sp, u0, s,
+                           nflags, sv, cfg, out, [&](uint32_t v, Rec<W>& r) {
+                             r.meta = rMeta[v];
+                             r.metric = (v == s) ? kInf : dist[v];
 #pragma unroll
-                       for (int w = 0; w < W; ++w) r.mask[w] = nh[v * W + w];
-                     });
+                             for (int w = 0; w < W; ++w) r.mask[w] = nh[v * W + w];
+                           }, &dc);
+    if constexpr (DIFF) {
+      __syncthreads();
+      if (tid < 2) diff.counts[size_t(u0) * 2 + tid] = cnt[tid];
+    }
   }
 #ifdef OGS_STAMPS  // diagnostic build only: phase clocks into out.sel row u0
   __syncthreads();
@@ -327,15 +366,16 @@ __global__ __launch_bounds__(kBlock) void spf_frontier_kernel(
 #endif
 }
 
-template <int W, bool ROUTES>
+template <int W, bool ROUTES, bool MODS = false, bool DIFF = false>
 hipError_t launch_frontier(const ogs_graph& g, const ogs_prefix_table& pt,
                            const uint32_t* key, const uint64_t* chunks,
                            const uint32_t* nChunk, const ogs_unit* units,
                            int nUnits, uint32_t flags, uint32_t* dist,
                            uint32_t* nh, const ogs_spf_out& out,
-                           hipStream_t stream) {
+                           hipStream_t stream, const ogs_unit_mods& mods = {},
+                           const ogs_route_diff& diff = {}) {
   const uint32_t lds = frontier_lds_bytes(uint32_t(g.max_nodes), W);
-  auto k = spf_frontier_kernel<W, ROUTES>;
+  auto k = spf_frontier_kernel<W, ROUTES, MODS, DIFF>;
   if (lds > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
                                        hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -343,7 +383,8 @@ hipError_t launch_frontier(const ogs_graph& g, const ogs_prefix_table& pt,
     if (e != hipSuccess) return e;
   }
   hipLaunchKernelGGL(k, dim3(nUnits), dim3(kBlock), lds, stream, g, pt, key,
-                     chunks, nChunk, chunk_cap(g), units, flags, dist, nh, out);
+                     chunks, nChunk, chunk_cap(g), units, flags, dist, nh, out,
+                     mods, diff);
   return hipGetLastError();
 }
 
@@ -409,6 +450,42 @@ hipError_t launch_frontier_routes(const ogs_graph& g, const ogs_prefix_table& pt
     case 1: return launch_frontier<1, true>(g, pt, key, chunks, nChunk, units, nUnits, flags, dist, out.nh, out, stream);
     case 2: return launch_frontier<2, true>(g, pt, key, chunks, nChunk, units, nUnits, flags, dist, out.nh, out, stream);
     case 4: return launch_frontier<4, true>(g, pt, key, chunks, nChunk, units, nUnits, flags, dist, out.nh, out, stream);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+// Link-failure variants with an optional route diff (fused SPF + RouteDb).
+template <int W>
+hipError_t launch_variants_w(const ogs_graph& g, const ogs_prefix_table& pt,
+                             const uint32_t* key, const uint64_t* chunks,
+                             const uint32_t* nChunk, const ogs_unit* units,
+                             int n, uint32_t flags, const ogs_spf_out& out,
+                             const ogs_unit_mods* mods, const ogs_route_diff* diff,
+                             hipStream_t stream) {
+  uint32_t* dist = static_cast<uint32_t*>(out.dist);
+  const ogs_unit_mods m = mods ? *mods : ogs_unit_mods{};
+  const ogs_route_diff d = diff ? *diff : ogs_route_diff{};
+  if (mods && diff) return launch_frontier<W, true, true, true>(g, pt, key, chunks, nChunk, units, n, flags, dist, out.nh, out, stream, m, d);
+  if (mods) return launch_frontier<W, true, true, false>(g, pt, key, chunks, nChunk, units, n, flags, dist, out.nh, out, stream, m, d);
+  if (diff) return launch_frontier<W, true, false, true>(g, pt, key, chunks, nChunk, units, n, flags, dist, out.nh, out, stream, m, d);
+  return launch_frontier<W, true>(g, pt, key, chunks, nChunk, units, n, flags, dist, out.nh, out, stream);
+}
+
+hipError_t launch_frontier_variants(const ogs_graph& g, const ogs_prefix_table& pt,
+                                    const uint32_t* key, const ogs_unit* units,
+                                    int n, uint32_t flags, int W,
+                                    const ogs_spf_out& out,
+                                    const ogs_unit_mods* mods,
+                                    const ogs_route_diff* diff, void* scratch,
+                                    hipStream_t stream) {
+  uint64_t* chunks = nullptr;
+  uint32_t* nChunk = nullptr;
+  hipError_t e = prep_chunks(g, scratch, stream, &chunks, &nChunk);
+  if (e != hipSuccess) return e;
+  switch (W) {
+    case 1: return launch_variants_w<1>(g, pt, key, chunks, nChunk, units, n, flags, out, mods, diff, stream);
+    case 2: return launch_variants_w<2>(g, pt, key, chunks, nChunk, units, n, flags, out, mods, diff, stream);
+    case 4: return launch_variants_w<4>(g, pt, key, chunks, nChunk, units, n, flags, out, mods, diff, stream);
     default: return hipErrorInvalidValue;
   }
 }

@@ -4,6 +4,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <algorithm>
 #include <chrono>
 #include <sstream>
 #include <thread>
@@ -584,6 +585,45 @@ PYBIND11_MODULE(_refcpu, m) {
         },
         py::arg("opts"), py::arg("sources"), py::arg("enableV4") = true,
         py::arg("sr") = false, py::arg("brs") = false);
+
+  // Link-failure variants (config C4): the reference's adjacency-DB update
+  // with the links removed at both ends, buildRouteDb, and calculateUpdate
+  // against the base RouteDb. Returns (base canonical, [(variant canonical,
+  // sorted changed prefixes, #update, #delete)], [[(a, ifA, b, ifB)...]]).
+  m.def("variant_route_updates",
+        [](const std::string& kind, py::dict opts, const std::string& source,
+           int count, uint64_t seed, int dualPermille, bool enableV4, bool brs) {
+          auto g = genLsdb(kind, opts);
+          auto variants = topogen::linkFailureVariants(g, count, seed, dualPermille);
+          auto solve = [&](const topogen::Lsdb& db) {
+            Workspace w;
+            auto& ls = w.als.emplace(db.area, LinkState(db.area, "test_node")).first->second;
+            loadLsdb(db, ls, w.ps);
+            SpfSolver solver("test_node", enableV4, false, brs);
+            auto r = solver.buildRouteDb(source, w.als, w.ps);
+            return r ? *r : DecisionRouteDb{};
+          };
+          const DecisionRouteDb base = solve(g);
+          py::list out, links;
+          for (const auto& v : variants) {
+            const DecisionRouteDb db = solve(topogen::withoutLinks(g, v));
+            const auto upd = base.calculateUpdate(db);
+            std::vector<std::string> changed;
+            for (const auto& [p, _] : upd.unicastRoutesToUpdate) changed.push_back(p);
+            for (const auto& p : upd.unicastRoutesToDelete) changed.push_back(p);
+            std::sort(changed.begin(), changed.end());
+            out.append(py::make_tuple(py::bytes(canonical(db)), changed,
+                                      upd.unicastRoutesToUpdate.size(),
+                                      upd.unicastRoutesToDelete.size()));
+            py::list l;
+            for (const auto& f : v) l.append(py::make_tuple(f.a, f.ifA, f.b, f.ifB));
+            links.append(l);
+          }
+          return py::make_tuple(py::bytes(canonical(base)), out, links);
+        },
+        py::arg("kind"), py::arg("opts"), py::arg("source"), py::arg("count"),
+        py::arg("seed") = 0xC4F, py::arg("dualPermille") = 500,
+        py::arg("enableV4") = true, py::arg("brs") = false);
 
   m.def("gen_route_dbs",
         [](const std::string& kind, py::dict opts, std::vector<std::string> sources,

@@ -1,0 +1,53 @@
+"""Config C4 path: link-failure variants solved in one launch with the route
+diff fused in (ogs_spf_routes_variants), bit-exact against the oracle's
+adjacency-DB update + buildRouteDb + calculateUpdate for every variant."""
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+CASES = [
+    ("wan", dict(nodes=300, seed=0xC4, prefixesPerNode=2), "0", False),
+    ("wan", dict(nodes=400, seed=0xC5, prefixesPerNode=1, nodeOverloadPermille=20,
+                 adjOverloadPermille=20, anycastPermille=100, minNhPermille=50,
+                 v4Permille=50, drainPermille=50), "7", True),
+    ("fabric", dict(pods=4, planes=4, sswPerPlane=8, rswPerPod=16, prefixesPerNode=2),
+     "3-1-5", False),
+    ("grid", dict(n=8, metricSeed=0xC2000003, prefixesPerNode=2), "9", False),
+]
+
+
+@pytest.mark.parametrize("kind,opts,source,brs", CASES, ids=lambda x: str(x)[:12])
+def test_link_failure_variants(product, oracle, kind, opts, source, brs):
+    n = 48
+    vr = product.VariantRunner(True, brs)
+    vr.setup(kind, opts, source, n, 0xC4F, 500)
+    vr.run_base()
+    vr.launch()
+    vr.download()
+    base, variants, links = oracle.variant_route_updates(kind, opts, source, n, 0xC4F,
+                                                         500, True, brs)
+    assert vr.num_variants() == len(variants) == n
+    some_change = False
+    for v, (canon, changed, nu, nd) in enumerate(variants):
+        got = vr.canonical(v)
+        if got != canon:
+            a, b = got.decode().splitlines(), canon.decode().splitlines()
+            pytest.fail(f"variant {v} {links[v]}: {[(x, y) for x, y in zip(a, b) if x != y][:4]}")
+        assert vr.changed(v) == changed, f"variant {v} {links[v]}"
+        assert vr.counts(v) == (nu, nd), f"variant {v} {links[v]}"
+        some_change |= bool(changed)
+    assert some_change  # the sample exercises real route changes
+
+
+def test_variants_records_optional(product):
+    """Diff-only launches (no route records written) give the same diff."""
+    opts = dict(nodes=300, seed=0xC4, prefixesPerNode=2)
+    vr = product.VariantRunner(True, False)
+    vr.setup("wan", opts, "0", 32, 0xC4F, 500)
+    vr.run_base()
+    vr.launch(0, True)
+    vr.download()
+    full = [(vr.changed(v), vr.counts(v)) for v in range(32)]
+    vr.launch(0, False)
+    vr.download()
+    assert [(vr.changed(v), vr.counts(v)) for v in range(32)] == full

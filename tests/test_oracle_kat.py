@@ -55,3 +55,26 @@ def test_oracle_multi_area_generator(oracle):
     n_plain = plain.count(b"\nU ") + plain.startswith(b"U ")
     assert n_abr >= 2 * 40 - 2  # two areas' worth of routes
     assert 30 <= n_plain < n_abr
+
+
+def test_oracle_variant_updates(oracle):
+    """Removing a link changes routes only through it: the oracle's per-variant
+    calculateUpdate lists exactly the prefixes whose route text changed."""
+    base, variants, links = oracle.variant_route_updates(
+        "wan", dict(nodes=120, seed=0xC4, prefixesPerNode=1), "0", 12, 0xC4F, 500)
+
+    def routes(c):
+        out, cur = {}, None
+        for line in c.decode().splitlines():
+            if line.startswith("U "):
+                cur = line.split()[1]
+                out[cur] = [line.split(" c=")[0]]
+            elif cur:
+                out[cur].append(line)
+        return out
+    b = routes(base)
+    for canon, changed, nu, nd in variants:
+        v = routes(canon)
+        diff = sorted(p for p in set(b) | set(v) if b.get(p) != v.get(p))
+        assert changed == diff
+        assert nd == len(set(b) - set(v))
