@@ -242,9 +242,104 @@ def run_c3(args, torch, dist, rank, world, local_rank):
     return None
 
 
+C4_VARIANTS = 10000
+C4_OPTS = dict(nodes=2000, seed=0xC4, prefixesPerNode=1)
+
+
+def run_c4(args, torch, dist, rank, world, local_rank):
+    """Config C4: link-failure sweep. WAN N=2000 (seed 0xC4), one prefix per
+    node, source "0"; 10,000 single/dual link-removal variants (seed 0xC4F,
+    50 % dual). One step = this rank's block of variants in ONE launch:
+    frontier SPF without the failed links + RouteDb + route diff against the
+    base RouteDb (changed-prefix bitmap + update/delete counts); one build =
+    one variant. Strong scaling: the 10,000 variants split over the ranks."""
+    import openr_amd
+    import openr_amd.capi as capi
+    openr_amd.require_gpu()
+    lib = capi.load()
+    lib.ogs_set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    steps = args.steps if args.config == "c4" else args.c4_steps
+    warmup = args.warmup if args.config == "c4" else 2
+    lo, hi = shard.block_range(C4_VARIANTS, rank, world)
+    vr = openr_amd.decision.VariantRunner(True, False)
+    vr.setup("wan", C4_OPTS, "0", C4_VARIANTS, 0xC4F, 500, lo, hi)
+    sh = vr.shape()
+    stream = torch.cuda.current_stream(dev)
+    sptr = stream.cuda_stream
+    vr.run_base(sptr)
+    for _ in range(warmup):
+        vr.launch(sptr, True)
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for _ in range(steps):
+        vr.launch(sptr, True)
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t0
+    kernel_ms = e0.elapsed_time(e1) / steps
+    vr.download()
+    U = vr.num_variants()
+    changed = sum(len(vr.changed(v)) for v in range(U))
+    counts = [vr.counts(v) for v in range(U)]
+    digest = shard.route_digest(
+        bytearray(repr(counts).encode()))
+    total_units, total_changed, job_digest, tmax, _ = shard.reduce_stats(
+        dist, torch, dev, U, changed, digest, wall)
+    if rank != 0:
+        return None
+    N, E, P = sh["nodes"], sh["directed_edges"], sh["prefixes"]
+    T, W = sh["advertisements"], sh["nh_words"]
+    inputs = 4 * (N + 1) + 8 * E + (N + 7) // 8 + 16 * T
+    bpu = inputs / C4_VARIANTS + 4 * N + 4 * W * N + P * (4 * W + 8) + 16 + P / 8
+    achieved = bpu * U / (kernel_ms * 1e-3) / 1e9
+    value = total_units * steps / tmax
+    line = {
+        "metric": "link-failure variant builds/sec (SPF + RouteDb + route diff)",
+        "value": round(value, 1), "unit": "variants/s",
+        "n_gpus": world, "steps": steps, "warmup": warmup,
+        "ms_per_step": round(tmax / steps * 1e3, 4), "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
+        "config": {"workload": "C4: 10,000 single/dual link-failure variants of a "
+                               "2,000-node WAN (seed 0xC4), source '0', 1 prefix/node, "
+                               "masked SPF + RouteDb + diff vs base",
+                   "nodes": N, "directed_edges": E, "prefixes": P,
+                   "variants": C4_VARIANTS,
+                   "parallelism": f"shard-by-variant x{world}"},
+        "changed_routes_per_step": total_changed, "route_digest": f"{job_digest:016x}",
+        "gteps": round(E * value / 1e9, 3), "kernel_ms": round(kernel_ms, 4),
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": None, "bytes_alg_per_unit": round(bpu, 1)},
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import _refcpu
+        threads = max(1, min(16, os.cpu_count() or 1))
+        sample = 32 * threads
+        secs, n, _ = _refcpu.cpu_baseline_variants("wan", C4_OPTS, "0", sample, 0xC4F, 500,
+                                                   threads)
+        line["cpu_baseline"] = {
+            "value": round(n / secs, 2), "unit": "variants/s", "cores": threads,
+            "kind": "port",
+            "sample": f"first {sample} of the C4 variants, refcpu incremental "
+                      f"updateAdjacencyDatabase + buildRouteDb + calculateUpdate, "
+                      f"{threads} threads, ingestion excluded"}
+    return line
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--config", default="c2", choices=["c2", "c3"])
+    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4"])
     ap.add_argument("--prefixes-per-node", type=int, default=100)
     ap.add_argument("--c3-streams", type=int, default=2, choices=[1, 2],
                     help="C3: HIP streams for the two source groups")
@@ -256,6 +351,9 @@ def main():
     ap.add_argument("--no-c3", action="store_true",
                     help="skip the C3 fabric all-sources line embedded in the C2 result")
     ap.add_argument("--c3-steps", type=int, default=10)
+    ap.add_argument("--no-c4", action="store_true",
+                    help="skip the C4 link-failure sweep line embedded in the C2 result")
+    ap.add_argument("--c4-steps", type=int, default=5)
     ap.add_argument("--opt", action="append", default=[],
                     help="engine option name=value (ogs_set_option), for A/B runs")
     args = ap.parse_args()
@@ -276,6 +374,13 @@ def main():
         name, val = o.split("=", 1)
         lib0 = capi.load()
         capi.check(lib0, lib0.ogs_set_option(name.encode(), int(val)), name)
+    if args.config == "c4":
+        line = run_c4(args, torch, dist, rank, world, local_rank)
+        if line is not None:
+            print(json.dumps(line), flush=True)
+        if dist:
+            dist.destroy_process_group()
+        return
     if args.config == "c3":
         line = run_c3(args, torch, dist, rank, world, local_rank)
         if line is not None:
@@ -427,6 +532,15 @@ def main():
                                    "route_dbs_per_s", "gteps", "routes_per_step",
                                    "route_digest", "roofline", "config")}
             line["c3_fabric_all_sources"]["steps"] = c3["steps"]
+    if not args.no_c4:
+        c4 = run_c4(args, torch, dist, rank, world, local_rank)
+        if rank == 0:
+            line["c4_link_failure_sweep"] = {
+                k: c4[k] for k in ("value", "unit", "ms_per_step", "kernel_ms", "gteps",
+                                   "changed_routes_per_step", "route_digest", "roofline",
+                                   "config", "steps") if k in c4}
+            if "cpu_baseline" in c4:
+                line["c4_link_failure_sweep"]["cpu_baseline"] = c4["cpu_baseline"]
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist:

@@ -532,9 +532,14 @@ class VariantRunner {
   VariantRunner(bool enableV4, bool brs) : enableV4_(enableV4), brs_(brs) {}
 
   void setup(const std::string& kind, const py::dict& opts, const std::string& source,
-             int count, uint64_t seed, int dualPermille) {
+             int count, uint64_t seed, int dualPermille, int lo, int hi) {
     g_ = genLsdb(kind, opts);
     variants_ = topogen::linkFailureVariants(g_, count, seed, dualPermille);
+    // this rank's block [lo, hi) of the job's variants (hi < 0: to the end)
+    hi = hi < 0 ? int(variants_.size()) : std::min(hi, int(variants_.size()));
+    lo = std::max(0, std::min(lo, hi));
+    variants_ = std::vector<std::vector<topogen::LinkRef>>(variants_.begin() + lo,
+                                                           variants_.begin() + hi);
     area_ = g_.area;
     als_.emplace(area_, LinkState(area_, "test_node"));
     LinkState& ls = als_.at(area_);
@@ -1006,7 +1011,7 @@ PYBIND11_MODULE(_decision, m) {
            py::arg("enableBestRouteSelection") = false)
       .def("setup", &VariantRunner::setup, py::arg("kind"), py::arg("opts"),
            py::arg("source"), py::arg("count"), py::arg("seed") = 0xC4F,
-           py::arg("dualPermille") = 500)
+           py::arg("dualPermille") = 500, py::arg("lo") = 0, py::arg("hi") = -1)
       .def("run_base", [](VariantRunner& r, uintptr_t stream) {
              py::gil_scoped_release nogil;
              r.runBase(stream);

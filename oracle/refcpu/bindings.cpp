@@ -5,6 +5,9 @@
 #include <pybind11/stl.h>
 
 #include <algorithm>
+#include <set>
+#include <optional>
+#include <map>
 #include <chrono>
 #include <sstream>
 #include <thread>
@@ -213,6 +216,29 @@ py::dict fromUpdate(const DecisionRouteUpdate& u) {
 
 // Bulk workloads (CPU baseline + parity at scale) -----------------------------
 namespace {
+
+AdjacencyDatabase toAdjDb(const topogen::AdjDb& d, const std::string& area) {
+  AdjacencyDatabase db;
+  db.thisNodeName = d.thisNodeName;
+  db.isOverloaded = d.isOverloaded;
+  db.nodeLabel = d.nodeLabel;
+  db.area = area;
+  db.nodeMetricIncrementVal = d.nodeMetricIncrementVal;
+  for (const auto& a : d.adjs) {
+    Adjacency x;
+    x.otherNodeName = a.otherNodeName;
+    x.ifName = a.ifName;
+    x.otherIfName = a.otherIfName;
+    x.nextHopV6 = a.nextHopV6;
+    x.nextHopV4 = a.nextHopV4;
+    x.metric = a.metric;
+    x.adjLabel = a.adjLabel;
+    x.isOverloaded = a.isOverloaded;
+    x.weight = a.weight;
+    db.adjacencies.push_back(x);
+  }
+  return db;
+}
 
 void loadLsdb(const topogen::Lsdb& g, LinkState& ls, PrefixState& ps) {
   for (const auto& d : g.adjDbs) {
@@ -624,6 +650,84 @@ PYBIND11_MODULE(_refcpu, m) {
         py::arg("kind"), py::arg("opts"), py::arg("source"), py::arg("count"),
         py::arg("seed") = 0xC4F, py::arg("dualPermille") = 500,
         py::arg("enableV4") = true, py::arg("brs") = false);
+
+  // CPU baseline for config C4: T threads, each with a private replica of
+  // the base LinkState/PrefixState and the base RouteDb; per variant the
+  // reference's incremental path: updateAdjacencyDatabase of the failed
+  // links' endpoints (adjacency removed at both ends), buildRouteDb,
+  // calculateUpdate against the base, then the endpoints' original
+  // databases restored. Ingestion and the base build are untimed. Returns
+  // (seconds, variants, total changed routes).
+  m.def("cpu_baseline_variants",
+        [](const std::string& kind, py::dict opts, const std::string& source,
+           int count, uint64_t seed, int dualPermille, int threads) {
+          auto g = genLsdb(kind, opts);
+          auto variants = topogen::linkFailureVariants(g, count, seed, dualPermille);
+          if (threads <= 0) threads = std::max(1u, std::thread::hardware_concurrency());
+          std::map<std::string, const topogen::AdjDb*> byName;
+          for (const auto& d : g.adjDbs) byName[d.thisNodeName] = &d;
+          struct Replica {
+            Workspace w;
+            std::optional<DecisionRouteDb> base;
+          };
+          std::vector<std::unique_ptr<Replica>> reps(threads);
+          for (auto& r : reps) {
+            r = std::make_unique<Replica>();
+            auto& ls = r->w.als.emplace(g.area, LinkState(g.area, "test_node")).first->second;
+            loadLsdb(g, ls, r->w.ps);
+            SpfSolver solver("test_node", true, false, false);
+            r->base = solver.buildRouteDb(source, r->w.als, r->w.ps);
+          }
+          std::vector<size_t> changed(threads, 0);
+          double secs = 0;
+          {
+            py::gil_scoped_release nogil;
+            auto t0 = std::chrono::steady_clock::now();
+            std::vector<std::thread> pool;
+            for (int th = 0; th < threads; ++th) {
+              pool.emplace_back([&, th] {
+                Replica& r = *reps[th];
+                LinkState& ls = r.w.als.at(g.area);
+                SpfSolver solver("test_node", true, false, false);
+                for (size_t v = th; v < variants.size(); v += threads) {
+                  std::set<std::string> nodes;
+                  for (const auto& f : variants[v]) {
+                    nodes.insert(f.a);
+                    nodes.insert(f.b);
+                  }
+                  for (const auto& n : nodes) {
+                    topogen::AdjDb d = *byName.at(n);
+                    auto& a = d.adjs;
+                    a.erase(std::remove_if(a.begin(), a.end(), [&](const topogen::Adj& x) {
+                              for (const auto& f : variants[v]) {
+                                if ((n == f.a && x.ifName == f.ifA) ||
+                                    (n == f.b && x.ifName == f.ifB)) {
+                                  return true;
+                                }
+                              }
+                              return false;
+                            }), a.end());
+                    ls.updateAdjacencyDatabase(toAdjDb(d, g.area), g.area);
+                  }
+                  auto db = solver.buildRouteDb(source, r.w.als, r.w.ps);
+                  if (db && r.base) {
+                    const auto upd = r.base->calculateUpdate(*db);
+                    changed[th] += upd.unicastRoutesToUpdate.size() +
+                        upd.unicastRoutesToDelete.size();
+                  }
+                  for (const auto& n : nodes) {
+                    ls.updateAdjacencyDatabase(toAdjDb(*byName.at(n), g.area), g.area);
+                  }
+                }
+              });
+            }
+            for (auto& p : pool) p.join();
+            secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+          }
+          size_t total = 0;
+          for (auto c : changed) total += c;
+          return py::make_tuple(secs, variants.size(), total);
+        });
 
   m.def("gen_route_dbs",
         [](const std::string& kind, py::dict opts, std::vector<std::string> sources,
