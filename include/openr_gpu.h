@@ -322,6 +322,36 @@ int ogs_spf_routes_variants(const ogs_graph* graph,
                             const ogs_route_diff* diff, uint32_t flags,
                             int32_t nh_words, ogs_spf_out* out, void* stream);
 
+/* RibPolicy compiled against one prefix table (SURVEY.md §8(a) a16;
+ * RibPolicy.cpp:74-249): statements 0..K-1 in policy order. */
+typedef struct ogs_rib_policy {
+  int32_t num_statements;        /* K <= 32                                  */
+  uint32_t active;               /* bit k: statement k has a prefix or tag
+                                    matcher (no matcher never matches,
+                                    RibPolicy.cpp:76-78)                    */
+  const uint32_t* pfx_match;     /* [P_total] bit k: the prefix is in k's
+                                    prefix set, or k has none                */
+  const uint32_t* adv_tag_match; /* [A_total] bit k: the entry's tags meet
+                                    k's tags, or k has none                 */
+  const uint32_t* slot_nonzero;  /* [n_units][K][num_areas][W] link slots
+                                    of the unit's source whose weight under
+                                    statement k (neighbor > area > default,
+                                    RibPolicy.cpp:122-137) is > 0           */
+} ogs_rib_policy;
+
+/* Applies the policy to n_units RouteDbs in place (meta[U*S_p + p] read,
+ * mask[((U*A + a)*W + w)*S_p + p] rewritten: next hops of weight 0 dropped
+ * unless that drops all of them, RibPolicy.cpp:138-158). applied[U*S_p+p] =
+ * statement whose weights the route took, counter[...] = statement whose
+ * counterID the route carries (the last matching one tried), 0xFF = none.
+ * The prefix table is one topology's (pfx_base[0..1]); single-area callers
+ * pass num_areas = 1. */
+int ogs_rib_policy_apply(const ogs_prefix_table* prefixes,
+                         const ogs_rib_policy* policy, int32_t num_areas,
+                         int32_t n_units, int32_t nh_words,
+                         const uint32_t* meta, uint32_t* mask,
+                         uint8_t* applied, uint8_t* counter, void* stream);
+
 /* Multi-area RouteDb for n_units sources from their per-area SPF results
  * (a prior ogs_spf_routes launch over the area batch without a prefix
  * table): units[u] = the source's name id; spf_row[u*A + a] = the row of

@@ -48,6 +48,7 @@ struct Prefix {  // one advertisement (node, prefix) with PrefixMetrics
   int32_t path_preference{0}, source_preference{0}, distance{0};
   int32_t drain_metric{0};
   int64_t minNexthop{-1};  // < 0: unset
+  std::vector<std::string> tags;
 };
 
 struct Lsdb {
@@ -173,10 +174,18 @@ inline void applyOverloads(Lsdb& db, int adjPermille, int nodePermille,
 // drained (drain_metric = 1, LsdbUtil.cpp:760-823).
 struct PrefixMix {
   int v4Permille{0}, anycastPermille{0}, minNhPermille{0}, drainPermille{0};
+  int tagPermille{0};  // RibPolicy matchers: "ucmp" (this share) + "c0".."c3"
   uint64_t seed{0x3F};
 };
 
 inline void applyPrefixMix(Lsdb& db, const PrefixMix& m) {
+  if (m.tagPermille) {  // own stream: leaves the other draws unchanged
+    uint64_t t = m.seed ^ 0x7a65u;
+    for (auto& p : db.prefixes) {
+      if (int(splitmix64(t) % 1000) < m.tagPermille) p.tags.push_back("ucmp");
+      p.tags.push_back("c" + std::to_string(splitmix64(t) % 4));
+    }
+  }
   if (!m.v4Permille && !m.anycastPermille && !m.minNhPermille &&
       !m.drainPermille) {
     return;
@@ -500,8 +509,15 @@ inline std::vector<Lsdb> multiArea(const MultiAreaOpts& o) {
     p.source_preference = (splitmix64(s) & 1) ? 200 : 100;
     p.distance = int32_t(splitmix64(s) % 11);
   };
+  auto tag = [&](Prefix& p) {  // RibPolicy matchers (config C5 UCMP)
+    if (splitmix64(s) & 1) p.tags.push_back("ucmp");
+    p.tags.push_back("c" + std::to_string(splitmix64(s) % 4));
+  };
   for (auto& db : out) {
-    for (auto& p : db.prefixes) metrics(p);
+    for (auto& p : db.prefixes) {
+      metrics(p);
+      tag(p);
+    }
   }
   std::vector<std::vector<int>> abrAreas(o.abrs);
   for (int k = 0; k < o.abrs; ++k) {
@@ -546,6 +562,7 @@ inline std::vector<Lsdb> multiArea(const MultiAreaOpts& o) {
     for (int i = 0; i < o.prefixesPerNode; ++i) {
       Prefix p{name, seededV6Prefix(s)};
       metrics(p);
+      tag(p);
       out[abrAreas[k][0]].prefixes.push_back(p);
     }
   }
@@ -571,6 +588,7 @@ inline std::vector<Lsdb> multiArea(const MultiAreaOpts& o) {
         q.node = dbs[splitmix64(s) % dbs.size()].thisNodeName;
       }
       metrics(q);
+      tag(q);
       out[b].prefixes.push_back(q);
     }
   }

@@ -376,6 +376,8 @@ struct RouteSelectionResult {  // SpfSolver.h:37-66
 
 using AreaLinkStates = std::map<std::string, LinkState>;
 
+class RibPolicy;
+
 // ------------------------------------------------------------- SpfSolver --
 class SpfSolver {
  public:
@@ -397,6 +399,11 @@ class SpfSolver {
       const {
     return bestRoutesCache_;
   }
+  // GPU-side RibPolicy (UCMP weights): when set and active, buildRouteDb
+  // returns the routes RibPolicy::applyPolicy would leave (the reference's
+  // buildRouteDb + Decision's applyPolicy on the result, Decision.cpp:
+  // 912-925), computed on the device before materialisation. nullptr: off.
+  void setRibPolicy(const RibPolicy* policy) { ribPolicy_ = policy; }
 
  private:
   // several areas (SpfSolver.cpp:160-311 across LinkStates)
@@ -408,6 +415,7 @@ class SpfSolver {
   struct MultiAreaResult {  // host copies of one source's GPU results
     std::vector<uint32_t> row;  // [A] SPF row of each area or OGS_NODE_NONE
     std::vector<uint32_t> dist32, nh, meta, metric, mask, sel;
+    std::vector<uint8_t> applied, counter;  // RibPolicy (empty: none)
     int W{1};
     size_t Sn{0}, P{0};
   };
@@ -418,6 +426,7 @@ class SpfSolver {
   std::unique_ptr<Impl> impl_;
   std::map<std::string, RibUnicastEntry> staticUnicastRoutes_;
   std::map<std::string, RouteSelectionResult> bestRoutesCache_;
+  const RibPolicy* ribPolicy_{nullptr};
   std::string myNodeName_;
   bool enableV4_, enableNodeSegmentLabel_, enableBestRouteSelection_,
       v4OverV6Nexthop_;
@@ -446,6 +455,20 @@ class RibPolicy {  // RibPolicy.h:70-124
   bool applyAction(RibUnicastEntry& route) const;
   std::vector<std::string> applyPolicy(
       std::map<std::string, RibUnicastEntry>& unicastEntries) const;
+
+  // compiled form for the GPU (ogs_rib_policy, SpfSolver::setRibPolicy)
+  size_t numStatements() const { return stmts_.size(); }
+  bool hasMatcher(size_t k) const {
+    return !stmts_[k].prefixes.empty() || !stmts_[k].tags.empty();
+  }
+  bool matchesPrefix(size_t k, const std::string& prefix) const {
+    return stmts_[k].prefixes.empty() || stmts_[k].prefixes.count(prefix) != 0;
+  }
+  bool matchesTags(size_t k, const std::set<std::string>& tags) const;
+  int32_t weightOf(size_t k, const NextHopThrift& nh) const;  // RibPolicy.cpp:122-137
+  const std::optional<std::string>& counterIDOf(size_t k) const {
+    return stmts_[k].counterID;
+  }
 
  private:
   struct Stmt {
@@ -500,6 +523,11 @@ struct UnitView {
   const uint32_t* mask{nullptr};
   size_t maskStride{0};  // mask[w * maskStride + p]
   const uint32_t* sel{nullptr};
+  // device-applied RibPolicy (SpfSolver::setRibPolicy): statement whose
+  // weights / counterID each route took, 0xFF = none
+  const RibPolicy* policy{nullptr};
+  const uint8_t* applied{nullptr};
+  const uint8_t* counter{nullptr};
 };
 
 struct PrefixHostTable {

@@ -142,6 +142,11 @@ int HostBatch::slotOrder(std::vector<uint16_t>& out,
 }
 
 // ------------------------------------------------------------- SpfSolver --
+// device tables of a RibPolicy compiled for one source (runPolicyOnDevice)
+struct PolicyDevice {
+  DeviceBuffer pfxMatch, tagMatch, nonzero, applied, counter;
+};
+
 struct SpfSolver::Impl {
   DeviceBuffer pfxBase, advOff, advNode, advMetrics, advMinNh, pfxFlags, desc;
   DeviceBuffer unit, dist, nh, meta, metric, mask, sel;
@@ -149,6 +154,7 @@ struct SpfSolver::Impl {
   uint64_t cachedPsVersion{~0ull}, cachedTopoVersion{~0ull};
   const FlatTopology* cachedTopo{nullptr};
   PrefixHostTable table;
+  PolicyDevice policy;
 
   // multi-area domain (buildRouteDbMultiArea): the areas' CSR as one graph
   // batch + the domain prefix table with per-entry area / node-name ids
@@ -208,6 +214,79 @@ NextHopThrift makeNh(const Link& l, const std::string& me, bool useV4,
   nh.neighborNodeName = l.getOtherNodeName(me);
   nh.weight = 0;
   return nh;
+}
+
+// RibPolicy compiled on the host against the prefix table and the source's
+// links (per area), applied on the device (ogs_rib_policy_apply): next hops
+// of weight 0 dropped in the device masks; statement choices downloaded.
+void runPolicyOnDevice(const RibPolicy& pol, const PrefixHostTable& table,
+                       const ogs_prefix_table& pt,
+                       const std::vector<std::pair<const FlatTopology*, uint32_t>>& src,
+                       const std::string& me, int W, uint32_t* dMeta, uint32_t* dMask,
+                       PolicyDevice& D, std::vector<uint8_t>& applied,
+                       std::vector<uint8_t>& counter) {
+  const size_t K = pol.numStatements();
+  if (K > 32) throw std::domain_error("RibPolicy: more than 32 statements on the GPU path");
+  const size_t P = table.prefixes.size(), A = src.size();
+  std::vector<uint32_t> pm(std::max<size_t>(P, 1), 0), tm(std::max<size_t>(table.advEntry.size(), 1), 0);
+  std::vector<uint32_t> nz(std::max<size_t>(K * A * W, 1), 0);
+  uint32_t active = 0;
+  for (size_t k = 0; k < K; ++k) {
+    if (pol.hasMatcher(k)) active |= 1u << k;
+  }
+  for (size_t p = 0; p < P; ++p) {
+    for (size_t k = 0; k < K; ++k) {
+      if (pol.matchesPrefix(k, table.prefixes[p])) pm[p] |= 1u << k;
+    }
+  }
+  for (size_t a = 0; a < table.advEntry.size(); ++a) {
+    for (size_t k = 0; k < K; ++k) {
+      if (pol.matchesTags(k, table.advEntry[a]->tags)) tm[a] |= 1u << k;
+    }
+  }
+  for (size_t a = 0; a < A; ++a) {
+    const FlatTopology* f = src[a].first;
+    const uint32_t s = src[a].second;
+    if (s == OGS_NODE_NONE) continue;
+    const uint32_t rb = f->rowPtr[s], deg = f->rowPtr[s + 1] - rb;
+    for (uint32_t j = 0; j < deg && j < 32u * uint32_t(W); ++j) {
+      const NextHopThrift nh = makeNh(*f->edgeLink[rb + j], me, false, 0, std::nullopt);
+      for (size_t k = 0; k < K; ++k) {
+        if (pol.weightOf(k, nh) > 0) nz[(k * A + a) * W + j / 32] |= 1u << (j % 32);
+      }
+    }
+  }
+  D.pfxMatch.upload(pm.data(), pm.size());
+  D.tagMatch.upload(tm.data(), tm.size());
+  D.nonzero.upload(nz.data(), nz.size());
+  D.applied.resize(std::max<size_t>(P, 1));
+  D.counter.resize(std::max<size_t>(P, 1));
+  ogs_rib_policy rp{int32_t(K), active, D.pfxMatch.as<uint32_t>(), D.tagMatch.as<uint32_t>(),
+                    D.nonzero.as<uint32_t>()};
+  ogsCheck(ogs_rib_policy_apply(&pt, &rp, int32_t(A), 1, W, dMeta, dMask,
+                                D.applied.as<uint8_t>(), D.counter.as<uint8_t>(), nullptr),
+           "ogs_rib_policy_apply");
+  applied.assign(P, 0xFF);
+  counter.assign(P, 0xFF);
+  if (P) {
+    D.applied.download(applied.data(), P);
+    D.counter.download(counter.data(), P);
+  }
+}
+
+// Route-level effect of the device policy: counterID of the last matching
+// statement, weights of the applied one (RibPolicy.cpp:115-160).
+void finishPolicy(const RibPolicy* pol, uint8_t applied, uint8_t counter,
+                  RibUnicastEntry& e) {
+  if (!pol) return;
+  if (counter != 0xFF) e.counterID = pol->counterIDOf(counter);
+  if (applied == 0xFF) return;
+  NextHops w;
+  for (NextHopThrift nh : e.nexthops) {
+    nh.weight = pol->weightOf(applied, nh);
+    w.insert(std::move(nh));
+  }
+  e.nexthops = std::move(w);
 }
 
 }  // namespace
@@ -281,10 +360,13 @@ DecisionRouteDb materializeRouteDb(
     e.bestArea = pt.advKey[best].second;
     e.igpCost = static_cast<unsigned int>(r.metric[p]);
     e.localRouteConsidered = meta & OGS_ROUTE_LOCAL;
+    if (r.policy) finishPolicy(r.policy, r.applied[p], r.counter[p], e);
     rdb.unicastRoutes.emplace(e.prefix, std::move(e));
   }
   for (const auto& [prefix, e] : statics) {  // SpfSolver.cpp:343-349
-    if (!rdb.unicastRoutes.count(prefix)) rdb.unicastRoutes.emplace(prefix, e);
+    if (rdb.unicastRoutes.count(prefix)) continue;
+    auto it = rdb.unicastRoutes.emplace(prefix, e).first;
+    if (r.policy) r.policy->applyAction(it->second);  // policy covers statics too
   }
 
   // node-label MPLS routes from the SPF result (SpfSolver.cpp:354-445)
@@ -439,6 +521,13 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(
                           flags, W, &out, nullptr),
            "ogs_spf_routes");
   ls.noteSpfRuns(1);
+  const RibPolicy* policy = (ribPolicy_ && ribPolicy_->isActive()) ? ribPolicy_ : nullptr;
+  std::vector<uint8_t> applied, counter;
+  if (policy && P) {
+    if (wide) throw std::domain_error("RibPolicy on the GPU path needs 32-bit distances");
+    runPolicyOnDevice(*policy, I.table, pt, {{&f, s}}, me, W, I.meta.as<uint32_t>(),
+                      I.mask.as<uint32_t>(), I.policy, applied, counter);
+  }
 
   auto widen = [&](const DeviceBuffer& b, size_t n, std::vector<uint64_t>& v) {
     v.resize(n);
@@ -474,6 +563,11 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(
   view.mask = mask.data();
   view.maskStride = P;
   view.sel = sel.data();
+  if (policy && P) {
+    view.policy = policy;
+    view.applied = applied.data();
+    view.counter = counter.data();
+  }
   return materializeRouteDb(ls, f, area, me, view, I.table, v4OverV6Nexthop_,
                             enableNodeSegmentLabel_, staticUnicastRoutes_,
                             &bestRoutesCache_);
@@ -625,10 +719,13 @@ DecisionRouteDb SpfSolver::materializeMultiArea(const std::string& me,
     e.bestArea = pt.advKey[best].second;
     e.igpCost = static_cast<unsigned int>(R.metric[p]);
     e.localRouteConsidered = m & OGS_ROUTE_LOCAL;
+    if (!R.applied.empty()) finishPolicy(ribPolicy_, R.applied[p], R.counter[p], e);
     rdb.unicastRoutes.emplace(e.prefix, std::move(e));
   }
   for (const auto& [prefix, e] : staticUnicastRoutes_) {  // SpfSolver.cpp:343-349
-    if (!rdb.unicastRoutes.count(prefix)) rdb.unicastRoutes.emplace(prefix, e);
+    if (rdb.unicastRoutes.count(prefix)) continue;
+    auto it = rdb.unicastRoutes.emplace(prefix, e).first;
+    if (ribPolicy_ && ribPolicy_->isActive()) ribPolicy_->applyAction(it->second);
   }
   if (enableNodeSegmentLabel_) {
     LabelRoutes labelToNode;
@@ -735,6 +832,15 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDbMultiArea(
                                   M.spfRow.as<uint32_t>(), M.dist.as<uint32_t>(),
                                   M.nh.as<uint32_t>(), flags, W, &out, nullptr),
              "ogs_routes_multiarea");
+    if (ribPolicy_ && ribPolicy_->isActive()) {
+      std::vector<std::pair<const FlatTopology*, uint32_t>> src;
+      for (uint32_t a = 0; a < A; ++a) {
+        auto it = M.flats[a]->id.find(me);
+        src.emplace_back(M.flats[a], it == M.flats[a]->id.end() ? OGS_NODE_NONE : it->second);
+      }
+      runPolicyOnDevice(*ribPolicy_, M.table, pt, src, me, W, M.meta.as<uint32_t>(),
+                        M.mask.as<uint32_t>(), impl_->policy, R.applied, R.counter);
+    }
   }
   R.dist32.resize(su.size() * Sn);
   R.nh.resize(su.size() * W * Sn);
@@ -822,6 +928,33 @@ bool RibPolicy::matchStmt(const Stmt& s, const RibUnicastEntry& r) const {
     }
   }
   return tag && (s.prefixes.empty() || s.prefixes.count(r.prefix));
+}
+
+bool RibPolicy::matchesTags(size_t k, const std::set<std::string>& tags) const {
+  const Stmt& s = stmts_[k];
+  if (s.tags.empty()) return true;
+  for (const auto& t : s.tags) {
+    if (tags.count(t)) return true;
+  }
+  return false;
+}
+
+int32_t RibPolicy::weightOf(size_t k, const NextHopThrift& nh) const {
+  const Stmt& s = stmts_[k];  // neighbor > area > default (RibPolicy.cpp:122-137)
+  int32_t w = s.weight.default_weight;
+  if (nh.area) {
+    if (auto it = s.weight.area_to_weight.find(*nh.area);
+        it != s.weight.area_to_weight.end()) {
+      w = it->second;
+    }
+  }
+  if (nh.neighborNodeName) {
+    if (auto it = s.weight.neighbor_to_weight.find(*nh.neighborNodeName);
+        it != s.weight.neighbor_to_weight.end()) {
+      w = it->second;
+    }
+  }
+  return w;
 }
 
 bool RibPolicy::match(const RibUnicastEntry& r) const {

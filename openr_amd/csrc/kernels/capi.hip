@@ -28,6 +28,10 @@ hipError_t launch_variants(const ogs_graph& g, const ogs_prefix_table& pt,
                            const ogs_unit_mods* mods, const ogs_route_diff* diff,
                            uint32_t flags, int W, const ogs_spf_out& out,
                            hipStream_t stream, int* unsupported);
+hipError_t launch_rib_policy(const ogs_prefix_table& pt, const ogs_rib_policy& pol,
+                             int A, int nUnits, int W, const uint32_t* meta,
+                             uint32_t* mask, uint8_t* applied, uint8_t* counter,
+                             hipStream_t stream);
 hipError_t launch_ksp(const ogs_graph& g, const ogs_path_unit* units,
                       int nUnits, const uint32_t* masks, uint32_t maskWords,
                       uint32_t flags, const ogs_path_out& out,
@@ -270,6 +274,32 @@ int ogs_spf_routes_variants(const ogs_graph* graph,
                 "32-bit distances)");
   }
   return e == hipSuccess ? OGS_OK : hipFail(e, "variant launch");
+}
+
+int ogs_rib_policy_apply(const ogs_prefix_table* prefixes,
+                         const ogs_rib_policy* policy, int32_t num_areas,
+                         int32_t n_units, int32_t nh_words,
+                         const uint32_t* meta, uint32_t* mask,
+                         uint8_t* applied, uint8_t* counter, void* stream) {
+  if (!prefixes || !policy || !meta || !mask) {
+    return fail(OGS_E_INVALID, "prefixes/policy/meta/mask is NULL");
+  }
+  if (n_units < 0 || num_areas < 1 || num_areas > 32) {
+    return fail(OGS_E_INVALID, "n_units < 0 or num_areas outside [1, 32]");
+  }
+  if (n_units == 0 || policy->num_statements == 0) return OGS_OK;
+  if (policy->num_statements < 0 || policy->num_statements > 32 ||
+      !policy->pfx_match || !policy->adv_tag_match || !policy->slot_nonzero ||
+      !prefixes->pfx_base || !prefixes->adv_off) {
+    return fail(OGS_E_INVALID, "policy tables NULL or more than 32 statements");
+  }
+  if (ogs_nh_words_for_degree(nh_words * 32) != nh_words) {
+    return fail(OGS_E_UNSUPPORTED, "nh_words must be 1, 2, 4, 8 or 16");
+  }
+  hipError_t e = ogs::launch_rib_policy(*prefixes, *policy, num_areas, n_units, nh_words,
+                                        meta, mask, applied, counter,
+                                        static_cast<hipStream_t>(stream));
+  return e == hipSuccess ? OGS_OK : hipFail(e, "rib policy launch");
 }
 
 int ogs_routes_multiarea(const ogs_graph* graph,

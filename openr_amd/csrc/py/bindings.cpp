@@ -5,6 +5,8 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <optional>
+
 #include <sstream>
 
 #include "../gen/topogen.h"
@@ -212,6 +214,7 @@ std::string canonical(const DecisionRouteDb& db) {
     os << "U " << p << " c=" << r.igpCost << " a=" << r.bestArea
        << " dm=" << r.bestPrefixEntry.metrics.drain_metric
        << " bp=" << r.bestPrefixEntry.prefix << " l=" << r.localRouteConsidered
+       << " cid=" << r.counterID.value_or("-")
        << "\n";
     for (const auto& nh : r.nexthops) {
       os << "  " << nh.address << "%" << nh.ifName.value_or("") << " m=" << nh.metric
@@ -272,6 +275,7 @@ void loadLsdb(const topogen::Lsdb& g, LinkState& ls, PrefixState& ps) {
     e.metrics.distance = p.distance;
     e.metrics.drain_metric = p.drain_metric;
     if (p.minNexthop >= 0) e.minNexthop = p.minNexthop;
+    e.tags.insert(p.tags.begin(), p.tags.end());
     ps.updatePrefix(p.node, g.area, e);
   }
 }
@@ -298,6 +302,7 @@ topogen::Lsdb genLsdb(const std::string& kind, const py::dict& d) {
   m.anycastPermille = get<int>(d, "anycastPermille", 0);
   m.minNhPermille = get<int>(d, "minNhPermille", 0);
   m.drainPermille = get<int>(d, "drainPermille", 0);
+  m.tagPermille = get<int>(d, "tagPermille", 0);
   m.seed = get<uint64_t>(d, "mixSeed", 0x3F);
   topogen::applyPrefixMix(db, m);
   return db;
@@ -749,6 +754,37 @@ py::array_t<T> npcopy(const std::vector<T>& v) {
 
 }  // namespace
 
+namespace {
+std::vector<RibPolicyStatementSpec> parseStatements(py::list stmts) {
+  std::vector<RibPolicyStatementSpec> v;
+  for (auto h : stmts) {
+    py::dict d = h.cast<py::dict>();
+    RibPolicyStatementSpec s;
+    s.name = get<std::string>(d, "name", "");
+    if (d.contains("prefixes") && !d["prefixes"].is_none())
+      s.prefixes = d["prefixes"].cast<std::vector<std::string>>();
+    if (d.contains("tags") && !d["tags"].is_none())
+      s.tags = d["tags"].cast<std::vector<std::string>>();
+    if (d.contains("set_weight") && !d["set_weight"].is_none()) {
+      py::dict w = d["set_weight"];
+      RibRouteActionWeight a;
+      a.default_weight = get<int32_t>(w, "default_weight", 0);
+      if (w.contains("area_to_weight"))
+        a.area_to_weight = w["area_to_weight"].cast<std::map<std::string, int32_t>>();
+      if (w.contains("neighbor_to_weight"))
+        a.neighbor_to_weight =
+            w["neighbor_to_weight"].cast<std::map<std::string, int32_t>>();
+      s.set_weight = a;
+    }
+    if (d.contains("counterID") && !d["counterID"].is_none())
+      s.counterID = d["counterID"].cast<std::string>();
+    v.push_back(s);
+  }
+  return v;
+}
+
+}  // namespace
+
 PYBIND11_MODULE(_decision, m) {
   m.doc() = "MI355X (gfx950) SPF + RouteDb engine: Open/R Decision drop-in";
 
@@ -882,6 +918,9 @@ PYBIND11_MODULE(_decision, m) {
              for (auto kv : upd) u[kv.first.cast<std::string>()] = toRoute(kv.second.cast<py::dict>());
              s.updateStaticUnicastRoutes(u, del);
            })
+      .def("setRibPolicy",
+           [](SpfSolver& s, const RibPolicy* p) { s.setRibPolicy(p); },
+           py::arg("policy").none(true), py::keep_alive<1, 2>())
       .def("getBestRoutesCache", [](const SpfSolver& s) {
         py::dict out;
         for (const auto& [p, r] : s.getBestRoutesCache()) {
@@ -896,31 +935,7 @@ PYBIND11_MODULE(_decision, m) {
 
   py::class_<RibPolicy>(m, "RibPolicy")
       .def(py::init([](py::list stmts, int64_t ttl) {
-             std::vector<RibPolicyStatementSpec> v;
-             for (auto h : stmts) {
-               py::dict d = h.cast<py::dict>();
-               RibPolicyStatementSpec s;
-               s.name = get<std::string>(d, "name", "");
-               if (d.contains("prefixes") && !d["prefixes"].is_none())
-                 s.prefixes = d["prefixes"].cast<std::vector<std::string>>();
-               if (d.contains("tags") && !d["tags"].is_none())
-                 s.tags = d["tags"].cast<std::vector<std::string>>();
-               if (d.contains("set_weight") && !d["set_weight"].is_none()) {
-                 py::dict w = d["set_weight"];
-                 RibRouteActionWeight a;
-                 a.default_weight = get<int32_t>(w, "default_weight", 0);
-                 if (w.contains("area_to_weight"))
-                   a.area_to_weight = w["area_to_weight"].cast<std::map<std::string, int32_t>>();
-                 if (w.contains("neighbor_to_weight"))
-                   a.neighbor_to_weight =
-                       w["neighbor_to_weight"].cast<std::map<std::string, int32_t>>();
-                 s.set_weight = a;
-               }
-               if (d.contains("counterID") && !d["counterID"].is_none())
-                 s.counterID = d["counterID"].cast<std::string>();
-               v.push_back(s);
-             }
-             return RibPolicy(v, ttl);
+             return RibPolicy(parseStatements(stmts), ttl);
            }),
            py::arg("statements"), py::arg("ttl_secs") = 3600)
       .def("isActive", &RibPolicy::isActive)
@@ -952,7 +967,7 @@ PYBIND11_MODULE(_decision, m) {
   // Multi-area domain (topogen::multiArea): canonical RouteDbs per source.
   m.def("gen_route_dbs_multiarea",
         [](py::dict d, std::vector<std::string> sources, bool enableV4, bool sr,
-           bool brs) {
+           bool brs, py::list policy) {
           topogen::MultiAreaOpts o;
           o.areas = get<int>(d, "areas", 8);
           o.nodesPerArea = get<int>(d, "nodesPerArea", 1250);
@@ -972,6 +987,7 @@ PYBIND11_MODULE(_decision, m) {
             m.v4Permille = get<int>(d, "v4Permille", 0);
             m.minNhPermille = get<int>(d, "minNhPermille", 0);
             m.drainPermille = get<int>(d, "drainPermille", 0);
+            m.tagPermille = get<int>(d, "tagPermille", 0);
             m.seed = get<uint64_t>(d, "mixSeed", 0x3F) + a;
             topogen::applyPrefixMix(lsdbs[a], m);
             auto& ls = als.emplace(lsdbs[a].area, LinkState(lsdbs[a].area, "test_node"))
@@ -979,6 +995,11 @@ PYBIND11_MODULE(_decision, m) {
             loadLsdb(lsdbs[a], ls, ps);
           }
           SpfSolver solver("test_node", enableV4, sr, brs);
+          std::optional<RibPolicy> pol;
+          if (!policy.empty()) {
+            pol.emplace(parseStatements(policy), 3600);
+            solver.setRibPolicy(&*pol);
+          }
           std::vector<py::bytes> out;
           for (const auto& s : sources) {
             auto db = solver.buildRouteDb(s, als, ps);
@@ -987,24 +1008,31 @@ PYBIND11_MODULE(_decision, m) {
           return out;
         },
         py::arg("opts"), py::arg("sources"), py::arg("enableV4") = true,
-        py::arg("sr") = false, py::arg("brs") = false);
+        py::arg("sr") = false, py::arg("brs") = false, py::arg("policy") = py::list());
 
   m.def("gen_route_dbs",
         [](const std::string& kind, py::dict opts, std::vector<std::string> sources,
-           bool enableV4, bool sr, bool brs) {
+           bool enableV4, bool sr, bool brs, py::list policy) {
           auto g = genLsdb(kind, opts);
           AreaLinkStates als;
           auto& ls = als.emplace(g.area, LinkState(g.area, "test_node")).first->second;
           PrefixState ps;
           loadLsdb(g, ls, ps);
           SpfSolver solver("test_node", enableV4, sr, brs);
+          std::optional<RibPolicy> pol;
+          if (!policy.empty()) {
+            pol.emplace(parseStatements(policy), 3600);
+            solver.setRibPolicy(&*pol);
+          }
           std::vector<py::bytes> out;
           for (const auto& s : sources) {
             auto db = solver.buildRouteDb(s, als, ps);
             out.push_back(py::bytes(db ? canonical(*db) : std::string("NONE")));
           }
           return out;
-        });
+        },
+        py::arg("kind"), py::arg("opts"), py::arg("sources"), py::arg("enableV4") = true,
+        py::arg("sr") = false, py::arg("brs") = false, py::arg("policy") = py::list());
 
   py::class_<VariantRunner>(m, "VariantRunner")
       .def(py::init<bool, bool>(), py::arg("enableV4") = true,

@@ -272,6 +272,7 @@ void loadLsdb(const topogen::Lsdb& g, LinkState& ls, PrefixState& ps) {
     e.metrics.distance = p.distance;
     e.metrics.drain_metric = p.drain_metric;
     if (p.minNexthop >= 0) e.minNexthop = p.minNexthop;
+    e.tags.insert(p.tags.begin(), p.tags.end());
     ps.updatePrefix(p.node, g.area, e);
   }
 }
@@ -283,6 +284,7 @@ std::string canonical(const DecisionRouteDb& db) {
     os << "U " << p << " c=" << r.igpCost << " a=" << r.bestArea
        << " dm=" << r.bestPrefixEntry.metrics.drain_metric
        << " bp=" << r.bestPrefixEntry.prefix << " l=" << r.localRouteConsidered
+       << " cid=" << r.counterID.value_or("-")
        << "\n";
     for (const auto& nh : r.nexthops) {
       os << "  " << nh.addr << "%" << nh.ifName.value_or("") << " m=" << nh.metric
@@ -332,6 +334,7 @@ topogen::Lsdb genLsdb(const std::string& kind, const py::dict& d) {
   m.anycastPermille = get<int>(d, "anycastPermille", 0);
   m.minNhPermille = get<int>(d, "minNhPermille", 0);
   m.drainPermille = get<int>(d, "drainPermille", 0);
+  m.tagPermille = get<int>(d, "tagPermille", 0);
   m.seed = get<uint64_t>(d, "mixSeed", 0x3F);
   topogen::applyPrefixMix(db, m);
   return db;
@@ -373,6 +376,37 @@ struct Workspace {  // one private replica (LinkState is not thread-safe)
   AreaLinkStates als;
   PrefixState ps;
 };
+
+}  // namespace
+
+namespace {
+std::vector<RibPolicyStatementSpec> parseStatements(py::list stmts) {
+  std::vector<RibPolicyStatementSpec> v;
+  for (auto h : stmts) {
+    py::dict d = h.cast<py::dict>();
+    RibPolicyStatementSpec s;
+    s.name = get<std::string>(d, "name", "");
+    if (d.contains("prefixes") && !d["prefixes"].is_none())
+      s.prefixes = d["prefixes"].cast<std::vector<std::string>>();
+    if (d.contains("tags") && !d["tags"].is_none())
+      s.tags = d["tags"].cast<std::vector<std::string>>();
+    if (d.contains("set_weight") && !d["set_weight"].is_none()) {
+      py::dict w = d["set_weight"];
+      RibRouteActionWeight a;
+      a.default_weight = get<int32_t>(w, "default_weight", 0);
+      if (w.contains("area_to_weight"))
+        a.area_to_weight = w["area_to_weight"].cast<std::map<std::string, int32_t>>();
+      if (w.contains("neighbor_to_weight"))
+        a.neighbor_to_weight =
+            w["neighbor_to_weight"].cast<std::map<std::string, int32_t>>();
+      s.set_weight = a;
+    }
+    if (d.contains("counterID") && !d["counterID"].is_none())
+      s.counterID = d["counterID"].cast<std::string>();
+    v.push_back(s);
+  }
+  return v;
+}
 
 }  // namespace
 
@@ -517,31 +551,7 @@ PYBIND11_MODULE(_refcpu, m) {
 
   py::class_<RibPolicy>(m, "RibPolicy")
       .def(py::init([](py::list stmts, int64_t ttl) {
-             std::vector<RibPolicyStatementSpec> v;
-             for (auto h : stmts) {
-               py::dict d = h.cast<py::dict>();
-               RibPolicyStatementSpec s;
-               s.name = get<std::string>(d, "name", "");
-               if (d.contains("prefixes") && !d["prefixes"].is_none())
-                 s.prefixes = d["prefixes"].cast<std::vector<std::string>>();
-               if (d.contains("tags") && !d["tags"].is_none())
-                 s.tags = d["tags"].cast<std::vector<std::string>>();
-               if (d.contains("set_weight") && !d["set_weight"].is_none()) {
-                 py::dict w = d["set_weight"];
-                 RibRouteActionWeight a;
-                 a.default_weight = get<int32_t>(w, "default_weight", 0);
-                 if (w.contains("area_to_weight"))
-                   a.area_to_weight = w["area_to_weight"].cast<std::map<std::string, int32_t>>();
-                 if (w.contains("neighbor_to_weight"))
-                   a.neighbor_to_weight =
-                       w["neighbor_to_weight"].cast<std::map<std::string, int32_t>>();
-                 s.set_weight = a;
-               }
-               if (d.contains("counterID") && !d["counterID"].is_none())
-                 s.counterID = d["counterID"].cast<std::string>();
-               v.push_back(s);
-             }
-             return RibPolicy(v, ttl);
+             return RibPolicy(parseStatements(stmts), ttl);
            }),
            py::arg("statements"), py::arg("ttl_secs") = 3600)
       .def("isActive", &RibPolicy::isActive)
@@ -575,7 +585,7 @@ PYBIND11_MODULE(_refcpu, m) {
   // Multi-area domain (topogen::multiArea): canonical RouteDbs per source.
   m.def("gen_route_dbs_multiarea",
         [](py::dict d, std::vector<std::string> sources, bool enableV4, bool sr,
-           bool brs) {
+           bool brs, py::list policy) {
           topogen::MultiAreaOpts o;
           o.areas = get<int>(d, "areas", 8);
           o.nodesPerArea = get<int>(d, "nodesPerArea", 1250);
@@ -595,6 +605,7 @@ PYBIND11_MODULE(_refcpu, m) {
             m.v4Permille = get<int>(d, "v4Permille", 0);
             m.minNhPermille = get<int>(d, "minNhPermille", 0);
             m.drainPermille = get<int>(d, "drainPermille", 0);
+            m.tagPermille = get<int>(d, "tagPermille", 0);
             m.seed = get<uint64_t>(d, "mixSeed", 0x3F) + a;
             topogen::applyPrefixMix(lsdbs[a], m);
             auto& ls = als.emplace(lsdbs[a].area, LinkState(lsdbs[a].area, "test_node"))
@@ -605,12 +616,16 @@ PYBIND11_MODULE(_refcpu, m) {
           std::vector<py::bytes> out;
           for (const auto& s : sources) {
             auto db = solver.buildRouteDb(s, als, ps);
+            if (db && !policy.empty()) {
+              RibPolicy pol(parseStatements(policy), 3600);
+              pol.applyPolicy(db->unicastRoutes);
+            }
             out.push_back(py::bytes(db ? canonical(*db) : std::string("NONE")));
           }
           return out;
         },
         py::arg("opts"), py::arg("sources"), py::arg("enableV4") = true,
-        py::arg("sr") = false, py::arg("brs") = false);
+        py::arg("sr") = false, py::arg("brs") = false, py::arg("policy") = py::list());
 
   // Link-failure variants (config C4): the reference's adjacency-DB update
   // with the links removed at both ends, buildRouteDb, and calculateUpdate
@@ -731,7 +746,7 @@ PYBIND11_MODULE(_refcpu, m) {
 
   m.def("gen_route_dbs",
         [](const std::string& kind, py::dict opts, std::vector<std::string> sources,
-           bool enableV4, bool sr, bool bestRouteSel) {
+           bool enableV4, bool sr, bool bestRouteSel, py::list policy) {
           auto g = genLsdb(kind, opts);
           Workspace w;
           auto& ls = w.als.emplace(g.area, LinkState(g.area, "test_node")).first->second;
@@ -740,10 +755,16 @@ PYBIND11_MODULE(_refcpu, m) {
           std::vector<py::bytes> out;
           for (const auto& s : sources) {
             auto db = solver.buildRouteDb(s, w.als, w.ps);
+            if (db && !policy.empty()) {
+              RibPolicy pol(parseStatements(policy), 3600);
+              pol.applyPolicy(db->unicastRoutes);
+            }
             out.push_back(py::bytes(db ? canonical(*db) : std::string("NONE")));
           }
           return out;
-        });
+        },
+        py::arg("kind"), py::arg("opts"), py::arg("sources"), py::arg("enableV4") = true,
+        py::arg("sr") = false, py::arg("brs") = false, py::arg("policy") = py::list());
 
   // Grid batch (config C2): topology i uses metric seed base+i and prefix
   // seed pbase+i. Returns canonical DBs for topologies [lo, hi).

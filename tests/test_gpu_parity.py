@@ -395,3 +395,63 @@ def test_multi_area_large_areas(product, oracle):
     srcs = ["abr-1", "a1-399", "a0-5"]
     _cmp(product.gen_route_dbs_multiarea(opts, srcs, True, False, True),
          oracle.gen_route_dbs_multiarea(opts, srcs, True, False, True), "multiarea400")
+
+
+def _ucmp_policy(plain, zero_nbr, area):
+    """UCMP statements over prefixes picked from a policy-free DB (so the
+    prefix matcher hits): tag / prefix / area / neighbor weights incl. zero
+    weights (next hop dropped, route removed when none is left) and
+    overlapping statements (last matching counterID wins)."""
+    pfx = [ln.split()[1] for ln in plain.decode().splitlines() if ln.startswith("U ")]
+    return [
+        dict(name="ucmp", tags=["ucmp"], counterID="cnt-ucmp",
+             set_weight=dict(default_weight=3, area_to_weight={area: 5, "area2": 0},
+                             neighbor_to_weight={zero_nbr: 0, "abr-1": 4})),
+        dict(name="pfx", prefixes=pfx[::7], counterID="cnt-pfx",
+             set_weight=dict(default_weight=0, neighbor_to_weight={zero_nbr: 6})),
+        dict(name="c1", tags=["c1"], counterID="cnt-c1",
+             set_weight=dict(default_weight=2, area_to_weight={"area0": 9})),
+        dict(name="c3", tags=["c3", "nope"],  # no counterID: keeps the earlier one
+             set_weight=dict(default_weight=1, neighbor_to_weight={zero_nbr: 8})),
+    ]
+
+
+@pytest.mark.parametrize("brs", [False, True])
+def test_rib_policy_wan(product, oracle, brs):
+    """RibPolicy (UCMP weights, counterIDs) applied on the GPU to every route
+    of a 500-node WAN with the prefix mix: bit-exact vs the oracle's
+    RibPolicy::applyPolicy over its RouteDb."""
+    opts = dict(nodes=500, seed=0xC6, prefixesPerNode=2, tagPermille=500, **MIX)
+    srcs = ["0", "17", "250", "499"]
+    plain = oracle.gen_route_dbs("wan", opts, srcs[:1], True, False, brs)[0]
+    pol = _ucmp_policy(plain, "1", "0")
+    _cmp(product.gen_route_dbs("wan", opts, srcs, True, False, brs, pol),
+         oracle.gen_route_dbs("wan", opts, srcs, True, False, brs, pol), "policy_wan")
+
+
+def test_rib_policy_statement_without_action(product):
+    """A statement without set_weight is rejected (RibPolicy.cpp:20-30)."""
+    with pytest.raises(ValueError):
+        product.RibPolicy([dict(name="bad", tags=["c1"])])
+
+
+def test_rib_policy_grid_small(product, oracle):
+    """Policy on the wave (small-topology) kernel path."""
+    opts = dict(n=6, metricSeed=0xC2000001, prefixSeed=1, tagPermille=400)
+    srcs = [str(i) for i in range(0, 36, 5)]
+    plain = oracle.gen_route_dbs("grid", opts, srcs[:1], True, True, False)[0]
+    pol = _ucmp_policy(plain, "1", "0")
+    _cmp(product.gen_route_dbs("grid", opts, srcs, True, True, False, pol),
+         oracle.gen_route_dbs("grid", opts, srcs, True, True, False, pol), "policy_grid")
+
+
+@pytest.mark.parametrize("brs", [False, True])
+def test_rib_policy_multi_area(product, oracle, brs):
+    """Policy over multi-area RouteDbs (area weights per next-hop area)."""
+    opts = dict(MA, v4Permille=100, drainPermille=50)
+    srcs = ["abr-0", "abr-1", "a0-7", "a2-59"]
+    plain = oracle.gen_route_dbs_multiarea(opts, srcs[:1], True, False, brs)[0]
+    pol = _ucmp_policy(plain, "a0-3", "area1")
+    _cmp(product.gen_route_dbs_multiarea(opts, srcs, True, False, brs, pol),
+         oracle.gen_route_dbs_multiarea(opts, srcs, True, False, brs, pol),
+         "policy_multiarea")

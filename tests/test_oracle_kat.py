@@ -78,3 +78,37 @@ def test_oracle_variant_updates(oracle):
         diff = sorted(p for p in set(b) | set(v) if b.get(p) != v.get(p))
         assert changed == diff
         assert nd == len(set(b) - set(v))
+
+
+def _policy(prefixes=(), zero_nbr="", area="area1"):
+    """UCMP RibPolicy statements (RibPolicy.h:40-90 semantics): tag matcher with
+    area/neighbor weights (incl. zero = drop next hop), a prefix matcher, and a
+    second tag statement whose counterID overrides the first's on overlap."""
+    return [
+        dict(name="ucmp", tags=["ucmp"], counterID="cnt-ucmp",
+             set_weight=dict(default_weight=3, area_to_weight={area: 5, "area2": 0},
+                             neighbor_to_weight={zero_nbr: 0} if zero_nbr else {})),
+        dict(name="pfx", prefixes=list(prefixes), counterID="cnt-pfx",
+             set_weight=dict(default_weight=0, neighbor_to_weight={})),
+        dict(name="c1", tags=["c1"], counterID="cnt-c1",
+             set_weight=dict(default_weight=2, area_to_weight={"area0": 9})),
+    ]
+
+
+def _weights(c):
+    return [ln.split(" w=")[1].split()[0] for ln in c.decode().splitlines()
+            if " w=" in ln]
+
+
+def test_oracle_policy_changes_weights(oracle):
+    """The generated-DB helper applies the policy: weights other than 0 appear,
+    counterIDs are set, and an empty policy leaves the DB unchanged."""
+    opts = dict(nodes=120, seed=0xC5, prefixesPerNode=2, tagPermille=500)
+    [plain] = oracle.gen_route_dbs("wan", opts, ["3"], True, False, False)
+    [same] = oracle.gen_route_dbs("wan", opts, ["3"], True, False, False, [])
+    [pol] = oracle.gen_route_dbs("wan", opts, ["3"], True, False, False,
+                                 _policy(area="0"))
+    assert plain == same and plain != pol
+    assert set(_weights(plain)) == {"0"}
+    assert {"2", "3"} <= set(_weights(pol))
+    assert b"cid=cnt-ucmp" in pol and b"cid=cnt-c1" in pol
