@@ -281,6 +281,21 @@ int ogs_ksp_paths(const ogs_graph* graph, const ogs_path_unit* units,
                   int32_t n_units, const uint32_t* masks, uint32_t mask_words,
                   uint32_t flags, ogs_path_out* out, void* stream);
 
+/* Batched KSP2 (config C5): for each unit (topo, src, dest, reserved), the
+ * paths of getKthPaths(src, dest, 1) into k1 and of getKthPaths(src, dest, 2)
+ * into k2 (LinkState.cpp:674-703), in two launches on `stream`: one
+ * unmasked SPF per entry of `sources` (device, n_sources (topo, src) pairs:
+ * the memoised getSpfResult(src)), then per unit the k = 1 trace on that
+ * SPF, a rerun with the k = 1 links ignored and the k = 2 trace. A unit's
+ * `reserved` field is the index of its (topo, src) in `sources`; a unit
+ * whose index is out of range or names another (topo, src) gets
+ * path_count 0xC0000000 in both outputs. Distances of the sources live in
+ * the per-device workspace. */
+int ogs_ksp2_paths(const ogs_graph* graph, const ogs_unit* sources,
+                   int32_t n_sources, const ogs_path_unit* units,
+                   int32_t n_units, uint32_t flags, ogs_path_out* k1,
+                   ogs_path_out* k2, void* stream);
+
 /* Link-failure variants (config C4, the SURVEY §5 "link-flap variant"):
  * per unit, topology-local DIRECTED edge ids that are treated as removed --
  * the links an adjacency-database update deleted at both ends

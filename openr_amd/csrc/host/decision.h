@@ -254,6 +254,10 @@ class LinkState {
   const std::vector<Path>& getKthPaths(const std::string& src,
                                        const std::string& dest,
                                        size_t k) const;
+  // Fills getKthPaths(src, d, 1) and (src, d, 2) for every d of `dests` in
+  // one batched GPU call (Ksp2Batch); later getKthPaths calls hit the memo.
+  void prefetchKthPaths(const std::string& src,
+                        const std::vector<std::string>& dests) const;
   LinkStateChange updateAdjacencyDatabase(const AdjacencyDatabase& db,
                                           const std::string& area,
                                           bool inInitialization = false);
@@ -279,6 +283,7 @@ class LinkState {
   // GPU plumbing (used by SpfSolver and the batch builders)
   const FlatTopology& flat() const;          // re-flattens when stale
   const FlatTopology& flatOnDevice() const;  // + uploads when stale
+  LinkPtr linkByKey(const Link::Key& k) const { return links_.at(k); }
   void noteSpfRuns(uint64_t n) const { spfRuns_ += n; }
 
  private:
@@ -378,6 +383,36 @@ using AreaLinkStates = std::map<std::string, LinkState>;
 
 class RibPolicy;
 
+// ------------------------------------------------------------- Ksp2Batch --
+// getKthPaths(src, d, 1) and (src, d, 2) for many destinations d of one
+// LinkState, on the GPU (ogs_ksp2_paths): one unmasked SPF of src, then per
+// destination the k = 1 trace, the masked rerun and the k = 2 trace. The
+// device buffers stay resident; launch() may be repeated (benchmarks).
+class Ksp2Batch {
+ public:
+  Ksp2Batch(const LinkState& ls, const std::string& src,
+            const std::vector<std::string>& dests);
+  void launch(void* stream = nullptr) const;  // asynchronous
+  void fetch();                               // D2H of both path sets (sync)
+  size_t size() const { return dests_.size(); }
+  const std::vector<std::string>& dests() const { return dests_; }
+  // unit i's k-th (1 or 2) paths as topology-local directed edge ids
+  std::vector<std::vector<uint32_t>> edgePaths(size_t i, int k) const;
+  std::vector<LinkState::Path> paths(size_t i, int k) const;
+  size_t numUnits() const { return nUnits_; }
+  uint64_t totalPathEdges(int k) const;
+
+ private:
+  const LinkState& ls_;
+  std::vector<std::string> dests_;
+  std::vector<int64_t> unitOf_;  // dest index -> unit (-1: unknown dest)
+  size_t nUnits_{0};
+  uint32_t flags_{0}, maxPaths_{0}, maxEdges_{0};
+  ogs_graph g_{};
+  DeviceBuffer dSrc_, dUnits_, dCount_[2], dLen_[2], dEdges_[2];
+  std::vector<uint32_t> count_[2], len_[2], edges_[2];
+};
+
 // ------------------------------------------------------------- SpfSolver --
 class SpfSolver {
  public:
@@ -395,6 +430,13 @@ class SpfSolver {
   std::optional<RibUnicastEntry> createRouteForPrefixOrGetStaticRoute(
       const std::string& myNodeName, const AreaLinkStates& areaLinkStates,
       const PrefixState& prefixState, const std::string& prefix);
+  // Device-only buildRouteDb over the multi-area kernels (any number of
+  // areas): the source's SPF in every area, the RouteDb and the RibPolicy
+  // are enqueued on `stream` and left in device memory -- no download, no
+  // DecisionRouteDb. Returns false when myNodeName is in no area.
+  bool enqueueRouteDb(const std::string& myNodeName,
+                      const AreaLinkStates& areaLinkStates,
+                      const PrefixState& prefixState, void* stream);
   const std::map<std::string, RouteSelectionResult>& getBestRoutesCache()
       const {
     return bestRoutesCache_;
@@ -407,6 +449,11 @@ class SpfSolver {
 
  private:
   // several areas (SpfSolver.cpp:160-311 across LinkStates)
+  struct MultiAreaResult;
+  void enqueueMultiArea(const std::string& myNodeName,
+                        const AreaLinkStates& areaLinkStates,
+                        const PrefixState& prefixState, void* stream,
+                        MultiAreaResult& r);
   std::optional<DecisionRouteDb> buildRouteDbMultiArea(
       const std::string& myNodeName, const AreaLinkStates& areaLinkStates,
       const PrefixState& prefixState);
@@ -480,6 +527,12 @@ class RibPolicy {  // RibPolicy.h:70-124
   bool matchStmt(const Stmt& s, const RibUnicastEntry& r) const;
   std::vector<Stmt> stmts_;
   int64_t ttlSecs_;
+
+ public:
+  uint64_t uid() const { return uid_; }  // compiled-policy cache key
+
+ private:
+  uint64_t uid_;
 };
 
 // ---------------------------------------------------- batch flattening --
@@ -535,6 +588,7 @@ struct PrefixHostTable {
   std::vector<const PrefixEntry*> advEntry;
   std::vector<NodeAndArea> advKey;
   std::vector<uint32_t> advOff;
+  uint64_t generation{0};  // bumped by every build (compiled-policy cache key)
   void build(const PrefixState& ps);
 };
 

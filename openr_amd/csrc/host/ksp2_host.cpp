@@ -2,6 +2,7 @@
 // LinkState.cpp:674-703): the k-th call masks every link of the paths for
 // 1..k-1 and launches one KSP unit (masked SPF + greedy trace).
 #include <algorithm>
+#include <stdexcept>
 #include <unordered_map>
 
 #include "decision.h"
@@ -95,6 +96,138 @@ const std::vector<LinkState::Path>& LinkState::getKthPaths(
     paths.push_back(std::move(p));
   }
   return kthMemo_.emplace(key, std::move(paths)).first->second;
+}
+
+// ---- Ksp2Batch ----------------------------------------------------------
+Ksp2Batch::Ksp2Batch(const LinkState& ls, const std::string& src,
+                     const std::vector<std::string>& dests)
+    : ls_(ls), dests_(dests), unitOf_(dests.size(), -1) {
+  const FlatTopology& f = ls.flatOnDevice();
+  auto sIt = f.id.find(src);
+  if (sIt == f.id.end()) return;  // unknown source: no paths anywhere
+  if (f.hasZeroMetric || f.hasWideMetric) {
+    throw std::domain_error(
+        "Ksp2Batch: zero or negative link metric is outside the GPU engine's "
+        "exact domain");
+  }
+  std::vector<ogs_path_unit> units;
+  for (size_t i = 0; i < dests.size(); ++i) {
+    auto dIt = f.id.find(dests[i]);
+    if (dIt == f.id.end()) continue;
+    unitOf_[i] = int64_t(units.size());
+    units.push_back(ogs_path_unit{0, sIt->second, dIt->second, 0});
+  }
+  nUnits_ = units.size();
+  if (!nUnits_) return;
+  const uint32_t E = uint32_t(f.edges.size());
+  // edge-disjoint paths into d: at most deg(d) of them, at most E/2 links
+  maxPaths_ = uint32_t(f.maxDegree) + 1;
+  maxEdges_ = E / 2 + 1;
+  flags_ = wideDistancesNeeded(f) ? OGS_F_WIDE_METRIC : 0u;
+  const ogs_unit s{0, sIt->second};
+  dSrc_.upload(&s, 1);
+  dUnits_.upload(units.data(), units.size());
+  for (int k = 0; k < 2; ++k) {
+    dCount_[k].resize(nUnits_ * 4);
+    dLen_[k].resize(nUnits_ * maxPaths_ * 4);
+    dEdges_[k].resize(nUnits_ * maxEdges_ * 4);
+  }
+  g_.num_topos = 1;
+  g_.max_nodes = int32_t(f.names.size());
+  g_.max_edges = int32_t(E);
+  g_.max_degree = f.maxDegree;
+  g_.node_base = f.dNodeBase.as<uint32_t>();
+  g_.row_ptr = f.dRow.as<uint32_t>();
+  g_.edges = f.dEdges.as<uint64_t>();
+  g_.node_flags = f.dFlags.as<uint8_t>();
+}
+
+void Ksp2Batch::launch(void* stream) const {
+  if (!nUnits_) return;
+  ogs_path_out o[2];
+  for (int k = 0; k < 2; ++k) {
+    o[k] = ogs_path_out{const_cast<DeviceBuffer&>(dCount_[k]).as<uint32_t>(),
+                        const_cast<DeviceBuffer&>(dLen_[k]).as<uint32_t>(),
+                        const_cast<DeviceBuffer&>(dEdges_[k]).as<uint32_t>(),
+                        maxPaths_, maxEdges_};
+  }
+  ogsCheck(ogs_ksp2_paths(&g_, const_cast<DeviceBuffer&>(dSrc_).as<ogs_unit>(), 1,
+                          const_cast<DeviceBuffer&>(dUnits_).as<ogs_path_unit>(),
+                          int32_t(nUnits_), flags_, &o[0], &o[1], stream),
+           "ogs_ksp2_paths");
+}
+
+void Ksp2Batch::fetch() {
+  if (!nUnits_) return;
+  for (int k = 0; k < 2; ++k) {
+    count_[k].resize(nUnits_);
+    len_[k].resize(nUnits_ * maxPaths_);
+    edges_[k].resize(nUnits_ * maxEdges_);
+    dCount_[k].download(count_[k].data(), nUnits_);
+    dLen_[k].download(len_[k].data(), len_[k].size());
+    dEdges_[k].download(edges_[k].data(), edges_[k].size());
+  }
+  ogsCheck(ogs_stream_sync(nullptr), "ogs_stream_sync");
+  for (int k = 0; k < 2; ++k) {
+    for (uint32_t c : count_[k]) {
+      if (c >> 31) throw std::runtime_error("Ksp2Batch: path buffer overflow");
+    }
+  }
+}
+
+std::vector<std::vector<uint32_t>> Ksp2Batch::edgePaths(size_t i, int k) const {
+  std::vector<std::vector<uint32_t>> out;
+  if (k < 1 || k > 2) throw std::invalid_argument("Ksp2Batch: k must be 1 or 2");
+  const int64_t u = unitOf_.at(i);
+  if (u < 0) return out;
+  if (count_[k - 1].empty()) throw std::logic_error("Ksp2Batch: fetch() first");
+  const uint32_t n = count_[k - 1][u];
+  const uint32_t* len = len_[k - 1].data() + size_t(u) * maxPaths_;
+  const uint32_t* e = edges_[k - 1].data() + size_t(u) * maxEdges_;
+  for (uint32_t p = 0; p < n; ++p) {
+    out.emplace_back(e, e + len[p]);
+    e += len[p];
+  }
+  return out;
+}
+
+std::vector<LinkState::Path> Ksp2Batch::paths(size_t i, int k) const {
+  const FlatTopology& f = ls_.flat();
+  std::vector<LinkState::Path> out;
+  for (const auto& ep : edgePaths(i, k)) {
+    LinkState::Path p;
+    for (uint32_t e : ep) p.push_back(ls_.linkByKey(f.edgeLink[e]->key()));
+    out.push_back(std::move(p));
+  }
+  return out;
+}
+
+uint64_t Ksp2Batch::totalPathEdges(int k) const {
+  uint64_t t = 0;
+  for (size_t u = 0; u < nUnits_ && !count_[k - 1].empty(); ++u) {
+    const uint32_t* len = len_[k - 1].data() + u * maxPaths_;
+    for (uint32_t p = 0; p < count_[k - 1][u]; ++p) t += len[p];
+  }
+  return t;
+}
+
+void LinkState::prefetchKthPaths(const std::string& src,
+                                 const std::vector<std::string>& dests) const {
+  std::vector<std::string> todo;
+  for (const auto& d : dests) {
+    if (!kthMemo_.count({src, d, 1}) || !kthMemo_.count({src, d, 2})) {
+      todo.push_back(d);
+    }
+  }
+  if (todo.empty()) return;
+  Ksp2Batch b(*this, src, todo);
+  b.launch();
+  b.fetch();
+  if (b.numUnits()) spfRuns_ += 1 + b.numUnits();
+  for (size_t i = 0; i < todo.size(); ++i) {
+    kthMemo_[{src, todo[i], 1}] = b.paths(i, 1);
+    kthMemo_[{src, todo[i], 2}] = b.paths(i, 2);
+  }
 }
 
 }  // namespace openr_amd

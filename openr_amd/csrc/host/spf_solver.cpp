@@ -4,6 +4,7 @@
 // source and materialises the compact route records into RibUnicastEntry /
 // RibMplsEntry objects.
 #include <algorithm>
+#include <atomic>
 
 #include "decision.h"
 #include "slot_order.h"
@@ -145,6 +146,19 @@ int HostBatch::slotOrder(std::vector<uint16_t>& out,
 // device tables of a RibPolicy compiled for one source (runPolicyOnDevice)
 struct PolicyDevice {
   DeviceBuffer pfxMatch, tagMatch, nonzero, applied, counter;
+  // what the matcher tables were compiled for (recompiled on change)
+  struct Key {
+    uint64_t policy{0}, tableGen{0};
+    const PrefixHostTable* table{nullptr};
+    std::vector<std::tuple<const FlatTopology*, uint64_t, uint32_t>> src;
+    int W{0};
+    std::string me;
+    bool operator==(const Key& o) const {
+      return policy == o.policy && tableGen == o.tableGen && table == o.table &&
+          src == o.src && W == o.W && me == o.me;
+    }
+  } key;
+  ogs_rib_policy rp{};
 };
 
 struct SpfSolver::Impl {
@@ -217,55 +231,66 @@ NextHopThrift makeNh(const Link& l, const std::string& me, bool useV4,
 }
 
 // RibPolicy compiled on the host against the prefix table and the source's
-// links (per area), applied on the device (ogs_rib_policy_apply): next hops
-// of weight 0 dropped in the device masks; statement choices downloaded.
+// links (per area) -- cached until the policy, table or topology changes --
+// and applied on the device (ogs_rib_policy_apply): next hops of weight 0
+// dropped in the device masks, statement choices left in D.applied /
+// D.counter (downloadPolicy).
 void runPolicyOnDevice(const RibPolicy& pol, const PrefixHostTable& table,
                        const ogs_prefix_table& pt,
                        const std::vector<std::pair<const FlatTopology*, uint32_t>>& src,
                        const std::string& me, int W, uint32_t* dMeta, uint32_t* dMask,
-                       PolicyDevice& D, std::vector<uint8_t>& applied,
-                       std::vector<uint8_t>& counter) {
+                       PolicyDevice& D, void* stream) {
   const size_t K = pol.numStatements();
   if (K > 32) throw std::domain_error("RibPolicy: more than 32 statements on the GPU path");
   const size_t P = table.prefixes.size(), A = src.size();
-  std::vector<uint32_t> pm(std::max<size_t>(P, 1), 0), tm(std::max<size_t>(table.advEntry.size(), 1), 0);
-  std::vector<uint32_t> nz(std::max<size_t>(K * A * W, 1), 0);
-  uint32_t active = 0;
-  for (size_t k = 0; k < K; ++k) {
-    if (pol.hasMatcher(k)) active |= 1u << k;
-  }
-  for (size_t p = 0; p < P; ++p) {
+  PolicyDevice::Key key{pol.uid(), table.generation, &table, {}, W, me};
+  for (const auto& [f, s] : src) key.src.emplace_back(f, f->version, s);
+  if (!(key == D.key)) {
+    std::vector<uint32_t> pm(std::max<size_t>(P, 1), 0),
+        tm(std::max<size_t>(table.advEntry.size(), 1), 0);
+    std::vector<uint32_t> nz(std::max<size_t>(K * A * W, 1), 0);
+    uint32_t active = 0;
     for (size_t k = 0; k < K; ++k) {
-      if (pol.matchesPrefix(k, table.prefixes[p])) pm[p] |= 1u << k;
+      if (pol.hasMatcher(k)) active |= 1u << k;
     }
-  }
-  for (size_t a = 0; a < table.advEntry.size(); ++a) {
-    for (size_t k = 0; k < K; ++k) {
-      if (pol.matchesTags(k, table.advEntry[a]->tags)) tm[a] |= 1u << k;
-    }
-  }
-  for (size_t a = 0; a < A; ++a) {
-    const FlatTopology* f = src[a].first;
-    const uint32_t s = src[a].second;
-    if (s == OGS_NODE_NONE) continue;
-    const uint32_t rb = f->rowPtr[s], deg = f->rowPtr[s + 1] - rb;
-    for (uint32_t j = 0; j < deg && j < 32u * uint32_t(W); ++j) {
-      const NextHopThrift nh = makeNh(*f->edgeLink[rb + j], me, false, 0, std::nullopt);
+    for (size_t p = 0; p < P; ++p) {
       for (size_t k = 0; k < K; ++k) {
-        if (pol.weightOf(k, nh) > 0) nz[(k * A + a) * W + j / 32] |= 1u << (j % 32);
+        if (pol.matchesPrefix(k, table.prefixes[p])) pm[p] |= 1u << k;
       }
     }
+    for (size_t a = 0; a < table.advEntry.size(); ++a) {
+      for (size_t k = 0; k < K; ++k) {
+        if (pol.matchesTags(k, table.advEntry[a]->tags)) tm[a] |= 1u << k;
+      }
+    }
+    for (size_t a = 0; a < A; ++a) {
+      const FlatTopology* f = src[a].first;
+      const uint32_t s = src[a].second;
+      if (s == OGS_NODE_NONE) continue;
+      const uint32_t rb = f->rowPtr[s], deg = f->rowPtr[s + 1] - rb;
+      for (uint32_t j = 0; j < deg && j < 32u * uint32_t(W); ++j) {
+        const NextHopThrift nh = makeNh(*f->edgeLink[rb + j], me, false, 0, std::nullopt);
+        for (size_t k = 0; k < K; ++k) {
+          if (pol.weightOf(k, nh) > 0) nz[(k * A + a) * W + j / 32] |= 1u << (j % 32);
+        }
+      }
+    }
+    D.pfxMatch.upload(pm.data(), pm.size(), stream);
+    D.tagMatch.upload(tm.data(), tm.size(), stream);
+    D.nonzero.upload(nz.data(), nz.size(), stream);
+    D.applied.resize(std::max<size_t>(P, 1));
+    D.counter.resize(std::max<size_t>(P, 1));
+    D.rp = ogs_rib_policy{int32_t(K), active, D.pfxMatch.as<uint32_t>(),
+                          D.tagMatch.as<uint32_t>(), D.nonzero.as<uint32_t>()};
+    D.key = std::move(key);
   }
-  D.pfxMatch.upload(pm.data(), pm.size());
-  D.tagMatch.upload(tm.data(), tm.size());
-  D.nonzero.upload(nz.data(), nz.size());
-  D.applied.resize(std::max<size_t>(P, 1));
-  D.counter.resize(std::max<size_t>(P, 1));
-  ogs_rib_policy rp{int32_t(K), active, D.pfxMatch.as<uint32_t>(), D.tagMatch.as<uint32_t>(),
-                    D.nonzero.as<uint32_t>()};
-  ogsCheck(ogs_rib_policy_apply(&pt, &rp, int32_t(A), 1, W, dMeta, dMask,
-                                D.applied.as<uint8_t>(), D.counter.as<uint8_t>(), nullptr),
+  ogsCheck(ogs_rib_policy_apply(&pt, &D.rp, int32_t(A), 1, W, dMeta, dMask,
+                                D.applied.as<uint8_t>(), D.counter.as<uint8_t>(), stream),
            "ogs_rib_policy_apply");
+}
+
+void downloadPolicy(const PolicyDevice& D, size_t P, std::vector<uint8_t>& applied,
+                    std::vector<uint8_t>& counter) {
   applied.assign(P, 0xFF);
   counter.assign(P, 0xFF);
   if (P) {
@@ -298,6 +323,7 @@ bool wideDistancesNeeded(const FlatTopology& f) {
 }
 
 void PrefixHostTable::build(const PrefixState& ps) {
+  ++generation;
   prefixes.clear();
   advEntry.clear();
   advKey.clear();
@@ -526,7 +552,8 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(
   if (policy && P) {
     if (wide) throw std::domain_error("RibPolicy on the GPU path needs 32-bit distances");
     runPolicyOnDevice(*policy, I.table, pt, {{&f, s}}, me, W, I.meta.as<uint32_t>(),
-                      I.mask.as<uint32_t>(), I.policy, applied, counter);
+                      I.mask.as<uint32_t>(), I.policy, nullptr);
+    downloadPolicy(I.policy, P, applied, counter);
   }
 
   auto widen = [&](const DeviceBuffer& b, size_t n, std::vector<uint64_t>& v) {
@@ -752,13 +779,16 @@ DecisionRouteDb SpfSolver::materializeMultiArea(const std::string& me,
   return rdb;
 }
 
-std::optional<DecisionRouteDb> SpfSolver::buildRouteDbMultiArea(
-    const std::string& me, const AreaLinkStates& als, const PrefixState& ps) {
+// Kernels of a multi-area build on `stream`: SPF of the source in every
+// area holding it (one launch), the multi-area RouteDb, the RibPolicy.
+// Fills R's shape fields (row, W, Sn, P); results stay on the device.
+void SpfSolver::enqueueMultiArea(const std::string& me, const AreaLinkStates& als,
+                                 const PrefixState& ps, void* stream,
+                                 MultiAreaResult& R) {
   if (als.size() > 32) throw std::domain_error("buildRouteDb: more than 32 areas");
   prepareMultiArea(als, ps);
   Impl::MultiArea& M = impl_->ma;
   const uint32_t A = uint32_t(als.size());
-  MultiAreaResult R;
 
   // ---- SPF of the source in every area holding it (one launch) -----------
   std::vector<ogs_unit> su;
@@ -777,9 +807,9 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDbMultiArea(
   R.P = M.maxPrefixes;
   const size_t Sn = R.Sn, P = R.P, P1 = std::max<size_t>(P, 1);
   const uint32_t S = M.nameId.at(me);
-  M.units.upload(su.data(), su.size());
-  M.spfRow.upload(R.row.data(), R.row.size());
-  M.srcName.upload(&S, 1);
+  M.units.upload(su.data(), su.size(), stream);
+  M.spfRow.upload(R.row.data(), R.row.size(), stream);
+  M.srcName.upload(&S, 1, stream);
   M.dist.resize(su.size() * Sn * 4);
   M.nh.resize(su.size() * W * Sn * 4);
   M.meta.resize(P1 * 4);
@@ -804,7 +834,7 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDbMultiArea(
   spf.dist = M.dist.get();
   spf.nh = M.nh.as<uint32_t>();
   ogsCheck(ogs_spf_routes(&g, nullptr, M.units.as<ogs_unit>(), int32_t(su.size()),
-                          flags, W, &spf, nullptr),
+                          flags, W, &spf, stream),
            "ogs_spf_routes");
   for (const auto& [area, ls] : als) {
     if (ls.flat().id.count(me)) ls.noteSpfRuns(1);
@@ -830,7 +860,7 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDbMultiArea(
     out.sel = M.sel.as<uint32_t>();
     ogsCheck(ogs_routes_multiarea(&g, &pt, &at, M.srcName.as<uint32_t>(), 1,
                                   M.spfRow.as<uint32_t>(), M.dist.as<uint32_t>(),
-                                  M.nh.as<uint32_t>(), flags, W, &out, nullptr),
+                                  M.nh.as<uint32_t>(), flags, W, &out, stream),
              "ogs_routes_multiarea");
     if (ribPolicy_ && ribPolicy_->isActive()) {
       std::vector<std::pair<const FlatTopology*, uint32_t>> src;
@@ -839,11 +869,36 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDbMultiArea(
         src.emplace_back(M.flats[a], it == M.flats[a]->id.end() ? OGS_NODE_NONE : it->second);
       }
       runPolicyOnDevice(*ribPolicy_, M.table, pt, src, me, W, M.meta.as<uint32_t>(),
-                        M.mask.as<uint32_t>(), impl_->policy, R.applied, R.counter);
+                        M.mask.as<uint32_t>(), impl_->policy, stream);
     }
   }
-  R.dist32.resize(su.size() * Sn);
-  R.nh.resize(su.size() * W * Sn);
+}
+
+bool SpfSolver::enqueueRouteDb(const std::string& me, const AreaLinkStates& als,
+                               const PrefixState& ps, void* stream) {
+  bool found = false;
+  for (const auto& [_, ls] : als) found |= ls.hasNode(me);
+  if (!found) return false;
+  MultiAreaResult R;
+  enqueueMultiArea(me, als, ps, stream, R);
+  return true;
+}
+
+std::optional<DecisionRouteDb> SpfSolver::buildRouteDbMultiArea(
+    const std::string& me, const AreaLinkStates& als, const PrefixState& ps) {
+  MultiAreaResult R;
+  enqueueMultiArea(me, als, ps, nullptr, R);
+  Impl::MultiArea& M = impl_->ma;
+  const uint32_t A = uint32_t(als.size());
+  const int W = R.W;
+  const size_t Sn = R.Sn, P = R.P;
+  const size_t nSpf = size_t(std::count_if(R.row.begin(), R.row.end(),
+                                           [](uint32_t r) { return r != OGS_NODE_NONE; }));
+  if (P && ribPolicy_ && ribPolicy_->isActive()) {
+    downloadPolicy(impl_->policy, P, R.applied, R.counter);
+  }
+  R.dist32.resize(nSpf * Sn);
+  R.nh.resize(nSpf * W * Sn);
   R.meta.resize(P);
   R.metric.resize(P);
   R.mask.resize(P * A * W);
@@ -895,6 +950,8 @@ std::optional<RibUnicastEntry> SpfSolver::createRouteForPrefixOrGetStaticRoute(
 RibPolicy::RibPolicy(const std::vector<RibPolicyStatementSpec>& statements,
                      int64_t ttlSecs)
     : ttlSecs_(ttlSecs) {  // RibPolicy.cpp:20-50, 167-182
+  static std::atomic<uint64_t> nextUid{1};
+  uid_ = nextUid++;
   if (statements.empty()) {
     throw std::invalid_argument("Missing policy.statements attribute");
   }

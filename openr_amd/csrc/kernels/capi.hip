@@ -36,6 +36,11 @@ hipError_t launch_ksp(const ogs_graph& g, const ogs_path_unit* units,
                       int nUnits, const uint32_t* masks, uint32_t maskWords,
                       uint32_t flags, const ogs_path_out& out,
                       hipStream_t stream, int* unsupported);
+hipError_t launch_ksp2(const ogs_graph& g, const ogs_unit* sources,
+                       int nSources, const ogs_path_unit* units, int nUnits,
+                       uint32_t flags, const ogs_path_out& o1,
+                       const ogs_path_out& o2, hipStream_t stream,
+                       int* unsupported);
 }
 
 namespace {
@@ -234,6 +239,36 @@ int ogs_ksp_paths(const ogs_graph* graph, const ogs_path_unit* units,
     return fail(OGS_E_UNSUPPORTED, "topology too large for the LDS KSP path");
   }
   return e == hipSuccess ? OGS_OK : hipFail(e, "ksp launch");
+}
+
+int ogs_ksp2_paths(const ogs_graph* graph, const ogs_unit* sources,
+                   int32_t n_sources, const ogs_path_unit* units,
+                   int32_t n_units, uint32_t flags, ogs_path_out* k1,
+                   ogs_path_out* k2, void* stream) {
+  if (!graph || !k1 || !k2) return fail(OGS_E_INVALID, "graph/outputs are NULL");
+  if (n_units < 0 || n_sources < 0) return fail(OGS_E_INVALID, "negative count");
+  if (n_units == 0) return OGS_OK;
+  if (n_sources == 0 || !sources || !units || !graph->node_base ||
+      !graph->row_ptr || !graph->edges) {
+    return fail(OGS_E_INVALID, "graph/source/unit arrays are NULL");
+  }
+  for (const ogs_path_out* o : {k1, k2}) {
+    if (!o->path_count || !o->path_len || !o->path_edges) {
+      return fail(OGS_E_INVALID, "path output arrays are NULL");
+    }
+  }
+  if (graph->max_nodes <= 0 ||
+      uint32_t(graph->max_nodes) > OGS_MAX_NODES_PER_TOPO) {
+    return fail(OGS_E_UNSUPPORTED, "max_nodes outside (0, 2^21]");
+  }
+  int unsupported = 0;
+  hipError_t e = ogs::launch_ksp2(*graph, sources, n_sources, units, n_units,
+                                  flags, *k1, *k2,
+                                  static_cast<hipStream_t>(stream), &unsupported);
+  if (unsupported) {
+    return fail(OGS_E_UNSUPPORTED, "topology too large for the LDS KSP path");
+  }
+  return e == hipSuccess ? OGS_OK : hipFail(e, "ksp2 launch");
 }
 
 int ogs_spf_routes_variants(const ogs_graph* graph,

@@ -40,12 +40,99 @@ __device__ bool key_less(D da, uint32_t ua, uint32_t sa, D db, uint32_t ub,
   return sa < sb;
 }
 
+// Every edge-disjoint path of one getKthPaths(src, dest, k) call (lane 0):
+// traceOnePath repeated with one visited-link set until it fails. Writes the
+// paths of output row `row`; also sets each emitted path's links in
+// `pathMask` (the next k's linksToIgnore) when non-NULL. Returns the
+// path_count word (bit 31 = output capacity exceeded).
+template <typename D, bool MASKED>
+__device__ uint32_t trace_paths(const UnitCsr& csr, const D* dist, uint32_t s,
+                                uint32_t t, uint32_t* visited, Frame* stack,
+                                const uint32_t* ignore, const ogs_path_out& out,
+                                size_t row, uint32_t* pathMask) {
+  constexpr D kInf = DistInf<D>::value;
+  uint32_t* pathLen = out.path_len + row * out.max_paths;
+  uint32_t* pathEdges = out.path_edges + row * out.max_edges;
+  uint32_t nPaths = 0, nEdges = 0, status = 0;
+  const bool reachable = (s != t) && dist[t] != kInf;
+  while (reachable) {
+    // one traceOnePath(src, dest) call
+    int sp = 0;
+    // a frame without a resume key yet carries lastSlot's top bit
+    stack[0] = Frame{t, 0xFFFFFFFFu, 0u, 0x80000000u, 0ull};
+    bool found = false;
+    while (sp >= 0) {
+      Frame& f = stack[sp];
+      const uint32_t v = f.node;
+      const D dv = dist[v];
+      // next unvisited pathLink of v after the resume key
+      D bd = kInf;
+      uint32_t bu = 0xFFFFFFFFu, bs = 0xFFFFFFFFu, be = 0xFFFFFFFFu;
+      const bool fresh = (f.lastSlot & 0x80000000u) != 0;
+      const D ld = static_cast<D>(f.lastD);
+      for (uint32_t e = csr.rowp[v]; e < csr.rowp[v + 1]; ++e) {
+        const uint64_t ed = csr.edg[e];
+        const uint32_t lo = static_cast<uint32_t>(ed);
+        if (lo & OGS_EDGE_DOWN) continue;
+        const uint32_t u = edge_dst(lo);
+        if ((lo & OGS_EDGE_DST_OVERLOADED) && u != s) continue;
+        if constexpr (MASKED) {
+          const uint32_t l = link_id(csr, e, lo);
+          if ((ignore[l >> 5] >> (l & 31u)) & 1u) continue;
+        }
+        const D du = dist[u];
+        if (du == kInf || du + static_cast<D>(ed >> 32) != dv) continue;
+        const uint32_t slot = edge_rslot(lo);
+        if (!fresh && !key_less<D>(ld, f.lastU, f.lastSlot, du, u, slot)) continue;
+        if (key_less<D>(du, u, slot, bd, bu, bs)) {
+          bd = du;
+          bu = u;
+          bs = slot;
+          be = e;
+        }
+      }
+      if (be == 0xFFFFFFFFu) {  // exhausted: this recursion level fails
+        --sp;
+        continue;
+      }
+      f.lastD = static_cast<uint64_t>(bd);
+      f.lastU = bu;
+      f.lastSlot = bs;
+      const uint32_t l = link_id(csr, be, static_cast<uint32_t>(csr.edg[be]));
+      if ((visited[l >> 5] >> (l & 31u)) & 1u) continue;  // already used
+      visited[l >> 5] |= 1u << (l & 31u);
+      f.edge = be;
+      if (bu == s) {
+        found = true;
+        break;
+      }
+      ++sp;
+      stack[sp] = Frame{bu, 0xFFFFFFFFu, 0u, 0x80000000u, 0ull};
+    }
+    if (!found) break;
+    // path src -> dest = chosen edges from the top frame down to frame 0
+    if (nPaths >= out.max_paths || nEdges + uint32_t(sp + 1) > out.max_edges) {
+      status = 1;  // output capacity exceeded
+      break;
+    }
+    for (int i = sp; i >= 0; --i) {
+      const uint32_t e = stack[i].edge;
+      pathEdges[nEdges++] = e - csr.eBase;
+      if (pathMask) {
+        const uint32_t l = link_id(csr, e, static_cast<uint32_t>(csr.edg[e]));
+        pathMask[l >> 5] |= 1u << (l & 31u);
+      }
+    }
+    pathLen[nPaths++] = uint32_t(sp + 1);
+  }
+  return nPaths | (status << 31);
+}
+
 template <typename D, int UT, bool STAGE, bool MASKED>
 __global__ __launch_bounds__(kBlock) void ksp_kernel(
     ogs_graph g, const ogs_path_unit* __restrict__ units, int nUnits,
     const uint32_t* __restrict__ masks, uint32_t maskWords,
     ogs_path_out out, uint32_t ldsPerUnit) {
-  constexpr D kInf = DistInf<D>::value;
   constexpr int kUnitsPerBlock = kBlock / UT;
   const int uib = threadIdx.x / UT;
   const int lane = threadIdx.x % UT;
@@ -86,75 +173,8 @@ __global__ __launch_bounds__(kBlock) void ksp_kernel(
                                         ignore);
 
   if (lane != 0) return;
-  // ---- greedy trace (lane 0) ----------------------------------------------
-  uint32_t* pathLen = out.path_len + size_t(uidx) * out.max_paths;
-  uint32_t* pathEdges = out.path_edges + size_t(uidx) * out.max_edges;
-  uint32_t nPaths = 0, nEdges = 0, status = 0;
-  const bool reachable = (s != t) && dist[t] != kInf;
-  while (reachable) {
-    // one traceOnePath(src, dest) call
-    int sp = 0;
-    // a frame without a resume key yet carries lastSlot's top bit
-    stack[0] = Frame{t, 0xFFFFFFFFu, 0u, 0x80000000u, 0ull};
-    bool found = false;
-    while (sp >= 0) {
-      Frame& f = stack[sp];
-      const uint32_t v = f.node;
-      const D dv = dist[v];
-      // next unvisited pathLink of v after the resume key
-      D bd = kInf;
-      uint32_t bu = 0xFFFFFFFFu, bs = 0xFFFFFFFFu, be = 0xFFFFFFFFu;
-      const bool fresh = (f.lastSlot & 0x80000000u) != 0;
-      const D ld = static_cast<D>(f.lastD);
-      for (uint32_t e = csr.rowp[v]; e < csr.rowp[v + 1]; ++e) {
-        const uint64_t ed = csr.edg[e];
-        const uint32_t lo = static_cast<uint32_t>(ed);
-        if (lo & OGS_EDGE_DOWN) continue;
-        const uint32_t u = edge_dst(lo);
-        if ((lo & OGS_EDGE_DST_OVERLOADED) && u != s) continue;
-        const uint32_t l = link_id(csr, e, lo);
-        if constexpr (MASKED) {
-          if ((ignore[l >> 5] >> (l & 31u)) & 1u) continue;
-        }
-        const D du = dist[u];
-        if (du == kInf || du + static_cast<D>(ed >> 32) != dv) continue;
-        const uint32_t slot = edge_rslot(lo);
-        if (!fresh && !key_less<D>(ld, f.lastU, f.lastSlot, du, u, slot)) continue;
-        if (key_less<D>(du, u, slot, bd, bu, bs)) {
-          bd = du;
-          bu = u;
-          bs = slot;
-          be = e;
-        }
-      }
-      if (be == 0xFFFFFFFFu) {  // exhausted: this recursion level fails
-        --sp;
-        continue;
-      }
-      f.lastD = static_cast<uint64_t>(bd);
-      f.lastU = bu;
-      f.lastSlot = bs;
-      const uint32_t l = link_id(csr, be, static_cast<uint32_t>(csr.edg[be]));
-      if ((visited[l >> 5] >> (l & 31u)) & 1u) continue;  // already used
-      visited[l >> 5] |= 1u << (l & 31u);
-      f.edge = be;
-      if (bu == s) {
-        found = true;
-        break;
-      }
-      ++sp;
-      stack[sp] = Frame{bu, 0xFFFFFFFFu, 0u, 0x80000000u, 0ull};
-    }
-    if (!found) break;
-    // path src -> dest = chosen edges from the top frame down to frame 0
-    if (nPaths >= out.max_paths || nEdges + uint32_t(sp + 1) > out.max_edges) {
-      status = 1;  // output capacity exceeded
-      break;
-    }
-    for (int i = sp; i >= 0; --i) pathEdges[nEdges++] = stack[i].edge - csr.eBase;
-    pathLen[nPaths++] = uint32_t(sp + 1);
-  }
-  out.path_count[uidx] = nPaths | (status << 31);
+  out.path_count[uidx] = trace_paths<D, MASKED>(
+      csr, dist, s, t, visited, stack, ignore, out, uidx, nullptr);
 }
 
 template <typename D, int UT, bool STAGE, bool MASKED>
@@ -222,6 +242,233 @@ hipError_t launch_ksp(const ogs_graph& g, const ogs_path_unit* units,
                                               out, stream, unsupported)
               : ksp_dispatch<uint32_t, false>(g, units, nUnits, nullptr, 0, out,
                                               stream, unsupported);
+}
+
+// ---- KSP2 batch: getKthPaths(src, d, 1) and (src, d, 2) for many d -------
+// Launch 1 (ksp_base_kernel): one unmasked SPF per distinct (topology,
+// source) -- the reference's memoised getSpfResult(src) -- into HBM.
+// Launch 2 (ksp2_kernel): per unit, the source's distances are copied into
+// LDS, lane 0 traces the k = 1 paths and marks their links in an LDS mask,
+// the unit reruns SPF with those links ignored (runSpf(src, true,
+// linksToIgnore), LinkState.cpp:691-693) and lane 0 traces the k = 2 paths.
+
+// Per-unit LDS carve-up of both launches: dist, visited + mask link bitsets,
+// trace stack, optionally the staged CSR.
+template <typename D>
+struct KspLds {
+  D* dist;
+  uint32_t* visited;
+  uint32_t* mask;
+  Frame* stack;
+  UnitCsr csr;
+  uint32_t N, linkWords;
+};
+
+template <typename D>
+__host__ __device__ inline uint64_t ksp2_lds_bytes(uint64_t N, uint64_t E,
+                                                   bool stage) {
+  const uint64_t core = align16(N * sizeof(D)) + 2 * align16((E + 31) / 32 * 4) +
+      align16(N * sizeof(Frame));
+  return stage ? core + align16((N + 1) * 4) + align16(E * 8) : core;
+}
+
+template <typename D, bool STAGE, int UT>
+__device__ KspLds<D> ksp_lds(char* base, const ogs_graph& g, uint32_t topo,
+                             int lane) {
+  const uint32_t nb = g.node_base[topo];
+  const uint32_t N = g.node_base[topo + 1] - nb;
+  const uint32_t* __restrict__ gRow = g.row_ptr + nb;
+  const uint32_t e0 = gRow[0];
+  const uint32_t E = gRow[N] - e0;
+  KspLds<D> l;
+  l.N = N;
+  l.linkWords = (E + 31) / 32;
+  l.dist = reinterpret_cast<D*>(base);
+  uint32_t off = align16(uint64_t(N) * sizeof(D));
+  l.visited = reinterpret_cast<uint32_t*>(base + off);
+  off += align16(uint64_t(l.linkWords) * 4);
+  l.mask = reinterpret_cast<uint32_t*>(base + off);
+  off += align16(uint64_t(l.linkWords) * 4);
+  l.stack = reinterpret_cast<Frame*>(base + off);
+  off += align16(uint64_t(N) * sizeof(Frame));
+  if constexpr (STAGE) {
+    uint32_t* lrow = reinterpret_cast<uint32_t*>(base + off);
+    off += align16(uint64_t(N + 1) * 4);
+    uint64_t* ledg = reinterpret_cast<uint64_t*>(base + off);
+    for (uint32_t i = lane; i <= N; i += UT) lrow[i] = gRow[i] - e0;
+    for (uint32_t i = lane; i < E; i += UT) ledg[i] = g.edges[e0 + i];
+    l.csr = UnitCsr{lrow, ledg, 0u};
+  } else {
+    l.csr = UnitCsr{gRow, g.edges, e0};
+  }
+  for (uint32_t i = lane; i < l.linkWords; i += UT) {
+    l.visited[i] = 0u;
+    l.mask[i] = 0u;
+  }
+  return l;
+}
+
+// Lane 0's value to every lane of the unit.
+template <int UT>
+__device__ __forceinline__ uint32_t unit_bcast(uint32_t x) {
+  if constexpr (UT == 64) {
+    return __shfl(x, 0, 64);
+  } else {
+    __shared__ uint32_t b;
+    __syncthreads();
+    if (threadIdx.x == 0) b = x;
+    __syncthreads();
+    return b;
+  }
+}
+
+template <typename D, int UT, bool STAGE>
+__global__ __launch_bounds__(kBlock) void ksp_base_kernel(
+    ogs_graph g, const ogs_unit* __restrict__ sources, int nSources,
+    D* __restrict__ srcDist, uint32_t ldsPerUnit) {
+  constexpr int kUnitsPerBlock = kBlock / UT;
+  const int uib = threadIdx.x / UT;
+  const int lane = threadIdx.x % UT;
+  const int sidx = blockIdx.x * kUnitsPerBlock + uib;
+  if (sidx >= nSources) return;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const ogs_unit src = sources[sidx];
+  auto l = ksp_lds<D, STAGE, UT>(smem + uib * ldsPerUnit, g, src.topo, lane);
+  spf_fixpoint<D, 1, UT, false, false>(l.N, src.src, lane, l.csr, false, l.dist,
+                                       nullptr, nullptr);
+  D* row = srcDist + size_t(sidx) * uint32_t(g.max_nodes);
+  for (uint32_t v = lane; v < l.N; v += UT) row[v] = l.dist[v];
+}
+
+template <typename D, int UT, bool STAGE>
+__global__ __launch_bounds__(kBlock) void ksp2_kernel(
+    ogs_graph g, const ogs_unit* __restrict__ sources, int nSources,
+    const D* __restrict__ srcDist, const ogs_path_unit* __restrict__ units,
+    int nUnits, ogs_path_out o1, ogs_path_out o2, uint32_t ldsPerUnit) {
+  constexpr int kUnitsPerBlock = kBlock / UT;
+  using Scope = UnitScope<UT>;
+  const int uib = threadIdx.x / UT;
+  const int lane = threadIdx.x % UT;
+  const int uidx = blockIdx.x * kUnitsPerBlock + uib;
+  // whole-block early exit only: the workgroup-scope path has barriers
+  if (blockIdx.x * kUnitsPerBlock >= nUnits) return;
+  const bool live = uidx < nUnits;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  if (!live) return;  // UT == 64 only: a wave of its own, no block barrier
+  const ogs_path_unit unit = units[uidx];
+  const uint32_t slot = unit.reserved;
+  if (slot >= uint32_t(nSources) || sources[slot].topo != unit.topo ||
+      sources[slot].src != unit.src) {
+    if (lane == 0) {  // malformed unit: reported, never traced
+      o1.path_count[uidx] = 0xC0000000u;
+      o2.path_count[uidx] = 0xC0000000u;
+    }
+    return;
+  }
+  auto l = ksp_lds<D, STAGE, UT>(smem + uib * ldsPerUnit, g, unit.topo, lane);
+  const D* row = srcDist + size_t(slot) * uint32_t(g.max_nodes);
+  for (uint32_t v = lane; v < l.N; v += UT) l.dist[v] = row[v];
+  Scope::sync();
+  const uint32_t s = unit.src, t = unit.dest;
+  uint32_t c1 = 0;
+  if (lane == 0) {
+    c1 = trace_paths<D, false>(l.csr, l.dist, s, t, l.visited, l.stack, nullptr,
+                               o1, uidx, l.mask);
+    o1.path_count[uidx] = c1;
+  }
+  c1 = unit_bcast<UT>(c1);
+  // k = 1 found no path (src == dest or unreachable): linksToIgnore is empty,
+  // so k = 2 re-traces the same SPF and finds none either. A k = 1 overflow
+  // leaves the mask incomplete: reported for k = 2 as well.
+  if (c1 == 0u || (c1 >> 31)) {
+    if (lane == 0) o2.path_count[uidx] = c1 & 0x80000000u;
+    return;
+  }
+  for (uint32_t i = lane; i < l.linkWords; i += UT) l.visited[i] = 0u;
+  spf_fixpoint<D, 1, UT, false, true>(l.N, s, lane, l.csr, false, l.dist,
+                                      nullptr, l.mask);
+  if (lane != 0) return;
+  o2.path_count[uidx] = trace_paths<D, true>(l.csr, l.dist, s, t, l.visited,
+                                             l.stack, l.mask, o2, uidx, nullptr);
+}
+
+template <typename D, int UT, bool STAGE>
+hipError_t ksp2_launch(const ogs_graph& g, const ogs_unit* sources,
+                       int nSources, D* srcDist, const ogs_path_unit* units,
+                       int nUnits, const ogs_path_out& o1,
+                       const ogs_path_out& o2, uint32_t lds,
+                       hipStream_t stream) {
+  constexpr int upb = kBlock / UT;
+  const size_t bytes = size_t(lds) * upb;
+  auto kb = ksp_base_kernel<D, UT, STAGE>;
+  auto k2 = ksp2_kernel<D, UT, STAGE>;
+  if (bytes > 64 * 1024) {
+    for (const void* f : {reinterpret_cast<const void*>(kb),
+                          reinterpret_cast<const void*>(k2)}) {
+      hipError_t e = hipFuncSetAttribute(
+          f, hipFuncAttributeMaxDynamicSharedMemorySize, int(bytes));
+      if (e != hipSuccess) return e;
+    }
+  }
+  hipLaunchKernelGGL(kb, dim3((nSources + upb - 1) / upb), dim3(kBlock), bytes,
+                     stream, g, sources, nSources, srcDist, lds);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k2, dim3((nUnits + upb - 1) / upb), dim3(kBlock), bytes,
+                     stream, g, sources, nSources,
+                     static_cast<const D*>(srcDist), units, nUnits, o1, o2, lds);
+  return hipGetLastError();
+}
+
+hipError_t workspace(size_t bytes, hipStream_t stream, void** out);
+
+template <typename D>
+hipError_t ksp2_dispatch(const ogs_graph& g, const ogs_unit* sources,
+                         int nSources, const ogs_path_unit* units, int nUnits,
+                         const ogs_path_out& o1, const ogs_path_out& o2,
+                         hipStream_t stream, int* unsupported) {
+  const uint64_t N = g.max_nodes, E = g.max_edges;
+  const uint64_t core = ksp2_lds_bytes<D>(N, E, false);
+  const uint64_t staged = ksp2_lds_bytes<D>(N, E, true);
+  constexpr uint64_t kBudget = 160 * 1024;
+  void* ws = nullptr;
+  auto dist = [&](hipError_t* e) {
+    *e = workspace(size_t(nSources) * size_t(N) * sizeof(D), stream, &ws);
+    return static_cast<D*>(ws);
+  };
+  hipError_t e = hipSuccess;
+  if (N <= 256 && staged * 4 <= kBudget / 2) {
+    D* d = dist(&e);
+    if (e != hipSuccess) return e;
+    return ksp2_launch<D, 64, true>(g, sources, nSources, d, units, nUnits, o1,
+                                    o2, uint32_t(staged), stream);
+  }
+  if (staged <= kBudget / 2) {
+    D* d = dist(&e);
+    if (e != hipSuccess) return e;
+    return ksp2_launch<D, kBlock, true>(g, sources, nSources, d, units, nUnits,
+                                        o1, o2, uint32_t(staged), stream);
+  }
+  if (core <= kBudget) {
+    D* d = dist(&e);
+    if (e != hipSuccess) return e;
+    return ksp2_launch<D, kBlock, false>(g, sources, nSources, d, units, nUnits,
+                                         o1, o2, uint32_t(core), stream);
+  }
+  *unsupported = 1;
+  return hipSuccess;
+}
+
+hipError_t launch_ksp2(const ogs_graph& g, const ogs_unit* sources,
+                       int nSources, const ogs_path_unit* units, int nUnits,
+                       uint32_t flags, const ogs_path_out& o1,
+                       const ogs_path_out& o2, hipStream_t stream,
+                       int* unsupported) {
+  return (flags & OGS_F_WIDE_METRIC)
+      ? ksp2_dispatch<uint64_t>(g, sources, nSources, units, nUnits, o1, o2,
+                                stream, unsupported)
+      : ksp2_dispatch<uint32_t>(g, sources, nSources, units, nUnits, o1, o2,
+                                stream, unsupported);
 }
 
 }  // namespace ogs

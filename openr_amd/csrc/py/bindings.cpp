@@ -280,6 +280,51 @@ void loadLsdb(const topogen::Lsdb& g, LinkState& ls, PrefixState& ps) {
   }
 }
 
+// The multi-area domain of MultiAreaOpts (config C5 defaults) + overloads
+// and prefix mix per area, loaded into one LinkState per area.
+void loadMultiArea(const py::dict& d, AreaLinkStates& als, PrefixState& ps) {
+  topogen::MultiAreaOpts o;
+  o.areas = get<int>(d, "areas", 8);
+  o.nodesPerArea = get<int>(d, "nodesPerArea", 1250);
+  o.abrs = get<int>(d, "abrs", 64);
+  o.k = get<int>(d, "k", 3);
+  o.seed = get<uint64_t>(d, "seed", 0xC5A0);
+  o.prefixesPerNode = get<int>(d, "prefixesPerNode", 10);
+  o.anycastPermille = get<int>(d, "anycastPermille", 50);
+  auto lsdbs = topogen::multiArea(o);
+  for (size_t a = 0; a < lsdbs.size(); ++a) {
+    topogen::applyOverloads(lsdbs[a], get<int>(d, "adjOverloadPermille", 0),
+                            get<int>(d, "nodeOverloadPermille", 0),
+                            get<uint64_t>(d, "overloadSeed", 0x0F) + a);
+    topogen::PrefixMix m;
+    m.v4Permille = get<int>(d, "v4Permille", 0);
+    m.minNhPermille = get<int>(d, "minNhPermille", 0);
+    m.drainPermille = get<int>(d, "drainPermille", 0);
+    m.tagPermille = get<int>(d, "tagPermille", 0);
+    m.seed = get<uint64_t>(d, "mixSeed", 0x3F) + a;
+    topogen::applyPrefixMix(lsdbs[a], m);
+    auto& ls = als.emplace(lsdbs[a].area, LinkState(lsdbs[a].area, "test_node"))
+                   .first->second;
+    loadLsdb(lsdbs[a], ls, ps);
+  }
+}
+
+// Directed text of a link (KSP parity): n1/if1-n2/if2 in key order.
+std::string linkText(const Link& l) {
+  const auto& k = l.key();
+  return k.first.first + "/" + k.first.second + "-" + k.second.first + "/" +
+      k.second.second;
+}
+
+std::string pathsText(const std::vector<LinkState::Path>& paths) {
+  std::string out;
+  for (size_t i = 0; i < paths.size(); ++i) {
+    if (i) out += " |";
+    for (const auto& l : paths[i]) out += " " + linkText(*l);
+  }
+  return out;
+}
+
 topogen::GridOpts gridOpts(const py::dict& d) {
   topogen::GridOpts o;
   o.n = get<int>(d, "n", 10);
@@ -783,6 +828,178 @@ std::vector<RibPolicyStatementSpec> parseStatements(py::list stmts) {
   return v;
 }
 
+// ------------------------------------------------------------ C5Runner ---
+// Config C5: one multi-area domain, source `source`; a job
+// = the source's multi-area RouteDb with the UCMP RibPolicy
+// (SpfSolver::enqueueRouteDb, results left on the device) + getKthPaths(src,
+// d, 1) and (src, d, 2) for every other node d of every area holding the
+// source (one Ksp2Batch per area). Rank r of `world` keeps block r of the
+// prefix table and of the destinations: routes and KSP2 units are
+// independent, so there is no exchange.
+class C5Runner {
+ public:
+  void setup(const py::dict& opts, const std::string& source, py::list policy,
+             bool brs, int rank, int world) {
+    loadMultiArea(opts, als_, ps_);
+    if (world > 1) {
+      const size_t P = ps_.prefixes().size();
+      const size_t lo = P * rank / world, hi = P * (rank + 1) / world;
+      PrefixState sub;
+      size_t i = 0;
+      for (const auto& [pfx, entries] : ps_.prefixes()) {
+        if (i >= lo && i < hi) {
+          for (const auto& [na, e] : entries) sub.updatePrefix(na.first, na.second, *e);
+        }
+        ++i;
+      }
+      ps_ = std::move(sub);
+    }
+    source_ = source;
+    solver_ = std::make_unique<SpfSolver>(source, true, false, brs);
+    if (!policy.empty()) {
+      pol_.emplace(parseStatements(policy), 3600);
+      solver_->setRibPolicy(&*pol_);
+    }
+    std::vector<std::pair<std::string, std::string>> all;  // (area, dest)
+    for (const auto& [area, ls] : als_) {
+      if (!ls.hasNode(source)) continue;
+      for (const auto& n : ls.flat().names) {
+        if (n != source) all.emplace_back(area, n);
+      }
+    }
+    totalDests_ = all.size();
+    const size_t lo = all.size() * rank / world, hi = all.size() * (rank + 1) / world;
+    for (const auto& [area, ls] : als_) {
+      std::vector<std::string> dests;
+      for (size_t i = lo; i < hi; ++i) {
+        if (all[i].first == area) dests.push_back(all[i].second);
+      }
+      if (dests.empty()) continue;
+      areas_.push_back(area);
+      batches_.push_back(std::make_unique<Ksp2Batch>(ls, source, dests));
+    }
+  }
+
+  void setPolicy(py::list policy) {
+    solver_->setRibPolicy(nullptr);
+    pol_.reset();
+    if (!policy.empty()) {
+      pol_.emplace(parseStatements(policy), 3600);
+      solver_->setRibPolicy(&*pol_);
+    }
+  }
+  // the source's neighbours over all areas (UCMP neighbor_to_weight keys)
+  std::vector<std::string> sourceNeighbors() const {
+    std::set<std::string> out;
+    for (const auto& [area, ls] : als_) {
+      if (!ls.hasNode(source_)) continue;
+      for (const auto& l : ls.linksFromNode(source_)) {
+        out.insert(l->getOtherNodeName(source_));
+      }
+    }
+    return {out.begin(), out.end()};
+  }
+  std::vector<std::string> areaNames() const {
+    std::vector<std::string> out;
+    for (const auto& [area, _] : als_) out.push_back(area);
+    return out;
+  }
+
+  void launchRoutes(uintptr_t stream) {
+    solver_->enqueueRouteDb(source_, als_, ps_, reinterpret_cast<void*>(stream));
+  }
+  void launchKsp(uintptr_t stream) {
+    for (const auto& b : batches_) b->launch(reinterpret_cast<void*>(stream));
+  }
+  void fetch() {
+    for (const auto& b : batches_) b->fetch();
+  }
+  py::bytes routes() {
+    auto db = solver_->buildRouteDb(source_, als_, ps_);
+    return py::bytes(db ? canonical(*db) : std::string("NONE"));
+  }
+  // "area dest k:" + the paths, one line per (destination, k), batch order
+  std::vector<std::string> kspText() const {
+    std::vector<std::string> out;
+    for (size_t b = 0; b < batches_.size(); ++b) {
+      for (size_t i = 0; i < batches_[b]->size(); ++i) {
+        for (int k = 1; k <= 2; ++k) {
+          out.push_back(areas_[b] + " " + batches_[b]->dests()[i] + " " +
+                        std::to_string(k) + ":" + pathsText(batches_[b]->paths(i, k)));
+        }
+      }
+    }
+    return out;
+  }
+  std::vector<std::pair<std::string, std::string>> kspDests() const {
+    std::vector<std::pair<std::string, std::string>> out;
+    for (size_t b = 0; b < batches_.size(); ++b) {
+      for (const auto& d : batches_[b]->dests()) out.emplace_back(areas_[b], d);
+    }
+    return out;
+  }
+  // FNV-1a over every unit's k = 1 and k = 2 paths (edge ids)
+  uint64_t digest() const {
+    uint64_t h = 1469598103934665603ull;
+    auto mix = [&](uint64_t x) { h = (h ^ x) * 1099511628211ull; };
+    for (const auto& b : batches_) {
+      for (size_t i = 0; i < b->size(); ++i) {
+        for (int k = 1; k <= 2; ++k) {
+          const auto paths = b->edgePaths(i, k);
+          mix(paths.size());
+          for (const auto& p : paths) {
+            for (uint32_t e : p) mix(e);
+            mix(~0ull);
+          }
+        }
+      }
+    }
+    return h;
+  }
+  py::dict shape() const {
+    py::dict d;
+    size_t nodes = 0, edges = 0, srcNodes = 0, srcEdges = 0, units = 0, adv = 0;
+    for (const auto& [area, ls] : als_) {
+      const FlatTopology& f = ls.flat();
+      nodes += f.names.size();
+      edges += f.edges.size();
+      if (ls.hasNode(source_)) {
+        srcNodes += f.names.size();
+        srcEdges += f.edges.size();
+      }
+    }
+    for (const auto& b : batches_) units += b->numUnits();
+    for (const auto& [p, e] : ps_.prefixes()) adv += e.size();
+    uint64_t pe1 = 0, pe2 = 0;
+    for (const auto& b : batches_) {
+      pe1 += b->totalPathEdges(1);
+      pe2 += b->totalPathEdges(2);
+    }
+    d["areas"] = als_.size();
+    d["nodes"] = nodes;
+    d["directed_edges"] = edges;
+    d["source_area_nodes"] = srcNodes;
+    d["source_area_edges"] = srcEdges;
+    d["prefixes"] = ps_.prefixes().size();
+    d["advertisements"] = adv;
+    d["ksp_units"] = units;
+    d["total_dests"] = totalDests_;
+    d["path_edges_k1"] = pe1;
+    d["path_edges_k2"] = pe2;
+    return d;
+  }
+
+ private:
+  AreaLinkStates als_;
+  PrefixState ps_;
+  std::string source_;
+  std::optional<RibPolicy> pol_;
+  std::unique_ptr<SpfSolver> solver_;
+  std::vector<std::string> areas_;
+  std::vector<std::unique_ptr<Ksp2Batch>> batches_;
+  size_t totalDests_{0};
+};
+
 }  // namespace
 
 PYBIND11_MODULE(_decision, m) {
@@ -816,6 +1033,8 @@ PYBIND11_MODULE(_decision, m) {
              return out;
            },
            py::arg("node"), py::arg("useLinkMetric") = true)
+      .def("prefetchKthPaths", &LinkState::prefetchKthPaths, py::arg("src"),
+           py::arg("dests"))
       .def("getKthPaths",
            [](const LinkState& s, const std::string& a, const std::string& b, size_t k) {
              py::list out;
@@ -968,32 +1187,9 @@ PYBIND11_MODULE(_decision, m) {
   m.def("gen_route_dbs_multiarea",
         [](py::dict d, std::vector<std::string> sources, bool enableV4, bool sr,
            bool brs, py::list policy) {
-          topogen::MultiAreaOpts o;
-          o.areas = get<int>(d, "areas", 8);
-          o.nodesPerArea = get<int>(d, "nodesPerArea", 1250);
-          o.abrs = get<int>(d, "abrs", 64);
-          o.k = get<int>(d, "k", 3);
-          o.seed = get<uint64_t>(d, "seed", 0xC5A0);
-          o.prefixesPerNode = get<int>(d, "prefixesPerNode", 10);
-          o.anycastPermille = get<int>(d, "anycastPermille", 50);
-          auto lsdbs = topogen::multiArea(o);
           AreaLinkStates als;
           PrefixState ps;
-          for (size_t a = 0; a < lsdbs.size(); ++a) {
-            topogen::applyOverloads(lsdbs[a], get<int>(d, "adjOverloadPermille", 0),
-                                    get<int>(d, "nodeOverloadPermille", 0),
-                                    get<uint64_t>(d, "overloadSeed", 0x0F) + a);
-            topogen::PrefixMix m;
-            m.v4Permille = get<int>(d, "v4Permille", 0);
-            m.minNhPermille = get<int>(d, "minNhPermille", 0);
-            m.drainPermille = get<int>(d, "drainPermille", 0);
-            m.tagPermille = get<int>(d, "tagPermille", 0);
-            m.seed = get<uint64_t>(d, "mixSeed", 0x3F) + a;
-            topogen::applyPrefixMix(lsdbs[a], m);
-            auto& ls = als.emplace(lsdbs[a].area, LinkState(lsdbs[a].area, "test_node"))
-                           .first->second;
-            loadLsdb(lsdbs[a], ls, ps);
-          }
+          loadMultiArea(d, als, ps);
           SpfSolver solver("test_node", enableV4, sr, brs);
           std::optional<RibPolicy> pol;
           if (!policy.empty()) {
@@ -1054,6 +1250,29 @@ PYBIND11_MODULE(_decision, m) {
       .def("changed", &VariantRunner::changedOf)
       .def("counts", &VariantRunner::countsOf)
       .def("shape", &VariantRunner::shape);
+
+  py::class_<C5Runner>(m, "C5Runner")
+      .def(py::init<>())
+      .def("setup", &C5Runner::setup, py::arg("opts"), py::arg("source"),
+           py::arg("policy") = py::list(), py::arg("brs") = true, py::arg("rank") = 0,
+           py::arg("world") = 1)
+      .def("launch_routes", [](C5Runner& r, uintptr_t stream) {
+             py::gil_scoped_release nogil;
+             r.launchRoutes(stream);
+           }, py::arg("stream") = 0)
+      .def("launch_ksp", [](C5Runner& r, uintptr_t stream) {
+             py::gil_scoped_release nogil;
+             r.launchKsp(stream);
+           }, py::arg("stream") = 0)
+      .def("set_policy", &C5Runner::setPolicy, py::arg("policy"))
+      .def("source_neighbors", &C5Runner::sourceNeighbors)
+      .def("area_names", &C5Runner::areaNames)
+      .def("fetch", &C5Runner::fetch)
+      .def("routes", &C5Runner::routes)
+      .def("ksp_text", &C5Runner::kspText)
+      .def("ksp_dests", &C5Runner::kspDests)
+      .def("digest", &C5Runner::digest)
+      .def("shape", &C5Runner::shape);
 
   py::class_<BatchRunner>(m, "BatchRunner")
       .def(py::init<bool, bool, bool>(), py::arg("enableV4") = true,

@@ -377,6 +377,52 @@ struct Workspace {  // one private replica (LinkState is not thread-safe)
   PrefixState ps;
 };
 
+// The multi-area domain of MultiAreaOpts (config C5 defaults) + overloads
+// and prefix mix per area, loaded into one LinkState per area.
+void loadMultiArea(const py::dict& d, AreaLinkStates& als, PrefixState& ps) {
+  topogen::MultiAreaOpts o;
+  o.areas = get<int>(d, "areas", 8);
+  o.nodesPerArea = get<int>(d, "nodesPerArea", 1250);
+  o.abrs = get<int>(d, "abrs", 64);
+  o.k = get<int>(d, "k", 3);
+  o.seed = get<uint64_t>(d, "seed", 0xC5A0);
+  o.prefixesPerNode = get<int>(d, "prefixesPerNode", 10);
+  o.anycastPermille = get<int>(d, "anycastPermille", 50);
+  auto lsdbs = topogen::multiArea(o);
+  for (size_t a = 0; a < lsdbs.size(); ++a) {
+    topogen::applyOverloads(lsdbs[a], get<int>(d, "adjOverloadPermille", 0),
+                            get<int>(d, "nodeOverloadPermille", 0),
+                            get<uint64_t>(d, "overloadSeed", 0x0F) + a);
+    topogen::PrefixMix m;
+    m.v4Permille = get<int>(d, "v4Permille", 0);
+    m.minNhPermille = get<int>(d, "minNhPermille", 0);
+    m.drainPermille = get<int>(d, "drainPermille", 0);
+    m.tagPermille = get<int>(d, "tagPermille", 0);
+    m.seed = get<uint64_t>(d, "mixSeed", 0x3F) + a;
+    topogen::applyPrefixMix(lsdbs[a], m);
+    auto& ls = als.emplace(lsdbs[a].area, LinkState(lsdbs[a].area, "test_node"))
+                   .first->second;
+    loadLsdb(lsdbs[a], ls, ps);
+  }
+}
+
+// Same text as the product's C5Runner.ksp_text: links as n1/if1-n2/if2 in
+// the link's name order, paths separated by " |".
+std::string linkText(const Link& l) {
+  const auto& o = l.orderedNames();
+  return o.first.first + "/" + o.first.second + "-" + o.second.first + "/" +
+      o.second.second;
+}
+
+std::string pathsText(const std::vector<LinkState::Path>& paths) {
+  std::string out;
+  for (size_t i = 0; i < paths.size(); ++i) {
+    if (i) out += " |";
+    for (const auto& l : paths[i]) out += " " + linkText(*l);
+  }
+  return out;
+}
+
 }  // namespace
 
 namespace {
@@ -586,32 +632,9 @@ PYBIND11_MODULE(_refcpu, m) {
   m.def("gen_route_dbs_multiarea",
         [](py::dict d, std::vector<std::string> sources, bool enableV4, bool sr,
            bool brs, py::list policy) {
-          topogen::MultiAreaOpts o;
-          o.areas = get<int>(d, "areas", 8);
-          o.nodesPerArea = get<int>(d, "nodesPerArea", 1250);
-          o.abrs = get<int>(d, "abrs", 64);
-          o.k = get<int>(d, "k", 3);
-          o.seed = get<uint64_t>(d, "seed", 0xC5A0);
-          o.prefixesPerNode = get<int>(d, "prefixesPerNode", 10);
-          o.anycastPermille = get<int>(d, "anycastPermille", 50);
-          auto lsdbs = topogen::multiArea(o);
           AreaLinkStates als;
           PrefixState ps;
-          for (size_t a = 0; a < lsdbs.size(); ++a) {
-            topogen::applyOverloads(lsdbs[a], get<int>(d, "adjOverloadPermille", 0),
-                                    get<int>(d, "nodeOverloadPermille", 0),
-                                    get<uint64_t>(d, "overloadSeed", 0x0F) + a);
-            topogen::PrefixMix m;
-            m.v4Permille = get<int>(d, "v4Permille", 0);
-            m.minNhPermille = get<int>(d, "minNhPermille", 0);
-            m.drainPermille = get<int>(d, "drainPermille", 0);
-            m.tagPermille = get<int>(d, "tagPermille", 0);
-            m.seed = get<uint64_t>(d, "mixSeed", 0x3F) + a;
-            topogen::applyPrefixMix(lsdbs[a], m);
-            auto& ls = als.emplace(lsdbs[a].area, LinkState(lsdbs[a].area, "test_node"))
-                           .first->second;
-            loadLsdb(lsdbs[a], ls, ps);
-          }
+          loadMultiArea(d, als, ps);
           SpfSolver solver("test_node", enableV4, sr, brs);
           std::vector<py::bytes> out;
           for (const auto& s : sources) {
@@ -626,6 +649,91 @@ PYBIND11_MODULE(_refcpu, m) {
         },
         py::arg("opts"), py::arg("sources"), py::arg("enableV4") = true,
         py::arg("sr") = false, py::arg("brs") = false, py::arg("policy") = py::list());
+
+  // KSP2 over a multi-area domain: for each (area, dest), the lines
+  // "area dest k:<paths>" for k = 1, 2 (LinkState::getKthPaths,
+  // LinkState.cpp:674-703), in the given order.
+  m.def("kth_paths_multiarea",
+        [](py::dict d, const std::string& source,
+           const std::vector<std::pair<std::string, std::string>>& dests) {
+          AreaLinkStates als;
+          PrefixState ps;
+          loadMultiArea(d, als, ps);
+          std::vector<std::string> out;
+          for (const auto& [area, dest] : dests) {
+            const LinkState& ls = als.at(area);
+            for (size_t k = 1; k <= 2; ++k) {
+              out.push_back(area + " " + dest + " " + std::to_string(k) + ":" +
+                            pathsText(ls.getKthPaths(source, dest, k)));
+            }
+          }
+          return out;
+        },
+        py::arg("opts"), py::arg("source"), py::arg("dests"));
+
+  // CPU baseline for config C5. Routes: buildRouteDb(source) + the UCMP
+  // RibPolicy on one thread (one source's build is sequential in the
+  // reference). KSP2: T threads, each with a private replica of the domain
+  // (LinkState is not thread-safe), getKthPaths(source, d, 1) and (.., 2)
+  // for `sample` destinations of the source's areas (strided over the full
+  // destination list, split over the threads). Ingestion is untimed.
+  // Returns (route_secs, ksp_secs, sampled dests, total dests, routes).
+  m.def("cpu_baseline_c5",
+        [](py::dict d, const std::string& source, py::list policy, bool brs,
+           int sample, int threads) {
+          if (threads <= 0) threads = std::max(1u, std::thread::hardware_concurrency());
+          std::vector<std::unique_ptr<Workspace>> reps(threads);
+          for (auto& r : reps) {
+            r = std::make_unique<Workspace>();
+            loadMultiArea(d, r->als, r->ps);
+          }
+          std::vector<std::pair<std::string, std::string>> all;
+          for (const auto& [area, ls] : reps[0]->als) {
+            if (!ls.getAdjacencyDatabases().count(source)) continue;
+            std::set<std::string> names;
+            for (const auto& [n, _] : ls.getAdjacencyDatabases()) names.insert(n);
+            for (const auto& n : names) {
+              if (n != source) all.emplace_back(area, n);
+            }
+          }
+          std::vector<std::pair<std::string, std::string>> pick;
+          const size_t stride = std::max<size_t>(1, all.size() / std::max(1, sample));
+          for (size_t i = 0; i < all.size() && int(pick.size()) < sample; i += stride) {
+            pick.push_back(all[i]);
+          }
+          double routeSecs = 0, kspSecs = 0;
+          size_t routes = 0;
+          {
+            auto specs = parseStatements(policy);
+            py::gil_scoped_release nogil;
+            auto t0 = std::chrono::steady_clock::now();
+            SpfSolver solver("test_node", true, false, brs);
+            auto db = solver.buildRouteDb(source, reps[0]->als, reps[0]->ps);
+            if (db && !specs.empty()) {
+              RibPolicy pol(specs, 3600);
+              pol.applyPolicy(db->unicastRoutes);
+            }
+            routes = db ? db->unicastRoutes.size() : 0;
+            routeSecs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+            auto t1 = std::chrono::steady_clock::now();
+            std::vector<std::thread> pool;
+            for (int th = 0; th < threads; ++th) {
+              pool.emplace_back([&, th] {
+                const Workspace& w = *reps[th];
+                for (size_t i = th; i < pick.size(); i += threads) {
+                  const LinkState& ls = w.als.at(pick[i].first);
+                  ls.getKthPaths(source, pick[i].second, 1);
+                  ls.getKthPaths(source, pick[i].second, 2);
+                }
+              });
+            }
+            for (auto& t : pool) t.join();
+            kspSecs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count();
+          }
+          return py::make_tuple(routeSecs, kspSecs, pick.size(), all.size(), routes);
+        },
+        py::arg("opts"), py::arg("source"), py::arg("policy"), py::arg("brs"),
+        py::arg("sample"), py::arg("threads"));
 
   // Link-failure variants (config C4): the reference's adjacency-DB update
   // with the links removed at both ends, buildRouteDb, and calculateUpdate

@@ -455,3 +455,70 @@ def test_rib_policy_multi_area(product, oracle, brs):
     _cmp(product.gen_route_dbs_multiarea(opts, srcs, True, False, brs, pol),
          oracle.gen_route_dbs_multiarea(opts, srcs, True, False, brs, pol),
          "policy_multiarea")
+
+
+@pytest.mark.parametrize("parallel", [False, True])
+def test_ksp2_batch_prefetch(product, oracle, parallel):
+    """LinkState.prefetchKthPaths (one ogs_ksp2_paths call for every
+    destination: shared source SPF, k = 1 trace, masked rerun, k = 2 trace)
+    fills getKthPaths exactly as the oracle computes it one by one; the
+    source itself and unknown nodes give no paths."""
+    n = 7
+    pls = _grid_ls(product, n, 21, 4, parallel)
+    ols = _grid_ls(oracle, n, 21, 4, parallel)
+    dests = [str(i) for i in range(n * n)] + ["nope"]
+    for s in ("0", "24", "48"):
+        pls.prefetchKthPaths(s, dests)
+        for d in dests:
+            for k in (1, 2):
+                assert _paths(pls, s, d, k) == _paths(ols, s, d, k), (s, d, k)
+
+
+C5_SMALL = dict(areas=3, nodesPerArea=150, abrs=8, prefixesPerNode=3, anycastPermille=80,
+                nodeOverloadPermille=20, adjOverloadPermille=20, v4Permille=50)
+
+
+def _c5_runner(product, rank=0, world=1):
+    from openr_amd.workloads import c5_policy
+    r = product.C5Runner()
+    r.setup(C5_SMALL, "abr-0", [], True, rank, world)
+    pol = c5_policy(r.area_names(), r.source_neighbors())
+    r.set_policy(pol)
+    return r, pol
+
+
+def test_c5_runner_parity(product, oracle):
+    """Config C5 job at reduced size (3 areas x 150 nodes + 8 ABRs, overloads,
+    anycast, v4 mix): the device build (enqueueRouteDb + UCMP policy) then
+    download equals the oracle's buildRouteDb + RibPolicy::applyPolicy, and
+    the batched KSP2 of every destination of the source's areas equals the
+    oracle's getKthPaths(src, d, 1 / 2)."""
+    r, pol = _c5_runner(product)
+    r.launch_routes(0)
+    r.launch_ksp(0)
+    r.fetch()
+    _cmp([r.routes()], oracle.gen_route_dbs_multiarea(C5_SMALL, ["abr-0"], True, False, True,
+                                                       pol), "c5routes")
+    dests = r.ksp_dests()
+    assert len(dests) == r.shape()["total_dests"] > 300
+    got, want = r.ksp_text(), oracle.kth_paths_multiarea(C5_SMALL, "abr-0", dests)
+    assert len(got) == len(want)
+    bad = [(g, w) for g, w in zip(got, want) if g != w]
+    assert not bad, bad[:3]
+    # random metrics: mostly one shortest path each; k = 2 finds the detours
+    assert sum(1 for line in got if " 2: " in line) > len(dests) // 2
+
+
+def test_c5_runner_sharded(product):
+    """Two ranks' blocks (prefix range + destination range) reassemble the
+    single-rank job exactly: no exchange is needed between ranks."""
+    full, _ = _c5_runner(product)
+    full.launch_ksp(0)
+    full.fetch()
+    parts = [_c5_runner(product, rank, 2)[0] for rank in range(2)]
+    for p in parts:
+        p.launch_ksp(0)
+        p.fetch()
+    assert parts[0].ksp_text() + parts[1].ksp_text() == full.ksp_text()
+    routes = [p.routes().decode() for p in parts]
+    assert routes[0] + routes[1] == full.routes().decode()
