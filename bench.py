@@ -337,9 +337,123 @@ def run_c4(args, torch, dist, rank, world, local_rank):
     return line
 
 
+def run_c5(args, torch, dist, rank, world, local_rank):
+    """Config C5: multi-area WAN (8 areas x 1,250 nodes + 64 ABRs, ~100k
+    prefixes, 5 % anycast, best-route selection), source "abr-0". One step =
+    one job: the source's multi-area RouteDb + UCMP RibPolicy (SPF per area,
+    route kernel, policy kernel; results left in HBM) and KSP2 (k = 1 and 2)
+    for every destination of the source's two areas. Strong scaling: rank r
+    owns block r of the prefix table and of the destinations."""
+    import openr_amd
+    import openr_amd.capi as capi
+    from openr_amd.workloads import C5_OPTS, C5_SOURCE, c5_policy
+    openr_amd.require_gpu()
+    lib = capi.load()
+    lib.ogs_set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    steps = args.steps if args.config == "c5" else args.c5_steps
+    warmup = args.warmup if args.config == "c5" else 2
+    r = openr_amd.decision.C5Runner()
+    r.setup(C5_OPTS, C5_SOURCE, [], True, rank, world)
+    # every rank holds the whole topology: the policy is the same everywhere
+    pol = c5_policy(r.area_names(), r.source_neighbors())
+    r.set_policy(pol)
+    stream = torch.cuda.current_stream(dev)
+    sptr = stream.cuda_stream
+
+    def job():
+        r.launch_routes(sptr)
+        r.launch_ksp(sptr)
+
+    for _ in range(warmup):
+        job()
+    torch.cuda.synchronize(dev)
+    # per-part kernel time (events on the launch stream), outside the job clock
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    ev[0].record(stream)
+    r.launch_routes(sptr)
+    ev[1].record(stream)
+    r.launch_ksp(sptr)
+    ev[2].record(stream)
+    torch.cuda.synchronize(dev)
+    route_ms, ksp_ms = ev[0].elapsed_time(ev[1]), ev[1].elapsed_time(ev[2])
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for _ in range(steps):
+        job()
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t0
+    job_ms = e0.elapsed_time(e1) / steps
+    r.fetch()
+    sh = r.shape()
+    U = sh["ksp_units"]
+    digest = r.digest() >> 1
+    total_units, total_prefixes, job_digest, tmax, _ = shard.reduce_stats(
+        dist, torch, dev, U, sh["prefixes"], digest, wall)
+    if rank != 0:
+        return None
+    # KSP2 unit (SURVEY.md §8(d): CSR + E/8 mask + 4N + path output): the
+    # area's CSR staged once (4(N+1) + 8E), the source's distance row (4N),
+    # both path sets (4 B per path edge, 4 B per path, 4 B count each)
+    Na = sh["source_area_nodes"] / 2
+    Ea = sh["source_area_edges"] / 2
+    pe = sh["path_edges_k1"] + sh["path_edges_k2"]
+    bpu = 4 * (Na + 1) + 8 * Ea + 4 * Na + (4 * pe + 8 * 2 * U) / max(U, 1) + 8
+    achieved = bpu * U / (ksp_ms * 1e-3) / 1e9
+    value = steps / tmax
+    line = {
+        "metric": "C5 jobs/sec (multi-area RouteDb + UCMP RibPolicy + KSP2 of every "
+                  "destination)",
+        "value": round(value, 2), "unit": "jobs/s",
+        "n_gpus": world, "steps": steps, "warmup": warmup,
+        "ms_per_step": round(tmax / steps * 1e3, 4), "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
+        "config": {"workload": "C5: 8 areas x 1,250-node WAN + 64 ABRs (seed 0xC5A0), "
+                               "10 prefixes/node, 5% anycast, best-route selection, "
+                               "source abr-0, UCMP policy by tag, KSP2 k=1,2 to every "
+                               "destination of its areas",
+                   "nodes": sh["nodes"], "areas": sh["areas"],
+                   "prefixes": total_prefixes, "ksp2_destinations": sh["total_dests"],
+                   "parallelism": f"shard-by-prefix+destination x{world}"},
+        "ksp2_dests_per_s": round(total_units * steps / tmax, 1),
+        "route_kernels_ms": round(route_ms, 4), "ksp2_kernels_ms": round(ksp_ms, 4),
+        "job_kernel_ms": round(job_ms, 4),
+        "path_digest": f"{job_digest:016x}",
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
+                     "traffic": None, "bytes_alg_per_unit": round(bpu, 1),
+                     "kernel": "ksp_base_kernel + ksp2_kernel (per-area launches)"},
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import _refcpu
+        threads = max(1, min(16, os.cpu_count() or 1))
+        sample = 24 * threads
+        rs, ks, n, total, routes = _refcpu.cpu_baseline_c5(C5_OPTS, C5_SOURCE, pol, True,
+                                                           sample, threads)
+        job_s = rs + ks * total / n
+        line["cpu_baseline"] = {
+            "value": round(1.0 / job_s, 4), "unit": "jobs/s", "cores": threads,
+            "kind": "port",
+            "sample": f"refcpu buildRouteDb + RibPolicy::applyPolicy ({rs:.3f} s, 1 thread, "
+                      f"{routes} routes) + getKthPaths k=1,2 for {n} of {total} "
+                      f"destinations on {threads} threads ({ks:.3f} s), extrapolated to "
+                      f"all destinations; ingestion excluded"}
+    return line
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4"])
+    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5"])
     ap.add_argument("--prefixes-per-node", type=int, default=100)
     ap.add_argument("--c3-streams", type=int, default=2, choices=[1, 2],
                     help="C3: HIP streams for the two source groups")
@@ -354,6 +468,9 @@ def main():
     ap.add_argument("--no-c4", action="store_true",
                     help="skip the C4 link-failure sweep line embedded in the C2 result")
     ap.add_argument("--c4-steps", type=int, default=5)
+    ap.add_argument("--no-c5", action="store_true",
+                    help="skip the C5 multi-area KSP2 + UCMP line embedded in the C2 result")
+    ap.add_argument("--c5-steps", type=int, default=5)
     ap.add_argument("--opt", action="append", default=[],
                     help="engine option name=value (ogs_set_option), for A/B runs")
     args = ap.parse_args()
@@ -374,8 +491,9 @@ def main():
         name, val = o.split("=", 1)
         lib0 = capi.load()
         capi.check(lib0, lib0.ogs_set_option(name.encode(), int(val)), name)
-    if args.config == "c4":
-        line = run_c4(args, torch, dist, rank, world, local_rank)
+    if args.config in ("c4", "c5"):
+        run = run_c4 if args.config == "c4" else run_c5
+        line = run(args, torch, dist, rank, world, local_rank)
         if line is not None:
             print(json.dumps(line), flush=True)
         if dist:
@@ -541,6 +659,14 @@ def main():
                                    "config", "steps") if k in c4}
             if "cpu_baseline" in c4:
                 line["c4_link_failure_sweep"]["cpu_baseline"] = c4["cpu_baseline"]
+    if not args.no_c5:
+        c5 = run_c5(args, torch, dist, rank, world, local_rank)
+        if rank == 0:
+            line["c5_multiarea_ksp2_ucmp"] = {
+                k: c5[k] for k in ("value", "unit", "ms_per_step", "ksp2_dests_per_s",
+                                   "route_kernels_ms", "ksp2_kernels_ms", "job_kernel_ms",
+                                   "path_digest", "roofline", "config", "steps",
+                                   "cpu_baseline") if k in c5}
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist:
