@@ -249,7 +249,11 @@ int ogs_stream_sync(void* stream);
  *                 per-device workspace.
  *   "spf_frontier": 1 (default) large topologies (edge_src given) solve
  *                 SPF with the frontier kernel (one workgroup per unit,
- *                 only changed rows pushed); 0 the multi-source edge sweep. */
+ *                 only changed rows pushed); 0 the multi-source edge sweep.
+ *   "spf_queue":  frontier kernel round schedule: -1 (default) LDS node
+ *                 lists for sparse topologies (max degree <= 16), the chunk
+ *                 scan otherwise; 0 always the scan; 1 lists whenever they
+ *                 fit in LDS. */
 int ogs_set_option(const char* name, int64_t value);
 
 /* Smallest supported next-hop bitset width (words) for a source degree. */

@@ -13,6 +13,7 @@ extern int g_waveWgLds;
 extern int g_msGroup;
 extern int g_routeStream;
 extern int g_spfFrontier;
+extern int g_spfQueue;
 hipError_t launch_spf_routes(const ogs_graph& g, const ogs_prefix_table* pt,
                              const ogs_unit* units, int nUnits, uint32_t flags,
                              int W, const ogs_spf_out& out, hipStream_t stream,
@@ -150,6 +151,13 @@ int ogs_set_option(const char* name, int64_t value) {
       return fail(OGS_E_INVALID, "spf_frontier must be 0 or 1");
     }
     ogs::g_spfFrontier = int(value);
+    return OGS_OK;
+  }
+  if (std::strcmp(name, "spf_queue") == 0) {
+    if (value < -1 || value > 1) {
+      return fail(OGS_E_INVALID, "spf_queue must be -1, 0 or 1");
+    }
+    ogs::g_spfQueue = int(value);
     return OGS_OK;
   }
   if (std::strcmp(name, "wave_wg_lds") == 0) {

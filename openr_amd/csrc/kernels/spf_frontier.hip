@@ -260,14 +260,150 @@ __device__ __forceinline__ void frontier_spf(
 #endif
 }
 
-uint32_t frontier_lds_bytes(uint32_t Sn, int W) {
-  return 4u * (((Sn + 3u) & ~3u) + ((Sn * W + 3u) & ~3u)) + 2u * ((Sn + 1u) & ~1u);
+// ---- queue form: sparse, deep topologies (C4 / C5 WAN areas) ---------------
+// The chunk scan above reads every chunk record of the topology each round
+// to find the changed nodes: cheap per round on the dense fabric (few,
+// wide rounds), but a WAN needs ~70 narrow rounds per phase and the scan
+// dominates. Here the nodes changed in round r are appended (once, stamp
+// dedupe by LDS atomicMax) to an LDS list that round r + 1 walks; a round
+// touches only the rows of those nodes and ends at ONE workgroup barrier
+// (three rotating list counters, so the next count is reset while the
+// current one is live). Same fixpoint, same outputs as frontier_spf.
+template <int W, bool MODS>
+__device__ __forceinline__ void queue_spf(
+    uint32_t N, uint32_t s, const uint64_t* __restrict__ edges,
+    const uint32_t* __restrict__ gRow, uint32_t e0,
+    const uint8_t* __restrict__ nflags, bool hop, uint32_t* dist, uint32_t* nh,
+    uint32_t* stamp, uint16_t* q0, uint16_t* q1, uint32_t* qcnt, uint64_t* tp,
+    const DeadEdges& dead) {
+  constexpr uint32_t kInf = 0xFFFFFFFFu;
+  const int tid = threadIdx.x;
+  for (uint32_t v = tid; v < N; v += kBlock) {
+    dist[v] = (v == s) ? 0u : kInf;
+    stamp[v] = 0u;
+#pragma unroll
+    for (int w = 0; w < W; ++w) nh[v * W + w] = 0u;
+  }
+  if (tid == 0) {
+    q1[0] = uint16_t(s);  // round 1's list: buffer 1 & 1, count slot 1 % 3
+    qcnt[0] = 0u;
+    qcnt[1] = 1u;
+    qcnt[2] = 0u;
+  }
+  __syncthreads();
+#ifdef OGS_STAMPS
+  tp[0] = __builtin_amdgcn_s_memtime();
+#endif
+  // list of round r: buffer r & 1, count slot r % 3; appends go to round
+  // r + 1's buffer / slot; slot (r + 2) % 3 is idle during round r
+  auto append = [&](uint32_t t, uint32_t r) {
+    if (atomicMax(&stamp[t], r + 1) < r + 1) {
+      const uint32_t at = atomicAdd(&qcnt[(r + 1) % 3], 1u);
+      ((r + 1) & 1 ? q1 : q0)[at] = uint16_t(t);
+    }
+  };
+  uint32_t r = 1, n = 1;
+  for (; n; ++r) {
+    if (tid == 0) qcnt[(r + 2) % 3] = 0u;
+    const uint16_t* cur = (r & 1) ? q1 : q0;
+    for (uint32_t i = tid; i < n; i += kBlock) {
+      const uint32_t v = cur[i];
+      if (v != s && (nflags[v] & OGS_NODE_OVERLOADED)) continue;  // 741-752
+      const uint32_t dv = dist[v];
+      const uint32_t b = gRow[v] - e0, m = gRow[v + 1] - e0 - b;
+      for (uint32_t j = 0; j < m; ++j) {
+        const uint64_t x = edges[b + j];
+        const uint32_t lo = static_cast<uint32_t>(x);
+        if (lo & OGS_EDGE_DOWN) continue;
+        if constexpr (MODS) {
+          if (dead.has(b + j)) continue;
+        }
+        const uint32_t t = edge_dst(lo);
+        const uint32_t c = dv + (hop ? 1u : static_cast<uint32_t>(x >> 32));
+        if (c < dist[t] && c < atomicMin(&dist[t], c)) append(t, r);
+      }
+    }
+    __syncthreads();
+    n = qcnt[(r + 1) % 3];
+  }
+#ifdef OGS_STAMPS
+  tp[1] = __builtin_amdgcn_s_memtime();
+  tp[3] = r;
+#endif
+  // ---- next-hop phase: seeds from the source's row, then tight pushes -----
+  const uint32_t r0 = r;
+  __syncthreads();  // every thread has read the last (zero) count
+  if (tid == 0) qcnt[0] = qcnt[1] = qcnt[2] = 0u;
+  __syncthreads();
+  {
+    const uint32_t b = gRow[s] - e0, m = gRow[s + 1] - e0 - b;
+    for (uint32_t j = tid; j < m && j < 32u * W; j += kBlock) {
+      const uint64_t x = edges[b + j];
+      const uint32_t lo = static_cast<uint32_t>(x);
+      if (lo & OGS_EDGE_DOWN) continue;
+      if constexpr (MODS) {
+        if (dead.has(b + j)) continue;
+      }
+      const uint32_t t = edge_dst(lo);
+      const uint32_t w = hop ? 1u : static_cast<uint32_t>(x >> 32);
+      if (w == dist[t]) {
+        atomicOr(&nh[t * W + (j >> 5)], 1u << (j & 31u));
+        append(t, r0);
+      }
+    }
+  }
+  __syncthreads();
+  n = qcnt[(r0 + 1) % 3];
+  for (r = r0 + 1; n; ++r) {
+    if (tid == 0) qcnt[(r + 2) % 3] = 0u;
+    const uint16_t* cur = (r & 1) ? q1 : q0;
+    for (uint32_t i = tid; i < n; i += kBlock) {
+      const uint32_t v = cur[i];
+      if (v == s || (nflags[v] & OGS_NODE_OVERLOADED)) continue;
+      const uint32_t dv = dist[v];
+      uint32_t nv[W];
+#pragma unroll
+      for (int w = 0; w < W; ++w) nv[w] = nh[v * W + w];
+      const uint32_t b = gRow[v] - e0, m = gRow[v + 1] - e0 - b;
+      for (uint32_t j = 0; j < m; ++j) {
+        const uint64_t x = edges[b + j];
+        const uint32_t lo = static_cast<uint32_t>(x);
+        if (lo & OGS_EDGE_DOWN) continue;
+        if constexpr (MODS) {
+          if (dead.has(b + j)) continue;
+        }
+        const uint32_t t = edge_dst(lo);
+        if (dv + (hop ? 1u : static_cast<uint32_t>(x >> 32)) != dist[t]) continue;
+        bool add = false;
+#pragma unroll
+        for (int k = 0; k < W; ++k) {
+          const uint32_t a = nv[k] & ~nh[t * W + k];
+          if (a && (a & ~atomicOr(&nh[t * W + k], a))) add = true;
+        }
+        if (add) append(t, r);
+      }
+    }
+    __syncthreads();
+    n = qcnt[(r + 1) % 3];
+  }
+#ifdef OGS_STAMPS
+  tp[2] = __builtin_amdgcn_s_memtime();
+  tp[4] = r - r0;
+#endif
+}
+
+uint32_t frontier_lds_bytes(uint32_t Sn, int W, bool queue = false) {
+  const uint32_t core = 4u * (((Sn + 3u) & ~3u) + ((Sn * W + 3u) & ~3u));
+  if (!queue) return core + 2u * ((Sn + 1u) & ~1u);
+  // + u32 stamps + two u16 node lists
+  return core + 4u * ((Sn + 3u) & ~3u) + 2u * 2u * ((Sn + 1u) & ~1u);
 }
 
 // ROUTES = false: SPF only, dist / nh to HBM.
 // ROUTES = true: SPF + the unit's RouteDb stream (route_stream.h) from LDS;
 // dist / nh go to HBM only when requested.
-template <int W, bool ROUTES, bool MODS = false, bool DIFF = false>
+template <int W, bool ROUTES, bool MODS = false, bool DIFF = false,
+          bool QUEUE = false>
 __global__ __launch_bounds__(kBlock) void spf_frontier_kernel(
     ogs_graph g, ogs_prefix_table pt, const uint32_t* __restrict__ key,
     const uint64_t* __restrict__ chunks, const uint32_t* __restrict__ nChunk,
@@ -290,6 +426,11 @@ __global__ __launch_bounds__(kBlock) void spf_frontier_kernel(
   uint32_t* dist = reinterpret_cast<uint32_t*>(smem);              // [Sn]
   uint32_t* nh = dist + ((Sn + 3u) & ~3u);                           // [Sn*W]
   uint16_t* stamp = reinterpret_cast<uint16_t*>(nh + ((Sn * W + 3u) & ~3u));  // [Sn]
+  // queue form: u32 stamps [Sn] over the same start, then two u16 lists
+  uint32_t* stamp32 = reinterpret_cast<uint32_t*>(stamp);
+  uint16_t* q0 = reinterpret_cast<uint16_t*>(stamp32 + ((Sn + 3u) & ~3u));
+  uint16_t* q1 = q0 + ((Sn + 1u) & ~1u);
+  __shared__ uint32_t qcnt[3];
 
   DeadEdges dead;
 #pragma unroll
@@ -303,9 +444,15 @@ __global__ __launch_bounds__(kBlock) void spf_frontier_kernel(
   const uint64_t t0 = __builtin_amdgcn_s_memtime();
   const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
 #endif
-  frontier_spf<W, MODS>(N, s, g.edges + e0, chunks + size_t(unit.topo) * cap,
-                        nChunk[unit.topo], (flags & OGS_F_HOP_METRIC) != 0, gRow,
-                        e0, dist, nh, stamp, tp, dead);
+  if constexpr (QUEUE) {
+    queue_spf<W, MODS>(N, s, g.edges + e0, gRow, e0, nflags,
+                       (flags & OGS_F_HOP_METRIC) != 0, dist, nh, stamp32, q0, q1,
+                       qcnt, tp, dead);
+  } else {
+    frontier_spf<W, MODS>(N, s, g.edges + e0, chunks + size_t(unit.topo) * cap,
+                          nChunk[unit.topo], (flags & OGS_F_HOP_METRIC) != 0, gRow,
+                          e0, dist, nh, stamp, tp, dead);
+  }
 
   for (uint32_t v = tid; v < N; v += kBlock) {
     if (oDist) oDist[size_t(u0) * Sn + v] = dist[v];
@@ -366,16 +513,26 @@ __global__ __launch_bounds__(kBlock) void spf_frontier_kernel(
 #endif
 }
 
-template <int W, bool ROUTES, bool MODS = false, bool DIFF = false>
-hipError_t launch_frontier(const ogs_graph& g, const ogs_prefix_table& pt,
-                           const uint32_t* key, const uint64_t* chunks,
-                           const uint32_t* nChunk, const ogs_unit* units,
-                           int nUnits, uint32_t flags, uint32_t* dist,
-                           uint32_t* nh, const ogs_spf_out& out,
-                           hipStream_t stream, const ogs_unit_mods& mods = {},
-                           const ogs_route_diff& diff = {}) {
-  const uint32_t lds = frontier_lds_bytes(uint32_t(g.max_nodes), W);
-  auto k = spf_frontier_kernel<W, ROUTES, MODS, DIFF>;
+// "spf_queue" option: -1 (default) the queue form for sparse topologies
+// (max degree <= 16, <= 65,535 nodes), 0 never, 1 whenever it fits.
+int g_spfQueue = -1;
+
+bool use_queue(const ogs_graph& g, int W) {
+  if (g_spfQueue == 0 || g.max_nodes > 65535) return false;
+  if (frontier_lds_bytes(uint32_t(g.max_nodes), W, true) > 160u * 1024u) return false;
+  return g_spfQueue == 1 || g.max_degree <= 16;
+}
+
+template <int W, bool ROUTES, bool MODS, bool DIFF, bool QUEUE>
+hipError_t launch_frontier_q(const ogs_graph& g, const ogs_prefix_table& pt,
+                             const uint32_t* key, const uint64_t* chunks,
+                             const uint32_t* nChunk, const ogs_unit* units,
+                             int nUnits, uint32_t flags, uint32_t* dist,
+                             uint32_t* nh, const ogs_spf_out& out,
+                             hipStream_t stream, const ogs_unit_mods& mods,
+                             const ogs_route_diff& diff) {
+  const uint32_t lds = frontier_lds_bytes(uint32_t(g.max_nodes), W, QUEUE);
+  auto k = spf_frontier_kernel<W, ROUTES, MODS, DIFF, QUEUE>;
   if (lds > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
                                        hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -386,6 +543,24 @@ hipError_t launch_frontier(const ogs_graph& g, const ogs_prefix_table& pt,
                      chunks, nChunk, chunk_cap(g), units, flags, dist, nh, out,
                      mods, diff);
   return hipGetLastError();
+}
+
+template <int W, bool ROUTES, bool MODS = false, bool DIFF = false>
+hipError_t launch_frontier(const ogs_graph& g, const ogs_prefix_table& pt,
+                           const uint32_t* key, const uint64_t* chunks,
+                           const uint32_t* nChunk, const ogs_unit* units,
+                           int nUnits, uint32_t flags, uint32_t* dist,
+                           uint32_t* nh, const ogs_spf_out& out,
+                           hipStream_t stream, const ogs_unit_mods& mods = {},
+                           const ogs_route_diff& diff = {}) {
+  if (use_queue(g, W)) {
+    return launch_frontier_q<W, ROUTES, MODS, DIFF, true>(
+        g, pt, key, chunks, nChunk, units, nUnits, flags, dist, nh, out, stream,
+        mods, diff);
+  }
+  return launch_frontier_q<W, ROUTES, MODS, DIFF, false>(
+      g, pt, key, chunks, nChunk, units, nUnits, flags, dist, nh, out, stream,
+      mods, diff);
 }
 
 // "spf_frontier" option: 1 (default) large topologies use this kernel for
