@@ -14,6 +14,8 @@ extern int g_msGroup;
 extern int g_routeStream;
 extern int g_spfFrontier;
 extern int g_spfQueue;
+extern int g_kspQueue;
+extern int g_kspStage;
 hipError_t launch_spf_routes(const ogs_graph& g, const ogs_prefix_table* pt,
                              const ogs_unit* units, int nUnits, uint32_t flags,
                              int W, const ogs_spf_out& out, hipStream_t stream,
@@ -151,6 +153,16 @@ int ogs_set_option(const char* name, int64_t value) {
       return fail(OGS_E_INVALID, "spf_frontier must be 0 or 1");
     }
     ogs::g_spfFrontier = int(value);
+    return OGS_OK;
+  }
+  if (std::strcmp(name, "ksp_queue") == 0) {
+    if (value != 0 && value != 1) return fail(OGS_E_INVALID, "ksp_queue must be 0 or 1");
+    ogs::g_kspQueue = int(value);
+    return OGS_OK;
+  }
+  if (std::strcmp(name, "ksp_stage") == 0) {
+    if (value < -1 || value > 1) return fail(OGS_E_INVALID, "ksp_stage must be -1, 0 or 1");
+    ogs::g_kspStage = int(value);
     return OGS_OK;
   }
   if (std::strcmp(name, "spf_queue") == 0) {

@@ -27,9 +27,8 @@ namespace ogs {
 struct Frame {
   uint32_t node;
   uint32_t edge;    // edge (node -> pred) chosen at this frame
-  uint32_t lastU;   // resume key: (dist[pred], pred, rslot)
+  uint32_t lastU;   // resume key: (dist[lastU], lastU, lastSlot)
   uint32_t lastSlot;
-  uint64_t lastD;
 };
 
 template <typename D>
@@ -59,7 +58,7 @@ __device__ uint32_t trace_paths(const UnitCsr& csr, const D* dist, uint32_t s,
     // one traceOnePath(src, dest) call
     int sp = 0;
     // a frame without a resume key yet carries lastSlot's top bit
-    stack[0] = Frame{t, 0xFFFFFFFFu, 0u, 0x80000000u, 0ull};
+    stack[0] = Frame{t, 0xFFFFFFFFu, 0u, 0x80000000u};
     bool found = false;
     while (sp >= 0) {
       Frame& f = stack[sp];
@@ -69,7 +68,7 @@ __device__ uint32_t trace_paths(const UnitCsr& csr, const D* dist, uint32_t s,
       D bd = kInf;
       uint32_t bu = 0xFFFFFFFFu, bs = 0xFFFFFFFFu, be = 0xFFFFFFFFu;
       const bool fresh = (f.lastSlot & 0x80000000u) != 0;
-      const D ld = static_cast<D>(f.lastD);
+      const D ld = fresh ? D(0) : dist[f.lastU];
       for (uint32_t e = csr.rowp[v]; e < csr.rowp[v + 1]; ++e) {
         const uint64_t ed = csr.edg[e];
         const uint32_t lo = static_cast<uint32_t>(ed);
@@ -95,7 +94,6 @@ __device__ uint32_t trace_paths(const UnitCsr& csr, const D* dist, uint32_t s,
         --sp;
         continue;
       }
-      f.lastD = static_cast<uint64_t>(bd);
       f.lastU = bu;
       f.lastSlot = bs;
       const uint32_t l = link_id(csr, be, static_cast<uint32_t>(csr.edg[be]));
@@ -107,7 +105,7 @@ __device__ uint32_t trace_paths(const UnitCsr& csr, const D* dist, uint32_t s,
         break;
       }
       ++sp;
-      stack[sp] = Frame{bu, 0xFFFFFFFFu, 0u, 0x80000000u, 0ull};
+      stack[sp] = Frame{bu, 0xFFFFFFFFu, 0u, 0x80000000u};
     }
     if (!found) break;
     // path src -> dest = chosen edges from the top frame down to frame 0
@@ -252,27 +250,85 @@ hipError_t launch_ksp(const ogs_graph& g, const ogs_path_unit* units,
 // the unit reruns SPF with those links ignored (runSpf(src, true,
 // linksToIgnore), LinkState.cpp:691-693) and lane 0 traces the k = 2 paths.
 
+// Dist-only SPF with LDS node lists (the queue form of spf_frontier.hip's
+// queue_spf, workgroup units only): round r walks the nodes changed in round
+// r - 1 and pushes dist + w over their usable, unmasked links; one barrier
+// per round. Same least fixpoint as spf_fixpoint (spf_core.h).
+template <typename D, bool MASKED>
+__device__ void queue_dist(uint32_t N, uint32_t s, const UnitCsr& c,
+                           const uint8_t* __restrict__ nflags, D* dist,
+                           uint32_t* stamp, uint16_t* q0, uint16_t* q1,
+                           uint32_t* qcnt, const uint32_t* ignore) {
+  constexpr D kInf = DistInf<D>::value;
+  const int tid = threadIdx.x;
+  for (uint32_t v = tid; v < N; v += kBlock) {
+    dist[v] = (v == s) ? D(0) : kInf;
+    stamp[v] = 0u;
+  }
+  if (tid == 0) {
+    q1[0] = uint16_t(s);  // round 1's list: buffer 1 & 1, count slot 1 % 3
+    qcnt[0] = 0u;
+    qcnt[1] = 1u;
+    qcnt[2] = 0u;
+  }
+  __syncthreads();
+  uint32_t n = 1;
+  for (uint32_t r = 1; n; ++r) {
+    if (tid == 0) qcnt[(r + 2) % 3] = 0u;
+    const uint16_t* cur = (r & 1) ? q1 : q0;
+    uint16_t* nxt = (r & 1) ? q0 : q1;
+    for (uint32_t i = tid; i < n; i += kBlock) {
+      const uint32_t v = cur[i];
+      if (v != s && (nflags[v] & OGS_NODE_OVERLOADED)) continue;
+      const D dv = dist[v];
+      for (uint32_t e = c.rowp[v]; e < c.rowp[v + 1]; ++e) {
+        const uint64_t ed = c.edg[e];
+        const uint32_t lo = static_cast<uint32_t>(ed);
+        if (lo & OGS_EDGE_DOWN) continue;
+        if constexpr (MASKED) {
+          const uint32_t l = link_id(c, e, lo);
+          if ((ignore[l >> 5] >> (l & 31u)) & 1u) continue;
+        }
+        const uint32_t t = edge_dst(lo);
+        const D cand = dv + static_cast<D>(ed >> 32);
+        if (cand < dist[t] && cand < atomicMin(&dist[t], cand)) {
+          if (atomicMax(&stamp[t], r + 1) < r + 1) nxt[atomicAdd(&qcnt[(r + 1) % 3], 1u)] = uint16_t(t);
+        }
+      }
+    }
+    __syncthreads();
+    n = qcnt[(r + 1) % 3];
+  }
+}
+
 // Per-unit LDS carve-up of both launches: dist, visited + mask link bitsets,
-// trace stack, optionally the staged CSR.
+// trace stack, the queue form's stamps / lists / counters, optionally the
+// staged CSR.
 template <typename D>
 struct KspLds {
   D* dist;
   uint32_t* visited;
   uint32_t* mask;
   Frame* stack;
+  uint32_t* stamp;
+  uint16_t *q0, *q1;
+  uint32_t* qcnt;
+  const uint8_t* nflags;
   UnitCsr csr;
   uint32_t N, linkWords;
 };
 
 template <typename D>
 __host__ __device__ inline uint64_t ksp2_lds_bytes(uint64_t N, uint64_t E,
-                                                   bool stage) {
-  const uint64_t core = align16(N * sizeof(D)) + 2 * align16((E + 31) / 32 * 4) +
+                                                   bool stage, bool queue) {
+  uint64_t b = align16(N * sizeof(D)) + 2 * align16((E + 31) / 32 * 4) +
       align16(N * sizeof(Frame));
-  return stage ? core + align16((N + 1) * 4) + align16(E * 8) : core;
+  if (queue) b += align16(N * 4) + 2 * align16(N * 2) + 16;
+  if (stage) b += align16((N + 1) * 4) + align16(E * 8);
+  return b;
 }
 
-template <typename D, bool STAGE, int UT>
+template <typename D, bool STAGE, bool QUEUE, int UT>
 __device__ KspLds<D> ksp_lds(char* base, const ogs_graph& g, uint32_t topo,
                              int lane) {
   const uint32_t nb = g.node_base[topo];
@@ -283,6 +339,7 @@ __device__ KspLds<D> ksp_lds(char* base, const ogs_graph& g, uint32_t topo,
   KspLds<D> l;
   l.N = N;
   l.linkWords = (E + 31) / 32;
+  l.nflags = g.node_flags + nb;
   l.dist = reinterpret_cast<D*>(base);
   uint32_t off = align16(uint64_t(N) * sizeof(D));
   l.visited = reinterpret_cast<uint32_t*>(base + off);
@@ -291,6 +348,16 @@ __device__ KspLds<D> ksp_lds(char* base, const ogs_graph& g, uint32_t topo,
   off += align16(uint64_t(l.linkWords) * 4);
   l.stack = reinterpret_cast<Frame*>(base + off);
   off += align16(uint64_t(N) * sizeof(Frame));
+  if constexpr (QUEUE) {
+    l.stamp = reinterpret_cast<uint32_t*>(base + off);
+    off += align16(uint64_t(N) * 4);
+    l.q0 = reinterpret_cast<uint16_t*>(base + off);
+    off += align16(uint64_t(N) * 2);
+    l.q1 = reinterpret_cast<uint16_t*>(base + off);
+    off += align16(uint64_t(N) * 2);
+    l.qcnt = reinterpret_cast<uint32_t*>(base + off);
+    off += 16;
+  }
   if constexpr (STAGE) {
     uint32_t* lrow = reinterpret_cast<uint32_t*>(base + off);
     off += align16(uint64_t(N + 1) * 4);
@@ -322,7 +389,21 @@ __device__ __forceinline__ uint32_t unit_bcast(uint32_t x) {
   }
 }
 
-template <typename D, int UT, bool STAGE>
+// The unit's SPF into l.dist: queue form (workgroup units) or the pull
+// fixpoint (spf_core.h).
+template <typename D, int UT, bool QUEUE, bool MASKED>
+__device__ __forceinline__ void ksp_spf(const KspLds<D>& l, uint32_t s, int lane) {
+  if constexpr (QUEUE) {
+    static_assert(UT == kBlock, "queue form: one workgroup per unit");
+    queue_dist<D, MASKED>(l.N, s, l.csr, l.nflags, l.dist, l.stamp, l.q0, l.q1,
+                          l.qcnt, l.mask);
+  } else {
+    spf_fixpoint<D, 1, UT, false, MASKED>(l.N, s, lane, l.csr, false, l.dist,
+                                          nullptr, MASKED ? l.mask : nullptr);
+  }
+}
+
+template <typename D, int UT, bool STAGE, bool QUEUE>
 __global__ __launch_bounds__(kBlock) void ksp_base_kernel(
     ogs_graph g, const ogs_unit* __restrict__ sources, int nSources,
     D* __restrict__ srcDist, uint32_t ldsPerUnit) {
@@ -333,14 +414,13 @@ __global__ __launch_bounds__(kBlock) void ksp_base_kernel(
   if (sidx >= nSources) return;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const ogs_unit src = sources[sidx];
-  auto l = ksp_lds<D, STAGE, UT>(smem + uib * ldsPerUnit, g, src.topo, lane);
-  spf_fixpoint<D, 1, UT, false, false>(l.N, src.src, lane, l.csr, false, l.dist,
-                                       nullptr, nullptr);
+  auto l = ksp_lds<D, STAGE, QUEUE, UT>(smem + uib * ldsPerUnit, g, src.topo, lane);
+  ksp_spf<D, UT, QUEUE, false>(l, src.src, lane);
   D* row = srcDist + size_t(sidx) * uint32_t(g.max_nodes);
   for (uint32_t v = lane; v < l.N; v += UT) row[v] = l.dist[v];
 }
 
-template <typename D, int UT, bool STAGE>
+template <typename D, int UT, bool STAGE, bool QUEUE>
 __global__ __launch_bounds__(kBlock) void ksp2_kernel(
     ogs_graph g, const ogs_unit* __restrict__ sources, int nSources,
     const D* __restrict__ srcDist, const ogs_path_unit* __restrict__ units,
@@ -365,7 +445,7 @@ __global__ __launch_bounds__(kBlock) void ksp2_kernel(
     }
     return;
   }
-  auto l = ksp_lds<D, STAGE, UT>(smem + uib * ldsPerUnit, g, unit.topo, lane);
+  auto l = ksp_lds<D, STAGE, QUEUE, UT>(smem + uib * ldsPerUnit, g, unit.topo, lane);
   const D* row = srcDist + size_t(slot) * uint32_t(g.max_nodes);
   for (uint32_t v = lane; v < l.N; v += UT) l.dist[v] = row[v];
   Scope::sync();
@@ -385,14 +465,13 @@ __global__ __launch_bounds__(kBlock) void ksp2_kernel(
     return;
   }
   for (uint32_t i = lane; i < l.linkWords; i += UT) l.visited[i] = 0u;
-  spf_fixpoint<D, 1, UT, false, true>(l.N, s, lane, l.csr, false, l.dist,
-                                      nullptr, l.mask);
+  ksp_spf<D, UT, QUEUE, true>(l, s, lane);
   if (lane != 0) return;
   o2.path_count[uidx] = trace_paths<D, true>(l.csr, l.dist, s, t, l.visited,
                                              l.stack, l.mask, o2, uidx, nullptr);
 }
 
-template <typename D, int UT, bool STAGE>
+template <typename D, int UT, bool STAGE, bool QUEUE>
 hipError_t ksp2_launch(const ogs_graph& g, const ogs_unit* sources,
                        int nSources, D* srcDist, const ogs_path_unit* units,
                        int nUnits, const ogs_path_out& o1,
@@ -400,8 +479,8 @@ hipError_t ksp2_launch(const ogs_graph& g, const ogs_unit* sources,
                        hipStream_t stream) {
   constexpr int upb = kBlock / UT;
   const size_t bytes = size_t(lds) * upb;
-  auto kb = ksp_base_kernel<D, UT, STAGE>;
-  auto k2 = ksp2_kernel<D, UT, STAGE>;
+  auto kb = ksp_base_kernel<D, UT, STAGE, QUEUE>;
+  auto k2 = ksp2_kernel<D, UT, STAGE, QUEUE>;
   if (bytes > 64 * 1024) {
     for (const void* f : {reinterpret_cast<const void*>(kb),
                           reinterpret_cast<const void*>(k2)}) {
@@ -422,39 +501,44 @@ hipError_t ksp2_launch(const ogs_graph& g, const ogs_unit* sources,
 
 hipError_t workspace(size_t bytes, hipStream_t stream, void** out);
 
+// "ksp_queue": 1 (default) workgroup units solve SPF with LDS node lists,
+// 0 with the pull fixpoint. "ksp_stage": -1 (default) stage the CSR in LDS
+// only when three units still fit a CU, 0 never, 1 whenever it fits.
+int g_kspQueue = 1;
+int g_kspStage = -1;
+
 template <typename D>
 hipError_t ksp2_dispatch(const ogs_graph& g, const ogs_unit* sources,
                          int nSources, const ogs_path_unit* units, int nUnits,
                          const ogs_path_out& o1, const ogs_path_out& o2,
                          hipStream_t stream, int* unsupported) {
   const uint64_t N = g.max_nodes, E = g.max_edges;
-  const uint64_t core = ksp2_lds_bytes<D>(N, E, false);
-  const uint64_t staged = ksp2_lds_bytes<D>(N, E, true);
   constexpr uint64_t kBudget = 160 * 1024;
   void* ws = nullptr;
-  auto dist = [&](hipError_t* e) {
-    *e = workspace(size_t(nSources) * size_t(N) * sizeof(D), stream, &ws);
-    return static_cast<D*>(ws);
-  };
-  hipError_t e = hipSuccess;
-  if (N <= 256 && staged * 4 <= kBudget / 2) {
-    D* d = dist(&e);
-    if (e != hipSuccess) return e;
-    return ksp2_launch<D, 64, true>(g, sources, nSources, d, units, nUnits, o1,
-                                    o2, uint32_t(staged), stream);
+  hipError_t e = workspace(size_t(nSources) * size_t(N) * sizeof(D), stream, &ws);
+  if (e != hipSuccess) return e;
+  D* d = static_cast<D*>(ws);
+  const uint64_t tiny = ksp2_lds_bytes<D>(N, E, true, false);
+  if (N <= 256 && tiny * 4 <= kBudget / 2) {
+    return ksp2_launch<D, 64, true, false>(g, sources, nSources, d, units, nUnits,
+                                           o1, o2, uint32_t(tiny), stream);
   }
-  if (staged <= kBudget / 2) {
-    D* d = dist(&e);
-    if (e != hipSuccess) return e;
-    return ksp2_launch<D, kBlock, true>(g, sources, nSources, d, units, nUnits,
-                                        o1, o2, uint32_t(staged), stream);
+  const bool q = g_kspQueue != 0 && N <= 65535;
+  const uint64_t staged = ksp2_lds_bytes<D>(N, E, true, q);
+  const uint64_t core = ksp2_lds_bytes<D>(N, E, false, q);
+  const bool stage = g_kspStage == 1 ? staged <= kBudget
+                   : g_kspStage == 0 ? false
+                                     : staged * 3 <= kBudget;
+#define OGS_KSP2(ST_, Q_, B_)                                                     return ksp2_launch<D, kBlock, ST_, Q_>(g, sources, nSources, d, units, nUnits,                                          o1, o2, uint32_t(B_), stream);
+  if (stage) {
+    if (q) { OGS_KSP2(true, true, staged) }
+    OGS_KSP2(true, false, staged)
   }
   if (core <= kBudget) {
-    D* d = dist(&e);
-    if (e != hipSuccess) return e;
-    return ksp2_launch<D, kBlock, false>(g, sources, nSources, d, units, nUnits,
-                                         o1, o2, uint32_t(core), stream);
+    if (q) { OGS_KSP2(false, true, core) }
+    OGS_KSP2(false, false, core)
   }
+#undef OGS_KSP2
   *unsupported = 1;
   return hipSuccess;
 }
