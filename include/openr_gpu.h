@@ -255,8 +255,8 @@ int ogs_stream_sync(void* stream);
  *                 scan otherwise; 0 always the scan; 1 lists whenever they
  *                 fit in LDS.
  *   "ksp_queue":  KSP2 batch SPF: 1 (default) LDS node lists, 0 the pull
- *                 fixpoint. "ksp_stage": -1 (default) stage the CSR in LDS
- *                 when 3 units still fit a CU, 0 never, 1 whenever it fits. */
+ *                 fixpoint. "ksp_stage": -1 (default) auto, 0 CSR read
+ *                 from HBM/L2, 1 row offsets in LDS, 2 rows + edges in LDS. */
 int ogs_set_option(const char* name, int64_t value);
 
 /* Smallest supported next-hop bitset width (words) for a source degree. */

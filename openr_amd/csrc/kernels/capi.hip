@@ -161,7 +161,7 @@ int ogs_set_option(const char* name, int64_t value) {
     return OGS_OK;
   }
   if (std::strcmp(name, "ksp_stage") == 0) {
-    if (value < -1 || value > 1) return fail(OGS_E_INVALID, "ksp_stage must be -1, 0 or 1");
+    if (value < -1 || value > 2) return fail(OGS_E_INVALID, "ksp_stage must be -1, 0, 1 or 2");
     ogs::g_kspStage = int(value);
     return OGS_OK;
   }

@@ -69,25 +69,37 @@ __device__ uint32_t trace_paths(const UnitCsr& csr, const D* dist, uint32_t s,
       uint32_t bu = 0xFFFFFFFFu, bs = 0xFFFFFFFFu, be = 0xFFFFFFFFu;
       const bool fresh = (f.lastSlot & 0x80000000u) != 0;
       const D ld = fresh ? D(0) : dist[f.lastU];
-      for (uint32_t e = csr.rowp[v]; e < csr.rowp[v + 1]; ++e) {
-        const uint64_t ed = csr.edg[e];
-        const uint32_t lo = static_cast<uint32_t>(ed);
-        if (lo & OGS_EDGE_DOWN) continue;
-        const uint32_t u = edge_dst(lo);
-        if ((lo & OGS_EDGE_DST_OVERLOADED) && u != s) continue;
-        if constexpr (MASKED) {
-          const uint32_t l = link_id(csr, e, lo);
-          if ((ignore[l >> 5] >> (l & 31u)) & 1u) continue;
+      // the row's edges 8 at a time: the loads of a batch are independent
+      // (HBM/L2 latency once per batch, not once per edge)
+      const uint32_t rEnd = csr.rowp[v + 1];
+      for (uint32_t eb = csr.rowp[v]; eb < rEnd; eb += 8) {
+        uint64_t xs[8];
+#pragma unroll
+        for (uint32_t k = 0; k < 8; ++k) {
+          xs[k] = eb + k < rEnd ? csr.edg[eb + k] : uint64_t(OGS_EDGE_DOWN);
         }
-        const D du = dist[u];
-        if (du == kInf || du + static_cast<D>(ed >> 32) != dv) continue;
-        const uint32_t slot = edge_rslot(lo);
-        if (!fresh && !key_less<D>(ld, f.lastU, f.lastSlot, du, u, slot)) continue;
-        if (key_less<D>(du, u, slot, bd, bu, bs)) {
-          bd = du;
-          bu = u;
-          bs = slot;
-          be = e;
+#pragma unroll
+        for (uint32_t k = 0; k < 8; ++k) {
+          const uint32_t e = eb + k;
+          const uint64_t ed = xs[k];
+          const uint32_t lo = static_cast<uint32_t>(ed);
+          if (lo & OGS_EDGE_DOWN) continue;
+          const uint32_t u = edge_dst(lo);
+          if ((lo & OGS_EDGE_DST_OVERLOADED) && u != s) continue;
+          if constexpr (MASKED) {
+            const uint32_t l = link_id(csr, e, lo);
+            if ((ignore[l >> 5] >> (l & 31u)) & 1u) continue;
+          }
+          const D du = dist[u];
+          if (du == kInf || du + static_cast<D>(ed >> 32) != dv) continue;
+          const uint32_t slot = edge_rslot(lo);
+          if (!fresh && !key_less<D>(ld, f.lastU, f.lastSlot, du, u, slot)) continue;
+          if (key_less<D>(du, u, slot, bd, bu, bs)) {
+            bd = du;
+            bu = u;
+            bs = slot;
+            be = e;
+          }
         }
       }
       if (be == 0xFFFFFFFFu) {  // exhausted: this recursion level fails
@@ -281,18 +293,29 @@ __device__ void queue_dist(uint32_t N, uint32_t s, const UnitCsr& c,
       const uint32_t v = cur[i];
       if (v != s && (nflags[v] & OGS_NODE_OVERLOADED)) continue;
       const D dv = dist[v];
-      for (uint32_t e = c.rowp[v]; e < c.rowp[v + 1]; ++e) {
-        const uint64_t ed = c.edg[e];
-        const uint32_t lo = static_cast<uint32_t>(ed);
-        if (lo & OGS_EDGE_DOWN) continue;
-        if constexpr (MASKED) {
-          const uint32_t l = link_id(c, e, lo);
-          if ((ignore[l >> 5] >> (l & 31u)) & 1u) continue;
+      const uint32_t rEnd = c.rowp[v + 1];
+      for (uint32_t eb = c.rowp[v]; eb < rEnd; eb += 8) {
+        uint64_t xs[8];
+#pragma unroll
+        for (uint32_t k = 0; k < 8; ++k) {
+          xs[k] = eb + k < rEnd ? c.edg[eb + k] : uint64_t(OGS_EDGE_DOWN);
         }
-        const uint32_t t = edge_dst(lo);
-        const D cand = dv + static_cast<D>(ed >> 32);
-        if (cand < dist[t] && cand < atomicMin(&dist[t], cand)) {
-          if (atomicMax(&stamp[t], r + 1) < r + 1) nxt[atomicAdd(&qcnt[(r + 1) % 3], 1u)] = uint16_t(t);
+#pragma unroll
+        for (uint32_t k = 0; k < 8; ++k) {
+          const uint64_t ed = xs[k];
+          const uint32_t lo = static_cast<uint32_t>(ed);
+          if (lo & OGS_EDGE_DOWN) continue;
+          if constexpr (MASKED) {
+            const uint32_t l = link_id(c, eb + k, lo);
+            if ((ignore[l >> 5] >> (l & 31u)) & 1u) continue;
+          }
+          const uint32_t t = edge_dst(lo);
+          const D cand = dv + static_cast<D>(ed >> 32);
+          if (cand < dist[t] && cand < atomicMin(&dist[t], cand)) {
+            if (atomicMax(&stamp[t], r + 1) < r + 1) {
+              nxt[atomicAdd(&qcnt[(r + 1) % 3], 1u)] = uint16_t(t);
+            }
+          }
         }
       }
     }
@@ -318,17 +341,19 @@ struct KspLds {
   uint32_t N, linkWords;
 };
 
+// stage: 0 CSR read from HBM/L2, 1 row offsets in LDS, 2 rows + edges
 template <typename D>
 __host__ __device__ inline uint64_t ksp2_lds_bytes(uint64_t N, uint64_t E,
-                                                   bool stage, bool queue) {
+                                                   int stage, bool queue) {
   uint64_t b = align16(N * sizeof(D)) + 2 * align16((E + 31) / 32 * 4) +
       align16(N * sizeof(Frame));
   if (queue) b += align16(N * 4) + 2 * align16(N * 2) + 16;
-  if (stage) b += align16((N + 1) * 4) + align16(E * 8);
+  if (stage >= 1) b += align16((N + 1) * 4);
+  if (stage >= 2) b += align16(E * 8);
   return b;
 }
 
-template <typename D, bool STAGE, bool QUEUE, int UT>
+template <typename D, int STAGE, bool QUEUE, int UT>
 __device__ KspLds<D> ksp_lds(char* base, const ogs_graph& g, uint32_t topo,
                              int lane) {
   const uint32_t nb = g.node_base[topo];
@@ -358,13 +383,17 @@ __device__ KspLds<D> ksp_lds(char* base, const ogs_graph& g, uint32_t topo,
     l.qcnt = reinterpret_cast<uint32_t*>(base + off);
     off += 16;
   }
-  if constexpr (STAGE) {
+  if constexpr (STAGE >= 1) {
     uint32_t* lrow = reinterpret_cast<uint32_t*>(base + off);
     off += align16(uint64_t(N + 1) * 4);
-    uint64_t* ledg = reinterpret_cast<uint64_t*>(base + off);
     for (uint32_t i = lane; i <= N; i += UT) lrow[i] = gRow[i] - e0;
-    for (uint32_t i = lane; i < E; i += UT) ledg[i] = g.edges[e0 + i];
-    l.csr = UnitCsr{lrow, ledg, 0u};
+    if constexpr (STAGE >= 2) {
+      uint64_t* ledg = reinterpret_cast<uint64_t*>(base + off);
+      for (uint32_t i = lane; i < E; i += UT) ledg[i] = g.edges[e0 + i];
+      l.csr = UnitCsr{lrow, ledg, 0u};
+    } else {
+      l.csr = UnitCsr{lrow, g.edges + e0, 0u};
+    }
   } else {
     l.csr = UnitCsr{gRow, g.edges, e0};
   }
@@ -403,7 +432,7 @@ __device__ __forceinline__ void ksp_spf(const KspLds<D>& l, uint32_t s, int lane
   }
 }
 
-template <typename D, int UT, bool STAGE, bool QUEUE>
+template <typename D, int UT, int STAGE, bool QUEUE>
 __global__ __launch_bounds__(kBlock) void ksp_base_kernel(
     ogs_graph g, const ogs_unit* __restrict__ sources, int nSources,
     D* __restrict__ srcDist, uint32_t ldsPerUnit) {
@@ -420,7 +449,7 @@ __global__ __launch_bounds__(kBlock) void ksp_base_kernel(
   for (uint32_t v = lane; v < l.N; v += UT) row[v] = l.dist[v];
 }
 
-template <typename D, int UT, bool STAGE, bool QUEUE>
+template <typename D, int UT, int STAGE, bool QUEUE>
 __global__ __launch_bounds__(kBlock) void ksp2_kernel(
     ogs_graph g, const ogs_unit* __restrict__ sources, int nSources,
     const D* __restrict__ srcDist, const ogs_path_unit* __restrict__ units,
@@ -471,7 +500,7 @@ __global__ __launch_bounds__(kBlock) void ksp2_kernel(
                                              l.stack, l.mask, o2, uidx, nullptr);
 }
 
-template <typename D, int UT, bool STAGE, bool QUEUE>
+template <typename D, int UT, int STAGE, bool QUEUE>
 hipError_t ksp2_launch(const ogs_graph& g, const ogs_unit* sources,
                        int nSources, D* srcDist, const ogs_path_unit* units,
                        int nUnits, const ogs_path_out& o1,
@@ -502,8 +531,9 @@ hipError_t ksp2_launch(const ogs_graph& g, const ogs_unit* sources,
 hipError_t workspace(size_t bytes, hipStream_t stream, void** out);
 
 // "ksp_queue": 1 (default) workgroup units solve SPF with LDS node lists,
-// 0 with the pull fixpoint. "ksp_stage": -1 (default) stage the CSR in LDS
-// only when three units still fit a CU, 0 never, 1 whenever it fits.
+// 0 with the pull fixpoint. "ksp_stage": -1 (default) auto -- the edges in
+// LDS only when three units still fit a CU, else the row offsets only --;
+// 0 nothing staged, 1 row offsets, 2 rows + edges whenever they fit.
 int g_kspQueue = 1;
 int g_kspStage = -1;
 
@@ -518,29 +548,32 @@ hipError_t ksp2_dispatch(const ogs_graph& g, const ogs_unit* sources,
   hipError_t e = workspace(size_t(nSources) * size_t(N) * sizeof(D), stream, &ws);
   if (e != hipSuccess) return e;
   D* d = static_cast<D*>(ws);
-  const uint64_t tiny = ksp2_lds_bytes<D>(N, E, true, false);
+  const uint64_t tiny = ksp2_lds_bytes<D>(N, E, 2, false);
   if (N <= 256 && tiny * 4 <= kBudget / 2) {
-    return ksp2_launch<D, 64, true, false>(g, sources, nSources, d, units, nUnits,
-                                           o1, o2, uint32_t(tiny), stream);
+    return ksp2_launch<D, 64, 2, false>(g, sources, nSources, d, units, nUnits,
+                                        o1, o2, uint32_t(tiny), stream);
   }
   const bool q = g_kspQueue != 0 && N <= 65535;
-  const uint64_t staged = ksp2_lds_bytes<D>(N, E, true, q);
-  const uint64_t core = ksp2_lds_bytes<D>(N, E, false, q);
-  const bool stage = g_kspStage == 1 ? staged <= kBudget
-                   : g_kspStage == 0 ? false
-                                     : staged * 3 <= kBudget;
-#define OGS_KSP2(ST_, Q_, B_)                                                     return ksp2_launch<D, kBlock, ST_, Q_>(g, sources, nSources, d, units, nUnits,                                          o1, o2, uint32_t(B_), stream);
-  if (stage) {
-    if (q) { OGS_KSP2(true, true, staged) }
-    OGS_KSP2(true, false, staged)
+  int st = g_kspStage;
+  if (st < 0) st = ksp2_lds_bytes<D>(N, E, 2, q) * 3 <= kBudget ? 2 : 1;
+  while (st > 0 && ksp2_lds_bytes<D>(N, E, st, q) > kBudget) --st;
+  const uint64_t b = ksp2_lds_bytes<D>(N, E, st, q);
+  if (b > kBudget) {
+    *unsupported = 1;
+    return hipSuccess;
   }
-  if (core <= kBudget) {
-    if (q) { OGS_KSP2(false, true, core) }
-    OGS_KSP2(false, false, core)
+#define OGS_KSP2(ST_, Q_)                                                      \
+  return ksp2_launch<D, kBlock, ST_, Q_>(g, sources, nSources, d, units, nUnits, \
+                                         o1, o2, uint32_t(b), stream);
+  if (q) {
+    if (st == 2) { OGS_KSP2(2, true) }
+    if (st == 1) { OGS_KSP2(1, true) }
+    OGS_KSP2(0, true)
   }
+  if (st == 2) { OGS_KSP2(2, false) }
+  if (st == 1) { OGS_KSP2(1, false) }
+  OGS_KSP2(0, false)
 #undef OGS_KSP2
-  *unsupported = 1;
-  return hipSuccess;
 }
 
 hipError_t launch_ksp2(const ogs_graph& g, const ogs_unit* sources,

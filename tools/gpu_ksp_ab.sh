@@ -6,7 +6,7 @@ timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout
   -k "ksp or c5 or kat" > gpurun_out/k_pytest.log 2>&1 || { tail -30 gpurun_out/k_pytest.log; exit 1; }
 tail -2 gpurun_out/k_pytest.log
 i=0
-for opts in "--opt ksp_queue=1" "--opt ksp_queue=0" "--opt ksp_queue=1 --opt ksp_stage=1" "--opt ksp_queue=0 --opt ksp_stage=0"; do
+for opts in "--opt ksp_stage=-1" "--opt ksp_stage=0" "--opt ksp_stage=2" "--opt ksp_queue=0"; do
   i=$((i+1))
   timeout -k 10 300 python3 -u bench.py --config c5 --steps 10 --warmup 2 --no-cpu-baseline \
     $opts > gpurun_out/k_c5_$i.log 2>&1 || { tail -5 gpurun_out/k_c5_$i.log; exit 1; }
