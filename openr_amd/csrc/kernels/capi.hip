@@ -10,6 +10,7 @@
 namespace ogs {
 extern int g_unitWidth;
 extern int g_waveWgLds;
+extern int g_waveUpb;
 extern int g_msGroup;
 extern int g_routeStream;
 extern int g_spfFrontier;
@@ -170,6 +171,13 @@ int ogs_set_option(const char* name, int64_t value) {
       return fail(OGS_E_INVALID, "spf_queue must be -1, 0 or 1");
     }
     ogs::g_spfQueue = int(value);
+    return OGS_OK;
+  }
+  if (std::strcmp(name, "wave_upb") == 0) {
+    if (value != 4 && value != 8 && value != 16) {
+      return fail(OGS_E_INVALID, "wave_upb must be 4, 8 or 16");
+    }
+    ogs::g_waveUpb = int(value);
     return OGS_OK;
   }
   if (std::strcmp(name, "wave_wg_lds") == 0) {

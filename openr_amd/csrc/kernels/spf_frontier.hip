@@ -269,20 +269,43 @@ __device__ __forceinline__ void frontier_spf(
 // touches only the rows of those nodes and ends at ONE workgroup barrier
 // (three rotating list counters, so the next count is reset while the
 // current one is live). Same fixpoint, same outputs as frontier_spf.
+// Edges of a row, 8 loads in flight at a time: fn(local edge id, edge).
+template <typename Fn>
+__device__ __forceinline__ void for_row(const uint64_t* __restrict__ edges,
+                                        uint32_t b, uint32_t m, Fn fn) {
+  for (uint32_t jb = 0; jb < m; jb += 8) {
+    uint64_t xs[8];
+#pragma unroll
+    for (uint32_t k = 0; k < 8; ++k) {
+      xs[k] = jb + k < m ? edges[b + jb + k] : uint64_t(OGS_EDGE_DOWN);
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < 8; ++k) {
+      if (jb + k < m) fn(b + jb + k, xs[k]);
+    }
+  }
+}
+
 template <int W, bool MODS>
 __device__ __forceinline__ void queue_spf(
     uint32_t N, uint32_t s, const uint64_t* __restrict__ edges,
     const uint32_t* __restrict__ gRow, uint32_t e0,
     const uint8_t* __restrict__ nflags, bool hop, uint32_t* dist, uint32_t* nh,
-    uint32_t* stamp, uint16_t* q0, uint16_t* q1, uint32_t* qcnt, uint64_t* tp,
-    const DeadEdges& dead) {
+    uint32_t* stamp, uint16_t* q0, uint16_t* q1, uint32_t* qcnt, uint32_t* ninfo,
+    uint64_t* tp, const DeadEdges& dead) {
   constexpr uint32_t kInf = 0xFFFFFFFFu;
+  constexpr uint32_t kDrained = 0x80000000u;
   const int tid = threadIdx.x;
   for (uint32_t v = tid; v < N; v += kBlock) {
     dist[v] = (v == s) ? 0u : kInf;
     stamp[v] = 0u;
 #pragma unroll
     for (int w = 0; w < W; ++w) nh[v * W + w] = 0u;
+  }
+  // node info: local row begin | hard-drained bit (one LDS read per node)
+  for (uint32_t v = tid; v <= N; v += kBlock) {
+    ninfo[v] = (gRow[v] - e0) |
+        ((v < N && (nflags[v] & OGS_NODE_OVERLOADED)) ? kDrained : 0u);
   }
   if (tid == 0) {
     q1[0] = uint16_t(s);  // round 1's list: buffer 1 & 1, count slot 1 % 3
@@ -308,20 +331,19 @@ __device__ __forceinline__ void queue_spf(
     const uint16_t* cur = (r & 1) ? q1 : q0;
     for (uint32_t i = tid; i < n; i += kBlock) {
       const uint32_t v = cur[i];
-      if (v != s && (nflags[v] & OGS_NODE_OVERLOADED)) continue;  // 741-752
+      const uint32_t iv = ninfo[v], b = iv & ~kDrained;
+      if (v != s && (iv & kDrained)) continue;  // LinkState.cpp:741-752
       const uint32_t dv = dist[v];
-      const uint32_t b = gRow[v] - e0, m = gRow[v + 1] - e0 - b;
-      for (uint32_t j = 0; j < m; ++j) {
-        const uint64_t x = edges[b + j];
+      for_row(edges, b, (ninfo[v + 1] & ~kDrained) - b, [&](uint32_t e, uint64_t x) {
         const uint32_t lo = static_cast<uint32_t>(x);
-        if (lo & OGS_EDGE_DOWN) continue;
+        if (lo & OGS_EDGE_DOWN) return;
         if constexpr (MODS) {
-          if (dead.has(b + j)) continue;
+          if (dead.has(e)) return;
         }
         const uint32_t t = edge_dst(lo);
         const uint32_t c = dv + (hop ? 1u : static_cast<uint32_t>(x >> 32));
         if (c < dist[t] && c < atomicMin(&dist[t], c)) append(t, r);
-      }
+      });
     }
     __syncthreads();
     n = qcnt[(r + 1) % 3];
@@ -359,21 +381,20 @@ __device__ __forceinline__ void queue_spf(
     const uint16_t* cur = (r & 1) ? q1 : q0;
     for (uint32_t i = tid; i < n; i += kBlock) {
       const uint32_t v = cur[i];
-      if (v == s || (nflags[v] & OGS_NODE_OVERLOADED)) continue;
+      const uint32_t iv = ninfo[v], b = iv & ~kDrained;
+      if (v == s || (iv & kDrained)) continue;
       const uint32_t dv = dist[v];
       uint32_t nv[W];
 #pragma unroll
       for (int w = 0; w < W; ++w) nv[w] = nh[v * W + w];
-      const uint32_t b = gRow[v] - e0, m = gRow[v + 1] - e0 - b;
-      for (uint32_t j = 0; j < m; ++j) {
-        const uint64_t x = edges[b + j];
+      for_row(edges, b, (ninfo[v + 1] & ~kDrained) - b, [&](uint32_t e, uint64_t x) {
         const uint32_t lo = static_cast<uint32_t>(x);
-        if (lo & OGS_EDGE_DOWN) continue;
+        if (lo & OGS_EDGE_DOWN) return;
         if constexpr (MODS) {
-          if (dead.has(b + j)) continue;
+          if (dead.has(e)) return;
         }
         const uint32_t t = edge_dst(lo);
-        if (dv + (hop ? 1u : static_cast<uint32_t>(x >> 32)) != dist[t]) continue;
+        if (dv + (hop ? 1u : static_cast<uint32_t>(x >> 32)) != dist[t]) return;
         bool add = false;
 #pragma unroll
         for (int k = 0; k < W; ++k) {
@@ -381,7 +402,7 @@ __device__ __forceinline__ void queue_spf(
           if (a && (a & ~atomicOr(&nh[t * W + k], a))) add = true;
         }
         if (add) append(t, r);
-      }
+      });
     }
     __syncthreads();
     n = qcnt[(r + 1) % 3];
@@ -395,8 +416,9 @@ __device__ __forceinline__ void queue_spf(
 uint32_t frontier_lds_bytes(uint32_t Sn, int W, bool queue = false) {
   const uint32_t core = 4u * (((Sn + 3u) & ~3u) + ((Sn * W + 3u) & ~3u));
   if (!queue) return core + 2u * ((Sn + 1u) & ~1u);
-  // + u32 stamps + two u16 node lists
-  return core + 4u * ((Sn + 3u) & ~3u) + 2u * 2u * ((Sn + 1u) & ~1u);
+  // + u32 stamps + two u16 node lists + u32 node info [Sn + 1]
+  return core + 4u * ((Sn + 3u) & ~3u) + 2u * 2u * ((Sn + 1u) & ~1u) +
+      4u * ((Sn + 4u) & ~3u);
 }
 
 // ROUTES = false: SPF only, dist / nh to HBM.
@@ -430,6 +452,7 @@ __global__ __launch_bounds__(kBlock) void spf_frontier_kernel(
   uint32_t* stamp32 = reinterpret_cast<uint32_t*>(stamp);
   uint16_t* q0 = reinterpret_cast<uint16_t*>(stamp32 + ((Sn + 3u) & ~3u));
   uint16_t* q1 = q0 + ((Sn + 1u) & ~1u);
+  uint32_t* ninfo = reinterpret_cast<uint32_t*>(q1 + ((Sn + 1u) & ~1u));
   __shared__ uint32_t qcnt[3];
 
   DeadEdges dead;
@@ -447,7 +470,7 @@ __global__ __launch_bounds__(kBlock) void spf_frontier_kernel(
   if constexpr (QUEUE) {
     queue_spf<W, MODS>(N, s, g.edges + e0, gRow, e0, nflags,
                        (flags & OGS_F_HOP_METRIC) != 0, dist, nh, stamp32, q0, q1,
-                       qcnt, tp, dead);
+                       qcnt, ninfo, tp, dead);
   } else {
     frontier_spf<W, MODS>(N, s, g.edges + e0, chunks + size_t(unit.topo) * cap,
                           nChunk[unit.topo], (flags & OGS_F_HOP_METRIC) != 0, gRow,

@@ -136,8 +136,8 @@ __device__ __forceinline__ void route_single(uint32_t n, int64_t minNh,
   }
 }
 
-template <int NPL, int MAXD>
-__global__ __launch_bounds__(256) void spf_route_wave_kernel(
+template <int NPL, int MAXD, int UPB>
+__global__ __launch_bounds__(64 * UPB) void spf_route_wave_kernel(
     ogs_graph g, ogs_prefix_table pt, int hasPrefixes,
     const ogs_unit* __restrict__ units, int nUnits, uint32_t flags,
     ogs_spf_out out, uint32_t ldsPerUnit, uint32_t maxA) {
@@ -146,7 +146,7 @@ __global__ __launch_bounds__(256) void spf_route_wave_kernel(
   // so the unit record and its descriptor come through scalar loads
   const int uib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  const int uidx = blockIdx.x * 4 + uib;
+  const int uidx = blockIdx.x * UPB + uib;
   if (uidx >= nUnits) return;
 #ifdef OGS_STAMPS  // diagnostic build only: phase clocks into out.sel
   const uint64_t tStart = __builtin_amdgcn_s_memtime();
@@ -587,25 +587,44 @@ __global__ __launch_bounds__(256) void spf_route_wave_kernel(
 // "wave_wg_lds" option: minimum LDS bytes per workgroup (occupancy probe for
 // A/B measurements; 0 = just what the units need)
 int g_waveWgLds = 0;
+// "wave_upb" option: units (wavefronts) per workgroup, 4, 8 or 16
+int g_waveUpb = 4;
 
-template <int NPL, int MAXD>
-hipError_t launch_wave(const ogs_graph& g, const ogs_prefix_table& pt,
-                       int hasPrefixes, const ogs_unit* units, int nUnits,
-                       uint32_t flags, const ogs_spf_out& out, uint32_t lds,
-                       uint32_t maxA, hipStream_t stream) {
-  const int grid = (nUnits + 3) / 4;
-  size_t bytes = size_t(lds) * 4;
+template <int NPL, int MAXD, int UPB>
+hipError_t launch_wave_upb(const ogs_graph& g, const ogs_prefix_table& pt,
+                           int hasPrefixes, const ogs_unit* units, int nUnits,
+                           uint32_t flags, const ogs_spf_out& out, uint32_t lds,
+                           uint32_t maxA, hipStream_t stream) {
+  const int grid = (nUnits + UPB - 1) / UPB;
+  size_t bytes = size_t(lds) * UPB;
   if (bytes < size_t(g_waveWgLds)) bytes = size_t(g_waveWgLds);
-  auto k = spf_route_wave_kernel<NPL, MAXD>;
+  auto k = spf_route_wave_kernel<NPL, MAXD, UPB>;
   if (bytes > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute(
         reinterpret_cast<const void*>(k),
         hipFuncAttributeMaxDynamicSharedMemorySize, int(bytes));
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL(k, dim3(grid), dim3(256), bytes, stream, g, pt,
+  hipLaunchKernelGGL(k, dim3(grid), dim3(64 * UPB), bytes, stream, g, pt,
                      hasPrefixes, units, nUnits, flags, out, lds, maxA);
   return hipGetLastError();
+}
+
+template <int NPL, int MAXD>
+hipError_t launch_wave(const ogs_graph& g, const ogs_prefix_table& pt,
+                       int hasPrefixes, const ogs_unit* units, int nUnits,
+                       uint32_t flags, const ogs_spf_out& out, uint32_t lds,
+                       uint32_t maxA, hipStream_t stream) {
+  if (g_waveUpb == 16 && uint64_t(lds) * 16 <= 160 * 1024) {
+    return launch_wave_upb<NPL, MAXD, 16>(g, pt, hasPrefixes, units, nUnits, flags,
+                                          out, lds, maxA, stream);
+  }
+  if (g_waveUpb == 8 && uint64_t(lds) * 8 <= 160 * 1024) {
+    return launch_wave_upb<NPL, MAXD, 8>(g, pt, hasPrefixes, units, nUnits, flags,
+                                         out, lds, maxA, stream);
+  }
+  return launch_wave_upb<NPL, MAXD, 4>(g, pt, hasPrefixes, units, nUnits, flags,
+                                       out, lds, maxA, stream);
 }
 
 bool try_wave(const ogs_graph& g, const ogs_prefix_table& pt, int hasPrefixes,

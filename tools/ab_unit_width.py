@@ -22,8 +22,8 @@ def main():
     times = {name: [] for name, *_ in vs}
     graphs = {o: c.graph(o) for o in (None, "p", "pi")}
     for rnd in range(12):
-        for name, uw, order, lds, use_b in vs:
-            apply(c, uw, lds, use_b)
+        for name, uw, order, lds, use_b, upb in vs:
+            apply(c, uw, lds, use_b, upb)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
             for _ in range(10):

@@ -78,17 +78,20 @@ def variants(default):
     out = []
     for x in os.environ.get("VARIANTS", default).split(","):
         spec, _, which = x.partition("#")
+        spec, _, upb = spec.partition("^")  # ^U = wave_upb option
         base, _, lds = spec.partition("@")
         uw = int(base.rstrip("pi"))
         flags = base[len(str(uw)):]
         # order: "p" = slot order only, "pi" = slot order + edge image
         order = {"": None, "p": "p", "pi": "pi"}[flags]
-        out.append((x, uw, order, int(lds or 0), which == "b"))
+        out.append((x, uw, order, int(lds or 0), which == "b", int(upb or 4)))
     return out
 
 
-def apply(c, uw, lds, use_b=False):
+def apply(c, uw, lds, use_b=False, upb=4):
     c.lib = c.libb if use_b else c.liba
     c.capi.check(c.lib, c.lib.ogs_set_option(b"unit_width", uw), "unit_width")
     if lds or not use_b:
         c.capi.check(c.lib, c.lib.ogs_set_option(b"wave_wg_lds", lds), "wave_wg_lds")
+    if upb != 4 or not use_b:
+        c.capi.check(c.lib, c.lib.ogs_set_option(b"wave_upb", upb), "wave_upb")
