@@ -251,9 +251,10 @@ int ogs_stream_sync(void* stream);
  *                 SPF with the frontier kernel (one workgroup per unit,
  *                 only changed rows pushed); 0 the multi-source edge sweep.
  *   "spf_queue":  frontier kernel round schedule: -1 (default) LDS node
- *                 lists for sparse topologies (max degree <= 16), the chunk
- *                 scan otherwise; 0 always the scan; 1 lists whenever they
- *                 fit in LDS.
+ *                 lists for sparse topologies (max degree <= 16; one phase
+ *                 over packed {dist, next hops} words when the next-hop sets
+ *                 fit one word), the chunk scan otherwise; 0 always the scan;
+ *                 1 lists whenever they fit in LDS; 2 lists, two phases.
  *   "ksp_queue":  KSP2 batch SPF: 1 (default) LDS node lists, 0 the pull
  *                 fixpoint. "ksp_stage": -1 (default) auto, 0 CSR read
  *                 from HBM/L2, 1 row offsets in LDS, 2 rows + edges in LDS. */

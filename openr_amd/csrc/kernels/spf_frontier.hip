@@ -413,6 +413,90 @@ __device__ __forceinline__ void queue_spf(
 #endif
 }
 
+// Queue form with ONE phase (next-hop sets of one word): dist and next-hop
+// bits packed per node in a u64 LDS word {dist | nh << 32} updated by CAS,
+// so a push carries both -- a strictly shorter candidate replaces the word,
+// an equal one ORs its bits in -- and a node whose word changed is queued
+// again. Converges to the same least fixpoint as the two-phase form in about
+// half the rounds (a node's final push carries its final word; contributions
+// of a pred survive only while it stays tight, since a strictly shorter path
+// resets the word).
+template <bool MODS>
+__device__ __forceinline__ void queue_spf_packed(
+    uint32_t N, uint32_t s, const uint64_t* __restrict__ edges,
+    const uint32_t* __restrict__ gRow, uint32_t e0,
+    const uint8_t* __restrict__ nflags, bool hop, uint64_t* dn, uint32_t* stamp,
+    uint16_t* q0, uint16_t* q1, uint32_t* qcnt, uint32_t* ninfo, uint64_t* tp,
+    const DeadEdges& dead) {
+  constexpr uint32_t kInf = 0xFFFFFFFFu;
+  constexpr uint32_t kDrained = 0x80000000u;
+  const int tid = threadIdx.x;
+  for (uint32_t v = tid; v < N; v += kBlock) {
+    dn[v] = (v == s) ? 0ull : uint64_t(kInf);
+    stamp[v] = 0u;
+  }
+  for (uint32_t v = tid; v <= N; v += kBlock) {
+    ninfo[v] = (gRow[v] - e0) |
+        ((v < N && (nflags[v] & OGS_NODE_OVERLOADED)) ? kDrained : 0u);
+  }
+  if (tid == 0) {
+    q1[0] = uint16_t(s);
+    qcnt[0] = 0u;
+    qcnt[1] = 1u;
+    qcnt[2] = 0u;
+  }
+  __syncthreads();
+#ifdef OGS_STAMPS
+  tp[0] = __builtin_amdgcn_s_memtime();
+#endif
+  uint32_t r = 1, n = 1;
+  for (; n; ++r) {
+    if (tid == 0) qcnt[(r + 2) % 3] = 0u;
+    const uint16_t* cur = (r & 1) ? q1 : q0;
+    uint16_t* nxt = (r & 1) ? q0 : q1;
+    for (uint32_t i = tid; i < n; i += kBlock) {
+      const uint32_t v = cur[i];
+      const uint32_t iv = ninfo[v], b = iv & ~kDrained;
+      if (v != s && (iv & kDrained)) continue;  // LinkState.cpp:741-752
+      const uint64_t xv = dn[v];
+      const uint32_t dv = static_cast<uint32_t>(xv), nv = static_cast<uint32_t>(xv >> 32);
+      for_row(edges, b, (ninfo[v + 1] & ~kDrained) - b, [&](uint32_t e, uint64_t x) {
+        const uint32_t lo = static_cast<uint32_t>(x);
+        if (lo & OGS_EDGE_DOWN) return;
+        if constexpr (MODS) {
+          if (dead.has(e)) return;
+        }
+        const uint32_t t = edge_dst(lo);
+        const uint32_t c = dv + (hop ? 1u : static_cast<uint32_t>(x >> 32));
+        // the source contributes the link slot (its row index), others NH(v)
+        const uint32_t bits = (v == s) ? (1u << (e - b)) : nv;
+        uint64_t old = dn[t];
+        for (;;) {
+          const uint32_t dt = static_cast<uint32_t>(old), nt = static_cast<uint32_t>(old >> 32);
+          if (c > dt || (c == dt && !(bits & ~nt))) return;
+          const uint64_t nw = c < dt ? (uint64_t(c) | (uint64_t(bits) << 32))
+                                     : (uint64_t(dt) | (uint64_t(nt | bits) << 32));
+          const uint64_t seen = atomicCAS(reinterpret_cast<unsigned long long*>(&dn[t]),
+                                          static_cast<unsigned long long>(old),
+                                          static_cast<unsigned long long>(nw));
+          if (seen == old) break;
+          old = seen;
+        }
+        if (atomicMax(&stamp[t], r + 1) < r + 1) {
+          nxt[atomicAdd(&qcnt[(r + 1) % 3], 1u)] = uint16_t(t);
+        }
+      });
+    }
+    __syncthreads();
+    n = qcnt[(r + 1) % 3];
+  }
+#ifdef OGS_STAMPS
+  tp[1] = tp[2] = __builtin_amdgcn_s_memtime();
+  tp[3] = r;
+  tp[4] = 0;
+#endif
+}
+
 uint32_t frontier_lds_bytes(uint32_t Sn, int W, bool queue = false) {
   const uint32_t core = 4u * (((Sn + 3u) & ~3u) + ((Sn * W + 3u) & ~3u));
   if (!queue) return core + 2u * ((Sn + 1u) & ~1u);
@@ -425,7 +509,7 @@ uint32_t frontier_lds_bytes(uint32_t Sn, int W, bool queue = false) {
 // ROUTES = true: SPF + the unit's RouteDb stream (route_stream.h) from LDS;
 // dist / nh go to HBM only when requested.
 template <int W, bool ROUTES, bool MODS = false, bool DIFF = false,
-          bool QUEUE = false>
+          int QMODE = 0>
 __global__ __launch_bounds__(kBlock) void spf_frontier_kernel(
     ogs_graph g, ogs_prefix_table pt, const uint32_t* __restrict__ key,
     const uint64_t* __restrict__ chunks, const uint32_t* __restrict__ nChunk,
@@ -467,7 +551,14 @@ __global__ __launch_bounds__(kBlock) void spf_frontier_kernel(
   const uint64_t t0 = __builtin_amdgcn_s_memtime();
   const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
 #endif
-  if constexpr (QUEUE) {
+  constexpr bool PACKED = QMODE == 2;
+  static_assert(!PACKED || W == 1, "packed words hold one next-hop word");
+  uint64_t* dn64 = reinterpret_cast<uint64_t*>(smem);  // PACKED: over dist + nh
+  if constexpr (PACKED) {
+    queue_spf_packed<MODS>(N, s, g.edges + e0, gRow, e0, nflags,
+                           (flags & OGS_F_HOP_METRIC) != 0, dn64, stamp32, q0, q1,
+                           qcnt, ninfo, tp, dead);
+  } else if constexpr (QMODE == 1) {
     queue_spf<W, MODS>(N, s, g.edges + e0, gRow, e0, nflags,
                        (flags & OGS_F_HOP_METRIC) != 0, dist, nh, stamp32, q0, q1,
                        qcnt, ninfo, tp, dead);
@@ -477,11 +568,19 @@ __global__ __launch_bounds__(kBlock) void spf_frontier_kernel(
                           e0, dist, nh, stamp, tp, dead);
   }
 
+  auto dOf = [&](uint32_t v) -> uint32_t {
+    if constexpr (PACKED) return static_cast<uint32_t>(dn64[v]);
+    else return dist[v];
+  };
+  auto nOf = [&](uint32_t v, int w) -> uint32_t {
+    if constexpr (PACKED) return static_cast<uint32_t>(dn64[v] >> 32);
+    else return nh[v * W + w];
+  };
   for (uint32_t v = tid; v < N; v += kBlock) {
-    if (oDist) oDist[size_t(u0) * Sn + v] = dist[v];
+    if (oDist) oDist[size_t(u0) * Sn + v] = dOf(v);
 #pragma unroll
     for (int w = 0; w < W; ++w) {
-      if (oNh) oNh[(size_t(u0) * W + w) * Sn + v] = nh[v * W + w];
+      if (oNh) oNh[(size_t(u0) * W + w) * Sn + v] = nOf(v, w);
     }
   }
   if constexpr (ROUTES) {
@@ -490,8 +589,8 @@ __global__ __launch_bounds__(kBlock) void spf_frontier_kernel(
     for (uint32_t v = tid; v < N; v += kBlock) {
       uint32_t cnt = 0;
 #pragma unroll
-      for (int w = 0; w < W; ++w) cnt += __popc(nh[v * W + w]);
-      rMeta[v] = uint16_t(node_route_meta(v, s, dist[v] != kInf, cnt, nflags[v]));
+      for (int w = 0; w < W; ++w) cnt += __popc(nOf(v, w));
+      rMeta[v] = uint16_t(node_route_meta(v, s, dOf(v) != kInf, cnt, nflags[v]));
     }
     __syncthreads();
     const uint32_t Sp = uint32_t(pt.max_prefixes);
@@ -500,7 +599,6 @@ __global__ __launch_bounds__(kBlock) void spf_frontier_kernel(
     const RouteCfg cfg{(flags & OGS_F_ENABLE_V4) != 0,
                        (flags & OGS_F_V4_OVER_V6) != 0,
                        (flags & OGS_F_BEST_ROUTE_SELECTION) != 0};
-    const SplitView<uint32_t, W> sv{dist, nh};
     __shared__ uint32_t cnt[2];
     if constexpr (DIFF) {
       if (tid < 2) cnt[tid] = 0u;
@@ -508,13 +606,20 @@ __global__ __launch_bounds__(kBlock) void spf_frontier_kernel(
     }
     const DiffCtx dc{diff.base_meta, diff.base_metric, diff.base_mask,
                      diff.changed + size_t(u0) * ((Sp + 31u) / 32u), cnt};
-    stream_routes<W, DIFF>(pt, key + size_t(unit.topo) * Sp, p0, P, Sp, u0, s,
-                           nflags, sv, cfg, out, [&](uint32_t v, Rec<W>& r) {
-                             r.meta = rMeta[v];
-                             r.metric = (v == s) ? kInf : dist[v];
+    auto rec = [&](uint32_t v, Rec<W>& r) {
+      r.meta = rMeta[v];
+      r.metric = (v == s) ? kInf : dOf(v);
 #pragma unroll
-                             for (int w = 0; w < W; ++w) r.mask[w] = nh[v * W + w];
-                           }, &dc);
+      for (int w = 0; w < W; ++w) r.mask[w] = nOf(v, w);
+    };
+    if constexpr (PACKED) {
+      stream_routes<W, DIFF>(pt, key + size_t(unit.topo) * Sp, p0, P, Sp, u0, s,
+                             nflags, PackedView{dn64}, cfg, out, rec, &dc);
+    } else {
+      stream_routes<W, DIFF>(pt, key + size_t(unit.topo) * Sp, p0, P, Sp, u0, s,
+                             nflags, SplitView<uint32_t, W>{dist, nh}, cfg, out, rec,
+                             &dc);
+    }
     if constexpr (DIFF) {
       __syncthreads();
       if (tid < 2) diff.counts[size_t(u0) * 2 + tid] = cnt[tid];
@@ -537,16 +642,20 @@ __global__ __launch_bounds__(kBlock) void spf_frontier_kernel(
 }
 
 // "spf_queue" option: -1 (default) the queue form for sparse topologies
-// (max degree <= 16, <= 65,535 nodes), 0 never, 1 whenever it fits.
+// (max degree <= 16, <= 65,535 nodes; one-phase packed words when the
+// next-hop sets fit one word), 0 never, 1 whenever it fits, 2 the two-phase
+// queue form even for one-word sets (A/B).
 int g_spfQueue = -1;
 
-bool use_queue(const ogs_graph& g, int W) {
-  if (g_spfQueue == 0 || g.max_nodes > 65535) return false;
-  if (frontier_lds_bytes(uint32_t(g.max_nodes), W, true) > 160u * 1024u) return false;
-  return g_spfQueue == 1 || g.max_degree <= 16;
+// 0 chunk scan, 1 two-phase queue, 2 packed one-phase queue
+int queue_mode(const ogs_graph& g, int W) {
+  if (g_spfQueue == 0 || g.max_nodes > 65535) return 0;
+  if (frontier_lds_bytes(uint32_t(g.max_nodes), W, true) > 160u * 1024u) return 0;
+  if (g_spfQueue == -1 && g.max_degree > 16) return 0;
+  return (W == 1 && g_spfQueue != 2) ? 2 : 1;
 }
 
-template <int W, bool ROUTES, bool MODS, bool DIFF, bool QUEUE>
+template <int W, bool ROUTES, bool MODS, bool DIFF, int QMODE>
 hipError_t launch_frontier_q(const ogs_graph& g, const ogs_prefix_table& pt,
                              const uint32_t* key, const uint64_t* chunks,
                              const uint32_t* nChunk, const ogs_unit* units,
@@ -554,8 +663,8 @@ hipError_t launch_frontier_q(const ogs_graph& g, const ogs_prefix_table& pt,
                              uint32_t* nh, const ogs_spf_out& out,
                              hipStream_t stream, const ogs_unit_mods& mods,
                              const ogs_route_diff& diff) {
-  const uint32_t lds = frontier_lds_bytes(uint32_t(g.max_nodes), W, QUEUE);
-  auto k = spf_frontier_kernel<W, ROUTES, MODS, DIFF, QUEUE>;
+  const uint32_t lds = frontier_lds_bytes(uint32_t(g.max_nodes), W, QMODE != 0);
+  auto k = spf_frontier_kernel<W, ROUTES, MODS, DIFF, QMODE>;
   if (lds > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
                                        hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -576,12 +685,20 @@ hipError_t launch_frontier(const ogs_graph& g, const ogs_prefix_table& pt,
                            uint32_t* nh, const ogs_spf_out& out,
                            hipStream_t stream, const ogs_unit_mods& mods = {},
                            const ogs_route_diff& diff = {}) {
-  if (use_queue(g, W)) {
-    return launch_frontier_q<W, ROUTES, MODS, DIFF, true>(
+  const int qm = queue_mode(g, W);
+  if constexpr (W == 1) {
+    if (qm == 2) {
+      return launch_frontier_q<W, ROUTES, MODS, DIFF, 2>(
+          g, pt, key, chunks, nChunk, units, nUnits, flags, dist, nh, out, stream,
+          mods, diff);
+    }
+  }
+  if (qm != 0) {
+    return launch_frontier_q<W, ROUTES, MODS, DIFF, 1>(
         g, pt, key, chunks, nChunk, units, nUnits, flags, dist, nh, out, stream,
         mods, diff);
   }
-  return launch_frontier_q<W, ROUTES, MODS, DIFF, false>(
+  return launch_frontier_q<W, ROUTES, MODS, DIFF, 0>(
       g, pt, key, chunks, nChunk, units, nUnits, flags, dist, nh, out, stream,
       mods, diff);
 }
