@@ -526,8 +526,12 @@ __global__ __launch_bounds__(64 * UPB) void spf_route_wave_kernel(
   for (int k = 0; k < NPL; ++k) {
     const uint32_t v = vk[k];
     if (v >= N) continue;
-    if (out.dist) static_cast<uint32_t*>(out.dist)[size_t(uidx) * Sn + v] = dcur[k];
-    if (out.nh) out.nh[size_t(uidx) * Sn + v] = ncur[k];
+    // streaming (non-temporal) stores: outputs are not re-read by the
+    // kernel, keep them out of the way of the inputs in L2
+    if (out.dist) {
+      __builtin_nontemporal_store(dcur[k], static_cast<uint32_t*>(out.dist) + size_t(uidx) * Sn + v);
+    }
+    if (out.nh) __builtin_nontemporal_store(ncur[k], out.nh + size_t(uidx) * Sn + v);
   }
   if (!hasPrefixes) return;
 
@@ -563,10 +567,10 @@ __global__ __launch_bounds__(64 * UPB) void spf_route_wave_kernel(
       mask = mk[0];
     }
     const size_t o = size_t(uidx) * Sp + p;
-    if (out.meta) out.meta[o] = meta;
-    if (out.metric) static_cast<uint32_t*>(out.metric)[o] = metric;
-    if (out.sel) out.sel[o] = selBits;
-    if (out.mask) out.mask[o] = mask;
+    if (out.meta) __builtin_nontemporal_store(meta, out.meta + o);
+    if (out.metric) __builtin_nontemporal_store(metric, static_cast<uint32_t*>(out.metric) + o);
+    if (out.sel) __builtin_nontemporal_store(selBits, out.sel + o);
+    if (out.mask) __builtin_nontemporal_store(mask, out.mask + o);
   }
 #ifdef OGS_STAMPS
   wave_sync();
