@@ -321,6 +321,11 @@ def run_c4(args, torch, dist, rank, world, local_rank):
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": None, "bytes_alg_per_unit": round(bpu, 1)},
     }
+    # PMC HBM bytes of the variant launch (10k units; committed passes)
+    traffic, src = pmc_traffic("c4", "spf_frontier_kernel<1, true, true, true")
+    if traffic is not None and world == 1:
+        line["roofline"]["traffic"] = round(traffic, 1)
+        line["roofline"]["traffic_source"] = src
     if world == 1 and not args.no_cpu_baseline:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import _refcpu
@@ -433,6 +438,11 @@ def run_c5(args, torch, dist, rank, world, local_rank):
                      "traffic": None, "bytes_alg_per_unit": round(bpu, 1),
                      "kernel": "ksp_base_kernel + ksp2_kernel (per-area launches)"},
     }
+    # PMC HBM bytes per launch of both KSP kernels x the job's per-area batches
+    traffic, src = pmc_traffic("c5", "ksp")
+    if traffic is not None and world == 1:
+        line["roofline"]["traffic"] = round(traffic * sh["ksp_batches"], 1)
+        line["roofline"]["traffic_source"] = src
     if world == 1 and not args.no_cpu_baseline:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import _refcpu

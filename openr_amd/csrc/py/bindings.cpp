@@ -983,6 +983,7 @@ class C5Runner {
     d["prefixes"] = ps_.prefixes().size();
     d["advertisements"] = adv;
     d["ksp_units"] = units;
+    d["ksp_batches"] = batches_.size();
     d["total_dests"] = totalDests_;
     d["path_edges_k1"] = pe1;
     d["path_edges_k2"] = pe2;
