@@ -436,7 +436,7 @@ def run_c5(args, torch, dist, rank, world, local_rank):
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                      "traffic": None, "bytes_alg_per_unit": round(bpu, 1),
-                     "kernel": "ksp_base_kernel + ksp2_kernel (per-area launches)"},
+                     "kernel": "ksp_base_kernel + ksp2_kernel (one launch pair over the source's areas)"},
     }
     # PMC HBM bytes per launch of both KSP kernels x the job's per-area batches
     traffic, src = pmc_traffic("c5", "ksp")

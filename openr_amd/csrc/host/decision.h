@@ -392,10 +392,16 @@ class Ksp2Batch {
  public:
   Ksp2Batch(const LinkState& ls, const std::string& src,
             const std::vector<std::string>& dests);
+  // several topologies (e.g. the areas of a multi-area source) in ONE pair
+  // of launches: destinations[i] is searched in areas[i]
+  Ksp2Batch(const std::vector<const LinkState*>& areas, const std::string& src,
+            const std::vector<std::vector<std::string>>& destinations);
   void launch(void* stream = nullptr) const;  // asynchronous
   void fetch();                               // D2H of both path sets (sync)
   size_t size() const { return dests_.size(); }
   const std::vector<std::string>& dests() const { return dests_; }
+  // topology index (position in `areas`) of destination i
+  size_t areaOf(size_t i) const { return destArea_.at(i); }
   // unit i's k-th (1 or 2) paths as topology-local directed edge ids
   std::vector<std::vector<uint32_t>> edgePaths(size_t i, int k) const;
   std::vector<LinkState::Path> paths(size_t i, int k) const;
@@ -403,13 +409,17 @@ class Ksp2Batch {
   uint64_t totalPathEdges(int k) const;
 
  private:
-  const LinkState& ls_;
+  void init(const std::string& src,
+            const std::vector<std::vector<std::string>>& destinations);
+  std::vector<const LinkState*> ls_;
   std::vector<std::string> dests_;
+  std::vector<size_t> destArea_;
   std::vector<int64_t> unitOf_;  // dest index -> unit (-1: unknown dest)
-  size_t nUnits_{0};
+  size_t nUnits_{0}, nSources_{0};
   uint32_t flags_{0}, maxPaths_{0}, maxEdges_{0};
   ogs_graph g_{};
-  DeviceBuffer dSrc_, dUnits_, dCount_[2], dLen_[2], dEdges_[2];
+  DeviceBuffer dNodeBase_, dRow_, dEdges_, dFlags_;  // multi-topology batch
+  DeviceBuffer dSrc_, dUnits_, dCount_[2], dLen_[2], dEdges2_[2];
   std::vector<uint32_t> count_[2], len_[2], edges_[2];
 };
 

@@ -101,45 +101,107 @@ const std::vector<LinkState::Path>& LinkState::getKthPaths(
 // ---- Ksp2Batch ----------------------------------------------------------
 Ksp2Batch::Ksp2Batch(const LinkState& ls, const std::string& src,
                      const std::vector<std::string>& dests)
-    : ls_(ls), dests_(dests), unitOf_(dests.size(), -1) {
-  const FlatTopology& f = ls.flatOnDevice();
-  auto sIt = f.id.find(src);
-  if (sIt == f.id.end()) return;  // unknown source: no paths anywhere
-  if (f.hasZeroMetric || f.hasWideMetric) {
-    throw std::domain_error(
-        "Ksp2Batch: zero or negative link metric is outside the GPU engine's "
-        "exact domain");
+    : ls_{&ls} {
+  init(src, {dests});
+}
+
+Ksp2Batch::Ksp2Batch(const std::vector<const LinkState*>& areas,
+                     const std::string& src,
+                     const std::vector<std::vector<std::string>>& destinations)
+    : ls_(areas) {
+  if (areas.size() != destinations.size()) {
+    throw std::invalid_argument("Ksp2Batch: one destination list per topology");
+  }
+  init(src, destinations);
+}
+
+void Ksp2Batch::init(const std::string& src,
+                     const std::vector<std::vector<std::string>>& destinations) {
+  const size_t T = ls_.size();
+  std::vector<const FlatTopology*> fl(T);
+  for (size_t a = 0; a < T; ++a) {
+    fl[a] = T == 1 ? &ls_[a]->flatOnDevice() : &ls_[a]->flat();
+    for (const auto& d : destinations[a]) {
+      dests_.push_back(d);
+      destArea_.push_back(a);
+    }
+  }
+  unitOf_.assign(dests_.size(), -1);
+  std::vector<ogs_unit> sources;
+  std::vector<int64_t> srcOf(T, -1);
+  for (size_t a = 0; a < T; ++a) {
+    auto it = fl[a]->id.find(src);
+    if (it == fl[a]->id.end()) continue;  // no source there: no paths there
+    if (fl[a]->hasZeroMetric || fl[a]->hasWideMetric) {
+      throw std::domain_error(
+          "Ksp2Batch: zero or negative link metric is outside the GPU engine's "
+          "exact domain");
+    }
+    srcOf[a] = int64_t(sources.size());
+    sources.push_back(ogs_unit{uint32_t(a), it->second});
   }
   std::vector<ogs_path_unit> units;
-  for (size_t i = 0; i < dests.size(); ++i) {
-    auto dIt = f.id.find(dests[i]);
-    if (dIt == f.id.end()) continue;
+  for (size_t i = 0; i < dests_.size(); ++i) {
+    const size_t a = destArea_[i];
+    if (srcOf[a] < 0) continue;
+    auto dIt = fl[a]->id.find(dests_[i]);
+    if (dIt == fl[a]->id.end()) continue;
     unitOf_[i] = int64_t(units.size());
-    units.push_back(ogs_path_unit{0, sIt->second, dIt->second, 0});
+    units.push_back(ogs_path_unit{uint32_t(a), sources[srcOf[a]].src, dIt->second,
+                                  uint32_t(srcOf[a])});
   }
   nUnits_ = units.size();
+  nSources_ = sources.size();
   if (!nUnits_) return;
-  const uint32_t E = uint32_t(f.edges.size());
+  uint32_t maxN = 0, maxE = 0;
+  int maxDeg = 0;
+  for (const auto* f : fl) {
+    maxN = std::max<uint32_t>(maxN, uint32_t(f->names.size()));
+    maxE = std::max<uint32_t>(maxE, uint32_t(f->edges.size()));
+    maxDeg = std::max(maxDeg, f->maxDegree);
+    if (wideDistancesNeeded(*f)) flags_ = OGS_F_WIDE_METRIC;
+  }
   // edge-disjoint paths into d: at most deg(d) of them, at most E/2 links
-  maxPaths_ = uint32_t(f.maxDegree) + 1;
-  maxEdges_ = E / 2 + 1;
-  flags_ = wideDistancesNeeded(f) ? OGS_F_WIDE_METRIC : 0u;
-  const ogs_unit s{0, sIt->second};
-  dSrc_.upload(&s, 1);
+  maxPaths_ = uint32_t(maxDeg) + 1;
+  maxEdges_ = maxE / 2 + 1;
+  dSrc_.upload(sources.data(), sources.size());
   dUnits_.upload(units.data(), units.size());
   for (int k = 0; k < 2; ++k) {
     dCount_[k].resize(nUnits_ * 4);
     dLen_[k].resize(nUnits_ * maxPaths_ * 4);
-    dEdges_[k].resize(nUnits_ * maxEdges_ * 4);
+    dEdges2_[k].resize(nUnits_ * maxEdges_ * 4);
   }
-  g_.num_topos = 1;
-  g_.max_nodes = int32_t(f.names.size());
-  g_.max_edges = int32_t(E);
-  g_.max_degree = f.maxDegree;
-  g_.node_base = f.dNodeBase.as<uint32_t>();
-  g_.row_ptr = f.dRow.as<uint32_t>();
-  g_.edges = f.dEdges.as<uint64_t>();
-  g_.node_flags = f.dFlags.as<uint8_t>();
+  g_.num_topos = int32_t(T);
+  g_.max_nodes = int32_t(maxN);
+  g_.max_edges = int32_t(maxE);
+  g_.max_degree = maxDeg;
+  if (T == 1) {  // the LinkState's own device CSR
+    g_.node_base = fl[0]->dNodeBase.as<uint32_t>();
+    g_.row_ptr = fl[0]->dRow.as<uint32_t>();
+    g_.edges = fl[0]->dEdges.as<uint64_t>();
+    g_.node_flags = fl[0]->dFlags.as<uint8_t>();
+    return;
+  }
+  // concatenated batch: global row offsets, topology-local edge targets
+  std::vector<uint32_t> nodeBase{0}, row;
+  std::vector<uint64_t> edges;
+  std::vector<uint8_t> flags;
+  for (const auto* f : fl) {
+    const uint32_t eb = uint32_t(edges.size());
+    for (size_t v = 0; v + 1 < f->rowPtr.size(); ++v) row.push_back(eb + f->rowPtr[v]);
+    edges.insert(edges.end(), f->edges.begin(), f->edges.end());
+    flags.insert(flags.end(), f->nodeFlags.begin(), f->nodeFlags.end());
+    nodeBase.push_back(nodeBase.back() + uint32_t(f->names.size()));
+  }
+  row.push_back(uint32_t(edges.size()));
+  dNodeBase_.upload(nodeBase.data(), nodeBase.size());
+  dRow_.upload(row.data(), row.size());
+  dEdges_.upload(edges.data(), edges.size());
+  dFlags_.upload(flags.data(), flags.size());
+  g_.node_base = dNodeBase_.as<uint32_t>();
+  g_.row_ptr = dRow_.as<uint32_t>();
+  g_.edges = dEdges_.as<uint64_t>();
+  g_.node_flags = dFlags_.as<uint8_t>();
 }
 
 void Ksp2Batch::launch(void* stream) const {
@@ -148,10 +210,11 @@ void Ksp2Batch::launch(void* stream) const {
   for (int k = 0; k < 2; ++k) {
     o[k] = ogs_path_out{const_cast<DeviceBuffer&>(dCount_[k]).as<uint32_t>(),
                         const_cast<DeviceBuffer&>(dLen_[k]).as<uint32_t>(),
-                        const_cast<DeviceBuffer&>(dEdges_[k]).as<uint32_t>(),
+                        const_cast<DeviceBuffer&>(dEdges2_[k]).as<uint32_t>(),
                         maxPaths_, maxEdges_};
   }
-  ogsCheck(ogs_ksp2_paths(&g_, const_cast<DeviceBuffer&>(dSrc_).as<ogs_unit>(), 1,
+  ogsCheck(ogs_ksp2_paths(&g_, const_cast<DeviceBuffer&>(dSrc_).as<ogs_unit>(),
+                          int32_t(nSources_),
                           const_cast<DeviceBuffer&>(dUnits_).as<ogs_path_unit>(),
                           int32_t(nUnits_), flags_, &o[0], &o[1], stream),
            "ogs_ksp2_paths");
@@ -165,7 +228,7 @@ void Ksp2Batch::fetch() {
     edges_[k].resize(nUnits_ * maxEdges_);
     dCount_[k].download(count_[k].data(), nUnits_);
     dLen_[k].download(len_[k].data(), len_[k].size());
-    dEdges_[k].download(edges_[k].data(), edges_[k].size());
+    dEdges2_[k].download(edges_[k].data(), edges_[k].size());
   }
   ogsCheck(ogs_stream_sync(nullptr), "ogs_stream_sync");
   for (int k = 0; k < 2; ++k) {
@@ -192,11 +255,12 @@ std::vector<std::vector<uint32_t>> Ksp2Batch::edgePaths(size_t i, int k) const {
 }
 
 std::vector<LinkState::Path> Ksp2Batch::paths(size_t i, int k) const {
-  const FlatTopology& f = ls_.flat();
+  const LinkState& ls = *ls_.at(destArea_.at(i));
+  const FlatTopology& f = ls.flat();
   std::vector<LinkState::Path> out;
   for (const auto& ep : edgePaths(i, k)) {
     LinkState::Path p;
-    for (uint32_t e : ep) p.push_back(ls_.linkByKey(f.edgeLink[e]->key()));
+    for (uint32_t e : ep) p.push_back(ls.linkByKey(f.edgeLink[e]->key()));
     out.push_back(std::move(p));
   }
   return out;

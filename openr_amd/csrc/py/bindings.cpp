@@ -869,15 +869,20 @@ class C5Runner {
     }
     totalDests_ = all.size();
     const size_t lo = all.size() * rank / world, hi = all.size() * (rank + 1) / world;
+    // every area's destinations in ONE Ksp2Batch (one pair of launches)
+    std::vector<const LinkState*> lss;
+    std::vector<std::vector<std::string>> dests;
     for (const auto& [area, ls] : als_) {
-      std::vector<std::string> dests;
+      std::vector<std::string> d;
       for (size_t i = lo; i < hi; ++i) {
-        if (all[i].first == area) dests.push_back(all[i].second);
+        if (all[i].first == area) d.push_back(all[i].second);
       }
-      if (dests.empty()) continue;
+      if (d.empty()) continue;
       areas_.push_back(area);
-      batches_.push_back(std::make_unique<Ksp2Batch>(ls, source, dests));
+      lss.push_back(&ls);
+      dests.push_back(std::move(d));
     }
+    if (!lss.empty()) batches_.push_back(std::make_unique<Ksp2Batch>(lss, source, dests));
   }
 
   void setPolicy(py::list policy) {
@@ -921,11 +926,11 @@ class C5Runner {
   // "area dest k:" + the paths, one line per (destination, k), batch order
   std::vector<std::string> kspText() const {
     std::vector<std::string> out;
-    for (size_t b = 0; b < batches_.size(); ++b) {
-      for (size_t i = 0; i < batches_[b]->size(); ++i) {
+    for (const auto& b : batches_) {
+      for (size_t i = 0; i < b->size(); ++i) {
         for (int k = 1; k <= 2; ++k) {
-          out.push_back(areas_[b] + " " + batches_[b]->dests()[i] + " " +
-                        std::to_string(k) + ":" + pathsText(batches_[b]->paths(i, k)));
+          out.push_back(areas_[b->areaOf(i)] + " " + b->dests()[i] + " " +
+                        std::to_string(k) + ":" + pathsText(b->paths(i, k)));
         }
       }
     }
@@ -933,8 +938,10 @@ class C5Runner {
   }
   std::vector<std::pair<std::string, std::string>> kspDests() const {
     std::vector<std::pair<std::string, std::string>> out;
-    for (size_t b = 0; b < batches_.size(); ++b) {
-      for (const auto& d : batches_[b]->dests()) out.emplace_back(areas_[b], d);
+    for (const auto& b : batches_) {
+      for (size_t i = 0; i < b->size(); ++i) {
+        out.emplace_back(areas_[b->areaOf(i)], b->dests()[i]);
+      }
     }
     return out;
   }
@@ -983,7 +990,7 @@ class C5Runner {
     d["prefixes"] = ps_.prefixes().size();
     d["advertisements"] = adv;
     d["ksp_units"] = units;
-    d["ksp_batches"] = batches_.size();
+    d["ksp_batches"] = batches_.size();  // launch pairs per job
     d["total_dests"] = totalDests_;
     d["path_edges_k1"] = pe1;
     d["path_edges_k2"] = pe2;
