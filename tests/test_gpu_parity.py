@@ -522,3 +522,47 @@ def test_c5_runner_sharded(product):
     assert parts[0].ksp_text() + parts[1].ksp_text() == full.ksp_text()
     routes = [p.routes().decode() for p in parts]
     assert routes[0] + routes[1] == full.routes().decode()
+
+
+# ---- edge cases: sizes at kernel boundaries, empty / degenerate inputs ------
+
+@pytest.mark.parametrize("n", [1, 2, 8, 9, 16, 17])
+def test_grid_sizes_at_kernel_boundaries(product, oracle, n):
+    """Grids of 1, 4, 64, 81, 256 and 289 nodes: single node (no links),
+    exactly one / two / four 64-lane slots of the wave kernel and the first
+    sizes past them (workgroup kernels), every node a source."""
+    opts = dict(n=n, metricSeed=0xB0 + n, prefixSeed=n, adjOverloadPermille=30,
+                nodeOverloadPermille=20, overloadSeed=n)
+    srcs = [str(i) for i in range(0, n * n, max(1, (n * n) // 9))]
+    for brs in (False, True):
+        _cmp(product.gen_route_dbs("grid", opts, srcs, True, True, brs),
+             oracle.gen_route_dbs("grid", opts, srcs, True, True, brs), f"grid{n}")
+
+
+def test_long_prefix_tables(product, oracle):
+    """More prefixes per topology than the wave kernel stages in registers
+    (P > 64 * (NPL + 1)): the plain staging loop, anycast mix included."""
+    opts = dict(n=5, metricSeed=0xB7, prefixSeed=7, prefixesPerNode=40, **MIX)
+    srcs = ["0", "12", "24"]
+    _cmp(product.gen_route_dbs("grid", opts, srcs, True, False, True),
+         oracle.gen_route_dbs("grid", opts, srcs, True, False, True), "longpfx")
+
+
+def test_unknown_source_gives_no_route_db(product, oracle):
+    """buildRouteDb for a node in no area returns nullopt (SpfSolver.cpp:318-324)."""
+    opts = dict(n=4, metricSeed=1, prefixSeed=1)
+    a = product.gen_route_dbs("grid", opts, ["nope", "3"], True, False, False)
+    b = oracle.gen_route_dbs("grid", opts, ["nope", "3"], True, False, False)
+    assert a[0] == b[0] == b"NONE"
+    _cmp(a, b, "unknown")
+
+
+def test_empty_batch_is_a_no_op(product):
+    """n_units = 0 returns OGS_OK without touching the (NULL) buffers."""
+    import ctypes
+    import openr_amd.capi as capi
+    lib = capi.load()
+    g = capi.Graph(1, 4, 8, 2, None, None, None, None, None)
+    out = capi.SpfOut(None, None, None, None, None, None)
+    assert lib.ogs_spf_routes(ctypes.byref(g), None, None, 0, 0, 1, ctypes.byref(out),
+                              None) == 0
