@@ -27,6 +27,7 @@ sys.path.insert(0, ROOT)
 # torch first: its HIP runtime must be the one libopenr_gpu.so binds to (one
 # HIP runtime per process); openr_amd's import loads the engine library
 import torch  # noqa: E402,F401
+import numpy as np  # noqa: E402
 
 from openr_amd import shard  # noqa: E402
 
@@ -126,6 +127,13 @@ def c3_launches(torch, M, capi, dev, rank, world, ppn, with_sel=False):
     return launches, N
 
 
+def hash_list(xs):
+    """63-bit hash of an int list (C4 changed-prefix lists inside the digest)."""
+    import hashlib
+    return int.from_bytes(hashlib.sha256(repr(list(xs)).encode()).digest()[:8],
+                          "little") >> 1
+
+
 def pmc_traffic(tag, match):
     """HBM bytes per launch of the kernels whose name contains `match`, from
     the newest committed PMC summary profiles/r*_pmc_<tag>.json
@@ -204,8 +212,10 @@ def run_c3(args, torch, dist, rank, world, local_rank):
     units = sum(L["U"] for L in launches)
     nbytes = sum(L["bytes"] for L in launches)
     routes = sum(int(((L["o"]["meta"] & 1) != 0).sum().item()) for L in launches)
+    # keyed by source name: the same job digest at any rank count
     digest = shard.combine_digests(
-        shard.route_digest(L["o"]["meta"].cpu().numpy(), L["o"]["metric"].cpu().numpy())
+        shard.unit_digest(L["names"], L["o"]["meta"].cpu().numpy(),
+                          L["o"]["metric"].cpu().numpy())
         for L in launches)
     total_units, total_routes, job_digest, tmax, _ = shard.reduce_stats(
         dist, torch, dev, units, routes, digest, wall)
@@ -291,8 +301,21 @@ def run_c4(args, torch, dist, rank, world, local_rank):
     U = vr.num_variants()
     changed = sum(len(vr.changed(v)) for v in range(U))
     counts = [vr.counts(v) for v in range(U)]
-    digest = shard.route_digest(
-        bytearray(repr(counts).encode()))
+    # keyed by global variant index: the same job digest at any rank count
+    digest = shard.unit_digest(
+        list(range(lo, lo + U)),
+        np.array([[c[0], c[1], hash_list(vr.changed(v))]
+                  for v, c in enumerate(counts)], dtype="int64"))
+    # §8(f) f1, outside the timed region: the DecisionRouteUpdate of every
+    # variant from the device-gathered changed records (ogs_route_changes_gather
+    # + D2H of those records), then host materialisation of all of them
+    t1 = time.perf_counter()
+    vr.fetch_updates(sptr)
+    fetch_ms = (time.perf_counter() - t1) * 1e3
+    t1 = time.perf_counter()
+    n_changes = vr.materialize_all()
+    mat_ms = (time.perf_counter() - t1) * 1e3
+    assert n_changes == changed == vr.total_changes()
     total_units, total_changed, job_digest, tmax, _ = shard.reduce_stats(
         dist, torch, dev, U, changed, digest, wall)
     if rank != 0:
@@ -316,6 +339,12 @@ def run_c4(args, torch, dist, rank, world, local_rank):
                    "variants": C4_VARIANTS,
                    "parallelism": f"shard-by-variant x{world}"},
         "changed_routes_per_step": total_changed, "route_digest": f"{job_digest:016x}",
+        "route_update": {
+            "changes": n_changes, "gather_fetch_ms": round(fetch_ms, 3),
+            "materialize_ms": round(mat_ms, 3),
+            "note": "rank 0, after the timed region: counts D2H + scan + "
+                    "ogs_route_changes_gather + D2H of the changed records, then host "
+                    "DecisionRouteUpdate materialisation of every variant"},
         "gteps": round(E * value / 1e9, 3), "kernel_ms": round(kernel_ms, 4),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
@@ -489,11 +518,21 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # OGS_BENCH_SHARE_DEVICE=1: rehearsal of the N>1 path on a box with fewer
+    # GPUs than ranks (ranks share devices round-robin; gloo carries the
+    # per-rank records since RCCL refuses two ranks on one GPU). Never set by
+    # the driver; the numbers of such a run are not scaling numbers.
+    share = os.environ.get("OGS_BENCH_SHARE_DEVICE") == "1"
+    if share:
+        local_rank %= torch.cuda.device_count()
     torch.cuda.set_device(local_rank)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if share:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 
     import openr_amd
     import openr_amd.capi as capi
@@ -600,7 +639,8 @@ def main():
     # ---- per-rank digest (result sanity) + cross-rank reduction -----------
     meta = o_meta.cpu().numpy()
     n_routes = int(((meta & 1) != 0).sum())
-    digest = shard.route_digest(meta, o_metric.cpu().numpy(), o_mask.cpu().numpy())
+    digest = shard.unit_digest(list(range(lo, hi)), meta, o_metric.cpu().numpy(),
+                               o_mask.cpu().numpy())
     total_units, total_routes, job_digest, tmax, _ = shard.reduce_stats(
         dist, torch, dev, U, n_routes, digest, wall)
 
@@ -665,7 +705,7 @@ def main():
         if rank == 0:
             line["c4_link_failure_sweep"] = {
                 k: c4[k] for k in ("value", "unit", "ms_per_step", "kernel_ms", "gteps",
-                                   "changed_routes_per_step", "route_digest", "roofline",
+                                   "changed_routes_per_step", "route_digest", "route_update", "roofline",
                                    "config", "steps") if k in c4}
             if "cpu_baseline" in c4:
                 line["c4_link_failure_sweep"]["cpu_baseline"] = c4["cpu_baseline"]

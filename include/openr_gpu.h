@@ -345,6 +345,32 @@ int ogs_spf_routes_variants(const ogs_graph* graph,
                             const ogs_route_diff* diff, uint32_t flags,
                             int32_t nh_words, ogs_spf_out* out, void* stream);
 
+/* Compact list of the changed routes of n_units variants (SURVEY.md §8(f)
+ * f1): what DecisionRouteDb::calculateUpdate (SpfSolver.cpp:21-56) hands
+ * Fib through Decision::rebuildRoutes (Decision.cpp:929-951), gathered from
+ * ogs_spf_routes_variants' records and changed bitmap. Unit-major, prefix
+ * index ascending within a unit. A record whose meta lacks OGS_ROUTE_VALID
+ * is a deletion (unicastRoutesToDelete), any other an update. */
+typedef struct ogs_route_changes {
+  const uint32_t* offsets; /* [n_units + 1] exclusive scan of each unit's
+                              changed count (counts[2u] + counts[2u+1]);
+                              offsets[n_units] == total                 */
+  size_t total;            /* number of records (mask stride)           */
+  uint32_t* prefix;        /* [total] prefix index in the unit's table  */
+  uint32_t* meta;          /* [total] record meta (OGS_ROUTE_*)         */
+  uint32_t* metric;        /* [total] route metric                      */
+  uint32_t* mask;          /* [nh_words * total] link-slot mask, word w
+                              of record i at mask[w * total + i]        */
+} ogs_route_changes;
+
+/* Gathers the changed records (diff->changed bitmap of the same call's
+ * units, out->meta/metric/mask records of ogs_spf_routes_variants) into
+ * `changes`. nh_words 1, 2 or 4 as for the variants call. */
+int ogs_route_changes_gather(const uint32_t* changed, int32_t n_units,
+                             int32_t max_prefixes, const ogs_spf_out* records,
+                             int32_t nh_words, const ogs_route_changes* changes,
+                             void* stream);
+
 /* RibPolicy compiled against one prefix table (SURVEY.md §8(a) a16;
  * RibPolicy.cpp:74-249): statements 0..K-1 in policy order. */
 typedef struct ogs_rib_policy {

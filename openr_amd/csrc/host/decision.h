@@ -614,11 +614,86 @@ void addNodeLabelRoutes(const LinkState& ls, const FlatTopology& f,
                         const uint64_t* dist, const uint32_t* nhWords,
                         size_t nhStride, int W, LabelRoutes& labelToNode);
 
+std::optional<RibUnicastEntry> materializeRoute(
+    const FlatTopology& f, const std::string& me, const PrefixHostTable& pt,
+    uint32_t p, uint32_t meta, uint64_t metric, const uint32_t* mask,
+    size_t maskStride, int W, bool v4OverV6Nexthop, const RibPolicy* policy,
+    uint8_t applied, uint8_t counter);
+
 DecisionRouteDb materializeRouteDb(
     const LinkState& ls, const FlatTopology& f, const std::string& area,
     const std::string& me, const UnitView& r, const PrefixHostTable& pt,
     bool v4OverV6Nexthop, bool enableNodeSegmentLabel,
     const std::map<std::string, RibUnicastEntry>& statics,
     std::map<std::string, RouteSelectionResult>* bestRoutesCache);
+
+// ------------------------------------------------------ LinkFailureSweep --
+// SURVEY.md §8(f) f1 over config C4: the route updates Decision would hand
+// Fib (Decision::rebuildRoutes incremental branch, Decision.cpp:929-951 =
+// buildRouteDb + DecisionRouteDb::calculateUpdate, SpfSolver.cpp:21-56) for
+// many what-if variants of ONE area, a variant being a set of <= 2 links taken
+// down (adjacency withdrawn at both ends, LinkState.cpp:406-659). All variants
+// run in one launch (ogs_spf_routes_variants, route diff fused in); only the
+// changed records are gathered on the device (ogs_route_changes_gather) and
+// materialised. Node-segment labels are not part of the sweep (off in the
+// DecisionBenchmark config). `ls` and `ps` must outlive the
+// sweep unchanged.
+class LinkFailureSweep {
+ public:
+  struct LinkDown {  // one end of the link: (node, its interface)
+    std::string node, ifName;
+  };
+  LinkFailureSweep(const std::string& myNodeName, const LinkState& ls,
+                   const PrefixState& ps,
+                   const std::vector<std::vector<LinkDown>>& variants,
+                   bool enableV4, bool enableBestRouteSelection = false,
+                   bool v4OverV6Nexthop = false);
+  // base RouteDb records (the diff's reference); launch() runs it when needed
+  void runBase(void* stream = nullptr);
+  // every variant + diff, one launch; records = false keeps only the diff
+  // (bitmap + counts) -- fetchUpdates() then needs records, so it re-runs
+  void launch(void* stream = nullptr, bool records = true);
+  // counts -> offsets -> device gather of the changed records -> host
+  void fetchUpdates(void* stream = nullptr);
+  // bitmap + counts, and every variant's full records when the launch wrote
+  // them (parity tests)
+  void fetchRecords(void* stream = nullptr);
+
+  size_t numVariants() const { return dead_.size() / kDeadMax; }
+  const DecisionRouteDb& baseRouteDb() const;             // after a launch
+  DecisionRouteUpdate routeUpdate(size_t v) const;        // after fetchUpdates
+  DecisionRouteDb routeDb(size_t v) const;                // after fetchRecords
+  std::vector<std::string> changedPrefixes(size_t v) const;  // after either
+  std::pair<uint32_t, uint32_t> counts(size_t v) const;   // {update, delete}
+  uint64_t totalChanges() const { return offsets_.empty() ? 0 : offsets_.back(); }
+  int nhWords() const { return W_; }
+  const HostBatch& batch() const { return hb_; }
+  uint32_t flags() const;
+
+ private:
+  static constexpr int kDeadMax = 4;  // <= 2 links x 2 directions
+  ogs_graph graph() const;
+  ogs_prefix_table table() const;
+  const LinkState& ls_;
+  std::string me_, area_;
+  bool enableV4_, brs_, v4OverV6_;
+  PrefixHostTable table_;
+  HostBatch hb_;
+  int W_{1};
+  size_t words_{1}, Sp_{1};
+  bool baseRun_{false}, recordsRun_{false};
+  std::vector<uint32_t> dead_;
+  DeviceBuffer dNodeBase_, dDesc_, dRow_, dEdges_, dEdgeSrc_, dFlags_, dPfxBase_,
+      dAdvOff_, dAdvNode_, dAdvMetrics_, dAdvMinNh_, dPfxFlags_, dUnits_,
+      dBaseUnit_, dDead_;
+  DeviceBuffer bDist_, bNh_, bMeta_, bMetric_, bMask_, bSel_;
+  DeviceBuffer dDist_, dNh_, dMeta_, dMetric_, dMask_, dSel_, dChanged_, dCounts_;
+  DeviceBuffer dOffsets_, cPrefix_, cMeta_, cMetric_, cMask_;
+  mutable std::optional<DecisionRouteDb> base_;
+  std::vector<uint32_t> baseMeta_, baseMetric_, baseMask_;
+  std::vector<uint32_t> counts_, changed_, offsets_;
+  std::vector<uint32_t> cPrefixH_, cMetaH_, cMetricH_, cMaskH_;  // compact
+  std::vector<uint32_t> meta_, metric_, mask_;                   // full
+};
 
 }  // namespace openr_amd

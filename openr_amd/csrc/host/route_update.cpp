@@ -1,0 +1,330 @@
+// route_update.cpp — LinkFailureSweep: batched what-if route updates
+// (SURVEY.md §8(f) f1 over config C4).
+//
+// Reference: Decision::rebuildRoutes (Decision.cpp:912-951) rebuilds the
+// RouteDb after a topology change and publishes
+// DecisionRouteDb::calculateUpdate(old, new) (SpfSolver.cpp:21-56) to Fib.
+// Here the "new" RouteDbs of many link-failure variants come out of one
+// ogs_spf_routes_variants launch with that diff fused in; the changed records
+// are gathered on the device and only those are materialised into
+// DecisionRouteUpdate (unicastRoutesToUpdate / unicastRoutesToDelete).
+#include <algorithm>
+#include <stdexcept>
+
+#include "decision.h"
+
+namespace openr_amd {
+
+LinkFailureSweep::LinkFailureSweep(
+    const std::string& myNodeName, const LinkState& ls, const PrefixState& ps,
+    const std::vector<std::vector<LinkDown>>& variants, bool enableV4,
+    bool enableBestRouteSelection, bool v4OverV6Nexthop)
+    : ls_(ls),
+      me_(myNodeName),
+      area_(ls.getArea()),
+      enableV4_(enableV4),
+      brs_(enableBestRouteSelection),
+      v4OverV6_(v4OverV6Nexthop) {
+  const FlatTopology& f = ls.flat();
+  auto sIt = f.id.find(me_);
+  if (sIt == f.id.end()) {
+    throw std::invalid_argument("LinkFailureSweep: " + me_ + " is not in area " + area_);
+  }
+  if (wideDistancesNeeded(f)) {
+    throw std::domain_error("LinkFailureSweep: path metrics need 64-bit distances");
+  }
+  table_.build(ps);
+  hb_.append(f, ps, area_);
+  if (hb_.hasZeroMetric) {
+    throw std::domain_error(
+        "LinkFailureSweep: zero or negative link metric is outside the GPU "
+        "engine's exact domain");
+  }
+  const uint32_t s = sIt->second;
+  W_ = std::max(1, ogs_nh_words_for_degree(int(f.rowPtr[s + 1] - f.rowPtr[s])));
+  if (W_ > 4) throw std::domain_error("LinkFailureSweep: source degree > 128");
+
+  // dead directed edges: both directions of every failed link
+  auto edgeOf = [&](const std::string& node, auto&& pred) -> uint32_t {
+    auto it = f.id.find(node);
+    if (it == f.id.end()) throw std::invalid_argument("LinkFailureSweep: unknown node " + node);
+    for (uint32_t e = f.rowPtr[it->second]; e < f.rowPtr[it->second + 1]; ++e) {
+      if (pred(*f.edgeLink[e])) return e;
+    }
+    return OGS_NODE_NONE;
+  };
+  dead_.assign(variants.size() * kDeadMax, OGS_NODE_NONE);
+  for (size_t v = 0; v < variants.size(); ++v) {
+    if (variants[v].size() * 2 > size_t(kDeadMax)) {
+      throw std::invalid_argument("LinkFailureSweep: more than 2 links in a variant");
+    }
+    size_t k = 0;
+    for (const auto& d : variants[v]) {
+      const Link* link = nullptr;
+      const uint32_t e = edgeOf(d.node, [&](const Link& l) {
+        if (l.getIfaceFromNode(d.node) != d.ifName) return false;
+        link = &l;
+        return true;
+      });
+      if (e == OGS_NODE_NONE) {
+        throw std::invalid_argument("LinkFailureSweep: no link " + d.node + "%" + d.ifName);
+      }
+      const std::string other = link->getOtherNodeName(d.node);
+      const uint32_t r = edgeOf(other, [&](const Link& l) { return &l == link; });
+      dead_[v * kDeadMax + k++] = e;
+      if (r != OGS_NODE_NONE) dead_[v * kDeadMax + k++] = r;
+    }
+  }
+
+  const size_t U = variants.size(), Sn = size_t(std::max(hb_.maxNodes, 1));
+  Sp_ = size_t(std::max(hb_.maxPrefixes, 1));
+  words_ = (Sp_ + 31) / 32;
+  std::vector<ogs_unit> units(U, ogs_unit{0, s});
+  const ogs_unit base{0, s};
+  dNodeBase_.upload(hb_.nodeBase.data(), hb_.nodeBase.size());
+  dDesc_.upload(hb_.topoDesc.data(), hb_.topoDesc.size());
+  dRow_.upload(hb_.rowPtr.data(), hb_.rowPtr.size());
+  dEdges_.upload(hb_.edges.data(), hb_.edges.size());
+  dEdgeSrc_.upload(hb_.edgeSrc.data(), hb_.edgeSrc.size());
+  dFlags_.upload(hb_.nodeFlags.data(), hb_.nodeFlags.size());
+  dPfxBase_.upload(hb_.pfxBase.data(), hb_.pfxBase.size());
+  dAdvOff_.upload(hb_.advOff.data(), hb_.advOff.size());
+  dAdvNode_.upload(hb_.advNode.data(), hb_.advNode.size());
+  dAdvMetrics_.upload(hb_.advMetrics.data(), hb_.advMetrics.size());
+  dAdvMinNh_.upload(hb_.advMinNh.data(), hb_.advMinNh.size());
+  dPfxFlags_.upload(hb_.pfxFlags.data(), hb_.pfxFlags.size());
+  dUnits_.upload(units.data(), units.size());
+  dBaseUnit_.upload(&base, 1);
+  dDead_.upload(dead_.data(), dead_.size());
+  bDist_.resize(Sn * 4);
+  bNh_.resize(W_ * Sn * 4);
+  for (auto* b : {&bMeta_, &bMetric_, &bSel_}) b->resize(Sp_ * 4);
+  bMask_.resize(W_ * Sp_ * 4);
+  const size_t Uc = std::max<size_t>(U, 1);
+  dDist_.resize(Uc * Sn * 4);
+  dNh_.resize(Uc * W_ * Sn * 4);
+  for (auto* b : {&dMeta_, &dMetric_, &dSel_}) b->resize(Uc * Sp_ * 4);
+  dMask_.resize(Uc * W_ * Sp_ * 4);
+  dChanged_.resize(Uc * words_ * 4);
+  dCounts_.resize(Uc * 2 * 4);
+}
+
+uint32_t LinkFailureSweep::flags() const {
+  return (enableV4_ ? OGS_F_ENABLE_V4 : 0u) | (brs_ ? OGS_F_BEST_ROUTE_SELECTION : 0u);
+}
+
+ogs_graph LinkFailureSweep::graph() const {
+  ogs_graph g{};
+  g.num_topos = 1;
+  g.max_nodes = hb_.maxNodes;
+  g.max_edges = hb_.maxEdges;
+  g.max_degree = hb_.maxDegree;
+  g.topo_desc = dDesc_.as<uint32_t>();
+  g.node_base = dNodeBase_.as<uint32_t>();
+  g.row_ptr = dRow_.as<uint32_t>();
+  g.edges = dEdges_.as<uint64_t>();
+  g.node_flags = dFlags_.as<uint8_t>();
+  g.edge_src = dEdgeSrc_.as<uint32_t>();
+  return g;
+}
+
+ogs_prefix_table LinkFailureSweep::table() const {
+  ogs_prefix_table pt{};
+  pt.max_prefixes = hb_.maxPrefixes;
+  pt.max_advertisements = hb_.maxAdvs;
+  pt.pfx_base = dPfxBase_.as<uint32_t>();
+  pt.adv_off = dAdvOff_.as<uint32_t>();
+  pt.adv_node = dAdvNode_.as<uint32_t>();
+  pt.adv_metrics = dAdvMetrics_.as<int32_t>();
+  pt.adv_min_nh = dAdvMinNh_.as<int64_t>();
+  pt.pfx_flags = dPfxFlags_.as<uint8_t>();
+  return pt;
+}
+
+void LinkFailureSweep::runBase(void* stream) {
+  ogs_graph g = graph();
+  ogs_prefix_table pt = table();
+  ogs_spf_out out{bDist_.get(), bNh_.as<uint32_t>(), bMeta_.as<uint32_t>(),
+                  bMetric_.get(), bMask_.as<uint32_t>(), bSel_.as<uint32_t>()};
+  ogsCheck(ogs_spf_routes(&g, &pt, dBaseUnit_.as<ogs_unit>(), 1, flags(), W_, &out, stream),
+           "ogs_spf_routes(base)");
+  baseRun_ = true;
+  base_.reset();
+}
+
+void LinkFailureSweep::launch(void* stream, bool records) {
+  if (!baseRun_) runBase(stream);
+  offsets_.clear();  // results of an earlier launch are stale now
+  changed_.clear();
+  meta_.clear();
+  counts_.clear();
+  ogs_graph g = graph();
+  ogs_prefix_table pt = table();
+  ogs_spf_out out{};
+  if (records) {
+    out = ogs_spf_out{dDist_.get(), dNh_.as<uint32_t>(), dMeta_.as<uint32_t>(),
+                      dMetric_.get(), dMask_.as<uint32_t>(), dSel_.as<uint32_t>()};
+  }
+  ogs_unit_mods mods{dDead_.as<uint32_t>(), kDeadMax};
+  ogs_route_diff diff{bMeta_.as<uint32_t>(), bMetric_.as<uint32_t>(), bMask_.as<uint32_t>(),
+                      dChanged_.as<uint32_t>(), dCounts_.as<uint32_t>()};
+  ogsCheck(ogs_spf_routes_variants(&g, &pt, dUnits_.as<ogs_unit>(), int32_t(numVariants()),
+                                   &mods, &diff, flags(), W_, &out, stream),
+           "ogs_spf_routes_variants");
+  recordsRun_ = records;
+}
+
+void LinkFailureSweep::fetchUpdates(void* stream) {
+  if (!recordsRun_) {
+    throw std::logic_error("LinkFailureSweep::fetchUpdates: launch(records=true) first");
+  }
+  const size_t U = numVariants();
+  counts_.resize(U * 2);
+  if (U) dCounts_.download(counts_.data(), U * 2, stream);
+  ogsCheck(ogs_stream_sync(stream), "ogs_stream_sync");
+  offsets_.assign(U + 1, 0);
+  uint64_t total = 0;
+  for (size_t v = 0; v < U; ++v) {
+    offsets_[v] = uint32_t(total);
+    total += uint64_t(counts_[2 * v]) + counts_[2 * v + 1];
+    if (total > 0xFFFFFFFFull) throw std::length_error("LinkFailureSweep: > 2^32 changes");
+  }
+  offsets_[U] = uint32_t(total);
+  const size_t T = std::max<size_t>(total, 1);
+  dOffsets_.upload(offsets_.data(), offsets_.size(), stream);
+  cPrefix_.resize(T * 4);
+  cMeta_.resize(T * 4);
+  cMetric_.resize(T * 4);
+  cMask_.resize(T * W_ * 4);
+  ogs_spf_out rec{nullptr, nullptr, dMeta_.as<uint32_t>(), dMetric_.get(),
+                  dMask_.as<uint32_t>(), nullptr};
+  ogs_route_changes ch{dOffsets_.as<uint32_t>(), size_t(total), cPrefix_.as<uint32_t>(),
+                       cMeta_.as<uint32_t>(), cMetric_.as<uint32_t>(),
+                       cMask_.as<uint32_t>()};
+  ogsCheck(ogs_route_changes_gather(dChanged_.as<uint32_t>(), int32_t(U), int32_t(Sp_), &rec,
+                                    W_, &ch, stream),
+           "ogs_route_changes_gather");
+  cPrefixH_.resize(total);
+  cMetaH_.resize(total);
+  cMetricH_.resize(total);
+  cMaskH_.resize(total * W_);
+  if (total) {
+    cPrefix_.download(cPrefixH_.data(), total, stream);
+    cMeta_.download(cMetaH_.data(), total, stream);
+    cMetric_.download(cMetricH_.data(), total, stream);
+    cMask_.download(cMaskH_.data(), total * W_, stream);
+  }
+  baseMeta_.resize(Sp_);
+  baseMetric_.resize(Sp_);
+  baseMask_.resize(W_ * Sp_);
+  bMeta_.download(baseMeta_.data(), Sp_, stream);
+  bMetric_.download(baseMetric_.data(), Sp_, stream);
+  bMask_.download(baseMask_.data(), W_ * Sp_, stream);
+  ogsCheck(ogs_stream_sync(stream), "ogs_stream_sync");
+  base_.reset();
+}
+
+void LinkFailureSweep::fetchRecords(void* stream) {
+  // the diff (bitmap + counts) always; the records when the launch wrote them
+  const size_t U = numVariants();
+  const size_t R = recordsRun_ ? U : 0;
+  counts_.resize(U * 2);
+  changed_.resize(U * words_);
+  meta_.resize(R * Sp_);
+  metric_.resize(R * Sp_);
+  mask_.resize(R * W_ * Sp_);
+  if (U) {
+    dCounts_.download(counts_.data(), U * 2, stream);
+    dChanged_.download(changed_.data(), U * words_, stream);
+  }
+  if (R) {
+    dMeta_.download(meta_.data(), U * Sp_, stream);
+    dMetric_.download(metric_.data(), U * Sp_, stream);
+    dMask_.download(mask_.data(), U * W_ * Sp_, stream);
+  }
+  baseMeta_.resize(Sp_);
+  baseMetric_.resize(Sp_);
+  baseMask_.resize(W_ * Sp_);
+  bMeta_.download(baseMeta_.data(), Sp_, stream);
+  bMetric_.download(baseMetric_.data(), Sp_, stream);
+  bMask_.download(baseMask_.data(), W_ * Sp_, stream);
+  ogsCheck(ogs_stream_sync(stream), "ogs_stream_sync");
+  base_.reset();
+}
+
+const DecisionRouteDb& LinkFailureSweep::baseRouteDb() const {
+  if (baseMeta_.empty()) throw std::logic_error("LinkFailureSweep: nothing fetched yet");
+  if (!base_) {
+    DecisionRouteDb db;
+    const FlatTopology& f = ls_.flat();
+    for (uint32_t p = 0; p < uint32_t(table_.prefixes.size()); ++p) {
+      auto e = materializeRoute(f, me_, table_, p, baseMeta_[p], baseMetric_[p],
+                                &baseMask_[p], Sp_, W_, v4OverV6_, nullptr, 0xFF, 0xFF);
+      if (e) db.unicastRoutes.emplace(e->prefix, std::move(*e));
+    }
+    base_ = std::move(db);
+  }
+  return *base_;
+}
+
+DecisionRouteUpdate LinkFailureSweep::routeUpdate(size_t v) const {
+  if (v >= numVariants() || offsets_.size() != numVariants() + 1) {
+    throw std::out_of_range("LinkFailureSweep::routeUpdate: variant / fetchUpdates");
+  }
+  DecisionRouteUpdate u;  // SpfSolver.cpp:21-56, prefixes in table order
+  const FlatTopology& f = ls_.flat();
+  const size_t T = cPrefixH_.size();
+  for (uint32_t i = offsets_[v]; i < offsets_[v + 1]; ++i) {
+    const uint32_t p = cPrefixH_[i];
+    auto e = materializeRoute(f, me_, table_, p, cMetaH_[i], cMetricH_[i], &cMaskH_[i], T, W_,
+                              v4OverV6_, nullptr, 0xFF, 0xFF);
+    if (e) {
+      u.unicastRoutesToUpdate.emplace(e->prefix, std::move(*e));
+    } else {
+      u.unicastRoutesToDelete.push_back(table_.prefixes.at(p));
+    }
+  }
+  return u;
+}
+
+DecisionRouteDb LinkFailureSweep::routeDb(size_t v) const {
+  if (v >= numVariants() || meta_.size() != numVariants() * Sp_) {
+    throw std::out_of_range("LinkFailureSweep::routeDb: variant / fetchRecords");
+  }
+  DecisionRouteDb db;
+  const FlatTopology& f = ls_.flat();
+  for (uint32_t p = 0; p < uint32_t(table_.prefixes.size()); ++p) {
+    auto e = materializeRoute(f, me_, table_, p, meta_[v * Sp_ + p], metric_[v * Sp_ + p],
+                              &mask_[v * W_ * Sp_ + p], Sp_, W_, v4OverV6_, nullptr, 0xFF,
+                              0xFF);
+    if (e) db.unicastRoutes.emplace(e->prefix, std::move(*e));
+  }
+  return db;
+}
+
+std::vector<std::string> LinkFailureSweep::changedPrefixes(size_t v) const {
+  if (v >= numVariants()) throw std::out_of_range("LinkFailureSweep: variant");
+  std::vector<std::string> out;
+  if (offsets_.size() == numVariants() + 1) {
+    for (uint32_t i = offsets_[v]; i < offsets_[v + 1]; ++i) {
+      out.push_back(table_.prefixes.at(cPrefixH_[i]));
+    }
+  } else if (changed_.size() == numVariants() * words_) {
+    for (size_t p = 0; p < table_.prefixes.size(); ++p) {
+      if (changed_[v * words_ + p / 32] >> (p % 32) & 1u) out.push_back(table_.prefixes[p]);
+    }
+  } else {
+    throw std::logic_error("LinkFailureSweep: nothing fetched yet");
+  }
+  std::sort(out.begin(), out.end());
+  return out;
+}
+
+std::pair<uint32_t, uint32_t> LinkFailureSweep::counts(size_t v) const {
+  if (v >= numVariants() || counts_.size() != 2 * numVariants()) {
+    throw std::out_of_range("LinkFailureSweep::counts: variant / fetch");
+  }
+  return {counts_[2 * v], counts_[2 * v + 1]};
+}
+
+}  // namespace openr_amd

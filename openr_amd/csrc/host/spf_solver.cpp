@@ -338,6 +338,40 @@ void PrefixHostTable::build(const PrefixState& ps) {
   }
 }
 
+// One prefix's route from the unit's compact records (RibUnicastEntry of
+// createRouteForPrefix, SpfSolver.cpp:160-311 + addBestPaths 595-639).
+// `meta`, `metric` and the link-slot mask words (word w at mask[w * stride])
+// are the record of prefix p; nullopt when the record holds no route.
+std::optional<RibUnicastEntry> materializeRoute(
+    const FlatTopology& f, const std::string& me, const PrefixHostTable& pt,
+    uint32_t p, uint32_t meta, uint64_t metric, const uint32_t* mask,
+    size_t maskStride, int W, bool v4OverV6Nexthop, const RibPolicy* policy,
+    uint8_t applied, uint8_t counter) {
+  if (!(meta & OGS_ROUTE_VALID)) return std::nullopt;
+  const uint32_t rb = f.rowPtr[f.id.at(me)];
+  const uint32_t best = pt.advOff[p] + (meta >> OGS_ROUTE_BEST_SHIFT);
+  RibUnicastEntry e;
+  e.prefix = pt.prefixes[p];
+  const bool useV4 = isV4Prefix(e.prefix) && !v4OverV6Nexthop;
+  const int32_t m32 = static_cast<int32_t>(metric);
+  for (int w = 0; w < W; ++w) {
+    uint32_t bits = mask[w * maskStride];
+    while (bits) {
+      const int b = __builtin_ctz(bits);
+      bits &= bits - 1;
+      e.nexthops.insert(makeNh(*f.edgeLink[rb + w * 32 + b], me, useV4, m32, std::nullopt));
+    }
+  }
+  e.bestPrefixEntry = *pt.advEntry[best];
+  if (meta & OGS_ROUTE_DRAINED) e.bestPrefixEntry.metrics.drain_metric = 1;
+  e.bestPrefixEntry.weight = std::nullopt;  // RibEntry.h:77
+  e.bestArea = pt.advKey[best].second;
+  e.igpCost = static_cast<unsigned int>(metric);
+  e.localRouteConsidered = meta & OGS_ROUTE_LOCAL;
+  if (policy) finishPolicy(policy, applied, counter, e);
+  return e;
+}
+
 DecisionRouteDb materializeRouteDb(
     const LinkState& ls, const FlatTopology& f, const std::string& area,
     const std::string& me, const UnitView& r, const PrefixHostTable& pt,
@@ -346,48 +380,24 @@ DecisionRouteDb materializeRouteDb(
     std::map<std::string, RouteSelectionResult>* bestRoutesCache) {
   DecisionRouteDb rdb;
   if (bestRoutesCache) bestRoutesCache->clear();
-  const uint32_t s = f.id.at(me);
-  const uint32_t rb = f.rowPtr[s];
-  auto linksOf = [&](const uint32_t* words, size_t stride, auto&& fn) {
-    for (int w = 0; w < r.W; ++w) {
-      uint32_t bits = words[w * stride];
-      while (bits) {
-        const int b = __builtin_ctz(bits);
-        bits &= bits - 1;
-        fn(*f.edgeLink[rb + w * 32 + b]);
-      }
-    }
-  };
   for (uint32_t p = 0; p < r.P; ++p) {
     const uint32_t meta = r.meta[p];
-    const uint32_t a0 = pt.advOff[p];
-    const uint32_t best = a0 + (meta >> OGS_ROUTE_BEST_SHIFT);
     if (bestRoutesCache && (meta & OGS_ROUTE_SELECTED)) {  // SpfSolver.cpp:247
+      const uint32_t a0 = pt.advOff[p];
       RouteSelectionResult sel;
       const uint32_t a1 = pt.advOff[p + 1];
       for (uint32_t a = a0; a < std::min(a1, a0 + 32); ++a) {
         if (r.sel[p] >> (a - a0) & 1u) sel.allNodeAreas.insert(pt.advKey[a]);
       }
-      sel.bestNodeArea = pt.advKey[best];
+      sel.bestNodeArea = pt.advKey[a0 + (meta >> OGS_ROUTE_BEST_SHIFT)];
       sel.isBestNodeDrained = meta & OGS_ROUTE_DRAINED;
       (*bestRoutesCache)[pt.prefixes[p]] = std::move(sel);
     }
-    if (!(meta & OGS_ROUTE_VALID)) continue;
-    RibUnicastEntry e;
-    e.prefix = pt.prefixes[p];
-    const bool useV4 = isV4Prefix(e.prefix) && !v4OverV6Nexthop;
-    const int32_t m32 = static_cast<int32_t>(r.metric[p]);
-    linksOf(&r.mask[p], r.maskStride, [&](const Link& l) {
-      e.nexthops.insert(makeNh(l, me, useV4, m32, std::nullopt));
-    });
-    e.bestPrefixEntry = *pt.advEntry[best];
-    if (meta & OGS_ROUTE_DRAINED) e.bestPrefixEntry.metrics.drain_metric = 1;
-    e.bestPrefixEntry.weight = std::nullopt;  // RibEntry.h:77
-    e.bestArea = pt.advKey[best].second;
-    e.igpCost = static_cast<unsigned int>(r.metric[p]);
-    e.localRouteConsidered = meta & OGS_ROUTE_LOCAL;
-    if (r.policy) finishPolicy(r.policy, r.applied[p], r.counter[p], e);
-    rdb.unicastRoutes.emplace(e.prefix, std::move(e));
+    auto e = materializeRoute(f, me, pt, p, meta, r.metric[p], &r.mask[p], r.maskStride,
+                              r.W, v4OverV6Nexthop, r.policy,
+                              r.policy ? r.applied[p] : 0xFF,
+                              r.policy ? r.counter[p] : 0xFF);
+    if (e) rdb.unicastRoutes.emplace(e->prefix, std::move(*e));
   }
   for (const auto& [prefix, e] : statics) {  // SpfSolver.cpp:343-349
     if (rdb.unicastRoutes.count(prefix)) continue;

@@ -36,6 +36,10 @@ hipError_t launch_rib_policy(const ogs_prefix_table& pt, const ogs_rib_policy& p
                              int A, int nUnits, int W, const uint32_t* meta,
                              uint32_t* mask, uint8_t* applied, uint8_t* counter,
                              hipStream_t stream);
+hipError_t launch_route_changes(const uint32_t* changed, int nUnits, int Sp, int W,
+                                const uint32_t* meta, const uint32_t* metric,
+                                const uint32_t* mask, const ogs_route_changes& out,
+                                hipStream_t stream);
 hipError_t launch_ksp(const ogs_graph& g, const ogs_path_unit* units,
                       int nUnits, const uint32_t* masks, uint32_t maskWords,
                       uint32_t flags, const ogs_path_out& out,
@@ -337,6 +341,34 @@ int ogs_spf_routes_variants(const ogs_graph* graph,
                 "32-bit distances)");
   }
   return e == hipSuccess ? OGS_OK : hipFail(e, "variant launch");
+}
+
+int ogs_route_changes_gather(const uint32_t* changed, int32_t n_units,
+                             int32_t max_prefixes, const ogs_spf_out* records,
+                             int32_t nh_words, const ogs_route_changes* changes,
+                             void* stream) {
+  if (n_units < 0 || max_prefixes < 0) {
+    return fail(OGS_E_INVALID, "n_units or max_prefixes < 0");
+  }
+  if (n_units == 0 || max_prefixes == 0) return OGS_OK;
+  if (!changed || !records || !changes || !changes->offsets) {
+    return fail(OGS_E_INVALID, "changed/records/changes/offsets is NULL");
+  }
+  if (!records->meta || !records->metric || !records->mask) {
+    return fail(OGS_E_INVALID, "records need meta, metric and mask");
+  }
+  if (nh_words != 1 && nh_words != 2 && nh_words != 4) {
+    return fail(OGS_E_UNSUPPORTED, "nh_words must be 1, 2 or 4");
+  }
+  if (changes->total == 0) return OGS_OK;
+  if (!changes->prefix || !changes->meta || !changes->metric || !changes->mask) {
+    return fail(OGS_E_INVALID, "change record arrays are NULL");
+  }
+  hipError_t e = ogs::launch_route_changes(
+      changed, n_units, max_prefixes, nh_words, records->meta,
+      reinterpret_cast<const uint32_t*>(records->metric), records->mask, *changes,
+      static_cast<hipStream_t>(stream));
+  return e == hipSuccess ? OGS_OK : hipFail(e, "route changes gather");
 }
 
 int ogs_rib_policy_apply(const ogs_prefix_table* prefixes,

@@ -574,9 +574,10 @@ class BatchRunner {
 };
 
 // -------------------------------------------------------- VariantRunner ---
-// Config C4: one topology, its base RouteDb from `source`, and `count`
-// seeded link-failure variants solved in ONE launch with the route diff
-// against the base fused in (ogs_spf_routes_variants). Owns its device memory.
+// Config C4: one generated topology, its base RouteDb from `source`, and
+// `count` seeded link-failure variants (this rank's block [lo, hi)) solved in
+// ONE launch with the route diff fused in -- a LinkFailureSweep (§8(f) f1)
+// over a generated LSDB.
 class VariantRunner {
  public:
   VariantRunner(bool enableV4, bool brs) : enableV4_(enableV4), brs_(brs) {}
@@ -584,210 +585,84 @@ class VariantRunner {
   void setup(const std::string& kind, const py::dict& opts, const std::string& source,
              int count, uint64_t seed, int dualPermille, int lo, int hi) {
     g_ = genLsdb(kind, opts);
-    variants_ = topogen::linkFailureVariants(g_, count, seed, dualPermille);
+    auto variants = topogen::linkFailureVariants(g_, count, seed, dualPermille);
     // this rank's block [lo, hi) of the job's variants (hi < 0: to the end)
-    hi = hi < 0 ? int(variants_.size()) : std::min(hi, int(variants_.size()));
+    hi = hi < 0 ? int(variants.size()) : std::min(hi, int(variants.size()));
     lo = std::max(0, std::min(lo, hi));
-    variants_ = std::vector<std::vector<topogen::LinkRef>>(variants_.begin() + lo,
-                                                           variants_.begin() + hi);
+    std::vector<std::vector<LinkFailureSweep::LinkDown>> downs;
+    for (int v = lo; v < hi; ++v) {
+      auto& d = downs.emplace_back();
+      for (const auto& l : variants[v]) d.push_back({l.a, l.ifA});
+    }
     area_ = g_.area;
+    sweep_.reset();
+    als_.clear();
+    ps_ = PrefixState();
     als_.emplace(area_, LinkState(area_, "test_node"));
-    LinkState& ls = als_.at(area_);
-    loadLsdb(g_, ls, ps_);
-    const FlatTopology& f = ls.flat();
-    table_.build(ps_);
-    hb_.append(f, ps_, area_);
-    if (hb_.hasZeroMetric) throw std::domain_error("zero metric in batch");
-    source_ = source;
-    const uint32_t s = f.id.at(source);
-    W_ = std::max(1, ogs_nh_words_for_degree(int(f.rowPtr[s + 1] - f.rowPtr[s])));
-    // dead directed edges: both directions of every failed link
-    std::vector<uint32_t> dead(size_t(variants_.size()) * kDead, OGS_NODE_NONE);
-    for (size_t v = 0; v < variants_.size(); ++v) {
-      size_t k = 0;
-      for (const auto& l : variants_[v]) {
-        for (const auto& [n, ifn] : {std::make_pair(l.a, l.ifA), std::make_pair(l.b, l.ifB)}) {
-          const uint32_t u = f.id.at(n);
-          for (uint32_t e = f.rowPtr[u]; e < f.rowPtr[u + 1]; ++e) {
-            if (f.edgeLink[e]->getIfaceFromNode(n) == ifn) {
-              if (k < kDead) dead[v * kDead + k++] = e;
-              break;
-            }
-          }
-        }
-      }
-    }
-    std::vector<ogs_unit> units(variants_.size(), ogs_unit{0, s});
-    const ogs_unit base{0, s};
-    dNodeBase_.upload(hb_.nodeBase.data(), hb_.nodeBase.size());
-    dDesc_.upload(hb_.topoDesc.data(), hb_.topoDesc.size());
-    dRow_.upload(hb_.rowPtr.data(), hb_.rowPtr.size());
-    dEdges_.upload(hb_.edges.data(), hb_.edges.size());
-    dEdgeSrc_.upload(hb_.edgeSrc.data(), hb_.edgeSrc.size());
-    dFlags_.upload(hb_.nodeFlags.data(), hb_.nodeFlags.size());
-    dPfxBase_.upload(hb_.pfxBase.data(), hb_.pfxBase.size());
-    dAdvOff_.upload(hb_.advOff.data(), hb_.advOff.size());
-    dAdvNode_.upload(hb_.advNode.data(), hb_.advNode.size());
-    dAdvMetrics_.upload(hb_.advMetrics.data(), hb_.advMetrics.size());
-    dAdvMinNh_.upload(hb_.advMinNh.data(), hb_.advMinNh.size());
-    dPfxFlags_.upload(hb_.pfxFlags.data(), hb_.pfxFlags.size());
-    dUnits_.upload(units.data(), units.size());
-    dBaseUnit_.upload(&base, 1);
-    dDead_.upload(dead.data(), dead.size());
-    const size_t U = variants_.size(), Sn = hb_.maxNodes, Sp = std::max(hb_.maxPrefixes, 1);
-    words_ = (Sp + 31) / 32;
-    for (auto* b : {&bDist_, &dDist_}) b->resize((b == &bDist_ ? 1 : U) * Sn * 4);
-    bNh_.resize(W_ * Sn * 4);
-    dNh_.resize(U * W_ * Sn * 4);
-    for (auto* b : {&bMeta_, &bMetric_, &bSel_}) b->resize(Sp * 4);
-    bMask_.resize(W_ * Sp * 4);
-    for (auto* b : {&dMeta_, &dMetric_, &dSel_}) b->resize(U * Sp * 4);
-    dMask_.resize(U * W_ * Sp * 4);
-    dChanged_.resize(U * words_ * 4);
-    dCounts_.resize(U * 2 * 4);
+    loadLsdb(g_, als_.at(area_), ps_);
+    sweep_ = std::make_unique<LinkFailureSweep>(source, als_.at(area_), ps_, downs, enableV4_,
+                                                brs_);
   }
-
-  // base RouteDb (regular launch), then every variant + diff (one launch)
-  void runBase(uintptr_t stream) {
-    ogs_graph g = graph();
-    ogs_prefix_table pt = table();
-    ogs_spf_out out{bDist_.get(), bNh_.as<uint32_t>(), bMeta_.as<uint32_t>(),
-                    bMetric_.get(), bMask_.as<uint32_t>(), bSel_.as<uint32_t>()};
-    ogsCheck(ogs_spf_routes(&g, &pt, dBaseUnit_.as<ogs_unit>(), 1, flags(), W_, &out,
-                            reinterpret_cast<void*>(stream)),
-             "ogs_spf_routes(base)");
-  }
+  void runBase(uintptr_t stream) { sw().runBase(reinterpret_cast<void*>(stream)); }
   void launch(uintptr_t stream, bool records) {
-    ogs_graph g = graph();
-    ogs_prefix_table pt = table();
-    ogs_spf_out out{};
-    if (records) {
-      out = ogs_spf_out{dDist_.get(), dNh_.as<uint32_t>(), dMeta_.as<uint32_t>(),
-                        dMetric_.get(), dMask_.as<uint32_t>(), dSel_.as<uint32_t>()};
+    sw().launch(reinterpret_cast<void*>(stream), records);
+  }
+  void download() { sw().fetchRecords(); }
+  void fetchUpdates(uintptr_t stream) { sw().fetchUpdates(reinterpret_cast<void*>(stream)); }
+  std::string canonicalOf(size_t v) const { return canonical(sw().routeDb(v)); }
+  std::string baseCanonical() const { return canonical(sw().baseRouteDb()); }
+  // base RouteDb with variant v's DecisionRouteUpdate applied
+  // (DecisionRouteDb::update, SpfSolver.cpp:58-72)
+  std::string updatedCanonical(size_t v) const {
+    DecisionRouteDb db = sw().baseRouteDb();
+    db.update(sw().routeUpdate(v));
+    return canonical(db);
+  }
+  py::tuple updateOf(size_t v) const {
+    const DecisionRouteUpdate u = sw().routeUpdate(v);
+    py::list upd;
+    for (const auto& [p, _] : u.unicastRoutesToUpdate) upd.append(p);
+    py::list del;
+    for (const auto& p : u.unicastRoutesToDelete) del.append(p);
+    return py::make_tuple(upd, del);
+  }
+  // every variant's DecisionRouteUpdate materialised (host cost of the
+  // update path); returns the number of route changes
+  uint64_t materializeAll() const {
+    uint64_t n = 0;
+    for (size_t v = 0; v < sw().numVariants(); ++v) {
+      const DecisionRouteUpdate u = sw().routeUpdate(v);
+      n += u.unicastRoutesToUpdate.size() + u.unicastRoutesToDelete.size();
     }
-    ogs_unit_mods mods{dDead_.as<uint32_t>(), kDead};
-    ogs_route_diff diff{bMeta_.as<uint32_t>(), bMetric_.as<uint32_t>(),
-                        bMask_.as<uint32_t>(), dChanged_.as<uint32_t>(),
-                        dCounts_.as<uint32_t>()};
-    ogsCheck(ogs_spf_routes_variants(&g, &pt, dUnits_.as<ogs_unit>(),
-                                     int32_t(variants_.size()), &mods, &diff, flags(),
-                                     W_, &out, reinterpret_cast<void*>(stream)),
-             "ogs_spf_routes_variants");
+    return n;
   }
-  void download() {
-    const size_t U = variants_.size(), Sn = hb_.maxNodes, Sp = std::max(hb_.maxPrefixes, 1);
-    auto get32 = [](const DeviceBuffer& b, size_t n, std::vector<uint32_t>& v) {
-      v.resize(n);
-      b.download(v.data(), n);
-    };
-    get32(dDist_, U * Sn, dist_);
-    get32(dNh_, U * W_ * Sn, nh_);
-    get32(dMeta_, U * Sp, meta_);
-    get32(dMetric_, U * Sp, metric_);
-    get32(dMask_, U * W_ * Sp, mask_);
-    get32(dSel_, U * Sp, sel_);
-    get32(dChanged_, U * words_, changed_);
-    get32(dCounts_, U * 2, counts_);
-    ogsCheck(ogs_stream_sync(nullptr), "ogs_stream_sync");
-  }
-  std::string canonicalOf(size_t v) const {
-    const size_t Sn = hb_.maxNodes, Sp = std::max(hb_.maxPrefixes, 1);
-    const LinkState& ls = als_.at(area_);
-    std::vector<uint64_t> d(Sn), m(Sp);
-    for (size_t i = 0; i < Sn; ++i) {
-      const uint32_t x = dist_[v * Sn + i];
-      d[i] = x == 0xFFFFFFFFu ? ~0ull : x;
-    }
-    for (size_t i = 0; i < Sp; ++i) {
-      const uint32_t x = metric_[v * Sp + i];
-      m[i] = x == 0xFFFFFFFFu ? ~0ull : x;
-    }
-    UnitView uv;
-    uv.W = W_;
-    uv.N = uint32_t(ls.flat().names.size());
-    uv.P = uint32_t(table_.prefixes.size());
-    uv.dist = d.data();
-    uv.nh = &nh_[v * W_ * Sn];
-    uv.nhStride = Sn;
-    uv.meta = &meta_[v * Sp];
-    uv.metric = m.data();
-    uv.mask = &mask_[v * W_ * Sp];
-    uv.maskStride = Sp;
-    uv.sel = &sel_[v * Sp];
-    static const std::map<std::string, RibUnicastEntry> kNoStatics;
-    return canonical(materializeRouteDb(ls, ls.flat(), area_, source_, uv, table_,
-                                        false, false, kNoStatics, nullptr));
-  }
-  std::vector<std::string> changedOf(size_t v) const {
-    std::vector<std::string> out;
-    for (size_t p = 0; p < table_.prefixes.size(); ++p) {
-      if (changed_[v * words_ + p / 32] >> (p % 32) & 1u) out.push_back(table_.prefixes[p]);
-    }
-    std::sort(out.begin(), out.end());
-    return out;
-  }
-  std::pair<uint32_t, uint32_t> countsOf(size_t v) const {
-    return {counts_[2 * v], counts_[2 * v + 1]};
-  }
-  size_t numVariants() const { return variants_.size(); }
-  uint32_t flags() const {
-    return (enableV4_ ? OGS_F_ENABLE_V4 : 0u) | (brs_ ? OGS_F_BEST_ROUTE_SELECTION : 0u);
-  }
+  std::vector<std::string> changedOf(size_t v) const { return sw().changedPrefixes(v); }
+  std::pair<uint32_t, uint32_t> countsOf(size_t v) const { return sw().counts(v); }
+  size_t numVariants() const { return sw().numVariants(); }
+  uint64_t totalChanges() const { return sw().totalChanges(); }
   py::dict shape() const {
+    const HostBatch& hb = sw().batch();
     py::dict d;
-    d["nodes"] = hb_.maxNodes;
-    d["directed_edges"] = hb_.maxEdges;
-    d["prefixes"] = hb_.maxPrefixes;
-    d["advertisements"] = hb_.maxAdvs;
-    d["nh_words"] = W_;
-    d["variants"] = variants_.size();
+    d["nodes"] = hb.maxNodes;
+    d["directed_edges"] = hb.maxEdges;
+    d["prefixes"] = hb.maxPrefixes;
+    d["advertisements"] = hb.maxAdvs;
+    d["nh_words"] = sw().nhWords();
+    d["variants"] = sw().numVariants();
     return d;
   }
 
  private:
-  static constexpr int kDead = 4;  // <= 2 links x 2 directions
-  ogs_graph graph() const {
-    ogs_graph g{};
-    g.num_topos = 1;
-    g.max_nodes = hb_.maxNodes;
-    g.max_edges = hb_.maxEdges;
-    g.max_degree = hb_.maxDegree;
-    g.topo_desc = dDesc_.as<uint32_t>();
-    g.node_base = dNodeBase_.as<uint32_t>();
-    g.row_ptr = dRow_.as<uint32_t>();
-    g.edges = dEdges_.as<uint64_t>();
-    g.node_flags = dFlags_.as<uint8_t>();
-    g.edge_src = dEdgeSrc_.as<uint32_t>();
-    return g;
-  }
-  ogs_prefix_table table() const {
-    ogs_prefix_table pt{};
-    pt.max_prefixes = hb_.maxPrefixes;
-    pt.max_advertisements = hb_.maxAdvs;
-    pt.pfx_base = dPfxBase_.as<uint32_t>();
-    pt.adv_off = dAdvOff_.as<uint32_t>();
-    pt.adv_node = dAdvNode_.as<uint32_t>();
-    pt.adv_metrics = dAdvMetrics_.as<int32_t>();
-    pt.adv_min_nh = dAdvMinNh_.as<int64_t>();
-    pt.pfx_flags = dPfxFlags_.as<uint8_t>();
-    return pt;
+  LinkFailureSweep& sw() const {
+    if (!sweep_) throw std::logic_error("VariantRunner: setup() first");
+    return *sweep_;
   }
   bool enableV4_, brs_;
   topogen::Lsdb g_;
-  std::vector<std::vector<topogen::LinkRef>> variants_;
-  std::string area_, source_;
+  std::string area_;
   AreaLinkStates als_;
   PrefixState ps_;
-  PrefixHostTable table_;
-  HostBatch hb_;
-  int W_{1};
-  size_t words_{1};
-  DeviceBuffer dNodeBase_, dDesc_, dRow_, dEdges_, dEdgeSrc_, dFlags_, dPfxBase_,
-      dAdvOff_, dAdvNode_, dAdvMetrics_, dAdvMinNh_, dPfxFlags_, dUnits_,
-      dBaseUnit_, dDead_;
-  DeviceBuffer bDist_, bNh_, bMeta_, bMetric_, bMask_, bSel_;
-  DeviceBuffer dDist_, dNh_, dMeta_, dMetric_, dMask_, dSel_, dChanged_, dCounts_;
-  std::vector<uint32_t> dist_, nh_, meta_, metric_, mask_, sel_, changed_, counts_;
+  std::unique_ptr<LinkFailureSweep> sweep_;
 };
 
 template <typename T>
@@ -1253,6 +1128,15 @@ PYBIND11_MODULE(_decision, m) {
              r.launch(stream, records);
            }, py::arg("stream") = 0, py::arg("records") = true)
       .def("download", &VariantRunner::download)
+      .def("fetch_updates", [](VariantRunner& r, uintptr_t stream) { r.fetchUpdates(stream); },
+           py::arg("stream") = 0)
+      .def("base_canonical", [](const VariantRunner& r) { return py::bytes(r.baseCanonical()); })
+      .def("updated_canonical",
+           [](const VariantRunner& r, size_t v) { return py::bytes(r.updatedCanonical(v)); })
+      .def("update", &VariantRunner::updateOf)
+      .def("total_changes", &VariantRunner::totalChanges)
+      .def("materialize_all", &VariantRunner::materializeAll,
+           py::call_guard<py::gil_scoped_release>())
       .def("num_variants", &VariantRunner::numVariants)
       .def("canonical", [](const VariantRunner& r, size_t v) { return py::bytes(r.canonicalOf(v)); })
       .def("changed", &VariantRunner::changedOf)

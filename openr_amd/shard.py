@@ -38,6 +38,23 @@ def route_digest(*arrays):
     return int.from_bytes(h.digest()[:8], "little") >> 1
 
 
+def unit_digest(keys, *arrays):
+    """63-bit digest of a set of units that does not depend on how the units
+    are split over ranks: XOR over units of sha256(key, the unit's rows).
+    `keys` are global unit ids (ints or strings); every array's leading
+    dimension is split into len(keys) equal rows, one per unit."""
+    import numpy as np
+    n = len(keys)
+    rows = [np.ascontiguousarray(a).reshape(n, -1) if n else a for a in arrays]
+    out = 0
+    for i, k in enumerate(keys):
+        h = hashlib.sha256(str(k).encode() + b"\0")
+        for r in rows:
+            h.update(memoryview(r[i]).cast("B"))
+        out ^= int.from_bytes(h.digest()[:8], "little") >> 1
+    return out
+
+
 def combine_digests(digests):
     """Order-independent combination of per-rank digests: XOR (each rank's
     block is fixed by its rank, so XOR of the blocks is the whole job's)."""
@@ -50,7 +67,11 @@ def combine_digests(digests):
 def reduce_stats(dist, torch, device, units, routes, digest, elapsed_s):
     """All-gather per-rank {units, routes, digest}, MAX-reduce elapsed.
     Returns (total_units, total_routes, combined_digest, max_elapsed_s,
-    per_rank list). With dist None (single process) it returns the inputs."""
+    per_rank list). With dist None (single process) it returns the inputs.
+    Under gloo (CPU tests, shared-device rehearsal) the records stay on the
+    host."""
+    if dist is not None and dist.get_backend() == "gloo":
+        device = "cpu"
     local = torch.tensor([int(units), int(routes), int(digest), 0],
                          dtype=torch.int64, device=device)
     elapsed = torch.tensor([float(elapsed_s)], dtype=torch.float64, device=device)

@@ -51,3 +51,55 @@ def test_variants_records_optional(product):
     vr.launch(0, False)
     vr.download()
     assert [(vr.changed(v), vr.counts(v)) for v in range(32)] == full
+
+
+@pytest.mark.parametrize("kind,opts,source,brs", CASES, ids=lambda x: str(x)[:12])
+def test_route_updates_from_changed_records(product, oracle, kind, opts, source, brs):
+    """§8(f) f1: the DecisionRouteUpdate of every variant, materialised from the
+    device-gathered changed records only (ogs_route_changes_gather), is
+    DecisionRouteDb::calculateUpdate(base, variant) (SpfSolver.cpp:21-56):
+    its update keys + deletions are exactly the changed prefixes with the
+    oracle's counts, and base.update(it) (SpfSolver.cpp:58-72) is the
+    oracle's variant RouteDb."""
+    n = 48
+    vr = product.VariantRunner(True, brs)
+    vr.setup(kind, opts, source, n, 0xC4F, 500)
+    vr.launch(0, True)
+    vr.fetch_updates(0)
+    base, variants, links = oracle.variant_route_updates(kind, opts, source, n, 0xC4F,
+                                                         500, True, brs)
+    assert vr.base_canonical() == base
+    assert vr.total_changes() == sum(nu + nd for _, _, nu, nd in variants)
+    for v, (canon, changed, nu, nd) in enumerate(variants):
+        upd, dele = vr.update(v)
+        assert (len(upd), len(dele)) == (nu, nd), f"variant {v} {links[v]}"
+        assert sorted(upd + dele) == changed, f"variant {v} {links[v]}"
+        got = vr.updated_canonical(v)
+        if got != canon:
+            a, b = got.decode().splitlines(), canon.decode().splitlines()
+            pytest.fail(f"variant {v} {links[v]}: {[(x, y) for x, y in zip(a, b) if x != y][:4]}")
+
+
+def test_route_updates_c4_sample(product, oracle):
+    """The C4 bench workload (2,000-node WAN, seed 0xC4, source '0'): the first
+    64 of its 10,000 variants, route updates vs the oracle."""
+    opts = dict(nodes=2000, seed=0xC4, prefixesPerNode=1)
+    vr = product.VariantRunner(True, False)
+    vr.setup("wan", opts, "0", 10000, 0xC4F, 500, 0, 64)
+    vr.launch(0, True)
+    vr.fetch_updates(0)
+    _, variants, links = oracle.variant_route_updates("wan", opts, "0", 64, 0xC4F, 500,
+                                                      True, False)
+    for v, (canon, changed, nu, nd) in enumerate(variants):
+        upd, dele = vr.update(v)
+        assert sorted(upd + dele) == changed and (len(upd), len(dele)) == (nu, nd), v
+        assert vr.updated_canonical(v) == canon, f"variant {v} {links[v]}"
+
+
+def test_route_updates_need_records(product):
+    opts = dict(nodes=120, seed=0xC4, prefixesPerNode=1)
+    vr = product.VariantRunner(True, False)
+    vr.setup("wan", opts, "0", 8, 0xC4F, 500)
+    vr.launch(0, False)
+    with pytest.raises(Exception, match="records"):
+        vr.fetch_updates(0)

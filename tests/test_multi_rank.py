@@ -96,3 +96,28 @@ def test_bad_rank_rejected():
         shard.block_range(10, 2, 2)
     with pytest.raises(ValueError):
         shard.interleave([1, 2], -1, 2)
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_unit_digest_independent_of_sharding(world):
+    """bench.py's job digest (XOR of per-unit keyed hashes) is the same
+    whether the units are solved on one rank or split over `world` ranks,
+    block-wise or interleaved."""
+    import numpy as np
+    rng = np.random.default_rng(7)
+    U = 37
+    meta = rng.integers(0, 2**31, size=(U, 16), dtype=np.int32)
+    mask = rng.integers(0, 2**31, size=(U, 2, 16), dtype=np.int32)
+    keys = list(range(U))
+    whole = shard.unit_digest(keys, meta, mask)
+    blocks = []
+    for r in range(world):
+        lo, hi = shard.block_range(U, r, world)
+        blocks.append(shard.unit_digest(keys[lo:hi], meta[lo:hi], mask[lo:hi]))
+    assert shard.combine_digests(blocks) == whole
+    inter = [shard.unit_digest(shard.interleave(keys, r, world),
+                               meta[r::world], mask[r::world]) for r in range(world)]
+    assert shard.combine_digests(inter) == whole
+    flipped = meta.copy()
+    flipped[5, 3] ^= 1
+    assert shard.unit_digest(keys, flipped, mask) != whole
