@@ -316,6 +316,20 @@ def run_c4(args, torch, dist, rank, world, local_rank):
     n_changes = vr.materialize_all()
     mat_ms = (time.perf_counter() - t1) * 1e3
     assert n_changes == changed == vr.total_changes()
+    # §8(f) f3, outside the timed region: one link-metric flap made current on
+    # the device -- in-place CSR patch (ogs_csr_patch) vs re-flatten + upload
+    csr_update = None
+    if rank == 0:
+        M = openr_amd.decision
+        csr_update = {}
+        for tag, kind, opts in (
+                ("c4_wan", "wan", C4_OPTS),
+                ("c3_fabric", "fabric", dict(pods=32, planes=8, sswPerPlane=36,
+                                             rswPerPod=48, full=True, prefixesPerNode=1))):
+            patch_us, rebuild_us, edges, flaps = M.flap_update_bench(kind, opts, 200, 0xF3)
+            csr_update[tag] = {"directed_edges": edges, "flaps": flaps,
+                               "patch_us": round(patch_us, 2),
+                               "rebuild_us": round(rebuild_us, 2)}
     total_units, total_changed, job_digest, tmax, _ = shard.reduce_stats(
         dist, torch, dev, U, changed, digest, wall)
     if rank != 0:
@@ -339,6 +353,7 @@ def run_c4(args, torch, dist, rank, world, local_rank):
                    "variants": C4_VARIANTS,
                    "parallelism": f"shard-by-variant x{world}"},
         "changed_routes_per_step": total_changed, "route_digest": f"{job_digest:016x}",
+        "csr_update": csr_update,
         "route_update": {
             "changes": n_changes, "gather_fetch_ms": round(fetch_ms, 3),
             "materialize_ms": round(mat_ms, 3),
@@ -705,7 +720,8 @@ def main():
         if rank == 0:
             line["c4_link_failure_sweep"] = {
                 k: c4[k] for k in ("value", "unit", "ms_per_step", "kernel_ms", "gteps",
-                                   "changed_routes_per_step", "route_digest", "route_update", "roofline",
+                                   "changed_routes_per_step", "route_digest", "route_update", "csr_update",
+                                   "roofline",
                                    "config", "steps") if k in c4}
             if "cpu_baseline" in c4:
                 line["c4_link_failure_sweep"]["cpu_baseline"] = c4["cpu_baseline"]

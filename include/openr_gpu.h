@@ -371,6 +371,15 @@ int ogs_route_changes_gather(const uint32_t* changed, int32_t n_units,
                              int32_t nh_words, const ogs_route_changes* changes,
                              void* stream);
 
+/* Incremental CSR update: edges[idx[i]] = val[i] for
+ * i < n, idx / val device arrays (encoded as ogs_graph.edges). Replaces the
+ * re-flatten + full re-upload after LinkState::updateAdjacencyDatabase
+ * (LinkState.cpp:440-640) changed only link / node attributes (metric,
+ * overload, usability): the CSR structure is unchanged. Indices must be
+ * < the edge array's length (not checked on the device). */
+int ogs_csr_patch(uint64_t* edges, const uint32_t* idx, const uint64_t* val,
+                  int32_t n, void* stream);
+
 /* RibPolicy compiled against one prefix table (SURVEY.md §8(a) a16;
  * RibPolicy.cpp:74-249): statements 0..K-1 in policy order. */
 typedef struct ogs_rib_policy {

@@ -219,6 +219,7 @@ struct FlatTopology {
   int slotStride{0};  // ogs_graph.slot_stride of dSlot (0: none)
   int slotDegree{0};  // ogs_graph.slot_degree of dSlotEdges (0: none)
   DeviceBuffer dRow, dEdges, dFlags, dNodeBase, dSlot, dSlotEdges, dEdgeSrc;
+  DeviceBuffer dPatchIdx, dPatchVal;  // ogs_csr_patch staging (§8(f) f3)
 };
 
 // ------------------------------------------------------------- LinkState --
@@ -285,10 +286,23 @@ class LinkState {
   const FlatTopology& flatOnDevice() const;  // + uploads when stale
   LinkPtr linkByKey(const Link::Key& k) const { return links_.at(k); }
   void noteSpfRuns(uint64_t n) const { spfRuns_ += n; }
+  // attribute-only updates patch the CSR in place (default) or, off,
+  // re-flatten + re-upload it (A/B measurements)
+  void setIncrementalFlatten(bool on) { incrementalFlatten_ = on; }
+  // full CSR builds vs in-place patches (§8(f) f3) so far
+  uint64_t flatBuilds() const { return flatBuilds_; }
+  uint64_t flatPatches() const { return flatPatches_; }
+  uint64_t edgesPatched() const { return edgesPatched_; }
 
  private:
   LinkPtr makeLink(const std::string& node, const Adjacency& adj) const;
   void invalidate(bool topologyChanged);
+  // attribute-only change of `node` (no link / node added or removed):
+  // re-encode the touched edges in the current CSR image and scatter them
+  // into the device copy (ogs_csr_patch) instead of re-flattening
+  void patchFlat(const std::string& node, const std::vector<const Link*>& touched,
+                 bool nodeFlagsChanged);
+  void uploadSlotImages(FlatTopology& m) const;
 
   std::string area_, myNodeName_;
   std::map<std::string, AdjacencyDatabase> adjDbs_;
@@ -305,6 +319,9 @@ class LinkState {
   mutable bool deviceStale_{true};
   mutable uint64_t spfRuns_{0};
   uint64_t mutation_{0};
+  mutable uint64_t flatBuilds_{0};
+  uint64_t flatPatches_{0}, edgesPatched_{0};
+  bool incrementalFlatten_{true};
 };
 
 // ----------------------------------------------------------- PrefixState --

@@ -89,7 +89,15 @@ LinkState::LinkStateChange LinkState::updateAdjacencyDatabase(
   LinkStateChange ch;
   const std::string name = db.thisNodeName;
   AdjacencyDatabase prior;
-  if (auto it = adjDbs_.find(name); it != adjDbs_.end()) prior = it->second;
+  // §8(f) f3: a known node whose link set is unchanged only moves link /
+  // node attributes -> patch the CSR in place (patchFlat)
+  bool structural = true;
+  if (auto it = adjDbs_.find(name); it != adjDbs_.end()) {
+    prior = it->second;
+    structural = false;
+  }
+  std::vector<const Link*> touched;
+  bool nodeFlagsChanged = false;
   adjDbs_[name] = db;
 
   std::map<Link::Key, LinkPtr> fresh;
@@ -105,8 +113,10 @@ LinkState::LinkStateChange LinkState::updateAdjacencyDatabase(
     } else if (it->second != db.isOverloaded) {
       it->second = db.isOverloaded;
       ch.topologyChanged = true;
+      nodeFlagsChanged = true;
     }
   }
+  nodeFlagsChanged |= prior.nodeMetricIncrementVal != db.nodeMetricIncrementVal;
   ch.topologyChanged |= prior.nodeMetricIncrementVal != db.nodeMetricIncrementVal;
   metricInc_[name] =
       static_cast<uint64_t>(static_cast<int64_t>(db.nodeMetricIncrementVal));
@@ -127,6 +137,7 @@ LinkState::LinkStateChange LinkState::updateAdjacencyDatabase(
       byNode_[l->firstNodeName()].insert(l->key());
       byNode_[l->secondNodeName()].insert(l->key());
       ch.addedLinks.push_back(l);
+      structural = true;
       ++ni;
       continue;
     }
@@ -136,11 +147,17 @@ LinkState::LinkStateChange LinkState::updateAdjacencyDatabase(
       byNode_.at(l->firstNodeName()).erase(l->key());
       byNode_.at(l->secondNodeName()).erase(l->key());
       links_.erase(l->key());
+      structural = true;
       ++oi;
       continue;
     }
     Link& nl = *ni->second;
     Link& ol = *links_.at(oldKeys[oi]);
+    if (nl.getMetricFromNode(name) != ol.getMetricFromNode(name) ||
+        nl.isUp() != ol.isUp() ||
+        nl.getOverloadFromNode(name) != ol.getOverloadFromNode(name)) {
+      touched.push_back(&ol);
+    }
     if (nl.getMetricFromNode(name) != ol.getMetricFromNode(name)) {
       ch.topologyChanged |= ol.setMetricFromNode(name, nl.getMetricFromNode(name));
     }
@@ -168,8 +185,87 @@ LinkState::LinkStateChange LinkState::updateAdjacencyDatabase(
     ++ni;
     ++oi;
   }
-  invalidate(ch.topologyChanged);
+  if (!structural && incrementalFlatten_ && flat_ && !flatStale_) {
+    patchFlat(name, touched, nodeFlagsChanged);
+    if (ch.topologyChanged) {  // LinkState.cpp:635-638
+      spfMemo_.clear();
+      kthMemo_.clear();
+    }
+  } else {
+    invalidate(ch.topologyChanged);
+  }
   return ch;
+}
+
+void LinkState::patchFlat(const std::string& node, const std::vector<const Link*>& touched,
+                          bool nodeFlagsChanged) {
+  FlatTopology& f = *flat_;
+  ++mutation_;
+  f.version = mutation_;  // version-keyed caches (prefix tables, policies) rebuild
+  ++flatPatches_;
+  const uint32_t u = f.id.at(node);
+  std::vector<uint32_t> dirty;
+  // same encoding as flat(): keep dst + rslot, recompute the rest
+  auto reencode = [&](uint32_t e) {
+    const Link* l = f.edgeLink[e];
+    const uint64_t old = f.edges[e];
+    const uint32_t keep = OGS_EDGE_DST_MASK | (OGS_EDGE_RSLOT_MASK << OGS_EDGE_RSLOT_SHIFT);
+    uint32_t lo = uint32_t(old) & keep;
+    if (isNodeOverloaded(f.names[lo & OGS_EDGE_DST_MASK])) lo |= OGS_EDGE_DST_OVERLOADED;
+    if (!l->isUp()) lo |= OGS_EDGE_DOWN;
+    const uint64_t w = uint64_t(lo) | (uint64_t(uint32_t(l->getMaxMetric())) << 32);
+    if (w != old) {
+      f.edges[e] = w;
+      dirty.push_back(e);
+    }
+  };
+  auto reverseOf = [&](uint32_t e) {
+    const uint32_t lo = uint32_t(f.edges[e]);
+    return f.rowPtr[lo & OGS_EDGE_DST_MASK] + ((lo >> OGS_EDGE_RSLOT_SHIFT) & OGS_EDGE_RSLOT_MASK);
+  };
+  for (uint32_t e = f.rowPtr[u]; e < f.rowPtr[u + 1]; ++e) {
+    const bool linkTouched =
+        std::find(touched.begin(), touched.end(), f.edgeLink[e]) != touched.end();
+    // an overload flip of `node` changes DST_OVERLOADED on every edge into it
+    if (linkTouched || nodeFlagsChanged) {
+      reencode(e);
+      reencode(reverseOf(e));
+    }
+  }
+  bool flagsDirty = false;
+  if (nodeFlagsChanged) {
+    uint8_t fl = 0;
+    if (isNodeOverloaded(node)) fl |= OGS_NODE_OVERLOADED;
+    const uint64_t inc = getNodeMetricIncrement(node);
+    if (static_cast<int>(inc) > 0) fl |= OGS_NODE_SOFTDRAIN;
+    if (inc != 0) fl |= OGS_NODE_METRICINC;
+    flagsDirty = fl != f.nodeFlags[u];
+    f.nodeFlags[u] = fl;
+  }
+  if (!dirty.empty()) {  // the domain checks of flat() over the up links
+    f.maxMetric = 0;
+    f.hasZeroMetric = f.hasWideMetric = false;
+    for (const Link* l : f.edgeLink) {
+      if (!l->isUp()) continue;
+      const LinkStateMetric m = l->getMaxMetric();
+      f.maxMetric = std::max(f.maxMetric, m);
+      if (m == 0) f.hasZeroMetric = true;
+      if (m > 0xFFFFFFFFull) f.hasWideMetric = true;
+    }
+  }
+  edgesPatched_ += dirty.size();
+  if (deviceStale_) return;  // the next flatOnDevice() uploads everything
+  if (!dirty.empty()) {
+    std::vector<uint64_t> val(dirty.size());
+    for (size_t i = 0; i < dirty.size(); ++i) val[i] = f.edges[dirty[i]];
+    f.dPatchIdx.upload(dirty.data(), dirty.size());
+    f.dPatchVal.upload(val.data(), val.size());
+    ogsCheck(ogs_csr_patch(f.dEdges.as<uint64_t>(), f.dPatchIdx.as<uint32_t>(),
+                           f.dPatchVal.as<uint64_t>(), int32_t(dirty.size()), nullptr),
+             "ogs_csr_patch");
+  }
+  if (flagsDirty) f.dFlags.upload(f.nodeFlags.data(), f.nodeFlags.size());
+  if (!dirty.empty() && f.slotStride) uploadSlotImages(f);
 }
 
 LinkState::LinkStateChange LinkState::deleteAdjacencyDatabase(
@@ -285,6 +381,7 @@ const FlatTopology& LinkState::flat() const {
   flat_ = std::move(f);
   flatStale_ = false;
   deviceStale_ = true;
+  ++flatBuilds_;
   return *flat_;
 }
 
@@ -305,6 +402,14 @@ const FlatTopology& LinkState::flatOnDevice() const {
     }
     m.dEdgeSrc.upload(esrc.data(), esrc.size());
   }
+  uploadSlotImages(m);
+  deviceStale_ = false;
+  return f;
+}
+
+// wave-kernel relaxation order + per-slot edge image (slot_order.h); the
+// image carries edge weights, so a patched CSR re-derives it
+void LinkState::uploadSlotImages(FlatTopology& m) const {
   m.slotStride = slotStrideFor(int(m.names.size()));
   if (m.slotStride) {
     std::vector<uint16_t> slots(m.slotStride);
@@ -323,8 +428,6 @@ const FlatTopology& LinkState::flatOnDevice() const {
   } else {
     m.slotDegree = 0;
   }
-  deviceStale_ = false;
-  return f;
 }
 
 // ------------------------------------------------------------------- SPF --

@@ -40,6 +40,8 @@ hipError_t launch_route_changes(const uint32_t* changed, int nUnits, int Sp, int
                                 const uint32_t* meta, const uint32_t* metric,
                                 const uint32_t* mask, const ogs_route_changes& out,
                                 hipStream_t stream);
+hipError_t launch_csr_patch(uint64_t* edges, const uint32_t* idx, const uint64_t* val,
+                            int n, hipStream_t stream);
 hipError_t launch_ksp(const ogs_graph& g, const ogs_path_unit* units,
                       int nUnits, const uint32_t* masks, uint32_t maskWords,
                       uint32_t flags, const ogs_path_out& out,
@@ -369,6 +371,15 @@ int ogs_route_changes_gather(const uint32_t* changed, int32_t n_units,
       reinterpret_cast<const uint32_t*>(records->metric), records->mask, *changes,
       static_cast<hipStream_t>(stream));
   return e == hipSuccess ? OGS_OK : hipFail(e, "route changes gather");
+}
+
+int ogs_csr_patch(uint64_t* edges, const uint32_t* idx, const uint64_t* val,
+                  int32_t n, void* stream) {
+  if (n < 0) return fail(OGS_E_INVALID, "n < 0");
+  if (n == 0) return OGS_OK;
+  if (!edges || !idx || !val) return fail(OGS_E_INVALID, "edges/idx/val is NULL");
+  hipError_t e = ogs::launch_csr_patch(edges, idx, val, n, static_cast<hipStream_t>(stream));
+  return e == hipSuccess ? OGS_OK : hipFail(e, "csr patch");
 }
 
 int ogs_rib_policy_apply(const ogs_prefix_table* prefixes,

@@ -1,6 +1,7 @@
 // openr_amd._decision — Python binding of the GPU drop-in (product path).
 // Exposes the same surface as the CPU oracle binding so tests can drive one
 // scenario through both. Every computation goes through libopenr_gpu.so.
+#include <chrono>
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
@@ -936,6 +937,32 @@ PYBIND11_MODULE(_decision, m) {
       .def("isNodeOverloaded", &LinkState::isNodeOverloaded)
       .def("getNodeMetricIncrement", &LinkState::getNodeMetricIncrement)
       .def("numLinks", &LinkState::numLinks)
+      .def("flatBuilds", &LinkState::flatBuilds)
+      .def("flatPatches", &LinkState::flatPatches)
+      .def("edgesPatched", &LinkState::edgesPatched)
+      .def("flat_image", [](const LinkState& s) {  // host CSR image (tests)
+        const FlatTopology& f = s.flat();
+        py::dict d;
+        d["names"] = f.names;
+        d["row_ptr"] = f.rowPtr;
+        d["edges"] = f.edges;
+        d["node_flags"] = f.nodeFlags;
+        d["max_metric"] = f.maxMetric;
+        d["max_degree"] = f.maxDegree;
+        d["has_zero_metric"] = f.hasZeroMetric;
+        d["has_wide_metric"] = f.hasWideMetric;
+        return d;
+      })
+      .def("device_edges", [](const LinkState& s) {  // device CSR edge words (tests)
+        const FlatTopology& f = s.flatOnDevice();
+        std::vector<uint64_t> out(f.edges.size());
+        if (!out.empty()) f.dEdges.download(out.data(), out.size());
+        ogsCheck(ogs_stream_sync(nullptr), "ogs_stream_sync");
+        std::vector<uint8_t> fl(f.nodeFlags.size());
+        if (!fl.empty()) f.dFlags.download(fl.data(), fl.size());
+        ogsCheck(ogs_stream_sync(nullptr), "ogs_stream_sync");
+        return py::make_tuple(out, fl);
+      })
       .def("numNodes", &LinkState::numNodes)
       .def("spfRuns", &LinkState::spfRuns)
       .def("getArea", &LinkState::getArea)
@@ -1089,6 +1116,43 @@ PYBIND11_MODULE(_decision, m) {
         py::arg("opts"), py::arg("sources"), py::arg("enableV4") = true,
         py::arg("sr") = false, py::arg("brs") = false, py::arg("policy") = py::list());
 
+  // §8(f) f3 measurement: mean host+device cost of one link-metric flap
+  // (updateAdjacencyDatabase of one node with one adjacency metric changed,
+  // then the CSR made current on the device and the stream drained), with the
+  // in-place patch and with a full re-flatten + upload. Returns
+  // (patch_us, rebuild_us, edges, flaps).
+  m.def("flap_update_bench",
+        [](const std::string& kind, py::dict opts, int flaps, uint64_t seed) {
+          const topogen::Lsdb g = genLsdb(kind, opts);
+          auto run = [&](bool incremental) {
+            py::gil_scoped_release nogil;
+            LinkState ls(g.area, "test_node");
+            PrefixState ps;
+            loadLsdb(g, ls, ps);
+            ls.setIncrementalFlatten(incremental);
+            ls.flatOnDevice();
+            ogsCheck(ogs_stream_sync(nullptr), "ogs_stream_sync");
+            std::vector<AdjacencyDatabase> dbs;
+            for (const auto& [_, db] : ls.getAdjacencyDatabases()) dbs.push_back(db);
+            uint64_t s = seed;
+            const auto t0 = std::chrono::steady_clock::now();
+            for (int i = 0; i < flaps; ++i) {
+              AdjacencyDatabase& db = dbs[topogen::splitmix64(s) % dbs.size()];
+              if (db.adjacencies.empty()) continue;
+              Adjacency& a = db.adjacencies[topogen::splitmix64(s) % db.adjacencies.size()];
+              a.metric = 1 + int32_t(topogen::splitmix64(s) % 1000);
+              ls.updateAdjacencyDatabase(db, g.area);
+              ls.flatOnDevice();
+              ogsCheck(ogs_stream_sync(nullptr), "ogs_stream_sync");
+            }
+            const double us = std::chrono::duration<double, std::micro>(
+                                  std::chrono::steady_clock::now() - t0).count();
+            return std::make_pair(us / std::max(flaps, 1), ls.flat().edges.size());
+          };
+          const auto [patchUs, edges] = run(true);
+          const auto [rebuildUs, _] = run(false);
+          return py::make_tuple(patchUs, rebuildUs, edges, flaps);
+        });
   m.def("gen_route_dbs",
         [](const std::string& kind, py::dict opts, std::vector<std::string> sources,
            bool enableV4, bool sr, bool brs, py::list policy) {

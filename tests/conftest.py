@@ -26,3 +26,11 @@ def product():
     import openr_amd
     openr_amd.require_gpu()
     return openr_amd.decision
+
+
+@pytest.fixture(scope="session")
+def host_module():
+    """The product module for host-only checks (CSR images, layouts): no
+    device call is made through it, so it is usable without a GPU."""
+    import openr_amd
+    return openr_amd.decision
