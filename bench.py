@@ -244,6 +244,18 @@ def run_c3(args, torch, dist, rank, world, local_rank):
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
                          "bytes_alg_per_step_rank0": round(nbytes, 1)},
         }
+        # §8(f) f2, outside the timed region: the same build as a resident
+        # RouteDbBatch served per node (getRouteDbComputed: D2H of one node's
+        # records + host materialisation + toThrift)
+        import openr_amd
+        launch_ms, serve_ms, routes, ns = openr_amd.decision.route_db_batch_serve_bench(
+            "fabric", dict(pods=32, planes=8, sswPerPlane=36, rswPerPod=48, full=True,
+                           prefixesPerNode=args.prefixes_per_node), 3)
+        line["serve"] = {"sources": ns, "batch_launch_ms": round(launch_ms, 3),
+                         "getRouteDbComputed_ms": round(serve_ms, 2),
+                         "routes_per_node": round(routes, 1),
+                         "note": "RouteDbBatch (C++ drop-in) over all 2,080 sources, then "
+                                 "3 nodes served; rank 0, after the timed region"}
         traffic, src = pmc_traffic("c3", "spf_frontier_kernel")
         if traffic is not None and world == 1:
             line["roofline"]["traffic"] = round(traffic, 1)
@@ -713,7 +725,7 @@ def main():
             line["c3_fabric_all_sources"] = {
                 k: c3[k] for k in ("value", "unit", "ms_per_step", "kernel_ms",
                                    "route_dbs_per_s", "gteps", "routes_per_step",
-                                   "route_digest", "roofline", "config")}
+                                   "route_digest", "serve", "roofline", "config") if k in c3}
             line["c3_fabric_all_sources"]["steps"] = c3["steps"]
     if not args.no_c4:
         c4 = run_c4(args, torch, dist, rank, world, local_rank)

@@ -377,9 +377,29 @@ struct DecisionRouteUpdate {  // RouteUpdate.h:28-110
   std::vector<int32_t> mplsRoutesToDelete;
 };
 
+// thrift::UnicastRoute / MplsRoute / RouteDatabase (Network.thrift,
+// OpenrCtrl's getRouteDbComputed payload) as plain structs; the prefix stays
+// in its CIDR text form (toIpPrefix is the thrift adapter's job)
+struct UnicastRoute {
+  std::string dest;
+  std::vector<NextHopThrift> nextHops;
+  std::optional<std::string> counterID;
+};
+struct MplsRoute {
+  int32_t topLabel{0};
+  std::vector<NextHopThrift> nextHops;
+};
+struct RouteDatabase {
+  std::string thisNodeName;
+  std::vector<UnicastRoute> unicastRoutes;
+  std::vector<MplsRoute> mplsRoutes;
+};
+
 struct DecisionRouteDb {  // SpfSolver.h:68-109
   std::map<std::string, RibUnicastEntry> unicastRoutes;
   std::map<int32_t, RibMplsEntry> mplsRoutes;
+  // SpfSolver.h:82-94 + RibEntry.h:95-103 (unicast) / MplsRoute of RibMplsEntry
+  RouteDatabase toThrift() const;
   DecisionRouteUpdate calculateUpdate(const DecisionRouteDb& newDb) const;
   void update(const DecisionRouteUpdate& u);
 };
@@ -496,6 +516,7 @@ class SpfSolver {
   DecisionRouteDb materializeMultiArea(const std::string& myNodeName,
                                        const AreaLinkStates& areaLinkStates,
                                        const MultiAreaResult& r);
+  friend class RouteDbBatch;
   struct Impl;
   std::unique_ptr<Impl> impl_;
   std::map<std::string, RibUnicastEntry> staticUnicastRoutes_;
@@ -711,6 +732,52 @@ class LinkFailureSweep {
   std::vector<uint32_t> counts_, changed_, offsets_;
   std::vector<uint32_t> cPrefixH_, cMetaH_, cMetricH_, cMaskH_;  // compact
   std::vector<uint32_t> meta_, metric_, mask_;                   // full
+};
+
+// ----------------------------------------------------------- RouteDbBatch --
+// the RouteDbs of MANY sources of one area computed in
+// one launch per next-hop width group and kept in HBM, then served per node
+// the way Decision::getDecisionRouteDb (Decision.cpp:341-360, behind
+// OpenrCtrl getRouteDbComputed, OpenrCtrlHandler.cpp:640-643) serves one:
+// SpfSolver::buildRouteDb(node) (incl. the solver's static routes and node
+// labels) -> DecisionRouteDb::toThrift with thisNodeName. Only the requested
+// node's records cross PCIe. No RibPolicy (getDecisionRouteDb applies none).
+// Single-area; `solver`, the LinkState and `ps` must outlive the batch
+// unchanged.
+class RouteDbBatch {
+ public:
+  RouteDbBatch(const SpfSolver& solver, const AreaLinkStates& areaLinkStates,
+               const PrefixState& ps, const std::vector<std::string>& sources);
+  void launch(void* stream = nullptr);  // asynchronous
+  // nullopt when `node` has no adjacency database (SpfSolver.cpp:318-324);
+  // std::out_of_range when `node` is not one of the batch's sources
+  std::optional<DecisionRouteDb> routeDb(const std::string& node, void* stream = nullptr) const;
+  // getDecisionRouteDb: empty routes when there is no RouteDb
+  RouteDatabase getRouteDbComputed(const std::string& node, void* stream = nullptr) const;
+  size_t numSources() const { return units_.size(); }
+  size_t numGroups() const { return groups_.size(); }
+
+ private:
+  struct Group {
+    int W{1};
+    std::vector<uint32_t> members;  // source index per unit of this group
+    DeviceBuffer units, dist, nh, meta, metric, mask, sel;
+  };
+  ogs_graph graph() const;
+  ogs_prefix_table table() const;
+  const SpfSolver& solver_;
+  const LinkState* ls_{nullptr};
+  std::string area_;
+  PrefixHostTable table_;
+  HostBatch hb_;
+  bool wide_{false};
+  std::vector<std::string> sources_;
+  std::map<std::string, size_t> index_;
+  std::vector<std::pair<size_t, size_t>> units_;  // source -> (group, unit)
+  std::vector<Group> groups_;
+  DeviceBuffer dDesc_, dPfxBase_, dAdvOff_, dAdvNode_, dAdvMetrics_, dAdvMinNh_,
+      dPfxFlags_;
+  bool launched_{false};
 };
 
 }  // namespace openr_amd

@@ -1007,6 +1007,37 @@ PYBIND11_MODULE(_decision, m) {
         return out;
       });
 
+  py::class_<RouteDbBatch>(m, "RouteDbBatch")
+      .def(py::init<const SpfSolver&, const AreaLinkStates&, const PrefixState&,
+                    const std::vector<std::string>&>(),
+           py::keep_alive<1, 2>(), py::keep_alive<1, 3>(), py::keep_alive<1, 4>())
+      .def("launch", [](RouteDbBatch& b, uintptr_t stream) {
+             b.launch(reinterpret_cast<void*>(stream));
+           }, py::arg("stream") = 0)
+      .def("routeDb", [](const RouteDbBatch& b, const std::string& n) { return b.routeDb(n); })
+      .def("getRouteDbComputed", [](const RouteDbBatch& b, const std::string& n) {
+        const RouteDatabase r = b.getRouteDbComputed(n);
+        py::list uni, mpls;
+        for (const auto& u : r.unicastRoutes) {
+          py::list nhs;
+          for (const auto& nh : u.nextHops) nhs.append(fromNh(nh));
+          uni.append(py::make_tuple(u.dest, nhs, u.counterID ? py::object(py::str(*u.counterID))
+                                                            : py::object(py::none())));
+        }
+        for (const auto& mr : r.mplsRoutes) {
+          py::list nhs;
+          for (const auto& nh : mr.nextHops) nhs.append(fromNh(nh));
+          mpls.append(py::make_tuple(mr.topLabel, nhs));
+        }
+        py::dict d;
+        d["thisNodeName"] = r.thisNodeName;
+        d["unicastRoutes"] = uni;
+        d["mplsRoutes"] = mpls;
+        return d;
+      })
+      .def("numSources", &RouteDbBatch::numSources)
+      .def("numGroups", &RouteDbBatch::numGroups);
+
   py::class_<DecisionRouteDb>(m, "DecisionRouteDb")
       .def(py::init<>())
       .def("unicastRoutes",
@@ -1176,6 +1207,73 @@ PYBIND11_MODULE(_decision, m) {
         },
         py::arg("kind"), py::arg("opts"), py::arg("sources"), py::arg("enableV4") = true,
         py::arg("sr") = false, py::arg("brs") = false, py::arg("policy") = py::list());
+
+  // §8(f) f2 parity: a generated topology's RouteDbs for `sources` from ONE
+  // RouteDbBatch (resident records, per-node materialisation); canonical text
+  // per source ("NONE" without a RouteDb) and the getRouteDbComputed shape
+  // (thisNodeName, unicast routes, mpls routes, next hops in total)
+  m.def("gen_route_db_batch",
+        [](const std::string& kind, py::dict opts, std::vector<std::string> sources,
+           bool enableV4, bool sr, bool brs) {
+          auto g = genLsdb(kind, opts);
+          AreaLinkStates als;
+          auto& ls = als.emplace(g.area, LinkState(g.area, "test_node")).first->second;
+          PrefixState ps;
+          loadLsdb(g, ls, ps);
+          SpfSolver solver("test_node", enableV4, sr, brs);
+          RouteDbBatch batch(solver, als, ps, sources);
+          batch.launch();
+          std::vector<py::bytes> out;
+          py::list shapes;
+          for (const auto& s : sources) {
+            auto db = batch.routeDb(s);
+            out.push_back(py::bytes(db ? canonical(*db) : std::string("NONE")));
+            const RouteDatabase r = batch.getRouteDbComputed(s);
+            size_t nhs = 0;
+            for (const auto& u : r.unicastRoutes) nhs += u.nextHops.size();
+            for (const auto& mr : r.mplsRoutes) nhs += mr.nextHops.size();
+            shapes.append(py::make_tuple(r.thisNodeName, r.unicastRoutes.size(),
+                                         r.mplsRoutes.size(), nhs));
+          }
+          return py::make_tuple(out, shapes, batch.numGroups());
+        },
+        py::arg("kind"), py::arg("opts"), py::arg("sources"), py::arg("enableV4") = true,
+        py::arg("sr") = false, py::arg("brs") = false);
+
+  // §8(f) f2 measurement: RouteDbBatch over ALL nodes of a generated
+  // topology (one launch per width group, records resident), then
+  // getRouteDbComputed for `serve` nodes (D2H of that node's records + host
+  // materialisation + toThrift). Returns (launch_ms, serve_ms_mean,
+  // routes_per_served_node_mean, sources).
+  m.def("route_db_batch_serve_bench",
+        [](const std::string& kind, py::dict opts, int serve) {
+          auto g = genLsdb(kind, opts);
+          py::gil_scoped_release nogil;
+          AreaLinkStates als;
+          auto& ls = als.emplace(g.area, LinkState(g.area, "test_node")).first->second;
+          PrefixState ps;
+          loadLsdb(g, ls, ps);
+          SpfSolver solver("test_node", true, false, false);
+          const std::vector<std::string> names = ls.flat().names;
+          RouteDbBatch batch(solver, als, ps, names);
+          batch.launch();  // warm-up (workspace, code objects)
+          ogsCheck(ogs_stream_sync(nullptr), "ogs_stream_sync");
+          auto t0 = std::chrono::steady_clock::now();
+          batch.launch();
+          ogsCheck(ogs_stream_sync(nullptr), "ogs_stream_sync");
+          const double launchMs = std::chrono::duration<double, std::milli>(
+                                      std::chrono::steady_clock::now() - t0).count();
+          uint64_t routes = 0;
+          const int n = std::max(1, std::min<int>(serve, int(names.size())));
+          t0 = std::chrono::steady_clock::now();
+          for (int i = 0; i < n; ++i) {
+            const RouteDatabase r = batch.getRouteDbComputed(names[(size_t(i) * 7919) % names.size()]);
+            routes += r.unicastRoutes.size();
+          }
+          const double serveMs = std::chrono::duration<double, std::milli>(
+                                     std::chrono::steady_clock::now() - t0).count() / n;
+          return std::make_tuple(launchMs, serveMs, double(routes) / n, names.size());
+        });
 
   py::class_<VariantRunner>(m, "VariantRunner")
       .def(py::init<bool, bool>(), py::arg("enableV4") = true,
