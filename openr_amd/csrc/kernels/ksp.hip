@@ -24,11 +24,12 @@
 
 namespace ogs {
 
+// 8 B per recursion level: the last edge (node -> pred) chosen at this frame
+// is both the path edge once the recursion below it succeeds and the resume
+// key (dist[pred], pred, rslot) of the next choice; ~0u = nothing chosen yet
 struct Frame {
   uint32_t node;
-  uint32_t edge;    // edge (node -> pred) chosen at this frame
-  uint32_t lastU;   // resume key: (dist[lastU], lastU, lastSlot)
-  uint32_t lastSlot;
+  uint32_t edge;
 };
 
 template <typename D>
@@ -57,8 +58,7 @@ __device__ uint32_t trace_paths(const UnitCsr& csr, const D* dist, uint32_t s,
   while (reachable) {
     // one traceOnePath(src, dest) call
     int sp = 0;
-    // a frame without a resume key yet carries lastSlot's top bit
-    stack[0] = Frame{t, 0xFFFFFFFFu, 0u, 0x80000000u};
+    stack[0] = Frame{t, 0xFFFFFFFFu};
     bool found = false;
     while (sp >= 0) {
       Frame& f = stack[sp];
@@ -67,8 +67,14 @@ __device__ uint32_t trace_paths(const UnitCsr& csr, const D* dist, uint32_t s,
       // next unvisited pathLink of v after the resume key
       D bd = kInf;
       uint32_t bu = 0xFFFFFFFFu, bs = 0xFFFFFFFFu, be = 0xFFFFFFFFu;
-      const bool fresh = (f.lastSlot & 0x80000000u) != 0;
-      const D ld = fresh ? D(0) : dist[f.lastU];
+      const bool fresh = f.edge == 0xFFFFFFFFu;
+      uint32_t lastU = 0u, lastSlot = 0u;
+      if (!fresh) {
+        const uint32_t llo = static_cast<uint32_t>(csr.edg[f.edge]);
+        lastU = edge_dst(llo);
+        lastSlot = edge_rslot(llo);
+      }
+      const D ld = fresh ? D(0) : dist[lastU];
       // the row's edges 8 at a time: the loads of a batch are independent
       // (HBM/L2 latency once per batch, not once per edge)
       const uint32_t rEnd = csr.rowp[v + 1];
@@ -93,7 +99,7 @@ __device__ uint32_t trace_paths(const UnitCsr& csr, const D* dist, uint32_t s,
           const D du = dist[u];
           if (du == kInf || du + static_cast<D>(ed >> 32) != dv) continue;
           const uint32_t slot = edge_rslot(lo);
-          if (!fresh && !key_less<D>(ld, f.lastU, f.lastSlot, du, u, slot)) continue;
+          if (!fresh && !key_less<D>(ld, lastU, lastSlot, du, u, slot)) continue;
           if (key_less<D>(du, u, slot, bd, bu, bs)) {
             bd = du;
             bu = u;
@@ -106,18 +112,16 @@ __device__ uint32_t trace_paths(const UnitCsr& csr, const D* dist, uint32_t s,
         --sp;
         continue;
       }
-      f.lastU = bu;
-      f.lastSlot = bs;
+      f.edge = be;  // resume key (and the path edge if the recursion succeeds)
       const uint32_t l = link_id(csr, be, static_cast<uint32_t>(csr.edg[be]));
       if ((visited[l >> 5] >> (l & 31u)) & 1u) continue;  // already used
       visited[l >> 5] |= 1u << (l & 31u);
-      f.edge = be;
       if (bu == s) {
         found = true;
         break;
       }
       ++sp;
-      stack[sp] = Frame{bu, 0xFFFFFFFFu, 0u, 0x80000000u};
+      stack[sp] = Frame{bu, 0xFFFFFFFFu};
     }
     if (!found) break;
     // path src -> dest = chosen edges from the top frame down to frame 0
