@@ -168,6 +168,10 @@ def run_c3(args, torch, dist, rank, world, local_rank):
     steps = args.steps if args.config == "c3" else args.c3_steps
     warmup = args.warmup if args.config == "c3" else 2
     launches, N = c3_launches(torch, M, capi, dev, rank, world, args.prefixes_per_node)
+    if args.c3_order == "wide-first":
+        # the wide (FSW, 4-word) group has the longest units: dispatch it
+        # first so it is not the lone tail after the 1-word group
+        launches = launches[::-1]
     # the width groups are independent: with --c3-streams 2 the second group
     # runs on its own HIP stream, overlapped with the first
     main = torch.cuda.current_stream(dev)
@@ -531,6 +535,8 @@ def main():
     ap.add_argument("--no-c3", action="store_true",
                     help="skip the C3 fabric all-sources line embedded in the C2 result")
     ap.add_argument("--c3-steps", type=int, default=10)
+    ap.add_argument("--c3-order", default="wide-first", choices=["narrow-first", "wide-first"],
+                    help="C3: which next-hop width group is dispatched first")
     ap.add_argument("--no-c4", action="store_true",
                     help="skip the C4 link-failure sweep line embedded in the C2 result")
     ap.add_argument("--c4-steps", type=int, default=5)

@@ -131,7 +131,7 @@ __device__ __forceinline__ void stream_routes(
       reinterpret_cast<uintptr_t>(out.sel) | reinterpret_cast<uintptr_t>(out.mask);
   const bool vec = (Sp & 3u) == 0u && (align & 15u) == 0u;
   const uint32_t Pv = vec ? (P & ~3u) : 0u;
-  for (uint32_t q = uint32_t(tid) * 4u; q < Pv; q += kBlock * 4u) {
+  auto quad = [&](uint32_t q) {
     const uint4 k4 = *reinterpret_cast<const uint4*>(tkey + q);
     Rec<W> r0, r1, r2, r3;
     one(q + 0, k4.x, r0);
@@ -171,7 +171,9 @@ __device__ __forceinline__ void stream_routes(
         if (word) atomicOr(diff->changed + w0, word);
       }
     }
-  }
+  };
+  uint32_t q = uint32_t(tid) * 4u;
+  for (; q < Pv; q += kBlock * 4u) quad(q);
   for (uint32_t p = Pv + tid; p < P; p += kBlock) {  // tail / unaligned rows
     Rec<W> r;
     one(p, tkey[p], r);
