@@ -15,6 +15,7 @@ extern int g_msGroup;
 extern int g_routeStream;
 extern int g_spfFrontier;
 extern int g_spfQueue;
+extern int g_spfNinfo;
 extern int g_kspQueue;
 extern int g_kspStage;
 hipError_t launch_spf_routes(const ogs_graph& g, const ogs_prefix_table* pt,
@@ -170,6 +171,11 @@ int ogs_set_option(const char* name, int64_t value) {
   if (std::strcmp(name, "ksp_stage") == 0) {
     if (value < -1 || value > 2) return fail(OGS_E_INVALID, "ksp_stage must be -1, 0, 1 or 2");
     ogs::g_kspStage = int(value);
+    return OGS_OK;
+  }
+  if (std::strcmp(name, "spf_ninfo") == 0) {
+    if (value < -1 || value > 1) return fail(OGS_E_INVALID, "spf_ninfo must be -1, 0 or 1");
+    ogs::g_spfNinfo = int(value);
     return OGS_OK;
   }
   if (std::strcmp(name, "spf_queue") == 0) {

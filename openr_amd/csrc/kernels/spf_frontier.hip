@@ -303,7 +303,7 @@ __device__ __forceinline__ void queue_spf(
     for (int w = 0; w < W; ++w) nh[v * W + w] = 0u;
   }
   // node info: local row begin | hard-drained bit (one LDS read per node)
-  for (uint32_t v = tid; v <= N; v += kBlock) {
+  for (uint32_t v = tid; ninfo && v <= N; v += kBlock) {  // nullptr: CSR reads
     ninfo[v] = (gRow[v] - e0) |
         ((v < N && (nflags[v] & OGS_NODE_OVERLOADED)) ? kDrained : 0u);
   }
@@ -331,10 +331,14 @@ __device__ __forceinline__ void queue_spf(
     const uint16_t* cur = (r & 1) ? q1 : q0;
     for (uint32_t i = tid; i < n; i += kBlock) {
       const uint32_t v = cur[i];
-      const uint32_t iv = ninfo[v], b = iv & ~kDrained;
+      const uint32_t iv = ninfo ? ninfo[v]
+                                : ((gRow[v] - e0) |
+                                   ((nflags[v] & OGS_NODE_OVERLOADED) ? kDrained : 0u));
+      const uint32_t b = iv & ~kDrained;
+      const uint32_t rowEnd = ninfo ? (ninfo[v + 1] & ~kDrained) : gRow[v + 1] - e0;
       if (v != s && (iv & kDrained)) continue;  // LinkState.cpp:741-752
       const uint32_t dv = dist[v];
-      for_row(edges, b, (ninfo[v + 1] & ~kDrained) - b, [&](uint32_t e, uint64_t x) {
+      for_row(edges, b, rowEnd - b, [&](uint32_t e, uint64_t x) {
         const uint32_t lo = static_cast<uint32_t>(x);
         if (lo & OGS_EDGE_DOWN) return;
         if constexpr (MODS) {
@@ -381,13 +385,17 @@ __device__ __forceinline__ void queue_spf(
     const uint16_t* cur = (r & 1) ? q1 : q0;
     for (uint32_t i = tid; i < n; i += kBlock) {
       const uint32_t v = cur[i];
-      const uint32_t iv = ninfo[v], b = iv & ~kDrained;
+      const uint32_t iv = ninfo ? ninfo[v]
+                                : ((gRow[v] - e0) |
+                                   ((nflags[v] & OGS_NODE_OVERLOADED) ? kDrained : 0u));
+      const uint32_t b = iv & ~kDrained;
+      const uint32_t rowEnd = ninfo ? (ninfo[v + 1] & ~kDrained) : gRow[v + 1] - e0;
       if (v == s || (iv & kDrained)) continue;
       const uint32_t dv = dist[v];
       uint32_t nv[W];
 #pragma unroll
       for (int w = 0; w < W; ++w) nv[w] = nh[v * W + w];
-      for_row(edges, b, (ninfo[v + 1] & ~kDrained) - b, [&](uint32_t e, uint64_t x) {
+      for_row(edges, b, rowEnd - b, [&](uint32_t e, uint64_t x) {
         const uint32_t lo = static_cast<uint32_t>(x);
         if (lo & OGS_EDGE_DOWN) return;
         if constexpr (MODS) {
@@ -435,7 +443,7 @@ __device__ __forceinline__ void queue_spf_packed(
     dn[v] = (v == s) ? 0ull : uint64_t(kInf);
     stamp[v] = 0u;
   }
-  for (uint32_t v = tid; v <= N; v += kBlock) {
+  for (uint32_t v = tid; ninfo && v <= N; v += kBlock) {  // nullptr: CSR reads
     ninfo[v] = (gRow[v] - e0) |
         ((v < N && (nflags[v] & OGS_NODE_OVERLOADED)) ? kDrained : 0u);
   }
@@ -456,11 +464,15 @@ __device__ __forceinline__ void queue_spf_packed(
     uint16_t* nxt = (r & 1) ? q0 : q1;
     for (uint32_t i = tid; i < n; i += kBlock) {
       const uint32_t v = cur[i];
-      const uint32_t iv = ninfo[v], b = iv & ~kDrained;
+      const uint32_t iv = ninfo ? ninfo[v]
+                                : ((gRow[v] - e0) |
+                                   ((nflags[v] & OGS_NODE_OVERLOADED) ? kDrained : 0u));
+      const uint32_t b = iv & ~kDrained;
+      const uint32_t rowEnd = ninfo ? (ninfo[v + 1] & ~kDrained) : gRow[v + 1] - e0;
       if (v != s && (iv & kDrained)) continue;  // LinkState.cpp:741-752
       const uint64_t xv = dn[v];
       const uint32_t dv = static_cast<uint32_t>(xv), nv = static_cast<uint32_t>(xv >> 32);
-      for_row(edges, b, (ninfo[v + 1] & ~kDrained) - b, [&](uint32_t e, uint64_t x) {
+      for_row(edges, b, rowEnd - b, [&](uint32_t e, uint64_t x) {
         const uint32_t lo = static_cast<uint32_t>(x);
         if (lo & OGS_EDGE_DOWN) return;
         if constexpr (MODS) {
@@ -497,13 +509,17 @@ __device__ __forceinline__ void queue_spf_packed(
 #endif
 }
 
-uint32_t frontier_lds_bytes(uint32_t Sn, int W, bool queue = false) {
+uint32_t frontier_lds_bytes(uint32_t Sn, int W, bool queue = false, bool ninfo = true) {
   const uint32_t core = 4u * (((Sn + 3u) & ~3u) + ((Sn * W + 3u) & ~3u));
   if (!queue) return core + 2u * ((Sn + 1u) & ~1u);
-  // + u32 stamps + two u16 node lists + u32 node info [Sn + 1]
+  // + u32 stamps + two u16 node lists (+ u32 node info [Sn + 1])
   return core + 4u * ((Sn + 3u) & ~3u) + 2u * 2u * ((Sn + 1u) & ~1u) +
-      4u * ((Sn + 4u) & ~3u);
+      (ninfo ? 4u * ((Sn + 4u) & ~3u) : 0u);
 }
+
+// internal launch flag (above the public OGS_F_* bits): the queue forms read
+// row bounds / drained bits from the CSR instead of an LDS node-info array
+constexpr uint32_t kFlagNinfoGlobal = 1u << 30;
 
 // ROUTES = false: SPF only, dist / nh to HBM.
 // ROUTES = true: SPF + the unit's RouteDb stream (route_stream.h) from LDS;
@@ -536,7 +552,9 @@ __global__ __launch_bounds__(kBlock) void spf_frontier_kernel(
   uint32_t* stamp32 = reinterpret_cast<uint32_t*>(stamp);
   uint16_t* q0 = reinterpret_cast<uint16_t*>(stamp32 + ((Sn + 3u) & ~3u));
   uint16_t* q1 = q0 + ((Sn + 1u) & ~1u);
-  uint32_t* ninfo = reinterpret_cast<uint32_t*>(q1 + ((Sn + 1u) & ~1u));
+  uint32_t* ninfo = (flags & kFlagNinfoGlobal)
+      ? nullptr
+      : reinterpret_cast<uint32_t*>(q1 + ((Sn + 1u) & ~1u));
   __shared__ uint32_t qcnt[3];
 
   DeadEdges dead;
@@ -647,6 +665,18 @@ __global__ __launch_bounds__(kBlock) void spf_frontier_kernel(
 // queue form even for one-word sets (A/B).
 int g_spfQueue = -1;
 
+// "spf_ninfo" option: 1 (default) the queue forms keep row begin | drained
+// per node in LDS, 0 read them from the CSR (L2) -- 4 B/node less LDS, more
+// units per CU --, -1 the CSR form whenever that raises the units per CU.
+int g_spfNinfo = 1;
+
+bool ninfo_in_lds(uint32_t Sn, int W) {
+  if (g_spfNinfo >= 0) return g_spfNinfo != 0;
+  constexpr uint32_t kCu = 160u * 1024u;
+  return kCu / frontier_lds_bytes(Sn, W, true, true) >=
+      kCu / frontier_lds_bytes(Sn, W, true, false);
+}
+
 // 0 chunk scan, 1 two-phase queue, 2 packed one-phase queue
 int queue_mode(const ogs_graph& g, int W) {
   if (g_spfQueue == 0 || g.max_nodes > 65535) return 0;
@@ -663,7 +693,9 @@ hipError_t launch_frontier_q(const ogs_graph& g, const ogs_prefix_table& pt,
                              uint32_t* nh, const ogs_spf_out& out,
                              hipStream_t stream, const ogs_unit_mods& mods,
                              const ogs_route_diff& diff) {
-  const uint32_t lds = frontier_lds_bytes(uint32_t(g.max_nodes), W, QMODE != 0);
+  const bool ninfo = QMODE == 0 || ninfo_in_lds(uint32_t(g.max_nodes), W);
+  const uint32_t lds = frontier_lds_bytes(uint32_t(g.max_nodes), W, QMODE != 0, ninfo);
+  if (!ninfo) flags |= kFlagNinfoGlobal;
   auto k = spf_frontier_kernel<W, ROUTES, MODS, DIFF, QMODE>;
   if (lds > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),

@@ -103,3 +103,34 @@ def test_route_updates_need_records(product):
     vr.launch(0, False)
     with pytest.raises(Exception, match="records"):
         vr.fetch_updates(0)
+
+
+@pytest.mark.parametrize("ninfo,queue", [(0, 2), (0, 1), (-1, -1), (1, 1)])
+def test_queue_forms_node_info_option(product, oracle, ninfo, queue):
+    """The queue SPF forms (packed one-phase = spf_queue 2 when one next-hop
+    word, two-phase = 1) with node info in LDS (spf_ninfo 1) or read from the
+    CSR (0; -1 = whenever it raises units per CU): same variant RouteDbs and
+    diffs, and the same plain RouteDbs, as the oracle."""
+    import openr_amd.capi as capi
+    lib = capi.load()
+    kind, opts = "wan", dict(nodes=400, seed=0xC5, prefixesPerNode=1, nodeOverloadPermille=20,
+                             adjOverloadPermille=20, anycastPermille=100, minNhPermille=50,
+                             drainPermille=50)
+    try:
+        capi.check(lib, lib.ogs_set_option(b"spf_ninfo", ninfo), "spf_ninfo")
+        capi.check(lib, lib.ogs_set_option(b"spf_queue", queue), "spf_queue")
+        vr = product.VariantRunner(True, True)
+        vr.setup(kind, opts, "7", 32, 0xC4F, 500)
+        vr.launch(0, True)
+        vr.download()
+        base, variants, links = oracle.variant_route_updates(kind, opts, "7", 32, 0xC4F,
+                                                             500, True, True)
+        for v, (canon, changed, nu, nd) in enumerate(variants):
+            assert vr.canonical(v) == canon, f"variant {v} {links[v]}"
+            assert vr.changed(v) == changed and vr.counts(v) == (nu, nd), v
+        srcs = [str(i) for i in range(0, 400, 37)]
+        got, _, _ = product.gen_route_db_batch(kind, opts, srcs, True, True, True)
+        assert got == oracle.gen_route_dbs(kind, opts, srcs, True, True, True)
+    finally:
+        lib.ogs_set_option(b"spf_ninfo", 1)
+        lib.ogs_set_option(b"spf_queue", -1)
