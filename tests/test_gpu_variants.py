@@ -134,3 +134,34 @@ def test_queue_forms_node_info_option(product, oracle, ninfo, queue):
     finally:
         lib.ogs_set_option(b"spf_ninfo", 1)
         lib.ogs_set_option(b"spf_queue", -1)
+
+
+def test_route_updates_wide_source(product, oracle):
+    """A source with more than 32 links (fabric FSW: 40 SSWs + 4 RSWs -> two
+    next-hop words): the gathered records carry both mask words, and the
+    variants include failures of the source's own links."""
+    opts = dict(pods=2, planes=2, sswPerPlane=40, rswPerPod=4, full=True, prefixesPerNode=2)
+    vr = product.VariantRunner(True, False)
+    vr.setup("fabric", opts, "2-0-0", 40, 0xC4F, 500)
+    assert vr.shape()["nh_words"] == 2
+    vr.launch(0, True)
+    vr.fetch_updates(0)
+    base, variants, links = oracle.variant_route_updates("fabric", opts, "2-0-0", 40, 0xC4F,
+                                                         500, True, False)
+    assert vr.base_canonical() == base
+    own = 0
+    for v, (canon, changed, nu, nd) in enumerate(variants):
+        own += any("2-0-0" in (t[0], t[2]) for t in links[v])
+        upd, dele = vr.update(v)
+        assert sorted(upd + dele) == changed and (len(upd), len(dele)) == (nu, nd), v
+        assert vr.updated_canonical(v) == canon, f"variant {v} {links[v]}"
+    assert own > 0  # some variants fail the source's own links
+
+
+def test_route_updates_empty_sweep(product):
+    vr = product.VariantRunner(True, False)
+    vr.setup("wan", dict(nodes=50, seed=3, prefixesPerNode=1), "0", 10, 0xC4F, 500, 0, 0)
+    assert vr.num_variants() == 0
+    vr.launch(0, True)
+    vr.fetch_updates(0)
+    assert vr.total_changes() == 0
