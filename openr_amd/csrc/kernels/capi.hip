@@ -179,8 +179,8 @@ int ogs_set_option(const char* name, int64_t value) {
     return OGS_OK;
   }
   if (std::strcmp(name, "spf_queue") == 0) {
-    if (value < -1 || value > 2) {
-      return fail(OGS_E_INVALID, "spf_queue must be -1, 0, 1 or 2");
+    if (value < -1 || value > 3) {
+      return fail(OGS_E_INVALID, "spf_queue must be -1, 0, 1, 2 or 3");
     }
     ogs::g_spfQueue = int(value);
     return OGS_OK;

@@ -429,7 +429,12 @@ __device__ __forceinline__ void queue_spf(
 // half the rounds (a node's final push carries its final word; contributions
 // of a pred survive only while it stays tight, since a strictly shorter path
 // resets the word).
-template <bool MODS>
+// FOLD: the push stamp lives in bits 48..63 of the packed word itself
+// ({dist | nh<<32 | stamp<<48}, next-hop sets of <= 16 link slots): the CAS
+// that improves a node also claims its push for round r+1, so there is no
+// separate stamp array (4 B/node less LDS) and no second atomic per update.
+// The stamp bits are cleared when the SPF ends.
+template <bool MODS, bool FOLD = false>
 __device__ __forceinline__ void queue_spf_packed(
     uint32_t N, uint32_t s, const uint64_t* __restrict__ edges,
     const uint32_t* __restrict__ gRow, uint32_t e0,
@@ -441,7 +446,7 @@ __device__ __forceinline__ void queue_spf_packed(
   const int tid = threadIdx.x;
   for (uint32_t v = tid; v < N; v += kBlock) {
     dn[v] = (v == s) ? 0ull : uint64_t(kInf);
-    stamp[v] = 0u;
+    if constexpr (!FOLD) stamp[v] = 0u;
   }
   for (uint32_t v = tid; ninfo && v <= N; v += kBlock) {  // nullptr: CSR reads
     ninfo[v] = (gRow[v] - e0) |
@@ -471,7 +476,9 @@ __device__ __forceinline__ void queue_spf_packed(
       const uint32_t rowEnd = ninfo ? (ninfo[v + 1] & ~kDrained) : gRow[v + 1] - e0;
       if (v != s && (iv & kDrained)) continue;  // LinkState.cpp:741-752
       const uint64_t xv = dn[v];
-      const uint32_t dv = static_cast<uint32_t>(xv), nv = static_cast<uint32_t>(xv >> 32);
+      const uint32_t dv = static_cast<uint32_t>(xv);
+      const uint32_t nv = FOLD ? static_cast<uint32_t>(xv >> 32) & 0xFFFFu  // not the stamp
+                               : static_cast<uint32_t>(xv >> 32);
       for_row(edges, b, rowEnd - b, [&](uint32_t e, uint64_t x) {
         const uint32_t lo = static_cast<uint32_t>(x);
         if (lo & OGS_EDGE_DOWN) return;
@@ -483,24 +490,34 @@ __device__ __forceinline__ void queue_spf_packed(
         // the source contributes the link slot (its row index), others NH(v)
         const uint32_t bits = (v == s) ? (1u << (e - b)) : nv;
         uint64_t old = dn[t];
+        bool push = false;
         for (;;) {
-          const uint32_t dt = static_cast<uint32_t>(old), nt = static_cast<uint32_t>(old >> 32);
+          const uint32_t dt = static_cast<uint32_t>(old);
+          const uint32_t nt = FOLD ? static_cast<uint32_t>(old >> 32) & 0xFFFFu
+                                   : static_cast<uint32_t>(old >> 32);
           if (c > dt || (c == dt && !(bits & ~nt))) return;
-          const uint64_t nw = c < dt ? (uint64_t(c) | (uint64_t(bits) << 32))
-                                     : (uint64_t(dt) | (uint64_t(nt | bits) << 32));
+          uint64_t nw = c < dt ? (uint64_t(c) | (uint64_t(bits) << 32))
+                               : (uint64_t(dt) | (uint64_t(nt | bits) << 32));
+          if constexpr (FOLD) nw |= uint64_t(r + 1) << 48;
           const uint64_t seen = atomicCAS(reinterpret_cast<unsigned long long*>(&dn[t]),
                                           static_cast<unsigned long long>(old),
                                           static_cast<unsigned long long>(nw));
-          if (seen == old) break;
+          if (seen == old) {
+            if constexpr (FOLD) push = uint32_t(old >> 48) < r + 1;
+            break;
+          }
           old = seen;
         }
-        if (atomicMax(&stamp[t], r + 1) < r + 1) {
-          nxt[atomicAdd(&qcnt[(r + 1) % 3], 1u)] = uint16_t(t);
-        }
+        if constexpr (!FOLD) push = atomicMax(&stamp[t], r + 1) < r + 1;
+        if (push) nxt[atomicAdd(&qcnt[(r + 1) % 3], 1u)] = uint16_t(t);
       });
     }
     __syncthreads();
     n = qcnt[(r + 1) % 3];
+  }
+  if constexpr (FOLD) {  // the plain packed form for everything downstream
+    for (uint32_t v = tid; v < N; v += kBlock) dn[v] &= 0x0000FFFFFFFFFFFFull;
+    __syncthreads();
   }
 #ifdef OGS_STAMPS
   tp[1] = tp[2] = __builtin_amdgcn_s_memtime();
@@ -509,11 +526,13 @@ __device__ __forceinline__ void queue_spf_packed(
 #endif
 }
 
-uint32_t frontier_lds_bytes(uint32_t Sn, int W, bool queue = false, bool ninfo = true) {
+uint32_t frontier_lds_bytes(uint32_t Sn, int W, bool queue = false, bool ninfo = true,
+                            bool stamps = true) {
   const uint32_t core = 4u * (((Sn + 3u) & ~3u) + ((Sn * W + 3u) & ~3u));
   if (!queue) return core + 2u * ((Sn + 1u) & ~1u);
-  // + u32 stamps + two u16 node lists (+ u32 node info [Sn + 1])
-  return core + 4u * ((Sn + 3u) & ~3u) + 2u * 2u * ((Sn + 1u) & ~1u) +
+  // + u32 stamps (not with folded stamps) + two u16 node lists (+ u32 node
+  // info [Sn + 1])
+  return core + (stamps ? 4u * ((Sn + 3u) & ~3u) : 0u) + 2u * 2u * ((Sn + 1u) & ~1u) +
       (ninfo ? 4u * ((Sn + 4u) & ~3u) : 0u);
 }
 
@@ -550,7 +569,10 @@ __global__ __launch_bounds__(kBlock) void spf_frontier_kernel(
   uint16_t* stamp = reinterpret_cast<uint16_t*>(nh + ((Sn * W + 3u) & ~3u));  // [Sn]
   // queue form: u32 stamps [Sn] over the same start, then two u16 lists
   uint32_t* stamp32 = reinterpret_cast<uint32_t*>(stamp);
-  uint16_t* q0 = reinterpret_cast<uint16_t*>(stamp32 + ((Sn + 3u) & ~3u));
+  // folded stamps (QMODE 3): no stamp array, the lists start there (and the
+  // per-node route flags below reuse the dead lists)
+  uint16_t* q0 = QMODE == 3 ? stamp
+                            : reinterpret_cast<uint16_t*>(stamp32 + ((Sn + 3u) & ~3u));
   uint16_t* q1 = q0 + ((Sn + 1u) & ~1u);
   uint32_t* ninfo = (flags & kFlagNinfoGlobal)
       ? nullptr
@@ -569,11 +591,11 @@ __global__ __launch_bounds__(kBlock) void spf_frontier_kernel(
   const uint64_t t0 = __builtin_amdgcn_s_memtime();
   const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
 #endif
-  constexpr bool PACKED = QMODE == 2;
+  constexpr bool PACKED = QMODE >= 2;
   static_assert(!PACKED || W == 1, "packed words hold one next-hop word");
   uint64_t* dn64 = reinterpret_cast<uint64_t*>(smem);  // PACKED: over dist + nh
   if constexpr (PACKED) {
-    queue_spf_packed<MODS>(N, s, g.edges + e0, gRow, e0, nflags,
+    queue_spf_packed<MODS, QMODE == 3>(N, s, g.edges + e0, gRow, e0, nflags,
                            (flags & OGS_F_HOP_METRIC) != 0, dn64, stamp32, q0, q1,
                            qcnt, ninfo, tp, dead);
   } else if constexpr (QMODE == 1) {
@@ -661,8 +683,9 @@ __global__ __launch_bounds__(kBlock) void spf_frontier_kernel(
 
 // "spf_queue" option: -1 (default) the queue form for sparse topologies
 // (max degree <= 16, <= 65,535 nodes; one-phase packed words when the
-// next-hop sets fit one word), 0 never, 1 whenever it fits, 2 the two-phase
-// queue form even for one-word sets (A/B).
+// next-hop sets fit one word, with the push stamps folded into the words
+// when max degree <= 16), 0 never, 1 whenever it fits, 2 the two-phase
+// queue form even for one-word sets, 3 packed with folded stamps (A/B).
 int g_spfQueue = -1;
 
 // "spf_ninfo" option: 1 (default) the queue forms keep row begin | drained
@@ -677,12 +700,18 @@ bool ninfo_in_lds(uint32_t Sn, int W) {
       kCu / frontier_lds_bytes(Sn, W, true, false);
 }
 
-// 0 chunk scan, 1 two-phase queue, 2 packed one-phase queue
+// 0 chunk scan, 1 two-phase queue, 2 packed one-phase queue, 3 packed with
+// folded stamps (next-hop sets of <= 16 link slots: max degree <= 16; and
+// < 65,535 rounds) -- only with spf_queue 3: on C4 it is 8 % slower than
+// form 2 at 5 instead of 4 units per CU (the stamp bits make concurrent
+// CASes on a node conflict more), so form 2 stays the default.
 int queue_mode(const ogs_graph& g, int W) {
   if (g_spfQueue == 0 || g.max_nodes > 65535) return 0;
   if (frontier_lds_bytes(uint32_t(g.max_nodes), W, true) > 160u * 1024u) return 0;
   if (g_spfQueue == -1 && g.max_degree > 16) return 0;
-  return (W == 1 && g_spfQueue != 2) ? 2 : 1;
+  if (W != 1 || g_spfQueue == 2) return 1;
+  const bool fold = g_spfQueue == 3 && g.max_degree <= 16 && g.max_nodes < 65000;
+  return fold ? 3 : 2;
 }
 
 template <int W, bool ROUTES, bool MODS, bool DIFF, int QMODE>
@@ -694,7 +723,8 @@ hipError_t launch_frontier_q(const ogs_graph& g, const ogs_prefix_table& pt,
                              hipStream_t stream, const ogs_unit_mods& mods,
                              const ogs_route_diff& diff) {
   const bool ninfo = QMODE == 0 || ninfo_in_lds(uint32_t(g.max_nodes), W);
-  const uint32_t lds = frontier_lds_bytes(uint32_t(g.max_nodes), W, QMODE != 0, ninfo);
+  const uint32_t lds =
+      frontier_lds_bytes(uint32_t(g.max_nodes), W, QMODE != 0, ninfo, QMODE != 3);
   if (!ninfo) flags |= kFlagNinfoGlobal;
   auto k = spf_frontier_kernel<W, ROUTES, MODS, DIFF, QMODE>;
   if (lds > 64 * 1024) {
@@ -719,6 +749,11 @@ hipError_t launch_frontier(const ogs_graph& g, const ogs_prefix_table& pt,
                            const ogs_route_diff& diff = {}) {
   const int qm = queue_mode(g, W);
   if constexpr (W == 1) {
+    if (qm == 3) {
+      return launch_frontier_q<W, ROUTES, MODS, DIFF, 3>(
+          g, pt, key, chunks, nChunk, units, nUnits, flags, dist, nh, out, stream,
+          mods, diff);
+    }
     if (qm == 2) {
       return launch_frontier_q<W, ROUTES, MODS, DIFF, 2>(
           g, pt, key, chunks, nChunk, units, nUnits, flags, dist, nh, out, stream,

@@ -105,10 +105,10 @@ def test_route_updates_need_records(product):
         vr.fetch_updates(0)
 
 
-@pytest.mark.parametrize("ninfo,queue", [(0, 2), (0, 1), (-1, -1), (1, 1)])
+@pytest.mark.parametrize("ninfo,queue", [(0, 2), (0, 1), (-1, -1), (1, 1), (1, 3), (0, -1)])
 def test_queue_forms_node_info_option(product, oracle, ninfo, queue):
-    """The queue SPF forms (packed one-phase = spf_queue 2 when one next-hop
-    word, two-phase = 1) with node info in LDS (spf_ninfo 1) or read from the
+    """The queue SPF forms (packed one-phase = the default and spf_queue 1,
+    packed with folded push stamps = 3, two-phase = 2) with node info in LDS (spf_ninfo 1) or read from the
     CSR (0; -1 = whenever it raises units per CU): same variant RouteDbs and
     diffs, and the same plain RouteDbs, as the oracle."""
     import openr_amd.capi as capi
