@@ -17,7 +17,15 @@ KERNEL_H := $(wildcard openr_amd/csrc/kernels/*.h)
 HOST := $(wildcard openr_amd/csrc/host/*.cpp)
 HOST_H := $(wildcard openr_amd/csrc/host/*.h) include/openr_gpu.h openr_amd/csrc/gen/topogen.h
 
-all: $(LIB) $(MOD) oracle
+CCONS := tests/c_consumer/spf_square
+
+all: $(LIB) $(MOD) oracle $(CCONS)
+
+# plain-C consumer of the C-ABI (tests/test_capi.py runs it)
+$(CCONS): tests/c_consumer/spf_square.c include/openr_gpu.h $(LIB)
+	gcc -std=c11 -O2 -Wall -Iinclude $< -o $@ -Lopenr_amd/lib -lopenr_gpu \
+	  -Wl,-rpath,'$$ORIGIN/../../openr_amd/lib'
+
 
 $(LIB): $(KERNELS) $(KERNEL_H) include/openr_gpu.h
 	@mkdir -p openr_amd/lib
@@ -41,7 +49,7 @@ $(STAMPS): $(KERNELS) $(KERNEL_H) include/openr_gpu.h
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -shared -DOGS_STAMPS -Iinclude $(KERNELS) -o $@
 
 clean:
-	rm -f $(LIB) $(MOD) $(STAMPS)
+	rm -f $(LIB) $(MOD) $(STAMPS) $(CCONS)
 	$(MAKE) -C oracle clean
 
 .PHONY: all oracle clean stamps
