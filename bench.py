@@ -425,10 +425,19 @@ def run_c5(args, torch, dist, rank, world, local_rank):
     r.set_policy(pol)
     stream = torch.cuda.current_stream(dev)
     sptr = stream.cuda_stream
+    # the RouteDb (+ policy) and the KSP2 batch are independent: with
+    # --c5-streams 2 the KSP2 launches run on a second HIP stream, overlapped
+    side = torch.cuda.Stream(dev) if args.c5_streams > 1 else stream
 
     def job():
+        fork = torch.cuda.Event()
+        fork.record(stream)
+        side.wait_event(fork)
         r.launch_routes(sptr)
-        r.launch_ksp(sptr)
+        r.launch_ksp(side.cuda_stream)
+        join = torch.cuda.Event()
+        join.record(side)
+        stream.wait_event(join)
 
     for _ in range(warmup):
         job()
@@ -543,6 +552,8 @@ def main():
     ap.add_argument("--no-c5", action="store_true",
                     help="skip the C5 multi-area KSP2 + UCMP line embedded in the C2 result")
     ap.add_argument("--c5-steps", type=int, default=5)
+    ap.add_argument("--c5-streams", type=int, default=2, choices=[1, 2],
+                    help="C5: HIP streams (RouteDb+policy || KSP2)")
     ap.add_argument("--opt", action="append", default=[],
                     help="engine option name=value (ogs_set_option), for A/B runs")
     args = ap.parse_args()
