@@ -1,0 +1,747 @@
+// lsdb_codec.cpp — compact-protocol decode of KvStore publications and the
+// Decision per-key ingestion step (§8(f) f4). See lsdb_codec.h for the
+// reference interfaces replaced.
+//
+// Wire format (thrift compact protocol, as written by fbthrift's
+// CompactSerializer): a struct is a run of field headers closed by a 0 byte.
+// A header byte carries (id delta << 4 | type) when 1 <= delta <= 15, else
+// (type) followed by the zigzag-varint i16 id. Booleans live in the header's
+// type nibble (1 true / 2 false). i16/i32/i64 are zigzag varints, strings and
+// binaries a varint length + bytes, lists/sets a (size << 4 | elem) byte
+// (size >= 15: 0xF0 | elem then a varint size), maps a varint size then
+// (key << 4 | value) when non-empty.
+#include "lsdb_codec.h"
+
+#include <arpa/inet.h>
+
+#include <cstring>
+
+namespace openr_amd {
+namespace {
+
+enum CType : uint8_t {
+  CT_STOP = 0,
+  CT_TRUE = 1,
+  CT_FALSE = 2,
+  CT_BYTE = 3,
+  CT_I16 = 4,
+  CT_I32 = 5,
+  CT_I64 = 6,
+  CT_DOUBLE = 7,
+  CT_BINARY = 8,
+  CT_LIST = 9,
+  CT_SET = 10,
+  CT_MAP = 11,
+  CT_STRUCT = 12,
+  CT_FLOAT = 13,
+};
+
+constexpr int kMaxDepth = 64;
+
+[[noreturn]] void fail(const char* what) { throw LsdbDecodeError(what); }
+
+class Reader {
+ public:
+  explicit Reader(std::string_view b)
+      : p_(reinterpret_cast<const uint8_t*>(b.data())), e_(p_ + b.size()) {}
+
+  uint8_t byte() {
+    if (p_ >= e_) fail("compact: truncated input");
+    return *p_++;
+  }
+  uint64_t varint() {
+    uint64_t v = 0;
+    for (int shift = 0; shift < 70; shift += 7) {
+      uint8_t b = byte();
+      v |= uint64_t(b & 0x7f) << shift;
+      if (!(b & 0x80)) return v;
+    }
+    fail("compact: varint too long");
+  }
+  int64_t zz64() {
+    uint64_t u = varint();
+    return int64_t(u >> 1) ^ -int64_t(u & 1);
+  }
+  int32_t zz32() {
+    int64_t v = zz64();
+    if (v < INT32_MIN || v > INT32_MAX) fail("compact: i32 out of range");
+    return int32_t(v);
+  }
+  int16_t zz16() {
+    int64_t v = zz64();
+    if (v < INT16_MIN || v > INT16_MAX) fail("compact: i16 out of range");
+    return int16_t(v);
+  }
+  std::string_view bytes() {
+    uint64_t n = varint();
+    if (n > uint64_t(e_ - p_)) fail("compact: string past end of input");
+    std::string_view s(reinterpret_cast<const char*>(p_), size_t(n));
+    p_ += n;
+    return s;
+  }
+  void skipN(uint64_t n) {
+    if (n > uint64_t(e_ - p_)) fail("compact: truncated input");
+    p_ += n;
+  }
+  // list / set header -> (elem type, size)
+  std::pair<uint8_t, uint32_t> listHeader() {
+    uint8_t h = byte();
+    uint64_t n = h >> 4;
+    if (n == 15) n = varint();
+    // every element occupies at least one byte on the wire
+    if (n > uint64_t(e_ - p_)) fail("compact: container size past end of input");
+    return {uint8_t(h & 0x0f), uint32_t(n)};
+  }
+
+  // field header; returns false at the struct's stop byte
+  bool field(int16_t& lastId, int16_t& id, uint8_t& type) {
+    uint8_t h = byte();
+    if (h == CT_STOP) return false;
+    type = h & 0x0f;
+    uint8_t delta = h >> 4;
+    id = delta ? int16_t(lastId + delta) : zz16();
+    lastId = id;
+    return true;
+  }
+
+  bool boolElem() {
+    uint8_t b = byte();
+    // fbthrift writes 1 / 2 (CT_TRUE / CT_FALSE); accept 0 as false too
+    if (b == CT_TRUE) return true;
+    if (b == CT_FALSE || b == 0) return false;
+    fail("compact: bad bool element");
+  }
+
+  void skip(uint8_t type, int depth = 0) {
+    if (depth > kMaxDepth) fail("compact: nesting too deep");
+    switch (type) {
+      case CT_TRUE:
+      case CT_FALSE:
+        return;  // field-header bool: value is in the type nibble
+      case CT_BYTE:
+        skipN(1);
+        return;
+      case CT_I16:
+      case CT_I32:
+      case CT_I64:
+        varint();
+        return;
+      case CT_DOUBLE:
+        skipN(8);
+        return;
+      case CT_FLOAT:
+        skipN(4);
+        return;
+      case CT_BINARY:
+        bytes();
+        return;
+      case CT_LIST:
+      case CT_SET: {
+        auto [et, n] = listHeader();
+        for (uint32_t i = 0; i < n; ++i) skipElem(et, depth + 1);
+        return;
+      }
+      case CT_MAP: {
+        uint64_t n = varint();
+        if (n == 0) return;
+        if (n > uint64_t(e_ - p_)) fail("compact: map size past end of input");
+        uint8_t kv = byte();
+        for (uint64_t i = 0; i < n; ++i) {
+          skipElem(kv >> 4, depth + 1);
+          skipElem(kv & 0x0f, depth + 1);
+        }
+        return;
+      }
+      case CT_STRUCT: {
+        int16_t last = 0, id;
+        uint8_t t;
+        while (field(last, id, t)) skip(t, depth + 1);
+        return;
+      }
+      default:
+        fail("compact: unknown wire type");
+    }
+  }
+  // container elements: bools take a byte of their own
+  void skipElem(uint8_t type, int depth) {
+    if (type == CT_TRUE || type == CT_FALSE) {
+      boolElem();
+      return;
+    }
+    skip(type, depth);
+  }
+
+  bool done() const { return p_ == e_; }
+
+ private:
+  const uint8_t* p_;
+  const uint8_t* e_;
+};
+
+bool isBoolType(uint8_t t) { return t == CT_TRUE || t == CT_FALSE; }
+
+// BinaryAddress (Network.thrift:49-52) -> raw addr bytes (ifName dropped)
+std::string_view readBinaryAddress(Reader& r) {
+  std::string_view addr;
+  int16_t last = 0, id;
+  uint8_t t;
+  while (r.field(last, id, t)) {
+    if (id == 1 && t == CT_BINARY) {
+      addr = r.bytes();
+    } else {
+      r.skip(t, 1);
+    }
+  }
+  return addr;
+}
+
+std::string readAddressText(Reader& r) {
+  return binaryAddressToString(readBinaryAddress(r));
+}
+
+void readPerfEvents(Reader& r, std::vector<PerfEvent>& out) {  // Types.thrift:80-95
+  int16_t last = 0, id;
+  uint8_t t;
+  while (r.field(last, id, t)) {
+    if (id == 1 && t == CT_LIST) {
+      auto [et, n] = r.listHeader();
+      if (et != CT_STRUCT) {
+        for (uint32_t i = 0; i < n; ++i) r.skipElem(et, 2);
+        continue;
+      }
+      out.reserve(n);
+      for (uint32_t i = 0; i < n; ++i) {
+        PerfEvent ev;
+        int16_t l2 = 0, id2;
+        uint8_t t2;
+        while (r.field(l2, id2, t2)) {
+          if (id2 == 1 && t2 == CT_BINARY) ev.nodeName = r.bytes();
+          else if (id2 == 2 && t2 == CT_BINARY) ev.eventDescr = r.bytes();
+          else if (id2 == 3 && t2 == CT_I64) ev.unixTs = r.zz64();
+          else r.skip(t2, 3);
+        }
+        out.push_back(std::move(ev));
+      }
+    } else {
+      r.skip(t, 1);
+    }
+  }
+}
+
+Adjacency readAdjacency(Reader& r) {  // Types.thrift:145-215
+  Adjacency a;
+  int16_t last = 0, id;
+  uint8_t t;
+  while (r.field(last, id, t)) {
+    switch (id) {
+      case 1:
+        if (t == CT_BINARY) { a.otherNodeName = r.bytes(); continue; }
+        break;
+      case 2:
+        if (t == CT_BINARY) { a.ifName = r.bytes(); continue; }
+        break;
+      case 3:
+        if (t == CT_STRUCT) { a.nextHopV6 = readAddressText(r); continue; }
+        break;
+      case 5:
+        if (t == CT_STRUCT) { a.nextHopV4 = readAddressText(r); continue; }
+        break;
+      case 4:
+        if (t == CT_I32) { a.metric = r.zz32(); continue; }
+        break;
+      case 6:
+        if (t == CT_I32) { a.adjLabel = r.zz32(); continue; }
+        break;
+      case 7:
+        if (isBoolType(t)) { a.isOverloaded = t == CT_TRUE; continue; }
+        break;
+      case 8:
+        if (t == CT_I32) { a.rtt = r.zz32(); continue; }
+        break;
+      case 9:
+        if (t == CT_I64) { a.timestamp = r.zz64(); continue; }
+        break;
+      case 10:
+        if (t == CT_I64) { a.weight = r.zz64(); continue; }
+        break;
+      case 11:
+        if (t == CT_BINARY) { a.otherIfName = r.bytes(); continue; }
+        break;
+      case 12:
+        if (isBoolType(t)) { a.adjOnlyUsedByOtherNode = t == CT_TRUE; continue; }
+        break;
+    }
+    r.skip(t, 1);
+  }
+  return a;
+}
+
+std::string readIpPrefix(Reader& r) {  // Network.thrift:55-58
+  std::string addr;
+  int16_t len = 0;
+  int16_t last = 0, id;
+  uint8_t t;
+  while (r.field(last, id, t)) {
+    if (id == 1 && t == CT_STRUCT) addr = std::string(readBinaryAddress(r));
+    else if (id == 2 && t == CT_I16) len = r.zz16();
+    else r.skip(t, 2);
+  }
+  return ipPrefixToNetworkString(addr, len);
+}
+
+void readMetrics(Reader& r, PrefixMetrics& m) {  // Types.thrift:287-317
+  int16_t last = 0, id;
+  uint8_t t;
+  while (r.field(last, id, t)) {
+    if (t == CT_I32 && id >= 1 && id <= 5) {
+      int32_t v = r.zz32();
+      switch (id) {
+        case 1: m.version = v; break;
+        case 2: m.path_preference = v; break;
+        case 3: m.source_preference = v; break;
+        case 4: m.distance = v; break;
+        case 5: m.drain_metric = v; break;
+      }
+    } else {
+      r.skip(t, 2);
+    }
+  }
+}
+
+void readStringList(Reader& r, uint8_t t, std::vector<std::string>* vec,
+                    std::set<std::string>* set) {
+  auto [et, n] = r.listHeader();
+  if (et != CT_BINARY) {
+    for (uint32_t i = 0; i < n; ++i) r.skipElem(et, 2);
+    return;
+  }
+  (void)t;
+  for (uint32_t i = 0; i < n; ++i) {
+    std::string_view s = r.bytes();
+    if (vec) vec->emplace_back(s);
+    else set->emplace(s);
+  }
+}
+
+PrefixEntry readPrefixEntry(Reader& r) {  // Types.thrift:349-408
+  PrefixEntry e;
+  int16_t last = 0, id;
+  uint8_t t;
+  while (r.field(last, id, t)) {
+    switch (id) {
+      case 1:
+        if (t == CT_STRUCT) { e.prefix = readIpPrefix(r); continue; }
+        break;
+      case 2:
+        if (t == CT_I32) { e.type = r.zz32(); continue; }
+        break;
+      case 4:
+        if (t == CT_I32) { e.forwardingType = r.zz32(); continue; }
+        break;
+      case 7:
+        if (t == CT_I32) { e.forwardingAlgorithm = r.zz32(); continue; }
+        break;
+      case 8:
+        if (t == CT_I64) { e.minNexthop = r.zz64(); continue; }
+        break;
+      case 10:
+        if (t == CT_STRUCT) { readMetrics(r, e.metrics); continue; }
+        break;
+      case 11:
+        if (t == CT_SET) { readStringList(r, t, nullptr, &e.tags); continue; }
+        break;
+      case 12:
+        if (t == CT_LIST) { readStringList(r, t, &e.area_stack, nullptr); continue; }
+        break;
+      case 13:
+        if (t == CT_I64) { e.weight = r.zz64(); continue; }
+        break;
+    }
+    r.skip(t, 1);
+  }
+  return e;
+}
+
+// ------------------------------------------------------------- writer --
+class Writer {
+ public:
+  std::string out;
+  void byte(uint8_t b) { out.push_back(char(b)); }
+  void varint(uint64_t v) {
+    while (v >= 0x80) {
+      byte(uint8_t(v | 0x80));
+      v >>= 7;
+    }
+    byte(uint8_t(v));
+  }
+  void zz(int64_t v) { varint((uint64_t(v) << 1) ^ uint64_t(v >> 63)); }
+  void bytes(std::string_view s) {
+    varint(s.size());
+    out.append(s.data(), s.size());
+  }
+  void field(int16_t& last, int16_t id, uint8_t type) {
+    int d = id - last;
+    if (d > 0 && d <= 15) {
+      byte(uint8_t(d << 4 | type));
+    } else {
+      byte(type);
+      zz(id);
+    }
+    last = id;
+  }
+  void boolField(int16_t& last, int16_t id, bool v) { field(last, id, v ? CT_TRUE : CT_FALSE); }
+  void listHeader(uint8_t et, size_t n) {
+    if (n < 15) {
+      byte(uint8_t(n << 4 | et));
+    } else {
+      byte(uint8_t(0xf0 | et));
+      varint(n);
+    }
+  }
+  void stop() { byte(CT_STOP); }
+};
+
+void writeBinaryAddress(Writer& w, const std::string& text) {
+  int16_t last = 0;
+  w.field(last, 1, CT_BINARY);
+  w.bytes(stringToBinaryAddress(text));
+  w.stop();
+}
+
+void writeAdjacency(Writer& w, const Adjacency& a) {
+  int16_t l = 0;
+  w.field(l, 1, CT_BINARY); w.bytes(a.otherNodeName);
+  w.field(l, 2, CT_BINARY); w.bytes(a.ifName);
+  w.field(l, 3, CT_STRUCT); writeBinaryAddress(w, a.nextHopV6);
+  w.field(l, 4, CT_I32); w.zz(a.metric);
+  w.field(l, 5, CT_STRUCT); writeBinaryAddress(w, a.nextHopV4);
+  w.field(l, 6, CT_I32); w.zz(a.adjLabel);
+  w.boolField(l, 7, a.isOverloaded);
+  w.field(l, 8, CT_I32); w.zz(a.rtt);
+  w.field(l, 9, CT_I64); w.zz(a.timestamp);
+  w.field(l, 10, CT_I64); w.zz(a.weight);
+  w.field(l, 11, CT_BINARY); w.bytes(a.otherIfName);
+  w.boolField(l, 12, a.adjOnlyUsedByOtherNode);
+  w.stop();
+}
+
+void writePerfEvents(Writer& w, const std::vector<PerfEvent>& evs) {
+  int16_t l = 0;
+  w.field(l, 1, CT_LIST);
+  w.listHeader(CT_STRUCT, evs.size());
+  for (const auto& ev : evs) {
+    int16_t l2 = 0;
+    w.field(l2, 1, CT_BINARY); w.bytes(ev.nodeName);
+    w.field(l2, 2, CT_BINARY); w.bytes(ev.eventDescr);
+    w.field(l2, 3, CT_I64); w.zz(ev.unixTs);
+    w.stop();
+  }
+  w.stop();
+}
+
+void writePrefixEntry(Writer& w, const PrefixEntry& e) {
+  int16_t l = 0;
+  auto slash = e.prefix.rfind('/');
+  if (slash == std::string::npos) throw std::invalid_argument("prefix without length: " + e.prefix);
+  w.field(l, 1, CT_STRUCT);
+  {
+    int16_t l2 = 0;
+    w.field(l2, 1, CT_STRUCT); writeBinaryAddress(w, e.prefix.substr(0, slash));
+    w.field(l2, 2, CT_I16); w.zz(std::stoi(e.prefix.substr(slash + 1)));
+    w.stop();
+  }
+  w.field(l, 2, CT_I32); w.zz(e.type);
+  w.field(l, 4, CT_I32); w.zz(e.forwardingType);
+  w.field(l, 7, CT_I32); w.zz(e.forwardingAlgorithm);
+  if (e.minNexthop) { w.field(l, 8, CT_I64); w.zz(*e.minNexthop); }
+  w.field(l, 10, CT_STRUCT);
+  {
+    int16_t l2 = 0;
+    w.field(l2, 1, CT_I32); w.zz(e.metrics.version);
+    w.field(l2, 2, CT_I32); w.zz(e.metrics.path_preference);
+    w.field(l2, 3, CT_I32); w.zz(e.metrics.source_preference);
+    w.field(l2, 4, CT_I32); w.zz(e.metrics.distance);
+    w.field(l2, 5, CT_I32); w.zz(e.metrics.drain_metric);
+    w.stop();
+  }
+  w.field(l, 11, CT_SET);
+  w.listHeader(CT_BINARY, e.tags.size());
+  for (const auto& s : e.tags) w.bytes(s);
+  w.field(l, 12, CT_LIST);
+  w.listHeader(CT_BINARY, e.area_stack.size());
+  for (const auto& s : e.area_stack) w.bytes(s);
+  if (e.weight) { w.field(l, 13, CT_I64); w.zz(*e.weight); }
+  w.stop();
+}
+
+bool parseAddress(const std::string& text, unsigned char buf[16], int& family) {
+  if (text.find(':') != std::string::npos) {
+    family = AF_INET6;
+    return inet_pton(AF_INET6, text.c_str(), buf) == 1;
+  }
+  family = AF_INET;
+  return inet_pton(AF_INET, text.c_str(), buf) == 1;
+}
+
+std::string formatAddress(const unsigned char* raw, int family) {
+  char buf[INET6_ADDRSTRLEN];
+  if (!inet_ntop(family, raw, buf, sizeof buf)) fail("address: inet_ntop failed");
+  return buf;
+}
+
+bool validNodeChar(char c) {  // LsdbTypes.h:452-457 node class
+  return (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z') || (c >= '0' && c <= '9') ||
+         c == '.' || c == '-' || c == '_';
+}
+
+bool validIpChar(char c) {
+  return (c >= 'a' && c <= 'f') || (c >= 'A' && c <= 'F') || (c >= '0' && c <= '9') ||
+         c == '.' || c == ':';
+}
+
+// PrefixKey::fromStr (LsdbTypes.cpp:28-48): "prefix:<node>:[<ip>/<plen>]"
+std::optional<std::pair<std::string, std::string>> parsePrefixKey(const std::string& key) {
+  static const std::string marker = "prefix:";
+  if (key.compare(0, marker.size(), marker) != 0) return std::nullopt;
+  size_t i = marker.size(), n = key.size();
+  // node is greedy over its class; the class excludes ':' so the first ':'
+  // ends it
+  size_t b = i;
+  while (i < n && validNodeChar(key[i])) ++i;
+  if (i == b || i + 1 >= n || key[i] != ':' || key[i + 1] != '[') return std::nullopt;
+  std::string node = key.substr(b, i - b);
+  i += 2;
+  // IPAddr is greedy over [a-fA-F\d.:]+ followed by '/'
+  b = i;
+  while (i < n && validIpChar(key[i])) ++i;
+  if (i == b || i >= n || key[i] != '/') return std::nullopt;
+  std::string ip = key.substr(b, i - b);
+  ++i;
+  b = i;
+  while (i < n && key[i] >= '0' && key[i] <= '9') ++i;
+  if (i == b || i - b > 3 || i + 1 != n || key[i] != ']') return std::nullopt;
+  int plen = std::stoi(key.substr(b, i - b));
+  unsigned char buf[16];
+  int fam;
+  if (!parseAddress(ip, buf, fam)) return std::nullopt;
+  std::string raw(reinterpret_cast<char*>(buf), fam == AF_INET6 ? 16 : 4);
+  try {
+    return std::make_pair(node, ipPrefixToNetworkString(raw, int16_t(plen)));
+  } catch (const LsdbDecodeError&) {
+    return std::nullopt;
+  }
+}
+
+}  // namespace
+
+// ------------------------------------------------------------ public --
+std::string binaryAddressToString(std::string_view raw) {
+  if (raw.empty()) return {};
+  if (raw.size() == 4) return formatAddress(reinterpret_cast<const unsigned char*>(raw.data()), AF_INET);
+  if (raw.size() == 16) return formatAddress(reinterpret_cast<const unsigned char*>(raw.data()), AF_INET6);
+  fail("address: BinaryAddress.addr must be 4 or 16 bytes");  // IPAddress::fromBinary
+}
+
+std::string stringToBinaryAddress(const std::string& text) {
+  if (text.empty()) return {};
+  unsigned char buf[16];
+  int fam;
+  if (!parseAddress(text, buf, fam)) throw std::invalid_argument("bad IP address: " + text);
+  return std::string(reinterpret_cast<char*>(buf), fam == AF_INET6 ? 16 : 4);
+}
+
+// toIPNetwork(prefix, applyMask=true) (NetworkUtil.h:196-208) printed as
+// folly::IPAddress::networkToString: "<masked addr>/<len>"
+std::string ipPrefixToNetworkString(std::string_view raw, int16_t len) {
+  if (raw.size() != 4 && raw.size() != 16) fail("prefix: address must be 4 or 16 bytes");
+  int bits = int(raw.size()) * 8;
+  if (len < 0 || len > bits) fail("prefix: length out of range");
+  unsigned char buf[16];
+  std::memcpy(buf, raw.data(), raw.size());
+  for (int bit = len; bit < bits; ++bit) buf[bit >> 3] &= uint8_t(~(0x80u >> (bit & 7)));
+  return formatAddress(buf, raw.size() == 16 ? AF_INET6 : AF_INET) + "/" + std::to_string(len);
+}
+
+AdjacencyDatabase readAdjacencyDatabase(std::string_view bytes) {  // Types.thrift:223-270
+  Reader r(bytes);
+  AdjacencyDatabase db;
+  int16_t last = 0, id;
+  uint8_t t;
+  while (r.field(last, id, t)) {
+    switch (id) {
+      case 1:
+        if (t == CT_BINARY) { db.thisNodeName = r.bytes(); continue; }
+        break;
+      case 2:
+        if (isBoolType(t)) { db.isOverloaded = t == CT_TRUE; continue; }
+        break;
+      case 3:
+        if (t == CT_LIST) {
+          auto [et, n] = r.listHeader();
+          if (et != CT_STRUCT) {
+            for (uint32_t i = 0; i < n; ++i) r.skipElem(et, 1);
+            continue;
+          }
+          db.adjacencies.reserve(n);
+          for (uint32_t i = 0; i < n; ++i) db.adjacencies.push_back(readAdjacency(r));
+          continue;
+        }
+        break;
+      case 4:
+        if (t == CT_I32) { db.nodeLabel = r.zz32(); continue; }
+        break;
+      case 6:
+        if (t == CT_BINARY) { db.area = r.bytes(); continue; }
+        break;
+      case 7:
+        if (t == CT_I32) { db.nodeMetricIncrementVal = r.zz32(); continue; }
+        break;
+    }
+    r.skip(t, 0);  // perfEvents (5) is not kept by the route path
+  }
+  return db;
+}
+
+PrefixDatabase readPrefixDatabase(std::string_view bytes) {  // Types.thrift:415-430
+  Reader r(bytes);
+  PrefixDatabase db;
+  int16_t last = 0, id;
+  uint8_t t;
+  while (r.field(last, id, t)) {
+    switch (id) {
+      case 1:
+        if (t == CT_BINARY) { db.thisNodeName = r.bytes(); continue; }
+        break;
+      case 3:
+        if (t == CT_LIST) {
+          auto [et, n] = r.listHeader();
+          if (et != CT_STRUCT) {
+            for (uint32_t i = 0; i < n; ++i) r.skipElem(et, 1);
+            continue;
+          }
+          db.prefixEntries.reserve(n);
+          for (uint32_t i = 0; i < n; ++i) db.prefixEntries.push_back(readPrefixEntry(r));
+          continue;
+        }
+        break;
+      case 4:
+        if (t == CT_STRUCT) {
+          db.perfEvents.emplace();
+          readPerfEvents(r, *db.perfEvents);
+          continue;
+        }
+        break;
+      case 5:
+        if (isBoolType(t)) { db.deletePrefix = t == CT_TRUE; continue; }
+        break;
+    }
+    r.skip(t, 0);
+  }
+  return db;
+}
+
+std::string writeAdjacencyDatabase(const AdjacencyDatabase& db) {
+  Writer w;
+  w.out.reserve(64 + 96 * db.adjacencies.size());
+  int16_t l = 0;
+  w.field(l, 1, CT_BINARY); w.bytes(db.thisNodeName);
+  w.boolField(l, 2, db.isOverloaded);
+  w.field(l, 3, CT_LIST);
+  w.listHeader(CT_STRUCT, db.adjacencies.size());
+  for (const auto& a : db.adjacencies) writeAdjacency(w, a);
+  w.field(l, 4, CT_I32); w.zz(db.nodeLabel);
+  w.field(l, 6, CT_BINARY); w.bytes(db.area);
+  w.field(l, 7, CT_I32); w.zz(db.nodeMetricIncrementVal);
+  w.stop();
+  return std::move(w.out);
+}
+
+std::string writePrefixDatabase(const PrefixDatabase& db) {
+  Writer w;
+  int16_t l = 0;
+  w.field(l, 1, CT_BINARY); w.bytes(db.thisNodeName);
+  w.field(l, 3, CT_LIST);
+  w.listHeader(CT_STRUCT, db.prefixEntries.size());
+  for (const auto& e : db.prefixEntries) writePrefixEntry(w, e);
+  if (db.perfEvents) { w.field(l, 4, CT_STRUCT); writePerfEvents(w, *db.perfEvents); }
+  w.boolField(l, 5, db.deletePrefix);
+  w.stop();
+  return std::move(w.out);
+}
+
+std::string getNodeNameFromKey(const std::string& key) {  // LsdbUtil.cpp:691-698
+  size_t a = key.find(':');
+  if (a == std::string::npos) return "";
+  size_t b = key.find(':', a + 1);
+  return key.substr(a + 1, b == std::string::npos ? std::string::npos : b - a - 1);
+}
+
+LsdbKeyUpdate LsdbIngest::updateKeyInLsdb(const std::string& area, LinkState& areaLinkState,
+                                          PrefixState& prefixState, const std::string& key,
+                                          const std::optional<std::string_view>& rawVal,
+                                          bool inInitialization) const {
+  LsdbKeyUpdate u;
+  if (!rawVal) return u;  // TTL update (Decision.cpp:716-720)
+  try {
+    if (key.compare(0, 4, "adj:") == 0) {
+      AdjacencyDatabase db = readAdjacencyDatabase(*rawVal);
+      db.area = area;  // Decision.cpp:732
+      u.kind = LsdbKeyUpdate::kAdjacency;
+      u.nodeName = db.thisNodeName;
+      u.linkChange = areaLinkState.updateAdjacencyDatabase(db, area, inInitialization);
+      return u;
+    }
+    if (key.compare(0, 7, "prefix:") == 0) {
+      PrefixDatabase db = readPrefixDatabase(*rawVal);
+      u.nodeName = db.thisNodeName;
+      if (db.prefixEntries.size() != 1) {  // Decision.cpp:750-756
+        u.kind = LsdbKeyUpdate::kError;
+        u.error = "Expecting exactly one entry per prefix key, publication received from " +
+                  db.thisNodeName;
+        return u;
+      }
+      const PrefixEntry& entry = db.prefixEntries.front();
+      // self-redistributed route reflection (Decision.cpp:761-769)
+      if (db.thisNodeName == myNodeName_ && !entry.area_stack.empty() &&
+          areas_.count(entry.area_stack.back())) {
+        return u;
+      }
+      u.kind = LsdbKeyUpdate::kPrefix;
+      u.changedPrefixes = db.deletePrefix
+                              ? prefixState.deletePrefix(db.thisNodeName, area, entry.prefix)
+                              : prefixState.updatePrefix(db.thisNodeName, area, entry);
+      return u;
+    }
+  } catch (const std::exception& e) {  // Decision.cpp:781-784: log, drop the key
+    u = LsdbKeyUpdate{};
+    u.kind = LsdbKeyUpdate::kError;
+    u.error = "Failed to deserialize info for key " + key + ". Exception: " + e.what();
+  }
+  return u;
+}
+
+LsdbKeyUpdate LsdbIngest::deleteKeyFromLsdb(const std::string& area, LinkState& areaLinkState,
+                                            PrefixState& prefixState,
+                                            const std::string& key) const {
+  LsdbKeyUpdate u;
+  if (key.compare(0, 4, "adj:") == 0) {  // Decision.cpp:795-802
+    u.kind = LsdbKeyUpdate::kAdjacency;
+    u.nodeName = getNodeNameFromKey(key);
+    u.linkChange = areaLinkState.deleteAdjacencyDatabase(u.nodeName);
+    return u;
+  }
+  if (key.compare(0, 7, "prefix:") == 0) {  // Decision.cpp:804-818
+    auto pk = parsePrefixKey(key);
+    if (!pk) {
+      u.kind = LsdbKeyUpdate::kError;
+      u.error = "Invalid format for key: " + key + ".";
+      return u;
+    }
+    u.kind = LsdbKeyUpdate::kPrefix;
+    u.nodeName = pk->first;
+    u.changedPrefixes = prefixState.deletePrefix(pk->first, area, pk->second);
+  }
+  return u;
+}
+
+}  // namespace openr_amd

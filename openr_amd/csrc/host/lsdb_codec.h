@@ -1,0 +1,107 @@
+// lsdb_codec.h — KvStore publication decode on the update path (§8(f) f4).
+//
+// Replaces, for the Decision route-computation path:
+//   Decision::updateKeyInLsdb          Decision.cpp:710-785
+//   Decision::deleteKeyFromLsdb        Decision.cpp:787-820
+//   readThriftObjStr<AdjacencyDatabase / PrefixDatabase> with fbthrift's
+//   CompactSerializer (the serializer_ member, Decision.h) over the structs
+//   of Types.thrift:80-95 (PerfEvent[s]), 145-270 (Adjacency[Database]),
+//   283-430 (PrefixMetrics / PrefixEntry / PrefixDatabase) and
+//   Network.thrift:49-58 (BinaryAddress / IpPrefix).
+//
+// The decoder reads the thrift compact protocol directly into the host
+// structs of decision.h (no intermediate thrift objects): strings are copied
+// once, BinaryAddress bytes become the text form the host layer keys on
+// (inet_ntop, which is what folly::IPAddress::str() prints), and IpPrefix
+// becomes the masked "addr/len" network string of toIPNetwork
+// (NetworkUtil.h:196-208). Unknown fields and fields whose wire type does
+// not match the IDL are skipped, as generated thrift readers do; malformed
+// input throws LsdbDecodeError. The encoder is the inverse, used by
+// benchmarks and tests to produce publications.
+#pragma once
+
+#include <cstdint>
+#include <optional>
+#include <set>
+#include <stdexcept>
+#include <string>
+#include <string_view>
+#include <vector>
+
+#include "decision.h"
+
+namespace openr_amd {
+
+struct LsdbDecodeError : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
+struct PerfEvent {  // Types.thrift:80-84
+  std::string nodeName, eventDescr;
+  int64_t unixTs{0};
+};
+
+struct PrefixDatabase {  // Types.thrift:415-430
+  std::string thisNodeName;
+  std::vector<PrefixEntry> prefixEntries;
+  std::optional<std::vector<PerfEvent>> perfEvents;
+  bool deletePrefix{false};
+};
+
+// compact-protocol codecs (fbthrift CompactSerializer wire format)
+AdjacencyDatabase readAdjacencyDatabase(std::string_view bytes);
+PrefixDatabase readPrefixDatabase(std::string_view bytes);
+std::string writeAdjacencyDatabase(const AdjacencyDatabase& db);
+std::string writePrefixDatabase(const PrefixDatabase& db);
+
+// address helpers shared by the codec and its tests
+std::string binaryAddressToString(std::string_view raw);  // "" for empty
+std::string stringToBinaryAddress(const std::string& text);
+std::string ipPrefixToNetworkString(std::string_view raw, int16_t len);
+
+// Decision::getNodeNameFromKey (Decision.cpp:100-110 via LsdbUtil): the text
+// between the first and second ':' of "adj:<node>" / "prefix:<node>:<...>".
+std::string getNodeNameFromKey(const std::string& key);
+
+// Outcome of one key, mirroring what Decision::updateKeyInLsdb feeds into
+// pendingUpdates_ (applyLinkStateChange / applyPrefixStateChange).
+struct LsdbKeyUpdate {
+  enum Kind : int {
+    kSkipped = 0,       // TTL-only update, unknown key, self reflection
+    kAdjacency = 1,     // LinkState updated; linkChange holds the change
+    kPrefix = 2,        // PrefixState updated / deleted; changedPrefixes
+    kError = 3,         // decode failure or malformed publication (logged
+                        // and dropped by the reference, state untouched)
+  };
+  Kind kind{kSkipped};
+  std::string nodeName;
+  LinkState::LinkStateChange linkChange;
+  std::set<std::string> changedPrefixes;
+  std::string error;
+};
+
+// The per-key ingestion step of Decision (Decision.cpp:710-820) for one
+// node: decodes a publication value and applies it to the area's LinkState
+// and the shared PrefixState. `areas` is the set of areas this node has
+// LinkStates for (areaLinkStates_ keys, used by the self-reflection check).
+class LsdbIngest {
+ public:
+  explicit LsdbIngest(std::string myNodeName, std::set<std::string> areas)
+      : myNodeName_(std::move(myNodeName)), areas_(std::move(areas)) {}
+
+  // rawVal == nullopt models a thrift::Value without `value` (TTL refresh).
+  LsdbKeyUpdate updateKeyInLsdb(const std::string& area, LinkState& areaLinkState,
+                                PrefixState& prefixState, const std::string& key,
+                                const std::optional<std::string_view>& rawVal,
+                                bool inInitialization = false) const;
+
+  LsdbKeyUpdate deleteKeyFromLsdb(const std::string& area, LinkState& areaLinkState,
+                                  PrefixState& prefixState,
+                                  const std::string& key) const;
+
+ private:
+  std::string myNodeName_;
+  std::set<std::string> areas_;
+};
+
+}  // namespace openr_amd

@@ -1,6 +1,7 @@
 // openr_amd._decision — Python binding of the GPU drop-in (product path).
 // Exposes the same surface as the CPU oracle binding so tests can drive one
 // scenario through both. Every computation goes through libopenr_gpu.so.
+#include <algorithm>
 #include <chrono>
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
@@ -12,6 +13,7 @@
 
 #include "../gen/topogen.h"
 #include "../host/decision.h"
+#include "../host/lsdb_codec.h"
 
 namespace py = pybind11;
 using namespace openr_amd;
@@ -182,6 +184,80 @@ py::dict fromChange(const LinkState::LinkStateChange& c) {
   return d;
 }
 
+py::dict fromAdjDb(const AdjacencyDatabase& db) {
+  py::dict d;
+  d["thisNodeName"] = db.thisNodeName;
+  d["isOverloaded"] = db.isOverloaded;
+  d["nodeLabel"] = db.nodeLabel;
+  d["area"] = db.area;
+  d["nodeMetricIncrementVal"] = db.nodeMetricIncrementVal;
+  py::list adjs;
+  for (const auto& a : db.adjacencies) {
+    py::dict x;
+    x["otherNodeName"] = a.otherNodeName;
+    x["ifName"] = a.ifName;
+    x["otherIfName"] = a.otherIfName;
+    x["nextHopV6"] = a.nextHopV6;
+    x["nextHopV4"] = a.nextHopV4;
+    x["metric"] = a.metric;
+    x["adjLabel"] = a.adjLabel;
+    x["isOverloaded"] = a.isOverloaded;
+    x["rtt"] = a.rtt;
+    x["timestamp"] = a.timestamp;
+    x["weight"] = a.weight;
+    x["adjOnlyUsedByOtherNode"] = a.adjOnlyUsedByOtherNode;
+    adjs.append(x);
+  }
+  d["adjacencies"] = adjs;
+  return d;
+}
+
+PrefixDatabase toPrefixDb(const py::dict& d) {
+  PrefixDatabase db;
+  db.thisNodeName = get<std::string>(d, "thisNodeName", "");
+  db.deletePrefix = get<bool>(d, "deletePrefix", false);
+  if (d.contains("prefixEntries")) {
+    for (auto h : d["prefixEntries"]) db.prefixEntries.push_back(toEntry(h.cast<py::dict>()));
+  }
+  if (d.contains("perfEvents") && !d["perfEvents"].is_none()) {
+    db.perfEvents.emplace();
+    for (auto h : d["perfEvents"]) {
+      py::tuple t = h.cast<py::tuple>();
+      db.perfEvents->push_back(
+          PerfEvent{t[0].cast<std::string>(), t[1].cast<std::string>(), t[2].cast<int64_t>()});
+    }
+  }
+  return db;
+}
+
+py::dict fromPrefixDb(const PrefixDatabase& db) {
+  py::dict d;
+  d["thisNodeName"] = db.thisNodeName;
+  d["deletePrefix"] = db.deletePrefix;
+  py::list es;
+  for (const auto& e : db.prefixEntries) es.append(fromEntry(e));
+  d["prefixEntries"] = es;
+  if (db.perfEvents) {
+    py::list evs;
+    for (const auto& ev : *db.perfEvents) evs.append(py::make_tuple(ev.nodeName, ev.eventDescr, ev.unixTs));
+    d["perfEvents"] = evs;
+  } else {
+    d["perfEvents"] = py::none();
+  }
+  return d;
+}
+
+py::dict fromKeyUpdate(const LsdbKeyUpdate& u) {
+  py::dict d;
+  d["kind"] = int(u.kind);
+  d["nodeName"] = u.nodeName;
+  d["linkChange"] = u.kind == LsdbKeyUpdate::kAdjacency ? py::object(fromChange(u.linkChange))
+                                                         : py::object(py::none());
+  d["changedPrefixes"] = u.changedPrefixes;
+  d["error"] = u.error;
+  return d;
+}
+
 py::dict fromLink(const Link& l) {
   py::dict d;
   const auto& k = l.key();
@@ -244,40 +320,63 @@ std::string canonical(const DecisionRouteDb& db) {
 }
 
 // ------------------------------------------------------ generated LSDBs ---
+AdjacencyDatabase toAdjacencyDatabase(const topogen::AdjDb& d, const std::string& area) {
+  AdjacencyDatabase db;
+  db.thisNodeName = d.thisNodeName;
+  db.isOverloaded = d.isOverloaded;
+  db.nodeLabel = d.nodeLabel;
+  db.area = area;
+  db.nodeMetricIncrementVal = d.nodeMetricIncrementVal;
+  for (const auto& a : d.adjs) {
+    Adjacency x;
+    x.otherNodeName = a.otherNodeName;
+    x.ifName = a.ifName;
+    x.otherIfName = a.otherIfName;
+    x.nextHopV6 = a.nextHopV6;
+    x.nextHopV4 = a.nextHopV4;
+    x.metric = a.metric;
+    x.adjLabel = a.adjLabel;
+    x.isOverloaded = a.isOverloaded;
+    x.weight = a.weight;
+    db.adjacencies.push_back(x);
+  }
+  return db;
+}
+
+PrefixEntry toPrefixEntry(const topogen::Prefix& p) {
+  PrefixEntry e;
+  e.prefix = p.prefix;
+  e.type = 1;  // LOOPBACK (RoutingBenchmarkUtils.cpp:281)
+  e.metrics.path_preference = p.path_preference;
+  e.metrics.source_preference = p.source_preference;
+  e.metrics.distance = p.distance;
+  e.metrics.drain_metric = p.drain_metric;
+  if (p.minNexthop >= 0) e.minNexthop = p.minNexthop;
+  e.tags.insert(p.tags.begin(), p.tags.end());
+  return e;
+}
+
 void loadLsdb(const topogen::Lsdb& g, LinkState& ls, PrefixState& ps) {
+  for (const auto& d : g.adjDbs) ls.updateAdjacencyDatabase(toAdjacencyDatabase(d, g.area), g.area);
+  for (const auto& p : g.prefixes) ps.updatePrefix(p.node, g.area, toPrefixEntry(p));
+}
+
+// A generated LSDB as one KvStore publication (§8(f) f4): "adj:<node>" ->
+// compact AdjacencyDatabase, "prefix:<node>:[<prefix>]" -> compact
+// PrefixDatabase holding that one entry (the per-prefix key format of
+// PrefixKey, LsdbTypes.cpp:15-26).
+void lsdbPublication(const topogen::Lsdb& g, std::vector<std::string>& keys,
+                     std::vector<std::string>& vals) {
   for (const auto& d : g.adjDbs) {
-    AdjacencyDatabase db;
-    db.thisNodeName = d.thisNodeName;
-    db.isOverloaded = d.isOverloaded;
-    db.nodeLabel = d.nodeLabel;
-    db.area = g.area;
-    db.nodeMetricIncrementVal = d.nodeMetricIncrementVal;
-    for (const auto& a : d.adjs) {
-      Adjacency x;
-      x.otherNodeName = a.otherNodeName;
-      x.ifName = a.ifName;
-      x.otherIfName = a.otherIfName;
-      x.nextHopV6 = a.nextHopV6;
-      x.nextHopV4 = a.nextHopV4;
-      x.metric = a.metric;
-      x.adjLabel = a.adjLabel;
-      x.isOverloaded = a.isOverloaded;
-      x.weight = a.weight;
-      db.adjacencies.push_back(x);
-    }
-    ls.updateAdjacencyDatabase(db, g.area);
+    keys.push_back("adj:" + d.thisNodeName);
+    vals.push_back(writeAdjacencyDatabase(toAdjacencyDatabase(d, g.area)));
   }
   for (const auto& p : g.prefixes) {
-    PrefixEntry e;
-    e.prefix = p.prefix;
-    e.type = 1;  // LOOPBACK (RoutingBenchmarkUtils.cpp:281)
-    e.metrics.path_preference = p.path_preference;
-    e.metrics.source_preference = p.source_preference;
-    e.metrics.distance = p.distance;
-    e.metrics.drain_metric = p.drain_metric;
-    if (p.minNexthop >= 0) e.minNexthop = p.minNexthop;
-    e.tags.insert(p.tags.begin(), p.tags.end());
-    ps.updatePrefix(p.node, g.area, e);
+    PrefixDatabase db;
+    db.thisNodeName = p.node;
+    db.prefixEntries.push_back(toPrefixEntry(p));
+    keys.push_back("prefix:" + p.node + ":[" + p.prefix + "]");
+    vals.push_back(writePrefixDatabase(db));
   }
 }
 
@@ -1007,6 +1106,78 @@ PYBIND11_MODULE(_decision, m) {
         return out;
       });
 
+  // ---- f4: KvStore publication decode (lsdb_codec.h) ----
+  m.def("encodeAdjDb", [](py::dict d) { return py::bytes(writeAdjacencyDatabase(toAdjDb(d))); });
+  m.def("decodeAdjDb", [](py::bytes b) {
+    std::string_view v = b;
+    return fromAdjDb(readAdjacencyDatabase(v));
+  });
+  m.def("encodePrefixDb", [](py::dict d) { return py::bytes(writePrefixDatabase(toPrefixDb(d))); });
+  m.def("decodePrefixDb", [](py::bytes b) {
+    std::string_view v = b;
+    return fromPrefixDb(readPrefixDatabase(v));
+  });
+  m.def("getNodeNameFromKey", &getNodeNameFromKey);
+  py::register_exception<LsdbDecodeError>(m, "LsdbDecodeError", PyExc_ValueError);
+
+  py::class_<LsdbIngest>(m, "LsdbIngest")
+      .def(py::init<std::string, std::set<std::string>>(), py::arg("myNodeName"),
+           py::arg("areas"))
+      .def("updateKeyInLsdb",
+           [](const LsdbIngest& g, const std::string& area, LinkState& ls, PrefixState& ps,
+              const std::string& key, py::object val, bool init) {
+             std::optional<std::string_view> v;
+             std::string hold;
+             if (!val.is_none()) {
+               hold = val.cast<py::bytes>();
+               v = hold;
+             }
+             return fromKeyUpdate(g.updateKeyInLsdb(area, ls, ps, key, v, init));
+           },
+           py::arg("area"), py::arg("linkState"), py::arg("prefixState"), py::arg("key"),
+           py::arg("value"), py::arg("inInitialization") = false)
+      .def("deleteKeyFromLsdb",
+           [](const LsdbIngest& g, const std::string& area, LinkState& ls, PrefixState& ps,
+              const std::string& key) {
+             return fromKeyUpdate(g.deleteKeyFromLsdb(area, ls, ps, key));
+           })
+      // one publication's key/value pairs applied in C++ (bench / bulk load):
+      // returns per-kind counts and the wall time of the loop alone
+      .def("processPublication",
+           [](const LsdbIngest& g, const std::string& area, LinkState& ls, PrefixState& ps,
+              const std::vector<std::string>& keys, const std::vector<py::bytes>& vals,
+              bool init) {
+             if (keys.size() != vals.size()) throw std::invalid_argument("keys/values size");
+             std::vector<std::string> raw;
+             raw.reserve(vals.size());
+             size_t bytes = 0;
+             for (const auto& b : vals) {
+               raw.emplace_back(b);
+               bytes += raw.back().size();
+             }
+             size_t counts[4] = {0, 0, 0, 0};
+             size_t topo = 0;
+             auto t0 = std::chrono::steady_clock::now();
+             for (size_t i = 0; i < keys.size(); ++i) {
+               auto u = g.updateKeyInLsdb(area, ls, ps, keys[i], std::string_view(raw[i]), init);
+               counts[u.kind]++;
+               topo += u.kind == LsdbKeyUpdate::kAdjacency && u.linkChange.topologyChanged;
+             }
+             double ns = std::chrono::duration<double, std::nano>(
+                             std::chrono::steady_clock::now() - t0).count();
+             py::dict d;
+             d["skipped"] = counts[0];
+             d["adjacency"] = counts[1];
+             d["prefix"] = counts[2];
+             d["error"] = counts[3];
+             d["topologyChanged"] = topo;
+             d["bytes"] = bytes;
+             d["ns"] = ns;
+             return d;
+           },
+           py::arg("area"), py::arg("linkState"), py::arg("prefixState"), py::arg("keys"),
+           py::arg("values"), py::arg("inInitialization") = false);
+
   py::class_<RouteDbBatch>(m, "RouteDbBatch")
       .def(py::init<const SpfSolver&, const AreaLinkStates&, const PrefixState&,
                     const std::vector<std::string>&>(),
@@ -1184,6 +1355,64 @@ PYBIND11_MODULE(_decision, m) {
           const auto [rebuildUs, _] = run(false);
           return py::make_tuple(patchUs, rebuildUs, edges, flaps);
         });
+  m.def("gen_publication",
+        [](const std::string& kind, py::dict opts) {
+          auto g = genLsdb(kind, opts);
+          std::vector<std::string> keys, vals;
+          lsdbPublication(g, keys, vals);
+          std::vector<py::bytes> out;
+          out.reserve(vals.size());
+          for (auto& v : vals) out.emplace_back(v);
+          return py::make_tuple(g.area, keys, out);
+        });
+  // f4 bench: encode a generated LSDB, then decode + ingest every key into a
+  // fresh LinkState / PrefixState (Decision::updateKeyInLsdb per key), and
+  // decode alone; medians over `reps`. Host-only (no device call).
+  m.def("publication_ingest_bench",
+        [](const std::string& kind, py::dict opts, int reps) {
+          auto g = genLsdb(kind, opts);
+          std::vector<std::string> keys, vals;
+          lsdbPublication(g, keys, vals);
+          size_t bytes = 0, adjBytes = 0, nAdj = g.adjDbs.size();
+          for (size_t i = 0; i < vals.size(); ++i) {
+            bytes += vals[i].size();
+            if (i < nAdj) adjBytes += vals[i].size();
+          }
+          std::vector<double> ingest, decode;
+          size_t routesKept = 0;
+          for (int r = 0; r < reps; ++r) {
+            LinkState ls(g.area, "test_node");
+            PrefixState ps;
+            LsdbIngest ing("test_node", {g.area});
+            auto t0 = std::chrono::steady_clock::now();
+            for (size_t i = 0; i < keys.size(); ++i) {
+              auto u = ing.updateKeyInLsdb(g.area, ls, ps, keys[i], std::string_view(vals[i]));
+              if (u.kind == LsdbKeyUpdate::kError) throw std::runtime_error(u.error);
+            }
+            auto t1 = std::chrono::steady_clock::now();
+            size_t sink = 0;
+            for (size_t i = 0; i < keys.size(); ++i) {
+              if (i < nAdj) sink += readAdjacencyDatabase(vals[i]).adjacencies.size();
+              else sink += readPrefixDatabase(vals[i]).prefixEntries.size();
+            }
+            auto t2 = std::chrono::steady_clock::now();
+            routesKept = ps.prefixes().size() + (sink & 0);
+            ingest.push_back(std::chrono::duration<double, std::milli>(t1 - t0).count());
+            decode.push_back(std::chrono::duration<double, std::milli>(t2 - t1).count());
+          }
+          std::sort(ingest.begin(), ingest.end());
+          std::sort(decode.begin(), decode.end());
+          py::dict d;
+          d["adj_dbs"] = nAdj;
+          d["prefix_keys"] = keys.size() - nAdj;
+          d["bytes"] = bytes;
+          d["adj_bytes"] = adjBytes;
+          d["prefixes"] = routesKept;
+          d["ingest_ms"] = ingest[ingest.size() / 2];
+          d["decode_ms"] = decode[decode.size() / 2];
+          return d;
+        },
+        py::arg("kind"), py::arg("opts"), py::arg("reps") = 3);
   m.def("gen_route_dbs",
         [](const std::string& kind, py::dict opts, std::vector<std::string> sources,
            bool enableV4, bool sr, bool brs, py::list policy) {
