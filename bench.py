@@ -260,6 +260,20 @@ def run_c3(args, torch, dist, rank, world, local_rank):
                          "routes_per_node": round(routes, 1),
                          "note": "RouteDbBatch (C++ drop-in) over all 2,080 sources, then "
                                  "3 nodes served; rank 0, after the timed region"}
+        # §8(f) f4, host only: the same fabric as one KvStore publication
+        # (2,080 "adj:" + 208k "prefix:" keys, compact thrift) decoded and
+        # ingested per key (Decision::updateKeyInLsdb) into a fresh LSDB
+        pub = openr_amd.decision.publication_ingest_bench(
+            "fabric", dict(pods=32, planes=8, sswPerPlane=36, rswPerPod=48, full=True,
+                           prefixesPerNode=args.prefixes_per_node), 3)
+        keys = pub["adj_dbs"] + pub["prefix_keys"]
+        line["publication_ingest"] = {
+            "keys": keys, "bytes": pub["bytes"], "ingest_ms": round(pub["ingest_ms"], 2),
+            "decode_ms": round(pub["decode_ms"], 2),
+            "keys_per_s": round(keys / pub["ingest_ms"] * 1e3, 1),
+            "decode_MB_per_s": round(pub["bytes"] / pub["decode_ms"] / 1e3, 1),
+            "note": "LsdbIngest (C++ drop-in), 1 host thread, median of 3; rank 0, "
+                    "after the timed region"}
         traffic, src = pmc_traffic("c3", "spf_frontier_kernel")
         if traffic is not None and world == 1:
             line["roofline"]["traffic"] = round(traffic, 1)
@@ -742,7 +756,8 @@ def main():
             line["c3_fabric_all_sources"] = {
                 k: c3[k] for k in ("value", "unit", "ms_per_step", "kernel_ms",
                                    "route_dbs_per_s", "gteps", "routes_per_step",
-                                   "route_digest", "serve", "roofline", "config") if k in c3}
+                                   "route_digest", "serve", "publication_ingest", "roofline",
+                                   "config") if k in c3}
             line["c3_fabric_all_sources"]["steps"] = c3["steps"]
     if not args.no_c4:
         c4 = run_c4(args, torch, dist, rank, world, local_rank)

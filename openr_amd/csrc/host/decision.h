@@ -332,6 +332,8 @@ class PrefixState {
   std::set<std::string> updatePrefix(const std::string& node,
                                      const std::string& area,
                                      const PrefixEntry& entry);
+  std::set<std::string> updatePrefix(const std::string& node,
+                                     const std::string& area, PrefixEntry&& entry);
   std::set<std::string> deletePrefix(const std::string& node,
                                      const std::string& area,
                                      const std::string& prefix);

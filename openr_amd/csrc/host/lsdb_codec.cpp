@@ -483,10 +483,59 @@ bool parseAddress(const std::string& text, unsigned char buf[16], int& family) {
   return inet_pton(AF_INET, text.c_str(), buf) == 1;
 }
 
+char* formatV4(const unsigned char* b, char* o) {
+  for (int i = 0; i < 4; ++i) {
+    if (i) *o++ = '.';
+    unsigned v = b[i];
+    if (v >= 100) *o++ = char('0' + v / 100);
+    if (v >= 10) *o++ = char('0' + v / 10 % 10);
+    *o++ = char('0' + v % 10);
+  }
+  return o;
+}
+
+// inet_ntop's text, without its per-word sprintf: the longest run (first on
+// ties) of >= 2 zero words becomes "::", and ::a.b.c.d / ::ffff:a.b.c.d
+// print the embedded IPv4 address (glibc resolv/inet_ntop.c inet_ntop6 --
+// the form folly::IPAddressV6::str() returns).
 std::string formatAddress(const unsigned char* raw, int family) {
-  char buf[INET6_ADDRSTRLEN];
-  if (!inet_ntop(family, raw, buf, sizeof buf)) fail("address: inet_ntop failed");
-  return buf;
+  char buf[48];
+  char* o = buf;
+  if (family == AF_INET) return std::string(buf, formatV4(raw, o));
+  unsigned w[8];
+  for (int i = 0; i < 8; ++i) w[i] = unsigned(raw[2 * i]) << 8 | raw[2 * i + 1];
+  int bestBase = -1, bestLen = 0, curBase = -1, curLen = 0;
+  for (int i = 0; i < 8; ++i) {
+    if (w[i] == 0) {
+      if (curBase < 0) curBase = i, curLen = 1;
+      else ++curLen;
+    } else if (curBase >= 0) {
+      if (bestBase < 0 || curLen > bestLen) bestBase = curBase, bestLen = curLen;
+      curBase = -1;
+    }
+  }
+  if (curBase >= 0 && (bestBase < 0 || curLen > bestLen)) bestBase = curBase, bestLen = curLen;
+  if (bestBase >= 0 && bestLen < 2) bestBase = -1;
+  static const char hexd[] = "0123456789abcdef";
+  for (int i = 0; i < 8; ++i) {
+    if (bestBase >= 0 && i >= bestBase && i < bestBase + bestLen) {
+      if (i == bestBase) *o++ = ':';
+      continue;
+    }
+    if (i) *o++ = ':';
+    if (i == 6 && bestBase == 0 && (bestLen == 6 || (bestLen == 5 && w[5] == 0xffff))) {
+      o = formatV4(raw + 12, o);
+      return std::string(buf, o);
+    }
+    unsigned v = w[i];
+    bool lead = true;
+    for (int sh = 12; sh >= 0; sh -= 4) {
+      unsigned d = (v >> sh) & 0xf;
+      if (d || !lead || sh == 0) *o++ = hexd[d], lead = false;
+    }
+  }
+  if (bestBase >= 0 && bestBase + bestLen == 8) *o++ = ':';
+  return std::string(buf, o);
 }
 
 bool validNodeChar(char c) {  // LsdbTypes.h:452-457 node class
@@ -700,7 +749,7 @@ LsdbKeyUpdate LsdbIngest::updateKeyInLsdb(const std::string& area, LinkState& ar
                   db.thisNodeName;
         return u;
       }
-      const PrefixEntry& entry = db.prefixEntries.front();
+      PrefixEntry& entry = db.prefixEntries.front();
       // self-redistributed route reflection (Decision.cpp:761-769)
       if (db.thisNodeName == myNodeName_ && !entry.area_stack.empty() &&
           areas_.count(entry.area_stack.back())) {
@@ -709,7 +758,7 @@ LsdbKeyUpdate LsdbIngest::updateKeyInLsdb(const std::string& area, LinkState& ar
       u.kind = LsdbKeyUpdate::kPrefix;
       u.changedPrefixes = db.deletePrefix
                               ? prefixState.deletePrefix(db.thisNodeName, area, entry.prefix)
-                              : prefixState.updatePrefix(db.thisNodeName, area, entry);
+                              : prefixState.updatePrefix(db.thisNodeName, area, std::move(entry));
       return u;
     }
   } catch (const std::exception& e) {  // Decision.cpp:781-784: log, drop the key

@@ -26,6 +26,20 @@ std::set<std::string> PrefixState::updatePrefix(const std::string& node,
   return changed;
 }
 
+std::set<std::string> PrefixState::updatePrefix(const std::string& node,
+                                                const std::string& area,
+                                                PrefixEntry&& entry) {
+  std::set<std::string> changed;  // as above, moving the decoded entry in
+  auto& entries = prefixes_[entry.prefix];
+  auto key = std::make_pair(node, area);
+  auto it = entries.find(key);
+  if (it != entries.end() && *it->second == entry) return changed;
+  changed.insert(entry.prefix);
+  entries[key] = std::make_shared<PrefixEntry>(std::move(entry));
+  ++version_;
+  return changed;
+}
+
 std::set<std::string> PrefixState::deletePrefix(const std::string& node,
                                                 const std::string& area,
                                                 const std::string& prefix) {

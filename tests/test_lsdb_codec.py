@@ -202,6 +202,30 @@ def test_prefix_masking(host_module):
         assert got_p == got_o == want
 
 
+def test_address_text_matches_inet_ntop(host_module):
+    """Every zero/non-zero word pattern of an IPv6 address (and the embedded
+    IPv4 forms) prints as socket.inet_ntop does (the folly str() form)."""
+    import socket
+    M = host_module
+    rng = random.Random(3)
+    addrs = []
+    for mask in range(256):
+        for fill in (1, 0xffff, None):
+            words = [0 if not (mask >> i) & 1 else (fill or rng.randrange(1, 1 << 16)) for i in range(8)]
+            addrs.append(b"".join(w.to_bytes(2, "big") for w in words))
+    addrs += [bytes(10) + b"\xff\xff" + bytes([a, b, c, d])
+              for a, b, c, d in ((1, 2, 3, 4), (0, 0, 0, 0), (255, 255, 255, 255), (10, 0, 0, 1))]
+    addrs += [bytes(12) + bytes([a, b, c, d]) for a, b, c, d in ((1, 2, 3, 4), (0, 0, 0, 1), (0, 0, 1, 0))]
+    adjs = [createAdjacency("n", "i", "o", socket.inet_ntop(socket.AF_INET6, a), "", 1, 1) for a in addrs]
+    for i in range(0, len(adjs), 50):
+        db = createAdjDb("x", adjs[i:i + 50], 1)
+        got = [a["nextHopV6"] for a in M.decodeAdjDb(tc.encode_adj_db(db))["adjacencies"]]
+        assert got == [a["nextHopV6"] for a in adjs[i:i + 50]]
+    for v4 in ("0.0.0.0", "1.2.3.4", "255.255.255.255", "10.100.0.9"):
+        db = createAdjDb("x", [createAdjacency("n", "i", "o", "", v4, 1, 1)], 1)
+        assert M.decodeAdjDb(tc.encode_adj_db(db))["adjacencies"][0]["nextHopV4"] == v4
+
+
 def test_golden_vectors(host_module):
     """Committed vectors (tests/golden/make_f4.py): both decoders give the
     recorded structs and both encoders the recorded bytes."""
