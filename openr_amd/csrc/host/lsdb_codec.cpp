@@ -793,4 +793,34 @@ LsdbKeyUpdate LsdbIngest::deleteKeyFromLsdb(const std::string& area, LinkState& 
   return u;
 }
 
+void DecisionPendingUpdates::apply(const LsdbKeyUpdate& u) {
+  if (u.kind == LsdbKeyUpdate::kAdjacency) applyLinkStateChange(u.nodeName, u.linkChange);
+  else if (u.kind == LsdbKeyUpdate::kPrefix) applyPrefixStateChange(u.changedPrefixes);
+}
+
+void LsdbIngest::processPublication(const std::string& area, AreaLinkStates& areaLinkStates,
+                                    PrefixState& prefixState,
+                                    const std::vector<PublicationKeyVal>& keyVals,
+                                    const std::vector<std::string>& expiredKeys,
+                                    DecisionPendingUpdates& pending,
+                                    bool inInitialization) {
+  if (area.empty()) throw std::invalid_argument("publication without area");  // CHECK
+  auto it = areaLinkStates.find(area);
+  if (it == areaLinkStates.end()) {
+    it = areaLinkStates.emplace(area, LinkState(area, myNodeName_)).first;
+  }
+  areas_.clear();
+  for (const auto& [a, _] : areaLinkStates) areas_.insert(a);
+  LinkState& ls = it->second;
+  if (keyVals.empty() && expiredKeys.empty()) return;
+  std::map<std::string_view, const PublicationKeyVal*> ordered;
+  for (const auto& kv : keyVals) ordered[kv.key] = &kv;
+  for (const auto& [key, kv] : ordered) {
+    std::optional<std::string_view> v;
+    if (kv->value) v = *kv->value;
+    pending.apply(updateKeyInLsdb(area, ls, prefixState, kv->key, v, inInitialization));
+  }
+  for (const auto& key : expiredKeys) pending.apply(deleteKeyFromLsdb(area, ls, prefixState, key));
+}
+
 }  // namespace openr_amd

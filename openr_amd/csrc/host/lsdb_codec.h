@@ -21,6 +21,7 @@
 #pragma once
 
 #include <cstdint>
+#include <map>
 #include <optional>
 #include <set>
 #include <stdexcept>
@@ -59,7 +60,7 @@ std::string binaryAddressToString(std::string_view raw);  // "" for empty
 std::string stringToBinaryAddress(const std::string& text);
 std::string ipPrefixToNetworkString(std::string_view raw, int16_t len);
 
-// Decision::getNodeNameFromKey (Decision.cpp:100-110 via LsdbUtil): the text
+// getNodeNameFromKey (LsdbUtil.cpp:691-698): the text
 // between the first and second ':' of "adj:<node>" / "prefix:<node>:<...>".
 std::string getNodeNameFromKey(const std::string& key);
 
@@ -80,6 +81,46 @@ struct LsdbKeyUpdate {
   std::string error;
 };
 
+// DecisionPendingUpdates (Decision.h:40-105, Decision.cpp:35-60) without the
+// perf-event bookkeeping: what the next rebuildRoutes must do.
+class DecisionPendingUpdates {
+ public:
+  explicit DecisionPendingUpdates(std::string myNodeName) : myNodeName_(std::move(myNodeName)) {}
+  void applyLinkStateChange(const std::string& nodeName, const LinkState::LinkStateChange& c) {
+    // a full rebuild only when link attributes change locally
+    needsFullRebuild_ |= c.topologyChanged || c.nodeLabelChanged ||
+                         (c.linkAttributesChanged && nodeName == myNodeName_);
+    ++count_;
+  }
+  void applyPrefixStateChange(const std::set<std::string>& change) {
+    updatedPrefixes_.insert(change.begin(), change.end());
+    ++count_;
+  }
+  void apply(const LsdbKeyUpdate& u);  // routes kAdjacency / kPrefix results
+  void setNeedsFullRebuild() { needsFullRebuild_ = true; }
+  bool needsFullRebuild() const { return needsFullRebuild_; }
+  bool needsRouteUpdate() const { return needsFullRebuild_ || !updatedPrefixes_.empty(); }
+  const std::set<std::string>& updatedPrefixes() const { return updatedPrefixes_; }
+  uint32_t getCount() const { return count_; }
+  void reset() {
+    count_ = 0;
+    needsFullRebuild_ = false;
+    updatedPrefixes_.clear();
+  }
+
+ private:
+  std::string myNodeName_;
+  uint32_t count_{0};
+  bool needsFullRebuild_{false};
+  std::set<std::string> updatedPrefixes_;
+};
+
+// One KvStore publication's key/values (rawVal nullopt = TTL-only Value).
+struct PublicationKeyVal {
+  std::string key;
+  std::optional<std::string> value;
+};
+
 // The per-key ingestion step of Decision (Decision.cpp:710-820) for one
 // node: decodes a publication value and applies it to the area's LinkState
 // and the shared PrefixState. `areas` is the set of areas this node has
@@ -98,6 +139,18 @@ class LsdbIngest {
   LsdbKeyUpdate deleteKeyFromLsdb(const std::string& area, LinkState& areaLinkState,
                                   PrefixState& prefixState,
                                   const std::string& key) const;
+
+  // Decision::processPublication (Decision.cpp:821-846): the area's LinkState
+  // is created on first sight, keyVals are applied in key order (thrift
+  // KeyVals is a std::map; a repeated key keeps its last value), then the
+  // expired keys are deleted; every applied change lands in `pending`. The
+  // self-reflection area set is refreshed from `areaLinkStates` first.
+  void processPublication(const std::string& area, AreaLinkStates& areaLinkStates,
+                          PrefixState& prefixState,
+                          const std::vector<PublicationKeyVal>& keyVals,
+                          const std::vector<std::string>& expiredKeys,
+                          DecisionPendingUpdates& pending,
+                          bool inInitialization = false);
 
  private:
   std::string myNodeName_;

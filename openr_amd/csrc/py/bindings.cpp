@@ -1120,6 +1120,14 @@ PYBIND11_MODULE(_decision, m) {
   m.def("getNodeNameFromKey", &getNodeNameFromKey);
   py::register_exception<LsdbDecodeError>(m, "LsdbDecodeError", PyExc_ValueError);
 
+  py::class_<DecisionPendingUpdates>(m, "DecisionPendingUpdates")
+      .def(py::init<std::string>())
+      .def("needsFullRebuild", &DecisionPendingUpdates::needsFullRebuild)
+      .def("needsRouteUpdate", &DecisionPendingUpdates::needsRouteUpdate)
+      .def("updatedPrefixes", &DecisionPendingUpdates::updatedPrefixes)
+      .def("getCount", &DecisionPendingUpdates::getCount)
+      .def("reset", &DecisionPendingUpdates::reset);
+
   py::class_<LsdbIngest>(m, "LsdbIngest")
       .def(py::init<std::string, std::set<std::string>>(), py::arg("myNodeName"),
            py::arg("areas"))
@@ -1141,6 +1149,23 @@ PYBIND11_MODULE(_decision, m) {
               const std::string& key) {
              return fromKeyUpdate(g.deleteKeyFromLsdb(area, ls, ps, key));
            })
+      .def("processPublicationKeyVals",
+           [](LsdbIngest& g, const std::string& area, AreaLinkStates& als, PrefixState& ps,
+              py::list keyVals, const std::vector<std::string>& expired,
+              DecisionPendingUpdates& pending, bool init) {
+             std::vector<PublicationKeyVal> kvs;
+             for (auto h : keyVals) {
+               py::tuple t = h.cast<py::tuple>();
+               PublicationKeyVal kv;
+               kv.key = t[0].cast<std::string>();
+               if (!t[1].is_none()) kv.value = std::string(t[1].cast<py::bytes>());
+               kvs.push_back(std::move(kv));
+             }
+             g.processPublication(area, als, ps, kvs, expired, pending, init);
+           },
+           py::arg("area"), py::arg("areaLinkStates"), py::arg("prefixState"),
+           py::arg("keyVals"), py::arg("expiredKeys"), py::arg("pending"),
+           py::arg("inInitialization") = false)
       // one publication's key/value pairs applied in C++ (bench / bulk load):
       // returns per-kind counts and the wall time of the loop alone
       .def("processPublication",

@@ -462,3 +462,38 @@ def delete_key_from_lsdb(area, link_state, prefix_state, key):
             return 3, "", None
         return 2, pk[0], set(prefix_state.deletePrefix(pk[0], area, pk[1]))
     return 0, "", None
+
+
+class PendingUpdates:
+    """DecisionPendingUpdates (Decision.h:40-105, Decision.cpp:35-60) without
+    perf events."""
+
+    def __init__(self, my_node):
+        self.me, self.count, self.full, self.prefixes = my_node, 0, False, set()
+
+    def apply(self, kind, node, payload):
+        if kind == 1:
+            self.full |= bool(payload["topologyChanged"] or payload["nodeLabelChanged"]
+                              or (payload["linkAttributesChanged"] and node == self.me))
+            self.count += 1
+        elif kind == 2:
+            self.prefixes |= set(payload)
+            self.count += 1
+
+
+def process_publication(my_node, area_link_states, make_link_state, prefix_state, area,
+                        key_vals, expired_keys, pending, in_initialization=False):
+    """Decision::processPublication (Decision.cpp:821-846); area_link_states
+    is a plain dict area -> LinkState, key_vals (key, bytes|None) pairs
+    applied as a std::map (sorted keys, last duplicate wins)."""
+    if area not in area_link_states:
+        area_link_states[area] = make_link_state(area, my_node)
+    ls = area_link_states[area]
+    if not key_vals and not expired_keys:
+        return
+    areas = set(area_link_states)
+    for key, val in sorted(dict(key_vals).items()):
+        pending.apply(*update_key_in_lsdb(my_node, areas, area, ls, prefix_state, key, val,
+                                          in_initialization))
+    for key in expired_keys:
+        pending.apply(*delete_key_from_lsdb(area, ls, prefix_state, key))

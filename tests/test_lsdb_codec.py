@@ -374,3 +374,58 @@ def test_gpu_routes_from_publication(product, oracle):
         assert (p_db is None) == (o_db is None), src
         if p_db is not None:
             assert p_db.unicastRoutes() == o_db.unicastRoutes(), src
+
+
+def test_process_publication_sequence(host_module, oracle):
+    """Decision::processPublication (Decision.cpp:821-846) over a sequence of
+    publications in two areas (+ an empty one for a third): new areas,
+    unordered and repeated keys, TTL-only values, self reflection, attribute
+    changes from self vs. others, expired adj / prefix keys; the pending
+    updates (full rebuild, changed prefixes, count) and the LSDB match the
+    oracle after every publication."""
+    M = host_module
+    me = "3"
+    rng = random.Random(0xF4F4)
+    _, ka, va = M.gen_publication("grid", {"n": 5, "metricSeed": 2, "prefixesPerNode": 2,
+                                           "v4Permille": 300})
+    _, kb, vb = M.gen_publication("grid", {"n": 4, "metricSeed": 3, "prefixSeed": 77})
+    refl = createPrefixEntry("fc00::33/128")
+    refl["area_stack"] = ["A"]
+    mine = createAdjDb(me, [createAdjacency("2", "if_3_2", "if_2_3", "fe80::2", "10.0.0.2", 9, 1),
+                            createAdjacency("4", "if_3_4", "if_4_3", "fe80::4", "10.0.0.4", 1, 1)], 4)
+    other = createAdjDb("0", [createAdjacency("1", "if_0_1", "if_1_0", "fe80::1", "10.0.0.1", 50, 1),
+                              createAdjacency("5", "if_0_5", "if_5_0", "fe80::5", "10.0.0.5", 1, 1)], 1)
+    other_lbl = createAdjDb("0", [dict(a, adjLabel=a["adjLabel"] + 7) for a in other["adjacencies"]], 1)
+    mine_lbl = createAdjDb(me, [dict(a, adjLabel=a["adjLabel"] + 7) for a in mine["adjacencies"]], 4)
+    pa = list(zip(ka, va))
+    rng.shuffle(pa)
+    pubs = [
+        ("A", [("adj:1", b"\x19\xfc")] + pa, []),
+        ("B", list(zip(kb, vb)) + [("prefix:3:[fc00::33/128]", tc.encode_prefix_db(
+            dict(thisNodeName=me, prefixEntries=[refl])))], []),
+        ("A", [("adj:0", tc.encode_adj_db(other)), ("adj:2", None), (ka[7], None)], []),
+        ("A", [("adj:3", tc.encode_adj_db(mine))], [ka[-1], "adj:4", "prefix:9:[bad]"]),
+        ("A", [("adj:0", tc.encode_adj_db(other_lbl))], []),   # attributes only, not self
+        ("A", [("adj:3", tc.encode_adj_db(mine_lbl))], []),    # attributes only, self
+        ("C", [], []),
+        ("B", [], [kb[0], kb[-2]]),
+    ]
+    p_als, p_ps = M.AreaLinkStates(), M.PrefixState()
+    o_als, o_ps = {}, oracle.PrefixState()
+    ing = M.LsdbIngest(me, set())
+    fulls = []
+    for area, kvs, expired in pubs:
+        p_pend, o_pend = M.DecisionPendingUpdates(me), tc.PendingUpdates(me)
+        ing.processPublicationKeyVals(area, p_als, p_ps, kvs, expired, p_pend)
+        tc.process_publication(me, o_als, oracle.LinkState, o_ps, area, kvs, expired, o_pend)
+        assert sorted(p_als.areas()) == sorted(o_als)
+        assert (p_pend.needsFullRebuild(), set(p_pend.updatedPrefixes()), p_pend.getCount()) == \
+            (o_pend.full, o_pend.prefixes, o_pend.count), area
+        assert p_ps.prefixes() == o_ps.prefixes()
+        for a in o_als:
+            for n in [str(i) for i in range(25)]:
+                assert p_als[a].linksFromNode(n) == o_als[a].linksFromNode(n), (a, n)
+        fulls.append(p_pend.needsFullRebuild())
+    # spot checks of the reference rules the sequence exercises
+    assert fulls[4:6] == [False, True]
+    assert "fc00::33/128" not in p_ps.prefixes()  # self reflection skipped
