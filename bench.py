@@ -357,9 +357,12 @@ def run_c4(args, torch, dist, rank, world, local_rank):
                 ("c3_fabric", "fabric", dict(pods=32, planes=8, sswPerPlane=36,
                                              rswPerPod=48, full=True, prefixesPerNode=1))):
             patch_us, rebuild_us, edges, flaps = M.flap_update_bench(kind, opts, 200, 0xF3)
+            pub_us, n_pub, d_dev, d_fresh = M.publication_flap_bench(kind, opts, 200, 0xF3)
+            assert d_dev == d_fresh, "publication-driven CSR patch diverged from a fresh flatten"
             csr_update[tag] = {"directed_edges": edges, "flaps": flaps,
                                "patch_us": round(patch_us, 2),
-                               "rebuild_us": round(rebuild_us, 2)}
+                               "rebuild_us": round(rebuild_us, 2),
+                               "via_publication_us": round(pub_us, 2)}
     total_units, total_changed, job_digest, tmax, _ = shard.reduce_stats(
         dist, torch, dev, U, changed, digest, wall)
     if rank != 0:

@@ -1380,6 +1380,55 @@ PYBIND11_MODULE(_decision, m) {
           const auto [rebuildUs, _] = run(false);
           return py::make_tuple(patchUs, rebuildUs, edges, flaps);
         });
+  // §8(f) f4 + f3 end to end: the same flaps arriving as KvStore values
+  // (compact AdjacencyDatabase bytes, encoded before timing, as the sender
+  // would) -> LsdbIngest::updateKeyInLsdb -> in-place CSR patch -> device
+  // current. Returns (us per flap, flaps applied, digest of the final device
+  // edge words == digest of a fresh flatten of the same LSDB).
+  m.def("publication_flap_bench",
+        [](const std::string& kind, py::dict opts, int flaps, uint64_t seed) {
+          const topogen::Lsdb g = genLsdb(kind, opts);
+          py::gil_scoped_release nogil;
+          LinkState ls(g.area, "test_node");
+          PrefixState ps;
+          loadLsdb(g, ls, ps);
+          ls.flatOnDevice();
+          ogsCheck(ogs_stream_sync(nullptr), "ogs_stream_sync");
+          std::vector<AdjacencyDatabase> dbs;
+          for (const auto& [_, db] : ls.getAdjacencyDatabases()) dbs.push_back(db);
+          std::vector<std::pair<std::string, std::string>> pubs;
+          uint64_t s = seed;
+          for (int i = 0; i < flaps; ++i) {
+            AdjacencyDatabase& db = dbs[topogen::splitmix64(s) % dbs.size()];
+            if (db.adjacencies.empty()) continue;
+            Adjacency& a = db.adjacencies[topogen::splitmix64(s) % db.adjacencies.size()];
+            a.metric = 1 + int32_t(topogen::splitmix64(s) % 1000);
+            pubs.emplace_back("adj:" + db.thisNodeName, writeAdjacencyDatabase(db));
+          }
+          LsdbIngest ing("test_node", {g.area});
+          const auto t0 = std::chrono::steady_clock::now();
+          for (const auto& [key, val] : pubs) {
+            auto u = ing.updateKeyInLsdb(g.area, ls, ps, key, std::string_view(val));
+            if (u.kind != LsdbKeyUpdate::kAdjacency) throw std::runtime_error(u.error);
+            ls.flatOnDevice();
+            ogsCheck(ogs_stream_sync(nullptr), "ogs_stream_sync");
+          }
+          const double us = std::chrono::duration<double, std::micro>(
+                                std::chrono::steady_clock::now() - t0).count();
+          auto digest = [](const std::vector<uint64_t>& v) {
+            uint64_t h = 0xcbf29ce484222325ull;
+            for (uint64_t x : v) h = (h ^ x) * 0x100000001b3ull;
+            return h;
+          };
+          const FlatTopology& f = ls.flatOnDevice();
+          std::vector<uint64_t> dev(f.edges.size());
+          if (!dev.empty()) f.dEdges.download(dev.data(), dev.size());
+          ogsCheck(ogs_stream_sync(nullptr), "ogs_stream_sync");
+          LinkState fresh(g.area, "test_node");
+          for (const auto& db : dbs) fresh.updateAdjacencyDatabase(db, g.area);
+          const uint64_t dDev = digest(dev), dFresh = digest(fresh.flat().edges);
+          return py::make_tuple(us / std::max<size_t>(pubs.size(), 1), pubs.size(), dDev, dFresh);
+        });
   m.def("gen_publication",
         [](const std::string& kind, py::dict opts) {
           auto g = genLsdb(kind, opts);

@@ -429,3 +429,14 @@ def test_process_publication_sequence(host_module, oracle):
     # spot checks of the reference rules the sequence exercises
     assert fulls[4:6] == [False, True]
     assert "fc00::33/128" not in p_ps.prefixes()  # self reflection skipped
+
+
+@pytest.mark.gpu
+def test_gpu_publication_flaps_patch_device_csr(product):
+    """f4 -> f3: metric flaps arriving as compact AdjacencyDatabase values,
+    ingested by LsdbIngest, leave the device CSR equal to a fresh flatten."""
+    M = product
+    for kind, opts in (("wan", {"nodes": 200, "k": 3, "seed": 0xC4}),
+                       ("grid", {"n": 8, "metricSeed": 1})):
+        us, n, d_dev, d_fresh = M.publication_flap_bench(kind, opts, 40, 0xF4)
+        assert n == 40 and d_dev == d_fresh, kind
