@@ -1388,7 +1388,7 @@ PYBIND11_MODULE(_decision, m) {
   m.def("publication_flap_bench",
         [](const std::string& kind, py::dict opts, int flaps, uint64_t seed) {
           const topogen::Lsdb g = genLsdb(kind, opts);
-          py::gil_scoped_release nogil;
+          std::optional<py::gil_scoped_release> nogil(std::in_place);
           LinkState ls(g.area, "test_node");
           PrefixState ps;
           loadLsdb(g, ls, ps);
@@ -1427,6 +1427,7 @@ PYBIND11_MODULE(_decision, m) {
           LinkState fresh(g.area, "test_node");
           for (const auto& db : dbs) fresh.updateAdjacencyDatabase(db, g.area);
           const uint64_t dDev = digest(dev), dFresh = digest(fresh.flat().edges);
+          nogil.reset();  // the GIL is needed again to build the result
           return py::make_tuple(us / std::max<size_t>(pubs.size(), 1), pubs.size(), dDev, dFresh);
         });
   m.def("gen_publication",
