@@ -17,10 +17,9 @@ std::set<std::string> PrefixState::updatePrefix(const std::string& node,
                                                 const PrefixEntry& entry) {
   std::set<std::string> changed;  // PrefixState.cpp:15-38
   auto& entries = prefixes_[entry.prefix];
-  auto key = std::make_pair(node, area);
-  auto it = entries.find(key);
-  if (it != entries.end() && *it->second == entry) return changed;
-  entries[key] = std::make_shared<PrefixEntry>(entry);
+  auto [it, inserted] = entries.try_emplace(NodeAndArea(node, area));
+  if (!inserted && *it->second == entry) return changed;
+  it->second = std::make_shared<PrefixEntry>(entry);
   changed.insert(entry.prefix);
   ++version_;
   return changed;
@@ -31,11 +30,10 @@ std::set<std::string> PrefixState::updatePrefix(const std::string& node,
                                                 PrefixEntry&& entry) {
   std::set<std::string> changed;  // as above, moving the decoded entry in
   auto& entries = prefixes_[entry.prefix];
-  auto key = std::make_pair(node, area);
-  auto it = entries.find(key);
-  if (it != entries.end() && *it->second == entry) return changed;
+  auto [it, inserted] = entries.try_emplace(NodeAndArea(node, area));
+  if (!inserted && *it->second == entry) return changed;
   changed.insert(entry.prefix);
-  entries[key] = std::make_shared<PrefixEntry>(std::move(entry));
+  it->second = std::make_shared<PrefixEntry>(std::move(entry));
   ++version_;
   return changed;
 }
