@@ -479,6 +479,13 @@ class SpfSolver {
   std::optional<RibUnicastEntry> createRouteForPrefixOrGetStaticRoute(
       const std::string& myNodeName, const AreaLinkStates& areaLinkStates,
       const PrefixState& prefixState, const std::string& prefix);
+  // The incremental branch of Decision::rebuildRoutes (Decision.cpp:929-951)
+  // calls the above once per changed prefix; this answers a whole changed
+  // set (DecisionPendingUpdates::updatedPrefixes) with ONE build over a
+  // sub-table of those prefixes. Same per-prefix result (nullopt = delete).
+  std::map<std::string, std::optional<RibUnicastEntry>> createRoutesForPrefixes(
+      const std::string& myNodeName, const AreaLinkStates& areaLinkStates,
+      const PrefixState& prefixState, const std::set<std::string>& prefixes);
   // Device-only buildRouteDb over the multi-area kernels (any number of
   // areas): the source's SPF in every area, the RouteDb and the RibPolicy
   // are enqueued on `stream` and left in device memory -- no download, no

@@ -968,6 +968,45 @@ std::optional<RibUnicastEntry> SpfSolver::createRouteForPrefixOrGetStaticRoute(
   return std::nullopt;
 }
 
+std::map<std::string, std::optional<RibUnicastEntry>> SpfSolver::createRoutesForPrefixes(
+    const std::string& me, const AreaLinkStates& als, const PrefixState& ps,
+    const std::set<std::string>& prefixes) {
+  std::map<std::string, std::optional<RibUnicastEntry>> out;
+  bool exists = false;
+  for (const auto& [_, l] : als) exists |= l.hasNode(me);
+  PrefixState sub;  // the changed prefixes through one GPU build
+  std::set<std::string> asked;
+  for (const auto& prefix : prefixes) {
+    out[prefix] = std::nullopt;
+    auto pit = ps.prefixes().find(prefix);
+    const bool gated = isV4Prefix(prefix) && !enableV4_ && !v4OverV6Nexthop_;
+    if (!exists || gated || pit == ps.prefixes().end()) continue;
+    for (const auto& [na, e] : pit->second) sub.updatePrefix(na.first, na.second, *e);
+    asked.insert(prefix);
+  }
+  if (!asked.empty()) {
+    SpfSolver probe(myNodeName_, enableV4_, false, enableBestRouteSelection_,
+                    v4OverV6Nexthop_);
+    auto db = probe.buildRouteDb(me, als, sub);
+    const auto& bcache = probe.getBestRoutesCache();
+    for (const auto& prefix : asked) {
+      if (db) {
+        auto it = db->unicastRoutes.find(prefix);
+        if (it != db->unicastRoutes.end()) out[prefix] = it->second;
+      }
+      auto bc = bcache.find(prefix);
+      if (bc != bcache.end()) bestRoutesCache_[prefix] = bc->second;
+      else bestRoutesCache_.erase(prefix);
+    }
+  }
+  for (auto& [prefix, route] : out) {  // static routes as the fallback
+    if (route) continue;
+    auto it = staticUnicastRoutes_.find(prefix);
+    if (it != staticUnicastRoutes_.end()) route = it->second;
+  }
+  return out;
+}
+
 // ------------------------------------------------------------- RibPolicy --
 RibPolicy::RibPolicy(const std::vector<RibPolicyStatementSpec>& statements,
                      int64_t ttlSecs)

@@ -1268,6 +1268,15 @@ PYBIND11_MODULE(_decision, m) {
              if (!r) return py::none();
              return fromRoute(*r);
            })
+      .def("createRoutesForPrefixes",
+           [](SpfSolver& s, const std::string& me, const AreaLinkStates& a,
+              const PrefixState& ps, const std::set<std::string>& prefixes) {
+             py::dict out;
+             for (const auto& [p, r] : s.createRoutesForPrefixes(me, a, ps, prefixes)) {
+               out[py::str(p)] = r ? py::object(fromRoute(*r)) : py::object(py::none());
+             }
+             return out;
+           })
       .def("updateStaticUnicastRoutes",
            [](SpfSolver& s, py::dict upd, std::vector<std::string> del) {
              std::map<std::string, RibUnicastEntry> u;

@@ -440,3 +440,60 @@ def test_gpu_publication_flaps_patch_device_csr(product):
                        ("grid", {"n": 8, "metricSeed": 1})):
         us, n, d_dev, d_fresh = M.publication_flap_bench(kind, opts, 40, 0xF4)
         assert n == 40 and d_dev == d_fresh, kind
+
+
+@pytest.mark.gpu
+def test_gpu_incremental_routes_after_prefix_publication(product, oracle):
+    """f4 -> f1: a prefix publication's changed set (DecisionPendingUpdates)
+    answered by createRoutesForPrefixes (one GPU build) equals the oracle's
+    per-prefix createRouteForPrefixOrGetStaticRoute (Decision.cpp:929-951)
+    and the product's own per-prefix call and full build."""
+    M = product
+    me = "0"
+    _, keys, vals = M.gen_publication(
+        "grid", {"n": 6, "prefixesPerNode": 2, "metricSeed": 6, "v4Permille": 300,
+                 "anycastPermille": 200, "minNhPermille": 100, "nodeOverloadPermille": 40,
+                 "overloadSeed": 2})
+    area = "test_area_name"
+    p_als, p_ps, o_als, o_ps = M.AreaLinkStates(), M.PrefixState(), {}, oracle.PrefixState()
+    ing = M.LsdbIngest(me, set())
+    ing.processPublicationKeyVals(area, p_als, p_ps, list(zip(keys, vals)), [],
+                                  M.DecisionPendingUpdates(me))
+    tc.process_publication(me, o_als, oracle.LinkState, o_ps, area, list(zip(keys, vals)), [],
+                           tc.PendingUpdates(me))
+    # second publication: changed metrics, a new anycast advertiser, deletes
+    pkeys = [k for k in keys if k.startswith("prefix:")]
+    rng = random.Random(5)
+    upd = []
+    for k in rng.sample(pkeys, 12):
+        db = tc.decode_prefix_db(vals[keys.index(k)])
+        e = db["prefixEntries"][0]
+        if rng.random() < 0.3:
+            db["deletePrefix"] = True
+        else:
+            e["metrics"]["path_preference"] += rng.choice([0, 50])
+            e["metrics"]["distance"] = rng.randint(0, 5)
+            if rng.random() < 0.4:
+                db["thisNodeName"] = str(rng.randrange(36))  # another advertiser
+        upd.append(("prefix:%s:[%s]" % (db["thisNodeName"], e["prefix"]), tc.encode_prefix_db(db)))
+    p_pend, o_pend = M.DecisionPendingUpdates(me), tc.PendingUpdates(me)
+    ing.processPublicationKeyVals(area, p_als, p_ps, upd, [], p_pend)
+    o_areas = oracle.AreaLinkStates()
+    tc.process_publication(me, o_als, oracle.LinkState, o_ps, area, upd, [], o_pend)
+    changed = set(p_pend.updatedPrefixes())
+    assert changed == o_pend.prefixes and changed and not p_pend.needsFullRebuild()
+    # oracle LinkState lives in a dict; rebuild an AreaLinkStates for its solver
+    o_ls = o_areas.add(area, me)
+    for k, v in zip(keys, vals):
+        if k.startswith("adj:"):
+            tc.update_key_in_lsdb(me, {area}, area, o_ls, oracle.PrefixState(), k, v)
+    p_s = M.SpfSolver(me, True, False, True, False)
+    o_s = oracle.SpfSolver(me, True, False, True, False)
+    batch = p_s.createRoutesForPrefixes(me, p_als, p_ps, changed | {"fc00::dead/128"})
+    full = p_s.buildRouteDb(me, p_als, p_ps).unicastRoutes()
+    assert batch["fc00::dead/128"] is None
+    for pfx in sorted(changed):
+        want = o_s.createRouteForPrefixOrGetStaticRoute(me, o_areas, o_ps, pfx)
+        assert batch[pfx] == want, pfx
+        assert p_s.createRouteForPrefixOrGetStaticRoute(me, p_als, p_ps, pfx) == want, pfx
+        assert full.get(pfx) == want, pfx
