@@ -35,6 +35,7 @@ TOPOS_PER_GPU = 4096
 GRID_N = 10
 METRIC_SEED = 0xC2000000
 PREFIX_SEED = 0xC1
+C3_INC_SOURCE = "2-0-0"  # a fabric node (incremental-routes sub-line)
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 
 
@@ -274,6 +275,14 @@ def run_c3(args, torch, dist, rank, world, local_rank):
             "decode_MB_per_s": round(pub["bytes"] / pub["decode_ms"] / 1e3, 1),
             "note": "LsdbIngest (C++ drop-in), 1 host thread, median of 3; rank 0, "
                     "after the timed region"}
+        # §8(f) f1 incremental branch: 100 changed prefixes of node "ssw-0-0"'s
+        # RouteDb in one sub-table build vs the per-prefix loop
+        b_ms, l_ms, same, n_chg = openr_amd.decision.incremental_routes_bench(
+            "fabric", dict(pods=32, planes=8, sswPerPlane=36, rswPerPod=48, full=True,
+                           prefixesPerNode=args.prefixes_per_node), C3_INC_SOURCE, 100)
+        assert same, "createRoutesForPrefixes differs from the per-prefix loop"
+        line["incremental_routes"] = {"changed_prefixes": n_chg, "batch_ms": round(b_ms, 3),
+                                      "per_prefix_loop_ms": round(l_ms, 2)}
         traffic, src = pmc_traffic("c3", "spf_frontier_kernel")
         if traffic is not None and world == 1:
             line["roofline"]["traffic"] = round(traffic, 1)
@@ -759,7 +768,8 @@ def main():
             line["c3_fabric_all_sources"] = {
                 k: c3[k] for k in ("value", "unit", "ms_per_step", "kernel_ms",
                                    "route_dbs_per_s", "gteps", "routes_per_step",
-                                   "route_digest", "serve", "publication_ingest", "roofline",
+                                   "route_digest", "serve", "publication_ingest",
+                                   "incremental_routes", "roofline",
                                    "config") if k in c3}
             line["c3_fabric_all_sources"]["steps"] = c3["steps"]
     if not args.no_c4:

@@ -1439,6 +1439,39 @@ PYBIND11_MODULE(_decision, m) {
           nogil.reset();  // the GIL is needed again to build the result
           return py::make_tuple(us / std::max<size_t>(pubs.size(), 1), pubs.size(), dDev, dFresh);
         });
+  // f1 incremental branch after a prefix publication: `n` changed prefixes
+  // answered by createRoutesForPrefixes (one build) vs the reference's loop
+  // of createRouteForPrefixOrGetStaticRoute; returns (batch ms, loop ms,
+  // identical results)
+  m.def("incremental_routes_bench",
+        [](const std::string& kind, py::dict opts, const std::string& me, int n) {
+          auto g = genLsdb(kind, opts);
+          py::gil_scoped_release nogil;
+          AreaLinkStates als;
+          auto& ls = als.emplace(g.area, LinkState(g.area, "test_node")).first->second;
+          PrefixState ps;
+          loadLsdb(g, ls, ps);
+          std::set<std::string> changed;
+          const size_t stride = std::max<size_t>(1, ps.prefixes().size() / std::max(n, 1));
+          size_t i = 0;
+          for (const auto& [p, _] : ps.prefixes()) {
+            if (i++ % stride == 0 && int(changed.size()) < n) changed.insert(p);
+          }
+          SpfSolver a("test_node", true, false, false, false), b("test_node", true, false, false, false);
+          a.createRoutesForPrefixes(me, als, ps, changed);  // warm (SPF memo, device)
+          auto t0 = std::chrono::steady_clock::now();
+          auto batch = a.createRoutesForPrefixes(me, als, ps, changed);
+          auto t1 = std::chrono::steady_clock::now();
+          bool same = true;
+          for (const auto& p : changed) {
+            auto r = b.createRouteForPrefixOrGetStaticRoute(me, als, ps, p);
+            same &= (r.has_value() == batch[p].has_value()) && (!r || *r == *batch[p]);
+          }
+          auto t2 = std::chrono::steady_clock::now();
+          return std::make_tuple(std::chrono::duration<double, std::milli>(t1 - t0).count(),
+                                 std::chrono::duration<double, std::milli>(t2 - t1).count(),
+                                 same, changed.size());
+        });
   m.def("gen_publication",
         [](const std::string& kind, py::dict opts) {
           auto g = genLsdb(kind, opts);
