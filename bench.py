@@ -9,10 +9,16 @@ One "step" = one launch of the fused SPF+RouteDb kernel over the whole
 batch; one "build" = one (topology, source) SPF + RouteDb. Inputs are
 HBM-resident (torch-owned device buffers) before timing starts.
 
-Multi-GPU (--gpus N via torch.distributed.run): weak scaling, each rank owns
-its own 4096-topology shard (topology indices rank*4096 ...), no data-path
-collective; RCCL only all-gathers per-rank digests/counts and max-reduces
-the elapsed time.
+The same JSON line carries sub-lines for C1 (single-source drop-in latency),
+C3 (fabric all-sources), C4 (link-failure sweep) and C5 (multi-area KSP2 +
+UCMP). Every config's output digest (openr_amd/csrc/host/route_digest.h,
+openr_amd/shard.py) is checked against the ORACLE's digest of the same
+workload (tests/golden/bench_digests.json, tests/golden/make_bench_digests.py):
+a mismatch prints the line and exits non-zero.
+
+Multi-GPU (--gpus N via torch.distributed.run): each config shards its units
+over the ranks with no data-path collective; RCCL only all-gathers per-rank
+digests/counts and max-reduces the elapsed time.
 """
 import argparse
 import ctypes
@@ -30,13 +36,68 @@ import torch  # noqa: E402,F401
 import numpy as np  # noqa: E402
 
 from openr_amd import shard  # noqa: E402
+from openr_amd.workloads import (C2_OPTS, C2_SOURCE, C2_TOPOS, C3_OPTS, C4_OPTS,  # noqa: E402
+                                 C4_SOURCE, C4_VARIANTS, C4_SEED, C4_DUAL_PERMILLE,
+                                 c3_source_names)
 
-TOPOS_PER_GPU = 4096
-GRID_N = 10
-METRIC_SEED = 0xC2000000
-PREFIX_SEED = 0xC1
-C3_INC_SOURCE = "2-0-0"  # a fabric node (incremental-routes sub-line)
+GRID_N = C2_OPTS["n"]
+C1_OPTS = dict(n=10, prefixSeed=0xC1)  # createGrid(10) wiring, metric 1
+C3_INC_SOURCE = "2-0-0"  # a fabric FSW (incremental-routes sub-line)
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+CPU_REPS = 5  # BASELINE.md timing rule: median of >= 5 repetitions
+
+# oracle-generated digests of the exact bench workloads
+# (tests/golden/make_bench_digests.py); a mismatch fails the run
+GOLDEN_PATH = os.path.join(ROOT, "tests", "golden", "bench_digests.json")
+GOLDEN = json.load(open(GOLDEN_PATH)) if os.path.exists(GOLDEN_PATH) else {}
+DIGEST_FAILURES = []
+
+
+def golden_check(line, key, got, want):
+    """Records got vs the oracle's golden digest in line["golden"]; a
+    mismatch is remembered and fails the run once the line is printed."""
+    g = line.setdefault("golden", {})
+    if want is None:
+        g[key] = "n/a (no golden value for this workload)"
+        return
+    ok = f"{got:016x}" == want
+    g[key] = "match" if ok else f"MISMATCH got {got:016x} want {want}"
+    if not ok:
+        DIGEST_FAILURES.append(f"{key}: got {got:016x}, oracle golden {want}")
+
+
+def log(msg):
+    """Progress on stderr (the JSON line alone goes to stdout)."""
+    print(f"bench.py [{time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
+def cpu_threads():
+    return max(1, min(16, os.cpu_count() or 1))  # the box's CPU share
+
+
+def host_info():
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    model = ln.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"nproc": os.cpu_count(), "model": model}
+
+
+def median(xs):
+    xs = sorted(xs)
+    n = len(xs)
+    return xs[n // 2] if n % 2 else 0.5 * (xs[n // 2 - 1] + xs[n // 2])
+
+
+def oracle():
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import _refcpu
+    return _refcpu
 
 
 def algorithmic_bytes_per_unit(N, E, T, P, W, Wl, S=1):
@@ -46,42 +107,96 @@ def algorithmic_bytes_per_unit(N, E, T, P, W, Wl, S=1):
     return inputs / S + 4 * N + 4 * W * N + P * (4 * Wl + 8)
 
 
-def cpu_baseline(units, reps=3):
-    """The oracle (refcpu, a faithful port of LinkState/SpfSolver) timed on
-    this host's cores over the same workload; ingestion excluded."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import _refcpu
-    threads = max(1, min(16, os.cpu_count() or 1))  # the box's CPU share
-    opts = dict(n=GRID_N, metricSeed=METRIC_SEED, prefixSeed=PREFIX_SEED)
-    rates = []
-    for _ in range(reps):
-        secs, n, routes = _refcpu.cpu_baseline_grid_batch(opts, units, threads, "1")
-        rates.append(n / secs)
-    rates.sort()
-    return {"value": round(rates[len(rates) // 2], 1), "unit": "builds/s",
-            "cores": threads, "kind": "port",
-            "sample": f"{units} C2 topologies x {reps} reps (median), "
-                      f"refcpu buildRouteDb('1'), {threads} threads, ingestion excluded"}
+def pmc_traffic(tag, match):
+    """HBM bytes per launch of the kernels whose name contains `match`, from
+    the newest committed PMC summary profiles/r*_pmc_<tag>.json
+    (tools/gpu_pmc.sh: FETCH_SIZE and WRITE_SIZE passes, gfx950 FETCH_SIZE
+    x2 correction). Returns (bytes summed over matching kernels, file) or
+    (None, None)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_pmc_{tag}.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    hits = [v["hbm_bytes_per_launch"] for k, v in d.items()
+            if match in k and v.get("hbm_bytes_per_launch") is not None]
+    if not hits:
+        return None, None
+    return float(sum(hits)), os.path.relpath(files[-1], ROOT)
 
 
-def fabric_names(pods, planes, ssw, rsw):
-    """Node names of topogen::fabric (RoutingBenchmarkUtils.cpp:421-473)."""
-    return ([f"1-{p}-{s}" for p in range(planes) for s in range(ssw)],
-            [f"2-{p}-{f}" for p in range(pods) for f in range(planes)],
-            [f"3-{p}-{r}" for p in range(pods) for r in range(rsw)])
+def set_traffic(line, tag, match, scale=1.0):
+    traffic, src = pmc_traffic(tag, match)
+    if traffic is not None:
+        line["roofline"]["traffic"] = round(traffic * scale, 1)
+        line["roofline"]["traffic_source"] = src
 
 
-def c3_launches(torch, M, capi, dev, rank, world, ppn, with_sel=False):
-    """Host build + device upload of this rank's C3 launches: sources grouped
-    by next-hop bitset width (SSW+RSW: 1 word, FSW: 3 words -> 4) so each
-    launch writes masks of its own width."""
-    opts = dict(pods=32, planes=8, sswPerPlane=36, rswPerPod=48, full=True,
-                prefixesPerNode=ppn)
-    ssw, fsw, rsw = fabric_names(32, 8, 36, 48)
-    N = len(ssw) + len(fsw) + len(rsw)
+# ----------------------------------------------------------------- C2 ---
+def cpu_baseline_c2(units):
+    """refcpu (a faithful port of LinkState/SpfSolver) on this host's cores
+    over the C2 workload, private replicas per thread, ingestion excluded:
+    median of CPU_REPS repetitions at T threads (all `units` topologies) and
+    at 1 thread (512 of them)."""
+    R = oracle()
+    T = cpu_threads()
+    rate = {}
+    for threads, n in ((T, units), (1, min(units, 512))):
+        rs = []
+        for _ in range(CPU_REPS):
+            secs, k, _ = R.cpu_baseline_grid_batch(C2_OPTS, n, threads, C2_SOURCE)
+            rs.append(k / secs)
+        rate[threads] = median(rs)
+    return {"value": round(rate[T], 1), "unit": "builds/s", "cores": T, "kind": "port",
+            "value_1thread": round(rate[1], 1), "reps": CPU_REPS, "host": host_info(),
+            "sample": f"{units} C2 topologies at {T} threads, 512 at 1 thread; median of "
+                      f"{CPU_REPS} reps; refcpu buildRouteDb('1'), private replicas, "
+                      "ingestion excluded"}
+
+
+# ----------------------------------------------------------------- C1 ---
+def run_c1(args, rank):
+    """Config C1 (BASELINE.json configs[0]): one buildRouteDb("1") on the
+    10x10 metric-1 grid through the C++ drop-in (SpfSolver::buildRouteDb:
+    flatten + uploads, the fused kernel, D2H, DecisionRouteDb
+    materialisation) next to refcpu's buildRouteDb on one host thread. A
+    single-unit latency, not a throughput: no roofline (the kernel is C2's
+    at one unit)."""
+    if rank != 0:
+        return None
+    import openr_amd
+    reps = 21
+    cold, warm, routes = openr_amd.decision.build_latency_bench("grid", C1_OPTS, "1", reps)
+    out = {"unit": "us/build", "gpu_cold_us": round(median(cold), 1),
+           "gpu_warm_us": round(median(warm), 1), "routes": routes, "reps": reps,
+           "note": "drop-in SpfSolver::buildRouteDb('1'): cold = fresh LinkState/PrefixState/"
+                   "solver (CSR flatten + H2D + kernel + D2H + materialisation), warm = same "
+                   "objects again (device tables cached); median of reps"}
+    if not args.no_cpu_baseline:
+        n = 2 * CPU_REPS + 1
+        cpu = oracle().cpu_time_build("grid", C1_OPTS, "1", n)
+        out["cpu_baseline"] = {
+            "value": round(median(cpu), 1), "unit": "us/build", "cores": 1, "kind": "port",
+            "reps": n, "host": host_info(),
+            "sample": "refcpu buildRouteDb('1') on a fresh replica per rep (ingestion "
+                      "untimed), 1 thread, median"}
+    return out
+
+
+# ----------------------------------------------------------------- C3 ---
+def c3_launches(torch, M, capi, dev, names, ppn=100, with_sel=False):
+    """Host build + device upload of the C3 launches for the sources
+    `names`: grouped by next-hop bitset width (SSW+RSW: 1 word, FSW: 3 words
+    -> 4) so each launch writes masks of its own width."""
+    opts = dict(C3_OPTS, prefixesPerNode=ppn)
+    N = len(c3_source_names())
     launches = []
-    for names in (ssw + rsw, fsw):
-        mine = shard.interleave(names, rank, world)
+    fsw = [n for n in names if n.startswith("2-")]
+    rest = [n for n in names if not n.startswith("2-")]
+    for mine in (rest, fsw):
+        if not mine:
+            continue
         br = M.BatchRunner(True, False, False)
         br.add_generated("fabric", opts, mine)
         h = br.host_arrays()
@@ -128,30 +243,55 @@ def c3_launches(torch, M, capi, dev, rank, world, ppn, with_sel=False):
     return launches, N
 
 
-def hash_list(xs):
-    """63-bit hash of an int list (C4 changed-prefix lists inside the digest)."""
-    import hashlib
-    return int.from_bytes(hashlib.sha256(repr(list(xs)).encode()).digest()[:8],
-                          "little") >> 1
+def c3_launch_all(lib, capi, launches, main, side):
+    """One C3 step: every width group's ogs_spf_routes, the second group on
+    its own HIP stream (`side`), joined back into `main`."""
+    streams = [main, side] + [main] * max(0, len(launches) - 2)
+    fork = torch.cuda.Event()
+    fork.record(main)
+    side.wait_event(fork)
+    for L, st in zip(launches, streams):
+        rc = lib.ogs_spf_routes(ctypes.byref(L["g"]), ctypes.byref(L["pt"]),
+                                ctypes.c_void_p(L["t"]["units"].data_ptr()), L["U"],
+                                L["flags"], L["W"], ctypes.byref(L["so"]),
+                                ctypes.c_void_p(st.cuda_stream))
+        if rc != 0:
+            capi.check(lib, rc, "ogs_spf_routes")
+    join = torch.cuda.Event()
+    join.record(side)
+    main.wait_event(join)
 
 
-def pmc_traffic(tag, match):
-    """HBM bytes per launch of the kernels whose name contains `match`, from
-    the newest committed PMC summary profiles/r*_pmc_<tag>.json
-    (tools/gpu_pmc.sh: FETCH_SIZE and WRITE_SIZE passes, gfx950 FETCH_SIZE
-    x2 correction). Returns (bytes summed over matching kernels, file) or
-    (None, None)."""
-    import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_pmc_{tag}.json")))
-    if not files:
-        return None, None
-    with open(files[-1]) as f:
-        d = json.load(f)
-    hits = [v["hbm_bytes_per_launch"] for k, v in d.items()
-            if match in k and v.get("hbm_bytes_per_launch") is not None]
-    if not hits:
-        return None, None
-    return float(sum(hits)), os.path.relpath(files[-1], ROOT)
+def c3_digest(L, threads=16):
+    """route_digest.h unit digests of one launch's records (keys = source
+    names), XOR-combined."""
+    o = L["o"]
+    d = L["br"].records_digests([], o["meta"].cpu().numpy(), o["metric"].cpu().numpy(),
+                                o["mask"].cpu().numpy(), L["W"], threads)
+    return shard.combine_digests(d)
+
+
+def cpu_baseline_c3(N):
+    """refcpu buildRouteDb(s) for a stratified sample of the 2,080 sources
+    (every 130th name: 3 SSW, 2 FSW, 11 RSW) on T threads with private
+    replicas, and 2 sources (1 SSW, 1 RSW) on 1 thread; 3 reps each (one
+    source's build takes seconds on refcpu, so >= 5 reps would dominate the
+    run); extrapolated to whole-node builds/s = 1 / (mean s per source x
+    2080 / threads)."""
+    R = oracle()
+    T = cpu_threads()
+    names = c3_source_names()
+    out = {}
+    for threads, sample in ((T, names[::130][:16]), (1, [names[0], names[-1]])):
+        secs, _ = R.cpu_baseline_sources("fabric", C3_OPTS, sample, threads, 3)
+        # thread-seconds per source -> whole-node builds/s at `threads`
+        out[threads] = median(1.0 / (s * min(threads, len(sample)) / len(sample) * N / threads)
+                              for s in secs)
+    return {"value": round(out[T], 6), "unit": "builds/s", "cores": T, "kind": "port",
+            "value_1thread": round(out[1], 7), "reps": 3, "host": host_info(),
+            "sample": f"refcpu buildRouteDb(s) of 16 stratified sources on {T} threads and "
+                      "2 (1-0-0, 3-31-47) on 1 thread, private replicas, ingestion excluded, "
+                      "median of 3 reps, extrapolated to all 2,080 sources"}
 
 
 def run_c3(args, torch, dist, rank, world, local_rank):
@@ -168,34 +308,19 @@ def run_c3(args, torch, dist, rank, world, local_rank):
     dev = torch.device("cuda", local_rank)
     steps = args.steps if args.config == "c3" else args.c3_steps
     warmup = args.warmup if args.config == "c3" else 2
-    launches, N = c3_launches(torch, M, capi, dev, rank, world, args.prefixes_per_node)
+    ppn = args.prefixes_per_node
+    # sources interleaved over ranks (balances SSW/FSW/RSW degree classes)
+    mine = shard.interleave(c3_source_names(), rank, world)
+    launches, N = c3_launches(torch, M, capi, dev, mine, ppn)
     if args.c3_order == "wide-first":
         # the wide (FSW, 4-word) group has the longest units: dispatch it
         # first so it is not the lone tail after the 1-word group
         launches = launches[::-1]
-    # the width groups are independent: with --c3-streams 2 the second group
-    # runs on its own HIP stream, overlapped with the first
     main = torch.cuda.current_stream(dev)
     side = torch.cuda.Stream(dev) if args.c3_streams > 1 else main
-    streams = [main, side] + [main] * max(0, len(launches) - 2)
-
-    def step():
-        fork = torch.cuda.Event()
-        fork.record(main)
-        side.wait_event(fork)
-        for L, st in zip(launches, streams):
-            rc = lib.ogs_spf_routes(ctypes.byref(L["g"]), ctypes.byref(L["pt"]),
-                                    ctypes.c_void_p(L["t"]["units"].data_ptr()), L["U"],
-                                    L["flags"], L["W"], ctypes.byref(L["so"]),
-                                    ctypes.c_void_p(st.cuda_stream))
-            if rc != 0:
-                capi.check(lib, rc, "ogs_spf_routes")
-        join = torch.cuda.Event()
-        join.record(side)
-        main.wait_event(join)
 
     for _ in range(warmup):
-        step()
+        c3_launch_all(lib, capi, launches, main, side)
     torch.cuda.synchronize(dev)
     if dist:
         dist.barrier()
@@ -205,7 +330,7 @@ def run_c3(args, torch, dist, rank, world, local_rank):
     t0 = time.perf_counter()
     e0.record(main)
     for _ in range(steps):
-        step()
+        c3_launch_all(lib, capi, launches, main, side)
     e1.record(main)
     torch.cuda.synchronize(dev)
     if dist:
@@ -217,82 +342,104 @@ def run_c3(args, torch, dist, rank, world, local_rank):
     units = sum(L["U"] for L in launches)
     nbytes = sum(L["bytes"] for L in launches)
     routes = sum(int(((L["o"]["meta"] & 1) != 0).sum().item()) for L in launches)
-    # keyed by source name: the same job digest at any rank count
-    digest = shard.combine_digests(
-        shard.unit_digest(L["names"], L["o"]["meta"].cpu().numpy(),
-                          L["o"]["metric"].cpu().numpy())
-        for L in launches)
-    total_units, total_routes, job_digest, tmax, _ = shard.reduce_stats(
-        dist, torch, dev, units, routes, digest, wall)
-    if rank == 0:
-        achieved = nbytes / (kernel_ms * 1e-3) / 1e9
-        value = total_units * steps / tmax / N
-        line = {
-            "metric": "SPF+RouteDb builds/sec (whole node)",
-            "value": round(value, 4), "unit": "builds/s",
-            "n_gpus": world, "steps": steps, "warmup": warmup,
-            "ms_per_step": round(tmax / steps * 1e3, 4),
-            "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
-            "dtype": "u32", "data": "synthetic",
-            "config": {"workload": f"C3-full: fabric all-sources (N=2080, E=43008, "
-                                   f"{args.prefixes_per_node} prefixes/node), one build = "
-                                   "RouteDb of every node",
-                       "sources": N, "prefixes": N * args.prefixes_per_node,
-                       "parallelism": f"shard-by-source x{world}"},
-            "route_dbs_per_s": round(total_units * steps / tmax, 1),
-            "routes_per_step": total_routes,
-            "route_digest": f"{job_digest:016x}",
-            "gteps": round(43008 * total_units * steps / tmax / 1e9, 3),
-            "kernel_ms": round(kernel_ms, 4),
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1),
-                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                         "bytes_alg_per_step_rank0": round(nbytes, 1)},
-        }
-        # §8(f) f2, outside the timed region: the same build as a resident
-        # RouteDbBatch served per node (getRouteDbComputed: D2H of one node's
-        # records + host materialisation + toThrift)
-        import openr_amd
-        launch_ms, serve_ms, routes, ns = openr_amd.decision.route_db_batch_serve_bench(
-            "fabric", dict(pods=32, planes=8, sswPerPlane=36, rswPerPod=48, full=True,
-                           prefixesPerNode=args.prefixes_per_node), 3)
-        line["serve"] = {"sources": ns, "batch_launch_ms": round(launch_ms, 3),
-                         "getRouteDbComputed_ms": round(serve_ms, 2),
-                         "routes_per_node": round(routes, 1),
-                         "note": "RouteDbBatch (C++ drop-in) over all 2,080 sources, then "
-                                 "3 nodes served; rank 0, after the timed region"}
-        # §8(f) f4, host only: the same fabric as one KvStore publication
-        # (2,080 "adj:" + 208k "prefix:" keys, compact thrift) decoded and
-        # ingested per key (Decision::updateKeyInLsdb) into a fresh LSDB
-        pub = openr_amd.decision.publication_ingest_bench(
-            "fabric", dict(pods=32, planes=8, sswPerPlane=36, rswPerPod=48, full=True,
-                           prefixesPerNode=args.prefixes_per_node), 3)
-        keys = pub["adj_dbs"] + pub["prefix_keys"]
-        line["publication_ingest"] = {
-            "keys": keys, "bytes": pub["bytes"], "ingest_ms": round(pub["ingest_ms"], 2),
-            "decode_ms": round(pub["decode_ms"], 2),
-            "keys_per_s": round(keys / pub["ingest_ms"] * 1e3, 1),
-            "decode_MB_per_s": round(pub["bytes"] / pub["decode_ms"] / 1e3, 1),
-            "note": "LsdbIngest (C++ drop-in), 1 host thread, median of 3; rank 0, "
-                    "after the timed region"}
-        # §8(f) f1 incremental branch: 100 changed prefixes of node "ssw-0-0"'s
-        # RouteDb in one sub-table build vs the per-prefix loop
-        b_ms, l_ms, same, n_chg = openr_amd.decision.incremental_routes_bench(
-            "fabric", dict(pods=32, planes=8, sswPerPlane=36, rswPerPod=48, full=True,
-                           prefixesPerNode=args.prefixes_per_node), C3_INC_SOURCE, 100)
-        assert same, "createRoutesForPrefixes differs from the per-prefix loop"
-        line["incremental_routes"] = {"changed_prefixes": n_chg, "batch_ms": round(b_ms, 3),
-                                      "per_prefix_loop_ms": round(l_ms, 2)}
-        traffic, src = pmc_traffic("c3", "spf_frontier_kernel")
-        if traffic is not None and world == 1:
-            line["roofline"]["traffic"] = round(traffic, 1)
-            line["roofline"]["traffic_source"] = src
-        return line
-    return None
+    digest = shard.combine_digests(c3_digest(L) for L in launches)
+    total_units, total_routes, _, tmax, _ = shard.reduce_stats(
+        dist, torch, dev, units, routes, 0, wall)
+    job_digest = shard.reduce_xor(dist, torch, dev, [digest])[0]
+    if rank != 0:
+        return None
+    achieved = nbytes / (kernel_ms * 1e-3) / 1e9
+    value = total_units * steps / tmax / N
+    line = {
+        "metric": "SPF+RouteDb builds/sec (whole node)",
+        "value": round(value, 4), "unit": "builds/s",
+        "n_gpus": world, "steps": steps, "warmup": warmup,
+        "ms_per_step": round(tmax / steps * 1e3, 4),
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+        "dtype": "u32", "data": "synthetic",
+        "config": {"workload": f"C3-full: fabric all-sources (N=2080, E=43008, "
+                               f"{ppn} prefixes/node), one build = RouteDb of every node",
+                   "sources": N, "prefixes": N * ppn,
+                   "parallelism": f"shard-by-source x{world}"},
+        "route_dbs_per_s": round(total_units * steps / tmax, 1),
+        "routes_per_step": total_routes,
+        "route_digest": f"{job_digest:016x}",
+        "gteps": round(43008 * total_units * steps / tmax / 1e9, 3),
+        "kernel_ms": round(kernel_ms, 4),
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "bytes_alg_per_step_rank0": round(nbytes, 1)},
+    }
+    log(f"c3 timed: {kernel_ms:.4f} ms/build, digest {job_digest:016x}")
+    golden_check(line, "c3", job_digest, GOLDEN.get("c3") if ppn == 100 else None)
+    if world == 1:
+        set_traffic(line, "c3", "spf_frontier_kernel")
+    # §8(f) f2, outside the timed region: the same build as a resident
+    # RouteDbBatch served per node (getRouteDbComputed: D2H of one node's
+    # records + host materialisation + toThrift)
+    fab = dict(C3_OPTS, prefixesPerNode=ppn)
+    launch_ms, serve_ms, nroutes, ns = M.route_db_batch_serve_bench("fabric", fab, 3)
+    line["serve"] = {"sources": ns, "batch_launch_ms": round(launch_ms, 3),
+                     "getRouteDbComputed_ms": round(serve_ms, 2),
+                     "routes_per_node": round(nroutes, 1),
+                     "note": "RouteDbBatch (C++ drop-in) over all 2,080 sources, then "
+                             "3 nodes served; rank 0, after the timed region"}
+    # §8(f) f4, host only: the same fabric as one KvStore publication
+    # (2,080 "adj:" + 208k "prefix:" keys, compact thrift) decoded and
+    # ingested per key (Decision::updateKeyInLsdb) into a fresh LSDB
+    pub = M.publication_ingest_bench("fabric", fab, 3)
+    keys = pub["adj_dbs"] + pub["prefix_keys"]
+    line["publication_ingest"] = {
+        "keys": keys, "bytes": pub["bytes"], "ingest_ms": round(pub["ingest_ms"], 2),
+        "decode_ms": round(pub["decode_ms"], 2),
+        "keys_per_s": round(keys / pub["ingest_ms"] * 1e3, 1),
+        "decode_MB_per_s": round(pub["bytes"] / pub["decode_ms"] / 1e3, 1),
+        "note": "LsdbIngest (C++ drop-in), 1 host thread, median of 3; rank 0, "
+                "after the timed region"}
+    # §8(f) f1 incremental branch: 100 changed prefixes of FSW "2-0-0"'s
+    # RouteDb in one sub-table build, vs the engine's per-prefix loop and vs
+    # refcpu's createRouteForPrefixOrGetStaticRoute loop (SPF memo warm, as
+    # in the reference's Decision::rebuildRoutes, Decision.cpp:929-938)
+    b_ms, l_ms, same, n_chg = M.incremental_routes_bench("fabric", fab, C3_INC_SOURCE, 100)
+    assert same, "createRoutesForPrefixes differs from the per-prefix loop"
+    line["incremental_routes"] = {"changed_prefixes": n_chg, "batch_ms": round(b_ms, 3),
+                                  "per_prefix_loop_ms": round(l_ms, 2)}
+    if not args.no_cpu_baseline:
+        ms = [oracle().cpu_incremental_routes("fabric", fab, C3_INC_SOURCE, 100)[0]
+              for _ in range(CPU_REPS)]
+        line["incremental_routes"]["cpu_baseline"] = {
+            "value": round(median(ms), 2), "unit": "ms", "cores": 1, "kind": "port",
+            "reps": CPU_REPS,
+            "sample": "refcpu createRouteForPrefixOrGetStaticRoute over the same 100 "
+                      "prefixes, SPF memo warm, 1 thread, median"}
+        if world == 1 and ppn == 100:
+            log("c3 cpu baseline ...")
+            line["cpu_baseline"] = cpu_baseline_c3(N)
+    return line
 
 
-C4_VARIANTS = 10000
-C4_OPTS = dict(nodes=2000, seed=0xC4, prefixesPerNode=1)
+# ----------------------------------------------------------------- C4 ---
+def cpu_baseline_c4():
+    """refcpu per variant: updateAdjacencyDatabase of the failed links'
+    endpoints, buildRouteDb, calculateUpdate, restore -- private replicas;
+    first 32*T variants on T threads and 64 on 1 thread; median of
+    CPU_REPS reps."""
+    R = oracle()
+    T = cpu_threads()
+    rate = {}
+    for threads, n in ((T, 32 * T), (1, 64)):
+        rs = []
+        for _ in range(CPU_REPS):
+            secs, k, _ = R.cpu_baseline_variants("wan", C4_OPTS, C4_SOURCE, n, C4_SEED,
+                                                 C4_DUAL_PERMILLE, threads)
+            rs.append(k / secs)
+        rate[threads] = median(rs)
+    return {"value": round(rate[T], 2), "unit": "variants/s", "cores": T, "kind": "port",
+            "value_1thread": round(rate[1], 2), "reps": CPU_REPS, "host": host_info(),
+            "sample": f"first {32 * T} C4 variants on {T} threads, 64 on 1 thread; refcpu "
+                      "incremental updateAdjacencyDatabase + buildRouteDb + calculateUpdate, "
+                      f"ingestion excluded, median of {CPU_REPS} reps"}
 
 
 def run_c4(args, torch, dist, rank, world, local_rank):
@@ -312,7 +459,7 @@ def run_c4(args, torch, dist, rank, world, local_rank):
     warmup = args.warmup if args.config == "c4" else 2
     lo, hi = shard.block_range(C4_VARIANTS, rank, world)
     vr = openr_amd.decision.VariantRunner(True, False)
-    vr.setup("wan", C4_OPTS, "0", C4_VARIANTS, 0xC4F, 500, lo, hi)
+    vr.setup("wan", C4_OPTS, C4_SOURCE, C4_VARIANTS, C4_SEED, C4_DUAL_PERMILLE, lo, hi)
     sh = vr.shape()
     stream = torch.cuda.current_stream(dev)
     sptr = stream.cuda_stream
@@ -338,13 +485,9 @@ def run_c4(args, torch, dist, rank, world, local_rank):
     kernel_ms = e0.elapsed_time(e1) / steps
     vr.download()
     U = vr.num_variants()
-    changed = sum(len(vr.changed(v)) for v in range(U))
-    counts = [vr.counts(v) for v in range(U)]
-    # keyed by global variant index: the same job digest at any rank count
-    digest = shard.unit_digest(
-        list(range(lo, lo + U)),
-        np.array([[c[0], c[1], hash_list(vr.changed(v))]
-                  for v, c in enumerate(counts)], dtype="int64"))
+    ch = [(*vr.counts(v), vr.changed(v)) for v in range(U)]
+    changed = sum(len(c[2]) for c in ch)
+    digest = shard.changes_digest(range(lo, lo + U), ch)
     # §8(f) f1, outside the timed region: the DecisionRouteUpdate of every
     # variant from the device-gathered changed records (ogs_route_changes_gather
     # + D2H of those records), then host materialisation of all of them
@@ -361,10 +504,8 @@ def run_c4(args, torch, dist, rank, world, local_rank):
     if rank == 0:
         M = openr_amd.decision
         csr_update = {}
-        for tag, kind, opts in (
-                ("c4_wan", "wan", C4_OPTS),
-                ("c3_fabric", "fabric", dict(pods=32, planes=8, sswPerPlane=36,
-                                             rswPerPod=48, full=True, prefixesPerNode=1))):
+        for tag, kind, opts in (("c4_wan", "wan", C4_OPTS),
+                                ("c3_fabric", "fabric", dict(C3_OPTS, prefixesPerNode=1))):
             patch_us, rebuild_us, edges, flaps = M.flap_update_bench(kind, opts, 200, 0xF3)
             pub_us, n_pub, d_dev, d_fresh = M.publication_flap_bench(kind, opts, 200, 0xF3)
             assert d_dev == d_fresh, "publication-driven CSR patch diverged from a fresh flatten"
@@ -372,8 +513,9 @@ def run_c4(args, torch, dist, rank, world, local_rank):
                                "patch_us": round(patch_us, 2),
                                "rebuild_us": round(rebuild_us, 2),
                                "via_publication_us": round(pub_us, 2)}
-    total_units, total_changed, job_digest, tmax, _ = shard.reduce_stats(
-        dist, torch, dev, U, changed, digest, wall)
+    total_units, total_changed, _, tmax, _ = shard.reduce_stats(
+        dist, torch, dev, U, changed, 0, wall)
+    job_digest = shard.reduce_xor(dist, torch, dev, [digest])[0]
     if rank != 0:
         return None
     N, E, P = sh["nodes"], sh["directed_edges"], sh["prefixes"]
@@ -407,25 +549,40 @@ def run_c4(args, torch, dist, rank, world, local_rank):
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": None, "bytes_alg_per_unit": round(bpu, 1)},
     }
-    # PMC HBM bytes of the variant launch (10k units; committed passes)
-    traffic, src = pmc_traffic("c4", "spf_frontier_kernel<1, true, true, true")
-    if traffic is not None and world == 1:
-        line["roofline"]["traffic"] = round(traffic, 1)
-        line["roofline"]["traffic_source"] = src
-    if world == 1 and not args.no_cpu_baseline:
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        import _refcpu
-        threads = max(1, min(16, os.cpu_count() or 1))
-        sample = 32 * threads
-        secs, n, _ = _refcpu.cpu_baseline_variants("wan", C4_OPTS, "0", sample, 0xC4F, 500,
-                                                   threads)
-        line["cpu_baseline"] = {
-            "value": round(n / secs, 2), "unit": "variants/s", "cores": threads,
-            "kind": "port",
-            "sample": f"first {sample} of the C4 variants, refcpu incremental "
-                      f"updateAdjacencyDatabase + buildRouteDb + calculateUpdate, "
-                      f"{threads} threads, ingestion excluded"}
+    log(f"c4 timed: {kernel_ms:.4f} ms/sweep, digest {job_digest:016x}")
+    golden_check(line, "c4", job_digest, GOLDEN.get("c4"))
+    if world == 1:
+        set_traffic(line, "c4", "spf_frontier_kernel<1, true, true, true")
+        if not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline_c4()
     return line
+
+
+# ----------------------------------------------------------------- C5 ---
+def cpu_baseline_c5(pol):
+    """refcpu per job: buildRouteDb + RibPolicy::applyPolicy on one thread
+    (one source's build is sequential in the reference) + getKthPaths k=1,2
+    for a strided destination sample on T threads (24 per thread) or 1
+    thread (48), extrapolated to all destinations; median of CPU_REPS."""
+    from openr_amd.workloads import C5_OPTS, C5_SOURCE
+    R = oracle()
+    T = cpu_threads()
+    out = {}
+    for threads, sample in ((T, 24 * T), (1, 48)):
+        rs, detail = [], None
+        for _ in range(CPU_REPS):
+            rsec, ksec, n, total, routes = R.cpu_baseline_c5(C5_OPTS, C5_SOURCE, pol, True,
+                                                             sample, threads)
+            rs.append(1.0 / (rsec + ksec * total / n))
+            detail = (rsec, ksec, n, total, routes)
+        out[threads] = (median(rs), detail)
+    rsec, ksec, n, total, routes = out[T][1]
+    return {"value": round(out[T][0], 4), "unit": "jobs/s", "cores": T, "kind": "port",
+            "value_1thread": round(out[1][0], 4), "reps": CPU_REPS, "host": host_info(),
+            "sample": f"refcpu buildRouteDb + RibPolicy::applyPolicy ({rsec:.3f} s, 1 thread, "
+                      f"{routes} routes) + getKthPaths k=1,2 for {n} of {total} destinations on "
+                      f"{T} threads ({ksec:.3f} s; 48 on 1 thread), extrapolated to all "
+                      f"destinations; ingestion excluded; median of {CPU_REPS} reps"}
 
 
 def run_c5(args, torch, dist, rank, world, local_rank):
@@ -493,12 +650,16 @@ def run_c5(args, torch, dist, rank, world, local_rank):
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t0
     job_ms = e0.elapsed_time(e1) / steps
+    # digests of the last timed job's results: its RouteDb (device records
+    # downloaded + materialised) and its KSP2 paths
+    routes_digest = r.routes_digest(sptr)
     r.fetch()
+    paths_digest = shard.lines_digest(r.ksp_text())
     sh = r.shape()
     U = sh["ksp_units"]
-    digest = r.digest() >> 1
-    total_units, total_prefixes, job_digest, tmax, _ = shard.reduce_stats(
-        dist, torch, dev, U, sh["prefixes"], digest, wall)
+    total_units, total_prefixes, _, tmax, _ = shard.reduce_stats(
+        dist, torch, dev, U, sh["prefixes"], 0, wall)
+    routes_job, paths_job = shard.reduce_xor(dist, torch, dev, [routes_digest, paths_digest])
     if rank != 0:
         return None
     # KSP2 unit (CSR + E/8 mask + 4N + path output): the
@@ -527,33 +688,32 @@ def run_c5(args, torch, dist, rank, world, local_rank):
         "ksp2_dests_per_s": round(total_units * steps / tmax, 1),
         "route_kernels_ms": round(route_ms, 4), "ksp2_kernels_ms": round(ksp_ms, 4),
         "job_kernel_ms": round(job_ms, 4),
-        "path_digest": f"{job_digest:016x}",
+        "route_digest": f"{routes_job:016x}", "path_digest": f"{paths_job:016x}",
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                      "traffic": None, "bytes_alg_per_unit": round(bpu, 1),
-                     "kernel": "ksp_base_kernel + ksp2_kernel (one launch pair over the source's areas)"},
+                     "kernel": "ksp_base_kernel + ksp2_kernel (one launch pair over the "
+                               "source's areas)"},
     }
-    # PMC HBM bytes per launch of both KSP kernels x the job's per-area batches
-    traffic, src = pmc_traffic("c5", "ksp")
-    if traffic is not None and world == 1:
-        line["roofline"]["traffic"] = round(traffic * sh["ksp_batches"], 1)
-        line["roofline"]["traffic_source"] = src
-    if world == 1 and not args.no_cpu_baseline:
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        import _refcpu
-        threads = max(1, min(16, os.cpu_count() or 1))
-        sample = 24 * threads
-        rs, ks, n, total, routes = _refcpu.cpu_baseline_c5(C5_OPTS, C5_SOURCE, pol, True,
-                                                           sample, threads)
-        job_s = rs + ks * total / n
-        line["cpu_baseline"] = {
-            "value": round(1.0 / job_s, 4), "unit": "jobs/s", "cores": threads,
-            "kind": "port",
-            "sample": f"refcpu buildRouteDb + RibPolicy::applyPolicy ({rs:.3f} s, 1 thread, "
-                      f"{routes} routes) + getKthPaths k=1,2 for {n} of {total} "
-                      f"destinations on {threads} threads ({ks:.3f} s), extrapolated to "
-                      f"all destinations; ingestion excluded"}
+    log(f"c5 timed: {job_ms:.4f} ms/job")
+    golden_check(line, "c5_routes", routes_job, GOLDEN.get("c5_routes"))
+    golden_check(line, "c5_paths", paths_job, GOLDEN.get("c5_paths"))
+    if world == 1:
+        # PMC HBM bytes per launch of both KSP kernels x the job's per-area batches
+        set_traffic(line, "c5", "ksp", sh["ksp_batches"])
+        if not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline_c5(pol)
     return line
+
+
+# --------------------------------------------------------------- main ---
+def finish(line):
+    print(json.dumps(line), flush=True)
+    if DIGEST_FAILURES:
+        for f in DIGEST_FAILURES:
+            print(f"bench.py: DIGEST MISMATCH vs oracle golden: {f}", file=sys.stderr,
+                  flush=True)
+        raise SystemExit(1)
 
 
 def main():
@@ -565,8 +725,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--topos", type=int, default=TOPOS_PER_GPU)
+    ap.add_argument("--topos", type=int, default=C2_TOPOS)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-c1", action="store_true",
+                    help="skip the C1 single-source latency line embedded in the C2 result")
     ap.add_argument("--no-c3", action="store_true",
                     help="skip the C3 fabric all-sources line embedded in the C2 result")
     ap.add_argument("--c3-steps", type=int, default=10)
@@ -584,7 +746,6 @@ def main():
                     help="engine option name=value (ogs_set_option), for A/B runs")
     args = ap.parse_args()
 
-    import torch
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -610,20 +771,13 @@ def main():
         name, val = o.split("=", 1)
         lib0 = capi.load()
         capi.check(lib0, lib0.ogs_set_option(name.encode(), int(val)), name)
-    if args.config in ("c4", "c5"):
-        run = run_c4 if args.config == "c4" else run_c5
-        line = run(args, torch, dist, rank, world, local_rank)
-        if line is not None:
-            print(json.dumps(line), flush=True)
+    single = {"c3": run_c3, "c4": run_c4, "c5": run_c5}.get(args.config)
+    if single is not None:
+        line = single(args, torch, dist, rank, world, local_rank)
         if dist:
             dist.destroy_process_group()
-        return
-    if args.config == "c3":
-        line = run_c3(args, torch, dist, rank, world, local_rank)
         if line is not None:
-            print(json.dumps(line), flush=True)
-        if dist:
-            dist.destroy_process_group()
+            finish(line)
         return
     openr_amd.require_gpu()
     M = openr_amd.decision
@@ -634,8 +788,7 @@ def main():
     # weak scaling: the job is world x --topos topologies, rank r owns block r
     lo, hi = shard.block_range(world * args.topos, rank, world)
     br = M.BatchRunner(True, False, False)
-    br.add_grid_batch(dict(n=GRID_N, metricSeed=METRIC_SEED, prefixSeed=PREFIX_SEED),
-                      lo, hi, "1")
+    br.add_grid_batch(C2_OPTS, lo, hi, C2_SOURCE)
     h = br.host_arrays()
     dev = torch.device("cuda", local_rank)
 
@@ -706,14 +859,17 @@ def main():
     wall = time.perf_counter() - t0
     kernel_ms = ev0.elapsed_time(ev1) / args.steps  # one launch per step
 
-    # ---- per-rank digest (result sanity) + cross-rank reduction -----------
+    # ---- digest of the timed launches' records + cross-rank reduction -----
     meta = o_meta.cpu().numpy()
     n_routes = int(((meta & 1) != 0).sum())
-    digest = shard.unit_digest(list(range(lo, hi)), meta, o_metric.cpu().numpy(),
-                               o_mask.cpu().numpy())
-    total_units, total_routes, job_digest, tmax, _ = shard.reduce_stats(
-        dist, torch, dev, U, n_routes, digest, wall)
+    digest = shard.combine_digests(br.records_digests(
+        [str(t) for t in range(lo, hi)], meta, o_metric.cpu().numpy(), o_mask.cpu().numpy(),
+        W, 16))
+    total_units, total_routes, _, tmax, _ = shard.reduce_stats(
+        dist, torch, dev, U, n_routes, 0, wall)
+    job_digest = shard.reduce_xor(dist, torch, dev, [digest])[0]
 
+    line = None
     if rank == 0:
         N, E, P = GRID_N * GRID_N, 4 * GRID_N * (GRID_N - 1), GRID_N * GRID_N
         bpu = algorithmic_bytes_per_unit(N, E, P, P, W, W)
@@ -738,7 +894,7 @@ def main():
                             "(100 prefixes/topology)",
                 "topologies_per_gpu": U,
                 "nodes": N, "directed_edges": E, "prefixes_per_topology": P,
-                "source": "1",
+                "source": C2_SOURCE,
                 "parallelism": f"shard-by-topology x{world}",
             },
             "gteps": round(E * value / 1e9, 3),
@@ -755,12 +911,18 @@ def main():
                 "bytes_alg_per_unit": round(bpu, 1),
             },
         }
-        traffic, src = pmc_traffic("c2", "spf_route_wave_kernel")
-        if traffic is not None:
-            line["roofline"]["traffic"] = round(traffic, 1)
-            line["roofline"]["traffic_source"] = src
+        blocks = GOLDEN.get("c2_blocks", [])
+        want = None
+        if args.topos == GOLDEN.get("c2_block_size") and world <= len(blocks):
+            want = f"{shard.combine_digests(int(b, 16) for b in blocks[:world]):016x}"
+        log(f"c2 timed: {kernel_ms * 1e3:.2f} us/launch, digest {job_digest:016x}")
+        golden_check(line, "c2", job_digest, want)
+        set_traffic(line, "c2", "spf_route_wave_kernel")
         if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(U)
+            line["cpu_baseline"] = cpu_baseline_c2(U)
+            log("c2 cpu baseline done")
+        if not args.no_c1:
+            line["c1_single_source"] = run_c1(args, rank)
     if not args.no_c3:
         # the north-star headline config, sharded by source over the ranks
         c3 = run_c3(args, torch, dist, rank, world, local_rank)
@@ -768,32 +930,35 @@ def main():
             line["c3_fabric_all_sources"] = {
                 k: c3[k] for k in ("value", "unit", "ms_per_step", "kernel_ms",
                                    "route_dbs_per_s", "gteps", "routes_per_step",
-                                   "route_digest", "serve", "publication_ingest",
-                                   "incremental_routes", "roofline",
-                                   "config") if k in c3}
-            line["c3_fabric_all_sources"]["steps"] = c3["steps"]
+                                   "route_digest", "golden", "serve", "publication_ingest",
+                                   "incremental_routes", "roofline", "cpu_baseline",
+                                   "config", "steps") if k in c3}
     if not args.no_c4:
         c4 = run_c4(args, torch, dist, rank, world, local_rank)
         if rank == 0:
             line["c4_link_failure_sweep"] = {
                 k: c4[k] for k in ("value", "unit", "ms_per_step", "kernel_ms", "gteps",
-                                   "changed_routes_per_step", "route_digest", "route_update", "csr_update",
-                                   "roofline",
+                                   "changed_routes_per_step", "route_digest", "golden",
+                                   "route_update", "csr_update", "roofline", "cpu_baseline",
                                    "config", "steps") if k in c4}
-            if "cpu_baseline" in c4:
-                line["c4_link_failure_sweep"]["cpu_baseline"] = c4["cpu_baseline"]
     if not args.no_c5:
         c5 = run_c5(args, torch, dist, rank, world, local_rank)
         if rank == 0:
             line["c5_multiarea_ksp2_ucmp"] = {
                 k: c5[k] for k in ("value", "unit", "ms_per_step", "ksp2_dests_per_s",
                                    "route_kernels_ms", "ksp2_kernels_ms", "job_kernel_ms",
-                                   "path_digest", "roofline", "config", "steps",
-                                   "cpu_baseline") if k in c5}
-    if rank == 0:
-        print(json.dumps(line), flush=True)
+                                   "route_digest", "path_digest", "golden", "roofline",
+                                   "config", "steps", "cpu_baseline") if k in c5}
     if dist:
         dist.destroy_process_group()
+    if rank == 0:
+        # sub-line digest results roll up into the headline line's golden map
+        for sub in ("c3_fabric_all_sources", "c4_link_failure_sweep", "c5_multiarea_ksp2_ucmp"):
+            for k, v in line.get(sub, {}).get("golden", {}).items():
+                line["golden"][k] = v
+        finish(line)
+    elif DIGEST_FAILURES:
+        raise SystemExit(1)
 
 
 if __name__ == "__main__":

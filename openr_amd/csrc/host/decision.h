@@ -493,6 +493,12 @@ class SpfSolver {
   bool enqueueRouteDb(const std::string& myNodeName,
                       const AreaLinkStates& areaLinkStates,
                       const PrefixState& prefixState, void* stream);
+  // The DecisionRouteDb of the last enqueueRouteDb(myNodeName, ...) (syncs
+  // `stream`, downloads and materialises those device results; the
+  // AreaLinkStates / PrefixState must be unchanged since).
+  std::optional<DecisionRouteDb> collectRouteDb(const std::string& myNodeName,
+                                                const AreaLinkStates& areaLinkStates,
+                                                void* stream = nullptr);
   const std::map<std::string, RouteSelectionResult>& getBestRoutesCache()
       const {
     return bestRoutesCache_;
@@ -525,6 +531,9 @@ class SpfSolver {
   DecisionRouteDb materializeMultiArea(const std::string& myNodeName,
                                        const AreaLinkStates& areaLinkStates,
                                        const MultiAreaResult& r);
+  DecisionRouteDb downloadMultiArea(const std::string& myNodeName,
+                                    const AreaLinkStates& areaLinkStates,
+                                    MultiAreaResult& r);
   friend class RouteDbBatch;
   struct Impl;
   std::unique_ptr<Impl> impl_;

@@ -199,6 +199,9 @@ struct SpfSolver::Impl {
         advArea, advName, nameLocal;
     DeviceBuffer units, srcName, spfRow, dist, nh, meta, metric, mask, sel;
   } ma;
+  // shape of the last enqueueRouteDb (collectRouteDb downloads its results)
+  std::optional<MultiAreaResult> enqueued;
+  std::string enqueuedMe;
 };
 
 SpfSolver::SpfSolver(const std::string& me, bool enableV4, bool sr, bool brs,
@@ -901,15 +904,35 @@ bool SpfSolver::enqueueRouteDb(const std::string& me, const AreaLinkStates& als,
   bool found = false;
   for (const auto& [_, ls] : als) found |= ls.hasNode(me);
   if (!found) return false;
-  MultiAreaResult R;
-  enqueueMultiArea(me, als, ps, stream, R);
+  impl_->enqueued.emplace();
+  impl_->enqueuedMe = me;
+  enqueueMultiArea(me, als, ps, stream, *impl_->enqueued);
   return true;
+}
+
+std::optional<DecisionRouteDb> SpfSolver::collectRouteDb(const std::string& me,
+                                                         const AreaLinkStates& als,
+                                                         void* stream) {
+  if (!impl_->enqueued || impl_->enqueuedMe != me) {
+    throw std::logic_error("collectRouteDb: no enqueueRouteDb(" + me + ") to collect");
+  }
+  ogsCheck(ogs_stream_sync(stream), "ogs_stream_sync");
+  MultiAreaResult R = *impl_->enqueued;
+  return downloadMultiArea(me, als, R);
 }
 
 std::optional<DecisionRouteDb> SpfSolver::buildRouteDbMultiArea(
     const std::string& me, const AreaLinkStates& als, const PrefixState& ps) {
   MultiAreaResult R;
   enqueueMultiArea(me, als, ps, nullptr, R);
+  return downloadMultiArea(me, als, R);
+}
+
+// D2H of a multi-area build's device results (default stream after the
+// launches) + materialisation.
+DecisionRouteDb SpfSolver::downloadMultiArea(const std::string& me,
+                                             const AreaLinkStates& als,
+                                             MultiAreaResult& R) {
   Impl::MultiArea& M = impl_->ma;
   const uint32_t A = uint32_t(als.size());
   const int W = R.W;

@@ -14,6 +14,8 @@
 #include "../gen/topogen.h"
 #include "../host/decision.h"
 #include "../host/lsdb_codec.h"
+#include "../host/route_digest.h"
+#include <thread>
 
 namespace py = pybind11;
 using namespace openr_amd;
@@ -608,6 +610,46 @@ class BatchRunner {
         (brs_ ? OGS_F_BEST_ROUTE_SELECTION : 0u) |
         (wide_ ? OGS_F_WIDE_METRIC : 0u);
   }
+  // route_digest.h unit(K, db) of every unit, straight from record arrays
+  // laid out like this runner's outputs (meta / metric [U*Sp], mask
+  // [U*W*Sp]; 32-bit metrics, all-ones = none): the bench digests the
+  // buffers of its timed launches with this. keys[u] = the unit's key
+  // (empty list: the unit's source name). Spread over `threads` threads.
+  std::vector<uint64_t> recordsDigests(const std::vector<std::string>& keys,
+                                       const uint32_t* meta, const uint32_t* metric,
+                                       const uint32_t* mask, int W, int threads) const {
+    const size_t U = units_.size(), Sp = std::max(hb_.maxPrefixes, 1);
+    if (!keys.empty() && keys.size() != U) throw std::invalid_argument("keys: one per unit");
+    if (W != W_) throw std::invalid_argument("mask width differs from the runner's");
+    for (const auto& t : topos_) {
+      if (!t->hashes) t->hashes = std::make_unique<digest::TableHashes>(t->table);
+    }
+    std::vector<uint64_t> out(U, 0);
+    threads = std::max(1, std::min<int>(threads, int(U)));
+    auto work = [&](int th) {
+      std::vector<uint64_t> m64(Sp);
+      for (size_t u = th; u < U; u += threads) {
+        const Topo& t = *topos_[units_[u].topo];
+        const LinkState& ls = t.als.at(t.area);
+        UnitView v;
+        v.W = W;
+        v.N = uint32_t(ls.flat().names.size());
+        v.P = uint32_t(t.table.prefixes.size());
+        v.meta = meta + u * Sp;
+        for (size_t p = 0; p < v.P; ++p) m64[p] = metric[u * Sp + p];
+        v.metric = m64.data();
+        v.mask = mask + u * W * Sp;
+        v.maskStride = Sp;
+        out[u] = digest::unitFromRecords(keys.empty() ? unitSrc_[u] : keys[u], ls.flat(),
+                                         unitSrc_[u], t.table, *t.hashes, v, false);
+      }
+    };
+    std::vector<std::thread> pool;
+    for (int th = 1; th < threads; ++th) pool.emplace_back(work, th);
+    work(0);
+    for (auto& p : pool) p.join();
+    return out;
+  }
   size_t numUnits() const { return units_.size(); }
   void setSlotOrder(bool on) { slotOrder_ = on; }
   void setSlotEdgeImage(bool on) { slotEdgeImage_ = on; }
@@ -618,6 +660,7 @@ class BatchRunner {
   const std::vector<uint64_t>& dist() const { return dist_; }
   const std::vector<uint32_t>& meta() const { return meta_; }
   const std::vector<uint64_t>& metric() const { return metric_; }
+  const std::vector<uint32_t>& mask() const { return mask_; }
 
  private:
   ogs_graph graph() const {
@@ -655,6 +698,7 @@ class BatchRunner {
     std::string area;
     PrefixState ps;
     PrefixHostTable table;
+    mutable std::unique_ptr<digest::TableHashes> hashes;
   };
   bool enableV4_, sr_, brs_;
   bool slotOrder_{true}, slotEdgeImage_{true};
@@ -920,23 +964,12 @@ class C5Runner {
     }
     return out;
   }
-  // FNV-1a over every unit's k = 1 and k = 2 paths (edge ids)
-  uint64_t digest() const {
-    uint64_t h = 1469598103934665603ull;
-    auto mix = [&](uint64_t x) { h = (h ^ x) * 1099511628211ull; };
-    for (const auto& b : batches_) {
-      for (size_t i = 0; i < b->size(); ++i) {
-        for (int k = 1; k <= 2; ++k) {
-          const auto paths = b->edgePaths(i, k);
-          mix(paths.size());
-          for (const auto& p : paths) {
-            for (uint32_t e : p) mix(e);
-            mix(~0ull);
-          }
-        }
-      }
-    }
-    return h;
+  // route_digest.h unit(source, RouteDb) of the last launch_routes (its
+  // device results downloaded and materialised; rank-invariant: the ranks'
+  // prefix blocks XOR to the whole job's)
+  uint64_t routesDigest(uintptr_t stream) {
+    return digest::unit(source_, solver_->collectRouteDb(source_, als_,
+                                                         reinterpret_cast<void*>(stream)));
   }
   py::dict shape() const {
     py::dict d;
@@ -1252,7 +1285,10 @@ PYBIND11_MODULE(_decision, m) {
            [](const DecisionRouteDb& a, const DecisionRouteDb& b) {
              return fromUpdate(a.calculateUpdate(b));
            })
-      .def("canonical", [](const DecisionRouteDb& db) { return py::bytes(canonical(db)); });
+      .def("canonical", [](const DecisionRouteDb& db) { return py::bytes(canonical(db)); })
+      .def("digest", [](const DecisionRouteDb& db, const std::string& key) {
+        return digest::unit(key, db);
+      });
 
   py::class_<SpfSolver>(m, "SpfSolver")
       .def(py::init<const std::string&, bool, bool, bool, bool>(), py::arg("myNodeName"),
@@ -1591,6 +1627,43 @@ PYBIND11_MODULE(_decision, m) {
   // getRouteDbComputed for `serve` nodes (D2H of that node's records + host
   // materialisation + toThrift). Returns (launch_ms, serve_ms_mean,
   // routes_per_served_node_mean, sources).
+  // Config C1 latency of the drop-in SpfSolver::buildRouteDb(source) as a
+  // Decision caller sees it. cold: fresh LinkState / PrefixState / solver per
+  // repetition (CSR flatten + uploads, launch, D2H, materialisation; the
+  // ingestion of the adjacency / prefix databases is untimed); warm: the same
+  // objects again (device tables cached, the SPF + RouteDb launch, D2H and
+  // materialisation still run every call). Returns (cold us, warm us, routes).
+  m.def("build_latency_bench",
+        [](const std::string& kind, py::dict opts, const std::string& me, int reps) {
+          auto g = genLsdb(kind, opts);
+          py::gil_scoped_release nogil;
+          std::vector<double> cold, warm;
+          size_t routes = 0;
+          for (int r = 0; r < reps + 1; ++r) {
+            AreaLinkStates als;
+            auto& ls = als.emplace(g.area, LinkState(g.area, "test_node")).first->second;
+            PrefixState ps;
+            loadLsdb(g, ls, ps);
+            SpfSolver solver("test_node", true, false, false);
+            auto t0 = std::chrono::steady_clock::now();
+            auto db = solver.buildRouteDb(me, als, ps);
+            const double us = std::chrono::duration<double, std::micro>(
+                                  std::chrono::steady_clock::now() - t0).count();
+            if (!db) throw std::runtime_error("no RouteDb for " + me);
+            routes = db->unicastRoutes.size();
+            if (r) cold.push_back(us);  // rep 0 warms code objects / workspace
+            if (r == reps) {
+              for (int k = 0; k < reps; ++k) {
+                t0 = std::chrono::steady_clock::now();
+                db = solver.buildRouteDb(me, als, ps);
+                warm.push_back(std::chrono::duration<double, std::micro>(
+                                   std::chrono::steady_clock::now() - t0).count());
+              }
+            }
+          }
+          return std::make_tuple(cold, warm, routes);
+        },
+        py::arg("kind"), py::arg("opts"), py::arg("me"), py::arg("reps"));
   m.def("route_db_batch_serve_bench",
         [](const std::string& kind, py::dict opts, int serve) {
           auto g = genLsdb(kind, opts);
@@ -1671,7 +1744,7 @@ PYBIND11_MODULE(_decision, m) {
       .def("routes", &C5Runner::routes)
       .def("ksp_text", &C5Runner::kspText)
       .def("ksp_dests", &C5Runner::kspDests)
-      .def("digest", &C5Runner::digest)
+      .def("routes_digest", &C5Runner::routesDigest, py::arg("stream") = 0)
       .def("shape", &C5Runner::shape);
 
   py::class_<BatchRunner>(m, "BatchRunner")
@@ -1701,6 +1774,30 @@ PYBIND11_MODULE(_decision, m) {
       .def("download", &BatchRunner::download)
       .def("num_units", &BatchRunner::numUnits)
       .def("canonical", [](const BatchRunner& b, size_t u) { return py::bytes(canonical(b.routeDb(u))); })
+      .def("unit_digest",  // route_digest.h unit() of the materialised RouteDb
+           [](const BatchRunner& b, size_t u, const std::string& key) {
+             return digest::unit(key, b.routeDb(u));
+           })
+      .def("records_digests",
+           [](const BatchRunner& b, const std::vector<std::string>& keys, py::array meta,
+              py::array metric, py::array mask, int W, int threads) {
+             auto words = [](const py::array& a, size_t n, const char* what) {
+               if (a.itemsize() != 4 || !(a.flags() & py::array::c_style) ||
+                   size_t(a.size()) < n) {
+                 throw std::invalid_argument(std::string(what) +
+                                             ": contiguous 32-bit array of the runner's shape");
+               }
+               return static_cast<const uint32_t*>(a.data());
+             };
+             const size_t U = b.numUnits(), Sp = std::max(b.host().maxPrefixes, 1);
+             const uint32_t* me = words(meta, U * Sp, "meta");
+             const uint32_t* mt = words(metric, U * Sp, "metric");
+             const uint32_t* mk = words(mask, U * W * Sp, "mask");
+             py::gil_scoped_release nogil;
+             return b.recordsDigests(keys, me, mt, mk, W, threads);
+           },
+           py::arg("keys"), py::arg("meta"), py::arg("metric"), py::arg("mask"),
+           py::arg("nh_words"), py::arg("threads") = 8)
       .def("route_counts",
            [](const BatchRunner& b) {
              std::vector<size_t> c;
@@ -1755,5 +1852,6 @@ PYBIND11_MODULE(_decision, m) {
       })
       .def("dist", [](const BatchRunner& b) { return npcopy(b.dist()); })
       .def("meta", [](const BatchRunner& b) { return npcopy(b.meta()); })
-      .def("metric", [](const BatchRunner& b) { return npcopy(b.metric()); });
+      .def("metric", [](const BatchRunner& b) { return npcopy(b.metric()); })
+      .def("mask", [](const BatchRunner& b) { return npcopy(b.mask()); });
 }

@@ -84,3 +84,54 @@ def reduce_stats(dist, torch, device, units, routes, digest, elapsed_s):
         rows = [g.tolist() for g in gathered]
     return (sum(r[0] for r in rows), sum(r[1] for r in rows),
             combine_digests(r[2] for r in rows), float(elapsed.item()), rows)
+
+
+def _h63(b):
+    return int.from_bytes(hashlib.sha256(b).digest()[:8], "little") >> 1
+
+
+def changes_digest(keys, changes):
+    """Config C4 job digest, independent of how variants are split over
+    ranks: XOR over variants of a hash of (global variant index, #routes to
+    update, #routes to delete, sorted changed prefixes) -- the
+    DecisionRouteUpdate key sets of calculateUpdate (SpfSolver.cpp:21-56).
+    `changes[i]` = (upd, del, prefixes) of variant keys[i]."""
+    out = 0
+    for k, (upd, dele, prefixes) in zip(keys, changes):
+        out ^= _h63(f"{k}\0{upd}\0{dele}\0".encode() +
+                    "\0".join(sorted(prefixes)).encode())
+    return out
+
+
+def lines_digest(lines):
+    """XOR of per-line hashes (config C5 KSP2 path lines "area dest k:...",
+    one per (destination, k)): independent of destination order and of the
+    destination blocks the ranks own."""
+    out = 0
+    for ln in lines:
+        out ^= _h63(ln.encode() if isinstance(ln, str) else bytes(ln))
+    return out
+
+
+def _to_i64(d):
+    d = int(d) & 0xFFFFFFFFFFFFFFFF
+    return d - (1 << 64) if d >= (1 << 63) else d
+
+
+def reduce_xor(dist, torch, device, digests):
+    """XOR-combine a list of 64-bit digests over all ranks (one all-gather);
+    with dist None the inputs are returned. The route digests of
+    route_digest.h are XOR-decomposable over units / prefixes, so the result
+    is the whole job's digest whatever the split."""
+    if dist is None:
+        return [int(d) & 0xFFFFFFFFFFFFFFFF for d in digests]
+    if dist.get_backend() == "gloo":
+        device = "cpu"
+    local = torch.tensor([_to_i64(d) for d in digests], dtype=torch.int64, device=device)
+    gathered = [torch.zeros_like(local) for _ in range(dist.get_world_size())]
+    dist.all_gather(gathered, local)
+    out = [0] * len(digests)
+    for g in gathered:
+        for i, v in enumerate(g.tolist()):
+            out[i] ^= int(v) & 0xFFFFFFFFFFFFFFFF
+    return out

@@ -11,6 +11,35 @@ areas (LinkState.cpp:674-703).
 """
 import random
 
+# C2 (BASELINE.json configs[1]): 4096 random-metric 10x10 grids per GPU
+# (topology t: metric seed 0xC2000000 + t, prefix seed 0xC1 + t), source "1"
+C2_OPTS = dict(n=10, metricSeed=0xC2000000, prefixSeed=0xC1)
+C2_SOURCE = "1"
+C2_TOPOS = 4096
+
+# C3-full: DecisionBenchmark fabric (RoutingBenchmarkUtils.cpp:421-473) with
+# every SSW wired to its plane's FSW in every pod, 100 prefixes per node,
+# every node a source
+C3_OPTS = dict(pods=32, planes=8, sswPerPlane=36, rswPerPod=48, full=True,
+               prefixesPerNode=100)
+
+
+def c3_source_names(pods=32, planes=8, ssw=36, rsw=48):
+    """Node names of topogen::fabric: SSW "1-plane-i", FSW "2-pod-plane",
+    RSW "3-pod-i"."""
+    return ([f"1-{p}-{s}" for p in range(planes) for s in range(ssw)] +
+            [f"2-{p}-{f}" for p in range(pods) for f in range(planes)] +
+            [f"3-{p}-{r}" for p in range(pods) for r in range(rsw)])
+
+
+# C4: 2,000-node WAN (seed 0xC4), one prefix per node, source "0"; 10,000
+# single/dual link-failure variants (seed 0xC4F, 50 % dual)
+C4_OPTS = dict(nodes=2000, seed=0xC4, prefixesPerNode=1)
+C4_SOURCE = "0"
+C4_VARIANTS = 10000
+C4_SEED = 0xC4F
+C4_DUAL_PERMILLE = 500
+
 C5_OPTS = dict(areas=8, nodesPerArea=1250, abrs=64, k=3, seed=0xC5A0,
                prefixesPerNode=10, anycastPermille=50)
 C5_SOURCE = "abr-0"

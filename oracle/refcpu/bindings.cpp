@@ -456,6 +456,64 @@ std::vector<RibPolicyStatementSpec> parseStatements(py::list stmts) {
 
 }  // namespace
 
+namespace rd {
+// Route digest (test infrastructure): the spec of
+// openr_amd/csrc/host/route_digest.h restated over the oracle's RouteDb --
+// FNV-1a 64 + splitmix64 over the RibUnicastEntry / NextHopThrift fields,
+// next hops summed, routes XOR-ed per unit key.
+uint64_t fnv(const std::string& s) {
+  uint64_t h = 1469598103934665603ull;
+  for (unsigned char c : s) h = (h ^ c) * 1099511628211ull;
+  return h;
+}
+uint64_t mix(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+uint64_t route(const RibUnicastEntry& r) {
+  uint64_t sum = 0;
+  for (const auto& n : r.nexthops) {
+    std::string k = n.addr + "%" + n.ifName.value_or("") + "|" +
+        n.neighborNodeName.value_or("") + "|" + n.area.value_or("") + "|";
+    if (n.mplsAction) {
+      k += std::to_string(n.mplsAction->action) + ":" +
+          std::to_string(n.mplsAction->swapLabel.value_or(-1));
+    }
+    sum += mix(fnv(k) ^ (uint64_t(uint32_t(n.metric)) << 32 | uint32_t(n.weight)));
+  }
+  uint64_t h = fnv(r.prefix);
+  h = mix(h ^ r.igpCost);
+  h = mix(h ^ fnv(r.bestArea));
+  h = mix(h ^ uint32_t(r.bestPrefixEntry.metrics.drain_metric));
+  h = mix(h ^ fnv(r.bestPrefixEntry.prefix));
+  h = mix(h ^ (r.localRouteConsidered ? 1u : 0u) ^ (r.doNotInstall ? 2u : 0u));
+  h = mix(h ^ fnv(r.counterID.value_or("-")));
+  return mix(h ^ sum);
+}
+uint64_t unit(const std::string& key, const std::optional<DecisionRouteDb>& db) {
+  const uint64_t k = fnv(key);
+  if (!db) return mix(k ^ 0x4E4F4E45ull);
+  uint64_t d = 0;
+  for (const auto& [_, r] : db->unicastRoutes) d ^= mix(k ^ route(r));
+  return d;
+}
+// Runs f(thread, i) for i in [0, n) on `threads` threads (static stride).
+template <typename F>
+void parallelFor(size_t n, int threads, F f) {
+  if (threads <= 0) threads = std::max(1u, std::thread::hardware_concurrency());
+  threads = std::max(1, std::min<int>(threads, int(std::max<size_t>(n, 1))));
+  std::vector<std::thread> pool;
+  for (int th = 0; th < threads; ++th) {
+    pool.emplace_back([&, th] {
+      for (size_t i = th; i < n; i += threads) f(th, i);
+    });
+  }
+  for (auto& t : pool) t.join();
+}
+}  // namespace rd
+
 PYBIND11_MODULE(_refcpu, m) {
   m.doc() = "CPU oracle (refcpu) for the Open/R Decision SPF+RouteDb path";
 
@@ -939,4 +997,291 @@ PYBIND11_MODULE(_refcpu, m) {
         return py::make_tuple(secs, units, total);
       },
       py::arg("opts"), py::arg("units"), py::arg("threads"), py::arg("source") = "1");
+
+  // ---- route digests (route_digest.h spec) of bench-size workloads ---------
+  // Per-source digests of a generated single-area LSDB: `threads` private
+  // replicas, sources strided over them.
+  m.def("gen_route_digests",
+        [](const std::string& kind, py::dict opts, std::vector<std::string> sources,
+           bool enableV4, bool sr, bool brs, int threads) {
+          auto g = genLsdb(kind, opts);
+          if (threads <= 0) threads = std::max(1u, std::thread::hardware_concurrency());
+          threads = std::max(1, std::min<int>(threads, int(std::max<size_t>(sources.size(), 1))));
+          std::vector<std::unique_ptr<Workspace>> reps(threads);
+          std::vector<uint64_t> out(sources.size());
+          {
+            py::gil_scoped_release nogil;
+            rd::parallelFor(reps.size(), threads, [&](int, size_t i) {
+              reps[i] = std::make_unique<Workspace>();
+              auto& ls =
+                  reps[i]->als.emplace(g.area, LinkState(g.area, "test_node")).first->second;
+              loadLsdb(g, ls, reps[i]->ps);
+            });
+            rd::parallelFor(sources.size(), threads, [&](int th, size_t i) {
+              SpfSolver solver("test_node", enableV4, sr, brs);
+              out[i] = rd::unit(sources[i], solver.buildRouteDb(sources[i], reps[th]->als,
+                                                                reps[th]->ps));
+            });
+          }
+          return out;
+        },
+        py::arg("kind"), py::arg("opts"), py::arg("sources"), py::arg("enableV4") = true,
+        py::arg("sr") = false, py::arg("brs") = false, py::arg("threads") = 0);
+
+  // Per-topology digests of the C2 grid batch [lo, hi) (key = str(index)).
+  m.def("grid_batch_digests",
+        [](py::dict opts, int lo, int hi, const std::string& source, bool brs, int threads) {
+          auto base = gridOpts(opts);
+          std::vector<uint64_t> out(std::max(0, hi - lo));
+          py::gil_scoped_release nogil;
+          rd::parallelFor(out.size(), threads, [&](int, size_t i) {
+            const int t = lo + int(i);
+            auto o = base;
+            o.metricSeed = base.metricSeed + t;
+            o.prefixSeed = base.prefixSeed + t;
+            if (o.overloadSeed) o.overloadSeed = base.overloadSeed + t;
+            auto g = topogen::grid(o);
+            Workspace w;
+            auto& ls = w.als.emplace(g.area, LinkState(g.area, "test_node")).first->second;
+            loadLsdb(g, ls, w.ps);
+            SpfSolver solver("test_node", true, false, brs);
+            out[i] = rd::unit(std::to_string(t), solver.buildRouteDb(source, w.als, w.ps));
+          });
+          return out;
+        },
+        py::arg("opts"), py::arg("lo"), py::arg("hi"), py::arg("source") = "1",
+        py::arg("brs") = false, py::arg("threads") = 0);
+
+  // Config C4 job: per variant (#update, #delete, sorted changed prefixes)
+  // of calculateUpdate(base, variant) -- the reference's incremental path on
+  // private replicas (updateAdjacencyDatabase of the endpoints, buildRouteDb,
+  // calculateUpdate, restore), like cpu_baseline_variants.
+  m.def("variant_changes",
+        [](const std::string& kind, py::dict opts, const std::string& source, int count,
+           uint64_t seed, int dualPermille, int threads) {
+          auto g = genLsdb(kind, opts);
+          auto variants = topogen::linkFailureVariants(g, count, seed, dualPermille);
+          if (threads <= 0) threads = std::max(1u, std::thread::hardware_concurrency());
+          std::map<std::string, const topogen::AdjDb*> byName;
+          for (const auto& d : g.adjDbs) byName[d.thisNodeName] = &d;
+          struct Replica {
+            Workspace w;
+            std::optional<DecisionRouteDb> base;
+          };
+          std::vector<std::unique_ptr<Replica>> reps(threads);
+          for (auto& r : reps) {
+            r = std::make_unique<Replica>();
+            auto& ls = r->w.als.emplace(g.area, LinkState(g.area, "test_node")).first->second;
+            loadLsdb(g, ls, r->w.ps);
+            SpfSolver solver("test_node", true, false, false);
+            r->base = solver.buildRouteDb(source, r->w.als, r->w.ps);
+          }
+          struct Out {
+            size_t upd{0}, del{0};
+            std::vector<std::string> changed;
+          };
+          std::vector<Out> out(variants.size());
+          {
+            py::gil_scoped_release nogil;
+            rd::parallelFor(variants.size(), threads, [&](int th, size_t v) {
+              Replica& r = *reps[th];
+              LinkState& ls = r.w.als.at(g.area);
+              std::set<std::string> nodes;
+              for (const auto& f : variants[v]) {
+                nodes.insert(f.a);
+                nodes.insert(f.b);
+              }
+              for (const auto& n : nodes) {
+                topogen::AdjDb d = *byName.at(n);
+                auto& a = d.adjs;
+                a.erase(std::remove_if(a.begin(), a.end(), [&](const topogen::Adj& x) {
+                          for (const auto& f : variants[v]) {
+                            if ((n == f.a && x.ifName == f.ifA) ||
+                                (n == f.b && x.ifName == f.ifB)) {
+                              return true;
+                            }
+                          }
+                          return false;
+                        }), a.end());
+                ls.updateAdjacencyDatabase(toAdjDb(d, g.area), g.area);
+              }
+              SpfSolver solver("test_node", true, false, false);
+              auto db = solver.buildRouteDb(source, r.w.als, r.w.ps);
+              const auto upd = r.base->calculateUpdate(db ? *db : DecisionRouteDb{});
+              Out& o = out[v];
+              o.upd = upd.unicastRoutesToUpdate.size();
+              o.del = upd.unicastRoutesToDelete.size();
+              for (const auto& [p, _] : upd.unicastRoutesToUpdate) o.changed.push_back(p);
+              for (const auto& p : upd.unicastRoutesToDelete) o.changed.push_back(p);
+              std::sort(o.changed.begin(), o.changed.end());
+              for (const auto& n : nodes) {
+                ls.updateAdjacencyDatabase(toAdjDb(*byName.at(n), g.area), g.area);
+              }
+            });
+          }
+          py::list res;
+          for (const auto& o : out) res.append(py::make_tuple(o.upd, o.del, o.changed));
+          return res;
+        },
+        py::arg("kind"), py::arg("opts"), py::arg("source"), py::arg("count"),
+        py::arg("seed") = 0xC4F, py::arg("dualPermille") = 500, py::arg("threads") = 0);
+
+  // Multi-area RouteDb digest (+ RibPolicy) of one source.
+  m.def("gen_route_digest_multiarea",
+        [](py::dict d, const std::string& source, bool enableV4, bool sr, bool brs,
+           py::list policy) {
+          AreaLinkStates als;
+          PrefixState ps;
+          loadMultiArea(d, als, ps);
+          SpfSolver solver("test_node", enableV4, sr, brs);
+          auto db = solver.buildRouteDb(source, als, ps);
+          if (db && !policy.empty()) {
+            RibPolicy pol(parseStatements(policy), 3600);
+            pol.applyPolicy(db->unicastRoutes);
+          }
+          return rd::unit(source, db);
+        },
+        py::arg("opts"), py::arg("source"), py::arg("enableV4") = true, py::arg("sr") = false,
+        py::arg("brs") = false, py::arg("policy") = py::list());
+
+  // KSP2 of every destination of the source's areas (config C5): lines
+  // "area dest k:<paths>" for k = 1, 2, areas in name order, destinations in
+  // name order; `threads` private replicas.
+  m.def("kth_paths_all_multiarea",
+        [](py::dict d, const std::string& source, int threads) {
+          if (threads <= 0) threads = std::max(1u, std::thread::hardware_concurrency());
+          std::vector<std::unique_ptr<Workspace>> reps(threads);
+          for (auto& r : reps) {
+            r = std::make_unique<Workspace>();
+            loadMultiArea(d, r->als, r->ps);
+          }
+          std::vector<std::pair<std::string, std::string>> all;
+          for (const auto& [area, ls] : reps[0]->als) {
+            if (!ls.getAdjacencyDatabases().count(source)) continue;
+            for (const auto& [n, _] : ls.getAdjacencyDatabases()) {
+              if (n != source) all.emplace_back(area, n);
+            }
+          }
+          std::vector<std::string> out(2 * all.size());
+          {
+            py::gil_scoped_release nogil;
+            rd::parallelFor(all.size(), threads, [&](int th, size_t i) {
+              const LinkState& ls = reps[th]->als.at(all[i].first);
+              for (size_t k = 1; k <= 2; ++k) {
+                out[2 * i + k - 1] = all[i].first + " " + all[i].second + " " +
+                    std::to_string(k) + ":" + pathsText(ls.getKthPaths(source, all[i].second, k));
+              }
+            });
+          }
+          return out;
+        },
+        py::arg("opts"), py::arg("source"), py::arg("threads") = 0);
+
+  m.def("route_db_digest", [](const DecisionRouteDb& db, const std::string& key) {
+    return rd::unit(key, db);
+  });
+
+  // (area names, the source's neighbours over all areas) of a multi-area
+  // domain: the inputs of openr_amd.workloads.c5_policy
+  m.def("multiarea_source_info", [](py::dict d, const std::string& source) {
+    AreaLinkStates als;
+    PrefixState ps;
+    loadMultiArea(d, als, ps);
+    std::vector<std::string> areas;
+    std::set<std::string> nbrs;
+    for (const auto& [area, ls] : als) {
+      areas.push_back(area);
+      for (const auto& l : ls.linksFromNode(source)) nbrs.insert(l->getOtherNodeName(source));
+    }
+    return py::make_tuple(areas, std::vector<std::string>(nbrs.begin(), nbrs.end()));
+  });
+
+  // ---- CPU baselines (timed on the GPU box's host cores by bench.py) -------
+  // Config C1: buildRouteDb(source) on a fresh replica per repetition
+  // (ingestion untimed), one thread. Returns the microseconds of each rep.
+  m.def("cpu_time_build",
+        [](const std::string& kind, py::dict opts, const std::string& source, int reps) {
+          auto g = genLsdb(kind, opts);
+          std::vector<double> us;
+          for (int r = 0; r < reps; ++r) {
+            Workspace w;
+            auto& ls = w.als.emplace(g.area, LinkState(g.area, "test_node")).first->second;
+            loadLsdb(g, ls, w.ps);
+            SpfSolver solver("test_node", true, false, false);
+            auto t0 = std::chrono::steady_clock::now();
+            auto db = solver.buildRouteDb(source, w.als, w.ps);
+            us.push_back(std::chrono::duration<double, std::micro>(
+                             std::chrono::steady_clock::now() - t0).count());
+            if (!db) throw std::runtime_error("no RouteDb for " + source);
+          }
+          return us;
+        },
+        py::arg("kind"), py::arg("opts"), py::arg("source"), py::arg("reps"));
+
+  // Config C3 sample: buildRouteDb of `sources` on `threads` threads, each
+  // with a private replica (built untimed, in parallel), sources strided
+  // over threads; `reps` timed repetitions. Returns ([wall seconds], routes).
+  m.def("cpu_baseline_sources",
+        [](const std::string& kind, py::dict opts, std::vector<std::string> sources,
+           int threads, int reps) {
+          auto g = genLsdb(kind, opts);
+          threads = std::max(1, std::min<int>(threads, int(std::max<size_t>(sources.size(), 1))));
+          std::vector<std::unique_ptr<Workspace>> ws(threads);
+          std::vector<size_t> routes(threads, 0);
+          std::vector<double> secs;
+          {
+            py::gil_scoped_release nogil;
+            rd::parallelFor(ws.size(), threads, [&](int, size_t i) {
+              ws[i] = std::make_unique<Workspace>();
+              auto& ls = ws[i]->als.emplace(g.area, LinkState(g.area, "test_node")).first->second;
+              loadLsdb(g, ls, ws[i]->ps);
+            });
+            for (int r = 0; r < reps; ++r) {
+              std::fill(routes.begin(), routes.end(), 0);
+              auto t0 = std::chrono::steady_clock::now();
+              rd::parallelFor(sources.size(), threads, [&](int th, size_t i) {
+                SpfSolver solver("test_node", true, false, false);
+                auto db = solver.buildRouteDb(sources[i], ws[th]->als, ws[th]->ps);
+                if (db) routes[th] += db->unicastRoutes.size();
+              });
+              secs.push_back(std::chrono::duration<double>(
+                                 std::chrono::steady_clock::now() - t0).count());
+            }
+          }
+          size_t total = 0;
+          for (auto r : routes) total += r;
+          return py::make_tuple(secs, total);
+        },
+        py::arg("kind"), py::arg("opts"), py::arg("sources"), py::arg("threads"),
+        py::arg("reps") = 1);
+
+  // Decision's incremental branch in the reference (Decision.cpp:929-938):
+  // createRouteForPrefixOrGetStaticRoute per changed prefix, the SPF memo
+  // warm (a prefix-only change leaves the topology, hence the memo, valid).
+  // The changed set: every (P / n)-th prefix, as the engine's
+  // incremental_routes_bench picks it. Returns (ms, prefixes, routes).
+  m.def("cpu_incremental_routes",
+        [](const std::string& kind, py::dict opts, const std::string& me, int n) {
+          auto g = genLsdb(kind, opts);
+          Workspace w;
+          auto& ls = w.als.emplace(g.area, LinkState(g.area, "test_node")).first->second;
+          loadLsdb(g, ls, w.ps);
+          std::vector<std::string> changed;
+          const size_t stride = std::max<size_t>(1, w.ps.prefixes().size() / std::max(n, 1));
+          size_t i = 0;
+          for (const auto& [p, _] : w.ps.prefixes()) {
+            if (i++ % stride == 0 && int(changed.size()) < n) changed.push_back(p);
+          }
+          SpfSolver solver("test_node", true, false, false);
+          ls.getSpfResult(me, true);  // the memo a previous build left
+          size_t routes = 0;
+          auto t0 = std::chrono::steady_clock::now();
+          for (const auto& p : changed) {
+            routes += solver.createRouteForPrefixOrGetStaticRoute(me, w.als, w.ps, p) ? 1 : 0;
+          }
+          const double ms = std::chrono::duration<double, std::milli>(
+                                std::chrono::steady_clock::now() - t0).count();
+          return py::make_tuple(ms, changed.size(), routes);
+        },
+        py::arg("kind"), py::arg("opts"), py::arg("me"), py::arg("n"));
 }
