@@ -15,6 +15,7 @@
 // missing device or an input outside the GPU engine's domain throws.
 #pragma once
 
+#include <chrono>
 #include <cstdint>
 #include <limits>
 #include <map>
@@ -563,7 +564,13 @@ class RibPolicy {  // RibPolicy.h:70-124
  public:
   RibPolicy(const std::vector<RibPolicyStatementSpec>& statements,
             int64_t ttlSecs);
-  bool isActive() const { return ttlSecs_ > 0; }
+  // RibPolicy.cpp:167-171,199-208: valid until ctor time + ttl_secs
+  bool isActive() const { return std::chrono::steady_clock::now() < validUntil_; }
+  int64_t getTtlDurationMs() const {
+    return std::chrono::duration_cast<std::chrono::milliseconds>(
+               validUntil_ - std::chrono::steady_clock::now())
+        .count();
+  }
   bool match(const RibUnicastEntry& route) const;
   bool applyAction(RibUnicastEntry& route) const;
   std::vector<std::string> applyPolicy(
@@ -592,7 +599,7 @@ class RibPolicy {  // RibPolicy.h:70-124
   };
   bool matchStmt(const Stmt& s, const RibUnicastEntry& r) const;
   std::vector<Stmt> stmts_;
-  int64_t ttlSecs_;
+  std::chrono::steady_clock::time_point validUntil_;
 
  public:
   uint64_t uid() const { return uid_; }  // compiled-policy cache key

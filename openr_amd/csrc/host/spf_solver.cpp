@@ -1033,7 +1033,7 @@ std::map<std::string, std::optional<RibUnicastEntry>> SpfSolver::createRoutesFor
 // ------------------------------------------------------------- RibPolicy --
 RibPolicy::RibPolicy(const std::vector<RibPolicyStatementSpec>& statements,
                      int64_t ttlSecs)
-    : ttlSecs_(ttlSecs) {  // RibPolicy.cpp:20-50, 167-182
+    : validUntil_(std::chrono::steady_clock::now() + std::chrono::seconds(ttlSecs)) {  // RibPolicy.cpp:20-50, 167-182
   static std::atomic<uint64_t> nextUid{1};
   uid_ = nextUid++;
   if (statements.empty()) {

@@ -927,7 +927,7 @@ bool RibPolicyStatement::applyAction(RibUnicastEntry& r) const {
 
 RibPolicy::RibPolicy(const std::vector<RibPolicyStatementSpec>& stmts,
                      int64_t ttlSecs)
-    : ttlSecs_(ttlSecs) {
+    : validUntil_(std::chrono::steady_clock::now() + std::chrono::seconds(ttlSecs)) {
   if (stmts.empty()) {
     throw std::invalid_argument("Missing policy.statements attribute");
   }

@@ -20,6 +20,7 @@
 // links by their ordered name tuple instead (canonical order).
 #pragma once
 
+#include <chrono>
 #include <cstdint>
 #include <limits>
 #include <map>
@@ -497,7 +498,13 @@ class RibPolicyStatement {
 class RibPolicy {
  public:
   RibPolicy(const std::vector<RibPolicyStatementSpec>& stmts, int64_t ttlSecs);
-  bool isActive() const { return ttlSecs_ > 0; }
+  // RibPolicy.cpp:167-171,199-208: valid until ctor time + ttl_secs
+  bool isActive() const { return std::chrono::steady_clock::now() < validUntil_; }
+  int64_t getTtlDurationMs() const {
+    return std::chrono::duration_cast<std::chrono::milliseconds>(
+               validUntil_ - std::chrono::steady_clock::now())
+        .count();
+  }
   bool match(const RibUnicastEntry& r) const;
   bool applyAction(RibUnicastEntry& r) const;
   std::vector<std::string> applyPolicy(
@@ -505,7 +512,7 @@ class RibPolicy {
 
  private:
   std::vector<RibPolicyStatement> statements_;
-  int64_t ttlSecs_;
+  std::chrono::steady_clock::time_point validUntil_;
 };
 
 }  // namespace refcpu

@@ -3,6 +3,11 @@ import sys
 
 import pytest
 
+# torch before the engine library: one HIP runtime per process, and torch's
+# must be the one libopenr_gpu.so binds to (the bench-size tests drive the
+# engine through torch-owned device buffers and streams, as bench.py does)
+import torch  # noqa: F401
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 for p in (ROOT, os.path.join(ROOT, "tests"), os.path.join(ROOT, "oracle")):
     if p not in sys.path:

@@ -687,3 +687,7 @@ ALL_KATS = [
 # multi-area known-answer tests (tests/kat_multiarea.py)
 from kat_multiarea import MULTI_AREA_KATS  # noqa: E402
 ALL_KATS += MULTI_AREA_KATS
+
+# further cases (tests/kat_more.py)
+from kat_more import MORE_KATS  # noqa: E402
+ALL_KATS += MORE_KATS
