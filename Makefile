@@ -27,9 +27,16 @@ $(CCONS): tests/c_consumer/spf_square.c include/openr_gpu.h $(LIB)
 	  -Wl,-rpath,'$$ORIGIN/../../openr_amd/lib'
 
 
-$(LIB): $(KERNELS) $(KERNEL_H) include/openr_gpu.h
+# one object per kernel translation unit (parallel make), then one link
+KOBJ := $(patsubst openr_amd/csrc/kernels/%.hip,build/kernels/%.o,$(KERNELS))
+
+build/kernels/%.o: openr_amd/csrc/kernels/%.hip $(KERNEL_H) include/openr_gpu.h
+	@mkdir -p build/kernels
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Iinclude -c $< -o $@
+
+$(LIB): $(KOBJ)
 	@mkdir -p openr_amd/lib
-	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -shared -Iinclude $(KERNELS) -o $@
+	$(HIPCC) --offload-arch=$(ARCH) -shared $(KOBJ) -o $@.tmp && mv -f $@.tmp $@
 
 $(MOD): $(HOST) $(HOST_H) openr_amd/csrc/py/bindings.cpp $(LIB)
 	$(CXX) -O2 -std=c++17 -fPIC -shared -Wall -Wno-unused-function \
@@ -49,7 +56,7 @@ $(STAMPS): $(KERNELS) $(KERNEL_H) include/openr_gpu.h
 	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -shared -DOGS_STAMPS -Iinclude $(KERNELS) -o $@
 
 clean:
-	rm -f $(LIB) $(MOD) $(STAMPS) $(CCONS)
+	rm -f $(LIB) $(MOD) $(STAMPS) $(CCONS) $(KOBJ)
 	$(MAKE) -C oracle clean
 
 .PHONY: all oracle clean stamps

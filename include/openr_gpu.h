@@ -255,6 +255,11 @@ int ogs_stream_sync(void* stream);
  *                 over packed {dist, next hops} words when the next-hop sets
  *                 fit one word), the chunk scan otherwise; 0 always the scan;
  *                 1 lists whenever they fit in LDS; 2 lists, two phases.
+ *   "spf_global": 0 (default) units whose SPF state does not fit LDS
+ *                 (tens of thousands of nodes) run the global-state path
+ *                 (dist / next-hop sets / frontier lists in HBM, one 1024-
+ *                 thread workgroup per unit, then one thread per route); 1
+ *                 every ogs_spf_routes call takes that path (A/B, tests).
  *   "ksp_queue":  KSP2 batch SPF: 1 (default) LDS node lists, 0 the pull
  *                 fixpoint. "ksp_stage": -1 (default) auto, 0 CSR read
  *                 from HBM/L2, 1 row offsets in LDS, 2 rows + edges in LDS. */

@@ -14,6 +14,7 @@ extern int g_waveUpb;
 extern int g_msGroup;
 extern int g_routeStream;
 extern int g_spfFrontier;
+extern int g_spfGlobal;
 extern int g_spfQueue;
 extern int g_spfNinfo;
 extern int g_kspQueue;
@@ -161,6 +162,11 @@ int ogs_set_option(const char* name, int64_t value) {
       return fail(OGS_E_INVALID, "spf_frontier must be 0 or 1");
     }
     ogs::g_spfFrontier = int(value);
+    return OGS_OK;
+  }
+  if (std::strcmp(name, "spf_global") == 0) {
+    if (value != 0 && value != 1) return fail(OGS_E_INVALID, "spf_global must be 0 or 1");
+    ogs::g_spfGlobal = int(value);
     return OGS_OK;
   }
   if (std::strcmp(name, "ksp_queue") == 0) {

@@ -1,0 +1,288 @@
+// spf_global.hip — SPF + RouteDb for topologies past the LDS budget (SURVEY
+// §8 row g1 "global frontier": WAN areas of tens of thousands of nodes, the
+// reference's 99x99 GridTopology.StressTest, SpfSolverTest.cpp:2858-2873).
+//
+// Same fixpoint as spf_core.h / spf_frontier.hip (reference: LinkState::runSpf,
+// LinkState.cpp:720-820; distances are the least solution of dist(v) = min
+// over usable u of dist(u) + w(u, v), next-hop sets the least solution of
+// NH(v) = U over tight u of (u == src ? {slot} : NH(u)), u relaxing iff u is
+// the source or not hard-drained, 741-752). What differs is where the unit's
+// state lives: dist / next-hop sets / push stamps / the two frontier lists
+// are in HBM (the caller's output rows or the workspace), so there is no
+// size limit but the 21-bit node ids of the edge encoding. One workgroup of
+// 1024 threads per unit walks the frontier list of the round; relaxations
+// are L2 atomics (atomicMin / atomicOr); after each workgroup barrier an
+// agent-scope acquire fence invalidates the CU's vector L1 so the next
+// round reads what the atomics left in L2. Every round costs one barrier
+// and touches only the rows of the nodes changed in the previous round.
+//
+// Routes: route_global_kernel, one thread per (unit, prefix): route_one
+// (route_core.h) against the unit's state in HBM (no per-node LDS staging),
+// coalesced record stores. u32 or u64 distances (OGS_F_WIDE_METRIC).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "openr_gpu.h"
+#include "route_core.h"
+#include "spf_core.h"
+
+namespace ogs {
+
+constexpr int kGBlock = 1024;
+
+__device__ __forceinline__ void round_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+}
+
+template <typename D>
+__device__ __forceinline__ D atomic_min_d(D* p, D v) {
+  return atomicMin(p, v);
+}
+
+// One unit's SPF into HBM. dist[v] (D), nh[w * Sn + v], stamp/q0/q1 scratch
+// rows of this unit (>= N entries each).
+template <typename D, int W>
+__global__ __launch_bounds__(kGBlock) void spf_global_kernel(
+    ogs_graph g, const ogs_unit* __restrict__ units, uint32_t flags,
+    D* __restrict__ oDist, uint32_t* __restrict__ oNh, uint32_t* __restrict__ scratch) {
+  constexpr D kInf = DistInf<D>::value;
+  const int tid = threadIdx.x;
+  const uint32_t u0 = blockIdx.x;
+  const ogs_unit unit = units[u0];
+  const uint32_t s = unit.src;
+  const uint32_t nb = g.node_base[unit.topo];
+  const uint32_t N = g.node_base[unit.topo + 1] - nb;
+  const size_t Sn = size_t(g.max_nodes);
+  const uint32_t* __restrict__ gRow = g.row_ptr + nb;
+  const uint32_t e0 = gRow[0];
+  const uint64_t* __restrict__ edges = g.edges + e0;
+  const uint8_t* __restrict__ nflags = g.node_flags + nb;
+  const bool hop = (flags & OGS_F_HOP_METRIC) != 0;
+  D* dist = oDist + u0 * Sn;
+  uint32_t* nh = oNh + u0 * W * Sn;
+  uint32_t* stamp = scratch + u0 * 3 * Sn;
+  uint32_t* q0 = stamp + Sn;
+  uint32_t* q1 = q0 + Sn;
+  __shared__ uint32_t qcnt[3];
+
+  for (uint32_t v = tid; v < N; v += kGBlock) {
+    dist[v] = (v == s) ? D(0) : kInf;
+    stamp[v] = 0u;
+#pragma unroll
+    for (int w = 0; w < W; ++w) nh[w * Sn + v] = 0u;
+  }
+  if (tid == 0) {
+    q1[0] = s;  // round 1's list: buffer r & 1, count slot r % 3
+    qcnt[0] = 0u;
+    qcnt[1] = 1u;
+    qcnt[2] = 0u;
+  }
+  round_sync();
+  auto append = [&](uint32_t t, uint32_t r) {
+    if (atomicMax(&stamp[t], r + 1) < r + 1) {
+      const uint32_t at = atomicAdd(&qcnt[(r + 1) % 3], 1u);
+      ((r + 1) & 1 ? q1 : q0)[at] = t;
+    }
+  };
+  auto weight = [&](uint64_t x) -> D {
+    return hop ? D(1) : D(static_cast<uint32_t>(x >> 32));
+  };
+
+  // ---- dist phase: rows of the nodes whose distance dropped last round ----
+  uint32_t r = 1, n = 1;
+  for (; n; ++r) {
+    if (tid == 0) qcnt[(r + 2) % 3] = 0u;
+    const uint32_t* cur = (r & 1) ? q1 : q0;
+    for (uint32_t i = tid; i < n; i += kGBlock) {
+      const uint32_t v = cur[i];
+      if (v != s && (nflags[v] & OGS_NODE_OVERLOADED)) continue;  // 741-752
+      const D dv = dist[v];
+      const uint32_t b = gRow[v] - e0, m = gRow[v + 1] - e0 - b;
+      for (uint32_t j = 0; j < m; ++j) {
+        const uint64_t x = edges[b + j];
+        const uint32_t lo = static_cast<uint32_t>(x);
+        if (lo & OGS_EDGE_DOWN) continue;
+        const uint32_t t = edge_dst(lo);
+        const D c = dv + weight(x);
+        if (c < dist[t] && c < atomic_min_d(&dist[t], c)) append(t, r);
+      }
+    }
+    round_sync();
+    n = qcnt[(r + 1) % 3];
+    __syncthreads();  // every thread has read the count before it is reset
+  }
+
+  // ---- next-hop phase: the source's row seeds link slots, tight pushes ----
+  const uint32_t r0 = r;
+  if (tid == 0) qcnt[0] = qcnt[1] = qcnt[2] = 0u;
+  round_sync();
+  {
+    const uint32_t b = gRow[s] - e0, m = gRow[s + 1] - e0 - b;
+    for (uint32_t j = tid; j < m && j < 32u * W; j += kGBlock) {
+      const uint64_t x = edges[b + j];
+      const uint32_t lo = static_cast<uint32_t>(x);
+      if (lo & OGS_EDGE_DOWN) continue;
+      const uint32_t t = edge_dst(lo);
+      if (weight(x) == dist[t]) {
+        atomicOr(&nh[(j >> 5) * Sn + t], 1u << (j & 31u));
+        append(t, r0);
+      }
+    }
+  }
+  round_sync();
+  n = qcnt[(r0 + 1) % 3];
+  __syncthreads();
+  for (r = r0 + 1; n; ++r) {
+    if (tid == 0) qcnt[(r + 2) % 3] = 0u;
+    const uint32_t* cur = (r & 1) ? q1 : q0;
+    for (uint32_t i = tid; i < n; i += kGBlock) {
+      const uint32_t v = cur[i];
+      if (v == s || (nflags[v] & OGS_NODE_OVERLOADED)) continue;
+      const D dv = dist[v];
+      uint32_t nv[W];
+#pragma unroll
+      for (int w = 0; w < W; ++w) nv[w] = nh[w * Sn + v];
+      const uint32_t b = gRow[v] - e0, m = gRow[v + 1] - e0 - b;
+      for (uint32_t j = 0; j < m; ++j) {
+        const uint64_t x = edges[b + j];
+        const uint32_t lo = static_cast<uint32_t>(x);
+        if (lo & OGS_EDGE_DOWN) continue;
+        const uint32_t t = edge_dst(lo);
+        if (dv + weight(x) != dist[t]) continue;
+        bool add = false;
+#pragma unroll
+        for (int k = 0; k < W; ++k) {
+          const uint32_t a = nv[k] & ~nh[k * Sn + t];
+          if (a && (a & ~atomicOr(&nh[k * Sn + t], a))) add = true;
+        }
+        if (add) append(t, r);
+      }
+    }
+    round_sync();
+    n = qcnt[(r + 1) % 3];
+    __syncthreads();
+  }
+}
+
+// Unit state in HBM as the route kernel reads it.
+template <typename D, int W>
+struct GlobalView {
+  const D* d;
+  const uint32_t* n;
+  size_t Sn;
+  __device__ __forceinline__ D dist(uint32_t v) const { return d[v]; }
+  __device__ __forceinline__ uint32_t nh(uint32_t v, int w) const {
+    return n[size_t(w) * Sn + v];
+  }
+};
+
+// One thread per (unit, prefix): route_one against the unit's HBM state
+// (grid x = unit, y = prefix block of 256).
+template <typename D, int W>
+__global__ __launch_bounds__(kBlock) void route_global_kernel(
+    ogs_graph g, ogs_prefix_table pt, const ogs_unit* __restrict__ units,
+    uint32_t flags, const D* __restrict__ sDist, const uint32_t* __restrict__ sNh,
+    ogs_spf_out out) {
+  const uint32_t u = blockIdx.x;
+  const uint32_t p = blockIdx.y * kBlock + threadIdx.x;
+  const ogs_unit unit = units[u];
+  const uint32_t Sp = uint32_t(pt.max_prefixes);
+  const uint32_t p0 = pt.pfx_base[unit.topo];
+  const uint32_t P = pt.pfx_base[unit.topo + 1] - p0;
+  if (p >= Sp) return;
+  const size_t Sn = size_t(g.max_nodes);
+  const size_t rec = size_t(u) * Sp + p;
+  uint32_t meta = 0, selBits = 0, mask[W];
+  D metric = DistInf<D>::value;
+#pragma unroll
+  for (int w = 0; w < W; ++w) mask[w] = 0u;
+  if (p < P) {
+    const RouteCfg cfg{(flags & OGS_F_ENABLE_V4) != 0, (flags & OGS_F_V4_OVER_V6) != 0,
+                       (flags & OGS_F_BEST_ROUTE_SELECTION) != 0};
+    const GlobalView<D, W> sv{sDist + u * Sn, sNh + size_t(u) * W * Sn, Sn};
+    route_one<D, W>(pt, p0 + p, unit.src, g.node_flags + g.node_base[unit.topo], sv, cfg,
+                    meta, metric, mask, selBits);
+  }
+  if (out.meta) out.meta[rec] = meta;
+  if (out.metric) static_cast<D*>(out.metric)[rec] = metric;
+  if (out.sel) out.sel[rec] = selBits;
+  if (out.mask) {
+#pragma unroll
+    for (int w = 0; w < W; ++w) out.mask[(size_t(u) * W + w) * Sp + p] = mask[w];
+  }
+}
+
+hipError_t workspace(size_t bytes, hipStream_t stream, void** out);
+
+// "spf_global" option: 0 (default) the global path only where the LDS paths
+// cannot hold a unit, 1 every ogs_spf_routes call (A/B, parity tests).
+int g_spfGlobal = 0;
+
+// Does the LDS-resident workgroup path fit a unit of this graph? (the last
+// fallback of spf_route.hip: dist + next-hop words, CSR read from L2)
+bool lds_unit_fits(const ogs_graph& g, int W, uint32_t flags) {
+  const uint64_t d = (flags & OGS_F_WIDE_METRIC) ? 8 : 4;
+  const uint64_t b = ((uint64_t(g.max_nodes) * d + 15) & ~15ull) +
+      ((uint64_t(g.max_nodes) * W * 4 + 15) & ~15ull);
+  return b <= 160u * 1024u;
+}
+
+bool use_global(const ogs_graph& g, int W, uint32_t flags) {
+  return g_spfGlobal == 1 || !lds_unit_fits(g, W, flags);
+}
+
+template <typename D, int W>
+hipError_t launch_global_w(const ogs_graph& g, const ogs_prefix_table* pt,
+                           const ogs_unit* units, int nUnits, uint32_t flags,
+                           const ogs_spf_out& out, hipStream_t stream) {
+  const size_t Sn = size_t(g.max_nodes);
+  const size_t U = size_t(nUnits);
+  auto r256 = [](size_t x) { return (x + 255) & ~size_t(255); };
+  const size_t distBytes = out.dist ? 0 : r256(U * Sn * sizeof(D));
+  const size_t nhBytes = out.nh ? 0 : r256(U * W * Sn * 4);
+  const size_t scratchBytes = r256(U * 3 * Sn * 4);
+  void* ws = nullptr;
+  hipError_t e = workspace(distBytes + nhBytes + scratchBytes, stream, &ws);
+  if (e != hipSuccess) return e;
+  char* base = static_cast<char*>(ws);
+  D* dist = out.dist ? static_cast<D*>(out.dist) : reinterpret_cast<D*>(base);
+  uint32_t* nh = out.nh ? out.nh : reinterpret_cast<uint32_t*>(base + distBytes);
+  uint32_t* scratch = reinterpret_cast<uint32_t*>(base + distBytes + nhBytes);
+  hipLaunchKernelGGL((spf_global_kernel<D, W>), dim3(nUnits), dim3(kGBlock), 0, stream, g,
+                     units, flags, dist, nh, scratch);
+  e = hipGetLastError();
+  if (e != hipSuccess || !pt || pt->max_prefixes == 0) return e;
+  const unsigned bx = unsigned((pt->max_prefixes + kBlock - 1) / kBlock);
+  hipLaunchKernelGGL((route_global_kernel<D, W>), dim3(unsigned(nUnits), bx), dim3(kBlock), 0,
+                     stream, g, *pt, units, flags, dist, nh, out);
+  return hipGetLastError();
+}
+
+template <typename D>
+hipError_t launch_global_d(const ogs_graph& g, const ogs_prefix_table* pt,
+                           const ogs_unit* units, int nUnits, uint32_t flags, int W,
+                           const ogs_spf_out& out, hipStream_t stream) {
+  switch (W) {
+    case 1: return launch_global_w<D, 1>(g, pt, units, nUnits, flags, out, stream);
+    case 2: return launch_global_w<D, 2>(g, pt, units, nUnits, flags, out, stream);
+    case 4: return launch_global_w<D, 4>(g, pt, units, nUnits, flags, out, stream);
+    case 8: return launch_global_w<D, 8>(g, pt, units, nUnits, flags, out, stream);
+    case 16: return launch_global_w<D, 16>(g, pt, units, nUnits, flags, out, stream);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+// SPF (+ RouteDb when pt is non-NULL) of every unit through the global path.
+hipError_t launch_spf_routes_global(const ogs_graph& g, const ogs_prefix_table* pt,
+                                    const ogs_unit* units, int nUnits, uint32_t flags,
+                                    int W, const ogs_spf_out& out, hipStream_t stream) {
+  if (flags & OGS_F_WIDE_METRIC) {
+    return launch_global_d<uint64_t>(g, pt, units, nUnits, flags, W, out, stream);
+  }
+  return launch_global_d<uint32_t>(g, pt, units, nUnits, flags, W, out, stream);
+}
+
+}  // namespace ogs

@@ -223,10 +223,19 @@ int g_unitWidth = [] {
 }();
 int small_unit_width() { return g_unitWidth; }
 
+bool use_global(const ogs_graph& g, int W, uint32_t flags);
+hipError_t launch_spf_routes_global(const ogs_graph& g, const ogs_prefix_table* pt,
+                                    const ogs_unit* units, int nUnits, uint32_t flags,
+                                    int W, const ogs_spf_out& out, hipStream_t stream);
+
 hipError_t launch_spf_routes(const ogs_graph& g, const ogs_prefix_table* pt,
                              const ogs_unit* units, int nUnits,
                              uint32_t flags, int W, const ogs_spf_out& out,
                              hipStream_t stream, int* unsupported) {
+  // units too large for LDS (or the "spf_global" option): state in HBM
+  if (use_global(g, W, flags)) {
+    return launch_spf_routes_global(g, pt, units, nUnits, flags, W, out, stream);
+  }
   ogs_prefix_table empty{};
   const ogs_prefix_table& p = pt ? *pt : empty;
   const int hasPrefixes = pt ? 1 : 0;
