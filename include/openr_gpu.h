@@ -93,6 +93,12 @@ extern "C" {
 #define OGS_F_BEST_ROUTE_SELECTION 0x04u /* enableBestRouteSelection       */
 #define OGS_F_HOP_METRIC 0x08u         /* getSpfResult(useLinkMetric=false)*/
 #define OGS_F_WIDE_METRIC 0x10u        /* 64-bit distances (else 32-bit)   */
+/* Settle nodes in the reference's DijkstraQ order (smallest (metric, node
+ * name), LinkState.h:618-626) instead of solving the order-free fixpoint:
+ * exact for zero link metrics and for negative i32 metrics (edge metric =
+ * the sign-extended i32, u64 sums wrap, LinkState.cpp:77-78, 789). Needs
+ * OGS_F_WIDE_METRIC; one wavefront per unit, one extraction per step. */
+#define OGS_F_EXACT_ORDER 0x20u
 
 /* CSR of T topologies. */
 typedef struct ogs_graph {

@@ -165,6 +165,33 @@ inline void applyOverloads(Lsdb& db, int adjPermille, int nodePermille,
   }
 }
 
+// Metric variants for any generator (the exact-order domain, spf_exact.hip):
+// per mille of the LINKS get metric 0 in both directions, or a negative
+// metric -U[1, 100] in the direction from the smaller node name (the link's
+// max metric, a u64 of the sign-extended i32, is then huge and sums wrap,
+// LinkState.cpp:77-78, LinkState.h:171-174). Decided per unordered node pair
+// from a hash, so both adjacencies of a link agree.
+inline void applySpecialMetrics(Lsdb& db, int zeroPermille, int negPermille,
+                                uint64_t seed) {
+  if (!zeroPermille && !negPermille) return;
+  for (auto& d : db.adjDbs) {
+    for (auto& a : d.adjs) {
+      const std::string& x = d.thisNodeName;
+      const std::string& y = a.otherNodeName;
+      const std::string key = x < y ? x + "|" + y + "|" + a.ifName + "|" + a.otherIfName
+                                    : y + "|" + x + "|" + a.otherIfName + "|" + a.ifName;
+      uint64_t h = seed;
+      for (unsigned char c : key) h = (h ^ c) * 1099511628211ull;
+      const uint64_t r = splitmix64(h);
+      if (int(r % 1000) < zeroPermille) {
+        a.metric = 0;
+      } else if (int((r >> 20) % 1000) < negPermille && x < y) {
+        a.metric = -1 - int32_t((r >> 40) % 100);
+      }
+    }
+  }
+}
+
 // Prefix-table variants for any generator (parity cases for the RouteDb
 // paths beyond one plain advertisement per prefix): per mille of the
 // generated prefixes become IPv4 (v4 gate, SpfSolver.cpp:169-176), anycast

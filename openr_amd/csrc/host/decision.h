@@ -795,7 +795,7 @@ class RouteDbBatch {
   std::string area_;
   PrefixHostTable table_;
   HostBatch hb_;
-  bool wide_{false};
+  bool wide_{false}, exact_{false};
   std::vector<std::string> sources_;
   std::map<std::string, size_t> index_;
   std::vector<std::pair<size_t, size_t>> units_;  // source -> (group, unit)

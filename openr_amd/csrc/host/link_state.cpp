@@ -462,16 +462,14 @@ const LinkState::SpfResult& LinkState::getSpfResult(const std::string& node,
     res.emplace(node, NodeSpfResult(0));  // unknown source settles only itself
     return spfMemo_.emplace(key, std::move(res)).first->second;
   }
-  if (useLinkMetric && (f.hasZeroMetric || f.hasWideMetric)) {
-    throw std::domain_error(
-        "getSpfResult: zero or negative link metric is outside the GPU "
-        "engine's exact domain");
-  }
+  // zero / negative link metrics: the reference's extraction order replayed
+  // on the device (spf_exact.hip, OGS_F_EXACT_ORDER), 64-bit distances
+  const bool exact = useLinkMetric && (f.hasZeroMetric || f.hasWideMetric);
   const uint32_t s = idIt->second;
   const uint32_t N = uint32_t(f.names.size());
   const int degree = int(f.rowPtr[s + 1] - f.rowPtr[s]);
   const int W = std::max(1, ogs_nh_words_for_degree(degree));
-  const bool wide = needsWide(f, useLinkMetric);
+  const bool wide = exact || needsWide(f, useLinkMetric);
   const size_t db = wide ? 8 : 4;
 
   auto& sc = scratch();
@@ -498,7 +496,7 @@ const LinkState::SpfResult& LinkState::getSpfResult(const std::string& node,
   out.dist = sc.dist.get();
   out.nh = sc.nh.as<uint32_t>();
   uint32_t flags = (useLinkMetric ? 0u : OGS_F_HOP_METRIC) |
-      (wide ? OGS_F_WIDE_METRIC : 0u);
+      (wide ? OGS_F_WIDE_METRIC : 0u) | (exact ? OGS_F_EXACT_ORDER : 0u);
   ogsCheck(ogs_spf_routes(&g, nullptr, sc.unit.as<ogs_unit>(), 1, flags, W,
                           &out, nullptr),
            "ogs_spf_routes");

@@ -38,11 +38,9 @@ RouteDbBatch::RouteDbBatch(const SpfSolver& solver, const AreaLinkStates& als,
   area_ = als.begin()->first;
   ls_ = &als.begin()->second;
   const FlatTopology& f = ls_->flatOnDevice();
-  if (f.hasZeroMetric || f.hasWideMetric) {
-    throw std::domain_error(
-        "RouteDbBatch: zero or negative link metric is outside the GPU engine's exact domain");
-  }
-  wide_ = wideDistancesNeeded(f);
+  // zero / negative metrics: the reference's extraction order (spf_exact.hip)
+  exact_ = f.hasZeroMetric || f.hasWideMetric;
+  wide_ = exact_ || wideDistancesNeeded(f);
   table_.build(ps);
   hb_.append(f, ps, area_);
   // group sources by next-hop bitset width so each launch writes masks of
@@ -127,7 +125,7 @@ void RouteDbBatch::launch(void* stream) {
   const uint32_t flags = (solver_.enableV4_ ? OGS_F_ENABLE_V4 : 0u) |
       (solver_.v4OverV6Nexthop_ ? OGS_F_V4_OVER_V6 : 0u) |
       (solver_.enableBestRouteSelection_ ? OGS_F_BEST_ROUTE_SELECTION : 0u) |
-      (wide_ ? OGS_F_WIDE_METRIC : 0u);
+      (wide_ ? OGS_F_WIDE_METRIC : 0u) | (exact_ ? OGS_F_EXACT_ORDER : 0u);
   for (Group& G : groups_) {
     ogs_spf_out out{G.dist.get(), G.nh.as<uint32_t>(), G.meta.as<uint32_t>(),
                     G.metric.get(), G.mask.as<uint32_t>(), G.sel.as<uint32_t>()};

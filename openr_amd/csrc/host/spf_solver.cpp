@@ -489,11 +489,9 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(
   std::string area;
   const LinkState& ls = singleArea(als, area);
   const FlatTopology& f = ls.flatOnDevice();
-  if (f.hasZeroMetric || f.hasWideMetric) {
-    throw std::domain_error(
-        "buildRouteDb: zero or negative link metric is outside the GPU "
-        "engine's exact domain");
-  }
+  // zero / negative link metrics: the reference's extraction order replayed
+  // on the device (spf_exact.hip), 64-bit distances
+  const bool exact = f.hasZeroMetric || f.hasWideMetric;
   Impl& I = *impl_;
 
   // ---- prefix table (cached on PrefixState / topology version) ------------
@@ -521,7 +519,7 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(
   const uint32_t P = uint32_t(I.table.prefixes.size());
   const int degree = int(f.rowPtr[s + 1] - f.rowPtr[s]);
   const int W = std::max(1, ogs_nh_words_for_degree(degree));
-  const bool wide = wideDistancesNeeded(f);
+  const bool wide = exact || wideDistancesNeeded(f);
   const size_t db = wide ? 8 : 4;
   const ogs_unit u{0, s};
   I.unit.upload(&u, 1);
@@ -567,7 +565,7 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(
   const uint32_t flags = (enableV4_ ? OGS_F_ENABLE_V4 : 0u) |
       (v4OverV6Nexthop_ ? OGS_F_V4_OVER_V6 : 0u) |
       (enableBestRouteSelection_ ? OGS_F_BEST_ROUTE_SELECTION : 0u) |
-      (wide ? OGS_F_WIDE_METRIC : 0u);
+      (wide ? OGS_F_WIDE_METRIC : 0u) | (exact ? OGS_F_EXACT_ORDER : 0u);
   ogsCheck(ogs_spf_routes(&g, P ? &pt : nullptr, I.unit.as<ogs_unit>(), 1,
                           flags, W, &out, nullptr),
            "ogs_spf_routes");
@@ -575,7 +573,6 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(
   const RibPolicy* policy = (ribPolicy_ && ribPolicy_->isActive()) ? ribPolicy_ : nullptr;
   std::vector<uint8_t> applied, counter;
   if (policy && P) {
-    if (wide) throw std::domain_error("RibPolicy on the GPU path needs 32-bit distances");
     runPolicyOnDevice(*policy, I.table, pt, {{&f, s}}, me, W, I.meta.as<uint32_t>(),
                       I.mask.as<uint32_t>(), I.policy, nullptr);
     downloadPolicy(I.policy, P, applied, counter);

@@ -249,13 +249,18 @@ int ogs_spf_routes(const ogs_graph* graph, const ogs_prefix_table* prefixes,
   if (ogs_nh_words_for_degree(nh_words * 32) != nh_words) {
     return fail(OGS_E_UNSUPPORTED, "nh_words must be 1, 2, 4, 8 or 16");
   }
+  if ((flags & OGS_F_EXACT_ORDER) && !(flags & OGS_F_WIDE_METRIC)) {
+    return fail(OGS_E_INVALID, "OGS_F_EXACT_ORDER needs OGS_F_WIDE_METRIC");
+  }
+  if ((flags & OGS_F_EXACT_ORDER) && graph->max_degree > OGS_MAX_DEGREE) {
+    return fail(OGS_E_UNSUPPORTED, "OGS_F_EXACT_ORDER: degree > OGS_MAX_DEGREE");
+  }
   int unsupported = 0;
   hipError_t e = ogs::launch_spf_routes(
       *graph, prefixes, units, n_units, flags, nh_words, *out,
       static_cast<hipStream_t>(stream), &unsupported);
   if (unsupported) {
-    return fail(OGS_E_UNSUPPORTED,
-                "topology too large for the LDS-resident SPF path");
+    return fail(OGS_E_UNSUPPORTED, "no SPF path for these shapes");
   }
   return e == hipSuccess ? OGS_OK : hipFail(e, "spf_route launch");
 }

@@ -16,15 +16,15 @@
 // round reads what the atomics left in L2. Every round costs one barrier
 // and touches only the rows of the nodes changed in the previous round.
 //
-// Routes: route_global_kernel, one thread per (unit, prefix): route_one
-// (route_core.h) against the unit's state in HBM (no per-node LDS staging),
-// coalesced record stores. u32 or u64 distances (OGS_F_WIDE_METRIC).
+// Routes: route_global.h, one thread per (unit, prefix) against the unit's
+// state in HBM. u32 or u64 distances (OGS_F_WIDE_METRIC).
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
 
 #include "openr_gpu.h"
 #include "route_core.h"
+#include "route_global.h"
 #include "spf_core.h"
 
 namespace ogs {
@@ -167,54 +167,6 @@ __global__ __launch_bounds__(kGBlock) void spf_global_kernel(
   }
 }
 
-// Unit state in HBM as the route kernel reads it.
-template <typename D, int W>
-struct GlobalView {
-  const D* d;
-  const uint32_t* n;
-  size_t Sn;
-  __device__ __forceinline__ D dist(uint32_t v) const { return d[v]; }
-  __device__ __forceinline__ uint32_t nh(uint32_t v, int w) const {
-    return n[size_t(w) * Sn + v];
-  }
-};
-
-// One thread per (unit, prefix): route_one against the unit's HBM state
-// (grid x = unit, y = prefix block of 256).
-template <typename D, int W>
-__global__ __launch_bounds__(kBlock) void route_global_kernel(
-    ogs_graph g, ogs_prefix_table pt, const ogs_unit* __restrict__ units,
-    uint32_t flags, const D* __restrict__ sDist, const uint32_t* __restrict__ sNh,
-    ogs_spf_out out) {
-  const uint32_t u = blockIdx.x;
-  const uint32_t p = blockIdx.y * kBlock + threadIdx.x;
-  const ogs_unit unit = units[u];
-  const uint32_t Sp = uint32_t(pt.max_prefixes);
-  const uint32_t p0 = pt.pfx_base[unit.topo];
-  const uint32_t P = pt.pfx_base[unit.topo + 1] - p0;
-  if (p >= Sp) return;
-  const size_t Sn = size_t(g.max_nodes);
-  const size_t rec = size_t(u) * Sp + p;
-  uint32_t meta = 0, selBits = 0, mask[W];
-  D metric = DistInf<D>::value;
-#pragma unroll
-  for (int w = 0; w < W; ++w) mask[w] = 0u;
-  if (p < P) {
-    const RouteCfg cfg{(flags & OGS_F_ENABLE_V4) != 0, (flags & OGS_F_V4_OVER_V6) != 0,
-                       (flags & OGS_F_BEST_ROUTE_SELECTION) != 0};
-    const GlobalView<D, W> sv{sDist + u * Sn, sNh + size_t(u) * W * Sn, Sn};
-    route_one<D, W>(pt, p0 + p, unit.src, g.node_flags + g.node_base[unit.topo], sv, cfg,
-                    meta, metric, mask, selBits);
-  }
-  if (out.meta) out.meta[rec] = meta;
-  if (out.metric) static_cast<D*>(out.metric)[rec] = metric;
-  if (out.sel) out.sel[rec] = selBits;
-  if (out.mask) {
-#pragma unroll
-    for (int w = 0; w < W; ++w) out.mask[(size_t(u) * W + w) * Sp + p] = mask[w];
-  }
-}
-
 hipError_t workspace(size_t bytes, hipStream_t stream, void** out);
 
 // "spf_global" option: 0 (default) the global path only where the LDS paths
@@ -255,10 +207,7 @@ hipError_t launch_global_w(const ogs_graph& g, const ogs_prefix_table* pt,
                      units, flags, dist, nh, scratch);
   e = hipGetLastError();
   if (e != hipSuccess || !pt || pt->max_prefixes == 0) return e;
-  const unsigned bx = unsigned((pt->max_prefixes + kBlock - 1) / kBlock);
-  hipLaunchKernelGGL((route_global_kernel<D, W>), dim3(unsigned(nUnits), bx), dim3(kBlock), 0,
-                     stream, g, *pt, units, flags, dist, nh, out);
-  return hipGetLastError();
+  return launch_route_global<D, W>(g, *pt, units, nUnits, flags, dist, nh, out, stream);
 }
 
 template <typename D>

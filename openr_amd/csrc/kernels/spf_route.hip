@@ -224,6 +224,9 @@ int g_unitWidth = [] {
 int small_unit_width() { return g_unitWidth; }
 
 bool use_global(const ogs_graph& g, int W, uint32_t flags);
+hipError_t launch_spf_routes_exact(const ogs_graph& g, const ogs_prefix_table* pt,
+                                   const ogs_unit* units, int nUnits, uint32_t flags,
+                                   int W, const ogs_spf_out& out, hipStream_t stream);
 hipError_t launch_spf_routes_global(const ogs_graph& g, const ogs_prefix_table* pt,
                                     const ogs_unit* units, int nUnits, uint32_t flags,
                                     int W, const ogs_spf_out& out, hipStream_t stream);
@@ -232,6 +235,10 @@ hipError_t launch_spf_routes(const ogs_graph& g, const ogs_prefix_table* pt,
                              const ogs_unit* units, int nUnits,
                              uint32_t flags, int W, const ogs_spf_out& out,
                              hipStream_t stream, int* unsupported) {
+  // zero / negative metrics: the reference's extraction order, replayed
+  if (flags & OGS_F_EXACT_ORDER) {
+    return launch_spf_routes_exact(g, pt, units, nUnits, flags, W, out, stream);
+  }
   // units too large for LDS (or the "spf_global" option): state in HBM
   if (use_global(g, W, flags)) {
     return launch_spf_routes_global(g, pt, units, nUnits, flags, W, out, stream);

@@ -444,6 +444,9 @@ topogen::Lsdb genLsdbRaw(const std::string& kind, const py::dict& d);
 
 topogen::Lsdb genLsdb(const std::string& kind, const py::dict& d) {
   auto db = genLsdbRaw(kind, d);
+  topogen::applySpecialMetrics(db, get<int>(d, "zeroMetricPermille", 0),
+                               get<int>(d, "negMetricPermille", 0),
+                               get<uint64_t>(d, "specialSeed", 0x5E));
   topogen::PrefixMix m;
   m.v4Permille = get<int>(d, "v4Permille", 0);
   m.anycastPermille = get<int>(d, "anycastPermille", 0);
@@ -512,11 +515,12 @@ class BatchRunner {
       W_ = std::max(W_, std::max(1, ogs_nh_words_for_degree(deg)));
     }
     wide_ |= wideDistancesNeeded(f);
+    exact_ |= f.hasZeroMetric || f.hasWideMetric;
     topos_.push_back(std::move(w));
   }
 
   void upload() {
-    if (hb_.hasZeroMetric) throw std::domain_error("zero metric in batch");
+    wide_ |= exact_;  // spf_exact.hip writes 64-bit distances
     dNodeBase_.upload(hb_.nodeBase.data(), hb_.nodeBase.size());
     dDesc_.upload(hb_.topoDesc.data(), hb_.topoDesc.size());
     dRow_.upload(hb_.rowPtr.data(), hb_.rowPtr.size());
@@ -608,7 +612,7 @@ class BatchRunner {
   uint32_t flags() const {
     return (enableV4_ ? OGS_F_ENABLE_V4 : 0u) |
         (brs_ ? OGS_F_BEST_ROUTE_SELECTION : 0u) |
-        (wide_ ? OGS_F_WIDE_METRIC : 0u);
+        (wide_ ? OGS_F_WIDE_METRIC : 0u) | (exact_ ? OGS_F_EXACT_ORDER : 0u);
   }
   // route_digest.h unit(K, db) of every unit, straight from record arrays
   // laid out like this runner's outputs (meta / metric [U*Sp], mask
@@ -709,7 +713,7 @@ class BatchRunner {
   std::vector<ogs_unit> units_;
   std::vector<std::string> unitSrc_;
   int W_{1};
-  bool wide_{false};
+  bool wide_{false}, exact_{false};
   DeviceBuffer dDesc_, dNodeBase_, dRow_, dEdges_, dFlags_, dPfxBase_, dAdvOff_,
       dAdvNode_, dAdvMetrics_, dAdvMinNh_, dPfxFlags_, dUnits_, dDist_, dNh_,
       dMeta_, dMetric_, dMask_, dSel_;

@@ -329,6 +329,9 @@ topogen::Lsdb genLsdbRaw(const std::string& kind, const py::dict& d);
 
 topogen::Lsdb genLsdb(const std::string& kind, const py::dict& d) {
   auto db = genLsdbRaw(kind, d);
+  topogen::applySpecialMetrics(db, get<int>(d, "zeroMetricPermille", 0),
+                               get<int>(d, "negMetricPermille", 0),
+                               get<uint64_t>(d, "specialSeed", 0x5E));
   topogen::PrefixMix m;
   m.v4Permille = get<int>(d, "v4Permille", 0);
   m.anycastPermille = get<int>(d, "anycastPermille", 0);
