@@ -216,7 +216,7 @@ typedef struct ogs_path_out {
  * of selected advertisers in every area (SpfSolver.cpp:664-665) are one
  * table read. */
 typedef struct ogs_area_table {
-  int32_t num_areas;          /* A <= 32                                  */
+  int32_t num_areas;          /* A >= 1 (any number of areas)             */
   int32_t num_names;          /* G distinct node names of the domain      */
   const uint32_t* name_local; /* [G*A] id of name g in area a, or
                                  OGS_NODE_NONE if a has no such node     */
@@ -392,9 +392,14 @@ int ogs_csr_patch(uint64_t* edges, const uint32_t* idx, const uint64_t* val,
                   int32_t n, void* stream);
 
 /* RibPolicy compiled against one prefix table (SURVEY.md §8(a) a16;
- * RibPolicy.cpp:74-249): statements 0..K-1 in policy order. */
+ * RibPolicy.cpp:74-249): statements 0..K-1 in policy order. A policy of
+ * more than 32 statements is applied as consecutive calls over chunks of
+ * <= 32 (statement_base = 0, 32, 64, ...): a call with statement_base > 0
+ * leaves the routes an earlier chunk transformed (applied != 0xFF) as they
+ * are and continues the others' counter. Statement indexes are u8 (0xFF =
+ * none): statement_base + K <= 255. */
 typedef struct ogs_rib_policy {
-  int32_t num_statements;        /* K <= 32                                  */
+  int32_t num_statements;        /* K <= 32 (this chunk)                     */
   uint32_t active;               /* bit k: statement k has a prefix or tag
                                     matcher (no matcher never matches,
                                     RibPolicy.cpp:76-78)                    */
@@ -406,6 +411,7 @@ typedef struct ogs_rib_policy {
                                     of the unit's source whose weight under
                                     statement k (neighbor > area > default,
                                     RibPolicy.cpp:122-137) is > 0           */
+  int32_t statement_base;        /* policy index of this chunk's statement 0 */
 } ogs_rib_policy;
 
 /* Applies the policy to n_units RouteDbs in place (meta[U*S_p + p] read,
@@ -430,7 +436,8 @@ int ogs_rib_policy_apply(const ogs_prefix_table* prefixes,
  * alone, LinkState.cpp:730-734). Outputs per unit as ogs_spf_out (meta,
  * metric, sel over S_p = prefixes->max_prefixes) with one next-hop mask per
  * area: mask[((U*A + a)*W + w)*S_p + p] over the source's links in area a.
- * 32-bit distances only. Replaces createRouteForPrefix across areas
+ * spf_dist / out->metric are uint32, or uint64 with OGS_F_WIDE_METRIC (the
+ * SPF launch's width, e.g. after OGS_F_EXACT_ORDER). Replaces createRouteForPrefix across areas
  * (SpfSolver.cpp:160-311: per-area reachability, selectBestRoutes 455-486,
  * areas with best routes, getNextHopsWithMetric per area 648-688, minimum
  * metric union over areas, addBestPaths 595-639). */
@@ -439,7 +446,7 @@ int ogs_routes_multiarea(const ogs_graph* graph,
                          const ogs_area_table* areas,
                          const uint32_t* units /* device, [n_units] */,
                          int32_t n_units, const uint32_t* spf_row /* device */,
-                         const uint32_t* spf_dist, const uint32_t* spf_nh,
+                         const void* spf_dist, const uint32_t* spf_nh,
                          uint32_t flags, int32_t nh_words, ogs_spf_out* out,
                          void* stream);
 

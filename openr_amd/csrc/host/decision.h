@@ -524,7 +524,9 @@ class SpfSolver {
                         const PrefixState& prefixState);
   struct MultiAreaResult {  // host copies of one source's GPU results
     std::vector<uint32_t> row;  // [A] SPF row of each area or OGS_NODE_NONE
-    std::vector<uint32_t> dist32, nh, meta, metric, mask, sel;
+    std::vector<uint64_t> dist, metric;  // widened, all-ones = unreachable
+    std::vector<uint32_t> nh, meta, mask, sel;
+    bool wide{false};  // device buffers hold 64-bit distances
     std::vector<uint8_t> applied, counter;  // RibPolicy (empty: none)
     int W{1};
     size_t Sn{0}, P{0};

@@ -155,9 +155,15 @@ int HostBatch::slotOrder(std::vector<uint16_t>& out,
 }
 
 // ------------------------------------------------------------- SpfSolver --
-// device tables of a RibPolicy compiled for one source (runPolicyOnDevice)
+// device tables of a RibPolicy compiled for one source (runPolicyOnDevice):
+// one ogs_rib_policy per chunk of <= 32 statements (statement_base = 32c)
 struct PolicyDevice {
-  DeviceBuffer pfxMatch, tagMatch, nonzero, applied, counter;
+  struct Chunk {
+    DeviceBuffer pfxMatch, tagMatch, nonzero;
+    ogs_rib_policy rp{};
+  };
+  std::vector<Chunk> chunks;
+  DeviceBuffer applied, counter;
   // what the matcher tables were compiled for (recompiled on change)
   struct Key {
     uint64_t policy{0}, tableGen{0};
@@ -170,7 +176,6 @@ struct PolicyDevice {
           src == o.src && W == o.W && me == o.me;
     }
   } key;
-  ogs_rib_policy rp{};
 };
 
 struct SpfSolver::Impl {
@@ -198,6 +203,7 @@ struct SpfSolver::Impl {
     DeviceBuffer pfxBase, advOff, advNode, advMetrics, advMinNh, pfxFlags,
         advArea, advName, nameLocal;
     DeviceBuffer units, srcName, spfRow, dist, nh, meta, metric, mask, sel;
+    bool exact{false}, wide{false};  // domain needs OGS_F_EXACT_ORDER / u64
   } ma;
   // shape of the last enqueueRouteDb (collectRouteDb downloads its results)
   std::optional<MultiAreaResult> enqueued;
@@ -256,52 +262,74 @@ void runPolicyOnDevice(const RibPolicy& pol, const PrefixHostTable& table,
                        const std::string& me, int W, uint32_t* dMeta, uint32_t* dMask,
                        PolicyDevice& D, void* stream) {
   const size_t K = pol.numStatements();
-  if (K > 32) throw std::domain_error("RibPolicy: more than 32 statements on the GPU path");
+  // applied / counter are u8 statement indexes with 0xFF = none
+  if (K > 254) throw std::domain_error("RibPolicy: more than 254 statements");
   const size_t P = table.prefixes.size(), A = src.size();
   PolicyDevice::Key key{pol.uid(), table.generation, &table, {}, W, me};
   for (const auto& [f, s] : src) key.src.emplace_back(f, f->version, s);
   if (!(key == D.key)) {
-    std::vector<uint32_t> pm(std::max<size_t>(P, 1), 0),
-        tm(std::max<size_t>(table.advEntry.size(), 1), 0);
-    std::vector<uint32_t> nz(std::max<size_t>(K * A * W, 1), 0);
-    uint32_t active = 0;
-    for (size_t k = 0; k < K; ++k) {
-      if (pol.hasMatcher(k)) active |= 1u << k;
-    }
-    for (size_t p = 0; p < P; ++p) {
-      for (size_t k = 0; k < K; ++k) {
-        if (pol.matchesPrefix(k, table.prefixes[p])) pm[p] |= 1u << k;
-      }
-    }
-    for (size_t a = 0; a < table.advEntry.size(); ++a) {
-      for (size_t k = 0; k < K; ++k) {
-        if (pol.matchesTags(k, table.advEntry[a]->tags)) tm[a] |= 1u << k;
-      }
-    }
+    D.chunks.clear();
+    D.chunks.resize((K + 31) / 32);
+    // source link slots' next hops (weight 0, v6 form: the weight rules
+    // read only the area and the neighbour name, RibPolicy.cpp:122-137)
+    std::vector<std::vector<NextHopThrift>> slots(A);
     for (size_t a = 0; a < A; ++a) {
       const FlatTopology* f = src[a].first;
       const uint32_t s = src[a].second;
       if (s == OGS_NODE_NONE) continue;
       const uint32_t rb = f->rowPtr[s], deg = f->rowPtr[s + 1] - rb;
       for (uint32_t j = 0; j < deg && j < 32u * uint32_t(W); ++j) {
-        const NextHopThrift nh = makeNh(*f->edgeLink[rb + j], me, false, 0, std::nullopt);
-        for (size_t k = 0; k < K; ++k) {
-          if (pol.weightOf(k, nh) > 0) nz[(k * A + a) * W + j / 32] |= 1u << (j % 32);
-        }
+        slots[a].push_back(makeNh(*f->edgeLink[rb + j], me, false, 0, std::nullopt));
       }
     }
-    D.pfxMatch.upload(pm.data(), pm.size(), stream);
-    D.tagMatch.upload(tm.data(), tm.size(), stream);
-    D.nonzero.upload(nz.data(), nz.size(), stream);
+    for (size_t c = 0; c < D.chunks.size(); ++c) {
+      const size_t k0 = 32 * c, kn = std::min<size_t>(32, K - k0);
+      std::vector<uint32_t> pm(std::max<size_t>(P, 1), 0),
+          tm(std::max<size_t>(table.advEntry.size(), 1), 0);
+      std::vector<uint32_t> nz(std::max<size_t>(kn * A * W, 1), 0);
+      uint32_t active = 0;
+      for (size_t k = 0; k < kn; ++k) {
+        if (pol.hasMatcher(k0 + k)) active |= 1u << k;
+      }
+      for (size_t p = 0; p < P; ++p) {
+        for (size_t k = 0; k < kn; ++k) {
+          if (pol.matchesPrefix(k0 + k, table.prefixes[p])) pm[p] |= 1u << k;
+        }
+      }
+      for (size_t a = 0; a < table.advEntry.size(); ++a) {
+        for (size_t k = 0; k < kn; ++k) {
+          if (pol.matchesTags(k0 + k, table.advEntry[a]->tags)) tm[a] |= 1u << k;
+        }
+      }
+      for (size_t a = 0; a < A; ++a) {
+        for (size_t j = 0; j < slots[a].size(); ++j) {
+          for (size_t k = 0; k < kn; ++k) {
+            if (pol.weightOf(k0 + k, slots[a][j]) > 0) {
+              nz[(k * A + a) * W + j / 32] |= 1u << (j % 32);
+            }
+          }
+        }
+      }
+      PolicyDevice::Chunk& C = D.chunks[c];
+      C.pfxMatch.upload(pm.data(), pm.size(), stream);
+      C.tagMatch.upload(tm.data(), tm.size(), stream);
+      C.nonzero.upload(nz.data(), nz.size(), stream);
+      C.rp = ogs_rib_policy{int32_t(kn), active, C.pfxMatch.as<uint32_t>(),
+                            C.tagMatch.as<uint32_t>(), C.nonzero.as<uint32_t>(),
+                            int32_t(k0)};
+    }
     D.applied.resize(std::max<size_t>(P, 1));
     D.counter.resize(std::max<size_t>(P, 1));
-    D.rp = ogs_rib_policy{int32_t(K), active, D.pfxMatch.as<uint32_t>(),
-                          D.tagMatch.as<uint32_t>(), D.nonzero.as<uint32_t>()};
     D.key = std::move(key);
   }
-  ogsCheck(ogs_rib_policy_apply(&pt, &D.rp, int32_t(A), 1, W, dMeta, dMask,
-                                D.applied.as<uint8_t>(), D.counter.as<uint8_t>(), stream),
-           "ogs_rib_policy_apply");
+  // chunks in statement order; a later chunk continues the routes no
+  // earlier statement transformed (first transforming statement wins,
+  // RibPolicy.cpp:222-229)
+  for (const auto& C : D.chunks) {
+    ogsCheck(ogs_rib_policy_apply(&pt, &C.rp, int32_t(A), 1, W, dMeta, dMask,
+                                  D.applied.as<uint8_t>(), D.counter.as<uint8_t>(), stream),
+             "ogs_rib_policy_apply");
+  }
 }
 
 void downloadPolicy(const PolicyDevice& D, size_t P, std::vector<uint8_t>& applied,
@@ -631,13 +659,19 @@ void SpfSolver::prepareMultiArea(const AreaLinkStates& als, const PrefixState& p
   std::vector<std::pair<const FlatTopology*, uint64_t>> key;
   for (const auto& [area, ls] : als) {
     const FlatTopology& f = ls.flat();
-    if (f.hasZeroMetric || f.hasWideMetric || wideDistancesNeeded(f)) {
-      throw std::domain_error(
-          "buildRouteDb: zero, negative or > 2^31 path metric is outside the "
-          "multi-area GPU path's exact domain");
-    }
     key.emplace_back(&f, f.version);
   }
+  // zero / negative metrics anywhere: the whole domain's SPF launch replays
+  // the reference's extraction order (spf_exact.hip); 64-bit distances then
+  // or when a 32-bit path sum could overflow
+  M.exact = false;
+  M.wide = false;
+  for (const auto& [area, ls] : als) {
+    const FlatTopology& f = ls.flat();
+    M.exact |= f.hasZeroMetric || f.hasWideMetric;
+    M.wide |= wideDistancesNeeded(f);
+  }
+  M.wide |= M.exact;
   const bool topoChanged = key != M.topoKey;
   if (topoChanged) {
     static const PrefixState kNoPrefixes;
@@ -784,10 +818,7 @@ DecisionRouteDb SpfSolver::materializeMultiArea(const std::string& me,
       const uint64_t* dist = nullptr;
       const uint32_t* nhw = nullptr;
       if (R.row[a] != OGS_NODE_NONE) {
-        for (size_t v = 0; v < Sn; ++v) {
-          const uint32_t d = R.dist32[R.row[a] * Sn + v];
-          d64[v] = d == 0xFFFFFFFFu ? ~0ull : d;
-        }
+        for (size_t v = 0; v < Sn; ++v) d64[v] = R.dist[R.row[a] * Sn + v];
         dist = d64.data();
         nhw = &R.nh[size_t(R.row[a]) * W * Sn];
       }
@@ -807,7 +838,6 @@ DecisionRouteDb SpfSolver::materializeMultiArea(const std::string& me,
 void SpfSolver::enqueueMultiArea(const std::string& me, const AreaLinkStates& als,
                                  const PrefixState& ps, void* stream,
                                  MultiAreaResult& R) {
-  if (als.size() > 32) throw std::domain_error("buildRouteDb: more than 32 areas");
   prepareMultiArea(als, ps);
   Impl::MultiArea& M = impl_->ma;
   const uint32_t A = uint32_t(als.size());
@@ -832,10 +862,12 @@ void SpfSolver::enqueueMultiArea(const std::string& me, const AreaLinkStates& al
   M.units.upload(su.data(), su.size(), stream);
   M.spfRow.upload(R.row.data(), R.row.size(), stream);
   M.srcName.upload(&S, 1, stream);
-  M.dist.resize(su.size() * Sn * 4);
+  R.wide = M.wide;
+  const size_t db = M.wide ? 8 : 4;
+  M.dist.resize(su.size() * Sn * db);
   M.nh.resize(su.size() * W * Sn * 4);
   M.meta.resize(P1 * 4);
-  M.metric.resize(P1 * 4);
+  M.metric.resize(P1 * db);
   M.mask.resize(P1 * A * W * 4);
   M.sel.resize(P1 * 4);
   ogs_graph g{};
@@ -851,7 +883,8 @@ void SpfSolver::enqueueMultiArea(const std::string& me, const AreaLinkStates& al
   g.edge_src = M.edgeSrc.as<uint32_t>();
   const uint32_t flags = (enableV4_ ? OGS_F_ENABLE_V4 : 0u) |
       (v4OverV6Nexthop_ ? OGS_F_V4_OVER_V6 : 0u) |
-      (enableBestRouteSelection_ ? OGS_F_BEST_ROUTE_SELECTION : 0u);
+      (enableBestRouteSelection_ ? OGS_F_BEST_ROUTE_SELECTION : 0u) |
+      (M.wide ? OGS_F_WIDE_METRIC : 0u) | (M.exact ? OGS_F_EXACT_ORDER : 0u);
   ogs_spf_out spf{};
   spf.dist = M.dist.get();
   spf.nh = M.nh.as<uint32_t>();
@@ -881,7 +914,7 @@ void SpfSolver::enqueueMultiArea(const std::string& me, const AreaLinkStates& al
     out.mask = M.mask.as<uint32_t>();
     out.sel = M.sel.as<uint32_t>();
     ogsCheck(ogs_routes_multiarea(&g, &pt, &at, M.srcName.as<uint32_t>(), 1,
-                                  M.spfRow.as<uint32_t>(), M.dist.as<uint32_t>(),
+                                  M.spfRow.as<uint32_t>(), M.dist.get(),
                                   M.nh.as<uint32_t>(), flags, W, &out, stream),
              "ogs_routes_multiarea");
     if (ribPolicy_ && ribPolicy_->isActive()) {
@@ -939,17 +972,27 @@ DecisionRouteDb SpfSolver::downloadMultiArea(const std::string& me,
   if (P && ribPolicy_ && ribPolicy_->isActive()) {
     downloadPolicy(impl_->policy, P, R.applied, R.counter);
   }
-  R.dist32.resize(nSpf * Sn);
   R.nh.resize(nSpf * W * Sn);
   R.meta.resize(P);
-  R.metric.resize(P);
   R.mask.resize(P * A * W);
   R.sel.resize(P);
-  M.dist.download(R.dist32.data(), R.dist32.size());
+  // distances / route metrics widened to 64 bits, all-ones = unreachable
+  auto widen = [&](const DeviceBuffer& b, size_t n, std::vector<uint64_t>& v) {
+    v.resize(n);
+    if (!n) return;
+    if (R.wide) {
+      b.download(v.data(), n);
+    } else {
+      std::vector<uint32_t> t(n);
+      b.download(t.data(), n);
+      for (size_t i = 0; i < n; ++i) v[i] = t[i] == 0xFFFFFFFFu ? ~0ull : t[i];
+    }
+  };
+  widen(M.dist, nSpf * Sn, R.dist);
   M.nh.download(R.nh.data(), R.nh.size());
   if (P) {
     M.meta.download(R.meta.data(), P);
-    M.metric.download(R.metric.data(), P);
+    widen(M.metric, P, R.metric);
     M.mask.download(R.mask.data(), R.mask.size());
     M.sel.download(R.sel.data(), P);
   }

@@ -26,7 +26,7 @@ hipError_t launch_spf_routes(const ogs_graph& g, const ogs_prefix_table* pt,
 hipError_t launch_routes_multiarea(const ogs_graph& g, const ogs_prefix_table& pt,
                                    const ogs_area_table& at,
                                    const uint32_t* units, int n,
-                                   const uint32_t* spfRow, const uint32_t* dist,
+                                   const uint32_t* spfRow, const void* dist,
                                    const uint32_t* nh, uint32_t flags, int W,
                                    const ogs_spf_out& out, hipStream_t stream);
 hipError_t launch_variants(const ogs_graph& g, const ogs_prefix_table& pt,
@@ -407,14 +407,21 @@ int ogs_rib_policy_apply(const ogs_prefix_table* prefixes,
   if (!prefixes || !policy || !meta || !mask) {
     return fail(OGS_E_INVALID, "prefixes/policy/meta/mask is NULL");
   }
-  if (n_units < 0 || num_areas < 1 || num_areas > 32) {
-    return fail(OGS_E_INVALID, "n_units < 0 or num_areas outside [1, 32]");
+  if (n_units < 0 || num_areas < 1) {
+    return fail(OGS_E_INVALID, "n_units < 0 or num_areas < 1");
   }
   if (n_units == 0 || policy->num_statements == 0) return OGS_OK;
   if (policy->num_statements < 0 || policy->num_statements > 32 ||
       !policy->pfx_match || !policy->adv_tag_match || !policy->slot_nonzero ||
       !prefixes->pfx_base || !prefixes->adv_off) {
-    return fail(OGS_E_INVALID, "policy tables NULL or more than 32 statements");
+    return fail(OGS_E_INVALID, "policy tables NULL or more than 32 statements per chunk");
+  }
+  if (policy->statement_base < 0 ||
+      policy->statement_base + policy->num_statements > 255) {
+    return fail(OGS_E_INVALID, "statement_base + num_statements outside [0, 255]");
+  }
+  if (policy->statement_base > 0 && (!applied || !counter)) {
+    return fail(OGS_E_INVALID, "a continuation chunk needs applied / counter");
   }
   if (ogs_nh_words_for_degree(nh_words * 32) != nh_words) {
     return fail(OGS_E_UNSUPPORTED, "nh_words must be 1, 2, 4, 8 or 16");
@@ -429,7 +436,7 @@ int ogs_routes_multiarea(const ogs_graph* graph,
                          const ogs_prefix_table* prefixes,
                          const ogs_area_table* areas, const uint32_t* units,
                          int32_t n_units, const uint32_t* spf_row,
-                         const uint32_t* spf_dist, const uint32_t* spf_nh,
+                         const void* spf_dist, const uint32_t* spf_nh,
                          uint32_t flags, int32_t nh_words, ogs_spf_out* out,
                          void* stream) {
   if (!graph || !prefixes || !areas || !out) {
@@ -444,12 +451,8 @@ int ogs_routes_multiarea(const ogs_graph* graph,
       !prefixes->pfx_flags) {
     return fail(OGS_E_INVALID, "multi-area input arrays are NULL");
   }
-  if (areas->num_areas <= 0 || areas->num_areas > 32 ||
-      areas->num_areas > graph->num_topos) {
-    return fail(OGS_E_INVALID, "num_areas outside [1, min(32, num_topos)]");
-  }
-  if (flags & OGS_F_WIDE_METRIC) {
-    return fail(OGS_E_UNSUPPORTED, "multi-area RouteDb uses 32-bit distances");
+  if (areas->num_areas <= 0 || areas->num_areas > graph->num_topos) {
+    return fail(OGS_E_INVALID, "num_areas outside [1, num_topos]");
   }
   if (ogs_nh_words_for_degree(nh_words * 32) != nh_words) {
     return fail(OGS_E_UNSUPPORTED, "nh_words must be 1, 2, 4, 8 or 16");

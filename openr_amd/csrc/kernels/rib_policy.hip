@@ -36,7 +36,13 @@ __global__ __launch_bounds__(kBlock) void rib_policy_kernel(
   const uint32_t K = uint32_t(pol.num_statements);
   const size_t o = size_t(u) * Sp + p;
   const uint32_t m = meta[o];
+  const uint32_t base = uint32_t(pol.statement_base);
   uint32_t app = 0xFFu, cnt = 0xFFu;
+  if (base) {  // a later chunk: keep what earlier statements decided
+    app = applied[o];
+    cnt = counter[o];
+    if (app != 0xFFu) return;
+  }
   if (m & OGS_ROUTE_VALID) {
     const uint32_t gp = p0 + p;
     const uint32_t best = pt.adv_off[gp] + (m >> OGS_ROUTE_BEST_SHIFT);
@@ -44,7 +50,7 @@ __global__ __launch_bounds__(kBlock) void rib_policy_kernel(
     const uint32_t* nz = pol.slot_nonzero + size_t(u) * K * A * W;
     for (; cand; cand &= cand - 1) {
       const uint32_t k = __builtin_ctz(cand);
-      cnt = k;  // counterID set by every matching statement
+      cnt = base + k;  // counterID set by every matching statement
       bool any = false;
       for (uint32_t a = 0; a < A; ++a) {
 #pragma unroll
@@ -54,7 +60,7 @@ __global__ __launch_bounds__(kBlock) void rib_policy_kernel(
         }
       }
       if (!any) continue;  // every next hop weighted 0: route unchanged
-      app = k;
+      app = base + k;
       for (uint32_t a = 0; a < A; ++a) {
 #pragma unroll
         for (int w = 0; w < W; ++w) {

@@ -33,13 +33,13 @@
 
 namespace ogs {
 
-template <int W>
+template <typename D, int W>
 __global__ __launch_bounds__(kBlock) void route_multiarea_kernel(
     ogs_graph g, ogs_prefix_table pt, ogs_area_table at,
     const uint32_t* __restrict__ units, const uint32_t* __restrict__ spfRow,
-    const uint32_t* __restrict__ sDist, const uint32_t* __restrict__ sNh,
+    const D* __restrict__ sDist, const uint32_t* __restrict__ sNh,
     uint32_t flags, ogs_spf_out out) {
-  constexpr uint32_t kInf = 0xFFFFFFFFu;
+  constexpr D kInf = DistInf<D>::value;
   const uint32_t u = blockIdx.y;
   const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
   const uint32_t p0 = pt.pfx_base[0];
@@ -55,8 +55,8 @@ __global__ __launch_bounds__(kBlock) void route_multiarea_kernel(
   const bool brs = flags & OGS_F_BEST_ROUTE_SELECTION;
 
   // SPF of (source, area b) looked up by node NAME
-  auto distOf = [&](uint32_t b, uint32_t name) -> uint32_t {
-    if (name == S) return 0u;
+  auto distOf = [&](uint32_t b, uint32_t name) -> D {
+    if (name == S) return D(0);
     const uint32_t r = row[b];
     const uint32_t v = at.name_local[size_t(name) * A + b];
     if (r == OGS_NODE_NONE || v == OGS_NODE_NONE) return kInf;
@@ -78,9 +78,9 @@ __global__ __launch_bounds__(kBlock) void route_multiarea_kernel(
   const uint32_t gp = p0 + p;
   uint32_t meta = 0, selBits = 0;
   const size_t o = size_t(u) * Sp + p;
-  auto finish = [&](uint32_t m, uint32_t d) {
+  auto finish = [&](uint32_t m, D d) {
     if (out.meta) out.meta[o] = m;
-    if (out.metric) static_cast<uint32_t*>(out.metric)[o] = d;
+    if (out.metric) static_cast<D*>(out.metric)[o] = d;
     if (out.sel) out.sel[o] = selBits;
   };
   auto clearMasks = [&]() {
@@ -151,7 +151,7 @@ __global__ __launch_bounds__(kBlock) void route_multiarea_kernel(
 
   // selected set: best entry, self, areas holding selected entries
   bool self = false;
-  uint32_t bestIdx = 0xFFFFFFFFu, selfIdx = 0xFFFFFFFFu, areaBits = 0;
+  uint32_t bestIdx = 0xFFFFFFFFu, selfIdx = 0xFFFFFFFFu;
   for (uint32_t a = a0; a < a1; ++a) {
     if (!selected(a)) continue;
     if (a - a0 < 32) selBits |= 1u << (a - a0);
@@ -160,7 +160,6 @@ __global__ __launch_bounds__(kBlock) void route_multiarea_kernel(
       self = true;
       if (selfIdx == 0xFFFFFFFFu) selfIdx = a - a0;
     }
-    areaBits |= 1u << at.adv_area[a];
   }
   if (brs && self) bestIdx = selfIdx;  // selectBestNodeArea
   meta |= OGS_ROUTE_SELECTED | (bestIdx << OGS_ROUTE_BEST_SHIFT);
@@ -175,28 +174,35 @@ __global__ __launch_bounds__(kBlock) void route_multiarea_kernel(
 
   // per area: shortest over all selected names in that area's SPF, next-hop
   // union over the closest ones; keep the areas with the smallest metric
-  uint32_t shortest = kInf, cnt = 0;
-  uint32_t keep = 0;  // areas whose masks are part of the route
-  for (uint32_t bits = areaBits; bits; bits &= bits - 1) {
-    const uint32_t b = __builtin_ctz(bits);
-    uint32_t sb = kInf;
+  // (any number of areas: an area counts iff it holds a selected entry,
+  // hasBestRoutesInArea, and is re-derived per pass instead of a bitmask)
+  auto holds = [&](uint32_t b) {
+    for (uint32_t a = a0; a < a1; ++a) {
+      if (at.adv_area[a] == b && selected(a)) return true;
+    }
+    return false;
+  };
+  auto areaShortest = [&](uint32_t b) {
+    D sb = kInf;
     for (uint32_t a = a0; a < a1; ++a) {
       if (!selected(a)) continue;
-      const uint32_t d = distOf(b, at.adv_name[a]);
+      const D d = distOf(b, at.adv_name[a]);
       if (d < sb) sb = d;
     }
-    if (shortest < sb) continue;
-    if (shortest > sb) {
-      shortest = sb;
-      keep = 0;
-    }
-    keep |= 1u << b;
+    return sb;
+  };
+  D shortest = kInf;
+  uint32_t cnt = 0;
+  for (uint32_t b = 0; b < A; ++b) {
+    if (!holds(b)) continue;
+    const D sb = areaShortest(b);
+    if (sb < shortest) shortest = sb;
   }
   for (uint32_t b = 0; b < A; ++b) {
     uint32_t m[W];
 #pragma unroll
     for (int w = 0; w < W; ++w) m[w] = 0u;
-    if ((keep >> b) & 1u) {
+    if (holds(b) && areaShortest(b) == shortest) {
       for (uint32_t a = a0; a < a1; ++a) {
         if (!selected(a)) continue;
         const uint32_t name = at.adv_name[a];
@@ -237,20 +243,26 @@ __global__ __launch_bounds__(kBlock) void route_multiarea_kernel(
 template <int W>
 hipError_t launch_ma(const ogs_graph& g, const ogs_prefix_table& pt,
                      const ogs_area_table& at, const uint32_t* units, int n,
-                     const uint32_t* spfRow, const uint32_t* dist,
+                     const uint32_t* spfRow, const void* dist,
                      const uint32_t* nh, uint32_t flags, const ogs_spf_out& out,
                      hipStream_t stream) {
   const unsigned bx = unsigned((pt.max_prefixes + kBlock - 1) / kBlock);
-  hipLaunchKernelGGL(route_multiarea_kernel<W>, dim3(bx, unsigned(n)),
-                     dim3(kBlock), 0, stream, g, pt, at, units, spfRow, dist,
-                     nh, flags, out);
+  if (flags & OGS_F_WIDE_METRIC) {
+    hipLaunchKernelGGL((route_multiarea_kernel<uint64_t, W>), dim3(bx, unsigned(n)),
+                       dim3(kBlock), 0, stream, g, pt, at, units, spfRow,
+                       static_cast<const uint64_t*>(dist), nh, flags, out);
+  } else {
+    hipLaunchKernelGGL((route_multiarea_kernel<uint32_t, W>), dim3(bx, unsigned(n)),
+                       dim3(kBlock), 0, stream, g, pt, at, units, spfRow,
+                       static_cast<const uint32_t*>(dist), nh, flags, out);
+  }
   return hipGetLastError();
 }
 
 hipError_t launch_routes_multiarea(const ogs_graph& g, const ogs_prefix_table& pt,
                                    const ogs_area_table& at,
                                    const uint32_t* units, int n,
-                                   const uint32_t* spfRow, const uint32_t* dist,
+                                   const uint32_t* spfRow, const void* dist,
                                    const uint32_t* nh, uint32_t flags, int W,
                                    const ogs_spf_out& out, hipStream_t stream) {
   if (pt.max_prefixes <= 0) return hipSuccess;

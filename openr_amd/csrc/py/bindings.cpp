@@ -398,6 +398,9 @@ void loadMultiArea(const py::dict& d, AreaLinkStates& als, PrefixState& ps) {
     topogen::applyOverloads(lsdbs[a], get<int>(d, "adjOverloadPermille", 0),
                             get<int>(d, "nodeOverloadPermille", 0),
                             get<uint64_t>(d, "overloadSeed", 0x0F) + a);
+    topogen::applySpecialMetrics(lsdbs[a], get<int>(d, "zeroMetricPermille", 0),
+                                 get<int>(d, "negMetricPermille", 0),
+                                 get<uint64_t>(d, "specialSeed", 0x5E) + a);
     topogen::PrefixMix m;
     m.v4Permille = get<int>(d, "v4Permille", 0);
     m.minNhPermille = get<int>(d, "minNhPermille", 0);
