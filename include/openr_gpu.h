@@ -235,6 +235,10 @@ int ogs_memcpy_h2d(void* dst, const void* src, size_t bytes, void* stream);
 int ogs_memcpy_d2h(void* dst, const void* src, size_t bytes, void* stream);
 int ogs_memset(void* dst, int value, size_t bytes, void* stream);
 int ogs_stream_sync(void* stream);
+/* Page-locked host memory (one DMA per transfer, no staging copy): the
+ * adapter's per-call result blocks. */
+int ogs_host_alloc(void** hptr, size_t bytes);
+int ogs_host_free(void* hptr);
 
 /* Tuning knobs (process-wide; for A/B measurement):
  *   "unit_width": small-topology kernel choice: -1 automatic (default),
@@ -288,6 +292,21 @@ int ogs_spf_routes(const ogs_graph* graph, const ogs_prefix_table* prefixes,
                    const ogs_unit* units /* device */, int32_t n_units,
                    uint32_t flags, int32_t nh_words, ogs_spf_out* out,
                    void* stream);
+
+/* RouteDb records of n_units units from SPF state a previous ogs_spf_routes
+ * launch left in device memory (spf_dist [U*S_n] uint32, or uint64 with
+ * OGS_F_WIDE_METRIC; spf_nh [(U*W + w)*S_n + v] link-slot sets; row u of the
+ * state belongs to units[u]). One thread per (unit, prefix), route_one of
+ * route_core.h. Replaces, for a prefix set whose SPF is already known, the
+ * per-prefix createRouteForPrefix (SpfSolver.cpp:160-311) that
+ * Decision::rebuildRoutes calls in its incremental branch (Decision.cpp:
+ * 929-938): the SPF memo (LinkState::getSpfResult) reused, only the
+ * changed prefixes routed. */
+int ogs_routes_from_spf(const ogs_graph* graph, const ogs_prefix_table* prefixes,
+                        const ogs_unit* units /* device */, int32_t n_units,
+                        const void* spf_dist, const uint32_t* spf_nh,
+                        uint32_t flags, int32_t nh_words, ogs_spf_out* out,
+                        void* stream);
 
 /* Batched edge-disjoint path tracing (KSP2). For each unit: SPF from src
  * over the links not set in the unit's mask (`masks` + U*mask_words, bit l =

@@ -19,7 +19,7 @@ EXPORTS = [
     "ogs_stream_sync", "ogs_nh_words_for_degree", "ogs_spf_routes",
     "ogs_ksp_paths", "ogs_ksp2_paths", "ogs_set_option", "ogs_routes_multiarea",
     "ogs_spf_routes_variants", "ogs_rib_policy_apply", "ogs_route_changes_gather",
-    "ogs_csr_patch",
+    "ogs_csr_patch", "ogs_host_alloc", "ogs_host_free", "ogs_routes_from_spf",
 ]
 
 

@@ -203,6 +203,11 @@ class Link {
 };
 using LinkPtr = std::shared_ptr<Link>;
 
+// Process-wide version stamps of FlatTopology / PrefixState contents: a
+// (pointer, stamp) cache key never matches a different object that reuses
+// the address.
+uint64_t nextVersionStamp();
+
 // ---------------------------------------------------- flattened topology --
 // Host image of one LinkState in the C-ABI's CSR encoding + the device copy.
 struct FlatTopology {
@@ -219,6 +224,8 @@ struct FlatTopology {
   uint64_t version{0};
   int slotStride{0};  // ogs_graph.slot_stride of dSlot (0: none)
   int slotDegree{0};  // ogs_graph.slot_degree of dSlotEdges (0: none)
+  // views into dBlock (one H2D per full upload); patches write in place
+  DeviceBuffer dBlock;
   DeviceBuffer dRow, dEdges, dFlags, dNodeBase, dSlot, dSlotEdges, dEdgeSrc;
   DeviceBuffer dPatchIdx, dPatchVal;  // ogs_csr_patch staging (§8(f) f3)
 };
@@ -304,6 +311,8 @@ class LinkState {
   void patchFlat(const std::string& node, const std::vector<const Link*>& touched,
                  bool nodeFlagsChanged);
   void uploadSlotImages(FlatTopology& m) const;
+  void slotImages(FlatTopology& m, std::vector<uint16_t>& slots,
+                  std::vector<uint32_t>& img) const;
 
   std::string area_, myNodeName_;
   std::map<std::string, AdjacencyDatabase> adjDbs_;
@@ -520,6 +529,13 @@ class SpfSolver {
   std::optional<DecisionRouteDb> buildRouteDbMultiArea(
       const std::string& myNodeName, const AreaLinkStates& areaLinkStates,
       const PrefixState& prefixState);
+  // single-area prefix table (packed, one H2D) cached on (ps, f) versions
+  void prepareSingleArea(const FlatTopology& f, const PrefixState& ps,
+                         const std::string& area);
+  void routesFromSpfMemo(const std::string& me, const LinkState& ls,
+                         const std::string& area, const PrefixState& ps,
+                         const PrefixState& sub,
+                         std::map<std::string, std::optional<RibUnicastEntry>>& out);
   void prepareMultiArea(const AreaLinkStates& areaLinkStates,
                         const PrefixState& prefixState);
   struct MultiAreaResult {  // host copies of one source's GPU results
@@ -629,6 +645,10 @@ struct HostBatch {
   bool hasZeroMetric{false};
   void append(const FlatTopology& t, const PrefixState& ps,
               const std::string& area);
+  // only the prefix-table half of append (no CSR, colouring or topoDesc);
+  // returns the number of prefixes appended
+  uint32_t appendPrefixes(const FlatTopology& t, const PrefixState& ps,
+                          const std::string& area);
   // ogs_graph.slot_node image ([T*stride]); returns the stride, 0 if none.
   // With `edgesOut`, also the slot_edges image and its degree (0 if the
   // batch does not qualify).

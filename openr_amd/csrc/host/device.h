@@ -32,16 +32,28 @@ class DeviceBuffer {
     swap(o);
     return *this;
   }
-  ~DeviceBuffer() { ogs_free(ptr_); }
+  ~DeviceBuffer() {
+    if (owned_) ogs_free(ptr_);
+  }
+
+  // non-owning view of `bytes` at `base` (a span of a packed block that
+  // outlives it); growing past the span re-homes it into its own allocation
+  void view(void* base, size_t bytes) {
+    if (owned_) ogs_free(ptr_);
+    ptr_ = base;
+    cap_ = size_ = bytes;
+    owned_ = false;
+  }
 
   void resize(size_t bytes) {  // grow-only, contents not preserved
     if (bytes <= cap_) {
       size_ = bytes;
       return;
     }
-    ogs_free(ptr_);
+    if (owned_) ogs_free(ptr_);
     ptr_ = nullptr;
     cap_ = size_ = 0;
+    owned_ = true;
     ogsCheck(ogs_malloc(&ptr_, bytes), "ogs_malloc");
     cap_ = size_ = bytes;
   }
@@ -72,9 +84,49 @@ class DeviceBuffer {
     std::swap(ptr_, o.ptr_);
     std::swap(size_, o.size_);
     std::swap(cap_, o.cap_);
+    std::swap(owned_, o.owned_);
   }
   void* ptr_{nullptr};
   size_t size_{0}, cap_{0};
+  bool owned_{true};
 };
+
+// Process-wide cache of page-locked blocks: page-locking is a syscall +
+// page-table update (tens of microseconds), a solver's staging blocks are
+// recycled instead. Owners synchronise their transfers before release.
+void* pinnedAcquire(size_t bytes, size_t* cap);
+void pinnedRelease(void* p, size_t cap);
+
+// Page-locked host block (grow-only, contents not preserved): the staging
+// side of one-transfer H2D / D2H round trips.
+class PinnedBuffer {
+ public:
+  PinnedBuffer() = default;
+  PinnedBuffer(const PinnedBuffer&) = delete;
+  PinnedBuffer& operator=(const PinnedBuffer&) = delete;
+  ~PinnedBuffer() { pinnedRelease(ptr_, cap_); }
+  void resize(size_t bytes) {
+    if (bytes <= cap_) return;
+    pinnedRelease(ptr_, cap_);
+    ptr_ = nullptr;
+    cap_ = 0;
+    ptr_ = pinnedAcquire(bytes, &cap_);
+  }
+  template <typename T>
+  T* at(size_t byteOffset) const {
+    return reinterpret_cast<T*>(static_cast<char*>(ptr_) + byteOffset);
+  }
+  void* get() const { return ptr_; }
+
+ private:
+  void* ptr_{nullptr};
+  size_t cap_{0};
+};
+
+// byte offset `off` into a device block
+template <typename T>
+inline T* devAt(const DeviceBuffer& b, size_t off) {
+  return reinterpret_cast<T*>(static_cast<char*>(b.get()) + off);
+}
 
 }  // namespace openr_amd

@@ -1,5 +1,6 @@
 // link_state.cpp — ingestion, change detection and CSR flattening for the
 // GPU LinkState (reference: openr/decision/LinkState.cpp:50-715).
+#include <cstring>
 #include <algorithm>
 #include <unordered_map>
 
@@ -201,7 +202,7 @@ void LinkState::patchFlat(const std::string& node, const std::vector<const Link*
                           bool nodeFlagsChanged) {
   FlatTopology& f = *flat_;
   ++mutation_;
-  f.version = mutation_;  // version-keyed caches (prefix tables, policies) rebuild
+  f.version = nextVersionStamp();  // version-keyed caches (prefix tables, policies) rebuild
   ++flatPatches_;
   const uint32_t u = f.id.at(node);
   std::vector<uint32_t> dirty;
@@ -322,7 +323,7 @@ bool LinkState::pathAInPathB(const Path& a, const Path& b) {
 const FlatTopology& LinkState::flat() const {
   if (flat_ && !flatStale_) return *flat_;
   auto f = std::make_unique<FlatTopology>();
-  f->version = mutation_;
+  f->version = nextVersionStamp();
   f->names.reserve(adjDbs_.size());
   for (const auto& [n, _] : adjDbs_) {  // byte-wise name order == id order
     f->id.emplace(n, uint32_t(f->names.size()));
@@ -389,45 +390,76 @@ const FlatTopology& LinkState::flatOnDevice() const {
   const FlatTopology& f = flat();
   if (!deviceStale_) return f;
   FlatTopology& m = *flat_;
-  const uint32_t nodeBase[2] = {0, uint32_t(m.names.size())};
-  m.dNodeBase.upload(nodeBase, 2);
-  m.dRow.upload(m.rowPtr.data(), m.rowPtr.size());
-  m.dEdges.upload(m.edges.data(), m.edges.size());
-  m.dFlags.upload(m.nodeFlags.data(), m.nodeFlags.size());
-  {
-    std::vector<uint32_t> esrc;
-    esrc.reserve(m.edges.size());
-    for (uint32_t v = 0; v + 1 < m.rowPtr.size(); ++v) {
-      esrc.insert(esrc.end(), m.rowPtr[v + 1] - m.rowPtr[v], v);
-    }
-    m.dEdgeSrc.upload(esrc.data(), esrc.size());
+  // every device image of the CSR packed into one block: one H2D
+  const uint32_t N = uint32_t(m.names.size());
+  const size_t E = m.edges.size();
+  const uint32_t nodeBase[2] = {0, N};
+  std::vector<uint32_t> esrc;
+  esrc.reserve(E);
+  for (uint32_t v = 0; v < N; ++v) esrc.insert(esrc.end(), m.rowPtr[v + 1] - m.rowPtr[v], v);
+  std::vector<uint16_t> slots;
+  std::vector<uint32_t> img;
+  slotImages(m, slots, img);
+  struct Span {
+    const void* src;
+    size_t bytes;
+    DeviceBuffer* dst;
+  };
+  const Span spans[] = {{nodeBase, sizeof nodeBase, &m.dNodeBase},
+                        {m.rowPtr.data(), m.rowPtr.size() * 4, &m.dRow},
+                        {m.edges.data(), E * 8, &m.dEdges},
+                        {m.nodeFlags.data(), m.nodeFlags.size(), &m.dFlags},
+                        {esrc.data(), esrc.size() * 4, &m.dEdgeSrc},
+                        {slots.data(), slots.size() * 2, &m.dSlot},
+                        {img.data(), img.size() * 4, &m.dSlotEdges}};
+  auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
+  size_t total = 0;
+  for (const Span& sp : spans) total += al(std::max<size_t>(sp.bytes, 16));
+  std::vector<char> host(total);
+  size_t off = 0;
+  for (const Span& sp : spans) {
+    if (sp.bytes) std::memcpy(host.data() + off, sp.src, sp.bytes);
+    off += al(std::max<size_t>(sp.bytes, 16));
   }
-  uploadSlotImages(m);
+  m.dBlock.resize(total);
+  ogsCheck(ogs_memcpy_h2d(m.dBlock.get(), host.data(), total, nullptr), "ogs_memcpy_h2d");
+  off = 0;
+  for (const Span& sp : spans) {
+    sp.dst->view(static_cast<char*>(m.dBlock.get()) + off, std::max<size_t>(sp.bytes, 16));
+    off += al(std::max<size_t>(sp.bytes, 16));
+  }
   deviceStale_ = false;
   return f;
+}
+
+// host images of the wave-kernel relaxation order and per-slot edges
+// (slot_order.h); sets m.slotStride / m.slotDegree (0: none)
+void LinkState::slotImages(FlatTopology& m, std::vector<uint16_t>& slots,
+                           std::vector<uint32_t>& img) const {
+  slots.clear();
+  img.clear();
+  m.slotStride = slotStrideFor(int(m.names.size()));
+  m.slotDegree = 0;
+  if (!m.slotStride) return;
+  slots.resize(m.slotStride);
+  placeSlots(colorNodes(m.rowPtr.data(), m.edges.data(), uint32_t(m.names.size())),
+             m.slotStride, slots.data());
+  m.slotDegree = slotDegreeFor(m.maxDegree, m.maxMetric, m.slotStride);
+  if (m.slotDegree) {
+    img.resize(size_t(m.slotDegree) * m.slotStride);
+    placeSlotEdges(slots.data(), m.slotStride, m.rowPtr.data(), m.edges.data(),
+                   uint32_t(m.names.size()), m.slotDegree, img.data());
+  }
 }
 
 // wave-kernel relaxation order + per-slot edge image (slot_order.h); the
 // image carries edge weights, so a patched CSR re-derives it
 void LinkState::uploadSlotImages(FlatTopology& m) const {
-  m.slotStride = slotStrideFor(int(m.names.size()));
-  if (m.slotStride) {
-    std::vector<uint16_t> slots(m.slotStride);
-    placeSlots(colorNodes(m.rowPtr.data(), m.edges.data(),
-                          uint32_t(m.names.size())),
-               m.slotStride, slots.data());
-    m.dSlot.upload(slots.data(), slots.size());
-    m.slotDegree = slotDegreeFor(m.maxDegree, m.maxMetric, m.slotStride);
-    if (m.slotDegree) {
-      std::vector<uint32_t> img(size_t(m.slotDegree) * m.slotStride);
-      placeSlotEdges(slots.data(), m.slotStride, m.rowPtr.data(),
-                     m.edges.data(), uint32_t(m.names.size()), m.slotDegree,
-                     img.data());
-      m.dSlotEdges.upload(img.data(), img.size());
-    }
-  } else {
-    m.slotDegree = 0;
-  }
+  std::vector<uint16_t> slots;
+  std::vector<uint32_t> img;
+  slotImages(m, slots, img);
+  if (m.slotStride) m.dSlot.upload(slots.data(), slots.size());
+  if (m.slotDegree) m.dSlotEdges.upload(img.data(), img.size());
 }
 
 // ------------------------------------------------------------------- SPF --

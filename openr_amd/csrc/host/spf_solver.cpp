@@ -5,11 +5,71 @@
 // RibMplsEntry objects.
 #include <algorithm>
 #include <atomic>
+#include <cstring>
+#include <map>
+#include <mutex>
 
 #include "decision.h"
 #include "slot_order.h"
 
 namespace openr_amd {
+
+namespace {
+struct PinnedPool {
+  std::mutex mu;
+  std::multimap<size_t, void*> free;  // capacity -> block
+  size_t bytes{0};
+  static constexpr size_t kMaxBytes = size_t(256) << 20, kMaxBlock = size_t(64) << 20;
+  ~PinnedPool() {
+    for (auto& [_, p] : free) ogs_host_free(p);
+  }
+};
+PinnedPool& pinnedPool() {
+  static PinnedPool* pool = new PinnedPool;  // outlives static destructors
+  return *pool;
+}
+}  // namespace
+
+void* pinnedAcquire(size_t bytes, size_t* cap) {
+  // power-of-two classes from 4 KiB: a recycled block fits the next request
+  size_t c = 4096;
+  while (c < bytes) c <<= 1;
+  PinnedPool& P = pinnedPool();
+  {
+    std::lock_guard<std::mutex> g(P.mu);
+    auto it = P.free.lower_bound(c);
+    if (it != P.free.end() && it->first <= 4 * c) {
+      void* p = it->second;
+      *cap = it->first;
+      P.bytes -= it->first;
+      P.free.erase(it);
+      return p;
+    }
+  }
+  void* p = nullptr;
+  ogsCheck(ogs_host_alloc(&p, c), "ogs_host_alloc");
+  *cap = c;
+  return p;
+}
+
+void pinnedRelease(void* p, size_t cap) {
+  if (!p) return;
+  PinnedPool& P = pinnedPool();
+  {
+    std::lock_guard<std::mutex> g(P.mu);
+    if (cap <= PinnedPool::kMaxBlock && P.bytes + cap <= PinnedPool::kMaxBytes) {
+      P.free.emplace(cap, p);
+      P.bytes += cap;
+      return;
+    }
+  }
+  ogs_host_free(p);
+}
+
+uint64_t nextVersionStamp() {
+  static std::atomic<uint64_t> stamp{0};
+  return ++stamp;
+}
 
 // ----------------------------------------------------------- PrefixState --
 std::set<std::string> PrefixState::updatePrefix(const std::string& node,
@@ -21,7 +81,7 @@ std::set<std::string> PrefixState::updatePrefix(const std::string& node,
   if (!inserted && *it->second == entry) return changed;
   it->second = std::make_shared<PrefixEntry>(entry);
   changed.insert(entry.prefix);
-  ++version_;
+  version_ = nextVersionStamp();
   return changed;
 }
 
@@ -34,7 +94,7 @@ std::set<std::string> PrefixState::updatePrefix(const std::string& node,
   if (!inserted && *it->second == entry) return changed;
   changed.insert(entry.prefix);
   it->second = std::make_shared<PrefixEntry>(std::move(entry));
-  ++version_;
+  version_ = nextVersionStamp();
   return changed;
 }
 
@@ -46,7 +106,7 @@ std::set<std::string> PrefixState::deletePrefix(const std::string& node,
   if (it != prefixes_.end() && it->second.erase(std::make_pair(node, area))) {
     changed.insert(prefix);
     if (it->second.empty()) prefixes_.erase(it);
-    ++version_;
+    version_ = nextVersionStamp();
   }
   return changed;
 }
@@ -100,9 +160,19 @@ void HostBatch::append(const FlatTopology& t, const PrefixState& ps,
   maxDegree = std::max(maxDegree, t.maxDegree);
   maxMetric = std::max(maxMetric, t.maxMetric);
   hasZeroMetric |= t.hasZeroMetric;
+  const size_t a0 = advNode.size();
+  const uint32_t np = appendPrefixes(t, ps, area);
+  topoDesc.insert(topoDesc.end(),
+                  {n0, N, e0, uint32_t(t.edges.size()), pb0, np, ab0,
+                   uint32_t(advNode.size() - a0)});
+}
+
+uint32_t HostBatch::appendPrefixes(const FlatTopology& t, const PrefixState& ps,
+                                   const std::string& area) {
   uint32_t np = 0;
   const size_t a0 = advNode.size();
   for (const auto& [prefix, entries] : ps.prefixes()) {
+    bool anyMinNh = false;
     for (const auto& [na, e] : entries) {
       if (na.second != area) {
         throw std::out_of_range("prefix advertised in unknown area " + na.second);
@@ -113,10 +183,9 @@ void HostBatch::append(const FlatTopology& t, const PrefixState& ps,
                         {e->metrics.drain_metric, e->metrics.path_preference,
                          e->metrics.source_preference, e->metrics.distance});
       advMinNh.push_back(e->minNexthop ? *e->minNexthop : INT64_MIN);
+      anyMinNh |= e->minNexthop.has_value();
     }
     advOff.push_back(uint32_t(advNode.size()));
-    bool anyMinNh = false;
-    for (const auto& [na, e] : entries) anyMinNh |= e->minNexthop.has_value();
     pfxFlags.push_back((isV4Prefix(prefix) ? OGS_PFX_V4 : 0u) |
                        (anyMinNh ? OGS_PFX_HAS_MIN_NH : 0u));
     ++np;
@@ -124,9 +193,7 @@ void HostBatch::append(const FlatTopology& t, const PrefixState& ps,
   pfxBase.push_back(pfxBase.back() + np);
   maxPrefixes = std::max<int>(maxPrefixes, int(np));
   maxAdvs = std::max<int>(maxAdvs, int(advNode.size() - a0));
-  topoDesc.insert(topoDesc.end(),
-                  {n0, N, e0, uint32_t(t.edges.size()), pb0, np, ab0,
-                   uint32_t(advNode.size()) - ab0});
+  return np;
 }
 
 int HostBatch::slotOrder(std::vector<uint16_t>& out,
@@ -178,13 +245,91 @@ struct PolicyDevice {
   } key;
 };
 
+// Byte layout of a single-topology prefix table packed into one block (one
+// H2D), and of one unit's result records (one D2H): 256-byte aligned spans.
+inline size_t al256(size_t x) { return (x + 255) & ~size_t(255); }
+
+struct TableImage {
+  size_t desc{0}, pfxBase{0}, advOff{0}, advNode{0}, advMetrics{0}, advMinNh{0},
+      pfxFlags{0}, end{0};
+  uint32_t P{0}, A{0};
+  // packs hb (one topology, appendPrefixes) + its topoDesc into `h`
+  void pack(const HostBatch& hb, const uint32_t desc8[8], PinnedBuffer& h) {
+    P = uint32_t(hb.pfxFlags.size());
+    A = uint32_t(hb.advNode.size());
+    desc = 0;
+    pfxBase = al256(desc + 8 * 4);
+    advOff = al256(pfxBase + 2 * 4);
+    advNode = al256(advOff + (P + 1) * 4);
+    advMetrics = al256(advNode + std::max<size_t>(A, 1) * 4);
+    advMinNh = al256(advMetrics + std::max<size_t>(A, 1) * 16);
+    pfxFlags = al256(advMinNh + std::max<size_t>(A, 1) * 8);
+    end = al256(pfxFlags + std::max<size_t>(P, 1));
+    h.resize(end);
+    std::memcpy(h.at<uint32_t>(desc), desc8, 8 * 4);
+    std::memcpy(h.at<uint32_t>(pfxBase), hb.pfxBase.data(), 2 * 4);
+    std::memcpy(h.at<uint32_t>(advOff), hb.advOff.data(), (P + 1) * 4);
+    std::memcpy(h.at<uint32_t>(advNode), hb.advNode.data(), A * 4);
+    std::memcpy(h.at<int32_t>(advMetrics), hb.advMetrics.data(), A * 16);
+    std::memcpy(h.at<int64_t>(advMinNh), hb.advMinNh.data(), A * 8);
+    std::memcpy(h.at<uint8_t>(pfxFlags), hb.pfxFlags.data(), P);
+  }
+  ogs_prefix_table view(const DeviceBuffer& d) const {
+    ogs_prefix_table pt{};
+    pt.max_prefixes = int32_t(P);
+    pt.max_advertisements = int32_t(A);
+    pt.pfx_base = devAt<uint32_t>(d, pfxBase);
+    pt.adv_off = devAt<uint32_t>(d, advOff);
+    pt.adv_node = devAt<uint32_t>(d, advNode);
+    pt.adv_metrics = devAt<int32_t>(d, advMetrics);
+    pt.adv_min_nh = devAt<int64_t>(d, advMinNh);
+    pt.pfx_flags = devAt<uint8_t>(d, pfxFlags);
+    return pt;
+  }
+};
+
+// dist [N] | nh [W][N] | meta [P] | metric [P] | mask [W][P] | sel [P]
+struct ResultImage {
+  size_t dist{0}, nh{0}, meta{0}, metric{0}, mask{0}, sel{0}, end{0};
+  ResultImage() = default;
+  ResultImage(uint32_t N, uint32_t P, int W, size_t db) {
+    const size_t P1 = std::max<uint32_t>(P, 1);
+    nh = al256(size_t(N) * db);
+    meta = nh + al256(size_t(N) * W * 4);
+    metric = meta + al256(P1 * 4);
+    mask = metric + al256(P1 * db);
+    sel = mask + al256(P1 * W * 4);
+    end = sel + al256(P1 * 4);
+  }
+};
+
 struct SpfSolver::Impl {
-  DeviceBuffer pfxBase, advOff, advNode, advMetrics, advMinNh, pfxFlags, desc;
-  DeviceBuffer unit, dist, nh, meta, metric, mask, sel;
+  // ---- single-area buildRouteDb ----
+  // prefix table of (cachedPs, cachedTopo), packed: one H2D per change
+  DeviceBuffer tab;
+  PinnedBuffer hTab;
+  TableImage tabImg;
   const PrefixState* cachedPs{nullptr};
   uint64_t cachedPsVersion{~0ull}, cachedTopoVersion{~0ull};
   const FlatTopology* cachedTopo{nullptr};
   PrefixHostTable table;
+  // the unit (uploaded when the source changes) and the result block: one
+  // D2H per build (the SPF part only when node-label routes need it)
+  DeviceBuffer unit, res;
+  PinnedBuffer hRes;
+  uint32_t unitSrc{~0u};
+  // SPF memo: res's dist / nh spans hold the SPF of spfSrc in spfTopo at
+  // spfVersion (ResultImage of spfN / spfW / spfDb) -- what
+  // createRoutesForPrefixes routes a changed prefix set against
+  const FlatTopology* spfTopo{nullptr};
+  uint64_t spfVersion{~0ull};
+  uint32_t spfSrc{~0u}, spfN{0};
+  int spfW{0};
+  size_t spfDb{0};
+  // createRoutesForPrefixes: the changed prefixes' sub-table and records
+  DeviceBuffer subTab, subRes;
+  PinnedBuffer hSubTab, hSubRes;
+  PrefixHostTable subTable;
   PolicyDevice policy;
 
   // multi-area domain (buildRouteDbMultiArea): the areas' CSR as one graph
@@ -508,6 +653,62 @@ void addNodeLabelRoutes(const LinkState& ls, const FlatTopology& f,
   }
 }
 
+namespace {
+
+ogs_graph singleGraph(const FlatTopology& f, const uint32_t* desc) {
+  ogs_graph g{};
+  g.num_topos = 1;
+  g.max_nodes = int32_t(f.names.size());
+  g.max_edges = int32_t(f.edges.size());
+  g.max_degree = f.maxDegree;
+  g.topo_desc = desc;
+  g.node_base = f.dNodeBase.as<uint32_t>();
+  g.row_ptr = f.dRow.as<uint32_t>();
+  g.edges = f.dEdges.as<uint64_t>();
+  g.node_flags = f.dFlags.as<uint8_t>();
+  g.slot_node = f.slotStride ? f.dSlot.as<uint16_t>() : nullptr;
+  g.slot_stride = f.slotStride;
+  g.slot_edges = f.slotDegree ? f.dSlotEdges.as<uint32_t>() : nullptr;
+  g.slot_degree = f.slotDegree;
+  g.edge_src = f.dEdgeSrc.as<uint32_t>();
+  return g;
+}
+
+// host widening of a u32 / u64 record span (all-ones = unreachable)
+void widenSpan(const void* src, size_t n, bool wide, std::vector<uint64_t>& v) {
+  v.resize(n);
+  if (wide) {
+    std::memcpy(v.data(), src, n * 8);
+    return;
+  }
+  const uint32_t* t = static_cast<const uint32_t*>(src);
+  for (size_t i = 0; i < n; ++i) v[i] = t[i] == 0xFFFFFFFFu ? ~0ull : t[i];
+}
+
+}  // namespace
+
+void SpfSolver::prepareSingleArea(const FlatTopology& f, const PrefixState& ps,
+                                  const std::string& area) {
+  Impl& I = *impl_;
+  // prefix table (cached on PrefixState / topology version): one packed H2D
+  if (I.cachedPs == &ps && I.cachedPsVersion == ps.version() && I.cachedTopo == &f &&
+      I.cachedTopoVersion == f.version) {
+    return;
+  }
+  HostBatch hb;
+  const uint32_t np = hb.appendPrefixes(f, ps, area);
+  const uint32_t desc[8] = {0, uint32_t(f.names.size()), 0, uint32_t(f.edges.size()),
+                            0, np, 0, uint32_t(hb.advNode.size())};
+  I.table.build(ps);
+  I.tabImg.pack(hb, desc, I.hTab);
+  I.tab.resize(I.tabImg.end);
+  ogsCheck(ogs_memcpy_h2d(I.tab.get(), I.hTab.get(), I.tabImg.end, nullptr), "ogs_memcpy_h2d");
+  I.cachedPs = &ps;
+  I.cachedPsVersion = ps.version();
+  I.cachedTopo = &f;
+  I.cachedTopoVersion = f.version;
+}
+
 std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(
     const std::string& me, const AreaLinkStates& als, const PrefixState& ps) {
   bool exists = false;  // SpfSolver.cpp:318-324
@@ -521,25 +722,7 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(
   // on the device (spf_exact.hip), 64-bit distances
   const bool exact = f.hasZeroMetric || f.hasWideMetric;
   Impl& I = *impl_;
-
-  // ---- prefix table (cached on PrefixState / topology version) ------------
-  if (I.cachedPs != &ps || I.cachedPsVersion != ps.version() ||
-      I.cachedTopo != &f || I.cachedTopoVersion != f.version) {
-    HostBatch hb;
-    hb.append(f, ps, area);
-    I.table.build(ps);
-    I.pfxBase.upload(hb.pfxBase.data(), hb.pfxBase.size());
-    I.desc.upload(hb.topoDesc.data(), hb.topoDesc.size());
-    I.advOff.upload(hb.advOff.data(), hb.advOff.size());
-    I.advNode.upload(hb.advNode.data(), hb.advNode.size());
-    I.advMetrics.upload(hb.advMetrics.data(), hb.advMetrics.size());
-    I.advMinNh.upload(hb.advMinNh.data(), hb.advMinNh.size());
-    I.pfxFlags.upload(hb.pfxFlags.data(), hb.pfxFlags.size());
-    I.cachedPs = &ps;
-    I.cachedPsVersion = ps.version();
-    I.cachedTopo = &f;
-    I.cachedTopoVersion = f.version;
-  }
+  prepareSingleArea(f, ps, area);
 
   // ---- launch the fused kernel for (topology, me) -------------------------
   const uint32_t s = f.id.at(me);
@@ -549,47 +732,25 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(
   const int W = std::max(1, ogs_nh_words_for_degree(degree));
   const bool wide = exact || wideDistancesNeeded(f);
   const size_t db = wide ? 8 : 4;
-  const ogs_unit u{0, s};
-  I.unit.upload(&u, 1);
-  I.dist.resize(N * db);
-  I.nh.resize(size_t(N) * W * 4);
-  const size_t P1 = std::max<uint32_t>(P, 1);
-  I.meta.resize(P1 * 4);
-  I.metric.resize(P1 * db);
-  I.mask.resize(P1 * W * 4);
-  I.sel.resize(P1 * 4);
+  if (I.unitSrc != s) {
+    const ogs_unit u{0, s};
+    I.unit.upload(&u, 1);
+    I.unitSrc = s;
+  }
+  const ResultImage L(N, P, W, db);
+  I.spfTopo = nullptr;  // res is overwritten below
+  I.res.resize(L.end);
+  I.hRes.resize(L.end);
 
-  ogs_graph g{};
-  g.num_topos = 1;
-  g.max_nodes = int32_t(N);
-  g.max_edges = int32_t(f.edges.size());
-  g.max_degree = f.maxDegree;
-  g.topo_desc = I.desc.as<uint32_t>();
-  g.node_base = f.dNodeBase.as<uint32_t>();
-  g.row_ptr = f.dRow.as<uint32_t>();
-  g.edges = f.dEdges.as<uint64_t>();
-  g.node_flags = f.dFlags.as<uint8_t>();
-  g.slot_node = f.slotStride ? f.dSlot.as<uint16_t>() : nullptr;
-  g.slot_stride = f.slotStride;
-  g.slot_edges = f.slotDegree ? f.dSlotEdges.as<uint32_t>() : nullptr;
-  g.slot_degree = f.slotDegree;
-  g.edge_src = f.dEdgeSrc.as<uint32_t>();
-  ogs_prefix_table pt{};
-  pt.max_prefixes = int32_t(P);
-  pt.max_advertisements = int32_t(I.table.advEntry.size());
-  pt.pfx_base = I.pfxBase.as<uint32_t>();
-  pt.adv_off = I.advOff.as<uint32_t>();
-  pt.adv_node = I.advNode.as<uint32_t>();
-  pt.adv_metrics = I.advMetrics.as<int32_t>();
-  pt.adv_min_nh = I.advMinNh.as<int64_t>();
-  pt.pfx_flags = I.pfxFlags.as<uint8_t>();
+  const ogs_graph g = singleGraph(f, devAt<uint32_t>(I.tab, I.tabImg.desc));
+  const ogs_prefix_table pt = I.tabImg.view(I.tab);
   ogs_spf_out out{};
-  out.dist = I.dist.get();
-  out.nh = I.nh.as<uint32_t>();
-  out.meta = I.meta.as<uint32_t>();
-  out.metric = I.metric.get();
-  out.mask = I.mask.as<uint32_t>();
-  out.sel = I.sel.as<uint32_t>();
+  out.dist = devAt<void>(I.res, L.dist);
+  out.nh = devAt<uint32_t>(I.res, L.nh);
+  out.meta = devAt<uint32_t>(I.res, L.meta);
+  out.metric = devAt<void>(I.res, L.metric);
+  out.mask = devAt<uint32_t>(I.res, L.mask);
+  out.sel = devAt<uint32_t>(I.res, L.sel);
   const uint32_t flags = (enableV4_ ? OGS_F_ENABLE_V4 : 0u) |
       (v4OverV6Nexthop_ ? OGS_F_V4_OVER_V6 : 0u) |
       (enableBestRouteSelection_ ? OGS_F_BEST_ROUTE_SELECTION : 0u) |
@@ -598,48 +759,41 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(
                           flags, W, &out, nullptr),
            "ogs_spf_routes");
   ls.noteSpfRuns(1);
+  I.spfTopo = &f;
+  I.spfVersion = f.version;
+  I.spfSrc = s;
+  I.spfN = N;
+  I.spfW = W;
+  I.spfDb = db;
   const RibPolicy* policy = (ribPolicy_ && ribPolicy_->isActive()) ? ribPolicy_ : nullptr;
   std::vector<uint8_t> applied, counter;
   if (policy && P) {
-    runPolicyOnDevice(*policy, I.table, pt, {{&f, s}}, me, W, I.meta.as<uint32_t>(),
-                      I.mask.as<uint32_t>(), I.policy, nullptr);
+    runPolicyOnDevice(*policy, I.table, pt, {{&f, s}}, me, W, out.meta, out.mask,
+                      I.policy, nullptr);
     downloadPolicy(I.policy, P, applied, counter);
   }
-
-  auto widen = [&](const DeviceBuffer& b, size_t n, std::vector<uint64_t>& v) {
-    v.resize(n);
-    if (wide) {
-      b.download(v.data(), n);
-    } else {
-      std::vector<uint32_t> t(n);
-      b.download(t.data(), n);
-      for (size_t i = 0; i < n; ++i) v[i] = t[i] == 0xFFFFFFFFu ? ~0ull : t[i];
-    }
-  };
-  std::vector<uint64_t> dist, metric;
-  std::vector<uint32_t> nh(size_t(N) * W), meta(P), mask(size_t(P) * W), sel(P);
-  widen(I.dist, N, dist);
-  I.nh.download(nh.data(), nh.size());
-  if (P) {
-    I.meta.download(meta.data(), P);
-    widen(I.metric, P, metric);
-    I.mask.download(mask.data(), mask.size());
-    I.sel.download(sel.data(), P);
-  }
+  // ONE D2H of the records (+ the SPF when node-label routes read it)
+  const size_t from = enableNodeSegmentLabel_ ? 0 : L.meta;
+  ogsCheck(ogs_memcpy_d2h(I.hRes.at<char>(from), devAt<char>(I.res, from), L.end - from,
+                          nullptr),
+           "ogs_memcpy_d2h");
   ogsCheck(ogs_stream_sync(nullptr), "ogs_stream_sync");
 
+  std::vector<uint64_t> dist, metric;
+  if (enableNodeSegmentLabel_) widenSpan(I.hRes.at<void>(L.dist), N, wide, dist);
+  widenSpan(I.hRes.at<void>(L.metric), P, wide, metric);
   UnitView view;
   view.W = W;
   view.N = N;
   view.P = P;
-  view.dist = dist.data();
-  view.nh = nh.data();
+  view.dist = enableNodeSegmentLabel_ ? dist.data() : nullptr;
+  view.nh = I.hRes.at<uint32_t>(L.nh);
   view.nhStride = N;
-  view.meta = meta.data();
+  view.meta = I.hRes.at<uint32_t>(L.meta);
   view.metric = metric.data();
-  view.mask = mask.data();
+  view.mask = I.hRes.at<uint32_t>(L.mask);
   view.maskStride = P;
-  view.sel = sel.data();
+  view.sel = I.hRes.at<uint32_t>(L.sel);
   if (policy && P) {
     view.policy = policy;
     view.applied = applied.data();
@@ -648,6 +802,105 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(
   return materializeRouteDb(ls, f, area, me, view, I.table, v4OverV6Nexthop_,
                             enableNodeSegmentLabel_, staticUnicastRoutes_,
                             &bestRoutesCache_);
+}
+
+// The incremental branch's routes (createRoutesForPrefixes) of a single-area
+// source: the SPF memo of the last build (SPF-only launch on a miss), the
+// changed prefixes' sub-table in one H2D, ogs_routes_from_spf, one D2H.
+void SpfSolver::routesFromSpfMemo(const std::string& me, const LinkState& ls,
+                                  const std::string& area, const PrefixState& ps,
+                                  const PrefixState& sub,
+                                  std::map<std::string, std::optional<RibUnicastEntry>>& out) {
+  Impl& I = *impl_;
+  const FlatTopology& f = ls.flatOnDevice();
+  const bool exact = f.hasZeroMetric || f.hasWideMetric;
+  const uint32_t s = f.id.at(me);
+  const uint32_t N = uint32_t(f.names.size());
+  const int degree = int(f.rowPtr[s + 1] - f.rowPtr[s]);
+  const int W = std::max(1, ogs_nh_words_for_degree(degree));
+  const bool wide = exact || wideDistancesNeeded(f);
+  const size_t db = wide ? 8 : 4;
+  const uint32_t flags = (enableV4_ ? OGS_F_ENABLE_V4 : 0u) |
+      (v4OverV6Nexthop_ ? OGS_F_V4_OVER_V6 : 0u) |
+      (enableBestRouteSelection_ ? OGS_F_BEST_ROUTE_SELECTION : 0u) |
+      (wide ? OGS_F_WIDE_METRIC : 0u) | (exact ? OGS_F_EXACT_ORDER : 0u);
+  if (I.unitSrc != s) {
+    const ogs_unit u{0, s};
+    I.unit.upload(&u, 1);
+    I.unitSrc = s;
+  }
+  prepareSingleArea(f, ps, area);  // the topoDesc the SPF launch reads
+  if (!(I.spfTopo == &f && I.spfVersion == f.version && I.spfSrc == s)) {
+    const ResultImage L(N, 0, W, db);
+    I.spfTopo = nullptr;
+    I.res.resize(L.end);
+    const ogs_graph g = singleGraph(f, devAt<uint32_t>(I.tab, I.tabImg.desc));
+    ogs_spf_out so{};
+    so.dist = devAt<void>(I.res, L.dist);
+    so.nh = devAt<uint32_t>(I.res, L.nh);
+    ogsCheck(ogs_spf_routes(&g, nullptr, I.unit.as<ogs_unit>(), 1, flags, W, &so, nullptr),
+             "ogs_spf_routes");
+    ls.noteSpfRuns(1);
+    I.spfTopo = &f;
+    I.spfVersion = f.version;
+    I.spfSrc = s;
+    I.spfN = N;
+    I.spfW = W;
+    I.spfDb = db;
+  }
+  const ResultImage S(I.spfN, 0, I.spfW, I.spfDb);
+
+  // the changed prefixes' table: one packed H2D
+  HostBatch hb;
+  const uint32_t np = hb.appendPrefixes(f, sub, area);
+  const uint32_t desc[8] = {0, N, 0, uint32_t(f.edges.size()), 0, np, 0,
+                            uint32_t(hb.advNode.size())};
+  I.subTable.build(sub);
+  TableImage T;
+  T.pack(hb, desc, I.hSubTab);
+  I.subTab.resize(T.end);
+  ogsCheck(ogs_memcpy_h2d(I.subTab.get(), I.hSubTab.get(), T.end, nullptr), "ogs_memcpy_h2d");
+  const ResultImage R(0, np, W, db);  // records only (dist / nh spans empty)
+  I.subRes.resize(R.end);
+  I.hSubRes.resize(R.end);
+  const ogs_graph g = singleGraph(f, devAt<uint32_t>(I.subTab, T.desc));
+  const ogs_prefix_table pt = T.view(I.subTab);
+  ogs_spf_out ro{};
+  ro.meta = devAt<uint32_t>(I.subRes, R.meta);
+  ro.metric = devAt<void>(I.subRes, R.metric);
+  ro.mask = devAt<uint32_t>(I.subRes, R.mask);
+  ro.sel = devAt<uint32_t>(I.subRes, R.sel);
+  ogsCheck(ogs_routes_from_spf(&g, &pt, I.unit.as<ogs_unit>(), 1, devAt<void>(I.res, S.dist),
+                               devAt<uint32_t>(I.res, S.nh), flags, W, &ro, nullptr),
+           "ogs_routes_from_spf");
+  ogsCheck(ogs_memcpy_d2h(I.hSubRes.at<char>(R.meta), devAt<char>(I.subRes, R.meta),
+                          R.end - R.meta, nullptr),
+           "ogs_memcpy_d2h");
+  ogsCheck(ogs_stream_sync(nullptr), "ogs_stream_sync");
+
+  std::vector<uint64_t> metric;
+  widenSpan(I.hSubRes.at<void>(R.metric), np, wide, metric);
+  const uint32_t* meta = I.hSubRes.at<uint32_t>(R.meta);
+  const uint32_t* mask = I.hSubRes.at<uint32_t>(R.mask);
+  const uint32_t* sel = I.hSubRes.at<uint32_t>(R.sel);
+  const PrefixHostTable& st = I.subTable;
+  for (uint32_t p = 0; p < np; ++p) {
+    const std::string& prefix = st.prefixes[p];
+    if (meta[p] & OGS_ROUTE_SELECTED) {  // SpfSolver.cpp:247
+      RouteSelectionResult rs;
+      const uint32_t a0 = st.advOff[p], a1 = st.advOff[p + 1];
+      for (uint32_t a = a0; a < std::min(a1, a0 + 32); ++a) {
+        if (sel[p] >> (a - a0) & 1u) rs.allNodeAreas.insert(st.advKey[a]);
+      }
+      rs.bestNodeArea = st.advKey[a0 + (meta[p] >> OGS_ROUTE_BEST_SHIFT)];
+      rs.isBestNodeDrained = meta[p] & OGS_ROUTE_DRAINED;
+      bestRoutesCache_[prefix] = std::move(rs);
+    } else {
+      bestRoutesCache_.erase(prefix);
+    }
+    out[prefix] = materializeRoute(f, me, st, p, meta[p], metric[p], &mask[p], np, W,
+                                   v4OverV6Nexthop_, nullptr, 0xFF, 0xFF);
+  }
 }
 
 // Domain tables of a multi-area buildRouteDb: the areas' CSR as one graph
@@ -1003,51 +1256,37 @@ DecisionRouteDb SpfSolver::downloadMultiArea(const std::string& me,
 std::optional<RibUnicastEntry> SpfSolver::createRouteForPrefixOrGetStaticRoute(
     const std::string& me, const AreaLinkStates& als, const PrefixState& ps,
     const std::string& prefix) {  // SpfSolver.cpp:139-158
-  std::optional<RibUnicastEntry> route;
-  bool exists = false;
-  for (const auto& [_, l] : als) exists |= l.hasNode(me);
-  auto pit = ps.prefixes().find(prefix);
-  const bool gated = isV4Prefix(prefix) && !enableV4_ && !v4OverV6Nexthop_;
-  if (exists && !gated && pit != ps.prefixes().end()) {
-    PrefixState one;  // a one-prefix table through the same GPU path
-    for (const auto& [na, e] : pit->second) one.updatePrefix(na.first, na.second, *e);
-    SpfSolver probe(myNodeName_, enableV4_, false, enableBestRouteSelection_,
-                    v4OverV6Nexthop_);
-    auto db = probe.buildRouteDb(me, als, one);
-    if (db) {
-      auto it = db->unicastRoutes.find(prefix);
-      if (it != db->unicastRoutes.end()) route = it->second;
-    }
-    auto bc = probe.getBestRoutesCache().find(prefix);
-    if (bc != probe.getBestRoutesCache().end()) {
-      bestRoutesCache_[prefix] = bc->second;
-    } else {
-      bestRoutesCache_.erase(prefix);
-    }
-  }
-  if (route) return route;
-  auto it = staticUnicastRoutes_.find(prefix);
-  if (it != staticUnicastRoutes_.end()) return it->second;
-  return std::nullopt;
+  return createRoutesForPrefixes(me, als, ps, {prefix}).at(prefix);
 }
 
 std::map<std::string, std::optional<RibUnicastEntry>> SpfSolver::createRoutesForPrefixes(
     const std::string& me, const AreaLinkStates& als, const PrefixState& ps,
     const std::set<std::string>& prefixes) {
   std::map<std::string, std::optional<RibUnicastEntry>> out;
-  bool exists = false;
+  bool exists = false;  // SpfSolver.cpp:139-158 per prefix
   for (const auto& [_, l] : als) exists |= l.hasNode(me);
-  PrefixState sub;  // the changed prefixes through one GPU build
+  PrefixState sub;  // the changed prefixes through one route launch
   std::set<std::string> asked;
   for (const auto& prefix : prefixes) {
     out[prefix] = std::nullopt;
     auto pit = ps.prefixes().find(prefix);
     const bool gated = isV4Prefix(prefix) && !enableV4_ && !v4OverV6Nexthop_;
-    if (!exists || gated || pit == ps.prefixes().end()) continue;
+    // gated or unknown prefix: returned before the selection cache is
+    // touched (SpfSolver.cpp:170-182); known prefix: its entry is cleared,
+    // then set again only by a successful selection (:185, :239)
+    if (gated || pit == ps.prefixes().end()) continue;
+    if (!exists) {
+      bestRoutesCache_.erase(prefix);
+      continue;
+    }
     for (const auto& [na, e] : pit->second) sub.updatePrefix(na.first, na.second, *e);
     asked.insert(prefix);
   }
-  if (!asked.empty()) {
+  if (!asked.empty() && als.size() == 1) {
+    std::string area;
+    const LinkState& ls = singleArea(als, area);
+    routesFromSpfMemo(me, ls, area, ps, sub, out);
+  } else if (!asked.empty()) {
     SpfSolver probe(myNodeName_, enableV4_, false, enableBestRouteSelection_,
                     v4OverV6Nexthop_);
     auto db = probe.buildRouteDb(me, als, sub);

@@ -44,6 +44,10 @@ hipError_t launch_route_changes(const uint32_t* changed, int nUnits, int Sp, int
                                 hipStream_t stream);
 hipError_t launch_csr_patch(uint64_t* edges, const uint32_t* idx, const uint64_t* val,
                             int n, hipStream_t stream);
+hipError_t launch_routes_from_spf(const ogs_graph& g, const ogs_prefix_table& pt,
+                                  const ogs_unit* units, int n, const void* dist,
+                                  const uint32_t* nh, uint32_t flags, int W,
+                                  const ogs_spf_out& out, hipStream_t stream);
 hipError_t launch_ksp(const ogs_graph& g, const ogs_path_unit* units,
                       int nUnits, const uint32_t* masks, uint32_t maskWords,
                       uint32_t flags, const ogs_path_out& out,
@@ -126,6 +130,21 @@ int ogs_memset(void* dst, int value, size_t bytes, void* stream) {
   hipError_t e =
       hipMemsetAsync(dst, value, bytes, static_cast<hipStream_t>(stream));
   return e == hipSuccess ? OGS_OK : hipFail(e, "hipMemsetAsync");
+}
+
+int ogs_host_alloc(void** hptr, size_t bytes) {
+  if (!hptr) return fail(OGS_E_INVALID, "hptr is NULL");
+  *hptr = nullptr;
+  if (bytes == 0) return OGS_OK;
+  hipError_t e = hipHostMalloc(hptr, bytes, hipHostMallocDefault);
+  if (e == hipErrorOutOfMemory) return fail(OGS_E_NOMEM, "hipHostMalloc: out of memory");
+  return e == hipSuccess ? OGS_OK : hipFail(e, "hipHostMalloc");
+}
+
+int ogs_host_free(void* hptr) {
+  if (!hptr) return OGS_OK;
+  hipError_t e = hipHostFree(hptr);
+  return e == hipSuccess ? OGS_OK : hipFail(e, "hipHostFree");
 }
 
 int ogs_stream_sync(void* stream) {
@@ -263,6 +282,27 @@ int ogs_spf_routes(const ogs_graph* graph, const ogs_prefix_table* prefixes,
     return fail(OGS_E_UNSUPPORTED, "no SPF path for these shapes");
   }
   return e == hipSuccess ? OGS_OK : hipFail(e, "spf_route launch");
+}
+
+int ogs_routes_from_spf(const ogs_graph* graph, const ogs_prefix_table* prefixes,
+                        const ogs_unit* units, int32_t n_units, const void* spf_dist,
+                        const uint32_t* spf_nh, uint32_t flags, int32_t nh_words,
+                        ogs_spf_out* out, void* stream) {
+  if (!graph || !prefixes || !out) return fail(OGS_E_INVALID, "graph/prefixes/out is NULL");
+  if (n_units < 0) return fail(OGS_E_INVALID, "n_units < 0");
+  if (n_units == 0 || prefixes->max_prefixes <= 0) return OGS_OK;
+  if (!units || !spf_dist || !spf_nh || !graph->node_base || !graph->node_flags ||
+      !prefixes->pfx_base || !prefixes->adv_off || !prefixes->adv_node ||
+      !prefixes->adv_metrics || !prefixes->adv_min_nh || !prefixes->pfx_flags) {
+    return fail(OGS_E_INVALID, "input arrays are NULL");
+  }
+  if (ogs_nh_words_for_degree(nh_words * 32) != nh_words) {
+    return fail(OGS_E_UNSUPPORTED, "nh_words must be 1, 2, 4, 8 or 16");
+  }
+  hipError_t e = ogs::launch_routes_from_spf(*graph, *prefixes, units, n_units, spf_dist,
+                                            spf_nh, flags, nh_words, *out,
+                                            static_cast<hipStream_t>(stream));
+  return e == hipSuccess ? OGS_OK : hipFail(e, "routes-from-spf launch");
 }
 
 int ogs_ksp_paths(const ogs_graph* graph, const ogs_path_unit* units,

@@ -234,4 +234,27 @@ hipError_t launch_spf_routes_global(const ogs_graph& g, const ogs_prefix_table* 
   return launch_global_d<uint32_t>(g, pt, units, nUnits, flags, W, out, stream);
 }
 
+// ogs_routes_from_spf: route_global_kernel over caller-held SPF state.
+hipError_t launch_routes_from_spf(const ogs_graph& g, const ogs_prefix_table& pt,
+                                  const ogs_unit* units, int n, const void* dist,
+                                  const uint32_t* nh, uint32_t flags, int W,
+                                  const ogs_spf_out& out, hipStream_t stream) {
+  const bool wide = (flags & OGS_F_WIDE_METRIC) != 0;
+#define OGS_RFS(W_)                                                                         \
+  return wide ? launch_route_global<uint64_t, W_>(g, pt, units, n, flags,                   \
+                                                  static_cast<const uint64_t*>(dist), nh,   \
+                                                  out, stream)                              \
+              : launch_route_global<uint32_t, W_>(g, pt, units, n, flags,                   \
+                                                  static_cast<const uint32_t*>(dist), nh,   \
+                                                  out, stream);
+  switch (W) {
+    case 1: OGS_RFS(1)
+    case 2: OGS_RFS(2)
+    case 4: OGS_RFS(4)
+    case 8: OGS_RFS(8)
+    default: OGS_RFS(16)
+  }
+#undef OGS_RFS
+}
+
 }  // namespace ogs
