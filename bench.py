@@ -818,7 +818,6 @@ def main():
     o_meta = torch.empty(U * Sp, dtype=torch.int32, device=dev)
     o_metric = torch.empty(U * Sp, dtype=torch.int32, device=dev)
     o_mask = torch.empty(U * W * Sp, dtype=torch.int32, device=dev)
-    o_sel = torch.empty(U * Sp, dtype=torch.int32, device=dev)
 
     g = capi.Graph(h["num_topos"], Sn, h["max_edges"], h["max_degree"], node_base.data_ptr(),
                    row_ptr.data_ptr(), edges.data_ptr(), node_flags.data_ptr(), topo_desc.data_ptr(),
@@ -827,8 +826,10 @@ def main():
     pt = capi.PrefixTable(Sp, h["max_advertisements"], pfx_base.data_ptr(), adv_off.data_ptr(),
                           adv_node.data_ptr(), adv_metrics.data_ptr(),
                           adv_min_nh.data_ptr(), pfx_flags.data_ptr())
+    # no selection bits: BatchRunner-style consumers read them only for
+    # bestRoutesCache (not part of the §8(d) output bytes)
     out = capi.SpfOut(o_dist.data_ptr(), o_nh.data_ptr(), o_meta.data_ptr(),
-                      o_metric.data_ptr(), o_mask.data_ptr(), o_sel.data_ptr())
+                      o_metric.data_ptr(), o_mask.data_ptr(), None)
     stream = torch.cuda.current_stream(dev)
     sptr = ctypes.c_void_p(stream.cuda_stream)
     gref, pref, oref = ctypes.byref(g), ctypes.byref(pt), ctypes.byref(out)

@@ -11,6 +11,7 @@ namespace ogs {
 extern int g_unitWidth;
 extern int g_waveWgLds;
 extern int g_waveUpb;
+extern int g_waveOpt;
 extern int g_msGroup;
 extern int g_routeStream;
 extern int g_spfFrontier;
@@ -215,6 +216,11 @@ int ogs_set_option(const char* name, int64_t value) {
       return fail(OGS_E_INVALID, "wave_upb must be 4, 8 or 16");
     }
     ogs::g_waveUpb = int(value);
+    return OGS_OK;
+  }
+  if (std::strcmp(name, "wave_opt") == 0) {
+    if (value < 0 || value > 3) return fail(OGS_E_INVALID, "wave_opt must be in [0, 3]");
+    ogs::g_waveOpt = int(value);
     return OGS_OK;
   }
   if (std::strcmp(name, "wave_wg_lds") == 0) {

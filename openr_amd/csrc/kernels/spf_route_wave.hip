@@ -3,9 +3,14 @@
 //
 // Algorithm and outputs are those of spf_route.hip (reference mapping in its
 // header). Measured on MI355X, a C2 launch is 4096 units all resident at
-// once (16 waves/CU), and the relaxation rounds are LDS-throughput bound
-// (random-address reads into 16 units' working sets). This variant cuts LDS
-// instructions, not latency:
+// once (16 waves/CU), and the relaxation rounds are bound by the per-round
+// dependency chain (LDS gather -> ~10 dependent VALU ops -> ballot/branch)
+// at 4 waves per SIMD. Measured and rejected (tools/ab_wave_opt.py,
+// DESIGN.md §3): register-resident words gathered with ds_bpermute (no LDS
+// traffic, no bank conflicts: same round time) and persistent waves running
+// 2-4 units with the next unit's loads in flight during the rounds (half the
+// waves per SIMD doubles the round latency). This variant cuts LDS
+// instructions:
 //  * per node ONE 64-bit LDS word {dist, next-hop bits}: one ds_read_b64
 //    per edge instead of two ds_read_b32;
 //  * branch-free relaxation: unusable edges read a dummy word, edges into
@@ -17,7 +22,10 @@
 //  * edges (<= MAXD per node) and the node's own value stay in registers;
 //  * one dependent global load for the unit's offsets (ogs_graph.topo_desc)
 //    and one batch of staging loads for CSR + prefix table;
-//  * single-advertiser prefixes take a straight-line route path.
+//  * single-advertiser prefixes take a straight-line route path; when every
+//    prefix has exactly one advertisement at its own index (identity
+//    segments) the route phase reads advertiser and flags from the staging
+//    registers and the prefix tables never touch LDS.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -27,6 +35,9 @@
 #include "spf_core.h"
 
 namespace ogs {
+
+constexpr uint32_t OGS_WAVE_OPT_BPERMUTE = 1;    // register-resident SPF words
+constexpr uint32_t OGS_WAVE_OPT_REG_ROUTES = 2;  // identity-segment route path
 
 // LDS image of one unit. Advertisement metrics are staged only when best
 // route selection reads them; minNexthop is read from HBM on demand (only
@@ -140,7 +151,7 @@ template <int NPL, int MAXD, int UPB>
 __global__ __launch_bounds__(64 * UPB) void spf_route_wave_kernel(
     ogs_graph g, ogs_prefix_table pt, int hasPrefixes,
     const ogs_unit* __restrict__ units, int nUnits, uint32_t flags,
-    ogs_spf_out out, uint32_t ldsPerUnit, uint32_t maxA) {
+    ogs_spf_out out, uint32_t ldsPerUnit, uint32_t maxA, uint32_t wopt) {
   constexpr uint32_t kInf = 0xFFFFFFFFu;
   // wave-uniform by construction; readfirstlane lets the compiler prove it,
   // so the unit record and its descriptor come through scalar loads
@@ -215,6 +226,13 @@ __global__ __launch_bounds__(64 * UPB) void spf_route_wave_kernel(
   constexpr uint32_t P0 = NPL * 64;
   const bool img = perm && g.slot_edges && g.slot_degree == MAXD;
   uint32_t ie[NPL][MAXD];
+  constexpr int KP = NPL + 1;  // prefixes per lane per pass (P <= 64*KP)
+  WStage<KP, uint32_t> sOff, sNode;
+  WStage<KP, uint8_t> sPf;
+  // identity segments (every prefix has exactly one advertisement, at its
+  // own index: the common single-advertiser table): the route phase reads
+  // advertiser and flags from these registers, the tables skip LDS
+  bool ident = false;
   {
     WStage<NPL + 1, uint32_t> sRow;
     WStage<NPL * MAXD, uint64_t> sEdge;  // E <= N * MAXD <= 64 * NPL * MAXD
@@ -243,10 +261,7 @@ __global__ __launch_bounds__(64 * UPB) void spf_route_wave_kernel(
     uint32_t rawSlot[NPL];
 #pragma unroll
     for (int k = 0; k < NPL; ++k) rawSlot[k] = so[k * 64 + lane];
-    constexpr int KP = NPL + 1;  // prefixes per lane per pass (P <= 64*KP)
-    WStage<KP, uint32_t> sOff, sNode;
     WStage<KP, int4> sMet;
-    WStage<KP, uint8_t> sPf;
     const bool pfxFits = (P + 1 <= 64u * KP) && (A <= 64u * KP);
     if (hasPrefixes && pfxFits) {
       sOff.load(pt.adv_off + p0, P + 1, lane);
@@ -258,10 +273,21 @@ __global__ __launch_bounds__(64 * UPB) void spf_route_wave_kernel(
     for (int k = 0; k < NPL; ++k) {
       vk[k] = rawSlot[k] == 0xFFFFu ? 0xFFFFFFFFu : rawSlot[k];
     }
+    if (hasPrefixes && pfxFits && A == P && (wopt & OGS_WAVE_OPT_REG_ROUTES)) {
+      bool off = false;
+#pragma unroll
+      for (int k = 0; k < KP; ++k) {
+        const uint32_t i = uint32_t(k * 64 + lane);
+        off |= i <= P && sOff.v[k] - a0 != i;
+      }
+      ident = __builtin_amdgcn_ballot_w64(off) == 0ull;
+    }
     sRow.store(lrow, img ? 0u : N + 1, lane);
     sEdge.store(ledg, img ? 0u : E, lane);
     sFlag.store(lflags, N, lane);
-    if (hasPrefixes && pfxFits) {
+    if (ident) {
+      // tables stay in registers
+    } else if (hasPrefixes && pfxFits) {
       sOff.store(lAdvOff, P + 1, lane);
       sNode.store(lAdvNode, A, lane);
       sMet.store(lAdvMetrics, brs ? A : 0u, lane);
@@ -295,13 +321,13 @@ __global__ __launch_bounds__(64 * UPB) void spf_route_wave_kernel(
   const bool hop = flags & OGS_F_HOP_METRIC;
   uint32_t ea[NPL][MAXD], ew[NPL][MAXD];  // word position, weight (0 if unusable)
   uint32_t wmax = 0;
-  if (img) {
-    uint32_t posS = 0;  // the source's position (uniform)
+  uint32_t posS = P0;  // the source's position (uniform; P0: not placed)
 #pragma unroll
-    for (int k = 0; k < NPL; ++k) {
-      const uint64_t m = __builtin_amdgcn_ballot_w64(vk[k] == s);
-      if (m) posS = uint32_t(k * 64) + uint32_t(__builtin_ctzll(m));
-    }
+  for (int k = 0; k < NPL; ++k) {
+    const uint64_t m = __builtin_amdgcn_ballot_w64(vk[k] == s);
+    if (m) posS = uint32_t(k * 64) + uint32_t(__builtin_ctzll(m));
+  }
+  if (img) {
 #pragma unroll
     for (int k = 0; k < NPL; ++k) {
 #pragma unroll
@@ -378,6 +404,21 @@ __global__ __launch_bounds__(64 * UPB) void spf_route_wave_kernel(
     }
     sep = __builtin_amdgcn_ballot_w64(bad) == 0ull;
   }
+  // register-resident relaxation (ds_bpermute gathers, no LDS words):
+  // one slot (Jacobi), or two separated slots whose source edges cross
+  // slots too (each slot reads only the other slot's register)
+  bool regSpf = (wopt & OGS_WAVE_OPT_BPERMUTE) && posS < P0 && (NPL == 1 || (NPL == 2 && sep));
+  if (NPL == 2 && regSpf) {
+    bool bad = false;
+#pragma unroll
+    for (int k = 0; k < NPL; ++k) {
+#pragma unroll
+      for (int j = 0; j < MAXD; ++j) {
+        bad |= ((actMask[k] >> lane) & 1ull) && ea[k][j] > P0 && (posS >> 6) == uint32_t(k);
+      }
+    }
+    regSpf = __builtin_amdgcn_ballot_w64(bad) == 0ull;
+  }
   wave_sync();  // posOf scratch is overwritten below
 
   // ---- SPF: pull rounds to the fixpoint -------------------------------------
@@ -390,7 +431,77 @@ __global__ __launch_bounds__(64 * UPB) void spf_route_wave_kernel(
   // Wide form (paths < 2^31 - 1, host-guaranteed): 64-bit {dist, nh} words,
   // tie test by equality.
   const bool narrow = uint64_t(wmax) * (N > 0 ? N - 1 : 0) < 0x7FFFFFull;
-  if (narrow) {
+  if (narrow && regSpf) {
+    // Words as in the narrow form below, held in registers: slot k's lane
+    // gathers its neighbours' words from the other slot's register with
+    // ds_bpermute (no LDS traffic, no bank conflicts). Per edge a lane
+    // address and an addend: unusable edges add kUnr (saturating, so the
+    // candidate is >= kUnr and never below a reachable word); edges into
+    // the source read the source lane (word 0, kept there by the active
+    // mask) and add w << 8 | the source's link-slot bit.
+    constexpr uint32_t kUnr = 0x80000000u;
+    uint32_t ba[NPL][MAXD], wb[NPL][MAXD], cur[NPL];
+    bool act[NPL];
+#pragma unroll
+    for (int k = 0; k < NPL; ++k) {
+      act[k] = (actMask[k] >> lane) & 1ull;
+      cur[k] = vk[k] == s ? 0u : kUnr;
+#pragma unroll
+      for (int j = 0; j < MAXD; ++j) {
+        const uint32_t e = ea[k][j];
+        ba[k][j] = (e < P0 ? (e & 63u) : e == P0 ? uint32_t(lane) : (posS & 63u)) << 2;
+        wb[k][j] = e == P0 ? kUnr
+                           : (ew[k][j] << 8) | (e > P0 ? 1u << (e - P0 - 1) : 0u);
+      }
+    }
+    auto relax = [&](int k, uint32_t other) {
+      uint32_t cand[MAXD];
+      uint32_t best = kUnr;
+#pragma unroll
+      for (int j = 0; j < MAXD; ++j) {
+        const uint32_t x = uint32_t(__builtin_amdgcn_ds_bpermute(int(ba[k][j]), int(other)));
+        cand[j] = __builtin_elementwise_add_sat(x, wb[k][j]);
+        best = cand[j] < best ? cand[j] : best;
+      }
+      const uint32_t hiB = best | 0xFFu;
+      uint32_t word = best & kUnr;
+#pragma unroll
+      for (int j = 0; j < MAXD; ++j) word |= cand[j] <= hiB ? cand[j] : 0u;
+      return act[k] ? word : cur[k];
+    };
+    if (NPL == 1) {
+      for (;;) {
+        const uint32_t w = relax(0, cur[0]);
+        const bool ch = __builtin_amdgcn_ballot_w64(w != cur[0]) != 0ull;
+        cur[0] = w;
+#ifdef OGS_STAMPS
+        ++rounds;
+#endif
+        if (!ch) break;
+      }
+    } else {
+      // Gauss-Seidel over the two slots; after the first sub-step, one
+      // that changes nothing means the other slot's inputs are unchanged
+      for (int step = 0;; ++step) {
+        const uint32_t w0 = relax(0, cur[NPL - 1]);
+        const bool ch0 = __builtin_amdgcn_ballot_w64(w0 != cur[0]) != 0ull;
+        cur[0] = w0;
+#ifdef OGS_STAMPS
+        ++rounds;
+#endif
+        if (step > 0 && !ch0) break;
+        const uint32_t w1 = relax(NPL - 1, cur[0]);
+        const bool ch1 = __builtin_amdgcn_ballot_w64(w1 != cur[NPL - 1]) != 0ull;
+        cur[NPL - 1] = w1;
+        if (!ch1) break;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < NPL; ++k) {
+      dcur[k] = cur[k] >= kUnr ? kInf : cur[k] >> 8;
+      ncur[k] = cur[k] >= kUnr ? 0u : cur[k] & 0xFFu;
+    }
+  } else if (narrow) {
     constexpr uint32_t kUnr = 0x80000000u;
     uint32_t* d32 = reinterpret_cast<uint32_t*>(base + L.dn32);
     uint32_t ws[NPL][MAXD], cur[NPL];
@@ -547,7 +658,38 @@ __global__ __launch_bounds__(64 * UPB) void spf_route_wave_kernel(
   lp.adv_min_nh = pt.adv_min_nh;  // HBM, absolute advertisement index
   lp.pfx_flags = lPfxFlags;
   const uint32_t Sp = pt.max_prefixes;
-  for (uint32_t p = lane; p < P; p += 64) {
+  if (ident) {
+    // all of the lane's prefixes first (loads), then the stores
+    uint32_t meta[KP], metric[KP], mask[KP];
+#pragma unroll
+    for (int k = 0; k < KP; ++k) {
+      const uint32_t p = uint32_t(k * 64 + lane);
+      const uint8_t pf = sPf.v[k];
+      if ((pf & OGS_PFX_V4) && !cfg.enableV4 && !cfg.v4OverV6) {
+        meta[k] = OGS_REASON_V4_DISABLED << OGS_ROUTE_REASON_SHIFT;  // route_one's gate
+        metric[k] = kInf;
+        mask[k] = 0u;
+      } else {
+        const int64_t minNh = (p < P && (pf & OGS_PFX_HAS_MIN_NH)) ? pt.adv_min_nh[a0 + p]
+                                                                  : INT64_MIN;
+        route_single(p < P ? sNode.v[k] : OGS_NODE_NONE, minNh, s, lflags, dn, meta[k],
+                     metric[k], mask[k]);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < KP; ++k) {
+      const uint32_t p = uint32_t(k * 64 + lane);
+      if (p >= P) continue;
+      const size_t o = size_t(uidx) * Sp + p;
+      if (out.meta) __builtin_nontemporal_store(meta[k], out.meta + o);
+      if (out.metric) __builtin_nontemporal_store(metric[k], static_cast<uint32_t*>(out.metric) + o);
+      if (out.sel) {
+        __builtin_nontemporal_store((meta[k] & OGS_ROUTE_SELECTED) ? 1u : 0u, out.sel + o);
+      }
+      if (out.mask) __builtin_nontemporal_store(mask[k], out.mask + o);
+    }
+  }
+  for (uint32_t p = ident ? P : lane; p < P; p += 64) {
     uint32_t meta, metric, mask, selBits;
     const uint32_t b0 = lAdvOff[p] - a0, b1 = lAdvOff[p + 1] - a0;
     const uint8_t pf = lPfxFlags[p];
@@ -593,6 +735,10 @@ __global__ __launch_bounds__(64 * UPB) void spf_route_wave_kernel(
 int g_waveWgLds = 0;
 // "wave_upb" option: units (wavefronts) per workgroup, 4, 8 or 16
 int g_waveUpb = 4;
+// "wave_opt" option: OGS_WAVE_OPT_* bits (A/B of the register paths); the
+// ds_bpermute SPF measured no faster than the LDS words (latency-bound
+// rounds), so only the register route path is on by default
+int g_waveOpt = OGS_WAVE_OPT_REG_ROUTES;
 
 template <int NPL, int MAXD, int UPB>
 hipError_t launch_wave_upb(const ogs_graph& g, const ogs_prefix_table& pt,
@@ -610,7 +756,7 @@ hipError_t launch_wave_upb(const ogs_graph& g, const ogs_prefix_table& pt,
     if (e != hipSuccess) return e;
   }
   hipLaunchKernelGGL(k, dim3(grid), dim3(64 * UPB), bytes, stream, g, pt,
-                     hasPrefixes, units, nUnits, flags, out, lds, maxA);
+                     hasPrefixes, units, nUnits, flags, out, lds, maxA, uint32_t(g_waveOpt));
   return hipGetLastError();
 }
 

@@ -16,13 +16,18 @@ def main():
     c = C2()
     pt = c.table()
     o = c.outputs()
-    for name, uw, order, lds, use_b in variants("1,1p"):
-        apply(c, uw, lds, use_b)
+    runs = [(v, o) for v in variants("1,1p")
+            for o in [int(x) for x in os.environ.get("WAVE_OPTS", "3").split(",")]]
+    for (name, uw, order, lds, use_b, upb), wopt in runs:
+        apply(c, uw, lds, use_b, upb)
+        c.capi.check(c.lib, c.lib.ogs_set_option(b"wave_opt", wopt), "wave_opt")
+        name = f"{name}/opt{wopt}"
         g = c.graph(order)
         for _ in range(3):
             c.run(g, pt, o)
         torch.cuda.synchronize()
         raw = o[5].cpu().numpy().reshape(c.U, c.Sp)[:, :7].astype(np.int64)
+        raw = raw[raw[:, 0] > 16]  # rows of wave-first units (others: sel bits)
         st = raw[:, :5].astype(np.float64)
         names = ["stage", "spf", "routes", "rounds", "desc"]
         rt0 = raw[:, 5] - raw[:, 5].min()  # 100 MHz realtime, 10 ns ticks
