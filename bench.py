@@ -460,6 +460,9 @@ def run_c4(args, torch, dist, rank, world, local_rank):
     lo, hi = shard.block_range(C4_VARIANTS, rank, world)
     vr = openr_amd.decision.VariantRunner(True, False)
     vr.setup("wan", C4_OPTS, C4_SOURCE, C4_VARIANTS, C4_SEED, C4_DUAL_PERMILLE, lo, hi)
+    # repair the base SPF below the failed tight links, write changed records
+    # only (OGS_F_INCREMENTAL | OGS_F_CHANGED_ONLY; --opt-free A/B: C4_MODE=0)
+    vr.set_mode(int(os.environ.get("C4_MODE", "2")))
     sh = vr.shape()
     stream = torch.cuda.current_stream(dev)
     sptr = stream.cuda_stream
@@ -521,7 +524,18 @@ def run_c4(args, torch, dist, rank, world, local_rank):
     N, E, P = sh["nodes"], sh["directed_edges"], sh["prefixes"]
     T, W = sh["advertisements"], sh["nh_words"]
     inputs = 4 * (N + 1) + 8 * E + (N + 7) // 8 + 16 * T
-    bpu = inputs / C4_VARIANTS + 4 * N + 4 * W * N + P * (4 * W + 8) + 16 + P / 8
+    mode = vr.mode()
+    if mode == 2:
+        # repair: per variant the failed-edge list (16 B),
+        # the changed bitmap (P/8) and counts (8), its changed records
+        # (prefix-indexed meta + metric + W mask words), and -- for variants
+        # that change routes, i.e. whose failed links were tight -- the base
+        # SPF words it starts from (8 B/node)
+        repaired = sum(1 for c in ch if c[0] or c[1])
+        bpu = (inputs / C4_VARIANTS + 16 + P / 8 + 8 + changed * (8 + 4 * W) / U +
+               8 * N * repaired / U)
+    else:
+        bpu = inputs / C4_VARIANTS + 4 * N + 4 * W * N + P * (4 * W + 8) + 16 + P / 8
     achieved = bpu * U / (kernel_ms * 1e-3) / 1e9
     value = total_units * steps / tmax
     line = {
@@ -551,8 +565,11 @@ def run_c4(args, torch, dist, rank, world, local_rank):
     }
     log(f"c4 timed: {kernel_ms:.4f} ms/sweep, digest {job_digest:016x}")
     golden_check(line, "c4", job_digest, GOLDEN.get("c4"))
+    line["config"]["mode"] = {0: "full SPF per variant", 1: "base-SPF repair",
+                              2: "base-SPF repair, changed records only"}[mode]
     if world == 1:
-        set_traffic(line, "c4", "spf_frontier_kernel<1, true, true, true")
+        set_traffic(line, "c4", "spf_variant_repair_kernel<true>" if mode == 2
+                    else "spf_frontier_kernel<1, true, true, true")
         if not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline_c4()
     return line

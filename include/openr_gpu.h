@@ -99,6 +99,15 @@ extern "C" {
  * the sign-extended i32, u64 sums wrap, LinkState.cpp:77-78, 789). Needs
  * OGS_F_WIDE_METRIC; one wavefront per unit, one extraction per step. */
 #define OGS_F_EXACT_ORDER 0x20u
+/* ogs_spf_routes_variants only: repair the base unit's SPF (diff->base_dist /
+ * base_nh) instead of recomputing it -- only nodes below a failed link that
+ * was tight in the base shortest-path DAG are re-relaxed; next-hop sets of
+ * one word (nh_words 1), else the full recompute runs. */
+#define OGS_F_INCREMENTAL 0x40u
+/* ogs_spf_routes_variants only (with a diff): write only the records of
+ * changed routes (bit set in diff->changed); the other records of out->meta
+ * / metric / mask / sel are left as they were. Needs OGS_F_INCREMENTAL. */
+#define OGS_F_CHANGED_ONLY 0x80u
 
 /* CSR of T topologies. */
 typedef struct ogs_graph {
@@ -361,6 +370,18 @@ typedef struct ogs_route_diff {
                                   deleted (zeroed by the call)          */
   uint32_t* counts;            /* [n_units * 2] {routes to update,
                                   routes to delete}                     */
+  const uint32_t* base_dist;   /* [S_n] base unit's distances and       */
+  const uint32_t* base_nh;     /* [S_n] next-hop sets (ogs_spf_out of its
+                                  ogs_spf_routes): OGS_F_INCREMENTAL    */
+  /* [2 * A] optional: equality classes of the best entry a route would
+   * carry -- adv_class[2a] for advertisement a as is, [2a + 1] with the
+   * hard-drain override (drain_metric = 1); two routes' best entries are
+   * equal (PrefixEntry ==, RibEntry.h:81-87) iff their classes are equal
+   * (class = first position in the prefix's list [entries as is, entries
+   * drained] holding an equal entry). NULL: compared by advertisement index
+   * and DRAINED bit (a different but equal advertiser then counts as a
+   * change). */
+  const uint32_t* adv_class;
 } ogs_route_diff;
 
 /* Batched SPF + RouteDb of link-failure variants with an optional route

@@ -738,6 +738,14 @@ class LinkFailureSweep {
   // every variant + diff, one launch; records = false keeps only the diff
   // (bitmap + counts) -- fetchUpdates() then needs records, so it re-runs
   void launch(void* stream = nullptr, bool records = true);
+  // how launch() computes a variant: kFull re-runs its SPF from scratch,
+  // kRepair repairs the base SPF below the failed tight links
+  // (OGS_F_INCREMENTAL, every record written), kChangedOnly repairs and
+  // writes only changed records and no per-variant SPF state
+  // (OGS_F_CHANGED_ONLY: routeUpdate / counts / changedPrefixes only)
+  enum Mode { kFull = 0, kRepair = 1, kChangedOnly = 2 };
+  void setMode(Mode m) { mode_ = m; }
+  Mode mode() const { return mode_; }
   // counts -> offsets -> device gather of the changed records -> host
   void fetchUpdates(void* stream = nullptr);
   // bitmap + counts, and every variant's full records when the launch wrote
@@ -766,11 +774,12 @@ class LinkFailureSweep {
   HostBatch hb_;
   int W_{1};
   size_t words_{1}, Sp_{1};
-  bool baseRun_{false}, recordsRun_{false};
+  bool baseRun_{false}, recordsRun_{false}, changedOnlyRun_{false};
+  Mode mode_{kRepair};
   std::vector<uint32_t> dead_;
   DeviceBuffer dNodeBase_, dDesc_, dRow_, dEdges_, dEdgeSrc_, dFlags_, dPfxBase_,
       dAdvOff_, dAdvNode_, dAdvMetrics_, dAdvMinNh_, dPfxFlags_, dUnits_,
-      dBaseUnit_, dDead_;
+      dBaseUnit_, dDead_, dAdvClass_;
   DeviceBuffer bDist_, bNh_, bMeta_, bMetric_, bMask_, bSel_;
   DeviceBuffer dDist_, dNh_, dMeta_, dMetric_, dMask_, dSel_, dChanged_, dCounts_;
   DeviceBuffer dOffsets_, cPrefix_, cMeta_, cMetric_, cMask_;

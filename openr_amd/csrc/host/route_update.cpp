@@ -96,6 +96,38 @@ LinkFailureSweep::LinkFailureSweep(
   dUnits_.upload(units.data(), units.size());
   dBaseUnit_.upload(&base, 1);
   dDead_.upload(dead_.data(), dead_.size());
+  // best-entry equality classes for the diff (ogs_route_diff.adv_class):
+  // per prefix, the list [entries as is, entries with the drain override]
+  // of materialised best entries (weight cleared, RibEntry.h:77), each
+  // numbered by the first equal one
+  {
+    std::vector<uint32_t> cls(std::max<size_t>(2 * table_.advEntry.size(), 1), 0);
+    for (size_t p = 0; p + 1 < table_.advOff.size(); ++p) {
+      const uint32_t a0 = table_.advOff[p], k = table_.advOff[p + 1] - a0;
+      std::vector<PrefixEntry> eff;
+      eff.reserve(2 * k);
+      for (int drained = 0; drained < 2; ++drained) {
+        for (uint32_t i = 0; i < k; ++i) {
+          PrefixEntry e = *table_.advEntry[a0 + i];
+          e.weight = std::nullopt;
+          if (drained) e.metrics.drain_metric = 1;
+          eff.push_back(std::move(e));
+        }
+      }
+      for (uint32_t j = 0; j < 2 * k; ++j) {
+        uint32_t c = j;
+        for (uint32_t i = 0; i < j; ++i) {
+          if (eff[i] == eff[j]) {
+            c = i;
+            break;
+          }
+        }
+        const uint32_t i = j % k, drained = j / k;
+        cls[2 * (a0 + i) + drained] = c;
+      }
+    }
+    dAdvClass_.upload(cls.data(), cls.size());
+  }
   bDist_.resize(Sn * 4);
   bNh_.resize(W_ * Sn * 4);
   for (auto* b : {&bMeta_, &bMetric_, &bSel_}) b->resize(Sp_ * 4);
@@ -160,18 +192,25 @@ void LinkFailureSweep::launch(void* stream, bool records) {
   counts_.clear();
   ogs_graph g = graph();
   ogs_prefix_table pt = table();
+  const bool changedOnly = mode_ == kChangedOnly && W_ == 1;
   ogs_spf_out out{};
   if (records) {
     out = ogs_spf_out{dDist_.get(), dNh_.as<uint32_t>(), dMeta_.as<uint32_t>(),
                       dMetric_.get(), dMask_.as<uint32_t>(), dSel_.as<uint32_t>()};
+    if (changedOnly) out.dist = out.nh = nullptr;  // records of changed routes only
   }
   ogs_unit_mods mods{dDead_.as<uint32_t>(), kDeadMax};
   ogs_route_diff diff{bMeta_.as<uint32_t>(), bMetric_.as<uint32_t>(), bMask_.as<uint32_t>(),
-                      dChanged_.as<uint32_t>(), dCounts_.as<uint32_t>()};
+                      dChanged_.as<uint32_t>(), dCounts_.as<uint32_t>(),
+                      bDist_.as<uint32_t>(), bNh_.as<uint32_t>(), dAdvClass_.as<uint32_t>()};
+  uint32_t fl = flags();
+  if (mode_ != kFull) fl |= OGS_F_INCREMENTAL;
+  if (changedOnly) fl |= OGS_F_CHANGED_ONLY;
   ogsCheck(ogs_spf_routes_variants(&g, &pt, dUnits_.as<ogs_unit>(), int32_t(numVariants()),
-                                   &mods, &diff, flags(), W_, &out, stream),
+                                   &mods, &diff, fl, W_, &out, stream),
            "ogs_spf_routes_variants");
   recordsRun_ = records;
+  changedOnlyRun_ = records && changedOnly;
 }
 
 void LinkFailureSweep::fetchUpdates(void* stream) {
@@ -227,7 +266,7 @@ void LinkFailureSweep::fetchUpdates(void* stream) {
 void LinkFailureSweep::fetchRecords(void* stream) {
   // the diff (bitmap + counts) always; the records when the launch wrote them
   const size_t U = numVariants();
-  const size_t R = recordsRun_ ? U : 0;
+  const size_t R = (recordsRun_ && !changedOnlyRun_) ? U : 0;
   counts_.resize(U * 2);
   changed_.resize(U * words_);
   meta_.resize(R * Sp_);

@@ -390,6 +390,12 @@ int ogs_spf_routes_variants(const ogs_graph* graph,
                !diff->changed || !diff->counts)) {
     return fail(OGS_E_INVALID, "diff arrays are NULL");
   }
+  if ((flags & OGS_F_INCREMENTAL) && (!mods || !diff || !diff->base_dist || !diff->base_nh)) {
+    return fail(OGS_E_INVALID, "OGS_F_INCREMENTAL needs mods and diff with base_dist / base_nh");
+  }
+  if ((flags & OGS_F_CHANGED_ONLY) && (!(flags & OGS_F_INCREMENTAL) || nh_words != 1)) {
+    return fail(OGS_E_INVALID, "OGS_F_CHANGED_ONLY needs OGS_F_INCREMENTAL and nh_words 1");
+  }
   if (graph->max_nodes <= 0 || uint32_t(graph->max_nodes) > OGS_MAX_NODES_PER_TOPO) {
     return fail(OGS_E_UNSUPPORTED, "max_nodes outside (0, 2^21]");
   }

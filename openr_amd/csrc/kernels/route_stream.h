@@ -66,7 +66,16 @@ struct DiffCtx {
   const uint32_t* bMask;    // [W][Sp]
   uint32_t* changed;        // this unit's bitmap row (zeroed)
   uint32_t* counts;         // LDS {update, delete} accumulators
+  const uint32_t* advOff;   // prefix p's first advertisement (pt.adv_off + p0)
+  const uint32_t* advClass; // ogs_route_diff.adv_class or NULL
 };
+
+// Best-entry class of a valid route (ogs_route_diff.adv_class): the
+// advertisement's entry as is, or with the hard-drain override.
+__device__ __forceinline__ uint32_t best_class(const DiffCtx& d, uint32_t p, uint32_t meta) {
+  const uint32_t a = d.advOff[p] + (meta >> OGS_ROUTE_BEST_SHIFT);
+  return d.advClass[2u * a + ((meta & OGS_ROUTE_DRAINED) ? 1u : 0u)];
+}
 
 template <int W>
 __device__ __forceinline__ bool route_changed(const Rec<W>& r, const DiffCtx& d,
@@ -78,7 +87,11 @@ __device__ __forceinline__ bool route_changed(const Rec<W>& r, const DiffCtx& d,
   const bool va = r.meta & OGS_ROUTE_VALID, vb = bm & OGS_ROUTE_VALID;
   bool ch = va != vb;
   if (va && vb) {
-    ch = ((r.meta ^ bm) & kEq) != 0u || r.metric != d.bMetric[p];
+    // bestPrefixEntry by value (RibEntry.h:81-87) when classes are given
+    ch = (d.advClass ? (((r.meta ^ bm) & OGS_ROUTE_LOCAL) != 0u ||
+                        best_class(d, p, r.meta) != best_class(d, p, bm))
+                     : ((r.meta ^ bm) & kEq) != 0u) ||
+        r.metric != d.bMetric[p];
 #pragma unroll
     for (int w = 0; w < W; ++w) ch |= r.mask[w] != d.bMask[size_t(w) * Sp + p];
   }

@@ -434,35 +434,17 @@ __device__ __forceinline__ void queue_spf(
 // that improves a node also claims its push for round r+1, so there is no
 // separate stamp array (4 B/node less LDS) and no second atomic per update.
 // The stamp bits are cleared when the SPF ends.
-template <bool MODS, bool FOLD = false>
-__device__ __forceinline__ void queue_spf_packed(
-    uint32_t N, uint32_t s, const uint64_t* __restrict__ edges,
-    const uint32_t* __restrict__ gRow, uint32_t e0,
-    const uint8_t* __restrict__ nflags, bool hop, uint64_t* dn, uint32_t* stamp,
-    uint16_t* q0, uint16_t* q1, uint32_t* qcnt, uint32_t* ninfo, uint64_t* tp,
-    const DeadEdges& dead) {
-  constexpr uint32_t kInf = 0xFFFFFFFFu;
+// Rounds of the packed queue SPF from the current list state: round r's
+// list is buffer r & 1 with count slot r % 3 holding n entries (stamps
+// already claim them). Returns the round after the last non-empty one.
+template <bool MODS, bool FOLD>
+__device__ __forceinline__ uint32_t packed_rounds(
+    uint32_t s, const uint64_t* __restrict__ edges, const uint32_t* __restrict__ gRow,
+    uint32_t e0, const uint8_t* __restrict__ nflags, bool hop, uint64_t* dn,
+    uint32_t* stamp, uint16_t* q0, uint16_t* q1, uint32_t* qcnt, const uint32_t* ninfo,
+    const DeadEdges& dead, uint32_t r, uint32_t n) {
   constexpr uint32_t kDrained = 0x80000000u;
   const int tid = threadIdx.x;
-  for (uint32_t v = tid; v < N; v += kBlock) {
-    dn[v] = (v == s) ? 0ull : uint64_t(kInf);
-    if constexpr (!FOLD) stamp[v] = 0u;
-  }
-  for (uint32_t v = tid; ninfo && v <= N; v += kBlock) {  // nullptr: CSR reads
-    ninfo[v] = (gRow[v] - e0) |
-        ((v < N && (nflags[v] & OGS_NODE_OVERLOADED)) ? kDrained : 0u);
-  }
-  if (tid == 0) {
-    q1[0] = uint16_t(s);
-    qcnt[0] = 0u;
-    qcnt[1] = 1u;
-    qcnt[2] = 0u;
-  }
-  __syncthreads();
-#ifdef OGS_STAMPS
-  tp[0] = __builtin_amdgcn_s_memtime();
-#endif
-  uint32_t r = 1, n = 1;
   for (; n; ++r) {
     if (tid == 0) qcnt[(r + 2) % 3] = 0u;
     const uint16_t* cur = (r & 1) ? q1 : q0;
@@ -515,6 +497,39 @@ __device__ __forceinline__ void queue_spf_packed(
     __syncthreads();
     n = qcnt[(r + 1) % 3];
   }
+  return r;
+}
+
+template <bool MODS, bool FOLD = false>
+__device__ __forceinline__ void queue_spf_packed(
+    uint32_t N, uint32_t s, const uint64_t* __restrict__ edges,
+    const uint32_t* __restrict__ gRow, uint32_t e0,
+    const uint8_t* __restrict__ nflags, bool hop, uint64_t* dn, uint32_t* stamp,
+    uint16_t* q0, uint16_t* q1, uint32_t* qcnt, uint32_t* ninfo, uint64_t* tp,
+    const DeadEdges& dead) {
+  constexpr uint32_t kInf = 0xFFFFFFFFu;
+  constexpr uint32_t kDrained = 0x80000000u;
+  const int tid = threadIdx.x;
+  for (uint32_t v = tid; v < N; v += kBlock) {
+    dn[v] = (v == s) ? 0ull : uint64_t(kInf);
+    if constexpr (!FOLD) stamp[v] = 0u;
+  }
+  for (uint32_t v = tid; ninfo && v <= N; v += kBlock) {  // nullptr: CSR reads
+    ninfo[v] = (gRow[v] - e0) |
+        ((v < N && (nflags[v] & OGS_NODE_OVERLOADED)) ? kDrained : 0u);
+  }
+  if (tid == 0) {
+    q1[0] = uint16_t(s);
+    qcnt[0] = 0u;
+    qcnt[1] = 1u;
+    qcnt[2] = 0u;
+  }
+  __syncthreads();
+#ifdef OGS_STAMPS
+  tp[0] = __builtin_amdgcn_s_memtime();
+#endif
+  const uint32_t r = packed_rounds<MODS, FOLD>(s, edges, gRow, e0, nflags, hop, dn, stamp,
+                                               q0, q1, qcnt, ninfo, dead, 1u, 1u);
   if constexpr (FOLD) {  // the plain packed form for everything downstream
     for (uint32_t v = tid; v < N; v += kBlock) dn[v] &= 0x0000FFFFFFFFFFFFull;
     __syncthreads();
@@ -523,6 +538,8 @@ __device__ __forceinline__ void queue_spf_packed(
   tp[1] = tp[2] = __builtin_amdgcn_s_memtime();
   tp[3] = r;
   tp[4] = 0;
+#else
+  (void)r;
 #endif
 }
 
@@ -645,7 +662,8 @@ __global__ __launch_bounds__(kBlock) void spf_frontier_kernel(
       __syncthreads();
     }
     const DiffCtx dc{diff.base_meta, diff.base_metric, diff.base_mask,
-                     diff.changed + size_t(u0) * ((Sp + 31u) / 32u), cnt};
+                     diff.changed + size_t(u0) * ((Sp + 31u) / 32u), cnt,
+                     pt.adv_off + p0, diff.adv_class};
     auto rec = [&](uint32_t v, Rec<W>& r) {
       r.meta = rMeta[v];
       r.metric = (v == s) ? kInf : dOf(v);
@@ -836,6 +854,234 @@ hipError_t launch_frontier_routes(const ogs_graph& g, const ogs_prefix_table& pt
   }
 }
 
+// ---- incremental link-failure variants (OGS_F_INCREMENTAL) -----------------
+// A failed link changes nothing unless one of its directed edges is tight in
+// the base SPF (base dist(u) + w == base dist(v), u relaxing): removing
+// edges only lengthens paths, so a node whose base shortest-path DAG does
+// not reach it through a failed tight edge keeps its distance, its tight
+// predecessors and (by induction) its next-hop set. The variant's SPF is
+// the base state with A = the failed tight edges' heads and their
+// descendants in that DAG reset to unreachable and re-relaxed from A's
+// boundary (packed queue rounds, same fixpoint as a full run: the boundary
+// pushes its final words, A's nodes converge as in queue_spf_packed). Only
+// prefixes with an advertiser in A can change route (a route depends on its
+// advertisers' dist / next-hop sets: SpfSolver.cpp:160-311).
+// LDS: dn64 [Sn] | stamp [Sn] | two u16 node lists [Sn] | A bitset.
+uint32_t repair_lds_bytes(uint32_t Sn) {
+  return 8u * Sn + 4u * ((Sn + 3u) & ~3u) + 2u * 2u * ((Sn + 1u) & ~1u) +
+      4u * ((Sn + 31u) / 32u) + 16u;
+}
+
+template <bool CHANGED_ONLY>
+__global__ __launch_bounds__(kBlock) void spf_variant_repair_kernel(
+    ogs_graph g, ogs_prefix_table pt, const uint32_t* __restrict__ key,
+    const ogs_unit* __restrict__ units, uint32_t flags, uint32_t* __restrict__ oDist,
+    uint32_t* __restrict__ oNh, ogs_spf_out out, ogs_unit_mods mods,
+    ogs_route_diff diff) {
+  constexpr uint32_t kInf = 0xFFFFFFFFu;
+  const int tid = threadIdx.x;
+  const uint32_t u0 = blockIdx.x;
+  const ogs_unit unit = units[u0];
+  const uint32_t s = unit.src;
+  const uint32_t nb = g.node_base[unit.topo];
+  const uint32_t N = g.node_base[unit.topo + 1] - nb;
+  const uint32_t* __restrict__ gRow = g.row_ptr + nb;
+  const uint32_t e0 = gRow[0];
+  const uint64_t* __restrict__ edges = g.edges + e0;
+  const uint8_t* __restrict__ nflags = g.node_flags + nb;
+  const uint32_t Sn = uint32_t(g.max_nodes);
+  const bool hop = (flags & OGS_F_HOP_METRIC) != 0;
+  const uint32_t* __restrict__ bD = diff.base_dist;
+  const uint32_t* __restrict__ bN = diff.base_nh;
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint64_t* dn = reinterpret_cast<uint64_t*>(smem);                      // [Sn]
+  uint32_t* stamp = reinterpret_cast<uint32_t*>(dn + Sn);                // [Sn]
+  uint16_t* q0 = reinterpret_cast<uint16_t*>(stamp + ((Sn + 3u) & ~3u));  // [Sn]
+  uint16_t* q1 = q0 + ((Sn + 1u) & ~1u);                                 // [Sn]
+  uint32_t* inA = reinterpret_cast<uint32_t*>(q1 + ((Sn + 1u) & ~1u));   // [Sn/32]
+  __shared__ uint32_t qcnt[3], cnt[2];
+  auto isA = [&](uint32_t v) { return (inA[v >> 5] >> (v & 31u)) & 1u; };
+  auto relaxes = [&](uint32_t v) { return v == s || !(nflags[v] & OGS_NODE_OVERLOADED); };
+
+  DeadEdges dead;
+#pragma unroll
+  for (int k = 0; k < kMaxDead; ++k) {
+    dead.e[k] = k < mods.dead_per_unit ? mods.dead_edges[size_t(u0) * mods.dead_per_unit + k]
+                                       : OGS_NODE_NONE;
+  }
+  for (uint32_t w = tid; w < (N + 31u) / 32u; w += kBlock) inA[w] = 0u;
+  if (tid < 3) qcnt[tid] = 0u;
+  if (tid < 2) cnt[tid] = 0u;
+  __syncthreads();
+  // ---- seeds: heads of the failed edges that are tight in the base --------
+  if (tid < kMaxDead && dead.e[tid] != OGS_NODE_NONE) {
+    const uint32_t e = dead.e[tid];
+    const uint32_t u = g.edge_src[e0 + e];
+    const uint64_t x = edges[e];
+    const uint32_t lo = static_cast<uint32_t>(x);
+    const uint32_t v = edge_dst(lo);
+    const uint32_t w = hop ? 1u : static_cast<uint32_t>(x >> 32);
+    if (!(lo & OGS_EDGE_DOWN) && relaxes(u) && bD[u] != kInf && bD[u] + w == bD[v]) {
+      if (!(atomicOr(&inA[v >> 5], 1u << (v & 31u)) & (1u << (v & 31u)))) {
+        q1[atomicAdd(&qcnt[1], 1u)] = uint16_t(v);
+      }
+    }
+  }
+  __syncthreads();
+  uint32_t n = qcnt[1];
+  if (CHANGED_ONLY && n == 0) {  // no failed link on a shortest path: no change
+    if (tid < 2) diff.counts[size_t(u0) * 2 + tid] = 0u;
+    if (oDist || oNh) {
+      for (uint32_t v = tid; v < N; v += kBlock) {
+        if (oDist) oDist[size_t(u0) * Sn + v] = bD[v];
+        if (oNh) oNh[size_t(u0) * Sn + v] = bN[v];
+      }
+    }
+    return;
+  }
+  for (uint32_t v = tid; v < N; v += kBlock) {
+    dn[v] = uint64_t(bD[v]) | (uint64_t(bN[v]) << 32);
+    stamp[v] = 0u;
+  }
+  __syncthreads();
+  // ---- A: the seeds' descendants in the base tight DAG (list rounds) ------
+  for (uint32_t r = 1; n; ++r) {
+    if (tid == 0) qcnt[(r + 2) % 3] = 0u;
+    const uint16_t* cur = (r & 1) ? q1 : q0;
+    uint16_t* nxt = (r & 1) ? q0 : q1;
+    for (uint32_t i = tid; i < n; i += kBlock) {
+      const uint32_t x = cur[i];
+      if (!relaxes(x)) continue;
+      const uint32_t dx = static_cast<uint32_t>(dn[x]);
+      const uint32_t b = gRow[x] - e0;
+      for_row(edges, b, gRow[x + 1] - e0 - b, [&](uint32_t, uint64_t y) {
+        const uint32_t lo = static_cast<uint32_t>(y);
+        if (lo & OGS_EDGE_DOWN) return;
+        const uint32_t t = edge_dst(lo);
+        if (dx + (hop ? 1u : static_cast<uint32_t>(y >> 32)) != static_cast<uint32_t>(dn[t])) {
+          return;
+        }
+        if (!(atomicOr(&inA[t >> 5], 1u << (t & 31u)) & (1u << (t & 31u)))) {
+          nxt[atomicAdd(&qcnt[(r + 1) % 3], 1u)] = uint16_t(t);
+        }
+      });
+    }
+    __syncthreads();
+    n = qcnt[(r + 1) % 3];
+  }
+  // ---- reset A, seed its boundary, re-relax --------------------------------
+  __syncthreads();  // every thread has read the last (zero) count
+  if (tid < 3) qcnt[tid] = 0u;
+  for (uint32_t v = tid; v < N; v += kBlock) {
+    if (isA(v)) dn[v] = uint64_t(kInf);
+  }
+  __syncthreads();
+  for (uint32_t x = tid; x < N; x += kBlock) {
+    if (!isA(x)) continue;
+    const uint32_t b = gRow[x] - e0, m = gRow[x + 1] - e0 - b;
+    for (uint32_t j = 0; j < m; ++j) {  // links are two-way: out-neighbours = in-neighbours
+      const uint32_t p = edge_dst(static_cast<uint32_t>(edges[b + j]));
+      if (isA(p) || !relaxes(p) || static_cast<uint32_t>(dn[p]) == kInf) continue;
+      if (atomicMax(&stamp[p], 1u) < 1u) q1[atomicAdd(&qcnt[1], 1u)] = uint16_t(p);
+    }
+  }
+  __syncthreads();
+  packed_rounds<true, false>(s, edges, gRow, e0, nflags, hop, dn, stamp, q0, q1, qcnt,
+                             nullptr, dead, 1u, qcnt[1]);
+  __syncthreads();
+  if (oDist || oNh) {
+    for (uint32_t v = tid; v < N; v += kBlock) {
+      if (oDist) oDist[size_t(u0) * Sn + v] = static_cast<uint32_t>(dn[v]);
+      if (oNh) oNh[size_t(u0) * Sn + v] = static_cast<uint32_t>(dn[v] >> 32);
+    }
+  }
+
+  // ---- routes --------------------------------------------------------------
+  const uint32_t Sp = uint32_t(pt.max_prefixes);
+  const uint32_t p0 = pt.pfx_base[unit.topo];
+  const uint32_t P = pt.pfx_base[unit.topo + 1] - p0;
+  const RouteCfg cfg{(flags & OGS_F_ENABLE_V4) != 0, (flags & OGS_F_V4_OVER_V6) != 0,
+                     (flags & OGS_F_BEST_ROUTE_SELECTION) != 0};
+  const DiffCtx dc{diff.base_meta, diff.base_metric, diff.base_mask,
+                   diff.changed + size_t(u0) * ((Sp + 31u) / 32u), cnt, pt.adv_off + p0,
+                   diff.adv_class};
+  const uint32_t* tkey = key + size_t(unit.topo) * Sp;
+  auto nodeRec = [&](uint32_t v, Rec<1>& r) {
+    const uint64_t x = dn[v];
+    const uint32_t d = static_cast<uint32_t>(x), nv = static_cast<uint32_t>(x >> 32);
+    r.meta = node_route_meta(v, s, d != kInf, __popc(nv), nflags[v]);
+    r.metric = (v == s) ? kInf : d;
+    r.mask[0] = nv;
+  };
+  if constexpr (!CHANGED_ONLY) {
+    stream_routes<1, true>(pt, tkey, p0, P, Sp, u0, s, nflags, PackedView{dn}, cfg, out,
+                           nodeRec, &dc);
+  } else {
+    const bool v4Gated = !cfg.enableV4 && !cfg.v4OverV6;
+    uint32_t upd = 0, del = 0;
+    for (uint32_t p = tid; p < P; p += kBlock) {
+      const uint32_t k = tkey[p];
+      bool hit = false;
+      if (!(k & kKeySlow)) {
+        hit = isA(k & kKeyNode);
+      } else {
+        for (uint32_t a = pt.adv_off[p0 + p]; a < pt.adv_off[p0 + p + 1]; ++a) {
+          const uint32_t v = pt.adv_node[a];
+          hit |= v != OGS_NODE_NONE && isA(v);
+        }
+      }
+      if (!hit) continue;  // every advertiser keeps its base state
+      Rec<1> r;
+      if (!(k & kKeySlow)) {
+        if ((k & kKeyV4) && v4Gated) continue;  // the gate's record never changes
+        nodeRec(k & kKeyNode, r);
+        r.sel = (r.meta & OGS_ROUTE_SELECTED) ? 1u : 0u;
+      } else {
+        route_one<uint32_t, 1>(pt, p0 + p, s, nflags, PackedView{dn}, cfg, r.meta, r.metric,
+                               r.mask, r.sel);
+      }
+      if (!route_changed<1>(r, dc, Sp, p, upd, del)) continue;
+      atomicOr(dc.changed + p / 32u, 1u << (p % 32u));
+      const size_t o = size_t(u0) * Sp + p;
+      if (out.meta) out.meta[o] = r.meta;
+      if (out.metric) static_cast<uint32_t*>(out.metric)[o] = r.metric;
+      if (out.sel) out.sel[o] = r.sel;
+      if (out.mask) out.mask[o] = r.mask[0];
+    }
+    if (upd) atomicAdd(&cnt[0], upd);
+    if (del) atomicAdd(&cnt[1], del);
+  }
+  __syncthreads();
+  if (tid < 2) diff.counts[size_t(u0) * 2 + tid] = cnt[tid];
+}
+
+// ogs_spf_routes_variants with OGS_F_INCREMENTAL (W = 1); false when the
+// repair does not apply (the caller then runs the full recompute).
+bool launch_variants_repair(const ogs_graph& g, const ogs_prefix_table& pt,
+                            const uint32_t* key, const ogs_unit* units, int n,
+                            uint32_t flags, int W, const ogs_spf_out& out,
+                            const ogs_unit_mods* mods, const ogs_route_diff* diff,
+                            hipStream_t stream, hipError_t* err) {
+  if (!(flags & OGS_F_INCREMENTAL) || !mods || !diff || !diff->base_dist || !diff->base_nh ||
+      W != 1 || mods->dead_per_unit > kMaxDead || g.max_nodes > 65535) {
+    return false;
+  }
+  const uint32_t lds = repair_lds_bytes(uint32_t(g.max_nodes));
+  if (lds > 160u * 1024u) return false;
+  const bool changedOnly = (flags & OGS_F_CHANGED_ONLY) != 0;
+  auto k = changedOnly ? spf_variant_repair_kernel<true> : spf_variant_repair_kernel<false>;
+  if (lds > 64 * 1024) {
+    *err = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
+    if (*err != hipSuccess) return true;
+  }
+  hipLaunchKernelGGL(k, dim3(n), dim3(kBlock), lds, stream, g, pt, key, units, flags,
+                     static_cast<uint32_t*>(out.dist), out.nh, out, *mods, *diff);
+  *err = hipGetLastError();
+  return true;
+}
+
 // Link-failure variants with an optional route diff (fused SPF + RouteDb).
 template <int W>
 hipError_t launch_variants_w(const ogs_graph& g, const ogs_prefix_table& pt,
@@ -860,9 +1106,13 @@ hipError_t launch_frontier_variants(const ogs_graph& g, const ogs_prefix_table& 
                                     const ogs_unit_mods* mods,
                                     const ogs_route_diff* diff, void* scratch,
                                     hipStream_t stream) {
+  hipError_t e = hipSuccess;
+  if (launch_variants_repair(g, pt, key, units, n, flags, W, out, mods, diff, stream, &e)) {
+    return e;
+  }
   uint64_t* chunks = nullptr;
   uint32_t* nChunk = nullptr;
-  hipError_t e = prep_chunks(g, scratch, stream, &chunks, &nChunk);
+  e = prep_chunks(g, scratch, stream, &chunks, &nChunk);
   if (e != hipSuccess) return e;
   switch (W) {
     case 1: return launch_variants_w<1>(g, pt, key, chunks, nChunk, units, n, flags, out, mods, diff, stream);

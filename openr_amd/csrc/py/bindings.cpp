@@ -755,6 +755,11 @@ class VariantRunner {
                                                 brs_);
   }
   void runBase(uintptr_t stream) { sw().runBase(reinterpret_cast<void*>(stream)); }
+  void setMode(int m) {
+    if (m < 0 || m > 2) throw std::invalid_argument("mode must be 0, 1 or 2");
+    sw().setMode(LinkFailureSweep::Mode(m));
+  }
+  int mode() const { return int(sw().mode()); }
   void launch(uintptr_t stream, bool records) {
     sw().launch(reinterpret_cast<void*>(stream), records);
   }
@@ -1716,6 +1721,8 @@ PYBIND11_MODULE(_decision, m) {
              r.launch(stream, records);
            }, py::arg("stream") = 0, py::arg("records") = true)
       .def("download", &VariantRunner::download)
+      .def("set_mode", &VariantRunner::setMode, py::arg("mode"))
+      .def("mode", &VariantRunner::mode)
       .def("fetch_updates", [](VariantRunner& r, uintptr_t stream) { r.fetchUpdates(stream); },
            py::arg("stream") = 0)
       .def("base_canonical", [](const VariantRunner& r) { return py::bytes(r.baseCanonical()); })

@@ -130,12 +130,16 @@ def test_c3_companion_canonical_text(product, oracle):
         assert x == y, n
 
 
-def test_c4_full_sweep_matches_oracle(product, oracle):
-    """C4 at bench size: all 10,000 variants in one launch; the change-list
-    digest equals the oracle's golden one, the first 600 variants' change
-    lists equal a live oracle run, and the total matches."""
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_c4_full_sweep_matches_oracle(product, oracle, mode):
+    """C4 at bench size: all 10,000 variants in one launch -- full SPF per
+    variant (mode 0), base-SPF repair (1) and repair writing changed records
+    only (2, what bench.py times); the change-list digest equals the
+    oracle's golden one, the first 600 variants' change lists equal a live
+    oracle run, and the total matches."""
     vr = product.VariantRunner(True, False)
     vr.setup("wan", C4_OPTS, C4_SOURCE, C4_VARIANTS, C4_SEED, C4_DUAL_PERMILLE, 0, -1)
+    vr.set_mode(mode)
     vr.run_base(0)
     vr.launch(0, True)
     vr.download()

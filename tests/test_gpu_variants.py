@@ -16,11 +16,16 @@ CASES = [
 ]
 
 
+@pytest.mark.parametrize("mode", [0, 1])
 @pytest.mark.parametrize("kind,opts,source,brs", CASES, ids=lambda x: str(x)[:12])
-def test_link_failure_variants(product, oracle, kind, opts, source, brs):
+def test_link_failure_variants(product, oracle, kind, opts, source, brs, mode):
+    """Every variant's full RouteDb, by a full SPF per variant (mode 0) and
+    by repairing the base SPF below the failed tight links (mode 1,
+    OGS_F_INCREMENTAL)."""
     n = 48
     vr = product.VariantRunner(True, brs)
     vr.setup(kind, opts, source, n, 0xC4F, 500)
+    vr.set_mode(mode)
     vr.run_base()
     vr.launch()
     vr.download()
@@ -53,8 +58,9 @@ def test_variants_records_optional(product):
     assert [(vr.changed(v), vr.counts(v)) for v in range(32)] == full
 
 
+@pytest.mark.parametrize("mode", [0, 1, 2])
 @pytest.mark.parametrize("kind,opts,source,brs", CASES, ids=lambda x: str(x)[:12])
-def test_route_updates_from_changed_records(product, oracle, kind, opts, source, brs):
+def test_route_updates_from_changed_records(product, oracle, kind, opts, source, brs, mode):
     """§8(f) f1: the DecisionRouteUpdate of every variant, materialised from the
     device-gathered changed records only (ogs_route_changes_gather), is
     DecisionRouteDb::calculateUpdate(base, variant) (SpfSolver.cpp:21-56):
@@ -64,6 +70,7 @@ def test_route_updates_from_changed_records(product, oracle, kind, opts, source,
     n = 48
     vr = product.VariantRunner(True, brs)
     vr.setup(kind, opts, source, n, 0xC4F, 500)
+    vr.set_mode(mode)  # 2: repair writing changed records only (OGS_F_CHANGED_ONLY)
     vr.launch(0, True)
     vr.fetch_updates(0)
     base, variants, links = oracle.variant_route_updates(kind, opts, source, n, 0xC4F,
@@ -80,12 +87,14 @@ def test_route_updates_from_changed_records(product, oracle, kind, opts, source,
             pytest.fail(f"variant {v} {links[v]}: {[(x, y) for x, y in zip(a, b) if x != y][:4]}")
 
 
-def test_route_updates_c4_sample(product, oracle):
+@pytest.mark.parametrize("mode", [0, 2])
+def test_route_updates_c4_sample(product, oracle, mode):
     """The C4 bench workload (2,000-node WAN, seed 0xC4, source '0'): the first
     64 of its 10,000 variants, route updates vs the oracle."""
     opts = dict(nodes=2000, seed=0xC4, prefixesPerNode=1)
     vr = product.VariantRunner(True, False)
     vr.setup("wan", opts, "0", 10000, 0xC4F, 500, 0, 64)
+    vr.set_mode(mode)
     vr.launch(0, True)
     vr.fetch_updates(0)
     _, variants, links = oracle.variant_route_updates("wan", opts, "0", 64, 0xC4F, 500,
@@ -165,3 +174,42 @@ def test_route_updates_empty_sweep(product):
     vr.launch(0, True)
     vr.fetch_updates(0)
     assert vr.total_changes() == 0
+
+
+def test_changed_only_launch_has_no_full_records(product):
+    """OGS_F_CHANGED_ONLY leaves unchanged records unwritten: the full
+    per-variant RouteDb is not available from such a launch."""
+    opts = dict(nodes=200, seed=0xC4, prefixesPerNode=1)
+    vr = product.VariantRunner(True, False)
+    vr.setup("wan", opts, "0", 8, 0xC4F, 500)
+    vr.set_mode(2)
+    vr.launch(0, True)
+    vr.download()
+    with pytest.raises(Exception, match="fetchRecords"):
+        vr.canonical(0)
+
+
+def test_repair_edge_cases(product, oracle):
+    """Repair on topologies with overloaded nodes / links, drained
+    advertisers, anycast and minNexthop prefixes, hop-free ECMP grids
+    (many tight ties) and failures of the source's own links."""
+    cases = [
+        ("grid", dict(n=9, metricSeed=0xC2000011, metricMax=2, prefixesPerNode=1,
+                      anycastPermille=200, minNhPermille=100), "40"),
+        ("wan", dict(nodes=250, seed=0xD4, prefixesPerNode=2, nodeOverloadPermille=60,
+                     adjOverloadPermille=60, drainPermille=80, anycastPermille=150), "3"),
+    ]
+    for kind, opts, src in cases:
+        n = 96
+        base, variants, links = oracle.variant_route_updates(kind, opts, src, n, 0xBEE, 700,
+                                                             True, True)
+        for mode in (1, 2):
+            vr = product.VariantRunner(True, True)
+            vr.setup(kind, opts, src, n, 0xBEE, 700)
+            vr.set_mode(mode)
+            vr.launch(0, True)
+            vr.fetch_updates(0)
+            for v, (canon, changed, nu, nd) in enumerate(variants):
+                upd, dele = vr.update(v)
+                assert sorted(upd + dele) == changed, (kind, mode, v, links[v])
+                assert vr.updated_canonical(v) == canon, (kind, mode, v, links[v])
