@@ -184,6 +184,59 @@ def run_c1(args, rank):
     return out
 
 
+# ----------------------------------------------------------------- G1 ---
+def run_g1(args, rank):
+    """Row g1: the global-state SPF path on a single-area WAN
+    past every LDS path -- 20,000 nodes, one prefix per node, 64 sources in
+    ONE batched launch (spf_global.hip: frontier rounds with dist /
+    next-hop sets / queues in HBM, then one thread per (unit, prefix)).
+    Digest of the 64 RouteDbs vs the oracle's golden; refcpu beside it."""
+    if rank != 0:
+        return None
+    import openr_amd
+    from openr_amd.workloads import G1_OPTS, G1_SOURCES
+    M = openr_amd.decision
+    br = M.BatchRunner(True, False, False)
+    br.add_generated("wan", G1_OPTS, G1_SOURCES)
+    br.upload()
+    br.run()  # warm-up (code objects, workspace)
+    reps = 5
+    times = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        br.run()  # one launch + stream sync
+        times.append(time.perf_counter() - t0)
+    sec = median(times)
+    br.download()
+    digest = shard.combine_digests(br.unit_digest(u, G1_SOURCES[u])
+                                   for u in range(len(G1_SOURCES)))
+    U, N = len(G1_SOURCES), G1_OPTS["nodes"]
+    out = {"unit": "RouteDbs/s", "value": round(U / sec, 2), "ms_per_launch": round(sec * 1e3, 3),
+           "sources": U, "nodes": N, "prefixes": N, "reps": reps,
+           "route_digest": f"{digest:016x}",
+           "note": "one ogs_spf_routes launch (global-state path) for 64 sources incl. "
+                   "the launch-to-sync latency; median of reps"}
+    want = GOLDEN.get("g1")
+    out["golden"] = "n/a" if want is None else ("match" if f"{digest:016x}" == want
+                                                 else "MISMATCH")
+    if want is not None and out["golden"] != "match":
+        DIGEST_FAILURES.append(f"g1: {digest:016x} != golden {want}")
+    if not args.no_cpu_baseline:
+        R = oracle()
+        T = cpu_threads()
+        sample = G1_SOURCES[:2 * T]
+        rates = {}
+        for threads, srcs in ((T, sample), (1, G1_SOURCES[:4])):
+            secs, _ = R.cpu_baseline_sources("wan", G1_OPTS, srcs, threads, CPU_REPS)
+            rates[threads] = len(srcs) / median(secs)
+        out["cpu_baseline"] = {
+            "value": round(rates[T], 2), "unit": "RouteDbs/s", "cores": T, "kind": "port",
+            "value_1thread": round(rates[1], 2), "reps": CPU_REPS, "host": host_info(),
+            "sample": f"refcpu buildRouteDb of the first {len(sample)} of the 64 sources on "
+                      f"{T} threads (4 on 1 thread), ingestion untimed, median"}
+    return out
+
+
 # ----------------------------------------------------------------- C3 ---
 def c3_launches(torch, M, capi, dev, names, ppn=100, with_sel=False):
     """Host build + device upload of the C3 launches for the sources
@@ -746,6 +799,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-c1", action="store_true",
                     help="skip the C1 single-source latency line embedded in the C2 result")
+    ap.add_argument("--no-g1", action="store_true",
+                    help="skip the 20,000-node WAN sub-line (global-state SPF path)")
     ap.add_argument("--no-c3", action="store_true",
                     help="skip the C3 fabric all-sources line embedded in the C2 result")
     ap.add_argument("--c3-steps", type=int, default=10)
@@ -941,6 +996,9 @@ def main():
             log("c2 cpu baseline done")
         if not args.no_c1:
             line["c1_single_source"] = run_c1(args, rank)
+        if not args.no_g1:
+            log("g1 large WAN ...")
+            line["g1_large_wan"] = run_g1(args, rank)
     if not args.no_c3:
         # the north-star headline config, sharded by source over the ranks
         c3 = run_c3(args, torch, dist, rank, world, local_rank)

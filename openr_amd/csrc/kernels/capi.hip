@@ -12,6 +12,7 @@ extern int g_unitWidth;
 extern int g_waveWgLds;
 extern int g_waveUpb;
 extern int g_waveOpt;
+extern int g_kspWaveTrace;
 extern int g_msGroup;
 extern int g_routeStream;
 extern int g_spfFrontier;
@@ -216,6 +217,11 @@ int ogs_set_option(const char* name, int64_t value) {
       return fail(OGS_E_INVALID, "wave_upb must be 4, 8 or 16");
     }
     ogs::g_waveUpb = int(value);
+    return OGS_OK;
+  }
+  if (std::strcmp(name, "ksp_wave_trace") == 0) {
+    if (value != 0 && value != 1) return fail(OGS_E_INVALID, "ksp_wave_trace must be 0 or 1");
+    ogs::g_kspWaveTrace = int(value);
     return OGS_OK;
   }
   if (std::strcmp(name, "wave_opt") == 0) {

@@ -142,11 +142,147 @@ __device__ uint32_t trace_paths(const UnitCsr& csr, const D* dist, uint32_t s,
   return nPaths | (status << 31);
 }
 
+// trace_paths by one whole wavefront (32-bit distances): the same greedy
+// DFS with the same choices, but each step's scan of the node's row is
+// spread over the lanes (lane j tests edge j of a 64-edge window) and the
+// next pathLink is a wave-wide min of the packed key (dist, pred, slot) --
+// one LDS round trip and a 6-step reduction per step instead of a serial
+// walk of the row by lane 0. Every lane runs the uniform control flow and
+// holds the same frame state; LDS state (stack, visited, masks, outputs) is
+// written by lane 0 and made visible to the wave before it is read.
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint32_t lo = __shfl_xor(static_cast<uint32_t>(x), o);
+    const uint32_t hi = __shfl_xor(static_cast<uint32_t>(x >> 32), o);
+    const uint64_t y = (uint64_t(hi) << 32) | lo;
+    x = y < x ? y : x;
+  }
+  return x;
+}
+
+__device__ __forceinline__ void lane_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <bool MASKED>
+__device__ uint32_t trace_paths_wave(const UnitCsr& csr, const uint32_t* dist, uint32_t s,
+                                     uint32_t t, uint32_t* visited, Frame* stack,
+                                     const uint32_t* ignore, const ogs_path_out& out,
+                                     size_t row, uint32_t* pathMask, int lane) {
+  constexpr uint32_t kInf = 0xFFFFFFFFu;
+  constexpr uint64_t kNone = ~0ull;
+  // packed key: dist | pred << 9 | slot (pred < 2^21, slot < 512): the
+  // lexicographic (dist, pred, slot) order of key_less
+  auto pack = [](uint32_t d, uint32_t u, uint32_t slot) {
+    return (uint64_t(d) << 32) | (uint64_t(u) << 9) | slot;
+  };
+  uint32_t* pathLen = out.path_len + row * out.max_paths;
+  uint32_t* pathEdges = out.path_edges + row * out.max_edges;
+  uint32_t nPaths = 0, nEdges = 0, status = 0;
+  const bool reachable = (s != t) && dist[t] != kInf;
+  while (reachable) {
+    int sp = 0;
+    if (lane == 0) stack[0] = Frame{t, 0xFFFFFFFFu};
+    lane_sync();
+    bool found = false;
+    while (sp >= 0) {
+      const Frame f = stack[sp];
+      const uint32_t v = f.node;
+      const uint32_t dv = dist[v];
+      const bool fresh = f.edge == 0xFFFFFFFFu;
+      uint64_t lastKey = 0;
+      if (!fresh) {
+        const uint32_t llo = static_cast<uint32_t>(csr.edg[f.edge]);
+        lastKey = pack(dist[edge_dst(llo)], edge_dst(llo), edge_rslot(llo));
+      }
+      uint64_t best = kNone;
+      uint32_t be = 0xFFFFFFFFu;
+      const uint32_t rEnd = csr.rowp[v + 1];
+      for (uint32_t eb = csr.rowp[v]; eb < rEnd; eb += 64) {
+        const uint32_t e = eb + uint32_t(lane);
+        uint64_t key = kNone;
+        if (e < rEnd) {
+          const uint64_t ed = csr.edg[e];
+          const uint32_t lo = static_cast<uint32_t>(ed);
+          const uint32_t u = edge_dst(lo);
+          bool ok = !(lo & OGS_EDGE_DOWN) && !((lo & OGS_EDGE_DST_OVERLOADED) && u != s);
+          if constexpr (MASKED) {
+            if (ok) {
+              const uint32_t l = link_id(csr, e, lo);
+              ok = !((ignore[l >> 5] >> (l & 31u)) & 1u);
+            }
+          }
+          if (ok) {
+            const uint32_t du = dist[u];
+            if (du != kInf && du + static_cast<uint32_t>(ed >> 32) == dv) {
+              const uint64_t k = pack(du, u, edge_rslot(lo));
+              if (fresh || k > lastKey) key = k;
+            }
+          }
+        }
+        const uint64_t m = wave_min_u64(key);
+        if (m < best) {
+          const uint64_t who = __ballot(key == m);
+          best = m;
+          be = __shfl(e, int(__builtin_ctzll(who)));
+        }
+      }
+      if (best == kNone) {  // exhausted: this recursion level fails
+        --sp;
+        continue;
+      }
+      const uint32_t bu = static_cast<uint32_t>(best >> 9) & OGS_EDGE_DST_MASK;
+      if (lane == 0) stack[sp].edge = be;  // resume key (+ path edge on success)
+      const uint32_t l = link_id(csr, be, static_cast<uint32_t>(csr.edg[be]));
+      const bool seen = (visited[l >> 5] >> (l & 31u)) & 1u;
+      lane_sync();
+      if (seen) continue;  // already used
+      if (lane == 0) visited[l >> 5] |= 1u << (l & 31u);
+      if (bu == s) {
+        lane_sync();
+        found = true;
+        break;
+      }
+      ++sp;
+      if (lane == 0) stack[sp] = Frame{bu, 0xFFFFFFFFu};
+      lane_sync();
+    }
+    if (!found) break;
+    // path src -> dest = chosen edges from the top frame down to frame 0
+    if (nPaths >= out.max_paths || nEdges + uint32_t(sp + 1) > out.max_edges) {
+      status = 1;  // output capacity exceeded
+      break;
+    }
+    for (int i = sp; i >= 0; --i) {
+      const uint32_t e = stack[i].edge;
+      if (lane == 0) {
+        pathEdges[nEdges] = e - csr.eBase;
+        if (pathMask) {
+          const uint32_t l = link_id(csr, e, static_cast<uint32_t>(csr.edg[e]));
+          pathMask[l >> 5] |= 1u << (l & 31u);
+        }
+      }
+      ++nEdges;
+    }
+    if (lane == 0) pathLen[nPaths] = uint32_t(sp + 1);
+    ++nPaths;
+    lane_sync();
+  }
+  return nPaths | (status << 31);
+}
+
+// "ksp_wave_trace" option: 1 (default) the traces of 32-bit-distance units
+// run on a whole wavefront (trace_paths_wave), 0 on lane 0 (A/B)
+int g_kspWaveTrace = 1;
+
 template <typename D, int UT, bool STAGE, bool MASKED>
 __global__ __launch_bounds__(kBlock) void ksp_kernel(
     ogs_graph g, const ogs_path_unit* __restrict__ units, int nUnits,
     const uint32_t* __restrict__ masks, uint32_t maskWords,
-    ogs_path_out out, uint32_t ldsPerUnit) {
+    ogs_path_out out, uint32_t ldsPerUnit, int waveTrace) {
   constexpr int kUnitsPerBlock = kBlock / UT;
   const int uib = threadIdx.x / UT;
   const int lane = threadIdx.x % UT;
@@ -186,6 +322,15 @@ __global__ __launch_bounds__(kBlock) void ksp_kernel(
   spf_fixpoint<D, 1, UT, false, MASKED>(N, s, lane, csr, false, dist, nullptr,
                                         ignore);
 
+  if constexpr (sizeof(D) == 4) {
+    if (waveTrace) {
+      if (lane >= 64) return;  // wave 0 of a workgroup unit traces
+      const uint32_t c = trace_paths_wave<MASKED>(csr, dist, s, t, visited, stack, ignore,
+                                                  out, uidx, nullptr, lane);
+      if (lane == 0) out.path_count[uidx] = c;
+      return;
+    }
+  }
   if (lane != 0) return;
   out.path_count[uidx] = trace_paths<D, MASKED>(
       csr, dist, s, t, visited, stack, ignore, out, uidx, nullptr);
@@ -207,7 +352,7 @@ hipError_t ksp_launch(const ogs_graph& g, const ogs_path_unit* units,
     if (e != hipSuccess) return e;
   }
   hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), bytes, stream, g, units,
-                     nUnits, masks, maskWords, out, lds);
+                     nUnits, masks, maskWords, out, lds, g_kspWaveTrace);
   return hipGetLastError();
 }
 
@@ -457,7 +602,7 @@ template <typename D, int UT, int STAGE, bool QUEUE>
 __global__ __launch_bounds__(kBlock) void ksp2_kernel(
     ogs_graph g, const ogs_unit* __restrict__ sources, int nSources,
     const D* __restrict__ srcDist, const ogs_path_unit* __restrict__ units,
-    int nUnits, ogs_path_out o1, ogs_path_out o2, uint32_t ldsPerUnit) {
+    int nUnits, ogs_path_out o1, ogs_path_out o2, uint32_t ldsPerUnit, int waveTrace) {
   constexpr int kUnitsPerBlock = kBlock / UT;
   using Scope = UnitScope<UT>;
   const int uib = threadIdx.x / UT;
@@ -484,7 +629,14 @@ __global__ __launch_bounds__(kBlock) void ksp2_kernel(
   Scope::sync();
   const uint32_t s = unit.src, t = unit.dest;
   uint32_t c1 = 0;
-  if (lane == 0) {
+  const bool wt = sizeof(D) == 4 && waveTrace;
+  if (wt && lane < 64) {
+    if constexpr (sizeof(D) == 4) {
+      c1 = trace_paths_wave<false>(l.csr, l.dist, s, t, l.visited, l.stack, nullptr, o1,
+                                   uidx, l.mask, lane);
+    }
+    if (lane == 0) o1.path_count[uidx] = c1;
+  } else if (!wt && lane == 0) {
     c1 = trace_paths<D, false>(l.csr, l.dist, s, t, l.visited, l.stack, nullptr,
                                o1, uidx, l.mask);
     o1.path_count[uidx] = c1;
@@ -499,6 +651,15 @@ __global__ __launch_bounds__(kBlock) void ksp2_kernel(
   }
   for (uint32_t i = lane; i < l.linkWords; i += UT) l.visited[i] = 0u;
   ksp_spf<D, UT, QUEUE, true>(l, s, lane);
+  if constexpr (sizeof(D) == 4) {
+    if (wt) {
+      if (lane >= 64) return;
+      const uint32_t c2 = trace_paths_wave<true>(l.csr, l.dist, s, t, l.visited, l.stack,
+                                                 l.mask, o2, uidx, nullptr, lane);
+      if (lane == 0) o2.path_count[uidx] = c2;
+      return;
+    }
+  }
   if (lane != 0) return;
   o2.path_count[uidx] = trace_paths<D, true>(l.csr, l.dist, s, t, l.visited,
                                              l.stack, l.mask, o2, uidx, nullptr);
@@ -528,7 +689,8 @@ hipError_t ksp2_launch(const ogs_graph& g, const ogs_unit* sources,
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k2, dim3((nUnits + upb - 1) / upb), dim3(kBlock), bytes,
                      stream, g, sources, nSources,
-                     static_cast<const D*>(srcDist), units, nUnits, o1, o2, lds);
+                     static_cast<const D*>(srcDist), units, nUnits, o1, o2, lds,
+                     g_kspWaveTrace);
   return hipGetLastError();
 }
 

@@ -58,3 +58,11 @@ def c5_policy(areas, neighbors, seed=0xC5):
     return [dict(name="c5-ucmp", tags=["ucmp"], counterID="c5-ucmp",
                  set_weight=dict(default_weight=1, area_to_weight=area_w,
                                  neighbor_to_weight=nbr_w))]
+
+# G1 (north_star "large WAN graphs"): a single-area WAN
+# past every LDS path (20,000 nodes, one prefix per node), 64 sources spread
+# over the node ids, solved in one batched launch through the global-state
+# SPF path (spf_global.hip).
+G1_OPTS = dict(nodes=20000, seed=0x61, prefixesPerNode=1)
+G1_SOURCES = [str(i * 20000 // 64) for i in range(64)]
+

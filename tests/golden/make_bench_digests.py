@@ -9,7 +9,7 @@ XOR over routes of a hash of the RibUnicastEntry fields) and
 openr_amd/shard.py (C4 change lists, C5 KSP2 path lines). Every value here
 comes from oracle/refcpu (test infrastructure), never from the engine.
 
-  python tests/golden/make_bench_digests.py [c2] [c3] [c4] [c5] [--threads T]
+  python tests/golden/make_bench_digests.py [c2] [c3] [c4] [c5] [g1] [--threads T]
 
 C3 takes long (2,080 oracle buildRouteDb over 208k prefixes each, ~1.5 h on
 8 cores): it is resumable, per-source digests accumulate in
@@ -30,7 +30,8 @@ import _refcpu as R  # noqa: E402
 from openr_amd import shard  # noqa: E402  (pure Python: digest helpers)
 from openr_amd.workloads import (C2_OPTS, C2_SOURCE, C2_TOPOS, C3_OPTS, C4_OPTS,  # noqa: E402
                                  C4_SOURCE, C4_VARIANTS, C4_SEED, C4_DUAL_PERMILLE,
-                                 C5_OPTS, C5_SOURCE, c3_source_names, c5_policy)
+                                 C5_OPTS, C5_SOURCE, G1_OPTS, G1_SOURCES, c3_source_names,
+                                 c5_policy)
 
 OUT = os.path.join(HERE, "bench_digests.json")
 C3_PART = os.path.join(HERE, "c3_source_digests.json")
@@ -95,6 +96,12 @@ def gen_c5(out, threads):
     out["c5_ksp_lines"] = len(lines)
 
 
+def gen_g1(out, threads):
+    """Per source the RouteDb digest (key = source name), XOR-combined."""
+    ds = R.gen_route_digests("wan", G1_OPTS, G1_SOURCES, True, False, False, threads)
+    out["g1"] = f"{shard.combine_digests(ds):016x}"
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("configs", nargs="*", default=["c2", "c4", "c5", "c3"])
@@ -112,6 +119,8 @@ def main():
             gen_c4(out, a.threads)
         elif c == "c5":
             gen_c5(out, a.threads)
+        elif c == "g1":
+            gen_g1(out, a.threads)
         else:
             raise SystemExit(f"unknown config {c}")
         out["generator"] = "tests/golden/make_bench_digests.py (oracle/refcpu)"
