@@ -814,6 +814,12 @@ class RouteDbBatch {
   size_t numGroups() const { return groups_.size(); }
 
  private:
+  struct UnitRecords;
+  bool fetchUnit(const std::string& node, void* stream, UnitRecords& r) const;
+
+ public:
+
+ private:
   struct Group {
     int W{1};
     std::vector<uint32_t> members;  // source index per unit of this group

@@ -8,6 +8,7 @@
 // The batch runs that build for every listed source in one launch per
 // next-hop width group (the C3 all-sources kernels), leaves the compact
 // records in HBM and materialises a node's RouteDb only when it is asked for.
+#include <thread>
 #include <algorithm>
 #include <stdexcept>
 
@@ -137,63 +138,174 @@ void RouteDbBatch::launch(void* stream) {
   launched_ = true;
 }
 
-std::optional<DecisionRouteDb> RouteDbBatch::routeDb(const std::string& node,
-                                                     void* stream) const {
+// one unit's records D2H (its slices only: dist[u*Sn], nh[(u*W+w)*Sn],
+// meta/metric/sel[u*Sp], mask[(u*W+w)*Sp]), distances widened
+struct RouteDbBatch::UnitRecords {
+  std::vector<uint64_t> dist, metric;
+  std::vector<uint32_t> nh, meta, mask, sel;
+  int W{1};
+  size_t Sn{1}, Sp{1};
+};
+
+bool RouteDbBatch::fetchUnit(const std::string& node, void* stream, UnitRecords& r) const {
   auto it = index_.find(node);
   if (it == index_.end()) throw std::out_of_range("RouteDbBatch: not a source: " + node);
   if (!launched_) throw std::logic_error("RouteDbBatch: launch() first");
   const auto [gi, u] = units_[it->second];
-  if (gi == SIZE_MAX) return std::nullopt;  // SpfSolver.cpp:318-324
+  if (gi == SIZE_MAX) return false;  // SpfSolver.cpp:318-324
   const Group& G = groups_[gi];
   const FlatTopology& f = ls_->flat();
   const size_t N = f.names.size(), P = table_.prefixes.size();
-  const size_t Sn = size_t(std::max(hb_.maxNodes, 1)), Sp = size_t(std::max(hb_.maxPrefixes, 1));
-  const size_t db = wide_ ? 8 : 4;
-  const int W = G.W;
-  // this unit's slices only: dist[u*Sn], nh[(u*W+w)*Sn], meta/metric/sel[u*Sp],
-  // mask[(u*W+w)*Sp]
+  r.Sn = size_t(std::max(hb_.maxNodes, 1));
+  r.Sp = size_t(std::max(hb_.maxPrefixes, 1));
+  const size_t db = wide_ ? 8 : 4, Sn = r.Sn, Sp = r.Sp;
+  const int W = r.W = G.W;
   auto fetch = [&](const DeviceBuffer& b, size_t elemOff, size_t n, size_t esz, void* host) {
     if (n == 0) return;
     ogsCheck(ogs_memcpy_d2h(host, static_cast<const char*>(b.get()) + elemOff * esz, n * esz,
                             stream),
              "ogs_memcpy_d2h");
   };
-  std::vector<uint64_t> dist(N), metric(P);
+  r.dist.resize(N);
+  r.metric.resize(P);
   std::vector<uint32_t> d32(wide_ ? 0 : N), m32(wide_ ? 0 : P);
-  std::vector<uint32_t> nh(W * Sn), meta(P), mask(W * Sp), sel(P);
-  fetch(G.dist, u * Sn, N, db, wide_ ? static_cast<void*>(dist.data()) : d32.data());
-  fetch(G.nh, u * W * Sn, W * Sn, 4, nh.data());
-  fetch(G.meta, u * Sp, P, 4, meta.data());
-  fetch(G.metric, u * Sp, P, db, wide_ ? static_cast<void*>(metric.data()) : m32.data());
-  fetch(G.mask, u * W * Sp, W * Sp, 4, mask.data());
-  fetch(G.sel, u * Sp, P, 4, sel.data());
+  r.nh.resize(W * Sn);
+  r.meta.resize(P);
+  r.mask.resize(W * Sp);
+  r.sel.resize(P);
+  fetch(G.dist, u * Sn, N, db, wide_ ? static_cast<void*>(r.dist.data()) : d32.data());
+  fetch(G.nh, u * W * Sn, W * Sn, 4, r.nh.data());
+  fetch(G.meta, u * Sp, P, 4, r.meta.data());
+  fetch(G.metric, u * Sp, P, db, wide_ ? static_cast<void*>(r.metric.data()) : m32.data());
+  fetch(G.mask, u * W * Sp, W * Sp, 4, r.mask.data());
+  fetch(G.sel, u * Sp, P, 4, r.sel.data());
   ogsCheck(ogs_stream_sync(stream), "ogs_stream_sync");
   if (!wide_) {
-    for (size_t i = 0; i < N; ++i) dist[i] = d32[i] == 0xFFFFFFFFu ? ~0ull : d32[i];
-    for (size_t i = 0; i < P; ++i) metric[i] = m32[i] == 0xFFFFFFFFu ? ~0ull : m32[i];
+    for (size_t i = 0; i < N; ++i) r.dist[i] = d32[i] == 0xFFFFFFFFu ? ~0ull : d32[i];
+    for (size_t i = 0; i < P; ++i) r.metric[i] = m32[i] == 0xFFFFFFFFu ? ~0ull : m32[i];
   }
+  return true;
+}
+
+std::optional<DecisionRouteDb> RouteDbBatch::routeDb(const std::string& node,
+                                                     void* stream) const {
+  UnitRecords r;
+  if (!fetchUnit(node, stream, r)) return std::nullopt;
+  const FlatTopology& f = ls_->flat();
   UnitView view;
-  view.W = W;
-  view.N = uint32_t(N);
-  view.P = uint32_t(P);
-  view.dist = dist.data();
-  view.nh = nh.data();
-  view.nhStride = Sn;
-  view.meta = meta.data();
-  view.metric = metric.data();
-  view.mask = mask.data();
-  view.maskStride = Sp;
-  view.sel = sel.data();
+  view.W = r.W;
+  view.N = uint32_t(f.names.size());
+  view.P = uint32_t(table_.prefixes.size());
+  view.dist = r.dist.data();
+  view.nh = r.nh.data();
+  view.nhStride = r.Sn;
+  view.meta = r.meta.data();
+  view.metric = r.metric.data();
+  view.mask = r.mask.data();
+  view.maskStride = r.Sp;
+  view.sel = r.sel.data();
   return materializeRouteDb(*ls_, f, area_, node, view, table_, solver_.v4OverV6Nexthop_,
                             solver_.enableNodeSegmentLabel_, solver_.staticUnicastRoutes_,
                             nullptr);
 }
 
+// getDecisionRouteDb + toThrift (Decision.cpp:341-360, SpfSolver.h:82-94,
+// RibEntry.h:95-103 / 144-151) straight from the records: the thrift form
+// carries only prefix, next hops and counterID, so no DecisionRouteDb /
+// RibUnicastEntry (best entry, area, ...) is built. Next hops come from
+// per-link-slot templates pre-sorted in NextHopThrift order (a route's next
+// hops share its metric, so slot order = set order), prefixes in table
+// order (= the DecisionRouteDb map order), built in parallel chunks and
+// merged with the static routes. Equal to routeDb(node)->toThrift()
+// (tests/test_gpu_route_db_batch.py).
 RouteDatabase RouteDbBatch::getRouteDbComputed(const std::string& node, void* stream) const {
   RouteDatabase out;  // Decision.cpp:341-360
   const std::string& n = node.empty() ? solver_.myNodeName_ : node;
-  if (auto db = routeDb(n, stream)) out = db->toThrift();
   out.thisNodeName = n;
+  UnitRecords r;
+  if (!fetchUnit(n, stream, r)) return out;
+  const FlatTopology& f = ls_->flat();
+  const uint32_t s = f.id.at(n);
+  const uint32_t rb = f.rowPtr[s], deg = f.rowPtr[s + 1] - rb;
+  const size_t P = table_.prefixes.size();
+  // next-hop templates per link slot, v6 (0) and v4 (1) address flavours,
+  // and the slots of each flavour in NextHopThrift order
+  std::vector<NextHopThrift> tmpl[2];
+  std::vector<uint32_t> order[2];
+  for (int fl = 0; fl < 2; ++fl) {
+    tmpl[fl].reserve(deg);
+    for (uint32_t j = 0; j < deg; ++j) {
+      const Link& l = *f.edgeLink[rb + j];
+      NextHopThrift nh;
+      nh.address = fl ? l.getNhV4FromNode(n) : l.getNhV6FromNode(n);
+      nh.ifName = l.getIfaceFromNode(n);
+      nh.area = l.getArea();
+      nh.neighborNodeName = l.getOtherNodeName(n);
+      tmpl[fl].push_back(std::move(nh));
+    }
+    order[fl].resize(deg);
+    for (uint32_t j = 0; j < deg; ++j) order[fl][j] = j;
+    std::stable_sort(order[fl].begin(), order[fl].end(),
+                     [&](uint32_t a, uint32_t b) { return tmpl[fl][a] < tmpl[fl][b]; });
+  }
+  const int W = r.W;
+  const size_t Sp = r.Sp;
+  auto build = [&](size_t p0, size_t p1, std::vector<UnicastRoute>& dst) {
+    for (size_t p = p0; p < p1; ++p) {
+      if (!(r.meta[p] & OGS_ROUTE_VALID)) continue;
+      const std::string& prefix = table_.prefixes[p];
+      const int fl = (isV4Prefix(prefix) && !solver_.v4OverV6Nexthop_) ? 1 : 0;
+      const int32_t m32 = static_cast<int32_t>(r.metric[p]);
+      UnicastRoute ur;
+      ur.dest = prefix;
+      for (uint32_t j : order[fl]) {
+        if (!((r.mask[size_t(j / 32) * Sp + p] >> (j % 32)) & 1u)) continue;
+        NextHopThrift nh = tmpl[fl][j];
+        nh.metric = m32;
+        ur.nextHops.push_back(std::move(nh));
+      }
+      dst.push_back(std::move(ur));
+    }
+  };
+  (void)W;
+  const size_t T = std::max<size_t>(
+      1, std::min<size_t>({16, std::max(1u, std::thread::hardware_concurrency()), P / 8192 + 1}));
+  std::vector<std::vector<UnicastRoute>> parts(T);
+  {
+    std::vector<std::thread> pool;
+    for (size_t t = 1; t < T; ++t) {
+      pool.emplace_back(build, P * t / T, P * (t + 1) / T, std::ref(parts[t]));
+    }
+    build(0, P / T, parts[0]);
+    for (auto& th : pool) th.join();
+  }
+  // merge with the statics (a computed route wins, SpfSolver.cpp:343-349)
+  const auto& statics = solver_.staticUnicastRoutes_;
+  size_t total = statics.size();
+  for (const auto& part : parts) total += part.size();
+  out.unicastRoutes.reserve(total);
+  auto st = statics.begin();
+  auto emitStatic = [&](const RibUnicastEntry& e) {
+    out.unicastRoutes.push_back(UnicastRoute{
+        e.prefix, std::vector<NextHopThrift>(e.nexthops.begin(), e.nexthops.end()), e.counterID});
+  };
+  for (auto& part : parts) {
+    for (auto& ur : part) {
+      while (st != statics.end() && st->first < ur.dest) emitStatic((st++)->second);
+      if (st != statics.end() && st->first == ur.dest) ++st;
+      out.unicastRoutes.push_back(std::move(ur));
+    }
+  }
+  for (; st != statics.end(); ++st) emitStatic(st->second);
+  // node-label MPLS routes (SpfSolver.cpp:354-445), label order
+  if (solver_.enableNodeSegmentLabel_) {
+    LabelRoutes labelToNode;
+    addNodeLabelRoutes(*ls_, f, area_, n, r.dist.data(), r.nh.data(), r.Sn, r.W, labelToNode);
+    for (auto& [label, ne] : labelToNode) {
+      out.mplsRoutes.push_back(MplsRoute{
+          label, std::vector<NextHopThrift>(ne.second.nexthops.begin(), ne.second.nexthops.end())});
+    }
+  }
   return out;
 }
 

@@ -327,7 +327,7 @@ struct SpfSolver::Impl {
   int spfW{0};
   size_t spfDb{0};
   // createRoutesForPrefixes: the changed prefixes' sub-table and records
-  DeviceBuffer subTab, subRes;
+  DeviceBuffer subTab, subRes, spfDesc;
   PinnedBuffer hSubTab, hSubRes;
   PrefixHostTable subTable;
   PolicyDevice policy;
@@ -808,7 +808,7 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(
 // source: the SPF memo of the last build (SPF-only launch on a miss), the
 // changed prefixes' sub-table in one H2D, ogs_routes_from_spf, one D2H.
 void SpfSolver::routesFromSpfMemo(const std::string& me, const LinkState& ls,
-                                  const std::string& area, const PrefixState& ps,
+                                  const std::string& area, const PrefixState& /*ps*/,
                                   const PrefixState& sub,
                                   std::map<std::string, std::optional<RibUnicastEntry>>& out) {
   Impl& I = *impl_;
@@ -829,12 +829,15 @@ void SpfSolver::routesFromSpfMemo(const std::string& me, const LinkState& ls,
     I.unit.upload(&u, 1);
     I.unitSrc = s;
   }
-  prepareSingleArea(f, ps, area);  // the topoDesc the SPF launch reads
   if (!(I.spfTopo == &f && I.spfVersion == f.version && I.spfSrc == s)) {
+    // SPF only: the topology's descriptor without a prefix table (the full
+    // table is not needed to answer a few prefixes)
+    const uint32_t desc[8] = {0, N, 0, uint32_t(f.edges.size()), 0, 0, 0, 0};
+    I.spfDesc.upload(desc, 8);
     const ResultImage L(N, 0, W, db);
     I.spfTopo = nullptr;
     I.res.resize(L.end);
-    const ogs_graph g = singleGraph(f, devAt<uint32_t>(I.tab, I.tabImg.desc));
+    const ogs_graph g = singleGraph(f, I.spfDesc.as<uint32_t>());
     ogs_spf_out so{};
     so.dist = devAt<void>(I.res, L.dist);
     so.nh = devAt<uint32_t>(I.res, L.nh);

@@ -1626,8 +1626,22 @@ PYBIND11_MODULE(_decision, m) {
             size_t nhs = 0;
             for (const auto& u : r.unicastRoutes) nhs += u.nextHops.size();
             for (const auto& mr : r.mplsRoutes) nhs += mr.nextHops.size();
+            // the direct thrift build equals toThrift() of the materialised
+            // DecisionRouteDb, route for route, next hop for next hop
+            RouteDatabase want;
+            if (db) want = db->toThrift();
+            bool same = r.unicastRoutes.size() == want.unicastRoutes.size() &&
+                r.mplsRoutes.size() == want.mplsRoutes.size();
+            for (size_t i = 0; same && i < r.unicastRoutes.size(); ++i) {
+              const auto &a = r.unicastRoutes[i], &b = want.unicastRoutes[i];
+              same = a.dest == b.dest && a.nextHops == b.nextHops && a.counterID == b.counterID;
+            }
+            for (size_t i = 0; same && i < r.mplsRoutes.size(); ++i) {
+              same = r.mplsRoutes[i].topLabel == want.mplsRoutes[i].topLabel &&
+                  r.mplsRoutes[i].nextHops == want.mplsRoutes[i].nextHops;
+            }
             shapes.append(py::make_tuple(r.thisNodeName, r.unicastRoutes.size(),
-                                         r.mplsRoutes.size(), nhs));
+                                         r.mplsRoutes.size(), nhs, same));
           }
           return py::make_tuple(out, shapes, batch.numGroups());
         },

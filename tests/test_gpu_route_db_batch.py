@@ -16,8 +16,10 @@ def _check(product, oracle, kind, opts, srcs, sr, brs, groups=None):
     got, shapes, n_groups = product.gen_route_db_batch(kind, opts, srcs, True, sr, brs)
     want = oracle.gen_route_dbs(kind, opts, srcs, True, sr, brs)
     _cmp(got, want, f"{kind} batch")
-    for s, canon, (name, n_uni, n_mpls, n_nh) in zip(srcs, want, shapes):
+    for s, canon, (name, n_uni, n_mpls, n_nh, same) in zip(srcs, want, shapes):
         assert name == s
+        # getRouteDbComputed's direct thrift build == routeDb(s)->toThrift()
+        assert same, s
         if canon == b"NONE":
             assert (n_uni, n_mpls, n_nh) == (0, 0, 0)  # empty RouteDatabase
         else:
