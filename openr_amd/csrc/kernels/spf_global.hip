@@ -182,8 +182,16 @@ bool lds_unit_fits(const ogs_graph& g, int W, uint32_t flags) {
   return b <= 160u * 1024u;
 }
 
+uint32_t frontier_lds_bytes(uint32_t Sn, int W, bool queue, bool ninfo, bool stamps);
+
 bool use_global(const ogs_graph& g, int W, uint32_t flags) {
-  return g_spfGlobal == 1 || !lds_unit_fits(g, W, flags);
+  if (g_spfGlobal == 1 || !lds_unit_fits(g, W, flags)) return true;
+  // past the frontier kernel's LDS budget the remaining LDS paths sweep
+  // every edge every round; on such graphs (large sparse / deep: WAN areas
+  // of 16k+ nodes) the HBM frontier wins -- G1, 20,000-node WAN x 64
+  // sources: 12.4 ms vs 35.0 ms for the multi-source sweep
+  return g.max_nodes > 256 && !(flags & OGS_F_WIDE_METRIC) &&
+      frontier_lds_bytes(uint32_t(g.max_nodes), W, false, true, true) > 160u * 1024u;
 }
 
 template <typename D, int W>
