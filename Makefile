@@ -51,12 +51,16 @@ oracle:
 # (tools/stamps.py); never loaded by the product
 STAMPS := openr_amd/lib/libopenr_gpu_stamps.so
 stamps: $(STAMPS)
-$(STAMPS): $(KERNELS) $(KERNEL_H) include/openr_gpu.h
+SOBJ := $(patsubst openr_amd/csrc/kernels/%.hip,build/stamps/%.o,$(KERNELS))
+build/stamps/%.o: openr_amd/csrc/kernels/%.hip $(KERNEL_H) include/openr_gpu.h
+	@mkdir -p build/stamps
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -DOGS_STAMPS -Iinclude -c $< -o $@
+$(STAMPS): $(SOBJ)
 	@mkdir -p openr_amd/lib
-	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -shared -DOGS_STAMPS -Iinclude $(KERNELS) -o $@
+	$(HIPCC) --offload-arch=$(ARCH) -shared $(SOBJ) -o $@
 
 clean:
-	rm -f $(LIB) $(MOD) $(STAMPS) $(CCONS) $(KOBJ)
+	rm -f $(LIB) $(MOD) $(STAMPS) $(CCONS) $(KOBJ) $(SOBJ)
 	$(MAKE) -C oracle clean
 
 .PHONY: all oracle clean stamps

@@ -175,9 +175,30 @@ __global__ __launch_bounds__(64 * UPB) void spf_route_wave_kernel(
   uint32_t vk[NPL];
   uint32_t nb, N, e0, E, p0 = 0, P = 0, a0 = 0, A = 0;
   if (g.topo_desc) {
-    const uint4* d = reinterpret_cast<const uint4*>(g.topo_desc) + 2 * unit.topo;
-    const uint4 x = d[0];
-    const uint4 y = d[1];
+    // batch builds put unit i on topology i: the descriptor of topology
+    // uidx is loaded together with the unit record (one scalar latency
+    // instead of two dependent ones) and reloaded only when it is not
+    const uint4* td = reinterpret_cast<const uint4*>(g.topo_desc);
+    const uint32_t guess = uint32_t(uidx) < uint32_t(g.num_topos) ? uint32_t(uidx) : 0u;
+    uint4 x = td[2 * guess];
+    uint4 y = td[2 * guess + 1];
+    // opaque to the optimiser (otherwise it folds the guess into a load at
+    // unit.topo, i.e. back into two dependent latencies); readfirstlane
+    // returns the values to scalar registers
+    asm volatile("" : "+v"(x.x), "+v"(x.y), "+v"(x.z), "+v"(x.w), "+v"(y.x),
+                 "+v"(y.y), "+v"(y.z), "+v"(y.w));
+    x.x = __builtin_amdgcn_readfirstlane(x.x);
+    x.y = __builtin_amdgcn_readfirstlane(x.y);
+    x.z = __builtin_amdgcn_readfirstlane(x.z);
+    x.w = __builtin_amdgcn_readfirstlane(x.w);
+    y.x = __builtin_amdgcn_readfirstlane(y.x);
+    y.y = __builtin_amdgcn_readfirstlane(y.y);
+    y.z = __builtin_amdgcn_readfirstlane(y.z);
+    y.w = __builtin_amdgcn_readfirstlane(y.w);
+    if (unit.topo != guess) {
+      x = td[2 * unit.topo];
+      y = td[2 * unit.topo + 1];
+    }
     nb = x.x;
     N = x.y;
     e0 = x.z;
@@ -227,16 +248,17 @@ __global__ __launch_bounds__(64 * UPB) void spf_route_wave_kernel(
   const bool img = perm && g.slot_edges && g.slot_degree == MAXD;
   uint32_t ie[NPL][MAXD];
   constexpr int KP = NPL + 1;  // prefixes per lane per pass (P <= 64*KP)
+  // Node flags and the prefix tables are needed only by the route phase:
+  // their loads are issued with the SPF inputs but waited on (and stored to
+  // LDS) after the SPF rounds, so their latency hides behind the rounds.
   WStage<KP, uint32_t> sOff, sNode;
   WStage<KP, uint8_t> sPf;
-  // identity segments (every prefix has exactly one advertisement, at its
-  // own index: the common single-advertiser table): the route phase reads
-  // advertiser and flags from these registers, the tables skip LDS
-  bool ident = false;
+  WStage<KP, int4> sMet;
+  WStage<NPL, uint8_t> sFlag;
+  const bool pfxFits = (P + 1 <= 64u * KP) && (A <= 64u * KP);
   {
     WStage<NPL + 1, uint32_t> sRow;
     WStage<NPL * MAXD, uint64_t> sEdge;  // E <= N * MAXD <= 64 * NPL * MAXD
-    WStage<NPL, uint8_t> sFlag;
     sRow.load(g.row_ptr + nb, img ? 0u : N + 1, lane);
     sEdge.load(g.edges + e0, img ? 0u : E, lane);
     if (img) {
@@ -261,8 +283,6 @@ __global__ __launch_bounds__(64 * UPB) void spf_route_wave_kernel(
     uint32_t rawSlot[NPL];
 #pragma unroll
     for (int k = 0; k < NPL; ++k) rawSlot[k] = so[k * 64 + lane];
-    WStage<KP, int4> sMet;
-    const bool pfxFits = (P + 1 <= 64u * KP) && (A <= 64u * KP);
     if (hasPrefixes && pfxFits) {
       sOff.load(pt.adv_off + p0, P + 1, lane);
       sNode.load(pt.adv_node + a0, A, lane);
@@ -273,33 +293,8 @@ __global__ __launch_bounds__(64 * UPB) void spf_route_wave_kernel(
     for (int k = 0; k < NPL; ++k) {
       vk[k] = rawSlot[k] == 0xFFFFu ? 0xFFFFFFFFu : rawSlot[k];
     }
-    if (hasPrefixes && pfxFits && A == P && (wopt & OGS_WAVE_OPT_REG_ROUTES)) {
-      bool off = false;
-#pragma unroll
-      for (int k = 0; k < KP; ++k) {
-        const uint32_t i = uint32_t(k * 64 + lane);
-        off |= i <= P && sOff.v[k] - a0 != i;
-      }
-      ident = __builtin_amdgcn_ballot_w64(off) == 0ull;
-    }
     sRow.store(lrow, img ? 0u : N + 1, lane);
     sEdge.store(ledg, img ? 0u : E, lane);
-    sFlag.store(lflags, N, lane);
-    if (ident) {
-      // tables stay in registers
-    } else if (hasPrefixes && pfxFits) {
-      sOff.store(lAdvOff, P + 1, lane);
-      sNode.store(lAdvNode, A, lane);
-      sMet.store(lAdvMetrics, brs ? A : 0u, lane);
-      sPf.store(lPfxFlags, P, lane);
-    } else if (hasPrefixes) {  // rare: long prefix tables, plain loop
-      for (uint32_t i = lane; i <= P; i += 64) lAdvOff[i] = pt.adv_off[p0 + i];
-      for (uint32_t i = lane; i < P; i += 64) lPfxFlags[i] = pt.pfx_flags[p0 + i];
-      for (uint32_t i = lane; i < A; i += 64) {
-        lAdvNode[i] = pt.adv_node[a0 + i];
-        if (brs) lAdvMetrics[i] = reinterpret_cast<const int4*>(pt.adv_metrics)[a0 + i];
-      }
-    }
   }
   wave_sync();
 #ifdef OGS_STAMPS
@@ -502,18 +497,24 @@ __global__ __launch_bounds__(64 * UPB) void spf_route_wave_kernel(
       ncur[k] = cur[k] >= kUnr ? 0u : cur[k] & 0xFFu;
     }
   } else if (narrow) {
-    constexpr uint32_t kUnr = 0x80000000u;
+    // The next-hop byte is stored COMPLEMENTED (dist << 8 | ~nh & 0xFF):
+    // with hi = min | 0xFF, min(cand, hi) is the candidate itself when it
+    // ties the minimum distance and hi otherwise, so the AND over the edges
+    // is {min dist, ~(OR of the tied next-hop sets)} -- min + and per edge,
+    // no compare / select pairs. Unreachable = 0x800000FF (dist field 2^23,
+    // empty set); unusable edges read the dummy word with weight 0.
+    constexpr uint32_t kUnr = 0x800000FFu;
     uint32_t* d32 = reinterpret_cast<uint32_t*>(base + L.dn32);
     uint32_t ws[NPL][MAXD], cur[NPL];
 #pragma unroll
     for (int k = 0; k < NPL; ++k) {
 #pragma unroll
       for (int j = 0; j < MAXD; ++j) ws[k][j] = ew[k][j] << 8;
-      cur[k] = vk[k] == s ? 0u : kUnr;
+      cur[k] = vk[k] == s ? 0xFFu : kUnr;
       d32[k * 64 + lane] = cur[k];
     }
     if (lane == 0) d32[P0] = kUnr;
-    if (lane < 8) d32[P0 + 1 + lane] = 1u << lane;
+    if (lane < 8) d32[P0 + 1 + lane] = ~(1u << lane) & 0xFFu;
     wave_sync();
     for (int step = 0;; ) {
       uint64_t now = 0ull;
@@ -528,9 +529,9 @@ __global__ __launch_bounds__(64 * UPB) void spf_route_wave_kernel(
           best = cand[j] < best ? cand[j] : best;
         }
         const uint32_t hiB = best | 0xFFu;
-        uint32_t word = best & kUnr;
+        uint32_t word = hiB;
 #pragma unroll
-        for (int j = 0; j < MAXD; ++j) word |= cand[j] <= hiB ? cand[j] : 0u;
+        for (int j = 0; j < MAXD; ++j) word &= cand[j] < hiB ? cand[j] : hiB;
         const uint64_t diff = __builtin_amdgcn_ballot_w64(word != cur[k]);
         cur[k] = word;
         d32[k * 64 + lane] = word;
@@ -548,8 +549,9 @@ __global__ __launch_bounds__(64 * UPB) void spf_route_wave_kernel(
     }
 #pragma unroll
     for (int k = 0; k < NPL; ++k) {
-      dcur[k] = cur[k] >= kUnr ? kInf : cur[k] >> 8;
-      ncur[k] = cur[k] >= kUnr ? 0u : cur[k] & 0xFFu;
+      const bool unr = cur[k] >= 0x80000000u;
+      dcur[k] = unr ? kInf : cur[k] >> 8;
+      ncur[k] = unr ? 0u : ~cur[k] & 0xFFu;
     }
   } else {
     constexpr uint32_t kUnr = 0x80000000u;
@@ -625,6 +627,35 @@ __global__ __launch_bounds__(64 * UPB) void spf_route_wave_kernel(
       ncur[k] = 0u;
     }
     if (v < N) dn[v] = uint64_t(dcur[k]) | (uint64_t(ncur[k]) << 32);
+  }
+  // identity segments (every prefix has exactly one advertisement, at its
+  // own index: the common single-advertiser table): the route phase reads
+  // advertiser and flags from the staging registers, the tables skip LDS
+  bool ident = false;
+  if (hasPrefixes && pfxFits && A == P && (wopt & OGS_WAVE_OPT_REG_ROUTES)) {
+    bool off = false;
+#pragma unroll
+    for (int k = 0; k < KP; ++k) {
+      const uint32_t i = uint32_t(k * 64 + lane);
+      off |= i <= P && sOff.v[k] - a0 != i;
+    }
+    ident = __builtin_amdgcn_ballot_w64(off) == 0ull;
+  }
+  sFlag.store(lflags, N, lane);
+  if (ident) {
+    // tables stay in registers
+  } else if (hasPrefixes && pfxFits) {
+    sOff.store(lAdvOff, P + 1, lane);
+    sNode.store(lAdvNode, A, lane);
+    sMet.store(lAdvMetrics, brs ? A : 0u, lane);
+    sPf.store(lPfxFlags, P, lane);
+  } else if (hasPrefixes) {  // rare: long prefix tables, plain loop
+    for (uint32_t i = lane; i <= P; i += 64) lAdvOff[i] = pt.adv_off[p0 + i];
+    for (uint32_t i = lane; i < P; i += 64) lPfxFlags[i] = pt.pfx_flags[p0 + i];
+    for (uint32_t i = lane; i < A; i += 64) {
+      lAdvNode[i] = pt.adv_node[a0 + i];
+      if (brs) lAdvMetrics[i] = reinterpret_cast<const int4*>(pt.adv_metrics)[a0 + i];
+    }
   }
   wave_sync();
 #ifdef OGS_STAMPS
