@@ -28,11 +28,6 @@ const std::vector<LinkState::Path>& LinkState::getKthPaths(
     // unknown endpoints or src == dest: the reference finds no path
     return kthMemo_.emplace(key, std::move(paths)).first->second;
   }
-  if (f.hasZeroMetric || f.hasWideMetric) {
-    throw std::domain_error(
-        "getKthPaths: zero or negative link metric is outside the GPU "
-        "engine's exact domain");
-  }
   const uint32_t E = uint32_t(f.edges.size());
   const uint32_t maskWords = std::max<uint32_t>(1, (E + 31) / 32);
   std::vector<uint32_t> mask;
@@ -68,7 +63,11 @@ const std::vector<LinkState::Path>& LinkState::getKthPaths(
   g.node_flags = f.dFlags.as<uint8_t>();
   ogs_path_out out{dCount.as<uint32_t>(), dLen.as<uint32_t>(),
                    dEdges.as<uint32_t>(), maxPaths, maxEdges};
-  const uint32_t flags = wideDistancesNeeded(f) ? OGS_F_WIDE_METRIC : 0u;
+  // zero / negative metrics: pathLinks follow the reference's extraction
+  // order (ksp.hip, HBM-state path with OGS_F_EXACT_ORDER)
+  const bool exact = f.hasZeroMetric || f.hasWideMetric;
+  const uint32_t flags = (exact || wideDistancesNeeded(f) ? OGS_F_WIDE_METRIC : 0u) |
+      (exact ? OGS_F_EXACT_ORDER : 0u);
   ogsCheck(ogs_ksp_paths(&g, dUnit.as<ogs_path_unit>(), 1,
                          mask.empty() ? nullptr : dMask.as<uint32_t>(),
                          maskWords, flags, &out, nullptr),
@@ -133,9 +132,7 @@ void Ksp2Batch::init(const std::string& src,
     auto it = fl[a]->id.find(src);
     if (it == fl[a]->id.end()) continue;  // no source there: no paths there
     if (fl[a]->hasZeroMetric || fl[a]->hasWideMetric) {
-      throw std::domain_error(
-          "Ksp2Batch: zero or negative link metric is outside the GPU engine's "
-          "exact domain");
+      flags_ |= OGS_F_EXACT_ORDER | OGS_F_WIDE_METRIC;  // extraction order
     }
     srcOf[a] = int64_t(sources.size());
     sources.push_back(ogs_unit{uint32_t(a), it->second});
@@ -159,7 +156,7 @@ void Ksp2Batch::init(const std::string& src,
     maxN = std::max<uint32_t>(maxN, uint32_t(f->names.size()));
     maxE = std::max<uint32_t>(maxE, uint32_t(f->edges.size()));
     maxDeg = std::max(maxDeg, f->maxDegree);
-    if (wideDistancesNeeded(*f)) flags_ = OGS_F_WIDE_METRIC;
+    if (wideDistancesNeeded(*f)) flags_ |= OGS_F_WIDE_METRIC;
   }
   // edge-disjoint paths into d: at most deg(d) of them, at most E/2 links
   maxPaths_ = uint32_t(maxDeg) + 1;

@@ -21,6 +21,7 @@ extern int g_spfQueue;
 extern int g_spfNinfo;
 extern int g_kspQueue;
 extern int g_kspStage;
+extern int g_kspHbm;
 hipError_t launch_spf_routes(const ogs_graph& g, const ogs_prefix_table* pt,
                              const ogs_unit* units, int nUnits, uint32_t flags,
                              int W, const ogs_spf_out& out, hipStream_t stream,
@@ -195,6 +196,11 @@ int ogs_set_option(const char* name, int64_t value) {
     ogs::g_kspQueue = int(value);
     return OGS_OK;
   }
+  if (std::strcmp(name, "ksp_hbm") == 0) {
+    if (value != 0 && value != 1) return fail(OGS_E_INVALID, "ksp_hbm must be 0 or 1");
+    ogs::g_kspHbm = int(value);
+    return OGS_OK;
+  }
   if (std::strcmp(name, "ksp_stage") == 0) {
     if (value < -1 || value > 2) return fail(OGS_E_INVALID, "ksp_stage must be -1, 0, 1 or 2");
     ogs::g_kspStage = int(value);
@@ -339,7 +345,7 @@ int ogs_ksp_paths(const ogs_graph* graph, const ogs_path_unit* units,
                                  flags, *out, static_cast<hipStream_t>(stream),
                                  &unsupported);
   if (unsupported) {
-    return fail(OGS_E_UNSUPPORTED, "topology too large for the LDS KSP path");
+    return fail(OGS_E_UNSUPPORTED, "degree > OGS_MAX_DEGREE for the exact-order KSP path");
   }
   return e == hipSuccess ? OGS_OK : hipFail(e, "ksp launch");
 }
@@ -369,7 +375,7 @@ int ogs_ksp2_paths(const ogs_graph* graph, const ogs_unit* sources,
                                   flags, *k1, *k2,
                                   static_cast<hipStream_t>(stream), &unsupported);
   if (unsupported) {
-    return fail(OGS_E_UNSUPPORTED, "topology too large for the LDS KSP path");
+    return fail(OGS_E_UNSUPPORTED, "degree > OGS_MAX_DEGREE for the exact-order KSP path");
   }
   return e == hipSuccess ? OGS_OK : hipFail(e, "ksp2 launch");
 }

@@ -17,12 +17,16 @@
 //      resumes its scan from the last (dist, pred, slot) key it tried.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
+#include <type_traits>
 
 #include "openr_gpu.h"
 #include "spf_core.h"
 
 namespace ogs {
+
+constexpr uint32_t kExactRowK = OGS_MAX_DEGREE;  // exact-order row staging
 
 // 8 B per recursion level: the last edge (node -> pred) chosen at this frame
 // is both the path edge once the recursion below it succeeds and the resume
@@ -356,12 +360,513 @@ hipError_t ksp_launch(const ogs_graph& g, const ogs_path_unit* units,
   return hipGetLastError();
 }
 
+// ---- HBM-state KSP: units past the LDS budget, and the exact order -------
+// The LDS paths above hold a unit's distances, link bitsets and trace stack
+// in LDS (<= 160 kB per unit). Past that -- areas of tens of thousands of
+// nodes (LinkState::getKthPaths has no size bound) -- and
+// for zero / negative link metrics, where the reference's settle order
+// decides pathLinks, the unit's state lives in HBM scratch:
+//  * fixpoint domain (metrics >= 1): one 1024-thread workgroup per unit,
+//    frontier rounds as in spf_global.hip (atomics in L2, agent-scope
+//    fences between rounds); pathLinks(v) order = (dist, id) of the
+//    predecessor, then its CSR row;
+//  * exact domain (OGS_F_EXACT_ORDER): one wavefront per unit replays the
+//    DijkstraQ extraction order (as spf_exact.hip) and records each node's
+//    settle rank. runSpf (LinkState.cpp:720-820) appends link (u, v) to
+//    pathLinks(v) when u is settled before v, relaxes and u's metric + w <=
+//    v's current metric, and clears the list on a strict improvement; the
+//    entries that survive are exactly the links with rank(u) < rank(v), u
+//    relaxing and d(u) + w == d(v) in wrapping u64 arithmetic (an entry
+//    added before the last improvement has d(u) + w > d(v)), in (rank(u),
+//    u's row) order.
+// Both trace on one wavefront with a two-word key (trace_paths_wave's scan).
+constexpr int kKspHbmBlock = 1024;
+constexpr uint32_t kRankNew = 0xFFFFFFFFu;   // never inserted
+constexpr uint32_t kRankOpen = 0xFFFFFFFEu;  // in the open list
+int g_kspHbm = 0;  // "ksp_hbm" option: 1 = every KSP unit on the HBM path
+
+hipError_t workspace(size_t bytes, hipStream_t stream, void** out);
+
+__device__ __forceinline__ void hbm_block_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+}
+
+__device__ __forceinline__ void hbm_wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+// LinkStateMetric of an edge in the exact domain: the stored i32 sign-
+// extended to u64 (LinkState.cpp:77-78); sums wrap like the reference's.
+__device__ __forceinline__ uint64_t ksp_exact_weight(uint64_t x) {
+  return static_cast<uint64_t>(static_cast<int64_t>(static_cast<int32_t>(
+      static_cast<uint32_t>(x >> 32))));
+}
+
+// Fixpoint-domain distances with the unit's state in HBM (whole workgroup).
+template <typename D, bool MASKED>
+__device__ void frontier_dist_hbm(uint32_t N, uint32_t s, const UnitCsr& c,
+                                  const uint8_t* __restrict__ nflags, D* dist,
+                                  uint32_t* stamp, uint32_t* q0, uint32_t* q1,
+                                  uint32_t* qcnt, const uint32_t* ignore) {
+  constexpr D kInf = DistInf<D>::value;
+  const int tid = threadIdx.x;
+  for (uint32_t v = tid; v < N; v += kKspHbmBlock) {
+    dist[v] = (v == s) ? D(0) : kInf;
+    stamp[v] = 0u;
+  }
+  if (tid == 0) {
+    q1[0] = s;  // round r's list: buffer r & 1, count slot r % 3
+    qcnt[0] = 0u;
+    qcnt[1] = 1u;
+    qcnt[2] = 0u;
+  }
+  hbm_block_sync();
+  uint32_t n = 1;
+  for (uint32_t r = 1; n; ++r) {
+    if (tid == 0) qcnt[(r + 2) % 3] = 0u;
+    const uint32_t* cur = (r & 1) ? q1 : q0;
+    uint32_t* nxt = (r & 1) ? q0 : q1;
+    for (uint32_t i = tid; i < n; i += kKspHbmBlock) {
+      const uint32_t v = cur[i];
+      if (v != s && (nflags[v] & OGS_NODE_OVERLOADED)) continue;  // 741-752
+      const D dv = dist[v];
+      const uint32_t rEnd = c.rowp[v + 1];
+      for (uint32_t e = c.rowp[v]; e < rEnd; ++e) {
+        const uint64_t ed = c.edg[e];
+        const uint32_t lo = static_cast<uint32_t>(ed);
+        if (lo & OGS_EDGE_DOWN) continue;
+        if constexpr (MASKED) {
+          const uint32_t l = link_id(c, e, lo);
+          if ((ignore[l >> 5] >> (l & 31u)) & 1u) continue;
+        }
+        const uint32_t t = edge_dst(lo);
+        const D cand = dv + static_cast<D>(static_cast<uint32_t>(ed >> 32));
+        if (cand < dist[t] && cand < atomicMin(&dist[t], cand)) {
+          if (atomicMax(&stamp[t], r + 1) < r + 1) {
+            nxt[atomicAdd(&qcnt[(r + 1) % 3], 1u)] = t;
+          }
+        }
+      }
+    }
+    hbm_block_sync();
+    n = qcnt[(r + 1) % 3];
+    __syncthreads();  // every thread has read the count before it is reset
+  }
+}
+
+// Exact-domain distances + settle ranks (one wavefront; HBM state). The
+// unit's rows are staged in LDS one settled node at a time (degree <=
+// OGS_MAX_DEGREE); parallel links to one neighbour collapse to their minimum
+// first (the sequential loop reaches the same key).
+template <bool MASKED>
+__device__ void exact_dist_hbm(uint32_t N, uint32_t s, const UnitCsr& c,
+                               const uint8_t* __restrict__ nflags, uint64_t* key,
+                               uint32_t* rank, uint32_t* open, const uint32_t* ignore,
+                               uint32_t* rowT, uint64_t* rowC, uint8_t* rowV, int lane) {
+  constexpr uint64_t kInf = ~0ull;
+  for (uint32_t v = lane; v < N; v += 64) {
+    key[v] = kInf;
+    rank[v] = kRankNew;
+  }
+  hbm_wave_sync();
+  if (lane == 0) {
+    key[s] = 0;
+    rank[s] = kRankOpen;
+    open[0] = s;
+  }
+  hbm_wave_sync();
+  uint32_t nOpen = 1, step = 0;
+  while (nOpen) {
+    // extractMin: smallest (key, id) over the open list (LinkState.h:618-626)
+    uint64_t bk = kInf;
+    uint32_t bv = 0xFFFFFFFFu, bi = 0;
+    for (uint32_t i = lane; i < nOpen; i += 64) {
+      const uint32_t v = open[i];
+      const uint64_t k = key[v];
+      if (k < bk || (k == bk && v < bv)) {
+        bk = k;
+        bv = v;
+        bi = i;
+      }
+    }
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) {
+      const uint64_t ok = __shfl_xor(bk, d, 64);
+      const uint32_t ov = __shfl_xor(bv, d, 64);
+      const uint32_t oi = __shfl_xor(bi, d, 64);
+      if (ok < bk || (ok == bk && ov < bv)) {
+        bk = ok;
+        bv = ov;
+        bi = oi;
+      }
+    }
+    const uint32_t u = bv;
+    const uint64_t du = bk;
+    hbm_wave_sync();
+    if (lane == 0) {
+      open[bi] = open[nOpen - 1];
+      rank[u] = step;
+    }
+    --nOpen;
+    ++step;
+    hbm_wave_sync();
+    if (u != s && (nflags[u] & OGS_NODE_OVERLOADED)) continue;  // 741-752
+    const uint32_t b = c.rowp[u], m = c.rowp[u + 1] - b;
+    for (uint32_t j = lane; j < m; j += 64) {
+      const uint64_t x = c.edg[b + j];
+      const uint32_t lo = static_cast<uint32_t>(x);
+      const uint32_t t = edge_dst(lo);
+      bool ok = !(lo & OGS_EDGE_DOWN) && rank[t] >= kRankOpen;  // 762-763
+      if constexpr (MASKED) {
+        if (ok) {
+          const uint32_t l = link_id(c, b + j, lo);
+          ok = !((ignore[l >> 5] >> (l & 31u)) & 1u);
+        }
+      }
+      rowT[j] = t;
+      rowC[j] = du + ksp_exact_weight(x);  // wraps like the reference's u64
+      rowV[j] = ok;
+    }
+    hbm_wave_sync();
+    for (uint32_t j0 = 0; j0 < m; j0 += 64) {  // wave-uniform trip count
+      const uint32_t j = j0 + lane;
+      bool append = false;
+      uint32_t t = 0;
+      if (j < m && rowV[j]) {
+        t = rowT[j];
+        uint64_t cc = rowC[j];
+        bool rep = true;  // lowest valid slot of u's row leading to t
+        for (uint32_t k = 0; k < m; ++k) {
+          if (k == j || !rowV[k] || rowT[k] != t) continue;
+          if (k < j) rep = false;
+          if (rowC[k] < cc) cc = rowC[k];
+        }
+        if (rep) {
+          if (rank[t] == kRankNew) {  // insertNode(t, c)
+            key[t] = cc;
+            rank[t] = kRankOpen;
+            append = true;
+          } else if (key[t] > cc) {  // strictly better (791-795)
+            key[t] = cc;
+          }
+        }
+      }
+      const uint64_t ball = __ballot(append);
+      if (append) {
+        const uint32_t at = nOpen + __builtin_amdgcn_mbcnt_hi(
+            uint32_t(ball >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(ball), 0u));
+        open[at] = t;
+      }
+      nOpen += __popcll(ball);
+    }
+    hbm_wave_sync();
+  }
+}
+
+// The greedy trace (trace_paths_wave) over HBM state with a two-word key:
+// fixpoint (dist(u), u << 9 | slot), exact (rank(u), slot).
+template <typename D, bool EXACT, bool MASKED>
+__device__ uint32_t trace_paths_hbm(const UnitCsr& csr, const D* dist, const uint32_t* rank,
+                                    uint32_t s, uint32_t t, uint32_t* visited, Frame* stack,
+                                    const uint32_t* ignore, const ogs_path_out& out,
+                                    size_t row, uint32_t* pathMask, int lane) {
+  constexpr D kInf = DistInf<D>::value;
+  constexpr uint64_t kNoneHi = ~0ull;
+  constexpr uint32_t kNoneLo = 0xFFFFFFFFu;
+  auto less = [](uint64_t ah, uint32_t al, uint64_t bh, uint32_t bl) {
+    return ah < bh || (ah == bh && al < bl);
+  };
+  auto keyOf = [&](uint32_t u, uint32_t slot, uint64_t& hi, uint32_t& lo) {
+    if constexpr (EXACT) {
+      hi = rank[u];
+      lo = slot;
+    } else {
+      hi = static_cast<uint64_t>(dist[u]);
+      lo = (u << 9) | slot;
+    }
+  };
+  uint32_t* pathLen = out.path_len + row * out.max_paths;
+  uint32_t* pathEdges = out.path_edges + row * out.max_edges;
+  uint32_t nPaths = 0, nEdges = 0, status = 0;
+  const bool reachable = (s != t) && (EXACT ? rank[t] < kRankOpen : dist[t] != kInf);
+  while (reachable) {
+    int sp = 0;
+    if (lane == 0) stack[0] = Frame{t, 0xFFFFFFFFu};
+    hbm_wave_sync();
+    bool found = false;
+    while (sp >= 0) {
+      const Frame f = stack[sp];
+      const uint32_t v = f.node;
+      const D dv = dist[v];
+      const uint32_t rv = EXACT ? rank[v] : 0u;
+      const bool fresh = f.edge == 0xFFFFFFFFu;
+      uint64_t lastHi = 0;
+      uint32_t lastLo = 0;
+      if (!fresh) {
+        const uint32_t llo = static_cast<uint32_t>(csr.edg[f.edge]);
+        keyOf(edge_dst(llo), edge_rslot(llo), lastHi, lastLo);
+      }
+      uint64_t bHi = kNoneHi;
+      uint32_t bLo = kNoneLo, be = 0xFFFFFFFFu;
+      const uint32_t rEnd = csr.rowp[v + 1];
+      for (uint32_t eb = csr.rowp[v]; eb < rEnd; eb += 64) {
+        const uint32_t e = eb + uint32_t(lane);
+        uint64_t kh = kNoneHi;
+        uint32_t kl = kNoneLo;
+        if (e < rEnd) {
+          const uint64_t ed = csr.edg[e];
+          const uint32_t lo = static_cast<uint32_t>(ed);
+          const uint32_t u = edge_dst(lo);
+          bool ok = !(lo & OGS_EDGE_DOWN) && !((lo & OGS_EDGE_DST_OVERLOADED) && u != s);
+          if constexpr (MASKED) {
+            if (ok) {
+              const uint32_t l = link_id(csr, e, lo);
+              ok = !((ignore[l >> 5] >> (l & 31u)) & 1u);
+            }
+          }
+          if (ok) {
+            const D du = dist[u];
+            bool tight;
+            if constexpr (EXACT) {
+              tight = rank[u] < rv && du + ksp_exact_weight(ed) == dv;
+            } else {
+              tight = du != kInf && du + static_cast<D>(static_cast<uint32_t>(ed >> 32)) == dv;
+            }
+            if (tight) {
+              uint64_t h;
+              uint32_t l;
+              keyOf(u, edge_rslot(lo), h, l);
+              if (fresh || less(lastHi, lastLo, h, l)) {
+                kh = h;
+                kl = l;
+              }
+            }
+          }
+        }
+        uint64_t mh = kh;
+        uint32_t ml = kl;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+          const uint32_t a = __shfl_xor(static_cast<uint32_t>(mh), o);
+          const uint32_t b = __shfl_xor(static_cast<uint32_t>(mh >> 32), o);
+          const uint32_t c = __shfl_xor(ml, o);
+          const uint64_t oh = (uint64_t(b) << 32) | a;
+          if (less(oh, c, mh, ml)) {
+            mh = oh;
+            ml = c;
+          }
+        }
+        if (less(mh, ml, bHi, bLo)) {
+          const uint64_t who = __ballot(kh == mh && kl == ml);
+          bHi = mh;
+          bLo = ml;
+          be = __shfl(e, int(__builtin_ctzll(who)));
+        }
+      }
+      if (be == 0xFFFFFFFFu) {  // exhausted: this recursion level fails
+        --sp;
+        continue;
+      }
+      const uint32_t blo = static_cast<uint32_t>(csr.edg[be]);
+      const uint32_t bu = edge_dst(blo);
+      if (lane == 0) stack[sp].edge = be;  // resume key (+ path edge on success)
+      const uint32_t l = link_id(csr, be, blo);
+      const bool seen = (visited[l >> 5] >> (l & 31u)) & 1u;
+      hbm_wave_sync();
+      if (seen) continue;  // already used
+      if (lane == 0) visited[l >> 5] |= 1u << (l & 31u);
+      if (bu == s) {
+        hbm_wave_sync();
+        found = true;
+        break;
+      }
+      ++sp;
+      if (lane == 0) stack[sp] = Frame{bu, 0xFFFFFFFFu};
+      hbm_wave_sync();
+    }
+    if (!found) break;
+    if (nPaths >= out.max_paths || nEdges + uint32_t(sp + 1) > out.max_edges) {
+      status = 1;  // output capacity exceeded
+      break;
+    }
+    for (int i = sp; i >= 0; --i) {
+      const uint32_t e = stack[i].edge;
+      if (lane == 0) {
+        pathEdges[nEdges] = e - csr.eBase;
+        if (pathMask) {
+          const uint32_t l = link_id(csr, e, static_cast<uint32_t>(csr.edg[e]));
+          pathMask[l >> 5] |= 1u << (l & 31u);
+        }
+      }
+      ++nEdges;
+    }
+    if (lane == 0) pathLen[nPaths] = uint32_t(sp + 1);
+    ++nPaths;
+    hbm_wave_sync();
+  }
+  return nPaths | (status << 31);
+}
+
+// Per-unit HBM scratch: dist | stamp or rank | list 0 (open list) | list 1 |
+// visited | mask | stack, each 256-B aligned.
+struct KspHbmLayout {
+  size_t dist, aux, q0, q1, visited, mask, stack, total;
+  __host__ __device__ static KspHbmLayout make(uint64_t N, uint64_t E, uint64_t dsize) {
+    auto r = [](uint64_t x) { return (x + 255) & ~uint64_t(255); };
+    const uint64_t lw = (E + 31) / 32 + 1;
+    KspHbmLayout L;
+    size_t o = 0;
+    L.dist = o;
+    o += r(N * dsize);
+    L.aux = o;
+    o += r(N * 4);
+    L.q0 = o;
+    o += r(N * 4);
+    L.q1 = o;
+    o += r(N * 4);
+    L.visited = o;
+    o += r(lw * 4);
+    L.mask = o;
+    o += r(lw * 4);
+    L.stack = o;
+    o += r(N * sizeof(Frame));
+    L.total = o;
+    return L;
+  }
+};
+
+// TWO: the KSP2 batch (k = 1 into o1, k = 2 with the k = 1 links ignored
+// into o2; units carry their source index as in ksp2_kernel). Otherwise one
+// getKthPaths call per unit (masks = its linksToIgnore when MASKED) into o1.
+template <typename D, bool EXACT, bool TWO, bool MASKED>
+__global__ __launch_bounds__(EXACT ? 64 : kKspHbmBlock) void ksp_hbm_kernel(
+    ogs_graph g, const ogs_unit* __restrict__ sources, int nSources,
+    const ogs_path_unit* __restrict__ units, uint32_t uBase,
+    const uint32_t* __restrict__ masks, uint32_t maskWords, ogs_path_out o1,
+    ogs_path_out o2, char* __restrict__ scratch) {
+  static_assert(!EXACT || sizeof(D) == 8, "exact order: 64-bit distances");
+  const int tid = threadIdx.x, lane = tid & 63;
+  const uint32_t uidx = uBase + blockIdx.x;
+  const ogs_path_unit unit = units[uidx];
+  if constexpr (TWO) {
+    const uint32_t slot = unit.reserved;
+    if (slot >= uint32_t(nSources) || sources[slot].topo != unit.topo ||
+        sources[slot].src != unit.src) {
+      if (tid == 0) {  // malformed unit: reported, never traced
+        o1.path_count[uidx] = 0xC0000000u;
+        o2.path_count[uidx] = 0xC0000000u;
+      }
+      return;
+    }
+  }
+  const uint32_t nb = g.node_base[unit.topo];
+  const uint32_t N = g.node_base[unit.topo + 1] - nb;
+  const uint32_t* __restrict__ gRow = g.row_ptr + nb;
+  const uint32_t e0 = gRow[0];
+  const uint32_t E = gRow[N] - e0;
+  const uint8_t* __restrict__ nflags = g.node_flags + nb;
+  const UnitCsr csr{gRow, g.edges, e0};
+  const uint32_t s = unit.src, t = unit.dest;
+  const KspHbmLayout L = KspHbmLayout::make(uint32_t(g.max_nodes), uint32_t(g.max_edges), sizeof(D));
+  char* base = scratch + size_t(blockIdx.x) * L.total;
+  D* dist = reinterpret_cast<D*>(base + L.dist);
+  uint32_t* aux = reinterpret_cast<uint32_t*>(base + L.aux);
+  uint32_t* q0 = reinterpret_cast<uint32_t*>(base + L.q0);
+  uint32_t* q1 = reinterpret_cast<uint32_t*>(base + L.q1);
+  uint32_t* visited = reinterpret_cast<uint32_t*>(base + L.visited);
+  uint32_t* mask = reinterpret_cast<uint32_t*>(base + L.mask);
+  Frame* stack = reinterpret_cast<Frame*>(base + L.stack);
+  __shared__ uint32_t qcnt[3];
+  __shared__ uint32_t bcast;
+  __shared__ uint32_t rowT[EXACT ? kExactRowK : 1];
+  __shared__ uint64_t rowC[EXACT ? kExactRowK : 1];
+  __shared__ uint8_t rowV[EXACT ? kExactRowK : 1];
+  const uint32_t linkWords = (E + 31) / 32;
+  const int nt = EXACT ? 64 : kKspHbmBlock;
+  for (uint32_t i = tid; i < linkWords; i += nt) {
+    visited[i] = 0u;
+    if (TWO) mask[i] = 0u;
+  }
+  const uint32_t* ign = MASKED ? masks + size_t(uidx) * maskWords : nullptr;
+  auto spf = [&](const uint32_t* ignore, auto maskedTag) {
+    constexpr bool M = decltype(maskedTag)::value;
+    if constexpr (EXACT) {
+      exact_dist_hbm<M>(N, s, csr, nflags, reinterpret_cast<uint64_t*>(dist), aux, q0,
+                        ignore, rowT, rowC, rowV, lane);
+    } else {
+      frontier_dist_hbm<D, M>(N, s, csr, nflags, dist, aux, q0, q1, qcnt, ignore);
+    }
+    hbm_block_sync();
+  };
+  spf(ign, std::integral_constant<bool, MASKED>{});
+  uint32_t c1 = 0;
+  if (tid < 64) {
+    c1 = trace_paths_hbm<D, EXACT, MASKED>(csr, dist, aux, s, t, visited, stack, ign, o1,
+                                           uidx, TWO ? mask : nullptr, lane);
+    if (lane == 0) o1.path_count[uidx] = c1;
+  }
+  if constexpr (TWO) {
+    if (tid == 0) bcast = c1;
+    hbm_block_sync();
+    c1 = bcast;
+    // k = 1 found nothing: linksToIgnore is empty, k = 2 finds nothing
+    // either; a k = 1 overflow leaves the mask incomplete (reported)
+    if (c1 == 0u || (c1 >> 31)) {
+      if (tid == 0) o2.path_count[uidx] = c1 & 0x80000000u;
+      return;
+    }
+    for (uint32_t i = tid; i < linkWords; i += nt) visited[i] = 0u;
+    hbm_block_sync();
+    spf(mask, std::integral_constant<bool, true>{});
+    if (tid < 64) {
+      const uint32_t c2 = trace_paths_hbm<D, EXACT, true>(csr, dist, aux, s, t, visited, stack,
+                                                          mask, o2, uidx, nullptr, lane);
+      if (lane == 0) o2.path_count[uidx] = c2;
+    }
+  }
+}
+
+// Launches the HBM-state path over n units in chunks whose scratch stays
+// below kKspHbmScratch.
+template <typename D, bool EXACT, bool TWO, bool MASKED>
+hipError_t launch_ksp_hbm(const ogs_graph& g, const ogs_unit* sources, int nSources,
+                          const ogs_path_unit* units, int nUnits, const uint32_t* masks,
+                          uint32_t maskWords, const ogs_path_out& o1, const ogs_path_out& o2,
+                          hipStream_t stream) {
+  constexpr size_t kKspHbmScratch = size_t(4) << 30;
+  const size_t per = KspHbmLayout::make(uint32_t(g.max_nodes), uint32_t(g.max_edges),
+                                        sizeof(D)).total;
+  size_t chunk = kKspHbmScratch / per;
+  if (chunk < 1) chunk = 1;
+  if (chunk > size_t(nUnits)) chunk = size_t(nUnits);
+  void* ws = nullptr;
+  hipError_t e = workspace(chunk * per, stream, &ws);
+  if (e != hipSuccess) return e;
+  for (size_t u0 = 0; u0 < size_t(nUnits); u0 += chunk) {
+    const size_t n = std::min(chunk, size_t(nUnits) - u0);
+    hipLaunchKernelGGL((ksp_hbm_kernel<D, EXACT, TWO, MASKED>), dim3(uint32_t(n)),
+                       dim3(EXACT ? 64 : kKspHbmBlock), 0, stream, g, sources, nSources, units,
+                       uint32_t(u0), masks, maskWords, o1, o2, static_cast<char*>(ws));
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
 template <typename D, bool MASKED>
 hipError_t ksp_dispatch(const ogs_graph& g, const ogs_path_unit* units,
                         int nUnits, const uint32_t* masks, uint32_t maskWords,
                         const ogs_path_out& out, hipStream_t stream,
                         int* unsupported) {
   const uint64_t N = g.max_nodes, E = g.max_edges;
+  if (g_kspHbm) {
+    return launch_ksp_hbm<D, false, false, MASKED>(g, nullptr, 0, units, nUnits, masks,
+                                                   maskWords, out, out, stream);
+  }
   const uint64_t core = align16(N * sizeof(D)) + align16((E + 31) / 32 * 4) +
       align16(N * sizeof(Frame));
   const uint64_t staged = core + align16((N + 1) * 4) + align16(E * 8);
@@ -380,8 +885,9 @@ hipError_t ksp_dispatch(const ogs_graph& g, const ogs_path_unit* units,
                                                 maskWords, out, uint32_t(core),
                                                 stream);
   }
-  *unsupported = 1;
-  return hipSuccess;
+  (void)unsupported;  // past LDS: state in HBM
+  return launch_ksp_hbm<D, false, false, MASKED>(g, nullptr, 0, units, nUnits, masks,
+                                                 maskWords, out, out, stream);
 }
 
 hipError_t launch_ksp(const ogs_graph& g, const ogs_path_unit* units,
@@ -389,6 +895,16 @@ hipError_t launch_ksp(const ogs_graph& g, const ogs_path_unit* units,
                       uint32_t flags, const ogs_path_out& out,
                       hipStream_t stream, int* unsupported) {
   const bool wide = flags & OGS_F_WIDE_METRIC;
+  if (flags & OGS_F_EXACT_ORDER) {
+    if (!wide || g.max_degree > int(kExactRowK)) {
+      *unsupported = 1;
+      return hipSuccess;
+    }
+    return masks ? launch_ksp_hbm<uint64_t, true, false, true>(g, nullptr, 0, units, nUnits,
+                                                               masks, maskWords, out, out, stream)
+                 : launch_ksp_hbm<uint64_t, true, false, false>(g, nullptr, 0, units, nUnits,
+                                                                nullptr, 0, out, out, stream);
+  }
   if (masks) {
     return wide ? ksp_dispatch<uint64_t, true>(g, units, nUnits, masks,
                                                maskWords, out, stream,
@@ -710,6 +1226,10 @@ hipError_t ksp2_dispatch(const ogs_graph& g, const ogs_unit* sources,
                          hipStream_t stream, int* unsupported) {
   const uint64_t N = g.max_nodes, E = g.max_edges;
   constexpr uint64_t kBudget = 160 * 1024;
+  if (g_kspHbm) {
+    return launch_ksp_hbm<D, false, true, false>(g, sources, nSources, units, nUnits,
+                                                 nullptr, 0, o1, o2, stream);
+  }
   void* ws = nullptr;
   hipError_t e = workspace(size_t(nSources) * size_t(N) * sizeof(D), stream, &ws);
   if (e != hipSuccess) return e;
@@ -724,9 +1244,10 @@ hipError_t ksp2_dispatch(const ogs_graph& g, const ogs_unit* sources,
   if (st < 0) st = ksp2_lds_bytes<D>(N, E, 2, q) * 3 <= kBudget ? 2 : 1;
   while (st > 0 && ksp2_lds_bytes<D>(N, E, st, q) > kBudget) --st;
   const uint64_t b = ksp2_lds_bytes<D>(N, E, st, q);
-  if (b > kBudget) {
-    *unsupported = 1;
-    return hipSuccess;
+  if (b > kBudget) {  // past LDS: state in HBM
+    (void)unsupported;
+    return launch_ksp_hbm<D, false, true, false>(g, sources, nSources, units, nUnits,
+                                                 nullptr, 0, o1, o2, stream);
   }
 #define OGS_KSP2(ST_, Q_)                                                      \
   return ksp2_launch<D, kBlock, ST_, Q_>(g, sources, nSources, d, units, nUnits, \
@@ -747,6 +1268,14 @@ hipError_t launch_ksp2(const ogs_graph& g, const ogs_unit* sources,
                        uint32_t flags, const ogs_path_out& o1,
                        const ogs_path_out& o2, hipStream_t stream,
                        int* unsupported) {
+  if (flags & OGS_F_EXACT_ORDER) {
+    if (!(flags & OGS_F_WIDE_METRIC) || g.max_degree > int(kExactRowK)) {
+      *unsupported = 1;
+      return hipSuccess;
+    }
+    return launch_ksp_hbm<uint64_t, true, true, false>(g, sources, nSources, units, nUnits,
+                                                       nullptr, 0, o1, o2, stream);
+  }
   return (flags & OGS_F_WIDE_METRIC)
       ? ksp2_dispatch<uint64_t>(g, sources, nSources, units, nUnits, o1, o2,
                                 stream, unsupported)
