@@ -216,6 +216,19 @@ def run_g1(args, rank):
            "route_digest": f"{digest:016x}",
            "note": "one ogs_spf_routes launch (global-state path) for 64 sources incl. "
                    "the launch-to-sync latency; median of reps"}
+    # roofline of the launch (spf_global_kernel + route_global_kernel): the
+    # 64 units share one topology (S = 64), each writes dist / next-hop sets
+    # and its RouteDb; time = the launch's wall time
+    h = br.host_arrays()
+    E, W = len(h["edges"]), br.nh_words()
+    bpu = algorithmic_bytes_per_unit(N, E, N, N, W, W, S=U)
+    achieved = bpu * U / sec / 1e9
+    out["roofline"] = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                       "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
+                       "traffic": None, "bytes_alg_per_unit": round(bpu, 1),
+                       "kernel": "spf_global_kernel + route_global_kernel (one launch; "
+                                 "latency bound: frontier rounds of one workgroup per unit)"}
+    set_traffic(out, "g1", "global_kernel")
     want = GOLDEN.get("g1")
     out["golden"] = "n/a" if want is None else ("match" if f"{digest:016x}" == want
                                                  else "MISMATCH")

@@ -17,6 +17,7 @@ extern int g_msGroup;
 extern int g_routeStream;
 extern int g_spfFrontier;
 extern int g_spfGlobal;
+extern int g_spfGlobalSync;
 extern int g_spfQueue;
 extern int g_spfNinfo;
 extern int g_kspQueue;
@@ -194,6 +195,11 @@ int ogs_set_option(const char* name, int64_t value) {
   if (std::strcmp(name, "ksp_queue") == 0) {
     if (value != 0 && value != 1) return fail(OGS_E_INVALID, "ksp_queue must be 0 or 1");
     ogs::g_kspQueue = int(value);
+    return OGS_OK;
+  }
+  if (std::strcmp(name, "spf_global_sync") == 0) {
+    if (value != 0 && value != 1) return fail(OGS_E_INVALID, "spf_global_sync must be 0 or 1");
+    ogs::g_spfGlobalSync = int(value);
     return OGS_OK;
   }
   if (std::strcmp(name, "ksp_hbm") == 0) {

@@ -387,10 +387,19 @@ int g_kspHbm = 0;  // "ksp_hbm" option: 1 = every KSP unit on the HBM path
 
 hipError_t workspace(size_t bytes, hipStream_t stream, void** out);
 
+// A unit's workgroup runs on one CU: its HBM state stays in that XCD's L2
+// for the whole launch. Rounds end with every wave's stores drained and a
+// barrier; state written in this launch is read back through sc1 (L2-served,
+// L1-bypassing) loads -- the L1 may hold lines that L2 atomics have since
+// changed (MI355X_MICROARCH.md, inter-workgroup visibility).
 __device__ __forceinline__ void hbm_block_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+}
+
+template <typename T>
+__device__ __forceinline__ T ld_l2(const T* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __device__ __forceinline__ void hbm_wave_sync() {
@@ -431,9 +440,9 @@ __device__ void frontier_dist_hbm(uint32_t N, uint32_t s, const UnitCsr& c,
     const uint32_t* cur = (r & 1) ? q1 : q0;
     uint32_t* nxt = (r & 1) ? q0 : q1;
     for (uint32_t i = tid; i < n; i += kKspHbmBlock) {
-      const uint32_t v = cur[i];
+      const uint32_t v = ld_l2(cur + i);
       if (v != s && (nflags[v] & OGS_NODE_OVERLOADED)) continue;  // 741-752
-      const D dv = dist[v];
+      const D dv = ld_l2(dist + v);
       const uint32_t rEnd = c.rowp[v + 1];
       for (uint32_t e = c.rowp[v]; e < rEnd; ++e) {
         const uint64_t ed = c.edg[e];
@@ -445,7 +454,7 @@ __device__ void frontier_dist_hbm(uint32_t N, uint32_t s, const UnitCsr& c,
         }
         const uint32_t t = edge_dst(lo);
         const D cand = dv + static_cast<D>(static_cast<uint32_t>(ed >> 32));
-        if (cand < dist[t] && cand < atomicMin(&dist[t], cand)) {
+        if (cand < ld_l2(dist + t) && cand < atomicMin(&dist[t], cand)) {
           if (atomicMax(&stamp[t], r + 1) < r + 1) {
             nxt[atomicAdd(&qcnt[(r + 1) % 3], 1u)] = t;
           }
@@ -585,14 +594,14 @@ __device__ uint32_t trace_paths_hbm(const UnitCsr& csr, const D* dist, const uin
       hi = rank[u];
       lo = slot;
     } else {
-      hi = static_cast<uint64_t>(dist[u]);
+      hi = static_cast<uint64_t>(ld_l2(dist + u));
       lo = (u << 9) | slot;
     }
   };
   uint32_t* pathLen = out.path_len + row * out.max_paths;
   uint32_t* pathEdges = out.path_edges + row * out.max_edges;
   uint32_t nPaths = 0, nEdges = 0, status = 0;
-  const bool reachable = (s != t) && (EXACT ? rank[t] < kRankOpen : dist[t] != kInf);
+  const bool reachable = (s != t) && (EXACT ? rank[t] < kRankOpen : ld_l2(dist + t) != kInf);
   while (reachable) {
     int sp = 0;
     if (lane == 0) stack[0] = Frame{t, 0xFFFFFFFFu};
@@ -601,7 +610,7 @@ __device__ uint32_t trace_paths_hbm(const UnitCsr& csr, const D* dist, const uin
     while (sp >= 0) {
       const Frame f = stack[sp];
       const uint32_t v = f.node;
-      const D dv = dist[v];
+      const D dv = ld_l2(dist + v);
       const uint32_t rv = EXACT ? rank[v] : 0u;
       const bool fresh = f.edge == 0xFFFFFFFFu;
       uint64_t lastHi = 0;
@@ -629,7 +638,7 @@ __device__ uint32_t trace_paths_hbm(const UnitCsr& csr, const D* dist, const uin
             }
           }
           if (ok) {
-            const D du = dist[u];
+            const D du = ld_l2(dist + u);
             bool tight;
             if constexpr (EXACT) {
               tight = rank[u] < rv && du + ksp_exact_weight(ed) == dv;

@@ -11,10 +11,15 @@
 // are in HBM (the caller's output rows or the workspace), so there is no
 // size limit but the 21-bit node ids of the edge encoding. One workgroup of
 // 1024 threads per unit walks the frontier list of the round; relaxations
-// are L2 atomics (atomicMin / atomicOr); after each workgroup barrier an
-// agent-scope acquire fence invalidates the CU's vector L1 so the next
-// round reads what the atomics left in L2. Every round costs one barrier
-// and touches only the rows of the nodes changed in the previous round.
+// are L2 atomics (atomicMin / atomicOr). A unit's workgroup runs on ONE CU,
+// so its state never leaves that XCD's L2 until the kernel ends: a round
+// ends with every wave's stores drained (s_waitcnt vmcnt(0)) and a workgroup
+// barrier, and every read of state written in this launch is an L2-served
+// `sc1` load (L1 bypassed: MI355X_MICROARCH.md, inter-workgroup visibility
+// table) -- no L2 write-back / L1 invalidate per round. (The first form
+// used agent-scope release + acquire fences per round, ~3.5 us of cache
+// maintenance each: option "spf_global_sync" 0 keeps it for A/B.) Every
+// round touches only the rows of the nodes changed in the previous round.
 //
 // Routes: route_global.h, one thread per (unit, prefix) against the unit's
 // state in HBM. u32 or u64 distances (OGS_F_WIDE_METRIC).
@@ -31,10 +36,29 @@ namespace ogs {
 
 constexpr int kGBlock = 1024;
 
+// L2SYNC: stores drained + barrier (state read back through sc1 loads);
+// else agent-scope release / acquire fences around the barrier.
+template <bool L2SYNC>
 __device__ __forceinline__ void round_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-  __syncthreads();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  if constexpr (L2SYNC) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  } else {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+}
+
+// Read of state written earlier in this launch: an sc1 (L2-served) load
+// under L2SYNC, a plain load after the agent acquire otherwise.
+template <bool L2SYNC, typename T>
+__device__ __forceinline__ T ld_state(const T* p) {
+  if constexpr (L2SYNC) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    return *p;
+  }
 }
 
 template <typename D>
@@ -44,7 +68,7 @@ __device__ __forceinline__ D atomic_min_d(D* p, D v) {
 
 // One unit's SPF into HBM. dist[v] (D), nh[w * Sn + v], stamp/q0/q1 scratch
 // rows of this unit (>= N entries each).
-template <typename D, int W>
+template <typename D, int W, bool L2SYNC>
 __global__ __launch_bounds__(kGBlock) void spf_global_kernel(
     ogs_graph g, const ogs_unit* __restrict__ units, uint32_t flags,
     D* __restrict__ oDist, uint32_t* __restrict__ oNh, uint32_t* __restrict__ scratch) {
@@ -80,7 +104,7 @@ __global__ __launch_bounds__(kGBlock) void spf_global_kernel(
     qcnt[1] = 1u;
     qcnt[2] = 0u;
   }
-  round_sync();
+  round_sync<L2SYNC>();
   auto append = [&](uint32_t t, uint32_t r) {
     if (atomicMax(&stamp[t], r + 1) < r + 1) {
       const uint32_t at = atomicAdd(&qcnt[(r + 1) % 3], 1u);
@@ -97,9 +121,9 @@ __global__ __launch_bounds__(kGBlock) void spf_global_kernel(
     if (tid == 0) qcnt[(r + 2) % 3] = 0u;
     const uint32_t* cur = (r & 1) ? q1 : q0;
     for (uint32_t i = tid; i < n; i += kGBlock) {
-      const uint32_t v = cur[i];
+      const uint32_t v = ld_state<L2SYNC>(cur + i);
       if (v != s && (nflags[v] & OGS_NODE_OVERLOADED)) continue;  // 741-752
-      const D dv = dist[v];
+      const D dv = ld_state<L2SYNC>(dist + v);
       const uint32_t b = gRow[v] - e0, m = gRow[v + 1] - e0 - b;
       for (uint32_t j = 0; j < m; ++j) {
         const uint64_t x = edges[b + j];
@@ -107,10 +131,10 @@ __global__ __launch_bounds__(kGBlock) void spf_global_kernel(
         if (lo & OGS_EDGE_DOWN) continue;
         const uint32_t t = edge_dst(lo);
         const D c = dv + weight(x);
-        if (c < dist[t] && c < atomic_min_d(&dist[t], c)) append(t, r);
+        if (c < ld_state<L2SYNC>(dist + t) && c < atomic_min_d(&dist[t], c)) append(t, r);
       }
     }
-    round_sync();
+    round_sync<L2SYNC>();
     n = qcnt[(r + 1) % 3];
     __syncthreads();  // every thread has read the count before it is reset
   }
@@ -118,7 +142,7 @@ __global__ __launch_bounds__(kGBlock) void spf_global_kernel(
   // ---- next-hop phase: the source's row seeds link slots, tight pushes ----
   const uint32_t r0 = r;
   if (tid == 0) qcnt[0] = qcnt[1] = qcnt[2] = 0u;
-  round_sync();
+  round_sync<L2SYNC>();
   {
     const uint32_t b = gRow[s] - e0, m = gRow[s + 1] - e0 - b;
     for (uint32_t j = tid; j < m && j < 32u * W; j += kGBlock) {
@@ -126,42 +150,42 @@ __global__ __launch_bounds__(kGBlock) void spf_global_kernel(
       const uint32_t lo = static_cast<uint32_t>(x);
       if (lo & OGS_EDGE_DOWN) continue;
       const uint32_t t = edge_dst(lo);
-      if (weight(x) == dist[t]) {
+      if (weight(x) == ld_state<L2SYNC>(dist + t)) {
         atomicOr(&nh[(j >> 5) * Sn + t], 1u << (j & 31u));
         append(t, r0);
       }
     }
   }
-  round_sync();
+  round_sync<L2SYNC>();
   n = qcnt[(r0 + 1) % 3];
   __syncthreads();
   for (r = r0 + 1; n; ++r) {
     if (tid == 0) qcnt[(r + 2) % 3] = 0u;
     const uint32_t* cur = (r & 1) ? q1 : q0;
     for (uint32_t i = tid; i < n; i += kGBlock) {
-      const uint32_t v = cur[i];
+      const uint32_t v = ld_state<L2SYNC>(cur + i);
       if (v == s || (nflags[v] & OGS_NODE_OVERLOADED)) continue;
-      const D dv = dist[v];
+      const D dv = ld_state<L2SYNC>(dist + v);
       uint32_t nv[W];
 #pragma unroll
-      for (int w = 0; w < W; ++w) nv[w] = nh[w * Sn + v];
+      for (int w = 0; w < W; ++w) nv[w] = ld_state<L2SYNC>(nh + w * Sn + v);
       const uint32_t b = gRow[v] - e0, m = gRow[v + 1] - e0 - b;
       for (uint32_t j = 0; j < m; ++j) {
         const uint64_t x = edges[b + j];
         const uint32_t lo = static_cast<uint32_t>(x);
         if (lo & OGS_EDGE_DOWN) continue;
         const uint32_t t = edge_dst(lo);
-        if (dv + weight(x) != dist[t]) continue;
+        if (dv + weight(x) != ld_state<L2SYNC>(dist + t)) continue;
         bool add = false;
 #pragma unroll
         for (int k = 0; k < W; ++k) {
-          const uint32_t a = nv[k] & ~nh[k * Sn + t];
+          const uint32_t a = nv[k] & ~ld_state<L2SYNC>(nh + k * Sn + t);
           if (a && (a & ~atomicOr(&nh[k * Sn + t], a))) add = true;
         }
         if (add) append(t, r);
       }
     }
-    round_sync();
+    round_sync<L2SYNC>();
     n = qcnt[(r + 1) % 3];
     __syncthreads();
   }
@@ -172,6 +196,9 @@ hipError_t workspace(size_t bytes, hipStream_t stream, void** out);
 // "spf_global" option: 0 (default) the global path only where the LDS paths
 // cannot hold a unit, 1 every ogs_spf_routes call (A/B, parity tests).
 int g_spfGlobal = 0;
+// "spf_global_sync": 1 (default) rounds end with drained stores + barrier
+// and state is read through sc1 loads; 0 agent-scope fences per round (A/B)
+int g_spfGlobalSync = 1;
 
 // Does the LDS-resident workgroup path fit a unit of this graph? (the last
 // fallback of spf_route.hip: dist + next-hop words, CSR read from L2)
@@ -211,8 +238,13 @@ hipError_t launch_global_w(const ogs_graph& g, const ogs_prefix_table* pt,
   D* dist = out.dist ? static_cast<D*>(out.dist) : reinterpret_cast<D*>(base);
   uint32_t* nh = out.nh ? out.nh : reinterpret_cast<uint32_t*>(base + distBytes);
   uint32_t* scratch = reinterpret_cast<uint32_t*>(base + distBytes + nhBytes);
-  hipLaunchKernelGGL((spf_global_kernel<D, W>), dim3(nUnits), dim3(kGBlock), 0, stream, g,
-                     units, flags, dist, nh, scratch);
+  if (g_spfGlobalSync) {
+    hipLaunchKernelGGL((spf_global_kernel<D, W, true>), dim3(nUnits), dim3(kGBlock), 0, stream,
+                       g, units, flags, dist, nh, scratch);
+  } else {
+    hipLaunchKernelGGL((spf_global_kernel<D, W, false>), dim3(nUnits), dim3(kGBlock), 0, stream,
+                       g, units, flags, dist, nh, scratch);
+  }
   e = hipGetLastError();
   if (e != hipSuccess || !pt || pt->max_prefixes == 0) return e;
   return launch_route_global<D, W>(g, *pt, units, nUnits, flags, dist, nh, out, stream);

@@ -8,3 +8,4 @@ bash tools/gpu_pmc.sh c2 --no-c3 --no-c4 --no-c5 $F --steps 20 --warmup 3 || exi
 bash tools/gpu_pmc.sh c3 --config c3 $F --steps 2 --warmup 1 || exit $?
 bash tools/gpu_pmc.sh c4 --config c4 $F --steps 3 --warmup 1 || exit $?
 bash tools/gpu_pmc.sh c5 --config c5 $F --steps 5 --warmup 1 || exit $?
+bash tools/gpu_pmc.sh g1 --no-c3 --no-c4 --no-c5 --no-cpu-baseline --no-c1 --steps 1 --warmup 1 || exit $?
