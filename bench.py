@@ -482,6 +482,16 @@ def run_c3(args, torch, dist, rank, world, local_rank):
         if world == 1 and ppn == 100:
             log("c3 cpu baseline ...")
             line["cpu_baseline"] = cpu_baseline_c3(N)
+            # f2 beside the reference's serving path: getRouteDbComputed
+            # runs buildRouteDb(node) on the Decision thread (Decision.cpp:
+            # 341-360) -- refcpu's single-source time from the same run
+            # (toThrift not included: a lower bound of the reference's cost)
+            one = line["cpu_baseline"].get("value_1thread")
+            if one:
+                line["serve"]["cpu_baseline"] = {
+                    "value": round(1e3 / (one * N), 1), "unit": "ms per node", "cores": 1,
+                    "kind": "port", "sample": "refcpu buildRouteDb(node) on 1 thread, from "
+                    "this line's cpu_baseline (1-thread sources); toThrift excluded"}
     return line
 
 
@@ -638,6 +648,15 @@ def run_c4(args, torch, dist, rank, world, local_rank):
                     else "spf_frontier_kernel<1, true, true, true")
         if not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline_c4()
+            # f1 beside the reference: Decision::rebuildRoutes per variant =
+            # updateAdjacencyDatabase + buildRouteDb + calculateUpdate (the
+            # refcpu loop measured for cpu_baseline), for all variants
+            one = line["cpu_baseline"]["value_1thread"]
+            line["route_update"]["cpu_baseline"] = {
+                "value": round(C4_VARIANTS / one * 1e3, 1), "unit": "ms for all variants",
+                "cores": 1, "kind": "port",
+                "sample": "refcpu per-variant update + buildRouteDb + calculateUpdate at 1 "
+                          "thread (this line's cpu_baseline), scaled to every variant"}
     return line
 
 
