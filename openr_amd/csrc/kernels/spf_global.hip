@@ -35,6 +35,7 @@
 namespace ogs {
 
 constexpr int kGBlock = 1024;
+constexpr int kGRow = 4;  // row edges per step of a frontier node
 
 // L2SYNC: stores drained + barrier (state read back through sc1 loads);
 // else agent-scope release / acquire fences around the barrier.
@@ -105,11 +106,13 @@ __global__ __launch_bounds__(kGBlock) void spf_global_kernel(
     qcnt[2] = 0u;
   }
   round_sync<L2SYNC>();
+  // t's first push of round r + 1 (stamp claimed): append to that list
+  auto push = [&](uint32_t t, uint32_t r) {
+    const uint32_t at = atomicAdd(&qcnt[(r + 1) % 3], 1u);
+    ((r + 1) & 1 ? q1 : q0)[at] = t;
+  };
   auto append = [&](uint32_t t, uint32_t r) {
-    if (atomicMax(&stamp[t], r + 1) < r + 1) {
-      const uint32_t at = atomicAdd(&qcnt[(r + 1) % 3], 1u);
-      ((r + 1) & 1 ? q1 : q0)[at] = t;
-    }
+    if (atomicMax(&stamp[t], r + 1) < r + 1) push(t, r);
   };
   auto weight = [&](uint64_t x) -> D {
     return hop ? D(1) : D(static_cast<uint32_t>(x >> 32));
@@ -125,13 +128,38 @@ __global__ __launch_bounds__(kGBlock) void spf_global_kernel(
       if (v != s && (nflags[v] & OGS_NODE_OVERLOADED)) continue;  // 741-752
       const D dv = ld_state<L2SYNC>(dist + v);
       const uint32_t b = gRow[v] - e0, m = gRow[v + 1] - e0 - b;
-      for (uint32_t j = 0; j < m; ++j) {
-        const uint64_t x = edges[b + j];
-        const uint32_t lo = static_cast<uint32_t>(x);
-        if (lo & OGS_EDGE_DOWN) continue;
-        const uint32_t t = edge_dst(lo);
-        const D c = dv + weight(x);
-        if (c < ld_state<L2SYNC>(dist + t) && c < atomic_min_d(&dist[t], c)) append(t, r);
+      // kGRow edges at a time, each step's memory operations independent
+      // (edge words, then the targets' dist, then the atomicMins, then the
+      // stamps): one L2 round trip per step instead of one per edge and step
+      for (uint32_t j0 = 0; j0 < m; j0 += kGRow) {
+        uint32_t t[kGRow];
+        D c[kGRow], seen[kGRow];
+        bool ok[kGRow];
+#pragma unroll
+        for (int k = 0; k < kGRow; ++k) {
+          const uint64_t x = j0 + k < m ? edges[b + j0 + k] : uint64_t(OGS_EDGE_DOWN);
+          const uint32_t lo = static_cast<uint32_t>(x);
+          ok[k] = !(lo & OGS_EDGE_DOWN);
+          t[k] = edge_dst(lo);
+          c[k] = dv + weight(x);
+        }
+#pragma unroll
+        for (int k = 0; k < kGRow; ++k) seen[k] = ok[k] ? ld_state<L2SYNC>(dist + t[k]) : D(0);
+#pragma unroll
+        for (int k = 0; k < kGRow; ++k) {
+          ok[k] = ok[k] && c[k] < seen[k];
+          seen[k] = ok[k] ? atomic_min_d(&dist[t[k]], c[k]) : D(0);
+        }
+        uint32_t st[kGRow];
+#pragma unroll
+        for (int k = 0; k < kGRow; ++k) {
+          ok[k] = ok[k] && c[k] < seen[k];
+          st[k] = ok[k] ? atomicMax(&stamp[t[k]], r + 1) : r + 1;
+        }
+#pragma unroll
+        for (int k = 0; k < kGRow; ++k) {
+          if (ok[k] && st[k] < r + 1) push(t[k], r);
+        }
       }
     }
     round_sync<L2SYNC>();
@@ -170,19 +198,47 @@ __global__ __launch_bounds__(kGBlock) void spf_global_kernel(
 #pragma unroll
       for (int w = 0; w < W; ++w) nv[w] = ld_state<L2SYNC>(nh + w * Sn + v);
       const uint32_t b = gRow[v] - e0, m = gRow[v + 1] - e0 - b;
-      for (uint32_t j = 0; j < m; ++j) {
-        const uint64_t x = edges[b + j];
-        const uint32_t lo = static_cast<uint32_t>(x);
-        if (lo & OGS_EDGE_DOWN) continue;
-        const uint32_t t = edge_dst(lo);
-        if (dv + weight(x) != ld_state<L2SYNC>(dist + t)) continue;
-        bool add = false;
+      constexpr int kB = W <= 4 ? kGRow : 2;  // edges per step (as above)
+      for (uint32_t j0 = 0; j0 < m; j0 += kB) {
+        uint32_t t[kB];
+        bool ok[kB];
+        D c[kB];
 #pragma unroll
-        for (int k = 0; k < W; ++k) {
-          const uint32_t a = nv[k] & ~ld_state<L2SYNC>(nh + k * Sn + t);
-          if (a && (a & ~atomicOr(&nh[k * Sn + t], a))) add = true;
+        for (int k = 0; k < kB; ++k) {
+          const uint64_t x = j0 + k < m ? edges[b + j0 + k] : uint64_t(OGS_EDGE_DOWN);
+          const uint32_t lo = static_cast<uint32_t>(x);
+          ok[k] = !(lo & OGS_EDGE_DOWN);
+          t[k] = edge_dst(lo);
+          c[k] = dv + weight(x);
         }
-        if (add) append(t, r);
+#pragma unroll
+        for (int k = 0; k < kB; ++k) {
+          ok[k] = ok[k] && c[k] == ld_state<L2SYNC>(dist + t[k]);  // tight
+        }
+        uint32_t a[kB][W];
+#pragma unroll
+        for (int k = 0; k < kB; ++k) {
+#pragma unroll
+          for (int w = 0; w < W; ++w) {
+            a[k][w] = ok[k] ? nv[w] & ~ld_state<L2SYNC>(nh + w * Sn + t[k]) : 0u;
+          }
+        }
+        bool add[kB];
+#pragma unroll
+        for (int k = 0; k < kB; ++k) {
+          add[k] = false;
+#pragma unroll
+          for (int w = 0; w < W; ++w) {
+            if (a[k][w] && (a[k][w] & ~atomicOr(&nh[w * Sn + t[k]], a[k][w]))) add[k] = true;
+          }
+        }
+        uint32_t st[kB];
+#pragma unroll
+        for (int k = 0; k < kB; ++k) st[k] = add[k] ? atomicMax(&stamp[t[k]], r + 1) : r + 1;
+#pragma unroll
+        for (int k = 0; k < kB; ++k) {
+          if (add[k] && st[k] < r + 1) push(t[k], r);
+        }
       }
     }
     round_sync<L2SYNC>();
