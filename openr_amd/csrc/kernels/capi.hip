@@ -18,6 +18,7 @@ extern int g_routeStream;
 extern int g_spfFrontier;
 extern int g_spfGlobal;
 extern int g_spfGlobalSync;
+extern int g_spfGlobalLds;
 extern int g_spfQueue;
 extern int g_spfNinfo;
 extern int g_kspQueue;
@@ -200,6 +201,11 @@ int ogs_set_option(const char* name, int64_t value) {
   if (std::strcmp(name, "spf_global_sync") == 0) {
     if (value != 0 && value != 1) return fail(OGS_E_INVALID, "spf_global_sync must be 0 or 1");
     ogs::g_spfGlobalSync = int(value);
+    return OGS_OK;
+  }
+  if (std::strcmp(name, "spf_global_lds") == 0) {
+    if (value != 0 && value != 1) return fail(OGS_E_INVALID, "spf_global_lds must be 0 or 1");
+    ogs::g_spfGlobalLds = int(value);
     return OGS_OK;
   }
   if (std::strcmp(name, "ksp_hbm") == 0) {

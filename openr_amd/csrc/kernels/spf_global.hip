@@ -247,6 +247,177 @@ __global__ __launch_bounds__(kGBlock) void spf_global_kernel(
   }
 }
 
+// ---- dist in LDS (units whose distances fit: N * sizeof(D) + two list
+// bitsets <= 160 kB, e.g. 20k nodes at u32) ----------------------------------
+// The same rounds with the unit's distances in LDS: a dist round's chain is
+// then frontier entry -> row -> edge words (L2) with LDS atomics for the
+// relaxations, instead of dist loads and atomics whose lines the atomics
+// drop from L2. List membership is a bitset per round parity in LDS (bit set
+// on the first push of a round, cleared when the entry is consumed). The
+// next-hop words stay in HBM; the final distances are copied to the caller's
+// row for the route kernel.
+uint32_t global_lds_bytes(uint32_t Sn, uint32_t dsize) {
+  return ((Sn * dsize + 15u) & ~15u) + 2u * 4u * ((Sn + 31u) / 32u);
+}
+
+template <typename D, int W>
+__global__ __launch_bounds__(kGBlock) void spf_global_lds_kernel(
+    ogs_graph g, const ogs_unit* __restrict__ units, uint32_t flags,
+    D* __restrict__ oDist, uint32_t* __restrict__ oNh, uint32_t* __restrict__ scratch) {
+  constexpr D kInf = DistInf<D>::value;
+  const int tid = threadIdx.x;
+  const uint32_t u0 = blockIdx.x;
+  const ogs_unit unit = units[u0];
+  const uint32_t s = unit.src;
+  const uint32_t nb = g.node_base[unit.topo];
+  const uint32_t N = g.node_base[unit.topo + 1] - nb;
+  const size_t Sn = size_t(g.max_nodes);
+  const uint32_t* __restrict__ gRow = g.row_ptr + nb;
+  const uint32_t e0 = gRow[0];
+  const uint64_t* __restrict__ edges = g.edges + e0;
+  const uint8_t* __restrict__ nflags = g.node_flags + nb;
+  const bool hop = (flags & OGS_F_HOP_METRIC) != 0;
+  uint32_t* nh = oNh + u0 * W * Sn;
+  uint32_t* q0 = scratch + u0 * 3 * Sn + Sn;  // the HBM form's list rows
+  uint32_t* q1 = q0 + Sn;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  D* dist = reinterpret_cast<D*>(smem);
+  const uint32_t mw = (uint32_t(Sn) + 31u) / 32u;
+  uint32_t* mark = reinterpret_cast<uint32_t*>(smem + ((Sn * sizeof(D) + 15u) & ~size_t(15)));
+  __shared__ uint32_t qcnt[3];
+
+  for (uint32_t v = tid; v < N; v += kGBlock) {
+    dist[v] = (v == s) ? D(0) : kInf;
+#pragma unroll
+    for (int w = 0; w < W; ++w) nh[w * Sn + v] = 0u;
+  }
+  for (uint32_t i = tid; i < 2 * mw; i += kGBlock) mark[i] = 0u;
+  if (tid == 0) {
+    q1[0] = s;
+    qcnt[0] = 0u;
+    qcnt[1] = 1u;
+    qcnt[2] = 0u;
+  }
+  round_sync<true>();
+  auto weight = [&](uint64_t x) -> D {
+    return hop ? D(1) : D(static_cast<uint32_t>(x >> 32));
+  };
+  // first push of t into round r + 1's list
+  auto append = [&](uint32_t t, uint32_t r) {
+    const uint32_t bit = 1u << (t & 31u);
+    if (!(atomicOr(&mark[((r + 1) & 1) * mw + (t >> 5)], bit) & bit)) {
+      const uint32_t at = atomicAdd(&qcnt[(r + 1) % 3], 1u);
+      ((r + 1) & 1 ? q1 : q0)[at] = t;
+    }
+  };
+  auto consume = [&](uint32_t v, uint32_t r) {  // v leaves round r's list
+    atomicAnd(&mark[(r & 1) * mw + (v >> 5)], ~(1u << (v & 31u)));
+  };
+
+  // ---- dist phase ----------------------------------------------------------
+  uint32_t r = 1, n = 1;
+  for (; n; ++r) {
+    if (tid == 0) qcnt[(r + 2) % 3] = 0u;
+    const uint32_t* cur = (r & 1) ? q1 : q0;
+    for (uint32_t i = tid; i < n; i += kGBlock) {
+      const uint32_t v = ld_state<true>(cur + i);
+      if (r > 1) consume(v, r);
+      if (v != s && (nflags[v] & OGS_NODE_OVERLOADED)) continue;  // 741-752
+      const D dv = dist[v];
+      const uint32_t b = gRow[v] - e0, m = gRow[v + 1] - e0 - b;
+      for (uint32_t j0 = 0; j0 < m; j0 += kGRow) {
+        uint64_t x[kGRow];
+#pragma unroll
+        for (int k = 0; k < kGRow; ++k) {
+          x[k] = j0 + k < m ? edges[b + j0 + k] : uint64_t(OGS_EDGE_DOWN);
+        }
+#pragma unroll
+        for (int k = 0; k < kGRow; ++k) {
+          const uint32_t lo = static_cast<uint32_t>(x[k]);
+          if (lo & OGS_EDGE_DOWN) continue;
+          const uint32_t t = edge_dst(lo);
+          const D c = dv + weight(x[k]);
+          if (c < dist[t] && c < atomicMin(&dist[t], c)) append(t, r);
+        }
+      }
+    }
+    round_sync<true>();
+    n = qcnt[(r + 1) % 3];
+    __syncthreads();
+  }
+  // the last round consumed nothing: clear both parities for the next phase
+  for (uint32_t i = tid; i < 2 * mw; i += kGBlock) mark[i] = 0u;
+  D* oD = oDist + u0 * Sn;
+  for (uint32_t v = tid; v < N; v += kGBlock) oD[v] = dist[v];
+
+  // ---- next-hop phase (words in HBM, L2 atomics) ---------------------------
+  const uint32_t r0 = r;
+  if (tid == 0) qcnt[0] = qcnt[1] = qcnt[2] = 0u;
+  round_sync<true>();
+  {
+    const uint32_t b = gRow[s] - e0, m = gRow[s + 1] - e0 - b;
+    for (uint32_t j = tid; j < m && j < 32u * W; j += kGBlock) {
+      const uint64_t x = edges[b + j];
+      const uint32_t lo = static_cast<uint32_t>(x);
+      if (lo & OGS_EDGE_DOWN) continue;
+      const uint32_t t = edge_dst(lo);
+      if (weight(x) == dist[t]) {
+        atomicOr(&nh[(j >> 5) * Sn + t], 1u << (j & 31u));
+        append(t, r0);
+      }
+    }
+  }
+  round_sync<true>();
+  n = qcnt[(r0 + 1) % 3];
+  __syncthreads();
+  for (r = r0 + 1; n; ++r) {
+    if (tid == 0) qcnt[(r + 2) % 3] = 0u;
+    const uint32_t* cur = (r & 1) ? q1 : q0;
+    for (uint32_t i = tid; i < n; i += kGBlock) {
+      const uint32_t v = ld_state<true>(cur + i);
+      consume(v, r);
+      if (v == s || (nflags[v] & OGS_NODE_OVERLOADED)) continue;
+      const D dv = dist[v];
+      uint32_t nv[W];
+#pragma unroll
+      for (int w = 0; w < W; ++w) nv[w] = ld_state<true>(nh + w * Sn + v);
+      const uint32_t b = gRow[v] - e0, m = gRow[v + 1] - e0 - b;
+      constexpr int kB = W <= 4 ? kGRow : 2;
+      for (uint32_t j0 = 0; j0 < m; j0 += kB) {
+        uint32_t t[kB];
+        bool ok[kB];
+#pragma unroll
+        for (int k = 0; k < kB; ++k) {
+          const uint64_t x = j0 + k < m ? edges[b + j0 + k] : uint64_t(OGS_EDGE_DOWN);
+          const uint32_t lo = static_cast<uint32_t>(x);
+          t[k] = edge_dst(lo);
+          ok[k] = !(lo & OGS_EDGE_DOWN) && dv + weight(x) == dist[t[k]];  // tight
+        }
+        uint32_t a[kB][W];
+#pragma unroll
+        for (int k = 0; k < kB; ++k) {
+#pragma unroll
+          for (int w = 0; w < W; ++w) {
+            a[k][w] = ok[k] ? nv[w] & ~ld_state<true>(nh + w * Sn + t[k]) : 0u;
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < kB; ++k) {
+          bool add = false;
+#pragma unroll
+          for (int w = 0; w < W; ++w) {
+            if (a[k][w] && (a[k][w] & ~atomicOr(&nh[w * Sn + t[k]], a[k][w]))) add = true;
+          }
+          if (add) append(t[k], r);
+        }
+      }
+    }
+    round_sync<true>();
+    n = qcnt[(r + 1) % 3];
+    __syncthreads();
+  }
+}
+
 hipError_t workspace(size_t bytes, hipStream_t stream, void** out);
 
 // "spf_global" option: 0 (default) the global path only where the LDS paths
@@ -255,6 +426,9 @@ int g_spfGlobal = 0;
 // "spf_global_sync": 1 (default) rounds end with drained stores + barrier
 // and state is read through sc1 loads; 0 agent-scope fences per round (A/B)
 int g_spfGlobalSync = 1;
+// "spf_global_lds": 1 (default) distances in LDS where they fit
+// (spf_global_lds_kernel), 0 always the all-HBM form (A/B)
+int g_spfGlobalLds = 1;
 
 // Does the LDS-resident workgroup path fit a unit of this graph? (the last
 // fallback of spf_route.hip: dist + next-hop words, CSR read from L2)
@@ -294,7 +468,17 @@ hipError_t launch_global_w(const ogs_graph& g, const ogs_prefix_table* pt,
   D* dist = out.dist ? static_cast<D*>(out.dist) : reinterpret_cast<D*>(base);
   uint32_t* nh = out.nh ? out.nh : reinterpret_cast<uint32_t*>(base + distBytes);
   uint32_t* scratch = reinterpret_cast<uint32_t*>(base + distBytes + nhBytes);
-  if (g_spfGlobalSync) {
+  const uint32_t lds = global_lds_bytes(uint32_t(Sn), sizeof(D));
+  if (g_spfGlobalLds && g_spfGlobalSync && lds <= 160u * 1024u) {
+    auto k = spf_global_lds_kernel<D, W>;
+    if (lds > 64u * 1024u) {
+      e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
+      if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(k, dim3(nUnits), dim3(kGBlock), lds, stream, g, units, flags, dist, nh,
+                       scratch);
+  } else if (g_spfGlobalSync) {
     hipLaunchKernelGGL((spf_global_kernel<D, W, true>), dim3(nUnits), dim3(kGBlock), 0, stream,
                        g, units, flags, dist, nh, scratch);
   } else {
