@@ -50,9 +50,9 @@ extern "C" {
 #define OGS_E_INVALID (-1)     /* bad argument / inconsistent shapes         */
 #define OGS_E_NOMEM (-2)       /* device allocation failed                   */
 #define OGS_E_HIP (-3)         /* HIP runtime error, see ogs_last_error()    */
-#define OGS_E_UNSUPPORTED (-4) /* input outside the engine's exact domain:   */
-                               /* zero/negative metric, metric overflow,     */
-                               /* source degree > 256, ...                   */
+#define OGS_E_UNSUPPORTED (-4) /* input the encodings cannot hold: degree  */
+                               /* > 511, > 2^21 nodes per topology, an      */
+                               /* OGS_F_EXACT_ORDER call without u64 dist.  */
 #define OGS_E_NODEVICE (-5)    /* no HIP device visible                      */
 
 /* ---- packed edge / node encodings -------------------------------------- */
@@ -279,6 +279,14 @@ int ogs_host_free(void* hptr);
  *                 (dist / next-hop sets / frontier lists in HBM, one 1024-
  *                 thread workgroup per unit, then one thread per route); 1
  *                 every ogs_spf_routes call takes that path (A/B, tests).
+ *   "spf_global_sync": 1 (default) global-path rounds end with drained
+ *                 stores + a barrier and state is read through L2-served
+ *                 (sc1) loads; 0 agent-scope fences per round (A/B).
+ *   "spf_global_lds": 1 (default) global-path distances and next-hop words
+ *                 in LDS where both fit, else distances only; 2 distances
+ *                 only; 0 all state in HBM (A/B).
+ *   "ksp_hbm":    1 every KSP unit on the HBM-state path (A/B, tests); 0
+ *                 (default) only units past LDS and OGS_F_EXACT_ORDER units.
  *   "ksp_queue":  KSP2 batch SPF: 1 (default) LDS node lists, 0 the pull
  *                 fixpoint. "ksp_stage": -1 (default) auto, 0 CSR read
  *                 from HBM/L2, 1 row offsets in LDS, 2 rows + edges in LDS. */

@@ -204,7 +204,7 @@ int ogs_set_option(const char* name, int64_t value) {
     return OGS_OK;
   }
   if (std::strcmp(name, "spf_global_lds") == 0) {
-    if (value != 0 && value != 1) return fail(OGS_E_INVALID, "spf_global_lds must be 0 or 1");
+    if (value < 0 || value > 2) return fail(OGS_E_INVALID, "spf_global_lds must be 0, 1 or 2");
     ogs::g_spfGlobalLds = int(value);
     return OGS_OK;
   }

@@ -418,6 +418,176 @@ __global__ __launch_bounds__(kGBlock) void spf_global_lds_kernel(
   }
 }
 
+// ---- dist AND next-hop words in LDS (N * (sizeof(D) + 4W) + one list bitset
+// <= 160 kB, e.g. 20k nodes at u32, W = 1) ----------------------------------
+// Both phases relax with LDS atomics; only the frontier lists (HBM rows) and
+// the CSR are read from L2. List membership is ONE bitset ("already in the
+// next list"), cleared in bulk at the start of every round -- behind the
+// same barrier that the round's first frontier loads are already in flight
+// across. The final distances and next-hop words are copied to the caller's
+// rows for the route kernel.
+uint32_t global_lds2_bytes(uint32_t Sn, uint32_t dsize, int W) {
+  return ((Sn * dsize + 15u) & ~15u) + ((Sn * 4u * uint32_t(W) + 15u) & ~15u) +
+      4u * ((Sn + 31u) / 32u);
+}
+
+template <typename D, int W>
+__global__ __launch_bounds__(kGBlock) void spf_global_lds2_kernel(
+    ogs_graph g, const ogs_unit* __restrict__ units, uint32_t flags,
+    D* __restrict__ oDist, uint32_t* __restrict__ oNh, uint32_t* __restrict__ scratch) {
+  constexpr D kInf = DistInf<D>::value;
+  const int tid = threadIdx.x;
+  const uint32_t u0 = blockIdx.x;
+  const ogs_unit unit = units[u0];
+  const uint32_t s = unit.src;
+  const uint32_t nb = g.node_base[unit.topo];
+  const uint32_t N = g.node_base[unit.topo + 1] - nb;
+  const size_t Sn = size_t(g.max_nodes);
+  const uint32_t* __restrict__ gRow = g.row_ptr + nb;
+  const uint32_t e0 = gRow[0];
+  const uint64_t* __restrict__ edges = g.edges + e0;
+  const uint8_t* __restrict__ nflags = g.node_flags + nb;
+  const bool hop = (flags & OGS_F_HOP_METRIC) != 0;
+  uint32_t* q0 = scratch + u0 * 3 * Sn + Sn;
+  uint32_t* q1 = q0 + Sn;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  D* dist = reinterpret_cast<D*>(smem);
+  uint32_t* nh = reinterpret_cast<uint32_t*>(smem + ((Sn * sizeof(D) + 15u) & ~size_t(15)));
+  uint32_t* mark = nh + ((Sn * W + 3u) & ~size_t(3));
+  const uint32_t mw = (uint32_t(Sn) + 31u) / 32u;
+  __shared__ uint32_t qcnt[3];
+
+  for (uint32_t v = tid; v < N; v += kGBlock) {
+    dist[v] = (v == s) ? D(0) : kInf;
+#pragma unroll
+    for (int w = 0; w < W; ++w) nh[w * Sn + v] = 0u;
+  }
+  if (tid == 0) {
+    q1[0] = s;
+    qcnt[0] = 0u;
+    qcnt[1] = 1u;
+    qcnt[2] = 0u;
+  }
+  round_sync<true>();
+  auto weight = [&](uint64_t x) -> D {
+    return hop ? D(1) : D(static_cast<uint32_t>(x >> 32));
+  };
+  auto append = [&](uint32_t t, uint32_t r) {  // first push of t this round
+    const uint32_t bit = 1u << (t & 31u);
+    if (!(atomicOr(&mark[t >> 5], bit) & bit)) {
+      const uint32_t at = atomicAdd(&qcnt[(r + 1) % 3], 1u);
+      ((r + 1) & 1 ? q1 : q0)[at] = t;
+    }
+  };
+  // round r's first frontier entry per thread is loaded, then the bitset is
+  // cleared behind one barrier (the load's latency overlaps it)
+  auto begin_round = [&](const uint32_t* cur, uint32_t n) {
+    const uint32_t v0 = uint32_t(tid) < n ? ld_state<true>(cur + tid) : 0u;
+    for (uint32_t i = tid; i < mw; i += kGBlock) mark[i] = 0u;
+    __syncthreads();
+    return v0;
+  };
+
+  // ---- dist phase ----------------------------------------------------------
+  uint32_t r = 1, n = 1;
+  for (; n; ++r) {
+    if (tid == 0) qcnt[(r + 2) % 3] = 0u;
+    const uint32_t* cur = (r & 1) ? q1 : q0;
+    const uint32_t v0 = begin_round(cur, n);
+    for (uint32_t i = tid; i < n; i += kGBlock) {
+      const uint32_t v = i == uint32_t(tid) ? v0 : ld_state<true>(cur + i);
+      if (v != s && (nflags[v] & OGS_NODE_OVERLOADED)) continue;  // 741-752
+      const D dv = dist[v];
+      const uint32_t b = gRow[v] - e0, m = gRow[v + 1] - e0 - b;
+      for (uint32_t j0 = 0; j0 < m; j0 += kGRow) {
+        uint64_t x[kGRow];
+#pragma unroll
+        for (int k = 0; k < kGRow; ++k) {
+          x[k] = j0 + k < m ? edges[b + j0 + k] : uint64_t(OGS_EDGE_DOWN);
+        }
+#pragma unroll
+        for (int k = 0; k < kGRow; ++k) {
+          const uint32_t lo = static_cast<uint32_t>(x[k]);
+          if (lo & OGS_EDGE_DOWN) continue;
+          const uint32_t t = edge_dst(lo);
+          const D c = dv + weight(x[k]);
+          if (c < dist[t] && c < atomicMin(&dist[t], c)) append(t, r);
+        }
+      }
+    }
+    round_sync<true>();
+    n = qcnt[(r + 1) % 3];
+    __syncthreads();
+  }
+
+  // ---- next-hop phase ------------------------------------------------------
+  const uint32_t r0 = r;
+  if (tid == 0) qcnt[0] = qcnt[1] = qcnt[2] = 0u;
+  for (uint32_t i = tid; i < mw; i += kGBlock) mark[i] = 0u;
+  __syncthreads();
+  {
+    const uint32_t b = gRow[s] - e0, m = gRow[s + 1] - e0 - b;
+    for (uint32_t j = tid; j < m && j < 32u * W; j += kGBlock) {
+      const uint64_t x = edges[b + j];
+      const uint32_t lo = static_cast<uint32_t>(x);
+      if (lo & OGS_EDGE_DOWN) continue;
+      const uint32_t t = edge_dst(lo);
+      if (weight(x) == dist[t]) {
+        atomicOr(&nh[(j >> 5) * Sn + t], 1u << (j & 31u));
+        append(t, r0);
+      }
+    }
+  }
+  round_sync<true>();
+  n = qcnt[(r0 + 1) % 3];
+  __syncthreads();
+  for (r = r0 + 1; n; ++r) {
+    if (tid == 0) qcnt[(r + 2) % 3] = 0u;
+    const uint32_t* cur = (r & 1) ? q1 : q0;
+    const uint32_t v0 = begin_round(cur, n);
+    for (uint32_t i = tid; i < n; i += kGBlock) {
+      const uint32_t v = i == uint32_t(tid) ? v0 : ld_state<true>(cur + i);
+      if (v == s || (nflags[v] & OGS_NODE_OVERLOADED)) continue;
+      const D dv = dist[v];
+      uint32_t nv[W];
+#pragma unroll
+      for (int w = 0; w < W; ++w) nv[w] = nh[w * Sn + v];
+      const uint32_t b = gRow[v] - e0, m = gRow[v + 1] - e0 - b;
+      for (uint32_t j0 = 0; j0 < m; j0 += kGRow) {
+        uint64_t x[kGRow];
+#pragma unroll
+        for (int k = 0; k < kGRow; ++k) {
+          x[k] = j0 + k < m ? edges[b + j0 + k] : uint64_t(OGS_EDGE_DOWN);
+        }
+#pragma unroll
+        for (int k = 0; k < kGRow; ++k) {
+          const uint32_t lo = static_cast<uint32_t>(x[k]);
+          if (lo & OGS_EDGE_DOWN) continue;
+          const uint32_t t = edge_dst(lo);
+          if (dv + weight(x[k]) != dist[t]) continue;  // not tight
+          bool add = false;
+#pragma unroll
+          for (int w = 0; w < W; ++w) {
+            const uint32_t a = nv[w] & ~nh[w * Sn + t];
+            if (a && (a & ~atomicOr(&nh[w * Sn + t], a))) add = true;
+          }
+          if (add) append(t, r);
+        }
+      }
+    }
+    round_sync<true>();
+    n = qcnt[(r + 1) % 3];
+    __syncthreads();
+  }
+  D* oD = oDist + u0 * Sn;
+  uint32_t* oN = oNh + u0 * W * Sn;
+  for (uint32_t v = tid; v < N; v += kGBlock) {
+    oD[v] = dist[v];
+#pragma unroll
+    for (int w = 0; w < W; ++w) oN[w * Sn + v] = nh[w * Sn + v];
+  }
+}
+
 hipError_t workspace(size_t bytes, hipStream_t stream, void** out);
 
 // "spf_global" option: 0 (default) the global path only where the LDS paths
@@ -426,8 +596,9 @@ int g_spfGlobal = 0;
 // "spf_global_sync": 1 (default) rounds end with drained stores + barrier
 // and state is read through sc1 loads; 0 agent-scope fences per round (A/B)
 int g_spfGlobalSync = 1;
-// "spf_global_lds": 1 (default) distances in LDS where they fit
-// (spf_global_lds_kernel), 0 always the all-HBM form (A/B)
+// "spf_global_lds": 1 (default) distances and next-hop words in LDS where
+// both fit (spf_global_lds2_kernel), else distances only
+// (spf_global_lds_kernel); 2 distances only; 0 always the all-HBM form (A/B)
 int g_spfGlobalLds = 1;
 
 // Does the LDS-resident workgroup path fit a unit of this graph? (the last
@@ -469,7 +640,17 @@ hipError_t launch_global_w(const ogs_graph& g, const ogs_prefix_table* pt,
   uint32_t* nh = out.nh ? out.nh : reinterpret_cast<uint32_t*>(base + distBytes);
   uint32_t* scratch = reinterpret_cast<uint32_t*>(base + distBytes + nhBytes);
   const uint32_t lds = global_lds_bytes(uint32_t(Sn), sizeof(D));
-  if (g_spfGlobalLds && g_spfGlobalSync && lds <= 160u * 1024u) {
+  const uint32_t lds2 = global_lds2_bytes(uint32_t(Sn), sizeof(D), W);
+  if (g_spfGlobalLds == 1 && g_spfGlobalSync && lds2 <= 160u * 1024u) {
+    auto k = spf_global_lds2_kernel<D, W>;
+    if (lds2 > 64u * 1024u) {
+      e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, int(lds2));
+      if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(k, dim3(nUnits), dim3(kGBlock), lds2, stream, g, units, flags, dist, nh,
+                       scratch);
+  } else if (g_spfGlobalLds && g_spfGlobalSync && lds <= 160u * 1024u) {
     auto k = spf_global_lds_kernel<D, W>;
     if (lds > 64u * 1024u) {
       e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),

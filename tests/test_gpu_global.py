@@ -56,11 +56,12 @@ class _Opt:
         self.lib.ogs_set_option(self.name, self.reset)
 
 
-@pytest.mark.parametrize("lds", [0, 1])
+@pytest.mark.parametrize("lds", [0, 1, 2])
 def test_forced_global_both_state_forms(product, oracle, lds):
-    """The global path's two forms -- distances in LDS (default where they
-    fit) and everything in HBM -- on a grid with overloads and the prefix
-    mix (both metric widths) and a fabric with multi-word next-hop sets."""
+    """The global path's three state forms -- distances and next-hop words in
+    LDS (lds=1, default where they fit), distances only (2), everything in
+    HBM (0) -- on a grid with overloads and the prefix mix (both metric
+    widths) and a fabric with multi-word next-hop sets."""
     grid = dict(n=9, metricSeed=0xC2000099, prefixSeed=7, adjOverloadPermille=30,
                 nodeOverloadPermille=20, overloadSeed=0x79, **MIX)
     wide = dict(grid, metricMax=20000000)
