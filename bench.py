@@ -445,6 +445,8 @@ def run_c3(args, torch, dist, rank, world, local_rank):
     # RouteDbBatch served per node (getRouteDbComputed: D2H of one node's
     # records + host materialisation + toThrift)
     fab = dict(C3_OPTS, prefixesPerNode=ppn)
+    if args.no_extras:
+        return line
     launch_ms, serve_ms, nroutes, ns = M.route_db_batch_serve_bench("fabric", fab, 3)
     line["serve"] = {"sources": ns, "batch_launch_ms": round(launch_ms, 3),
                      "getRouteDbComputed_ms": round(serve_ms, 2),
@@ -829,6 +831,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--topos", type=int, default=C2_TOPOS)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="skip the f1-f4 sub-lines run after the timed regions (PMC "
+                         "passes: only the timed launches reach the counters)")
     ap.add_argument("--no-c1", action="store_true",
                     help="skip the C1 single-source latency line embedded in the C2 result")
     ap.add_argument("--no-g1", action="store_true",

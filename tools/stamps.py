@@ -13,7 +13,7 @@ from c2dev import C2, apply, variants  # noqa: E402
 
 def main():
     import torch
-    c = C2()
+    c = C2(int(os.environ.get("TOPOS", "4096")))  # batch size (contention probe)
     pt = c.table()
     o = c.outputs()
     runs = [(v, o) for v in variants("1,1p")
