@@ -108,7 +108,8 @@ def algorithmic_bytes_per_unit(N, E, T, P, W, Wl, S=1):
 
 
 def pmc_traffic(tag, match):
-    """HBM bytes per launch of the kernels whose name contains `match`, from
+    """HBM bytes per launch of the kernels whose name contains `match` (a
+    substring or a tuple of them), from
     the newest committed PMC summary profiles/r*_pmc_<tag>.json
     (tools/gpu_pmc.sh: FETCH_SIZE and WRITE_SIZE passes, gfx950 FETCH_SIZE
     x2 correction). Returns (bytes summed over matching kernels, file) or
@@ -119,8 +120,9 @@ def pmc_traffic(tag, match):
         return None, None
     with open(files[-1]) as f:
         d = json.load(f)
+    matches = (match,) if isinstance(match, str) else tuple(match)
     hits = [v["hbm_bytes_per_launch"] for k, v in d.items()
-            if match in k and v.get("hbm_bytes_per_launch") is not None]
+            if any(m in k for m in matches) and v.get("hbm_bytes_per_launch") is not None]
     if not hits:
         return None, None
     return float(sum(hits)), os.path.relpath(files[-1], ROOT)
@@ -226,9 +228,9 @@ def run_g1(args, rank):
     out["roofline"] = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                        "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                        "traffic": None, "bytes_alg_per_unit": round(bpu, 1),
-                       "kernel": "spf_global_kernel + route_global_kernel (one launch; "
+                       "kernel": "spf_global*_kernel + route_global_kernel (one launch; "
                                  "latency bound: frontier rounds of one workgroup per unit)"}
-    set_traffic(out, "g1", "global_kernel")
+    set_traffic(out, "g1", ("spf_global", "route_global_kernel"))
     want = GOLDEN.get("g1")
     out["golden"] = "n/a" if want is None else ("match" if f"{digest:016x}" == want
                                                  else "MISMATCH")
