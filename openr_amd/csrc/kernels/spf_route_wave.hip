@@ -50,10 +50,10 @@ struct WaveLayout {
     WaveLayout L;
     uint32_t o = 0;
     const uint32_t P0 = N <= 64 ? 64 : N <= 128 ? 128 : 256;  // = 64 * NPL
-    L.dn = o;  // P0 positions (later: N node words) + dummy + 8 source words
-    o += align16(uint64_t(P0 + 9) * 8);
+    L.dn = o;  // P0 positions (later: N node words) + dummy + 8 source words + source self
+    o += align16(uint64_t(P0 + 10) * 8);
     L.dn32 = o;  // narrow-form words, same positions (first: posOf scratch)
-    o += align16(uint64_t(P0 + 9) * 4);
+    o += align16(uint64_t(P0 + 10) * 4);  // + dummy, 8 source-slot words, source self
     L.row = o;
     o += align16(uint64_t(N + 1) * 4);
     L.edges = o;
@@ -385,9 +385,10 @@ __global__ __launch_bounds__(64 * UPB) void spf_route_wave_kernel(
   // joins slot 0 and slot 1, true for the 2-colour order on bipartite
   // graphs) converge at the first slot evaluation after the first one that
   // changes nothing: slot X unchanged means slot Y's inputs are those of its
-  // previous evaluation. Others stop after a full unchanged round.
+  // previous evaluation. Used by the register-resident (ds_bpermute) form
+  // only; the LDS forms test once per round (cheaper than a test per slot).
   bool sep = false;
-  if (NPL == 2) {
+  if (NPL == 2 && (wopt & OGS_WAVE_OPT_BPERMUTE)) {
     bool bad = false;
 #pragma unroll
     for (int k = 0; k < NPL; ++k) {
@@ -503,48 +504,55 @@ __global__ __launch_bounds__(64 * UPB) void spf_route_wave_kernel(
     // is {min dist, ~(OR of the tied next-hop sets)} -- min + and per edge,
     // no compare / select pairs. Unreachable = 0x800000FF (dist field 2^23,
     // empty set); unusable edges read the dummy word with weight 0.
+    // Every lane is stable at the fixpoint -- empty positions read only the
+    // dummy, the source's lane only word P0 + 9 (= its own {0, {}}) -- so
+    // convergence is ONE test per round: did any lane's word change. (Per
+    // round, measured alone with the diagnostic stamps build: 838 cycles
+    // with the per-slot ballots against the active mask and the early exit
+    // after a separated slot, 550 with no test at all.)
     constexpr uint32_t kUnr = 0x800000FFu;
     uint32_t* d32 = reinterpret_cast<uint32_t*>(base + L.dn32);
-    uint32_t ws[NPL][MAXD], cur[NPL];
+    uint32_t ws[NPL][MAXD], ra[NPL][MAXD], cur[NPL];
 #pragma unroll
     for (int k = 0; k < NPL; ++k) {
+      const bool src = vk[k] == s;
 #pragma unroll
-      for (int j = 0; j < MAXD; ++j) ws[k][j] = ew[k][j] << 8;
-      cur[k] = vk[k] == s ? 0xFFu : kUnr;
+      for (int j = 0; j < MAXD; ++j) {
+        ra[k][j] = src ? P0 + 9 : ea[k][j];
+        ws[k][j] = src ? 0u : ew[k][j] << 8;
+      }
+      cur[k] = src ? 0xFFu : kUnr;
       d32[k * 64 + lane] = cur[k];
     }
-    if (lane == 0) d32[P0] = kUnr;
+    if (lane == 0) {
+      d32[P0] = kUnr;
+      d32[P0 + 9] = 0xFFu;
+    }
     if (lane < 8) d32[P0 + 1 + lane] = ~(1u << lane) & 0xFFu;
     wave_sync();
-    for (int step = 0;; ) {
-      uint64_t now = 0ull;
-      bool done = false;
+    for (;;) {
+      uint32_t chg = 0u;
 #pragma unroll
       for (int k = 0; k < NPL; ++k) {
         uint32_t cand[MAXD];
         uint32_t best = kUnr;
 #pragma unroll
         for (int j = 0; j < MAXD; ++j) {
-          cand[j] = d32[ea[k][j]] + ws[k][j];
+          cand[j] = d32[ra[k][j]] + ws[k][j];
           best = cand[j] < best ? cand[j] : best;
         }
         const uint32_t hiB = best | 0xFFu;
         uint32_t word = hiB;
 #pragma unroll
         for (int j = 0; j < MAXD; ++j) word &= cand[j] < hiB ? cand[j] : hiB;
-        const uint64_t diff = __builtin_amdgcn_ballot_w64(word != cur[k]);
+        chg |= word ^ cur[k];
         cur[k] = word;
         d32[k * 64 + lane] = word;
-        now |= diff & actMask[k];
-        if (sep && ++step >= 2 && !(diff & actMask[k])) {
-          done = true;
-          break;
-        }
       }
 #ifdef OGS_STAMPS
       ++rounds;
 #endif
-      if (done || !now) break;
+      if (__builtin_amdgcn_ballot_w64(chg != 0u) == 0ull) break;
       wave_sync();
     }
 #pragma unroll
@@ -554,30 +562,37 @@ __global__ __launch_bounds__(64 * UPB) void spf_route_wave_kernel(
       ncur[k] = unr ? 0u : ~cur[k] & 0xFFu;
     }
   } else {
+    // 64-bit {dist, nh} words (paths < 2^31 - 1); the same single
+    // convergence test per round as the narrow form (the source's lane reads
+    // only word P0 + 9 = {0, {}}, empty positions only the dummy)
     constexpr uint32_t kUnr = 0x80000000u;
-    uint32_t we[NPL][MAXD];
+    uint32_t we[NPL][MAXD], ra[NPL][MAXD];
 #pragma unroll
     for (int k = 0; k < NPL; ++k) {
+      const bool src = vk[k] == s;
 #pragma unroll
       for (int j = 0; j < MAXD; ++j) {
+        ra[k][j] = src ? P0 + 9 : ea[k][j];
         // unusable: dummy {kUnr} + 2^31-1 = 2^32-1, never wins, never wraps
-        we[k][j] = ea[k][j] == P0 ? kUnr - 1 : ew[k][j];
+        we[k][j] = src ? 0u : ea[k][j] == P0 ? kUnr - 1 : ew[k][j];
       }
-      dcur[k] = vk[k] == s ? 0u : kUnr;
+      dcur[k] = src ? 0u : kUnr;
       ncur[k] = 0u;
       dn[k * 64 + lane] = dcur[k];
     }
-    if (lane == 0) dn[P0] = uint64_t(kUnr);
+    if (lane == 0) {
+      dn[P0] = uint64_t(kUnr);
+      dn[P0 + 9] = 0ull;
+    }
     if (lane < 8) dn[P0 + 1 + lane] = uint64_t(1u << lane) << 32;
     wave_sync();
-    for (int step = 0;; ) {
-      uint64_t now = 0ull;
-      bool done = false;
+    for (;;) {
+      uint32_t chg = 0u;
 #pragma unroll
       for (int k = 0; k < NPL; ++k) {
         uint64_t x[MAXD];
 #pragma unroll
-        for (int j = 0; j < MAXD; ++j) x[j] = dn[ea[k][j]];
+        for (int j = 0; j < MAXD; ++j) x[j] = dn[ra[k][j]];
         uint32_t best = kUnr;
         uint32_t cand[MAXD];
 #pragma unroll
@@ -590,21 +605,15 @@ __global__ __launch_bounds__(64 * UPB) void spf_route_wave_kernel(
         for (int j = 0; j < MAXD; ++j) {
           m |= (cand[j] == best) ? static_cast<uint32_t>(x[j] >> 32) : 0u;
         }
-        const uint64_t diff = __builtin_amdgcn_ballot_w64(best != dcur[k]) |
-            __builtin_amdgcn_ballot_w64(m != ncur[k]);
+        chg |= (best ^ dcur[k]) | (m ^ ncur[k]);
         dcur[k] = best;
         ncur[k] = m;
         dn[k * 64 + lane] = uint64_t(best) | (uint64_t(m) << 32);
-        now |= diff & actMask[k];
-        if (sep && ++step >= 2 && !(diff & actMask[k])) {
-          done = true;
-          break;
-        }
       }
 #ifdef OGS_STAMPS
       ++rounds;
 #endif
-      if (done || !now) break;
+      if (__builtin_amdgcn_ballot_w64(chg != 0u) == 0ull) break;
       wave_sync();
     }
 #pragma unroll

@@ -14,8 +14,8 @@ cp openr_amd/csrc/kernels/*.h "$T/"
 make -s all stamps
 $H --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Iinclude -I"$T" -c "$T/$K.hip" -o "$T/base.o"
 $H --offload-arch=gfx950 -O3 -std=c++17 -fPIC -DOGS_STAMPS -Iinclude -I"$T" -c "$T/$K.hip" -o "$T/base_st.o"
-objs=$(ls build/kernels/*.o | grep -v "/$K.o")
-sobjs=$(ls build/stamps/*.o | grep -v "/$K.o")
+objs=$(ls build/kernels/*.o | grep -v "/$K.o" | grep -v "/diag_")
+sobjs=$(ls build/stamps/*.o | grep -v "/$K.o" | grep -v "/diag_")
 $H --offload-arch=gfx950 -shared $objs "$T/base.o" -o openr_amd/lib/libopenr_gpu_base.so
 $H --offload-arch=gfx950 -shared $sobjs "$T/base_st.o" -o openr_amd/lib/libopenr_gpu_stamps_base.so
 rm -rf "$T"
