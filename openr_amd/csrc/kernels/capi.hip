@@ -3,12 +3,7 @@
 
 #include <cstdio>
 #include <cstring>
-#include <map>
-#include <mutex>
 #include <string>
-#include <unordered_map>
-#include <utility>
-#include <vector>
 
 #include "openr_gpu.h"
 
@@ -106,118 +101,19 @@ int ogs_set_device(int device) {
   return e == hipSuccess ? OGS_OK : hipFail(e, "hipSetDevice");
 }
 
-// ---- caching device allocator behind ogs_malloc / ogs_free ---------------
-// A Decision process builds and drops LinkState / solver device tables on
-// every topology change; hipMalloc + hipFree of each buffer cost tens of us
-// per build (a fresh C1 build was dominated by them). Freed blocks are kept
-// per (device, size class) and handed out again: classes are powers of two
-// from 256 B to 64 MiB, then 2 MiB multiples; at most kPoolCap bytes stay
-// cached (beyond that, and on an allocation failure, blocks are returned
-// with hipFree). ogs_free keeps hipFree's ordering guarantee -- the device
-// has finished with the block before anyone can reuse it -- with a device
-// synchronisation instead of the unmap.
-namespace {
-struct DevicePool {
-  std::mutex mu;
-  std::unordered_map<void*, std::pair<int, size_t>> live;  // ptr -> (device, class)
-  std::map<std::pair<int, size_t>, std::vector<void*>> idle;
-  size_t cached = 0;
-};
-constexpr size_t kPoolCap = size_t(2) << 30;
-
-DevicePool& pool() {
-  static DevicePool* p = new DevicePool;  // never destroyed: no exit-order issues
-  return *p;
-}
-
-size_t size_class(size_t b) {
-  if (b <= 256) return 256;
-  if (b <= (size_t(64) << 20)) {
-    size_t c = 512;
-    while (c < b) c <<= 1;
-    return c;
-  }
-  const size_t g = size_t(2) << 20;
-  return (b + g - 1) / g * g;
-}
-
-void release_idle(DevicePool& P, int dev) {  // caller holds P.mu
-  for (auto it = P.idle.begin(); it != P.idle.end();) {
-    if (it->first.first != dev) {
-      ++it;
-      continue;
-    }
-    for (void* q : it->second) {
-      (void)hipFree(q);
-      P.cached -= it->first.second;
-    }
-    it = P.idle.erase(it);
-  }
-}
-}  // namespace
-
 int ogs_malloc(void** dptr, size_t bytes) {
   if (!dptr) return fail(OGS_E_INVALID, "dptr is NULL");
   *dptr = nullptr;
   if (bytes == 0) return OGS_OK;
-  int dev = 0;
-  hipError_t e = hipGetDevice(&dev);
-  if (e != hipSuccess) return hipFail(e, "hipGetDevice");
-  const size_t cls = size_class(bytes);
-  DevicePool& P = pool();
-  std::lock_guard<std::mutex> lk(P.mu);
-  auto it = P.idle.find({dev, cls});
-  if (it != P.idle.end() && !it->second.empty()) {
-    *dptr = it->second.back();
-    it->second.pop_back();
-    P.cached -= cls;
-    P.live[*dptr] = {dev, cls};
-    return OGS_OK;
-  }
-  e = hipMalloc(dptr, cls);
-  if (e == hipErrorOutOfMemory) {  // give the cached blocks back, retry once
-    (void)hipGetLastError();
-    release_idle(P, dev);
-    e = hipMalloc(dptr, cls);
-  }
-  if (e == hipErrorOutOfMemory) {
-    *dptr = nullptr;
-    return fail(OGS_E_NOMEM, "hipMalloc: out of memory");
-  }
-  if (e != hipSuccess) {
-    *dptr = nullptr;
-    return hipFail(e, "hipMalloc");
-  }
-  P.live[*dptr] = {dev, cls};
-  return OGS_OK;
+  hipError_t e = hipMalloc(dptr, bytes);
+  if (e == hipErrorOutOfMemory) return fail(OGS_E_NOMEM, "hipMalloc: out of memory");
+  return e == hipSuccess ? OGS_OK : hipFail(e, "hipMalloc");
 }
 
 int ogs_free(void* dptr) {
   if (!dptr) return OGS_OK;
-  DevicePool& P = pool();
-  std::pair<int, size_t> owner{-1, 0};
-  {
-    std::lock_guard<std::mutex> lk(P.mu);
-    auto it = P.live.find(dptr);
-    if (it != P.live.end()) {
-      owner = it->second;
-      P.live.erase(it);
-    }
-  }
-  if (owner.first < 0) {  // not from ogs_malloc: plain hipFree
-    hipError_t e = hipFree(dptr);
-    return e == hipSuccess ? OGS_OK : hipFail(e, "hipFree");
-  }
-  hipError_t e = hipDeviceSynchronize();  // hipFree's ordering, without the unmap
-  if (e != hipSuccess) return hipFail(e, "hipDeviceSynchronize");
-  std::lock_guard<std::mutex> lk(P.mu);
-  if (P.cached + owner.second > kPoolCap) {
-    e = hipFree(dptr);
-    return e == hipSuccess ? OGS_OK : hipFail(e, "hipFree");
-  }
-  P.idle[owner].push_back(dptr);
-  P.cached += owner.second;
-  return OGS_OK;
+  hipError_t e = hipFree(dptr);
+  return e == hipSuccess ? OGS_OK : hipFail(e, "hipFree");
 }
 
 int ogs_memcpy_h2d(void* dst, const void* src, size_t bytes, void* stream) {
