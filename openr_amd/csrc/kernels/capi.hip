@@ -24,6 +24,7 @@ extern int g_spfNinfo;
 extern int g_kspQueue;
 extern int g_kspStage;
 extern int g_kspHbm;
+extern int g_c4Desc;
 hipError_t launch_spf_routes(const ogs_graph& g, const ogs_prefix_table* pt,
                              const ogs_unit* units, int nUnits, uint32_t flags,
                              int W, const ogs_spf_out& out, hipStream_t stream,
@@ -206,6 +207,11 @@ int ogs_set_option(const char* name, int64_t value) {
   if (std::strcmp(name, "spf_global_lds") == 0) {
     if (value < 0 || value > 2) return fail(OGS_E_INVALID, "spf_global_lds must be 0, 1 or 2");
     ogs::g_spfGlobalLds = int(value);
+    return OGS_OK;
+  }
+  if (std::strcmp(name, "c4_desc") == 0) {
+    if (value != 0 && value != 1) return fail(OGS_E_INVALID, "c4_desc must be 0 or 1");
+    ogs::g_c4Desc = int(value);
     return OGS_OK;
   }
   if (std::strcmp(name, "ksp_hbm") == 0) {

@@ -26,6 +26,7 @@
 // tests/test_gpu_parity.py compares both against the oracle).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <map>
 #include <mutex>
@@ -166,6 +167,7 @@ bool try_ms(const ogs_graph& g, const ogs_prefix_table& pt, int hasPrefixes,
             const ogs_spf_out& out, hipStream_t stream, hipError_t* err);
 bool frontier_fits(const ogs_graph& g, uint32_t flags, int W);
 size_t chunk_scratch_bytes(const ogs_graph& g);
+size_t desc_scratch_bytes(const ogs_graph& g);
 hipError_t launch_frontier_spf(const ogs_graph& g, const ogs_unit* units,
                                int nUnits, uint32_t flags, int W,
                                uint32_t* dist, uint32_t* nh, void* scratch,
@@ -233,7 +235,10 @@ hipError_t launch_variants(const ogs_graph& g, const ogs_prefix_table& pt,
   const size_t Sp = size_t(pt.max_prefixes);
   const size_t keyBytes = round256(size_t(g.num_topos) * Sp * 4);
   void* ws = nullptr;
-  hipError_t e = workspace(keyBytes + chunk_scratch_bytes(g), stream, &ws);
+  // after the keys: the chunk lists (full recompute) or the repair's
+  // descendant rows (OGS_F_INCREMENTAL) -- one launch uses one of them
+  const size_t scratchBytes = std::max(chunk_scratch_bytes(g), desc_scratch_bytes(g));
+  hipError_t e = workspace(keyBytes + scratchBytes, stream, &ws);
   if (e != hipSuccess) return e;
   uint32_t* key = static_cast<uint32_t*>(ws);
   if (diff) {

@@ -867,6 +867,86 @@ hipError_t launch_frontier_routes(const ogs_graph& g, const ogs_prefix_table& pt
 // prefixes with an advertiser in A can change route (a route depends on its
 // advertisers' dist / next-hop sets: SpfSolver.cpp:160-311).
 // LDS: dn64 [Sn] | stamp [Sn] | two u16 node lists [Sn] | A bitset.
+// Descendant sets of the base tight DAG, one row per node (bit t of row v:
+// t is reachable from v over base-tight edges (x -> t: x relaxes, the edge is
+// up, base dist(x) + w == base dist(t))), v included. One wavefront per v,
+// breadth-first in LDS. With these rows a variant's A is the OR of its
+// seeds' rows -- no growth rounds in the repair kernel. Built once per
+// launch over the base unit (units[0]); topologies up to kDescMaxN nodes.
+constexpr uint32_t kDescMaxN = 8192;
+
+__global__ __launch_bounds__(64) void tight_desc_kernel(ogs_graph g,
+                                                        const ogs_unit* __restrict__ units,
+                                                        uint32_t flags,
+                                                        const uint32_t* __restrict__ bD,
+                                                        uint32_t* __restrict__ desc,
+                                                        uint32_t words) {
+  constexpr uint32_t kInf = 0xFFFFFFFFu;
+  const int lane = threadIdx.x;
+  const ogs_unit unit = units[0];
+  const uint32_t nb = g.node_base[unit.topo];
+  const uint32_t N = g.node_base[unit.topo + 1] - nb;
+  const uint32_t v = blockIdx.x;
+  if (v >= N) return;
+  const uint32_t s = unit.src;
+  const uint32_t* __restrict__ gRow = g.row_ptr + nb;
+  const uint32_t e0 = gRow[0];
+  const uint64_t* __restrict__ edges = g.edges + e0;
+  const uint8_t* __restrict__ nflags = g.node_flags + nb;
+  const bool hop = (flags & OGS_F_HOP_METRIC) != 0;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint32_t* bits = reinterpret_cast<uint32_t*>(smem);          // [words]
+  uint16_t* q0 = reinterpret_cast<uint16_t*>(bits + words);    // [N]
+  uint16_t* q1 = q0 + ((N + 1u) & ~1u);                        // [N]
+  __shared__ uint32_t cnt;
+  for (uint32_t w = lane; w < words; w += 64) bits[w] = 0u;
+  if (lane == 0) cnt = 0u;
+  __syncthreads();
+  if (lane == 0) {
+    bits[v >> 5] = 1u << (v & 31u);
+    q0[0] = uint16_t(v);
+  }
+  __syncthreads();
+  uint32_t n = 1;
+  for (uint32_t r = 0; n; ++r) {
+    const uint16_t* cur = (r & 1) ? q1 : q0;
+    uint16_t* nxt = (r & 1) ? q0 : q1;
+    for (uint32_t i = lane; i < n; i += 64) {
+      const uint32_t x = cur[i];
+      if (x != s && (nflags[x] & OGS_NODE_OVERLOADED)) continue;  // relaxes nothing
+      const uint32_t dx = bD[x];
+      if (dx == kInf) continue;
+      const uint32_t b = gRow[x] - e0;
+      for_row(edges, b, gRow[x + 1] - e0 - b, [&](uint32_t, uint64_t y) {
+        const uint32_t lo = static_cast<uint32_t>(y);
+        if (lo & OGS_EDGE_DOWN) return;
+        const uint32_t t = edge_dst(lo);
+        if (dx + (hop ? 1u : static_cast<uint32_t>(y >> 32)) != bD[t]) return;
+        const uint32_t m = 1u << (t & 31u);
+        if (!(atomicOr(&bits[t >> 5], m) & m)) nxt[atomicAdd(&cnt, 1u)] = uint16_t(t);
+      });
+    }
+    __syncthreads();
+    n = cnt;
+    __syncthreads();
+    if (lane == 0) cnt = 0u;
+    __syncthreads();
+  }
+  uint32_t* row = desc + size_t(v) * words;
+  for (uint32_t w = lane; w < words; w += 64) row[w] = bits[w];
+}
+
+// "c4_desc" option: 1 (default) the repair's A from precomputed descendant
+// rows where the topology has <= kDescMaxN nodes, 0 the growth rounds (A/B)
+int g_c4Desc = 1;
+
+// scratch the descendant rows need (0: not used for this graph)
+size_t desc_scratch_bytes(const ogs_graph& g) {
+  const uint32_t Sn = uint32_t(g.max_nodes);
+  if (!g_c4Desc || Sn > kDescMaxN) return 0;
+  return size_t(Sn) * ((Sn + 31u) / 32u) * 4u;
+}
+
 uint32_t repair_lds_bytes(uint32_t Sn) {
   return 8u * Sn + 4u * ((Sn + 3u) & ~3u) + 2u * 2u * ((Sn + 1u) & ~1u) +
       4u * ((Sn + 31u) / 32u) + 16u;
@@ -877,7 +957,7 @@ __global__ __launch_bounds__(kBlock) void spf_variant_repair_kernel(
     ogs_graph g, ogs_prefix_table pt, const uint32_t* __restrict__ key,
     const ogs_unit* __restrict__ units, uint32_t flags, uint32_t* __restrict__ oDist,
     uint32_t* __restrict__ oNh, ogs_spf_out out, ogs_unit_mods mods,
-    ogs_route_diff diff) {
+    ogs_route_diff diff, const uint32_t* __restrict__ desc) {
   constexpr uint32_t kInf = 0xFFFFFFFFu;
   const int tid = threadIdx.x;
   const uint32_t u0 = blockIdx.x;
@@ -943,6 +1023,15 @@ __global__ __launch_bounds__(kBlock) void spf_variant_repair_kernel(
   for (uint32_t v = tid; v < N; v += kBlock) {
     dn[v] = uint64_t(bD[v]) | (uint64_t(bN[v]) << 32);
     stamp[v] = 0u;
+  }
+  if (desc) {  // ---- A = OR of the seeds' precomputed descendant rows ------
+    const uint32_t words = (N + 31u) / 32u;
+    for (uint32_t w = tid; w < words; w += kBlock) {
+      uint32_t a = 0u;
+      for (uint32_t i = 0; i < n; ++i) a |= desc[size_t(q1[i]) * words + w];
+      inA[w] = a;
+    }
+    n = 0;
   }
   __syncthreads();
   // ---- A: the seeds' descendants in the base tight DAG (list rounds) ------
@@ -1062,7 +1151,7 @@ bool launch_variants_repair(const ogs_graph& g, const ogs_prefix_table& pt,
                             const uint32_t* key, const ogs_unit* units, int n,
                             uint32_t flags, int W, const ogs_spf_out& out,
                             const ogs_unit_mods* mods, const ogs_route_diff* diff,
-                            hipStream_t stream, hipError_t* err) {
+                            void* scratch, hipStream_t stream, hipError_t* err) {
   if (!(flags & OGS_F_INCREMENTAL) || !mods || !diff || !diff->base_dist || !diff->base_nh ||
       W != 1 || mods->dead_per_unit > kMaxDead || g.max_nodes > 65535) {
     return false;
@@ -1076,8 +1165,21 @@ bool launch_variants_repair(const ogs_graph& g, const ogs_prefix_table& pt,
                                hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
     if (*err != hipSuccess) return true;
   }
+  // descendant rows of the base tight DAG (every variant shares topology,
+  // source and base SPF: units[0] / diff->base_dist), rebuilt each launch
+  uint32_t* desc = nullptr;
+  const uint32_t Sn = uint32_t(g.max_nodes);
+  if (desc_scratch_bytes(g) && scratch) {  // the caller sized scratch for it
+    const uint32_t words = (Sn + 31u) / 32u;
+    desc = static_cast<uint32_t*>(scratch);
+    const size_t dl = size_t(words) * 4u + 2u * 2u * ((Sn + 1u) & ~1u);
+    hipLaunchKernelGGL(tight_desc_kernel, dim3(Sn), dim3(64), dl, stream, g, units, flags,
+                       diff->base_dist, desc, words);
+    *err = hipGetLastError();
+    if (*err != hipSuccess) return true;
+  }
   hipLaunchKernelGGL(k, dim3(n), dim3(kBlock), lds, stream, g, pt, key, units, flags,
-                     static_cast<uint32_t*>(out.dist), out.nh, out, *mods, *diff);
+                     static_cast<uint32_t*>(out.dist), out.nh, out, *mods, *diff, desc);
   *err = hipGetLastError();
   return true;
 }
@@ -1107,7 +1209,8 @@ hipError_t launch_frontier_variants(const ogs_graph& g, const ogs_prefix_table& 
                                     const ogs_route_diff* diff, void* scratch,
                                     hipStream_t stream) {
   hipError_t e = hipSuccess;
-  if (launch_variants_repair(g, pt, key, units, n, flags, W, out, mods, diff, stream, &e)) {
+  if (launch_variants_repair(g, pt, key, units, n, flags, W, out, mods, diff, scratch, stream,
+                             &e)) {
     return e;
   }
   uint64_t* chunks = nullptr;
