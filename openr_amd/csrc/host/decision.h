@@ -755,6 +755,9 @@ class LinkFailureSweep {
   size_t numVariants() const { return dead_.size() / kDeadMax; }
   const DecisionRouteDb& baseRouteDb() const;             // after a launch
   DecisionRouteUpdate routeUpdate(size_t v) const;        // after fetchUpdates
+  // every variant's update, materialised on `threads` host threads (0: up to
+  // 16 / the hardware's); variants are independent, so the batch splits
+  std::vector<DecisionRouteUpdate> routeUpdates(int threads = 0) const;
   DecisionRouteDb routeDb(size_t v) const;                // after fetchRecords
   std::vector<std::string> changedPrefixes(size_t v) const;  // after either
   std::pair<uint32_t, uint32_t> counts(size_t v) const;   // {update, delete}

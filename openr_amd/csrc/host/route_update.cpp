@@ -9,7 +9,11 @@
 // are gathered on the device and only those are materialised into
 // DecisionRouteUpdate (unicastRoutesToUpdate / unicastRoutesToDelete).
 #include <algorithm>
+#include <atomic>
+#include <exception>
+#include <mutex>
 #include <stdexcept>
+#include <thread>
 
 #include "decision.h"
 
@@ -324,6 +328,38 @@ DecisionRouteUpdate LinkFailureSweep::routeUpdate(size_t v) const {
     }
   }
   return u;
+}
+
+std::vector<DecisionRouteUpdate> LinkFailureSweep::routeUpdates(int threads) const {
+  const size_t V = numVariants();
+  if (offsets_.size() != V + 1) {
+    throw std::out_of_range("LinkFailureSweep::routeUpdates: fetchUpdates first");
+  }
+  (void)ls_.flat();  // built before the workers read it
+  std::vector<DecisionRouteUpdate> out(V);
+  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+  constexpr size_t kBlockV = 16;  // variants per work item
+  const size_t T = std::min<size_t>(threads > 0 ? size_t(threads) : std::min(16u, hw),
+                                    (V + kBlockV - 1) / kBlockV);
+  std::atomic<size_t> next{0};
+  std::exception_ptr err;
+  std::mutex errMu;
+  auto work = [&] {
+    try {
+      for (size_t b; (b = next.fetch_add(kBlockV)) < V;) {
+        for (size_t v = b; v < std::min(V, b + kBlockV); ++v) out[v] = routeUpdate(v);
+      }
+    } catch (...) {
+      std::lock_guard<std::mutex> lk(errMu);
+      if (!err) err = std::current_exception();
+    }
+  };
+  std::vector<std::thread> pool;
+  for (size_t t = 1; t < T; ++t) pool.emplace_back(work);
+  work();
+  for (auto& th : pool) th.join();
+  if (err) std::rethrow_exception(err);
+  return out;
 }
 
 DecisionRouteDb LinkFailureSweep::routeDb(size_t v) const {

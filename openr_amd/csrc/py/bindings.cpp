@@ -774,6 +774,18 @@ class VariantRunner {
     db.update(sw().routeUpdate(v));
     return canonical(db);
   }
+  // every variant's updated RouteDb from the parallel materialisation
+  // (LinkFailureSweep::routeUpdates on `threads` host threads)
+  std::vector<std::string> updatedCanonicalsAll(int threads) const {
+    std::vector<std::string> out;
+    const DecisionRouteDb& base = sw().baseRouteDb();
+    for (const auto& u : sw().routeUpdates(threads)) {
+      DecisionRouteDb db = base;
+      db.update(u);
+      out.push_back(canonical(db));
+    }
+    return out;
+  }
   py::tuple updateOf(size_t v) const {
     const DecisionRouteUpdate u = sw().routeUpdate(v);
     py::list upd;
@@ -784,10 +796,9 @@ class VariantRunner {
   }
   // every variant's DecisionRouteUpdate materialised (host cost of the
   // update path); returns the number of route changes
-  uint64_t materializeAll() const {
+  uint64_t materializeAll(int threads) const {
     uint64_t n = 0;
-    for (size_t v = 0; v < sw().numVariants(); ++v) {
-      const DecisionRouteUpdate u = sw().routeUpdate(v);
+    for (const auto& u : sw().routeUpdates(threads)) {
       n += u.unicastRoutesToUpdate.size() + u.unicastRoutesToDelete.size();
     }
     return n;
@@ -1742,9 +1753,14 @@ PYBIND11_MODULE(_decision, m) {
       .def("base_canonical", [](const VariantRunner& r) { return py::bytes(r.baseCanonical()); })
       .def("updated_canonical",
            [](const VariantRunner& r, size_t v) { return py::bytes(r.updatedCanonical(v)); })
+      .def("updated_canonicals_all", [](const VariantRunner& r, int threads) {
+        py::list out;
+        for (auto& c : r.updatedCanonicalsAll(threads)) out.append(py::bytes(c));
+        return out;
+      }, py::arg("threads") = 0)
       .def("update", &VariantRunner::updateOf)
       .def("total_changes", &VariantRunner::totalChanges)
-      .def("materialize_all", &VariantRunner::materializeAll,
+      .def("materialize_all", &VariantRunner::materializeAll, py::arg("threads") = 0,
            py::call_guard<py::gil_scoped_release>())
       .def("num_variants", &VariantRunner::numVariants)
       .def("canonical", [](const VariantRunner& r, size_t v) { return py::bytes(r.canonicalOf(v)); })

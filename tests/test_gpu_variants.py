@@ -103,6 +103,9 @@ def test_route_updates_c4_sample(product, oracle, mode):
         upd, dele = vr.update(v)
         assert sorted(upd + dele) == changed and (len(upd), len(dele)) == (nu, nd), v
         assert vr.updated_canonical(v) == canon, f"variant {v} {links[v]}"
+    # the batch materialisation on several host threads gives the same updates
+    for threads in (1, 3, 8):
+        assert vr.updated_canonicals_all(threads) == [c for c, _, _, _ in variants], threads
 
 
 def test_route_updates_need_records(product):
