@@ -205,7 +205,7 @@ int ogs_set_option(const char* name, int64_t value) {
     return OGS_OK;
   }
   if (std::strcmp(name, "spf_global_lds") == 0) {
-    if (value < 0 || value > 2) return fail(OGS_E_INVALID, "spf_global_lds must be 0, 1 or 2");
+    if (value < 0 || value > 3) return fail(OGS_E_INVALID, "spf_global_lds must be 0..3");
     ogs::g_spfGlobalLds = int(value);
     return OGS_OK;
   }

@@ -588,6 +588,115 @@ __global__ __launch_bounds__(kGBlock) void spf_global_lds2_kernel(
   }
 }
 
+// ---- one phase, packed {dist, next-hop word} in LDS (W = 1, u32 distances;
+// N * 8 + one list bitset <= 160 kB, e.g. 20k nodes) -------------------------
+// As the frontier kernel's packed form (packed_rounds): each relaxation is a
+// 64-bit LDS compare-and-swap of {dist, nh}; a strictly shorter candidate
+// replaces the word, an equal one ORs its next hops in, and either change
+// pushes the target. Distances and next-hop sets converge in the same rounds
+// (the two-phase forms run the next-hop propagation as a second sequence of
+// rounds); the least fixpoint is the same (spf_core.h).
+uint32_t global_lds3_bytes(uint32_t Sn) { return Sn * 8u + 4u * ((Sn + 31u) / 32u); }
+
+__global__ __launch_bounds__(kGBlock) void spf_global_lds3_kernel(
+    ogs_graph g, const ogs_unit* __restrict__ units, uint32_t flags,
+    uint32_t* __restrict__ oDist, uint32_t* __restrict__ oNh, uint32_t* __restrict__ scratch) {
+  constexpr uint32_t kInf = 0xFFFFFFFFu;
+  const int tid = threadIdx.x;
+  const uint32_t u0 = blockIdx.x;
+  const ogs_unit unit = units[u0];
+  const uint32_t s = unit.src;
+  const uint32_t nb = g.node_base[unit.topo];
+  const uint32_t N = g.node_base[unit.topo + 1] - nb;
+  const size_t Sn = size_t(g.max_nodes);
+  const uint32_t* __restrict__ gRow = g.row_ptr + nb;
+  const uint32_t e0 = gRow[0];
+  const uint64_t* __restrict__ edges = g.edges + e0;
+  const uint8_t* __restrict__ nflags = g.node_flags + nb;
+  const bool hop = (flags & OGS_F_HOP_METRIC) != 0;
+  uint32_t* q0 = scratch + u0 * 3 * Sn + Sn;
+  uint32_t* q1 = q0 + Sn;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint64_t* dn = reinterpret_cast<uint64_t*>(smem);              // [N] {dist, nh}
+  uint32_t* mark = reinterpret_cast<uint32_t*>(dn + Sn);        // [ceil(N/32)]
+  const uint32_t mw = (uint32_t(Sn) + 31u) / 32u;
+  __shared__ uint32_t qcnt[3];
+
+  for (uint32_t v = tid; v < N; v += kGBlock) dn[v] = (v == s) ? 0ull : uint64_t(kInf);
+  if (tid == 0) {
+    q1[0] = s;
+    qcnt[0] = 0u;
+    qcnt[1] = 1u;
+    qcnt[2] = 0u;
+  }
+  round_sync<true>();
+  const uint32_t sb = gRow[s] - e0;  // the source's row: its link slots
+  uint32_t r = 1, n = 1;
+  for (; n; ++r) {
+    if (tid == 0) qcnt[(r + 2) % 3] = 0u;
+    const uint32_t* cur = (r & 1) ? q1 : q0;
+    uint32_t* nxt = (r & 1) ? q0 : q1;
+    const uint32_t v0 = uint32_t(tid) < n ? ld_state<true>(cur + tid) : 0u;
+    for (uint32_t i = tid; i < mw; i += kGBlock) mark[i] = 0u;
+    __syncthreads();
+    for (uint32_t i = tid; i < n; i += kGBlock) {
+      const uint32_t v = i == uint32_t(tid) ? v0 : ld_state<true>(cur + i);
+      if (v != s && (nflags[v] & OGS_NODE_OVERLOADED)) continue;  // 741-752
+      const uint64_t xv = dn[v];
+      const uint32_t dv = static_cast<uint32_t>(xv), nv = static_cast<uint32_t>(xv >> 32);
+      const uint32_t b = gRow[v] - e0, m = gRow[v + 1] - e0 - b;
+      for (uint32_t j0 = 0; j0 < m; j0 += kGRow) {
+        uint64_t x[kGRow];
+#pragma unroll
+        for (int k = 0; k < kGRow; ++k) {
+          x[k] = j0 + k < m ? edges[b + j0 + k] : uint64_t(OGS_EDGE_DOWN);
+        }
+#pragma unroll
+        for (int k = 0; k < kGRow; ++k) {
+          const uint32_t lo = static_cast<uint32_t>(x[k]);
+          if (lo & OGS_EDGE_DOWN) continue;
+          const uint32_t t = edge_dst(lo);
+          const uint32_t c = dv + (hop ? 1u : static_cast<uint32_t>(x[k] >> 32));
+          // the source contributes its link slot, every other node NH(v)
+          const uint32_t bits = (v == s) ? (1u << (b + j0 + k - sb)) : nv;
+          uint64_t old = dn[t];
+          bool changed = false;
+          for (;;) {
+            const uint32_t dt = static_cast<uint32_t>(old), nt = static_cast<uint32_t>(old >> 32);
+            if (c > dt || (c == dt && !(bits & ~nt))) break;
+            const uint64_t nw = c < dt ? (uint64_t(c) | (uint64_t(bits) << 32))
+                                       : (uint64_t(dt) | (uint64_t(nt | bits) << 32));
+            const uint64_t seen = atomicCAS(reinterpret_cast<unsigned long long*>(&dn[t]),
+                                            static_cast<unsigned long long>(old),
+                                            static_cast<unsigned long long>(nw));
+            if (seen == old) {
+              changed = true;
+              break;
+            }
+            old = seen;
+          }
+          if (changed) {
+            const uint32_t bit = 1u << (t & 31u);
+            if (!(atomicOr(&mark[t >> 5], bit) & bit)) {
+              nxt[atomicAdd(&qcnt[(r + 1) % 3], 1u)] = t;
+            }
+          }
+        }
+      }
+    }
+    round_sync<true>();
+    n = qcnt[(r + 1) % 3];
+    __syncthreads();
+  }
+  uint32_t* oD = oDist + u0 * Sn;
+  uint32_t* oN = oNh + u0 * Sn;
+  for (uint32_t v = tid; v < N; v += kGBlock) {
+    const uint64_t x = dn[v];
+    oD[v] = static_cast<uint32_t>(x);
+    oN[v] = static_cast<uint32_t>(x >> 32);
+  }
+}
+
 hipError_t workspace(size_t bytes, hipStream_t stream, void** out);
 
 // "spf_global" option: 0 (default) the global path only where the LDS paths
@@ -596,9 +705,11 @@ int g_spfGlobal = 0;
 // "spf_global_sync": 1 (default) rounds end with drained stores + barrier
 // and state is read through sc1 loads; 0 agent-scope fences per round (A/B)
 int g_spfGlobalSync = 1;
-// "spf_global_lds": 1 (default) distances and next-hop words in LDS where
-// both fit (spf_global_lds2_kernel), else distances only
-// (spf_global_lds_kernel); 2 distances only; 0 always the all-HBM form (A/B)
+// "spf_global_lds": 1 (default) the best LDS form that fits -- one-phase
+// packed {dist, nh} words (spf_global_lds3_kernel, W = 1, u32), else
+// distances and next-hop words in two phases (spf_global_lds2_kernel), else
+// distances only (spf_global_lds_kernel); 3 the two-phase form, 2 distances
+// only, 0 always the all-HBM form (A/B)
 int g_spfGlobalLds = 1;
 
 // Does the LDS-resident workgroup path fit a unit of this graph? (the last
@@ -641,7 +752,23 @@ hipError_t launch_global_w(const ogs_graph& g, const ogs_prefix_table* pt,
   uint32_t* scratch = reinterpret_cast<uint32_t*>(base + distBytes + nhBytes);
   const uint32_t lds = global_lds_bytes(uint32_t(Sn), sizeof(D));
   const uint32_t lds2 = global_lds2_bytes(uint32_t(Sn), sizeof(D), W);
-  if (g_spfGlobalLds == 1 && g_spfGlobalSync && lds2 <= 160u * 1024u) {
+  const uint32_t lds3 = global_lds3_bytes(uint32_t(Sn));
+  if constexpr (W == 1 && sizeof(D) == 4) {
+    if (g_spfGlobalLds == 1 && g_spfGlobalSync && lds3 <= 160u * 1024u) {
+      auto k = spf_global_lds3_kernel;
+      if (lds3 > 64u * 1024u) {
+        e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, int(lds3));
+        if (e != hipSuccess) return e;
+      }
+      hipLaunchKernelGGL(k, dim3(nUnits), dim3(kGBlock), lds3, stream, g, units, flags,
+                         reinterpret_cast<uint32_t*>(dist), nh, scratch);
+      e = hipGetLastError();
+      if (e != hipSuccess || !pt || pt->max_prefixes == 0) return e;
+      return launch_route_global<D, W>(g, *pt, units, nUnits, flags, dist, nh, out, stream);
+    }
+  }
+  if ((g_spfGlobalLds == 1 || g_spfGlobalLds == 3) && g_spfGlobalSync && lds2 <= 160u * 1024u) {
     auto k = spf_global_lds2_kernel<D, W>;
     if (lds2 > 64u * 1024u) {
       e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
@@ -650,7 +777,8 @@ hipError_t launch_global_w(const ogs_graph& g, const ogs_prefix_table* pt,
     }
     hipLaunchKernelGGL(k, dim3(nUnits), dim3(kGBlock), lds2, stream, g, units, flags, dist, nh,
                        scratch);
-  } else if (g_spfGlobalLds && g_spfGlobalSync && lds <= 160u * 1024u) {
+  } else if ((g_spfGlobalLds == 1 || g_spfGlobalLds == 2) && g_spfGlobalSync &&
+             lds <= 160u * 1024u) {
     auto k = spf_global_lds_kernel<D, W>;
     if (lds > 64u * 1024u) {
       e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),

@@ -56,12 +56,13 @@ class _Opt:
         self.lib.ogs_set_option(self.name, self.reset)
 
 
-@pytest.mark.parametrize("lds", [0, 1, 2])
+@pytest.mark.parametrize("lds", [0, 1, 2, 3])
 def test_forced_global_both_state_forms(product, oracle, lds):
-    """The global path's three state forms -- distances and next-hop words in
-    LDS (lds=1, default where they fit), distances only (2), everything in
-    HBM (0) -- on a grid with overloads and the prefix mix (both metric
-    widths) and a fabric with multi-word next-hop sets."""
+    """The global path's state forms -- one-phase packed {dist, nh} words in
+    LDS (lds=1, default where they fit: one next-hop word, u32 distances),
+    two-phase distances + next-hop words in LDS (3), distances only (2),
+    everything in HBM (0) -- on a grid with overloads and the prefix mix
+    (both metric widths) and a fabric with multi-word next-hop sets."""
     grid = dict(n=9, metricSeed=0xC2000099, prefixSeed=7, adjOverloadPermille=30,
                 nodeOverloadPermille=20, overloadSeed=0x79, **MIX)
     wide = dict(grid, metricMax=20000000)
