@@ -704,6 +704,13 @@ std::optional<RibUnicastEntry> materializeRoute(
     uint32_t p, uint32_t meta, uint64_t metric, const uint32_t* mask,
     size_t maskStride, int W, bool v4OverV6Nexthop, const RibPolicy* policy,
     uint8_t applied, uint8_t counter);
+// the same with the source's CSR row start `rb` (= f.rowPtr[f.id.at(me)])
+// looked up once by the caller: loops over many routes of one source
+std::optional<RibUnicastEntry> materializeRouteAt(
+    const FlatTopology& f, uint32_t rb, const std::string& me, const PrefixHostTable& pt,
+    uint32_t p, uint32_t meta, uint64_t metric, const uint32_t* mask,
+    size_t maskStride, int W, bool v4OverV6Nexthop, const RibPolicy* policy,
+    uint8_t applied, uint8_t counter);
 
 DecisionRouteDb materializeRouteDb(
     const LinkState& ls, const FlatTopology& f, const std::string& area,

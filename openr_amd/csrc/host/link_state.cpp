@@ -1,7 +1,7 @@
 // link_state.cpp — ingestion, change detection and CSR flattening for the
 // GPU LinkState (reference: openr/decision/LinkState.cpp:50-715).
-#include <cstring>
 #include <algorithm>
+#include <cstring>
 #include <unordered_map>
 
 #include "decision.h"
@@ -331,53 +331,61 @@ const FlatTopology& LinkState::flat() const {
   }
   const uint32_t N = uint32_t(f->names.size());
   if (N > OGS_MAX_NODES_PER_TOPO) throw std::domain_error("too many nodes");
-  // slot of every (link, endpoint) inside that endpoint's CSR row
-  std::unordered_map<const Link*, std::pair<uint32_t, uint32_t>> slot;
+  // rows in canonical link order, one Link lookup per directed edge; the
+  // reverse of every edge by pairing a link's two occurrences (sorted by
+  // Link*), so the neighbour id, its row slot and its overload bit come from
+  // indexes instead of string-keyed lookups
   f->rowPtr.assign(N + 1, 0);
-  for (uint32_t u = 0; u < N; ++u) {
-    uint32_t j = 0;
-    if (auto it = byNode_.find(f->names[u]); it != byNode_.end()) {
-      for (const auto& key : it->second) {
-        const Link* l = links_.at(key).get();
-        auto& s = slot[l];
-        (l->firstNodeName() == f->names[u] ? s.first : s.second) = j++;
-      }
-    }
-    f->rowPtr[u + 1] = f->rowPtr[u] + j;
-    f->maxDegree = std::max<int>(f->maxDegree, int(j));
-  }
-  if (f->maxDegree >= OGS_MAX_DEGREE) throw std::domain_error("degree > 511");
-  f->edges.resize(f->rowPtr[N]);
-  f->edgeLink.resize(f->rowPtr[N]);
   f->nodeFlags.assign(N, 0);
+  std::vector<std::pair<const Link*, uint32_t>> occ;  // (link, directed edge)
+  std::vector<uint32_t> owner;
   for (uint32_t u = 0; u < N; ++u) {
     const std::string& un = f->names[u];
     if (isNodeOverloaded(un)) f->nodeFlags[u] |= OGS_NODE_OVERLOADED;
     const uint64_t inc = getNodeMetricIncrement(un);
     if (static_cast<int>(inc) > 0) f->nodeFlags[u] |= OGS_NODE_SOFTDRAIN;
     if (inc != 0) f->nodeFlags[u] |= OGS_NODE_METRICINC;
-    uint32_t e = f->rowPtr[u];
+    uint32_t j = 0;
     if (auto it = byNode_.find(un); it != byNode_.end()) {
       for (const auto& key : it->second) {
         Link* l = links_.at(key).get();
-        const std::string& vn = l->getOtherNodeName(un);
-        const uint32_t v = f->id.at(vn);
-        const auto& s = slot.at(l);
-        const uint32_t rslot = (l->firstNodeName() == vn) ? s.first : s.second;
-        const LinkStateMetric m = l->getMaxMetric();
-        uint32_t lo = v | (rslot << OGS_EDGE_RSLOT_SHIFT);
-        if (isNodeOverloaded(vn)) lo |= OGS_EDGE_DST_OVERLOADED;
-        if (!l->isUp()) lo |= OGS_EDGE_DOWN;
-        if (l->isUp()) {
-          f->maxMetric = std::max(f->maxMetric, m);
-          if (m == 0) f->hasZeroMetric = true;
-          if (m > 0xFFFFFFFFull) f->hasWideMetric = true;
-        }
-        f->edges[e] = uint64_t(lo) | (uint64_t(uint32_t(m)) << 32);
-        f->edgeLink[e] = l;
-        ++e;
+        occ.emplace_back(l, uint32_t(f->edgeLink.size()));
+        f->edgeLink.push_back(l);
+        owner.push_back(u);
+        ++j;
       }
     }
+    f->rowPtr[u + 1] = f->rowPtr[u] + j;
+    f->maxDegree = std::max<int>(f->maxDegree, int(j));
+  }
+  if (f->maxDegree >= OGS_MAX_DEGREE) throw std::domain_error("degree > 511");
+  const uint32_t E = f->rowPtr[N];
+  std::vector<uint32_t> rev(E, 0xFFFFFFFFu);
+  std::sort(occ.begin(), occ.end());
+  for (size_t i = 0; i + 1 < occ.size(); ++i) {
+    if (occ[i].first != occ[i + 1].first) continue;
+    rev[occ[i].second] = occ[i + 1].second;
+    rev[occ[i + 1].second] = occ[i].second;
+    ++i;
+  }
+  f->edges.resize(E);
+  for (uint32_t e = 0; e < E; ++e) {
+    const Link* l = f->edgeLink[e];
+    const uint32_t r = rev[e];
+    if (r == 0xFFFFFFFFu) throw std::logic_error("LinkState::flat: link with one endpoint");
+    const uint32_t v = owner[r];
+    const uint32_t rslot = r - f->rowPtr[v];
+    const LinkStateMetric m = l->getMaxMetric();
+    uint32_t lo = v | (rslot << OGS_EDGE_RSLOT_SHIFT);
+    if (f->nodeFlags[v] & OGS_NODE_OVERLOADED) lo |= OGS_EDGE_DST_OVERLOADED;
+    const bool up = l->isUp();
+    if (!up) lo |= OGS_EDGE_DOWN;
+    if (up) {
+      f->maxMetric = std::max(f->maxMetric, m);
+      if (m == 0) f->hasZeroMetric = true;
+      if (m > 0xFFFFFFFFull) f->hasWideMetric = true;
+    }
+    f->edges[e] = uint64_t(lo) | (uint64_t(uint32_t(m)) << 32);
   }
   flat_ = std::move(f);
   flatStale_ = false;

@@ -317,12 +317,14 @@ DecisionRouteUpdate LinkFailureSweep::routeUpdate(size_t v) const {
   DecisionRouteUpdate u;  // SpfSolver.cpp:21-56, prefixes in table order
   const FlatTopology& f = ls_.flat();
   const size_t T = cPrefixH_.size();
+  const uint32_t rb = f.rowPtr[f.id.at(me_)];
   for (uint32_t i = offsets_[v]; i < offsets_[v + 1]; ++i) {
     const uint32_t p = cPrefixH_[i];
-    auto e = materializeRoute(f, me_, table_, p, cMetaH_[i], cMetricH_[i], &cMaskH_[i], T, W_,
-                              v4OverV6_, nullptr, 0xFF, 0xFF);
+    auto e = materializeRouteAt(f, rb, me_, table_, p, cMetaH_[i], cMetricH_[i], &cMaskH_[i],
+                                T, W_, v4OverV6_, nullptr, 0xFF, 0xFF);
     if (e) {
-      u.unicastRoutesToUpdate.emplace(e->prefix, std::move(*e));
+      u.unicastRoutesToUpdate.emplace_hint(u.unicastRoutesToUpdate.end(), e->prefix,
+                                           std::move(*e));
     } else {
       u.unicastRoutesToDelete.push_back(table_.prefixes.at(p));
     }

@@ -536,7 +536,16 @@ std::optional<RibUnicastEntry> materializeRoute(
     size_t maskStride, int W, bool v4OverV6Nexthop, const RibPolicy* policy,
     uint8_t applied, uint8_t counter) {
   if (!(meta & OGS_ROUTE_VALID)) return std::nullopt;
-  const uint32_t rb = f.rowPtr[f.id.at(me)];
+  return materializeRouteAt(f, f.rowPtr[f.id.at(me)], me, pt, p, meta, metric, mask,
+                            maskStride, W, v4OverV6Nexthop, policy, applied, counter);
+}
+
+std::optional<RibUnicastEntry> materializeRouteAt(
+    const FlatTopology& f, uint32_t rb, const std::string& me, const PrefixHostTable& pt,
+    uint32_t p, uint32_t meta, uint64_t metric, const uint32_t* mask,
+    size_t maskStride, int W, bool v4OverV6Nexthop, const RibPolicy* policy,
+    uint8_t applied, uint8_t counter) {
+  if (!(meta & OGS_ROUTE_VALID)) return std::nullopt;
   const uint32_t best = pt.advOff[p] + (meta >> OGS_ROUTE_BEST_SHIFT);
   RibUnicastEntry e;
   e.prefix = pt.prefixes[p];
@@ -568,6 +577,8 @@ DecisionRouteDb materializeRouteDb(
     std::map<std::string, RouteSelectionResult>* bestRoutesCache) {
   DecisionRouteDb rdb;
   if (bestRoutesCache) bestRoutesCache->clear();
+  const auto meIt = f.id.find(me);
+  const uint32_t rb = meIt == f.id.end() ? 0u : f.rowPtr[meIt->second];
   for (uint32_t p = 0; p < r.P; ++p) {
     const uint32_t meta = r.meta[p];
     if (bestRoutesCache && (meta & OGS_ROUTE_SELECTED)) {  // SpfSolver.cpp:247
@@ -579,13 +590,16 @@ DecisionRouteDb materializeRouteDb(
       }
       sel.bestNodeArea = pt.advKey[a0 + (meta >> OGS_ROUTE_BEST_SHIFT)];
       sel.isBestNodeDrained = meta & OGS_ROUTE_DRAINED;
-      (*bestRoutesCache)[pt.prefixes[p]] = std::move(sel);
+      // table order is prefix order: appending at the end is the hint
+      bestRoutesCache->insert_or_assign(bestRoutesCache->end(), pt.prefixes[p],
+                                        std::move(sel));
     }
-    auto e = materializeRoute(f, me, pt, p, meta, r.metric[p], &r.mask[p], r.maskStride,
-                              r.W, v4OverV6Nexthop, r.policy,
-                              r.policy ? r.applied[p] : 0xFF,
-                              r.policy ? r.counter[p] : 0xFF);
-    if (e) rdb.unicastRoutes.emplace(e->prefix, std::move(*e));
+    if (!(meta & OGS_ROUTE_VALID)) continue;
+    auto e = materializeRouteAt(f, rb, me, pt, p, meta, r.metric[p], &r.mask[p],
+                                r.maskStride, r.W, v4OverV6Nexthop, r.policy,
+                                r.policy ? r.applied[p] : 0xFF,
+                                r.policy ? r.counter[p] : 0xFF);
+    if (e) rdb.unicastRoutes.emplace_hint(rdb.unicastRoutes.end(), e->prefix, std::move(*e));
   }
   for (const auto& [prefix, e] : statics) {  // SpfSolver.cpp:343-349
     if (rdb.unicastRoutes.count(prefix)) continue;
