@@ -727,7 +727,10 @@ DecisionRouteDb materializeRouteDb(
 // down (adjacency withdrawn at both ends, LinkState.cpp:406-659). All variants
 // run in one launch (ogs_spf_routes_variants, route diff fused in); only the
 // changed records are gathered on the device (ogs_route_changes_gather) and
-// materialised. Node-segment labels are not part of the sweep (off in the
+// materialised. Areas with zero / negative link metrics or path sums past 32
+// bits run each variant as its own topology in one ogs_spf_routes launch
+// (exact extraction order, 64-bit distances) and diff on the host with
+// calculateUpdate. Node-segment labels are not part of the sweep (off in the
 // DecisionBenchmark config). `ls` and `ps` must outlive the
 // sweep unchanged.
 class LinkFailureSweep {
@@ -777,6 +780,8 @@ class LinkFailureSweep {
   static constexpr int kDeadMax = 4;  // <= 2 links x 2 directions
   ogs_graph graph() const;
   ogs_prefix_table table() const;
+  void exactLaunch(void* stream);
+  void exactFetch(void* stream);
   const LinkState& ls_;
   std::string me_, area_;
   bool enableV4_, brs_, v4OverV6_;
@@ -798,6 +803,11 @@ class LinkFailureSweep {
   std::vector<uint32_t> counts_, changed_, offsets_;
   std::vector<uint32_t> cPrefixH_, cMetaH_, cMetricH_, cMaskH_;  // compact
   std::vector<uint32_t> meta_, metric_, mask_;                   // full
+  // zero / negative metrics or 64-bit path sums: one topology per variant
+  // through ogs_spf_routes (exactLaunch), updates by calculateUpdate
+  bool exact_{false}, exactOrder_{false};
+  std::vector<DecisionRouteDb> xDb_;
+  std::vector<DecisionRouteUpdate> xUpd_;
 };
 
 // ----------------------------------------------------------- RouteDbBatch --

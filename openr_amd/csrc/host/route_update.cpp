@@ -34,16 +34,14 @@ LinkFailureSweep::LinkFailureSweep(
   if (sIt == f.id.end()) {
     throw std::invalid_argument("LinkFailureSweep: " + me_ + " is not in area " + area_);
   }
-  if (wideDistancesNeeded(f)) {
-    throw std::domain_error("LinkFailureSweep: path metrics need 64-bit distances");
-  }
+  const bool wide = wideDistancesNeeded(f);
   table_.build(ps);
   hb_.append(f, ps, area_);
-  if (hb_.hasZeroMetric) {
-    throw std::domain_error(
-        "LinkFailureSweep: zero or negative link metric is outside the GPU "
-        "engine's exact domain");
-  }
+  // zero / negative link metrics (extraction-order replay) or path sums past
+  // 32 bits: the variants kernel's packed 32-bit {dist, nh} repair does not
+  // apply, every variant runs as a topology of its own (exactLaunch)
+  exact_ = wide || hb_.hasZeroMetric;
+  exactOrder_ = f.hasZeroMetric || f.hasWideMetric;
   const uint32_t s = sIt->second;
   W_ = std::max(1, ogs_nh_words_for_degree(int(f.rowPtr[s + 1] - f.rowPtr[s])));
   if (W_ > 4) throw std::domain_error("LinkFailureSweep: source degree > 128");
@@ -80,10 +78,24 @@ LinkFailureSweep::LinkFailureSweep(
     }
   }
 
+  if (exact_) {  // topology 0 = the base, topology v + 1 = variant v
+    for (size_t v = 0; v < variants.size(); ++v) {
+      const uint32_t e0 = uint32_t(hb_.edges.size());
+      hb_.append(f, ps, area_);
+      for (int k = 0; k < kDeadMax; ++k) {
+        const uint32_t e = dead_[v * kDeadMax + k];
+        if (e != OGS_NODE_NONE) hb_.edges[e0 + e] |= OGS_EDGE_DOWN;
+      }
+    }
+  }
   const size_t U = variants.size(), Sn = size_t(std::max(hb_.maxNodes, 1));
   Sp_ = size_t(std::max(hb_.maxPrefixes, 1));
   words_ = (Sp_ + 31) / 32;
   std::vector<ogs_unit> units(U, ogs_unit{0, s});
+  if (exact_) {
+    units.assign(U + 1, ogs_unit{0, s});
+    for (size_t t = 0; t <= U; ++t) units[t].topo = uint32_t(t);
+  }
   const ogs_unit base{0, s};
   dNodeBase_.upload(hb_.nodeBase.data(), hb_.nodeBase.size());
   dDesc_.upload(hb_.topoDesc.data(), hb_.topoDesc.size());
@@ -143,6 +155,65 @@ LinkFailureSweep::LinkFailureSweep(
   dMask_.resize(Uc * W_ * Sp_ * 4);
   dChanged_.resize(Uc * words_ * 4);
   dCounts_.resize(Uc * 2 * 4);
+  if (exact_) {  // base + variants, 64-bit metrics
+    dMeta_.resize((U + 1) * Sp_ * 4);
+    dMetric_.resize((U + 1) * Sp_ * 8);
+    dMask_.resize((U + 1) * W_ * Sp_ * 4);
+  }
+}
+
+// Variants outside the repair kernel's domain: ONE ogs_spf_routes launch
+// over the base (unit 0) and every variant's own topology copy (the failed
+// links' edges marked down, the same skip the variants kernel applies to its
+// dead-edge list), in the exact extraction order when the area has zero or
+// negative metrics, with 64-bit distances. fetch materialises the records and
+// the update is DecisionRouteDb::calculateUpdate (SpfSolver.cpp:21-56) of the
+// base and variant RouteDbs, as Decision::rebuildRoutes computes it.
+void LinkFailureSweep::exactLaunch(void* stream) {
+  ogs_graph g = graph();
+  ogs_prefix_table pt = table();
+  ogs_spf_out out{nullptr, nullptr, dMeta_.as<uint32_t>(), dMetric_.get(),
+                  dMask_.as<uint32_t>(), nullptr};
+  const uint32_t fl = flags() | OGS_F_WIDE_METRIC | (exactOrder_ ? OGS_F_EXACT_ORDER : 0u);
+  ogsCheck(ogs_spf_routes(&g, &pt, dUnits_.as<ogs_unit>(), int32_t(numVariants() + 1), fl, W_,
+                          &out, stream),
+           "ogs_spf_routes(variant topologies)");
+  baseRun_ = recordsRun_ = true;
+  changedOnlyRun_ = false;
+}
+
+void LinkFailureSweep::exactFetch(void* stream) {
+  if (!recordsRun_) throw std::logic_error("LinkFailureSweep: launch() first");
+  const size_t U = numVariants(), T = U + 1;
+  std::vector<uint32_t> meta(T * Sp_), mask(T * W_ * Sp_);
+  std::vector<uint64_t> metric(T * Sp_);
+  dMeta_.download(meta.data(), meta.size(), stream);
+  dMetric_.download(metric.data(), metric.size(), stream);
+  dMask_.download(mask.data(), mask.size(), stream);
+  ogsCheck(ogs_stream_sync(stream), "ogs_stream_sync");
+  const FlatTopology& f = ls_.flat();
+  auto dbOf = [&](size_t t) {
+    DecisionRouteDb db;
+    for (uint32_t p = 0; p < uint32_t(table_.prefixes.size()); ++p) {
+      auto e = materializeRoute(f, me_, table_, p, meta[t * Sp_ + p], metric[t * Sp_ + p],
+                                &mask[t * W_ * Sp_ + p], Sp_, W_, v4OverV6_, nullptr, 0xFF,
+                                0xFF);
+      if (e) db.unicastRoutes.emplace(e->prefix, std::move(*e));
+    }
+    return db;
+  };
+  base_ = dbOf(0);
+  xDb_.clear();
+  xUpd_.clear();
+  counts_.assign(2 * U, 0);
+  offsets_.assign(U + 1, 0);
+  for (size_t v = 0; v < U; ++v) {
+    xDb_.push_back(dbOf(v + 1));
+    xUpd_.push_back(base_->calculateUpdate(xDb_.back()));
+    counts_[2 * v] = uint32_t(xUpd_.back().unicastRoutesToUpdate.size());
+    counts_[2 * v + 1] = uint32_t(xUpd_.back().unicastRoutesToDelete.size());
+    offsets_[v + 1] = offsets_[v] + counts_[2 * v] + counts_[2 * v + 1];
+  }
 }
 
 uint32_t LinkFailureSweep::flags() const {
@@ -178,6 +249,7 @@ ogs_prefix_table LinkFailureSweep::table() const {
 }
 
 void LinkFailureSweep::runBase(void* stream) {
+  if (exact_) return exactLaunch(stream);
   ogs_graph g = graph();
   ogs_prefix_table pt = table();
   ogs_spf_out out{bDist_.get(), bNh_.as<uint32_t>(), bMeta_.as<uint32_t>(),
@@ -189,6 +261,7 @@ void LinkFailureSweep::runBase(void* stream) {
 }
 
 void LinkFailureSweep::launch(void* stream, bool records) {
+  if (exact_) return exactLaunch(stream);  // records are always written
   if (!baseRun_) runBase(stream);
   offsets_.clear();  // results of an earlier launch are stale now
   changed_.clear();
@@ -218,6 +291,7 @@ void LinkFailureSweep::launch(void* stream, bool records) {
 }
 
 void LinkFailureSweep::fetchUpdates(void* stream) {
+  if (exact_) return exactFetch(stream);
   if (!recordsRun_) {
     throw std::logic_error("LinkFailureSweep::fetchUpdates: launch(records=true) first");
   }
@@ -268,6 +342,7 @@ void LinkFailureSweep::fetchUpdates(void* stream) {
 }
 
 void LinkFailureSweep::fetchRecords(void* stream) {
+  if (exact_) return exactFetch(stream);
   // the diff (bitmap + counts) always; the records when the launch wrote them
   const size_t U = numVariants();
   const size_t R = (recordsRun_ && !changedOnlyRun_) ? U : 0;
@@ -296,6 +371,10 @@ void LinkFailureSweep::fetchRecords(void* stream) {
 }
 
 const DecisionRouteDb& LinkFailureSweep::baseRouteDb() const {
+  if (exact_) {
+    if (!base_) throw std::logic_error("LinkFailureSweep: nothing fetched yet");
+    return *base_;
+  }
   if (baseMeta_.empty()) throw std::logic_error("LinkFailureSweep: nothing fetched yet");
   if (!base_) {
     DecisionRouteDb db;
@@ -314,6 +393,7 @@ DecisionRouteUpdate LinkFailureSweep::routeUpdate(size_t v) const {
   if (v >= numVariants() || offsets_.size() != numVariants() + 1) {
     throw std::out_of_range("LinkFailureSweep::routeUpdate: variant / fetchUpdates");
   }
+  if (exact_) return xUpd_.at(v);
   DecisionRouteUpdate u;  // SpfSolver.cpp:21-56, prefixes in table order
   const FlatTopology& f = ls_.flat();
   const size_t T = cPrefixH_.size();
@@ -365,6 +445,10 @@ std::vector<DecisionRouteUpdate> LinkFailureSweep::routeUpdates(int threads) con
 }
 
 DecisionRouteDb LinkFailureSweep::routeDb(size_t v) const {
+  if (exact_) {
+    if (v >= xDb_.size()) throw std::out_of_range("LinkFailureSweep::routeDb: variant / fetch");
+    return xDb_[v];
+  }
   if (v >= numVariants() || meta_.size() != numVariants() * Sp_) {
     throw std::out_of_range("LinkFailureSweep::routeDb: variant / fetchRecords");
   }
@@ -382,7 +466,12 @@ DecisionRouteDb LinkFailureSweep::routeDb(size_t v) const {
 std::vector<std::string> LinkFailureSweep::changedPrefixes(size_t v) const {
   if (v >= numVariants()) throw std::out_of_range("LinkFailureSweep: variant");
   std::vector<std::string> out;
-  if (offsets_.size() == numVariants() + 1) {
+  if (exact_) {
+    if (v >= xUpd_.size()) throw std::logic_error("LinkFailureSweep: nothing fetched yet");
+    for (const auto& [p, _] : xUpd_[v].unicastRoutesToUpdate) out.push_back(p);
+    out.insert(out.end(), xUpd_[v].unicastRoutesToDelete.begin(),
+               xUpd_[v].unicastRoutesToDelete.end());
+  } else if (offsets_.size() == numVariants() + 1) {
     for (uint32_t i = offsets_[v]; i < offsets_[v + 1]; ++i) {
       out.push_back(table_.prefixes.at(cPrefixH_[i]));
     }

@@ -1,0 +1,208 @@
+"""Seeded cross-feature sweep: every route-affecting input knob the
+generators have, drawn together at random, through the drop-in
+SpfSolver::buildRouteDb (and the f2 RouteDbBatch / multi-area domain) on the
+GPU, compared byte for byte with the oracle's canonical RouteDb text.
+
+The per-feature tests pin each knob alone; this sweep pins their
+combinations: zero / negative / wide link metrics (exact extraction order,
+LinkState.cpp:789-811) together with overloaded adjacencies and nodes
+(LinkState.cpp:741-752), v4 / anycast / minNexthop / drained prefixes
+(SpfSolver.cpp:139-311, LsdbUtil.cpp:760-823), best-route selection, node
+segment labels and RibPolicy (RibPolicy.cpp:74-161, 222-229), with sources
+that include an unknown node (no RouteDb, SpfSolver.cpp:95-107)."""
+import contextlib
+import random
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _cmp(a, b, label):
+    assert len(a) == len(b), label
+    for i, (x, y) in enumerate(zip(a, b)):
+        if x != y:
+            xa, ya = x.decode().splitlines(), y.decode().splitlines()
+            diff = [(p, q) for p, q in zip(xa, ya) if p != q][:4]
+            pytest.fail(f"{label} source #{i} differs: {diff} (len {len(xa)} vs {len(ya)})")
+
+
+def _permille(rng, hi):
+    return rng.choice([0, 0, rng.randint(1, hi)])
+
+
+def _mix(rng):
+    return dict(v4Permille=_permille(rng, 400), anycastPermille=_permille(rng, 400),
+                minNhPermille=_permille(rng, 300), drainPermille=_permille(rng, 300),
+                tagPermille=_permille(rng, 800), mixSeed=rng.getrandbits(32),
+                adjOverloadPermille=_permille(rng, 150),
+                nodeOverloadPermille=_permille(rng, 150), overloadSeed=rng.getrandbits(32),
+                zeroMetricPermille=_permille(rng, 300), negMetricPermille=rng.choice([0, 0, 0, 40]),
+                specialSeed=rng.getrandbits(32))
+
+
+def _topology(rng):
+    kind = rng.choice(["grid", "wan", "fabric"])
+    if kind == "grid":
+        n = rng.randint(2, 13)
+        opts = dict(n=n, prefixesPerNode=rng.randint(1, 3), prefixSeed=rng.getrandbits(32),
+                    metricSeed=rng.choice([0, rng.getrandbits(32) | 1]),
+                    metricMax=rng.choice([10, 100, 85000, 300000000]))
+        names = [str(i) for i in range(n * n)]
+    elif kind == "wan":
+        n = rng.randint(12, 400)
+        opts = dict(nodes=n, k=rng.randint(2, 4), seed=rng.getrandbits(32),
+                    prefixesPerNode=rng.randint(1, 3))
+        names = [str(i) for i in range(n)]
+    else:
+        pods, planes = rng.randint(1, 4), rng.randint(1, 4)
+        ssw, rsw = rng.randint(1, 6), rng.randint(1, 8)
+        opts = dict(pods=pods, planes=planes, sswPerPlane=ssw, rswPerPod=rsw,
+                    full=rng.random() < 0.7, prefixesPerNode=rng.randint(1, 2),
+                    prefixSeed=rng.getrandbits(32))
+        names = ([f"1-{p}-{s}" for p in range(planes) for s in range(ssw)] +
+                 [f"2-{p}-{f}" for p in range(pods) for f in range(planes)] +
+                 [f"3-{p}-{r}" for p in range(pods) for r in range(rsw)])
+    opts.update(_mix(rng))
+    return kind, opts, names
+
+
+def _policy(rng, names, areas):
+    if rng.random() < 0.6:
+        return []
+    tags = ["ucmp", "c0", "c1", "c2", "c3"]
+    out = []
+    for k in range(rng.randint(1, 40)):
+        nb = rng.sample(names, min(3, len(names)))
+        st = dict(name=f"s{k}", tags=rng.sample(tags, rng.randint(1, 2)),
+                  set_weight=dict(default_weight=rng.choice([0, 1, 3]),
+                                  area_to_weight={a: rng.randint(0, 2) for a in areas},
+                                  neighbor_to_weight={x: rng.randint(0, 4) for x in nb}))
+        if k % 3 == 0:
+            st["counterID"] = f"c{k}"
+        out.append(st)
+    return out
+
+
+@pytest.mark.parametrize("seed", range(160))
+def test_single_area_feature_sweep(product, oracle, seed):
+    rng = random.Random(0xF022 + seed)
+    kind, opts, names = _topology(rng)
+    srcs = rng.sample(names, min(len(names), rng.randint(1, 5))) + ["no-such-node"]
+    v4, sr, brs = rng.random() < 0.7, rng.random() < 0.4, rng.random() < 0.5
+    pol = _policy(rng, names, ["test_area_name"])
+    label = f"{kind} {opts} v4={v4} sr={sr} brs={brs} pol={len(pol)}"
+    _cmp(product.gen_route_dbs(kind, opts, srcs, v4, sr, brs, pol),
+         oracle.gen_route_dbs(kind, opts, srcs, v4, sr, brs, pol), label)
+
+
+@pytest.mark.parametrize("seed", range(40))
+def test_route_db_batch_feature_sweep(product, oracle, seed):
+    """f2: the same sources through ONE RouteDbBatch (resident records, per
+    node materialisation) against the oracle's per-source buildRouteDb."""
+    rng = random.Random(0xF2F2 + seed)
+    kind, opts, names = _topology(rng)
+    srcs = rng.sample(names, min(len(names), rng.randint(2, 8)))
+    v4, sr, brs = rng.random() < 0.7, rng.random() < 0.4, rng.random() < 0.5
+    got = product.gen_route_db_batch(kind, opts, srcs, v4, sr, brs)
+    want = oracle.gen_route_dbs(kind, opts, srcs, v4, sr, brs, [])
+    _cmp(got[0] if isinstance(got, tuple) else got, want, f"batch {kind} {opts}")
+
+
+@pytest.mark.parametrize("seed", range(60))
+def test_multi_area_feature_sweep(product, oracle, seed):
+    rng = random.Random(0xF0A5 + seed)
+    A = rng.randint(2, 6)
+    npa, abrs = rng.randint(5, 80), rng.randint(1, 10)
+    opts = dict(areas=A, nodesPerArea=npa, abrs=abrs, k=rng.randint(2, 4),
+                seed=rng.getrandbits(32), prefixesPerNode=rng.randint(1, 3))
+    opts.update(_mix(rng))
+    names = [f"a{a}-{i}" for a in range(A) for i in range(npa)] + [f"abr-{i}" for i in range(abrs)]
+    srcs = rng.sample(names, rng.randint(1, 4)) + ["no-such-node"]
+    v4, sr, brs = rng.random() < 0.7, rng.random() < 0.4, rng.random() < 0.5
+    pol = _policy(rng, names, [f"area{a}" for a in range(A)])
+    _cmp(product.gen_route_dbs_multiarea(opts, srcs, v4, sr, brs, pol),
+         oracle.gen_route_dbs_multiarea(opts, srcs, v4, sr, brs, pol),
+         f"multiarea {opts} v4={v4} sr={sr} brs={brs} pol={len(pol)}")
+
+
+class _Opt:
+    """Sets an engine option for the block, then restores `reset`."""
+
+    def __init__(self, name, value, reset):
+        import openr_amd.capi as capi
+        self.lib, self.name, self.value, self.reset = capi.load(), name, value, reset
+
+    def __enter__(self):
+        import openr_amd.capi as capi
+        capi.check(self.lib, self.lib.ogs_set_option(self.name, self.value), self.name.decode())
+
+    def __exit__(self, *a):
+        self.lib.ogs_set_option(self.name, self.reset)
+
+
+# kernel-path overrides (option, value, default): the same sweep through the
+# paths the size dispatcher would not pick for these small topologies
+PATHS = {
+    "global_lds0": [(b"spf_global", 1, 0), (b"spf_global_lds", 0, 1)],
+    "global_lds3": [(b"spf_global", 1, 0), (b"spf_global_lds", 3, 1)],
+    "global_hbm_nosync": [(b"spf_global", 1, 0), (b"spf_global_lds", 0, 1),
+                          (b"spf_global_sync", 0, 1)],
+    "workgroup_units": [(b"unit_width", 256, -1)],
+    "wave_plain": [(b"wave_opt", 0, 2)],
+}
+
+
+@pytest.mark.parametrize("path", sorted(PATHS))
+@pytest.mark.parametrize("seed", range(12))
+def test_forced_path_feature_sweep(product, oracle, path, seed):
+    rng = random.Random(0xF0F0 + seed)
+    kind, opts, names = _topology(rng)
+    srcs = rng.sample(names, min(len(names), rng.randint(1, 4))) + ["no-such-node"]
+    v4, sr, brs = rng.random() < 0.7, rng.random() < 0.4, rng.random() < 0.5
+    pol = _policy(rng, names, ["test_area_name"])
+    with contextlib.ExitStack() as st:
+        for name, value, reset in PATHS[path]:
+            st.enter_context(_Opt(name, value, reset))
+        got = product.gen_route_dbs(kind, opts, srcs, v4, sr, brs, pol)
+    _cmp(got, oracle.gen_route_dbs(kind, opts, srcs, v4, sr, brs, pol),
+         f"{path}: {kind} {opts} v4={v4} sr={sr} brs={brs} pol={len(pol)}")
+
+
+@pytest.mark.parametrize("desc", [1, 0])
+@pytest.mark.parametrize("seed", range(24))
+def test_link_failure_variants_feature_sweep(product, oracle, seed, desc):
+    """C4 / f1 on the random feature mix: single and dual link failures from
+    a random source, by a full SPF per variant (mode 0), by the tight-DAG
+    repair (mode 1; A from the descendant rows or grown per variant) and by
+    the repair writing changed records only (mode 2, then the route updates),
+    against the oracle's updateAdjacencyDatabase + buildRouteDb +
+    calculateUpdate per variant (SpfSolver.cpp:21-56)."""
+    rng = random.Random(0xF0C4 + seed)
+    kind, opts, names = _topology(rng)
+    src = rng.choice(names)
+    brs = rng.random() < 0.5
+    n, vseed = 24, rng.getrandbits(32)
+    base, variants, links = oracle.variant_route_updates(kind, opts, src, n, vseed, 500,
+                                                         True, brs)
+    label = f"{kind} {opts} src={src} brs={brs}"
+    with _Opt(b"c4_desc", desc, 1):
+        for mode in (0, 1, 2):
+            vr = product.VariantRunner(True, brs)
+            vr.setup(kind, opts, src, n, vseed, 500)
+            vr.set_mode(mode)
+            vr.launch(0, True)
+            if mode < 2:
+                vr.download()
+                for v, (canon, changed, nu, nd) in enumerate(variants):
+                    assert vr.canonical(v) == canon, f"mode {mode} variant {v} {links[v]}: {label}"
+                    assert vr.changed(v) == changed and vr.counts(v) == (nu, nd), \
+                        f"mode {mode} variant {v} {links[v]}: {label}"
+            else:
+                vr.fetch_updates(0)
+                assert vr.base_canonical() == base, label
+                for v, (canon, changed, nu, nd) in enumerate(variants):
+                    upd, dele = vr.update(v)
+                    assert sorted(upd + dele) == changed and (len(upd), len(dele)) == (nu, nd), \
+                        f"variant {v} {links[v]}: {label}"
+                    assert vr.updated_canonical(v) == canon, f"variant {v} {links[v]}: {label}"
