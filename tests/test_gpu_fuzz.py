@@ -206,3 +206,36 @@ def test_link_failure_variants_feature_sweep(product, oracle, seed, desc):
                     assert sorted(upd + dele) == changed and (len(upd), len(dele)) == (nu, nd), \
                         f"variant {v} {links[v]}: {label}"
                     assert vr.updated_canonical(v) == canon, f"variant {v} {links[v]}: {label}"
+
+
+KSP_PATHS = [[], [(b"ksp_hbm", 1, 0)], [(b"ksp_wave_trace", 0, 1)], [(b"ksp_queue", 0, 1)]]
+
+
+@pytest.mark.parametrize("seed", range(64))
+def test_ksp2_feature_sweep(product, oracle, seed):
+    """getKthPaths / prefetchKthPaths (LinkState.cpp:226-247, 674-703) on
+    random grids: metric sets with zeros / negatives / large values, parallel
+    links (engine and oracle share the canonical link order),
+    hard-drained nodes, k = 1..3 single calls and the k = 1, 2 batch, through
+    the default, HBM-state, lane-0-trace and queue KSP paths."""
+    import test_gpu_ksp_domains as K
+    rng = random.Random(0xF05B + seed)
+    n = rng.randint(2, 8)
+    metrics = rng.choice([[1], [1, 2, 3, 5], [0, 1, 2], [0], [1, 2, -3], [0, 1, -1, 9],
+                          [20000000, 21000000, 1]])
+    parallel = rng.random() < 0.3
+    overload = set(rng.sample(range(n * n), rng.randint(0, max(0, n * n // 8))))
+    path = KSP_PATHS[seed % len(KSP_PATHS)]
+    gseed = rng.getrandbits(16)
+    with contextlib.ExitStack() as st:
+        for name, value, reset in path:
+            st.enter_context(_Opt(name, value, reset))
+        pa, pls = K._grid(product, n, gseed, metrics, parallel, overload)
+        oa, ols = K._grid(oracle, n, gseed, metrics, parallel, overload)
+        K._check_single(pls, ols, K._pairs(n, 8, gseed), ks=(1, 2, 3))
+        src = str(rng.randrange(n * n))
+        pls.prefetchKthPaths(src, [str(i) for i in range(n * n)])
+        for d in range(n * n):
+            for k in (1, 2):
+                assert K._paths(pls, src, str(d), k) == K._paths(ols, src, str(d), k), \
+                    (path, n, metrics, parallel, sorted(overload), src, d, k)
