@@ -728,7 +728,7 @@ DecisionRouteDb materializeRouteDb(
 // run in one launch (ogs_spf_routes_variants, route diff fused in); only the
 // changed records are gathered on the device (ogs_route_changes_gather) and
 // materialised. Areas with zero / negative link metrics or path sums past 32
-// bits run each variant as its own topology in one ogs_spf_routes launch
+// bits, and sources of degree > 128, run each variant as its own topology in one ogs_spf_routes launch
 // (exact extraction order, 64-bit distances) and diff on the host with
 // calculateUpdate. Node-segment labels are not part of the sweep (off in the
 // DecisionBenchmark config). `ls` and `ps` must outlive the

@@ -44,7 +44,9 @@ LinkFailureSweep::LinkFailureSweep(
   exactOrder_ = f.hasZeroMetric || f.hasWideMetric;
   const uint32_t s = sIt->second;
   W_ = std::max(1, ogs_nh_words_for_degree(int(f.rowPtr[s + 1] - f.rowPtr[s])));
-  if (W_ > 4) throw std::domain_error("LinkFailureSweep: source degree > 128");
+  // next-hop sets of more than 4 words (source degree > 128): past the
+  // variants kernel, ogs_spf_routes takes up to 16
+  if (W_ > 4) exact_ = true;
 
   // dead directed edges: both directions of every failed link
   auto edgeOf = [&](const std::string& node, auto&& pred) -> uint32_t {

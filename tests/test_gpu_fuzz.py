@@ -295,3 +295,25 @@ def test_batch_runner_feature_sweep(product, oracle, seed):
         lib.ogs_set_option(b"ms_group", 0)
     _cmp(got, oracle.gen_route_dbs(kind, opts, srcs, v4, False, brs),
          f"batch {kind} {opts} {options} v4={v4} brs={brs}")
+
+
+@pytest.mark.parametrize("brs", [False, True])
+def test_link_failure_variants_wide_source(product, oracle, brs):
+    """A source of degree 140 (FSW of a fabric with 100 SSWs and 40 RSWs per
+    pod): 5-word next-hop sets, past the variants kernel, through the
+    per-variant-topology path."""
+    opts = dict(pods=2, planes=1, sswPerPlane=100, rswPerPod=40, prefixesPerNode=1,
+                anycastPermille=100, nodeOverloadPermille=20)
+    n = 24
+    base, variants, links = oracle.variant_route_updates("fabric", opts, "2-0-0", n, 0xC4F,
+                                                         500, True, brs)
+    vr = product.VariantRunner(True, brs)
+    vr.setup("fabric", opts, "2-0-0", n, 0xC4F, 500)
+    vr.launch(0, True)
+    vr.fetch_updates(0)
+    assert vr.base_canonical() == base
+    assert any(c for _, c, _, _ in variants)
+    for v, (canon, changed, nu, nd) in enumerate(variants):
+        upd, dele = vr.update(v)
+        assert sorted(upd + dele) == changed and (len(upd), len(dele)) == (nu, nd), v
+        assert vr.updated_canonical(v) == canon, f"variant {v} {links[v]}"
