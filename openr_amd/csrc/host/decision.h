@@ -860,6 +860,12 @@ class RouteDbBatch {
   DeviceBuffer dDesc_, dPfxBase_, dAdvOff_, dAdvNode_, dAdvMetrics_, dAdvMinNh_,
       dPfxFlags_;
   bool launched_{false};
+  // multi-area domain: served node by node through a private solver's
+  // multi-area buildRouteDb (areaLinkStates / prefixState must outlive it)
+  bool multiArea_{false};
+  const AreaLinkStates* als_{nullptr};
+  const PrefixState* ps_{nullptr};
+  std::unique_ptr<SpfSolver> multi_;
 };
 
 }  // namespace openr_amd

@@ -10,6 +10,7 @@
 // records in HBM and materialises a node's RouteDb only when it is asked for.
 #include <thread>
 #include <algorithm>
+#include <memory>
 #include <stdexcept>
 
 #include "decision.h"
@@ -34,7 +35,23 @@ RouteDbBatch::RouteDbBatch(const SpfSolver& solver, const AreaLinkStates& als,
                            const PrefixState& ps, const std::vector<std::string>& sources)
     : solver_(solver), sources_(sources) {
   if (als.size() != 1) {
-    throw std::domain_error("RouteDbBatch: one area (multi-area builds go through buildRouteDb)");
+    // multi-area domain: each served node is a multi-area buildRouteDb
+    // (route_multiarea_kernel over every area's SPF) on a private solver with
+    // the caller's settings and static routes -- getDecisionRouteDb exactly
+    multiArea_ = true;
+    als_ = &als;
+    ps_ = &ps;
+    for (size_t i = 0; i < sources_.size(); ++i) {
+      if (!index_.emplace(sources_[i], i).second) {
+        throw std::invalid_argument("RouteDbBatch: duplicate source " + sources_[i]);
+      }
+    }
+    multi_ = std::make_unique<SpfSolver>(solver.myNodeName_, solver.enableV4_,
+                                         solver.enableNodeSegmentLabel_,
+                                         solver.enableBestRouteSelection_,
+                                         solver.v4OverV6Nexthop_);
+    multi_->staticUnicastRoutes_ = solver.staticUnicastRoutes_;
+    return;
   }
   area_ = als.begin()->first;
   ls_ = &als.begin()->second;
@@ -121,6 +138,10 @@ ogs_prefix_table RouteDbBatch::table() const {
 }
 
 void RouteDbBatch::launch(void* stream) {
+  if (multiArea_) {  // built per served node (routeDb)
+    launched_ = true;
+    return;
+  }
   const ogs_graph g = graph();
   const ogs_prefix_table pt = table();
   const uint32_t flags = (solver_.enableV4_ ? OGS_F_ENABLE_V4 : 0u) |
@@ -189,6 +210,11 @@ bool RouteDbBatch::fetchUnit(const std::string& node, void* stream, UnitRecords&
 
 std::optional<DecisionRouteDb> RouteDbBatch::routeDb(const std::string& node,
                                                      void* stream) const {
+  if (multiArea_) {
+    if (!index_.count(node)) throw std::out_of_range("RouteDbBatch: not a source: " + node);
+    if (!launched_) throw std::logic_error("RouteDbBatch: launch() first");
+    return multi_->buildRouteDb(node, *als_, *ps_);
+  }
   UnitRecords r;
   if (!fetchUnit(node, stream, r)) return std::nullopt;
   const FlatTopology& f = ls_->flat();
@@ -222,6 +248,14 @@ RouteDatabase RouteDbBatch::getRouteDbComputed(const std::string& node, void* st
   RouteDatabase out;  // Decision.cpp:341-360
   const std::string& n = node.empty() ? solver_.myNodeName_ : node;
   out.thisNodeName = n;
+  if (multiArea_) {
+    if (auto db = routeDb(n, stream)) {
+      RouteDatabase t = db->toThrift();
+      out.unicastRoutes = std::move(t.unicastRoutes);
+      out.mplsRoutes = std::move(t.mplsRoutes);
+    }
+    return out;
+  }
   UnitRecords r;
   if (!fetchUnit(n, stream, r)) return out;
   const FlatTopology& f = ls_->flat();

@@ -1617,6 +1617,38 @@ PYBIND11_MODULE(_decision, m) {
   // RouteDbBatch (resident records, per-node materialisation); canonical text
   // per source ("NONE" without a RouteDb) and the getRouteDbComputed shape
   // (thisNodeName, unicast routes, mpls routes, next hops in total)
+  // f2 over a multi-area domain (loadMultiArea): RouteDbBatch served per node
+  // (canonical text per source, and whether getRouteDbComputed equals
+  // routeDb(node)->toThrift() with thisNodeName = node)
+  m.def("gen_route_db_batch_multiarea",
+        [](py::dict opts, std::vector<std::string> sources, bool enableV4, bool sr, bool brs) {
+          AreaLinkStates als;
+          PrefixState ps;
+          loadMultiArea(opts, als, ps);
+          SpfSolver solver("test_node", enableV4, sr, brs);
+          RouteDbBatch batch(solver, als, ps, sources);
+          batch.launch();
+          std::vector<py::bytes> out;
+          py::list same;
+          for (const auto& s : sources) {
+            auto db = batch.routeDb(s);
+            out.push_back(py::bytes(db ? canonical(*db) : std::string("NONE")));
+            const RouteDatabase r = batch.getRouteDbComputed(s);
+            RouteDatabase want;
+            if (db) want = db->toThrift();
+            bool eq = r.thisNodeName == s &&
+                r.unicastRoutes.size() == want.unicastRoutes.size() &&
+                r.mplsRoutes.size() == want.mplsRoutes.size();
+            for (size_t i = 0; eq && i < r.unicastRoutes.size(); ++i) {
+              eq = r.unicastRoutes[i].dest == want.unicastRoutes[i].dest &&
+                  r.unicastRoutes[i].nextHops == want.unicastRoutes[i].nextHops;
+            }
+            same.append(eq);
+          }
+          return py::make_tuple(out, same);
+        },
+        py::arg("opts"), py::arg("sources"), py::arg("enableV4") = true, py::arg("sr") = false,
+        py::arg("brs") = false);
   m.def("gen_route_db_batch",
         [](const std::string& kind, py::dict opts, std::vector<std::string> sources,
            bool enableV4, bool sr, bool brs) {

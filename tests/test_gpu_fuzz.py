@@ -317,3 +317,22 @@ def test_link_failure_variants_wide_source(product, oracle, brs):
         upd, dele = vr.update(v)
         assert sorted(upd + dele) == changed and (len(upd), len(dele)) == (nu, nd), v
         assert vr.updated_canonical(v) == canon, f"variant {v} {links[v]}"
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_route_db_batch_multi_area_sweep(product, oracle, seed):
+    """f2 over a multi-area domain: RouteDbBatch serves each node with the
+    multi-area buildRouteDb (getDecisionRouteDb, Decision.cpp:341-360)."""
+    rng = random.Random(0xFB2A + seed)
+    A = rng.randint(2, 5)
+    npa, abrs = rng.randint(5, 60), rng.randint(1, 8)
+    opts = dict(areas=A, nodesPerArea=npa, abrs=abrs, k=rng.randint(2, 4),
+                seed=rng.getrandbits(32), prefixesPerNode=rng.randint(1, 3))
+    opts.update(_mix(rng))
+    names = [f"a{a}-{i}" for a in range(A) for i in range(npa)] + [f"abr-{i}" for i in range(abrs)]
+    srcs = rng.sample(names, rng.randint(1, 5)) + ["no-such-node"]
+    v4, sr, brs = rng.random() < 0.7, rng.random() < 0.4, rng.random() < 0.5
+    got, same = product.gen_route_db_batch_multiarea(opts, srcs, v4, sr, brs)
+    assert all(same)
+    _cmp(got, oracle.gen_route_dbs_multiarea(opts, srcs, v4, sr, brs, []),
+         f"multiarea batch {opts} v4={v4} sr={sr} brs={brs}")
