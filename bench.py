@@ -36,12 +36,11 @@ import torch  # noqa: E402,F401
 import numpy as np  # noqa: E402
 
 from openr_amd import shard  # noqa: E402
-from openr_amd.workloads import (C2_OPTS, C2_SOURCE, C2_TOPOS, C3_OPTS, C4_OPTS,  # noqa: E402
+from openr_amd.workloads import (C1_OPTS, C1_SOURCE, C2_OPTS, C2_SOURCE, C2_TOPOS, C3_OPTS, C4_OPTS,  # noqa: E402
                                  C4_SOURCE, C4_VARIANTS, C4_SEED, C4_DUAL_PERMILLE,
                                  c3_source_names)
 
 GRID_N = C2_OPTS["n"]
-C1_OPTS = dict(n=10, prefixSeed=0xC1)  # createGrid(10) wiring, metric 1
 C3_INC_SOURCE = "2-0-0"  # a fabric FSW (incremental-routes sub-line)
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 CPU_REPS = 5  # BASELINE.md timing rule: median of >= 5 repetitions
@@ -71,8 +70,17 @@ def log(msg):
     print(f"bench.py [{time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
+def host_cores():
+    """The cores this process may run on (the lease's CPU share; os.cpu_count()
+    is the whole machine's)."""
+    try:
+        return len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        return os.cpu_count() or 1
+
+
 def cpu_threads():
-    return max(1, min(16, os.cpu_count() or 1))  # the box's CPU share
+    return max(1, host_cores())  # BASELINE.md: T = the cores actually available
 
 
 def host_info():
@@ -85,7 +93,7 @@ def host_info():
                     break
     except OSError:
         pass
-    return {"nproc": os.cpu_count(), "model": model}
+    return {"cores": host_cores(), "machine_cpus": os.cpu_count(), "model": model}
 
 
 def median(xs):
@@ -117,22 +125,27 @@ def pmc_traffic(tag, match):
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_pmc_{tag}.json")))
     if not files:
-        return None, None
+        return None, None, None
     with open(files[-1]) as f:
         d = json.load(f)
     matches = (match,) if isinstance(match, str) else tuple(match)
     hits = [v["hbm_bytes_per_launch"] for k, v in d.items()
-            if any(m in k for m in matches) and v.get("hbm_bytes_per_launch") is not None]
+            if not k.startswith("_") and any(m in k for m in matches)
+            and v.get("hbm_bytes_per_launch") is not None]
     if not hits:
-        return None, None
-    return float(sum(hits)), os.path.relpath(files[-1], ROOT)
+        return None, None, None
+    meta = d.get("_meta", {})
+    return float(sum(hits)), os.path.relpath(files[-1], ROOT), meta.get("commit")
 
 
 def set_traffic(line, tag, match, scale=1.0):
-    traffic, src = pmc_traffic(tag, match)
+    """roofline.traffic from the committed PMC summary (per launch of the
+    matching kernels, summed), with the commit that summary measured."""
+    traffic, src, commit = pmc_traffic(tag, match)
     if traffic is not None:
         line["roofline"]["traffic"] = round(traffic * scale, 1)
         line["roofline"]["traffic_source"] = src
+        line["roofline"]["traffic_commit"] = commit
 
 
 # ----------------------------------------------------------------- C2 ---
@@ -169,15 +182,20 @@ def run_c1(args, rank):
         return None
     import openr_amd
     reps = 21
-    cold, warm, routes = openr_amd.decision.build_latency_bench("grid", C1_OPTS, "1", reps)
+    cold, warm, routes, d_cold, d_warm = openr_amd.decision.build_latency_bench(
+        "grid", C1_OPTS, C1_SOURCE, reps)
     out = {"unit": "us/build", "gpu_cold_us": round(median(cold), 1),
            "gpu_warm_us": round(median(warm), 1), "routes": routes, "reps": reps,
+           "route_digest": f"{d_cold:016x}",
            "note": "drop-in SpfSolver::buildRouteDb('1'): cold = fresh LinkState/PrefixState/"
                    "solver (CSR flatten + H2D + kernel + D2H + materialisation), warm = same "
                    "objects again (device tables cached); median of reps"}
+    # the RouteDb of the cold and the warm build vs the oracle's golden
+    golden_check(out, "c1", d_cold, GOLDEN.get("c1"))
+    golden_check(out, "c1_warm", d_warm, GOLDEN.get("c1"))
     if not args.no_cpu_baseline:
         n = 2 * CPU_REPS + 1
-        cpu = oracle().cpu_time_build("grid", C1_OPTS, "1", n)
+        cpu = oracle().cpu_time_build("grid", C1_OPTS, C1_SOURCE, n)
         out["cpu_baseline"] = {
             "value": round(median(cpu), 1), "unit": "us/build", "cores": 1, "kind": "port",
             "reps": n, "host": host_info(),
@@ -374,8 +392,7 @@ def run_c3(args, torch, dist, rank, world, local_rank):
     lib = capi.load()
     lib.ogs_set_device(local_rank)
     dev = torch.device("cuda", local_rank)
-    steps = args.steps if args.config == "c3" else args.c3_steps
-    warmup = args.warmup if args.config == "c3" else 2
+    steps, warmup = args.steps, args.warmup  # C3 is the headline (or --config c3)
     ppn = args.prefixes_per_node
     # sources interleaved over ranks (balances SSW/FSW/RSW degree classes)
     mine = shard.interleave(c3_source_names(), rank, world)
@@ -650,8 +667,8 @@ def run_c4(args, torch, dist, rank, world, local_rank):
     line["config"]["mode"] = {0: "full SPF per variant", 1: "base-SPF repair",
                               2: "base-SPF repair, changed records only"}[mode]
     if world == 1:
-        set_traffic(line, "c4", "spf_variant_repair_kernel<true>" if mode == 2
-                    else "spf_frontier_kernel<1, true, true, true")
+        set_traffic(line, "c4", ("spf_variant_repair_kernel<true>", "tight_desc_kernel")
+                    if mode == 2 else "spf_frontier_kernel<1, true, true, true")
         if not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline_c4()
             # f1 beside the reference: Decision::rebuildRoutes per variant =
@@ -770,13 +787,16 @@ def run_c5(args, torch, dist, rank, world, local_rank):
     routes_job, paths_job = shard.reduce_xor(dist, torch, dev, [routes_digest, paths_digest])
     if rank != 0:
         return None
-    # KSP2 unit (CSR + E/8 mask + 4N + path output): the
-    # area's CSR staged once (4(N+1) + 8E), the source's distance row (4N),
-    # both path sets (4 B per path edge, 4 B per path, 4 B count each)
+    # KSP2 unit: the shared inputs counted once per batch
+    # that shares them -- the source area's CSR (4(N+1) + 8E + N/8) / S with
+    # S = the destinations of the job -- plus the unit's own E/8 link mask,
+    # 4N distance row and path output (4 B per path edge, 4 B per path,
+    # 4 B count, for k = 1 and k = 2)
     Na = sh["source_area_nodes"] / 2
     Ea = sh["source_area_edges"] / 2
     pe = sh["path_edges_k1"] + sh["path_edges_k2"]
-    bpu = 4 * (Na + 1) + 8 * Ea + 4 * Na + (4 * pe + 8 * 2 * U) / max(U, 1) + 8
+    shared = 2 * (4 * (Na + 1) + 8 * Ea + Na / 8)  # both areas of the source
+    bpu = (shared / max(U, 1) + Ea / 8 + 4 * Na + (4 * pe + 8 * 2 * U) / max(U, 1) + 8)
     achieved = bpu * U / (ksp_ms * 1e-3) / 1e9
     value = steps / tmax
     line = {
@@ -824,74 +844,17 @@ def finish(line):
         raise SystemExit(1)
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5"])
-    ap.add_argument("--prefixes-per-node", type=int, default=100)
-    ap.add_argument("--c3-streams", type=int, default=2, choices=[1, 2],
-                    help="C3: HIP streams for the two source groups")
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--topos", type=int, default=C2_TOPOS)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-extras", action="store_true",
-                    help="skip the f1-f4 sub-lines run after the timed regions (PMC "
-                         "passes: only the timed launches reach the counters)")
-    ap.add_argument("--no-c1", action="store_true",
-                    help="skip the C1 single-source latency line embedded in the C2 result")
-    ap.add_argument("--no-g1", action="store_true",
-                    help="skip the 20,000-node WAN sub-line (global-state SPF path)")
-    ap.add_argument("--no-c3", action="store_true",
-                    help="skip the C3 fabric all-sources line embedded in the C2 result")
-    ap.add_argument("--c3-steps", type=int, default=10)
-    ap.add_argument("--c3-order", default="wide-first", choices=["narrow-first", "wide-first"],
-                    help="C3: which next-hop width group is dispatched first")
-    ap.add_argument("--no-c4", action="store_true",
-                    help="skip the C4 link-failure sweep line embedded in the C2 result")
-    ap.add_argument("--c4-steps", type=int, default=5)
-    ap.add_argument("--no-c5", action="store_true",
-                    help="skip the C5 multi-area KSP2 + UCMP line embedded in the C2 result")
-    ap.add_argument("--c5-steps", type=int, default=5)
-    ap.add_argument("--c5-streams", type=int, default=2, choices=[1, 2],
-                    help="C5: HIP streams (RouteDb+policy || KSP2)")
-    ap.add_argument("--opt", action="append", default=[],
-                    help="engine option name=value (ogs_set_option), for A/B runs")
-    args = ap.parse_args()
-
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    # OGS_BENCH_SHARE_DEVICE=1: rehearsal of the N>1 path on a box with fewer
-    # GPUs than ranks (ranks share devices round-robin; gloo carries the
-    # per-rank records since RCCL refuses two ranks on one GPU). Never set by
-    # the driver; the numbers of such a run are not scaling numbers.
-    share = os.environ.get("OGS_BENCH_SHARE_DEVICE") == "1"
-    if share:
-        local_rank %= torch.cuda.device_count()
-    torch.cuda.set_device(local_rank)
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        if share:
-            dist.init_process_group("gloo")
-        else:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-
+# ----------------------------------------------------------------- C2 ---
+def run_c2(args, torch, dist, rank, world, local_rank):
+    """Config C2 (BASELINE.json configs[1]): a batch of 4096 random-metric
+    10x10 grid topologies per GPU (weak scaling: rank r owns block r), ECMP
+    SPF from node "1" + full RouteDb for each; one step = one launch of the
+    fused wave kernel over the batch; one build = one (topology, source)
+    SPF + RouteDb."""
     import openr_amd
     import openr_amd.capi as capi
-    for o in args.opt:
-        name, val = o.split("=", 1)
-        lib0 = capi.load()
-        capi.check(lib0, lib0.ogs_set_option(name.encode(), int(val)), name)
-    single = {"c3": run_c3, "c4": run_c4, "c5": run_c5}.get(args.config)
-    if single is not None:
-        line = single(args, torch, dist, rank, world, local_rank)
-        if dist:
-            dist.destroy_process_group()
-        if line is not None:
-            finish(line)
-        return
+    steps = args.steps if args.config == "c2" else args.c2_steps
+    warmup = args.warmup if args.config == "c2" else args.c2_warmup
     openr_amd.require_gpu()
     M = openr_amd.decision
     lib = capi.load()
@@ -953,7 +916,7 @@ def main():
         if rc != 0:
             capi.check(lib, rc, "ogs_spf_routes")
 
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         step()
     torch.cuda.synchronize(dev)
     if dist:
@@ -963,7 +926,7 @@ def main():
     ev1 = torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     ev0.record(stream)
-    for _ in range(args.steps):
+    for _ in range(steps):
         step()
     ev1.record(stream)
     torch.cuda.synchronize(dev)
@@ -971,7 +934,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t0
-    kernel_ms = ev0.elapsed_time(ev1) / args.steps  # one launch per step
+    kernel_ms = ev0.elapsed_time(ev1) / steps  # one launch per step
 
     # ---- digest of the timed launches' records + cross-rank reduction -----
     meta = o_meta.cpu().numpy()
@@ -988,15 +951,15 @@ def main():
         N, E, P = GRID_N * GRID_N, 4 * GRID_N * (GRID_N - 1), GRID_N * GRID_N
         bpu = algorithmic_bytes_per_unit(N, E, P, P, W, W)
         achieved = bpu * U / (kernel_ms * 1e-3) / 1e9
-        value = total_units * args.steps / tmax
+        value = total_units * steps / tmax
         line = {
-            "metric": "SPF+RouteDb builds/sec (whole node)",
+            "metric": "SPF+RouteDb (topology, source) builds/sec",
             "value": round(value, 1),
             "unit": "builds/s",
             "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(tmax / args.steps * 1e3, 4),
+            "steps": steps,
+            "warmup": warmup,
+            "ms_per_step": round(tmax / steps * 1e3, 4),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -1035,44 +998,184 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline_c2(U)
             log("c2 cpu baseline done")
+    return line
+
+
+SUB_KEYS = {
+    "c2_topology_batch": ("metric", "value", "unit", "ms_per_step", "kernel_ms", "gteps",
+                          "routes_per_step", "route_digest", "golden", "roofline",
+                          "cpu_baseline", "config", "steps", "warmup"),
+    "c4_link_failure_sweep": ("value", "unit", "ms_per_step", "kernel_ms", "gteps",
+                              "changed_routes_per_step", "route_digest", "golden",
+                              "route_update", "csr_update", "roofline", "cpu_baseline",
+                              "config", "steps"),
+    "c5_multiarea_ksp2_ucmp": ("value", "unit", "ms_per_step", "ksp2_dests_per_s",
+                               "route_kernels_ms", "ksp2_kernels_ms", "job_kernel_ms",
+                               "route_digest", "path_digest", "golden", "roofline",
+                               "config", "steps", "cpu_baseline"),
+}
+
+
+def launch_ranks(args):
+    """`--gpus N` without a torch.distributed launcher around us: start N
+    ranks as CHILD processes (torch.distributed.run, 127.0.0.1) and exit with
+    their status. Runs before anything touches the GPU; this process never
+    initialises HIP and never execs."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1",
+           f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    log(f"--gpus {args.gpus}: launching {args.gpus} ranks")
+    return subprocess.call(cmd)
+
+
+def check_world(args, world):
+    """The rank count must be the --gpus count: never silently measure fewer
+    GPUs than asked for."""
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        raise SystemExit(2)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="all",
+                    choices=["all", "c1", "c2", "c3", "c4", "c5", "g1"],
+                    help="all (default): the C3 headline line with the C1/C2/G1/C4/C5 "
+                         "sub-lines; cN: that config alone as the line")
+    ap.add_argument("--prefixes-per-node", type=int, default=100)
+    ap.add_argument("--c3-streams", type=int, default=2, choices=[1, 2],
+                    help="C3: HIP streams for the two source groups")
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one per GPU); without a launcher bench.py starts them")
+    ap.add_argument("--steps", type=int, default=20, help="timed steps of the headline line")
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--topos", type=int, default=C2_TOPOS)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="skip the f1-f4 sub-lines run after the timed regions (PMC "
+                         "passes: only the timed launches reach the counters)")
+    ap.add_argument("--no-c1", action="store_true", help="skip the C1 single-source line")
+    ap.add_argument("--no-g1", action="store_true",
+                    help="skip the 20,000-node WAN sub-line (global-state SPF path)")
+    ap.add_argument("--no-c2", action="store_true", help="skip the C2 topology-batch sub-line")
+    ap.add_argument("--c2-steps", type=int, default=50)
+    ap.add_argument("--c2-warmup", type=int, default=5)
+    ap.add_argument("--c3-order", default="wide-first", choices=["narrow-first", "wide-first"],
+                    help="C3: which next-hop width group is dispatched first")
+    ap.add_argument("--no-c4", action="store_true", help="skip the C4 link-failure sub-line")
+    ap.add_argument("--c4-steps", type=int, default=5)
+    ap.add_argument("--no-c5", action="store_true", help="skip the C5 multi-area sub-line")
+    ap.add_argument("--c5-steps", type=int, default=5)
+    ap.add_argument("--c5-streams", type=int, default=2, choices=[1, 2],
+                    help="C5: HIP streams (RouteDb+policy || KSP2)")
+    ap.add_argument("--opt", action="append", default=[],
+                    help="engine option name=value (ogs_set_option), for A/B runs")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="only join the process group and print the rank map (no GPU)")
+    args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        raise SystemExit(launch_ranks(args))
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    check_world(args, world)
+    if args.launch_check:
+        # CPU check of the launcher path: gloo group, all-gather of ranks
+        import torch.distributed as dist
+        if world > 1:
+            dist.init_process_group("gloo")
+        t = torch.tensor([rank, local_rank], dtype=torch.int64)
+        got = [torch.zeros_like(t) for _ in range(world)]
+        if world > 1:
+            dist.all_gather(got, t)
+            dist.destroy_process_group()
+        else:
+            got = [t]
+        if rank == 0:
+            print(json.dumps({"world": world, "ranks": [g.tolist() for g in got]}), flush=True)
+        return
+    # OGS_BENCH_SHARE_DEVICE=1: rehearsal of the N>1 path on a box with fewer
+    # GPUs than ranks (ranks share devices round-robin; gloo carries the
+    # per-rank records since RCCL refuses two ranks on one GPU). Never set by
+    # the driver; the numbers of such a run are not scaling numbers.
+    share = os.environ.get("OGS_BENCH_SHARE_DEVICE") == "1"
+    ndev = torch.cuda.device_count()
+    if share:
+        local_rank %= max(1, ndev)
+    elif world > 1 and local_rank >= ndev:
+        print(f"bench.py: rank {rank} needs GPU {local_rank}, {ndev} visible", file=sys.stderr)
+        raise SystemExit(2)
+    torch.cuda.set_device(local_rank)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        if share:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    import openr_amd
+    import openr_amd.capi as capi
+    openr_amd.require_gpu()
+    for o in args.opt:
+        name, val = o.split("=", 1)
+        lib0 = capi.load()
+        capi.check(lib0, lib0.ogs_set_option(name.encode(), int(val)), name)
+    single = {"c2": run_c2, "c3": run_c3, "c4": run_c4, "c5": run_c5,
+              "c1": lambda a, t, d, r, w, lr: run_c1(a, r),
+              "g1": lambda a, t, d, r, w, lr: run_g1(a, r)}.get(args.config)
+    if single is not None:
+        line = single(args, torch, dist, rank, world, local_rank)
+        if dist:
+            dist.destroy_process_group()
+        if line is not None:
+            finish(line)
+        elif DIGEST_FAILURES:
+            raise SystemExit(1)
+        return
+
+    # headline: the north-star config, C3 fabric all-sources (whole-node
+    # builds/s), sources sharded over the ranks; sub-lines after it
+    line = run_c3(args, torch, dist, rank, world, local_rank)
+    if not args.no_c2:
+        c2 = run_c2(args, torch, dist, rank, world, local_rank)
+        if rank == 0:
+            line["c2_topology_batch"] = {k: c2[k] for k in SUB_KEYS["c2_topology_batch"]
+                                         if k in c2}
+    if rank == 0:
         if not args.no_c1:
             line["c1_single_source"] = run_c1(args, rank)
         if not args.no_g1:
             log("g1 large WAN ...")
             line["g1_large_wan"] = run_g1(args, rank)
-    if not args.no_c3:
-        # the north-star headline config, sharded by source over the ranks
-        c3 = run_c3(args, torch, dist, rank, world, local_rank)
-        if rank == 0:
-            line["c3_fabric_all_sources"] = {
-                k: c3[k] for k in ("value", "unit", "ms_per_step", "kernel_ms",
-                                   "route_dbs_per_s", "gteps", "routes_per_step",
-                                   "route_digest", "golden", "serve", "publication_ingest",
-                                   "incremental_routes", "roofline", "cpu_baseline",
-                                   "config", "steps") if k in c3}
     if not args.no_c4:
         c4 = run_c4(args, torch, dist, rank, world, local_rank)
         if rank == 0:
-            line["c4_link_failure_sweep"] = {
-                k: c4[k] for k in ("value", "unit", "ms_per_step", "kernel_ms", "gteps",
-                                   "changed_routes_per_step", "route_digest", "golden",
-                                   "route_update", "csr_update", "roofline", "cpu_baseline",
-                                   "config", "steps") if k in c4}
+            line["c4_link_failure_sweep"] = {k: c4[k] for k in SUB_KEYS["c4_link_failure_sweep"]
+                                             if k in c4}
     if not args.no_c5:
         c5 = run_c5(args, torch, dist, rank, world, local_rank)
         if rank == 0:
-            line["c5_multiarea_ksp2_ucmp"] = {
-                k: c5[k] for k in ("value", "unit", "ms_per_step", "ksp2_dests_per_s",
-                                   "route_kernels_ms", "ksp2_kernels_ms", "job_kernel_ms",
-                                   "route_digest", "path_digest", "golden", "roofline",
-                                   "config", "steps", "cpu_baseline") if k in c5}
+            line["c5_multiarea_ksp2_ucmp"] = {k: c5[k] for k in SUB_KEYS["c5_multiarea_ksp2_ucmp"]
+                                              if k in c5}
     if dist:
         dist.destroy_process_group()
     if rank == 0:
         # sub-line digest results roll up into the headline line's golden map
-        for sub in ("c3_fabric_all_sources", "c4_link_failure_sweep", "c5_multiarea_ksp2_ucmp"):
-            for k, v in line.get(sub, {}).get("golden", {}).items():
-                line["golden"][k] = v
+        for sub in ("c2_topology_batch", "c1_single_source", "g1_large_wan",
+                    "c4_link_failure_sweep", "c5_multiarea_ksp2_ucmp"):
+            g = (line.get(sub) or {}).get("golden", {})
+            if isinstance(g, dict):
+                for k, v in g.items():
+                    line["golden"][k] = v
+            elif sub == "g1_large_wan":
+                line["golden"]["g1"] = g
         finish(line)
     elif DIGEST_FAILURES:
         raise SystemExit(1)

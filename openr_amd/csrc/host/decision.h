@@ -118,6 +118,11 @@ inline bool isV4Prefix(const std::string& p) {
   return p.find(':') == std::string::npos;
 }
 
+// "<addr>/<len>" -> the network folly::IPAddress::createNetwork(addr, len,
+// applyMask) prints (toIPNetwork, NetworkUtil.h:196-208); throws
+// std::invalid_argument on text toIPNetwork rejects. Defined in lsdb_codec.cpp.
+std::string prefixNetworkKey(const std::string& text, bool applyMask = true);
+
 using NodeAndArea = std::pair<std::string, std::string>;
 
 // ------------------------------------------------------------------ Link --
@@ -344,6 +349,14 @@ class PrefixState {
                                      const PrefixEntry& entry);
   std::set<std::string> updatePrefix(const std::string& node,
                                      const std::string& area, PrefixEntry&& entry);
+  // PrefixState::updatePrefix(PrefixKey, entry) (PrefixState.cpp:15-38) with
+  // the key's network given: `network` = toIPNetwork(entry.prefix) as
+  // Decision.cpp:772-773 builds it. The overloads above derive it from the
+  // entry; the entry itself is stored as advertised (host bits kept).
+  std::set<std::string> updatePrefixKeyed(const std::string& node, const std::string& area,
+                                          const std::string& network, PrefixEntry entry);
+  // `prefix` is the key's network as given (PrefixKey does not mask);
+  // compared by value, so the text is normalised first
   std::set<std::string> deletePrefix(const std::string& node,
                                      const std::string& area,
                                      const std::string& prefix);

@@ -276,7 +276,13 @@ Adjacency readAdjacency(Reader& r) {  // Types.thrift:145-215
   return a;
 }
 
-std::string readIpPrefix(Reader& r) {  // Network.thrift:55-58
+// The entry keeps the IpPrefix as advertised (host bits included), the way
+// Decision stores the raw thrift entry (Decision.cpp:758-778); `network`,
+// when asked for, receives toIPNetwork(prefix) (applyMask = true), the
+// PrefixState key. An address toIPNetwork rejects (not 4 / 16 bytes, length
+// out of range) throws here, so the key is dropped as Decision.cpp:781-784
+// drops it.
+std::string readIpPrefix(Reader& r, std::string* network) {  // Network.thrift:55-58
   std::string addr;
   int16_t len = 0;
   int16_t last = 0, id;
@@ -286,7 +292,8 @@ std::string readIpPrefix(Reader& r) {  // Network.thrift:55-58
     else if (id == 2 && t == CT_I16) len = r.zz16();
     else r.skip(t, 2);
   }
-  return ipPrefixToNetworkString(addr, len);
+  if (network) *network = ipPrefixToNetworkString(addr, len);
+  return ipPrefixToString(addr, len);
 }
 
 void readMetrics(Reader& r, PrefixMetrics& m) {  // Types.thrift:287-317
@@ -323,14 +330,14 @@ void readStringList(Reader& r, uint8_t t, std::vector<std::string>* vec,
   }
 }
 
-PrefixEntry readPrefixEntry(Reader& r) {  // Types.thrift:349-408
+PrefixEntry readPrefixEntry(Reader& r, std::string* network) {  // Types.thrift:349-408
   PrefixEntry e;
   int16_t last = 0, id;
   uint8_t t;
   while (r.field(last, id, t)) {
     switch (id) {
       case 1:
-        if (t == CT_STRUCT) { e.prefix = readIpPrefix(r); continue; }
+        if (t == CT_STRUCT) { e.prefix = readIpPrefix(r, network); continue; }
         break;
       case 2:
         if (t == CT_I32) { e.type = r.zz32(); continue; }
@@ -599,6 +606,38 @@ std::string stringToBinaryAddress(const std::string& text) {
   return std::string(reinterpret_cast<char*>(buf), fam == AF_INET6 ? 16 : 4);
 }
 
+// The IpPrefix as advertised, "<addr>/<len>" with the host bits kept
+// (toString of the raw thrift struct's address, NetworkUtil.h:26-40).
+std::string ipPrefixToString(std::string_view raw, int16_t len) {
+  if (raw.size() != 4 && raw.size() != 16) fail("prefix: address must be 4 or 16 bytes");
+  int bits = int(raw.size()) * 8;
+  if (len < 0 || len > bits) fail("prefix: length out of range");
+  return formatAddress(reinterpret_cast<const unsigned char*>(raw.data()),
+                       raw.size() == 16 ? AF_INET6 : AF_INET) + "/" + std::to_string(len);
+}
+
+// "<addr>/<len>" text -> toIPNetwork(prefix, applyMask) printed as
+// folly::IPAddress::networkToString (NetworkUtil.h:196-208).
+std::string prefixNetworkKey(const std::string& text, bool applyMask) {
+  auto slash = text.rfind('/');
+  if (slash == std::string::npos || slash + 1 == text.size() || text.size() - slash > 4)
+    throw std::invalid_argument("Invalid IPAddress: " + text);
+  int len = 0;
+  for (size_t i = slash + 1; i < text.size(); ++i) {
+    if (text[i] < '0' || text[i] > '9') throw std::invalid_argument("Invalid IPAddress: " + text);
+    len = len * 10 + (text[i] - '0');
+  }
+  unsigned char buf[16];
+  int fam;
+  if (!parseAddress(text.substr(0, slash), buf, fam))
+    throw std::invalid_argument("Invalid IPAddress: " + text);
+  const int bits = fam == AF_INET6 ? 128 : 32;
+  if (len > bits) throw std::invalid_argument("Invalid IPAddress: " + text);
+  if (applyMask)
+    for (int bit = len; bit < bits; ++bit) buf[bit >> 3] &= uint8_t(~(0x80u >> (bit & 7)));
+  return formatAddress(buf, fam) + "/" + std::to_string(len);
+}
+
 // toIPNetwork(prefix, applyMask=true) (NetworkUtil.h:196-208) printed as
 // folly::IPAddress::networkToString: "<masked addr>/<len>"
 std::string ipPrefixToNetworkString(std::string_view raw, int16_t len) {
@@ -651,8 +690,10 @@ AdjacencyDatabase readAdjacencyDatabase(std::string_view bytes) {  // Types.thri
   return db;
 }
 
-PrefixDatabase readPrefixDatabase(std::string_view bytes) {  // Types.thrift:415-430
+PrefixDatabase readPrefixDatabase(std::string_view bytes,
+                                  std::vector<std::string>* networks) {  // Types.thrift:415-430
   Reader r(bytes);
+  if (networks) networks->clear();
   PrefixDatabase db;
   int16_t last = 0, id;
   uint8_t t;
@@ -669,7 +710,11 @@ PrefixDatabase readPrefixDatabase(std::string_view bytes) {  // Types.thrift:415
             continue;
           }
           db.prefixEntries.reserve(n);
-          for (uint32_t i = 0; i < n; ++i) db.prefixEntries.push_back(readPrefixEntry(r));
+          if (networks) networks->resize(db.prefixEntries.size() + n);
+          for (uint32_t i = 0; i < n; ++i) {
+            std::string* net = networks ? &(*networks)[db.prefixEntries.size()] : nullptr;
+            db.prefixEntries.push_back(readPrefixEntry(r, net));
+          }
           continue;
         }
         break;
@@ -741,7 +786,8 @@ LsdbKeyUpdate LsdbIngest::updateKeyInLsdb(const std::string& area, LinkState& ar
       return u;
     }
     if (key.compare(0, 7, "prefix:") == 0) {
-      PrefixDatabase db = readPrefixDatabase(*rawVal);
+      std::vector<std::string> networks;
+      PrefixDatabase db = readPrefixDatabase(*rawVal, &networks);
       u.nodeName = db.thisNodeName;
       if (db.prefixEntries.size() != 1) {  // Decision.cpp:750-756
         u.kind = LsdbKeyUpdate::kError;
@@ -755,10 +801,15 @@ LsdbKeyUpdate LsdbIngest::updateKeyInLsdb(const std::string& area, LinkState& ar
           areas_.count(entry.area_stack.back())) {
         return u;
       }
+      // PrefixKey(node, toIPNetwork(*entry.prefix()), area) (Decision.cpp:772-773);
+      // a default IpPrefix (no prefix field) is rejected by toIPNetwork
+      const std::string& network = networks.front();
+      if (network.empty()) fail("prefix: PrefixEntry without a prefix");
       u.kind = LsdbKeyUpdate::kPrefix;
-      u.changedPrefixes = db.deletePrefix
-                              ? prefixState.deletePrefix(db.thisNodeName, area, entry.prefix)
-                              : prefixState.updatePrefix(db.thisNodeName, area, std::move(entry));
+      u.changedPrefixes =
+          db.deletePrefix
+              ? prefixState.deletePrefix(db.thisNodeName, area, network)
+              : prefixState.updatePrefixKeyed(db.thisNodeName, area, network, std::move(entry));
       return u;
     }
   } catch (const std::exception& e) {  // Decision.cpp:781-784: log, drop the key

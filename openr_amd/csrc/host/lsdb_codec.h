@@ -13,8 +13,9 @@
 // structs of decision.h (no intermediate thrift objects): strings are copied
 // once, BinaryAddress bytes become the text form the host layer keys on
 // (inet_ntop, which is what folly::IPAddress::str() prints), and IpPrefix
-// becomes the masked "addr/len" network string of toIPNetwork
-// (NetworkUtil.h:196-208). Unknown fields and fields whose wire type does
+// becomes "addr/len" text with the host bits kept, as Decision keeps the raw
+// entry; the PrefixState key is the masked network of toIPNetwork
+// (NetworkUtil.h:196-208, Decision.cpp:772-773). Unknown fields and fields whose wire type does
 // not match the IDL are skipped, as generated thrift readers do; malformed
 // input throws LsdbDecodeError. The encoder is the inverse, used by
 // benchmarks and tests to produce publications.
@@ -51,14 +52,18 @@ struct PrefixDatabase {  // Types.thrift:415-430
 
 // compact-protocol codecs (fbthrift CompactSerializer wire format)
 AdjacencyDatabase readAdjacencyDatabase(std::string_view bytes);
-PrefixDatabase readPrefixDatabase(std::string_view bytes);
+// networks (optional): toIPNetwork of each entry's prefix, the PrefixState
+// key ("" for an entry without a prefix field)
+PrefixDatabase readPrefixDatabase(std::string_view bytes,
+                                  std::vector<std::string>* networks = nullptr);
 std::string writeAdjacencyDatabase(const AdjacencyDatabase& db);
 std::string writePrefixDatabase(const PrefixDatabase& db);
 
 // address helpers shared by the codec and its tests
 std::string binaryAddressToString(std::string_view raw);  // "" for empty
 std::string stringToBinaryAddress(const std::string& text);
-std::string ipPrefixToNetworkString(std::string_view raw, int16_t len);
+std::string ipPrefixToNetworkString(std::string_view raw, int16_t len);  // masked
+std::string ipPrefixToString(std::string_view raw, int16_t len);         // as advertised
 
 // getNodeNameFromKey (LsdbUtil.cpp:691-698): the text
 // between the first and second ':' of "adj:<node>" / "prefix:<node>:<...>".

@@ -72,39 +72,40 @@ uint64_t nextVersionStamp() {
 }
 
 // ----------------------------------------------------------- PrefixState --
-std::set<std::string> PrefixState::updatePrefix(const std::string& node,
-                                                const std::string& area,
-                                                const PrefixEntry& entry) {
+std::set<std::string> PrefixState::updatePrefixKeyed(const std::string& node,
+                                                     const std::string& area,
+                                                     const std::string& network,
+                                                     PrefixEntry entry) {
   std::set<std::string> changed;  // PrefixState.cpp:15-38
-  auto& entries = prefixes_[entry.prefix];
+  auto& entries = prefixes_[network];
   auto [it, inserted] = entries.try_emplace(NodeAndArea(node, area));
   if (!inserted && *it->second == entry) return changed;
-  it->second = std::make_shared<PrefixEntry>(entry);
-  changed.insert(entry.prefix);
+  changed.insert(network);
+  it->second = std::make_shared<PrefixEntry>(std::move(entry));
   version_ = nextVersionStamp();
   return changed;
 }
 
 std::set<std::string> PrefixState::updatePrefix(const std::string& node,
                                                 const std::string& area,
+                                                const PrefixEntry& entry) {
+  return updatePrefixKeyed(node, area, prefixNetworkKey(entry.prefix), entry);
+}
+
+std::set<std::string> PrefixState::updatePrefix(const std::string& node,
+                                                const std::string& area,
                                                 PrefixEntry&& entry) {
-  std::set<std::string> changed;  // as above, moving the decoded entry in
-  auto& entries = prefixes_[entry.prefix];
-  auto [it, inserted] = entries.try_emplace(NodeAndArea(node, area));
-  if (!inserted && *it->second == entry) return changed;
-  changed.insert(entry.prefix);
-  it->second = std::make_shared<PrefixEntry>(std::move(entry));
-  version_ = nextVersionStamp();
-  return changed;
+  std::string network = prefixNetworkKey(entry.prefix);
+  return updatePrefixKeyed(node, area, network, std::move(entry));
 }
 
 std::set<std::string> PrefixState::deletePrefix(const std::string& node,
                                                 const std::string& area,
                                                 const std::string& prefix) {
   std::set<std::string> changed;  // PrefixState.cpp:40-57
-  auto it = prefixes_.find(prefix);
+  auto it = prefixes_.find(prefixNetworkKey(prefix, /*applyMask=*/false));
   if (it != prefixes_.end() && it->second.erase(std::make_pair(node, area))) {
-    changed.insert(prefix);
+    changed.insert(it->first);
     if (it->second.empty()) prefixes_.erase(it);
     version_ = nextVersionStamp();
   }
@@ -1296,7 +1297,7 @@ std::map<std::string, std::optional<RibUnicastEntry>> SpfSolver::createRoutesFor
       bestRoutesCache_.erase(prefix);
       continue;
     }
-    for (const auto& [na, e] : pit->second) sub.updatePrefix(na.first, na.second, *e);
+    for (const auto& [na, e] : pit->second) sub.updatePrefixKeyed(na.first, na.second, pit->first, *e);
     asked.insert(prefix);
   }
   if (!asked.empty() && als.size() == 1) {

@@ -890,7 +890,7 @@ class C5Runner {
       size_t i = 0;
       for (const auto& [pfx, entries] : ps_.prefixes()) {
         if (i >= lo && i < hi) {
-          for (const auto& [na, e] : entries) sub.updatePrefix(na.first, na.second, *e);
+          for (const auto& [na, e] : entries) sub.updatePrefixKeyed(na.first, na.second, pfx, *e);
         }
         ++i;
       }
@@ -1708,6 +1708,7 @@ PYBIND11_MODULE(_decision, m) {
           py::gil_scoped_release nogil;
           std::vector<double> cold, warm;
           size_t routes = 0;
+          uint64_t dCold = 0, dWarm = 0;  // route_digest.h unit(me, db)
           for (int r = 0; r < reps + 1; ++r) {
             AreaLinkStates als;
             auto& ls = als.emplace(g.area, LinkState(g.area, "test_node")).first->second;
@@ -1722,15 +1723,17 @@ PYBIND11_MODULE(_decision, m) {
             routes = db->unicastRoutes.size();
             if (r) cold.push_back(us);  // rep 0 warms code objects / workspace
             if (r == reps) {
+              dCold = digest::unit(me, *db);
               for (int k = 0; k < reps; ++k) {
                 t0 = std::chrono::steady_clock::now();
                 db = solver.buildRouteDb(me, als, ps);
                 warm.push_back(std::chrono::duration<double, std::micro>(
                                    std::chrono::steady_clock::now() - t0).count());
               }
+              dWarm = digest::unit(me, *db);
             }
           }
-          return std::make_tuple(cold, warm, routes);
+          return std::make_tuple(cold, warm, routes, dCold, dWarm);
         },
         py::arg("kind"), py::arg("opts"), py::arg("me"), py::arg("reps"));
   m.def("route_db_batch_serve_bench",

@@ -13,6 +13,9 @@ import random
 
 # C2 (BASELINE.json configs[1]): 4096 random-metric 10x10 grids per GPU
 # (topology t: metric seed 0xC2000000 + t, prefix seed 0xC1 + t), source "1"
+# C1: createGrid(10) wiring, metric 1, one seeded prefix per node, source "1"
+C1_OPTS = dict(n=10, prefixSeed=0xC1)
+C1_SOURCE = "1"
 C2_OPTS = dict(n=10, metricSeed=0xC2000000, prefixSeed=0xC1)
 C2_SOURCE = "1"
 C2_TOPOS = 4096

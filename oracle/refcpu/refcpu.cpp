@@ -1,6 +1,8 @@
 // refcpu — CPU ORACLE (test infrastructure only; see refcpu.h header).
 #include "refcpu.h"
 
+#include <arpa/inet.h>
+
 #include <algorithm>
 #include <stdexcept>
 
@@ -453,26 +455,52 @@ bool LinkState::pathAInPathB(const Path& a, const Path& b) {
 }
 
 // ===================== PrefixState (PrefixState.cpp:15-57) =================
+// toIPNetwork(prefix, applyMask) (NetworkUtil.h:196-208) printed as
+// folly::IPAddress::networkToString ("<addr>/<len>", addr = inet_ntop text).
+std::string networkOf(const std::string& text, bool applyMask) {
+  const auto slash = text.rfind('/');
+  if (slash == std::string::npos || slash + 1 == text.size())
+    throw std::invalid_argument("Invalid IPAddress: " + text);
+  const std::string addr = text.substr(0, slash), len = text.substr(slash + 1);
+  if (len.size() > 3 || len.find_first_not_of("0123456789") != std::string::npos)
+    throw std::invalid_argument("Invalid IPAddress: " + text);
+  const int fam = addr.find(':') != std::string::npos ? AF_INET6 : AF_INET;
+  unsigned char b[16];
+  if (inet_pton(fam, addr.c_str(), b) != 1) throw std::invalid_argument("Invalid IPAddress: " + text);
+  const int bits = fam == AF_INET6 ? 128 : 32, n = std::stoi(len);
+  if (n > bits) throw std::invalid_argument("Invalid IPAddress: " + text);
+  if (applyMask)
+    for (int i = n; i < bits; ++i) b[i / 8] &= static_cast<unsigned char>(~(0x80u >> (i % 8)));
+  char out[INET6_ADDRSTRLEN];
+  inet_ntop(fam, b, out, sizeof out);
+  return std::string(out) + "/" + std::to_string(n);
+}
+
+// The key is PrefixKey(node, toIPNetwork(*entry.prefix()), area), as every
+// caller builds it (Decision.cpp:772-773); the entry is kept as advertised.
 std::set<std::string> PrefixState::updatePrefix(const std::string& node,
                                                 const std::string& area,
                                                 const PrefixEntry& entry) {
   std::set<std::string> changed;
-  auto& entries = prefixes_[entry.prefix];
+  const std::string network = networkOf(entry.prefix, true);
+  auto& entries = prefixes_[network];
   auto key = std::make_pair(node, area);
   auto it = entries.find(key);
   if (it != entries.end() && *it->second == entry) return changed;
   entries[key] = std::make_shared<PrefixEntry>(entry);
-  changed.insert(entry.prefix);
+  changed.insert(network);
   return changed;
 }
 
+// `prefix` is the key's CIDRNetwork as given (not masked), compared by value
 std::set<std::string> PrefixState::deletePrefix(const std::string& node,
                                                 const std::string& area,
                                                 const std::string& prefix) {
   std::set<std::string> changed;
-  auto it = prefixes_.find(prefix);
+  const std::string network = networkOf(prefix, false);
+  auto it = prefixes_.find(network);
   if (it != prefixes_.end() && it->second.erase(std::make_pair(node, area))) {
-    changed.insert(prefix);
+    changed.insert(network);
     if (it->second.empty()) prefixes_.erase(it);
   }
   return changed;

@@ -312,6 +312,8 @@ class LinkState {
 };
 
 // ---- PrefixState (PrefixState.h:18-57, PrefixState.cpp:15-57)
+std::string networkOf(const std::string& text, bool applyMask);
+
 class PrefixState {
  public:
   const std::unordered_map<std::string, PrefixEntries>& prefixes() const {

@@ -121,6 +121,22 @@ def text_to_addr(text):
     return socket.inet_pton(fam, text)
 
 
+def prefix_string(raw, plen):
+    """IpPrefix as advertised (host bits kept): what Decision keeps in the
+    stored entry (Decision.cpp:758-778). Rejects what toIPNetwork rejects."""
+    if len(raw) not in (4, 16):
+        raise DecodeError("prefix address must be 4 or 16 bytes")
+    if plen < 0 or plen > 8 * len(raw):
+        raise DecodeError("prefix length out of range")
+    return "%s/%d" % (addr_to_text(raw), plen)
+
+
+def network_of_text(text):
+    """toIPNetwork(entry.prefix) of an "addr/len" text: the PrefixState key."""
+    addr, _, plen = text.rpartition("/")
+    return network_string(text_to_addr(addr), int(plen))
+
+
 def network_string(raw, plen):
     """toIPNetwork(IpPrefix, applyMask=true) printed as addr/len."""
     if len(raw) not in (4, 16):
@@ -269,7 +285,7 @@ def _read_struct(r, schema):
                     plen = r.zz(16)
                 else:
                     r.skip(t2, 2)
-            out[name] = network_string(addr, plen)
+            out[name] = prefix_string(addr, plen)
         elif kind == "struct":
             out[name] = _read_struct(r, arg)
         elif kind in ("structlist", "strlist", "strset"):
@@ -443,8 +459,10 @@ def update_key_in_lsdb(my_node, areas, area, link_state, prefix_state, key, valu
             if db["thisNodeName"] == my_node and e["area_stack"] and e["area_stack"][-1] in areas:
                 return 0, "", None
             node = db["thisNodeName"]
-            if db["deletePrefix"]:
-                return 2, node, set(prefix_state.deletePrefix(node, area, e["prefix"]))
+            if not e["prefix"]:  # default IpPrefix: toIPNetwork throws
+                return 3, "", None
+            if db["deletePrefix"]:  # PrefixKey(node, toIPNetwork(prefix), area)
+                return 2, node, set(prefix_state.deletePrefix(node, area, network_of_text(e["prefix"])))
             return 2, node, set(prefix_state.updatePrefix(node, area, e))
     except DecodeError:
         return 3, "", None

@@ -9,7 +9,7 @@ XOR over routes of a hash of the RibUnicastEntry fields) and
 openr_amd/shard.py (C4 change lists, C5 KSP2 path lines). Every value here
 comes from oracle/refcpu (test infrastructure), never from the engine.
 
-  python tests/golden/make_bench_digests.py [c2] [c3] [c4] [c5] [g1] [--threads T]
+  python tests/golden/make_bench_digests.py [c1] [c2] [c3] [c4] [c5] [g1] [--threads T]
 
 C3 takes long (2,080 oracle buildRouteDb over 208k prefixes each, ~1.5 h on
 8 cores): it is resumable, per-source digests accumulate in
@@ -28,7 +28,7 @@ sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
 import _refcpu as R  # noqa: E402
 from openr_amd import shard  # noqa: E402  (pure Python: digest helpers)
-from openr_amd.workloads import (C2_OPTS, C2_SOURCE, C2_TOPOS, C3_OPTS, C4_OPTS,  # noqa: E402
+from openr_amd.workloads import (C1_OPTS, C1_SOURCE, C2_OPTS, C2_SOURCE, C2_TOPOS, C3_OPTS, C4_OPTS,  # noqa: E402
                                  C4_SOURCE, C4_VARIANTS, C4_SEED, C4_DUAL_PERMILLE,
                                  C5_OPTS, C5_SOURCE, G1_OPTS, G1_SOURCES, c3_source_names,
                                  c5_policy)
@@ -50,6 +50,12 @@ def save(path, d):
         json.dump(d, f, indent=1, sort_keys=True)
         f.write("\n")
     os.replace(tmp, path)
+
+
+def gen_c1(out, threads):
+    """C1: the oracle's buildRouteDb("1") on the metric-1 10x10 grid (v4 on,
+    SR off, best-route selection off), keyed by the source name."""
+    out["c1"] = f"{R.gen_route_digests('grid', C1_OPTS, [C1_SOURCE], True, False, False, 1)[0]:016x}"
 
 
 def gen_c2(out, threads, blocks=8):
@@ -111,7 +117,9 @@ def main():
     out = load(OUT)
     for c in a.configs:
         t = time.time()
-        if c == "c2":
+        if c == "c1":
+            gen_c1(out, a.threads)
+        elif c == "c2":
             gen_c2(out, a.threads)
         elif c == "c3":
             gen_c3(out, a.threads, a.chunk)

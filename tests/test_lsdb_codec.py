@@ -187,19 +187,62 @@ def test_codec_rejects_truncation_and_garbage(host_module):
                 dec(blob)
 
 
-def test_prefix_masking(host_module):
-    """toIPNetwork(applyMask=true): host bits are cleared, the text is the
-    inet_ntop form (::ffff:a.b.c.d stays dotted, zero runs compress)."""
+def test_prefix_raw_entry_masked_key(host_module, oracle):
+    """The decoded entry keeps the IpPrefix as advertised (Decision stores the
+    raw thrift entry, Decision.cpp:758-778); the PrefixState key is
+    toIPNetwork(applyMask=true): host bits cleared, inet_ntop text."""
     M = host_module
-    cases = [("10.1.2.3/8", "10.0.0.0/8"), ("::ffff:10.1.1.1/128", "::ffff:10.1.1.1/128"),
-             ("fc00:0:0:0:0:0:0:1/64", "fc00::/64"), ("ff:ff::1/0", "::/0"),
-             ("1.2.3.4/32", "1.2.3.4/32")]
-    for text, want in cases:
+    cases = [("10.1.2.3/8", "10.1.2.3/8", "10.0.0.0/8"),
+             ("::ffff:10.1.1.1/128", "::ffff:10.1.1.1/128", "::ffff:10.1.1.1/128"),
+             ("fc00:0:0:0:0:0:0:1/64", "fc00::1/64", "fc00::/64"),
+             ("ff:ff::1/0", "ff:ff::1/0", "::/0"), ("1.2.3.4/32", "1.2.3.4/32", "1.2.3.4/32")]
+    for text, raw, key in cases:
         e = createPrefixEntry(text)
         pdb = dict(thisNodeName="n", prefixEntries=[e], deletePrefix=False)
         got_p = M.decodePrefixDb(M.encodePrefixDb(pdb))["prefixEntries"][0]["prefix"]
         got_o = tc.decode_prefix_db(tc.encode_prefix_db(pdb))["prefixEntries"][0]["prefix"]
-        assert got_p == got_o == want
+        assert got_p == got_o == raw
+        assert tc.network_of_text(raw) == key
+        (_, p_ps), (_, o_ps) = _ingest_both(M, oracle, "A", ["prefix:n:[%s]" % key],
+                                            [M.encodePrefixDb(pdb)])
+        assert list(p_ps.prefixes()) == list(o_ps.prefixes()) == [key]
+        assert p_ps.prefixes() == o_ps.prefixes()
+
+
+def test_host_bits_change_is_a_change(host_module, oracle):
+    """Two advertisements of one network that differ only in host bits: the
+    reference's entry equality (PrefixState.cpp:23-26) sees a change, and the
+    stored (best) entry carries the newer raw prefix."""
+    M = host_module
+    adj_a = createAdjDb("a", [createAdjacency("b", "a/b", "b/a", "fe80::b", "10.0.0.2", 5, 7)], 1, area="A")
+    adj_b = createAdjDb("b", [createAdjacency("a", "b/a", "a/b", "fe80::a", "10.0.0.1", 9, 8)], 2, area="A")
+    keys = ["adj:a", "adj:b"]
+    vals = [tc.encode_adj_db(adj_a), tc.encode_adj_db(adj_b)]
+    for raw in ("10.1.2.3/8", "10.1.2.4/8", "10.1.2.4/8", "10.0.0.0/8"):
+        keys.append("prefix:b:[10.0.0.0/8]")
+        vals.append(tc.encode_prefix_db(dict(thisNodeName="b", prefixEntries=[createPrefixEntry(raw)],
+                                             deletePrefix=False)))
+    area, me = "A", "a"
+    p_ls, p_ps = M.LinkState(area, me), M.PrefixState()
+    o_ls, o_ps = oracle.LinkState(area, me), oracle.PrefixState()
+    ing = M.LsdbIngest(me, {area})
+    changes = []
+    for k, v in zip(keys, vals):
+        up = ing.updateKeyInLsdb(area, p_ls, p_ps, k, v)
+        kind, node, payload = tc.update_key_in_lsdb(me, {area}, area, o_ls, o_ps, k, v)
+        assert up["kind"] == kind
+        if kind == 2:
+            assert set(up["changedPrefixes"]) == payload
+            changes.append(payload)
+    assert changes == [{"10.0.0.0/8"}, {"10.0.0.0/8"}, set(), {"10.0.0.0/8"}]
+    assert p_ps.prefixes() == o_ps.prefixes()
+    # delete by the masked network of the raw advertisement
+    dv = tc.encode_prefix_db(dict(thisNodeName="b", prefixEntries=[createPrefixEntry("10.7.7.7/8")],
+                                  deletePrefix=True))
+    up = ing.updateKeyInLsdb(area, p_ls, p_ps, "prefix:b:[10.0.0.0/8]", dv)
+    kind, node, payload = tc.update_key_in_lsdb(me, {area}, area, o_ls, o_ps, "prefix:b:[10.0.0.0/8]", dv)
+    assert set(up["changedPrefixes"]) == payload == {"10.0.0.0/8"}
+    assert p_ps.prefixes() == o_ps.prefixes() == {}
 
 
 def test_address_text_matches_inet_ntop(host_module):
@@ -429,6 +472,56 @@ def test_process_publication_sequence(host_module, oracle):
     # spot checks of the reference rules the sequence exercises
     assert fulls[4:6] == [False, True]
     assert "fc00::33/128" not in p_ps.prefixes()  # self reflection skipped
+
+
+@pytest.mark.gpu
+def test_gpu_routes_keep_raw_advertised_prefix(product, oracle):
+    """Advertisements with host bits set (Decision.cpp:758-778): the route is
+    keyed by the masked network, its bestPrefixEntry carries the raw prefix,
+    and a host-bit-only re-advertisement is a change the incremental path
+    answers -- GPU buildRouteDb / createRoutesForPrefixes vs the oracle."""
+    M = product
+    area, keys, vals = M.gen_publication(
+        "grid", {"n": 5, "prefixesPerNode": 1, "metricSeed": 3, "v4Permille": 500})
+    raws = {"0": "10.1.2.3/8", "7": "fc00:1::5/32", "12": "10.200.0.1/16", "24": "fc00:2::1:2/120"}
+    extra = []
+    for node, raw in sorted(raws.items()):
+        extra.append(("prefix:%s:[%s]" % (node, tc.network_of_text(raw)),
+                      tc.encode_prefix_db(dict(thisNodeName=node, prefixEntries=[createPrefixEntry(raw)],
+                                               deletePrefix=False))))
+    # anycast: node 18 advertises node 0's network with other host bits
+    extra.append(("prefix:18:[10.0.0.0/8]", tc.encode_prefix_db(
+        dict(thisNodeName="18", prefixEntries=[createPrefixEntry("10.9.9.9/8")], deletePrefix=False))))
+    kv = list(zip(keys, vals)) + extra
+    me = "6"
+    p_als, p_ps = M.AreaLinkStates(), M.PrefixState()
+    ing = M.LsdbIngest(me, set())
+    ing.processPublicationKeyVals(area, p_als, p_ps, kv, [], M.DecisionPendingUpdates(me))
+    o_als, o_ps = oracle.AreaLinkStates(), oracle.PrefixState()
+    o_ls = o_als.add(area, me)
+    for k, v in kv:
+        tc.update_key_in_lsdb(me, {area}, area, o_ls, o_ps, k, v)
+    p_s = M.SpfSolver(me, True, False, False, False)
+    o_s = oracle.SpfSolver(me, True, False, False, False)
+    for src in ("6", "0", "13"):
+        p_db = p_s.buildRouteDb(src, p_als, p_ps).unicastRoutes()
+        o_db = o_s.buildRouteDb(src, o_als, o_ps).unicastRoutes()
+        assert p_db == o_db, src
+        best = {k: v["bestPrefixEntry"]["prefix"] for k, v in p_db.items()}
+        assert best.get("10.200.0.0/16") == "10.200.0.1/16"
+        assert best.get("fc00:1::/32") == "fc00:1::5/32"
+    # host-bit-only change of node 12's advertisement: a change, answered by
+    # the incremental path with the new raw prefix
+    upd = ("prefix:12:[10.200.0.0/16]", tc.encode_prefix_db(
+        dict(thisNodeName="12", prefixEntries=[createPrefixEntry("10.200.0.2/16")], deletePrefix=False)))
+    pend_p = M.DecisionPendingUpdates(me)
+    ing.processPublicationKeyVals(area, p_als, p_ps, [upd], [], pend_p)
+    kind, _, payload = tc.update_key_in_lsdb(me, {area}, area, o_ls, o_ps, *upd)
+    assert set(pend_p.updatedPrefixes()) == payload == {"10.200.0.0/16"}
+    got = p_s.createRoutesForPrefixes(me, p_als, p_ps, {"10.200.0.0/16"})
+    want = o_s.createRouteForPrefixOrGetStaticRoute(me, o_als, o_ps, "10.200.0.0/16")
+    assert got["10.200.0.0/16"] == want
+    assert want["bestPrefixEntry"]["prefix"] == "10.200.0.2/16"
 
 
 @pytest.mark.gpu

@@ -121,3 +121,51 @@ def test_unit_digest_independent_of_sharding(world):
     flipped = meta.copy()
     flipped[5, 3] ^= 1
     assert shard.unit_digest(keys, flipped, mask) != whole
+
+
+# ------------------------------------------------ bench.py --gpus N launcher --
+BENCH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bench.py")
+
+
+def _bench(args, env_extra=None, timeout=280):
+    import json
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env.update(env_extra or {})
+    r = subprocess.run([sys.executable, BENCH] + args, env=env, capture_output=True,
+                       text=True, timeout=timeout)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    return r.returncode, (json.loads(lines[-1]) if lines else None), r.stderr
+
+
+@pytest.mark.timeout(300)
+def test_bench_gpus_flag_launches_ranks():
+    """`bench.py --gpus 2` with no launcher around it starts two ranks itself
+    (children, gloo here), and a WORLD_SIZE that disagrees with --gpus is an
+    error, never a silent N=1 run."""
+    rc, line, err = _bench(["--gpus", "2", "--launch-check"])
+    assert rc == 0, err[-2000:]
+    assert line == {"world": 2, "ranks": [[0, 0], [1, 1]]}
+    rc, line, _ = _bench(["--gpus", "2", "--launch-check"], {"WORLD_SIZE": "1"})
+    assert rc == 2 and line is None
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_bench_two_ranks_share_device_golden():
+    """The N=2 path end to end on one GPU (OGS_BENCH_SHARE_DEVICE=1: both
+    ranks on device 0, gloo for the records): `--gpus 2` launches the ranks,
+    and the C2 (weak: blocks 0+1) and C3 (strong: interleaved sources) job
+    digests equal the oracle's golden values at N=2."""
+    share = {"OGS_BENCH_SHARE_DEVICE": "1"}
+    rc, line, err = _bench(["--gpus", "2", "--config", "c2", "--steps", "3", "--warmup", "1",
+                            "--no-cpu-baseline"], share)
+    assert rc == 0, err[-3000:]
+    assert line["n_gpus"] == 2 and line["golden"]["c2"] == "match"
+    assert line["config"]["topologies_per_gpu"] == 4096
+    rc, line, err = _bench(["--gpus", "2", "--config", "c3", "--steps", "2", "--warmup", "1",
+                            "--no-cpu-baseline", "--no-extras"], share)
+    assert rc == 0, err[-3000:]
+    assert line["n_gpus"] == 2 and line["golden"]["c3"] == "match"

@@ -9,4 +9,4 @@ tag=$1; shift
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 120 rocprofv3 --pmc $c --output-format csv -d gpurun_out/pmc_${tag}_$c -o pmc -- python3 bench.py "$@" > gpurun_out/pmc_${tag}_$c.log 2>&1 || { echo "pmc pass $c failed"; tail -5 gpurun_out/pmc_${tag}_$c.log; exit 1; }
 done
-python3 tools/pmc_summary.py $tag
+python3 tools/pmc_summary.py $tag "$@"

@@ -11,11 +11,14 @@ step() {  # step <name> <timeout> <cmd...>
   echo "=== $name rc=$rc"; tail -4 "gpurun_out/$name.log" | cut -c1-400
   [ $rc -eq 0 ] || exit $rc
 }
-nproc > gpurun_out/host.txt; lscpu | grep "Model name" >> gpurun_out/host.txt
-step pytest_gpu 600 python -u -m pytest tests -m gpu -q -p no:cacheprovider -x --timeout 120 --timeout-method thread
-step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
-step bench 600 python bench.py
+nproc > gpurun_out/host.txt; python3 -c "import os;print(len(os.sched_getaffinity(0)))" >> gpurun_out/host.txt; lscpu | grep "Model name" >> gpurun_out/host.txt
+if [ -z "$NO_TESTS" ]; then
+  step pytest_gpu 900 python -u -m pytest tests -m gpu -q -p no:cacheprovider -x --timeout 120 --timeout-method thread
+  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+fi
+step bench 900 python bench.py
 if [ -n "$PROFILE" ]; then
-  step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o bench -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline
+  cd /tmp && cd "$GRAFT_REPO_ROOT"
+  step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o bench -- python3 bench.py --no-cpu-baseline --no-extras
   grep -v "at::native" gpurun_out/prof/bench_kernel_stats.csv | cut -c1-200
 fi

@@ -10,6 +10,7 @@ dispatches."""
 import csv
 import glob
 import json
+import os
 import sys
 from collections import defaultdict
 
@@ -43,8 +44,14 @@ def main():
                   "write_bytes_per_launch": wa * 1024 if wa is not None else None}
         if fa is not None and wa is not None:
             out[k]["hbm_bytes_per_launch"] = 2 * fa * 1024 + wa * 1024
+    # the commit measured (passed in from the repo side: the box has no .git)
+    # and the bench command the passes ran
+    out["_meta"] = {"commit": os.environ.get("OGS_COMMIT"),
+                    "bench_args": " ".join(sys.argv[2:])}
     json.dump(out, open(f"gpurun_out/pmc_{tag}.json", "w"), indent=1)
     for k, v in out.items():
+        if k.startswith("_"):
+            continue
         print(k[:90], json.dumps({a: b for a, b in v.items() if a != "dispatches"}))
 
 
