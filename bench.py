@@ -70,13 +70,35 @@ def log(msg):
     print(f"bench.py [{time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
-def host_cores():
-    """The cores this process may run on (the lease's CPU share; os.cpu_count()
-    is the whole machine's)."""
+def cgroup_cpus():
+    """CPU quota of this process's cgroup (cgroup v2 cpu.max "quota period"),
+    rounded up, or None when unlimited / unreadable."""
     try:
-        return len(os.sched_getaffinity(0))
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota == "max":
+            return None
+        return max(1, -(-int(quota) // int(period)))
+    except (OSError, ValueError):
+        return None
+
+
+def host_cores():
+    """The cores this process can actually use: its CPU affinity, capped by
+    the cgroup CPU quota and the lease's OMP_NUM_THREADS share (the GPU box
+    grants 16 cores while affinity and os.cpu_count() show the machine's
+    256; 256 threads on a 16-core share only thrash)."""
+    try:
+        n = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
-        return os.cpu_count() or 1
+        n = os.cpu_count() or 1
+    q = cgroup_cpus()
+    if q:
+        n = min(n, q)
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, n)
 
 
 def cpu_threads():
@@ -93,7 +115,13 @@ def host_info():
                     break
     except OSError:
         pass
-    return {"cores": host_cores(), "machine_cpus": os.cpu_count(), "model": model}
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = None
+    return {"cores": host_cores(), "affinity": aff, "cgroup_cpus": cgroup_cpus(),
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
+            "machine_cpus": os.cpu_count(), "model": model}
 
 
 def median(xs):

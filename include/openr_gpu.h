@@ -45,6 +45,12 @@
 extern "C" {
 #endif
 
+/* ABI version of this header: a consumer checks ogs_abi_version() ==
+ * OGS_ABI_VERSION once at start-up. 3: ogs_spf_out.reached,
+ * ogs_area_table.reached, ogs_routes_from_spf(spf_reached), u16 RibPolicy
+ * statement ids, ogs_graph.rslot_ext (rows of 511+ edges). */
+#define OGS_ABI_VERSION 3
+
 /* ---- status codes ------------------------------------------------------ */
 #define OGS_OK 0
 #define OGS_E_INVALID (-1)     /* bad argument / inconsistent shapes         */
@@ -184,7 +190,12 @@ typedef struct ogs_unit {
  *   metric [U*S_p + p]            shortest metric (dist width)
  *   mask   [(U*W + w)*S_p + p]    next-hop link-slot bitset of the route
  *   sel    [U*S_p + p]            selected-advertiser bitset (segments of
- *                                 <= 32 entries; bestRoutesCache)        */
+ *                                 <= 32 entries; bestRoutesCache)
+ *   reached [U*ceil(S_n/32) + v/32] bit v%32: node v settled. Written under
+ *                                 OGS_F_EXACT_ORDER only, where a wrapped
+ *                                 u64 distance of a reached node may be all
+ *                                 ones (LinkState.cpp:77-78, 789); the other
+ *                                 paths' distances never reach the sentinel */
 typedef struct ogs_spf_out {
   void* dist;
   uint32_t* nh;
@@ -192,6 +203,7 @@ typedef struct ogs_spf_out {
   void* metric;
   uint32_t* mask;
   uint32_t* sel;
+  uint32_t* reached;
 } ogs_spf_out;
 
 /* KSP2 unit: edge-disjoint paths src -> dest avoiding an optional
@@ -231,10 +243,15 @@ typedef struct ogs_area_table {
                                  OGS_NODE_NONE if a has no such node     */
   const uint32_t* adv_area;   /* [A_total] area index of each entry       */
   const uint32_t* adv_name;   /* [A_total] name id of each entry's node   */
+  /* Optional settled bitsets of the SPF rows ([row*ceil(S_n/32)], the
+   * `reached` output of an OGS_F_EXACT_ORDER launch); NULL: all-ones
+   * distance = unreachable. */
+  const uint32_t* reached;
 } ogs_area_table;
 
 /* ---- runtime ------------------------------------------------------------ */
 const char* ogs_version(void);
+int ogs_abi_version(void); /* OGS_ABI_VERSION of the library */
 const char* ogs_last_error(void); /* thread-local message of last failure */
 int ogs_device_count(int* count);
 int ogs_set_device(int device);
@@ -322,6 +339,7 @@ int ogs_spf_routes(const ogs_graph* graph, const ogs_prefix_table* prefixes,
 int ogs_routes_from_spf(const ogs_graph* graph, const ogs_prefix_table* prefixes,
                         const ogs_unit* units /* device */, int32_t n_units,
                         const void* spf_dist, const uint32_t* spf_nh,
+                        const uint32_t* spf_reached /* optional, as out->reached */,
                         uint32_t flags, int32_t nh_words, ogs_spf_out* out,
                         void* stream);
 
@@ -446,6 +464,8 @@ int ogs_csr_patch(uint64_t* edges, const uint32_t* idx, const uint64_t* val,
  * leaves the routes an earlier chunk transformed (applied != 0xFF) as they
  * are and continues the others' counter. Statement indexes are u8 (0xFF =
  * none): statement_base + K <= 255. */
+#define OGS_POLICY_NONE 0xFFFFu /* applied / counter: no statement */
+
 typedef struct ogs_rib_policy {
   int32_t num_statements;        /* K <= 32 (this chunk)                     */
   uint32_t active;               /* bit k: statement k has a prefix or tag
@@ -466,14 +486,16 @@ typedef struct ogs_rib_policy {
  * mask[((U*A + a)*W + w)*S_p + p] rewritten: next hops of weight 0 dropped
  * unless that drops all of them, RibPolicy.cpp:138-158). applied[U*S_p+p] =
  * statement whose weights the route took, counter[...] = statement whose
- * counterID the route carries (the last matching one tried), 0xFF = none.
+ * counterID the route carries (the last matching one tried), OGS_POLICY_NONE
+ * = none. Statement ids are u16: a policy of up to 65,535 statements runs in
+ * chunks of 32 (statement_base).
  * The prefix table is one topology's (pfx_base[0..1]); single-area callers
  * pass num_areas = 1. */
 int ogs_rib_policy_apply(const ogs_prefix_table* prefixes,
                          const ogs_rib_policy* policy, int32_t num_areas,
                          int32_t n_units, int32_t nh_words,
                          const uint32_t* meta, uint32_t* mask,
-                         uint8_t* applied, uint8_t* counter, void* stream);
+                         uint16_t* applied, uint16_t* counter, void* stream);
 
 /* Multi-area RouteDb for n_units sources from their per-area SPF results
  * (a prior ogs_spf_routes launch over the area batch without a prefix

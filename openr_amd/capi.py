@@ -6,6 +6,7 @@ import ctypes
 from . import LIB_PATH
 
 OGS_OK = 0
+OGS_ABI_VERSION = 3  # include/openr_gpu.h
 OGS_F_ENABLE_V4 = 0x01
 OGS_F_V4_OVER_V6 = 0x02
 OGS_F_BEST_ROUTE_SELECTION = 0x04
@@ -20,6 +21,7 @@ EXPORTS = [
     "ogs_ksp_paths", "ogs_ksp2_paths", "ogs_set_option", "ogs_routes_multiarea",
     "ogs_spf_routes_variants", "ogs_rib_policy_apply", "ogs_route_changes_gather",
     "ogs_csr_patch", "ogs_host_alloc", "ogs_host_free", "ogs_routes_from_spf",
+    "ogs_abi_version",
 ]
 
 
@@ -45,12 +47,16 @@ class PrefixTable(ctypes.Structure):
 class SpfOut(ctypes.Structure):
     _fields_ = [("dist", ctypes.c_void_p), ("nh", ctypes.c_void_p),
                 ("meta", ctypes.c_void_p), ("metric", ctypes.c_void_p),
-                ("mask", ctypes.c_void_p), ("sel", ctypes.c_void_p)]
+                ("mask", ctypes.c_void_p), ("sel", ctypes.c_void_p),
+                ("reached", ctypes.c_void_p)]
 
 
 def load(path=None):
     lib = ctypes.CDLL(path or LIB_PATH)
     lib.ogs_version.restype = ctypes.c_char_p
+    if lib.ogs_abi_version() != OGS_ABI_VERSION:
+        raise RuntimeError(f"libopenr_gpu ABI {lib.ogs_abi_version()}, "
+                           f"this binding expects {OGS_ABI_VERSION}")
     lib.ogs_last_error.restype = ctypes.c_char_p
     lib.ogs_spf_routes.argtypes = [
         ctypes.POINTER(Graph), ctypes.POINTER(PrefixTable), ctypes.c_void_p,

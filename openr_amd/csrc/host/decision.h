@@ -555,8 +555,9 @@ class SpfSolver {
     std::vector<uint32_t> row;  // [A] SPF row of each area or OGS_NODE_NONE
     std::vector<uint64_t> dist, metric;  // widened, all-ones = unreachable
     std::vector<uint32_t> nh, meta, mask, sel;
+    std::vector<uint32_t> reach;  // exact-order settled bitsets per SPF row
     bool wide{false};  // device buffers hold 64-bit distances
-    std::vector<uint8_t> applied, counter;  // RibPolicy (empty: none)
+    std::vector<uint16_t> applied, counter;  // RibPolicy (empty: none)
     int W{1};
     size_t Sn{0}, P{0};
   };
@@ -684,11 +685,14 @@ struct UnitView {
   const uint32_t* mask{nullptr};
   size_t maskStride{0};  // mask[w * maskStride + p]
   const uint32_t* sel{nullptr};
+  // settled bitset of an exact-order SPF (nullptr: all-ones dist =
+  // unreachable); a wrapped u64 distance of a reached node may be all ones
+  const uint32_t* reach{nullptr};
   // device-applied RibPolicy (SpfSolver::setRibPolicy): statement whose
-  // weights / counterID each route took, 0xFF = none
+  // weights / counterID each route took, OGS_POLICY_NONE = none
   const RibPolicy* policy{nullptr};
-  const uint8_t* applied{nullptr};
-  const uint8_t* counter{nullptr};
+  const uint16_t* applied{nullptr};
+  const uint16_t* counter{nullptr};
 };
 
 struct PrefixHostTable {
@@ -710,20 +714,24 @@ using LabelRoutes = std::map<int32_t, std::pair<std::string, RibMplsEntry>>;
 void addNodeLabelRoutes(const LinkState& ls, const FlatTopology& f,
                         const std::string& area, const std::string& me,
                         const uint64_t* dist, const uint32_t* nhWords,
-                        size_t nhStride, int W, LabelRoutes& labelToNode);
+                        size_t nhStride, int W, LabelRoutes& labelToNode,
+                        const uint32_t* reach = nullptr);
+
+// bit v of a settled bitset (exact-order SPF rows)
+inline bool bitAt(const uint32_t* bits, uint32_t v) { return (bits[v >> 5] >> (v & 31u)) & 1u; }
 
 std::optional<RibUnicastEntry> materializeRoute(
     const FlatTopology& f, const std::string& me, const PrefixHostTable& pt,
     uint32_t p, uint32_t meta, uint64_t metric, const uint32_t* mask,
     size_t maskStride, int W, bool v4OverV6Nexthop, const RibPolicy* policy,
-    uint8_t applied, uint8_t counter);
+    uint16_t applied, uint16_t counter);
 // the same with the source's CSR row start `rb` (= f.rowPtr[f.id.at(me)])
 // looked up once by the caller: loops over many routes of one source
 std::optional<RibUnicastEntry> materializeRouteAt(
     const FlatTopology& f, uint32_t rb, const std::string& me, const PrefixHostTable& pt,
     uint32_t p, uint32_t meta, uint64_t metric, const uint32_t* mask,
     size_t maskStride, int W, bool v4OverV6Nexthop, const RibPolicy* policy,
-    uint8_t applied, uint8_t counter);
+    uint16_t applied, uint16_t counter);
 
 DecisionRouteDb materializeRouteDb(
     const LinkState& ls, const FlatTopology& f, const std::string& area,
@@ -856,7 +864,7 @@ class RouteDbBatch {
   struct Group {
     int W{1};
     std::vector<uint32_t> members;  // source index per unit of this group
-    DeviceBuffer units, dist, nh, meta, metric, mask, sel;
+    DeviceBuffer units, dist, nh, meta, metric, mask, sel, reach;
   };
   ogs_graph graph() const;
   ogs_prefix_table table() const;

@@ -474,7 +474,7 @@ void LinkState::uploadSlotImages(FlatTopology& m) const {
 namespace {
 // Shared scratch for single-source launches made through the API surface.
 struct SpfScratch {
-  DeviceBuffer unit, dist, nh;
+  DeviceBuffer unit, dist, nh, reach;
 };
 SpfScratch& scratch() {
   static SpfScratch s;
@@ -517,6 +517,7 @@ const LinkState::SpfResult& LinkState::getSpfResult(const std::string& node,
   sc.unit.upload(&u, 1);
   sc.dist.resize(N * db);
   sc.nh.resize(size_t(N) * W * 4);
+  sc.reach.resize(((size_t(N) + 31) / 32) * 4 + 4);
 
   ogs_graph g{};
   g.num_topos = 1;
@@ -535,6 +536,7 @@ const LinkState::SpfResult& LinkState::getSpfResult(const std::string& node,
   ogs_spf_out out{};
   out.dist = sc.dist.get();
   out.nh = sc.nh.as<uint32_t>();
+  out.reached = exact ? sc.reach.as<uint32_t>() : nullptr;
   uint32_t flags = (useLinkMetric ? 0u : OGS_F_HOP_METRIC) |
       (wide ? OGS_F_WIDE_METRIC : 0u) | (exact ? OGS_F_EXACT_ORDER : 0u);
   ogsCheck(ogs_spf_routes(&g, nullptr, sc.unit.as<ogs_unit>(), 1, flags, W,
@@ -552,11 +554,15 @@ const LinkState::SpfResult& LinkState::getSpfResult(const std::string& node,
     }
   }
   sc.nh.download(nh.data(), nh.size());
+  // exact order: the settled bitset decides reachability (a wrapped u64
+  // distance of a settled node may be all ones, kept by the reference)
+  std::vector<uint32_t> reach(exact ? (size_t(N) + 31) / 32 : 0);
+  if (exact) sc.reach.download(reach.data(), reach.size());
   ogsCheck(ogs_stream_sync(nullptr), "ogs_stream_sync");
 
   const uint32_t rb = f.rowPtr[s];
   for (uint32_t v = 0; v < N; ++v) {
-    if (dist[v] == ~0ull) continue;
+    if (exact ? !bitAt(reach.data(), v) : dist[v] == ~0ull) continue;
     NodeSpfResult r(dist[v]);
     for (int w = 0; w < W; ++w) {
       uint32_t bits = nh[size_t(w) * N + v];

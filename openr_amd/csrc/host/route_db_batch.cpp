@@ -101,6 +101,7 @@ RouteDbBatch::RouteDbBatch(const SpfSolver& solver, const AreaLinkStates& als,
     g.metric.resize(U * Sp * db);
     g.mask.resize(U * g.W * Sp * 4);
     g.sel.resize(U * Sp * 4);
+    g.reach.resize(std::max<size_t>(U * ((Sn + 31) / 32) * 4, 4));
   }
 }
 
@@ -150,7 +151,8 @@ void RouteDbBatch::launch(void* stream) {
       (wide_ ? OGS_F_WIDE_METRIC : 0u) | (exact_ ? OGS_F_EXACT_ORDER : 0u);
   for (Group& G : groups_) {
     ogs_spf_out out{G.dist.get(), G.nh.as<uint32_t>(), G.meta.as<uint32_t>(),
-                    G.metric.get(), G.mask.as<uint32_t>(), G.sel.as<uint32_t>()};
+                    G.metric.get(), G.mask.as<uint32_t>(), G.sel.as<uint32_t>(),
+                    exact_ ? G.reach.as<uint32_t>() : nullptr};
     ogsCheck(ogs_spf_routes(&g, hb_.maxPrefixes ? &pt : nullptr, G.units.as<ogs_unit>(),
                             int32_t(G.members.size()), flags, G.W, &out, stream),
              "ogs_spf_routes(batch)");
@@ -164,6 +166,7 @@ void RouteDbBatch::launch(void* stream) {
 struct RouteDbBatch::UnitRecords {
   std::vector<uint64_t> dist, metric;
   std::vector<uint32_t> nh, meta, mask, sel;
+  std::vector<uint32_t> reach;  // exact-order settled bitset (else empty)
   int W{1};
   size_t Sn{1}, Sp{1};
 };
@@ -200,6 +203,11 @@ bool RouteDbBatch::fetchUnit(const std::string& node, void* stream, UnitRecords&
   fetch(G.metric, u * Sp, P, db, wide_ ? static_cast<void*>(r.metric.data()) : m32.data());
   fetch(G.mask, u * W * Sp, W * Sp, 4, r.mask.data());
   fetch(G.sel, u * Sp, P, 4, r.sel.data());
+  if (exact_) {
+    const size_t RW = (Sn + 31) / 32;
+    r.reach.resize(RW);
+    fetch(G.reach, u * RW, RW, 4, r.reach.data());
+  }
   ogsCheck(ogs_stream_sync(stream), "ogs_stream_sync");
   if (!wide_) {
     for (size_t i = 0; i < N; ++i) r.dist[i] = d32[i] == 0xFFFFFFFFu ? ~0ull : d32[i];
@@ -230,6 +238,7 @@ std::optional<DecisionRouteDb> RouteDbBatch::routeDb(const std::string& node,
   view.mask = r.mask.data();
   view.maskStride = r.Sp;
   view.sel = r.sel.data();
+  view.reach = r.reach.empty() ? nullptr : r.reach.data();
   return materializeRouteDb(*ls_, f, area_, node, view, table_, solver_.v4OverV6Nexthop_,
                             solver_.enableNodeSegmentLabel_, solver_.staticUnicastRoutes_,
                             nullptr);
@@ -334,7 +343,8 @@ RouteDatabase RouteDbBatch::getRouteDbComputed(const std::string& node, void* st
   // node-label MPLS routes (SpfSolver.cpp:354-445), label order
   if (solver_.enableNodeSegmentLabel_) {
     LabelRoutes labelToNode;
-    addNodeLabelRoutes(*ls_, f, area_, n, r.dist.data(), r.nh.data(), r.Sn, r.W, labelToNode);
+    addNodeLabelRoutes(*ls_, f, area_, n, r.dist.data(), r.nh.data(), r.Sn, r.W, labelToNode,
+                       r.reach.empty() ? nullptr : r.reach.data());
     for (auto& [label, ne] : labelToNode) {
       out.mplsRoutes.push_back(MplsRoute{
           label, std::vector<NextHopThrift>(ne.second.nexthops.begin(), ne.second.nexthops.end())});

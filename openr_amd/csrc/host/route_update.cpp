@@ -198,8 +198,8 @@ void LinkFailureSweep::exactFetch(void* stream) {
     DecisionRouteDb db;
     for (uint32_t p = 0; p < uint32_t(table_.prefixes.size()); ++p) {
       auto e = materializeRoute(f, me_, table_, p, meta[t * Sp_ + p], metric[t * Sp_ + p],
-                                &mask[t * W_ * Sp_ + p], Sp_, W_, v4OverV6_, nullptr, 0xFF,
-                                0xFF);
+                                &mask[t * W_ * Sp_ + p], Sp_, W_, v4OverV6_, nullptr, OGS_POLICY_NONE,
+                                OGS_POLICY_NONE);
       if (e) db.unicastRoutes.emplace(e->prefix, std::move(*e));
     }
     return db;
@@ -383,7 +383,7 @@ const DecisionRouteDb& LinkFailureSweep::baseRouteDb() const {
     const FlatTopology& f = ls_.flat();
     for (uint32_t p = 0; p < uint32_t(table_.prefixes.size()); ++p) {
       auto e = materializeRoute(f, me_, table_, p, baseMeta_[p], baseMetric_[p],
-                                &baseMask_[p], Sp_, W_, v4OverV6_, nullptr, 0xFF, 0xFF);
+                                &baseMask_[p], Sp_, W_, v4OverV6_, nullptr, OGS_POLICY_NONE, OGS_POLICY_NONE);
       if (e) db.unicastRoutes.emplace(e->prefix, std::move(*e));
     }
     base_ = std::move(db);
@@ -403,7 +403,7 @@ DecisionRouteUpdate LinkFailureSweep::routeUpdate(size_t v) const {
   for (uint32_t i = offsets_[v]; i < offsets_[v + 1]; ++i) {
     const uint32_t p = cPrefixH_[i];
     auto e = materializeRouteAt(f, rb, me_, table_, p, cMetaH_[i], cMetricH_[i], &cMaskH_[i],
-                                T, W_, v4OverV6_, nullptr, 0xFF, 0xFF);
+                                T, W_, v4OverV6_, nullptr, OGS_POLICY_NONE, OGS_POLICY_NONE);
     if (e) {
       u.unicastRoutesToUpdate.emplace_hint(u.unicastRoutesToUpdate.end(), e->prefix,
                                            std::move(*e));
@@ -458,8 +458,8 @@ DecisionRouteDb LinkFailureSweep::routeDb(size_t v) const {
   const FlatTopology& f = ls_.flat();
   for (uint32_t p = 0; p < uint32_t(table_.prefixes.size()); ++p) {
     auto e = materializeRoute(f, me_, table_, p, meta_[v * Sp_ + p], metric_[v * Sp_ + p],
-                              &mask_[v * W_ * Sp_ + p], Sp_, W_, v4OverV6_, nullptr, 0xFF,
-                              0xFF);
+                              &mask_[v * W_ * Sp_ + p], Sp_, W_, v4OverV6_, nullptr, OGS_POLICY_NONE,
+                              OGS_POLICY_NONE);
     if (e) db.unicastRoutes.emplace(e->prefix, std::move(*e));
   }
   return db;

@@ -289,14 +289,17 @@ struct TableImage {
   }
 };
 
-// dist [N] | nh [W][N] | meta [P] | metric [P] | mask [W][P] | sel [P]
+// dist [N] | nh [W][N] | reach [ceil(N/32)] (exact-order settled bitset) |
+// meta [P] | metric [P] | mask [W][P] | sel [P]  (the SPF spans depend on N
+// and W only: the memo's layout is the same with or without a table)
 struct ResultImage {
-  size_t dist{0}, nh{0}, meta{0}, metric{0}, mask{0}, sel{0}, end{0};
+  size_t dist{0}, nh{0}, reach{0}, meta{0}, metric{0}, mask{0}, sel{0}, end{0};
   ResultImage() = default;
   ResultImage(uint32_t N, uint32_t P, int W, size_t db) {
     const size_t P1 = std::max<uint32_t>(P, 1);
     nh = al256(size_t(N) * db);
-    meta = nh + al256(size_t(N) * W * 4);
+    reach = nh + al256(size_t(N) * W * 4);
+    meta = reach + al256((size_t(N) + 31) / 32 * 4 + 4);
     metric = meta + al256(P1 * 4);
     mask = metric + al256(P1 * db);
     sel = mask + al256(P1 * W * 4);
@@ -348,7 +351,7 @@ struct SpfSolver::Impl {
     DeviceBuffer nodeBase, rowPtr, edges, flags, edgeSrc, desc;
     DeviceBuffer pfxBase, advOff, advNode, advMetrics, advMinNh, pfxFlags,
         advArea, advName, nameLocal;
-    DeviceBuffer units, srcName, spfRow, dist, nh, meta, metric, mask, sel;
+    DeviceBuffer units, srcName, spfRow, dist, nh, meta, metric, mask, sel, reach;
     bool exact{false}, wide{false};  // domain needs OGS_F_EXACT_ORDER / u64
   } ma;
   // shape of the last enqueueRouteDb (collectRouteDb downloads its results)
@@ -408,8 +411,9 @@ void runPolicyOnDevice(const RibPolicy& pol, const PrefixHostTable& table,
                        const std::string& me, int W, uint32_t* dMeta, uint32_t* dMask,
                        PolicyDevice& D, void* stream) {
   const size_t K = pol.numStatements();
-  // applied / counter are u8 statement indexes with 0xFF = none
-  if (K > 254) throw std::domain_error("RibPolicy: more than 254 statements");
+  // applied / counter are u16 statement indexes with OGS_POLICY_NONE = none
+  // (RibPolicy.cpp:231-249 walks any number of statements)
+  if (K >= OGS_POLICY_NONE) throw std::domain_error("RibPolicy: more than 65,534 statements");
   const size_t P = table.prefixes.size(), A = src.size();
   PolicyDevice::Key key{pol.uid(), table.generation, &table, {}, W, me};
   for (const auto& [f, s] : src) key.src.emplace_back(f, f->version, s);
@@ -464,8 +468,8 @@ void runPolicyOnDevice(const RibPolicy& pol, const PrefixHostTable& table,
                             C.tagMatch.as<uint32_t>(), C.nonzero.as<uint32_t>(),
                             int32_t(k0)};
     }
-    D.applied.resize(std::max<size_t>(P, 1));
-    D.counter.resize(std::max<size_t>(P, 1));
+    D.applied.resize(2 * std::max<size_t>(P, 1));
+    D.counter.resize(2 * std::max<size_t>(P, 1));
     D.key = std::move(key);
   }
   // chunks in statement order; a later chunk continues the routes no
@@ -473,15 +477,15 @@ void runPolicyOnDevice(const RibPolicy& pol, const PrefixHostTable& table,
   // RibPolicy.cpp:222-229)
   for (const auto& C : D.chunks) {
     ogsCheck(ogs_rib_policy_apply(&pt, &C.rp, int32_t(A), 1, W, dMeta, dMask,
-                                  D.applied.as<uint8_t>(), D.counter.as<uint8_t>(), stream),
+                                  D.applied.as<uint16_t>(), D.counter.as<uint16_t>(), stream),
              "ogs_rib_policy_apply");
   }
 }
 
-void downloadPolicy(const PolicyDevice& D, size_t P, std::vector<uint8_t>& applied,
-                    std::vector<uint8_t>& counter) {
-  applied.assign(P, 0xFF);
-  counter.assign(P, 0xFF);
+void downloadPolicy(const PolicyDevice& D, size_t P, std::vector<uint16_t>& applied,
+                    std::vector<uint16_t>& counter) {
+  applied.assign(P, OGS_POLICY_NONE);
+  counter.assign(P, OGS_POLICY_NONE);
   if (P) {
     D.applied.download(applied.data(), P);
     D.counter.download(counter.data(), P);
@@ -490,11 +494,11 @@ void downloadPolicy(const PolicyDevice& D, size_t P, std::vector<uint8_t>& appli
 
 // Route-level effect of the device policy: counterID of the last matching
 // statement, weights of the applied one (RibPolicy.cpp:115-160).
-void finishPolicy(const RibPolicy* pol, uint8_t applied, uint8_t counter,
+void finishPolicy(const RibPolicy* pol, uint16_t applied, uint16_t counter,
                   RibUnicastEntry& e) {
   if (!pol) return;
-  if (counter != 0xFF) e.counterID = pol->counterIDOf(counter);
-  if (applied == 0xFF) return;
+  if (counter != OGS_POLICY_NONE) e.counterID = pol->counterIDOf(counter);
+  if (applied == OGS_POLICY_NONE) return;
   NextHops w;
   for (NextHopThrift nh : e.nexthops) {
     nh.weight = pol->weightOf(applied, nh);
@@ -535,7 +539,7 @@ std::optional<RibUnicastEntry> materializeRoute(
     const FlatTopology& f, const std::string& me, const PrefixHostTable& pt,
     uint32_t p, uint32_t meta, uint64_t metric, const uint32_t* mask,
     size_t maskStride, int W, bool v4OverV6Nexthop, const RibPolicy* policy,
-    uint8_t applied, uint8_t counter) {
+    uint16_t applied, uint16_t counter) {
   if (!(meta & OGS_ROUTE_VALID)) return std::nullopt;
   return materializeRouteAt(f, f.rowPtr[f.id.at(me)], me, pt, p, meta, metric, mask,
                             maskStride, W, v4OverV6Nexthop, policy, applied, counter);
@@ -545,7 +549,7 @@ std::optional<RibUnicastEntry> materializeRouteAt(
     const FlatTopology& f, uint32_t rb, const std::string& me, const PrefixHostTable& pt,
     uint32_t p, uint32_t meta, uint64_t metric, const uint32_t* mask,
     size_t maskStride, int W, bool v4OverV6Nexthop, const RibPolicy* policy,
-    uint8_t applied, uint8_t counter) {
+    uint16_t applied, uint16_t counter) {
   if (!(meta & OGS_ROUTE_VALID)) return std::nullopt;
   const uint32_t best = pt.advOff[p] + (meta >> OGS_ROUTE_BEST_SHIFT);
   RibUnicastEntry e;
@@ -598,8 +602,8 @@ DecisionRouteDb materializeRouteDb(
     if (!(meta & OGS_ROUTE_VALID)) continue;
     auto e = materializeRouteAt(f, rb, me, pt, p, meta, r.metric[p], &r.mask[p],
                                 r.maskStride, r.W, v4OverV6Nexthop, r.policy,
-                                r.policy ? r.applied[p] : 0xFF,
-                                r.policy ? r.counter[p] : 0xFF);
+                                r.policy ? r.applied[p] : OGS_POLICY_NONE,
+                                r.policy ? r.counter[p] : OGS_POLICY_NONE);
     if (e) rdb.unicastRoutes.emplace_hint(rdb.unicastRoutes.end(), e->prefix, std::move(*e));
   }
   for (const auto& [prefix, e] : statics) {  // SpfSolver.cpp:343-349
@@ -612,7 +616,7 @@ DecisionRouteDb materializeRouteDb(
   if (enableNodeSegmentLabel) {
     LabelRoutes labelToNode;
     addNodeLabelRoutes(ls, f, area, me, r.dist, r.nh, r.nhStride, r.W,
-                       labelToNode);
+                       labelToNode, r.reach);
     for (auto& [label, ne] : labelToNode) {
       rdb.mplsRoutes.emplace(label, std::move(ne.second));
     }
@@ -623,7 +627,8 @@ DecisionRouteDb materializeRouteDb(
 void addNodeLabelRoutes(const LinkState& ls, const FlatTopology& f,
                         const std::string& area, const std::string& me,
                         const uint64_t* dist, const uint32_t* nhWords,
-                        size_t nhStride, int W, LabelRoutes& labelToNode) {
+                        size_t nhStride, int W, LabelRoutes& labelToNode,
+                        const uint32_t* reach) {
   // SpfSolver.cpp:357-437, one area; dist == nullptr: the source has no
   // SPF in this area (no adjacency database), every other owner unreachable
   const auto sIt = f.id.find(me);
@@ -645,7 +650,7 @@ void addNodeLabelRoutes(const LinkState& ls, const FlatTopology& f,
     }
     if (!dist || sIt == f.id.end()) continue;
     const uint32_t v = f.id.at(node);
-    if (dist[v] == ~0ull) continue;  // no route to the label owner
+    if (reach ? !bitAt(reach, v) : dist[v] == ~0ull) continue;  // no route to the owner
     RibMplsEntry entry{label, {}};
     const int32_t m32 = static_cast<int32_t>(dist[v]);
     const uint32_t rb = f.rowPtr[sIt->second];
@@ -766,6 +771,7 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(
   out.metric = devAt<void>(I.res, L.metric);
   out.mask = devAt<uint32_t>(I.res, L.mask);
   out.sel = devAt<uint32_t>(I.res, L.sel);
+  out.reached = exact ? devAt<uint32_t>(I.res, L.reach) : nullptr;
   const uint32_t flags = (enableV4_ ? OGS_F_ENABLE_V4 : 0u) |
       (v4OverV6Nexthop_ ? OGS_F_V4_OVER_V6 : 0u) |
       (enableBestRouteSelection_ ? OGS_F_BEST_ROUTE_SELECTION : 0u) |
@@ -781,7 +787,7 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(
   I.spfW = W;
   I.spfDb = db;
   const RibPolicy* policy = (ribPolicy_ && ribPolicy_->isActive()) ? ribPolicy_ : nullptr;
-  std::vector<uint8_t> applied, counter;
+  std::vector<uint16_t> applied, counter;
   if (policy && P) {
     runPolicyOnDevice(*policy, I.table, pt, {{&f, s}}, me, W, out.meta, out.mask,
                       I.policy, nullptr);
@@ -809,6 +815,7 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(
   view.mask = I.hRes.at<uint32_t>(L.mask);
   view.maskStride = P;
   view.sel = I.hRes.at<uint32_t>(L.sel);
+  view.reach = exact && enableNodeSegmentLabel_ ? I.hRes.at<uint32_t>(L.reach) : nullptr;
   if (policy && P) {
     view.policy = policy;
     view.applied = applied.data();
@@ -856,6 +863,7 @@ void SpfSolver::routesFromSpfMemo(const std::string& me, const LinkState& ls,
     ogs_spf_out so{};
     so.dist = devAt<void>(I.res, L.dist);
     so.nh = devAt<uint32_t>(I.res, L.nh);
+    so.reached = exact ? devAt<uint32_t>(I.res, L.reach) : nullptr;
     ogsCheck(ogs_spf_routes(&g, nullptr, I.unit.as<ogs_unit>(), 1, flags, W, &so, nullptr),
              "ogs_spf_routes");
     ls.noteSpfRuns(1);
@@ -889,7 +897,9 @@ void SpfSolver::routesFromSpfMemo(const std::string& me, const LinkState& ls,
   ro.mask = devAt<uint32_t>(I.subRes, R.mask);
   ro.sel = devAt<uint32_t>(I.subRes, R.sel);
   ogsCheck(ogs_routes_from_spf(&g, &pt, I.unit.as<ogs_unit>(), 1, devAt<void>(I.res, S.dist),
-                               devAt<uint32_t>(I.res, S.nh), flags, W, &ro, nullptr),
+                               devAt<uint32_t>(I.res, S.nh),
+                               exact ? devAt<uint32_t>(I.res, S.reach) : nullptr, flags, W,
+                               &ro, nullptr),
            "ogs_routes_from_spf");
   ogsCheck(ogs_memcpy_d2h(I.hSubRes.at<char>(R.meta), devAt<char>(I.subRes, R.meta),
                           R.end - R.meta, nullptr),
@@ -917,7 +927,8 @@ void SpfSolver::routesFromSpfMemo(const std::string& me, const LinkState& ls,
       bestRoutesCache_.erase(prefix);
     }
     out[prefix] = materializeRoute(f, me, st, p, meta[p], metric[p], &mask[p], np, W,
-                                   v4OverV6Nexthop_, nullptr, 0xFF, 0xFF);
+                                   v4OverV6Nexthop_, nullptr, OGS_POLICY_NONE,
+                                   OGS_POLICY_NONE);
   }
 }
 
@@ -1088,12 +1099,14 @@ DecisionRouteDb SpfSolver::materializeMultiArea(const std::string& me,
     for (const auto& [area, ls] : als) {
       const uint64_t* dist = nullptr;
       const uint32_t* nhw = nullptr;
+      const uint32_t* reach = nullptr;
       if (R.row[a] != OGS_NODE_NONE) {
         for (size_t v = 0; v < Sn; ++v) d64[v] = R.dist[R.row[a] * Sn + v];
         dist = d64.data();
         nhw = &R.nh[size_t(R.row[a]) * W * Sn];
+        if (!R.reach.empty()) reach = &R.reach[size_t(R.row[a]) * ((Sn + 31) / 32)];
       }
-      addNodeLabelRoutes(ls, *M.flats[a], area, me, dist, nhw, Sn, W, labelToNode);
+      addNodeLabelRoutes(ls, *M.flats[a], area, me, dist, nhw, Sn, W, labelToNode, reach);
       ++a;
     }
     for (auto& [label, ne] : labelToNode) {
@@ -1141,6 +1154,8 @@ void SpfSolver::enqueueMultiArea(const std::string& me, const AreaLinkStates& al
   M.metric.resize(P1 * db);
   M.mask.resize(P1 * A * W * 4);
   M.sel.resize(P1 * 4);
+  const size_t RW = (Sn + 31) / 32;
+  M.reach.resize(std::max<size_t>(su.size() * RW * 4, 4));
   ogs_graph g{};
   g.num_topos = int32_t(A);
   g.max_nodes = int32_t(Sn);
@@ -1159,6 +1174,7 @@ void SpfSolver::enqueueMultiArea(const std::string& me, const AreaLinkStates& al
   ogs_spf_out spf{};
   spf.dist = M.dist.get();
   spf.nh = M.nh.as<uint32_t>();
+  spf.reached = M.exact ? M.reach.as<uint32_t>() : nullptr;
   ogsCheck(ogs_spf_routes(&g, nullptr, M.units.as<ogs_unit>(), int32_t(su.size()),
                           flags, W, &spf, stream),
            "ogs_spf_routes");
@@ -1178,7 +1194,8 @@ void SpfSolver::enqueueMultiArea(const std::string& me, const AreaLinkStates& al
     pt.adv_min_nh = M.advMinNh.as<int64_t>();
     pt.pfx_flags = M.pfxFlags.as<uint8_t>();
     ogs_area_table at{int32_t(A), int32_t(M.numNames), M.nameLocal.as<uint32_t>(),
-                      M.advArea.as<uint32_t>(), M.advName.as<uint32_t>()};
+                      M.advArea.as<uint32_t>(), M.advName.as<uint32_t>(),
+                      M.exact ? M.reach.as<uint32_t>() : nullptr};
     ogs_spf_out out{};
     out.meta = M.meta.as<uint32_t>();
     out.metric = M.metric.get();
@@ -1261,6 +1278,11 @@ DecisionRouteDb SpfSolver::downloadMultiArea(const std::string& me,
   };
   widen(M.dist, nSpf * Sn, R.dist);
   M.nh.download(R.nh.data(), R.nh.size());
+  R.reach.clear();
+  if (M.exact && nSpf) {
+    R.reach.resize(nSpf * ((Sn + 31) / 32));
+    M.reach.download(R.reach.data(), R.reach.size());
+  }
   if (P) {
     M.meta.download(R.meta.data(), P);
     widen(M.metric, P, R.metric);

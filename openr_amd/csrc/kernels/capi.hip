@@ -42,7 +42,7 @@ hipError_t launch_variants(const ogs_graph& g, const ogs_prefix_table& pt,
                            hipStream_t stream, int* unsupported);
 hipError_t launch_rib_policy(const ogs_prefix_table& pt, const ogs_rib_policy& pol,
                              int A, int nUnits, int W, const uint32_t* meta,
-                             uint32_t* mask, uint8_t* applied, uint8_t* counter,
+                             uint32_t* mask, uint16_t* applied, uint16_t* counter,
                              hipStream_t stream);
 hipError_t launch_route_changes(const uint32_t* changed, int nUnits, int Sp, int W,
                                 const uint32_t* meta, const uint32_t* metric,
@@ -52,8 +52,8 @@ hipError_t launch_csr_patch(uint64_t* edges, const uint32_t* idx, const uint64_t
                             int n, hipStream_t stream);
 hipError_t launch_routes_from_spf(const ogs_graph& g, const ogs_prefix_table& pt,
                                   const ogs_unit* units, int n, const void* dist,
-                                  const uint32_t* nh, uint32_t flags, int W,
-                                  const ogs_spf_out& out, hipStream_t stream);
+                                  const uint32_t* nh, const uint32_t* reach, uint32_t flags,
+                                  int W, const ogs_spf_out& out, hipStream_t stream);
 hipError_t launch_ksp(const ogs_graph& g, const ogs_path_unit* units,
                       int nUnits, const uint32_t* masks, uint32_t maskWords,
                       uint32_t flags, const ogs_path_out& out,
@@ -80,7 +80,8 @@ int hipFail(hipError_t e, const char* what) {
 
 extern "C" {
 
-const char* ogs_version(void) { return "openr-gpu-spf 0.1 (gfx950)"; }
+const char* ogs_version(void) { return "openr-gpu-spf 0.3 (gfx950)"; }
+int ogs_abi_version(void) { return OGS_ABI_VERSION; }
 
 const char* ogs_last_error(void) { return g_lastError.c_str(); }
 
@@ -322,8 +323,8 @@ int ogs_spf_routes(const ogs_graph* graph, const ogs_prefix_table* prefixes,
 
 int ogs_routes_from_spf(const ogs_graph* graph, const ogs_prefix_table* prefixes,
                         const ogs_unit* units, int32_t n_units, const void* spf_dist,
-                        const uint32_t* spf_nh, uint32_t flags, int32_t nh_words,
-                        ogs_spf_out* out, void* stream) {
+                        const uint32_t* spf_nh, const uint32_t* spf_reached, uint32_t flags,
+                        int32_t nh_words, ogs_spf_out* out, void* stream) {
   if (!graph || !prefixes || !out) return fail(OGS_E_INVALID, "graph/prefixes/out is NULL");
   if (n_units < 0) return fail(OGS_E_INVALID, "n_units < 0");
   if (n_units == 0 || prefixes->max_prefixes <= 0) return OGS_OK;
@@ -336,7 +337,7 @@ int ogs_routes_from_spf(const ogs_graph* graph, const ogs_prefix_table* prefixes
     return fail(OGS_E_UNSUPPORTED, "nh_words must be 1, 2, 4, 8 or 16");
   }
   hipError_t e = ogs::launch_routes_from_spf(*graph, *prefixes, units, n_units, spf_dist,
-                                            spf_nh, flags, nh_words, *out,
+                                            spf_nh, spf_reached, flags, nh_words, *out,
                                             static_cast<hipStream_t>(stream));
   return e == hipSuccess ? OGS_OK : hipFail(e, "routes-from-spf launch");
 }
@@ -485,7 +486,7 @@ int ogs_rib_policy_apply(const ogs_prefix_table* prefixes,
                          const ogs_rib_policy* policy, int32_t num_areas,
                          int32_t n_units, int32_t nh_words,
                          const uint32_t* meta, uint32_t* mask,
-                         uint8_t* applied, uint8_t* counter, void* stream) {
+                         uint16_t* applied, uint16_t* counter, void* stream) {
   if (!prefixes || !policy || !meta || !mask) {
     return fail(OGS_E_INVALID, "prefixes/policy/meta/mask is NULL");
   }
@@ -499,8 +500,8 @@ int ogs_rib_policy_apply(const ogs_prefix_table* prefixes,
     return fail(OGS_E_INVALID, "policy tables NULL or more than 32 statements per chunk");
   }
   if (policy->statement_base < 0 ||
-      policy->statement_base + policy->num_statements > 255) {
-    return fail(OGS_E_INVALID, "statement_base + num_statements outside [0, 255]");
+      policy->statement_base + policy->num_statements > int32_t(OGS_POLICY_NONE)) {
+    return fail(OGS_E_INVALID, "statement_base + num_statements outside [0, 65535]");
   }
   if (policy->statement_base > 0 && (!applied || !counter)) {
     return fail(OGS_E_INVALID, "a continuation chunk needs applied / counter");

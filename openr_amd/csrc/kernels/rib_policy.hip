@@ -26,7 +26,7 @@ template <int W>
 __global__ __launch_bounds__(kBlock) void rib_policy_kernel(
     ogs_prefix_table pt, ogs_rib_policy pol, uint32_t A,
     const uint32_t* __restrict__ meta, uint32_t* __restrict__ mask,
-    uint8_t* __restrict__ applied, uint8_t* __restrict__ counter) {
+    uint16_t* __restrict__ applied, uint16_t* __restrict__ counter) {
   const uint32_t u = blockIdx.y;
   const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
   const uint32_t p0 = pt.pfx_base[0];
@@ -37,11 +37,11 @@ __global__ __launch_bounds__(kBlock) void rib_policy_kernel(
   const size_t o = size_t(u) * Sp + p;
   const uint32_t m = meta[o];
   const uint32_t base = uint32_t(pol.statement_base);
-  uint32_t app = 0xFFu, cnt = 0xFFu;
+  uint32_t app = OGS_POLICY_NONE, cnt = OGS_POLICY_NONE;
   if (base) {  // a later chunk: keep what earlier statements decided
     app = applied[o];
     cnt = counter[o];
-    if (app != 0xFFu) return;
+    if (app != OGS_POLICY_NONE) return;
   }
   if (m & OGS_ROUTE_VALID) {
     const uint32_t gp = p0 + p;
@@ -70,13 +70,13 @@ __global__ __launch_bounds__(kBlock) void rib_policy_kernel(
       break;
     }
   }
-  if (applied) applied[o] = uint8_t(app);
-  if (counter) counter[o] = uint8_t(cnt);
+  if (applied) applied[o] = uint16_t(app);
+  if (counter) counter[o] = uint16_t(cnt);
 }
 
 hipError_t launch_rib_policy(const ogs_prefix_table& pt, const ogs_rib_policy& pol,
                              int A, int nUnits, int W, const uint32_t* meta,
-                             uint32_t* mask, uint8_t* applied, uint8_t* counter,
+                             uint32_t* mask, uint16_t* applied, uint16_t* counter,
                              hipStream_t stream) {
   if (pt.max_prefixes <= 0) return hipSuccess;
   const dim3 grid(unsigned((pt.max_prefixes + kBlock - 1) / kBlock), unsigned(nUnits));

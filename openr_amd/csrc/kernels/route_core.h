@@ -42,6 +42,20 @@ struct PackedView {
   }
 };
 
+// Is node v reached in the unit's SPF? Views over exact-order state carry
+// the settled bitset (a wrapped u64 distance may be all ones, LinkState.cpp:
+// 789 -- the reference keeps such a node with metric UINT64_MAX); every
+// other view uses the all-ones sentinel.
+template <typename D, typename View>
+__device__ __forceinline__ auto view_reached(const View& sv, uint32_t v, int)
+    -> decltype(sv.reached(v)) {
+  return sv.reached(v);
+}
+template <typename D, typename View>
+__device__ __forceinline__ bool view_reached(const View& sv, uint32_t v, long) {
+  return sv.dist(v) != DistInf<D>::value;
+}
+
 // Route for one prefix from the unit's SPF state.
 template <typename D, int W, typename View>
 __device__ void route_one(const ogs_prefix_table& pt, uint32_t gp, uint32_t s,
@@ -73,7 +87,7 @@ __device__ void route_one(const ogs_prefix_table& pt, uint32_t gp, uint32_t s,
   for (uint32_t a = a0; a < a1; ++a) {
     const uint32_t n = pt.adv_node[a];
     if (n == s) local = true;
-    if (n != OGS_NODE_NONE && sv.dist(n) != kInf) {
+    if (n != OGS_NODE_NONE && view_reached<D>(sv, n, 0)) {
       ++nReach;
       nReachUp += (nflags[n] & OGS_NODE_OVERLOADED) ? 0u : 1u;
     }
@@ -85,7 +99,7 @@ __device__ void route_one(const ogs_prefix_table& pt, uint32_t gp, uint32_t s,
   }
   const bool dropOverloaded = nReachUp != 0;
   auto filtered = [&](uint32_t n) {
-    return n != OGS_NODE_NONE && sv.dist(n) != kInf &&
+    return n != OGS_NODE_NONE && view_reached<D>(sv, n, 0) &&
         !(dropOverloaded && (nflags[n] & OGS_NODE_OVERLOADED));
   };
 

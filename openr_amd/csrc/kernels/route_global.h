@@ -20,7 +20,11 @@ struct GlobalView {
   const D* d;
   const uint32_t* n;
   size_t Sn;
+  const uint32_t* r;  // settled bitset (exact-order state) or nullptr
   __device__ __forceinline__ D dist(uint32_t v) const { return d[v]; }
+  __device__ __forceinline__ bool reached(uint32_t v) const {
+    return r ? ((r[v >> 5] >> (v & 31u)) & 1u) != 0u : d[v] != DistInf<D>::value;
+  }
   __device__ __forceinline__ uint32_t nh(uint32_t v, int w) const {
     return n[size_t(w) * Sn + v];
   }
@@ -32,7 +36,7 @@ template <typename D, int W>
 __global__ __launch_bounds__(kBlock) void route_global_kernel(
     ogs_graph g, ogs_prefix_table pt, const ogs_unit* __restrict__ units,
     uint32_t flags, const D* __restrict__ sDist, const uint32_t* __restrict__ sNh,
-    ogs_spf_out out) {
+    const uint32_t* __restrict__ sReach, ogs_spf_out out) {
   const uint32_t u = blockIdx.x;
   const uint32_t p = blockIdx.y * kBlock + threadIdx.x;
   const ogs_unit unit = units[u];
@@ -49,7 +53,8 @@ __global__ __launch_bounds__(kBlock) void route_global_kernel(
   if (p < P) {
     const RouteCfg cfg{(flags & OGS_F_ENABLE_V4) != 0, (flags & OGS_F_V4_OVER_V6) != 0,
                        (flags & OGS_F_BEST_ROUTE_SELECTION) != 0};
-    const GlobalView<D, W> sv{sDist + u * Sn, sNh + size_t(u) * W * Sn, Sn};
+    const GlobalView<D, W> sv{sDist + u * Sn, sNh + size_t(u) * W * Sn, Sn,
+                              sReach ? sReach + size_t(u) * ((Sn + 31) / 32) : nullptr};
     route_one<D, W>(pt, p0 + p, unit.src, g.node_flags + g.node_base[unit.topo], sv, cfg,
                     meta, metric, mask, selBits);
   }
@@ -66,10 +71,10 @@ template <typename D, int W>
 hipError_t launch_route_global(const ogs_graph& g, const ogs_prefix_table& pt,
                                const ogs_unit* units, int nUnits, uint32_t flags,
                                const D* dist, const uint32_t* nh, const ogs_spf_out& out,
-                               hipStream_t stream) {
+                               hipStream_t stream, const uint32_t* reach = nullptr) {
   const unsigned by = unsigned((pt.max_prefixes + kBlock - 1) / kBlock);
   hipLaunchKernelGGL((route_global_kernel<D, W>), dim3(unsigned(nUnits), by), dim3(kBlock), 0,
-                     stream, g, pt, units, flags, dist, nh, out);
+                     stream, g, pt, units, flags, dist, nh, reach, out);
   return hipGetLastError();
 }
 

@@ -62,6 +62,18 @@ __global__ __launch_bounds__(kBlock) void route_multiarea_kernel(
     if (r == OGS_NODE_NONE || v == OGS_NODE_NONE) return kInf;
     return sDist[size_t(r) * Sn + v];
   };
+  // reached in (source, area b)'s SPF: the settled bitset of exact-order
+  // rows when given (a wrapped u64 distance may be all ones), else the
+  // all-ones sentinel
+  const size_t RW = (size_t(Sn) + 31) / 32;
+  auto reachOf = [&](uint32_t b, uint32_t name) -> bool {
+    if (name == S) return true;
+    const uint32_t r = row[b];
+    const uint32_t v = at.name_local[size_t(name) * A + b];
+    if (r == OGS_NODE_NONE || v == OGS_NODE_NONE) return false;
+    if (at.reached) return ((at.reached[size_t(r) * RW + (v >> 5)] >> (v & 31u)) & 1u) != 0u;
+    return sDist[size_t(r) * Sn + v] != kInf;
+  };
   auto nhOf = [&](uint32_t b, uint32_t name, int w) -> uint32_t {
     const uint32_t r = row[b];
     const uint32_t v = at.name_local[size_t(name) * A + b];
@@ -105,7 +117,7 @@ __global__ __launch_bounds__(kBlock) void route_multiarea_kernel(
   for (uint32_t a = a0; a < a1; ++a) {
     const uint32_t name = at.adv_name[a];
     if (name == S) local = true;
-    if (distOf(at.adv_area[a], name) != kInf) {
+    if (reachOf(at.adv_area[a], name)) {
       ++nReach;
       nReachUp += (flagsOf(a) & OGS_NODE_OVERLOADED) ? 0u : 1u;
     }
@@ -118,7 +130,7 @@ __global__ __launch_bounds__(kBlock) void route_multiarea_kernel(
   }
   const bool dropOverloaded = nReachUp != 0;
   auto filtered = [&](uint32_t a) {
-    return distOf(at.adv_area[a], at.adv_name[a]) != kInf &&
+    return reachOf(at.adv_area[a], at.adv_name[a]) &&
         !(dropOverloaded && (flagsOf(a) & OGS_NODE_OVERLOADED));
   };
   int32_t bD = INT32_MIN, bP = INT32_MIN, bS = INT32_MIN, bDist = INT32_MAX;
@@ -185,7 +197,7 @@ __global__ __launch_bounds__(kBlock) void route_multiarea_kernel(
   auto areaShortest = [&](uint32_t b) {
     D sb = kInf;
     for (uint32_t a = a0; a < a1; ++a) {
-      if (!selected(a)) continue;
+      if (!selected(a) || !reachOf(b, at.adv_name[a])) continue;
       const D d = distOf(b, at.adv_name[a]);
       if (d < sb) sb = d;
     }
@@ -206,7 +218,7 @@ __global__ __launch_bounds__(kBlock) void route_multiarea_kernel(
       for (uint32_t a = a0; a < a1; ++a) {
         if (!selected(a)) continue;
         const uint32_t name = at.adv_name[a];
-        if (distOf(b, name) != shortest) continue;
+        if (!reachOf(b, name) || distOf(b, name) != shortest) continue;
 #pragma unroll
         for (int w = 0; w < W; ++w) m[w] |= nhOf(b, name, w);
       }

@@ -58,7 +58,7 @@ template <int W>
 __global__ __launch_bounds__(64) void spf_exact_kernel(
     ogs_graph g, const ogs_unit* __restrict__ units, uint32_t flags,
     uint64_t* __restrict__ oDist, uint32_t* __restrict__ oNh,
-    uint32_t* __restrict__ scratch) {
+    uint32_t* __restrict__ scratch, uint32_t* __restrict__ oReach) {
   constexpr uint64_t kInf = ~0ull;
   constexpr uint32_t kOpen = 1, kDone = 2;
   const int lane = threadIdx.x;
@@ -203,10 +203,21 @@ __global__ __launch_bounds__(64) void spf_exact_kernel(
     wave_sync();
   }
 
-  // ---- outputs: unreachable = all ones; getNextHopsThrift's link filter ----
+  // ---- outputs: unreachable = all ones, plus the settled bitset (a reached
+  // node's wrapped distance can itself be all ones); getNextHopsThrift's
+  // link filter ------------------------------------------------------------
   for (uint32_t v = lane; v < N; v += 64) {
     const bool done = st[v] == kDone;
     if (!done) key[v] = kInf;
+  }
+  uint32_t* reach = oReach + size_t(u0) * ((Sn + 31) / 32);
+  for (uint32_t i = lane; i < (uint32_t(Sn) + 31u) / 32u; i += 64) {
+    uint32_t word = 0u;
+    for (uint32_t b = 0; b < 32u; ++b) {
+      const uint32_t v = 32u * i + b;
+      if (v < N && st[v] == kDone) word |= 1u << b;
+    }
+    reach[i] = word;
   }
   wave_sync();
   uint32_t f[W];
@@ -216,7 +227,7 @@ __global__ __launch_bounds__(64) void spf_exact_kernel(
     const uint64_t x = edges[sb + k];
     const uint32_t lo = static_cast<uint32_t>(x);
     const uint32_t t = edge_dst(lo);
-    if (!(lo & OGS_EDGE_DOWN) && key[t] != kInf && exact_weight(x, hop) == key[t]) {
+    if (!(lo & OGS_EDGE_DOWN) && st[t] == kDone && exact_weight(x, hop) == key[t]) {
       f[k >> 5] |= 1u << (k & 31u);
     }
   }
@@ -237,18 +248,23 @@ hipError_t launch_exact_w(const ogs_graph& g, const ogs_prefix_table* pt,
   const size_t distBytes = out.dist ? 0 : r256(U * Sn * 8);
   const size_t nhBytes = out.nh ? 0 : r256(U * W * Sn * 4);
   const size_t scratchBytes = r256(U * 2 * Sn * 4);
+  const size_t reachBytes = out.reached ? 0 : r256(U * ((Sn + 31) / 32) * 4);
   void* ws = nullptr;
-  hipError_t e = workspace(distBytes + nhBytes + scratchBytes, stream, &ws);
+  hipError_t e = workspace(distBytes + nhBytes + scratchBytes + reachBytes, stream, &ws);
   if (e != hipSuccess) return e;
   char* base = static_cast<char*>(ws);
   uint64_t* dist = out.dist ? static_cast<uint64_t*>(out.dist) : reinterpret_cast<uint64_t*>(base);
   uint32_t* nh = out.nh ? out.nh : reinterpret_cast<uint32_t*>(base + distBytes);
   uint32_t* scratch = reinterpret_cast<uint32_t*>(base + distBytes + nhBytes);
+  uint32_t* reach = out.reached ? out.reached
+                                : reinterpret_cast<uint32_t*>(base + distBytes + nhBytes +
+                                                              scratchBytes);
   hipLaunchKernelGGL((spf_exact_kernel<W>), dim3(nUnits), dim3(64), 0, stream, g, units,
-                     flags, dist, nh, scratch);
+                     flags, dist, nh, scratch, reach);
   e = hipGetLastError();
   if (e != hipSuccess || !pt || pt->max_prefixes == 0) return e;
-  return launch_route_global<uint64_t, W>(g, *pt, units, nUnits, flags, dist, nh, out, stream);
+  return launch_route_global<uint64_t, W>(g, *pt, units, nUnits, flags, dist, nh, out, stream,
+                                          reach);
 }
 
 // OGS_F_EXACT_ORDER: SPF (+ RouteDb) in the reference's extraction order.

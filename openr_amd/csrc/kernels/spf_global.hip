@@ -826,16 +826,16 @@ hipError_t launch_spf_routes_global(const ogs_graph& g, const ogs_prefix_table* 
 // ogs_routes_from_spf: route_global_kernel over caller-held SPF state.
 hipError_t launch_routes_from_spf(const ogs_graph& g, const ogs_prefix_table& pt,
                                   const ogs_unit* units, int n, const void* dist,
-                                  const uint32_t* nh, uint32_t flags, int W,
-                                  const ogs_spf_out& out, hipStream_t stream) {
+                                  const uint32_t* nh, const uint32_t* reach, uint32_t flags,
+                                  int W, const ogs_spf_out& out, hipStream_t stream) {
   const bool wide = (flags & OGS_F_WIDE_METRIC) != 0;
 #define OGS_RFS(W_)                                                                         \
   return wide ? launch_route_global<uint64_t, W_>(g, pt, units, n, flags,                   \
                                                   static_cast<const uint64_t*>(dist), nh,   \
-                                                  out, stream)                              \
+                                                  out, stream, reach)                       \
               : launch_route_global<uint32_t, W_>(g, pt, units, n, flags,                   \
                                                   static_cast<const uint32_t*>(dist), nh,   \
-                                                  out, stream);
+                                                  out, stream, reach);
   switch (W) {
     case 1: OGS_RFS(1)
     case 2: OGS_RFS(2)

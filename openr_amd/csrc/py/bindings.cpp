@@ -551,13 +551,15 @@ class BatchRunner {
     dMetric_.resize(U * Sp * db);
     dMask_.resize(U * W_ * Sp * 4);
     dSel_.resize(U * Sp * 4);
+    dReach_.resize(std::max<size_t>(U * ((Sn + 31) / 32) * 4, 4));
   }
 
   void run() {
     ogs_graph g = graph();
     ogs_prefix_table pt = table();
     ogs_spf_out out{dDist_.get(), dNh_.as<uint32_t>(), dMeta_.as<uint32_t>(),
-                    dMetric_.get(), dMask_.as<uint32_t>(), dSel_.as<uint32_t>()};
+                    dMetric_.get(), dMask_.as<uint32_t>(), dSel_.as<uint32_t>(),
+                    exact_ ? dReach_.as<uint32_t>() : nullptr};
     ogsCheck(ogs_spf_routes(&g, hb_.maxPrefixes ? &pt : nullptr,
                             dUnits_.as<ogs_unit>(), int32_t(units_.size()),
                             flags(), W_, &out, nullptr),
@@ -588,6 +590,8 @@ class BatchRunner {
     dMask_.download(mask_.data(), mask_.size());
     sel_.resize(U * Sp);
     dSel_.download(sel_.data(), sel_.size());
+    reach_.assign(exact_ ? U * ((Sn + 31) / 32) : 0, 0u);
+    if (exact_) dReach_.download(reach_.data(), reach_.size());
     ogsCheck(ogs_stream_sync(nullptr), "ogs_stream_sync");
   }
 
@@ -607,6 +611,7 @@ class BatchRunner {
     v.mask = &mask_[u * W_ * Sp];
     v.maskStride = Sp;
     v.sel = &sel_[u * Sp];
+    v.reach = reach_.empty() ? nullptr : &reach_[u * ((Sn + 31) / 32)];
     static const std::map<std::string, RibUnicastEntry> kNoStatics;
     return materializeRouteDb(ls, ls.flat(), t.area, unitSrc_[u], v, t.table,
                               false, sr_, kNoStatics, nullptr);
@@ -719,9 +724,9 @@ class BatchRunner {
   bool wide_{false}, exact_{false};
   DeviceBuffer dDesc_, dNodeBase_, dRow_, dEdges_, dFlags_, dPfxBase_, dAdvOff_,
       dAdvNode_, dAdvMetrics_, dAdvMinNh_, dPfxFlags_, dUnits_, dDist_, dNh_,
-      dMeta_, dMetric_, dMask_, dSel_;
+      dMeta_, dMetric_, dMask_, dSel_, dReach_;
   std::vector<uint64_t> dist_, metric_;
-  std::vector<uint32_t> nh_, meta_, mask_, sel_;
+  std::vector<uint32_t> nh_, meta_, mask_, sel_, reach_;
 };
 
 // -------------------------------------------------------- VariantRunner ---

@@ -55,6 +55,10 @@ int main(void) {
   CHECK(ogs_memcpy_h2d(d_flags, flags, sizeof flags, NULL));
   CHECK(ogs_memcpy_h2d(d_unit, &unit, sizeof unit, NULL));
 
+  if (ogs_abi_version() != OGS_ABI_VERSION) {  /* header and library agree */
+    fprintf(stderr, "ABI %d, header %d\n", ogs_abi_version(), OGS_ABI_VERSION);
+    return 2;
+  }
   ogs_graph g;
   memset(&g, 0, sizeof g);
   g.num_topos = 1;

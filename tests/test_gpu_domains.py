@@ -60,6 +60,28 @@ def test_policy_more_than_32_statements_single_area(product, oracle, n):
          oracle.gen_route_dbs("wan", opts, srcs, True, False, True, pol), f"pol{n}")
 
 
+@pytest.mark.parametrize("n", [300, 700])
+def test_policy_more_than_255_statements(product, oracle, n):
+    """Statement ids past the former u8 range (applied / counter are u16):
+    n - 40 statements that never match (tag "none"), then 40 random ones, so
+    the statement each route takes and its counterID lie past index 255
+    (RibPolicy.cpp:222-249 walks any number of statements)."""
+    opts = dict(nodes=300, seed=0xD1, prefixesPerNode=3, tagPermille=500, anycastPermille=100)
+    srcs = ["0", "150"]
+    nbrs = [str(i) for i in range(300)]
+    dead = [dict(name=f"d{k}", tags=["none"], counterID=f"dead{k}",
+                 set_weight=dict(default_weight=1, area_to_weight={}, neighbor_to_weight={}))
+            for k in range(n - 40)]
+    live = _many_statements(40, n, nbrs, ["test_area_name"])
+    for k, st in enumerate(live):
+        st["counterID"] = f"live{k}"
+    pol = dead + live
+    got = product.gen_route_dbs("wan", opts, srcs, True, False, True, pol)
+    _cmp(got, oracle.gen_route_dbs("wan", opts, srcs, True, False, True, pol), f"pol{n}")
+    text = b"".join(got).decode()
+    assert "cid=live" in text and "dead" not in text  # late counterIDs reached the routes
+
+
 def test_policy_more_than_32_statements_multi_area(product, oracle):
     opts = dict(areas=3, nodesPerArea=60, abrs=6, prefixesPerNode=2, anycastPermille=200)
     srcs = ["abr-0", "abr-1", "a0-7"]

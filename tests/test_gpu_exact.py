@@ -143,3 +143,49 @@ def test_incremental_routes_zero_metric(product, oracle):
         want = os_.createRouteForPrefixOrGetStaticRoute("0", oa, ops, p)
         assert got[p] == want, p
         assert ps_.createRouteForPrefixOrGetStaticRoute("0", pa, pps, p) == want, p
+
+
+def _line_minus_one(M, two_areas=False):
+    """0 -(-1)- 1 (and, with two_areas, 0 -(1)- 2 in a second area): from
+    "0" node "1" is reached at the u64 distance 2^64 - 1 -- the all-ones
+    value, which the reference keeps as a reachable metric (LinkState.cpp:
+    77-78, 789; getNextHopsWithMetric accepts shortestMetric >= distance)."""
+    als = M.AreaLinkStates()
+    ls = als.add(L.kTestingAreaName, "0")
+    ps = M.PrefixState()
+    A = L.createAdjacency
+    for n, adjs in {"0": [A("1", "0/1", "1/0", "fe80::1", "10.0.0.1", -1, 101)],
+                    "1": [A("0", "1/0", "0/1", "fe80::10", "10.0.0.10", -1, 100)]}.items():
+        ls.updateAdjacencyDatabase(L.createAdjDb(n, adjs, int(n) + 1), L.kTestingAreaName)
+        L.updatePrefixDatabase(ps, L.createPrefixDb(n, [L.createPrefixEntry(f"fc00::{n}/128")]))
+    if two_areas:
+        lb = als.add("B", "0")
+        for n, adjs in {"0": [A("2", "0/2", "2/0", "fe80::2", "10.0.0.2", 1, 102)],
+                        "2": [A("0", "2/0", "0/2", "fe80::20", "10.0.0.20", 1, 100)]}.items():
+            lb.updateAdjacencyDatabase(L.createAdjDb(n, adjs, int(n) + 11, area="B"), "B")
+        L.updatePrefixDatabase(ps, L.createPrefixDb("2", [L.createPrefixEntry("fc00::2/128")]),
+                               area="B")
+    return als, ls, ps
+
+
+@pytest.mark.parametrize("two_areas", [False, True])
+def test_all_ones_distance_is_reachable(product, oracle, two_areas):
+    """A settled node whose wrapped distance is exactly all ones is reached:
+    getSpfResult keeps it, its prefix gets a route (metric -1 as i32) and its
+    node label an MPLS route -- on the GPU through the settled bitset of the
+    exact-order SPF, not the all-ones sentinel."""
+    pa, pls, pps = _line_minus_one(product, two_areas)
+    oa, ols, ops = _line_minus_one(oracle, two_areas)
+    x = {k: (v[0], sorted(v[1])) for k, v in pls.getSpfResult("0").items()}
+    y = {k: (v[0], sorted(v[1])) for k, v in ols.getSpfResult("0").items()}
+    assert x == y and x["1"][0] == (1 << 64) - 1
+    a = product.SpfSolver("0", True, True).buildRouteDb("0", pa, pps)
+    b = oracle.SpfSolver("0", True, True).buildRouteDb("0", oa, ops)
+    assert a.canonical() == b.canonical()
+    routes = a.unicastRoutes()
+    assert "fc00::1/128" in routes
+    if not two_areas:
+        s = product.SpfSolver("0", True, True)
+        s.buildRouteDb("0", pa, pps)
+        got = s.createRoutesForPrefixes("0", pa, pps, {"fc00::1/128"})
+        assert got["fc00::1/128"] == routes["fc00::1/128"]

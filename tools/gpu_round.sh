@@ -11,7 +11,7 @@ step() {  # step <name> <timeout> <cmd...>
   echo "=== $name rc=$rc"; tail -4 "gpurun_out/$name.log" | cut -c1-400
   [ $rc -eq 0 ] || exit $rc
 }
-nproc > gpurun_out/host.txt; python3 -c "import os;print(len(os.sched_getaffinity(0)))" >> gpurun_out/host.txt; lscpu | grep "Model name" >> gpurun_out/host.txt
+nproc > gpurun_out/host.txt; python3 -c "import os;print(len(os.sched_getaffinity(0)))" >> gpurun_out/host.txt; cat /sys/fs/cgroup/cpu.max >> gpurun_out/host.txt 2>/dev/null; lscpu | grep "Model name" >> gpurun_out/host.txt
 if [ -z "$NO_TESTS" ]; then
   step pytest_gpu 900 python -u -m pytest tests -m gpu -q -p no:cacheprovider -x --timeout 120 --timeout-method thread
   step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
