@@ -23,7 +23,8 @@
  *     bit  21      DST_OVERLOADED  neighbour is hard-drained: it is settled
  *                  but never relaxes (LinkState.cpp:741-752) unless it is
  *                  the SPF source itself
- *     bits 22..30  rslot index of the reverse edge inside dst's CSR row
+ *     bits 22..30  rslot index of the reverse edge inside dst's CSR row,
+ *                  saturated at 511 (rows of 512+ edges: ogs_graph.rslot_ext)
  *     bit  31      DOWN  link not up (Link::isUp false, LinkState.h:118-121)
  *     bits 32..63  metric (Link::getMaxMetric, LinkState.h:171-174)
  *   Node flags (uint8): OGS_NODE_OVERLOADED (hard drain, no transit,
@@ -56,9 +57,9 @@ extern "C" {
 #define OGS_E_INVALID (-1)     /* bad argument / inconsistent shapes         */
 #define OGS_E_NOMEM (-2)       /* device allocation failed                   */
 #define OGS_E_HIP (-3)         /* HIP runtime error, see ogs_last_error()    */
-#define OGS_E_UNSUPPORTED (-4) /* input the encodings cannot hold: degree  */
-                               /* > 511, > 2^21 nodes per topology, an      */
-                               /* OGS_F_EXACT_ORDER call without u64 dist.  */
+#define OGS_E_UNSUPPORTED (-4) /* input the encodings cannot hold: > 2^21  */
+                               /* nodes per topology, an OGS_F_EXACT_ORDER */
+                               /* call without u64 distances               */
 #define OGS_E_NODEVICE (-5)    /* no HIP device visible                      */
 
 /* ---- packed edge / node encodings -------------------------------------- */
@@ -69,6 +70,9 @@ extern "C" {
 #define OGS_EDGE_RSLOT_MASK 0x1FFu
 #define OGS_EDGE_DOWN (1u << 31)
 #define OGS_MAX_NODES_PER_TOPO (1u << 21)
+/* Rows up to this length fit the 9-bit reverse slot; longer rows need
+ * ogs_graph.rslot_ext. Next-hop sets of sources past 512 links are wider than
+ * 16 words (ogs_nh_words_for_degree). */
 #define OGS_MAX_DEGREE 512
 
 #define OGS_NODE_OVERLOADED 0x01u
@@ -153,6 +157,10 @@ typedef struct ogs_graph {
    * edge: enables the edge-parallel multi-source path for topologies too
    * large for the wave kernel (all-sources batches, C3/C4/C5). */
   const uint32_t* edge_src;
+  /* [E_total] exact reverse slot of every edge (the rslot field saturates at
+   * 511). Required when any row has 512+ edges (max_degree >= 512): the KSP
+   * path keys and link ids read it; optional (NULL) otherwise. */
+  const uint32_t* rslot_ext;
 } ogs_graph;
 
 #define OGS_SLOT_EDGE_DOWN (1u << 9)
@@ -309,7 +317,9 @@ int ogs_host_free(void* hptr);
  *                 from HBM/L2, 1 row offsets in LDS, 2 rows + edges in LDS. */
 int ogs_set_option(const char* name, int64_t value);
 
-/* Smallest supported next-hop bitset width (words) for a source degree. */
+/* Smallest supported next-hop bitset width (words) for a source degree:
+ * 1, 2, 4, 8 or 16 up to 512 links, ceil(degree / 32) past that (those
+ * widths run the HBM-state kernels with a runtime word count). */
 int ogs_nh_words_for_degree(int degree);
 
 /* ---- compute ------------------------------------------------------------ *

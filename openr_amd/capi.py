@@ -33,7 +33,7 @@ class Graph(ctypes.Structure):
                 ("node_flags", ctypes.c_void_p), ("topo_desc", ctypes.c_void_p),
                 ("slot_node", ctypes.c_void_p), ("slot_stride", ctypes.c_int32),
                 ("slot_edges", ctypes.c_void_p), ("slot_degree", ctypes.c_int32),
-                ("edge_src", ctypes.c_void_p)]
+                ("edge_src", ctypes.c_void_p), ("rslot_ext", ctypes.c_void_p)]
 
 
 class PrefixTable(ctypes.Structure):

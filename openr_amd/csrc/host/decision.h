@@ -222,6 +222,9 @@ struct FlatTopology {
   std::vector<uint64_t> edges;                   // [E] packed
   std::vector<uint8_t> nodeFlags;                // [N]
   std::vector<Link*> edgeLink;                   // [E] link of each edge
+  // [E] exact reverse slot of every edge when a row has 512+ edges (the
+  // edge word's 9-bit field saturates at 511; ogs_graph.rslot_ext), else empty
+  std::vector<uint32_t> rslotExt;
   uint64_t maxMetric{0};
   int maxDegree{0};
   bool hasZeroMetric{false};
@@ -231,7 +234,10 @@ struct FlatTopology {
   int slotDegree{0};  // ogs_graph.slot_degree of dSlotEdges (0: none)
   // views into dBlock (one H2D per full upload); patches write in place
   DeviceBuffer dBlock;
-  DeviceBuffer dRow, dEdges, dFlags, dNodeBase, dSlot, dSlotEdges, dEdgeSrc;
+  DeviceBuffer dRow, dEdges, dFlags, dNodeBase, dSlot, dSlotEdges, dEdgeSrc, dRslotExt;
+  const uint32_t* rslotExtDev() const {
+    return rslotExt.empty() ? nullptr : dRslotExt.as<uint32_t>();
+  }
   DeviceBuffer dPatchIdx, dPatchVal;  // ogs_csr_patch staging (§8(f) f3)
 };
 
@@ -480,7 +486,7 @@ class Ksp2Batch {
   size_t nUnits_{0}, nSources_{0};
   uint32_t flags_{0}, maxPaths_{0}, maxEdges_{0};
   ogs_graph g_{};
-  DeviceBuffer dNodeBase_, dRow_, dEdges_, dFlags_;  // multi-topology batch
+  DeviceBuffer dNodeBase_, dRow_, dEdges_, dFlags_, dRslot_;  // multi-topology batch
   DeviceBuffer dSrc_, dUnits_, dCount_[2], dLen_[2], dEdges2_[2];
   std::vector<uint32_t> count_[2], len_[2], edges_[2];
 };

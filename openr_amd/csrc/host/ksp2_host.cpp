@@ -61,6 +61,7 @@ const std::vector<LinkState::Path>& LinkState::getKthPaths(
   g.row_ptr = f.dRow.as<uint32_t>();
   g.edges = f.dEdges.as<uint64_t>();
   g.node_flags = f.dFlags.as<uint8_t>();
+  g.rslot_ext = f.rslotExtDev();  // rows of 512+ edges
   ogs_path_out out{dCount.as<uint32_t>(), dLen.as<uint32_t>(),
                    dEdges.as<uint32_t>(), maxPaths, maxEdges};
   // zero / negative metrics: pathLinks follow the reference's extraction
@@ -177,6 +178,7 @@ void Ksp2Batch::init(const std::string& src,
     g_.row_ptr = fl[0]->dRow.as<uint32_t>();
     g_.edges = fl[0]->dEdges.as<uint64_t>();
     g_.node_flags = fl[0]->dFlags.as<uint8_t>();
+    g_.rslot_ext = fl[0]->rslotExtDev();
     return;
   }
   // concatenated batch: global row offsets, topology-local edge targets
@@ -195,6 +197,21 @@ void Ksp2Batch::init(const std::string& src,
   dRow_.upload(row.data(), row.size());
   dEdges_.upload(edges.data(), edges.size());
   dFlags_.upload(flags.data(), flags.size());
+  if (maxDeg >= OGS_MAX_DEGREE) {  // exact reverse slots, concatenated
+    std::vector<uint32_t> ext;
+    ext.reserve(edges.size());
+    for (const auto* f : fl) {
+      if (!f->rslotExt.empty()) {
+        ext.insert(ext.end(), f->rslotExt.begin(), f->rslotExt.end());
+      } else {
+        for (uint64_t x : f->edges) {
+          ext.push_back((uint32_t(x) >> OGS_EDGE_RSLOT_SHIFT) & OGS_EDGE_RSLOT_MASK);
+        }
+      }
+    }
+    dRslot_.upload(ext.data(), ext.size());
+    g_.rslot_ext = dRslot_.as<uint32_t>();
+  }
   g_.node_base = dNodeBase_.as<uint32_t>();
   g_.row_ptr = dRow_.as<uint32_t>();
   g_.edges = dEdges_.as<uint64_t>();

@@ -222,7 +222,9 @@ void LinkState::patchFlat(const std::string& node, const std::vector<const Link*
   };
   auto reverseOf = [&](uint32_t e) {
     const uint32_t lo = uint32_t(f.edges[e]);
-    return f.rowPtr[lo & OGS_EDGE_DST_MASK] + ((lo >> OGS_EDGE_RSLOT_SHIFT) & OGS_EDGE_RSLOT_MASK);
+    const uint32_t slot = f.rslotExt.empty() ? (lo >> OGS_EDGE_RSLOT_SHIFT) & OGS_EDGE_RSLOT_MASK
+                                             : f.rslotExt[e];
+    return f.rowPtr[lo & OGS_EDGE_DST_MASK] + slot;
   };
   for (uint32_t e = f.rowPtr[u]; e < f.rowPtr[u + 1]; ++e) {
     const bool linkTouched =
@@ -358,8 +360,12 @@ const FlatTopology& LinkState::flat() const {
     f->rowPtr[u + 1] = f->rowPtr[u] + j;
     f->maxDegree = std::max<int>(f->maxDegree, int(j));
   }
-  if (f->maxDegree >= OGS_MAX_DEGREE) throw std::domain_error("degree > 511");
+  // rows of 512+ edges (a hub / route reflector): the edge word's reverse
+  // slot saturates at 511 and the exact slots go to rslotExt (LinkState.cpp:
+  // 760-813 iterates links of any count)
+  const bool extSlots = f->maxDegree >= OGS_MAX_DEGREE;
   const uint32_t E = f->rowPtr[N];
+  if (extSlots) f->rslotExt.assign(E, 0u);
   std::vector<uint32_t> rev(E, 0xFFFFFFFFu);
   std::sort(occ.begin(), occ.end());
   for (size_t i = 0; i + 1 < occ.size(); ++i) {
@@ -375,8 +381,9 @@ const FlatTopology& LinkState::flat() const {
     if (r == 0xFFFFFFFFu) throw std::logic_error("LinkState::flat: link with one endpoint");
     const uint32_t v = owner[r];
     const uint32_t rslot = r - f->rowPtr[v];
+    if (extSlots) f->rslotExt[e] = rslot;
     const LinkStateMetric m = l->getMaxMetric();
-    uint32_t lo = v | (rslot << OGS_EDGE_RSLOT_SHIFT);
+    uint32_t lo = v | (std::min<uint32_t>(rslot, OGS_EDGE_RSLOT_MASK) << OGS_EDGE_RSLOT_SHIFT);
     if (f->nodeFlags[v] & OGS_NODE_OVERLOADED) lo |= OGS_EDGE_DST_OVERLOADED;
     const bool up = l->isUp();
     if (!up) lo |= OGS_EDGE_DOWN;
@@ -419,7 +426,8 @@ const FlatTopology& LinkState::flatOnDevice() const {
                         {m.nodeFlags.data(), m.nodeFlags.size(), &m.dFlags},
                         {esrc.data(), esrc.size() * 4, &m.dEdgeSrc},
                         {slots.data(), slots.size() * 2, &m.dSlot},
-                        {img.data(), img.size() * 4, &m.dSlotEdges}};
+                        {img.data(), img.size() * 4, &m.dSlotEdges},
+                        {m.rslotExt.data(), m.rslotExt.size() * 4, &m.dRslotExt}};
   auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
   size_t total = 0;
   for (const Span& sp : spans) total += al(std::max<size_t>(sp.bytes, 16));

@@ -265,12 +265,12 @@ int ogs_set_option(const char* name, int64_t value) {
 }
 
 int ogs_nh_words_for_degree(int degree) {
-  if (degree < 0 || degree > OGS_MAX_DEGREE) return OGS_E_UNSUPPORTED;
+  if (degree < 0) return OGS_E_INVALID;
   const int words = (degree + 31) / 32;
   for (int w : {1, 2, 4, 8, 16}) {
     if (words <= w) return w;
   }
-  return OGS_E_UNSUPPORTED;
+  return words;  // sources of more than 512 links: exact width
 }
 
 int ogs_spf_routes(const ogs_graph* graph, const ogs_prefix_table* prefixes,
@@ -303,13 +303,10 @@ int ogs_spf_routes(const ogs_graph* graph, const ogs_prefix_table* prefixes,
     return fail(OGS_E_INVALID, "prefix table arrays are NULL");
   }
   if (ogs_nh_words_for_degree(nh_words * 32) != nh_words) {
-    return fail(OGS_E_UNSUPPORTED, "nh_words must be 1, 2, 4, 8 or 16");
+    return fail(OGS_E_UNSUPPORTED, "nh_words must be 1, 2, 4, 8, 16 or > 16");
   }
   if ((flags & OGS_F_EXACT_ORDER) && !(flags & OGS_F_WIDE_METRIC)) {
     return fail(OGS_E_INVALID, "OGS_F_EXACT_ORDER needs OGS_F_WIDE_METRIC");
-  }
-  if ((flags & OGS_F_EXACT_ORDER) && graph->max_degree > OGS_MAX_DEGREE) {
-    return fail(OGS_E_UNSUPPORTED, "OGS_F_EXACT_ORDER: degree > OGS_MAX_DEGREE");
   }
   int unsupported = 0;
   hipError_t e = ogs::launch_spf_routes(
@@ -334,7 +331,7 @@ int ogs_routes_from_spf(const ogs_graph* graph, const ogs_prefix_table* prefixes
     return fail(OGS_E_INVALID, "input arrays are NULL");
   }
   if (ogs_nh_words_for_degree(nh_words * 32) != nh_words) {
-    return fail(OGS_E_UNSUPPORTED, "nh_words must be 1, 2, 4, 8 or 16");
+    return fail(OGS_E_UNSUPPORTED, "nh_words must be 1, 2, 4, 8, 16 or > 16");
   }
   hipError_t e = ogs::launch_routes_from_spf(*graph, *prefixes, units, n_units, spf_dist,
                                             spf_nh, spf_reached, flags, nh_words, *out,
@@ -359,12 +356,15 @@ int ogs_ksp_paths(const ogs_graph* graph, const ogs_path_unit* units,
   if (masks && mask_words < uint32_t((graph->max_edges + 31) / 32)) {
     return fail(OGS_E_INVALID, "mask_words too small for max_edges");
   }
+  if (graph->max_degree >= OGS_MAX_DEGREE && !graph->rslot_ext) {
+    return fail(OGS_E_INVALID, "rows of 512+ edges need graph->rslot_ext");
+  }
   int unsupported = 0;
   hipError_t e = ogs::launch_ksp(*graph, units, n_units, masks, mask_words,
                                  flags, *out, static_cast<hipStream_t>(stream),
                                  &unsupported);
   if (unsupported) {
-    return fail(OGS_E_UNSUPPORTED, "degree > OGS_MAX_DEGREE for the exact-order KSP path");
+    return fail(OGS_E_INVALID, "OGS_F_EXACT_ORDER needs OGS_F_WIDE_METRIC");
   }
   return e == hipSuccess ? OGS_OK : hipFail(e, "ksp launch");
 }
@@ -389,12 +389,15 @@ int ogs_ksp2_paths(const ogs_graph* graph, const ogs_unit* sources,
       uint32_t(graph->max_nodes) > OGS_MAX_NODES_PER_TOPO) {
     return fail(OGS_E_UNSUPPORTED, "max_nodes outside (0, 2^21]");
   }
+  if (graph->max_degree >= OGS_MAX_DEGREE && !graph->rslot_ext) {
+    return fail(OGS_E_INVALID, "rows of 512+ edges need graph->rslot_ext");
+  }
   int unsupported = 0;
   hipError_t e = ogs::launch_ksp2(*graph, sources, n_sources, units, n_units,
                                   flags, *k1, *k2,
                                   static_cast<hipStream_t>(stream), &unsupported);
   if (unsupported) {
-    return fail(OGS_E_UNSUPPORTED, "degree > OGS_MAX_DEGREE for the exact-order KSP path");
+    return fail(OGS_E_INVALID, "OGS_F_EXACT_ORDER needs OGS_F_WIDE_METRIC");
   }
   return e == hipSuccess ? OGS_OK : hipFail(e, "ksp2 launch");
 }
@@ -431,7 +434,7 @@ int ogs_spf_routes_variants(const ogs_graph* graph,
     return fail(OGS_E_UNSUPPORTED, "max_nodes outside (0, 2^21]");
   }
   if (ogs_nh_words_for_degree(nh_words * 32) != nh_words) {
-    return fail(OGS_E_UNSUPPORTED, "nh_words must be 1, 2, 4, 8 or 16");
+    return fail(OGS_E_UNSUPPORTED, "nh_words must be 1, 2, 4, 8, 16 or > 16");
   }
   int unsupported = 0;
   hipError_t e = ogs::launch_variants(*graph, *prefixes, units, n_units, mods, diff,
@@ -507,7 +510,7 @@ int ogs_rib_policy_apply(const ogs_prefix_table* prefixes,
     return fail(OGS_E_INVALID, "a continuation chunk needs applied / counter");
   }
   if (ogs_nh_words_for_degree(nh_words * 32) != nh_words) {
-    return fail(OGS_E_UNSUPPORTED, "nh_words must be 1, 2, 4, 8 or 16");
+    return fail(OGS_E_UNSUPPORTED, "nh_words must be 1, 2, 4, 8, 16 or > 16");
   }
   hipError_t e = ogs::launch_rib_policy(*prefixes, *policy, num_areas, n_units, nh_words,
                                         meta, mask, applied, counter,
@@ -538,7 +541,7 @@ int ogs_routes_multiarea(const ogs_graph* graph,
     return fail(OGS_E_INVALID, "num_areas outside [1, num_topos]");
   }
   if (ogs_nh_words_for_degree(nh_words * 32) != nh_words) {
-    return fail(OGS_E_UNSUPPORTED, "nh_words must be 1, 2, 4, 8 or 16");
+    return fail(OGS_E_UNSUPPORTED, "nh_words must be 1, 2, 4, 8, 16 or > 16");
   }
   hipError_t e = ogs::launch_routes_multiarea(
       *graph, *prefixes, *areas, units, n_units, spf_row, spf_dist, spf_nh,

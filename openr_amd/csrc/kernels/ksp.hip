@@ -26,7 +26,7 @@
 
 namespace ogs {
 
-constexpr uint32_t kExactRowK = OGS_MAX_DEGREE;  // exact-order row staging
+constexpr uint32_t kExactRowK = 512;  // exact-order rows staged in LDS (longer: HBM)
 
 // 8 B per recursion level: the last edge (node -> pred) chosen at this frame
 // is both the path edge once the recursion below it succeeds and the resume
@@ -76,7 +76,7 @@ __device__ uint32_t trace_paths(const UnitCsr& csr, const D* dist, uint32_t s,
       if (!fresh) {
         const uint32_t llo = static_cast<uint32_t>(csr.edg[f.edge]);
         lastU = edge_dst(llo);
-        lastSlot = edge_rslot(llo);
+        lastSlot = csr_rslot(csr, f.edge, llo);
       }
       const D ld = fresh ? D(0) : dist[lastU];
       // the row's edges 8 at a time: the loads of a batch are independent
@@ -102,7 +102,7 @@ __device__ uint32_t trace_paths(const UnitCsr& csr, const D* dist, uint32_t s,
           }
           const D du = dist[u];
           if (du == kInf || du + static_cast<D>(ed >> 32) != dv) continue;
-          const uint32_t slot = edge_rslot(lo);
+          const uint32_t slot = csr_rslot(csr, e, lo);
           if (!fresh && !key_less<D>(ld, lastU, lastSlot, du, u, slot)) continue;
           if (key_less<D>(du, u, slot, bd, bu, bs)) {
             bd = du;
@@ -178,10 +178,11 @@ __device__ uint32_t trace_paths_wave(const UnitCsr& csr, const uint32_t* dist, u
                                      size_t row, uint32_t* pathMask, int lane) {
   constexpr uint32_t kInf = 0xFFFFFFFFu;
   constexpr uint64_t kNone = ~0ull;
-  // packed key: dist | pred << 9 | slot (pred < 2^21, slot < 512): the
-  // lexicographic (dist, pred, slot) order of key_less
-  auto pack = [](uint32_t d, uint32_t u, uint32_t slot) {
-    return (uint64_t(d) << 32) | (uint64_t(u) << 9) | slot;
+  // packed key: dist | reverse edge index (rowp[pred] + slot: rows are
+  // contiguous in pred order, so this is the lexicographic (dist, pred,
+  // slot) order of key_less for rows of any length)
+  auto pack = [&](uint32_t d, uint32_t u, uint32_t slot) {
+    return (uint64_t(d) << 32) | (csr.rowp[u] + slot);
   };
   uint32_t* pathLen = out.path_len + row * out.max_paths;
   uint32_t* pathEdges = out.path_edges + row * out.max_edges;
@@ -200,7 +201,7 @@ __device__ uint32_t trace_paths_wave(const UnitCsr& csr, const uint32_t* dist, u
       uint64_t lastKey = 0;
       if (!fresh) {
         const uint32_t llo = static_cast<uint32_t>(csr.edg[f.edge]);
-        lastKey = pack(dist[edge_dst(llo)], edge_dst(llo), edge_rslot(llo));
+        lastKey = pack(dist[edge_dst(llo)], edge_dst(llo), csr_rslot(csr, f.edge, llo));
       }
       uint64_t best = kNone;
       uint32_t be = 0xFFFFFFFFu;
@@ -222,7 +223,7 @@ __device__ uint32_t trace_paths_wave(const UnitCsr& csr, const uint32_t* dist, u
           if (ok) {
             const uint32_t du = dist[u];
             if (du != kInf && du + static_cast<uint32_t>(ed >> 32) == dv) {
-              const uint64_t k = pack(du, u, edge_rslot(lo));
+              const uint64_t k = pack(du, u, csr_rslot(csr, e, lo));
               if (fresh || k > lastKey) key = k;
             }
           }
@@ -316,9 +317,9 @@ __global__ __launch_bounds__(kBlock) void ksp_kernel(
     uint64_t* ledg = reinterpret_cast<uint64_t*>(base + off);
     for (uint32_t i = lane; i <= N; i += UT) lrow[i] = gRow[i] - e0;
     for (uint32_t i = lane; i < E; i += UT) ledg[i] = g.edges[e0 + i];
-    csr = UnitCsr{lrow, ledg, 0u};
+    csr = UnitCsr{lrow, ledg, 0u, g.rslot_ext ? g.rslot_ext + e0 : nullptr};
   } else {
-    csr = UnitCsr{gRow, g.edges, e0};
+    csr = UnitCsr{gRow, g.edges, e0, g.rslot_ext ? g.rslot_ext + e0 : nullptr};
   }
   for (uint32_t i = lane; i < (E + 31) / 32; i += UT) visited[i] = 0u;
   const uint32_t* ignore =
@@ -577,7 +578,7 @@ __device__ void exact_dist_hbm(uint32_t N, uint32_t s, const UnitCsr& c,
 }
 
 // The greedy trace (trace_paths_wave) over HBM state with a two-word key:
-// fixpoint (dist(u), u << 9 | slot), exact (rank(u), slot).
+// fixpoint (dist(u), rowp[u] + slot), exact (rank(u), slot).
 template <typename D, bool EXACT, bool MASKED>
 __device__ uint32_t trace_paths_hbm(const UnitCsr& csr, const D* dist, const uint32_t* rank,
                                     uint32_t s, uint32_t t, uint32_t* visited, Frame* stack,
@@ -595,7 +596,7 @@ __device__ uint32_t trace_paths_hbm(const UnitCsr& csr, const D* dist, const uin
       lo = slot;
     } else {
       hi = static_cast<uint64_t>(ld_l2(dist + u));
-      lo = (u << 9) | slot;
+      lo = csr.rowp[u] + slot;  // (u, slot) order for rows of any length
     }
   };
   uint32_t* pathLen = out.path_len + row * out.max_paths;
@@ -617,7 +618,7 @@ __device__ uint32_t trace_paths_hbm(const UnitCsr& csr, const D* dist, const uin
       uint32_t lastLo = 0;
       if (!fresh) {
         const uint32_t llo = static_cast<uint32_t>(csr.edg[f.edge]);
-        keyOf(edge_dst(llo), edge_rslot(llo), lastHi, lastLo);
+        keyOf(edge_dst(llo), csr_rslot(csr, f.edge, llo), lastHi, lastLo);
       }
       uint64_t bHi = kNoneHi;
       uint32_t bLo = kNoneLo, be = 0xFFFFFFFFu;
@@ -648,7 +649,7 @@ __device__ uint32_t trace_paths_hbm(const UnitCsr& csr, const D* dist, const uin
             if (tight) {
               uint64_t h;
               uint32_t l;
-              keyOf(u, edge_rslot(lo), h, l);
+              keyOf(u, csr_rslot(csr, e, lo), h, l);
               if (fresh || less(lastHi, lastLo, h, l)) {
                 kh = h;
                 kl = l;
@@ -723,8 +724,10 @@ __device__ uint32_t trace_paths_hbm(const UnitCsr& csr, const D* dist, const uin
 // Per-unit HBM scratch: dist | stamp or rank | list 0 (open list) | list 1 |
 // visited | mask | stack, each 256-B aligned.
 struct KspHbmLayout {
-  size_t dist, aux, q0, q1, visited, mask, stack, total;
-  __host__ __device__ static KspHbmLayout make(uint64_t N, uint64_t E, uint64_t dsize) {
+  size_t dist, aux, q0, q1, visited, mask, stack, rowT, rowC, rowV, total;
+  // rowDeg: rows staged in HBM for the exact replay (rows past kExactRowK)
+  __host__ __device__ static KspHbmLayout make(uint64_t N, uint64_t E, uint64_t dsize,
+                                               uint64_t rowDeg = 0) {
     auto r = [](uint64_t x) { return (x + 255) & ~uint64_t(255); };
     const uint64_t lw = (E + 31) / 32 + 1;
     KspHbmLayout L;
@@ -743,6 +746,12 @@ struct KspHbmLayout {
     o += r(lw * 4);
     L.stack = o;
     o += r(N * sizeof(Frame));
+    L.rowT = o;
+    o += r(rowDeg * 4);
+    L.rowC = o;
+    o += r(rowDeg * 8);
+    L.rowV = o;
+    o += r(rowDeg);
     L.total = o;
     return L;
   }
@@ -778,9 +787,11 @@ __global__ __launch_bounds__(EXACT ? 64 : kKspHbmBlock) void ksp_hbm_kernel(
   const uint32_t e0 = gRow[0];
   const uint32_t E = gRow[N] - e0;
   const uint8_t* __restrict__ nflags = g.node_flags + nb;
-  const UnitCsr csr{gRow, g.edges, e0};
+  const UnitCsr csr{gRow, g.edges, e0, g.rslot_ext ? g.rslot_ext + e0 : nullptr};
   const uint32_t s = unit.src, t = unit.dest;
-  const KspHbmLayout L = KspHbmLayout::make(uint32_t(g.max_nodes), uint32_t(g.max_edges), sizeof(D));
+  const bool hbmRows = EXACT && uint32_t(g.max_degree) > kExactRowK;
+  const KspHbmLayout L = KspHbmLayout::make(uint32_t(g.max_nodes), uint32_t(g.max_edges),
+                                            sizeof(D), hbmRows ? uint32_t(g.max_degree) : 0u);
   char* base = scratch + size_t(blockIdx.x) * L.total;
   D* dist = reinterpret_cast<D*>(base + L.dist);
   uint32_t* aux = reinterpret_cast<uint32_t*>(base + L.aux);
@@ -804,8 +815,11 @@ __global__ __launch_bounds__(EXACT ? 64 : kKspHbmBlock) void ksp_hbm_kernel(
   auto spf = [&](const uint32_t* ignore, auto maskedTag) {
     constexpr bool M = decltype(maskedTag)::value;
     if constexpr (EXACT) {
-      exact_dist_hbm<M>(N, s, csr, nflags, reinterpret_cast<uint64_t*>(dist), aux, q0,
-                        ignore, rowT, rowC, rowV, lane);
+      // rows of 512+ edges are staged in the unit's HBM scratch
+      exact_dist_hbm<M>(N, s, csr, nflags, reinterpret_cast<uint64_t*>(dist), aux, q0, ignore,
+                        hbmRows ? reinterpret_cast<uint32_t*>(base + L.rowT) : rowT,
+                        hbmRows ? reinterpret_cast<uint64_t*>(base + L.rowC) : rowC,
+                        hbmRows ? reinterpret_cast<uint8_t*>(base + L.rowV) : rowV, lane);
     } else {
       frontier_dist_hbm<D, M>(N, s, csr, nflags, dist, aux, q0, q1, qcnt, ignore);
     }
@@ -847,8 +861,10 @@ hipError_t launch_ksp_hbm(const ogs_graph& g, const ogs_unit* sources, int nSour
                           uint32_t maskWords, const ogs_path_out& o1, const ogs_path_out& o2,
                           hipStream_t stream) {
   constexpr size_t kKspHbmScratch = size_t(4) << 30;
+  const bool hbmRows = EXACT && uint32_t(g.max_degree) > kExactRowK;
   const size_t per = KspHbmLayout::make(uint32_t(g.max_nodes), uint32_t(g.max_edges),
-                                        sizeof(D)).total;
+                                        sizeof(D), hbmRows ? uint32_t(g.max_degree) : 0u)
+                         .total;
   size_t chunk = kKspHbmScratch / per;
   if (chunk < 1) chunk = 1;
   if (chunk > size_t(nUnits)) chunk = size_t(nUnits);
@@ -905,7 +921,7 @@ hipError_t launch_ksp(const ogs_graph& g, const ogs_path_unit* units,
                       hipStream_t stream, int* unsupported) {
   const bool wide = flags & OGS_F_WIDE_METRIC;
   if (flags & OGS_F_EXACT_ORDER) {
-    if (!wide || g.max_degree > int(kExactRowK)) {
+    if (!wide) {
       *unsupported = 1;
       return hipSuccess;
     }
@@ -1064,12 +1080,12 @@ __device__ KspLds<D> ksp_lds(char* base, const ogs_graph& g, uint32_t topo,
     if constexpr (STAGE >= 2) {
       uint64_t* ledg = reinterpret_cast<uint64_t*>(base + off);
       for (uint32_t i = lane; i < E; i += UT) ledg[i] = g.edges[e0 + i];
-      l.csr = UnitCsr{lrow, ledg, 0u};
+      l.csr = UnitCsr{lrow, ledg, 0u, g.rslot_ext ? g.rslot_ext + e0 : nullptr};
     } else {
-      l.csr = UnitCsr{lrow, g.edges + e0, 0u};
+      l.csr = UnitCsr{lrow, g.edges + e0, 0u, g.rslot_ext ? g.rslot_ext + e0 : nullptr};
     }
   } else {
-    l.csr = UnitCsr{gRow, g.edges, e0};
+    l.csr = UnitCsr{gRow, g.edges, e0, g.rslot_ext ? g.rslot_ext + e0 : nullptr};
   }
   for (uint32_t i = lane; i < l.linkWords; i += UT) {
     l.visited[i] = 0u;
@@ -1278,7 +1294,7 @@ hipError_t launch_ksp2(const ogs_graph& g, const ogs_unit* sources,
                        const ogs_path_out& o2, hipStream_t stream,
                        int* unsupported) {
   if (flags & OGS_F_EXACT_ORDER) {
-    if (!(flags & OGS_F_WIDE_METRIC) || g.max_degree > int(kExactRowK)) {
+    if (!(flags & OGS_F_WIDE_METRIC)) {
       *unsupported = 1;
       return hipSuccess;
     }

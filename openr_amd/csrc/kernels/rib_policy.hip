@@ -22,11 +22,13 @@
 
 namespace ogs {
 
+// W == 0: next-hop masks of runtime width Wr (sources of 512+ links)
 template <int W>
 __global__ __launch_bounds__(kBlock) void rib_policy_kernel(
     ogs_prefix_table pt, ogs_rib_policy pol, uint32_t A,
     const uint32_t* __restrict__ meta, uint32_t* __restrict__ mask,
-    uint16_t* __restrict__ applied, uint16_t* __restrict__ counter) {
+    uint16_t* __restrict__ applied, uint16_t* __restrict__ counter, int Wr) {
+  const int WW = W > 0 ? W : Wr;
   const uint32_t u = blockIdx.y;
   const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
   const uint32_t p0 = pt.pfx_base[0];
@@ -47,24 +49,24 @@ __global__ __launch_bounds__(kBlock) void rib_policy_kernel(
     const uint32_t gp = p0 + p;
     const uint32_t best = pt.adv_off[gp] + (m >> OGS_ROUTE_BEST_SHIFT);
     uint32_t cand = pol.pfx_match[gp] & pol.adv_tag_match[best] & pol.active;
-    const uint32_t* nz = pol.slot_nonzero + size_t(u) * K * A * W;
+    const uint32_t* nz = pol.slot_nonzero + size_t(u) * K * A * WW;
     for (; cand; cand &= cand - 1) {
       const uint32_t k = __builtin_ctz(cand);
       cnt = base + k;  // counterID set by every matching statement
       bool any = false;
       for (uint32_t a = 0; a < A; ++a) {
 #pragma unroll
-        for (int w = 0; w < W; ++w) {
-          any |= (mask[((size_t(u) * A + a) * W + w) * Sp + p] &
-                  nz[(size_t(k) * A + a) * W + w]) != 0u;
+        for (int w = 0; w < WW; ++w) {
+          any |= (mask[((size_t(u) * A + a) * WW + w) * Sp + p] &
+                  nz[(size_t(k) * A + a) * WW + w]) != 0u;
         }
       }
       if (!any) continue;  // every next hop weighted 0: route unchanged
       app = base + k;
       for (uint32_t a = 0; a < A; ++a) {
 #pragma unroll
-        for (int w = 0; w < W; ++w) {
-          mask[((size_t(u) * A + a) * W + w) * Sp + p] &= nz[(size_t(k) * A + a) * W + w];
+        for (int w = 0; w < WW; ++w) {
+          mask[((size_t(u) * A + a) * WW + w) * Sp + p] &= nz[(size_t(k) * A + a) * WW + w];
         }
       }
       break;
@@ -81,11 +83,12 @@ hipError_t launch_rib_policy(const ogs_prefix_table& pt, const ogs_rib_policy& p
   if (pt.max_prefixes <= 0) return hipSuccess;
   const dim3 grid(unsigned((pt.max_prefixes + kBlock - 1) / kBlock), unsigned(nUnits));
   switch (W) {
-    case 1: hipLaunchKernelGGL(rib_policy_kernel<1>, grid, dim3(kBlock), 0, stream, pt, pol, uint32_t(A), meta, mask, applied, counter); break;
-    case 2: hipLaunchKernelGGL(rib_policy_kernel<2>, grid, dim3(kBlock), 0, stream, pt, pol, uint32_t(A), meta, mask, applied, counter); break;
-    case 4: hipLaunchKernelGGL(rib_policy_kernel<4>, grid, dim3(kBlock), 0, stream, pt, pol, uint32_t(A), meta, mask, applied, counter); break;
-    case 8: hipLaunchKernelGGL(rib_policy_kernel<8>, grid, dim3(kBlock), 0, stream, pt, pol, uint32_t(A), meta, mask, applied, counter); break;
-    default: hipLaunchKernelGGL(rib_policy_kernel<16>, grid, dim3(kBlock), 0, stream, pt, pol, uint32_t(A), meta, mask, applied, counter); break;
+    case 1: hipLaunchKernelGGL(rib_policy_kernel<1>, grid, dim3(kBlock), 0, stream, pt, pol, uint32_t(A), meta, mask, applied, counter, 0); break;
+    case 2: hipLaunchKernelGGL(rib_policy_kernel<2>, grid, dim3(kBlock), 0, stream, pt, pol, uint32_t(A), meta, mask, applied, counter, 0); break;
+    case 4: hipLaunchKernelGGL(rib_policy_kernel<4>, grid, dim3(kBlock), 0, stream, pt, pol, uint32_t(A), meta, mask, applied, counter, 0); break;
+    case 8: hipLaunchKernelGGL(rib_policy_kernel<8>, grid, dim3(kBlock), 0, stream, pt, pol, uint32_t(A), meta, mask, applied, counter, 0); break;
+    case 16: hipLaunchKernelGGL(rib_policy_kernel<16>, grid, dim3(kBlock), 0, stream, pt, pol, uint32_t(A), meta, mask, applied, counter, 0); break;
+    default: hipLaunchKernelGGL(rib_policy_kernel<0>, grid, dim3(kBlock), 0, stream, pt, pol, uint32_t(A), meta, mask, applied, counter, W); break;
   }
   return hipGetLastError();
 }

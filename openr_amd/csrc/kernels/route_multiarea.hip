@@ -38,8 +38,10 @@ __global__ __launch_bounds__(kBlock) void route_multiarea_kernel(
     ogs_graph g, ogs_prefix_table pt, ogs_area_table at,
     const uint32_t* __restrict__ units, const uint32_t* __restrict__ spfRow,
     const D* __restrict__ sDist, const uint32_t* __restrict__ sNh,
-    uint32_t flags, ogs_spf_out out) {
+    uint32_t flags, ogs_spf_out out, int Wr) {
   constexpr D kInf = DistInf<D>::value;
+  // W == 0: next-hop sets of runtime width Wr (sources of 512+ links)
+  const int WW = W > 0 ? W : Wr;
   const uint32_t u = blockIdx.y;
   const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
   const uint32_t p0 = pt.pfx_base[0];
@@ -78,7 +80,7 @@ __global__ __launch_bounds__(kBlock) void route_multiarea_kernel(
     const uint32_t r = row[b];
     const uint32_t v = at.name_local[size_t(name) * A + b];
     if (name == S || r == OGS_NODE_NONE || v == OGS_NODE_NONE) return 0u;
-    return sNh[(size_t(r) * W + w) * Sn + v];
+    return sNh[(size_t(r) * WW + w) * Sn + v];
   };
   // node flags of an entry in its own area (no adjacency DB: none set)
   auto flagsOf = [&](uint32_t a) -> uint8_t {
@@ -98,8 +100,7 @@ __global__ __launch_bounds__(kBlock) void route_multiarea_kernel(
   auto clearMasks = [&]() {
     if (!out.mask) return;
     for (uint32_t b = 0; b < A; ++b) {
-#pragma unroll
-      for (int w = 0; w < W; ++w) out.mask[((size_t(u) * A + b) * W + w) * Sp + p] = 0u;
+      for (int w = 0; w < WW; ++w) out.mask[((size_t(u) * A + b) * WW + w) * Sp + p] = 0u;
     }
   };
 
@@ -211,22 +212,39 @@ __global__ __launch_bounds__(kBlock) void route_multiarea_kernel(
     if (sb < shortest) shortest = sb;
   }
   for (uint32_t b = 0; b < A; ++b) {
-    uint32_t m[W];
+    const bool use = holds(b) && areaShortest(b) == shortest;
+    if constexpr (W > 0) {
+      uint32_t m[W > 0 ? W : 1];
 #pragma unroll
-    for (int w = 0; w < W; ++w) m[w] = 0u;
-    if (holds(b) && areaShortest(b) == shortest) {
-      for (uint32_t a = a0; a < a1; ++a) {
-        if (!selected(a)) continue;
-        const uint32_t name = at.adv_name[a];
-        if (!reachOf(b, name) || distOf(b, name) != shortest) continue;
+      for (int w = 0; w < W; ++w) m[w] = 0u;
+      if (use) {
+        for (uint32_t a = a0; a < a1; ++a) {
+          if (!selected(a)) continue;
+          const uint32_t name = at.adv_name[a];
+          if (!reachOf(b, name) || distOf(b, name) != shortest) continue;
 #pragma unroll
-        for (int w = 0; w < W; ++w) m[w] |= nhOf(b, name, w);
+          for (int w = 0; w < W; ++w) m[w] |= nhOf(b, name, w);
+        }
       }
-    }
 #pragma unroll
-    for (int w = 0; w < W; ++w) {
-      cnt += __popc(m[w]);
-      if (out.mask) out.mask[((size_t(u) * A + b) * W + w) * Sp + p] = m[w];
+      for (int w = 0; w < W; ++w) {
+        cnt += __popc(m[w]);
+        if (out.mask) out.mask[((size_t(u) * A + b) * W + w) * Sp + p] = m[w];
+      }
+    } else {  // one word at a time
+      for (int w = 0; w < WW; ++w) {
+        uint32_t m = 0u;
+        if (use) {
+          for (uint32_t a = a0; a < a1; ++a) {
+            if (!selected(a)) continue;
+            const uint32_t name = at.adv_name[a];
+            if (!reachOf(b, name) || distOf(b, name) != shortest) continue;
+            m |= nhOf(b, name, w);
+          }
+        }
+        cnt += __popc(m);
+        if (out.mask) out.mask[((size_t(u) * A + b) * WW + w) * Sp + p] = m;
+      }
     }
   }
   // minimum next-hop threshold over the selected entries (496-509, 612)
@@ -257,16 +275,16 @@ hipError_t launch_ma(const ogs_graph& g, const ogs_prefix_table& pt,
                      const ogs_area_table& at, const uint32_t* units, int n,
                      const uint32_t* spfRow, const void* dist,
                      const uint32_t* nh, uint32_t flags, const ogs_spf_out& out,
-                     hipStream_t stream) {
+                     hipStream_t stream, int Wr = 0) {
   const unsigned bx = unsigned((pt.max_prefixes + kBlock - 1) / kBlock);
   if (flags & OGS_F_WIDE_METRIC) {
     hipLaunchKernelGGL((route_multiarea_kernel<uint64_t, W>), dim3(bx, unsigned(n)),
                        dim3(kBlock), 0, stream, g, pt, at, units, spfRow,
-                       static_cast<const uint64_t*>(dist), nh, flags, out);
+                       static_cast<const uint64_t*>(dist), nh, flags, out, Wr);
   } else {
     hipLaunchKernelGGL((route_multiarea_kernel<uint32_t, W>), dim3(bx, unsigned(n)),
                        dim3(kBlock), 0, stream, g, pt, at, units, spfRow,
-                       static_cast<const uint32_t*>(dist), nh, flags, out);
+                       static_cast<const uint32_t*>(dist), nh, flags, out, Wr);
   }
   return hipGetLastError();
 }
@@ -283,7 +301,8 @@ hipError_t launch_routes_multiarea(const ogs_graph& g, const ogs_prefix_table& p
     case 2: return launch_ma<2>(g, pt, at, units, n, spfRow, dist, nh, flags, out, stream);
     case 4: return launch_ma<4>(g, pt, at, units, n, spfRow, dist, nh, flags, out, stream);
     case 8: return launch_ma<8>(g, pt, at, units, n, spfRow, dist, nh, flags, out, stream);
-    default: return launch_ma<16>(g, pt, at, units, n, spfRow, dist, nh, flags, out, stream);
+    case 16: return launch_ma<16>(g, pt, at, units, n, spfRow, dist, nh, flags, out, stream);
+    default: return launch_ma<0>(g, pt, at, units, n, spfRow, dist, nh, flags, out, stream, W);
   }
 }
 

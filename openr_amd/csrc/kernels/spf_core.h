@@ -63,13 +63,22 @@ struct UnitCsr {
   const uint32_t* rowp;
   const uint64_t* edg;
   uint32_t eBase;
+  // exact reverse slots by topology-local edge id where the 9-bit field
+  // saturates (rows of 511+ edges, ogs_graph.rslot_ext), or nullptr
+  const uint32_t* rext;
 };
+
+// Index of edge e's reverse inside its neighbour's row (any row length).
+__device__ __forceinline__ uint32_t csr_rslot(const UnitCsr& c, uint32_t e, uint32_t lo) {
+  const uint32_t r = edge_rslot(lo);
+  return (r == OGS_EDGE_RSLOT_MASK && c.rext) ? c.rext[e - c.eBase] : r;
+}
 
 // Topology-local id of the link behind directed edge e (v -> u): the smaller
 // of the two directed edge ids. Used to test linksToIgnore masks.
 __device__ __forceinline__ uint32_t link_id(const UnitCsr& c, uint32_t e,
                                             uint32_t lo) {
-  const uint32_t rev = c.rowp[edge_dst(lo)] + edge_rslot(lo);
+  const uint32_t rev = c.rowp[edge_dst(lo)] + csr_rslot(c, e, lo);
   return (e < rev ? e : rev) - c.eBase;
 }
 

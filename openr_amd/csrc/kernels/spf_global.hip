@@ -247,6 +247,161 @@ __global__ __launch_bounds__(kGBlock) void spf_global_kernel(
   }
 }
 
+// ---- next-hop sets of any width (sources of more than 512 links): the
+// all-HBM form with a runtime word count; rslot is never read (push-style
+// relaxation, link slots from the source's own row) ---------------------
+template <typename D>
+__global__ __launch_bounds__(kGBlock) void spf_global_wide_kernel(
+    ogs_graph g, const ogs_unit* __restrict__ units, uint32_t flags, int W,
+    D* __restrict__ oDist, uint32_t* __restrict__ oNh, uint32_t* __restrict__ scratch) {
+  constexpr D kInf = DistInf<D>::value;
+  const int tid = threadIdx.x;
+  const uint32_t u0 = blockIdx.x;
+  const ogs_unit unit = units[u0];
+  const uint32_t s = unit.src;
+  const uint32_t nb = g.node_base[unit.topo];
+  const uint32_t N = g.node_base[unit.topo + 1] - nb;
+  const size_t Sn = size_t(g.max_nodes);
+  const uint32_t* __restrict__ gRow = g.row_ptr + nb;
+  const uint32_t e0 = gRow[0];
+  const uint64_t* __restrict__ edges = g.edges + e0;
+  const uint8_t* __restrict__ nflags = g.node_flags + nb;
+  const bool hop = (flags & OGS_F_HOP_METRIC) != 0;
+  D* dist = oDist + u0 * Sn;
+  uint32_t* nh = oNh + u0 * size_t(W) * Sn;
+  uint32_t* stamp = scratch + u0 * 3 * Sn;
+  uint32_t* q0 = stamp + Sn;
+  uint32_t* q1 = q0 + Sn;
+  __shared__ uint32_t qcnt[3];
+
+  for (uint32_t v = tid; v < N; v += kGBlock) {
+    dist[v] = (v == s) ? D(0) : kInf;
+    stamp[v] = 0u;
+    for (int w = 0; w < W; ++w) nh[w * Sn + v] = 0u;
+  }
+  if (tid == 0) {
+    q1[0] = s;
+    qcnt[0] = 0u;
+    qcnt[1] = 1u;
+    qcnt[2] = 0u;
+  }
+  round_sync<true>();
+  auto push = [&](uint32_t t, uint32_t r) {
+    const uint32_t at = atomicAdd(&qcnt[(r + 1) % 3], 1u);
+    ((r + 1) & 1 ? q1 : q0)[at] = t;
+  };
+  auto append = [&](uint32_t t, uint32_t r) {
+    if (atomicMax(&stamp[t], r + 1) < r + 1) push(t, r);
+  };
+  auto weight = [&](uint64_t x) -> D {
+    return hop ? D(1) : D(static_cast<uint32_t>(x >> 32));
+  };
+  // ---- dist phase ----------------------------------------------------------
+  uint32_t r = 1, n = 1;
+  for (; n; ++r) {
+    if (tid == 0) qcnt[(r + 2) % 3] = 0u;
+    const uint32_t* cur = (r & 1) ? q1 : q0;
+    for (uint32_t i = tid; i < n; i += kGBlock) {
+      const uint32_t v = ld_state<true>(cur + i);
+      if (v != s && (nflags[v] & OGS_NODE_OVERLOADED)) continue;  // 741-752
+      const D dv = ld_state<true>(dist + v);
+      const uint32_t b = gRow[v] - e0, m = gRow[v + 1] - e0 - b;
+      for (uint32_t j = 0; j < m; ++j) {
+        const uint64_t x = edges[b + j];
+        const uint32_t lo = static_cast<uint32_t>(x);
+        if (lo & OGS_EDGE_DOWN) continue;
+        const uint32_t t = edge_dst(lo);
+        const D c = dv + weight(x);
+        if (c < ld_state<true>(dist + t) && c < atomic_min_d(&dist[t], c)) append(t, r);
+      }
+    }
+    round_sync<true>();
+    n = qcnt[(r + 1) % 3];
+    __syncthreads();
+  }
+  // ---- next-hop phase ------------------------------------------------------
+  const uint32_t r0 = r;
+  if (tid == 0) qcnt[0] = qcnt[1] = qcnt[2] = 0u;
+  round_sync<true>();
+  {
+    const uint32_t b = gRow[s] - e0, m = gRow[s + 1] - e0 - b;
+    for (uint32_t j = tid; j < m && j < 32u * uint32_t(W); j += kGBlock) {
+      const uint64_t x = edges[b + j];
+      const uint32_t lo = static_cast<uint32_t>(x);
+      if (lo & OGS_EDGE_DOWN) continue;
+      const uint32_t t = edge_dst(lo);
+      if (weight(x) == ld_state<true>(dist + t)) {
+        atomicOr(&nh[(j >> 5) * Sn + t], 1u << (j & 31u));
+        append(t, r0);
+      }
+    }
+  }
+  round_sync<true>();
+  n = qcnt[(r0 + 1) % 3];
+  __syncthreads();
+  for (r = r0 + 1; n; ++r) {
+    if (tid == 0) qcnt[(r + 2) % 3] = 0u;
+    const uint32_t* cur = (r & 1) ? q1 : q0;
+    for (uint32_t i = tid; i < n; i += kGBlock) {
+      const uint32_t v = ld_state<true>(cur + i);
+      if (v == s || (nflags[v] & OGS_NODE_OVERLOADED)) continue;
+      const D dv = ld_state<true>(dist + v);
+      const uint32_t b = gRow[v] - e0, m = gRow[v + 1] - e0 - b;
+      for (uint32_t j = 0; j < m; ++j) {
+        const uint64_t x = edges[b + j];
+        const uint32_t lo = static_cast<uint32_t>(x);
+        if (lo & OGS_EDGE_DOWN) continue;
+        const uint32_t t = edge_dst(lo);
+        if (dv + weight(x) != ld_state<true>(dist + t)) continue;  // not tight
+        bool add = false;
+        for (int w = 0; w < W; ++w) {
+          const uint32_t a = ld_state<true>(nh + w * Sn + v) & ~ld_state<true>(nh + w * Sn + t);
+          if (a && (a & ~atomicOr(&nh[w * Sn + t], a))) add = true;
+        }
+        if (add) append(t, r);
+      }
+    }
+    round_sync<true>();
+    n = qcnt[(r + 1) % 3];
+    __syncthreads();
+  }
+}
+
+// SPF (+ RouteDb) with next-hop sets wider than 16 words.
+hipError_t workspace(size_t bytes, hipStream_t stream, void** out);
+
+template <typename D>
+hipError_t launch_global_wide(const ogs_graph& g, const ogs_prefix_table* pt,
+                              const ogs_unit* units, int nUnits, uint32_t flags, int W,
+                              const ogs_spf_out& out, hipStream_t stream) {
+  const size_t Sn = size_t(g.max_nodes), U = size_t(nUnits);
+  auto r256 = [](size_t x) { return (x + 255) & ~size_t(255); };
+  const size_t distBytes = out.dist ? 0 : r256(U * Sn * sizeof(D));
+  const size_t nhBytes = out.nh ? 0 : r256(U * W * Sn * 4);
+  const size_t scratchBytes = r256(U * 3 * Sn * 4);
+  void* ws = nullptr;
+  hipError_t e = workspace(distBytes + nhBytes + scratchBytes, stream, &ws);
+  if (e != hipSuccess) return e;
+  char* base = static_cast<char*>(ws);
+  D* dist = out.dist ? static_cast<D*>(out.dist) : reinterpret_cast<D*>(base);
+  uint32_t* nh = out.nh ? out.nh : reinterpret_cast<uint32_t*>(base + distBytes);
+  uint32_t* scratch = reinterpret_cast<uint32_t*>(base + distBytes + nhBytes);
+  hipLaunchKernelGGL((spf_global_wide_kernel<D>), dim3(nUnits), dim3(kGBlock), 0, stream, g,
+                     units, flags, W, dist, nh, scratch);
+  e = hipGetLastError();
+  if (e != hipSuccess || !pt || pt->max_prefixes == 0) return e;
+  return launch_route_global_wide<D>(g, *pt, units, nUnits, flags, W, dist, nh, out, stream);
+}
+
+hipError_t launch_spf_routes_global_wide(const ogs_graph& g, const ogs_prefix_table* pt,
+                                         const ogs_unit* units, int nUnits, uint32_t flags,
+                                         int W, const ogs_spf_out& out, hipStream_t stream) {
+  if (flags & OGS_F_WIDE_METRIC) {
+    return launch_global_wide<uint64_t>(g, pt, units, nUnits, flags, W, out, stream);
+  }
+  return launch_global_wide<uint32_t>(g, pt, units, nUnits, flags, W, out, stream);
+}
+
 // ---- dist in LDS (units whose distances fit: N * sizeof(D) + two list
 // bitsets <= 160 kB, e.g. 20k nodes at u32) ----------------------------------
 // The same rounds with the unit's distances in LDS: a dist round's chain is
@@ -658,7 +813,10 @@ __global__ __launch_bounds__(kGBlock) void spf_global_lds3_kernel(
           const uint32_t t = edge_dst(lo);
           const uint32_t c = dv + (hop ? 1u : static_cast<uint32_t>(x[k] >> 32));
           // the source contributes its link slot, every other node NH(v)
-          const uint32_t bits = (v == s) ? (1u << (b + j0 + k - sb)) : nv;
+          // (a source slot past bit 31 is not in a one-word set: dropped, as
+          // the two-phase forms drop slots >= 32 W)
+          const uint32_t slot = b + j0 + k - sb;
+          const uint32_t bits = (v == s) ? (slot < 32u ? 1u << slot : 0u) : nv;
           uint64_t old = dn[t];
           bool changed = false;
           for (;;) {
@@ -841,7 +999,14 @@ hipError_t launch_routes_from_spf(const ogs_graph& g, const ogs_prefix_table& pt
     case 2: OGS_RFS(2)
     case 4: OGS_RFS(4)
     case 8: OGS_RFS(8)
-    default: OGS_RFS(16)
+    case 16: OGS_RFS(16)
+    default:  // sources of more than 512 links
+      return wide ? launch_route_global_wide<uint64_t>(g, pt, units, n, flags, W,
+                                                       static_cast<const uint64_t*>(dist), nh,
+                                                       out, stream, reach)
+                  : launch_route_global_wide<uint32_t>(g, pt, units, n, flags, W,
+                                                       static_cast<const uint32_t*>(dist), nh,
+                                                       out, stream, reach);
   }
 #undef OGS_RFS
 }

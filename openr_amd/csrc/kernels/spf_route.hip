@@ -74,9 +74,9 @@ __global__ __launch_bounds__(kBlock) void spf_route_kernel(
     const uint32_t E = gRow[N] - e0;
     for (uint32_t i = lane; i <= N; i += UT) lrow[i] = gRow[i] - e0;
     for (uint32_t i = lane; i < E; i += UT) ledg[i] = g.edges[e0 + i];
-    csr = UnitCsr{lrow, ledg, 0u};
+    csr = UnitCsr{lrow, ledg, 0u, nullptr};
   } else {
-    csr = UnitCsr{gRow, g.edges, gRow[0]};
+    csr = UnitCsr{gRow, g.edges, gRow[0], nullptr};
   }
   // staging writes are ordered before the first reads by the init sync
   spf_fixpoint<D, W, UT, true, false>(N, s, lane, csr,
@@ -230,6 +230,9 @@ hipError_t launch_spf_routes_exact(const ogs_graph& g, const ogs_prefix_table* p
 hipError_t launch_spf_routes_global(const ogs_graph& g, const ogs_prefix_table* pt,
                                     const ogs_unit* units, int nUnits, uint32_t flags,
                                     int W, const ogs_spf_out& out, hipStream_t stream);
+hipError_t launch_spf_routes_global_wide(const ogs_graph& g, const ogs_prefix_table* pt,
+                                         const ogs_unit* units, int nUnits, uint32_t flags,
+                                         int W, const ogs_spf_out& out, hipStream_t stream);
 
 hipError_t launch_spf_routes(const ogs_graph& g, const ogs_prefix_table* pt,
                              const ogs_unit* units, int nUnits,
@@ -238,6 +241,11 @@ hipError_t launch_spf_routes(const ogs_graph& g, const ogs_prefix_table* pt,
   // zero / negative metrics: the reference's extraction order, replayed
   if (flags & OGS_F_EXACT_ORDER) {
     return launch_spf_routes_exact(g, pt, units, nUnits, flags, W, out, stream);
+  }
+  // sources of more than 512 links: next-hop sets past 16 words, state in
+  // HBM, runtime word count (push-style rounds: no reverse-slot reads)
+  if (W > 16) {
+    return launch_spf_routes_global_wide(g, pt, units, nUnits, flags, W, out, stream);
   }
   // units too large for LDS (or the "spf_global" option): state in HBM
   if (use_global(g, W, flags)) {
