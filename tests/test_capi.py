@@ -36,7 +36,10 @@ def test_pure_entry_points_without_device():
     assert b"gfx950" in lib.ogs_version()
     assert [lib.ogs_nh_words_for_degree(d) for d in (0, 1, 32, 33, 65, 200, 511)] == \
         [1, 1, 1, 2, 4, 8, 16]
-    assert lib.ogs_nh_words_for_degree(513) < 0
+    # past 512 links: the exact width (runtime-width kernels), never an error
+    assert [lib.ogs_nh_words_for_degree(d) for d in (512, 513, 700, 4096)] == [16, 17, 22, 128]
+    assert lib.ogs_nh_words_for_degree(-1) < 0
+    assert lib.ogs_abi_version() == capi.OGS_ABI_VERSION
 
 
 def test_spf_routes_rejects_bad_arguments():
