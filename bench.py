@@ -277,6 +277,26 @@ def run_g1(args, rank):
                        "kernel": "spf_global*_kernel + route_global_kernel (one launch; "
                                  "latency bound: frontier rounds of one workgroup per unit)"}
     set_traffic(out, "g1", ("spf_global", "route_global_kernel"))
+    # Decision's own call on this area: ONE buildRouteDb(myNode) through the
+    # drop-in (Decision.cpp:912-913 -> SpfSolver.cpp:313-453), cold (fresh
+    # LinkState / PrefixState / solver: flatten + uploads + launch + D2H +
+    # materialisation) and warm, beside refcpu's single-thread build
+    src = G1_SOURCES[0]
+    sreps = 5
+    cold, warm, routes, d_cold, d_warm = M.build_latency_bench("wan", G1_OPTS, src, sreps)
+    single = {"source": src, "unit": "ms/build", "gpu_cold_ms": round(median(cold) / 1e3, 3),
+              "gpu_warm_ms": round(median(warm) / 1e3, 3), "routes": routes, "reps": sreps,
+              "route_digest": f"{d_cold:016x}"}
+    golden_check(single, "g1_single", d_cold, GOLDEN.get("g1_single"))
+    golden_check(single, "g1_single_warm", d_warm, GOLDEN.get("g1_single"))
+    if not args.no_cpu_baseline:
+        cpu = oracle().cpu_time_build("wan", G1_OPTS, src, 3)
+        single["cpu_baseline"] = {
+            "value": round(median(cpu) / 1e3, 2), "unit": "ms/build", "cores": 1,
+            "kind": "port", "reps": 3,
+            "sample": f"refcpu buildRouteDb('{src}') on a fresh replica per rep, 1 thread, "
+                      "median (ingestion untimed)"}
+    out["single_source"] = single
     want = GOLDEN.get("g1")
     out["golden"] = "n/a" if want is None else ("match" if f"{digest:016x}" == want
                                                  else "MISMATCH")
@@ -1204,6 +1224,9 @@ def main():
                     line["golden"][k] = v
             elif sub == "g1_large_wan":
                 line["golden"]["g1"] = g
+        for k, v in ((line.get("g1_large_wan") or {}).get("single_source") or {}).get(
+                "golden", {}).items():
+            line["golden"][k] = v
         finish(line)
     elif DIGEST_FAILURES:
         raise SystemExit(1)

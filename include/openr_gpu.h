@@ -418,6 +418,15 @@ typedef struct ogs_route_diff {
    * and DRAINED bit (a different but equal advertiser then counts as a
    * change). */
   const uint32_t* adv_class;
+  /* Optional caller-held cache of the base unit's tight-DAG descendant rows
+   * (OGS_F_INCREMENTAL repair; [S_n * ceil(S_n/32)] words, S_n <= 8192):
+   * base_desc_valid == 0 -> the rows are computed into base_desc by this
+   * call, 1 -> reused as they are. They depend only on the topology, the
+   * source and the base SPF: the caller clears the flag when any of them
+   * changes (the memo rule of LinkState.cpp:635-638) and sets it after the
+   * first call. NULL: rebuilt in the workspace on every call. */
+  uint32_t* base_desc;
+  int32_t base_desc_valid;
 } ogs_route_diff;
 
 /* Batched SPF + RouteDb of link-failure variants with an optional route

@@ -723,6 +723,17 @@ void addNodeLabelRoutes(const LinkState& ls, const FlatTopology& f,
                         size_t nhStride, int W, LabelRoutes& labelToNode,
                         const uint32_t* reach = nullptr);
 
+// Next-hop words of a source in an all-sources batch (RouteDbBatch, the C3
+// launches): the smallest kernel width, except that sources of 65..96 links
+// on large topologies (the fused frontier + route stream's domain) keep three
+// words instead of rounding up to four -- one mask word per route less
+// (C3's FSWs, 84 links: 0.21 GB less per whole-node build).
+inline int batchNhWords(int degree, size_t nodes, bool wideMetric) {
+  const int w = std::max(1, ogs_nh_words_for_degree(degree));
+  if (w == 4 && degree <= 96 && nodes > 256 && nodes <= 30000 && !wideMetric) return 3;
+  return w;
+}
+
 // bit v of a settled bitset (exact-order SPF rows)
 inline bool bitAt(const uint32_t* bits, uint32_t v) { return (bits[v >> 5] >> (v & 31u)) & 1u; }
 
@@ -805,6 +816,7 @@ class LinkFailureSweep {
 
  private:
   static constexpr int kDeadMax = 4;  // <= 2 links x 2 directions
+  static constexpr size_t kDescMaxNodes = 8192;  // ogs_route_diff.base_desc bound
   ogs_graph graph() const;
   ogs_prefix_table table() const;
   void exactLaunch(void* stream);
@@ -817,6 +829,8 @@ class LinkFailureSweep {
   int W_{1};
   size_t words_{1}, Sp_{1};
   bool baseRun_{false}, recordsRun_{false}, changedOnlyRun_{false};
+  bool descValid_{false};  // bDesc_ holds the base's descendant rows
+  DeviceBuffer bDesc_;
   Mode mode_{kRepair};
   std::vector<uint32_t> dead_;
   DeviceBuffer dNodeBase_, dDesc_, dRow_, dEdges_, dEdgeSrc_, dFlags_, dPfxBase_,

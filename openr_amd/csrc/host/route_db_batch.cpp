@@ -71,7 +71,7 @@ RouteDbBatch::RouteDbBatch(const SpfSolver& solver, const AreaLinkStates& als,
     auto it = f.id.find(sources_[i]);
     if (it == f.id.end()) continue;  // no adjacency database: nullopt
     const uint32_t s = it->second;
-    const int W = std::max(1, ogs_nh_words_for_degree(int(f.rowPtr[s + 1] - f.rowPtr[s])));
+    const int W = batchNhWords(int(f.rowPtr[s + 1] - f.rowPtr[s]), f.names.size(), wide_);
     auto g = std::find_if(groups_.begin(), groups_.end(), [&](const Group& x) { return x.W == W; });
     if (g == groups_.end()) {
       groups_.emplace_back();

@@ -259,6 +259,7 @@ void LinkFailureSweep::runBase(void* stream) {
   ogsCheck(ogs_spf_routes(&g, &pt, dBaseUnit_.as<ogs_unit>(), 1, flags(), W_, &out, stream),
            "ogs_spf_routes(base)");
   baseRun_ = true;
+  descValid_ = false;  // a new base SPF: its descendant rows are rebuilt
   base_.reset();
 }
 
@@ -279,15 +280,22 @@ void LinkFailureSweep::launch(void* stream, bool records) {
     if (changedOnly) out.dist = out.nh = nullptr;  // records of changed routes only
   }
   ogs_unit_mods mods{dDead_.as<uint32_t>(), kDeadMax};
+  // the base's tight-DAG descendant rows: built by the first repair launch
+  // after runBase, reused by the next ones (same topology, source, base SPF)
+  const size_t Sn = size_t(std::max(hb_.maxNodes, 1));
+  if (Sn <= kDescMaxNodes) bDesc_.resize(Sn * ((Sn + 31) / 32) * 4);
   ogs_route_diff diff{bMeta_.as<uint32_t>(), bMetric_.as<uint32_t>(), bMask_.as<uint32_t>(),
                       dChanged_.as<uint32_t>(), dCounts_.as<uint32_t>(),
-                      bDist_.as<uint32_t>(), bNh_.as<uint32_t>(), dAdvClass_.as<uint32_t>()};
+                      bDist_.as<uint32_t>(), bNh_.as<uint32_t>(), dAdvClass_.as<uint32_t>(),
+                      Sn <= kDescMaxNodes ? bDesc_.as<uint32_t>() : nullptr,
+                      descValid_ ? 1 : 0};
   uint32_t fl = flags();
   if (mode_ != kFull) fl |= OGS_F_INCREMENTAL;
   if (changedOnly) fl |= OGS_F_CHANGED_ONLY;
   ogsCheck(ogs_spf_routes_variants(&g, &pt, dUnits_.as<ogs_unit>(), int32_t(numVariants()),
                                    &mods, &diff, fl, W_, &out, stream),
            "ogs_spf_routes_variants");
+  if (fl & OGS_F_INCREMENTAL) descValid_ = true;
   recordsRun_ = records;
   changedOnlyRun_ = records && changedOnly;
 }

@@ -264,6 +264,8 @@ int ogs_set_option(const char* name, int64_t value) {
   return fail(OGS_E_INVALID, std::string("unknown option ") + name);
 }
 
+// any width from ceil(degree/32) up is valid for a call; this is the
+// smallest power-of-two width (the templated kernels) up to 16 words
 int ogs_nh_words_for_degree(int degree) {
   if (degree < 0) return OGS_E_INVALID;
   const int words = (degree + 31) / 32;
@@ -302,8 +304,8 @@ int ogs_spf_routes(const ogs_graph* graph, const ogs_prefix_table* prefixes,
                    !prefixes->adv_min_nh || !prefixes->pfx_flags)) {
     return fail(OGS_E_INVALID, "prefix table arrays are NULL");
   }
-  if (ogs_nh_words_for_degree(nh_words * 32) != nh_words) {
-    return fail(OGS_E_UNSUPPORTED, "nh_words must be 1, 2, 4, 8, 16 or > 16");
+  if (nh_words < 1) {
+    return fail(OGS_E_INVALID, "nh_words < 1");
   }
   if ((flags & OGS_F_EXACT_ORDER) && !(flags & OGS_F_WIDE_METRIC)) {
     return fail(OGS_E_INVALID, "OGS_F_EXACT_ORDER needs OGS_F_WIDE_METRIC");
@@ -330,8 +332,8 @@ int ogs_routes_from_spf(const ogs_graph* graph, const ogs_prefix_table* prefixes
       !prefixes->adv_metrics || !prefixes->adv_min_nh || !prefixes->pfx_flags) {
     return fail(OGS_E_INVALID, "input arrays are NULL");
   }
-  if (ogs_nh_words_for_degree(nh_words * 32) != nh_words) {
-    return fail(OGS_E_UNSUPPORTED, "nh_words must be 1, 2, 4, 8, 16 or > 16");
+  if (nh_words < 1) {
+    return fail(OGS_E_INVALID, "nh_words < 1");
   }
   hipError_t e = ogs::launch_routes_from_spf(*graph, *prefixes, units, n_units, spf_dist,
                                             spf_nh, spf_reached, flags, nh_words, *out,
@@ -433,8 +435,8 @@ int ogs_spf_routes_variants(const ogs_graph* graph,
   if (graph->max_nodes <= 0 || uint32_t(graph->max_nodes) > OGS_MAX_NODES_PER_TOPO) {
     return fail(OGS_E_UNSUPPORTED, "max_nodes outside (0, 2^21]");
   }
-  if (ogs_nh_words_for_degree(nh_words * 32) != nh_words) {
-    return fail(OGS_E_UNSUPPORTED, "nh_words must be 1, 2, 4, 8, 16 or > 16");
+  if (nh_words < 1) {
+    return fail(OGS_E_INVALID, "nh_words < 1");
   }
   int unsupported = 0;
   hipError_t e = ogs::launch_variants(*graph, *prefixes, units, n_units, mods, diff,
@@ -509,8 +511,8 @@ int ogs_rib_policy_apply(const ogs_prefix_table* prefixes,
   if (policy->statement_base > 0 && (!applied || !counter)) {
     return fail(OGS_E_INVALID, "a continuation chunk needs applied / counter");
   }
-  if (ogs_nh_words_for_degree(nh_words * 32) != nh_words) {
-    return fail(OGS_E_UNSUPPORTED, "nh_words must be 1, 2, 4, 8, 16 or > 16");
+  if (nh_words < 1) {
+    return fail(OGS_E_INVALID, "nh_words < 1");
   }
   hipError_t e = ogs::launch_rib_policy(*prefixes, *policy, num_areas, n_units, nh_words,
                                         meta, mask, applied, counter,
@@ -540,8 +542,8 @@ int ogs_routes_multiarea(const ogs_graph* graph,
   if (areas->num_areas <= 0 || areas->num_areas > graph->num_topos) {
     return fail(OGS_E_INVALID, "num_areas outside [1, num_topos]");
   }
-  if (ogs_nh_words_for_degree(nh_words * 32) != nh_words) {
-    return fail(OGS_E_UNSUPPORTED, "nh_words must be 1, 2, 4, 8, 16 or > 16");
+  if (nh_words < 1) {
+    return fail(OGS_E_INVALID, "nh_words < 1");
   }
   hipError_t e = ogs::launch_routes_multiarea(
       *graph, *prefixes, *areas, units, n_units, spf_row, spf_dist, spf_nh,

@@ -55,7 +55,6 @@ __global__ __launch_bounds__(kBlock) void rib_policy_kernel(
       cnt = base + k;  // counterID set by every matching statement
       bool any = false;
       for (uint32_t a = 0; a < A; ++a) {
-#pragma unroll
         for (int w = 0; w < WW; ++w) {
           any |= (mask[((size_t(u) * A + a) * WW + w) * Sp + p] &
                   nz[(size_t(k) * A + a) * WW + w]) != 0u;
@@ -64,7 +63,6 @@ __global__ __launch_bounds__(kBlock) void rib_policy_kernel(
       if (!any) continue;  // every next hop weighted 0: route unchanged
       app = base + k;
       for (uint32_t a = 0; a < A; ++a) {
-#pragma unroll
         for (int w = 0; w < WW; ++w) {
           mask[((size_t(u) * A + a) * WW + w) * Sp + p] &= nz[(size_t(k) * A + a) * WW + w];
         }

@@ -263,10 +263,12 @@ bool try_ms_stream(const ogs_graph& g, const ogs_prefix_table& pt,
                    const ogs_unit* units, int nUnits, uint32_t flags, int W,
                    const ogs_spf_out& out, hipStream_t stream, hipError_t* err) {
   if (!g_routeStream || !g.edge_src || (flags & OGS_F_WIDE_METRIC)) return false;
-  if (W != 1 && W != 2 && W != 4) return false;
+  if (W != 1 && W != 2 && W != 3 && W != 4) return false;
   if (size_t(g.max_nodes) * (2 + W) * 4 > 160 * 1024) return false;
   const size_t Sn = size_t(g.max_nodes), Sp = size_t(pt.max_prefixes);
   const bool fused = g_routeStream == 2 && frontier_fits(g, flags, W);
+  // three-word sets (65..96 links: C3 FSWs) only through the fused kernel
+  if (W == 3 && !fused) return false;
   const bool frontier = frontier_fits(g, flags, W);
   const size_t keyBytes = round256(size_t(g.num_topos) * Sp * 4);
   const size_t chunkBytes = frontier ? chunk_scratch_bytes(g) : 0;

@@ -464,7 +464,7 @@ hipError_t launch_spf_routes_exact(const ogs_graph& g, const ogs_prefix_table* p
                                    int W, const ogs_spf_out& out, hipStream_t stream) {
   if (!(flags & OGS_F_WIDE_METRIC)) return hipErrorInvalidValue;
   // rows past the LDS row stage or sets past 16 words: rows read from HBM
-  if (g.max_degree > kExactRow || W > 16) {
+  if (g.max_degree > kExactRow || W > 16 || (W & (W - 1))) {
     return launch_exact_wide(g, pt, units, nUnits, flags, W, out, stream);
   }
   switch (W) {

@@ -835,7 +835,7 @@ hipError_t launch_frontier_spf(const ogs_graph& g, const ogs_unit* units,
 }
 
 // Fused frontier SPF + RouteDb stream (key = pfx_key_kernel output). W is
-// 1, 2 or 4.
+// 1, 2, 3 or 4 (3: sources of 65..96 links write three mask words, not four).
 hipError_t launch_frontier_routes(const ogs_graph& g, const ogs_prefix_table& pt,
                                   const uint32_t* key, const ogs_unit* units,
                                   int nUnits, uint32_t flags, int W,
@@ -849,6 +849,7 @@ hipError_t launch_frontier_routes(const ogs_graph& g, const ogs_prefix_table& pt
   switch (W) {
     case 1: return launch_frontier<1, true>(g, pt, key, chunks, nChunk, units, nUnits, flags, dist, out.nh, out, stream);
     case 2: return launch_frontier<2, true>(g, pt, key, chunks, nChunk, units, nUnits, flags, dist, out.nh, out, stream);
+    case 3: return launch_frontier<3, true>(g, pt, key, chunks, nChunk, units, nUnits, flags, dist, out.nh, out, stream);
     case 4: return launch_frontier<4, true>(g, pt, key, chunks, nChunk, units, nUnits, flags, dist, out.nh, out, stream);
     default: return hipErrorInvalidValue;
   }
@@ -1166,12 +1167,16 @@ bool launch_variants_repair(const ogs_graph& g, const ogs_prefix_table& pt,
     if (*err != hipSuccess) return true;
   }
   // descendant rows of the base tight DAG (every variant shares topology,
-  // source and base SPF: units[0] / diff->base_dist), rebuilt each launch
+  // source and base SPF: units[0] / diff->base_dist): from the caller's
+  // cache when it holds them, else built (into the cache when given)
   uint32_t* desc = nullptr;
   const uint32_t Sn = uint32_t(g.max_nodes);
-  if (desc_scratch_bytes(g) && scratch) {  // the caller sized scratch for it
+  const bool cached = desc_scratch_bytes(g) && diff->base_desc;
+  if (cached && diff->base_desc_valid) {
+    desc = diff->base_desc;
+  } else if (desc_scratch_bytes(g) && (cached || scratch)) {
     const uint32_t words = (Sn + 31u) / 32u;
-    desc = static_cast<uint32_t*>(scratch);
+    desc = cached ? diff->base_desc : static_cast<uint32_t*>(scratch);
     const size_t dl = size_t(words) * 4u + 2u * 2u * ((Sn + 1u) & ~1u);
     hipLaunchKernelGGL(tight_desc_kernel, dim3(Sn), dim3(64), dl, stream, g, units, flags,
                        diff->base_dist, desc, words);

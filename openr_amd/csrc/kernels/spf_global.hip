@@ -967,7 +967,7 @@ hipError_t launch_global_d(const ogs_graph& g, const ogs_prefix_table* pt,
     case 4: return launch_global_w<D, 4>(g, pt, units, nUnits, flags, out, stream);
     case 8: return launch_global_w<D, 8>(g, pt, units, nUnits, flags, out, stream);
     case 16: return launch_global_w<D, 16>(g, pt, units, nUnits, flags, out, stream);
-    default: return hipErrorInvalidValue;
+    default: return launch_global_wide<D>(g, pt, units, nUnits, flags, W, out, stream);
   }
 }
 

@@ -247,6 +247,14 @@ hipError_t launch_spf_routes(const ogs_graph& g, const ogs_prefix_table* pt,
   if (W > 16) {
     return launch_spf_routes_global_wide(g, pt, units, nUnits, flags, W, out, stream);
   }
+  // exact widths that are not a power of two (three words for 65..96 links):
+  // the fused frontier + route stream when it takes the launch, else the
+  // runtime-width HBM kernels
+  if (W & (W - 1)) {
+    hipError_t err = hipSuccess;
+    if (pt && try_ms_stream(g, *pt, units, nUnits, flags, W, out, stream, &err)) return err;
+    return launch_spf_routes_global_wide(g, pt, units, nUnits, flags, W, out, stream);
+  }
   // units too large for LDS (or the "spf_global" option): state in HBM
   if (use_global(g, W, flags)) {
     return launch_spf_routes_global(g, pt, units, nUnits, flags, W, out, stream);

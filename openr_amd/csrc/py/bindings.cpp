@@ -515,7 +515,9 @@ class BatchRunner {
       units_.push_back({t, f.id.at(s)});
       unitSrc_.push_back(s);
       const int deg = int(f.rowPtr[f.id.at(s) + 1] - f.rowPtr[f.id.at(s)]);
-      W_ = std::max(W_, std::max(1, ogs_nh_words_for_degree(deg)));
+      W_ = std::max(W_, batchNhWords(deg, f.names.size(),
+                                     wideDistancesNeeded(f) || f.hasZeroMetric ||
+                                         f.hasWideMetric));
     }
     wide_ |= wideDistancesNeeded(f);
     exact_ |= f.hasZeroMetric || f.hasWideMetric;

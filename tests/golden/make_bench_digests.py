@@ -103,9 +103,11 @@ def gen_c5(out, threads):
 
 
 def gen_g1(out, threads):
-    """Per source the RouteDb digest (key = source name), XOR-combined."""
+    """Per source the RouteDb digest (key = source name), XOR-combined; and
+    the first source's alone (the single-source drop-in sub-line)."""
     ds = R.gen_route_digests("wan", G1_OPTS, G1_SOURCES, True, False, False, threads)
     out["g1"] = f"{shard.combine_digests(ds):016x}"
+    out["g1_single"] = f"{ds[0]:016x}"
 
 
 def main():
