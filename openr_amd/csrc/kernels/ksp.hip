@@ -239,7 +239,7 @@ __device__ uint32_t trace_paths_wave(const UnitCsr& csr, const uint32_t* dist, u
         --sp;
         continue;
       }
-      const uint32_t bu = static_cast<uint32_t>(best >> 9) & OGS_EDGE_DST_MASK;
+      const uint32_t bu = edge_dst(static_cast<uint32_t>(csr.edg[be]));  // the chosen pred
       if (lane == 0) stack[sp].edge = be;  // resume key (+ path edge on success)
       const uint32_t l = link_id(csr, be, static_cast<uint32_t>(csr.edg[be]));
       const bool seen = (visited[l >> 5] >> (l & 31u)) & 1u;

@@ -91,7 +91,7 @@ def test_c3_full_every_source_matches_oracle(product):
                 bad.append(n)
     assert not bad, f"{len(bad)} sources differ from the oracle, e.g. {bad[:8]}"
     assert _h(job) == GOLDEN["c3"]
-    assert {L["W"] for L in launches} == {1, 4}  # FSW (degree 84) in the W=4 group
+    assert {L["W"] for L in launches} == {1, 3}  # FSW (degree 84): three mask words
 
 
 def test_c3_mixed_sources_live_oracle(product, oracle):
