@@ -103,8 +103,11 @@ __device__ __forceinline__ bool route_changed(const Rec<W>& r, const DiffCtx& d,
 // Streams unit u's P route records (rows of stride Sp). rec(v, r) fills
 // meta / metric / mask of node v's record; sv is the unit's SPF state for
 // route_one. Four consecutive prefixes per lane: one 16-B key load and one
-// 16-B non-temporal store per output array.
-template <int W, bool DIFF = false, typename View, typename RecFn>
+// 16-B non-temporal store per output array. OUTS3: the caller guarantees
+// meta, metric and mask outputs and no sel -- the stores are then
+// unconditional, so every path leaves the same number of stores in flight
+// and the key prefetch's wait stays partial (see the loop below).
+template <int W, bool DIFF = false, bool OUTS3 = false, typename View, typename RecFn>
 __device__ __forceinline__ void stream_routes(
     const ogs_prefix_table& pt, const uint32_t* __restrict__ tkey, uint32_t p0,
     uint32_t P, uint32_t Sp, size_t u, uint32_t s,
@@ -144,17 +147,16 @@ __device__ __forceinline__ void stream_routes(
       reinterpret_cast<uintptr_t>(out.sel) | reinterpret_cast<uintptr_t>(out.mask);
   const bool vec = (Sp & 3u) == 0u && (align & 15u) == 0u;
   const uint32_t Pv = vec ? (P & ~3u) : 0u;
-  auto quad = [&](uint32_t q) {
-    const uint4 k4 = *reinterpret_cast<const uint4*>(tkey + q);
+  auto quad = [&](uint32_t q, const uint4 k4) {
     Rec<W> r0, r1, r2, r3;
     one(q + 0, k4.x, r0);
     one(q + 1, k4.y, r1);
     one(q + 2, k4.z, r2);
     one(q + 3, k4.w, r3);
-    if (oMeta) nt_store4(oMeta + q, r0.meta, r1.meta, r2.meta, r3.meta);
-    if (oMetric) nt_store4(oMetric + q, r0.metric, r1.metric, r2.metric, r3.metric);
-    if (oSel) nt_store4(oSel + q, r0.sel, r1.sel, r2.sel, r3.sel);
-    if (oMask) {
+    if (OUTS3 || oMeta) nt_store4(oMeta + q, r0.meta, r1.meta, r2.meta, r3.meta);
+    if (OUTS3 || oMetric) nt_store4(oMetric + q, r0.metric, r1.metric, r2.metric, r3.metric);
+    if (!OUTS3 && oSel) nt_store4(oSel + q, r0.sel, r1.sel, r2.sel, r3.sel);
+    if (OUTS3 || oMask) {
 #pragma unroll
       for (int w = 0; w < W; ++w) {
         nt_store4(oMask + size_t(w) * Sp + q, r0.mask[w], r1.mask[w], r2.mask[w],
@@ -185,8 +187,38 @@ __device__ __forceinline__ void stream_routes(
       }
     }
   };
+  // Software-pipelined: the next quad's keys are loaded before this quad's
+  // stores are issued. vmcnt counts loads and stores together in issue order,
+  // so a key load issued AFTER the previous stores would wait for them to
+  // drain (one store round trip per iteration); issued before, its wait
+  // leaves the younger stores in flight (MI355X_MICROARCH.md, vmcnt).
+  // Software-pipelined key loads: each quad's keys are loaded BEFORE the
+  // previous quad's stores are issued. vmcnt counts loads and stores together
+  // in issue order, so a key load issued after those stores would wait for
+  // them to drain -- one store round trip per iteration. The first quad is
+  // peeled and the loop unrolled by two with the key registers alternating,
+  // so every entry to every use sees the same ops in flight (one key load +
+  // the previous quad's stores) and the compiler keeps the wait partial.
+  constexpr uint32_t kStep = kBlock * 4u;
   uint32_t q = uint32_t(tid) * 4u;
-  for (; q < Pv; q += kBlock * 4u) quad(q);
+  if (q < Pv) {
+    auto keyAt = [&](uint32_t x) {  // clamped: unconditional prefetch
+      return *reinterpret_cast<const uint4*>(tkey + (x < Pv ? x : Pv - 4u));
+    };
+    uint4 ka = keyAt(q);
+    uint4 kb = keyAt(q + kStep);
+    quad(q, ka);
+    q += kStep;
+    while (q < Pv) {
+      ka = keyAt(q + kStep);
+      quad(q, kb);
+      q += kStep;
+      if (q >= Pv) break;
+      kb = keyAt(q + kStep);
+      quad(q, ka);
+      q += kStep;
+    }
+  }
   for (uint32_t p = Pv + tid; p < P; p += kBlock) {  // tail / unaligned rows
     Rec<W> r;
     one(p, tkey[p], r);

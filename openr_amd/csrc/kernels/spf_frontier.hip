@@ -561,7 +561,7 @@ constexpr uint32_t kFlagNinfoGlobal = 1u << 30;
 // ROUTES = true: SPF + the unit's RouteDb stream (route_stream.h) from LDS;
 // dist / nh go to HBM only when requested.
 template <int W, bool ROUTES, bool MODS = false, bool DIFF = false,
-          int QMODE = 0>
+          int QMODE = 0, bool OUTS3 = false>
 __global__ __launch_bounds__(kBlock) void spf_frontier_kernel(
     ogs_graph g, ogs_prefix_table pt, const uint32_t* __restrict__ key,
     const uint64_t* __restrict__ chunks, const uint32_t* __restrict__ nChunk,
@@ -671,12 +671,12 @@ __global__ __launch_bounds__(kBlock) void spf_frontier_kernel(
       for (int w = 0; w < W; ++w) r.mask[w] = nOf(v, w);
     };
     if constexpr (PACKED) {
-      stream_routes<W, DIFF>(pt, key + size_t(unit.topo) * Sp, p0, P, Sp, u0, s,
-                             nflags, PackedView{dn64}, cfg, out, rec, &dc);
+      stream_routes<W, DIFF, OUTS3>(pt, key + size_t(unit.topo) * Sp, p0, P, Sp, u0, s,
+                                    nflags, PackedView{dn64}, cfg, out, rec, &dc);
     } else {
-      stream_routes<W, DIFF>(pt, key + size_t(unit.topo) * Sp, p0, P, Sp, u0, s,
-                             nflags, SplitView<uint32_t, W>{dist, nh}, cfg, out, rec,
-                             &dc);
+      stream_routes<W, DIFF, OUTS3>(pt, key + size_t(unit.topo) * Sp, p0, P, Sp, u0, s,
+                                    nflags, SplitView<uint32_t, W>{dist, nh}, cfg, out,
+                                    rec, &dc);
     }
     if constexpr (DIFF) {
       __syncthreads();
@@ -732,7 +732,7 @@ int queue_mode(const ogs_graph& g, int W) {
   return fold ? 3 : 2;
 }
 
-template <int W, bool ROUTES, bool MODS, bool DIFF, int QMODE>
+template <int W, bool ROUTES, bool MODS, bool DIFF, int QMODE, bool OUTS3 = false>
 hipError_t launch_frontier_q(const ogs_graph& g, const ogs_prefix_table& pt,
                              const uint32_t* key, const uint64_t* chunks,
                              const uint32_t* nChunk, const ogs_unit* units,
@@ -744,7 +744,7 @@ hipError_t launch_frontier_q(const ogs_graph& g, const ogs_prefix_table& pt,
   const uint32_t lds =
       frontier_lds_bytes(uint32_t(g.max_nodes), W, QMODE != 0, ninfo, QMODE != 3);
   if (!ninfo) flags |= kFlagNinfoGlobal;
-  auto k = spf_frontier_kernel<W, ROUTES, MODS, DIFF, QMODE>;
+  auto k = spf_frontier_kernel<W, ROUTES, MODS, DIFF, QMODE, OUTS3>;
   if (lds > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
                                        hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -766,6 +766,14 @@ hipError_t launch_frontier(const ogs_graph& g, const ogs_prefix_table& pt,
                            hipStream_t stream, const ogs_unit_mods& mods = {},
                            const ogs_route_diff& diff = {}) {
   const int qm = queue_mode(g, W);
+  // the all-sources RouteDb stream writes exactly meta / metric / mask:
+  // unconditional stores (stream_routes OUTS3)
+  if constexpr (ROUTES && !MODS && !DIFF) {
+    if (qm == 0 && out.meta && out.metric && out.mask && !out.sel) {
+      return launch_frontier_q<W, ROUTES, MODS, DIFF, 0, true>(
+          g, pt, key, chunks, nChunk, units, nUnits, flags, dist, nh, out, stream, mods, diff);
+    }
+  }
   if constexpr (W == 1) {
     if (qm == 3) {
       return launch_frontier_q<W, ROUTES, MODS, DIFF, 3>(
