@@ -802,13 +802,16 @@ class VariantRunner {
     return py::make_tuple(upd, del);
   }
   // every variant's DecisionRouteUpdate materialised (host cost of the
-  // update path); returns the number of route changes
-  uint64_t materializeAll(int threads) const {
+  // update path): (route changes, ms to build them on `threads` host threads;
+  // the updates' later destruction -- the consumer's -- is not timed)
+  std::pair<uint64_t, double> materializeAll(int threads) const {
+    const auto t0 = std::chrono::steady_clock::now();
+    std::vector<DecisionRouteUpdate> ups = sw().routeUpdates(threads);
+    const double ms =
+        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     uint64_t n = 0;
-    for (const auto& u : sw().routeUpdates(threads)) {
-      n += u.unicastRoutesToUpdate.size() + u.unicastRoutesToDelete.size();
-    }
-    return n;
+    for (const auto& u : ups) n += u.unicastRoutesToUpdate.size() + u.unicastRoutesToDelete.size();
+    return {n, ms};
   }
   std::vector<std::string> changedOf(size_t v) const { return sw().changedPrefixes(v); }
   std::pair<uint32_t, uint32_t> countsOf(size_t v) const { return sw().counts(v); }
