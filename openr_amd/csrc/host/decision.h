@@ -20,6 +20,7 @@
 #include <limits>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <optional>
 #include <set>
 #include <stdexcept>
@@ -750,6 +751,27 @@ std::optional<RibUnicastEntry> materializeRouteAt(
     size_t maskStride, int W, bool v4OverV6Nexthop, const RibPolicy* policy,
     uint16_t applied, uint16_t counter);
 
+// Changed records of many variants in the ogs_route_changes layout: variant
+// v owns records [offsets[v], offsets[v + 1]), record i = prefix index,
+// meta, metric and mask word w at mask[w * total + i].
+struct ChangeRecords {
+  const uint32_t* offsets{nullptr};  // [variants + 1]
+  size_t variants{0};
+  const uint32_t* prefix{nullptr};
+  const uint32_t* meta{nullptr};
+  const uint32_t* metric{nullptr};
+  const uint32_t* mask{nullptr};
+  size_t total{0};
+  int W{1};
+};
+// One DecisionRouteUpdate per variant (calculateUpdate, SpfSolver.cpp:21-56:
+// records without VALID are deletions, the rest materialised routes), built
+// on `threads` host threads (0: up to 16 / the hardware's).
+std::vector<DecisionRouteUpdate> materializeUpdates(const FlatTopology& f, const std::string& me,
+                                                    const PrefixHostTable& pt,
+                                                    const ChangeRecords& c, bool v4OverV6Nexthop,
+                                                    int threads);
+
 DecisionRouteDb materializeRouteDb(
     const LinkState& ls, const FlatTopology& f, const std::string& area,
     const std::string& me, const UnitView& r, const PrefixHostTable& pt,
@@ -806,6 +828,7 @@ class LinkFailureSweep {
   // every variant's update, materialised on `threads` host threads (0: up to
   // 16 / the hardware's); variants are independent, so the batch splits
   std::vector<DecisionRouteUpdate> routeUpdates(int threads = 0) const;
+  ChangeRecords changeRecords() const;  // the fetched compact records
   DecisionRouteDb routeDb(size_t v) const;                // after fetchRecords
   std::vector<std::string> changedPrefixes(size_t v) const;  // after either
   std::pair<uint32_t, uint32_t> counts(size_t v) const;   // {update, delete}
@@ -859,8 +882,11 @@ class LinkFailureSweep {
 // SpfSolver::buildRouteDb(node) (incl. the solver's static routes and node
 // labels) -> DecisionRouteDb::toThrift with thisNodeName. Only the requested
 // node's records cross PCIe. No RibPolicy (getDecisionRouteDb applies none).
-// Single-area; `solver`, the LinkState and `ps` must outlive the batch
-// unchanged.
+// `solver`, the LinkStates and `ps` must outlive the batch unchanged.
+// Over a multi-area domain the build is LAZY: launch() records nothing and
+// each routeDb(node) runs that node's multi-area buildRouteDb on a private
+// solver (serialised by a mutex, so concurrent routeDb calls are safe) from
+// the live LinkStates / PrefixState -- which is why they must stay unchanged.
 class RouteDbBatch {
  public:
   RouteDbBatch(const SpfSolver& solver, const AreaLinkStates& areaLinkStates,
@@ -871,7 +897,7 @@ class RouteDbBatch {
   std::optional<DecisionRouteDb> routeDb(const std::string& node, void* stream = nullptr) const;
   // getDecisionRouteDb: empty routes when there is no RouteDb
   RouteDatabase getRouteDbComputed(const std::string& node, void* stream = nullptr) const;
-  size_t numSources() const { return units_.size(); }
+  size_t numSources() const { return sources_.size(); }
   size_t numGroups() const { return groups_.size(); }
 
  private:
@@ -907,6 +933,7 @@ class RouteDbBatch {
   const AreaLinkStates* als_{nullptr};
   const PrefixState* ps_{nullptr};
   std::unique_ptr<SpfSolver> multi_;
+  mutable std::mutex multiMu_;  // routeDb() mutates multi_'s memo
 };
 
 }  // namespace openr_amd

@@ -221,6 +221,7 @@ std::optional<DecisionRouteDb> RouteDbBatch::routeDb(const std::string& node,
   if (multiArea_) {
     if (!index_.count(node)) throw std::out_of_range("RouteDbBatch: not a source: " + node);
     if (!launched_) throw std::logic_error("RouteDbBatch: launch() first");
+    std::lock_guard<std::mutex> lk(multiMu_);
     return multi_->buildRouteDb(node, *als_, *ps_);
   }
   UnitRecords r;

@@ -399,35 +399,35 @@ const DecisionRouteDb& LinkFailureSweep::baseRouteDb() const {
   return *base_;
 }
 
-DecisionRouteUpdate LinkFailureSweep::routeUpdate(size_t v) const {
-  if (v >= numVariants() || offsets_.size() != numVariants() + 1) {
-    throw std::out_of_range("LinkFailureSweep::routeUpdate: variant / fetchUpdates");
-  }
-  if (exact_) return xUpd_.at(v);
-  DecisionRouteUpdate u;  // SpfSolver.cpp:21-56, prefixes in table order
-  const FlatTopology& f = ls_.flat();
-  const size_t T = cPrefixH_.size();
-  const uint32_t rb = f.rowPtr[f.id.at(me_)];
-  for (uint32_t i = offsets_[v]; i < offsets_[v + 1]; ++i) {
-    const uint32_t p = cPrefixH_[i];
-    auto e = materializeRouteAt(f, rb, me_, table_, p, cMetaH_[i], cMetricH_[i], &cMaskH_[i],
-                                T, W_, v4OverV6_, nullptr, OGS_POLICY_NONE, OGS_POLICY_NONE);
+namespace {
+
+// SpfSolver.cpp:21-56 for one variant, prefixes in table order
+DecisionRouteUpdate updateOf(const FlatTopology& f, uint32_t rb, const std::string& me,
+                             const PrefixHostTable& pt, const ChangeRecords& c, size_t v,
+                             bool v4OverV6) {
+  DecisionRouteUpdate u;
+  for (uint32_t i = c.offsets[v]; i < c.offsets[v + 1]; ++i) {
+    const uint32_t p = c.prefix[i];
+    auto e = materializeRouteAt(f, rb, me, pt, p, c.meta[i], c.metric[i], &c.mask[i], c.total,
+                                c.W, v4OverV6, nullptr, OGS_POLICY_NONE, OGS_POLICY_NONE);
     if (e) {
       u.unicastRoutesToUpdate.emplace_hint(u.unicastRoutesToUpdate.end(), e->prefix,
                                            std::move(*e));
     } else {
-      u.unicastRoutesToDelete.push_back(table_.prefixes.at(p));
+      u.unicastRoutesToDelete.push_back(pt.prefixes.at(p));
     }
   }
   return u;
 }
 
-std::vector<DecisionRouteUpdate> LinkFailureSweep::routeUpdates(int threads) const {
-  const size_t V = numVariants();
-  if (offsets_.size() != V + 1) {
-    throw std::out_of_range("LinkFailureSweep::routeUpdates: fetchUpdates first");
-  }
-  (void)ls_.flat();  // built before the workers read it
+}  // namespace
+
+std::vector<DecisionRouteUpdate> materializeUpdates(const FlatTopology& f, const std::string& me,
+                                                    const PrefixHostTable& pt,
+                                                    const ChangeRecords& c, bool v4OverV6,
+                                                    int threads) {
+  const size_t V = c.variants;
+  const uint32_t rb = f.rowPtr[f.id.at(me)];
   std::vector<DecisionRouteUpdate> out(V);
   const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
   constexpr size_t kBlockV = 16;  // variants per work item
@@ -439,7 +439,9 @@ std::vector<DecisionRouteUpdate> LinkFailureSweep::routeUpdates(int threads) con
   auto work = [&] {
     try {
       for (size_t b; (b = next.fetch_add(kBlockV)) < V;) {
-        for (size_t v = b; v < std::min(V, b + kBlockV); ++v) out[v] = routeUpdate(v);
+        for (size_t v = b; v < std::min(V, b + kBlockV); ++v) {
+          out[v] = updateOf(f, rb, me, pt, c, v, v4OverV6);
+        }
       }
     } catch (...) {
       std::lock_guard<std::mutex> lk(errMu);
@@ -452,6 +454,37 @@ std::vector<DecisionRouteUpdate> LinkFailureSweep::routeUpdates(int threads) con
   for (auto& th : pool) th.join();
   if (err) std::rethrow_exception(err);
   return out;
+}
+
+ChangeRecords LinkFailureSweep::changeRecords() const {
+  ChangeRecords c;
+  c.offsets = offsets_.data();
+  c.variants = numVariants();
+  c.prefix = cPrefixH_.data();
+  c.meta = cMetaH_.data();
+  c.metric = cMetricH_.data();
+  c.mask = cMaskH_.data();
+  c.total = cPrefixH_.size();
+  c.W = W_;
+  return c;
+}
+
+DecisionRouteUpdate LinkFailureSweep::routeUpdate(size_t v) const {
+  if (v >= numVariants() || offsets_.size() != numVariants() + 1) {
+    throw std::out_of_range("LinkFailureSweep::routeUpdate: variant / fetchUpdates");
+  }
+  if (exact_) return xUpd_.at(v);
+  const FlatTopology& f = ls_.flat();
+  return updateOf(f, f.rowPtr[f.id.at(me_)], me_, table_, changeRecords(), v, v4OverV6_);
+}
+
+std::vector<DecisionRouteUpdate> LinkFailureSweep::routeUpdates(int threads) const {
+  const size_t V = numVariants();
+  if (offsets_.size() != V + 1) {
+    throw std::out_of_range("LinkFailureSweep::routeUpdates: fetchUpdates first");
+  }
+  if (exact_) return xUpd_;
+  return materializeUpdates(ls_.flat(), me_, table_, changeRecords(), v4OverV6_, threads);
 }
 
 DecisionRouteDb LinkFailureSweep::routeDb(size_t v) const {

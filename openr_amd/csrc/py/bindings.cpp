@@ -1746,6 +1746,74 @@ PYBIND11_MODULE(_decision, m) {
           return std::make_tuple(cold, warm, routes, dCold, dWarm);
         },
         py::arg("kind"), py::arg("opts"), py::arg("me"), py::arg("reps"));
+  // Host-only f1 materialisation harness (no device): synthetic changed
+  // records of `variants` variants x `perVariant` prefixes of a generated
+  // topology's source `me` (about 10 % deletions, random next-hop subsets of
+  // the source's links) through materializeUpdates on `threads` host threads.
+  // Returns (ms per rep, changes) -- destruction of the updates untimed.
+  m.def("materialize_updates_bench",
+        [](const std::string& kind, py::dict opts, const std::string& me, size_t variants,
+           size_t perVariant, int threads, int reps) {
+          auto g = genLsdb(kind, opts);
+          py::gil_scoped_release nogil;
+          LinkState ls(g.area, "test_node");
+          PrefixState ps;
+          loadLsdb(g, ls, ps);
+          const FlatTopology& f = ls.flat();
+          PrefixHostTable pt;
+          pt.build(ps);
+          const uint32_t s = f.id.at(me);
+          const uint32_t deg = f.rowPtr[s + 1] - f.rowPtr[s];
+          const int W = std::max(1, int((deg + 31) / 32));
+          const size_t P = pt.prefixes.size();
+          std::vector<uint32_t> off(variants + 1, 0), pfx, meta, metric;
+          uint64_t x = 0x9E3779B97F4A7C15ull;
+          auto rnd = [&] {
+            x ^= x << 13;
+            x ^= x >> 7;
+            x ^= x << 17;
+            return x;
+          };
+          for (size_t v = 0; v < variants; ++v) {
+            std::vector<uint32_t> ps_;
+            for (size_t k = 0; k < perVariant; ++k) ps_.push_back(uint32_t(rnd() % P));
+            std::sort(ps_.begin(), ps_.end());
+            ps_.erase(std::unique(ps_.begin(), ps_.end()), ps_.end());
+            for (uint32_t p : ps_) {
+              pfx.push_back(p);
+              meta.push_back(rnd() % 10 == 0 ? 0u : OGS_ROUTE_VALID);
+              metric.push_back(uint32_t(10 + rnd() % 1000));
+            }
+            off[v + 1] = uint32_t(pfx.size());
+          }
+          const size_t T = pfx.size();
+          std::vector<uint32_t> mask(T * W, 0);
+          for (size_t i = 0; i < T; ++i) {
+            for (int k = 0; k < 2; ++k) {
+              const uint32_t j = uint32_t(rnd() % deg);
+              mask[size_t(j / 32) * T + i] |= 1u << (j % 32);
+            }
+          }
+          ChangeRecords c;
+          c.offsets = off.data();
+          c.variants = variants;
+          c.prefix = pfx.data();
+          c.meta = meta.data();
+          c.metric = metric.data();
+          c.mask = mask.data();
+          c.total = T;
+          c.W = W;
+          std::vector<double> ms;
+          for (int r = 0; r < reps; ++r) {
+            auto t0 = std::chrono::steady_clock::now();
+            auto ups = materializeUpdates(f, me, pt, c, false, threads);
+            ms.push_back(std::chrono::duration<double, std::milli>(
+                             std::chrono::steady_clock::now() - t0).count());
+          }
+          return std::make_pair(ms, T);
+        },
+        py::arg("kind"), py::arg("opts"), py::arg("me"), py::arg("variants"),
+        py::arg("per_variant"), py::arg("threads"), py::arg("reps"));
   m.def("route_db_batch_serve_bench",
         [](const std::string& kind, py::dict opts, int serve) {
           auto g = genLsdb(kind, opts);
