@@ -250,7 +250,7 @@ int ogs_set_option(const char* name, int64_t value) {
     return OGS_OK;
   }
   if (std::strcmp(name, "wave_opt") == 0) {
-    if (value < 0 || value > 3) return fail(OGS_E_INVALID, "wave_opt must be in [0, 3]");
+    if (value < 0 || value > 7) return fail(OGS_E_INVALID, "wave_opt must be in [0, 7]");
     ogs::g_waveOpt = int(value);
     return OGS_OK;
   }

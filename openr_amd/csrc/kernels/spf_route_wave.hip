@@ -38,6 +38,7 @@ namespace ogs {
 
 constexpr uint32_t OGS_WAVE_OPT_BPERMUTE = 1;    // register-resident SPF words
 constexpr uint32_t OGS_WAVE_OPT_REG_ROUTES = 2;  // identity-segment route path
+constexpr uint32_t OGS_WAVE_OPT_PAIR = 4;        // two units per wave, 16-bit words
 
 // LDS image of one unit. Advertisement metrics are staged only when best
 // route selection reads them; minNexthop is read from HBM on demand (only
@@ -147,6 +148,339 @@ __device__ __forceinline__ void route_single(uint32_t n, int64_t minNh,
   }
 }
 
+// ---- pieces shared by the one-unit and the pair kernels ---------------------
+
+// Pull rounds of one unit to the fixpoint in the unit's LDS image; the
+// lane's node words come back in dcur / ncur (unreachable: kInf, {}).
+// Narrow form (every path < 2^23, decided per unit): one 32-bit word per
+// node, dist << 8 | next-hop bits (source degree <= 8). Adding w << 8 carries
+// the next-hop bits along, all candidates tied with the minimum share its
+// distance bits. Wide form (paths < 2^31 - 1, host-guaranteed): 64-bit
+// {dist, nh} words, tie test by equality.
+template <int NPL, int MAXD>
+__device__ __forceinline__ void wave_spf(char* base, const WaveLayout& L, bool narrow,
+                                         const uint32_t (&vk)[NPL],
+                                         const uint32_t (&ea)[NPL][MAXD],
+                                         const uint32_t (&ew)[NPL][MAXD], uint32_t s,
+                                         int lane, uint32_t (&dcur)[NPL],
+                                         uint32_t (&ncur)[NPL], uint32_t& rounds) {
+  constexpr uint32_t P0 = NPL * 64;
+  constexpr uint32_t kInf = 0xFFFFFFFFu;
+  (void)rounds;
+  if (narrow) {
+    // The next-hop byte is stored COMPLEMENTED (dist << 8 | ~nh & 0xFF):
+    // with hi = min | 0xFF, min(cand, hi) is the candidate itself when it
+    // ties the minimum distance and hi otherwise, so the AND over the edges
+    // is {min dist, ~(OR of the tied next-hop sets)} -- min + and per edge,
+    // no compare / select pairs. Unreachable = 0x800000FF (dist field 2^23,
+    // empty set); unusable edges read the dummy word with weight 0.
+    // Every lane is stable at the fixpoint -- empty positions read only the
+    // dummy, the source's lane only word P0 + 9 (= its own {0, {}}) -- so
+    // convergence is ONE test per round: did any lane's word change. (Per
+    // round, measured alone with the diagnostic stamps build: 838 cycles
+    // with the per-slot ballots against the active mask and the early exit
+    // after a separated slot, 550 with no test at all.)
+    constexpr uint32_t kUnr = 0x800000FFu;
+    uint32_t* d32 = reinterpret_cast<uint32_t*>(base + L.dn32);
+    uint32_t ws[NPL][MAXD], ra[NPL][MAXD], cur[NPL];
+#pragma unroll
+    for (int k = 0; k < NPL; ++k) {
+      const bool src = vk[k] == s;
+#pragma unroll
+      for (int j = 0; j < MAXD; ++j) {
+        ra[k][j] = src ? P0 + 9 : ea[k][j];
+        ws[k][j] = src ? 0u : ew[k][j] << 8;
+      }
+      cur[k] = src ? 0xFFu : kUnr;
+      d32[k * 64 + lane] = cur[k];
+    }
+    if (lane == 0) {
+      d32[P0] = kUnr;
+      d32[P0 + 9] = 0xFFu;
+    }
+    if (lane < 8) d32[P0 + 1 + lane] = ~(1u << lane) & 0xFFu;
+    wave_sync();
+    for (;;) {
+      uint32_t chg = 0u;
+#pragma unroll
+      for (int k = 0; k < NPL; ++k) {
+        uint32_t cand[MAXD];
+        uint32_t best = kUnr;
+#pragma unroll
+        for (int j = 0; j < MAXD; ++j) {
+          cand[j] = d32[ra[k][j]] + ws[k][j];
+          best = cand[j] < best ? cand[j] : best;
+        }
+        const uint32_t hiB = best | 0xFFu;
+        uint32_t word = hiB;
+#pragma unroll
+        for (int j = 0; j < MAXD; ++j) word &= cand[j] < hiB ? cand[j] : hiB;
+        chg |= word ^ cur[k];
+        cur[k] = word;
+        d32[k * 64 + lane] = word;
+      }
+#ifdef OGS_STAMPS
+      ++rounds;
+#endif
+      if (__builtin_amdgcn_ballot_w64(chg != 0u) == 0ull) break;
+      wave_sync();
+    }
+#pragma unroll
+    for (int k = 0; k < NPL; ++k) {
+      const bool unr = cur[k] >= 0x80000000u;
+      dcur[k] = unr ? kInf : cur[k] >> 8;
+      ncur[k] = unr ? 0u : ~cur[k] & 0xFFu;
+    }
+  } else {
+    // 64-bit {dist, nh} words (paths < 2^31 - 1); the same single
+    // convergence test per round as the narrow form (the source's lane reads
+    // only word P0 + 9 = {0, {}}, empty positions only the dummy)
+    constexpr uint32_t kUnr = 0x80000000u;
+    uint64_t* dn = reinterpret_cast<uint64_t*>(base + L.dn);
+    uint32_t we[NPL][MAXD], ra[NPL][MAXD];
+#pragma unroll
+    for (int k = 0; k < NPL; ++k) {
+      const bool src = vk[k] == s;
+#pragma unroll
+      for (int j = 0; j < MAXD; ++j) {
+        ra[k][j] = src ? P0 + 9 : ea[k][j];
+        // unusable: dummy {kUnr} + 2^31-1 = 2^32-1, never wins, never wraps
+        we[k][j] = src ? 0u : ea[k][j] == P0 ? kUnr - 1 : ew[k][j];
+      }
+      dcur[k] = src ? 0u : kUnr;
+      ncur[k] = 0u;
+      dn[k * 64 + lane] = dcur[k];
+    }
+    if (lane == 0) {
+      dn[P0] = uint64_t(kUnr);
+      dn[P0 + 9] = 0ull;
+    }
+    if (lane < 8) dn[P0 + 1 + lane] = uint64_t(1u << lane) << 32;
+    wave_sync();
+    for (;;) {
+      uint32_t chg = 0u;
+#pragma unroll
+      for (int k = 0; k < NPL; ++k) {
+        uint64_t x[MAXD];
+#pragma unroll
+        for (int j = 0; j < MAXD; ++j) x[j] = dn[ra[k][j]];
+        uint32_t best = kUnr;
+        uint32_t cand[MAXD];
+#pragma unroll
+        for (int j = 0; j < MAXD; ++j) {
+          cand[j] = static_cast<uint32_t>(x[j]) + we[k][j];
+          best = cand[j] < best ? cand[j] : best;
+        }
+        uint32_t m = 0u;
+#pragma unroll
+        for (int j = 0; j < MAXD; ++j) {
+          m |= (cand[j] == best) ? static_cast<uint32_t>(x[j] >> 32) : 0u;
+        }
+        chg |= (best ^ dcur[k]) | (m ^ ncur[k]);
+        dcur[k] = best;
+        ncur[k] = m;
+        dn[k * 64 + lane] = uint64_t(best) | (uint64_t(m) << 32);
+      }
+#ifdef OGS_STAMPS
+      ++rounds;
+#endif
+      if (__builtin_amdgcn_ballot_w64(chg != 0u) == 0ull) break;
+      wave_sync();
+    }
+#pragma unroll
+    for (int k = 0; k < NPL; ++k) {
+      if (dcur[k] >= kUnr) {
+        dcur[k] = kInf;
+        ncur[k] = 0u;
+      }
+    }
+  }
+}
+
+// Per-edge constants of the lane's positions from the per-position edge
+// image (ogs_graph.slot_edges): word position (P0: dummy, P0 + 1 + r: the
+// source through its link slot r) and weight (0 if unusable); wmax over the
+// wave.
+template <int NPL, int MAXD>
+__device__ __forceinline__ uint32_t wave_edges_from_image(const uint32_t (&ie)[NPL][MAXD],
+                                                          uint32_t posS, bool hop,
+                                                          uint32_t (&ea)[NPL][MAXD],
+                                                          uint32_t (&ew)[NPL][MAXD]) {
+  constexpr uint32_t P0 = NPL * 64;
+  uint32_t wmax = 0;
+#pragma unroll
+  for (int k = 0; k < NPL; ++k) {
+#pragma unroll
+    for (int j = 0; j < MAXD; ++j) {
+      const uint32_t x = ie[k][j];
+      const uint32_t nbr = x & 0x1FFu;
+      const bool ok = !(x & OGS_SLOT_EDGE_DOWN) &&
+          !((x & OGS_SLOT_EDGE_DST_OVERLOADED) && nbr != posS);
+      const uint32_t w = hop ? 1u : x >> 16;
+      ea[k][j] = !ok ? P0
+                     : (nbr == posS ? P0 + 1 + ((x >> OGS_SLOT_EDGE_RSLOT_SHIFT) & 7u) : nbr);
+      ew[k][j] = ok ? w : 0u;
+      wmax = ew[k][j] > wmax ? ew[k][j] : wmax;
+    }
+  }
+  return wmax;
+}
+
+__device__ __forceinline__ uint32_t wave_max(uint32_t x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint32_t t = __shfl_xor(x, o);
+    x = t > x ? t : x;
+  }
+  return __builtin_amdgcn_readfirstlane(x);
+}
+
+// Route-phase tables of one unit: node flags into LDS, prefix tables into
+// LDS unless they stay in the staging registers (identity segments: every
+// prefix has exactly one advertisement, at its own index -- the route phase
+// then reads advertiser and flags from the registers). Returns "identity".
+template <int NPL, int KP>
+__device__ __forceinline__ bool wave_stage_tables(
+    const ogs_prefix_table& pt, int hasPrefixes, bool pfxFits, bool brs, uint32_t wopt,
+    uint32_t N, uint32_t P, uint32_t A, uint32_t p0, uint32_t a0,
+    const WStage<KP, uint32_t>& sOff, const WStage<KP, uint32_t>& sNode,
+    const WStage<KP, uint8_t>& sPf, const WStage<KP, int4>& sMet,
+    const WStage<NPL, uint8_t>& sFlag, char* base, const WaveLayout& L, int lane) {
+  uint8_t* lflags = reinterpret_cast<uint8_t*>(base + L.flags);
+  uint32_t* lAdvOff = reinterpret_cast<uint32_t*>(base + L.advOff);
+  uint32_t* lAdvNode = reinterpret_cast<uint32_t*>(base + L.advNode);
+  int4* lAdvMetrics = reinterpret_cast<int4*>(base + L.advMetrics);
+  uint8_t* lPfxFlags = reinterpret_cast<uint8_t*>(base + L.pfxFlags);
+  bool ident = false;
+  if (hasPrefixes && pfxFits && A == P && (wopt & OGS_WAVE_OPT_REG_ROUTES)) {
+    bool off = false;
+#pragma unroll
+    for (int k = 0; k < KP; ++k) {
+      const uint32_t i = uint32_t(k * 64 + lane);
+      off |= i <= P && sOff.v[k] - a0 != i;
+    }
+    ident = __builtin_amdgcn_ballot_w64(off) == 0ull;
+  }
+  sFlag.store(lflags, N, lane);
+  if (ident) {
+    // tables stay in registers
+  } else if (hasPrefixes && pfxFits) {
+    sOff.store(lAdvOff, P + 1, lane);
+    sNode.store(lAdvNode, A, lane);
+    sMet.store(lAdvMetrics, brs ? A : 0u, lane);
+    sPf.store(lPfxFlags, P, lane);
+  } else if (hasPrefixes) {  // rare: long prefix tables, plain loop
+    for (uint32_t i = lane; i <= P; i += 64) lAdvOff[i] = pt.adv_off[p0 + i];
+    for (uint32_t i = lane; i < P; i += 64) lPfxFlags[i] = pt.pfx_flags[p0 + i];
+    for (uint32_t i = lane; i < A; i += 64) {
+      lAdvNode[i] = pt.adv_node[a0 + i];
+      if (brs) lAdvMetrics[i] = reinterpret_cast<const int4*>(pt.adv_metrics)[a0 + i];
+    }
+  }
+  return ident;
+}
+
+// SPF outputs and the fused RouteDb of one unit (LDS: final {dist, nh} words
+// by node id, node flags, and the prefix tables unless `ident`).
+template <int NPL, int KP>
+__device__ __forceinline__ void wave_outputs(
+    const ogs_graph& g, const ogs_prefix_table& pt, int hasPrefixes, uint32_t flags,
+    const ogs_spf_out& out, size_t uidx, uint32_t s, uint32_t N, uint32_t P, uint32_t a0,
+    bool ident, const uint32_t (&vk)[NPL], const uint32_t (&dcur)[NPL],
+    const uint32_t (&ncur)[NPL], const WStage<KP, uint32_t>& sNode,
+    const WStage<KP, uint8_t>& sPf, char* base, const WaveLayout& L, int lane) {
+  constexpr uint32_t kInf = 0xFFFFFFFFu;
+  const uint64_t* dn = reinterpret_cast<const uint64_t*>(base + L.dn);
+  const uint8_t* lflags = reinterpret_cast<const uint8_t*>(base + L.flags);
+  const uint32_t* lAdvOff = reinterpret_cast<const uint32_t*>(base + L.advOff);
+  const uint32_t* lAdvNode = reinterpret_cast<const uint32_t*>(base + L.advNode);
+  const int4* lAdvMetrics = reinterpret_cast<const int4*>(base + L.advMetrics);
+  const uint8_t* lPfxFlags = reinterpret_cast<const uint8_t*>(base + L.pfxFlags);
+  // ---- SPF outputs ----------------------------------------------------------
+  const uint32_t Sn = g.max_nodes;
+#pragma unroll
+  for (int k = 0; k < NPL; ++k) {
+    const uint32_t v = vk[k];
+    if (v >= N) continue;
+    // streaming (non-temporal) stores: outputs are not re-read by the
+    // kernel, keep them out of the way of the inputs in L2
+    if (out.dist) {
+      __builtin_nontemporal_store(dcur[k], static_cast<uint32_t*>(out.dist) + uidx * Sn + v);
+    }
+    if (out.nh) __builtin_nontemporal_store(ncur[k], out.nh + uidx * Sn + v);
+  }
+  if (!hasPrefixes) return;
+
+  // ---- fused RouteDb --------------------------------------------------------
+  const RouteCfg cfg{(flags & OGS_F_ENABLE_V4) != 0,
+                     (flags & OGS_F_V4_OVER_V6) != 0,
+                     (flags & OGS_F_BEST_ROUTE_SELECTION) != 0};
+  ogs_prefix_table lp{};
+  lp.max_prefixes = pt.max_prefixes;
+  lp.adv_off = lAdvOff;
+  lp.adv_node = lAdvNode;
+  lp.adv_metrics = reinterpret_cast<const int32_t*>(lAdvMetrics);
+  lp.adv_min_nh = pt.adv_min_nh;  // HBM, absolute advertisement index
+  lp.pfx_flags = lPfxFlags;
+  const uint32_t Sp = pt.max_prefixes;
+  if (ident) {
+    // all of the lane's prefixes first (loads), then the stores
+    uint32_t meta[KP], metric[KP], mask[KP];
+#pragma unroll
+    for (int k = 0; k < KP; ++k) {
+      const uint32_t p = uint32_t(k * 64 + lane);
+      const uint8_t pf = sPf.v[k];
+      if ((pf & OGS_PFX_V4) && !cfg.enableV4 && !cfg.v4OverV6) {
+        meta[k] = OGS_REASON_V4_DISABLED << OGS_ROUTE_REASON_SHIFT;  // route_one's gate
+        metric[k] = kInf;
+        mask[k] = 0u;
+      } else {
+        const int64_t minNh = (p < P && (pf & OGS_PFX_HAS_MIN_NH)) ? pt.adv_min_nh[a0 + p]
+                                                                  : INT64_MIN;
+        route_single(p < P ? sNode.v[k] : OGS_NODE_NONE, minNh, s, lflags, dn, meta[k],
+                     metric[k], mask[k]);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < KP; ++k) {
+      const uint32_t p = uint32_t(k * 64 + lane);
+      if (p >= P) continue;
+      const size_t o = uidx * Sp + p;
+      if (out.meta) __builtin_nontemporal_store(meta[k], out.meta + o);
+      if (out.metric) __builtin_nontemporal_store(metric[k], static_cast<uint32_t*>(out.metric) + o);
+      if (out.sel) {
+        __builtin_nontemporal_store((meta[k] & OGS_ROUTE_SELECTED) ? 1u : 0u, out.sel + o);
+      }
+      if (out.mask) __builtin_nontemporal_store(mask[k], out.mask + o);
+    }
+  }
+  for (uint32_t p = ident ? P : lane; p < P; p += 64) {
+    uint32_t meta, metric, mask, selBits;
+    const uint32_t b0 = lAdvOff[p] - a0, b1 = lAdvOff[p + 1] - a0;
+    const uint8_t pf = lPfxFlags[p];
+    const bool gated = (pf & OGS_PFX_V4) && !cfg.enableV4 && !cfg.v4OverV6;
+    if (b1 - b0 == 1 && !gated) {
+      const int64_t minNh = (pf & OGS_PFX_HAS_MIN_NH) ? pt.adv_min_nh[a0 + b0]
+                                                      : INT64_MIN;
+      route_single(lAdvNode[b0], minNh, s, lflags, dn, meta, metric, mask);
+      selBits = (meta & OGS_ROUTE_SELECTED) ? 1u : 0u;
+    } else {
+      uint32_t mk[1];
+      // route_one indexes the prefix table by prefix; rebase the segment
+      lp.adv_node = lAdvNode - a0;
+      lp.adv_metrics = reinterpret_cast<const int32_t*>(lAdvMetrics - a0);
+      route_one<uint32_t, 1>(lp, p, s, lflags, PackedView{dn}, cfg, meta,
+                             metric, mk, selBits);
+      mask = mk[0];
+    }
+    const size_t o = uidx * Sp + p;
+    if (out.meta) __builtin_nontemporal_store(meta, out.meta + o);
+    if (out.metric) __builtin_nontemporal_store(metric, static_cast<uint32_t*>(out.metric) + o);
+    if (out.sel) __builtin_nontemporal_store(selBits, out.sel + o);
+    if (out.mask) __builtin_nontemporal_store(mask, out.mask + o);
+  }
+}
+
 template <int NPL, int MAXD, int UPB>
 __global__ __launch_bounds__(64 * UPB) void spf_route_wave_kernel(
     ogs_graph g, ogs_prefix_table pt, int hasPrefixes,
@@ -159,11 +493,11 @@ __global__ __launch_bounds__(64 * UPB) void spf_route_wave_kernel(
   const int lane = threadIdx.x & 63;
   const int uidx = blockIdx.x * UPB + uib;
   if (uidx >= nUnits) return;
+  uint32_t rounds = 0;
 #ifdef OGS_STAMPS  // diagnostic build only: phase clocks into out.sel
   const uint64_t tStart = __builtin_amdgcn_s_memtime();
   const uint64_t rtStart = __builtin_amdgcn_s_memrealtime();  // 100 MHz
   uint64_t tDesc = 0, tStaged = 0, tSpf = 0;
-  uint32_t rounds = 0;
 #endif
 
   // ---- unit offsets -------------------------------------------------------
@@ -234,11 +568,6 @@ __global__ __launch_bounds__(64 * UPB) void spf_route_wave_kernel(
   uint64_t* dn = reinterpret_cast<uint64_t*>(base + L.dn);
   uint32_t* lrow = reinterpret_cast<uint32_t*>(base + L.row);
   uint64_t* ledg = reinterpret_cast<uint64_t*>(base + L.edges);
-  uint8_t* lflags = reinterpret_cast<uint8_t*>(base + L.flags);
-  uint32_t* lAdvOff = reinterpret_cast<uint32_t*>(base + L.advOff);
-  uint32_t* lAdvNode = reinterpret_cast<uint32_t*>(base + L.advNode);
-  int4* lAdvMetrics = reinterpret_cast<int4*>(base + L.advMetrics);
-  uint8_t* lPfxFlags = reinterpret_cast<uint8_t*>(base + L.pfxFlags);
 
   // ---- staging: one batch of loads, then LDS writes -----------------------
   // With the per-position edge image (ogs_graph.slot_edges) each lane loads
@@ -323,22 +652,7 @@ __global__ __launch_bounds__(64 * UPB) void spf_route_wave_kernel(
     if (m) posS = uint32_t(k * 64) + uint32_t(__builtin_ctzll(m));
   }
   if (img) {
-#pragma unroll
-    for (int k = 0; k < NPL; ++k) {
-#pragma unroll
-      for (int j = 0; j < MAXD; ++j) {
-        const uint32_t x = ie[k][j];
-        const uint32_t nbr = x & 0x1FFu;
-        const bool ok = !(x & OGS_SLOT_EDGE_DOWN) &&
-            !((x & OGS_SLOT_EDGE_DST_OVERLOADED) && nbr != posS);
-        const uint32_t w = hop ? 1u : x >> 16;
-        ea[k][j] = !ok ? P0
-                       : (nbr == posS ? P0 + 1 + ((x >> OGS_SLOT_EDGE_RSLOT_SHIFT) & 7u)
-                                      : nbr);
-        ew[k][j] = ok ? w : 0u;
-        wmax = ew[k][j] > wmax ? ew[k][j] : wmax;
-      }
-    }
+    wmax = wave_edges_from_image<NPL, MAXD>(ie, posS, hop, ea, ew);
   } else {
     {
       uint32_t* posOf = reinterpret_cast<uint32_t*>(base + L.dn32);  // scratch
@@ -369,12 +683,7 @@ __global__ __launch_bounds__(64 * UPB) void spf_route_wave_kernel(
       }
     }
   }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const uint32_t t = __shfl_xor(wmax, o);
-    wmax = t > wmax ? t : wmax;
-  }
-  wmax = __builtin_amdgcn_readfirstlane(wmax);
+  wmax = wave_max(wmax);
   uint64_t actMask[NPL];  // lanes holding a non-source node (uniform)
   uint32_t dcur[NPL], ncur[NPL];
 #pragma unroll
@@ -418,18 +727,10 @@ __global__ __launch_bounds__(64 * UPB) void spf_route_wave_kernel(
   wave_sync();  // posOf scratch is overwritten below
 
   // ---- SPF: pull rounds to the fixpoint -------------------------------------
-  // Narrow form (every path < 2^23, the common case, decided per unit): one
-  // 32-bit word per node, dist << 8 | next-hop bits (source degree <= 8).
-  // Adding w << 8 carries the next-hop bits along, all candidates tied with
-  // the minimum share its distance bits, so the new word is simply the OR of
-  // the candidates <= (min | 0xFF). Unreachable = 2^31 (dist field 2^23):
-  // unreachable candidates are > 2^31 and never tie with a reachable one.
-  // Wide form (paths < 2^31 - 1, host-guaranteed): 64-bit {dist, nh} words,
-  // tie test by equality.
   const bool narrow = uint64_t(wmax) * (N > 0 ? N - 1 : 0) < 0x7FFFFFull;
   if (narrow && regSpf) {
-    // Words as in the narrow form below, held in registers: slot k's lane
-    // gathers its neighbours' words from the other slot's register with
+    // Words as in the narrow form (wave_spf), held in registers: slot k's
+    // lane gathers its neighbours' words from the other slot's register with
     // ds_bpermute (no LDS traffic, no bank conflicts). Per edge a lane
     // address and an addend: unusable edges add kUnr (saturating, so the
     // candidate is >= kUnr and never below a reachable word); edges into
@@ -497,132 +798,8 @@ __global__ __launch_bounds__(64 * UPB) void spf_route_wave_kernel(
       dcur[k] = cur[k] >= kUnr ? kInf : cur[k] >> 8;
       ncur[k] = cur[k] >= kUnr ? 0u : cur[k] & 0xFFu;
     }
-  } else if (narrow) {
-    // The next-hop byte is stored COMPLEMENTED (dist << 8 | ~nh & 0xFF):
-    // with hi = min | 0xFF, min(cand, hi) is the candidate itself when it
-    // ties the minimum distance and hi otherwise, so the AND over the edges
-    // is {min dist, ~(OR of the tied next-hop sets)} -- min + and per edge,
-    // no compare / select pairs. Unreachable = 0x800000FF (dist field 2^23,
-    // empty set); unusable edges read the dummy word with weight 0.
-    // Every lane is stable at the fixpoint -- empty positions read only the
-    // dummy, the source's lane only word P0 + 9 (= its own {0, {}}) -- so
-    // convergence is ONE test per round: did any lane's word change. (Per
-    // round, measured alone with the diagnostic stamps build: 838 cycles
-    // with the per-slot ballots against the active mask and the early exit
-    // after a separated slot, 550 with no test at all.)
-    constexpr uint32_t kUnr = 0x800000FFu;
-    uint32_t* d32 = reinterpret_cast<uint32_t*>(base + L.dn32);
-    uint32_t ws[NPL][MAXD], ra[NPL][MAXD], cur[NPL];
-#pragma unroll
-    for (int k = 0; k < NPL; ++k) {
-      const bool src = vk[k] == s;
-#pragma unroll
-      for (int j = 0; j < MAXD; ++j) {
-        ra[k][j] = src ? P0 + 9 : ea[k][j];
-        ws[k][j] = src ? 0u : ew[k][j] << 8;
-      }
-      cur[k] = src ? 0xFFu : kUnr;
-      d32[k * 64 + lane] = cur[k];
-    }
-    if (lane == 0) {
-      d32[P0] = kUnr;
-      d32[P0 + 9] = 0xFFu;
-    }
-    if (lane < 8) d32[P0 + 1 + lane] = ~(1u << lane) & 0xFFu;
-    wave_sync();
-    for (;;) {
-      uint32_t chg = 0u;
-#pragma unroll
-      for (int k = 0; k < NPL; ++k) {
-        uint32_t cand[MAXD];
-        uint32_t best = kUnr;
-#pragma unroll
-        for (int j = 0; j < MAXD; ++j) {
-          cand[j] = d32[ra[k][j]] + ws[k][j];
-          best = cand[j] < best ? cand[j] : best;
-        }
-        const uint32_t hiB = best | 0xFFu;
-        uint32_t word = hiB;
-#pragma unroll
-        for (int j = 0; j < MAXD; ++j) word &= cand[j] < hiB ? cand[j] : hiB;
-        chg |= word ^ cur[k];
-        cur[k] = word;
-        d32[k * 64 + lane] = word;
-      }
-#ifdef OGS_STAMPS
-      ++rounds;
-#endif
-      if (__builtin_amdgcn_ballot_w64(chg != 0u) == 0ull) break;
-      wave_sync();
-    }
-#pragma unroll
-    for (int k = 0; k < NPL; ++k) {
-      const bool unr = cur[k] >= 0x80000000u;
-      dcur[k] = unr ? kInf : cur[k] >> 8;
-      ncur[k] = unr ? 0u : ~cur[k] & 0xFFu;
-    }
   } else {
-    // 64-bit {dist, nh} words (paths < 2^31 - 1); the same single
-    // convergence test per round as the narrow form (the source's lane reads
-    // only word P0 + 9 = {0, {}}, empty positions only the dummy)
-    constexpr uint32_t kUnr = 0x80000000u;
-    uint32_t we[NPL][MAXD], ra[NPL][MAXD];
-#pragma unroll
-    for (int k = 0; k < NPL; ++k) {
-      const bool src = vk[k] == s;
-#pragma unroll
-      for (int j = 0; j < MAXD; ++j) {
-        ra[k][j] = src ? P0 + 9 : ea[k][j];
-        // unusable: dummy {kUnr} + 2^31-1 = 2^32-1, never wins, never wraps
-        we[k][j] = src ? 0u : ea[k][j] == P0 ? kUnr - 1 : ew[k][j];
-      }
-      dcur[k] = src ? 0u : kUnr;
-      ncur[k] = 0u;
-      dn[k * 64 + lane] = dcur[k];
-    }
-    if (lane == 0) {
-      dn[P0] = uint64_t(kUnr);
-      dn[P0 + 9] = 0ull;
-    }
-    if (lane < 8) dn[P0 + 1 + lane] = uint64_t(1u << lane) << 32;
-    wave_sync();
-    for (;;) {
-      uint32_t chg = 0u;
-#pragma unroll
-      for (int k = 0; k < NPL; ++k) {
-        uint64_t x[MAXD];
-#pragma unroll
-        for (int j = 0; j < MAXD; ++j) x[j] = dn[ra[k][j]];
-        uint32_t best = kUnr;
-        uint32_t cand[MAXD];
-#pragma unroll
-        for (int j = 0; j < MAXD; ++j) {
-          cand[j] = static_cast<uint32_t>(x[j]) + we[k][j];
-          best = cand[j] < best ? cand[j] : best;
-        }
-        uint32_t m = 0u;
-#pragma unroll
-        for (int j = 0; j < MAXD; ++j) {
-          m |= (cand[j] == best) ? static_cast<uint32_t>(x[j] >> 32) : 0u;
-        }
-        chg |= (best ^ dcur[k]) | (m ^ ncur[k]);
-        dcur[k] = best;
-        ncur[k] = m;
-        dn[k * 64 + lane] = uint64_t(best) | (uint64_t(m) << 32);
-      }
-#ifdef OGS_STAMPS
-      ++rounds;
-#endif
-      if (__builtin_amdgcn_ballot_w64(chg != 0u) == 0ull) break;
-      wave_sync();
-    }
-#pragma unroll
-    for (int k = 0; k < NPL; ++k) {
-      if (dcur[k] >= kUnr) {
-        dcur[k] = kInf;
-        ncur[k] = 0u;
-      }
-    }
+    wave_spf<NPL, MAXD>(base, L, narrow, vk, ea, ew, s, lane, dcur, ncur, rounds);
   }
   // final {dist, nh} words, now by NODE ID, for the route phase (ABI
   // "unreachable" = all ones); the source lane's registers hold its unused
@@ -637,128 +814,20 @@ __global__ __launch_bounds__(64 * UPB) void spf_route_wave_kernel(
     }
     if (v < N) dn[v] = uint64_t(dcur[k]) | (uint64_t(ncur[k]) << 32);
   }
-  // identity segments (every prefix has exactly one advertisement, at its
-  // own index: the common single-advertiser table): the route phase reads
-  // advertiser and flags from the staging registers, the tables skip LDS
-  bool ident = false;
-  if (hasPrefixes && pfxFits && A == P && (wopt & OGS_WAVE_OPT_REG_ROUTES)) {
-    bool off = false;
-#pragma unroll
-    for (int k = 0; k < KP; ++k) {
-      const uint32_t i = uint32_t(k * 64 + lane);
-      off |= i <= P && sOff.v[k] - a0 != i;
-    }
-    ident = __builtin_amdgcn_ballot_w64(off) == 0ull;
-  }
-  sFlag.store(lflags, N, lane);
-  if (ident) {
-    // tables stay in registers
-  } else if (hasPrefixes && pfxFits) {
-    sOff.store(lAdvOff, P + 1, lane);
-    sNode.store(lAdvNode, A, lane);
-    sMet.store(lAdvMetrics, brs ? A : 0u, lane);
-    sPf.store(lPfxFlags, P, lane);
-  } else if (hasPrefixes) {  // rare: long prefix tables, plain loop
-    for (uint32_t i = lane; i <= P; i += 64) lAdvOff[i] = pt.adv_off[p0 + i];
-    for (uint32_t i = lane; i < P; i += 64) lPfxFlags[i] = pt.pfx_flags[p0 + i];
-    for (uint32_t i = lane; i < A; i += 64) {
-      lAdvNode[i] = pt.adv_node[a0 + i];
-      if (brs) lAdvMetrics[i] = reinterpret_cast<const int4*>(pt.adv_metrics)[a0 + i];
-    }
-  }
+  const bool ident = wave_stage_tables<NPL, KP>(pt, hasPrefixes, pfxFits, brs, wopt, N, P, A,
+                                                p0, a0, sOff, sNode, sPf, sMet, sFlag, base, L,
+                                                lane);
   wave_sync();
 #ifdef OGS_STAMPS
   tSpf = __builtin_amdgcn_s_memtime();
 #endif
-
-  // ---- SPF outputs ----------------------------------------------------------
-  const uint32_t Sn = g.max_nodes;
-#pragma unroll
-  for (int k = 0; k < NPL; ++k) {
-    const uint32_t v = vk[k];
-    if (v >= N) continue;
-    // streaming (non-temporal) stores: outputs are not re-read by the
-    // kernel, keep them out of the way of the inputs in L2
-    if (out.dist) {
-      __builtin_nontemporal_store(dcur[k], static_cast<uint32_t*>(out.dist) + size_t(uidx) * Sn + v);
-    }
-    if (out.nh) __builtin_nontemporal_store(ncur[k], out.nh + size_t(uidx) * Sn + v);
-  }
-  if (!hasPrefixes) return;
-
-  // ---- fused RouteDb --------------------------------------------------------
-  const RouteCfg cfg{(flags & OGS_F_ENABLE_V4) != 0,
-                     (flags & OGS_F_V4_OVER_V6) != 0,
-                     (flags & OGS_F_BEST_ROUTE_SELECTION) != 0};
-  ogs_prefix_table lp{};
-  lp.max_prefixes = pt.max_prefixes;
-  lp.adv_off = lAdvOff;
-  lp.adv_node = lAdvNode;
-  lp.adv_metrics = reinterpret_cast<const int32_t*>(lAdvMetrics);
-  lp.adv_min_nh = pt.adv_min_nh;  // HBM, absolute advertisement index
-  lp.pfx_flags = lPfxFlags;
-  const uint32_t Sp = pt.max_prefixes;
-  if (ident) {
-    // all of the lane's prefixes first (loads), then the stores
-    uint32_t meta[KP], metric[KP], mask[KP];
-#pragma unroll
-    for (int k = 0; k < KP; ++k) {
-      const uint32_t p = uint32_t(k * 64 + lane);
-      const uint8_t pf = sPf.v[k];
-      if ((pf & OGS_PFX_V4) && !cfg.enableV4 && !cfg.v4OverV6) {
-        meta[k] = OGS_REASON_V4_DISABLED << OGS_ROUTE_REASON_SHIFT;  // route_one's gate
-        metric[k] = kInf;
-        mask[k] = 0u;
-      } else {
-        const int64_t minNh = (p < P && (pf & OGS_PFX_HAS_MIN_NH)) ? pt.adv_min_nh[a0 + p]
-                                                                  : INT64_MIN;
-        route_single(p < P ? sNode.v[k] : OGS_NODE_NONE, minNh, s, lflags, dn, meta[k],
-                     metric[k], mask[k]);
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < KP; ++k) {
-      const uint32_t p = uint32_t(k * 64 + lane);
-      if (p >= P) continue;
-      const size_t o = size_t(uidx) * Sp + p;
-      if (out.meta) __builtin_nontemporal_store(meta[k], out.meta + o);
-      if (out.metric) __builtin_nontemporal_store(metric[k], static_cast<uint32_t*>(out.metric) + o);
-      if (out.sel) {
-        __builtin_nontemporal_store((meta[k] & OGS_ROUTE_SELECTED) ? 1u : 0u, out.sel + o);
-      }
-      if (out.mask) __builtin_nontemporal_store(mask[k], out.mask + o);
-    }
-  }
-  for (uint32_t p = ident ? P : lane; p < P; p += 64) {
-    uint32_t meta, metric, mask, selBits;
-    const uint32_t b0 = lAdvOff[p] - a0, b1 = lAdvOff[p + 1] - a0;
-    const uint8_t pf = lPfxFlags[p];
-    const bool gated = (pf & OGS_PFX_V4) && !cfg.enableV4 && !cfg.v4OverV6;
-    if (b1 - b0 == 1 && !gated) {
-      const int64_t minNh = (pf & OGS_PFX_HAS_MIN_NH) ? pt.adv_min_nh[a0 + b0]
-                                                      : INT64_MIN;
-      route_single(lAdvNode[b0], minNh, s, lflags, dn, meta, metric, mask);
-      selBits = (meta & OGS_ROUTE_SELECTED) ? 1u : 0u;
-    } else {
-      uint32_t mk[1];
-      // route_one indexes the prefix table by prefix; rebase the segment
-      lp.adv_node = lAdvNode - a0;
-      lp.adv_metrics = reinterpret_cast<const int32_t*>(lAdvMetrics - a0);
-      route_one<uint32_t, 1>(lp, p, s, lflags, PackedView{dn}, cfg, meta,
-                             metric, mk, selBits);
-      mask = mk[0];
-    }
-    const size_t o = size_t(uidx) * Sp + p;
-    if (out.meta) __builtin_nontemporal_store(meta, out.meta + o);
-    if (out.metric) __builtin_nontemporal_store(metric, static_cast<uint32_t*>(out.metric) + o);
-    if (out.sel) __builtin_nontemporal_store(selBits, out.sel + o);
-    if (out.mask) __builtin_nontemporal_store(mask, out.mask + o);
-  }
+  wave_outputs<NPL, KP>(g, pt, hasPrefixes, flags, out, size_t(uidx), s, N, P, a0, ident, vk,
+                        dcur, ncur, sNode, sPf, base, L, lane);
 #ifdef OGS_STAMPS
   wave_sync();
   if (lane == 0 && out.sel) {
     const uint64_t tEnd = __builtin_amdgcn_s_memtime();
-    uint32_t* d = out.sel + size_t(uidx) * Sp;
+    uint32_t* d = out.sel + size_t(uidx) * pt.max_prefixes;
     d[0] = uint32_t(tStaged - tStart);
     d[1] = uint32_t(tSpf - tStaged);
     d[2] = uint32_t(tEnd - tSpf);
@@ -770,6 +839,269 @@ __global__ __launch_bounds__(64 * UPB) void spf_route_wave_kernel(
 #endif
 }
 
+// ---- two units per wavefront: 16-bit packed words ---------------------------
+// Batches of many topologies of one structure (C2: 4096 random-metric
+// grids; what-if copies of one network) give adjacent units the same
+// relaxation order and the same edge positions -- only the metrics differ.
+// Such a PAIR shares one wavefront: every LDS word holds both units' 16-bit
+// words {A lo, B hi} = dist << 4 | ~nh & 0xF (source degree <= 4), and the
+// narrow form's add / min / min / and per edge become v_pk_add_u16 /
+// v_pk_min_u16 / v_pk_min_u16 / v_and_b32 on both units at once: one
+// relaxation round for two SPFs. Unreachable = 0x800F per half; candidates
+// never wrap (words are capped at 0x800F by the round's min and w << 4 <=
+// 0x7FF0), so the rounds compute min(dist, 2^11) exactly (the clamped
+// Bellman-Ford operator's fixpoint). A unit whose largest finite distance +
+// its largest weight reaches 2^11 might have been clamped: it reruns alone
+// in the 32-bit form (wave_spf), as do the two units of a pair whose
+// structure differs. Staging, table setup and routes are per unit, as in
+// spf_route_wave_kernel.
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint32_t pk_add(uint32_t a, uint32_t b) {
+  return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, a) + __builtin_bit_cast(u16x2, b));
+}
+__device__ __forceinline__ uint32_t pk_min(uint32_t a, uint32_t b) {
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(u16x2, a),
+                                                                __builtin_bit_cast(u16x2, b)));
+}
+
+template <int NPL, int MAXD, int UPB>
+__global__ __launch_bounds__(64 * UPB) void spf_route_wave_pair_kernel(
+    ogs_graph g, ogs_prefix_table pt, int hasPrefixes,
+    const ogs_unit* __restrict__ units, int nUnits, uint32_t flags,
+    ogs_spf_out out, uint32_t ldsPerUnit, uint32_t maxA, uint32_t wopt) {
+  constexpr uint32_t kInf = 0xFFFFFFFFu;
+  constexpr uint32_t P0 = NPL * 64;
+  constexpr int KP = NPL + 1;
+  const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int u0 = 2 * (blockIdx.x * UPB + wib);
+  if (u0 >= nUnits) return;
+  const int nu = nUnits - u0 >= 2 ? 2 : 1;  // uniform
+  uint32_t rounds = 0;
+
+  // ---- unit offsets: both records and both guessed descriptors at once ---
+  uint32_t topo[2], s[2], nb[2], N[2], p0[2] = {0, 0}, P[2] = {0, 0}, a0[2] = {0, 0},
+      A[2] = {0, 0};
+  {
+    const ogs_unit ua = units[u0];
+    const ogs_unit ub = units[u0 + nu - 1];
+    topo[0] = ua.topo;
+    s[0] = ua.src;
+    topo[1] = ub.topo;
+    s[1] = ub.src;
+    const uint4* td = reinterpret_cast<const uint4*>(g.topo_desc);
+#pragma unroll
+    for (int x = 0; x < 2; ++x) {
+      const uint32_t ux = uint32_t(u0 + (x < nu ? x : 0));
+      const uint32_t guess = ux < uint32_t(g.num_topos) ? ux : 0u;
+      uint4 dx = td[2 * guess];
+      uint4 dy = td[2 * guess + 1];
+      asm volatile("" : "+v"(dx.x), "+v"(dx.y), "+v"(dy.x), "+v"(dy.y), "+v"(dy.z),
+                   "+v"(dy.w));
+      dx.x = __builtin_amdgcn_readfirstlane(dx.x);
+      dx.y = __builtin_amdgcn_readfirstlane(dx.y);
+      dy.x = __builtin_amdgcn_readfirstlane(dy.x);
+      dy.y = __builtin_amdgcn_readfirstlane(dy.y);
+      dy.z = __builtin_amdgcn_readfirstlane(dy.z);
+      dy.w = __builtin_amdgcn_readfirstlane(dy.w);
+      if (topo[x] != guess) {
+        dx = td[2 * topo[x]];
+        dy = td[2 * topo[x] + 1];
+      }
+      nb[x] = dx.x;
+      N[x] = dx.y;
+      if (hasPrefixes) {
+        p0[x] = dy.x;
+        P[x] = dy.y;
+        a0[x] = dy.z;
+        A[x] = dy.w;
+      }
+    }
+  }
+  const bool brs = flags & OGS_F_BEST_ROUTE_SELECTION;
+  const WaveLayout L = WaveLayout::make(g.max_nodes, g.max_edges,
+                                        hasPrefixes ? pt.max_prefixes : 0,
+                                        hasPrefixes ? maxA : 0, brs);
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* base[2] = {smem + (2 * wib) * ldsPerUnit, smem + (2 * wib + 1) * ldsPerUnit};
+
+  // ---- staging: both units' loads in one batch ----------------------------
+  uint32_t ie[2][NPL][MAXD], vk[2][NPL];
+  WStage<KP, uint32_t> sOff[2], sNode[2];
+  WStage<KP, uint8_t> sPf[2];
+  WStage<KP, int4> sMet[2];
+  WStage<NPL, uint8_t> sFlag[2];
+  bool pfxFits[2];
+#pragma unroll
+  for (int x = 0; x < 2; ++x) {
+    const uint32_t* ib = g.slot_edges + size_t(topo[x]) * (MAXD * P0);
+#pragma unroll
+    for (int j = 0; j < MAXD; ++j) {
+#pragma unroll
+      for (int k = 0; k < NPL; ++k) ie[x][k][j] = ib[j * P0 + k * 64 + lane];
+    }
+    sFlag[x].load(g.node_flags + nb[x], N[x], lane);
+    const uint16_t* so = g.slot_node + size_t(topo[x]) * (NPL * 64);
+#pragma unroll
+    for (int k = 0; k < NPL; ++k) vk[x][k] = so[k * 64 + lane];
+    pfxFits[x] = (P[x] + 1 <= 64u * KP) && (A[x] <= 64u * KP);
+    if (hasPrefixes && pfxFits[x]) {
+      sOff[x].load(pt.adv_off + p0[x], P[x] + 1, lane);
+      sNode[x].load(pt.adv_node + a0[x], A[x], lane);
+      sMet[x].load(reinterpret_cast<const int4*>(pt.adv_metrics) + a0[x], brs ? A[x] : 0u,
+                   lane);
+      sPf[x].load(pt.pfx_flags + p0[x], P[x], lane);
+    }
+  }
+#pragma unroll
+  for (int x = 0; x < 2; ++x) {
+#pragma unroll
+    for (int k = 0; k < NPL; ++k) vk[x][k] = vk[x][k] == 0xFFFFu ? 0xFFFFFFFFu : vk[x][k];
+  }
+
+  // ---- per-edge constants of both units -----------------------------------
+  const bool hop = flags & OGS_F_HOP_METRIC;
+  uint32_t ea[2][NPL][MAXD], ew[2][NPL][MAXD], posS[2], wmax[2];
+#pragma unroll
+  for (int x = 0; x < 2; ++x) {
+    posS[x] = P0;
+#pragma unroll
+    for (int k = 0; k < NPL; ++k) {
+      const uint64_t m = __builtin_amdgcn_ballot_w64(vk[x][k] == s[x]);
+      if (m) posS[x] = uint32_t(k * 64) + uint32_t(__builtin_ctzll(m));
+    }
+    wmax[x] = wave_max(wave_edges_from_image<NPL, MAXD>(ie[x], posS[x], hop, ea[x], ew[x]));
+  }
+  // a pair: same order, same source position and edge positions, source
+  // degree <= 4 (slot words P0 + 1 .. P0 + 4), weights < 2^11
+  bool pair = nu == 2 && posS[0] == posS[1] && posS[0] < P0 && wmax[0] < 2048u &&
+      wmax[1] < 2048u;
+  if (pair) {
+    bool bad = false;
+#pragma unroll
+    for (int k = 0; k < NPL; ++k) {
+      bad |= vk[0][k] != vk[1][k];
+#pragma unroll
+      for (int j = 0; j < MAXD; ++j) {
+        bad |= ea[0][k][j] != ea[1][k][j] || ea[0][k][j] > P0 + 4;
+      }
+    }
+    pair = __builtin_amdgcn_ballot_w64(bad) == 0ull;
+  }
+
+  // ---- SPF ------------------------------------------------------------------
+  uint32_t dcur[2][NPL], ncur[2][NPL];
+  bool redo[2] = {!pair, !pair && nu == 2};
+  if (pair) {
+    constexpr uint32_t kUnr = 0x800F800Fu;  // both halves unreachable
+    uint32_t* d32 = reinterpret_cast<uint32_t*>(base[0] + L.dn32);
+    const uint32_t sv = s[0];
+    uint32_t ws[NPL][MAXD], ra[NPL][MAXD], cur[NPL];
+#pragma unroll
+    for (int k = 0; k < NPL; ++k) {
+      const bool src = vk[0][k] == sv;
+#pragma unroll
+      for (int j = 0; j < MAXD; ++j) {
+        ra[k][j] = src ? P0 + 9 : ea[0][k][j];
+        ws[k][j] = src ? 0u : (ew[0][k][j] << 4) | (ew[1][k][j] << 20);
+      }
+      cur[k] = src ? 0x000F000Fu : kUnr;
+      d32[k * 64 + lane] = cur[k];
+    }
+    if (lane == 0) {
+      d32[P0] = kUnr;
+      d32[P0 + 9] = 0x000F000Fu;
+    }
+    if (lane < 4) d32[P0 + 1 + lane] = (~(1u << lane) & 0xFu) * 0x00010001u;
+    wave_sync();
+    for (;;) {
+      uint32_t chg = 0u;
+#pragma unroll
+      for (int k = 0; k < NPL; ++k) {
+        uint32_t cand[MAXD];
+        uint32_t best = kUnr;
+#pragma unroll
+        for (int j = 0; j < MAXD; ++j) {
+          cand[j] = pk_add(d32[ra[k][j]], ws[k][j]);
+          best = pk_min(best, cand[j]);
+        }
+        const uint32_t hiB = best | 0x000F000Fu;
+        uint32_t word = hiB;
+#pragma unroll
+        for (int j = 0; j < MAXD; ++j) word &= pk_min(cand[j], hiB);
+        chg |= word ^ cur[k];
+        cur[k] = word;
+        d32[k * 64 + lane] = word;
+      }
+#ifdef OGS_STAMPS
+      ++rounds;
+#endif
+      if (__builtin_amdgcn_ballot_w64(chg != 0u) == 0ull) break;
+      wave_sync();
+    }
+    // unpack; a unit is exact when its largest finite distance + largest
+    // weight stays below the 2^11 clamp
+#pragma unroll
+    for (int x = 0; x < 2; ++x) {
+      uint32_t dmax = 0;
+#pragma unroll
+      for (int k = 0; k < NPL; ++k) {
+        const uint32_t h = (cur[k] >> (16 * x)) & 0xFFFFu;
+        const bool unr = h >= 0x8000u;
+        dcur[x][k] = unr ? kInf : h >> 4;
+        ncur[x][k] = unr ? 0u : ~h & 0xFu;
+        dmax = (!unr && dcur[x][k] > dmax) ? dcur[x][k] : dmax;
+      }
+      redo[x] = wave_max(dmax) + wmax[x] >= 2048u;
+    }
+    wave_sync();  // the packed words are overwritten by a redo
+  }
+#pragma unroll
+  for (int x = 0; x < 2; ++x) {
+    if (redo[x]) {
+      const bool narrow = uint64_t(wmax[x]) * (N[x] > 0 ? N[x] - 1 : 0) < 0x7FFFFFull;
+      wave_spf<NPL, MAXD>(base[x], L, narrow, vk[x], ea[x], ew[x], s[x], lane, dcur[x],
+                          ncur[x], rounds);
+    }
+  }
+
+  // ---- per unit: final words by node id, tables, outputs, routes ----------
+  bool ident[2];
+#pragma unroll
+  for (int x = 0; x < 2; ++x) {
+    if (x >= nu) break;
+    uint64_t* dn = reinterpret_cast<uint64_t*>(base[x] + L.dn);
+#pragma unroll
+    for (int k = 0; k < NPL; ++k) {
+      const uint32_t v = vk[x][k];
+      if (v == s[x]) {
+        dcur[x][k] = 0u;
+        ncur[x][k] = 0u;
+      }
+      if (v < N[x]) dn[v] = uint64_t(dcur[x][k]) | (uint64_t(ncur[x][k]) << 32);
+    }
+    ident[x] = wave_stage_tables<NPL, KP>(pt, hasPrefixes, pfxFits[x], brs, wopt, N[x], P[x],
+                                          A[x], p0[x], a0[x], sOff[x], sNode[x], sPf[x],
+                                          sMet[x], sFlag[x], base[x], L, lane);
+  }
+  wave_sync();
+#pragma unroll
+  for (int x = 0; x < 2; ++x) {
+    if (x >= nu) break;
+    wave_outputs<NPL, KP>(g, pt, hasPrefixes, flags, out, size_t(u0 + x), s[x], N[x], P[x],
+                          a0[x], ident[x], vk[x], dcur[x], ncur[x], sNode[x], sPf[x], base[x],
+                          L, lane);
+  }
+#ifdef OGS_STAMPS
+  wave_sync();
+  if (lane == 0 && out.sel) {
+    uint32_t* d = out.sel + size_t(u0) * pt.max_prefixes;
+    d[3] = rounds;
+  }
+#endif
+}
+
 // "wave_wg_lds" option: minimum LDS bytes per workgroup (occupancy probe for
 // A/B measurements; 0 = just what the units need)
 int g_waveWgLds = 0;
@@ -777,8 +1109,9 @@ int g_waveWgLds = 0;
 int g_waveUpb = 4;
 // "wave_opt" option: OGS_WAVE_OPT_* bits (A/B of the register paths); the
 // ds_bpermute SPF measured no faster than the LDS words (latency-bound
-// rounds), so only the register route path is on by default
-int g_waveOpt = OGS_WAVE_OPT_REG_ROUTES;
+// rounds), so only the register route path and the pair form are on by
+// default
+int g_waveOpt = OGS_WAVE_OPT_REG_ROUTES | OGS_WAVE_OPT_PAIR;
 
 template <int NPL, int MAXD, int UPB>
 hipError_t launch_wave_upb(const ogs_graph& g, const ogs_prefix_table& pt,
@@ -800,11 +1133,44 @@ hipError_t launch_wave_upb(const ogs_graph& g, const ogs_prefix_table& pt,
   return hipGetLastError();
 }
 
+// Two units per wavefront (spf_route_wave_pair_kernel): needs the descriptor
+// table, the relaxation order and the per-position edge image of every
+// topology; pairs whose structure differs run unpacked inside the kernel.
+template <int NPL, int MAXD>
+bool launch_wave_pair(const ogs_graph& g, const ogs_prefix_table& pt, int hasPrefixes,
+                      const ogs_unit* units, int nUnits, uint32_t flags,
+                      const ogs_spf_out& out, uint32_t lds, uint32_t maxA,
+                      hipStream_t stream, hipError_t* err) {
+  constexpr int UPB = 4;  // wavefronts per workgroup, two units each
+  if (!(g_waveOpt & OGS_WAVE_OPT_PAIR) || nUnits < 2 || !g.topo_desc || !g.slot_node ||
+      g.slot_stride != NPL * 64 || !g.slot_edges || g.slot_degree != MAXD) {
+    return false;
+  }
+  const size_t bytes = size_t(lds) * 2 * UPB;
+  if (bytes > 160 * 1024) return false;
+  auto k = spf_route_wave_pair_kernel<NPL, MAXD, UPB>;
+  if (bytes > 64 * 1024) {
+    *err = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, int(bytes));
+    if (*err != hipSuccess) return true;
+  }
+  const int grid = (nUnits + 2 * UPB - 1) / (2 * UPB);
+  hipLaunchKernelGGL(k, dim3(grid), dim3(64 * UPB), bytes, stream, g, pt, hasPrefixes, units,
+                     nUnits, flags, out, lds, maxA, uint32_t(g_waveOpt));
+  *err = hipGetLastError();
+  return true;
+}
+
 template <int NPL, int MAXD>
 hipError_t launch_wave(const ogs_graph& g, const ogs_prefix_table& pt,
                        int hasPrefixes, const ogs_unit* units, int nUnits,
                        uint32_t flags, const ogs_spf_out& out, uint32_t lds,
                        uint32_t maxA, hipStream_t stream) {
+  hipError_t err = hipSuccess;
+  if (launch_wave_pair<NPL, MAXD>(g, pt, hasPrefixes, units, nUnits, flags, out, lds, maxA,
+                                  stream, &err)) {
+    return err;
+  }
   if (g_waveUpb == 16 && uint64_t(lds) * 16 <= 160 * 1024) {
     return launch_wave_upb<NPL, MAXD, 16>(g, pt, hasPrefixes, units, nUnits, flags,
                                           out, lds, maxA, stream);

@@ -225,6 +225,40 @@ def test_wave_kernel_distance_forms(product, oracle, metric_max):
          oracle.grid_batch_route_dbs(opts, 0, T, "1"), f"c2 metricMax={metric_max}")
 
 
+@pytest.mark.parametrize("metric_max", [100, 125, 160, 2047, 2048])
+def test_wave_pair_form(product, oracle, metric_max):
+    """Two units per wavefront with 16-bit words (wave_opt bit 2, default):
+    pairs of one structure relax together with distances clamped at 2^11; a
+    unit whose largest distance + largest weight reaches the clamp reruns in
+    32-bit words (metricMax 125 / 160: some grids past 2^11, some not), as do
+    pairs whose source or structure differs (an odd batch split over two
+    sources, so one pair straddles them) and weights of 2^11 and more. Every
+    RouteDb equals the oracle's, and equals the one-unit-per-wave kernel's."""
+    import openr_amd.capi as capi
+    lib = capi.load()
+    opts = dict(n=10, metricSeed=0xC2400000 + metric_max, prefixSeed=0xC1,
+                metricMax=metric_max)
+    parts = [(0, 37, "1"), (37, 63, "12")]  # topologies [lo, hi), source
+    cpu = []
+    for lo, hi, src in parts:
+        cpu += oracle.grid_batch_route_dbs(opts, lo, hi, src)
+    got = {}
+    try:
+        for wopt in (6, 2):
+            capi.check(lib, lib.ogs_set_option(b"wave_opt", wopt), "wave_opt")
+            br = product.BatchRunner(True, False, False)
+            for lo, hi, src in parts:
+                br.add_grid_batch(opts, lo, hi, src)
+            br.upload()
+            br.run()
+            br.download()
+            got[wopt] = [br.canonical(u) for u in range(br.num_units())]
+    finally:
+        lib.ogs_set_option(b"wave_opt", 6)
+    _cmp(got[6], cpu, f"pair metricMax={metric_max}")
+    assert got[6] == got[2]
+
+
 def _tri_grid(M, n, seed):
     """n x n grid plus one diagonal per cell: odd cycles (not bipartite), so
     the 2-colour slot order leaves same-slot edges and the wave kernel must

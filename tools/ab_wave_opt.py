@@ -1,8 +1,9 @@
-"""A/B of the wave kernel's register paths (option "wave_opt": bit0 =
-ds_bpermute SPF words, bit1 = identity-segment route path) on the C2 batch,
-interleaved in ONE process against the base build OGS_LIB_B; checks every
-variant's outputs are identical to the base build's. SEL=0 hands the kernel
-no sel output (as bench.py)."""
+"""A/B of the wave kernel's paths (option "wave_opt": bit0 = ds_bpermute
+SPF words, bit1 = identity-segment route path, bit2 = two units per wave
+with 16-bit words) on the C2 batch, interleaved in ONE process against the
+base build OGS_LIB_B (without it: this build at wave_opt 2, one unit per
+wave); checks every variant's outputs are identical to the base's. SEL=0
+hands the kernel no sel output (as bench.py)."""
 import ctypes
 import os
 import sys
@@ -28,7 +29,9 @@ def main():
     times = {n: [] for n, _ in vs}
     for rnd in range(14):
         for name, o in vs:
-            c.lib = c.libb if o is None else c.liba
+            c.lib = c.libb if (o is None and c.libb is not None) else c.liba
+            if o is None and c.libb is None:
+                o = (2, 4)
             if o is not None:
                 c.capi.check(c.lib, c.lib.ogs_set_option(b"wave_opt", o[0]), "wave_opt")
                 c.capi.check(c.lib, c.lib.ogs_set_option(b"wave_upb", o[1]), "wave_upb")
