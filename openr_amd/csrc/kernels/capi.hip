@@ -10,6 +10,7 @@
 namespace ogs {
 extern int g_unitWidth;
 extern int g_waveWgLds;
+extern int g_frontierWgLds;
 extern int g_waveUpb;
 extern int g_waveOpt;
 extern int g_kspWaveTrace;
@@ -259,6 +260,13 @@ int ogs_set_option(const char* name, int64_t value) {
       return fail(OGS_E_INVALID, "wave_wg_lds must be in [0, 163840]");
     }
     ogs::g_waveWgLds = int(value);
+    return OGS_OK;
+  }
+  if (std::strcmp(name, "frontier_wg_lds") == 0) {
+    if (value < 0 || value > 160 * 1024) {
+      return fail(OGS_E_INVALID, "frontier_wg_lds must be in [0, 163840]");
+    }
+    ogs::g_frontierWgLds = int(value);
     return OGS_OK;
   }
   return fail(OGS_E_INVALID, std::string("unknown option ") + name);

@@ -699,6 +699,10 @@ __global__ __launch_bounds__(kBlock) void spf_frontier_kernel(
 #endif
 }
 
+// "frontier_wg_lds" option: minimum LDS bytes per fused frontier + route
+// stream workgroup (0: what the unit needs)
+int g_frontierWgLds = 0;
+
 // "spf_queue" option: -1 (default) the queue form for sparse topologies
 // (max degree <= 16, <= 65,535 nodes; one-phase packed words when the
 // next-hop sets fit one word, with the push stamps folded into the words
@@ -741,8 +745,11 @@ hipError_t launch_frontier_q(const ogs_graph& g, const ogs_prefix_table& pt,
                              hipStream_t stream, const ogs_unit_mods& mods,
                              const ogs_route_diff& diff) {
   const bool ninfo = QMODE == 0 || ninfo_in_lds(uint32_t(g.max_nodes), W);
-  const uint32_t lds =
+  uint32_t lds =
       frontier_lds_bytes(uint32_t(g.max_nodes), W, QMODE != 0, ninfo, QMODE != 3);
+  // occupancy probe (A/B): fewer workgroups per CU stagger the SPF and
+  // route-stream phases of the resident units
+  if (ROUTES && lds < uint32_t(g_frontierWgLds)) lds = uint32_t(g_frontierWgLds);
   if (!ninfo) flags |= kFlagNinfoGlobal;
   auto k = spf_frontier_kernel<W, ROUTES, MODS, DIFF, QMODE, OUTS3>;
   if (lds > 64 * 1024) {
