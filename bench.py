@@ -283,10 +283,16 @@ def run_g1(args, rank):
     # materialisation) and warm, beside refcpu's single-thread build
     src = G1_SOURCES[0]
     sreps = 5
+    M.reset_decision_counters()
     cold, warm, routes, d_cold, d_warm = M.build_latency_bench("wan", G1_OPTS, src, sreps)
+    ctr = M.decision_counters()
     single = {"source": src, "unit": "ms/build", "gpu_cold_ms": round(median(cold) / 1e3, 3),
               "gpu_warm_ms": round(median(warm) / 1e3, 3), "routes": routes, "reps": sreps,
-              "route_digest": f"{d_cold:016x}"}
+              "route_digest": f"{d_cold:016x}",
+              # the drop-in's own timers over these builds (cold and warm):
+              # flatten / uploads, kernels + D2H, host RouteDb materialisation
+              "split_ms_avg": {k: round(ctr.get(f"decision.gpu.{k}_ms.avg", 0.0), 3)
+                               for k in ("prepare", "launch", "materialize")}}
     golden_check(single, "g1_single", d_cold, GOLDEN.get("g1_single"))
     golden_check(single, "g1_single_warm", d_warm, GOLDEN.get("g1_single"))
     if not args.no_cpu_baseline:

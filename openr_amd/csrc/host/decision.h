@@ -209,6 +209,24 @@ class Link {
 };
 using LinkPtr = std::shared_ptr<Link>;
 
+// ---------------------------------------------------------------- stats --
+// fb303-style Decision counters (stats.cpp): the reference's
+// fb303::fbData->addStatValue keys (decision.spf_runs / spf_ms,
+// route_build_runs / route_build_ms, get_route_for_prefix,
+// no_route_to_prefix) plus the engine's split of a single-area build:
+// decision.gpu.prepare_ms (CSR flatten / uploads when stale), launch_ms
+// (kernels + D2H to stream sync) and materialize_ms (host RouteDb).
+// getDecisionCounters exports COUNT keys as "<key>.count" (the sum) and AVG
+// keys as "<key>.avg" / ".sum" / ".count" (samples); times in ms.
+enum class StatType { COUNT, AVG };
+void addStatValue(const std::string& key, double value, StatType type);
+std::map<std::string, double> getDecisionCounters();
+void resetDecisionCounters();
+inline double msSince(std::chrono::steady_clock::time_point t0) {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0)
+      .count();
+}
+
 // Process-wide version stamps of FlatTopology / PrefixState contents: a
 // (pointer, stamp) cache key never matches a different object that reuses
 // the address.
@@ -305,7 +323,10 @@ class LinkState {
   const FlatTopology& flat() const;          // re-flattens when stale
   const FlatTopology& flatOnDevice() const;  // + uploads when stale
   LinkPtr linkByKey(const Link::Key& k) const { return links_.at(k); }
-  void noteSpfRuns(uint64_t n) const { spfRuns_ += n; }
+  void noteSpfRuns(uint64_t n) const {
+    spfRuns_ += n;
+    addStatValue("decision.spf_runs", double(n), StatType::COUNT);  // LinkState.cpp:727
+  }
   // attribute-only updates patch the CSR in place (default) or, off,
   // re-flatten + re-upload it (A/B measurements)
   void setIncrementalFlatten(bool on) { incrementalFlatten_ = on; }
@@ -547,6 +568,9 @@ class SpfSolver {
                         const PrefixState& prefixState, void* stream,
                         MultiAreaResult& r);
   std::optional<DecisionRouteDb> buildRouteDbMultiArea(
+      const std::string& myNodeName, const AreaLinkStates& areaLinkStates,
+      const PrefixState& prefixState);
+  std::optional<DecisionRouteDb> buildRouteDbSingleArea(
       const std::string& myNodeName, const AreaLinkStates& areaLinkStates,
       const PrefixState& prefixState);
   // single-area prefix table (packed, one H2D) cached on (ps, f) versions

@@ -73,7 +73,7 @@ const std::vector<LinkState::Path>& LinkState::getKthPaths(
                          mask.empty() ? nullptr : dMask.as<uint32_t>(),
                          maskWords, flags, &out, nullptr),
            "ogs_ksp_paths");
-  ++spfRuns_;
+  noteSpfRuns(1);
   uint32_t count = 0;
   dCount.download(&count, 1);
   ogsCheck(ogs_stream_sync(nullptr), "ogs_stream_sync");
@@ -301,7 +301,7 @@ void LinkState::prefetchKthPaths(const std::string& src,
   Ksp2Batch b(*this, src, todo);
   b.launch();
   b.fetch();
-  if (b.numUnits()) spfRuns_ += 1 + b.numUnits();
+  if (b.numUnits()) noteSpfRuns(1 + b.numUnits());
   for (size_t i = 0; i < todo.size(); ++i) {
     kthMemo_[{src, todo[i], 1}] = b.paths(i, 1);
     kthMemo_[{src, todo[i], 2}] = b.paths(i, 2);

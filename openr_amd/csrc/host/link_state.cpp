@@ -503,11 +503,13 @@ const LinkState::SpfResult& LinkState::getSpfResult(const std::string& node,
   if (auto it = spfMemo_.find(key); it != spfMemo_.end()) return it->second;
 
   SpfResult res;
+  const auto t0 = std::chrono::steady_clock::now();  // decision.spf_ms (LinkState.cpp:818)
   const FlatTopology& f = flatOnDevice();
   auto idIt = f.id.find(node);
-  ++spfRuns_;
+  noteSpfRuns(1);
   if (idIt == f.id.end()) {
     res.emplace(node, NodeSpfResult(0));  // unknown source settles only itself
+    addStatValue("decision.spf_ms", msSince(t0), StatType::AVG);
     return spfMemo_.emplace(key, std::move(res)).first->second;
   }
   // zero / negative link metrics: the reference's extraction order replayed
@@ -583,6 +585,7 @@ const LinkState::SpfResult& LinkState::getSpfResult(const std::string& node,
     }
     res.emplace(f.names[v], std::move(r));
   }
+  addStatValue("decision.spf_ms", msSince(t0), StatType::AVG);
   return spfMemo_.emplace(key, std::move(res)).first->second;
 }
 

@@ -587,10 +587,14 @@ DecisionRouteDb materializeRouteDb(
   const uint32_t rb = meIt == f.id.end() ? 0u : f.rowPtr[meIt->second];
   // prefixes [p0, p1) into `routes` / `sel` (table order = prefix order, so
   // appending at the end is the hint)
+  std::atomic<uint64_t> noRoute{0};  // decision.no_route_to_prefix (SpfSolver.cpp:221, 242)
   auto build = [&](uint32_t p0, uint32_t p1, std::map<std::string, RibUnicastEntry>& routes,
                    std::map<std::string, RouteSelectionResult>* cache) {
+    uint64_t unreachable = 0;
     for (uint32_t p = p0; p < p1; ++p) {
       const uint32_t meta = r.meta[p];
+      unreachable += !(meta & OGS_ROUTE_VALID) &&
+          ((meta >> OGS_ROUTE_REASON_SHIFT) & 0xFu) == OGS_REASON_UNREACHABLE;
       if (cache && (meta & OGS_ROUTE_SELECTED)) {  // SpfSolver.cpp:247
         const uint32_t a0 = pt.advOff[p];
         RouteSelectionResult sel;
@@ -609,6 +613,7 @@ DecisionRouteDb materializeRouteDb(
                                   r.policy ? r.counter[p] : OGS_POLICY_NONE);
       if (e) routes.emplace_hint(routes.end(), e->prefix, std::move(*e));
     }
+    noRoute += unreachable;
   };
   // Large RouteDbs (a WAN area's 20k routes: ~1 us of allocations per route)
   // are built in prefix chunks on host threads into per-chunk maps whose
@@ -647,6 +652,7 @@ DecisionRouteDb materializeRouteDb(
       }
     }
   }
+  if (noRoute) addStatValue("decision.no_route_to_prefix", double(noRoute), StatType::COUNT);
   for (const auto& [prefix, e] : statics) {  // SpfSolver.cpp:343-349
     if (rdb.unicastRoutes.count(prefix)) continue;
     auto it = rdb.unicastRoutes.emplace(prefix, e).first;
@@ -775,7 +781,20 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(
   bool exists = false;  // SpfSolver.cpp:318-324
   for (const auto& [_, l] : als) exists |= l.hasNode(me);
   if (!exists) return std::nullopt;
-  if (als.size() > 1) return buildRouteDbMultiArea(me, als, ps);
+  const auto t0 = std::chrono::steady_clock::now();
+  addStatValue("decision.route_build_runs", 1, StatType::COUNT);  // SpfSolver.cpp:327
+  // SpfSolver.cpp:334-339: one createRouteForPrefix per known prefix
+  addStatValue("decision.get_route_for_prefix", double(ps.prefixes().size()),
+               StatType::COUNT);
+  auto db = als.size() > 1 ? buildRouteDbMultiArea(me, als, ps)
+                           : buildRouteDbSingleArea(me, als, ps);
+  addStatValue("decision.route_build_ms", msSince(t0), StatType::AVG);  // SpfSolver.cpp:450
+  return db;
+}
+
+std::optional<DecisionRouteDb> SpfSolver::buildRouteDbSingleArea(
+    const std::string& me, const AreaLinkStates& als, const PrefixState& ps) {
+  const auto tPrep = std::chrono::steady_clock::now();
   std::string area;
   const LinkState& ls = singleArea(als, area);
   const FlatTopology& f = ls.flatOnDevice();
@@ -784,6 +803,9 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(
   const bool exact = f.hasZeroMetric || f.hasWideMetric;
   Impl& I = *impl_;
   prepareSingleArea(f, ps, area);
+  // flatten / device CSR + prefix table when stale (cached otherwise)
+  addStatValue("decision.gpu.prepare_ms", msSince(tPrep), StatType::AVG);
+  const auto tLaunch = std::chrono::steady_clock::now();
 
   // ---- launch the fused kernel for (topology, me) -------------------------
   const uint32_t s = f.id.at(me);
@@ -840,6 +862,8 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(
                           nullptr),
            "ogs_memcpy_d2h");
   ogsCheck(ogs_stream_sync(nullptr), "ogs_stream_sync");
+  addStatValue("decision.gpu.launch_ms", msSince(tLaunch), StatType::AVG);
+  const auto tMat = std::chrono::steady_clock::now();
 
   std::vector<uint64_t> dist, metric;
   if (enableNodeSegmentLabel_) widenSpan(I.hRes.at<void>(L.dist), N, wide, dist);
@@ -862,9 +886,11 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(
     view.applied = applied.data();
     view.counter = counter.data();
   }
-  return materializeRouteDb(ls, f, area, me, view, I.table, v4OverV6Nexthop_,
-                            enableNodeSegmentLabel_, staticUnicastRoutes_,
-                            &bestRoutesCache_);
+  auto rdb = materializeRouteDb(ls, f, area, me, view, I.table, v4OverV6Nexthop_,
+                                enableNodeSegmentLabel_, staticUnicastRoutes_,
+                                &bestRoutesCache_);
+  addStatValue("decision.gpu.materialize_ms", msSince(tMat), StatType::AVG);
+  return rdb;
 }
 
 // The incremental branch's routes (createRoutesForPrefixes) of a single-area
@@ -1344,6 +1370,8 @@ std::map<std::string, std::optional<RibUnicastEntry>> SpfSolver::createRoutesFor
     const std::string& me, const AreaLinkStates& als, const PrefixState& ps,
     const std::set<std::string>& prefixes) {
   std::map<std::string, std::optional<RibUnicastEntry>> out;
+  // SpfSolver.cpp:166: one createRouteForPrefix per asked prefix
+  addStatValue("decision.get_route_for_prefix", double(prefixes.size()), StatType::COUNT);
   bool exists = false;  // SpfSolver.cpp:139-158 per prefix
   for (const auto& [_, l] : als) exists |= l.hasNode(me);
   PrefixState sub;  // the changed prefixes through one route launch

@@ -1060,6 +1060,9 @@ PYBIND11_MODULE(_decision, m) {
     return n;
   });
   m.def("version", []() { return std::string(ogs_version()); });
+  // fb303-style Decision counters (stats.cpp)
+  m.def("decision_counters", []() { return getDecisionCounters(); });
+  m.def("reset_decision_counters", []() { resetDecisionCounters(); });
 
   py::class_<LinkState>(m, "LinkState")
       .def(py::init<const std::string&, const std::string&>())
