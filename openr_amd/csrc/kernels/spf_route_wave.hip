@@ -1109,9 +1109,12 @@ int g_waveWgLds = 0;
 int g_waveUpb = 4;
 // "wave_opt" option: OGS_WAVE_OPT_* bits (A/B of the register paths); the
 // ds_bpermute SPF measured no faster than the LDS words (latency-bound
-// rounds), so only the register route path and the pair form are on by
-// default
-int g_waveOpt = OGS_WAVE_OPT_REG_ROUTES | OGS_WAVE_OPT_PAIR;
+// rounds), and the pair form slower (C2: 11.1 vs 10.0 us per launch,
+// profiles/r03_ab_wave_pair.log -- every wave is resident from the start, so
+// the launch lasts one wave's dependent chain; pairing halves the waves but
+// not that chain, and each wave then runs two route phases), so only the
+// register route path is on by default
+int g_waveOpt = OGS_WAVE_OPT_REG_ROUTES;
 
 template <int NPL, int MAXD, int UPB>
 hipError_t launch_wave_upb(const ogs_graph& g, const ogs_prefix_table& pt,

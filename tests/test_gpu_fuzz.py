@@ -149,7 +149,8 @@ PATHS = {
     "global_hbm_nosync": [(b"spf_global", 1, 0), (b"spf_global_lds", 0, 1),
                           (b"spf_global_sync", 0, 1)],
     "workgroup_units": [(b"unit_width", 256, -1)],
-    "wave_plain": [(b"wave_opt", 0, 6)],
+    "wave_plain": [(b"wave_opt", 0, 2)],
+    "wave_pair": [(b"wave_opt", 6, 2)],
 }
 
 

@@ -227,7 +227,7 @@ def test_wave_kernel_distance_forms(product, oracle, metric_max):
 
 @pytest.mark.parametrize("metric_max", [100, 125, 160, 2047, 2048])
 def test_wave_pair_form(product, oracle, metric_max):
-    """Two units per wavefront with 16-bit words (wave_opt bit 2, default):
+    """Two units per wavefront with 16-bit words (wave_opt bit 2, opt-in):
     pairs of one structure relax together with distances clamped at 2^11; a
     unit whose largest distance + largest weight reaches the clamp reruns in
     32-bit words (metricMax 125 / 160: some grids past 2^11, some not), as do
@@ -254,7 +254,7 @@ def test_wave_pair_form(product, oracle, metric_max):
             br.download()
             got[wopt] = [br.canonical(u) for u in range(br.num_units())]
     finally:
-        lib.ogs_set_option(b"wave_opt", 6)
+        lib.ogs_set_option(b"wave_opt", 2)
     _cmp(got[6], cpu, f"pair metricMax={metric_max}")
     assert got[6] == got[2]
 
