@@ -16,6 +16,7 @@ extern int g_waveOpt;
 extern int g_kspWaveTrace;
 extern int g_msGroup;
 extern int g_routeStream;
+extern int g_routeStreamChunks;
 extern int g_spfFrontier;
 extern int g_spfGlobal;
 extern int g_spfGlobalSync;
@@ -178,10 +179,13 @@ int ogs_set_option(const char* name, int64_t value) {
     return OGS_OK;
   }
   if (std::strcmp(name, "route_stream") == 0) {
-    if (value != 0 && value != 1 && value != 2) {
-      return fail(OGS_E_INVALID, "route_stream must be 0, 1 or 2");
-    }
+    if (value < 0 || value > 3) return fail(OGS_E_INVALID, "route_stream must be 0, 1, 2 or 3");
     ogs::g_routeStream = int(value);
+    return OGS_OK;
+  }
+  if (std::strcmp(name, "route_stream_chunks") == 0) {
+    if (value < 1 || value > 64) return fail(OGS_E_INVALID, "route_stream_chunks must be in [1, 64]");
+    ogs::g_routeStreamChunks = int(value);
     return OGS_OK;
   }
   if (std::strcmp(name, "spf_frontier") == 0) {

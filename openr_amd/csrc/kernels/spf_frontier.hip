@@ -828,6 +828,26 @@ hipError_t prep_chunks(const ogs_graph& g, void* scratch, hipStream_t stream,
   return hipGetLastError();
 }
 
+// SPF only over chunk lists already prepared (prep_chunks) in `scratch`
+// (dist / next-hop sets of unit i at dist + i * Sn, nh + i * W * Sn).
+hipError_t launch_frontier_spf_prepared(const ogs_graph& g, const ogs_unit* units,
+                                        int nUnits, uint32_t flags, int W, uint32_t* dist,
+                                        uint32_t* nh, void* scratch, hipStream_t stream) {
+  uint64_t* chunks = static_cast<uint64_t*>(scratch);
+  const uint32_t* nChunk =
+      reinterpret_cast<const uint32_t*>(chunks + size_t(g.num_topos) * chunk_cap(g));
+  const ogs_prefix_table pt{};
+  const ogs_spf_out none{};
+  switch (W) {
+    case 1: return launch_frontier<1, false>(g, pt, nullptr, chunks, nChunk, units, nUnits, flags, dist, nh, none, stream);
+    case 2: return launch_frontier<2, false>(g, pt, nullptr, chunks, nChunk, units, nUnits, flags, dist, nh, none, stream);
+    case 3: return launch_frontier<3, false>(g, pt, nullptr, chunks, nChunk, units, nUnits, flags, dist, nh, none, stream);
+    case 4: return launch_frontier<4, false>(g, pt, nullptr, chunks, nChunk, units, nUnits, flags, dist, nh, none, stream);
+    case 8: return launch_frontier<8, false>(g, pt, nullptr, chunks, nChunk, units, nUnits, flags, dist, nh, none, stream);
+    default: return hipErrorInvalidValue;
+  }
+}
+
 // SPF only (dist / next-hop sets to HBM); `scratch` holds
 // chunk_scratch_bytes(g). Call only when frontier_fits().
 hipError_t launch_frontier_spf(const ogs_graph& g, const ogs_unit* units,
@@ -838,15 +858,7 @@ hipError_t launch_frontier_spf(const ogs_graph& g, const ogs_unit* units,
   uint32_t* nChunk = nullptr;
   hipError_t e = prep_chunks(g, scratch, stream, &chunks, &nChunk);
   if (e != hipSuccess) return e;
-  const ogs_prefix_table pt{};
-  const ogs_spf_out none{};
-  switch (W) {
-    case 1: return launch_frontier<1, false>(g, pt, nullptr, chunks, nChunk, units, nUnits, flags, dist, nh, none, stream);
-    case 2: return launch_frontier<2, false>(g, pt, nullptr, chunks, nChunk, units, nUnits, flags, dist, nh, none, stream);
-    case 4: return launch_frontier<4, false>(g, pt, nullptr, chunks, nChunk, units, nUnits, flags, dist, nh, none, stream);
-    case 8: return launch_frontier<8, false>(g, pt, nullptr, chunks, nChunk, units, nUnits, flags, dist, nh, none, stream);
-    default: return hipErrorInvalidValue;
-  }
+  return launch_frontier_spf_prepared(g, units, nUnits, flags, W, dist, nh, scratch, stream);
 }
 
 // Fused frontier SPF + RouteDb stream (key = pfx_key_kernel output). W is

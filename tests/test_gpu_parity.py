@@ -355,6 +355,7 @@ def _batch_dbs(product, kind, opts, srcs, enable_v4, brs, **options):
         return [br.canonical(u) for u in range(len(srcs))]
     finally:
         lib.ogs_set_option(b"route_stream", 2)
+        lib.ogs_set_option(b"route_stream_chunks", 4)
         lib.ogs_set_option(b"spf_frontier", 1)
         lib.ogs_set_option(b"ms_group", 0)
 
@@ -362,7 +363,7 @@ def _batch_dbs(product, kind, opts, srcs, enable_v4, brs, **options):
 MIX = dict(v4Permille=150, anycastPermille=120, minNhPermille=60, drainPermille=50)
 
 
-@pytest.mark.parametrize("stream,frontier", [(0, 0), (1, 0), (1, 1), (2, 1)])
+@pytest.mark.parametrize("stream,frontier", [(0, 0), (1, 0), (1, 1), (2, 1), (3, 1)])
 @pytest.mark.parametrize("enable_v4,brs", [(True, False), (False, True), (True, True)])
 def test_route_stream_fabric_prefix_mix(product, oracle, stream, frontier, enable_v4, brs):
     """Split SPF / route-stream launches vs the fused multi-source kernel on a
@@ -381,7 +382,7 @@ def test_route_stream_fabric_prefix_mix(product, oracle, stream, frontier, enabl
     _cmp(a, oracle.gen_route_dbs("fabric", opts, srcs, enable_v4, False, brs), "fabricmix")
 
 
-@pytest.mark.parametrize("stream,frontier", [(0, 0), (1, 0), (1, 1), (2, 1)])
+@pytest.mark.parametrize("stream,frontier", [(0, 0), (1, 0), (1, 1), (2, 1), (3, 1)])
 def test_route_stream_wan_prefix_mix(product, oracle, stream, frontier):
     """700-node WAN, random metrics, overloads and the prefix mix, best-route
     selection on, through every large-topology SPF / RouteDb form."""
@@ -392,6 +393,20 @@ def test_route_stream_wan_prefix_mix(product, oracle, stream, frontier):
     a = _batch_dbs(product, "wan", opts, srcs, True, True, route_stream=stream,
                    spf_frontier=frontier)
     _cmp(a, oracle.gen_route_dbs("wan", opts, srcs, True, False, True), "wanmix")
+
+
+@pytest.mark.parametrize("stream,chunks", [(2, 4), (3, 1), (3, 3), (3, 7)])
+def test_route_stream_three_word_sources(product, oracle, stream, chunks):
+    """FSW sources of 84 links (36 SSW + 48 RSW, the C3 shape on 4 pods x 2
+    planes) keep three next-hop words: the fused kernel and the pipelined
+    split (route_stream 3: SPF chunks on a side stream, each chunk's route
+    stream after its SPF) at several chunk counts, vs the oracle."""
+    opts = dict(pods=4, planes=2, sswPerPlane=36, rswPerPod=48, full=True,
+                prefixesPerNode=3, nodeOverloadPermille=10, **MIX)
+    srcs = [f"2-{p}-{f}" for p in range(4) for f in range(2)]
+    a = _batch_dbs(product, "fabric", opts, srcs, True, False, route_stream=stream,
+                   route_stream_chunks=chunks)
+    _cmp(a, oracle.gen_route_dbs("fabric", opts, srcs, True, False, False), "fsw3")
 
 
 def test_route_stream_unaligned_prefix_rows(product, oracle):
