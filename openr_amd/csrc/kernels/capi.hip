@@ -17,6 +17,7 @@ extern int g_kspWaveTrace;
 extern int g_msGroup;
 extern int g_routeStream;
 extern int g_routeStreamChunks;
+extern int g_spfScanBatch;
 extern int g_spfFrontier;
 extern int g_spfGlobal;
 extern int g_spfGlobalSync;
@@ -181,6 +182,11 @@ int ogs_set_option(const char* name, int64_t value) {
   if (std::strcmp(name, "route_stream") == 0) {
     if (value < 0 || value > 3) return fail(OGS_E_INVALID, "route_stream must be 0, 1, 2 or 3");
     ogs::g_routeStream = int(value);
+    return OGS_OK;
+  }
+  if (std::strcmp(name, "spf_scan_batch") == 0) {
+    if (value != 0 && value != 1) return fail(OGS_E_INVALID, "spf_scan_batch must be 0 or 1");
+    ogs::g_spfScanBatch = int(value);
     return OGS_OK;
   }
   if (std::strcmp(name, "route_stream_chunks") == 0) {

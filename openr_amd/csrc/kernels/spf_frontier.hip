@@ -131,6 +131,34 @@ __device__ __forceinline__ void load_chunk(const uint64_t* __restrict__ edges,
   }
 }
 
+// fn(chunk record) for the thread's records c = tid, tid + kBlock, ... < C,
+// kScanBatch loads in flight per step (serial: one dependent load per
+// record, the former scan, for A/B: "spf_scan_batch" option 0).
+constexpr int kScanBatch = 8;
+int g_spfScanBatch = 1;
+
+template <typename Fn>
+__device__ __forceinline__ void scan_chunks(const uint64_t* __restrict__ chunks, uint32_t C,
+                                            bool serial, Fn fn) {
+  const uint32_t tid = threadIdx.x;
+  if (serial) {
+    for (uint32_t c = tid; c < C; c += kBlock) fn(chunks[c]);
+    return;
+  }
+  for (uint32_t c0 = tid; c0 < C; c0 += kScanBatch * kBlock) {
+    uint64_t chs[kScanBatch];
+#pragma unroll
+    for (int k = 0; k < kScanBatch; ++k) {
+      const uint32_t c = c0 + uint32_t(k) * kBlock;
+      chs[k] = c < C ? chunks[c] : ~0ull;
+    }
+#pragma unroll
+    for (int k = 0; k < kScanBatch; ++k) {
+      if (c0 + uint32_t(k) * kBlock < C) fn(chs[k]);
+    }
+  }
+}
+
 // One unit's SPF into LDS (dist[v], nh[v*W + w]); returns after the final
 // workgroup barrier. stamp[] is scratch.
 template <int W, bool MODS>
@@ -138,7 +166,7 @@ __device__ __forceinline__ void frontier_spf(
     uint32_t N, uint32_t s, const uint64_t* __restrict__ edges,
     const uint64_t* __restrict__ chunks, uint32_t C, bool hop,
     const uint32_t* __restrict__ gRow, uint32_t e0, uint32_t* dist,
-    uint32_t* nh, uint16_t* stamp, uint64_t* tp, const DeadEdges& dead) {
+    uint32_t* nh, uint16_t* stamp, uint64_t* tp, const DeadEdges& dead, bool serial) {
   constexpr uint32_t kInf = 0xFFFFFFFFu;
   const int tid = threadIdx.x;
   for (uint32_t v = tid; v < N; v += kBlock) {
@@ -153,14 +181,17 @@ __device__ __forceinline__ void frontier_spf(
 #endif
 
   // ---- dist phase: push dist(v) + w from the nodes changed last round ------
+  // The round scans every chunk record for changed nodes: the thread's
+  // records are loaded kScanBatch at a time (independent L2 loads in
+  // flight) before their stamps are tested, instead of one dependent load
+  // per record.
   uint32_t r = 1;
   for (;; ++r) {
     bool changed = false;
-    for (uint32_t c = tid; c < C; c += kBlock) {
-      const uint64_t ch = chunks[c];
+    scan_chunks(chunks, C, serial, [&](uint64_t ch) {
       const uint32_t v = uint32_t(ch) & OGS_EDGE_DST_MASK;
-      if (stamp[v] != r) continue;
-      if ((uint32_t(ch) & kChunkDrained) && v != s) continue;
+      if (stamp[v] != r) return;
+      if ((uint32_t(ch) & kChunkDrained) && v != s) return;
       const uint32_t dv = dist[v];
       uint64_t x[kChunk];
       load_chunk<MODS>(edges, ch, x, dead);
@@ -182,7 +213,7 @@ __device__ __forceinline__ void frontier_spf(
           changed = true;
         }
       }
-    }
+    });
     if (!__syncthreads_or(changed)) break;
   }
 #ifdef OGS_STAMPS
@@ -214,10 +245,9 @@ __device__ __forceinline__ void frontier_spf(
   // then changed nodes push NH(v) into tight neighbours
   for (r = r0;; ++r) {
     bool changed = false;
-    for (uint32_t c = tid; c < C; c += kBlock) {
-      const uint64_t ch = chunks[c];
+    scan_chunks(chunks, C, serial, [&](uint64_t ch) {
       const uint32_t v = uint32_t(ch) & OGS_EDGE_DST_MASK;
-      if (stamp[v] != r || v == s || (uint32_t(ch) & kChunkDrained)) continue;
+      if (stamp[v] != r || v == s || (uint32_t(ch) & kChunkDrained)) return;
       const uint32_t dv = dist[v];
       uint32_t nv[W];
 #pragma unroll
@@ -251,7 +281,7 @@ __device__ __forceinline__ void frontier_spf(
           changed = true;
         }
       }
-    }
+    });
     if (!__syncthreads_or(changed)) break;
   }
 #ifdef OGS_STAMPS
@@ -556,6 +586,8 @@ uint32_t frontier_lds_bytes(uint32_t Sn, int W, bool queue = false, bool ninfo =
 // internal launch flag (above the public OGS_F_* bits): the queue forms read
 // row bounds / drained bits from the CSR instead of an LDS node-info array
 constexpr uint32_t kFlagNinfoGlobal = 1u << 30;
+// internal launch flag: the chunk scan loads one record at a time (A/B)
+constexpr uint32_t kFlagScanSerial = 1u << 29;
 
 // ROUTES = false: SPF only, dist / nh to HBM.
 // ROUTES = true: SPF + the unit's RouteDb stream (route_stream.h) from LDS;
@@ -622,7 +654,7 @@ __global__ __launch_bounds__(kBlock) void spf_frontier_kernel(
   } else {
     frontier_spf<W, MODS>(N, s, g.edges + e0, chunks + size_t(unit.topo) * cap,
                           nChunk[unit.topo], (flags & OGS_F_HOP_METRIC) != 0, gRow,
-                          e0, dist, nh, stamp, tp, dead);
+                          e0, dist, nh, stamp, tp, dead, (flags & kFlagScanSerial) != 0);
   }
 
   auto dOf = [&](uint32_t v) -> uint32_t {
@@ -751,6 +783,7 @@ hipError_t launch_frontier_q(const ogs_graph& g, const ogs_prefix_table& pt,
   // route-stream phases of the resident units
   if (ROUTES && lds < uint32_t(g_frontierWgLds)) lds = uint32_t(g_frontierWgLds);
   if (!ninfo) flags |= kFlagNinfoGlobal;
+  if (!g_spfScanBatch) flags |= kFlagScanSerial;
   auto k = spf_frontier_kernel<W, ROUTES, MODS, DIFF, QMODE, OUTS3>;
   if (lds > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),

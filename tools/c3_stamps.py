@@ -20,8 +20,9 @@ def main():
     ppn = int(os.environ.get("PPN", "100"))
     lib = capi.load()
     dev = torch.device("cuda", 0)
-    launches, N = bench.c3_launches(torch, openr_amd.decision, capi, dev, 0, 1, ppn,
-                                    with_sel=True)
+    from openr_amd.workloads import c3_source_names
+    launches, N = bench.c3_launches(torch, openr_amd.decision, capi, dev, c3_source_names(),
+                                    ppn, with_sel=True)
     stream = torch.cuda.current_stream(dev)
     for _ in range(3):
         for L in launches:
