@@ -419,7 +419,7 @@ typedef struct ogs_route_diff {
    * change). */
   const uint32_t* adv_class;
   /* Optional caller-held cache of the base unit's tight-DAG descendant rows
-   * (OGS_F_INCREMENTAL repair; [S_n * ceil(S_n/32)] words, S_n <= 8192):
+   * (OGS_F_INCREMENTAL repair; [S_n * ceil(S_n/32)] words, S_n <= 16384):
    * base_desc_valid == 0 -> the rows are computed into base_desc by this
    * call, 1 -> reused as they are. They depend only on the topology, the
    * source and the base SPF: the caller clears the flag when any of them

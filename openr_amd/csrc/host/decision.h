@@ -863,7 +863,7 @@ class LinkFailureSweep {
 
  private:
   static constexpr int kDeadMax = 4;  // <= 2 links x 2 directions
-  static constexpr size_t kDescMaxNodes = 8192;  // ogs_route_diff.base_desc bound
+  static constexpr size_t kDescMaxNodes = 16384;  // ogs_route_diff.base_desc bound
   ogs_graph graph() const;
   ogs_prefix_table table() const;
   void exactLaunch(void* stream);

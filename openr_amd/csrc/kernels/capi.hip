@@ -18,6 +18,7 @@ extern int g_msGroup;
 extern int g_routeStream;
 extern int g_routeStreamChunks;
 extern int g_spfScanBatch;
+extern int g_spfPackedScan;
 extern int g_spfFrontier;
 extern int g_spfGlobal;
 extern int g_spfGlobalSync;
@@ -182,6 +183,11 @@ int ogs_set_option(const char* name, int64_t value) {
   if (std::strcmp(name, "route_stream") == 0) {
     if (value < 0 || value > 3) return fail(OGS_E_INVALID, "route_stream must be 0, 1, 2 or 3");
     ogs::g_routeStream = int(value);
+    return OGS_OK;
+  }
+  if (std::strcmp(name, "spf_packed_scan") == 0) {
+    if (value != 0 && value != 1) return fail(OGS_E_INVALID, "spf_packed_scan must be 0 or 1");
+    ogs::g_spfPackedScan = int(value);
     return OGS_OK;
   }
   if (std::strcmp(name, "spf_scan_batch") == 0) {

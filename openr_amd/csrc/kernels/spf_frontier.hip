@@ -290,6 +290,78 @@ __device__ __forceinline__ void frontier_spf(
 #endif
 }
 
+// One-phase packed form of the chunk scan (W = 1): each node's LDS word is
+// {dist, next-hop word}; a pushed edge replaces a longer word (64-bit LDS
+// compare-and-swap) or ORs its next hops into an equal one, so distances and
+// next-hop sets converge in the same rounds (the fabric: 5 rounds instead of
+// 5 + 4 for the two phases above) -- the least fixpoint of spf_core.h, as
+// queue_spf_packed. dn[v] is over dist + nh (8 B per node).
+template <bool MODS>
+__device__ __forceinline__ void frontier_spf_packed(
+    uint32_t N, uint32_t s, const uint64_t* __restrict__ edges,
+    const uint64_t* __restrict__ chunks, uint32_t C, bool hop,
+    const uint32_t* __restrict__ gRow, uint32_t e0, uint64_t* dn, uint16_t* stamp,
+    uint64_t* tp, const DeadEdges& dead, bool serial) {
+  constexpr uint32_t kInf = 0xFFFFFFFFu;
+  const int tid = threadIdx.x;
+  for (uint32_t v = tid; v < N; v += kBlock) {
+    dn[v] = (v == s) ? 0ull : uint64_t(kInf);
+    stamp[v] = (v == s) ? 1 : 0;
+  }
+  __syncthreads();
+#ifdef OGS_STAMPS
+  tp[0] = __builtin_amdgcn_s_memtime();
+#endif
+  const uint32_t sb = gRow[s] - e0;  // the source's row: its link slots
+  uint32_t r = 1;
+  for (;; ++r) {
+    bool changed = false;
+    scan_chunks(chunks, C, serial, [&](uint64_t ch) {
+      const uint32_t v = uint32_t(ch) & OGS_EDGE_DST_MASK;
+      if (stamp[v] != r) return;
+      if ((uint32_t(ch) & kChunkDrained) && v != s) return;
+      const uint64_t xv = dn[v];
+      const uint32_t dv = static_cast<uint32_t>(xv), nv = static_cast<uint32_t>(xv >> 32);
+      const uint32_t b = uint32_t(ch >> 32);
+      uint64_t x[kChunk];
+      load_chunk<MODS>(edges, ch, x, dead);
+#pragma unroll
+      for (uint32_t i = 0; i < kChunk; ++i) {
+        const uint32_t lo = static_cast<uint32_t>(x[i]);
+        if (lo & OGS_EDGE_DOWN) continue;
+        const uint32_t t = edge_dst(lo);
+        const uint32_t c = dv + (hop ? 1u : static_cast<uint32_t>(x[i] >> 32));
+        // the source contributes its link slot (W = 1: degree <= 32), every
+        // other node NH(v) (LinkState.cpp:808-811)
+        const uint32_t slot = b + i - sb;
+        const uint32_t bits = (v == s) ? (slot < 32u ? 1u << slot : 0u) : nv;
+        uint64_t old = dn[t];
+        for (;;) {
+          const uint32_t dt = static_cast<uint32_t>(old), nt = static_cast<uint32_t>(old >> 32);
+          if (c > dt || (c == dt && !(bits & ~nt))) break;
+          const uint64_t nw = c < dt ? (uint64_t(c) | (uint64_t(bits) << 32))
+                                     : (uint64_t(dt) | (uint64_t(nt | bits) << 32));
+          const uint64_t seen = atomicCAS(reinterpret_cast<unsigned long long*>(&dn[t]),
+                                          static_cast<unsigned long long>(old),
+                                          static_cast<unsigned long long>(nw));
+          if (seen == old) {
+            stamp[t] = uint16_t(r + 1);
+            changed = true;
+            break;
+          }
+          old = seen;
+        }
+      }
+    });
+    if (!__syncthreads_or(changed)) break;
+  }
+#ifdef OGS_STAMPS
+  tp[1] = tp[2] = __builtin_amdgcn_s_memtime();
+  tp[3] = r;
+  tp[4] = 0;
+#endif
+}
+
 // ---- queue form: sparse, deep topologies (C4 / C5 WAN areas) ---------------
 // The chunk scan above reads every chunk record of the topology each round
 // to find the changed nodes: cheap per round on the dense fabric (few,
@@ -643,7 +715,11 @@ __global__ __launch_bounds__(kBlock) void spf_frontier_kernel(
   constexpr bool PACKED = QMODE >= 2;
   static_assert(!PACKED || W == 1, "packed words hold one next-hop word");
   uint64_t* dn64 = reinterpret_cast<uint64_t*>(smem);  // PACKED: over dist + nh
-  if constexpr (PACKED) {
+  if constexpr (QMODE == 4) {  // packed words, chunk scan
+    frontier_spf_packed<MODS>(N, s, g.edges + e0, chunks + size_t(unit.topo) * cap,
+                              nChunk[unit.topo], (flags & OGS_F_HOP_METRIC) != 0, gRow, e0,
+                              dn64, stamp, tp, dead, (flags & kFlagScanSerial) != 0);
+  } else if constexpr (PACKED) {
     queue_spf_packed<MODS, QMODE == 3>(N, s, g.edges + e0, gRow, e0, nflags,
                            (flags & OGS_F_HOP_METRIC) != 0, dn64, stamp32, q0, q1,
                            qcnt, ninfo, tp, dead);
@@ -735,6 +811,11 @@ __global__ __launch_bounds__(kBlock) void spf_frontier_kernel(
 // stream workgroup (0: what the unit needs)
 int g_frontierWgLds = 0;
 
+// "spf_packed_scan" option: 1 (default) chunk-scan units with one-word
+// next-hop sets relax packed {dist, nh} words in one phase
+// (frontier_spf_packed), 0 the two-phase chunk scan (A/B)
+int g_spfPackedScan = 1;
+
 // "spf_queue" option: -1 (default) the queue form for sparse topologies
 // (max degree <= 16, <= 65,535 nodes; one-phase packed words when the
 // next-hop sets fit one word, with the push stamps folded into the words
@@ -776,9 +857,9 @@ hipError_t launch_frontier_q(const ogs_graph& g, const ogs_prefix_table& pt,
                              uint32_t* nh, const ogs_spf_out& out,
                              hipStream_t stream, const ogs_unit_mods& mods,
                              const ogs_route_diff& diff) {
-  const bool ninfo = QMODE == 0 || ninfo_in_lds(uint32_t(g.max_nodes), W);
-  uint32_t lds =
-      frontier_lds_bytes(uint32_t(g.max_nodes), W, QMODE != 0, ninfo, QMODE != 3);
+  const bool scan = QMODE == 0 || QMODE == 4;  // chunk-scan forms: no lists
+  const bool ninfo = scan || ninfo_in_lds(uint32_t(g.max_nodes), W);
+  uint32_t lds = frontier_lds_bytes(uint32_t(g.max_nodes), W, !scan, ninfo, QMODE != 3);
   // occupancy probe (A/B): fewer workgroups per CU stagger the SPF and
   // route-stream phases of the resident units
   if (ROUTES && lds < uint32_t(g_frontierWgLds)) lds = uint32_t(g_frontierWgLds);
@@ -806,13 +887,25 @@ hipError_t launch_frontier(const ogs_graph& g, const ogs_prefix_table& pt,
                            hipStream_t stream, const ogs_unit_mods& mods = {},
                            const ogs_route_diff& diff = {}) {
   const int qm = queue_mode(g, W);
+  // chunk scan with one-word next-hop sets: the one-phase packed form
+  constexpr int kScanMode = W == 1 ? 4 : 0;
+  const bool packedScan = W == 1 && g_spfPackedScan && qm == 0;
   // the all-sources RouteDb stream writes exactly meta / metric / mask:
   // unconditional stores (stream_routes OUTS3)
   if constexpr (ROUTES && !MODS && !DIFF) {
     if (qm == 0 && out.meta && out.metric && out.mask && !out.sel) {
+      if (packedScan) {
+        return launch_frontier_q<W, ROUTES, MODS, DIFF, kScanMode, true>(
+            g, pt, key, chunks, nChunk, units, nUnits, flags, dist, nh, out, stream, mods,
+            diff);
+      }
       return launch_frontier_q<W, ROUTES, MODS, DIFF, 0, true>(
           g, pt, key, chunks, nChunk, units, nUnits, flags, dist, nh, out, stream, mods, diff);
     }
+  }
+  if (packedScan) {
+    return launch_frontier_q<W, ROUTES, MODS, DIFF, kScanMode>(
+        g, pt, key, chunks, nChunk, units, nUnits, flags, dist, nh, out, stream, mods, diff);
   }
   if constexpr (W == 1) {
     if (qm == 3) {
@@ -934,7 +1027,7 @@ hipError_t launch_frontier_routes(const ogs_graph& g, const ogs_prefix_table& pt
 // breadth-first in LDS. With these rows a variant's A is the OR of its
 // seeds' rows -- no growth rounds in the repair kernel. Built once per
 // launch over the base unit (units[0]); topologies up to kDescMaxN nodes.
-constexpr uint32_t kDescMaxN = 8192;
+constexpr uint32_t kDescMaxN = 16384;
 
 __global__ __launch_bounds__(64) void tight_desc_kernel(ogs_graph g,
                                                         const ogs_unit* __restrict__ units,

@@ -409,6 +409,37 @@ def test_route_stream_three_word_sources(product, oracle, stream, chunks):
     _cmp(a, oracle.gen_route_dbs("fabric", opts, srcs, True, False, False), "fsw3")
 
 
+@pytest.mark.parametrize("packed", [1, 0])
+@pytest.mark.parametrize("kind", ["fabric", "wan"])
+def test_frontier_packed_chunk_scan(product, oracle, packed, kind):
+    """The chunk-scan frontier SPF in its one-phase packed {dist, nh} form
+    (spf_packed_scan 1, default for one-word next-hop sets) and in two
+    phases (0), fused with the route stream: fabric sources of every degree
+    class with drained nodes / links, and a WAN forced onto the chunk scan
+    (spf_queue 0) with overloads and the prefix mix, vs the oracle."""
+    if kind == "fabric":
+        opts = dict(pods=8, planes=4, sswPerPlane=16, rswPerPod=32, full=True,
+                    prefixesPerNode=3, nodeOverloadPermille=20, adjOverloadPermille=10, **MIX)
+        names = ([f"1-{p}-{s}" for p in range(4) for s in range(16)] +
+                 [f"3-{p}-{r}" for p in range(8) for r in range(32)])
+        srcs = names[::7]
+        extra = {}
+    else:
+        opts = dict(nodes=900, seed=0xC6, prefixesPerNode=2, nodeOverloadPermille=30,
+                    adjOverloadPermille=20, **MIX)
+        rng = random.Random(13)
+        srcs = [str(rng.randrange(900)) for _ in range(12)]
+        extra = dict(spf_queue=0)
+    try:
+        a = _batch_dbs(product, kind, opts, srcs, True, True, spf_packed_scan=packed, **extra)
+    finally:
+        import openr_amd.capi as capi
+        lib = capi.load()
+        lib.ogs_set_option(b"spf_packed_scan", 1)
+        lib.ogs_set_option(b"spf_queue", -1)
+    _cmp(a, oracle.gen_route_dbs(kind, opts, srcs, True, False, True), f"{kind} packed={packed}")
+
+
 def test_route_stream_unaligned_prefix_rows(product, oracle):
     """Prefix count not a multiple of 4 (scalar tail path of the stream)."""
     opts = dict(pods=4, planes=4, sswPerPlane=20, rswPerPod=60, full=True,

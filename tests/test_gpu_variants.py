@@ -216,3 +216,40 @@ def test_repair_edge_cases(product, oracle):
                 upd, dele = vr.update(v)
                 assert sorted(upd + dele) == changed, (kind, mode, v, links[v])
                 assert vr.updated_canonical(v) == canon, (kind, mode, v, links[v])
+
+
+@pytest.mark.parametrize("desc", [1, 0])
+@pytest.mark.parametrize("mode", [1, 2])
+def test_repair_large_wan(product, oracle, mode, desc):
+    """The base-SPF repair past 8,192 nodes: a 9,500-node WAN (the repair's
+    packed words, stamps, lists and affected-set bitset in 153 kB of LDS),
+    with the affected sets from the descendant rows of the base tight DAG
+    (9,500 x 297 words, desc 1) or grown per variant (desc 0); full records
+    (mode 1) and changed records -> route updates (mode 2) vs the oracle."""
+    import openr_amd.capi as capi
+    lib = capi.load()
+    opts = dict(nodes=9500, seed=0xC9, prefixesPerNode=1)
+    n = 24
+    base, variants, links = oracle.variant_route_updates("wan", opts, "5", n, 0xC4F, 500,
+                                                         True, False)
+    capi.check(lib, lib.ogs_set_option(b"c4_desc", desc), "c4_desc")
+    try:
+        vr = product.VariantRunner(True, False)
+        vr.setup("wan", opts, "5", n, 0xC4F, 500)
+        assert vr.shape()["nodes"] == 9500
+        vr.set_mode(mode)
+        vr.launch(0, True)
+        if mode == 1:
+            vr.download()
+            for v, (canon, changed, nu, nd) in enumerate(variants):
+                assert vr.canonical(v) == canon, f"variant {v} {links[v]}"
+                assert vr.changed(v) == changed and vr.counts(v) == (nu, nd), v
+        else:
+            vr.fetch_updates(0)
+            for v, (canon, changed, nu, nd) in enumerate(variants):
+                upd, dele = vr.update(v)
+                assert sorted(upd + dele) == changed, f"variant {v} {links[v]}"
+                assert vr.updated_canonical(v) == canon, f"variant {v} {links[v]}"
+    finally:
+        lib.ogs_set_option(b"c4_desc", 1)
+    assert any(changed for _, changed, _, _ in variants)
