@@ -705,6 +705,9 @@ struct HostBatch {
 // ---------------------------------------------------- materialisation --
 // One unit's compact GPU results (host copies, distances widened to 64-bit,
 // all-ones = unreachable) and the host side of the prefix table.
+// host threads of materializeRouteDb (0 / 1: the caller's thread only)
+extern int g_materializeThreads;
+
 struct UnitView {
   int W{1};
   uint32_t N{0}, P{0};

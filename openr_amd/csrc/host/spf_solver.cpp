@@ -575,6 +575,8 @@ std::optional<RibUnicastEntry> materializeRouteAt(
   return e;
 }
 
+int g_materializeThreads = 0;
+
 DecisionRouteDb materializeRouteDb(
     const LinkState& ls, const FlatTopology& f, const std::string& area,
     const std::string& me, const UnitView& r, const PrefixHostTable& pt,
@@ -615,11 +617,13 @@ DecisionRouteDb materializeRouteDb(
     }
     noRoute += unreachable;
   };
-  // Large RouteDbs (a WAN area's 20k routes: ~1 us of allocations per route)
-  // are built in prefix chunks on host threads into per-chunk maps whose
-  // nodes are then spliced, in order, into the result (no copies).
-  const size_t T = std::min<size_t>({16, std::max(1u, std::thread::hardware_concurrency()),
-                                     r.P / 4096 + 1});
+  // With g_materializeThreads > 1 the prefixes are built in chunks on host
+  // threads into per-chunk maps whose nodes are then spliced, in order, into
+  // the result (no copies). Off by default: on the GPU box's 16-core share
+  // the G1 warm build (20k routes) took 34 ms with 5 threads against 21 ms
+  // on one (the routes are freed later on the caller's thread, across the
+  // workers' malloc arenas).
+  const size_t T = g_materializeThreads > 0 ? size_t(g_materializeThreads) : 1;
   if (T <= 1) {
     build(0, r.P, rdb.unicastRoutes, bestRoutesCache);
   } else {

@@ -1817,6 +1817,59 @@ PYBIND11_MODULE(_decision, m) {
         },
         py::arg("kind"), py::arg("opts"), py::arg("me"), py::arg("variants"),
         py::arg("per_variant"), py::arg("threads"), py::arg("reps"));
+  // Host-only RouteDb materialisation harness (no device): every prefix of
+  // a generated topology a VALID single-advertiser record with a random
+  // next-hop subset of `me`'s links, through materializeRouteDb on
+  // `threads` threads (0: automatic). Returns (build ms, destroy ms) per rep.
+  m.def("materialize_routedb_bench",
+        [](const std::string& kind, py::dict opts, const std::string& me, int threads,
+           int reps) {
+          auto g = genLsdb(kind, opts);
+          py::gil_scoped_release nogil;
+          LinkState ls(g.area, "test_node");
+          PrefixState ps;
+          loadLsdb(g, ls, ps);
+          const FlatTopology& f = ls.flat();
+          PrefixHostTable pt;
+          pt.build(ps);
+          const uint32_t s = f.id.at(me);
+          const uint32_t deg = f.rowPtr[s + 1] - f.rowPtr[s];
+          const uint32_t P = uint32_t(pt.prefixes.size());
+          std::vector<uint32_t> meta(P, OGS_ROUTE_VALID | OGS_ROUTE_SELECTED), mask(P), sel(P, 1);
+          std::vector<uint64_t> metric(P);
+          uint64_t x = 0x9E3779B97F4A7C15ull;
+          for (uint32_t p = 0; p < P; ++p) {
+            x ^= x << 13; x ^= x >> 7; x ^= x << 17;
+            mask[p] = (1u << (x % std::min(deg, 32u))) | (1u << ((x >> 8) % std::min(deg, 32u)));
+            metric[p] = 10 + x % 1000;
+          }
+          UnitView v;
+          v.W = 1;
+          v.P = P;
+          v.N = uint32_t(f.names.size());
+          v.meta = meta.data();
+          v.metric = metric.data();
+          v.mask = mask.data();
+          v.maskStride = P;
+          v.sel = sel.data();
+          const int saved = g_materializeThreads;
+          g_materializeThreads = threads;
+          std::vector<std::pair<double, double>> out;
+          std::map<std::string, RibUnicastEntry> statics;
+          std::map<std::string, RouteSelectionResult> cache;
+          for (int r = 0; r < reps; ++r) {
+            auto t0 = std::chrono::steady_clock::now();
+            auto* db = new DecisionRouteDb(materializeRouteDb(ls, f, g.area, me, v, pt, false,
+                                                              false, statics, &cache));
+            const double b = msSince(t0);
+            t0 = std::chrono::steady_clock::now();
+            delete db;
+            out.emplace_back(b, msSince(t0));
+          }
+          g_materializeThreads = saved;
+          return out;
+        },
+        py::arg("kind"), py::arg("opts"), py::arg("me"), py::arg("threads"), py::arg("reps"));
   m.def("route_db_batch_serve_bench",
         [](const std::string& kind, py::dict opts, int serve) {
           auto g = genLsdb(kind, opts);
