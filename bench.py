@@ -724,7 +724,9 @@ def run_c4(args, torch, dist, rank, world, local_rank):
     line["config"]["mode"] = {0: "full SPF per variant", 1: "base-SPF repair",
                               2: "base-SPF repair, changed records only"}[mode]
     if world == 1:
-        set_traffic(line, "c4", ("spf_variant_repair_kernel<true>", "tight_desc_kernel")
+        # the base DAG's descendant rows (tight_desc_kernel) are built once
+        # per base SPF and cached (ogs_route_diff.base_desc): not per sweep
+        set_traffic(line, "c4", "spf_variant_repair_kernel<true>"
                     if mode == 2 else "spf_frontier_kernel<1, true, true, true")
         if not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline_c4()
