@@ -14,6 +14,7 @@ extern int g_frontierWgLds;
 extern int g_waveUpb;
 extern int g_waveOpt;
 extern int g_kspWaveTrace;
+extern int g_kspStop;
 extern int g_msGroup;
 extern int g_routeStream;
 extern int g_routeStreamChunks;
@@ -259,6 +260,11 @@ int ogs_set_option(const char* name, int64_t value) {
       return fail(OGS_E_INVALID, "wave_upb must be 4, 8 or 16");
     }
     ogs::g_waveUpb = int(value);
+    return OGS_OK;
+  }
+  if (std::strcmp(name, "ksp_stop") == 0) {
+    if (value != 0 && value != 1) return fail(OGS_E_INVALID, "ksp_stop must be 0 or 1");
+    ogs::g_kspStop = int(value);
     return OGS_OK;
   }
   if (std::strcmp(name, "ksp_wave_trace") == 0) {
