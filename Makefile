@@ -41,8 +41,8 @@ $(LIB): $(KOBJ)
 $(MOD): $(HOST) $(HOST_H) openr_amd/csrc/py/bindings.cpp $(LIB)
 	$(CXX) -O2 -std=c++17 -fPIC -shared -Wall -Wno-unused-function \
 	  -Iinclude -Iopenr_amd/csrc/host -I$(PY_INC) -I$(PYBIND_INC) \
-	  $(HOST) openr_amd/csrc/py/bindings.cpp -o $@ \
-	  -Lopenr_amd/lib -lopenr_gpu -Wl,-rpath,'$$ORIGIN/lib'
+	  $(HOST) openr_amd/csrc/py/bindings.cpp -o $@.tmp \
+	  -Lopenr_amd/lib -lopenr_gpu -Wl,-rpath,'$$ORIGIN/lib' && mv -f $@.tmp $@
 
 oracle:
 	$(MAKE) -C oracle

@@ -288,9 +288,23 @@ int ogs_host_free(void* hptr);
  *                 one launch per unit set, SPF then the unit's RouteDb write
  *                 stream from LDS; 1 an SPF launch then a route-stream launch
  *                 (dist/next-hop sets through HBM); 0 the fused multi-source
- *                 kernel. Scratch (prefix keys, dist/next-hop sets when
- *                 out->dist / out->nh are NULL) comes from a grow-only
- *                 per-device workspace.
+ *                 kernel; 3 the split pipelined over unit chunks (SPF of a
+ *                 chunk on an internal side stream, its route stream on the
+ *                 caller's; "route_stream_chunks" 1..64, default 4). Scratch
+ *                 (prefix keys, dist/next-hop sets when out->dist / out->nh
+ *                 are NULL) comes from a grow-only per-device workspace.
+ *   "spf_packed_scan": 1 (default) chunk-scan frontier units with one-word
+ *                 next-hop sets relax packed {dist, next hops} words in one
+ *                 phase; 0 two phases (A/B). "spf_scan_batch": 1 (default)
+ *                 a round's chunk records are loaded 8 at a time, 0 one by
+ *                 one (A/B). "frontier_wg_lds": minimum LDS bytes per fused
+ *                 frontier + route-stream workgroup (occupancy probe, 0).
+ *   "wave_opt":   wave-kernel paths, bits: 1 register-resident SPF words
+ *                 (ds_bpermute), 2 (default) identity-segment route path,
+ *                 4 two units per wavefront with 16-bit words.
+ *   "ksp_stop":   1 the KSP2 k = 2 SPF of a destination stops once every
+ *                 distance lowered in a round exceeds the destination's; 0
+ *                 (default) runs to the fixpoint. Both exact.
  *   "spf_frontier": 1 (default) large topologies (edge_src given) solve
  *                 SPF with the frontier kernel (one workgroup per unit,
  *                 only changed rows pushed); 0 the multi-source edge sweep.

@@ -872,6 +872,7 @@ class LinkFailureSweep {
   void exactLaunch(void* stream);
   void exactFetch(void* stream);
   const LinkState& ls_;
+  const PrefixState& ps_;
   std::string me_, area_;
   bool enableV4_, brs_, v4OverV6_;
   PrefixHostTable table_;
@@ -897,6 +898,12 @@ class LinkFailureSweep {
   // zero / negative metrics or 64-bit path sums: one topology per variant
   // through ogs_spf_routes (exactLaunch), updates by calculateUpdate
   bool exact_{false}, exactOrder_{false};
+  // the exact domain runs in chunks of kExactChunk topologies (device and
+  // host memory O(chunk x (E + P)) instead of O(variants x (E + P)));
+  // records of every topology (0 = base, v + 1 = variant v) on the host
+  static constexpr size_t kExactChunk = 256;
+  std::vector<uint32_t> xMeta_, xMask_;
+  std::vector<uint64_t> xMetric_;
   std::vector<DecisionRouteDb> xDb_;
   std::vector<DecisionRouteUpdate> xUpd_;
 };

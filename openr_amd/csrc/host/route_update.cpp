@@ -24,6 +24,7 @@ LinkFailureSweep::LinkFailureSweep(
     const std::vector<std::vector<LinkDown>>& variants, bool enableV4,
     bool enableBestRouteSelection, bool v4OverV6Nexthop)
     : ls_(ls),
+      ps_(ps),
       me_(myNodeName),
       area_(ls.getArea()),
       enableV4_(enableV4),
@@ -80,24 +81,10 @@ LinkFailureSweep::LinkFailureSweep(
     }
   }
 
-  if (exact_) {  // topology 0 = the base, topology v + 1 = variant v
-    for (size_t v = 0; v < variants.size(); ++v) {
-      const uint32_t e0 = uint32_t(hb_.edges.size());
-      hb_.append(f, ps, area_);
-      for (int k = 0; k < kDeadMax; ++k) {
-        const uint32_t e = dead_[v * kDeadMax + k];
-        if (e != OGS_NODE_NONE) hb_.edges[e0 + e] |= OGS_EDGE_DOWN;
-      }
-    }
-  }
   const size_t U = variants.size(), Sn = size_t(std::max(hb_.maxNodes, 1));
   Sp_ = size_t(std::max(hb_.maxPrefixes, 1));
   words_ = (Sp_ + 31) / 32;
   std::vector<ogs_unit> units(U, ogs_unit{0, s});
-  if (exact_) {
-    units.assign(U + 1, ogs_unit{0, s});
-    for (size_t t = 0; t <= U; ++t) units[t].topo = uint32_t(t);
-  }
   const ogs_unit base{0, s};
   dNodeBase_.upload(hb_.nodeBase.data(), hb_.nodeBase.size());
   dDesc_.upload(hb_.topoDesc.data(), hb_.topoDesc.size());
@@ -157,42 +144,96 @@ LinkFailureSweep::LinkFailureSweep(
   dMask_.resize(Uc * W_ * Sp_ * 4);
   dChanged_.resize(Uc * words_ * 4);
   dCounts_.resize(Uc * 2 * 4);
-  if (exact_) {  // base + variants, 64-bit metrics
-    dMeta_.resize((U + 1) * Sp_ * 4);
-    dMetric_.resize((U + 1) * Sp_ * 8);
-    dMask_.resize((U + 1) * W_ * Sp_ * 4);
-  }
 }
 
-// Variants outside the repair kernel's domain: ONE ogs_spf_routes launch
-// over the base (unit 0) and every variant's own topology copy (the failed
+// Variants outside the repair kernel's domain: ogs_spf_routes launches over
+// the base (topology 0) and every variant's own topology copy (the failed
 // links' edges marked down, the same skip the variants kernel applies to its
-// dead-edge list), in the exact extraction order when the area has zero or
-// negative metrics, with 64-bit distances. fetch materialises the records and
+// dead-edge list), kExactChunk topologies per launch so that device and host
+// copies stay bounded, in the exact extraction order when the area has zero
+// or negative metrics, with 64-bit distances. fetch materialises the records and
 // the update is DecisionRouteDb::calculateUpdate (SpfSolver.cpp:21-56) of the
 // base and variant RouteDbs, as Decision::rebuildRoutes computes it.
 void LinkFailureSweep::exactLaunch(void* stream) {
-  ogs_graph g = graph();
-  ogs_prefix_table pt = table();
-  ogs_spf_out out{nullptr, nullptr, dMeta_.as<uint32_t>(), dMetric_.get(),
-                  dMask_.as<uint32_t>(), nullptr};
+  const size_t U = numVariants(), T = U + 1;
+  const FlatTopology& f = ls_.flat();
+  const uint32_t s = f.id.at(me_);
   const uint32_t fl = flags() | OGS_F_WIDE_METRIC | (exactOrder_ ? OGS_F_EXACT_ORDER : 0u);
-  ogsCheck(ogs_spf_routes(&g, &pt, dUnits_.as<ogs_unit>(), int32_t(numVariants() + 1), fl, W_,
-                          &out, stream),
-           "ogs_spf_routes(variant topologies)");
+  xMeta_.assign(T * Sp_, 0);
+  xMetric_.assign(T * Sp_, 0);
+  xMask_.assign(T * W_ * Sp_, 0);
+  DeviceBuffer nodeBase, desc, row, edges, edgeSrc, nflags, pfxBase, advOff, advNode,
+      advMetrics, advMinNh, pfxFlags, units, meta, metric, mask;
+  for (size_t c0 = 0; c0 < T; c0 += kExactChunk) {
+    const size_t c1 = std::min(T, c0 + kExactChunk), n = c1 - c0;
+    HostBatch hb;  // topology t - c0 = the base (t = 0) or variant t - 1
+    for (size_t t = c0; t < c1; ++t) {
+      const uint32_t e0 = uint32_t(hb.edges.size());
+      hb.append(f, ps_, area_);
+      if (t == 0) continue;
+      for (int k = 0; k < kDeadMax; ++k) {
+        const uint32_t e = dead_[(t - 1) * kDeadMax + k];
+        if (e != OGS_NODE_NONE) hb.edges[e0 + e] |= OGS_EDGE_DOWN;
+      }
+    }
+    std::vector<ogs_unit> us(n);
+    for (size_t i = 0; i < n; ++i) us[i] = ogs_unit{uint32_t(i), s};
+    nodeBase.upload(hb.nodeBase.data(), hb.nodeBase.size(), stream);
+    desc.upload(hb.topoDesc.data(), hb.topoDesc.size(), stream);
+    row.upload(hb.rowPtr.data(), hb.rowPtr.size(), stream);
+    edges.upload(hb.edges.data(), hb.edges.size(), stream);
+    edgeSrc.upload(hb.edgeSrc.data(), hb.edgeSrc.size(), stream);
+    nflags.upload(hb.nodeFlags.data(), hb.nodeFlags.size(), stream);
+    pfxBase.upload(hb.pfxBase.data(), hb.pfxBase.size(), stream);
+    advOff.upload(hb.advOff.data(), hb.advOff.size(), stream);
+    advNode.upload(hb.advNode.data(), hb.advNode.size(), stream);
+    advMetrics.upload(hb.advMetrics.data(), hb.advMetrics.size(), stream);
+    advMinNh.upload(hb.advMinNh.data(), hb.advMinNh.size(), stream);
+    pfxFlags.upload(hb.pfxFlags.data(), hb.pfxFlags.size(), stream);
+    units.upload(us.data(), us.size(), stream);
+    meta.resize(n * Sp_ * 4);
+    metric.resize(n * Sp_ * 8);
+    mask.resize(n * W_ * Sp_ * 4);
+    ogs_graph g{};
+    g.num_topos = int32_t(n);
+    g.max_nodes = hb.maxNodes;
+    g.max_edges = hb.maxEdges;
+    g.max_degree = hb.maxDegree;
+    g.topo_desc = desc.as<uint32_t>();
+    g.node_base = nodeBase.as<uint32_t>();
+    g.row_ptr = row.as<uint32_t>();
+    g.edges = edges.as<uint64_t>();
+    g.node_flags = nflags.as<uint8_t>();
+    g.edge_src = edgeSrc.as<uint32_t>();
+    ogs_prefix_table pt{};
+    pt.max_prefixes = hb.maxPrefixes;
+    pt.max_advertisements = hb.maxAdvs;
+    pt.pfx_base = pfxBase.as<uint32_t>();
+    pt.adv_off = advOff.as<uint32_t>();
+    pt.adv_node = advNode.as<uint32_t>();
+    pt.adv_metrics = advMetrics.as<int32_t>();
+    pt.adv_min_nh = advMinNh.as<int64_t>();
+    pt.pfx_flags = pfxFlags.as<uint8_t>();
+    ogs_spf_out out{nullptr, nullptr, meta.as<uint32_t>(), metric.get(), mask.as<uint32_t>(),
+                    nullptr};
+    ogsCheck(ogs_spf_routes(&g, &pt, units.as<ogs_unit>(), int32_t(n), fl, W_, &out, stream),
+             "ogs_spf_routes(variant topologies)");
+    meta.download(xMeta_.data() + c0 * Sp_, n * Sp_, stream);
+    metric.download(xMetric_.data() + c0 * Sp_, n * Sp_, stream);
+    // mask rows [(i * W + w) * Sp + p] of the chunk follow the previous ones
+    mask.download(xMask_.data() + c0 * W_ * Sp_, n * W_ * Sp_, stream);
+    ogsCheck(ogs_stream_sync(stream), "ogs_stream_sync");  // buffers reused
+  }
   baseRun_ = recordsRun_ = true;
   changedOnlyRun_ = false;
 }
 
-void LinkFailureSweep::exactFetch(void* stream) {
+void LinkFailureSweep::exactFetch(void* /*stream*/) {
   if (!recordsRun_) throw std::logic_error("LinkFailureSweep: launch() first");
-  const size_t U = numVariants(), T = U + 1;
-  std::vector<uint32_t> meta(T * Sp_), mask(T * W_ * Sp_);
-  std::vector<uint64_t> metric(T * Sp_);
-  dMeta_.download(meta.data(), meta.size(), stream);
-  dMetric_.download(metric.data(), metric.size(), stream);
-  dMask_.download(mask.data(), mask.size(), stream);
-  ogsCheck(ogs_stream_sync(stream), "ogs_stream_sync");
+  const size_t U = numVariants();
+  const std::vector<uint32_t>& meta = xMeta_;
+  const std::vector<uint32_t>& mask = xMask_;
+  const std::vector<uint64_t>& metric = xMetric_;
   const FlatTopology& f = ls_.flat();
   auto dbOf = [&](size_t t) {
     DecisionRouteDb db;
