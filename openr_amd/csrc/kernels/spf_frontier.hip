@@ -30,6 +30,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <type_traits>
 
 #include "openr_gpu.h"
 #include "route_core.h"
@@ -300,8 +301,11 @@ template <bool MODS>
 __device__ __forceinline__ void frontier_spf_packed(
     uint32_t N, uint32_t s, const uint64_t* __restrict__ edges,
     const uint64_t* __restrict__ chunks, uint32_t C, bool hop,
-    const uint32_t* __restrict__ gRow, uint32_t e0, uint64_t* dn, uint16_t* stamp,
+    const uint32_t* __restrict__ gRow, uint32_t e0, uint64_t* dn, uint8_t* stamp,
     uint64_t* tp, const DeadEdges& dead, bool serial) {
+  // u8 round stamps (1 B per node, so 8 C3 units fit a CU): after 256
+  // rounds a stale stamp can match again -- that node is pushed once more
+  // with its current word, a no-op for the monotone fixpoint
   constexpr uint32_t kInf = 0xFFFFFFFFu;
   const int tid = threadIdx.x;
   for (uint32_t v = tid; v < N; v += kBlock) {
@@ -318,7 +322,7 @@ __device__ __forceinline__ void frontier_spf_packed(
     bool changed = false;
     scan_chunks(chunks, C, serial, [&](uint64_t ch) {
       const uint32_t v = uint32_t(ch) & OGS_EDGE_DST_MASK;
-      if (stamp[v] != r) return;
+      if (stamp[v] != uint8_t(r)) return;
       if ((uint32_t(ch) & kChunkDrained) && v != s) return;
       const uint64_t xv = dn[v];
       const uint32_t dv = static_cast<uint32_t>(xv), nv = static_cast<uint32_t>(xv >> 32);
@@ -345,7 +349,7 @@ __device__ __forceinline__ void frontier_spf_packed(
                                           static_cast<unsigned long long>(old),
                                           static_cast<unsigned long long>(nw));
           if (seen == old) {
-            stamp[t] = uint16_t(r + 1);
+            stamp[t] = uint8_t(r + 1);
             changed = true;
             break;
           }
@@ -646,9 +650,9 @@ __device__ __forceinline__ void queue_spf_packed(
 }
 
 uint32_t frontier_lds_bytes(uint32_t Sn, int W, bool queue = false, bool ninfo = true,
-                            bool stamps = true) {
+                            bool stamps = true, bool stamp8 = false) {
   const uint32_t core = 4u * (((Sn + 3u) & ~3u) + ((Sn * W + 3u) & ~3u));
-  if (!queue) return core + 2u * ((Sn + 1u) & ~1u);
+  if (!queue) return core + (stamp8 ? ((Sn + 3u) & ~3u) : 2u * ((Sn + 1u) & ~1u));
   // + u32 stamps (not with folded stamps) + two u16 node lists (+ u32 node
   // info [Sn + 1])
   return core + (stamps ? 4u * ((Sn + 3u) & ~3u) : 0u) + 2u * 2u * ((Sn + 1u) & ~1u) +
@@ -718,7 +722,8 @@ __global__ __launch_bounds__(kBlock) void spf_frontier_kernel(
   if constexpr (QMODE == 4) {  // packed words, chunk scan
     frontier_spf_packed<MODS>(N, s, g.edges + e0, chunks + size_t(unit.topo) * cap,
                               nChunk[unit.topo], (flags & OGS_F_HOP_METRIC) != 0, gRow, e0,
-                              dn64, stamp, tp, dead, (flags & kFlagScanSerial) != 0);
+                              dn64, reinterpret_cast<uint8_t*>(stamp), tp, dead,
+                              (flags & kFlagScanSerial) != 0);
   } else if constexpr (PACKED) {
     queue_spf_packed<MODS, QMODE == 3>(N, s, g.edges + e0, gRow, e0, nflags,
                            (flags & OGS_F_HOP_METRIC) != 0, dn64, stamp32, q0, q1,
@@ -749,13 +754,15 @@ __global__ __launch_bounds__(kBlock) void spf_frontier_kernel(
     }
   }
   if constexpr (ROUTES) {
-    // per-node record flags (8 bits) over the dead stamps
-    uint16_t* rMeta = stamp;
+    // per-node record flags (8 bits) over the dead stamps (u8 stamps in
+    // the packed chunk scan: one byte per node there)
+    using RMeta = std::conditional_t<QMODE == 4, uint8_t, uint16_t>;
+    RMeta* rMeta = reinterpret_cast<RMeta*>(stamp);
     for (uint32_t v = tid; v < N; v += kBlock) {
       uint32_t cnt = 0;
 #pragma unroll
       for (int w = 0; w < W; ++w) cnt += __popc(nOf(v, w));
-      rMeta[v] = uint16_t(node_route_meta(v, s, dOf(v) != kInf, cnt, nflags[v]));
+      rMeta[v] = RMeta(node_route_meta(v, s, dOf(v) != kInf, cnt, nflags[v]));
     }
     __syncthreads();
     const uint32_t Sp = uint32_t(pt.max_prefixes);
@@ -859,7 +866,8 @@ hipError_t launch_frontier_q(const ogs_graph& g, const ogs_prefix_table& pt,
                              const ogs_route_diff& diff) {
   const bool scan = QMODE == 0 || QMODE == 4;  // chunk-scan forms: no lists
   const bool ninfo = scan || ninfo_in_lds(uint32_t(g.max_nodes), W);
-  uint32_t lds = frontier_lds_bytes(uint32_t(g.max_nodes), W, !scan, ninfo, QMODE != 3);
+  uint32_t lds =
+      frontier_lds_bytes(uint32_t(g.max_nodes), W, !scan, ninfo, QMODE != 3, QMODE == 4);
   // occupancy probe (A/B): fewer workgroups per CU stagger the SPF and
   // route-stream phases of the resident units
   if (ROUTES && lds < uint32_t(g_frontierWgLds)) lds = uint32_t(g_frontierWgLds);
