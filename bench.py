@@ -533,7 +533,8 @@ def run_c3(args, torch, dist, rank, world, local_rank):
                      "getRouteDbComputed_ms": round(serve_ms, 2),
                      "routes_per_node": round(nroutes, 1),
                      "note": "RouteDbBatch (C++ drop-in) over all 2,080 sources, then "
-                             "3 nodes served; rank 0, after the timed region"}
+                             "3 nodes served after one untimed serve (warm process); "
+                             "rank 0, after the timed region"}
     # §8(f) f4, host only: the same fabric as one KvStore publication
     # (2,080 "adj:" + 208k "prefix:" keys, compact thrift) decoded and
     # ingested per key (Decision::updateKeyInLsdb) into a fresh LSDB
