@@ -39,7 +39,10 @@
 
 namespace ogs {
 
-constexpr uint32_t kChunk = 8;
+#ifndef OGS_CHUNK_EDGES  // edges per chunk record (A/B builds: -DOGS_CHUNK_EDGES=16)
+#define OGS_CHUNK_EDGES 8
+#endif
+constexpr uint32_t kChunk = OGS_CHUNK_EDGES;
 constexpr uint32_t kChunkCntShift = 21;  // bits 21..24: edge count - 1
 constexpr uint32_t kChunkDrained = 1u << 25;
 constexpr int kMaxDead = 8;  // ogs_unit_mods.dead_per_unit limit
