@@ -350,7 +350,9 @@ class LinkState {
   std::string area_, myNodeName_;
   std::map<std::string, AdjacencyDatabase> adjDbs_;
   std::map<Link::Key, LinkPtr> links_;                      // all links
-  std::unordered_map<std::string, std::set<Link::Key>> byNode_;
+  // per node its links in key order (LinkState.h linkMap_), with the link
+  // itself: the flatten walks rows without a links_ lookup per edge
+  std::unordered_map<std::string, std::map<Link::Key, LinkPtr>> byNode_;
   std::unordered_map<std::string, bool> overloaded_;
   std::unordered_map<std::string, uint64_t> metricInc_;
   mutable std::map<std::pair<std::string, bool>, SpfResult> spfMemo_;

@@ -126,7 +126,8 @@ LinkState::LinkStateChange LinkState::updateAdjacencyDatabase(
   // merge old vs new link sets, both in key order
   std::vector<Link::Key> oldKeys;
   if (auto it = byNode_.find(name); it != byNode_.end()) {
-    oldKeys.assign(it->second.begin(), it->second.end());
+    oldKeys.reserve(it->second.size());
+    for (const auto& [k, _] : it->second) oldKeys.push_back(k);
   }
   auto ni = fresh.begin();
   size_t oi = 0;
@@ -135,8 +136,8 @@ LinkState::LinkStateChange LinkState::updateAdjacencyDatabase(
       const LinkPtr& l = ni->second;
       ch.topologyChanged |= l->isUp();
       links_[l->key()] = l;
-      byNode_[l->firstNodeName()].insert(l->key());
-      byNode_[l->secondNodeName()].insert(l->key());
+      byNode_[l->firstNodeName()].emplace(l->key(), l);
+      byNode_[l->secondNodeName()].emplace(l->key(), l);
       ch.addedLinks.push_back(l);
       structural = true;
       ++ni;
@@ -277,7 +278,9 @@ LinkState::LinkStateChange LinkState::deleteAdjacencyDatabase(
   auto it = adjDbs_.find(name);
   if (it == adjDbs_.end()) return ch;
   if (auto bn = byNode_.find(name); bn != byNode_.end()) {
-    for (const auto& key : std::set<Link::Key>(bn->second)) {
+    std::vector<Link::Key> keys;
+    for (const auto& [k, _] : bn->second) keys.push_back(k);
+    for (const auto& key : keys) {
       const LinkPtr l = links_.at(key);
       byNode_.at(l->getOtherNodeName(name)).erase(key);
       links_.erase(key);
@@ -294,7 +297,7 @@ LinkState::LinkStateChange LinkState::deleteAdjacencyDatabase(
 std::vector<LinkPtr> LinkState::linksFromNode(const std::string& n) const {
   std::vector<LinkPtr> out;
   if (auto it = byNode_.find(n); it != byNode_.end()) {
-    for (const auto& k : it->second) out.push_back(links_.at(k));
+    for (const auto& [_, l] : it->second) out.push_back(l);
   }
   return out;
 }
@@ -327,38 +330,50 @@ const FlatTopology& LinkState::flat() const {
   auto f = std::make_unique<FlatTopology>();
   f->version = nextVersionStamp();
   f->names.reserve(adjDbs_.size());
-  for (const auto& [n, _] : adjDbs_) {  // byte-wise name order == id order
+  f->id.reserve(adjDbs_.size());
+  f->nodeFlags.reserve(adjDbs_.size());
+  for (const auto& [n, db] : adjDbs_) {  // byte-wise name order == id order
     f->id.emplace(n, uint32_t(f->names.size()));
     f->names.push_back(n);
+    // the node's flags straight from its adjacency database (overloaded_ /
+    // metricInc_ mirror these fields, set by updateAdjacencyDatabase)
+    uint8_t fl = db.isOverloaded ? OGS_NODE_OVERLOADED : 0;
+    const int64_t inc = db.nodeMetricIncrementVal;
+    if (static_cast<int>(static_cast<uint64_t>(inc)) > 0) fl |= OGS_NODE_SOFTDRAIN;
+    if (inc != 0) fl |= OGS_NODE_METRICINC;
+    f->nodeFlags.push_back(fl);
   }
   const uint32_t N = uint32_t(f->names.size());
   if (N > OGS_MAX_NODES_PER_TOPO) throw std::domain_error("too many nodes");
-  // rows in canonical link order, one Link lookup per directed edge; the
-  // reverse of every edge by pairing a link's two occurrences (sorted by
-  // Link*), so the neighbour id, its row slot and its overload bit come from
-  // indexes instead of string-keyed lookups
+  // Rows in canonical link order straight from links_ (key order): every
+  // link is appended to both endpoint rows, so each row is a subsequence of
+  // the sorted link sequence (the order of byNode_'s key-ordered sets), and
+  // a link's two directed edges are placed together -- the reverse of every
+  // edge is known without a sort or a string-keyed lookup per edge.
   f->rowPtr.assign(N + 1, 0);
-  f->nodeFlags.assign(N, 0);
-  std::vector<std::pair<const Link*, uint32_t>> occ;  // (link, directed edge)
-  std::vector<uint32_t> owner;
-  for (uint32_t u = 0; u < N; ++u) {
-    const std::string& un = f->names[u];
-    if (isNodeOverloaded(un)) f->nodeFlags[u] |= OGS_NODE_OVERLOADED;
-    const uint64_t inc = getNodeMetricIncrement(un);
-    if (static_cast<int>(inc) > 0) f->nodeFlags[u] |= OGS_NODE_SOFTDRAIN;
-    if (inc != 0) f->nodeFlags[u] |= OGS_NODE_METRICINC;
-    uint32_t j = 0;
-    if (auto it = byNode_.find(un); it != byNode_.end()) {
-      for (const auto& key : it->second) {
-        Link* l = links_.at(key).get();
-        occ.emplace_back(l, uint32_t(f->edgeLink.size()));
-        f->edgeLink.push_back(l);
-        owner.push_back(u);
-        ++j;
-      }
+  // links_ is ordered by (first node, ...) and names by name: the first
+  // endpoint's id follows a cursor; only the second is looked up
+  struct End {
+    const Link* l;
+    uint32_t a, b;
+  };
+  std::vector<End> ends;
+  ends.reserve(links_.size());
+  uint32_t cur = 0;
+  for (const auto& [_, lp] : links_) {
+    const std::string& n1 = lp->firstNodeName();
+    while (cur < N && f->names[cur] < n1) ++cur;
+    const auto b = f->id.find(lp->secondNodeName());
+    if (cur == N || f->names[cur] != n1 || b == f->id.end() || b->second == cur) {
+      throw std::logic_error("LinkState::flat: link with one endpoint");
     }
-    f->rowPtr[u + 1] = f->rowPtr[u] + j;
-    f->maxDegree = std::max<int>(f->maxDegree, int(j));
+    ends.push_back(End{lp.get(), cur, b->second});
+    ++f->rowPtr[cur + 1];
+    ++f->rowPtr[b->second + 1];
+  }
+  for (uint32_t u = 0; u < N; ++u) {
+    f->maxDegree = std::max<int>(f->maxDegree, int(f->rowPtr[u + 1]));
+    f->rowPtr[u + 1] += f->rowPtr[u];
   }
   // rows of 512+ edges (a hub / route reflector): the edge word's reverse
   // slot saturates at 511 and the exact slots go to rslotExt (LinkState.cpp:
@@ -366,19 +381,24 @@ const FlatTopology& LinkState::flat() const {
   const bool extSlots = f->maxDegree >= OGS_MAX_DEGREE;
   const uint32_t E = f->rowPtr[N];
   if (extSlots) f->rslotExt.assign(E, 0u);
-  std::vector<uint32_t> rev(E, 0xFFFFFFFFu);
-  std::sort(occ.begin(), occ.end());
-  for (size_t i = 0; i + 1 < occ.size(); ++i) {
-    if (occ[i].first != occ[i + 1].first) continue;
-    rev[occ[i].second] = occ[i + 1].second;
-    rev[occ[i + 1].second] = occ[i].second;
-    ++i;
+  f->edgeLink.assign(E, nullptr);
+  std::vector<uint32_t> owner(E), rev(E);
+  {
+    std::vector<uint32_t> pos(f->rowPtr.begin(), f->rowPtr.end() - 1);
+    for (const End& x : ends) {
+      const uint32_t a = x.a, b = x.b;
+      const uint32_t ea = pos[a]++, eb = pos[b]++;
+      f->edgeLink[ea] = f->edgeLink[eb] = const_cast<Link*>(x.l);
+      owner[ea] = a;
+      owner[eb] = b;
+      rev[ea] = eb;
+      rev[eb] = ea;
+    }
   }
   f->edges.resize(E);
   for (uint32_t e = 0; e < E; ++e) {
     const Link* l = f->edgeLink[e];
     const uint32_t r = rev[e];
-    if (r == 0xFFFFFFFFu) throw std::logic_error("LinkState::flat: link with one endpoint");
     const uint32_t v = owner[r];
     const uint32_t rslot = r - f->rowPtr[v];
     if (extSlots) f->rslotExt[e] = rslot;

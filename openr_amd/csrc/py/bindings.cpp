@@ -1870,6 +1870,34 @@ PYBIND11_MODULE(_decision, m) {
           return out;
         },
         py::arg("kind"), py::arg("opts"), py::arg("me"), py::arg("threads"), py::arg("reps"));
+  // Host-only split of a cold single-area build's preparation (no device):
+  // LinkState::flat() (CSR flatten), PrefixHostTable::build and
+  // HostBatch::appendPrefixes (the packed prefix table) in ms, per rep on a
+  // fresh LinkState / PrefixState (ingestion untimed).
+  m.def("prepare_split_bench",
+        [](const std::string& kind, py::dict opts, int reps) {
+          auto g = genLsdb(kind, opts);
+          py::gil_scoped_release nogil;
+          std::vector<std::tuple<double, double, double>> out;
+          for (int r = 0; r < reps; ++r) {
+            LinkState ls(g.area, "test_node");
+            PrefixState ps;
+            loadLsdb(g, ls, ps);
+            auto t0 = std::chrono::steady_clock::now();
+            const FlatTopology& f = ls.flat();
+            const double a = msSince(t0);
+            t0 = std::chrono::steady_clock::now();
+            PrefixHostTable pt;
+            pt.build(ps);
+            const double b = msSince(t0);
+            t0 = std::chrono::steady_clock::now();
+            HostBatch hb;
+            hb.appendPrefixes(f, ps, g.area);
+            out.emplace_back(a, b, msSince(t0));
+          }
+          return out;
+        },
+        py::arg("kind"), py::arg("opts"), py::arg("reps"));
   m.def("route_db_batch_serve_bench",
         [](const std::string& kind, py::dict opts, int serve) {
           auto g = genLsdb(kind, opts);
