@@ -281,7 +281,8 @@ int ogs_host_free(void* hptr);
  *                 3 multi-source edge-parallel kernel (needs edge_src),
  *                 64 / 128 / 256 split-state kernel at that unit width.
  *   "wave_wg_lds": minimum LDS bytes per wave-kernel workgroup (occupancy
- *                 probe; 0 default).
+ *                 probe; 0 default). "wave_upb": units (wavefronts) per
+ *                 wave-kernel workgroup, 4 (default), 8 or 16.
  *   "ms_group":   sources per workgroup of the multi-source kernel (0 auto,
  *                 1, 2, 4).
  *   "route_stream": RouteDb form for large shared topologies: 2 (default)
@@ -293,11 +294,18 @@ int ogs_host_free(void* hptr);
  *                 caller's; "route_stream_chunks" 1..64, default 4). Scratch
  *                 (prefix keys, dist/next-hop sets when out->dist / out->nh
  *                 are NULL) comes from a grow-only per-device workspace.
+ *                 "route_store_nt", bits: 1 the RouteDb stream's 16-B stores
+ *                 are non-temporal (else ordinary write-back stores), 2 the
+ *                 wave kernel's output stores are; default 2 (A/B).
  *   "spf_packed_scan": 1 (default) chunk-scan frontier units with one-word
  *                 next-hop sets relax packed {dist, next hops} words in one
  *                 phase; 0 two phases (A/B). "spf_scan_batch": 1 (default)
  *                 a round's chunk records are loaded 8 at a time, 0 one by
- *                 one (A/B). "frontier_wg_lds": minimum LDS bytes per fused
+ *                 one (A/B). "spf_seed_row": 1 (default) round 1 of the
+ *                 chunk scan relaxes the source's row directly, 0 it scans
+ *                 every chunk record (A/B). "spf_scan_pair": 1 the packed
+ *                 chunk scan relaxes a batch's active chunks two at a time,
+ *                 0 (default) one at a time. "frontier_wg_lds": minimum LDS bytes per fused
  *                 frontier + route-stream workgroup (occupancy probe, 0).
  *   "wave_opt":   wave-kernel paths, bits: 1 register-resident SPF words
  *                 (ds_bpermute), 2 (default) identity-segment route path,
@@ -312,7 +320,11 @@ int ogs_host_free(void* hptr);
  *                 lists for sparse topologies (max degree <= 16; one phase
  *                 over packed {dist, next hops} words when the next-hop sets
  *                 fit one word), the chunk scan otherwise; 0 always the scan;
- *                 1 lists whenever they fit in LDS; 2 lists, two phases.
+ *                 1 lists whenever they fit in LDS; 2 lists, two phases; 3
+ *                 packed with the push stamps folded into the words (A/B).
+ *                 "spf_ninfo": 1 (default) the list forms keep row begin |
+ *                 drained per node in LDS, 0 read them from the CSR, -1 the
+ *                 CSR form whenever that raises the units per CU.
  *   "spf_global": 0 (default) units whose SPF state does not fit LDS
  *                 (tens of thousands of nodes) run the global-state path
  *                 (dist / next-hop sets / frontier lists in HBM, one 1024-
@@ -326,6 +338,11 @@ int ogs_host_free(void* hptr);
  *                 only; 0 all state in HBM (A/B).
  *   "ksp_hbm":    1 every KSP unit on the HBM-state path (A/B, tests); 0
  *                 (default) only units past LDS and OGS_F_EXACT_ORDER units.
+ *                 "ksp_wave_trace": 1 (default) path traces of 32-bit
+ *                 distance units run on a whole wavefront, 0 on one lane.
+ *   "c4_desc":    1 (default) the link-failure repair (OGS_F_INCREMENTAL)
+ *                 seeds its affected set from precomputed descendant rows of
+ *                 the base tight DAG (S_n <= 16384), 0 by growth rounds.
  *   "ksp_queue":  KSP2 batch SPF: 1 (default) LDS node lists, 0 the pull
  *                 fixpoint. "ksp_stage": -1 (default) auto, 0 CSR read
  *                 from HBM/L2, 1 row offsets in LDS, 2 rows + edges in LDS. */

@@ -19,6 +19,9 @@ extern int g_msGroup;
 extern int g_routeStream;
 extern int g_routeStreamChunks;
 extern int g_spfScanBatch;
+extern int g_routeStoreNt;
+extern int g_spfSeedRow;
+extern int g_spfScanPair;
 extern int g_spfPackedScan;
 extern int g_spfFrontier;
 extern int g_spfGlobal;
@@ -189,6 +192,21 @@ int ogs_set_option(const char* name, int64_t value) {
   if (std::strcmp(name, "spf_packed_scan") == 0) {
     if (value != 0 && value != 1) return fail(OGS_E_INVALID, "spf_packed_scan must be 0 or 1");
     ogs::g_spfPackedScan = int(value);
+    return OGS_OK;
+  }
+  if (std::strcmp(name, "route_store_nt") == 0) {
+    if (value < 0 || value > 3) return fail(OGS_E_INVALID, "route_store_nt must be in [0, 3]");
+    ogs::g_routeStoreNt = int(value);
+    return OGS_OK;
+  }
+  if (std::strcmp(name, "spf_scan_pair") == 0) {
+    if (value != 0 && value != 1) return fail(OGS_E_INVALID, "spf_scan_pair must be 0 or 1");
+    ogs::g_spfScanPair = int(value);
+    return OGS_OK;
+  }
+  if (std::strcmp(name, "spf_seed_row") == 0) {
+    if (value != 0 && value != 1) return fail(OGS_E_INVALID, "spf_seed_row must be 0 or 1");
+    ogs::g_spfSeedRow = int(value);
     return OGS_OK;
   }
   if (std::strcmp(name, "spf_scan_batch") == 0) {

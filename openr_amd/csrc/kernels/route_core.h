@@ -17,6 +17,21 @@
 
 namespace ogs {
 
+// Store flavour of route / SPF output writes (launch flag bit kFlagNtStores,
+// set per kernel family from the "route_store_nt" option bits):
+// non-temporal stores, or ordinary write-back ones.
+constexpr uint32_t kFlagNtStores = 1u << 28;
+extern int g_routeStoreNt;
+
+template <typename T>
+__device__ __forceinline__ void store_out(T* p, T v, bool nt) {
+  if (nt) {
+    __builtin_nontemporal_store(v, p);
+  } else {
+    *p = v;
+  }
+}
+
 struct RouteCfg {
   bool enableV4, v4OverV6, bestRouteSel;
 };

@@ -47,10 +47,10 @@ __device__ __forceinline__ uint32_t node_route_meta(uint32_t v, uint32_t s,
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-__device__ __forceinline__ void nt_store4(uint32_t* p, uint32_t a, uint32_t b,
-                                          uint32_t c, uint32_t d) {
-  u32x4 v = {a, b, c, d};
-  __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
+// one 16-B output store (route_core.h store_out: kFlagNtStores flavour)
+__device__ __forceinline__ void store4(uint32_t* p, uint32_t a, uint32_t b, uint32_t c,
+                                       uint32_t d, bool nt) {
+  store_out(reinterpret_cast<u32x4*>(p), u32x4{a, b, c, d}, nt);
 }
 
 template <int W>
@@ -103,7 +103,7 @@ __device__ __forceinline__ bool route_changed(const Rec<W>& r, const DiffCtx& d,
 // Streams unit u's P route records (rows of stride Sp). rec(v, r) fills
 // meta / metric / mask of node v's record; sv is the unit's SPF state for
 // route_one. Four consecutive prefixes per lane: one 16-B key load and one
-// 16-B non-temporal store per output array. OUTS3: the caller guarantees
+// 16-B store per output array (non-temporal when nt). OUTS3: the caller guarantees
 // meta, metric and mask outputs and no sel -- the stores are then
 // unconditional, so every path leaves the same number of stores in flight
 // and the key prefetch's wait stays partial (see the loop below).
@@ -112,7 +112,7 @@ __device__ __forceinline__ void stream_routes(
     const ogs_prefix_table& pt, const uint32_t* __restrict__ tkey, uint32_t p0,
     uint32_t P, uint32_t Sp, size_t u, uint32_t s,
     const uint8_t* __restrict__ nflags, const View& sv, const RouteCfg& cfg,
-    const ogs_spf_out& out, RecFn rec, const DiffCtx* diff = nullptr) {
+    const ogs_spf_out& out, RecFn rec, const DiffCtx* diff = nullptr, bool nt = true) {
   uint32_t upd = 0, del = 0;
   constexpr uint32_t kInf = 0xFFFFFFFFu;
   const int tid = threadIdx.x;
@@ -153,14 +153,14 @@ __device__ __forceinline__ void stream_routes(
     one(q + 1, k4.y, r1);
     one(q + 2, k4.z, r2);
     one(q + 3, k4.w, r3);
-    if (OUTS3 || oMeta) nt_store4(oMeta + q, r0.meta, r1.meta, r2.meta, r3.meta);
-    if (OUTS3 || oMetric) nt_store4(oMetric + q, r0.metric, r1.metric, r2.metric, r3.metric);
-    if (!OUTS3 && oSel) nt_store4(oSel + q, r0.sel, r1.sel, r2.sel, r3.sel);
+    if (OUTS3 || oMeta) store4(oMeta + q, r0.meta, r1.meta, r2.meta, r3.meta, nt);
+    if (OUTS3 || oMetric) store4(oMetric + q, r0.metric, r1.metric, r2.metric, r3.metric, nt);
+    if (!OUTS3 && oSel) store4(oSel + q, r0.sel, r1.sel, r2.sel, r3.sel, nt);
     if (OUTS3 || oMask) {
 #pragma unroll
       for (int w = 0; w < W; ++w) {
-        nt_store4(oMask + size_t(w) * Sp + q, r0.mask[w], r1.mask[w], r2.mask[w],
-                  r3.mask[w]);
+        store4(oMask + size_t(w) * Sp + q, r0.mask[w], r1.mask[w], r2.mask[w], r3.mask[w],
+               nt);
       }
     }
     if constexpr (DIFF) {

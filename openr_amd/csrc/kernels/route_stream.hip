@@ -122,7 +122,8 @@ __global__ __launch_bounds__(kBlock) void route_stream_kernel(
                      r.metric = rMetric[v];
 #pragma unroll
                      for (int w = 0; w < W; ++w) r.mask[w] = rMask[w * Sn + v];
-                   });
+                   },
+                   nullptr, (flags & kFlagNtStores) != 0);
 }
 
 // ---- per-(device, stream) workspace (grow-only; freed at process exit) ----
@@ -165,6 +166,14 @@ hipError_t workspace(size_t bytes, hipStream_t stream, void** out) {
 int g_routeStream = 2;
 // "route_stream_chunks" option: unit chunks of the pipelined split (3)
 int g_routeStreamChunks = 4;
+// "route_store_nt" option, bits: 1 the RouteDb stream's 16-B stores are
+// non-temporal (else ordinary write-back stores), 2 the wave kernel's output
+// stores are. Default 2. The bare C3 store pattern drains faster with
+// ordinary stores (tools/store_pattern.hip: 5.4 vs 5.0 TB/s); the C3 build
+// gains 0.5-2 % from them (1.278 vs 1.283 ms mean of 5, 1.282-1.295 vs
+// 1.303-1.325 ms), the C2 wave kernel loses 3 % (10.9 vs 10.6 us):
+// profiles/r03_store_pattern.log, r03_store_nt_ab.log.
+int g_routeStoreNt = 2;
 
 // Side stream + events of the pipelined split, per (device, caller stream).
 namespace {
@@ -230,6 +239,7 @@ hipError_t launch_route_stream(const ogs_graph& g, const ogs_prefix_table& pt,
                                        int(lds));
     if (e != hipSuccess) return e;
   }
+  if (g_routeStoreNt & 1) flags |= kFlagNtStores;
   hipLaunchKernelGGL(k, dim3(nUnits), dim3(kBlock), lds, stream, g, pt, key,
                      units, flags, dist, nh, out);
   return hipGetLastError();

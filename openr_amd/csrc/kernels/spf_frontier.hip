@@ -163,6 +163,50 @@ __device__ __forceinline__ void scan_chunks(const uint64_t* __restrict__ chunks,
   }
 }
 
+// Paired form of scan_chunks for the packed SPF ("spf_scan_pair"): a
+// batch's active chunks (test(ch): the node changed last round) are relaxed
+// two at a time with both chunks' edge loads in flight together -- the
+// one-at-a-time form waits one L2 round trip per active chunk. The batch is
+// walked unrolled with one pending record (no dynamic register indexing).
+template <bool MODS, typename Test, typename Relax>
+__device__ __forceinline__ void scan_chunks_pair(const uint64_t* __restrict__ chunks,
+                                                 uint32_t C, const uint64_t* __restrict__ edges,
+                                                 const DeadEdges& dead, Test test,
+                                                 Relax relax) {
+  const uint32_t tid = threadIdx.x;
+  for (uint32_t c0 = tid; c0 < C; c0 += kScanBatch * kBlock) {
+    uint64_t chs[kScanBatch];
+#pragma unroll
+    for (int k = 0; k < kScanBatch; ++k) {
+      const uint32_t c = c0 + uint32_t(k) * kBlock;
+      chs[k] = c < C ? chunks[c] : ~0ull;
+    }
+    uint64_t pend = 0;
+    bool has = false;
+#pragma unroll
+    for (int k = 0; k < kScanBatch; ++k) {
+      if (c0 + uint32_t(k) * kBlock < C && test(chs[k])) {
+        if (has) {
+          uint64_t xa[kChunk], xb[kChunk];
+          load_chunk<MODS>(edges, pend, xa, dead);
+          load_chunk<MODS>(edges, chs[k], xb, dead);
+          relax(pend, xa);
+          relax(chs[k], xb);
+          has = false;
+        } else {
+          pend = chs[k];
+          has = true;
+        }
+      }
+    }
+    if (has) {
+      uint64_t xa[kChunk];
+      load_chunk<MODS>(edges, pend, xa, dead);
+      relax(pend, xa);
+    }
+  }
+}
+
 // One unit's SPF into LDS (dist[v], nh[v*W + w]); returns after the final
 // workgroup barrier. stamp[] is scratch.
 template <int W, bool MODS>
@@ -170,7 +214,8 @@ __device__ __forceinline__ void frontier_spf(
     uint32_t N, uint32_t s, const uint64_t* __restrict__ edges,
     const uint64_t* __restrict__ chunks, uint32_t C, bool hop,
     const uint32_t* __restrict__ gRow, uint32_t e0, uint32_t* dist,
-    uint32_t* nh, uint16_t* stamp, uint64_t* tp, const DeadEdges& dead, bool serial) {
+    uint32_t* nh, uint16_t* stamp, uint64_t* tp, const DeadEdges& dead, bool serial,
+    bool seedRow) {
   constexpr uint32_t kInf = 0xFFFFFFFFu;
   const int tid = threadIdx.x;
   for (uint32_t v = tid; v < N; v += kBlock) {
@@ -189,7 +234,27 @@ __device__ __forceinline__ void frontier_spf(
   // records are loaded kScanBatch at a time (independent L2 loads in
   // flight) before their stamps are tested, instead of one dependent load
   // per record.
-  uint32_t r = 1;
+  // round 1 is the source's row alone: relaxed directly, one edge per thread
+  // ("spf_seed_row"; off: round 1 scans like the others)
+  if (seedRow) {
+    const uint32_t b = gRow[s] - e0, n = gRow[s + 1] - e0 - b;
+    for (uint32_t j = tid; j < n; j += kBlock) {
+      const uint64_t x = edges[b + j];
+      const uint32_t lo = static_cast<uint32_t>(x);
+      if (lo & OGS_EDGE_DOWN) continue;
+      if constexpr (MODS) {
+        if (dead.has(b + j)) continue;
+      }
+      const uint32_t t = edge_dst(lo);
+      const uint32_t c = hop ? 1u : static_cast<uint32_t>(x >> 32);
+      if (c < dist[t]) {
+        atomicMin(&dist[t], c);
+        stamp[t] = 2;
+      }
+    }
+    __syncthreads();
+  }
+  uint32_t r = seedRow ? 2 : 1;
   for (;; ++r) {
     bool changed = false;
     scan_chunks(chunks, C, serial, [&](uint64_t ch) {
@@ -305,7 +370,7 @@ __device__ __forceinline__ void frontier_spf_packed(
     uint32_t N, uint32_t s, const uint64_t* __restrict__ edges,
     const uint64_t* __restrict__ chunks, uint32_t C, bool hop,
     const uint32_t* __restrict__ gRow, uint32_t e0, uint64_t* dn, uint8_t* stamp,
-    uint64_t* tp, const DeadEdges& dead, bool serial) {
+    uint64_t* tp, const DeadEdges& dead, bool serial, bool seedRow, bool pair) {
   // u8 round stamps (1 B per node, so 8 C3 units fit a CU): after 256
   // rounds a stale stamp can match again -- that node is pushed once more
   // with its current word, a no-op for the monotone fixpoint
@@ -320,18 +385,51 @@ __device__ __forceinline__ void frontier_spf_packed(
   tp[0] = __builtin_amdgcn_s_memtime();
 #endif
   const uint32_t sb = gRow[s] - e0;  // the source's row: its link slots
-  uint32_t r = 1;
+  // round 1 is the source's row alone: its edges are relaxed directly (one
+  // per thread) instead of a scan of every chunk record for one stamp
+  // ("spf_seed_row" option; off: round 1 scans like the others)
+  if (seedRow) {
+    const uint32_t n = gRow[s + 1] - e0 - sb;
+    for (uint32_t j = tid; j < n; j += kBlock) {
+      const uint64_t x = edges[sb + j];
+      const uint32_t lo = static_cast<uint32_t>(x);
+      if (lo & OGS_EDGE_DOWN) continue;
+      if constexpr (MODS) {
+        if (dead.has(sb + j)) continue;
+      }
+      const uint32_t t = edge_dst(lo);
+      const uint32_t c = hop ? 1u : static_cast<uint32_t>(x >> 32);
+      const uint32_t bits = j < 32u ? 1u << j : 0u;
+      uint64_t old = dn[t];
+      for (;;) {
+        const uint32_t dt = static_cast<uint32_t>(old), nt = static_cast<uint32_t>(old >> 32);
+        if (c > dt || (c == dt && !(bits & ~nt))) break;
+        const uint64_t nw = c < dt ? (uint64_t(c) | (uint64_t(bits) << 32))
+                                   : (uint64_t(dt) | (uint64_t(nt | bits) << 32));
+        const uint64_t seen = atomicCAS(reinterpret_cast<unsigned long long*>(&dn[t]),
+                                        static_cast<unsigned long long>(old),
+                                        static_cast<unsigned long long>(nw));
+        if (seen == old) {
+          stamp[t] = 2;
+          break;
+        }
+        old = seen;
+      }
+    }
+    __syncthreads();
+  }
+  uint32_t r = seedRow ? 2 : 1;
   for (;; ++r) {
     bool changed = false;
-    scan_chunks(chunks, C, serial, [&](uint64_t ch) {
+    auto active = [&](uint64_t ch) {
       const uint32_t v = uint32_t(ch) & OGS_EDGE_DST_MASK;
-      if (stamp[v] != uint8_t(r)) return;
-      if ((uint32_t(ch) & kChunkDrained) && v != s) return;
+      return stamp[v] == uint8_t(r) && (!(uint32_t(ch) & kChunkDrained) || v == s);
+    };
+    auto relax = [&](uint64_t ch, const uint64_t (&x)[kChunk]) {
+      const uint32_t v = uint32_t(ch) & OGS_EDGE_DST_MASK;
       const uint64_t xv = dn[v];
       const uint32_t dv = static_cast<uint32_t>(xv), nv = static_cast<uint32_t>(xv >> 32);
       const uint32_t b = uint32_t(ch >> 32);
-      uint64_t x[kChunk];
-      load_chunk<MODS>(edges, ch, x, dead);
 #pragma unroll
       for (uint32_t i = 0; i < kChunk; ++i) {
         const uint32_t lo = static_cast<uint32_t>(x[i]);
@@ -359,7 +457,17 @@ __device__ __forceinline__ void frontier_spf_packed(
           old = seen;
         }
       }
-    });
+    };
+    if (pair) {
+      scan_chunks_pair<MODS>(chunks, C, edges, dead, active, relax);
+    } else {
+      scan_chunks(chunks, C, serial, [&](uint64_t ch) {
+        if (!active(ch)) return;
+        uint64_t x[kChunk];
+        load_chunk<MODS>(edges, ch, x, dead);
+        relax(ch, x);
+      });
+    }
     if (!__syncthreads_or(changed)) break;
   }
 #ifdef OGS_STAMPS
@@ -667,6 +775,10 @@ uint32_t frontier_lds_bytes(uint32_t Sn, int W, bool queue = false, bool ninfo =
 constexpr uint32_t kFlagNinfoGlobal = 1u << 30;
 // internal launch flag: the chunk scan loads one record at a time (A/B)
 constexpr uint32_t kFlagScanSerial = 1u << 29;
+// round 1 of the chunk-scan forms scans the chunk records too (spf_seed_row 0)
+constexpr uint32_t kFlagScanRound1 = 1u << 27;
+// the packed chunk scan relaxes active chunks two at a time (spf_scan_pair)
+constexpr uint32_t kFlagScanPair = 1u << 26;
 
 // ROUTES = false: SPF only, dist / nh to HBM.
 // ROUTES = true: SPF + the unit's RouteDb stream (route_stream.h) from LDS;
@@ -726,7 +838,8 @@ __global__ __launch_bounds__(kBlock) void spf_frontier_kernel(
     frontier_spf_packed<MODS>(N, s, g.edges + e0, chunks + size_t(unit.topo) * cap,
                               nChunk[unit.topo], (flags & OGS_F_HOP_METRIC) != 0, gRow, e0,
                               dn64, reinterpret_cast<uint8_t*>(stamp), tp, dead,
-                              (flags & kFlagScanSerial) != 0);
+                              (flags & kFlagScanSerial) != 0,
+                              (flags & kFlagScanRound1) == 0, (flags & kFlagScanPair) != 0);
   } else if constexpr (PACKED) {
     queue_spf_packed<MODS, QMODE == 3>(N, s, g.edges + e0, gRow, e0, nflags,
                            (flags & OGS_F_HOP_METRIC) != 0, dn64, stamp32, q0, q1,
@@ -738,7 +851,8 @@ __global__ __launch_bounds__(kBlock) void spf_frontier_kernel(
   } else {
     frontier_spf<W, MODS>(N, s, g.edges + e0, chunks + size_t(unit.topo) * cap,
                           nChunk[unit.topo], (flags & OGS_F_HOP_METRIC) != 0, gRow,
-                          e0, dist, nh, stamp, tp, dead, (flags & kFlagScanSerial) != 0);
+                          e0, dist, nh, stamp, tp, dead, (flags & kFlagScanSerial) != 0,
+                          (flags & kFlagScanRound1) == 0);
   }
 
   auto dOf = [&](uint32_t v) -> uint32_t {
@@ -790,11 +904,12 @@ __global__ __launch_bounds__(kBlock) void spf_frontier_kernel(
     };
     if constexpr (PACKED) {
       stream_routes<W, DIFF, OUTS3>(pt, key + size_t(unit.topo) * Sp, p0, P, Sp, u0, s,
-                                    nflags, PackedView{dn64}, cfg, out, rec, &dc);
+                                    nflags, PackedView{dn64}, cfg, out, rec, &dc,
+                                    (flags & kFlagNtStores) != 0);
     } else {
       stream_routes<W, DIFF, OUTS3>(pt, key + size_t(unit.topo) * Sp, p0, P, Sp, u0, s,
                                     nflags, SplitView<uint32_t, W>{dist, nh}, cfg, out,
-                                    rec, &dc);
+                                    rec, &dc, (flags & kFlagNtStores) != 0);
     }
     if constexpr (DIFF) {
       __syncthreads();
@@ -816,6 +931,13 @@ __global__ __launch_bounds__(kBlock) void spf_frontier_kernel(
   }
 #endif
 }
+
+// "spf_seed_row" option: 1 (default) round 1 of the chunk-scan forms relaxes
+// the source's row directly, 0 it scans every chunk record (A/B)
+int g_spfSeedRow = 1;
+// "spf_scan_pair" option: 1 the packed chunk scan relaxes a batch's active
+// chunks two at a time (both chunks' edge loads in flight), 0 one at a time
+int g_spfScanPair = 0;
 
 // "frontier_wg_lds" option: minimum LDS bytes per fused frontier + route
 // stream workgroup (0: what the unit needs)
@@ -876,6 +998,9 @@ hipError_t launch_frontier_q(const ogs_graph& g, const ogs_prefix_table& pt,
   if (ROUTES && lds < uint32_t(g_frontierWgLds)) lds = uint32_t(g_frontierWgLds);
   if (!ninfo) flags |= kFlagNinfoGlobal;
   if (!g_spfScanBatch) flags |= kFlagScanSerial;
+  if (!g_spfSeedRow) flags |= kFlagScanRound1;
+  if (g_spfScanPair) flags |= kFlagScanPair;
+  if (g_routeStoreNt & 1) flags |= kFlagNtStores;
   auto k = spf_frontier_kernel<W, ROUTES, MODS, DIFF, QMODE, OUTS3>;
   if (lds > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
@@ -1270,7 +1395,7 @@ __global__ __launch_bounds__(kBlock) void spf_variant_repair_kernel(
   };
   if constexpr (!CHANGED_ONLY) {
     stream_routes<1, true>(pt, tkey, p0, P, Sp, u0, s, nflags, PackedView{dn}, cfg, out,
-                           nodeRec, &dc);
+                           nodeRec, &dc, (flags & kFlagNtStores) != 0);
   } else {
     const bool v4Gated = !cfg.enableV4 && !cfg.v4OverV6;
     uint32_t upd = 0, del = 0;
@@ -1347,7 +1472,8 @@ bool launch_variants_repair(const ogs_graph& g, const ogs_prefix_table& pt,
     *err = hipGetLastError();
     if (*err != hipSuccess) return true;
   }
-  hipLaunchKernelGGL(k, dim3(n), dim3(kBlock), lds, stream, g, pt, key, units, flags,
+  hipLaunchKernelGGL(k, dim3(n), dim3(kBlock), lds, stream, g, pt, key, units,
+                     flags | ((g_routeStoreNt & 1) ? kFlagNtStores : 0u),
                      static_cast<uint32_t*>(out.dist), out.nh, out, *mods, *diff, desc);
   *err = hipGetLastError();
   return true;

@@ -398,16 +398,15 @@ __device__ __forceinline__ void wave_outputs(
   const uint8_t* lPfxFlags = reinterpret_cast<const uint8_t*>(base + L.pfxFlags);
   // ---- SPF outputs ----------------------------------------------------------
   const uint32_t Sn = g.max_nodes;
+  const bool nt = (flags & kFlagNtStores) != 0;
 #pragma unroll
   for (int k = 0; k < NPL; ++k) {
     const uint32_t v = vk[k];
     if (v >= N) continue;
-    // streaming (non-temporal) stores: outputs are not re-read by the
-    // kernel, keep them out of the way of the inputs in L2
-    if (out.dist) {
-      __builtin_nontemporal_store(dcur[k], static_cast<uint32_t*>(out.dist) + uidx * Sn + v);
-    }
-    if (out.nh) __builtin_nontemporal_store(ncur[k], out.nh + uidx * Sn + v);
+    // outputs are not re-read by the kernel: non-temporal or ordinary
+    // stores by the launch's kFlagNtStores bit ("route_store_nt")
+    if (out.dist) store_out(static_cast<uint32_t*>(out.dist) + uidx * Sn + v, dcur[k], nt);
+    if (out.nh) store_out(out.nh + uidx * Sn + v, ncur[k], nt);
   }
   if (!hasPrefixes) return;
 
@@ -446,12 +445,10 @@ __device__ __forceinline__ void wave_outputs(
       const uint32_t p = uint32_t(k * 64 + lane);
       if (p >= P) continue;
       const size_t o = uidx * Sp + p;
-      if (out.meta) __builtin_nontemporal_store(meta[k], out.meta + o);
-      if (out.metric) __builtin_nontemporal_store(metric[k], static_cast<uint32_t*>(out.metric) + o);
-      if (out.sel) {
-        __builtin_nontemporal_store((meta[k] & OGS_ROUTE_SELECTED) ? 1u : 0u, out.sel + o);
-      }
-      if (out.mask) __builtin_nontemporal_store(mask[k], out.mask + o);
+      if (out.meta) store_out(out.meta + o, meta[k], nt);
+      if (out.metric) store_out(static_cast<uint32_t*>(out.metric) + o, metric[k], nt);
+      if (out.sel) store_out(out.sel + o, (meta[k] & OGS_ROUTE_SELECTED) ? 1u : 0u, nt);
+      if (out.mask) store_out(out.mask + o, mask[k], nt);
     }
   }
   for (uint32_t p = ident ? P : lane; p < P; p += 64) {
@@ -474,10 +471,10 @@ __device__ __forceinline__ void wave_outputs(
       mask = mk[0];
     }
     const size_t o = uidx * Sp + p;
-    if (out.meta) __builtin_nontemporal_store(meta, out.meta + o);
-    if (out.metric) __builtin_nontemporal_store(metric, static_cast<uint32_t*>(out.metric) + o);
-    if (out.sel) __builtin_nontemporal_store(selBits, out.sel + o);
-    if (out.mask) __builtin_nontemporal_store(mask, out.mask + o);
+    if (out.meta) store_out(out.meta + o, meta, nt);
+    if (out.metric) store_out(static_cast<uint32_t*>(out.metric) + o, metric, nt);
+    if (out.sel) store_out(out.sel + o, selBits, nt);
+    if (out.mask) store_out(out.mask + o, mask, nt);
   }
 }
 
@@ -1131,6 +1128,7 @@ hipError_t launch_wave_upb(const ogs_graph& g, const ogs_prefix_table& pt,
         hipFuncAttributeMaxDynamicSharedMemorySize, int(bytes));
     if (e != hipSuccess) return e;
   }
+  if (g_routeStoreNt & 2) flags |= kFlagNtStores;
   hipLaunchKernelGGL(k, dim3(grid), dim3(64 * UPB), bytes, stream, g, pt,
                      hasPrefixes, units, nUnits, flags, out, lds, maxA, uint32_t(g_waveOpt));
   return hipGetLastError();
@@ -1158,6 +1156,7 @@ bool launch_wave_pair(const ogs_graph& g, const ogs_prefix_table& pt, int hasPre
     if (*err != hipSuccess) return true;
   }
   const int grid = (nUnits + 2 * UPB - 1) / (2 * UPB);
+  if (g_routeStoreNt & 2) flags |= kFlagNtStores;
   hipLaunchKernelGGL(k, dim3(grid), dim3(64 * UPB), bytes, stream, g, pt, hasPrefixes, units,
                      nUnits, flags, out, lds, maxA, uint32_t(g_waveOpt));
   *err = hipGetLastError();

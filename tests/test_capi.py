@@ -42,6 +42,25 @@ def test_pure_entry_points_without_device():
     assert lib.ogs_abi_version() == capi.OGS_ABI_VERSION
 
 
+def test_engine_options_documented_and_validated():
+    """Every ogs_set_option knob the library parses is documented in the
+    header; unknown names and out-of-range values are rejected (no device
+    needed: options are process-wide settings)."""
+    import openr_amd.capi as capi
+    src = open(os.path.join(ROOT, "openr_amd", "csrc", "kernels", "capi.hip")).read()
+    names = re.findall(r'strcmp\(name, "([a-z0-9_]+)"\)', src)
+    header = open(os.path.join(ROOT, "include", "openr_gpu.h")).read()
+    assert len(names) >= 20
+    undocumented = [n for n in names if f'"{n}"' not in header]
+    assert not undocumented, undocumented
+    lib = capi.load()
+    assert lib.ogs_set_option(b"no_such_option", 1) != 0
+    assert lib.ogs_set_option(b"route_store_nt", 4) != 0
+    assert lib.ogs_set_option(b"route_store_nt", -1) != 0
+    assert lib.ogs_set_option(b"route_store_nt", 3) == 0
+    assert lib.ogs_set_option(b"route_store_nt", 2) == 0
+
+
 def test_spf_routes_rejects_bad_arguments():
     import openr_amd.capi as capi
     lib = capi.load()

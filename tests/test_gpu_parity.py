@@ -279,6 +279,27 @@ def test_wave_pair_form(product, oracle, metric_max):
     assert got[6] == got[2]
 
 
+@pytest.mark.parametrize("nt", [0, 2])
+def test_wave_store_flavours(product, oracle, nt):
+    """The wave kernel's non-temporal (route_store_nt bit 2, default) and
+    ordinary output stores write the same SPF outputs and RouteDbs."""
+    import openr_amd.capi as capi
+    lib = capi.load()
+    opts = dict(n=10, metricSeed=0xC2400077, prefixSeed=0xC1, metricMax=64)
+    cpu = oracle.grid_batch_route_dbs(opts, 0, 48, "3")
+    try:
+        capi.check(lib, lib.ogs_set_option(b"route_store_nt", nt), "route_store_nt")
+        br = product.BatchRunner(True, False, False)
+        br.add_grid_batch(opts, 0, 48, "3")
+        br.upload()
+        br.run()
+        br.download()
+        got = [br.canonical(u) for u in range(br.num_units())]
+    finally:
+        lib.ogs_set_option(b"route_store_nt", 2)
+    _cmp(got, cpu, f"wave store nt={nt}")
+
+
 def _tri_grid(M, n, seed):
     """n x n grid plus one diagonal per cell: odd cycles (not bipartite), so
     the 2-colour slot order leaves same-slot edges and the wave kernel must
@@ -378,6 +399,9 @@ def _batch_dbs(product, kind, opts, srcs, enable_v4, brs, **options):
         lib.ogs_set_option(b"route_stream_chunks", 4)
         lib.ogs_set_option(b"spf_frontier", 1)
         lib.ogs_set_option(b"ms_group", 0)
+        lib.ogs_set_option(b"route_store_nt", 2)
+        lib.ogs_set_option(b"spf_seed_row", 1)
+        lib.ogs_set_option(b"spf_scan_pair", 0)
 
 
 MIX = dict(v4Permille=150, anycastPermille=120, minNhPermille=60, drainPermille=50)
@@ -400,6 +424,44 @@ def test_route_stream_fabric_prefix_mix(product, oracle, stream, frontier, enabl
     a = _batch_dbs(product, "fabric", opts, srcs, enable_v4, brs, route_stream=stream,
                    spf_frontier=frontier)
     _cmp(a, oracle.gen_route_dbs("fabric", opts, srcs, enable_v4, False, brs), "fabricmix")
+
+
+@pytest.mark.parametrize("nt", [0, 1, 3])
+@pytest.mark.parametrize("stream", [1, 2])
+def test_route_stream_store_flavours(product, oracle, nt, stream):
+    """The RouteDb stream's ordinary (default) and non-temporal 16-B stores
+    (route_store_nt bit 1) write the same records: fused and split forms on the
+    fabric prefix mix, vs the oracle."""
+    opts = dict(pods=8, planes=4, sswPerPlane=16, rswPerPod=32, full=True,
+                prefixesPerNode=3, nodeOverloadPermille=20, adjOverloadPermille=10,
+                **MIX)
+    names = ([f"1-{p}-{s}" for p in range(4) for s in range(16)] +
+             [f"3-{p}-{r}" for p in range(8) for r in range(32)])
+    srcs = names[::7]
+    a = _batch_dbs(product, "fabric", opts, srcs, True, True, route_stream=stream,
+                   route_store_nt=nt)
+    _cmp(a, oracle.gen_route_dbs("fabric", opts, srcs, True, False, True), "storeflavour")
+
+
+@pytest.mark.parametrize("seed,pair", [(0, 0), (1, 0), (1, 1), (0, 1)])
+@pytest.mark.parametrize("wide", [False, True])
+def test_frontier_seed_row(product, oracle, seed, pair, wide):
+    """Round 1 of the chunk-scan SPF relaxes the source's row directly
+    (spf_seed_row 1, default) or scans every chunk record (0); the packed
+    scan relaxes active chunks two at a time (spf_scan_pair 1) or one at a
+    time: one-word (packed one-phase) and three-word (two-phase) sources,
+    with drained nodes / links and the prefix mix, vs the oracle."""
+    if wide:
+        opts = dict(pods=4, planes=2, sswPerPlane=36, rswPerPod=48, full=True,
+                    prefixesPerNode=2, nodeOverloadPermille=20, adjOverloadPermille=10, **MIX)
+        srcs = [f"2-{p}-{f}" for p in range(4) for f in range(2)] + ["1-0-3", "3-2-7"]
+    else:
+        opts = dict(pods=8, planes=4, sswPerPlane=16, rswPerPod=32, full=True,
+                    prefixesPerNode=3, nodeOverloadPermille=20, adjOverloadPermille=10, **MIX)
+        srcs = ["1-0-0", "1-3-15", "2-5-1", "3-0-0", "3-7-31"]
+    a = _batch_dbs(product, "fabric", opts, srcs, True, True, route_stream=2,
+                   spf_seed_row=seed, spf_scan_pair=pair)
+    _cmp(a, oracle.gen_route_dbs("fabric", opts, srcs, True, False, True), "seedrow")
 
 
 @pytest.mark.parametrize("stream,frontier", [(0, 0), (1, 0), (1, 1), (2, 1), (3, 1)])
