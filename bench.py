@@ -543,6 +543,8 @@ def run_c3(args, torch, dist, rank, world, local_rank):
     line["publication_ingest"] = {
         "keys": keys, "bytes": pub["bytes"], "ingest_ms": round(pub["ingest_ms"], 2),
         "decode_ms": round(pub["decode_ms"], 2),
+        "prefix_keyed_decode_ms": round(pub["prefix_keyed_decode_ms"], 2),
+        "prefix_insert_ms": round(pub["prefix_insert_ms"], 2),
         "keys_per_s": round(keys / pub["ingest_ms"] * 1e3, 1),
         "decode_MB_per_s": round(pub["bytes"] / pub["decode_ms"] / 1e3, 1),
         "note": "LsdbIngest (C++ drop-in), 1 host thread, median of 3; rank 0, "

@@ -1567,7 +1567,7 @@ PYBIND11_MODULE(_decision, m) {
             bytes += vals[i].size();
             if (i < nAdj) adjBytes += vals[i].size();
           }
-          std::vector<double> ingest, decode;
+          std::vector<double> ingest, decode, keyedDecode, insert;
           size_t routesKept = 0;
           for (int r = 0; r < reps; ++r) {
             LinkState ls(g.area, "test_node");
@@ -1585,10 +1585,30 @@ PYBIND11_MODULE(_decision, m) {
               else sink += readPrefixDatabase(vals[i]).prefixEntries.size();
             }
             auto t2 = std::chrono::steady_clock::now();
+            // split of the prefix-key ingest: decode with the keyed network,
+            // then PrefixState inserts of the decoded entries
+            std::vector<std::pair<std::string, PrefixDatabase>> decoded;
+            decoded.reserve(keys.size() - nAdj);
+            for (size_t i = nAdj; i < keys.size(); ++i) {
+              std::vector<std::string> nets;
+              PrefixDatabase db = readPrefixDatabase(vals[i], &nets);
+              decoded.emplace_back(nets.front(), std::move(db));
+            }
+            auto t3 = std::chrono::steady_clock::now();
+            PrefixState ps2;
+            for (auto& [net, db] : decoded) {
+              sink += ps2.updatePrefixKeyed(db.thisNodeName, g.area, net,
+                                            std::move(db.prefixEntries.front())).size();
+            }
+            auto t4 = std::chrono::steady_clock::now();
             routesKept = ps.prefixes().size() + (sink & 0);
             ingest.push_back(std::chrono::duration<double, std::milli>(t1 - t0).count());
             decode.push_back(std::chrono::duration<double, std::milli>(t2 - t1).count());
+            keyedDecode.push_back(std::chrono::duration<double, std::milli>(t3 - t2).count());
+            insert.push_back(std::chrono::duration<double, std::milli>(t4 - t3).count());
           }
+          std::sort(keyedDecode.begin(), keyedDecode.end());
+          std::sort(insert.begin(), insert.end());
           std::sort(ingest.begin(), ingest.end());
           std::sort(decode.begin(), decode.end());
           py::dict d;
@@ -1599,6 +1619,8 @@ PYBIND11_MODULE(_decision, m) {
           d["prefixes"] = routesKept;
           d["ingest_ms"] = ingest[ingest.size() / 2];
           d["decode_ms"] = decode[decode.size() / 2];
+          d["prefix_keyed_decode_ms"] = keyedDecode[keyedDecode.size() / 2];
+          d["prefix_insert_ms"] = insert[insert.size() / 2];
           return d;
         },
         py::arg("kind"), py::arg("opts"), py::arg("reps") = 3);
