@@ -303,9 +303,9 @@ int ogs_host_free(void* hptr);
  *                 a round's chunk records are loaded 8 at a time, 0 one by
  *                 one (A/B). "spf_seed_row": 1 (default) round 1 of the
  *                 chunk scan relaxes the source's row directly, 0 it scans
- *                 every chunk record (A/B). "spf_scan_pair": 1 the packed
- *                 chunk scan relaxes a batch's active chunks two at a time,
- *                 0 (default) one at a time. "frontier_wg_lds": minimum LDS bytes per fused
+ *                 every chunk record (A/B). "frontier_o8": 1 the all-sources
+ *                 RouteDb launches use the frontier kernel compiled for 8
+ *                 waves per SIMD, 0 (default) 7 (A/B). "frontier_wg_lds": minimum LDS bytes per fused
  *                 frontier + route-stream workgroup (occupancy probe, 0).
  *   "wave_opt":   wave-kernel paths, bits: 1 register-resident SPF words
  *                 (ds_bpermute), 2 (default) identity-segment route path,

@@ -21,7 +21,7 @@ extern int g_routeStreamChunks;
 extern int g_spfScanBatch;
 extern int g_routeStoreNt;
 extern int g_spfSeedRow;
-extern int g_spfScanPair;
+extern int g_frontierO8;
 extern int g_spfPackedScan;
 extern int g_spfFrontier;
 extern int g_spfGlobal;
@@ -199,9 +199,9 @@ int ogs_set_option(const char* name, int64_t value) {
     ogs::g_routeStoreNt = int(value);
     return OGS_OK;
   }
-  if (std::strcmp(name, "spf_scan_pair") == 0) {
-    if (value != 0 && value != 1) return fail(OGS_E_INVALID, "spf_scan_pair must be 0 or 1");
-    ogs::g_spfScanPair = int(value);
+  if (std::strcmp(name, "frontier_o8") == 0) {
+    if (value != 0 && value != 1) return fail(OGS_E_INVALID, "frontier_o8 must be 0 or 1");
+    ogs::g_frontierO8 = int(value);
     return OGS_OK;
   }
   if (std::strcmp(name, "spf_seed_row") == 0) {

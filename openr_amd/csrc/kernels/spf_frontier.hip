@@ -163,50 +163,6 @@ __device__ __forceinline__ void scan_chunks(const uint64_t* __restrict__ chunks,
   }
 }
 
-// Paired form of scan_chunks for the packed SPF ("spf_scan_pair"): a
-// batch's active chunks (test(ch): the node changed last round) are relaxed
-// two at a time with both chunks' edge loads in flight together -- the
-// one-at-a-time form waits one L2 round trip per active chunk. The batch is
-// walked unrolled with one pending record (no dynamic register indexing).
-template <bool MODS, typename Test, typename Relax>
-__device__ __forceinline__ void scan_chunks_pair(const uint64_t* __restrict__ chunks,
-                                                 uint32_t C, const uint64_t* __restrict__ edges,
-                                                 const DeadEdges& dead, Test test,
-                                                 Relax relax) {
-  const uint32_t tid = threadIdx.x;
-  for (uint32_t c0 = tid; c0 < C; c0 += kScanBatch * kBlock) {
-    uint64_t chs[kScanBatch];
-#pragma unroll
-    for (int k = 0; k < kScanBatch; ++k) {
-      const uint32_t c = c0 + uint32_t(k) * kBlock;
-      chs[k] = c < C ? chunks[c] : ~0ull;
-    }
-    uint64_t pend = 0;
-    bool has = false;
-#pragma unroll
-    for (int k = 0; k < kScanBatch; ++k) {
-      if (c0 + uint32_t(k) * kBlock < C && test(chs[k])) {
-        if (has) {
-          uint64_t xa[kChunk], xb[kChunk];
-          load_chunk<MODS>(edges, pend, xa, dead);
-          load_chunk<MODS>(edges, chs[k], xb, dead);
-          relax(pend, xa);
-          relax(chs[k], xb);
-          has = false;
-        } else {
-          pend = chs[k];
-          has = true;
-        }
-      }
-    }
-    if (has) {
-      uint64_t xa[kChunk];
-      load_chunk<MODS>(edges, pend, xa, dead);
-      relax(pend, xa);
-    }
-  }
-}
-
 // One unit's SPF into LDS (dist[v], nh[v*W + w]); returns after the final
 // workgroup barrier. stamp[] is scratch.
 template <int W, bool MODS>
@@ -370,7 +326,7 @@ __device__ __forceinline__ void frontier_spf_packed(
     uint32_t N, uint32_t s, const uint64_t* __restrict__ edges,
     const uint64_t* __restrict__ chunks, uint32_t C, bool hop,
     const uint32_t* __restrict__ gRow, uint32_t e0, uint64_t* dn, uint8_t* stamp,
-    uint64_t* tp, const DeadEdges& dead, bool serial, bool seedRow, bool pair) {
+    uint64_t* tp, const DeadEdges& dead, bool serial, bool seedRow) {
   // u8 round stamps (1 B per node, so 8 C3 units fit a CU): after 256
   // rounds a stale stamp can match again -- that node is pushed once more
   // with its current word, a no-op for the monotone fixpoint
@@ -458,16 +414,12 @@ __device__ __forceinline__ void frontier_spf_packed(
         }
       }
     };
-    if (pair) {
-      scan_chunks_pair<MODS>(chunks, C, edges, dead, active, relax);
-    } else {
-      scan_chunks(chunks, C, serial, [&](uint64_t ch) {
-        if (!active(ch)) return;
-        uint64_t x[kChunk];
-        load_chunk<MODS>(edges, ch, x, dead);
-        relax(ch, x);
-      });
-    }
+    scan_chunks(chunks, C, serial, [&](uint64_t ch) {
+      if (!active(ch)) return;
+      uint64_t x[kChunk];
+      load_chunk<MODS>(edges, ch, x, dead);
+      relax(ch, x);
+    });
     if (!__syncthreads_or(changed)) break;
   }
 #ifdef OGS_STAMPS
@@ -777,20 +729,17 @@ constexpr uint32_t kFlagNinfoGlobal = 1u << 30;
 constexpr uint32_t kFlagScanSerial = 1u << 29;
 // round 1 of the chunk-scan forms scans the chunk records too (spf_seed_row 0)
 constexpr uint32_t kFlagScanRound1 = 1u << 27;
-// the packed chunk scan relaxes active chunks two at a time (spf_scan_pair)
-constexpr uint32_t kFlagScanPair = 1u << 26;
 
 // ROUTES = false: SPF only, dist / nh to HBM.
 // ROUTES = true: SPF + the unit's RouteDb stream (route_stream.h) from LDS;
 // dist / nh go to HBM only when requested.
-template <int W, bool ROUTES, bool MODS = false, bool DIFF = false,
-          int QMODE = 0, bool OUTS3 = false>
-__global__ __launch_bounds__(kBlock) void spf_frontier_kernel(
-    ogs_graph g, ogs_prefix_table pt, const uint32_t* __restrict__ key,
+template <int W, bool ROUTES, bool MODS, bool DIFF, int QMODE, bool OUTS3>
+__device__ __forceinline__ void spf_frontier_body(
+    const ogs_graph& g, const ogs_prefix_table& pt, const uint32_t* __restrict__ key,
     const uint64_t* __restrict__ chunks, const uint32_t* __restrict__ nChunk,
     uint32_t cap, const ogs_unit* __restrict__ units, uint32_t flags,
-    uint32_t* __restrict__ oDist, uint32_t* __restrict__ oNh, ogs_spf_out out,
-    ogs_unit_mods mods, ogs_route_diff diff) {
+    uint32_t* __restrict__ oDist, uint32_t* __restrict__ oNh, const ogs_spf_out& out,
+    const ogs_unit_mods& mods, const ogs_route_diff& diff) {
   constexpr uint32_t kInf = 0xFFFFFFFFu;
   const int tid = threadIdx.x;
   const uint32_t u0 = blockIdx.x;
@@ -839,7 +788,7 @@ __global__ __launch_bounds__(kBlock) void spf_frontier_kernel(
                               nChunk[unit.topo], (flags & OGS_F_HOP_METRIC) != 0, gRow, e0,
                               dn64, reinterpret_cast<uint8_t*>(stamp), tp, dead,
                               (flags & kFlagScanSerial) != 0,
-                              (flags & kFlagScanRound1) == 0, (flags & kFlagScanPair) != 0);
+                              (flags & kFlagScanRound1) == 0);
   } else if constexpr (PACKED) {
     queue_spf_packed<MODS, QMODE == 3>(N, s, g.edges + e0, gRow, e0, nflags,
                            (flags & OGS_F_HOP_METRIC) != 0, dn64, stamp32, q0, q1,
@@ -932,12 +881,41 @@ __global__ __launch_bounds__(kBlock) void spf_frontier_kernel(
 #endif
 }
 
+#define OGS_FRONTIER_KERNEL_ARGS                                                        \
+  ogs_graph g, ogs_prefix_table pt, const uint32_t* __restrict__ key,                 \
+      const uint64_t* __restrict__ chunks, const uint32_t* __restrict__ nChunk,       \
+      uint32_t cap, const ogs_unit* __restrict__ units, uint32_t flags,               \
+      uint32_t* __restrict__ oDist, uint32_t* __restrict__ oNh, ogs_spf_out out,      \
+      ogs_unit_mods mods, ogs_route_diff diff
+
+template <int W, bool ROUTES, bool MODS = false, bool DIFF = false,
+          int QMODE = 0, bool OUTS3 = false>
+__global__ __launch_bounds__(kBlock) void spf_frontier_kernel(OGS_FRONTIER_KERNEL_ARGS) {
+  spf_frontier_body<W, ROUTES, MODS, DIFF, QMODE, OUTS3>(g, pt, key, chunks, nChunk, cap,
+                                                          units, flags, oDist, oNh, out,
+                                                          mods, diff);
+}
+
+// The same kernel compiled for 8 waves per SIMD (64 VGPRs; SGPRs spill to
+// VGPR lanes): the all-sources RouteDb launches (OUTS3) at 8 instead of 7
+// workgroups per CU when LDS allows ("frontier_o8" option).
+template <int W, bool ROUTES, bool MODS = false, bool DIFF = false,
+          int QMODE = 0, bool OUTS3 = false>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) void
+spf_frontier_kernel_o8(OGS_FRONTIER_KERNEL_ARGS) {
+  spf_frontier_body<W, ROUTES, MODS, DIFF, QMODE, OUTS3>(g, pt, key, chunks, nChunk, cap,
+                                                          units, flags, oDist, oNh, out,
+                                                          mods, diff);
+}
+#undef OGS_FRONTIER_KERNEL_ARGS
+
+// "frontier_o8" option: 1 the all-sources RouteDb launches use the kernel
+// compiled for 8 waves per SIMD (spf_frontier_kernel_o8), 0 the default 7
+int g_frontierO8 = 0;
+
 // "spf_seed_row" option: 1 (default) round 1 of the chunk-scan forms relaxes
 // the source's row directly, 0 it scans every chunk record (A/B)
 int g_spfSeedRow = 1;
-// "spf_scan_pair" option: 1 the packed chunk scan relaxes a batch's active
-// chunks two at a time (both chunks' edge loads in flight), 0 one at a time
-int g_spfScanPair = 0;
 
 // "frontier_wg_lds" option: minimum LDS bytes per fused frontier + route
 // stream workgroup (0: what the unit needs)
@@ -999,9 +977,11 @@ hipError_t launch_frontier_q(const ogs_graph& g, const ogs_prefix_table& pt,
   if (!ninfo) flags |= kFlagNinfoGlobal;
   if (!g_spfScanBatch) flags |= kFlagScanSerial;
   if (!g_spfSeedRow) flags |= kFlagScanRound1;
-  if (g_spfScanPair) flags |= kFlagScanPair;
   if (g_routeStoreNt & 1) flags |= kFlagNtStores;
   auto k = spf_frontier_kernel<W, ROUTES, MODS, DIFF, QMODE, OUTS3>;
+  if constexpr (OUTS3) {
+    if (g_frontierO8) k = spf_frontier_kernel_o8<W, ROUTES, MODS, DIFF, QMODE, OUTS3>;
+  }
   if (lds > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
                                        hipFuncAttributeMaxDynamicSharedMemorySize,

@@ -401,7 +401,6 @@ def _batch_dbs(product, kind, opts, srcs, enable_v4, brs, **options):
         lib.ogs_set_option(b"ms_group", 0)
         lib.ogs_set_option(b"route_store_nt", 2)
         lib.ogs_set_option(b"spf_seed_row", 1)
-        lib.ogs_set_option(b"spf_scan_pair", 0)
 
 
 MIX = dict(v4Permille=150, anycastPermille=120, minNhPermille=60, drainPermille=50)
@@ -443,14 +442,13 @@ def test_route_stream_store_flavours(product, oracle, nt, stream):
     _cmp(a, oracle.gen_route_dbs("fabric", opts, srcs, True, False, True), "storeflavour")
 
 
-@pytest.mark.parametrize("seed,pair", [(0, 0), (1, 0), (1, 1), (0, 1)])
+@pytest.mark.parametrize("seed", [0, 1])
 @pytest.mark.parametrize("wide", [False, True])
-def test_frontier_seed_row(product, oracle, seed, pair, wide):
+def test_frontier_seed_row(product, oracle, seed, wide):
     """Round 1 of the chunk-scan SPF relaxes the source's row directly
-    (spf_seed_row 1, default) or scans every chunk record (0); the packed
-    scan relaxes active chunks two at a time (spf_scan_pair 1) or one at a
-    time: one-word (packed one-phase) and three-word (two-phase) sources,
-    with drained nodes / links and the prefix mix, vs the oracle."""
+    (spf_seed_row 1, default) or scans every chunk record (0): one-word
+    (packed one-phase) and three-word (two-phase) sources, with drained
+    nodes / links and the prefix mix, vs the oracle."""
     if wide:
         opts = dict(pods=4, planes=2, sswPerPlane=36, rswPerPod=48, full=True,
                     prefixesPerNode=2, nodeOverloadPermille=20, adjOverloadPermille=10, **MIX)
@@ -460,7 +458,7 @@ def test_frontier_seed_row(product, oracle, seed, pair, wide):
                     prefixesPerNode=3, nodeOverloadPermille=20, adjOverloadPermille=10, **MIX)
         srcs = ["1-0-0", "1-3-15", "2-5-1", "3-0-0", "3-7-31"]
     a = _batch_dbs(product, "fabric", opts, srcs, True, True, route_stream=2,
-                   spf_seed_row=seed, spf_scan_pair=pair)
+                   spf_seed_row=seed)
     _cmp(a, oracle.gen_route_dbs("fabric", opts, srcs, True, False, True), "seedrow")
 
 
