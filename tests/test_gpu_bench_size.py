@@ -66,11 +66,13 @@ def _c3(product, names, ppn=100):
     return launches
 
 
-def test_c3_full_every_source_matches_oracle(product):
+@pytest.mark.parametrize("o8", [0, 1])
+def test_c3_full_every_source_matches_oracle(product, o8):
     """C3-full at bench size (2,080 sources x 208k prefixes) through
     bench.py's two-stream width-group launches: every source's digest equals
     the oracle's (golden per-source digests), and the job digest equals the
-    golden job digest bench.py asserts."""
+    golden job digest bench.py asserts; with the default frontier kernel and
+    its 8-waves-per-SIMD build (frontier_o8)."""
     if not os.path.exists(C3_SOURCES):
         pytest.skip("oracle C3 per-source digests not generated")
     want = json.load(open(C3_SOURCES))
@@ -78,7 +80,13 @@ def test_c3_full_every_source_matches_oracle(product):
     if len(want) != len(names):
         pytest.skip("oracle C3 per-source digests incomplete")
     assert set(want) == set(names)
-    launches = _c3(product, names)
+    import openr_amd.capi as capi
+    lib = capi.load()
+    capi.check(lib, lib.ogs_set_option(b"frontier_o8", o8), "frontier_o8")
+    try:
+        launches = _c3(product, names)
+    finally:
+        lib.ogs_set_option(b"frontier_o8", 0)
     job = 0
     bad = []
     for L in launches:

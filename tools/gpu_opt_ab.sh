@@ -14,5 +14,5 @@ for cfg in ${CONFIGS:-c3}; do
 done
 [ -n "$NOTEST" ] && exit 0
 timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu \
-  tests/test_gpu_parity.py -k "${K:-store_flavours or wave or route_stream}" > gpurun_out/opt_tests.log 2>&1 || { tail -30 gpurun_out/opt_tests.log; exit 1; }
+  tests/test_gpu_parity.py ${TEST_FILES} -k "${K:-store_flavours or wave or route_stream}" > gpurun_out/opt_tests.log 2>&1 || { tail -30 gpurun_out/opt_tests.log; exit 1; }
 tail -2 gpurun_out/opt_tests.log
