@@ -21,7 +21,8 @@ extern int g_routeStreamChunks;
 extern int g_spfScanBatch;
 extern int g_routeStoreNt;
 extern int g_spfSeedRow;
-extern int g_frontierO8;
+// "frontier_o8" option (spf_frontier.hip launch_frontier_q)
+int g_frontierO8 = 0;
 extern int g_spfPackedScan;
 extern int g_spfFrontier;
 extern int g_spfGlobal;

@@ -909,9 +909,10 @@ spf_frontier_kernel_o8(OGS_FRONTIER_KERNEL_ARGS) {
 }
 #undef OGS_FRONTIER_KERNEL_ARGS
 
-// "frontier_o8" option: 1 the all-sources RouteDb launches use the kernel
-// compiled for 8 waves per SIMD (spf_frontier_kernel_o8), 0 the default 7
-int g_frontierO8 = 0;
+// "frontier_o8" option (capi.hip): 1 the all-sources RouteDb launches use
+// the kernel compiled for 8 waves per SIMD (spf_frontier_kernel_o8), 0 the
+// default build (7 on the C3 one-word group)
+extern int g_frontierO8;
 
 // "spf_seed_row" option: 1 (default) round 1 of the chunk-scan forms relaxes
 // the source's row directly, 0 it scans every chunk record (A/B)
