@@ -385,10 +385,96 @@ def c3_launches(torch, M, capi, dev, names, ppn=100, with_sel=False):
         srcs = h["units"].reshape(-1, 2)[:, 1]
         deg = rp[srcs + 1] - rp[srcs]
         wl = (deg + 31) // 32
-        bpu = float((inputs / N + 4 * N + 4 * wl * N + P * (4 * wl + 8)).sum())
+        unit_bytes = inputs / N + 4 * N + 4 * wl * N + P * (4 * wl + 8)
         launches.append(dict(br=br, h=h, t=t, o=o, g=g, pt=pt, so=so, U=U, W=W,
-                             flags=h["flags"], bytes=bpu, names=mine))
+                             flags=h["flags"], bytes=float(unit_bytes.sum()),
+                             unit_bytes=unit_bytes, names=mine, rows=None))
     return launches, N
+
+
+def c3_subset(L, names):
+    """The launch L restricted to the units of `names` (a rank's shard of
+    the sources): same device inputs, a units array of those rows, outputs
+    in rows 0..U-1 of L's buffers; `rows` maps them back to L's units for
+    the digest. None when no unit of L is in `names`."""
+    pos = {n: i for i, n in enumerate(L["names"])}
+    idx = [pos[n] for n in names if n in pos]
+    if not idx:
+        return None
+    units = L["t"]["units"].view(-1, 2)[idx].contiguous().view(-1)
+    sub = dict(L, U=len(idx), bytes=float(L["unit_bytes"][idx].sum()),
+               names=[L["names"][i] for i in idx], rows=idx)
+    sub["t"] = dict(L["t"], units=units)
+    return sub
+
+
+def c3_time(lib, capi, launches, main, side, steps, warmup):
+    """Device ms of one step (every width-group launch of `launches`), from
+    HIP events on the launch stream over `steps` steps after `warmup`."""
+    for _ in range(warmup):
+        c3_launch_all(lib, capi, launches, main, side)
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    e0.record(main)
+    for _ in range(steps):
+        c3_launch_all(lib, capi, launches, main, side)
+    e1.record(main)
+    e1.synchronize()
+    return e0.elapsed_time(e1) / steps
+
+
+def c3_golden_shard(names):
+    """The oracle's digest of the sources `names`: XOR of their golden
+    per-source digests (tests/golden/c3_source_digests.json), or None."""
+    path = os.path.join(ROOT, "tests", "golden", "c3_source_digests.json")
+    if not os.path.exists(path):
+        return None
+    want = json.load(open(path))
+    if not set(names) <= set(want):
+        return None
+    out = 0
+    for n in names:
+        out ^= int(want[n], 16)
+    return f"{out:016x}"
+
+
+def c3_shard_projection(lib, capi, launches, main, side, world_sizes=(2, 4, 8),
+                        steps=10, warmup=2):
+    """North_star reports C3 at 1/2/4/8 GPUs with sources interleaved over
+    the ranks. On ONE GPU: every rank r of every N runs its exact
+    shard alone (the launches restricted to shard.interleave(names, r, N)),
+    timed like the headline; per N the slowest rank's ms and its fraction of
+    ONE GPU's HBM peak (a rank's algorithmic bytes / its ms), and the XOR of
+    all N shards' digests, which must equal the golden whole-build c3."""
+    names = [n for L in launches for n in L["names"]]
+    order = c3_source_names()
+    names = [n for n in order if n in set(names)]
+    out = {}
+    for N in world_sizes:
+        ranks, job = [], 0
+        for r in range(N):
+            mine = shard.interleave(names, r, N)
+            subs = [x for x in (c3_subset(L, mine) for L in launches) if x is not None]
+            ms = c3_time(lib, capi, subs, main, side, steps, warmup)
+            nbytes = sum(x["bytes"] for x in subs)
+            d = shard.combine_digests(c3_digest(x) for x in subs)
+            job ^= d
+            want = c3_golden_shard(mine)
+            ranks.append({"rank": r, "sources": len(mine), "ms": round(ms, 4),
+                          "frac": round(nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                          "digest": f"{d:016x}",
+                          "golden": None if want is None else
+                          ("match" if want == f"{d:016x}" else f"MISMATCH want {want}")})
+            if want is not None and want != f"{d:016x}":
+                DIGEST_FAILURES.append(f"c3 shard {r}/{N}: got {d:016x}, oracle golden {want}")
+        slow = max(ranks, key=lambda x: x["ms"])
+        out[str(N)] = {"slowest_rank": slow["rank"], "ms": slow["ms"], "frac": slow["frac"],
+                       "min_frac": min(x["frac"] for x in ranks),
+                       "builds_per_s_projected": round(1e3 / slow["ms"], 2),
+                       "xor_digest": f"{job:016x}", "ranks": ranks}
+        log(f"c3 shards N={N}: slowest {slow['ms']:.4f} ms (frac {slow['frac']:.3f}), "
+            f"xor {job:016x}")
+    return out
 
 
 def c3_launch_all(lib, capi, launches, main, side):
@@ -412,10 +498,15 @@ def c3_launch_all(lib, capi, launches, main, side):
 
 def c3_digest(L, threads=16):
     """route_digest.h unit digests of one launch's records (keys = source
-    names), XOR-combined."""
+    names), XOR-combined. A subset launch (c3_subset) digests its rows
+    0..U-1 as the units they came from."""
     o = L["o"]
-    d = L["br"].records_digests([], o["meta"].cpu().numpy(), o["metric"].cpu().numpy(),
-                                o["mask"].cpu().numpy(), L["W"], threads)
+    Sp, W, U = L["h"]["max_prefixes"], L["W"], L["U"]
+    rows = L.get("rows")
+    d = L["br"].records_digests([], o["meta"][:U * Sp].cpu().numpy(),
+                                o["metric"][:U * Sp].cpu().numpy(),
+                                o["mask"][:U * W * Sp].cpu().numpy(), W, threads,
+                                rows if rows is not None else [])
     return shard.combine_digests(d)
 
 
@@ -457,7 +548,15 @@ def run_c3(args, torch, dist, rank, world, local_rank):
     steps, warmup = args.steps, args.warmup  # C3 is the headline (or --config c3)
     ppn = args.prefixes_per_node
     # sources interleaved over ranks (balances SSW/FSW/RSW degree classes)
-    mine = shard.interleave(c3_source_names(), rank, world)
+    shard_of = (rank, world)
+    if args.as_rank:
+        # rank r's exact share of an N-rank run, alone on this one GPU
+        if world != 1:
+            raise SystemExit("bench.py: --as-rank runs one process (no --gpus)")
+        shard_of = tuple(int(x) for x in args.as_rank.split("/"))
+        if not 0 <= shard_of[0] < shard_of[1]:
+            raise SystemExit(f"bench.py: --as-rank {args.as_rank}: need 0 <= r < N")
+    mine = shard.interleave(c3_source_names(), *shard_of)
     launches, N = c3_launches(torch, M, capi, dev, mine, ppn)
     if args.c3_order == "wide-first":
         # the wide (FSW, 4-word) group has the longest units: dispatch it
@@ -519,9 +618,24 @@ def run_c3(args, torch, dist, rank, world, local_rank):
                      "bytes_alg_per_step_rank0": round(nbytes, 1)},
     }
     log(f"c3 timed: {kernel_ms:.4f} ms/build, digest {job_digest:016x}")
+    if args.as_rank:
+        r, n = shard_of
+        line["metric"] = "SPF+RouteDb shard time (one rank's share, alone on one GPU)"
+        line["value"] = round(kernel_ms, 4)
+        line["unit"] = "ms"
+        line["higher_is_better"] = False
+        line["config"]["parallelism"] = f"rank {r} of {n} (interleaved sources), 1 GPU"
+        line["config"]["sources"] = len(mine)
+        line["shard_builds_per_s_projected"] = round(1e3 / kernel_ms, 2)
+        golden_check(line, f"c3_shard_{r}_of_{n}", job_digest,
+                     c3_golden_shard(mine) if ppn == 100 else None)
+        return line
     golden_check(line, "c3", job_digest, GOLDEN.get("c3") if ppn == 100 else None)
     if world == 1:
         set_traffic(line, "c3", "spf_frontier_kernel")
+        if not args.no_shard_projection:
+            # the 2/4/8-GPU shards, each rank's share timed alone on this GPU
+            line["shard_projection"] = c3_shard_projection(lib, capi, launches, main, side)
     # §8(f) f2, outside the timed region: the same build as a resident
     # RouteDbBatch served per node (getRouteDbComputed: D2H of one node's
     # records + host materialisation + toThrift)
@@ -1135,6 +1249,11 @@ def main():
     ap.add_argument("--no-c2", action="store_true", help="skip the C2 topology-batch sub-line")
     ap.add_argument("--c2-steps", type=int, default=50)
     ap.add_argument("--c2-warmup", type=int, default=5)
+    ap.add_argument("--as-rank", default=None, metavar="r/N",
+                    help="C3: time rank r's interleaved share of an N-rank run alone "
+                         "on this GPU (the line reports that shard)")
+    ap.add_argument("--no-shard-projection", action="store_true",
+                    help="C3 at N=1: skip the per-rank shard timings for N=2/4/8")
     ap.add_argument("--c3-order", default="wide-first", choices=["narrow-first", "wide-first"],
                     help="C3: which next-hop width group is dispatched first")
     ap.add_argument("--no-c4", action="store_true", help="skip the C4 link-failure sub-line")

@@ -299,14 +299,25 @@ int ogs_host_free(void* hptr);
  *                 wave kernel's output stores are; default 2 (A/B).
  *   "spf_packed_scan": 1 (default) chunk-scan frontier units with one-word
  *                 next-hop sets relax packed {dist, next hops} words in one
- *                 phase; 0 two phases (A/B). "spf_scan_batch": 1 (default)
- *                 a round's chunk records are loaded 8 at a time, 0 one by
- *                 one (A/B). "spf_seed_row": 1 (default) round 1 of the
- *                 chunk scan relaxes the source's row directly, 0 it scans
- *                 every chunk record (A/B). "frontier_o8": 1 the all-sources
- *                 RouteDb launches use the frontier kernel compiled for 8
- *                 waves per SIMD, 0 (default) 7 (A/B). "frontier_wg_lds": minimum LDS bytes per fused
+ *                 phase; 0 two phases (A/B). "spf_seed_row": 1 (default)
+ *                 round 1 of the chunk scan relaxes the source's row
+ *                 directly, 0 it scans every chunk record (A/B).
+ *                 "spf_lane_walk": a round's active chunk records walked
+ *                 per lane (1) or per batch slot (0); -1 (default) per lane
+ *                 in workgroups of 512+ threads. "spf_preload": 1 (default)
+ *                 the packed relax reads its 8 targets' distances before
+ *                 any compare-and-swap, 0 not (A/B).
+ *                 "frontier_wg_lds": minimum LDS bytes per fused
  *                 frontier + route-stream workgroup (occupancy probe, 0).
+ *   "frontier_block": threads per workgroup of the all-sources RouteDb
+ *                 launches (fused frontier SPF + route stream, meta / metric
+ *                 / mask outputs): 256, 512 or 1024; 0 (default) by the
+ *                 launch's streamed bytes per CU (256 for a whole-node
+ *                 build, 512 for one rank's shard).
+ *   "frontier_parts": workgroups per one-word unit of those launches, each
+ *                 running the unit's SPF and streaming one prefix range
+ *                 (1..16; 0 default: by bytes per CU). "frontier_parts_wide":
+ *                 the same for units of wider next-hop sets.
  *   "wave_opt":   wave-kernel paths, bits: 1 register-resident SPF words
  *                 (ds_bpermute), 2 (default) identity-segment route path,
  *                 4 two units per wavefront with 16-bit words.

@@ -18,11 +18,13 @@ extern int g_kspStop;
 extern int g_msGroup;
 extern int g_routeStream;
 extern int g_routeStreamChunks;
-extern int g_spfScanBatch;
 extern int g_routeStoreNt;
 extern int g_spfSeedRow;
-// "frontier_o8" option (spf_frontier.hip launch_frontier_q)
-int g_frontierO8 = 0;
+extern int g_frontierBlock;
+extern int g_frontierParts;
+extern int g_frontierPartsWide;
+extern int g_spfLaneWalk;
+extern int g_spfPreload;
 extern int g_spfPackedScan;
 extern int g_spfFrontier;
 extern int g_spfGlobal;
@@ -200,19 +202,38 @@ int ogs_set_option(const char* name, int64_t value) {
     ogs::g_routeStoreNt = int(value);
     return OGS_OK;
   }
-  if (std::strcmp(name, "frontier_o8") == 0) {
-    if (value != 0 && value != 1) return fail(OGS_E_INVALID, "frontier_o8 must be 0 or 1");
-    ogs::g_frontierO8 = int(value);
+  if (std::strcmp(name, "frontier_block") == 0) {
+    if (value != 0 && value != 256 && value != 512 && value != 1024) {
+      return fail(OGS_E_INVALID, "frontier_block must be 0, 256, 512 or 1024");
+    }
+    ogs::g_frontierBlock = int(value);
+    return OGS_OK;
+  }
+  if (std::strcmp(name, "frontier_parts") == 0) {
+    if (value < 0 || value > 16) return fail(OGS_E_INVALID, "frontier_parts must be in [0, 16]");
+    ogs::g_frontierParts = int(value);
+    return OGS_OK;
+  }
+  if (std::strcmp(name, "spf_lane_walk") == 0) {
+    if (value < -1 || value > 1) return fail(OGS_E_INVALID, "spf_lane_walk must be -1, 0 or 1");
+    ogs::g_spfLaneWalk = int(value);
+    return OGS_OK;
+  }
+  if (std::strcmp(name, "spf_preload") == 0) {
+    if (value != 0 && value != 1) return fail(OGS_E_INVALID, "spf_preload must be 0 or 1");
+    ogs::g_spfPreload = int(value);
+    return OGS_OK;
+  }
+  if (std::strcmp(name, "frontier_parts_wide") == 0) {
+    if (value < 0 || value > 16) {
+      return fail(OGS_E_INVALID, "frontier_parts_wide must be in [0, 16]");
+    }
+    ogs::g_frontierPartsWide = int(value);
     return OGS_OK;
   }
   if (std::strcmp(name, "spf_seed_row") == 0) {
     if (value != 0 && value != 1) return fail(OGS_E_INVALID, "spf_seed_row must be 0 or 1");
     ogs::g_spfSeedRow = int(value);
-    return OGS_OK;
-  }
-  if (std::strcmp(name, "spf_scan_batch") == 0) {
-    if (value != 0 && value != 1) return fail(OGS_E_INVALID, "spf_scan_batch must be 0 or 1");
-    ogs::g_spfScanBatch = int(value);
     return OGS_OK;
   }
   if (std::strcmp(name, "route_stream_chunks") == 0) {

@@ -100,19 +100,22 @@ __device__ __forceinline__ bool route_changed(const Rec<W>& r, const DiffCtx& d,
   return ch;
 }
 
-// Streams unit u's P route records (rows of stride Sp). rec(v, r) fills
-// meta / metric / mask of node v's record; sv is the unit's SPF state for
-// route_one. Four consecutive prefixes per lane: one 16-B key load and one
-// 16-B store per output array (non-temporal when nt). OUTS3: the caller guarantees
-// meta, metric and mask outputs and no sel -- the stores are then
-// unconditional, so every path leaves the same number of stores in flight
-// and the key prefetch's wait stays partial (see the loop below).
-template <int W, bool DIFF = false, bool OUTS3 = false, typename View, typename RecFn>
+// Streams unit u's route records of prefixes [lo, hi) (lo a multiple of 4;
+// rows of stride Sp) with B threads. rec(v, r) fills meta / metric / mask of
+// node v's record; sv is the unit's SPF state for route_one. Four
+// consecutive prefixes per lane: one 16-B key load and one 16-B store per
+// output array (non-temporal when nt). OUTS3: the caller guarantees meta,
+// metric and mask outputs and no sel -- the stores are then unconditional,
+// so every path leaves the same number of stores in flight and the key
+// prefetch's wait stays partial (see the loop below).
+template <int W, bool DIFF = false, bool OUTS3 = false, int B = kBlock, typename View,
+          typename RecFn>
 __device__ __forceinline__ void stream_routes(
     const ogs_prefix_table& pt, const uint32_t* __restrict__ tkey, uint32_t p0,
     uint32_t P, uint32_t Sp, size_t u, uint32_t s,
     const uint8_t* __restrict__ nflags, const View& sv, const RouteCfg& cfg,
-    const ogs_spf_out& out, RecFn rec, const DiffCtx* diff = nullptr, bool nt = true) {
+    const ogs_spf_out& out, RecFn rec, const DiffCtx* diff = nullptr, bool nt = true,
+    uint32_t lo = 0, uint32_t hi = 0xFFFFFFFFu) {
   uint32_t upd = 0, del = 0;
   constexpr uint32_t kInf = 0xFFFFFFFFu;
   const int tid = threadIdx.x;
@@ -146,7 +149,9 @@ __device__ __forceinline__ void stream_routes(
       reinterpret_cast<uintptr_t>(out.metric) |
       reinterpret_cast<uintptr_t>(out.sel) | reinterpret_cast<uintptr_t>(out.mask);
   const bool vec = (Sp & 3u) == 0u && (align & 15u) == 0u;
-  const uint32_t Pv = vec ? (P & ~3u) : 0u;
+  hi = min(hi, P);
+  lo = min(lo, hi);
+  const uint32_t Pv = vec ? max(lo, hi & ~3u) : lo;
   auto quad = [&](uint32_t q, const uint4 k4) {
     Rec<W> r0, r1, r2, r3;
     one(q + 0, k4.x, r0);
@@ -187,11 +192,6 @@ __device__ __forceinline__ void stream_routes(
       }
     }
   };
-  // Software-pipelined: the next quad's keys are loaded before this quad's
-  // stores are issued. vmcnt counts loads and stores together in issue order,
-  // so a key load issued AFTER the previous stores would wait for them to
-  // drain (one store round trip per iteration); issued before, its wait
-  // leaves the younger stores in flight (MI355X_MICROARCH.md, vmcnt).
   // Software-pipelined key loads: each quad's keys are loaded BEFORE the
   // previous quad's stores are issued. vmcnt counts loads and stores together
   // in issue order, so a key load issued after those stores would wait for
@@ -199,8 +199,8 @@ __device__ __forceinline__ void stream_routes(
   // peeled and the loop unrolled by two with the key registers alternating,
   // so every entry to every use sees the same ops in flight (one key load +
   // the previous quad's stores) and the compiler keeps the wait partial.
-  constexpr uint32_t kStep = kBlock * 4u;
-  uint32_t q = uint32_t(tid) * 4u;
+  constexpr uint32_t kStep = uint32_t(B) * 4u;
+  uint32_t q = lo + uint32_t(tid) * 4u;
   if (q < Pv) {
     auto keyAt = [&](uint32_t x) {  // clamped: unconditional prefetch
       return *reinterpret_cast<const uint4*>(tkey + (x < Pv ? x : Pv - 4u));
@@ -219,7 +219,7 @@ __device__ __forceinline__ void stream_routes(
       q += kStep;
     }
   }
-  for (uint32_t p = Pv + tid; p < P; p += kBlock) {  // tail / unaligned rows
+  for (uint32_t p = Pv + tid; p < hi; p += B) {  // tail / unaligned rows
     Rec<W> r;
     one(p, tkey[p], r);
     if (oMeta) oMeta[p] = r.meta;

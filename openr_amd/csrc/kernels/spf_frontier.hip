@@ -29,6 +29,7 @@
 // fused form then streams the unit's RouteDb (route_stream.h) from LDS.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <type_traits>
 
@@ -135,46 +136,100 @@ __device__ __forceinline__ void load_chunk(const uint64_t* __restrict__ edges,
   }
 }
 
-// fn(chunk record) for the thread's records c = tid, tid + kBlock, ... < C,
-// kScanBatch loads in flight per step (serial: one dependent load per
-// record, the former scan, for A/B: "spf_scan_batch" option 0).
+// chunk records loaded per scan step (independent L2 loads in flight)
 constexpr int kScanBatch = 8;
-int g_spfScanBatch = 1;
 
-template <typename Fn>
-__device__ __forceinline__ void scan_chunks(const uint64_t* __restrict__ chunks, uint32_t C,
-                                            bool serial, Fn fn) {
+// The chunk scan of one round over the thread's records c = tid, tid + B,
+// ... < C, kScanBatch record loads in flight per step; relax(record, edges)
+// runs for the records that pass active(record). Each lane walks only ITS
+// active records (a lane-local bitmask, lowest first), so a wave runs as
+// many relaxations per batch as its busiest lane has active records, not one
+// per batch slot that any lane has active (a large frontier makes most slots
+// active in some lane). PIPE: the next active record's edges are loaded
+// before the current one is relaxed, two chunks of edges in registers (the
+// few-units-per-CU geometries, B >= 512, where a round is a chain of
+// dependent L2 round trips rather than a share of a busy CU).
+template <int B, bool PIPE, bool MODS, typename Act, typename Relax>
+__device__ __forceinline__ void scan_active(const uint64_t* __restrict__ chunks, uint32_t C,
+                                            const uint64_t* __restrict__ edges,
+                                            const DeadEdges& dead, bool slotWalk, Act active,
+                                            Relax relax) {
   const uint32_t tid = threadIdx.x;
-  if (serial) {
-    for (uint32_t c = tid; c < C; c += kBlock) fn(chunks[c]);
-    return;
-  }
-  for (uint32_t c0 = tid; c0 < C; c0 += kScanBatch * kBlock) {
-    uint64_t chs[kScanBatch];
+  for (uint32_t c0 = tid; c0 < C; c0 += kScanBatch * B) {
+    // eight records in named registers and record k by a select tree: an
+    // indexed register array would be demoted to scratch memory
+    static_assert(kScanBatch == 8, "eight records per scan step");
+    auto rec = [&](int k) {
+      const uint32_t c = c0 + uint32_t(k) * B;
+      return c < C ? chunks[c] : ~0ull;
+    };
+    const uint64_t r0 = rec(0), r1 = rec(1), r2 = rec(2), r3 = rec(3);
+    const uint64_t r4 = rec(4), r5 = rec(5), r6 = rec(6), r7 = rec(7);
+    uint32_t m = 0;
+    auto test = [&](int k, uint64_t ch) {
+      if (c0 + uint32_t(k) * B < C && active(ch)) m |= 1u << k;
+    };
+    test(0, r0), test(1, r1), test(2, r2), test(3, r3);
+    test(4, r4), test(5, r5), test(6, r6), test(7, r7);
+    auto pick = [=](uint32_t k) {
+      const uint64_t a01 = (k & 1u) ? r1 : r0, a23 = (k & 1u) ? r3 : r2;
+      const uint64_t a45 = (k & 1u) ? r5 : r4, a67 = (k & 1u) ? r7 : r6;
+      const uint64_t b0 = (k & 2u) ? a23 : a01, b1 = (k & 2u) ? a67 : a45;
+      return (k & 4u) ? b1 : b0;
+    };
+    if (!PIPE && slotWalk) {  // A/B: one relaxation per slot any lane has active
+      auto one = [&](int k, uint64_t ch) {
+        if (!((m >> k) & 1u)) return;
+        uint64_t x[kChunk];
+        load_chunk<MODS>(edges, ch, x, dead);
+        relax(ch, x);
+      };
+      one(0, r0), one(1, r1), one(2, r2), one(3, r3);
+      one(4, r4), one(5, r5), one(6, r6), one(7, r7);
+    } else if constexpr (!PIPE) {
+      while (m) {
+        const uint64_t ch = pick(uint32_t(__builtin_ctz(m)));
+        m &= m - 1u;
+        uint64_t x[kChunk];
+        load_chunk<MODS>(edges, ch, x, dead);
+        relax(ch, x);
+      }
+    } else {
+      if (!m) continue;
+      uint64_t ch = pick(uint32_t(__builtin_ctz(m)));
+      m &= m - 1u;
+      uint64_t x[kChunk];
+      load_chunk<MODS>(edges, ch, x, dead);
+      for (;;) {
+        const bool more = m != 0u;
+        uint64_t chn = 0, xn[kChunk];
+        if (more) {
+          chn = pick(uint32_t(__builtin_ctz(m)));
+          m &= m - 1u;
+          load_chunk<MODS>(edges, chn, xn, dead);
+        }
+        relax(ch, x);
+        if (!more) break;
+        ch = chn;
 #pragma unroll
-    for (int k = 0; k < kScanBatch; ++k) {
-      const uint32_t c = c0 + uint32_t(k) * kBlock;
-      chs[k] = c < C ? chunks[c] : ~0ull;
-    }
-#pragma unroll
-    for (int k = 0; k < kScanBatch; ++k) {
-      if (c0 + uint32_t(k) * kBlock < C) fn(chs[k]);
+        for (uint32_t i = 0; i < kChunk; ++i) x[i] = xn[i];
+      }
     }
   }
 }
 
 // One unit's SPF into LDS (dist[v], nh[v*W + w]); returns after the final
-// workgroup barrier. stamp[] is scratch.
-template <int W, bool MODS>
+// workgroup barrier. stamp[] is scratch. B = threads per workgroup.
+template <int W, bool MODS, int B = kBlock>
 __device__ __forceinline__ void frontier_spf(
     uint32_t N, uint32_t s, const uint64_t* __restrict__ edges,
     const uint64_t* __restrict__ chunks, uint32_t C, bool hop,
     const uint32_t* __restrict__ gRow, uint32_t e0, uint32_t* dist,
-    uint32_t* nh, uint16_t* stamp, uint64_t* tp, const DeadEdges& dead, bool serial,
-    bool seedRow) {
+    uint32_t* nh, uint16_t* stamp, uint64_t* tp, const DeadEdges& dead, bool seedRow,
+    bool slotWalk) {
   constexpr uint32_t kInf = 0xFFFFFFFFu;
   const int tid = threadIdx.x;
-  for (uint32_t v = tid; v < N; v += kBlock) {
+  for (uint32_t v = tid; v < N; v += B) {
     dist[v] = (v == s) ? 0u : kInf;
     stamp[v] = (v == s) ? 1 : 0;
 #pragma unroll
@@ -194,7 +249,7 @@ __device__ __forceinline__ void frontier_spf(
   // ("spf_seed_row"; off: round 1 scans like the others)
   if (seedRow) {
     const uint32_t b = gRow[s] - e0, n = gRow[s + 1] - e0 - b;
-    for (uint32_t j = tid; j < n; j += kBlock) {
+    for (uint32_t j = tid; j < n; j += B) {
       const uint64_t x = edges[b + j];
       const uint32_t lo = static_cast<uint32_t>(x);
       if (lo & OGS_EDGE_DOWN) continue;
@@ -211,15 +266,17 @@ __device__ __forceinline__ void frontier_spf(
     __syncthreads();
   }
   uint32_t r = seedRow ? 2 : 1;
+  constexpr bool kPipe = B >= 512;
   for (;; ++r) {
     bool changed = false;
-    scan_chunks(chunks, C, serial, [&](uint64_t ch) {
+    auto active = [&](uint64_t ch) {
       const uint32_t v = uint32_t(ch) & OGS_EDGE_DST_MASK;
-      if (stamp[v] != r) return;
-      if ((uint32_t(ch) & kChunkDrained) && v != s) return;
+      return stamp[v] == r && (!(uint32_t(ch) & kChunkDrained) || v == s);
+    };
+    scan_active<B, kPipe, MODS>(chunks, C, edges, dead, slotWalk, active,
+                                [&](uint64_t ch, const uint64_t (&x)[kChunk]) {
+      const uint32_t v = uint32_t(ch) & OGS_EDGE_DST_MASK;
       const uint32_t dv = dist[v];
-      uint64_t x[kChunk];
-      load_chunk<MODS>(edges, ch, x, dead);
       uint32_t t[kChunk], cand[kChunk], dt[kChunk];
 #pragma unroll
       for (uint32_t i = 0; i < kChunk; ++i) {
@@ -251,7 +308,7 @@ __device__ __forceinline__ void frontier_spf(
   const uint32_t r0 = r + 1;
   {
     const uint32_t b = gRow[s] - e0, n = gRow[s + 1] - e0 - b;
-    for (uint32_t j = tid; j < n && j < 32u * W; j += kBlock) {
+    for (uint32_t j = tid; j < n && j < 32u * W; j += B) {
       const uint64_t x = edges[b + j];
       const uint32_t lo = static_cast<uint32_t>(x);
       if (lo & OGS_EDGE_DOWN) continue;
@@ -270,15 +327,17 @@ __device__ __forceinline__ void frontier_spf(
   // then changed nodes push NH(v) into tight neighbours
   for (r = r0;; ++r) {
     bool changed = false;
-    scan_chunks(chunks, C, serial, [&](uint64_t ch) {
+    auto active = [&](uint64_t ch) {
       const uint32_t v = uint32_t(ch) & OGS_EDGE_DST_MASK;
-      if (stamp[v] != r || v == s || (uint32_t(ch) & kChunkDrained)) return;
+      return stamp[v] == r && v != s && !(uint32_t(ch) & kChunkDrained);
+    };
+    scan_active<B, kPipe, MODS>(chunks, C, edges, dead, slotWalk, active,
+                                [&](uint64_t ch, const uint64_t (&x)[kChunk]) {
+      const uint32_t v = uint32_t(ch) & OGS_EDGE_DST_MASK;
       const uint32_t dv = dist[v];
       uint32_t nv[W];
 #pragma unroll
       for (int w = 0; w < W; ++w) nv[w] = nh[v * W + w];
-      uint64_t x[kChunk];
-      load_chunk<MODS>(edges, ch, x, dead);
       uint32_t t[kChunk], cand[kChunk], dt[kChunk];
 #pragma unroll
       for (uint32_t i = 0; i < kChunk; ++i) {
@@ -321,18 +380,18 @@ __device__ __forceinline__ void frontier_spf(
 // next-hop sets converge in the same rounds (the fabric: 5 rounds instead of
 // 5 + 4 for the two phases above) -- the least fixpoint of spf_core.h, as
 // queue_spf_packed. dn[v] is over dist + nh (8 B per node).
-template <bool MODS>
+template <bool MODS, int B = kBlock>
 __device__ __forceinline__ void frontier_spf_packed(
     uint32_t N, uint32_t s, const uint64_t* __restrict__ edges,
     const uint64_t* __restrict__ chunks, uint32_t C, bool hop,
     const uint32_t* __restrict__ gRow, uint32_t e0, uint64_t* dn, uint8_t* stamp,
-    uint64_t* tp, const DeadEdges& dead, bool serial, bool seedRow) {
+    uint64_t* tp, const DeadEdges& dead, bool seedRow, bool slotWalk, bool preload) {
   // u8 round stamps (1 B per node, so 8 C3 units fit a CU): after 256
   // rounds a stale stamp can match again -- that node is pushed once more
   // with its current word, a no-op for the monotone fixpoint
   constexpr uint32_t kInf = 0xFFFFFFFFu;
   const int tid = threadIdx.x;
-  for (uint32_t v = tid; v < N; v += kBlock) {
+  for (uint32_t v = tid; v < N; v += B) {
     dn[v] = (v == s) ? 0ull : uint64_t(kInf);
     stamp[v] = (v == s) ? 1 : 0;
   }
@@ -346,7 +405,7 @@ __device__ __forceinline__ void frontier_spf_packed(
   // ("spf_seed_row" option; off: round 1 scans like the others)
   if (seedRow) {
     const uint32_t n = gRow[s + 1] - e0 - sb;
-    for (uint32_t j = tid; j < n; j += kBlock) {
+    for (uint32_t j = tid; j < n; j += B) {
       const uint64_t x = edges[sb + j];
       const uint32_t lo = static_cast<uint32_t>(x);
       if (lo & OGS_EDGE_DOWN) continue;
@@ -375,6 +434,7 @@ __device__ __forceinline__ void frontier_spf_packed(
     __syncthreads();
   }
   uint32_t r = seedRow ? 2 : 1;
+  const uint32_t* dn32 = reinterpret_cast<const uint32_t*>(dn);  // dist = low word
   for (;; ++r) {
     bool changed = false;
     auto active = [&](uint64_t ch) {
@@ -386,12 +446,22 @@ __device__ __forceinline__ void frontier_spf_packed(
       const uint64_t xv = dn[v];
       const uint32_t dv = static_cast<uint32_t>(xv), nv = static_cast<uint32_t>(xv >> 32);
       const uint32_t b = uint32_t(ch >> 32);
+      // the targets' distances first (independent LDS reads): a longer
+      // candidate -- most pushes of a dense frontier -- is dropped without
+      // the dependent read + compare-and-swap chain below (distances only
+      // fall, so a stale preload never drops a useful push)
+      uint32_t dt[kChunk];
+#pragma unroll
+      for (uint32_t i = 0; i < kChunk; ++i) {
+        dt[i] = preload ? dn32[2u * edge_dst(uint32_t(x[i]))] : 0xFFFFFFFFu;
+      }
 #pragma unroll
       for (uint32_t i = 0; i < kChunk; ++i) {
         const uint32_t lo = static_cast<uint32_t>(x[i]);
         if (lo & OGS_EDGE_DOWN) continue;
         const uint32_t t = edge_dst(lo);
         const uint32_t c = dv + (hop ? 1u : static_cast<uint32_t>(x[i] >> 32));
+        if (c > dt[i]) continue;
         // the source contributes its link slot (W = 1: degree <= 32), every
         // other node NH(v) (LinkState.cpp:808-811)
         const uint32_t slot = b + i - sb;
@@ -414,12 +484,7 @@ __device__ __forceinline__ void frontier_spf_packed(
         }
       }
     };
-    scan_chunks(chunks, C, serial, [&](uint64_t ch) {
-      if (!active(ch)) return;
-      uint64_t x[kChunk];
-      load_chunk<MODS>(edges, ch, x, dead);
-      relax(ch, x);
-    });
+    scan_active<B, (B >= 512), MODS>(chunks, C, edges, dead, slotWalk, active, relax);
     if (!__syncthreads_or(changed)) break;
   }
 #ifdef OGS_STAMPS
@@ -725,24 +790,45 @@ uint32_t frontier_lds_bytes(uint32_t Sn, int W, bool queue = false, bool ninfo =
 // internal launch flag (above the public OGS_F_* bits): the queue forms read
 // row bounds / drained bits from the CSR instead of an LDS node-info array
 constexpr uint32_t kFlagNinfoGlobal = 1u << 30;
-// internal launch flag: the chunk scan loads one record at a time (A/B)
-constexpr uint32_t kFlagScanSerial = 1u << 29;
 // round 1 of the chunk-scan forms scans the chunk records too (spf_seed_row 0)
 constexpr uint32_t kFlagScanRound1 = 1u << 27;
+// Chunk-scan walk: per slot ("spf_lane_walk" 0) or per lane (1); -1 (auto)
+// walks lanes in the few-units-per-CU geometries (B >= 512) only: at 256
+// threads and 7 units per CU the lane walk measured 3 % slower on C3
+// (1.316 vs 1.277 ms, profiles/r04_scan_ab.log). "spf_preload" 0: no
+// preloaded target distances in the packed relax (A/B).
+constexpr uint32_t kFlagSlotWalk = 1u << 29;
+constexpr uint32_t kFlagNoPreload = 1u << 26;
+int g_spfLaneWalk = -1;
+int g_spfPreload = 1;
+
+#ifdef OGS_STAMPS
+// diagnostic build (make stamps): 8 phase clocks per workgroup of the last
+// frontier launch, read back with ogs_diag_stamps (tools/c3_stamps.py)
+constexpr uint32_t kDiagWgs = 65536;
+__device__ uint32_t g_diagStamps[kDiagWgs * 8];
+#endif
 
 // ROUTES = false: SPF only, dist / nh to HBM.
 // ROUTES = true: SPF + the unit's RouteDb stream (route_stream.h) from LDS;
 // dist / nh go to HBM only when requested.
-template <int W, bool ROUTES, bool MODS, bool DIFF, int QMODE, bool OUTS3>
+// B threads per workgroup; `parts` workgroups per unit (OUTS3 launches
+// only): each runs the unit's SPF and streams one 1/parts prefix range of
+// its RouteDb, part 0 also writes dist / nh. A launch of few units (one
+// rank's shard of the C3 sources) so keeps enough waves streaming per CU.
+template <int W, bool ROUTES, bool MODS, bool DIFF, int QMODE, bool OUTS3, int B = kBlock>
 __device__ __forceinline__ void spf_frontier_body(
     const ogs_graph& g, const ogs_prefix_table& pt, const uint32_t* __restrict__ key,
     const uint64_t* __restrict__ chunks, const uint32_t* __restrict__ nChunk,
     uint32_t cap, const ogs_unit* __restrict__ units, uint32_t flags,
     uint32_t* __restrict__ oDist, uint32_t* __restrict__ oNh, const ogs_spf_out& out,
-    const ogs_unit_mods& mods, const ogs_route_diff& diff) {
+    const ogs_unit_mods& mods, const ogs_route_diff& diff, uint32_t parts) {
   constexpr uint32_t kInf = 0xFFFFFFFFu;
   const int tid = threadIdx.x;
-  const uint32_t u0 = blockIdx.x;
+  static_assert(B == kBlock || (OUTS3 && !MODS && !DIFF && (QMODE == 0 || QMODE == 4)),
+                "other block sizes only for the all-sources stream");
+  const uint32_t u0 = OUTS3 ? blockIdx.x / parts : blockIdx.x;
+  const uint32_t part = OUTS3 ? blockIdx.x - u0 * parts : 0u;
   const ogs_unit unit = units[u0];
   const uint32_t s = unit.src;
   const uint32_t nb = g.node_base[unit.topo];
@@ -784,11 +870,11 @@ __device__ __forceinline__ void spf_frontier_body(
   static_assert(!PACKED || W == 1, "packed words hold one next-hop word");
   uint64_t* dn64 = reinterpret_cast<uint64_t*>(smem);  // PACKED: over dist + nh
   if constexpr (QMODE == 4) {  // packed words, chunk scan
-    frontier_spf_packed<MODS>(N, s, g.edges + e0, chunks + size_t(unit.topo) * cap,
+    frontier_spf_packed<MODS, B>(N, s, g.edges + e0, chunks + size_t(unit.topo) * cap,
                               nChunk[unit.topo], (flags & OGS_F_HOP_METRIC) != 0, gRow, e0,
                               dn64, reinterpret_cast<uint8_t*>(stamp), tp, dead,
-                              (flags & kFlagScanSerial) != 0,
-                              (flags & kFlagScanRound1) == 0);
+                              (flags & kFlagScanRound1) == 0, (flags & kFlagSlotWalk) != 0,
+                              (flags & kFlagNoPreload) == 0);
   } else if constexpr (PACKED) {
     queue_spf_packed<MODS, QMODE == 3>(N, s, g.edges + e0, gRow, e0, nflags,
                            (flags & OGS_F_HOP_METRIC) != 0, dn64, stamp32, q0, q1,
@@ -798,10 +884,10 @@ __device__ __forceinline__ void spf_frontier_body(
                        (flags & OGS_F_HOP_METRIC) != 0, dist, nh, stamp32, q0, q1,
                        qcnt, ninfo, tp, dead);
   } else {
-    frontier_spf<W, MODS>(N, s, g.edges + e0, chunks + size_t(unit.topo) * cap,
+    frontier_spf<W, MODS, B>(N, s, g.edges + e0, chunks + size_t(unit.topo) * cap,
                           nChunk[unit.topo], (flags & OGS_F_HOP_METRIC) != 0, gRow,
-                          e0, dist, nh, stamp, tp, dead, (flags & kFlagScanSerial) != 0,
-                          (flags & kFlagScanRound1) == 0);
+                          e0, dist, nh, stamp, tp, dead,
+                          (flags & kFlagScanRound1) == 0, (flags & kFlagSlotWalk) != 0);
   }
 
   auto dOf = [&](uint32_t v) -> uint32_t {
@@ -812,7 +898,7 @@ __device__ __forceinline__ void spf_frontier_body(
     if constexpr (PACKED) return static_cast<uint32_t>(dn64[v] >> 32);
     else return nh[v * W + w];
   };
-  for (uint32_t v = tid; v < N; v += kBlock) {
+  for (uint32_t v = tid; part == 0u && v < N; v += B) {
     if (oDist) oDist[size_t(u0) * Sn + v] = dOf(v);
 #pragma unroll
     for (int w = 0; w < W; ++w) {
@@ -824,7 +910,7 @@ __device__ __forceinline__ void spf_frontier_body(
     // the packed chunk scan: one byte per node there)
     using RMeta = std::conditional_t<QMODE == 4, uint8_t, uint16_t>;
     RMeta* rMeta = reinterpret_cast<RMeta*>(stamp);
-    for (uint32_t v = tid; v < N; v += kBlock) {
+    for (uint32_t v = tid; v < N; v += B) {
       uint32_t cnt = 0;
 #pragma unroll
       for (int w = 0; w < W; ++w) cnt += __popc(nOf(v, w));
@@ -851,24 +937,28 @@ __device__ __forceinline__ void spf_frontier_body(
 #pragma unroll
       for (int w = 0; w < W; ++w) r.mask[w] = nOf(v, w);
     };
+    // this part's prefix range, 4-aligned (16-B accesses)
+    const uint32_t span = ((P + parts - 1u) / parts + 3u) & ~3u;
+    const uint32_t lo = min(P, part * span), hi = min(P, lo + span);
     if constexpr (PACKED) {
-      stream_routes<W, DIFF, OUTS3>(pt, key + size_t(unit.topo) * Sp, p0, P, Sp, u0, s,
-                                    nflags, PackedView{dn64}, cfg, out, rec, &dc,
-                                    (flags & kFlagNtStores) != 0);
+      stream_routes<W, DIFF, OUTS3, B>(pt, key + size_t(unit.topo) * Sp, p0, P, Sp, u0, s,
+                                       nflags, PackedView{dn64}, cfg, out, rec, &dc,
+                                       (flags & kFlagNtStores) != 0, lo, hi);
     } else {
-      stream_routes<W, DIFF, OUTS3>(pt, key + size_t(unit.topo) * Sp, p0, P, Sp, u0, s,
-                                    nflags, SplitView<uint32_t, W>{dist, nh}, cfg, out,
-                                    rec, &dc, (flags & kFlagNtStores) != 0);
+      stream_routes<W, DIFF, OUTS3, B>(pt, key + size_t(unit.topo) * Sp, p0, P, Sp, u0, s,
+                                       nflags, SplitView<uint32_t, W>{dist, nh}, cfg, out,
+                                       rec, &dc, (flags & kFlagNtStores) != 0, lo, hi);
     }
     if constexpr (DIFF) {
       __syncthreads();
       if (tid < 2) diff.counts[size_t(u0) * 2 + tid] = cnt[tid];
     }
   }
-#ifdef OGS_STAMPS  // diagnostic build only: phase clocks into out.sel row u0
+#ifdef OGS_STAMPS  // diagnostic build only: phase clocks per workgroup
   __syncthreads();
-  if (tid == 0 && out.sel) {
-    uint32_t* st = out.sel + size_t(u0) * uint32_t(pt.max_prefixes);
+  // rows (W - 1) * 16384 + blockIdx.x: two width groups' launches overlap
+  if (tid == 0 && blockIdx.x < kDiagWgs / 4) {
+    uint32_t* st = g_diagStamps + (size_t(W - 1) * (kDiagWgs / 4) + blockIdx.x) * 8u;
     st[0] = uint32_t(tp[0] - t0);       // setup
     st[1] = uint32_t(tp[1] - tp[0]);    // dist phase
     st[2] = uint32_t(tp[2] - tp[1]);    // next-hop phase
@@ -881,38 +971,18 @@ __device__ __forceinline__ void spf_frontier_body(
 #endif
 }
 
-#define OGS_FRONTIER_KERNEL_ARGS                                                        \
-  ogs_graph g, ogs_prefix_table pt, const uint32_t* __restrict__ key,                 \
-      const uint64_t* __restrict__ chunks, const uint32_t* __restrict__ nChunk,       \
-      uint32_t cap, const ogs_unit* __restrict__ units, uint32_t flags,               \
-      uint32_t* __restrict__ oDist, uint32_t* __restrict__ oNh, ogs_spf_out out,      \
-      ogs_unit_mods mods, ogs_route_diff diff
-
 template <int W, bool ROUTES, bool MODS = false, bool DIFF = false,
-          int QMODE = 0, bool OUTS3 = false>
-__global__ __launch_bounds__(kBlock) void spf_frontier_kernel(OGS_FRONTIER_KERNEL_ARGS) {
-  spf_frontier_body<W, ROUTES, MODS, DIFF, QMODE, OUTS3>(g, pt, key, chunks, nChunk, cap,
-                                                          units, flags, oDist, oNh, out,
-                                                          mods, diff);
+          int QMODE = 0, bool OUTS3 = false, int B = kBlock>
+__global__ __launch_bounds__(B) void spf_frontier_kernel(
+    ogs_graph g, ogs_prefix_table pt, const uint32_t* __restrict__ key,
+    const uint64_t* __restrict__ chunks, const uint32_t* __restrict__ nChunk,
+    uint32_t cap, const ogs_unit* __restrict__ units, uint32_t flags,
+    uint32_t* __restrict__ oDist, uint32_t* __restrict__ oNh, ogs_spf_out out,
+    ogs_unit_mods mods, ogs_route_diff diff, uint32_t parts) {
+  spf_frontier_body<W, ROUTES, MODS, DIFF, QMODE, OUTS3, B>(g, pt, key, chunks, nChunk, cap,
+                                                             units, flags, oDist, oNh, out,
+                                                             mods, diff, parts);
 }
-
-// The same kernel compiled for 8 waves per SIMD (64 VGPRs; SGPRs spill to
-// VGPR lanes): the all-sources RouteDb launches (OUTS3) at 8 instead of 7
-// workgroups per CU when LDS allows ("frontier_o8" option).
-template <int W, bool ROUTES, bool MODS = false, bool DIFF = false,
-          int QMODE = 0, bool OUTS3 = false>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) void
-spf_frontier_kernel_o8(OGS_FRONTIER_KERNEL_ARGS) {
-  spf_frontier_body<W, ROUTES, MODS, DIFF, QMODE, OUTS3>(g, pt, key, chunks, nChunk, cap,
-                                                          units, flags, oDist, oNh, out,
-                                                          mods, diff);
-}
-#undef OGS_FRONTIER_KERNEL_ARGS
-
-// "frontier_o8" option (capi.hip): 1 the all-sources RouteDb launches use
-// the kernel compiled for 8 waves per SIMD (spf_frontier_kernel_o8), 0 the
-// default build (7 on the C3 one-word group)
-extern int g_frontierO8;
 
 // "spf_seed_row" option: 1 (default) round 1 of the chunk-scan forms relaxes
 // the source's row directly, 0 it scans every chunk record (A/B)
@@ -960,14 +1030,15 @@ int queue_mode(const ogs_graph& g, int W) {
   return fold ? 3 : 2;
 }
 
-template <int W, bool ROUTES, bool MODS, bool DIFF, int QMODE, bool OUTS3 = false>
+template <int W, bool ROUTES, bool MODS, bool DIFF, int QMODE, bool OUTS3 = false,
+          int B = kBlock>
 hipError_t launch_frontier_q(const ogs_graph& g, const ogs_prefix_table& pt,
                              const uint32_t* key, const uint64_t* chunks,
                              const uint32_t* nChunk, const ogs_unit* units,
                              int nUnits, uint32_t flags, uint32_t* dist,
                              uint32_t* nh, const ogs_spf_out& out,
                              hipStream_t stream, const ogs_unit_mods& mods,
-                             const ogs_route_diff& diff) {
+                             const ogs_route_diff& diff, int parts = 1) {
   const bool scan = QMODE == 0 || QMODE == 4;  // chunk-scan forms: no lists
   const bool ninfo = scan || ninfo_in_lds(uint32_t(g.max_nodes), W);
   uint32_t lds =
@@ -976,23 +1047,72 @@ hipError_t launch_frontier_q(const ogs_graph& g, const ogs_prefix_table& pt,
   // route-stream phases of the resident units
   if (ROUTES && lds < uint32_t(g_frontierWgLds)) lds = uint32_t(g_frontierWgLds);
   if (!ninfo) flags |= kFlagNinfoGlobal;
-  if (!g_spfScanBatch) flags |= kFlagScanSerial;
   if (!g_spfSeedRow) flags |= kFlagScanRound1;
+  if (g_spfLaneWalk == 0 || (g_spfLaneWalk < 0 && B < 512)) flags |= kFlagSlotWalk;
+  if (!g_spfPreload) flags |= kFlagNoPreload;
   if (g_routeStoreNt & 1) flags |= kFlagNtStores;
-  auto k = spf_frontier_kernel<W, ROUTES, MODS, DIFF, QMODE, OUTS3>;
-  if constexpr (OUTS3) {
-    if (g_frontierO8) k = spf_frontier_kernel_o8<W, ROUTES, MODS, DIFF, QMODE, OUTS3>;
-  }
+  auto k = spf_frontier_kernel<W, ROUTES, MODS, DIFF, QMODE, OUTS3, B>;
   if (lds > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
                                        hipFuncAttributeMaxDynamicSharedMemorySize,
                                        int(lds));
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL(k, dim3(nUnits), dim3(kBlock), lds, stream, g, pt, key,
-                     chunks, nChunk, chunk_cap(g), units, flags, dist, nh, out,
-                     mods, diff);
+  hipLaunchKernelGGL(k, dim3(unsigned(nUnits) * unsigned(parts)), dim3(B), lds, stream, g, pt,
+                     key, chunks, nChunk, chunk_cap(g), units, flags, dist, nh, out, mods,
+                     diff, uint32_t(parts));
   return hipGetLastError();
+}
+
+// Geometry of an all-sources RouteDb launch (OUTS3): threads per workgroup
+// and workgroups per unit. A whole-node build (C3 at N = 1: 1,824 + 256
+// units) keeps 7 one-word units resident per CU, so 256-thread workgroups
+// and one per unit fill the chip and HBM is the bound. One rank's shard at
+// N = 4 / 8 (520 / 260 units on 256 CUs) leaves a CU one or two units: a
+// unit's single workgroup then streams its 2.5-4.2 MB latency-bound (four
+// waves, one key load in flight each) and the three-word units, 1.67x the
+// bytes of the others, form the tail. There the stream is split over
+// `parts` workgroups per unit, each running the SPF (L2-served, ~5 rounds)
+// and writing one prefix range; wider units get proportionally more parts.
+// Options "frontier_block" (0 auto, 256 / 512 / 1024), "frontier_parts"
+// (workgroups per one-word unit, 0 auto) and "frontier_parts_wide" (per
+// unit of wider next-hop sets, 0 auto) override the choice.
+int g_frontierBlock = 0;
+int g_frontierParts = 0;
+int g_frontierPartsWide = 0;
+
+namespace {
+int num_cus() {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+        n > 0) {
+      cus = n;
+    } else {
+      cus = 256;
+    }
+  }
+  return cus;
+}
+}  // namespace
+
+void stream_geometry(int nUnits, int W, int* block, int* parts) {
+  // the launch's streamed bytes per CU, in one-word units (12 B per prefix)
+  const double load = double(nUnits) * (8 + 4 * W) / 12.0 / num_cus();
+  int b = g_frontierBlock, k = W > 1 ? g_frontierPartsWide : g_frontierParts;
+  // Tuned on the C3 shards (profiles/r04_geometry_ab.log), where the one-
+  // word group (load 7.1 / 3.6 / 1.8 / 0.9 at N = 1 / 2 / 4 / 8) runs beside
+  // the three-word group (1.7 / 0.8 / 0.4 / 0.2) on a second stream: each
+  // launch sizes itself by its own load.
+  if (!b) b = load >= (W > 1 ? 1.2 : 5.0) ? 256 : 512;
+  if (!k) {
+    k = W > 1 ? std::max(1, std::min(8, int(0.83 / load + 0.5)))
+              : (load >= 1.2 ? 1 : 2);
+  }
+  *block = b;
+  *parts = k;
 }
 
 template <int W, bool ROUTES, bool MODS = false, bool DIFF = false>
@@ -1008,16 +1128,26 @@ hipError_t launch_frontier(const ogs_graph& g, const ogs_prefix_table& pt,
   constexpr int kScanMode = W == 1 ? 4 : 0;
   const bool packedScan = W == 1 && g_spfPackedScan && qm == 0;
   // the all-sources RouteDb stream writes exactly meta / metric / mask:
-  // unconditional stores (stream_routes OUTS3)
+  // unconditional stores (stream_routes OUTS3), geometry by stream_geometry
   if constexpr (ROUTES && !MODS && !DIFF) {
     if (qm == 0 && out.meta && out.metric && out.mask && !out.sel) {
-      if (packedScan) {
-        return launch_frontier_q<W, ROUTES, MODS, DIFF, kScanMode, true>(
+      int b = kBlock, k = 1;
+      stream_geometry(nUnits, W, &b, &k);
+      auto go = [&](auto qmode, auto block) {
+        return launch_frontier_q<W, ROUTES, MODS, DIFF, decltype(qmode)::value, true,
+                                 decltype(block)::value>(
             g, pt, key, chunks, nChunk, units, nUnits, flags, dist, nh, out, stream, mods,
-            diff);
+            diff, k);
+      };
+      using Q4 = std::integral_constant<int, kScanMode>;
+      using Q0 = std::integral_constant<int, 0>;
+      using B2 = std::integral_constant<int, 256>;
+      using B5 = std::integral_constant<int, 512>;
+      using B10 = std::integral_constant<int, 1024>;
+      if (packedScan) {
+        return b == 1024 ? go(Q4{}, B10{}) : b == 512 ? go(Q4{}, B5{}) : go(Q4{}, B2{});
       }
-      return launch_frontier_q<W, ROUTES, MODS, DIFF, 0, true>(
-          g, pt, key, chunks, nChunk, units, nUnits, flags, dist, nh, out, stream, mods, diff);
+      return b == 1024 ? go(Q0{}, B10{}) : b == 512 ? go(Q0{}, B5{}) : go(Q0{}, B2{});
     }
   }
   if (packedScan) {
@@ -1502,3 +1632,11 @@ hipError_t launch_frontier_variants(const ogs_graph& g, const ogs_prefix_table& 
 }
 
 }  // namespace ogs
+
+#ifdef OGS_STAMPS
+extern "C" int ogs_diag_stamps(uint32_t* host, int32_t words) {
+  const size_t n = std::min<size_t>(size_t(words), size_t(ogs::kDiagWgs) * 8);
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(ogs::g_diagStamps), n * 4, 0,
+                             hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif

@@ -629,11 +629,20 @@ class BatchRunner {
   // [U*W*Sp]; 32-bit metrics, all-ones = none): the bench digests the
   // buffers of its timed launches with this. keys[u] = the unit's key
   // (empty list: the unit's source name). Spread over `threads` threads.
+  // rows (optional): row i of the arrays holds unit rows[i] -- the records
+  // of a launch over a subset of this runner's units (a rank's shard).
   std::vector<uint64_t> recordsDigests(const std::vector<std::string>& keys,
                                        const uint32_t* meta, const uint32_t* metric,
-                                       const uint32_t* mask, int W, int threads) const {
-    const size_t U = units_.size(), Sp = std::max(hb_.maxPrefixes, 1);
-    if (!keys.empty() && keys.size() != U) throw std::invalid_argument("keys: one per unit");
+                                       const uint32_t* mask, int W, int threads,
+                                       const std::vector<int64_t>& rows = {}) const {
+    const size_t U = rows.empty() ? units_.size() : rows.size();
+    const size_t Sp = std::max(hb_.maxPrefixes, 1);
+    if (!keys.empty() && keys.size() != units_.size()) {
+      throw std::invalid_argument("keys: one per unit");
+    }
+    for (int64_t r : rows) {
+      if (r < 0 || size_t(r) >= units_.size()) throw std::out_of_range("rows: unit index");
+    }
     if (W != W_) throw std::invalid_argument("mask width differs from the runner's");
     for (const auto& t : topos_) {
       if (!t->hashes) t->hashes = std::make_unique<digest::TableHashes>(t->table);
@@ -642,19 +651,20 @@ class BatchRunner {
     threads = std::max(1, std::min<int>(threads, int(U)));
     auto work = [&](int th) {
       std::vector<uint64_t> m64(Sp);
-      for (size_t u = th; u < U; u += threads) {
+      for (size_t i = th; i < U; i += threads) {
+        const size_t u = rows.empty() ? i : size_t(rows[i]);
         const Topo& t = *topos_[units_[u].topo];
         const LinkState& ls = t.als.at(t.area);
         UnitView v;
         v.W = W;
         v.N = uint32_t(ls.flat().names.size());
         v.P = uint32_t(t.table.prefixes.size());
-        v.meta = meta + u * Sp;
-        for (size_t p = 0; p < v.P; ++p) m64[p] = metric[u * Sp + p];
+        v.meta = meta + i * Sp;
+        for (size_t p = 0; p < v.P; ++p) m64[p] = metric[i * Sp + p];
         v.metric = m64.data();
-        v.mask = mask + u * W * Sp;
+        v.mask = mask + i * W * Sp;
         v.maskStride = Sp;
-        out[u] = digest::unitFromRecords(keys.empty() ? unitSrc_[u] : keys[u], ls.flat(),
+        out[i] = digest::unitFromRecords(keys.empty() ? unitSrc_[u] : keys[u], ls.flat(),
                                          unitSrc_[u], t.table, *t.hashes, v, false);
       }
     };
@@ -2046,7 +2056,8 @@ PYBIND11_MODULE(_decision, m) {
            })
       .def("records_digests",
            [](const BatchRunner& b, const std::vector<std::string>& keys, py::array meta,
-              py::array metric, py::array mask, int W, int threads) {
+              py::array metric, py::array mask, int W, int threads,
+              const std::vector<int64_t>& rows) {
              auto words = [](const py::array& a, size_t n, const char* what) {
                if (a.itemsize() != 4 || !(a.flags() & py::array::c_style) ||
                    size_t(a.size()) < n) {
@@ -2055,15 +2066,17 @@ PYBIND11_MODULE(_decision, m) {
                }
                return static_cast<const uint32_t*>(a.data());
              };
-             const size_t U = b.numUnits(), Sp = std::max(b.host().maxPrefixes, 1);
+             const size_t U = rows.empty() ? b.numUnits() : rows.size();
+             const size_t Sp = std::max(b.host().maxPrefixes, 1);
              const uint32_t* me = words(meta, U * Sp, "meta");
              const uint32_t* mt = words(metric, U * Sp, "metric");
              const uint32_t* mk = words(mask, U * W * Sp, "mask");
              py::gil_scoped_release nogil;
-             return b.recordsDigests(keys, me, mt, mk, W, threads);
+             return b.recordsDigests(keys, me, mt, mk, W, threads, rows);
            },
            py::arg("keys"), py::arg("meta"), py::arg("metric"), py::arg("mask"),
-           py::arg("nh_words"), py::arg("threads") = 8)
+           py::arg("nh_words"), py::arg("threads") = 8,
+           py::arg("rows") = std::vector<int64_t>{})
       .def("route_counts",
            [](const BatchRunner& b) {
              std::vector<size_t> c;

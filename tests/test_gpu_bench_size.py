@@ -66,13 +66,14 @@ def _c3(product, names, ppn=100):
     return launches
 
 
-@pytest.mark.parametrize("o8", [0, 1])
-def test_c3_full_every_source_matches_oracle(product, o8):
+@pytest.mark.parametrize("geometry", [(0, 0), (1024, 1), (512, 3)])
+def test_c3_full_every_source_matches_oracle(product, geometry):
     """C3-full at bench size (2,080 sources x 208k prefixes) through
     bench.py's two-stream width-group launches: every source's digest equals
     the oracle's (golden per-source digests), and the job digest equals the
-    golden job digest bench.py asserts; with the default frontier kernel and
-    its 8-waves-per-SIMD build (frontier_o8)."""
+    golden job digest bench.py asserts; with the default stream geometry and
+    forced ones (frontier_block threads per workgroup, frontier_parts
+    workgroups per one-word unit, each streaming one prefix range)."""
     if not os.path.exists(C3_SOURCES):
         pytest.skip("oracle C3 per-source digests not generated")
     want = json.load(open(C3_SOURCES))
@@ -82,11 +83,14 @@ def test_c3_full_every_source_matches_oracle(product, o8):
     assert set(want) == set(names)
     import openr_amd.capi as capi
     lib = capi.load()
-    capi.check(lib, lib.ogs_set_option(b"frontier_o8", o8), "frontier_o8")
+    block, parts = geometry
+    capi.check(lib, lib.ogs_set_option(b"frontier_block", block), "frontier_block")
+    capi.check(lib, lib.ogs_set_option(b"frontier_parts", parts), "frontier_parts")
     try:
         launches = _c3(product, names)
     finally:
-        lib.ogs_set_option(b"frontier_o8", 0)
+        lib.ogs_set_option(b"frontier_block", 0)
+        lib.ogs_set_option(b"frontier_parts", 0)
     job = 0
     bad = []
     for L in launches:
@@ -102,8 +106,39 @@ def test_c3_full_every_source_matches_oracle(product, o8):
     assert {L["W"] for L in launches} == {1, 3}  # FSW (degree 84): three mask words
 
 
+@pytest.mark.parametrize("world", [8])
+def test_c3_rank_shards_xor_to_golden(product, world):
+    """The north_star's multi-GPU split: each of `world` ranks
+    runs its shard.interleave share of the 2,080 sources as its own
+    launches (bench.py --as-rank / shard_projection: c3_subset of the
+    width groups). Every shard's digest equals the XOR of its sources'
+    golden digests, and the shards XOR to the golden whole-build c3."""
+    if not os.path.exists(C3_SOURCES):
+        pytest.skip("oracle C3 per-source digests not generated")
+    import torch
+    import bench
+    import openr_amd.capi as capi
+    lib = capi.load()
+    names = c3_source_names()
+    dev = torch.device("cuda", 0)
+    launches, _ = bench.c3_launches(torch, product, capi, dev, names)
+    main = torch.cuda.current_stream(dev)
+    side = torch.cuda.Stream(dev)
+    job = 0
+    for r in range(world):
+        mine = shard.interleave(names, r, world)
+        subs = [x for x in (bench.c3_subset(L, mine) for L in launches) if x is not None]
+        assert sum(x["U"] for x in subs) == len(mine)
+        bench.c3_launch_all(lib, capi, subs, main, side)
+        torch.cuda.synchronize(dev)
+        d = shard.combine_digests(bench.c3_digest(x) for x in subs)
+        assert _h(d) == bench.c3_golden_shard(mine), r
+        job ^= d
+    assert _h(job) == GOLDEN["c3"]
+
+
 def test_c3_mixed_sources_live_oracle(product, oracle):
-    """12 C3 sources mixing SSW, FSW (W = 4) and RSW through the bench path,
+    """12 C3 sources mixing SSW, FSW (W = 3) and RSW through the bench path,
     against a LIVE oracle buildRouteDb of each (route digests)."""
     names = c3_source_names()
     pick = ["1-0-0", "1-3-17", "1-7-35", "2-0-0", "2-13-5", "2-31-7", "3-0-0", "3-4-40",

@@ -1,7 +1,11 @@
-"""Phase breakdown of the C3 frontier SPF + RouteDb kernel from a diagnostic
-(-DOGS_STAMPS) build: cycles per workgroup in setup / dist phase / next-hop
-phase / routes, relaxation rounds, and workgroup lifetimes. Run with
-OGS_LIB=openr_amd/lib/libopenr_gpu_stamps.so."""
+"""Phase breakdown of the C3 fused frontier SPF + RouteDb launches from a
+diagnostic (-DOGS_STAMPS, `make stamps`) build: per workgroup the cycles of
+setup / dist phase / next-hop phase / routes, the relaxation rounds, and
+start / end on the shader clock (100 MHz realtime), both width groups
+launched as bench.py does (two streams). Run with
+OGS_LIB=openr_amd/lib/libopenr_gpu_stamps.so; options: --as-rank r/N (one
+rank's shard), --opt name=value (ogs_set_option)."""
+import argparse
 import ctypes
 import os
 import sys
@@ -13,36 +17,51 @@ sys.path.insert(0, ROOT)
 
 
 def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--as-rank", default=None)
+    ap.add_argument("--opt", action="append", default=[])
+    a = ap.parse_args()
     import torch
     import bench
     import openr_amd
     import openr_amd.capi as capi
-    ppn = int(os.environ.get("PPN", "100"))
-    lib = capi.load()
-    dev = torch.device("cuda", 0)
+    from openr_amd import shard
     from openr_amd.workloads import c3_source_names
-    launches, N = bench.c3_launches(torch, openr_amd.decision, capi, dev, c3_source_names(),
-                                    ppn, with_sel=True)
-    stream = torch.cuda.current_stream(dev)
+    lib = capi.load()
+    for o in a.opt:
+        k, v = o.split("=")
+        capi.check(lib, lib.ogs_set_option(k.encode(), int(v)), k)
+    dev = torch.device("cuda", 0)
+    names = c3_source_names()
+    if a.as_rank:
+        r, n = (int(x) for x in a.as_rank.split("/"))
+        names = shard.interleave(names, r, n)
+    launches, _ = bench.c3_launches(torch, openr_amd.decision, capi, dev, names)
+    launches = launches[::-1]
+    main_s = torch.cuda.current_stream(dev)
+    side = torch.cuda.Stream(dev)
     for _ in range(3):
-        for L in launches:
-            capi.check(lib, lib.ogs_spf_routes(
-                ctypes.byref(L["g"]), ctypes.byref(L["pt"]),
-                ctypes.c_void_p(L["t"]["units"].data_ptr()), L["U"], L["flags"], L["W"],
-                ctypes.byref(L["so"]), ctypes.c_void_p(stream.cuda_stream)), "spf")
-        torch.cuda.synchronize()
+        bench.c3_launch_all(lib, capi, launches, main_s, side)
+    torch.cuda.synchronize()
+    raw = np.zeros(65536 * 8, dtype=np.uint32)
+    lib.ogs_diag_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int32]
+    assert lib.ogs_diag_stamps(raw.ctypes.data, raw.size) == 0
+    raw = raw.reshape(-1, 8)
+    rows = {}
     for L in launches:
-        Sp = L["h"]["max_prefixes"]
-        raw = L["o"]["sel"].cpu().numpy().view(np.uint32).reshape(L["U"], Sp)[:, :8]
-        st = raw[:, :6].astype(np.float64)
-        rt0 = raw[:, 6].astype(np.int64) - int(raw[:, 6].min())
-        rt1 = raw[:, 7].astype(np.int64) - int(raw[:, 6].min())
-        print(f"W={L['W']} units={L['U']}: WG start med={np.median(rt0)/100:.1f}us "
-              f"max={rt0.max()/100:.1f}us; end max={rt1.max()/100:.1f}us; "
-              f"life med={np.median(rt1-rt0)/100:.1f}us")
+        nwg = int(np.count_nonzero(raw[(L["W"] - 1) * 16384:(L["W"] - 1) * 16384 + 16384, 7]))
+        rows[L["W"]] = raw[(L["W"] - 1) * 16384:(L["W"] - 1) * 16384 + nwg]
+    t0 = min(int(x[:, 6].min()) for x in rows.values())
+    for W, st in sorted(rows.items()):
+        rt0 = st[:, 6].astype(np.int64) - t0
+        rt1 = st[:, 7].astype(np.int64) - t0
+        print(f"W={W} workgroups={len(st)}: start med={np.median(rt0)/100:.1f}us "
+              f"max={rt0.max()/100:.1f}us; end med={np.median(rt1)/100:.1f}us "
+              f"max={rt1.max()/100:.1f}us; life med={np.median(rt1-rt0)/100:.1f}us")
         for i, n in enumerate(["setup", "dist", "nh", "routes", "rounds_d", "rounds_nh"]):
-            print(f"   {n}: med={np.median(st[:, i]):.0f} p90={np.percentile(st[:, i], 90):.0f} "
-                  f"max={st[:, i].max():.0f}")
+            x = st[:, i].astype(np.float64)
+            print(f"   {n}: med={np.median(x):.0f} p90={np.percentile(x, 90):.0f} "
+                  f"max={x.max():.0f}")
 
 
 if __name__ == "__main__":
