@@ -323,9 +323,18 @@ class LinkState {
   const FlatTopology& flat() const;          // re-flattens when stale
   const FlatTopology& flatOnDevice() const;  // + uploads when stale
   LinkPtr linkByKey(const Link::Key& k) const { return links_.at(k); }
+  // runSpf calls the reference would make (decision.spf_runs,
+  // LinkState.cpp:727): noteSpfRuns for SPFs it never memoises (the masked
+  // getKthPaths runs, LinkState.cpp:692), noteSpf for the memoised
+  // getSpfResult(node, useLinkMetric) (LinkState.cpp:705-715) -- counted
+  // once per key until the topology changes, however many device launches
+  // or memo layers this engine uses for it
   void noteSpfRuns(uint64_t n) const {
     spfRuns_ += n;
     addStatValue("decision.spf_runs", double(n), StatType::COUNT);  // LinkState.cpp:727
+  }
+  void noteSpf(const std::string& node, bool useLinkMetric = true) const {
+    if (spfCounted_.emplace(node, useLinkMetric).second) noteSpfRuns(1);
   }
   // attribute-only updates patch the CSR in place (default) or, off,
   // re-flatten + re-upload it (A/B measurements)
@@ -356,6 +365,7 @@ class LinkState {
   std::unordered_map<std::string, bool> overloaded_;
   std::unordered_map<std::string, uint64_t> metricInc_;
   mutable std::map<std::pair<std::string, bool>, SpfResult> spfMemo_;
+  mutable std::set<std::pair<std::string, bool>> spfCounted_;  // noteSpf
   mutable std::map<std::tuple<std::string, std::string, size_t>,
                    std::vector<Path>>
       kthMemo_;
@@ -391,10 +401,23 @@ class PrefixState {
                                      const std::string& area,
                                      const std::string& prefix);
   uint64_t version() const { return version_; }
+  // Every changed network in change order -- what Decision collects as
+  // DecisionPendingUpdates::updatedPrefixes (Decision.cpp:35-60) and loops
+  // over in the incremental branch of rebuildRoutes (Decision.cpp:929-951).
+  // Entry i of changeLog() has the absolute position changeLogBase() + i;
+  // the oldest half is dropped past kChangeLogCap entries (a reader behind
+  // changeLogBase() has lost its place and must not rely on it).
+  const std::vector<std::string>& changeLog() const { return changeLog_; }
+  uint64_t changeLogBase() const { return changeLogBase_; }
+  uint64_t changeLogEnd() const { return changeLogBase_ + changeLog_.size(); }
+  static constexpr size_t kChangeLogCap = size_t(1) << 20;
 
  private:
+  void logChange(const std::string& network);
   std::map<std::string, Entries> prefixes_;
   uint64_t version_{0};
+  std::vector<std::string> changeLog_;
+  uint64_t changeLogBase_{0};
 };
 
 // ------------------------------------------------------------ RIB types --
@@ -556,6 +579,10 @@ class SpfSolver {
       const {
     return bestRoutesCache_;
   }
+  // per-prefix calls answered from one batch (createRouteForPrefixOr-
+  // GetStaticRoute): launches made / prefixes they computed (tests, bench)
+  uint64_t incrementalBatches() const { return incBatches_; }
+  uint64_t incrementalBatchPrefixes() const { return incBatchPrefixes_; }
   // GPU-side RibPolicy (UCMP weights): when set and active, buildRouteDb
   // returns the routes RibPolicy::applyPolicy would leave (the reference's
   // buildRouteDb + Decision's applyPolicy on the result, Decision.cpp:
@@ -582,6 +609,10 @@ class SpfSolver {
                          const std::string& area, const PrefixState& ps,
                          const PrefixState& sub,
                          std::map<std::string, std::optional<RibUnicastEntry>>& out);
+  // createRoutesForPrefixes without the counters or the static fallback
+  std::map<std::string, std::optional<RibUnicastEntry>> computeRoutes(
+      const std::string& me, const AreaLinkStates& als, const PrefixState& ps,
+      const std::set<std::string>& prefixes);
   void prepareMultiArea(const AreaLinkStates& areaLinkStates,
                         const PrefixState& prefixState);
   struct MultiAreaResult {  // host copies of one source's GPU results
@@ -605,6 +636,27 @@ class SpfSolver {
   std::unique_ptr<Impl> impl_;
   std::map<std::string, RibUnicastEntry> staticUnicastRoutes_;
   std::map<std::string, RouteSelectionResult> bestRoutesCache_;
+  // Per-prefix calls of Decision's incremental loop: the first call after a
+  // PrefixState / topology change computes every prefix changed since the
+  // last build or batch (PrefixState::changeLog) in ONE batch; the rest of
+  // the loop is served from incCache_, valid for (me, PrefixState version --
+  // a process-unique stamp --, the areas' topology versions). Each entry
+  // keeps the prefix's best-route selection too: the selection cache
+  // (getBestRoutesCache) changes only when the prefix itself is asked, as
+  // with the reference's per-prefix calls.
+  struct IncEntry {
+    std::optional<RibUnicastEntry> route;
+    std::optional<RouteSelectionResult> sel;  // nullopt: no cache entry
+    bool touched{false};  // a known, ungated prefix: its cache entry is reset
+  };
+  std::unordered_map<std::string, IncEntry> incCache_;
+  const PrefixState* incPs_{nullptr};
+  uint64_t incPsVersion_{~0ull}, incLogCursor_{0};
+  std::string incMe_;
+  std::vector<std::pair<const FlatTopology*, uint64_t>> incTopo_;
+  uint64_t incBatches_{0}, incBatchPrefixes_{0};
+  std::unique_ptr<SpfSolver> probe_;  // multi-area sub-table builds
+  bool quietStats_{false};             // probe_: no route-build counters
   const RibPolicy* ribPolicy_{nullptr};
   std::string myNodeName_;
   bool enableV4_, enableNodeSegmentLabel_, enableBestRouteSelection_,

@@ -45,7 +45,8 @@ class DeviceBuffer {
     owned_ = false;
   }
 
-  void resize(size_t bytes) {  // grow-only, contents not preserved
+  size_t capacity() const { return cap_; }
+  void resize(size_t bytes) {  // grow-only, contents kept within capacity()
     if (bytes <= cap_) {
       size_ = bytes;
       return;

@@ -25,7 +25,13 @@ const std::vector<LinkState::Path>& LinkState::getKthPaths(
   std::vector<Path> paths;
   auto sIt = f.id.find(src), dIt = f.id.find(dest);
   if (sIt == f.id.end() || dIt == f.id.end() || src == dest) {
-    // unknown endpoints or src == dest: the reference finds no path
+    // unknown endpoints or src == dest: the reference finds no path (after
+    // its SPF, which it counts)
+    if (ignore.empty()) {
+      noteSpf(src);
+    } else {
+      noteSpfRuns(1);
+    }
     return kthMemo_.emplace(key, std::move(paths)).first->second;
   }
   const uint32_t E = uint32_t(f.edges.size());
@@ -73,7 +79,13 @@ const std::vector<LinkState::Path>& LinkState::getKthPaths(
                          mask.empty() ? nullptr : dMask.as<uint32_t>(),
                          maskWords, flags, &out, nullptr),
            "ogs_ksp_paths");
-  noteSpfRuns(1);
+  // k = 1 traces the memoised getSpfResult(src), k > 1 a masked runSpf
+  // (LinkState.cpp:690-692)
+  if (ignore.empty()) {
+    noteSpf(src);
+  } else {
+    noteSpfRuns(1);
+  }
   uint32_t count = 0;
   dCount.download(&count, 1);
   ogsCheck(ogs_stream_sync(nullptr), "ogs_stream_sync");
@@ -301,7 +313,10 @@ void LinkState::prefetchKthPaths(const std::string& src,
   Ksp2Batch b(*this, src, todo);
   b.launch();
   b.fetch();
-  if (b.numUnits()) noteSpfRuns(1 + b.numUnits());
+  if (b.numUnits()) {
+    noteSpf(src);  // k = 1: getSpfResult(src)
+    noteSpfRuns(b.numUnits());  // k = 2: one masked runSpf per destination
+  }
   for (size_t i = 0; i < todo.size(); ++i) {
     kthMemo_[{src, todo[i], 1}] = b.paths(i, 1);
     kthMemo_[{src, todo[i], 2}] = b.paths(i, 2);

@@ -80,6 +80,7 @@ void LinkState::invalidate(bool topologyChanged) {
   flatStale_ = true;
   if (topologyChanged) {  // LinkState.cpp:635-638
     spfMemo_.clear();
+    spfCounted_.clear();
     kthMemo_.clear();
   }
 }
@@ -526,7 +527,7 @@ const LinkState::SpfResult& LinkState::getSpfResult(const std::string& node,
   const auto t0 = std::chrono::steady_clock::now();  // decision.spf_ms (LinkState.cpp:818)
   const FlatTopology& f = flatOnDevice();
   auto idIt = f.id.find(node);
-  noteSpfRuns(1);
+  noteSpf(node, useLinkMetric);
   if (idIt == f.id.end()) {
     res.emplace(node, NodeSpfResult(0));  // unknown source settles only itself
     addStatValue("decision.spf_ms", msSince(t0), StatType::AVG);

@@ -156,7 +156,7 @@ void RouteDbBatch::launch(void* stream) {
     ogsCheck(ogs_spf_routes(&g, hb_.maxPrefixes ? &pt : nullptr, G.units.as<ogs_unit>(),
                             int32_t(G.members.size()), flags, G.W, &out, stream),
              "ogs_spf_routes(batch)");
-    ls_->noteSpfRuns(G.members.size());
+    for (uint32_t m : G.members) ls_->noteSpf(sources_[m]);
   }
   launched_ = true;
 }

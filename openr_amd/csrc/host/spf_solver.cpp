@@ -73,6 +73,15 @@ uint64_t nextVersionStamp() {
 }
 
 // ----------------------------------------------------------- PrefixState --
+void PrefixState::logChange(const std::string& network) {
+  if (changeLog_.size() >= kChangeLogCap) {
+    const size_t drop = changeLog_.size() / 2;
+    changeLog_.erase(changeLog_.begin(), changeLog_.begin() + drop);
+    changeLogBase_ += drop;
+  }
+  changeLog_.push_back(network);
+}
+
 std::set<std::string> PrefixState::updatePrefixKeyed(const std::string& node,
                                                      const std::string& area,
                                                      const std::string& network,
@@ -84,6 +93,7 @@ std::set<std::string> PrefixState::updatePrefixKeyed(const std::string& node,
   changed.insert(network);
   it->second = std::make_shared<PrefixEntry>(std::move(entry));
   version_ = nextVersionStamp();
+  logChange(network);
   return changed;
 }
 
@@ -107,6 +117,7 @@ std::set<std::string> PrefixState::deletePrefix(const std::string& node,
   auto it = prefixes_.find(prefixNetworkKey(prefix, /*applyMask=*/false));
   if (it != prefixes_.end() && it->second.erase(std::make_pair(node, area))) {
     changed.insert(it->first);
+    logChange(it->first);
     if (it->second.empty()) prefixes_.erase(it);
     version_ = nextVersionStamp();
   }
@@ -786,13 +797,21 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(
   for (const auto& [_, l] : als) exists |= l.hasNode(me);
   if (!exists) return std::nullopt;
   const auto t0 = std::chrono::steady_clock::now();
-  addStatValue("decision.route_build_runs", 1, StatType::COUNT);  // SpfSolver.cpp:327
-  // SpfSolver.cpp:334-339: one createRouteForPrefix per known prefix
-  addStatValue("decision.get_route_for_prefix", double(ps.prefixes().size()),
-               StatType::COUNT);
+  if (!quietStats_) {
+    addStatValue("decision.route_build_runs", 1, StatType::COUNT);  // SpfSolver.cpp:327
+    // SpfSolver.cpp:334-339: one createRouteForPrefix per known prefix
+    addStatValue("decision.get_route_for_prefix", double(ps.prefixes().size()),
+                 StatType::COUNT);
+  }
   auto db = als.size() > 1 ? buildRouteDbMultiArea(me, als, ps)
                            : buildRouteDbSingleArea(me, als, ps);
-  addStatValue("decision.route_build_ms", msSince(t0), StatType::AVG);  // SpfSolver.cpp:450
+  // every change so far is in this build: the next incremental loop's
+  // batch starts after it
+  incPs_ = &ps;
+  incLogCursor_ = ps.changeLogEnd();
+  if (!quietStats_) {
+    addStatValue("decision.route_build_ms", msSince(t0), StatType::AVG);  // SpfSolver.cpp:450
+  }
   return db;
 }
 
@@ -825,7 +844,13 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDbSingleArea(
     I.unitSrc = s;
   }
   const ResultImage L(N, P, W, db);
-  I.spfTopo = nullptr;  // res is overwritten below
+  // SPF memo (LinkState::getSpfResult, LinkState.cpp:705-715): res still
+  // holds this source's SPF of this topology version (dist / nh / reach
+  // spans depend on N, W and the distance width only) -> the route pass
+  // alone, no SPF relaunch (ogs_routes_from_spf)
+  const bool memoHit = I.spfTopo == &f && I.spfVersion == f.version && I.spfSrc == s &&
+      I.spfN == N && I.spfW == W && I.spfDb == db && I.res.capacity() >= L.end;
+  if (!memoHit) I.spfTopo = nullptr;  // res is overwritten below
   I.res.resize(L.end);
   I.hRes.resize(L.end);
 
@@ -843,10 +868,22 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDbSingleArea(
       (v4OverV6Nexthop_ ? OGS_F_V4_OVER_V6 : 0u) |
       (enableBestRouteSelection_ ? OGS_F_BEST_ROUTE_SELECTION : 0u) |
       (wide ? OGS_F_WIDE_METRIC : 0u) | (exact ? OGS_F_EXACT_ORDER : 0u);
-  ogsCheck(ogs_spf_routes(&g, P ? &pt : nullptr, I.unit.as<ogs_unit>(), 1,
-                          flags, W, &out, nullptr),
-           "ogs_spf_routes");
-  ls.noteSpfRuns(1);
+  if (memoHit) {
+    if (P) {
+      ogs_spf_out ro = out;
+      ro.dist = nullptr;
+      ro.nh = nullptr;
+      ro.reached = nullptr;
+      ogsCheck(ogs_routes_from_spf(&g, &pt, I.unit.as<ogs_unit>(), 1, out.dist, out.nh,
+                                   exact ? out.reached : nullptr, flags, W, &ro, nullptr),
+               "ogs_routes_from_spf");
+    }
+  } else {
+    ogsCheck(ogs_spf_routes(&g, P ? &pt : nullptr, I.unit.as<ogs_unit>(), 1,
+                            flags, W, &out, nullptr),
+             "ogs_spf_routes");
+  }
+  ls.noteSpf(me);
   I.spfTopo = &f;
   I.spfVersion = f.version;
   I.spfSrc = s;
@@ -937,7 +974,7 @@ void SpfSolver::routesFromSpfMemo(const std::string& me, const LinkState& ls,
     so.reached = exact ? devAt<uint32_t>(I.res, L.reach) : nullptr;
     ogsCheck(ogs_spf_routes(&g, nullptr, I.unit.as<ogs_unit>(), 1, flags, W, &so, nullptr),
              "ogs_spf_routes");
-    ls.noteSpfRuns(1);
+    ls.noteSpf(me);
     I.spfTopo = &f;
     I.spfVersion = f.version;
     I.spfSrc = s;
@@ -1250,7 +1287,7 @@ void SpfSolver::enqueueMultiArea(const std::string& me, const AreaLinkStates& al
                           flags, W, &spf, stream),
            "ogs_spf_routes");
   for (const auto& [area, ls] : als) {
-    if (ls.flat().id.count(me)) ls.noteSpfRuns(1);
+    if (ls.flat().id.count(me)) ls.noteSpf(me);
   }
 
   // ---- multi-area RouteDb --------------------------------------------------
@@ -1367,15 +1404,92 @@ DecisionRouteDb SpfSolver::downloadMultiArea(const std::string& me,
 std::optional<RibUnicastEntry> SpfSolver::createRouteForPrefixOrGetStaticRoute(
     const std::string& me, const AreaLinkStates& als, const PrefixState& ps,
     const std::string& prefix) {  // SpfSolver.cpp:139-158
-  return createRoutesForPrefixes(me, als, ps, {prefix}).at(prefix);
+  addStatValue("decision.get_route_for_prefix", 1.0, StatType::COUNT);  // :166
+  std::vector<std::pair<const FlatTopology*, uint64_t>> topo;
+  for (const auto& [_, l] : als) {
+    const FlatTopology& f = l.flat();
+    topo.emplace_back(&f, f.version);
+  }
+  if (incMe_ != me || incPsVersion_ != ps.version() || incTopo_ != topo) {
+    incCache_.clear();
+    incMe_ = me;
+    incPsVersion_ = ps.version();
+    incTopo_ = std::move(topo);
+  }
+  auto hit = incCache_.find(prefix);
+  if (hit == incCache_.end()) {
+    // this call and every prefix changed since the last build / batch
+    // (Decision's pending updatedPrefixes, the loop this call is part of)
+    std::set<std::string> batch{prefix};
+    if (incPs_ != &ps || incLogCursor_ < ps.changeLogBase()) {
+      incPs_ = &ps;
+      incLogCursor_ = ps.changeLogBase();  // unknown position: the whole log
+    }
+    const auto& log = ps.changeLog();
+    for (size_t i = size_t(incLogCursor_ - ps.changeLogBase()); i < log.size(); ++i) {
+      batch.insert(log[i]);
+    }
+    incLogCursor_ = ps.changeLogEnd();
+    ++incBatches_;
+    incBatchPrefixes_ += batch.size();
+    // the batch's selections go into the entries; bestRoutesCache_ keeps
+    // the pre-batch state until each prefix is asked
+    std::vector<std::pair<std::string, std::optional<RouteSelectionResult>>> pre;
+    for (const auto& p : batch) {
+      auto b = bestRoutesCache_.find(p);
+      pre.emplace_back(p, b == bestRoutesCache_.end()
+                              ? std::nullopt
+                              : std::optional<RouteSelectionResult>(b->second));
+    }
+    auto routes = computeRoutes(me, als, ps, batch);
+    for (auto& [p, before] : pre) {
+      IncEntry& e = incCache_[p];
+      e.route = std::move(routes[p]);
+      auto b = bestRoutesCache_.find(p);
+      e.sel = b == bestRoutesCache_.end() ? std::nullopt
+                                          : std::optional<RouteSelectionResult>(b->second);
+      // SpfSolver.cpp:170-185: a gated or unknown prefix returns before the
+      // selection cache is touched
+      e.touched = ps.prefixes().count(p) && !(isV4Prefix(p) && !enableV4_ && !v4OverV6Nexthop_);
+      if (before) {
+        bestRoutesCache_[p] = std::move(*before);
+      } else if (b != bestRoutesCache_.end()) {
+        bestRoutesCache_.erase(b);
+      }
+    }
+    hit = incCache_.find(prefix);
+  }
+  if (hit->second.touched) {  // SpfSolver.cpp:185, :239 for this prefix
+    if (hit->second.sel) {
+      bestRoutesCache_[prefix] = *hit->second.sel;
+    } else {
+      bestRoutesCache_.erase(prefix);
+    }
+  }
+  if (hit->second.route) return hit->second.route;
+  auto it = staticUnicastRoutes_.find(prefix);  // static routes as the fallback
+  if (it != staticUnicastRoutes_.end()) return it->second;
+  return std::nullopt;
 }
 
 std::map<std::string, std::optional<RibUnicastEntry>> SpfSolver::createRoutesForPrefixes(
     const std::string& me, const AreaLinkStates& als, const PrefixState& ps,
     const std::set<std::string>& prefixes) {
-  std::map<std::string, std::optional<RibUnicastEntry>> out;
   // SpfSolver.cpp:166: one createRouteForPrefix per asked prefix
   addStatValue("decision.get_route_for_prefix", double(prefixes.size()), StatType::COUNT);
+  auto out = computeRoutes(me, als, ps, prefixes);
+  for (auto& [prefix, route] : out) {  // static routes as the fallback
+    if (route) continue;
+    auto it = staticUnicastRoutes_.find(prefix);
+    if (it != staticUnicastRoutes_.end()) route = it->second;
+  }
+  return out;
+}
+
+std::map<std::string, std::optional<RibUnicastEntry>> SpfSolver::computeRoutes(
+    const std::string& me, const AreaLinkStates& als, const PrefixState& ps,
+    const std::set<std::string>& prefixes) {
+  std::map<std::string, std::optional<RibUnicastEntry>> out;
   bool exists = false;  // SpfSolver.cpp:139-158 per prefix
   for (const auto& [_, l] : als) exists |= l.hasNode(me);
   PrefixState sub;  // the changed prefixes through one route launch
@@ -1400,8 +1514,15 @@ std::map<std::string, std::optional<RibUnicastEntry>> SpfSolver::createRoutesFor
     const LinkState& ls = singleArea(als, area);
     routesFromSpfMemo(me, ls, area, ps, sub, out);
   } else if (!asked.empty()) {
-    SpfSolver probe(myNodeName_, enableV4_, false, enableBestRouteSelection_,
-                    v4OverV6Nexthop_);
+    // several areas: the multi-area build over the sub-table on a private
+    // solver kept across calls (its domain CSR stays on the device while the
+    // topology is unchanged); its builds are not Decision's route builds
+    if (!probe_) {
+      probe_ = std::make_unique<SpfSolver>(myNodeName_, enableV4_, false,
+                                           enableBestRouteSelection_, v4OverV6Nexthop_);
+      probe_->quietStats_ = true;
+    }
+    SpfSolver& probe = *probe_;
     auto db = probe.buildRouteDb(me, als, sub);
     const auto& bcache = probe.getBestRoutesCache();
     for (const auto& prefix : asked) {
@@ -1413,11 +1534,6 @@ std::map<std::string, std::optional<RibUnicastEntry>> SpfSolver::createRoutesFor
       if (bc != bcache.end()) bestRoutesCache_[prefix] = bc->second;
       else bestRoutesCache_.erase(prefix);
     }
-  }
-  for (auto& [prefix, route] : out) {  // static routes as the fallback
-    if (route) continue;
-    auto it = staticUnicastRoutes_.find(prefix);
-    if (it != staticUnicastRoutes_.end()) route = it->second;
   }
   return out;
 }

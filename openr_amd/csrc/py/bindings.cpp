@@ -1359,6 +1359,8 @@ PYBIND11_MODULE(_decision, m) {
              }
              return out;
            })
+      .def("incrementalBatches", &SpfSolver::incrementalBatches)
+      .def("incrementalBatchPrefixes", &SpfSolver::incrementalBatchPrefixes)
       .def("updateStaticUnicastRoutes",
            [](SpfSolver& s, py::dict upd, std::vector<std::string> del) {
              std::map<std::string, RibUnicastEntry> u;
@@ -1540,7 +1542,21 @@ PYBIND11_MODULE(_decision, m) {
             if (i++ % stride == 0 && int(changed.size()) < n) changed.insert(p);
           }
           SpfSolver a("test_node", true, false, false, false), b("test_node", true, false, false, false);
-          a.createRoutesForPrefixes(me, als, ps, changed);  // warm (SPF memo, device)
+          // Decision's flow (Decision.cpp:912-951): a full build, then
+          // publications change the prefixes (a tag added to each entry),
+          // then the incremental branch over the changed set
+          a.buildRouteDb(me, als, ps);
+          b.buildRouteDb(me, als, ps);
+          std::vector<std::tuple<NodeAndArea, std::string, PrefixEntry>> upd;
+          for (const auto& p : changed) {
+            for (const auto& [na, e] : ps.prefixes().at(p)) {
+              PrefixEntry e2 = *e;
+              e2.tags.insert("incremental");
+              upd.emplace_back(na, p, std::move(e2));
+            }
+          }
+          for (auto& [na, p, e] : upd) ps.updatePrefixKeyed(na.first, na.second, p, std::move(e));
+          a.createRoutesForPrefixes(me, als, ps, changed);  // warm (device sub-table)
           auto t0 = std::chrono::steady_clock::now();
           auto batch = a.createRoutesForPrefixes(me, als, ps, changed);
           auto t1 = std::chrono::steady_clock::now();

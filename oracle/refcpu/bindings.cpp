@@ -1272,12 +1272,25 @@ PYBIND11_MODULE(_refcpu, m) {
           Workspace w;
           auto& ls = w.als.emplace(g.area, LinkState(g.area, "test_node")).first->second;
           loadLsdb(g, ls, w.ps);
-          std::vector<std::string> changed;
-          const size_t stride = std::max<size_t>(1, w.ps.prefixes().size() / std::max(n, 1));
-          size_t i = 0;
-          for (const auto& [p, _] : w.ps.prefixes()) {
-            if (i++ % stride == 0 && int(changed.size()) < n) changed.push_back(p);
+          // the engine bench's prefixes (every stride-th in sorted order) and
+          // change (a tag added to each entry), after the SPF memo a previous
+          // build left (Decision.cpp:912-951)
+          std::vector<std::string> all, changed;
+          for (const auto& [p, _] : w.ps.prefixes()) all.push_back(p);
+          std::sort(all.begin(), all.end());
+          const size_t stride = std::max<size_t>(1, all.size() / std::max(n, 1));
+          for (size_t i = 0; i < all.size(); ++i) {
+            if (i % stride == 0 && int(changed.size()) < n) changed.push_back(all[i]);
           }
+          std::vector<std::tuple<std::string, std::string, PrefixEntry>> upd;
+          for (const auto& p : changed) {
+            for (const auto& [na, e] : w.ps.prefixes().at(p)) {
+              PrefixEntry e2 = *e;
+              e2.tags.insert("incremental");
+              upd.emplace_back(na.first, na.second, std::move(e2));
+            }
+          }
+          for (auto& [node, area, e] : upd) w.ps.updatePrefix(node, area, e);
           SpfSolver solver("test_node", true, false, false);
           ls.getSpfResult(me, true);  // the memo a previous build left
           size_t routes = 0;

@@ -45,10 +45,46 @@ def test_decision_counters(product):
     assert c["decision.route_build_runs.count"] == 3
     assert c["decision.get_route_for_prefix.count"] == 3 * 4
     assert c["decision.no_route_to_prefix.count"] == 3  # fc00::4 each build
-    assert c["decision.spf_runs.count"] >= 4  # 3 builds (fused SPF) + getSpfResult("2")
+    # the reference memoises getSpfResult per (node, useLinkMetric) until the
+    # topology changes (LinkState.cpp:705-715): the 3 builds of "1" run ONE
+    # SPF, getSpfResult("2") another
+    assert c["decision.spf_runs.count"] == 2
     for key in ("decision.route_build_ms", "decision.spf_ms", "decision.gpu.prepare_ms",
                 "decision.gpu.launch_ms", "decision.gpu.materialize_ms"):
         assert c[key + ".count"] >= 1 and c[key + ".avg"] >= 0.0, key
     assert c["decision.route_build_ms.count"] == 3
     M.reset_decision_counters()
     assert M.decision_counters() == {}
+
+
+def test_spf_runs_ring_four_sources(product):
+    """SpfSolverTest.cpp:1655-1667 SimpleRingTopologyFixture.ShortestPathTest:
+    route maps of 4 sources with node segment labels run exactly 4 SPFs
+    (decision.spf_runs.count == 4). Building them again, or asking
+    getSpfResult / getKthPaths(k = 1) of those sources, runs none (the memo);
+    a topology change invalidates it (LinkState.cpp:635-638)."""
+    M = product
+    als = M.AreaLinkStates()
+    ls = als.add(A, "1")
+    for db in (L.createAdjDb("1", [L.adj12, L.adj13], 1), L.createAdjDb("2", [L.adj21, L.adj24], 2),
+               L.createAdjDb("3", [L.adj31, L.adj34], 3), L.createAdjDb("4", [L.adj42, L.adj43], 4)):
+        ls.updateAdjacencyDatabase(db, A)
+    ps = M.PrefixState()
+    for p in (L.prefixDb1, L.prefixDb2, L.prefixDb3, L.prefixDb4):
+        L.updatePrefixDatabase(ps, p)
+    solver = M.SpfSolver("1", False, True)
+    M.reset_decision_counters()
+    rm = L.getRouteMap(solver, ["1", "2", "3", "4"], als, ps)
+    assert len(rm) == 28
+    assert M.decision_counters()["decision.spf_runs.count"] == 4
+    assert L.getRouteMap(solver, ["1", "2", "3", "4"], als, ps) == rm
+    ls.getSpfResult("3")
+    ls.getKthPaths("2", "4", 1)
+    assert M.decision_counters()["decision.spf_runs.count"] == 4
+    ls.getKthPaths("2", "4", 2)  # a masked runSpf (LinkState.cpp:690-692)
+    assert M.decision_counters()["decision.spf_runs.count"] == 5
+    adj12b = L.createAdjacency("2", "1/2", "2/1", "fe80::2", "192.168.0.2", 30, 100002)
+    assert ls.updateAdjacencyDatabase(L.createAdjDb("1", [adj12b, L.adj13], 1), A)["topologyChanged"]
+    rm2 = L.getRouteMap(solver, ["1", "2", "3", "4"], als, ps)
+    assert rm2 != rm
+    assert M.decision_counters()["decision.spf_runs.count"] == 9

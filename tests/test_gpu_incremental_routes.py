@@ -135,3 +135,52 @@ def test_source_absent(product, oracle):
     pp, op = _prefixes(product), _prefixes(oracle)
     ps_, os_ = _solvers(product, oracle, "99", True, True)
     _check(ps_, os_, "99", pa, pp, oa, op, "absent")
+
+
+@pytest.mark.parametrize("areas", [1, 2])
+def test_incremental_loop_one_batch(product, oracle, areas):
+    """Decision's incremental loop as the reference runs it
+    (Decision.cpp:929-951): after a full build, publications change a set
+    of prefixes, then createRouteForPrefixOrGetStaticRoute is called once per
+    changed prefix. The engine answers the whole loop from ONE batch over the
+    PrefixState change log; every answer and the best-route selection cache
+    after every call equal the oracle's per-prefix calls; single area and a
+    two-area domain (the second area holds the source too)."""
+    doms = []
+    for M in (product, oracle):
+        als, ls = _grid(M)
+        if areas == 2:
+            ls2 = als.add("area2", "12")
+            ls2.updateAdjacencyDatabase(L.createAdjDb("12", [L.createAdjacency(
+                "x1", "e1", "f1", "fe80::e1", "10.7.0.1", 3, 200001)], 13), "area2")
+            ls2.updateAdjacencyDatabase(L.createAdjDb("x1", [L.createAdjacency(
+                "12", "f1", "e1", "fe80::c", "10.7.0.2", 3, 200002)], 300), "area2")
+        ps = _prefixes(M)
+        if areas == 2:
+            L.updatePrefixDatabase(ps, L.createPrefixDb("x1", [L.createPrefixEntry("fc00::aa/128")]),
+                                   "area2")
+        doms.append((als, ps))
+    ps_, os_ = _solvers(product, oracle, "12", True, True)
+    (pa, pp), (oa, op) = doms
+    assert ps_.buildRouteDb("12", pa, pp).canonical() == os_.buildRouteDb("12", oa, op).canonical()
+    assert ps_.getBestRoutesCache() == os_.getBestRoutesCache()
+    changed = set()
+    for ps in (pp, op):
+        for n, pfx in ((6, "fc00::aa/128"), (9, "fc00::3/128"), (17, "fc00::77/128"),
+                       (2, "10.0.3.0/24")):
+            changed |= set(L.updatePrefixDatabase(ps, L.createPrefixDb(
+                str(n), [L.createPrefixEntry(f"fc00::{n:x}/128"), L.createPrefixEntry(pfx)])))
+    changed = sorted(changed)
+    assert len(changed) >= 4
+    b0 = ps_.incrementalBatches()
+    for pfx in changed:
+        got = ps_.createRouteForPrefixOrGetStaticRoute("12", pa, pp, pfx)
+        want = os_.createRouteForPrefixOrGetStaticRoute("12", oa, op, pfx)
+        assert got == want, pfx
+        assert ps_.getBestRoutesCache() == os_.getBestRoutesCache(), pfx
+    assert ps_.incrementalBatches() == b0 + 1
+    # a prefix outside the changed set: one more (single-prefix) batch
+    for pfx in ("fc00::c/128", "fc00::beef/128"):
+        assert ps_.createRouteForPrefixOrGetStaticRoute("12", pa, pp, pfx) == \
+            os_.createRouteForPrefixOrGetStaticRoute("12", oa, op, pfx)
+        assert ps_.getBestRoutesCache() == os_.getBestRoutesCache(), pfx
