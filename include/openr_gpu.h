@@ -49,8 +49,9 @@ extern "C" {
 /* ABI version of this header: a consumer checks ogs_abi_version() ==
  * OGS_ABI_VERSION once at start-up. 3: ogs_spf_out.reached,
  * ogs_area_table.reached, ogs_routes_from_spf(spf_reached), u16 RibPolicy
- * statement ids, ogs_graph.rslot_ext (rows of 511+ edges). */
-#define OGS_ABI_VERSION 3
+ * statement ids, ogs_graph.rslot_ext (rows of 511+ edges). 4:
+ * ogs_spf_routes_variants writes ogs_route_diff.base_desc_valid back. */
+#define OGS_ABI_VERSION 4
 
 /* ---- status codes ------------------------------------------------------ */
 #define OGS_OK 0
@@ -463,10 +464,13 @@ typedef struct ogs_route_diff {
   /* Optional caller-held cache of the base unit's tight-DAG descendant rows
    * (OGS_F_INCREMENTAL repair; [S_n * ceil(S_n/32)] words, S_n <= 16384):
    * base_desc_valid == 0 -> the rows are computed into base_desc by this
-   * call, 1 -> reused as they are. They depend only on the topology, the
-   * source and the base SPF: the caller clears the flag when any of them
-   * changes (the memo rule of LinkState.cpp:635-638) and sets it after the
-   * first call. NULL: rebuilt in the workspace on every call. */
+   * call, 1 -> reused as they are. In / out: the call sets it to 1 when it
+   * wrote the rows into base_desc and leaves it as it was otherwise (the
+   * repair did not apply, or "c4_desc" is 0), so the caller keeps the
+   * flag across calls. The rows depend only on the topology, the source
+   * and the base SPF: the caller clears the flag when any of them changes
+   * (the memo rule of LinkState.cpp:635-638). NULL: rebuilt in the
+   * workspace on every call. */
   uint32_t* base_desc;
   int32_t base_desc_valid;
 } ogs_route_diff;
@@ -480,7 +484,7 @@ int ogs_spf_routes_variants(const ogs_graph* graph,
                             const ogs_prefix_table* prefixes,
                             const ogs_unit* units /* device */, int32_t n_units,
                             const ogs_unit_mods* mods,
-                            const ogs_route_diff* diff, uint32_t flags,
+                            ogs_route_diff* diff, uint32_t flags,
                             int32_t nh_words, ogs_spf_out* out, void* stream);
 
 /* Compact list of the changed routes of n_units variants (SURVEY.md §8(f)
@@ -522,9 +526,9 @@ int ogs_csr_patch(uint64_t* edges, const uint32_t* idx, const uint64_t* val,
  * RibPolicy.cpp:74-249): statements 0..K-1 in policy order. A policy of
  * more than 32 statements is applied as consecutive calls over chunks of
  * <= 32 (statement_base = 0, 32, 64, ...): a call with statement_base > 0
- * leaves the routes an earlier chunk transformed (applied != 0xFF) as they
- * are and continues the others' counter. Statement indexes are u8 (0xFF =
- * none): statement_base + K <= 255. */
+ * leaves the routes an earlier chunk transformed (applied !=
+ * OGS_POLICY_NONE) as they are and continues the others' counter. Statement
+ * indexes are u16 (OGS_POLICY_NONE = none): statement_base + K <= 65,535. */
 #define OGS_POLICY_NONE 0xFFFFu /* applied / counter: no statement */
 
 typedef struct ogs_rib_policy {

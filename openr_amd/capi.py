@@ -6,7 +6,7 @@ import ctypes
 from . import LIB_PATH
 
 OGS_OK = 0
-OGS_ABI_VERSION = 3  # include/openr_gpu.h
+OGS_ABI_VERSION = 4  # include/openr_gpu.h
 OGS_F_ENABLE_V4 = 0x01
 OGS_F_V4_OVER_V6 = 0x02
 OGS_F_BEST_ROUTE_SELECTION = 0x04

@@ -869,11 +869,12 @@ DecisionRouteDb materializeRouteDb(
 // run in one launch (ogs_spf_routes_variants, route diff fused in); only the
 // changed records are gathered on the device (ogs_route_changes_gather) and
 // materialised. Areas with zero / negative link metrics or path sums past 32
-// bits, and sources of degree > 128, run each variant as its own topology in one ogs_spf_routes launch
-// (exact extraction order, 64-bit distances) and diff on the host with
-// calculateUpdate. Node-segment labels are not part of the sweep (off in the
-// DecisionBenchmark config). `ls` and `ps` must outlive the
-// sweep unchanged.
+// bits, and sources of degree > 128, run each variant as its own topology
+// (exact extraction order, 64-bit distances), in ogs_spf_routes launches of
+// up to kExactChunk (256) topologies each, rebuilt from the live `ls` / `ps`
+// at launch time, and diff on the host with calculateUpdate. Node-segment
+// labels are not part of the sweep (off in the DecisionBenchmark config,
+// SURVEY.md A.8). `ls` and `ps` must outlive the sweep unchanged.
 class LinkFailureSweep {
  public:
   struct LinkDown {  // one end of the link: (node, its interface)

@@ -336,7 +336,7 @@ void LinkFailureSweep::launch(void* stream, bool records) {
   ogsCheck(ogs_spf_routes_variants(&g, &pt, dUnits_.as<ogs_unit>(), int32_t(numVariants()),
                                    &mods, &diff, fl, W_, &out, stream),
            "ogs_spf_routes_variants");
-  if (fl & OGS_F_INCREMENTAL) descValid_ = true;
+  descValid_ = diff.base_desc_valid != 0;  // set by the library when it wrote the rows
   recordsRun_ = records;
   changedOnlyRun_ = records && changedOnly;
 }

@@ -48,7 +48,7 @@ hipError_t launch_routes_multiarea(const ogs_graph& g, const ogs_prefix_table& p
                                    const ogs_spf_out& out, hipStream_t stream);
 hipError_t launch_variants(const ogs_graph& g, const ogs_prefix_table& pt,
                            const ogs_unit* units, int nUnits,
-                           const ogs_unit_mods* mods, const ogs_route_diff* diff,
+                           const ogs_unit_mods* mods, ogs_route_diff* diff,
                            uint32_t flags, int W, const ogs_spf_out& out,
                            hipStream_t stream, int* unsupported);
 hipError_t launch_rib_policy(const ogs_prefix_table& pt, const ogs_rib_policy& pol,
@@ -188,7 +188,7 @@ int ogs_set_option(const char* name, int64_t value) {
     return OGS_OK;
   }
   if (std::strcmp(name, "route_stream") == 0) {
-    if (value < 0 || value > 3) return fail(OGS_E_INVALID, "route_stream must be 0, 1, 2 or 3");
+    if (value < 0 || value > 4) return fail(OGS_E_INVALID, "route_stream must be in [0, 4]");
     ogs::g_routeStream = int(value);
     return OGS_OK;
   }
@@ -478,7 +478,7 @@ int ogs_spf_routes_variants(const ogs_graph* graph,
                             const ogs_prefix_table* prefixes,
                             const ogs_unit* units, int32_t n_units,
                             const ogs_unit_mods* mods,
-                            const ogs_route_diff* diff, uint32_t flags,
+                            ogs_route_diff* diff, uint32_t flags,
                             int32_t nh_words, ogs_spf_out* out, void* stream) {
   if (!graph || !prefixes || !out) return fail(OGS_E_INVALID, "graph/prefixes/out is NULL");
   if (n_units < 0) return fail(OGS_E_INVALID, "n_units < 0");

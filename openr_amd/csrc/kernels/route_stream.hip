@@ -73,15 +73,16 @@ struct HbmView {
   }
 };
 
+// `parts` workgroups per unit, each streaming one 4-aligned prefix range.
 template <int W>
 __global__ __launch_bounds__(kBlock) void route_stream_kernel(
     ogs_graph g, ogs_prefix_table pt, const uint32_t* __restrict__ key,
     const ogs_unit* __restrict__ units, uint32_t flags,
     const uint32_t* __restrict__ sDist, const uint32_t* __restrict__ sNh,
-    ogs_spf_out out) {
+    ogs_spf_out out, uint32_t parts) {
   constexpr uint32_t kInf = 0xFFFFFFFFu;
   const int tid = threadIdx.x;
-  const uint32_t u = blockIdx.x;
+  const uint32_t u = blockIdx.x / parts, part = blockIdx.x - u * parts;
   const ogs_unit unit = units[u];
   const uint32_t t = unit.topo, s = unit.src;
   const uint32_t nb = g.node_base[t];
@@ -116,14 +117,21 @@ __global__ __launch_bounds__(kBlock) void route_stream_kernel(
 
   const uint32_t p0 = pt.pfx_base[t];
   const uint32_t P = pt.pfx_base[t + 1] - p0;
-  stream_routes<W>(pt, key + size_t(t) * Sp, p0, P, Sp, u, s, nflags, sv, cfg, out,
-                   [&](uint32_t v, Rec<W>& r) {
-                     r.meta = rMeta[v];
-                     r.metric = rMetric[v];
+  const uint32_t span = ((P + parts - 1u) / parts + 3u) & ~3u;
+  const uint32_t lo = min(P, part * span), hi = min(P, lo + span);
+  auto rec = [&](uint32_t v, Rec<W>& r) {
+    r.meta = rMeta[v];
+    r.metric = rMetric[v];
 #pragma unroll
-                     for (int w = 0; w < W; ++w) r.mask[w] = rMask[w * Sn + v];
-                   },
-                   nullptr, (flags & kFlagNtStores) != 0);
+    for (int w = 0; w < W; ++w) r.mask[w] = rMask[w * Sn + v];
+  };
+  if (out.meta && out.metric && out.mask && !out.sel) {  // unconditional 16-B stores
+    stream_routes<W, false, true>(pt, key + size_t(t) * Sp, p0, P, Sp, u, s, nflags, sv, cfg,
+                                  out, rec, nullptr, (flags & kFlagNtStores) != 0, lo, hi);
+  } else {
+    stream_routes<W>(pt, key + size_t(t) * Sp, p0, P, Sp, u, s, nflags, sv, cfg, out, rec,
+                     nullptr, (flags & kFlagNtStores) != 0, lo, hi);
+  }
 }
 
 // ---- per-(device, stream) workspace (grow-only; freed at process exit) ----
@@ -224,13 +232,18 @@ hipError_t launch_frontier_routes(const ogs_graph& g, const ogs_prefix_table& pt
                                   int nUnits, uint32_t flags, int W,
                                   const ogs_spf_out& out, void* scratch,
                                   hipStream_t stream);
+size_t lds_image_bytes(const ogs_graph& g, int W);
+hipError_t launch_spf_lds(const ogs_graph& g, const ogs_unit* units, int nUnits,
+                          uint32_t flags, int W, uint32_t* dist, uint32_t* nh,
+                          void* scratch, hipStream_t stream);
+void stream_parts(int nUnits, int W, int P, int* parts);
 
 template <int W>
 hipError_t launch_route_stream(const ogs_graph& g, const ogs_prefix_table& pt,
                                const uint32_t* key, const ogs_unit* units,
                                int nUnits, uint32_t flags, const uint32_t* dist,
                                const uint32_t* nh, const ogs_spf_out& out,
-                               hipStream_t stream) {
+                               hipStream_t stream, int parts = 1) {
   const size_t lds = size_t(g.max_nodes) * (2 + W) * 4;
   auto k = route_stream_kernel<W>;
   if (lds > 64 * 1024) {
@@ -240,8 +253,8 @@ hipError_t launch_route_stream(const ogs_graph& g, const ogs_prefix_table& pt,
     if (e != hipSuccess) return e;
   }
   if (g_routeStoreNt & 1) flags |= kFlagNtStores;
-  hipLaunchKernelGGL(k, dim3(nUnits), dim3(kBlock), lds, stream, g, pt, key,
-                     units, flags, dist, nh, out);
+  hipLaunchKernelGGL(k, dim3(unsigned(nUnits) * unsigned(parts)), dim3(kBlock), lds, stream, g,
+                     pt, key, units, flags, dist, nh, out, uint32_t(parts));
   return hipGetLastError();
 }
 
@@ -265,14 +278,14 @@ hipError_t launch_frontier_variants(const ogs_graph& g, const ogs_prefix_table& 
                                     int n, uint32_t flags, int W,
                                     const ogs_spf_out& out,
                                     const ogs_unit_mods* mods,
-                                    const ogs_route_diff* diff, void* scratch,
+                                    ogs_route_diff* diff, void* scratch,
                                     hipStream_t stream);
 
 // ogs_spf_routes_variants: key fold + zeroed diff bitmap + fused frontier
 // SPF / RouteDb / diff launch. *unsupported when outside the frontier path.
 hipError_t launch_variants(const ogs_graph& g, const ogs_prefix_table& pt,
                            const ogs_unit* units, int nUnits,
-                           const ogs_unit_mods* mods, const ogs_route_diff* diff,
+                           const ogs_unit_mods* mods, ogs_route_diff* diff,
                            uint32_t flags, int W, const ogs_spf_out& out,
                            hipStream_t stream, int* unsupported) {
   if (!g.edge_src || (flags & OGS_F_WIDE_METRIC) || !frontier_fits(g, flags, W) ||
@@ -315,12 +328,17 @@ bool try_ms_stream(const ogs_graph& g, const ogs_prefix_table& pt,
   if (size_t(g.max_nodes) * (2 + W) * 4 > 160 * 1024) return false;
   const size_t Sn = size_t(g.max_nodes), Sp = size_t(pt.max_prefixes);
   const bool frontier = frontier_fits(g, flags, W);
-  const bool fused = g_routeStream == 2 && frontier;
+  // route_stream 4: SPF with the topology in LDS (spf_lds.hip), then the
+  // stream over `parts` workgroups per unit
+  const size_t ldsBytes = g_routeStream == 4 && !(flags & OGS_F_WIDE_METRIC) && Sp > 0
+                              ? lds_image_bytes(g, W) : 0;
+  const bool ldsSplit = ldsBytes != 0;
+  const bool fused = (g_routeStream == 2 || (g_routeStream == 4 && !ldsSplit)) && frontier;
   const bool piped = g_routeStream == 3 && frontier && Sp > 0 && nUnits > 1;
   // three-word sets (65..96 links: C3 FSWs) through the frontier forms only
-  if (W == 3 && !fused && !piped) return false;
+  if (W == 3 && !fused && !piped && !ldsSplit) return false;
   const size_t keyBytes = round256(size_t(g.num_topos) * Sp * 4);
-  const size_t chunkBytes = frontier ? chunk_scratch_bytes(g) : 0;
+  const size_t chunkBytes = ldsSplit ? round256(ldsBytes) : frontier ? chunk_scratch_bytes(g) : 0;
   const size_t distBytes = (fused || out.dist) ? 0 : round256(size_t(nUnits) * Sn * 4);
   const size_t nhBytes = (fused || out.nh) ? 0 : round256(size_t(nUnits) * W * Sn * 4);
   void* ws = nullptr;
@@ -345,6 +363,20 @@ bool try_ms_stream(const ogs_graph& g, const ogs_prefix_table& pt,
   spf.dist = out.dist ? out.dist : base + keyBytes + chunkBytes;
   spf.nh = out.nh ? out.nh
                   : reinterpret_cast<uint32_t*>(base + keyBytes + chunkBytes + distBytes);
+  if (ldsSplit) {
+    uint32_t* d = static_cast<uint32_t*>(spf.dist);
+    *err = launch_spf_lds(g, units, nUnits, flags, W, d, spf.nh, chunkScratch, stream);
+    if (*err != hipSuccess) return true;
+    int parts = 1;
+    stream_parts(nUnits, W, int(Sp), &parts);
+    switch (W) {
+      case 1: *err = launch_route_stream<1>(g, pt, key, units, nUnits, flags, d, spf.nh, out, stream, parts); break;
+      case 2: *err = launch_route_stream<2>(g, pt, key, units, nUnits, flags, d, spf.nh, out, stream, parts); break;
+      case 3: *err = launch_route_stream<3>(g, pt, key, units, nUnits, flags, d, spf.nh, out, stream, parts); break;
+      default: *err = launch_route_stream<4>(g, pt, key, units, nUnits, flags, d, spf.nh, out, stream, parts); break;
+    }
+    return true;
+  }
   if (piped) {
     // Pipelined split: the SPF of unit chunk c runs on a side stream while
     // the route stream of chunk c - 1 runs on the caller's -- a fused launch

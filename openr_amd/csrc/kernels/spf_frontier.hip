@@ -1098,6 +1098,23 @@ int num_cus() {
 }
 }  // namespace
 
+// Workgroups per unit of the split stream (route_stream 4, after the LDS
+// SPF). A launch of fewer than two units per CU (one rank's shard) splits
+// each unit's records into parts of about 1 MiB, so the parts of every
+// width group stream comparable bytes and outlast no one; larger launches
+// keep one workgroup per unit ("frontier_parts" / "frontier_parts_wide"
+// override, as for the fused launches).
+void stream_parts(int nUnits, int W, int P, int* parts) {
+  int k = W > 1 ? g_frontierPartsWide : g_frontierParts;
+  if (!k) {
+    const double unitBytes = double(P) * (8 + 4 * W);
+    k = nUnits >= 2 * num_cus()
+            ? 1
+            : std::max(1, std::min(16, int(unitBytes / double(1u << 20) + 0.5)));
+  }
+  *parts = k;
+}
+
 void stream_geometry(int nUnits, int W, int* block, int* parts) {
   // the launch's streamed bytes per CU, in one-word units (12 B per prefix)
   const double load = double(nUnits) * (8 + 4 * W) / 12.0 / num_cus();
@@ -1551,7 +1568,7 @@ __global__ __launch_bounds__(kBlock) void spf_variant_repair_kernel(
 bool launch_variants_repair(const ogs_graph& g, const ogs_prefix_table& pt,
                             const uint32_t* key, const ogs_unit* units, int n,
                             uint32_t flags, int W, const ogs_spf_out& out,
-                            const ogs_unit_mods* mods, const ogs_route_diff* diff,
+                            const ogs_unit_mods* mods, ogs_route_diff* diff,
                             void* scratch, hipStream_t stream, hipError_t* err) {
   if (!(flags & OGS_F_INCREMENTAL) || !mods || !diff || !diff->base_dist || !diff->base_nh ||
       W != 1 || mods->dead_per_unit > kMaxDead || g.max_nodes > 65535) {
@@ -1582,6 +1599,7 @@ bool launch_variants_repair(const ogs_graph& g, const ogs_prefix_table& pt,
                        diff->base_dist, desc, words);
     *err = hipGetLastError();
     if (*err != hipSuccess) return true;
+    if (cached) diff->base_desc_valid = 1;  // the caller's cache now holds them
   }
   hipLaunchKernelGGL(k, dim3(n), dim3(kBlock), lds, stream, g, pt, key, units,
                      flags | ((g_routeStoreNt & 1) ? kFlagNtStores : 0u),
@@ -1612,7 +1630,7 @@ hipError_t launch_frontier_variants(const ogs_graph& g, const ogs_prefix_table& 
                                     int n, uint32_t flags, int W,
                                     const ogs_spf_out& out,
                                     const ogs_unit_mods* mods,
-                                    const ogs_route_diff* diff, void* scratch,
+                                    ogs_route_diff* diff, void* scratch,
                                     hipStream_t stream) {
   hipError_t e = hipSuccess;
   if (launch_variants_repair(g, pt, key, units, n, flags, W, out, mods, diff, scratch, stream,

@@ -66,14 +66,19 @@ def _c3(product, names, ppn=100):
     return launches
 
 
-@pytest.mark.parametrize("geometry", [(0, 0), (1024, 1), (512, 3)])
-def test_c3_full_every_source_matches_oracle(product, geometry):
+@pytest.mark.parametrize("opts", [{}, dict(frontier_block=1024, frontier_parts=1),
+                                  dict(frontier_block=512, frontier_parts=3,
+                                       frontier_parts_wide=5),
+                                  dict(route_stream=4), dict(route_stream=4, frontier_parts=3,
+                                                             frontier_parts_wide=5)])
+def test_c3_full_every_source_matches_oracle(product, opts):
     """C3-full at bench size (2,080 sources x 208k prefixes) through
     bench.py's two-stream width-group launches: every source's digest equals
     the oracle's (golden per-source digests), and the job digest equals the
-    golden job digest bench.py asserts; with the default stream geometry and
-    forced ones (frontier_block threads per workgroup, frontier_parts
-    workgroups per one-word unit, each streaming one prefix range)."""
+    golden job digest bench.py asserts; with the default launch form and
+    forced ones (fused: frontier_block threads per workgroup, frontier_parts
+    workgroups per unit each streaming one prefix range; route_stream 4: the
+    LDS-resident SPF then the split stream)."""
     if not os.path.exists(C3_SOURCES):
         pytest.skip("oracle C3 per-source digests not generated")
     want = json.load(open(C3_SOURCES))
@@ -83,14 +88,14 @@ def test_c3_full_every_source_matches_oracle(product, geometry):
     assert set(want) == set(names)
     import openr_amd.capi as capi
     lib = capi.load()
-    block, parts = geometry
-    capi.check(lib, lib.ogs_set_option(b"frontier_block", block), "frontier_block")
-    capi.check(lib, lib.ogs_set_option(b"frontier_parts", parts), "frontier_parts")
+    defaults = dict(frontier_block=0, frontier_parts=0, frontier_parts_wide=0, route_stream=2)
+    for k, v in opts.items():
+        capi.check(lib, lib.ogs_set_option(k.encode(), v), k)
     try:
         launches = _c3(product, names)
     finally:
-        lib.ogs_set_option(b"frontier_block", 0)
-        lib.ogs_set_option(b"frontier_parts", 0)
+        for k, v in defaults.items():
+            lib.ogs_set_option(k.encode(), v)
     job = 0
     bad = []
     for L in launches:

@@ -253,3 +253,33 @@ def test_repair_large_wan(product, oracle, mode, desc):
     finally:
         lib.ogs_set_option(b"c4_desc", 1)
     assert any(changed for _, changed, _, _ in variants)
+
+
+@pytest.mark.parametrize("first,second", [(0, 1), (1, 0), (1, 1)])
+def test_repair_desc_cache_across_launches(product, oracle, first, second):
+    """Two launches on ONE sweep with the descendant-row option toggled in
+    between: the library reports whether it wrote the rows into
+    the sweep's cache (ogs_route_diff.base_desc_valid in / out, ABI 4), so a
+    launch after a c4_desc=0 launch builds them instead of reading rows
+    that were never written. Both launches' route updates vs the oracle."""
+    import openr_amd.capi as capi
+    lib = capi.load()
+    opts = dict(nodes=400, seed=0xC7, prefixesPerNode=2)
+    n = 32
+    _, variants, links = oracle.variant_route_updates("wan", opts, "3", n, 0xC4F, 500,
+                                                      True, False)
+    vr = product.VariantRunner(True, False)
+    vr.setup("wan", opts, "3", n, 0xC4F, 500)
+    vr.set_mode(2)
+    try:
+        for desc in (first, second):
+            capi.check(lib, lib.ogs_set_option(b"c4_desc", desc), "c4_desc")
+            vr.launch(0, True)
+            vr.fetch_updates(0)
+            for v, (canon, changed, nu, nd) in enumerate(variants):
+                upd, dele = vr.update(v)
+                assert sorted(upd + dele) == changed, (desc, v, links[v])
+                assert vr.updated_canonical(v) == canon, (desc, v, links[v])
+    finally:
+        lib.ogs_set_option(b"c4_desc", 1)
+    assert any(changed for _, changed, _, _ in variants)
