@@ -15,6 +15,7 @@
 // missing device or an input outside the GPU engine's domain throws.
 #pragma once
 
+#include <algorithm>
 #include <chrono>
 #include <cstdint>
 #include <limits>
@@ -380,10 +381,49 @@ class LinkState {
 };
 
 // ----------------------------------------------------------- PrefixState --
+// PrefixState.h:55: a hashed map keyed by the prefix network (the reference's
+// unordered_map<CIDRNetwork, PrefixEntries>): ingestion is one hash insert
+// per key. Nothing downstream depends on its iteration order -- the device
+// prefix table lists prefixes in that order and maps results back by index,
+// RouteDbs are keyed by prefix, route digests are XOR-combined.
+// A prefix's advertisements keyed by (node, area), in key order: a sorted
+// vector (one allocation for the one or few advertisers a prefix has, where
+// a node-based map allocates per entry). Iterates as pairs, like a map.
+class PrefixEntryList {
+ public:
+  using value_type = std::pair<NodeAndArea, std::shared_ptr<PrefixEntry>>;
+  using const_iterator = std::vector<value_type>::const_iterator;
+  using iterator = std::vector<value_type>::iterator;
+  const_iterator begin() const { return v_.begin(); }
+  const_iterator end() const { return v_.end(); }
+  iterator begin() { return v_.begin(); }
+  iterator end() { return v_.end(); }
+  size_t size() const { return v_.size(); }
+  bool empty() const { return v_.empty(); }
+  // the entry of `k` (inserted empty when absent) and whether it was new
+  std::pair<iterator, bool> try_emplace(const NodeAndArea& k) {
+    auto it = std::lower_bound(v_.begin(), v_.end(), k,
+                               [](const value_type& a, const NodeAndArea& b) { return a.first < b; });
+    if (it != v_.end() && it->first == k) return {it, false};
+    return {v_.insert(it, value_type(k, nullptr)), true};
+  }
+  size_t erase(const NodeAndArea& k) {
+    auto it = std::lower_bound(v_.begin(), v_.end(), k,
+                               [](const value_type& a, const NodeAndArea& b) { return a.first < b; });
+    if (it == v_.end() || it->first != k) return 0;
+    v_.erase(it);
+    return 1;
+  }
+
+ private:
+  std::vector<value_type> v_;
+};
+
 class PrefixState {
  public:
-  using Entries = std::map<NodeAndArea, std::shared_ptr<PrefixEntry>>;
-  const std::map<std::string, Entries>& prefixes() const { return prefixes_; }
+  using Entries = PrefixEntryList;
+  using Map = std::unordered_map<std::string, Entries>;
+  const Map& prefixes() const { return prefixes_; }
   std::set<std::string> updatePrefix(const std::string& node,
                                      const std::string& area,
                                      const PrefixEntry& entry);
@@ -407,17 +447,22 @@ class PrefixState {
   // Entry i of changeLog() has the absolute position changeLogBase() + i;
   // the oldest half is dropped past kChangeLogCap entries (a reader behind
   // changeLogBase() has lost its place and must not rely on it).
+  // The log is kept once a reader asked for it (trackChanges: the
+  // SpfSolver's first build / incremental call), so bulk ingestion before
+  // the first build records nothing.
   const std::vector<std::string>& changeLog() const { return changeLog_; }
   uint64_t changeLogBase() const { return changeLogBase_; }
   uint64_t changeLogEnd() const { return changeLogBase_ + changeLog_.size(); }
+  void trackChanges() const { tracking_ = true; }
   static constexpr size_t kChangeLogCap = size_t(1) << 20;
 
  private:
   void logChange(const std::string& network);
-  std::map<std::string, Entries> prefixes_;
+  Map prefixes_;
   uint64_t version_{0};
   std::vector<std::string> changeLog_;
   uint64_t changeLogBase_{0};
+  mutable bool tracking_{false};
 };
 
 // ------------------------------------------------------------ RIB types --

@@ -74,6 +74,7 @@ uint64_t nextVersionStamp() {
 
 // ----------------------------------------------------------- PrefixState --
 void PrefixState::logChange(const std::string& network) {
+  if (!tracking_) return;
   if (changeLog_.size() >= kChangeLogCap) {
     const size_t drop = changeLog_.size() / 2;
     changeLog_.erase(changeLog_.begin(), changeLog_.begin() + drop);
@@ -807,6 +808,7 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDb(
                            : buildRouteDbSingleArea(me, als, ps);
   // every change so far is in this build: the next incremental loop's
   // batch starts after it
+  ps.trackChanges();
   incPs_ = &ps;
   incLogCursor_ = ps.changeLogEnd();
   if (!quietStats_) {
@@ -1421,6 +1423,7 @@ std::optional<RibUnicastEntry> SpfSolver::createRouteForPrefixOrGetStaticRoute(
     // this call and every prefix changed since the last build / batch
     // (Decision's pending updatedPrefixes, the loop this call is part of)
     std::set<std::string> batch{prefix};
+    ps.trackChanges();
     if (incPs_ != &ps || incLogCursor_ < ps.changeLogBase()) {
       incPs_ = &ps;
       incLogCursor_ = ps.changeLogBase();  // unknown position: the whole log

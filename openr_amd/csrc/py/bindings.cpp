@@ -904,15 +904,17 @@ class C5Runner {
              bool brs, int rank, int world) {
     loadMultiArea(opts, als_, ps_);
     if (world > 1) {
-      const size_t P = ps_.prefixes().size();
+      // the rank's block of the prefixes in sorted order
+      std::vector<std::string> all;
+      for (const auto& [pfx, _] : ps_.prefixes()) all.push_back(pfx);
+      std::sort(all.begin(), all.end());
+      const size_t P = all.size();
       const size_t lo = P * rank / world, hi = P * (rank + 1) / world;
       PrefixState sub;
-      size_t i = 0;
-      for (const auto& [pfx, entries] : ps_.prefixes()) {
-        if (i >= lo && i < hi) {
-          for (const auto& [na, e] : entries) sub.updatePrefixKeyed(na.first, na.second, pfx, *e);
+      for (size_t i = lo; i < hi; ++i) {
+        for (const auto& [na, e] : ps_.prefixes().at(all[i])) {
+          sub.updatePrefixKeyed(na.first, na.second, all[i], *e);
         }
-        ++i;
       }
       ps_ = std::move(sub);
     }
@@ -1535,11 +1537,13 @@ PYBIND11_MODULE(_decision, m) {
           auto& ls = als.emplace(g.area, LinkState(g.area, "test_node")).first->second;
           PrefixState ps;
           loadLsdb(g, ls, ps);
-          std::set<std::string> changed;
-          const size_t stride = std::max<size_t>(1, ps.prefixes().size() / std::max(n, 1));
-          size_t i = 0;
-          for (const auto& [p, _] : ps.prefixes()) {
-            if (i++ % stride == 0 && int(changed.size()) < n) changed.insert(p);
+          std::set<std::string> changed;  // every stride-th in sorted order (refcpu's too)
+          std::vector<std::string> all;
+          for (const auto& [p, _] : ps.prefixes()) all.push_back(p);
+          std::sort(all.begin(), all.end());
+          const size_t stride = std::max<size_t>(1, all.size() / std::max(n, 1));
+          for (size_t i = 0; i < all.size(); ++i) {
+            if (i % stride == 0 && int(changed.size()) < n) changed.insert(all[i]);
           }
           SpfSolver a("test_node", true, false, false, false), b("test_node", true, false, false, false);
           // Decision's flow (Decision.cpp:912-951): a full build, then
