@@ -20,6 +20,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--as-rank", default=None)
     ap.add_argument("--opt", action="append", default=[])
+    ap.add_argument("--lds", action="store_true",
+                    help="stamps of the LDS-resident SPF kernel (route_stream 4)")
     a = ap.parse_args()
     import torch
     import bench
@@ -43,6 +45,21 @@ def main():
     for _ in range(3):
         bench.c3_launch_all(lib, capi, launches, main_s, side)
     torch.cuda.synchronize()
+    if a.lds:
+        raw = np.zeros(4 * 4096 * 16, dtype=np.uint32)
+        lib.ogs_diag_lds_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int32]
+        assert lib.ogs_diag_lds_stamps(raw.ctypes.data, raw.size) == 0
+        raw = raw.reshape(4, 4096, 16)
+        for L in launches:
+            st = raw[L["W"] - 1]
+            st = st[st[:, 12] != 0]
+            print(f"W={L['W']} workgroups={len(st)}: stage med={np.median(st[:, 0]):.0f} "
+                  f"first-unit(incl stage) med={np.median(st[:, 1]):.0f} "
+                  f"rounds med={np.median(st[:, 2]):.0f} units med={np.median(st[:, 11]):.0f} "
+                  f"kernel med={np.median(st[:, 12]):.0f} max={st[:, 12].max():.0f}")
+            print("   round cycles (med): " +
+                  " ".join(f"{np.median(st[:, k]):.0f}" for k in range(3, 11)))
+        return
     raw = np.zeros(65536 * 8, dtype=np.uint32)
     lib.ogs_diag_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int32]
     assert lib.ogs_diag_stamps(raw.ctypes.data, raw.size) == 0
