@@ -210,7 +210,7 @@ def run_c1(args, rank):
         return None
     import openr_amd
     reps = 21
-    cold, warm, routes, d_cold, d_warm = openr_amd.decision.build_latency_bench(
+    cold, warm, routes, d_cold, d_warm, _, _ = openr_amd.decision.build_latency_bench(
         "grid", C1_OPTS, C1_SOURCE, reps)
     out = {"unit": "us/build", "gpu_cold_us": round(median(cold), 1),
            "gpu_warm_us": round(median(warm), 1), "routes": routes, "reps": reps,
@@ -246,6 +246,7 @@ def run_g1(args, rank):
     M = openr_amd.decision
     br = M.BatchRunner(True, False, False)
     br.add_generated("wan", G1_OPTS, G1_SOURCES)
+    br.set_sel_output(False)  # no selection cache read here: 12 B per route (§8(d))
     br.upload()
     br.run()  # warm-up (code objects, workspace)
     reps = 5
@@ -285,16 +286,17 @@ def run_g1(args, rank):
     sreps = 5
     if args.no_extras:  # PMC passes: only the batch launches reach the counters
         return finish_g1(out, digest, args)
-    M.reset_decision_counters()
-    cold, warm, routes, d_cold, d_warm = M.build_latency_bench("wan", G1_OPTS, src, sreps)
-    ctr = M.decision_counters()
+    cold, warm, routes, d_cold, d_warm, s_cold, s_warm = M.build_latency_bench(
+        "wan", G1_OPTS, src, sreps)
+    names = ("prepare", "launch", "materialize")
     single = {"source": src, "unit": "ms/build", "gpu_cold_ms": round(median(cold) / 1e3, 3),
               "gpu_warm_ms": round(median(warm) / 1e3, 3), "routes": routes, "reps": sreps,
               "route_digest": f"{d_cold:016x}",
-              # the drop-in's own timers over these builds (cold and warm):
-              # flatten / uploads, kernels + D2H, host RouteDb materialisation
-              "split_ms_avg": {k: round(ctr.get(f"decision.gpu.{k}_ms.avg", 0.0), 3)
-                               for k in ("prepare", "launch", "materialize")}}
+              # the drop-in's own timers (decision.gpu.*_ms), averaged over the
+              # cold builds and over the warm ones: flatten / uploads, kernels +
+              # D2H (warm: the route pass over the SPF memo), host materialisation
+              "split_ms_cold": {k: round(v, 3) for k, v in zip(names, s_cold)},
+              "split_ms_warm": {k: round(v, 3) for k, v in zip(names, s_warm)}}
     golden_check(single, "g1_single", d_cold, GOLDEN.get("g1_single"))
     golden_check(single, "g1_single_warm", d_warm, GOLDEN.get("g1_single"))
     if not args.no_cpu_baseline:

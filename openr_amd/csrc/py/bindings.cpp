@@ -2,6 +2,7 @@
 // Exposes the same surface as the CPU oracle binding so tests can drive one
 // scenario through both. Every computation goes through libopenr_gpu.so.
 #include <algorithm>
+#include <array>
 #include <chrono>
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
@@ -560,7 +561,8 @@ class BatchRunner {
     ogs_graph g = graph();
     ogs_prefix_table pt = table();
     ogs_spf_out out{dDist_.get(), dNh_.as<uint32_t>(), dMeta_.as<uint32_t>(),
-                    dMetric_.get(), dMask_.as<uint32_t>(), dSel_.as<uint32_t>(),
+                    dMetric_.get(), dMask_.as<uint32_t>(),
+                    selOut_ ? dSel_.as<uint32_t>() : nullptr,
                     exact_ ? dReach_.as<uint32_t>() : nullptr};
     ogsCheck(ogs_spf_routes(&g, hb_.maxPrefixes ? &pt : nullptr,
                             dUnits_.as<ogs_unit>(), int32_t(units_.size()),
@@ -568,6 +570,9 @@ class BatchRunner {
              "ogs_spf_routes");
     ogsCheck(ogs_stream_sync(nullptr), "ogs_stream_sync");
   }
+  // the sel row (selected advertisers: only the best-route selection cache
+  // reads it) is written unless turned off (the G1 bench's digest needs none)
+  void setSelOutput(bool on) { selOut_ = on; }
 
   void download() {
     const size_t U = units_.size(), Sn = hb_.maxNodes,
@@ -590,8 +595,8 @@ class BatchRunner {
     widen(dMetric_, U * Sp, metric_);
     mask_.resize(U * W_ * Sp);
     dMask_.download(mask_.data(), mask_.size());
-    sel_.resize(U * Sp);
-    dSel_.download(sel_.data(), sel_.size());
+    sel_.assign(U * Sp, 0u);
+    if (selOut_) dSel_.download(sel_.data(), sel_.size());
     reach_.assign(exact_ ? U * ((Sn + 31) / 32) : 0, 0u);
     if (exact_) dReach_.download(reach_.data(), reach_.size());
     ogsCheck(ogs_stream_sync(nullptr), "ogs_stream_sync");
@@ -676,6 +681,7 @@ class BatchRunner {
   }
   size_t numUnits() const { return units_.size(); }
   void setSlotOrder(bool on) { slotOrder_ = on; }
+  bool selOut_{true};
   void setSlotEdgeImage(bool on) { slotEdgeImage_ = on; }
   const HostBatch& host() const { return hb_; }
   const std::vector<ogs_unit>& units() const { return units_; }
@@ -1774,31 +1780,49 @@ PYBIND11_MODULE(_decision, m) {
           std::vector<double> cold, warm;
           size_t routes = 0;
           uint64_t dCold = 0, dWarm = 0;  // route_digest.h unit(me, db)
+          // the drop-in's split timers (decision.gpu.*_ms) summed over the
+          // timed cold builds and over the warm ones, separately
+          const char* kSplit[3] = {"decision.gpu.prepare_ms.sum", "decision.gpu.launch_ms.sum",
+                                   "decision.gpu.materialize_ms.sum"};
+          auto sums = [&](std::array<double, 3>& acc, double sign) {
+            const auto c = getDecisionCounters();
+            for (int i = 0; i < 3; ++i) {
+              auto it = c.find(kSplit[i]);
+              acc[i] += sign * (it == c.end() ? 0.0 : it->second);
+            }
+          };
+          std::array<double, 3> splitCold{}, splitWarm{};
           for (int r = 0; r < reps + 1; ++r) {
             AreaLinkStates als;
             auto& ls = als.emplace(g.area, LinkState(g.area, "test_node")).first->second;
             PrefixState ps;
             loadLsdb(g, ls, ps);
             SpfSolver solver("test_node", true, false, false);
+            if (r) sums(splitCold, -1.0);
             auto t0 = std::chrono::steady_clock::now();
             auto db = solver.buildRouteDb(me, als, ps);
             const double us = std::chrono::duration<double, std::micro>(
                                   std::chrono::steady_clock::now() - t0).count();
+            if (r) sums(splitCold, 1.0);
             if (!db) throw std::runtime_error("no RouteDb for " + me);
             routes = db->unicastRoutes.size();
             if (r) cold.push_back(us);  // rep 0 warms code objects / workspace
             if (r == reps) {
               dCold = digest::unit(me, *db);
+              sums(splitWarm, -1.0);
               for (int k = 0; k < reps; ++k) {
                 t0 = std::chrono::steady_clock::now();
                 db = solver.buildRouteDb(me, als, ps);
                 warm.push_back(std::chrono::duration<double, std::micro>(
                                    std::chrono::steady_clock::now() - t0).count());
               }
+              sums(splitWarm, 1.0);
               dWarm = digest::unit(me, *db);
             }
           }
-          return std::make_tuple(cold, warm, routes, dCold, dWarm);
+          for (auto& x : splitCold) x /= std::max(reps, 1);
+          for (auto& x : splitWarm) x /= std::max(reps, 1);
+          return std::make_tuple(cold, warm, routes, dCold, dWarm, splitCold, splitWarm);
         },
         py::arg("kind"), py::arg("opts"), py::arg("me"), py::arg("reps"));
   // Host-only f1 materialisation harness (no device): synthetic changed
@@ -2063,6 +2087,7 @@ PYBIND11_MODULE(_decision, m) {
              }
            })
       .def("upload", &BatchRunner::upload)
+      .def("set_sel_output", &BatchRunner::setSelOutput)
       .def("run", [](BatchRunner& b) {
         py::gil_scoped_release nogil;
         b.run();

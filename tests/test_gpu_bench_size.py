@@ -249,3 +249,20 @@ def test_c5_digests_rank_invariant(product):
         p.fetch()
         pds ^= shard.lines_digest(p.ksp_text())
     assert (rds, pds) == (rd, pd)
+
+
+@pytest.mark.parametrize("sr", [False, True])
+def test_c1_exact_workload_canonical_text(product, oracle, sr):
+    """Config C1 exactly as bench.py runs it (createGrid(10) wiring, metric
+    1, prefix seed 0xC1, source "1", v4 on, best-route selection off)
+    through the drop-in SpfSolver::buildRouteDb: the full canonical RouteDb
+    text equals the oracle's -- also for the second build of the same
+    source, which routes over the SPF memo (LinkState.cpp:705-715) -- with
+    and without node segment labels."""
+    from openr_amd.workloads import C1_OPTS, C1_SOURCE
+    got = product.gen_route_dbs("grid", C1_OPTS, [C1_SOURCE, C1_SOURCE, "57", C1_SOURCE],
+                                True, sr, False)
+    want = oracle.gen_route_dbs("grid", C1_OPTS, [C1_SOURCE, C1_SOURCE, "57", C1_SOURCE],
+                                True, sr, False)
+    assert got == want
+    assert got[0] == got[1] == got[3] and got[0] != b"NONE"

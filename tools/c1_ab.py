@@ -24,7 +24,7 @@ def main():
     for rnd in range(4):
         for v in vals:
             capi.check(lib, lib.ogs_set_option(opt, v), opt.decode())
-            cold, warm, _ = openr_amd.decision.build_latency_bench("grid", C1_OPTS, "1", 21)
+            cold, warm = openr_amd.decision.build_latency_bench("grid", C1_OPTS, "1", 21)[:2]
             if rnd:
                 res[v][0].extend(cold)
                 res[v][1].extend(warm)
