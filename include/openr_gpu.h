@@ -289,10 +289,9 @@ int ogs_host_free(void* hptr);
  *   "route_stream": RouteDb form for large shared topologies: 2 (default)
  *                 one launch per unit set, SPF then the unit's RouteDb write
  *                 stream from LDS; 1 an SPF launch then a route-stream launch
- *                 (dist/next-hop sets through HBM); 0 the fused multi-source
- *                 kernel; 3 the split pipelined over unit chunks (SPF of a
- *                 chunk on an internal side stream, its route stream on the
- *                 caller's; "route_stream_chunks" 1..64, default 4). Scratch
+ *                 (dist/next-hop sets through HBM); 4 the SPF with the
+ *                 topology staged in LDS, then the route stream over
+ *                 "frontier_parts" workgroups per unit (A/B). Scratch
  *                 (prefix keys, dist/next-hop sets when out->dist / out->nh
  *                 are NULL) comes from a grow-only per-device workspace.
  *                 "route_store_nt", bits: 1 the RouteDb stream's 16-B stores
@@ -311,8 +310,6 @@ int ogs_host_free(void* hptr);
  *                 "spf_lds_form": route_stream 4's LDS-resident SPF runs
  *                 three-pass rounds without compare-and-swap (0, default)
  *                 or the packed CAS / two-phase rounds (1, A/B).
- *                 "frontier_wg_lds": minimum LDS bytes per fused
- *                 frontier + route-stream workgroup (occupancy probe, 0).
  *   "frontier_block": threads per workgroup of the all-sources RouteDb
  *                 launches (fused frontier SPF + route stream, meta / metric
  *                 / mask outputs): 256, 512 or 1024; 0 (default) by the
@@ -323,20 +320,14 @@ int ogs_host_free(void* hptr);
  *                 (1..16; 0 default: by bytes per CU). "frontier_parts_wide":
  *                 the same for units of wider next-hop sets.
  *   "wave_opt":   wave-kernel paths, bits: 1 register-resident SPF words
- *                 (ds_bpermute), 2 (default) identity-segment route path,
- *                 4 two units per wavefront with 16-bit words.
- *   "ksp_stop":   1 the KSP2 k = 2 SPF of a destination stops once every
- *                 distance lowered in a round exceeds the destination's; 0
- *                 (default) runs to the fixpoint. Both exact.
+ *                 (ds_bpermute), 2 (default) identity-segment route path.
  *   "spf_frontier": 1 (default) large topologies (edge_src given) solve
  *                 SPF with the frontier kernel (one workgroup per unit,
  *                 only changed rows pushed); 0 the multi-source edge sweep.
  *   "spf_queue":  frontier kernel round schedule: -1 (default) LDS node
  *                 lists for sparse topologies (max degree <= 16; one phase
  *                 over packed {dist, next hops} words when the next-hop sets
- *                 fit one word), the chunk scan otherwise; 0 always the scan;
- *                 1 lists whenever they fit in LDS; 2 lists, two phases; 3
- *                 packed with the push stamps folded into the words (A/B).
+ *                 fit one word), the chunk scan otherwise; 0 always the scan.
  *                 "spf_ninfo": 1 (default) the list forms keep row begin |
  *                 drained per node in LDS, 0 read them from the CSR, -1 the
  *                 CSR form whenever that raises the units per CU.

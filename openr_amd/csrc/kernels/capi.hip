@@ -10,14 +10,11 @@
 namespace ogs {
 extern int g_unitWidth;
 extern int g_waveWgLds;
-extern int g_frontierWgLds;
 extern int g_waveUpb;
 extern int g_waveOpt;
 extern int g_kspWaveTrace;
-extern int g_kspStop;
 extern int g_msGroup;
 extern int g_routeStream;
-extern int g_routeStreamChunks;
 extern int g_routeStoreNt;
 extern int g_spfSeedRow;
 extern int g_frontierBlock;
@@ -189,7 +186,9 @@ int ogs_set_option(const char* name, int64_t value) {
     return OGS_OK;
   }
   if (std::strcmp(name, "route_stream") == 0) {
-    if (value < 0 || value > 4) return fail(OGS_E_INVALID, "route_stream must be in [0, 4]");
+    if (value != 1 && value != 2 && value != 4) {
+      return fail(OGS_E_INVALID, "route_stream must be 1, 2 or 4");
+    }
     ogs::g_routeStream = int(value);
     return OGS_OK;
   }
@@ -242,11 +241,6 @@ int ogs_set_option(const char* name, int64_t value) {
     ogs::g_spfSeedRow = int(value);
     return OGS_OK;
   }
-  if (std::strcmp(name, "route_stream_chunks") == 0) {
-    if (value < 1 || value > 64) return fail(OGS_E_INVALID, "route_stream_chunks must be in [1, 64]");
-    ogs::g_routeStreamChunks = int(value);
-    return OGS_OK;
-  }
   if (std::strcmp(name, "spf_frontier") == 0) {
     if (value != 0 && value != 1) {
       return fail(OGS_E_INVALID, "spf_frontier must be 0 or 1");
@@ -295,9 +289,7 @@ int ogs_set_option(const char* name, int64_t value) {
     return OGS_OK;
   }
   if (std::strcmp(name, "spf_queue") == 0) {
-    if (value < -1 || value > 3) {
-      return fail(OGS_E_INVALID, "spf_queue must be -1, 0, 1, 2 or 3");
-    }
+    if (value != -1 && value != 0) return fail(OGS_E_INVALID, "spf_queue must be -1 or 0");
     ogs::g_spfQueue = int(value);
     return OGS_OK;
   }
@@ -308,18 +300,13 @@ int ogs_set_option(const char* name, int64_t value) {
     ogs::g_waveUpb = int(value);
     return OGS_OK;
   }
-  if (std::strcmp(name, "ksp_stop") == 0) {
-    if (value != 0 && value != 1) return fail(OGS_E_INVALID, "ksp_stop must be 0 or 1");
-    ogs::g_kspStop = int(value);
-    return OGS_OK;
-  }
   if (std::strcmp(name, "ksp_wave_trace") == 0) {
     if (value != 0 && value != 1) return fail(OGS_E_INVALID, "ksp_wave_trace must be 0 or 1");
     ogs::g_kspWaveTrace = int(value);
     return OGS_OK;
   }
   if (std::strcmp(name, "wave_opt") == 0) {
-    if (value < 0 || value > 7) return fail(OGS_E_INVALID, "wave_opt must be in [0, 7]");
+    if (value < 0 || value > 3) return fail(OGS_E_INVALID, "wave_opt must be in [0, 3]");
     ogs::g_waveOpt = int(value);
     return OGS_OK;
   }
@@ -328,13 +315,6 @@ int ogs_set_option(const char* name, int64_t value) {
       return fail(OGS_E_INVALID, "wave_wg_lds must be in [0, 163840]");
     }
     ogs::g_waveWgLds = int(value);
-    return OGS_OK;
-  }
-  if (std::strcmp(name, "frontier_wg_lds") == 0) {
-    if (value < 0 || value > 160 * 1024) {
-      return fail(OGS_E_INVALID, "frontier_wg_lds must be in [0, 163840]");
-    }
-    ogs::g_frontierWgLds = int(value);
     return OGS_OK;
   }
   return fail(OGS_E_INVALID, std::string("unknown option ") + name);

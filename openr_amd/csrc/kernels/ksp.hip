@@ -282,13 +282,10 @@ __device__ uint32_t trace_paths_wave(const UnitCsr& csr, const uint32_t* dist, u
 // "ksp_wave_trace" option: 1 (default) the traces of 32-bit-distance units
 // run on a whole wavefront (trace_paths_wave), 0 on lane 0 (A/B)
 int g_kspWaveTrace = 1;
-// "ksp_stop" option: 1 the k = 2 SPF of a destination ends once every
-// distance lowered in a round exceeds the destination's (queue_dist), 0
-// (default) runs it to the fixpoint. Exact either way; on C5 the stop saves
-// nothing (0.49 vs 0.49 ms of KSP2 kernels per job, one LDS atomic per wave
-// and round; profiles/r03_c5_ksp_stop_ab.log): the launch lasts as long as
-// its farthest destinations.
-int g_kspStop = 0;
+// (An early stop of the k = 2 SPF once every distance lowered in a round
+// exceeds the destination's saved nothing on C5 -- 0.49 vs 0.49 ms of KSP2
+// kernels per job, profiles/r03_c5_ksp_stop_ab.log: the launch lasts as
+// long as its farthest destinations -- and was removed in round 4.)
 
 template <typename D, int UT, bool STAGE, bool MASKED>
 __global__ __launch_bounds__(kBlock) void ksp_kernel(
@@ -963,22 +960,13 @@ hipError_t launch_ksp(const ogs_graph& g, const ogs_path_unit* units,
 // queue_spf, workgroup units only): round r walks the nodes changed in round
 // r - 1 and pushes dist + w over their usable, unmasked links; one barrier
 // per round. Same least fixpoint as spf_fixpoint (spf_core.h).
-//
-// stopAt != OGS_NODE_NONE (the k = 2 SPF of one destination): the rounds
-// end once every distance lowered in a round exceeds dist(stopAt) -- later
-// rounds can only produce candidates above it, so every node at distance
-// <= dist(stopAt) is final, and the trace back from stopAt reads only those
-// (a neighbour whose value is not final is above dist(stopAt), never tight).
 template <typename D, bool MASKED>
 __device__ void queue_dist(uint32_t N, uint32_t s, const UnitCsr& c,
                            const uint8_t* __restrict__ nflags, D* dist,
                            uint32_t* stamp, uint16_t* q0, uint16_t* q1,
-                           uint32_t* qcnt, const uint32_t* ignore,
-                           uint32_t stopAt = OGS_NODE_NONE) {
+                           uint32_t* qcnt, const uint32_t* ignore) {
   constexpr D kInf = DistInf<D>::value;
   const int tid = threadIdx.x;
-  __shared__ D lowered[3];  // smallest distance lowered per round (rotating)
-  const bool stop = stopAt < N;
   for (uint32_t v = tid; v < N; v += kBlock) {
     dist[v] = (v == s) ? D(0) : kInf;
     stamp[v] = 0u;
@@ -988,18 +976,13 @@ __device__ void queue_dist(uint32_t N, uint32_t s, const UnitCsr& c,
     qcnt[0] = 0u;
     qcnt[1] = 1u;
     qcnt[2] = 0u;
-    lowered[0] = lowered[1] = lowered[2] = kInf;
   }
   __syncthreads();
   uint32_t n = 1;
   for (uint32_t r = 1; n; ++r) {
-    if (tid == 0) {
-      qcnt[(r + 2) % 3] = 0u;
-      lowered[(r + 2) % 3] = kInf;
-    }
+    if (tid == 0) qcnt[(r + 2) % 3] = 0u;
     const uint16_t* cur = (r & 1) ? q1 : q0;
     uint16_t* nxt = (r & 1) ? q0 : q1;
-    D low = kInf;  // this thread's smallest lowered distance of the round
     for (uint32_t i = tid; i < n; i += kBlock) {
       const uint32_t v = cur[i];
       if (v != s && (nflags[v] & OGS_NODE_OVERLOADED)) continue;
@@ -1023,7 +1006,6 @@ __device__ void queue_dist(uint32_t N, uint32_t s, const UnitCsr& c,
           const uint32_t t = edge_dst(lo);
           const D cand = dv + static_cast<D>(ed >> 32);
           if (cand < dist[t] && cand < atomicMin(&dist[t], cand)) {
-            low = cand < low ? cand : low;
             if (atomicMax(&stamp[t], r + 1) < r + 1) {
               nxt[atomicAdd(&qcnt[(r + 1) % 3], 1u)] = uint16_t(t);
             }
@@ -1031,17 +1013,8 @@ __device__ void queue_dist(uint32_t N, uint32_t s, const UnitCsr& c,
         }
       }
     }
-    if (stop) {  // one LDS atomic per wave
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) {
-        const D y = __shfl_xor(low, o, 64);
-        low = y < low ? y : low;
-      }
-      if ((tid & 63) == 0 && low != kInf) atomicMin(&lowered[(r + 1) % 3], low);
-    }
     __syncthreads();
     n = qcnt[(r + 1) % 3];
-    if (stop && n && lowered[(r + 1) % 3] > dist[stopAt]) break;
   }
 }
 
@@ -1151,12 +1124,11 @@ __device__ __forceinline__ uint32_t unit_bcast(uint32_t x) {
 // The unit's SPF into l.dist: queue form (workgroup units) or the pull
 // fixpoint (spf_core.h).
 template <typename D, int UT, bool QUEUE, bool MASKED>
-__device__ __forceinline__ void ksp_spf(const KspLds<D>& l, uint32_t s, int lane,
-                                        uint32_t stopAt = OGS_NODE_NONE) {
+__device__ __forceinline__ void ksp_spf(const KspLds<D>& l, uint32_t s, int lane) {
   if constexpr (QUEUE) {
     static_assert(UT == kBlock, "queue form: one workgroup per unit");
     queue_dist<D, MASKED>(l.N, s, l.csr, l.nflags, l.dist, l.stamp, l.q0, l.q1,
-                          l.qcnt, l.mask, stopAt);
+                          l.qcnt, l.mask);
   } else {
     spf_fixpoint<D, 1, UT, false, MASKED>(l.N, s, lane, l.csr, false, l.dist,
                                           nullptr, MASKED ? l.mask : nullptr);
@@ -1184,8 +1156,7 @@ template <typename D, int UT, int STAGE, bool QUEUE>
 __global__ __launch_bounds__(kBlock) void ksp2_kernel(
     ogs_graph g, const ogs_unit* __restrict__ sources, int nSources,
     const D* __restrict__ srcDist, const ogs_path_unit* __restrict__ units,
-    int nUnits, ogs_path_out o1, ogs_path_out o2, uint32_t ldsPerUnit, int waveTrace,
-    int stopAt) {
+    int nUnits, ogs_path_out o1, ogs_path_out o2, uint32_t ldsPerUnit, int waveTrace) {
   constexpr int kUnitsPerBlock = kBlock / UT;
   using Scope = UnitScope<UT>;
   const int uib = threadIdx.x / UT;
@@ -1233,7 +1204,7 @@ __global__ __launch_bounds__(kBlock) void ksp2_kernel(
     return;
   }
   for (uint32_t i = lane; i < l.linkWords; i += UT) l.visited[i] = 0u;
-  ksp_spf<D, UT, QUEUE, true>(l, s, lane, stopAt ? t : OGS_NODE_NONE);
+  ksp_spf<D, UT, QUEUE, true>(l, s, lane);
   if constexpr (sizeof(D) == 4) {
     if (wt) {
       if (lane >= 64) return;
@@ -1273,7 +1244,7 @@ hipError_t ksp2_launch(const ogs_graph& g, const ogs_unit* sources,
   hipLaunchKernelGGL(k2, dim3((nUnits + upb - 1) / upb), dim3(kBlock), bytes,
                      stream, g, sources, nSources,
                      static_cast<const D*>(srcDist), units, nUnits, o1, o2, lds,
-                     g_kspWaveTrace, g_kspStop);
+                     g_kspWaveTrace);
   return hipGetLastError();
 }
 

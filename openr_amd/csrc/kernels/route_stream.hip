@@ -169,11 +169,13 @@ hipError_t workspace(size_t bytes, hipStream_t stream, void** out) {
 
 // "route_stream" option for large shared topologies: 2 (default) fused
 // frontier SPF + route stream, one launch; 1 SPF launch then route-stream
-// launch (dist / next-hop sets through HBM); 3 the same split pipelined over
-// unit chunks (below); 0 the fused multi-source kernel.
+// launch (dist / next-hop sets through HBM); 4 the LDS-resident SPF
+// (spf_lds.hip) then the route stream over parts. (0, the fused multi-source
+// kernel as the C3 form, and 3, the split pipelined over unit chunks on two
+// streams -- 1.40-1.64 vs 1.33 ms on C3, profiles/r03_c3_pipelined_split_
+// ab.log -- were removed in round 4; the multi-source kernel remains the
+// fallback where neither form applies.)
 int g_routeStream = 2;
-// "route_stream_chunks" option: unit chunks of the pipelined split (3)
-int g_routeStreamChunks = 4;
 // "route_store_nt" option, bits: 1 the RouteDb stream's 16-B stores are
 // non-temporal (else ordinary write-back stores), 2 the wave kernel's output
 // stores are. Default 2. The bare C3 store pattern drains faster with
@@ -182,35 +184,6 @@ int g_routeStreamChunks = 4;
 // 1.303-1.325 ms), the C2 wave kernel loses 3 % (10.9 vs 10.6 us):
 // profiles/r03_store_pattern.log, r03_store_nt_ab.log.
 int g_routeStoreNt = 2;
-
-// Side stream + events of the pipelined split, per (device, caller stream).
-namespace {
-struct Side {
-  hipStream_t stream = nullptr;
-  std::vector<hipEvent_t> ev;
-};
-std::map<std::pair<int, hipStream_t>, Side> g_side;
-
-hipError_t side_of(hipStream_t stream, size_t events, Side** out) {
-  int dev = 0;
-  hipError_t e = hipGetDevice(&dev);
-  if (e != hipSuccess) return e;
-  std::lock_guard<std::mutex> lock(g_wsMutex);
-  Side& s = g_side[{dev, stream}];
-  if (!s.stream) {
-    e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking);
-    if (e != hipSuccess) return e;
-  }
-  while (s.ev.size() < events) {
-    hipEvent_t x;
-    e = hipEventCreateWithFlags(&x, hipEventDisableTiming);
-    if (e != hipSuccess) return e;
-    s.ev.push_back(x);
-  }
-  *out = &s;
-  return hipSuccess;
-}
-}  // namespace
 
 bool try_ms(const ogs_graph& g, const ogs_prefix_table& pt, int hasPrefixes,
             const ogs_unit* units, int nUnits, uint32_t flags, int W,
@@ -222,11 +195,6 @@ hipError_t launch_frontier_spf(const ogs_graph& g, const ogs_unit* units,
                                int nUnits, uint32_t flags, int W,
                                uint32_t* dist, uint32_t* nh, void* scratch,
                                hipStream_t stream);
-hipError_t launch_frontier_spf_prepared(const ogs_graph& g, const ogs_unit* units,
-                                        int nUnits, uint32_t flags, int W, uint32_t* dist,
-                                        uint32_t* nh, void* scratch, hipStream_t stream);
-hipError_t prep_chunks(const ogs_graph& g, void* scratch, hipStream_t stream,
-                       uint64_t** chunks, uint32_t** nChunk);
 hipError_t launch_frontier_routes(const ogs_graph& g, const ogs_prefix_table& pt,
                                   const uint32_t* key, const ogs_unit* units,
                                   int nUnits, uint32_t flags, int W,
@@ -323,7 +291,7 @@ hipError_t launch_variants(const ogs_graph& g, const ogs_prefix_table& pt,
 bool try_ms_stream(const ogs_graph& g, const ogs_prefix_table& pt,
                    const ogs_unit* units, int nUnits, uint32_t flags, int W,
                    const ogs_spf_out& out, hipStream_t stream, hipError_t* err) {
-  if (!g_routeStream || !g.edge_src || (flags & OGS_F_WIDE_METRIC)) return false;
+  if (!g.edge_src || (flags & OGS_F_WIDE_METRIC)) return false;
   if (W != 1 && W != 2 && W != 3 && W != 4) return false;
   if (size_t(g.max_nodes) * (2 + W) * 4 > 160 * 1024) return false;
   const size_t Sn = size_t(g.max_nodes), Sp = size_t(pt.max_prefixes);
@@ -334,9 +302,8 @@ bool try_ms_stream(const ogs_graph& g, const ogs_prefix_table& pt,
                               ? lds_image_bytes(g, W) : 0;
   const bool ldsSplit = ldsBytes != 0;
   const bool fused = (g_routeStream == 2 || (g_routeStream == 4 && !ldsSplit)) && frontier;
-  const bool piped = g_routeStream == 3 && frontier && Sp > 0 && nUnits > 1;
   // three-word sets (65..96 links: C3 FSWs) through the frontier forms only
-  if (W == 3 && !fused && !piped && !ldsSplit) return false;
+  if (W == 3 && !fused && !ldsSplit) return false;
   const size_t keyBytes = round256(size_t(g.num_topos) * Sp * 4);
   const size_t chunkBytes = ldsSplit ? round256(ldsBytes) : frontier ? chunk_scratch_bytes(g) : 0;
   const size_t distBytes = (fused || out.dist) ? 0 : round256(size_t(nUnits) * Sn * 4);
@@ -374,50 +341,6 @@ bool try_ms_stream(const ogs_graph& g, const ogs_prefix_table& pt,
       case 2: *err = launch_route_stream<2>(g, pt, key, units, nUnits, flags, d, spf.nh, out, stream, parts); break;
       case 3: *err = launch_route_stream<3>(g, pt, key, units, nUnits, flags, d, spf.nh, out, stream, parts); break;
       default: *err = launch_route_stream<4>(g, pt, key, units, nUnits, flags, d, spf.nh, out, stream, parts); break;
-    }
-    return true;
-  }
-  if (piped) {
-    // Pipelined split: the SPF of unit chunk c runs on a side stream while
-    // the route stream of chunk c - 1 runs on the caller's -- a fused launch
-    // runs every unit's SPF phase at once (all units resident) and streams
-    // only afterwards, so HBM idles through the SPF phase.
-    const int C = std::max(1, std::min(g_routeStreamChunks, nUnits));
-    Side* side = nullptr;
-    *err = side_of(stream, size_t(C) + 1, &side);
-    if (*err != hipSuccess) return true;
-    // the side stream starts after everything already on the caller's
-    // (the keys above, and the previous call's readers of this workspace)
-    *err = hipEventRecord(side->ev[C], stream);
-    if (*err == hipSuccess) *err = hipStreamWaitEvent(side->stream, side->ev[C], 0);
-    uint64_t* chunks = nullptr;
-    uint32_t* nChunk = nullptr;
-    if (*err == hipSuccess) *err = prep_chunks(g, chunkScratch, side->stream, &chunks, &nChunk);
-    uint32_t* d = static_cast<uint32_t*>(spf.dist);
-    for (int c = 0; c < C && *err == hipSuccess; ++c) {
-      const size_t u0 = size_t(nUnits) * c / C, u1 = size_t(nUnits) * (c + 1) / C;
-      *err = launch_frontier_spf_prepared(g, units + u0, int(u1 - u0), flags, W, d + u0 * Sn,
-                                          spf.nh + u0 * W * Sn, chunkScratch, side->stream);
-      if (*err == hipSuccess) *err = hipEventRecord(side->ev[c], side->stream);
-    }
-    for (int c = 0; c < C && *err == hipSuccess; ++c) {
-      const size_t u0 = size_t(nUnits) * c / C, u1 = size_t(nUnits) * (c + 1) / C;
-      *err = hipStreamWaitEvent(stream, side->ev[c], 0);
-      if (*err != hipSuccess) break;
-      ogs_spf_out o = out;  // unit u0's rows
-      if (o.meta) o.meta += u0 * Sp;
-      if (o.metric) o.metric = static_cast<uint32_t*>(o.metric) + u0 * Sp;
-      if (o.sel) o.sel += u0 * Sp;
-      if (o.mask) o.mask += u0 * W * Sp;
-      const uint32_t* dc = d + u0 * Sn;
-      const uint32_t* nc = spf.nh + u0 * W * Sn;
-      const int n = int(u1 - u0);
-      switch (W) {
-        case 1: *err = launch_route_stream<1>(g, pt, key, units + u0, n, flags, dc, nc, o, stream); break;
-        case 2: *err = launch_route_stream<2>(g, pt, key, units + u0, n, flags, dc, nc, o, stream); break;
-        case 3: *err = launch_route_stream<3>(g, pt, key, units + u0, n, flags, dc, nc, o, stream); break;
-        default: *err = launch_route_stream<4>(g, pt, key, units + u0, n, flags, dc, nc, o, stream); break;
-      }
     }
     return true;
   }

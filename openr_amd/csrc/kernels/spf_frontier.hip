@@ -662,16 +662,13 @@ __device__ __forceinline__ void queue_spf(
 // again. Converges to the same least fixpoint as the two-phase form in about
 // half the rounds (a node's final push carries its final word; contributions
 // of a pred survive only while it stays tight, since a strictly shorter path
-// resets the word).
-// FOLD: the push stamp lives in bits 48..63 of the packed word itself
-// ({dist | nh<<32 | stamp<<48}, next-hop sets of <= 16 link slots): the CAS
-// that improves a node also claims its push for round r+1, so there is no
-// separate stamp array (4 B/node less LDS) and no second atomic per update.
-// The stamp bits are cleared when the SPF ends.
+// resets the word). (Push stamps folded into the words' top bits measured
+// 8 % slower on C4 -- concurrent CASes on a node conflict more -- and were
+// removed in round 4.)
 // Rounds of the packed queue SPF from the current list state: round r's
 // list is buffer r & 1 with count slot r % 3 holding n entries (stamps
 // already claim them). Returns the round after the last non-empty one.
-template <bool MODS, bool FOLD>
+template <bool MODS>
 __device__ __forceinline__ uint32_t packed_rounds(
     uint32_t s, const uint64_t* __restrict__ edges, const uint32_t* __restrict__ gRow,
     uint32_t e0, const uint8_t* __restrict__ nflags, bool hop, uint64_t* dn,
@@ -693,8 +690,7 @@ __device__ __forceinline__ uint32_t packed_rounds(
       if (v != s && (iv & kDrained)) continue;  // LinkState.cpp:741-752
       const uint64_t xv = dn[v];
       const uint32_t dv = static_cast<uint32_t>(xv);
-      const uint32_t nv = FOLD ? static_cast<uint32_t>(xv >> 32) & 0xFFFFu  // not the stamp
-                               : static_cast<uint32_t>(xv >> 32);
+      const uint32_t nv = static_cast<uint32_t>(xv >> 32);
       for_row(edges, b, rowEnd - b, [&](uint32_t e, uint64_t x) {
         const uint32_t lo = static_cast<uint32_t>(x);
         if (lo & OGS_EDGE_DOWN) return;
@@ -706,26 +702,19 @@ __device__ __forceinline__ uint32_t packed_rounds(
         // the source contributes the link slot (its row index), others NH(v)
         const uint32_t bits = (v == s) ? (1u << (e - b)) : nv;
         uint64_t old = dn[t];
-        bool push = false;
         for (;;) {
           const uint32_t dt = static_cast<uint32_t>(old);
-          const uint32_t nt = FOLD ? static_cast<uint32_t>(old >> 32) & 0xFFFFu
-                                   : static_cast<uint32_t>(old >> 32);
+          const uint32_t nt = static_cast<uint32_t>(old >> 32);
           if (c > dt || (c == dt && !(bits & ~nt))) return;
-          uint64_t nw = c < dt ? (uint64_t(c) | (uint64_t(bits) << 32))
-                               : (uint64_t(dt) | (uint64_t(nt | bits) << 32));
-          if constexpr (FOLD) nw |= uint64_t(r + 1) << 48;
+          const uint64_t nw = c < dt ? (uint64_t(c) | (uint64_t(bits) << 32))
+                                     : (uint64_t(dt) | (uint64_t(nt | bits) << 32));
           const uint64_t seen = atomicCAS(reinterpret_cast<unsigned long long*>(&dn[t]),
                                           static_cast<unsigned long long>(old),
                                           static_cast<unsigned long long>(nw));
-          if (seen == old) {
-            if constexpr (FOLD) push = uint32_t(old >> 48) < r + 1;
-            break;
-          }
+          if (seen == old) break;
           old = seen;
         }
-        if constexpr (!FOLD) push = atomicMax(&stamp[t], r + 1) < r + 1;
-        if (push) nxt[atomicAdd(&qcnt[(r + 1) % 3], 1u)] = uint16_t(t);
+        if (atomicMax(&stamp[t], r + 1) < r + 1) nxt[atomicAdd(&qcnt[(r + 1) % 3], 1u)] = uint16_t(t);
       });
     }
     __syncthreads();
@@ -734,7 +723,7 @@ __device__ __forceinline__ uint32_t packed_rounds(
   return r;
 }
 
-template <bool MODS, bool FOLD = false>
+template <bool MODS>
 __device__ __forceinline__ void queue_spf_packed(
     uint32_t N, uint32_t s, const uint64_t* __restrict__ edges,
     const uint32_t* __restrict__ gRow, uint32_t e0,
@@ -746,7 +735,7 @@ __device__ __forceinline__ void queue_spf_packed(
   const int tid = threadIdx.x;
   for (uint32_t v = tid; v < N; v += kBlock) {
     dn[v] = (v == s) ? 0ull : uint64_t(kInf);
-    if constexpr (!FOLD) stamp[v] = 0u;
+    stamp[v] = 0u;
   }
   for (uint32_t v = tid; ninfo && v <= N; v += kBlock) {  // nullptr: CSR reads
     ninfo[v] = (gRow[v] - e0) |
@@ -762,12 +751,8 @@ __device__ __forceinline__ void queue_spf_packed(
 #ifdef OGS_STAMPS
   tp[0] = __builtin_amdgcn_s_memtime();
 #endif
-  const uint32_t r = packed_rounds<MODS, FOLD>(s, edges, gRow, e0, nflags, hop, dn, stamp,
-                                               q0, q1, qcnt, ninfo, dead, 1u, 1u);
-  if constexpr (FOLD) {  // the plain packed form for everything downstream
-    for (uint32_t v = tid; v < N; v += kBlock) dn[v] &= 0x0000FFFFFFFFFFFFull;
-    __syncthreads();
-  }
+  const uint32_t r = packed_rounds<MODS>(s, edges, gRow, e0, nflags, hop, dn, stamp,
+                                         q0, q1, qcnt, ninfo, dead, 1u, 1u);
 #ifdef OGS_STAMPS
   tp[1] = tp[2] = __builtin_amdgcn_s_memtime();
   tp[3] = r;
@@ -778,12 +763,11 @@ __device__ __forceinline__ void queue_spf_packed(
 }
 
 uint32_t frontier_lds_bytes(uint32_t Sn, int W, bool queue = false, bool ninfo = true,
-                            bool stamps = true, bool stamp8 = false) {
+                            bool stamp8 = false) {
   const uint32_t core = 4u * (((Sn + 3u) & ~3u) + ((Sn * W + 3u) & ~3u));
   if (!queue) return core + (stamp8 ? ((Sn + 3u) & ~3u) : 2u * ((Sn + 1u) & ~1u));
-  // + u32 stamps (not with folded stamps) + two u16 node lists (+ u32 node
-  // info [Sn + 1])
-  return core + (stamps ? 4u * ((Sn + 3u) & ~3u) : 0u) + 2u * 2u * ((Sn + 1u) & ~1u) +
+  // + u32 stamps + two u16 node lists (+ u32 node info [Sn + 1])
+  return core + 4u * ((Sn + 3u) & ~3u) + 2u * 2u * ((Sn + 1u) & ~1u) +
       (ninfo ? 4u * ((Sn + 4u) & ~3u) : 0u);
 }
 
@@ -844,10 +828,7 @@ __device__ __forceinline__ void spf_frontier_body(
   uint16_t* stamp = reinterpret_cast<uint16_t*>(nh + ((Sn * W + 3u) & ~3u));  // [Sn]
   // queue form: u32 stamps [Sn] over the same start, then two u16 lists
   uint32_t* stamp32 = reinterpret_cast<uint32_t*>(stamp);
-  // folded stamps (QMODE 3): no stamp array, the lists start there (and the
-  // per-node route flags below reuse the dead lists)
-  uint16_t* q0 = QMODE == 3 ? stamp
-                            : reinterpret_cast<uint16_t*>(stamp32 + ((Sn + 3u) & ~3u));
+  uint16_t* q0 = reinterpret_cast<uint16_t*>(stamp32 + ((Sn + 3u) & ~3u));
   uint16_t* q1 = q0 + ((Sn + 1u) & ~1u);
   uint32_t* ninfo = (flags & kFlagNinfoGlobal)
       ? nullptr
@@ -876,7 +857,7 @@ __device__ __forceinline__ void spf_frontier_body(
                               (flags & kFlagScanRound1) == 0, (flags & kFlagSlotWalk) != 0,
                               (flags & kFlagNoPreload) == 0);
   } else if constexpr (PACKED) {
-    queue_spf_packed<MODS, QMODE == 3>(N, s, g.edges + e0, gRow, e0, nflags,
+    queue_spf_packed<MODS>(N, s, g.edges + e0, gRow, e0, nflags,
                            (flags & OGS_F_HOP_METRIC) != 0, dn64, stamp32, q0, q1,
                            qcnt, ninfo, tp, dead);
   } else if constexpr (QMODE == 1) {
@@ -988,9 +969,6 @@ __global__ __launch_bounds__(B) void spf_frontier_kernel(
 // the source's row directly, 0 it scans every chunk record (A/B)
 int g_spfSeedRow = 1;
 
-// "frontier_wg_lds" option: minimum LDS bytes per fused frontier + route
-// stream workgroup (0: what the unit needs)
-int g_frontierWgLds = 0;
 
 // "spf_packed_scan" option: 1 (default) chunk-scan units with one-word
 // next-hop sets relax packed {dist, nh} words in one phase
@@ -999,9 +977,7 @@ int g_spfPackedScan = 1;
 
 // "spf_queue" option: -1 (default) the queue form for sparse topologies
 // (max degree <= 16, <= 65,535 nodes; one-phase packed words when the
-// next-hop sets fit one word, with the push stamps folded into the words
-// when max degree <= 16), 0 never, 1 whenever it fits, 2 the two-phase
-// queue form even for one-word sets, 3 packed with folded stamps (A/B).
+// next-hop sets fit one word), 0 always the chunk scan (A/B, tests).
 int g_spfQueue = -1;
 
 // "spf_ninfo" option: 1 (default) the queue forms keep row begin | drained
@@ -1016,18 +992,12 @@ bool ninfo_in_lds(uint32_t Sn, int W) {
       kCu / frontier_lds_bytes(Sn, W, true, false);
 }
 
-// 0 chunk scan, 1 two-phase queue, 2 packed one-phase queue, 3 packed with
-// folded stamps (next-hop sets of <= 16 link slots: max degree <= 16; and
-// < 65,535 rounds) -- only with spf_queue 3: on C4 it is 8 % slower than
-// form 2 at 5 instead of 4 units per CU (the stamp bits make concurrent
-// CASes on a node conflict more), so form 2 stays the default.
+// 0 chunk scan, 1 two-phase queue, 2 packed one-phase queue
 int queue_mode(const ogs_graph& g, int W) {
   if (g_spfQueue == 0 || g.max_nodes > 65535) return 0;
   if (frontier_lds_bytes(uint32_t(g.max_nodes), W, true) > 160u * 1024u) return 0;
-  if (g_spfQueue == -1 && g.max_degree > 16) return 0;
-  if (W != 1 || g_spfQueue == 2) return 1;
-  const bool fold = g_spfQueue == 3 && g.max_degree <= 16 && g.max_nodes < 65000;
-  return fold ? 3 : 2;
+  if (g.max_degree > 16) return 0;
+  return W != 1 ? 1 : 2;
 }
 
 template <int W, bool ROUTES, bool MODS, bool DIFF, int QMODE, bool OUTS3 = false,
@@ -1042,10 +1012,7 @@ hipError_t launch_frontier_q(const ogs_graph& g, const ogs_prefix_table& pt,
   const bool scan = QMODE == 0 || QMODE == 4;  // chunk-scan forms: no lists
   const bool ninfo = scan || ninfo_in_lds(uint32_t(g.max_nodes), W);
   uint32_t lds =
-      frontier_lds_bytes(uint32_t(g.max_nodes), W, !scan, ninfo, QMODE != 3, QMODE == 4);
-  // occupancy probe (A/B): fewer workgroups per CU stagger the SPF and
-  // route-stream phases of the resident units
-  if (ROUTES && lds < uint32_t(g_frontierWgLds)) lds = uint32_t(g_frontierWgLds);
+      frontier_lds_bytes(uint32_t(g.max_nodes), W, !scan, ninfo, QMODE == 4);
   if (!ninfo) flags |= kFlagNinfoGlobal;
   if (!g_spfSeedRow) flags |= kFlagScanRound1;
   if (g_spfLaneWalk == 0 || (g_spfLaneWalk < 0 && B < 512)) flags |= kFlagSlotWalk;
@@ -1172,11 +1139,6 @@ hipError_t launch_frontier(const ogs_graph& g, const ogs_prefix_table& pt,
         g, pt, key, chunks, nChunk, units, nUnits, flags, dist, nh, out, stream, mods, diff);
   }
   if constexpr (W == 1) {
-    if (qm == 3) {
-      return launch_frontier_q<W, ROUTES, MODS, DIFF, 3>(
-          g, pt, key, chunks, nChunk, units, nUnits, flags, dist, nh, out, stream,
-          mods, diff);
-    }
     if (qm == 2) {
       return launch_frontier_q<W, ROUTES, MODS, DIFF, 2>(
           g, pt, key, chunks, nChunk, units, nUnits, flags, dist, nh, out, stream,
@@ -1494,7 +1456,7 @@ __global__ __launch_bounds__(kBlock) void spf_variant_repair_kernel(
     }
   }
   __syncthreads();
-  packed_rounds<true, false>(s, edges, gRow, e0, nflags, hop, dn, stamp, q0, q1, qcnt,
+  packed_rounds<true>(s, edges, gRow, e0, nflags, hop, dn, stamp, q0, q1, qcnt,
                              nullptr, dead, 1u, qcnt[1]);
   __syncthreads();
   if (oDist || oNh) {

@@ -879,8 +879,7 @@ bool lds_unit_fits(const ogs_graph& g, int W, uint32_t flags) {
   return b <= 160u * 1024u;
 }
 
-uint32_t frontier_lds_bytes(uint32_t Sn, int W, bool queue, bool ninfo, bool stamps,
-                            bool stamp8);
+uint32_t frontier_lds_bytes(uint32_t Sn, int W, bool queue, bool ninfo, bool stamp8);
 
 bool use_global(const ogs_graph& g, int W, uint32_t flags) {
   if (g_spfGlobal == 1 || !lds_unit_fits(g, W, flags)) return true;
@@ -889,7 +888,7 @@ bool use_global(const ogs_graph& g, int W, uint32_t flags) {
   // of 16k+ nodes) the HBM frontier wins -- G1, 20,000-node WAN x 64
   // sources: 12.4 ms vs 35.0 ms for the multi-source sweep
   return g.max_nodes > 256 && !(flags & OGS_F_WIDE_METRIC) &&
-      frontier_lds_bytes(uint32_t(g.max_nodes), W, false, true, true, false) > 160u * 1024u;
+      frontier_lds_bytes(uint32_t(g.max_nodes), W, false, true, false) > 160u * 1024u;
 }
 
 template <typename D, int W>

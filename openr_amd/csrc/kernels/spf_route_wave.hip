@@ -38,7 +38,6 @@ namespace ogs {
 
 constexpr uint32_t OGS_WAVE_OPT_BPERMUTE = 1;    // register-resident SPF words
 constexpr uint32_t OGS_WAVE_OPT_REG_ROUTES = 2;  // identity-segment route path
-constexpr uint32_t OGS_WAVE_OPT_PAIR = 4;        // two units per wave, 16-bit words
 
 // LDS image of one unit. Advertisement metrics are staged only when best
 // route selection reads them; minNexthop is read from HBM on demand (only
@@ -837,268 +836,6 @@ __global__ __launch_bounds__(64 * UPB) void spf_route_wave_kernel(
 }
 
 // ---- two units per wavefront: 16-bit packed words ---------------------------
-// Batches of many topologies of one structure (C2: 4096 random-metric
-// grids; what-if copies of one network) give adjacent units the same
-// relaxation order and the same edge positions -- only the metrics differ.
-// Such a PAIR shares one wavefront: every LDS word holds both units' 16-bit
-// words {A lo, B hi} = dist << 4 | ~nh & 0xF (source degree <= 4), and the
-// narrow form's add / min / min / and per edge become v_pk_add_u16 /
-// v_pk_min_u16 / v_pk_min_u16 / v_and_b32 on both units at once: one
-// relaxation round for two SPFs. Unreachable = 0x800F per half; candidates
-// never wrap (words are capped at 0x800F by the round's min and w << 4 <=
-// 0x7FF0), so the rounds compute min(dist, 2^11) exactly (the clamped
-// Bellman-Ford operator's fixpoint). A unit whose largest finite distance +
-// its largest weight reaches 2^11 might have been clamped: it reruns alone
-// in the 32-bit form (wave_spf), as do the two units of a pair whose
-// structure differs. Staging, table setup and routes are per unit, as in
-// spf_route_wave_kernel.
-typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ uint32_t pk_add(uint32_t a, uint32_t b) {
-  return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, a) + __builtin_bit_cast(u16x2, b));
-}
-__device__ __forceinline__ uint32_t pk_min(uint32_t a, uint32_t b) {
-  return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(u16x2, a),
-                                                                __builtin_bit_cast(u16x2, b)));
-}
-
-template <int NPL, int MAXD, int UPB>
-__global__ __launch_bounds__(64 * UPB) void spf_route_wave_pair_kernel(
-    ogs_graph g, ogs_prefix_table pt, int hasPrefixes,
-    const ogs_unit* __restrict__ units, int nUnits, uint32_t flags,
-    ogs_spf_out out, uint32_t ldsPerUnit, uint32_t maxA, uint32_t wopt) {
-  constexpr uint32_t kInf = 0xFFFFFFFFu;
-  constexpr uint32_t P0 = NPL * 64;
-  constexpr int KP = NPL + 1;
-  const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  const int u0 = 2 * (blockIdx.x * UPB + wib);
-  if (u0 >= nUnits) return;
-  const int nu = nUnits - u0 >= 2 ? 2 : 1;  // uniform
-  uint32_t rounds = 0;
-
-  // ---- unit offsets: both records and both guessed descriptors at once ---
-  uint32_t topo[2], s[2], nb[2], N[2], p0[2] = {0, 0}, P[2] = {0, 0}, a0[2] = {0, 0},
-      A[2] = {0, 0};
-  {
-    const ogs_unit ua = units[u0];
-    const ogs_unit ub = units[u0 + nu - 1];
-    topo[0] = ua.topo;
-    s[0] = ua.src;
-    topo[1] = ub.topo;
-    s[1] = ub.src;
-    const uint4* td = reinterpret_cast<const uint4*>(g.topo_desc);
-#pragma unroll
-    for (int x = 0; x < 2; ++x) {
-      const uint32_t ux = uint32_t(u0 + (x < nu ? x : 0));
-      const uint32_t guess = ux < uint32_t(g.num_topos) ? ux : 0u;
-      uint4 dx = td[2 * guess];
-      uint4 dy = td[2 * guess + 1];
-      asm volatile("" : "+v"(dx.x), "+v"(dx.y), "+v"(dy.x), "+v"(dy.y), "+v"(dy.z),
-                   "+v"(dy.w));
-      dx.x = __builtin_amdgcn_readfirstlane(dx.x);
-      dx.y = __builtin_amdgcn_readfirstlane(dx.y);
-      dy.x = __builtin_amdgcn_readfirstlane(dy.x);
-      dy.y = __builtin_amdgcn_readfirstlane(dy.y);
-      dy.z = __builtin_amdgcn_readfirstlane(dy.z);
-      dy.w = __builtin_amdgcn_readfirstlane(dy.w);
-      if (topo[x] != guess) {
-        dx = td[2 * topo[x]];
-        dy = td[2 * topo[x] + 1];
-      }
-      nb[x] = dx.x;
-      N[x] = dx.y;
-      if (hasPrefixes) {
-        p0[x] = dy.x;
-        P[x] = dy.y;
-        a0[x] = dy.z;
-        A[x] = dy.w;
-      }
-    }
-  }
-  const bool brs = flags & OGS_F_BEST_ROUTE_SELECTION;
-  const WaveLayout L = WaveLayout::make(g.max_nodes, g.max_edges,
-                                        hasPrefixes ? pt.max_prefixes : 0,
-                                        hasPrefixes ? maxA : 0, brs);
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* base[2] = {smem + (2 * wib) * ldsPerUnit, smem + (2 * wib + 1) * ldsPerUnit};
-
-  // ---- staging: both units' loads in one batch ----------------------------
-  uint32_t ie[2][NPL][MAXD], vk[2][NPL];
-  WStage<KP, uint32_t> sOff[2], sNode[2];
-  WStage<KP, uint8_t> sPf[2];
-  WStage<KP, int4> sMet[2];
-  WStage<NPL, uint8_t> sFlag[2];
-  bool pfxFits[2];
-#pragma unroll
-  for (int x = 0; x < 2; ++x) {
-    const uint32_t* ib = g.slot_edges + size_t(topo[x]) * (MAXD * P0);
-#pragma unroll
-    for (int j = 0; j < MAXD; ++j) {
-#pragma unroll
-      for (int k = 0; k < NPL; ++k) ie[x][k][j] = ib[j * P0 + k * 64 + lane];
-    }
-    sFlag[x].load(g.node_flags + nb[x], N[x], lane);
-    const uint16_t* so = g.slot_node + size_t(topo[x]) * (NPL * 64);
-#pragma unroll
-    for (int k = 0; k < NPL; ++k) vk[x][k] = so[k * 64 + lane];
-    pfxFits[x] = (P[x] + 1 <= 64u * KP) && (A[x] <= 64u * KP);
-    if (hasPrefixes && pfxFits[x]) {
-      sOff[x].load(pt.adv_off + p0[x], P[x] + 1, lane);
-      sNode[x].load(pt.adv_node + a0[x], A[x], lane);
-      sMet[x].load(reinterpret_cast<const int4*>(pt.adv_metrics) + a0[x], brs ? A[x] : 0u,
-                   lane);
-      sPf[x].load(pt.pfx_flags + p0[x], P[x], lane);
-    }
-  }
-#pragma unroll
-  for (int x = 0; x < 2; ++x) {
-#pragma unroll
-    for (int k = 0; k < NPL; ++k) vk[x][k] = vk[x][k] == 0xFFFFu ? 0xFFFFFFFFu : vk[x][k];
-  }
-
-  // ---- per-edge constants of both units -----------------------------------
-  const bool hop = flags & OGS_F_HOP_METRIC;
-  uint32_t ea[2][NPL][MAXD], ew[2][NPL][MAXD], posS[2], wmax[2];
-#pragma unroll
-  for (int x = 0; x < 2; ++x) {
-    posS[x] = P0;
-#pragma unroll
-    for (int k = 0; k < NPL; ++k) {
-      const uint64_t m = __builtin_amdgcn_ballot_w64(vk[x][k] == s[x]);
-      if (m) posS[x] = uint32_t(k * 64) + uint32_t(__builtin_ctzll(m));
-    }
-    wmax[x] = wave_max(wave_edges_from_image<NPL, MAXD>(ie[x], posS[x], hop, ea[x], ew[x]));
-  }
-  // a pair: same order, same source position and edge positions, source
-  // degree <= 4 (slot words P0 + 1 .. P0 + 4), weights < 2^11
-  bool pair = nu == 2 && posS[0] == posS[1] && posS[0] < P0 && wmax[0] < 2048u &&
-      wmax[1] < 2048u;
-  if (pair) {
-    bool bad = false;
-#pragma unroll
-    for (int k = 0; k < NPL; ++k) {
-      bad |= vk[0][k] != vk[1][k];
-#pragma unroll
-      for (int j = 0; j < MAXD; ++j) {
-        bad |= ea[0][k][j] != ea[1][k][j] || ea[0][k][j] > P0 + 4;
-      }
-    }
-    pair = __builtin_amdgcn_ballot_w64(bad) == 0ull;
-  }
-
-  // ---- SPF ------------------------------------------------------------------
-  uint32_t dcur[2][NPL], ncur[2][NPL];
-  bool redo[2] = {!pair, !pair && nu == 2};
-  if (pair) {
-    constexpr uint32_t kUnr = 0x800F800Fu;  // both halves unreachable
-    uint32_t* d32 = reinterpret_cast<uint32_t*>(base[0] + L.dn32);
-    const uint32_t sv = s[0];
-    uint32_t ws[NPL][MAXD], ra[NPL][MAXD], cur[NPL];
-#pragma unroll
-    for (int k = 0; k < NPL; ++k) {
-      const bool src = vk[0][k] == sv;
-#pragma unroll
-      for (int j = 0; j < MAXD; ++j) {
-        ra[k][j] = src ? P0 + 9 : ea[0][k][j];
-        ws[k][j] = src ? 0u : (ew[0][k][j] << 4) | (ew[1][k][j] << 20);
-      }
-      cur[k] = src ? 0x000F000Fu : kUnr;
-      d32[k * 64 + lane] = cur[k];
-    }
-    if (lane == 0) {
-      d32[P0] = kUnr;
-      d32[P0 + 9] = 0x000F000Fu;
-    }
-    if (lane < 4) d32[P0 + 1 + lane] = (~(1u << lane) & 0xFu) * 0x00010001u;
-    wave_sync();
-    for (;;) {
-      uint32_t chg = 0u;
-#pragma unroll
-      for (int k = 0; k < NPL; ++k) {
-        uint32_t cand[MAXD];
-        uint32_t best = kUnr;
-#pragma unroll
-        for (int j = 0; j < MAXD; ++j) {
-          cand[j] = pk_add(d32[ra[k][j]], ws[k][j]);
-          best = pk_min(best, cand[j]);
-        }
-        const uint32_t hiB = best | 0x000F000Fu;
-        uint32_t word = hiB;
-#pragma unroll
-        for (int j = 0; j < MAXD; ++j) word &= pk_min(cand[j], hiB);
-        chg |= word ^ cur[k];
-        cur[k] = word;
-        d32[k * 64 + lane] = word;
-      }
-#ifdef OGS_STAMPS
-      ++rounds;
-#endif
-      if (__builtin_amdgcn_ballot_w64(chg != 0u) == 0ull) break;
-      wave_sync();
-    }
-    // unpack; a unit is exact when its largest finite distance + largest
-    // weight stays below the 2^11 clamp
-#pragma unroll
-    for (int x = 0; x < 2; ++x) {
-      uint32_t dmax = 0;
-#pragma unroll
-      for (int k = 0; k < NPL; ++k) {
-        const uint32_t h = (cur[k] >> (16 * x)) & 0xFFFFu;
-        const bool unr = h >= 0x8000u;
-        dcur[x][k] = unr ? kInf : h >> 4;
-        ncur[x][k] = unr ? 0u : ~h & 0xFu;
-        dmax = (!unr && dcur[x][k] > dmax) ? dcur[x][k] : dmax;
-      }
-      redo[x] = wave_max(dmax) + wmax[x] >= 2048u;
-    }
-    wave_sync();  // the packed words are overwritten by a redo
-  }
-#pragma unroll
-  for (int x = 0; x < 2; ++x) {
-    if (redo[x]) {
-      const bool narrow = uint64_t(wmax[x]) * (N[x] > 0 ? N[x] - 1 : 0) < 0x7FFFFFull;
-      wave_spf<NPL, MAXD>(base[x], L, narrow, vk[x], ea[x], ew[x], s[x], lane, dcur[x],
-                          ncur[x], rounds);
-    }
-  }
-
-  // ---- per unit: final words by node id, tables, outputs, routes ----------
-  bool ident[2];
-#pragma unroll
-  for (int x = 0; x < 2; ++x) {
-    if (x >= nu) break;
-    uint64_t* dn = reinterpret_cast<uint64_t*>(base[x] + L.dn);
-#pragma unroll
-    for (int k = 0; k < NPL; ++k) {
-      const uint32_t v = vk[x][k];
-      if (v == s[x]) {
-        dcur[x][k] = 0u;
-        ncur[x][k] = 0u;
-      }
-      if (v < N[x]) dn[v] = uint64_t(dcur[x][k]) | (uint64_t(ncur[x][k]) << 32);
-    }
-    ident[x] = wave_stage_tables<NPL, KP>(pt, hasPrefixes, pfxFits[x], brs, wopt, N[x], P[x],
-                                          A[x], p0[x], a0[x], sOff[x], sNode[x], sPf[x],
-                                          sMet[x], sFlag[x], base[x], L, lane);
-  }
-  wave_sync();
-#pragma unroll
-  for (int x = 0; x < 2; ++x) {
-    if (x >= nu) break;
-    wave_outputs<NPL, KP>(g, pt, hasPrefixes, flags, out, size_t(u0 + x), s[x], N[x], P[x],
-                          a0[x], ident[x], vk[x], dcur[x], ncur[x], sNode[x], sPf[x], base[x],
-                          L, lane);
-  }
-#ifdef OGS_STAMPS
-  wave_sync();
-  if (lane == 0 && out.sel) {
-    uint32_t* d = out.sel + size_t(u0) * pt.max_prefixes;
-    d[3] = rounds;
-  }
-#endif
-}
-
 // "wave_wg_lds" option: minimum LDS bytes per workgroup (occupancy probe for
 // A/B measurements; 0 = just what the units need)
 int g_waveWgLds = 0;
@@ -1106,11 +843,11 @@ int g_waveWgLds = 0;
 int g_waveUpb = 4;
 // "wave_opt" option: OGS_WAVE_OPT_* bits (A/B of the register paths); the
 // ds_bpermute SPF measured no faster than the LDS words (latency-bound
-// rounds), and the pair form slower (C2: 11.1 vs 10.0 us per launch,
-// profiles/r03_ab_wave_pair.log -- every wave is resident from the start, so
-// the launch lasts one wave's dependent chain; pairing halves the waves but
-// not that chain, and each wave then runs two route phases), so only the
-// register route path is on by default
+// rounds), so only the register route path is on by default. (Two units per
+// wavefront with 16-bit packed words measured slower in round 3 -- C2 11.1
+// vs 10.0 us per launch, profiles/r03_ab_wave_pair.log: every wave is
+// resident from the start, so a launch lasts one wave's dependent chain --
+// and was removed in round 4.)
 int g_waveOpt = OGS_WAVE_OPT_REG_ROUTES;
 
 template <int NPL, int MAXD, int UPB>
@@ -1134,45 +871,11 @@ hipError_t launch_wave_upb(const ogs_graph& g, const ogs_prefix_table& pt,
   return hipGetLastError();
 }
 
-// Two units per wavefront (spf_route_wave_pair_kernel): needs the descriptor
-// table, the relaxation order and the per-position edge image of every
-// topology; pairs whose structure differs run unpacked inside the kernel.
-template <int NPL, int MAXD>
-bool launch_wave_pair(const ogs_graph& g, const ogs_prefix_table& pt, int hasPrefixes,
-                      const ogs_unit* units, int nUnits, uint32_t flags,
-                      const ogs_spf_out& out, uint32_t lds, uint32_t maxA,
-                      hipStream_t stream, hipError_t* err) {
-  constexpr int UPB = 4;  // wavefronts per workgroup, two units each
-  if (!(g_waveOpt & OGS_WAVE_OPT_PAIR) || nUnits < 2 || !g.topo_desc || !g.slot_node ||
-      g.slot_stride != NPL * 64 || !g.slot_edges || g.slot_degree != MAXD) {
-    return false;
-  }
-  const size_t bytes = size_t(lds) * 2 * UPB;
-  if (bytes > 160 * 1024) return false;
-  auto k = spf_route_wave_pair_kernel<NPL, MAXD, UPB>;
-  if (bytes > 64 * 1024) {
-    *err = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
-                               hipFuncAttributeMaxDynamicSharedMemorySize, int(bytes));
-    if (*err != hipSuccess) return true;
-  }
-  const int grid = (nUnits + 2 * UPB - 1) / (2 * UPB);
-  if (g_routeStoreNt & 2) flags |= kFlagNtStores;
-  hipLaunchKernelGGL(k, dim3(grid), dim3(64 * UPB), bytes, stream, g, pt, hasPrefixes, units,
-                     nUnits, flags, out, lds, maxA, uint32_t(g_waveOpt));
-  *err = hipGetLastError();
-  return true;
-}
-
 template <int NPL, int MAXD>
 hipError_t launch_wave(const ogs_graph& g, const ogs_prefix_table& pt,
                        int hasPrefixes, const ogs_unit* units, int nUnits,
                        uint32_t flags, const ogs_spf_out& out, uint32_t lds,
                        uint32_t maxA, hipStream_t stream) {
-  hipError_t err = hipSuccess;
-  if (launch_wave_pair<NPL, MAXD>(g, pt, hasPrefixes, units, nUnits, flags, out, lds, maxA,
-                                  stream, &err)) {
-    return err;
-  }
   if (g_waveUpb == 16 && uint64_t(lds) * 16 <= 160 * 1024) {
     return launch_wave_upb<NPL, MAXD, 16>(g, pt, hasPrefixes, units, nUnits, flags,
                                           out, lds, maxA, stream);

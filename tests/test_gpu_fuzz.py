@@ -150,7 +150,6 @@ PATHS = {
                           (b"spf_global_sync", 0, 1)],
     "workgroup_units": [(b"unit_width", 256, -1)],
     "wave_plain": [(b"wave_opt", 0, 2)],
-    "wave_pair": [(b"wave_opt", 6, 2)],
 }
 
 

@@ -162,24 +162,17 @@ def test_ksp2_exact_on_simple_graphs(product, oracle, seed):
             assert _paths(pls, s, d, k) == _paths(ols, s, d, k), (s, d, k)
 
 
-@pytest.mark.parametrize("stop", [1, 0])
-def test_ksp2_batch_stop_at_destination(product, oracle, stop):
-    """prefetchKthPaths' batched KSP2 with the k = 2 SPF ended at the
-    destination's distance (ksp_stop 1) and run to the fixpoint (0): the
-    same paths as the oracle's getKthPaths for every destination."""
-    import openr_amd.capi as capi
-    lib = capi.load()
+def test_ksp2_batch_prefetch(product, oracle):
+    """prefetchKthPaths' batched KSP2 (one k = 1 memo fill, then every
+    destination's masked k = 2 SPF in one launch): the same paths as the
+    oracle's getKthPaths for every destination."""
     n = 9
     pls, ols = _grid_ls(product, n, 21, 7), _grid_ls(oracle, n, 21, 7)
     dests = [str(d) for d in range(n * n)]
-    capi.check(lib, lib.ogs_set_option(b"ksp_stop", stop), "ksp_stop")
-    try:
-        pls.prefetchKthPaths("40", dests)
-        for d in dests:
-            for k in (1, 2):
-                assert _paths(pls, "40", d, k) == _paths(ols, "40", d, k), (d, k)
-    finally:
-        lib.ogs_set_option(b"ksp_stop", 0)
+    pls.prefetchKthPaths("40", dests)
+    for d in dests:
+        for k in (1, 2):
+            assert _paths(pls, "40", d, k) == _paths(ols, "40", d, k), (d, k)
 
 
 def test_ksp2_on_multigraphs(product, oracle):
@@ -243,40 +236,6 @@ def test_wave_kernel_distance_forms(product, oracle, metric_max):
     br.download()
     _cmp([br.canonical(u) for u in range(T)],
          oracle.grid_batch_route_dbs(opts, 0, T, "1"), f"c2 metricMax={metric_max}")
-
-
-@pytest.mark.parametrize("metric_max", [100, 125, 160, 2047, 2048])
-def test_wave_pair_form(product, oracle, metric_max):
-    """Two units per wavefront with 16-bit words (wave_opt bit 2, opt-in):
-    pairs of one structure relax together with distances clamped at 2^11; a
-    unit whose largest distance + largest weight reaches the clamp reruns in
-    32-bit words (metricMax 125 / 160: some grids past 2^11, some not), as do
-    pairs whose source or structure differs (an odd batch split over two
-    sources, so one pair straddles them) and weights of 2^11 and more. Every
-    RouteDb equals the oracle's, and equals the one-unit-per-wave kernel's."""
-    import openr_amd.capi as capi
-    lib = capi.load()
-    opts = dict(n=10, metricSeed=0xC2400000 + metric_max, prefixSeed=0xC1,
-                metricMax=metric_max)
-    parts = [(0, 37, "1"), (37, 63, "12")]  # topologies [lo, hi), source
-    cpu = []
-    for lo, hi, src in parts:
-        cpu += oracle.grid_batch_route_dbs(opts, lo, hi, src)
-    got = {}
-    try:
-        for wopt in (6, 2):
-            capi.check(lib, lib.ogs_set_option(b"wave_opt", wopt), "wave_opt")
-            br = product.BatchRunner(True, False, False)
-            for lo, hi, src in parts:
-                br.add_grid_batch(opts, lo, hi, src)
-            br.upload()
-            br.run()
-            br.download()
-            got[wopt] = [br.canonical(u) for u in range(br.num_units())]
-    finally:
-        lib.ogs_set_option(b"wave_opt", 2)
-    _cmp(got[6], cpu, f"pair metricMax={metric_max}")
-    assert got[6] == got[2]
 
 
 @pytest.mark.parametrize("nt", [0, 2])
@@ -396,7 +355,6 @@ def _batch_dbs(product, kind, opts, srcs, enable_v4, brs, **options):
         return [br.canonical(u) for u in range(len(srcs))]
     finally:
         lib.ogs_set_option(b"route_stream", 2)
-        lib.ogs_set_option(b"route_stream_chunks", 4)
         lib.ogs_set_option(b"frontier_parts", 0)
         lib.ogs_set_option(b"frontier_parts_wide", 0)
         lib.ogs_set_option(b"spf_frontier", 1)
@@ -408,7 +366,7 @@ def _batch_dbs(product, kind, opts, srcs, enable_v4, brs, **options):
 MIX = dict(v4Permille=150, anycastPermille=120, minNhPermille=60, drainPermille=50)
 
 
-@pytest.mark.parametrize("stream,frontier", [(0, 0), (1, 0), (1, 1), (2, 1), (3, 1), (4, 1)])
+@pytest.mark.parametrize("stream,frontier", [(1, 0), (1, 1), (2, 0), (2, 1), (4, 1)])
 @pytest.mark.parametrize("enable_v4,brs", [(True, False), (False, True), (True, True)])
 def test_route_stream_fabric_prefix_mix(product, oracle, stream, frontier, enable_v4, brs):
     """Split SPF / route-stream launches vs the fused multi-source kernel on a
@@ -464,7 +422,7 @@ def test_frontier_seed_row(product, oracle, seed, wide):
     _cmp(a, oracle.gen_route_dbs("fabric", opts, srcs, True, False, True), "seedrow")
 
 
-@pytest.mark.parametrize("stream,frontier", [(0, 0), (1, 0), (1, 1), (2, 1), (3, 1), (4, 1)])
+@pytest.mark.parametrize("stream,frontier", [(1, 0), (1, 1), (2, 0), (2, 1), (4, 1)])
 def test_route_stream_wan_prefix_mix(product, oracle, stream, frontier):
     """700-node WAN, random metrics, overloads and the prefix mix, best-route
     selection on, through every large-topology SPF / RouteDb form."""
@@ -477,17 +435,15 @@ def test_route_stream_wan_prefix_mix(product, oracle, stream, frontier):
     _cmp(a, oracle.gen_route_dbs("wan", opts, srcs, True, False, True), "wanmix")
 
 
-@pytest.mark.parametrize("stream,chunks", [(2, 4), (3, 1), (3, 3), (3, 7), (4, 4)])
-def test_route_stream_three_word_sources(product, oracle, stream, chunks):
+@pytest.mark.parametrize("stream", [1, 2, 4])
+def test_route_stream_three_word_sources(product, oracle, stream):
     """FSW sources of 84 links (36 SSW + 48 RSW, the C3 shape on 4 pods x 2
-    planes) keep three next-hop words: the fused kernel and the pipelined
-    split (route_stream 3: SPF chunks on a side stream, each chunk's route
-    stream after its SPF) at several chunk counts, vs the oracle."""
+    planes) keep three next-hop words: the fused kernel, the HBM split and
+    the LDS-resident split, vs the oracle."""
     opts = dict(pods=4, planes=2, sswPerPlane=36, rswPerPod=48, full=True,
                 prefixesPerNode=3, nodeOverloadPermille=10, **MIX)
     srcs = [f"2-{p}-{f}" for p in range(4) for f in range(2)]
-    a = _batch_dbs(product, "fabric", opts, srcs, True, False, route_stream=stream,
-                   route_stream_chunks=chunks)
+    a = _batch_dbs(product, "fabric", opts, srcs, True, False, route_stream=stream)
     _cmp(a, oracle.gen_route_dbs("fabric", opts, srcs, True, False, False), "fsw3")
 
 

@@ -117,12 +117,12 @@ def test_route_updates_need_records(product):
         vr.fetch_updates(0)
 
 
-@pytest.mark.parametrize("ninfo,queue", [(0, 2), (0, 1), (-1, -1), (1, 1), (1, 3), (0, -1)])
-def test_queue_forms_node_info_option(product, oracle, ninfo, queue):
-    """The queue SPF forms (packed one-phase = the default and spf_queue 1,
-    packed with folded push stamps = 3, two-phase = 2) with node info in LDS (spf_ninfo 1) or read from the
-    CSR (0; -1 = whenever it raises units per CU): same variant RouteDbs and
-    diffs, and the same plain RouteDbs, as the oracle."""
+@pytest.mark.parametrize("ninfo", [0, -1, 1])
+def test_queue_forms_node_info_option(product, oracle, ninfo):
+    """The queue SPF (packed one-phase {dist, nh} words for one-word next-hop
+    sets, two phases otherwise) with node info in LDS (spf_ninfo 1) or read
+    from the CSR (0; -1 = whenever it raises units per CU): same variant
+    RouteDbs and diffs, and the same plain RouteDbs, as the oracle."""
     import openr_amd.capi as capi
     lib = capi.load()
     kind, opts = "wan", dict(nodes=400, seed=0xC5, prefixesPerNode=1, nodeOverloadPermille=20,
@@ -130,7 +130,6 @@ def test_queue_forms_node_info_option(product, oracle, ninfo, queue):
                              drainPermille=50)
     try:
         capi.check(lib, lib.ogs_set_option(b"spf_ninfo", ninfo), "spf_ninfo")
-        capi.check(lib, lib.ogs_set_option(b"spf_queue", queue), "spf_queue")
         vr = product.VariantRunner(True, True)
         vr.setup(kind, opts, "7", 32, 0xC4F, 500)
         vr.launch(0, True)
@@ -145,7 +144,6 @@ def test_queue_forms_node_info_option(product, oracle, ninfo, queue):
         assert got == oracle.gen_route_dbs(kind, opts, srcs, True, True, True)
     finally:
         lib.ogs_set_option(b"spf_ninfo", 1)
-        lib.ogs_set_option(b"spf_queue", -1)
 
 
 def test_route_updates_wide_source(product, oracle):

@@ -4,7 +4,7 @@ process, launches built once): the variants alternate pair by pair, each
 timed like bench.py's headline (HIP events over STEPS builds), digest checked
 against the golden c3 after the last pair. Usage:
   python tools/c3_opt_ab.py [--pairs 5] [--steps 20] [--as-rank r/N] \\
-      "frontier_o8=0" "frontier_o8=1" ...
+      "route_stream=2" "route_stream=4" ...
 Each variant is a comma-separated list of name=value (ogs_set_option);
 "lib=base" runs that variant through openr_amd/lib/libopenr_gpu_base.so
 (tools/build_ab_base.sh: kernels from another revision)."""
