@@ -307,9 +307,6 @@ int ogs_host_free(void* hptr);
  *                 in workgroups of 512+ threads. "spf_preload": 1 (default)
  *                 the packed relax reads its 8 targets' distances before
  *                 any compare-and-swap, 0 not (A/B).
- *                 "spf_lds_form": route_stream 4's LDS-resident SPF runs
- *                 three-pass rounds without compare-and-swap (0, default)
- *                 or the packed CAS / two-phase rounds (1, A/B).
  *   "frontier_block": threads per workgroup of the all-sources RouteDb
  *                 launches (fused frontier SPF + route stream, meta / metric
  *                 / mask outputs): 256, 512 or 1024; 0 (default) by the

@@ -21,7 +21,6 @@ extern int g_frontierBlock;
 extern int g_frontierParts;
 extern int g_frontierPartsWide;
 extern int g_spfLaneWalk;
-extern int g_spfLdsForm;
 extern int g_spfPreload;
 extern int g_spfPackedScan;
 extern int g_spfFrontier;
@@ -212,11 +211,6 @@ int ogs_set_option(const char* name, int64_t value) {
   if (std::strcmp(name, "frontier_parts") == 0) {
     if (value < 0 || value > 16) return fail(OGS_E_INVALID, "frontier_parts must be in [0, 16]");
     ogs::g_frontierParts = int(value);
-    return OGS_OK;
-  }
-  if (std::strcmp(name, "spf_lds_form") == 0) {
-    if (value != 0 && value != 1) return fail(OGS_E_INVALID, "spf_lds_form must be 0 or 1");
-    ogs::g_spfLdsForm = int(value);
     return OGS_OK;
   }
   if (std::strcmp(name, "spf_lane_walk") == 0) {

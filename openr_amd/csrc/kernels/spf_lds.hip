@@ -12,8 +12,9 @@
 // two units (N = 4 / 8 GPUs: 60+ us per SPF, phase stamps in DESIGN §3.3).
 // Here one 1024-thread workgroup per CU stages a compact image of the CSR
 // into LDS ONCE (2 B per edge: 15-bit neighbour | down bit; chunk -> node
-// table; row offsets; node flags: 124 KB for C3) and then solves its share
-// of the units back to back with every round served from LDS.
+// table with the node's drained bit; row offsets: 113 KB for C3) and then
+// solves its share of the units back to back with every round served from
+// LDS, each round visiting only the chunk records of its active nodes.
 //
 // Edge weights: when every up edge of the topology has the same weight (the
 // fabric's metric 1, or OGS_F_HOP_METRIC) that weight is a constant; other
@@ -27,6 +28,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <type_traits>
 
 #include "openr_gpu.h"
 #include "route_core.h"
@@ -38,50 +40,51 @@ namespace {
 
 constexpr uint32_t kDown16 = 0x8000u;     // eimg: edge down
 constexpr uint32_t kNodeMax = 0x7FFFu;    // 15-bit neighbour ids
+constexpr uint32_t kDrained16 = 0x8000u;  // cnode: the chunk's node is hard-drained
 constexpr uint32_t kLdsChunk = 8;         // edges per chunk (one lane's push)
 constexpr int kLdsBlock = 1024;
 
 __host__ __device__ inline uint32_t al16(uint32_t x) { return (x + 15u) & ~15u; }
 
-// internal launch flag: the CAS (W = 1) / two-phase (W > 1) rounds instead
-// of the three-pass rounds ("spf_lds_form" option 1, A/B)
-constexpr uint32_t kFlagLdsCasForm = 1u << 25;
+// chunk records of one topology: sum over nodes of ceil(deg / 8) <= (E + 7 N) / 8
+__host__ __device__ inline uint32_t chunk_cap(uint32_t N, uint32_t E) {
+  return (E + (kLdsChunk - 1u) * N) / kLdsChunk;
+}
 
 // Byte layout of one topology's image (global, then the same block in LDS):
 // header (16 B, global only) | eimg u16[E] | cnode u16[cap] | row u32[N+1] |
-// first u16[N] | flags u8[N], sections 16-B aligned, sized by the batch's
-// maxima so every topology (and the LDS copy) shares the offsets.
+// first u16[N], sections 16-B aligned, sized by the batch's maxima so every
+// topology (and the LDS copy) shares the offsets. Then, LDS only, one unit's
+// state: dist u32[N] | nh u32[N * W] | stamp u8[N] | queue u16[cap].
 struct LdsImage {
-  uint32_t eimg, cnode, row, first, flags, block;  // offsets in the block
-  uint32_t state;                                  // per-unit state bytes
-  uint32_t stride;                                 // header + block
+  uint32_t eimg, cnode, row, first, block;  // offsets in the block
+  uint32_t nh, stamp, queue, state;         // offsets in the state; state bytes
+  uint32_t stride;                          // header + block
 };
 
 __host__ LdsImage lds_image(const ogs_graph& g, int W) {
   const uint32_t N = uint32_t(g.max_nodes), E = uint32_t(g.max_edges);
-  const uint32_t cap = E / kLdsChunk + N;
+  const uint32_t cap = chunk_cap(N, E);
   LdsImage L{};
   L.eimg = 0;
   L.cnode = L.eimg + al16(2u * E);
   L.row = L.cnode + al16(2u * cap);
   L.first = L.row + al16(4u * (N + 1u));
-  L.flags = L.first + al16(2u * N);
-  L.block = L.flags + al16(N);
-  // the larger of the forms' states: three-pass {dist, prev, nh[W], u8
-  // stamps}; W == 1 packed {dist | nh} words + u8 stamps; W > 1 two-phase
-  // {dist, nh[W], u16 stamps}
-  L.state = std::max(al16(4u * N) * 2u + al16(4u * N * uint32_t(W)) + al16(N),
-                     W == 1 ? al16(8u * N) + al16(N)
-                            : al16(4u * N) + al16(4u * N * uint32_t(W)) + al16(2u * N));
+  L.block = L.first + al16(2u * N);
+  L.nh = al16(4u * N);
+  L.stamp = L.nh + al16(4u * N * uint32_t(W));
+  L.queue = L.stamp + al16(N);
+  L.state = L.queue + al16(2u * cap);
   L.stride = 16u + L.block;
   return L;
 }
 
 // Image build, once per call: lds_scan_kernel (one workgroup per topology:
-// row offsets, node flags, chunk -> node table; header {chunks, weight min,
-// weight max, 0}) then lds_edges_kernel (many workgroups: the 2-B edge words
-// and the min / max weight of the up edges). Header of topology t at
-// img + t * L.stride; the weights are uniform iff min == max.
+// row offsets, chunk -> node table with the node's drained bit; header
+// {chunks, weight min, weight max, 0}) then lds_edges_kernel (many
+// workgroups: the 2-B edge words and the min / max weight of the up edges).
+// Header of topology t at img + t * L.stride; the weights are uniform iff
+// min == max.
 __global__ __launch_bounds__(kLdsBlock) void lds_scan_kernel(ogs_graph g, LdsImage L,
                                                             uint8_t* __restrict__ img) {
   constexpr uint32_t B = kLdsBlock;
@@ -97,10 +100,8 @@ __global__ __launch_bounds__(kLdsBlock) void lds_scan_kernel(ogs_graph g, LdsIma
   uint16_t* __restrict__ cnode = reinterpret_cast<uint16_t*>(blk + L.cnode);
   uint32_t* __restrict__ row = reinterpret_cast<uint32_t*>(blk + L.row);
   uint16_t* __restrict__ first = reinterpret_cast<uint16_t*>(blk + L.first);
-  uint8_t* __restrict__ fl = blk + L.flags;
   if (tid == 0) base = 0u;
   for (uint32_t v = tid; v <= N; v += B) row[v] = gRow[v] - e0;
-  for (uint32_t v = tid; v < N; v += B) fl[v] = g.node_flags[nb + v];
   __syncthreads();
   // chunk ids: exclusive scan of ceil(deg / 8) over the nodes, tile by tile
   const int lane = int(tid & 63u), wave = int(tid >> 6);
@@ -121,8 +122,11 @@ __global__ __launch_bounds__(kLdsBlock) void lds_scan_kernel(ogs_graph g, LdsIma
     __syncthreads();
     if (tid == B - 1u) base = off + inc;
     const uint32_t at = off + inc - n;
-    if (v < N) first[v] = uint16_t(at);
-    for (uint32_t k = 0; k < n; ++k) cnode[at + k] = uint16_t(v);
+    if (v < N) {
+      first[v] = uint16_t(at);
+      const uint32_t tag = (g.node_flags[nb + v] & OGS_NODE_OVERLOADED) ? kDrained16 : 0u;
+      for (uint32_t k = 0; k < n; ++k) cnode[at + k] = uint16_t(v | tag);
+    }
     __syncthreads();
   }
   if (tid == 0) {
@@ -178,18 +182,26 @@ __global__ __launch_bounds__(kBlock) void lds_edges_kernel(ogs_graph g, LdsImage
 }
 
 #ifdef OGS_STAMPS
-// diagnostic build: per workgroup {staging, first unit's SPF, rounds, the
-// first unit's round 2..9 cycles, units, kernel cycles, 0...} (16 words),
-// rows (W - 1) * 4096 + blockIdx.x; read with ogs_diag_lds_stamps
+// diagnostic build: per workgroup 32 words {staging, first unit's SPF
+// (incl. staging), rounds, units, kernel cycles, first unit's queue total,
+// 0, 0, then rounds 2..9 of the first unit x (queue, distances, next hops)
+// cycles}, rows (W - 1) * 4096 + blockIdx.x; read with ogs_diag_lds_stamps
 constexpr uint32_t kLdsDiagWgs = 4096;
-__device__ uint32_t g_ldsStamps[4 * kLdsDiagWgs * 16];
+__device__ uint32_t g_ldsStamps[4 * kLdsDiagWgs * 32];
 #endif
 
-// SPF of the workgroup's units over the LDS image. W == 1: packed
-// {dist, next-hop word} per node, one phase (every push a 64-bit LDS
-// compare-and-swap: a shorter candidate replaces, an equal one ORs its
-// bits in). W > 1: a distance phase (atomicMin), then a next-hop phase
-// (atomicOr along tight edges), as frontier_spf.
+// SPF of the workgroup's units over the LDS image. Every round r:
+//  (0) queue: the chunk records whose node is stamped r and relaxes (one
+//      pass over the chunk table, a wave-aggregated append);
+//  (1) distances: atomicMin of each queued chunk's candidates; a push that
+//      lowers its target stamps it r + 1 and clears its next hops;
+//  (2) next hops: atomicOr of each still-current queued node's next-hop
+//      words along the edges that are tight NOW; a target whose words grew
+//      is stamped r + 1.
+// A push from a longer stale distance ORs nothing (not tight); a node whose
+// distance later falls drops what it had. The least fixpoint of spf_core.h
+// with fire-and-forget LDS atomics, and every chunk record is visited only
+// in the rounds its node is active (each once, on unit-weight BFS layers).
 template <int W>
 __global__ __launch_bounds__(kLdsBlock) void spf_lds_kernel(
     ogs_graph g, LdsImage L, const uint8_t* __restrict__ img,
@@ -197,44 +209,38 @@ __global__ __launch_bounds__(kLdsBlock) void spf_lds_kernel(
     uint32_t* __restrict__ oDist, uint32_t* __restrict__ oNh) {
   constexpr uint32_t kInf = 0xFFFFFFFFu;
   constexpr uint32_t B = kLdsBlock;
-  const uint32_t tid = threadIdx.x;
+  const uint32_t tid = threadIdx.x, lane = tid & 63u;
   const uint32_t Sn = uint32_t(g.max_nodes);
   const bool hop = (flags & OGS_F_HOP_METRIC) != 0u;
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  __shared__ uint32_t qCount[2];
   char* blk = smem;
   const uint16_t* eimg = reinterpret_cast<const uint16_t*>(blk + L.eimg);
   const uint16_t* cnode = reinterpret_cast<const uint16_t*>(blk + L.cnode);
   const uint32_t* row = reinterpret_cast<const uint32_t*>(blk + L.row);
   const uint16_t* first = reinterpret_cast<const uint16_t*>(blk + L.first);
-  const uint8_t* nfl = reinterpret_cast<const uint8_t*>(blk + L.flags);
   char* st = blk + L.block;
-  // three-pass form (default)
-  uint32_t* prev = reinterpret_cast<uint32_t*>(st + al16(4u * Sn));
-  uint32_t* nh3 = reinterpret_cast<uint32_t*>(st + 2u * al16(4u * Sn));
-  uint8_t* stamp3 = reinterpret_cast<uint8_t*>(st + 2u * al16(4u * Sn) + al16(4u * Sn * W));
-  const bool threePass = (flags & kFlagLdsCasForm) == 0u;
-  // W == 1 packed form
-  uint64_t* dn = reinterpret_cast<uint64_t*>(st);
-  uint8_t* stamp8 = reinterpret_cast<uint8_t*>(st + al16(8u * Sn));
-  // W > 1
   uint32_t* dist = reinterpret_cast<uint32_t*>(st);
-  uint32_t* nh = reinterpret_cast<uint32_t*>(st + al16(4u * Sn));
-  uint16_t* stamp16 = reinterpret_cast<uint16_t*>(st + al16(4u * Sn) + al16(4u * Sn * W));
+  uint32_t* nh = reinterpret_cast<uint32_t*>(st + L.nh);
+  uint8_t* stamp = reinterpret_cast<uint8_t*>(st + L.stamp);
+  uint16_t* queue = reinterpret_cast<uint16_t*>(st + L.queue);
 
   uint32_t staged = 0xFFFFFFFFu;
   uint32_t C = 0, uniform = 0, w0 = 0, N = 0, e0 = 0;
 #ifdef OGS_STAMPS
-  uint32_t diag[16] = {};
+  uint32_t* diag = g_ldsStamps + (size_t(W - 1) * kLdsDiagWgs + blockIdx.x) * 32u;
+  const bool diagOn = tid == 0u && blockIdx.x < kLdsDiagWgs;
   const uint64_t k0 = __builtin_amdgcn_s_memtime();
   uint64_t tr = k0;
   bool firstUnit = true;
-  auto mark = [&](int slot) {  // cycles since the last mark of the first unit
+  uint32_t nUnitsDone = 0;
+  auto mark = [&](uint32_t slot) {  // cycles since the last mark of the first unit
     const uint64_t now = __builtin_amdgcn_s_memtime();
-    if (firstUnit && slot < 16) diag[slot] = uint32_t(now - tr);
+    if (diagOn && firstUnit && slot < 32u) diag[slot] = uint32_t(now - tr);
     tr = now;
   };
 #else
-  auto mark = [](int) {};
+  auto mark = [](uint32_t) {};
 #endif
   for (int u = int(blockIdx.x); u < nUnits; u += int(gridDim.x)) {
     const ogs_unit unit = units[u];
@@ -256,397 +262,260 @@ __global__ __launch_bounds__(kLdsBlock) void spf_lds_kernel(
     }
     mark(0);  // staging (the first unit only)
     const uint64_t* __restrict__ edges = g.edges + e0;
+    const uint32_t wc = hop ? 1u : w0;  // the weight when it is one constant
+    const bool constW = hop || uniform;
     auto weight = [&](uint32_t e) -> uint32_t {
-      return hop ? 1u : uniform ? w0 : static_cast<uint32_t>(edges[e] >> 32);
+      return constW ? wc : static_cast<uint32_t>(edges[e] >> 32);
     };
     const uint32_t s = unit.src;
     const uint32_t sb = row[s], se = row[s + 1];
-    if (threePass) {
-      // One phase without compare-and-swap: every round is (1) atomicMin of
-      // the active nodes' candidates into dist, (2) a node pass -- a node
-      // whose distance fell drops its next hops and is stamped for the next
-      // round --, (3) atomicOr of the active nodes' next hops along the edges
-      // that are tight NOW. A push from a longer stale distance ORs nothing
-      // (not tight), a node whose bits grew is stamped too: the least
-      // fixpoint of spf_core.h, in the rounds of the packed form, with
-      // fire-and-forget LDS atomics instead of contended CAS loops.
-      for (uint32_t v = tid; v < N; v += B) {
-        dist[v] = (v == s) ? 0u : kInf;
-        prev[v] = dist[v];
-        stamp3[v] = 0;
+    for (uint32_t v = tid; v < N; v += B) {
+      dist[v] = (v == s) ? 0u : kInf;
+      stamp[v] = 0;
 #pragma unroll
-        for (int w = 0; w < W; ++w) nh3[v * W + w] = 0u;
-      }
-      __syncthreads();
-      auto nodePass = [&](uint32_t r, bool& changed) {
-        for (uint32_t v = tid; v < N; v += B) {
-          const uint32_t d = dist[v];
-          if (d < prev[v]) {
-            prev[v] = d;
-#pragma unroll
-            for (int w = 0; w < W; ++w) nh3[v * W + w] = 0u;
-            stamp3[v] = uint8_t(r + 1u);
-            changed = true;
-          }
+      for (int w = 0; w < W; ++w) nh[v * W + w] = 0u;
+    }
+    if (tid < 2u) qCount[tid] = 0u;
+    __syncthreads();
+    // round 1: the source's row (slot j = j-th edge of the row; the source
+    // relaxes even when drained, LinkState.cpp:741-752)
+    for (uint32_t j = tid; j < se - sb; j += B) {
+      const uint32_t x = eimg[sb + j];
+      if (x & kDown16) continue;
+      atomicMin(&dist[x & kNodeMax], weight(sb + j));
+    }
+    __syncthreads();
+    for (uint32_t j = tid; j < se - sb && j < 32u * W; j += B) {
+      const uint32_t x = eimg[sb + j];
+      if (x & kDown16) continue;
+      const uint32_t t = x & kNodeMax;
+      if (weight(sb + j) != dist[t]) continue;
+      atomicOr(&nh[t * W + (j >> 5)], 1u << (j & 31u));
+      stamp[t] = 2;
+    }
+    __syncthreads();
+#ifdef OGS_STAMPS
+    uint32_t queued = 0;
+#endif
+    // rounds 2.., specialised on whether the weight is one constant (no
+    // per-edge weight reads at all) or read per edge from the CSR
+    auto rounds = [&](auto constant, auto layered) {
+      constexpr bool kConst = decltype(constant)::value;
+      constexpr bool kBfs = decltype(layered)::value;
+      auto wt = [&](uint32_t e) -> uint32_t {
+        if constexpr (kConst) {
+          return wc;
+        } else {
+          return static_cast<uint32_t>(edges[e] >> 32);
         }
       };
-      // round 1: the source's row (slot j = j-th edge of the row)
-      {
-        bool changed = false;
-        for (uint32_t j = tid; j < se - sb; j += B) {
-          const uint32_t x = eimg[sb + j];
-          if (x & kDown16) continue;
-          atomicMin(&dist[x & kNodeMax], weight(sb + j));
+      // one queued chunk: its node, edge words, targets' distances and the
+      // candidates, every LDS / weight read issued before any push
+      struct Chunk {
+        uint32_t v, dv;
+        uint32_t x[kLdsChunk], dt[kLdsChunk], cand[kLdsChunk];
+      };
+      auto load = [&](uint32_t q, Chunk& k) {
+        const uint32_t c = queue[q];
+        k.v = cnode[c] & kNodeMax;
+        k.dv = dist[k.v];
+        const uint32_t b = row[k.v] + kLdsChunk * (c - first[k.v]);
+        const uint32_t n = min(kLdsChunk, row[k.v + 1] - b);
+        // the words past the row are read too (inside LDS; branch-free) and
+        // masked down
+#pragma unroll
+        for (uint32_t i = 0; i < kLdsChunk; ++i) k.x[i] = eimg[b + i];
+#pragma unroll
+        for (uint32_t i = 0; i < kLdsChunk; ++i) k.x[i] = i < n ? k.x[i] : kDown16;
+#pragma unroll
+        for (uint32_t i = 0; i < kLdsChunk; ++i) {
+          k.dt[i] = dist[k.x[i] & kNodeMax];
+          k.cand[i] = k.dv + ((k.x[i] & kDown16) ? 0u : wt(b + i));
         }
-        __syncthreads();
-        nodePass(1u, changed);
-        __syncthreads();
-        for (uint32_t j = tid; j < se - sb && j < 32u * W; j += B) {
-          const uint32_t x = eimg[sb + j];
-          if (x & kDown16) continue;
-          const uint32_t t = x & kNodeMax;
-          if (weight(sb + j) != dist[t]) continue;
-          atomicOr(&nh3[t * W + (j >> 5)], 1u << (j & 31u));
-          stamp3[t] = 2;
-        }
-        __syncthreads();
-      }
-      // the thread's chunk slots whose node is stamped for round r and
-      // relaxes (LinkState.cpp:741-752: not a hard-drained node other than
-      // the source; the source itself is never stamped again)
-      auto scan = [&](uint32_t r, auto&& fn) {
-        for (uint32_t c0 = tid; c0 < C; c0 += 4u * B) {
+      };
+      for (uint32_t r = 2;; ++r) {
+        // (0) the queue of round r: four chunk slots per thread per step, the
+        // workgroup stepping together (every lane takes part in the ballots)
+        uint32_t* qc = &qCount[r & 1u];
+        for (uint32_t c0 = 0; c0 < C; c0 += 4u * B) {
           uint32_t cs[4], vs[4];
           bool act[4];
 #pragma unroll
           for (int k = 0; k < 4; ++k) {
-            cs[k] = c0 + uint32_t(k) * B;
-            vs[k] = cs[k] < C ? cnode[cs[k]] : 0u;
+            cs[k] = c0 + uint32_t(k) * B + tid;
+            vs[k] = cs[k] < C ? cnode[cs[k]] : kDrained16;
           }
 #pragma unroll
           for (int k = 0; k < 4; ++k) {
-            act[k] = cs[k] < C && stamp3[vs[k]] == uint8_t(r) &&
-                !(nfl[vs[k]] & OGS_NODE_OVERLOADED);
+            if constexpr (kBfs) {  // layer r - 1
+              act[k] = !(vs[k] & kDrained16) &&
+                  uint64_t(dist[vs[k] & kNodeMax]) == uint64_t(r - 1u) * wc;
+            } else {
+              act[k] = !(vs[k] & kDrained16) && stamp[vs[k]] == uint8_t(r);
+            }
           }
+          uint64_t m[4];
+          uint32_t tot = 0;
 #pragma unroll
           for (int k = 0; k < 4; ++k) {
-            if (act[k]) fn(cs[k], vs[k]);
+            m[k] = __ballot(act[k]);
+            tot += uint32_t(__popcll(m[k]));
+          }
+          if (tot == 0u) continue;  // wave-uniform
+          uint32_t at = 0;
+          if (lane == 0u) at = atomicAdd(qc, tot);
+          at = __shfl(at, 0, 64);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const uint32_t lo = static_cast<uint32_t>(m[k]), hi = static_cast<uint32_t>(m[k] >> 32);
+            const uint32_t before = __builtin_amdgcn_mbcnt_hi(hi, __builtin_amdgcn_mbcnt_lo(lo, 0u));
+            if (act[k]) queue[at + before] = uint16_t(cs[k]);
+            at += uint32_t(__popcll(m[k]));
           }
         }
-      };
-      auto edges8 = [&](uint32_t c, uint32_t v, uint32_t (&x)[kLdsChunk],
-                        uint32_t (&dt)[kLdsChunk]) {
-        const uint32_t b = row[v] + kLdsChunk * (c - first[v]);
-        const uint32_t n = min(kLdsChunk, row[v + 1] - b);
+        __syncthreads();
+        mark(8u + 3u * (r - 2u));
+        const uint32_t nq = *qc;
+        if (nq == 0u) break;  // nothing stamped r: the fixpoint
+#ifdef OGS_STAMPS
+        queued += nq;
+#endif
+        if (tid == 0u) qCount[(r + 1u) & 1u] = 0u;  // next round's counter
+        // the queue is walked transposed: lane l of a wave takes entries
+        // l * M + j (M = ceil(nq / 64)), so the lanes of one instruction
+        // hold chunks of nodes far apart in the queue (other pods / planes)
+        // instead of neighbours pushing into the same targets -- same-address
+        // LDS atomics within one instruction serialise
+        const uint32_t M = (nq + 63u) >> 6;
+        auto entry = [&](uint32_t i) { return (i & 63u) * M + (i >> 6); };
+        if constexpr (kBfs) {
+          // one constant weight wc > 0: the rounds are BFS layers. The nodes
+          // queued in round r are layer r - 1, final with complete next hops;
+          // a target is either unreached (dt = kInf: it joins layer r, every
+          // lane that finds it so stores the same distance) or already at
+          // cand (layer r, tight) or nearer (not tight). One pass: distances
+          // by plain stores, next hops by fire-and-forget atomicOr; layer
+          // membership is the distance itself (no stamps).
+          for (uint32_t i = tid; i < 64u * M; i += B) {
+            const uint32_t q = entry(i);
+            if (q >= nq) continue;
+            Chunk k;
+            load(q, k);
+            uint32_t nv[W];
 #pragma unroll
-        for (uint32_t i = 0; i < kLdsChunk; ++i) x[i] = i < n ? eimg[b + i] : kDown16;
+            for (int w = 0; w < W; ++w) nv[w] = nh[k.v * W + w];
 #pragma unroll
-        for (uint32_t i = 0; i < kLdsChunk; ++i) dt[i] = dist[x[i] & kNodeMax];
-        return b;
-      };
-      for (uint32_t r = 2;; ++r) {
-        bool changed = false;
-        scan(r, [&](uint32_t c, uint32_t v) {  // (1) distances
-          const uint32_t dv = dist[v];
-          uint32_t x[kLdsChunk], dt[kLdsChunk];
-          const uint32_t b = edges8(c, v, x, dt);
+            for (uint32_t e = 0; e < kLdsChunk; ++e) {
+              if ((k.x[e] & kDown16) || (k.dt[e] != kInf && k.dt[e] != k.cand[e])) continue;
+              const uint32_t t = k.x[e] & kNodeMax;
+              if (k.dt[e] == kInf) dist[t] = k.cand[e];
+#pragma unroll
+              for (int w = 0; w < W; ++w) {
+                if (nv[w]) atomicOr(&nh[t * W + w], nv[w]);
+              }
+            }
+          }
+          __syncthreads();
+          mark(8u + 3u * (r - 2u) + 2u);
+#ifdef OGS_STAMPS
+          if (diagOn && firstUnit) diag[2] = r;
+#endif
+          continue;
+        }
+        // (1) distances. A push with cand < dt (dt read during this pass;
+        // distances only fall) lowers its target whatever else lands there,
+        // so it restarts the target's next hops without the atomic's return
+        // value: every LDS operation here is fire-and-forget
+        for (uint32_t i = tid; i < 64u * M; i += B) {
+          const uint32_t q = entry(i);
+          if (q >= nq) continue;
+          Chunk k;
+          load(q, k);
 #pragma unroll
           for (uint32_t i = 0; i < kLdsChunk; ++i) {
-            if (x[i] & kDown16) continue;
-            const uint32_t cand = dv + weight(b + i);
-            if (cand < dt[i]) atomicMin(&dist[x[i] & kNodeMax], cand);
+            if ((k.x[i] & kDown16) || k.cand[i] >= k.dt[i]) continue;
+            const uint32_t t = k.x[i] & kNodeMax;
+            atomicMin(&dist[t], k.cand[i]);
+            stamp[t] = uint8_t(r + 1u);
+#pragma unroll
+            for (int w = 0; w < W; ++w) nh[t * W + w] = 0u;
           }
-        });
+        }
         __syncthreads();
-        nodePass(r, changed);  // (2)
-        __syncthreads();
-        scan(r, [&](uint32_t c, uint32_t v) {  // (3) next hops along tight edges
-          const uint32_t dv = dist[v];
+        mark(8u + 3u * (r - 2u) + 1u);
+        // (2) next hops along tight edges, from the queued nodes still at the
+        // distance they were queued with: the targets' words read first, then
+        // fire-and-forget atomicOr of the missing bits
+        for (uint32_t i = tid; i < 64u * M; i += B) {
+          const uint32_t q = entry(i);
+          if (q >= nq) continue;
+          Chunk k;
+          load(q, k);
+          if (stamp[k.v] != uint8_t(r)) continue;
           uint32_t nv[W];
 #pragma unroll
-          for (int w = 0; w < W; ++w) nv[w] = nh3[v * W + w];
-          uint32_t x[kLdsChunk], dt[kLdsChunk];
-          const uint32_t b = edges8(c, v, x, dt);
+          for (int w = 0; w < W; ++w) nv[w] = nh[k.v * W + w];
+          bool tight[kLdsChunk];
+          uint32_t have[kLdsChunk][W];
 #pragma unroll
           for (uint32_t i = 0; i < kLdsChunk; ++i) {
-            if ((x[i] & kDown16) || dv + weight(b + i) != dt[i]) continue;
-            const uint32_t t = x[i] & kNodeMax;
+            tight[i] = !(k.x[i] & kDown16) && k.cand[i] == k.dt[i];
+#pragma unroll
+            for (int w = 0; w < W; ++w) {
+              have[i][w] = nh[(k.x[i] & kNodeMax) * W + w];
+              have[i][w] = tight[i] ? have[i][w] : ~0u;
+            }
+          }
+#pragma unroll
+          for (uint32_t i = 0; i < kLdsChunk; ++i) {
+            const uint32_t t = k.x[i] & kNodeMax;
             bool add = false;
 #pragma unroll
-            for (int k = 0; k < W; ++k) {
-              const uint32_t a = nv[k] & ~nh3[t * W + k];
+            for (int w = 0; w < W; ++w) {
+              const uint32_t a = nv[w] & ~have[i][w];
               if (a) {
-                atomicOr(&nh3[t * W + k], a);
+                atomicOr(&nh[t * W + w], a);
                 add = true;
               }
             }
-            if (add) {
-              stamp3[t] = uint8_t(r + 1u);
-              changed = true;
-            }
+            if (add) stamp[t] = uint8_t(r + 1u);
           }
-        });
-        const bool more = __syncthreads_or(changed) != 0;
-        mark(int(r) + 1);
-#ifdef OGS_STAMPS
-        if (firstUnit) diag[2] = r;
-#endif
-        if (!more) break;
-      }
-      for (uint32_t v = tid; v < N; v += B) {
-        oDist[size_t(u) * Sn + v] = dist[v];
-#pragma unroll
-        for (int w = 0; w < W; ++w) oNh[(size_t(u) * W + w) * Sn + v] = nh3[v * W + w];
-      }
-    } else if constexpr (W == 1) {
-      for (uint32_t v = tid; v < N; v += B) {
-        dn[v] = (v == s) ? 0ull : uint64_t(kInf);
-        stamp8[v] = (v == s) ? 1 : 0;
-      }
-      __syncthreads();
-      // one push of edge e (local id) from v {dv, bits} in round r
-      auto push = [&](uint32_t e, uint32_t dv, uint32_t bits, uint32_t r,
-                      bool& changed) {
-        const uint32_t x = eimg[e];
-        if (x & kDown16) return;
-        const uint32_t t = x & kNodeMax;
-        const uint32_t c = dv + weight(e);
-        uint64_t old = dn[t];
-        for (;;) {
-          const uint32_t dt = static_cast<uint32_t>(old), nt = static_cast<uint32_t>(old >> 32);
-          if (c > dt || (c == dt && !(bits & ~nt))) return;
-          const uint64_t nw = c < dt ? (uint64_t(c) | (uint64_t(bits) << 32))
-                                     : (uint64_t(dt) | (uint64_t(nt | bits) << 32));
-          const uint64_t seen = atomicCAS(reinterpret_cast<unsigned long long*>(&dn[t]),
-                                          static_cast<unsigned long long>(old),
-                                          static_cast<unsigned long long>(nw));
-          if (seen == old) {
-            stamp8[t] = uint8_t(r + 1u);
-            changed = true;
-            return;
-          }
-          old = seen;
-        }
-      };
-      // round 1: the source's row, one edge per thread (slot j = j-th edge)
-      {
-        bool changed = false;
-        for (uint32_t j = tid; j < se - sb; j += B) {
-          push(sb + j, 0u, j < 32u ? 1u << j : 0u, 1u, changed);
         }
         __syncthreads();
-      }
-      const uint32_t* dn32 = reinterpret_cast<const uint32_t*>(dn);  // dist = low word
-      for (uint32_t r = 2;; ++r) {
-        bool changed = false;
-        // one chunk of v: its 8 edge words and their targets' distances read
-        // first (independent LDS reads), then a compare-and-swap only where
-        // the push can change the target (distances only fall, so a stale
-        // preload never drops a useful push)
-        auto chunk = [&](uint32_t c, uint32_t v) {
-          const uint64_t xv = dn[v];
-          const uint32_t dv = static_cast<uint32_t>(xv), nv = static_cast<uint32_t>(xv >> 32);
-          const uint32_t b = row[v] + kLdsChunk * (c - first[v]);
-          const uint32_t n = min(kLdsChunk, row[v + 1] - b);
-          uint32_t x[kLdsChunk], dt[kLdsChunk];
-#pragma unroll
-          for (uint32_t i = 0; i < kLdsChunk; ++i) x[i] = i < n ? eimg[b + i] : kDown16;
-#pragma unroll
-          for (uint32_t i = 0; i < kLdsChunk; ++i) dt[i] = dn32[2u * (x[i] & kNodeMax)];
-#pragma unroll
-          for (uint32_t i = 0; i < kLdsChunk; ++i) {
-            if (x[i] & kDown16) continue;
-            const uint32_t cand = dv + weight(b + i);
-            if (cand > dt[i]) continue;
-            // the source contributes its link slot, others NH(v) (LinkState.cpp:808-811)
-            const uint32_t slot = b + i - sb;
-            const uint32_t bits = v == s ? (slot < 32u ? 1u << slot : 0u) : nv;
-            const uint32_t t = x[i] & kNodeMax;
-            uint64_t old = dn[t];
-            for (;;) {
-              const uint32_t d0 = static_cast<uint32_t>(old), n0 = static_cast<uint32_t>(old >> 32);
-              if (cand > d0 || (cand == d0 && !(bits & ~n0))) break;
-              const uint64_t nw = cand < d0 ? (uint64_t(cand) | (uint64_t(bits) << 32))
-                                            : (uint64_t(d0) | (uint64_t(n0 | bits) << 32));
-              const uint64_t seen = atomicCAS(reinterpret_cast<unsigned long long*>(&dn[t]),
-                                              static_cast<unsigned long long>(old),
-                                              static_cast<unsigned long long>(nw));
-              if (seen == old) {
-                stamp8[t] = uint8_t(r + 1u);
-                changed = true;
-                break;
-              }
-              old = seen;
-            }
-          }
-        };
-        // four chunk slots per step: nodes and stamps read before any push
-        for (uint32_t c0 = tid; c0 < C; c0 += 4u * B) {
-          uint32_t cs[4], vs[4];
-          bool act[4];
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            cs[k] = c0 + uint32_t(k) * B;
-            vs[k] = cs[k] < C ? cnode[cs[k]] : 0u;
-          }
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            // LinkState.cpp:741-752: a hard-drained node other than the source does not relax
-            act[k] = cs[k] < C && stamp8[vs[k]] == uint8_t(r) &&
-                (!(nfl[vs[k]] & OGS_NODE_OVERLOADED) || vs[k] == s);
-          }
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            if (act[k]) chunk(cs[k], vs[k]);
-          }
-        }
-        const bool more = __syncthreads_or(changed) != 0;
-        mark(int(r) + 1);  // round r: slots 3..
+        mark(8u + 3u * (r - 2u) + 2u);
 #ifdef OGS_STAMPS
-        if (firstUnit) diag[2] = r;
+        if (diagOn && firstUnit) diag[2] = r;
 #endif
-        if (!more) break;
       }
-      for (uint32_t v = tid; v < N; v += B) {
-        const uint64_t x = dn[v];
-        oDist[size_t(u) * Sn + v] = static_cast<uint32_t>(x);
-        oNh[size_t(u) * Sn + v] = static_cast<uint32_t>(x >> 32);
-      }
+    };
+    if (constW && wc > 0u) {
+      rounds(std::true_type{}, std::true_type{});
+    } else if (constW) {
+      rounds(std::true_type{}, std::false_type{});
     } else {
-      for (uint32_t v = tid; v < N; v += B) {
-        dist[v] = (v == s) ? 0u : kInf;
-        stamp16[v] = (v == s) ? 1 : 0;
+      rounds(std::false_type{}, std::false_type{});
+    }
+#ifdef OGS_STAMPS
+    if (diagOn && firstUnit) diag[5] = queued;
+#endif
+    for (uint32_t v = tid; v < N; v += B) {
+      oDist[size_t(u) * Sn + v] = dist[v];
 #pragma unroll
-        for (int w = 0; w < W; ++w) nh[v * W + w] = 0u;
-      }
-      __syncthreads();
-      // ---- distances ----
-      for (uint32_t j = tid; j < se - sb; j += B) {
-        const uint32_t x = eimg[sb + j];
-        if (x & kDown16) continue;
-        const uint32_t t = x & kNodeMax, c = weight(sb + j);
-        if (c < dist[t]) {
-          atomicMin(&dist[t], c);
-          stamp16[t] = 2;
-        }
-      }
-      __syncthreads();
-      // the chunk slots of this thread whose node is stamped for round r and
-      // relaxes (a hard-drained node other than the source does not,
-      // LinkState.cpp:741-752; the next-hop phase skips the source too)
-      auto scan = [&](uint32_t r, bool skipSource, auto&& fn) {
-        for (uint32_t c0 = tid; c0 < C; c0 += 4u * B) {
-          uint32_t cs[4], vs[4];
-          bool act[4];
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            cs[k] = c0 + uint32_t(k) * B;
-            vs[k] = cs[k] < C ? cnode[cs[k]] : 0u;
-          }
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const bool drained = (nfl[vs[k]] & OGS_NODE_OVERLOADED) != 0;
-            act[k] = cs[k] < C && stamp16[vs[k]] == uint16_t(r) &&
-                (skipSource ? (vs[k] != s && !drained) : (!drained || vs[k] == s));
-          }
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            if (act[k]) fn(cs[k], vs[k]);
-          }
-        }
-      };
-      auto edges8 = [&](uint32_t c, uint32_t v, uint32_t (&x)[kLdsChunk], uint32_t (&dt)[kLdsChunk]) {
-        const uint32_t b = row[v] + kLdsChunk * (c - first[v]);
-        const uint32_t n = min(kLdsChunk, row[v + 1] - b);
-#pragma unroll
-        for (uint32_t i = 0; i < kLdsChunk; ++i) x[i] = i < n ? eimg[b + i] : kDown16;
-#pragma unroll
-        for (uint32_t i = 0; i < kLdsChunk; ++i) dt[i] = dist[x[i] & kNodeMax];
-        return b;
-      };
-      uint32_t r = 2;
-      for (;; ++r) {
-        bool changed = false;
-        scan(r, false, [&](uint32_t c, uint32_t v) {
-          const uint32_t dv = dist[v];
-          uint32_t x[kLdsChunk], dt[kLdsChunk];
-          const uint32_t b = edges8(c, v, x, dt);
-#pragma unroll
-          for (uint32_t i = 0; i < kLdsChunk; ++i) {
-            if (x[i] & kDown16) continue;
-            const uint32_t cand = dv + weight(b + i);
-            if (cand < dt[i]) {
-              atomicMin(&dist[x[i] & kNodeMax], cand);
-              stamp16[x[i] & kNodeMax] = uint16_t(r + 1u);
-              changed = true;
-            }
-          }
-        });
-        if (!__syncthreads_or(changed)) break;
-      }
-      // ---- next hops: seeds from the source's row, then tight pushes ----
-      const uint32_t r0 = r + 1u;
-      for (uint32_t j = tid; j < se - sb && j < 32u * W; j += B) {
-        const uint32_t x = eimg[sb + j];
-        if (x & kDown16) continue;
-        const uint32_t t = x & kNodeMax;
-        if (weight(sb + j) == dist[t]) {
-          atomicOr(&nh[t * W + (j >> 5)], 1u << (j & 31u));
-          stamp16[t] = uint16_t(r0);
-        }
-      }
-      __syncthreads();
-      for (r = r0;; ++r) {
-        bool changed = false;
-        scan(r, true, [&](uint32_t c, uint32_t v) {
-          const uint32_t dv = dist[v];
-          uint32_t nv[W];
-#pragma unroll
-          for (int w = 0; w < W; ++w) nv[w] = nh[v * W + w];
-          uint32_t x[kLdsChunk], dt[kLdsChunk];
-          const uint32_t b = edges8(c, v, x, dt);
-#pragma unroll
-          for (uint32_t i = 0; i < kLdsChunk; ++i) {
-            if (x[i] & kDown16) continue;
-            const uint32_t t = x[i] & kNodeMax;
-            if (dv + weight(b + i) != dt[i]) continue;  // not tight
-            bool add = false;
-#pragma unroll
-            for (int k = 0; k < W; ++k) {
-              const uint32_t a = nv[k] & ~nh[t * W + k];
-              if (a) {
-                atomicOr(&nh[t * W + k], a);
-                add = true;
-              }
-            }
-            if (add) {
-              stamp16[t] = uint16_t(r + 1u);
-              changed = true;
-            }
-          }
-        });
-        if (!__syncthreads_or(changed)) break;
-      }
-      for (uint32_t v = tid; v < N; v += B) {
-        oDist[size_t(u) * Sn + v] = dist[v];
-#pragma unroll
-        for (int w = 0; w < W; ++w) oNh[(size_t(u) * W + w) * Sn + v] = nh[v * W + w];
-      }
+      for (int w = 0; w < W; ++w) oNh[(size_t(u) * W + w) * Sn + v] = nh[v * W + w];
     }
     __syncthreads();  // state and outputs of this unit done before the next
 #ifdef OGS_STAMPS
     if (firstUnit) {
-      diag[1] = uint32_t(__builtin_amdgcn_s_memtime() - k0);  // staging + first unit
+      if (diagOn) diag[1] = uint32_t(__builtin_amdgcn_s_memtime() - k0);  // staging + first unit
       firstUnit = false;
     }
-    ++diag[11];
+    ++nUnitsDone;
 #endif
   }
 #ifdef OGS_STAMPS
-  diag[12] = uint32_t(__builtin_amdgcn_s_memtime() - k0);
-  if (threadIdx.x == 0 && blockIdx.x < kLdsDiagWgs) {
-    uint32_t* o = g_ldsStamps + (size_t(W - 1) * kLdsDiagWgs + blockIdx.x) * 16u;
-    for (int i = 0; i < 16; ++i) o[i] = diag[i];
+  if (diagOn) {
+    diag[3] = nUnitsDone;
+    diag[4] = uint32_t(__builtin_amdgcn_s_memtime() - k0);
   }
 #endif
 }
@@ -670,22 +539,19 @@ int num_cus() {
 // nodes fit 15 bits, chunk ids 16 bits, the image + one unit's state fit LDS.
 size_t lds_image_bytes(const ogs_graph& g, int W) {
   if (g.max_nodes <= 0 || uint32_t(g.max_nodes) > kNodeMax || W < 1 || W > 4) return 0;
-  const uint32_t cap = uint32_t(g.max_edges) / kLdsChunk + uint32_t(g.max_nodes);
+  const uint32_t cap = chunk_cap(uint32_t(g.max_nodes), uint32_t(g.max_edges));
   if (cap > 0xFFFFu || uint32_t(g.max_edges) > 0xFFFFFFu) return 0;
   const LdsImage L = lds_image(g, W);
-  if (L.block + L.state > 160u * 1024u) return 0;
+  if (L.block + L.state + 64u > 160u * 1024u) return 0;  // + the static counters
   return (size_t(g.num_topos) * L.stride + 255u) & ~size_t(255);
 }
 
 // SPF of every unit into dist / nh (u32 distances, W next-hop words): image
 // build (one workgroup per topology), then one persistent 1024-thread
 // workgroup per CU over the units. Call only when lds_image_bytes() != 0.
-int g_spfLdsForm = 0;  // "spf_lds_form": 0 three-pass rounds, 1 CAS / two-phase (A/B)
-
 hipError_t launch_spf_lds(const ogs_graph& g, const ogs_unit* units, int nUnits,
                           uint32_t flags, int W, uint32_t* dist, uint32_t* nh,
                           void* scratch, hipStream_t stream) {
-  if (g_spfLdsForm) flags |= kFlagLdsCasForm;
   const LdsImage L = lds_image(g, W);
   uint8_t* img = static_cast<uint8_t*>(scratch);
   hipLaunchKernelGGL(lds_scan_kernel, dim3(g.num_topos), dim3(kLdsBlock), 0, stream, g, L, img);
@@ -722,7 +588,7 @@ hipError_t launch_spf_lds(const ogs_graph& g, const ogs_unit* units, int nUnits,
 
 #ifdef OGS_STAMPS
 extern "C" int ogs_diag_lds_stamps(uint32_t* host, int32_t words) {
-  const size_t n = std::min<size_t>(size_t(words), size_t(4) * ogs::kLdsDiagWgs * 16);
+  const size_t n = std::min<size_t>(size_t(words), size_t(4) * ogs::kLdsDiagWgs * 32);
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(ogs::g_ldsStamps), n * 4, 0,
                              hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
 }

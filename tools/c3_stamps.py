@@ -46,19 +46,21 @@ def main():
         bench.c3_launch_all(lib, capi, launches, main_s, side)
     torch.cuda.synchronize()
     if a.lds:
-        raw = np.zeros(4 * 4096 * 16, dtype=np.uint32)
+        raw = np.zeros(4 * 4096 * 32, dtype=np.uint32)
         lib.ogs_diag_lds_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int32]
         assert lib.ogs_diag_lds_stamps(raw.ctypes.data, raw.size) == 0
-        raw = raw.reshape(4, 4096, 16)
+        raw = raw.reshape(4, 4096, 32)
         for L in launches:
             st = raw[L["W"] - 1]
-            st = st[st[:, 12] != 0]
+            st = st[st[:, 4] != 0]
             print(f"W={L['W']} workgroups={len(st)}: stage med={np.median(st[:, 0]):.0f} "
                   f"first-unit(incl stage) med={np.median(st[:, 1]):.0f} "
-                  f"rounds med={np.median(st[:, 2]):.0f} units med={np.median(st[:, 11]):.0f} "
-                  f"kernel med={np.median(st[:, 12]):.0f} max={st[:, 12].max():.0f}")
-            print("   round cycles (med): " +
-                  " ".join(f"{np.median(st[:, k]):.0f}" for k in range(3, 11)))
+                  f"rounds med={np.median(st[:, 2]):.0f} queued med={np.median(st[:, 5]):.0f} "
+                  f"units med={np.median(st[:, 3]):.0f} "
+                  f"kernel med={np.median(st[:, 4]):.0f} max={st[:, 4].max():.0f}")
+            print("   round (queue / dist / nh) cycles (med): " + "  ".join(
+                "/".join(f"{np.median(st[:, 8 + 3 * k + j]):.0f}" for j in range(3))
+                for k in range(8) if np.median(st[:, 8 + 3 * k + 2]) > 0))
         return
     raw = np.zeros(65536 * 8, dtype=np.uint32)
     lib.ogs_diag_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int32]

@@ -1,0 +1,17 @@
+#!/bin/bash
+# LDS SPF phase stamps
+set -o pipefail
+mkdir -p gpurun_out; export TMPDIR=/tmp
+S=openr_amd/lib/libopenr_gpu_stamps.so
+for r in 0/8 0/1; do
+  echo "=== lds stamps $r"
+  OGS_LIB=$S timeout -k 10 200 python -u tools/c3_stamps.py --lds --as-rank $r --opt route_stream=4 > gpurun_out/st.log 2>&1 || { tail -30 gpurun_out/st.log; exit 1; }
+  grep -v amdgpu.ids gpurun_out/st.log
+done
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -k "route_stream" -x -q --timeout 120 --timeout-method thread > gpurun_out/r04n_par.log 2>&1 || { tail -40 gpurun_out/r04n_par.log; exit 1; }
+tail -2 gpurun_out/r04n_par.log
+for r in 0/8 0/1; do
+  echo "=== A/B $r"
+  timeout -k 10 300 python -u tools/c3_opt_ab.py --pairs 3 --as-rank $r frontier_block=512,frontier_parts=2,frontier_parts_wide=4 route_stream=4 > gpurun_out/r04n_ab.log 2>&1 || { tail -30 gpurun_out/r04n_ab.log; exit 1; }
+  grep '^{' gpurun_out/r04n_ab.log | cut -c1-150
+done
