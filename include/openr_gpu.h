@@ -291,7 +291,11 @@ int ogs_host_free(void* hptr);
  *                 stream from LDS; 1 an SPF launch then a route-stream launch
  *                 (dist/next-hop sets through HBM); 4 the SPF with the
  *                 topology staged in LDS, then the route stream over
- *                 "frontier_parts" workgroups per unit (A/B). Scratch
+ *                 "frontier_parts" workgroups per unit (A/B); 5 that SPF
+ *                 and the stream in one persistent launch: "lds_grid"
+ *                 workgroups (0 = one per CU) take SPF and stream items
+ *                 ("lds_parts" prefix ranges per unit, default 4) from a
+ *                 device-wide counter, SPFs kept one grid ahead. Scratch
  *                 (prefix keys, dist/next-hop sets when out->dist / out->nh
  *                 are NULL) comes from a grow-only per-device workspace.
  *                 "route_store_nt", bits: 1 the RouteDb stream's 16-B stores

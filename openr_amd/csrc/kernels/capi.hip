@@ -15,6 +15,8 @@ extern int g_waveOpt;
 extern int g_kspWaveTrace;
 extern int g_msGroup;
 extern int g_routeStream;
+extern int g_ldsParts;
+extern int g_ldsGrid;
 extern int g_routeStoreNt;
 extern int g_spfSeedRow;
 extern int g_frontierBlock;
@@ -185,10 +187,20 @@ int ogs_set_option(const char* name, int64_t value) {
     return OGS_OK;
   }
   if (std::strcmp(name, "route_stream") == 0) {
-    if (value != 1 && value != 2 && value != 4) {
-      return fail(OGS_E_INVALID, "route_stream must be 1, 2 or 4");
+    if (value != 1 && value != 2 && value != 4 && value != 5) {
+      return fail(OGS_E_INVALID, "route_stream must be 1, 2, 4 or 5");
     }
     ogs::g_routeStream = int(value);
+    return OGS_OK;
+  }
+  if (std::strcmp(name, "lds_parts") == 0) {
+    if (value < 1 || value > 64) return fail(OGS_E_INVALID, "lds_parts must be in [1, 64]");
+    ogs::g_ldsParts = int(value);
+    return OGS_OK;
+  }
+  if (std::strcmp(name, "lds_grid") == 0) {
+    if (value < 0 || value > 4096) return fail(OGS_E_INVALID, "lds_grid must be in [0, 4096]");
+    ogs::g_ldsGrid = int(value);
     return OGS_OK;
   }
   if (std::strcmp(name, "spf_packed_scan") == 0) {

@@ -47,6 +47,25 @@ __device__ __forceinline__ uint32_t node_route_meta(uint32_t v, uint32_t s,
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
+// Route key of prefix p (local index) of topology t (pfx_key_kernel / the
+// LDS paths' prep kernel): the single advertiser's node | v4 bit, or SLOW.
+__device__ __forceinline__ uint32_t prefix_key(const ogs_prefix_table& pt, uint32_t t,
+                                               uint32_t p) {
+  const uint32_t p0 = pt.pfx_base[t];
+  const uint32_t P = pt.pfx_base[t + 1] - p0;
+  uint32_t k = kKeySlow;
+  if (p < P) {
+    const uint32_t gp = p0 + p;
+    const uint32_t a0 = pt.adv_off[gp], a1 = pt.adv_off[gp + 1];
+    const uint8_t f = pt.pfx_flags[gp];
+    if (a1 - a0 == 1 && !(f & OGS_PFX_HAS_MIN_NH)) {
+      const uint32_t n = pt.adv_node[a0];
+      if (n != OGS_NODE_NONE) k = n | ((f & OGS_PFX_V4) ? kKeyV4 : 0u);
+    }
+  }
+  return k;
+}
+
 // one 16-B output store (route_core.h store_out: kFlagNtStores flavour)
 __device__ __forceinline__ void store4(uint32_t* p, uint32_t a, uint32_t b, uint32_t c,
                                        uint32_t d, bool nt) {

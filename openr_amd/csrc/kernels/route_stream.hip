@@ -46,18 +46,7 @@ __global__ __launch_bounds__(kBlock) void pfx_key_kernel(
   const uint32_t t = blockIdx.y;
   const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
   if (t >= uint32_t(numTopos) || p >= Sp) return;
-  const uint32_t p0 = pt.pfx_base[t];
-  const uint32_t P = pt.pfx_base[t + 1] - p0;
-  uint32_t k = kKeySlow;
-  if (p < P) {
-    const uint32_t gp = p0 + p;
-    const uint32_t a0 = pt.adv_off[gp], a1 = pt.adv_off[gp + 1];
-    const uint8_t f = pt.pfx_flags[gp];
-    if (a1 - a0 == 1 && !(f & OGS_PFX_HAS_MIN_NH)) {
-      const uint32_t n = pt.adv_node[a0];
-      if (n != OGS_NODE_NONE) k = n | ((f & OGS_PFX_V4) ? kKeyV4 : 0u);
-    }
-  }
+  const uint32_t k = prefix_key(pt, t, p);
   key[size_t(t) * Sp + p] = k;
 }
 
@@ -170,7 +159,8 @@ hipError_t workspace(size_t bytes, hipStream_t stream, void** out) {
 // "route_stream" option for large shared topologies: 2 (default) fused
 // frontier SPF + route stream, one launch; 1 SPF launch then route-stream
 // launch (dist / next-hop sets through HBM); 4 the LDS-resident SPF
-// (spf_lds.hip) then the route stream over parts. (0, the fused multi-source
+// (spf_lds.hip) then the route stream over parts; 5 both of those in one
+// persistent launch (spf_lds.hip, spf_lds_route_kernel). (0, the fused multi-source
 // kernel as the C3 form, and 3, the split pipelined over unit chunks on two
 // streams -- 1.40-1.64 vs 1.33 ms on C3, profiles/r03_c3_pipelined_split_
 // ab.log -- were removed in round 4; the multi-source kernel remains the
@@ -200,7 +190,13 @@ hipError_t launch_frontier_routes(const ogs_graph& g, const ogs_prefix_table& pt
                                   int nUnits, uint32_t flags, int W,
                                   const ogs_spf_out& out, void* scratch,
                                   hipStream_t stream);
-size_t lds_image_bytes(const ogs_graph& g, int W);
+size_t lds_scratch_bytes(const ogs_graph& g, int W, int nUnits);
+hipError_t launch_lds_prep(const ogs_graph& g, const ogs_prefix_table* pt, uint32_t* key,
+                           int W, int nUnits, void* scratch, hipStream_t stream);
+hipError_t launch_spf_lds_routes(const ogs_graph& g, const ogs_prefix_table& pt,
+                                 const uint32_t* key, const ogs_unit* units, int nUnits,
+                                 uint32_t flags, int W, uint32_t* dist, uint32_t* nh,
+                                 const ogs_spf_out& out, void* scratch, hipStream_t stream);
 hipError_t launch_spf_lds(const ogs_graph& g, const ogs_unit* units, int nUnits,
                           uint32_t flags, int W, uint32_t* dist, uint32_t* nh,
                           void* scratch, hipStream_t stream);
@@ -297,11 +293,11 @@ bool try_ms_stream(const ogs_graph& g, const ogs_prefix_table& pt,
   const size_t Sn = size_t(g.max_nodes), Sp = size_t(pt.max_prefixes);
   const bool frontier = frontier_fits(g, flags, W);
   // route_stream 4: SPF with the topology in LDS (spf_lds.hip), then the
-  // stream over `parts` workgroups per unit
-  const size_t ldsBytes = g_routeStream == 4 && !(flags & OGS_F_WIDE_METRIC) && Sp > 0
-                              ? lds_image_bytes(g, W) : 0;
+  // stream over `parts` workgroups per unit; 5: both in one persistent launch
+  const bool ldsForm = (g_routeStream == 4 || g_routeStream == 5) && Sp > 0;
+  const size_t ldsBytes = ldsForm ? lds_scratch_bytes(g, W, nUnits) : 0;
   const bool ldsSplit = ldsBytes != 0;
-  const bool fused = (g_routeStream == 2 || (g_routeStream == 4 && !ldsSplit)) && frontier;
+  const bool fused = (g_routeStream == 2 || (ldsForm && !ldsSplit)) && frontier;
   // three-word sets (65..96 links: C3 FSWs) through the frontier forms only
   if (W == 3 && !fused && !ldsSplit) return false;
   const size_t keyBytes = round256(size_t(g.num_topos) * Sp * 4);
@@ -314,24 +310,20 @@ bool try_ms_stream(const ogs_graph& g, const ogs_prefix_table& pt,
   char* base = static_cast<char*>(ws);
   uint32_t* key = reinterpret_cast<uint32_t*>(base);
   void* chunkScratch = base + keyBytes;
-  if (Sp > 0) {
-    hipLaunchKernelGGL(pfx_key_kernel, dim3(unsigned((Sp + kBlock - 1) / kBlock),
-                                            unsigned(g.num_topos)),
-                       dim3(kBlock), 0, stream, pt, g.num_topos, key);
-    *err = hipGetLastError();
-    if (*err != hipSuccess) return true;
-  }
-  if (fused) {
-    *err = launch_frontier_routes(g, pt, key, units, nUnits, flags, W, out,
-                                  chunkScratch, stream);
-    return true;
-  }
   ogs_spf_out spf{};
   spf.dist = out.dist ? out.dist : base + keyBytes + chunkBytes;
   spf.nh = out.nh ? out.nh
                   : reinterpret_cast<uint32_t*>(base + keyBytes + chunkBytes + distBytes);
   if (ldsSplit) {
+    // one prep launch: LDS images, weight partials, counters, route keys
+    *err = launch_lds_prep(g, &pt, key, W, nUnits, chunkScratch, stream);
+    if (*err != hipSuccess) return true;
     uint32_t* d = static_cast<uint32_t*>(spf.dist);
+    if (g_routeStream == 5) {
+      *err = launch_spf_lds_routes(g, pt, key, units, nUnits, flags, W, d, spf.nh, out,
+                                   chunkScratch, stream);
+      return true;
+    }
     *err = launch_spf_lds(g, units, nUnits, flags, W, d, spf.nh, chunkScratch, stream);
     if (*err != hipSuccess) return true;
     int parts = 1;
@@ -342,6 +334,18 @@ bool try_ms_stream(const ogs_graph& g, const ogs_prefix_table& pt,
       case 3: *err = launch_route_stream<3>(g, pt, key, units, nUnits, flags, d, spf.nh, out, stream, parts); break;
       default: *err = launch_route_stream<4>(g, pt, key, units, nUnits, flags, d, spf.nh, out, stream, parts); break;
     }
+    return true;
+  }
+  if (Sp > 0) {
+    hipLaunchKernelGGL(pfx_key_kernel, dim3(unsigned((Sp + kBlock - 1) / kBlock),
+                                            unsigned(g.num_topos)),
+                       dim3(kBlock), 0, stream, pt, g.num_topos, key);
+    *err = hipGetLastError();
+    if (*err != hipSuccess) return true;
+  }
+  if (fused) {
+    *err = launch_frontier_routes(g, pt, key, units, nUnits, flags, W, out,
+                                  chunkScratch, stream);
     return true;
   }
   if (frontier) {

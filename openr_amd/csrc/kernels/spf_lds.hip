@@ -32,6 +32,7 @@
 
 #include "openr_gpu.h"
 #include "route_core.h"
+#include "route_stream.h"
 #include "spf_core.h"
 
 namespace ogs {
@@ -52,7 +53,7 @@ __host__ __device__ inline uint32_t chunk_cap(uint32_t N, uint32_t E) {
 }
 
 // Byte layout of one topology's image (global, then the same block in LDS):
-// header (16 B, global only) | eimg u16[E] | cnode u16[cap] | row u32[N+1] |
+// header (16 B, global only: {chunks, 0, 0, 0}) | eimg u16[E] | cnode u16[cap] | row u32[N+1] |
 // first u16[N], sections 16-B aligned, sized by the batch's maxima so every
 // topology (and the LDS copy) shares the offsets. Then, LDS only, one unit's
 // state: dist u32[N] | nh u32[N * W] | stamp u8[N] | queue u16[cap].
@@ -79,105 +80,147 @@ __host__ LdsImage lds_image(const ogs_graph& g, int W) {
   return L;
 }
 
-// Image build, once per call: lds_scan_kernel (one workgroup per topology:
-// row offsets, chunk -> node table with the node's drained bit; header
-// {chunks, weight min, weight max, 0}) then lds_edges_kernel (many
-// workgroups: the 2-B edge words and the min / max weight of the up edges).
-// Header of topology t at img + t * L.stride; the weights are uniform iff
-// min == max.
-__global__ __launch_bounds__(kLdsBlock) void lds_scan_kernel(ogs_graph g, LdsImage L,
-                                                            uint8_t* __restrict__ img) {
-  constexpr uint32_t B = kLdsBlock;
-  __shared__ uint32_t wsum[B / 64];
-  __shared__ uint32_t base;
-  const uint32_t t = blockIdx.x, tid = threadIdx.x;
-  const uint32_t nb = g.node_base[t];
-  const uint32_t N = g.node_base[t + 1] - nb;
-  const uint32_t* __restrict__ gRow = g.row_ptr + nb;
-  const uint32_t e0 = gRow[0];
-  uint8_t* hdr = img + size_t(t) * L.stride;
-  uint8_t* blk = hdr + 16;
-  uint16_t* __restrict__ cnode = reinterpret_cast<uint16_t*>(blk + L.cnode);
-  uint32_t* __restrict__ row = reinterpret_cast<uint32_t*>(blk + L.row);
-  uint16_t* __restrict__ first = reinterpret_cast<uint16_t*>(blk + L.first);
-  if (tid == 0) base = 0u;
-  for (uint32_t v = tid; v <= N; v += B) row[v] = gRow[v] - e0;
-  __syncthreads();
-  // chunk ids: exclusive scan of ceil(deg / 8) over the nodes, tile by tile
-  const int lane = int(tid & 63u), wave = int(tid >> 6);
-  for (uint32_t t0 = 0; t0 < N; t0 += B) {
-    const uint32_t v = t0 + tid;
-    const uint32_t deg = v < N ? gRow[v + 1] - gRow[v] : 0u;
-    const uint32_t n = (deg + kLdsChunk - 1u) / kLdsChunk;
-    uint32_t inc = n;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const uint32_t y = __shfl_up(inc, d, 64);
-      if (lane >= d) inc += y;
-    }
-    if (lane == 63) wsum[wave] = inc;
-    __syncthreads();
-    uint32_t off = base;
-    for (int w = 0; w < wave; ++w) off += wsum[w];
-    __syncthreads();
-    if (tid == B - 1u) base = off + inc;
-    const uint32_t at = off + inc - n;
-    if (v < N) {
-      first[v] = uint16_t(at);
-      const uint32_t tag = (g.node_flags[nb + v] & OGS_NODE_OVERLOADED) ? kDrained16 : 0u;
-      for (uint32_t k = 0; k < n; ++k) cnode[at + k] = uint16_t(v | tag);
-    }
-    __syncthreads();
-  }
-  if (tid == 0) {
-    uint32_t* h = reinterpret_cast<uint32_t*>(hdr);
-    h[0] = base;
-    h[1] = 0xFFFFFFFFu;  // weight min / max of the up edges (lds_edges_kernel)
-    h[2] = 0u;
-    h[3] = 0u;
-  }
+// Scratch of the LDS paths, one call: images [num_topos * stride] | weight
+// min / max partials uint2[num_topos * nEB] (one per prep edge block) | work
+// counter (u32, 256-B line) | unit ready flags u32[nUnits] (megakernel).
+constexpr uint32_t kPrepEdges = kLdsBlock * 8;  // edges per prep edge block
+struct LdsScratch {
+  size_t mm, ctr, ready, bytes;
+  uint32_t nEB;
+};
+
+__host__ LdsScratch lds_scratch(const ogs_graph& g, const LdsImage& L, int nUnits) {
+  auto r256 = [](size_t x) { return (x + 255u) & ~size_t(255); };
+  LdsScratch S{};
+  S.nEB = (uint32_t(std::max(g.max_edges, 1)) + kPrepEdges - 1u) / kPrepEdges;
+  S.mm = r256(size_t(g.num_topos) * L.stride);
+  S.ctr = S.mm + r256(size_t(g.num_topos) * S.nEB * 8u);
+  S.ready = S.ctr + 256u;
+  S.bytes = S.ready + r256(size_t(std::max(nUnits, 1)) * 4u);
+  return S;
 }
 
-constexpr uint32_t kEdgesPerThread = 8;
-
-__global__ __launch_bounds__(kBlock) void lds_edges_kernel(ogs_graph g, LdsImage L,
-                                                          uint8_t* __restrict__ img) {
-  const uint32_t t = blockIdx.y;
-  const uint32_t nb = g.node_base[t];
-  const uint32_t N = g.node_base[t + 1] - nb;
-  const uint32_t e0 = g.row_ptr[nb];
-  const uint32_t E = g.row_ptr[nb + N] - e0;
-  uint8_t* hdr = img + size_t(t) * L.stride;
-  uint16_t* __restrict__ eimg = reinterpret_cast<uint16_t*>(hdr + 16 + L.eimg);
-  const uint64_t* __restrict__ edges = g.edges + e0;
-  const uint32_t base = blockIdx.x * kBlock * kEdgesPerThread + threadIdx.x;
-  uint64_t x[kEdgesPerThread];
-#pragma unroll
-  for (uint32_t k = 0; k < kEdgesPerThread; ++k) {
-    const uint32_t e = base + k * kBlock;
-    x[k] = e < E ? edges[e] : uint64_t(OGS_EDGE_DOWN);
-  }
-  uint32_t lo = 0xFFFFFFFFu, hi = 0u;
-#pragma unroll
-  for (uint32_t k = 0; k < kEdgesPerThread; ++k) {
-    const uint32_t e = base + k * kBlock;
-    const uint32_t w = static_cast<uint32_t>(x[k]);
-    const bool down = (w & OGS_EDGE_DOWN) != 0u;
-    if (e < E) eimg[e] = uint16_t(edge_dst(w) | (down ? kDown16 : 0u));
-    if (!down) {
-      lo = min(lo, static_cast<uint32_t>(x[k] >> 32));
-      hi = max(hi, static_cast<uint32_t>(x[k] >> 32));
+// Prep, once per call, one launch of 1024-thread blocks in three roles:
+//  blocks [0, T): topology t's row offsets, chunk -> node table (with the
+//    node's drained bit) and header {chunks}; block 0 also zeroes the work
+//    counter and the ready flags;
+//  next T * nEB: 8,192 edges each -> the 2-B edge words and the block's
+//    min / max weight over up edges (uniform weights iff min == max);
+//  next T * nKB (when keys are asked for): 1,024 prefixes each -> the route
+//    keys of route_stream.h (pfx_key_kernel's).
+__global__ __launch_bounds__(kLdsBlock) void lds_prep_kernel(
+    ogs_graph g, ogs_prefix_table pt, uint32_t* __restrict__ key, uint32_t nKB, LdsImage L,
+    uint8_t* __restrict__ img, uint2* __restrict__ mm, uint32_t nEB, uint32_t* __restrict__ ctr,
+    uint32_t* __restrict__ ready, uint32_t nReady) {
+  constexpr uint32_t B = kLdsBlock;
+  __shared__ uint32_t wsum[B / 64];
+  __shared__ uint32_t whi[B / 64];
+  __shared__ uint32_t base;
+  const uint32_t T = uint32_t(g.num_topos), tid = threadIdx.x;
+  const int lane = int(tid & 63u), wave = int(tid >> 6);
+  uint32_t blk = blockIdx.x;
+  if (blk < T) {
+    const uint32_t t = blk;
+    if (t == 0u) {
+      if (tid == 0u) *ctr = 0u;
+      for (uint32_t i = tid; i < nReady; i += B) ready[i] = 0u;
     }
-  }
+    const uint32_t nb = g.node_base[t];
+    const uint32_t N = g.node_base[t + 1] - nb;
+    const uint32_t* __restrict__ gRow = g.row_ptr + nb;
+    const uint32_t e0 = gRow[0];
+    uint8_t* hdr = img + size_t(t) * L.stride;
+    uint8_t* b8 = hdr + 16;
+    uint16_t* __restrict__ cnode = reinterpret_cast<uint16_t*>(b8 + L.cnode);
+    uint32_t* __restrict__ row = reinterpret_cast<uint32_t*>(b8 + L.row);
+    uint16_t* __restrict__ first = reinterpret_cast<uint16_t*>(b8 + L.first);
+    if (tid == 0) base = 0u;
+    for (uint32_t v = tid; v <= N; v += B) row[v] = gRow[v] - e0;
+    __syncthreads();
+    // chunk ids: exclusive scan of ceil(deg / 8) over the nodes, tile by tile
+    for (uint32_t t0 = 0; t0 < N; t0 += B) {
+      const uint32_t v = t0 + tid;
+      const uint32_t deg = v < N ? gRow[v + 1] - gRow[v] : 0u;
+      const uint32_t n = (deg + kLdsChunk - 1u) / kLdsChunk;
+      uint32_t inc = n;
 #pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) {
-    lo = min(lo, __shfl_xor(lo, d, 64));
-    hi = max(hi, __shfl_xor(hi, d, 64));
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(inc, d, 64);
+        if (lane >= d) inc += y;
+      }
+      if (lane == 63) wsum[wave] = inc;
+      __syncthreads();
+      uint32_t off = base;
+      for (int w = 0; w < wave; ++w) off += wsum[w];
+      __syncthreads();
+      if (tid == B - 1u) base = off + inc;
+      const uint32_t at = off + inc - n;
+      if (v < N) {
+        first[v] = uint16_t(at);
+        const uint32_t tag = (g.node_flags[nb + v] & OGS_NODE_OVERLOADED) ? kDrained16 : 0u;
+        for (uint32_t k = 0; k < n; ++k) cnode[at + k] = uint16_t(v | tag);
+      }
+      __syncthreads();
+    }
+    if (tid == 0) {
+      uint32_t* h = reinterpret_cast<uint32_t*>(hdr);
+      h[0] = base;
+      h[1] = h[2] = h[3] = 0u;
+    }
+    return;
   }
-  if ((threadIdx.x & 63u) == 0u) {
-    uint32_t* h = reinterpret_cast<uint32_t*>(hdr);
-    if (lo != 0xFFFFFFFFu) atomicMin(&h[1], lo);
-    if (hi != 0u) atomicMax(&h[2], hi);
+  blk -= T;
+  if (blk < T * nEB) {
+    const uint32_t t = blk / nEB, eb = blk - t * nEB;
+    const uint32_t nb = g.node_base[t];
+    const uint32_t N = g.node_base[t + 1] - nb;
+    const uint32_t e0 = g.row_ptr[nb];
+    const uint32_t E = g.row_ptr[nb + N] - e0;
+    uint16_t* __restrict__ eimg = reinterpret_cast<uint16_t*>(img + size_t(t) * L.stride + 16 + L.eimg);
+    const uint64_t* __restrict__ edges = g.edges + e0;
+    const uint32_t e00 = eb * kPrepEdges + tid;
+    uint64_t x[8];
+#pragma unroll
+    for (uint32_t k = 0; k < 8; ++k) {
+      const uint32_t e = e00 + k * B;
+      x[k] = e < E ? edges[e] : uint64_t(OGS_EDGE_DOWN);
+    }
+    uint32_t lo = 0xFFFFFFFFu, hi = 0u;
+#pragma unroll
+    for (uint32_t k = 0; k < 8; ++k) {
+      const uint32_t e = e00 + k * B;
+      const uint32_t w = static_cast<uint32_t>(x[k]);
+      const bool down = (w & OGS_EDGE_DOWN) != 0u;
+      if (e < E) eimg[e] = uint16_t(edge_dst(w) | (down ? kDown16 : 0u));
+      if (!down) {
+        lo = min(lo, static_cast<uint32_t>(x[k] >> 32));
+        hi = max(hi, static_cast<uint32_t>(x[k] >> 32));
+      }
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+      lo = min(lo, __shfl_xor(lo, d, 64));
+      hi = max(hi, __shfl_xor(hi, d, 64));
+    }
+    if (lane == 0) {
+      wsum[wave] = lo;
+      whi[wave] = hi;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      for (uint32_t w = 1; w < B / 64u; ++w) {
+        lo = min(lo, wsum[w]);
+        hi = max(hi, whi[w]);
+      }
+      mm[size_t(t) * nEB + eb] = make_uint2(lo, hi);
+    }
+    return;
+  }
+  blk -= T * nEB;
+  if (key && blk < T * nKB) {
+    const uint32_t t = blk / nKB, p = (blk - t * nKB) * B + tid;
+    const uint32_t Sp = uint32_t(pt.max_prefixes);
+    if (p < Sp) key[size_t(t) * Sp + p] = prefix_key(pt, t, p);
   }
 }
 
@@ -202,11 +245,16 @@ __device__ uint32_t g_ldsStamps[4 * kLdsDiagWgs * 32];
 // distance later falls drops what it had. The least fixpoint of spf_core.h
 // with fire-and-forget LDS atomics, and every chunk record is visited only
 // in the rounds its node is active (each once, on unit-weight BFS layers).
-template <int W>
-__global__ __launch_bounds__(kLdsBlock) void spf_lds_kernel(
-    ogs_graph g, LdsImage L, const uint8_t* __restrict__ img,
-    const ogs_unit* __restrict__ units, int nUnits, uint32_t flags,
-    uint32_t* __restrict__ oDist, uint32_t* __restrict__ oNh) {
+//
+// spf_lds_body runs that solver for the units its driver hands it:
+// driver(solve) calls solve(u) for each unit index u of this workgroup (the
+// image of unit u's topology is staged on first use and kept).
+template <int W, typename Driver>
+__device__ __forceinline__ void spf_lds_body(
+    const ogs_graph& g, const LdsImage& L, const uint8_t* __restrict__ img,
+    const uint2* __restrict__ mm, uint32_t nEB, const ogs_unit* __restrict__ units,
+    uint32_t flags, uint32_t* __restrict__ oDist, uint32_t* __restrict__ oNh,
+    Driver&& driver) {
   constexpr uint32_t kInf = 0xFFFFFFFFu;
   constexpr uint32_t B = kLdsBlock;
   const uint32_t tid = threadIdx.x, lane = tid & 63u;
@@ -242,7 +290,7 @@ __global__ __launch_bounds__(kLdsBlock) void spf_lds_kernel(
 #else
   auto mark = [](uint32_t) {};
 #endif
-  for (int u = int(blockIdx.x); u < nUnits; u += int(gridDim.x)) {
+  auto solve = [&](uint32_t u) {
     const ogs_unit unit = units[u];
     if (unit.topo != staged) {
       __syncthreads();  // the previous unit's state reads are done
@@ -252,8 +300,15 @@ __global__ __launch_bounds__(kLdsBlock) void spf_lds_kernel(
       for (uint32_t i = tid; i < L.block / 16u; i += B) dst[i] = src[i];
       const uint32_t* h = reinterpret_cast<const uint32_t*>(hdr);
       C = h[0];
-      uniform = h[1] == h[2] ? 1u : 0u;  // every up edge of this weight
-      w0 = h[1];
+      // weight min / max of the up edges, from the prep blocks' partials
+      uint32_t lo = 0xFFFFFFFFu, hi = 0u;
+      for (uint32_t b = 0; b < nEB; ++b) {
+        const uint2 x = mm[size_t(unit.topo) * nEB + b];
+        lo = min(lo, x.x);
+        hi = max(hi, x.y);
+      }
+      uniform = lo == hi ? 1u : 0u;  // every up edge of this weight
+      w0 = lo;
       const uint32_t nb = g.node_base[unit.topo];
       N = g.node_base[unit.topo + 1] - nb;
       e0 = g.row_ptr[nb];
@@ -511,13 +566,152 @@ __global__ __launch_bounds__(kLdsBlock) void spf_lds_kernel(
     }
     ++nUnitsDone;
 #endif
-  }
+  };
+  driver(solve);
 #ifdef OGS_STAMPS
   if (diagOn) {
     diag[3] = nUnitsDone;
     diag[4] = uint32_t(__builtin_amdgcn_s_memtime() - k0);
   }
 #endif
+}
+
+template <int W>
+__global__ __launch_bounds__(kLdsBlock) void spf_lds_kernel(
+    ogs_graph g, LdsImage L, const uint8_t* __restrict__ img, const uint2* __restrict__ mm,
+    uint32_t nEB, const ogs_unit* __restrict__ units, int nUnits, uint32_t flags,
+    uint32_t* __restrict__ oDist, uint32_t* __restrict__ oNh) {
+  spf_lds_body<W>(g, L, img, mm, nEB, units, flags, oDist, oNh, [&](auto& solve) {
+    for (int u = int(blockIdx.x); u < nUnits; u += int(gridDim.x)) solve(uint32_t(u));
+  });
+}
+
+// The unit's SPF state as published in HBM (ogs_spf_out layout), for the
+// stream's route_one on SLOW prefixes.
+template <int W>
+struct PublishedView {
+  const uint32_t* d;  // dist + u*Sn
+  const uint32_t* n;  // nh + u*W*Sn
+  uint32_t Sn;
+  __device__ __forceinline__ uint32_t dist(uint32_t v) const { return d[v]; }
+  __device__ __forceinline__ uint32_t nh(uint32_t v, int w) const {
+    return n[size_t(w) * Sn + v];
+  }
+};
+
+// SPF and RouteDb stream in ONE persistent launch (route_stream 5): each
+// workgroup takes items from a device-wide counter --
+//   items [0, G): the SPF of unit i (G = the grid: every workgroup starts
+//     with one);
+//   then per unit b, P + 1 items: the SPF of unit G + b (when there is
+//     one), then the P prefix ranges of unit b's route stream.
+// So SPFs stay G units ahead of the streams, a stream item never waits for
+// an SPF that is not already taken by a running workgroup (it was handed
+// out earlier), and a shard with a few more units than CUs streams the
+// other units' rows while its last SPFs run instead of a whole SPF launch
+// waiting on them. Hand-off (MI355X_MICROARCH.md, inter-workgroup
+// visibility): the SPF's dist / nh rows are plain stores, drained by every
+// wave, then a barrier, lane 0's agent release and a relaxed agent flag
+// store; a stream item's lane 0 polls the flag (relaxed agent loads), takes
+// an agent acquire, and the workgroup reads the rows after a barrier.
+template <int W, bool OUTS3>
+__global__ __launch_bounds__(kLdsBlock) void spf_lds_route_kernel(
+    ogs_graph g, ogs_prefix_table pt, const uint32_t* __restrict__ key, LdsImage L,
+    const uint8_t* __restrict__ img, const uint2* __restrict__ mm, uint32_t nEB,
+    const ogs_unit* __restrict__ units, int nUnits, uint32_t flags,
+    uint32_t* __restrict__ oDist, uint32_t* __restrict__ oNh, ogs_spf_out out,
+    uint32_t* __restrict__ ctr, uint32_t* __restrict__ ready, uint32_t P) {
+  __shared__ uint32_t item;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr uint32_t kInf = 0xFFFFFFFFu;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t U = uint32_t(nUnits);
+  const uint32_t G = min(U, gridDim.x);
+  const uint32_t total = G + U * (P + 1u);
+  const uint32_t Sn = uint32_t(g.max_nodes), Sp = uint32_t(pt.max_prefixes);
+  const RouteCfg cfg{(flags & OGS_F_ENABLE_V4) != 0, (flags & OGS_F_V4_OVER_V6) != 0,
+                     (flags & OGS_F_BEST_ROUTE_SELECTION) != 0};
+  spf_lds_body<W>(g, L, img, mm, nEB, units, flags, oDist, oNh, [&](auto& solve) {
+    for (;;) {
+      if (tid == 0u) item = atomicAdd(ctr, 1u);
+      __syncthreads();
+      const uint32_t i = item;
+      __syncthreads();  // every lane has read item before lane 0 takes the next
+      if (i >= total) break;
+      uint32_t u = i, part = 0;
+      bool spf = true;
+      if (i >= G) {
+        const uint32_t j = i - G;
+        u = j / (P + 1u);
+        const uint32_t r = j - u * (P + 1u);
+        if (r == 0u) {
+          u += G;
+          if (u >= U) continue;
+        } else {
+          spf = false;
+          part = r - 1u;
+        }
+      }
+      if (spf) {
+        solve(u);  // ends with the dist / nh row stores and a barrier
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0u) {
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __hip_atomic_store(&ready[u], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        continue;
+      }
+      // stream item: prefix range `part` of unit u
+      if (tid == 0u) {
+        while (__hip_atomic_load(&ready[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+          __builtin_amdgcn_s_sleep(8);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __syncthreads();
+      const ogs_unit unit = units[u];
+      const uint32_t t = unit.topo, s = unit.src;
+      const uint32_t nb = g.node_base[t];
+      const uint32_t N = g.node_base[t + 1] - nb;
+      const uint8_t* __restrict__ nflags = g.node_flags + nb;
+      const PublishedView<W> sv{oDist + size_t(u) * Sn, oNh + size_t(u) * W * Sn, Sn};
+      // per-node records in the state region of LDS (the image stays)
+      uint32_t* rMeta = reinterpret_cast<uint32_t*>(smem + L.block);
+      uint32_t* rMetric = rMeta + Sn;
+      uint32_t* rMask = rMetric + Sn;  // [W][Sn]
+      for (uint32_t v = tid; v < N; v += kLdsBlock) {
+        const uint32_t d = sv.dist(v);
+        uint32_t m[W], cnt = 0;
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+          m[w] = sv.nh(v, w);
+          cnt += __popc(m[w]);
+        }
+        rMeta[v] = node_route_meta(v, s, d != kInf, cnt, nflags[v]);
+        rMetric[v] = (v == s) ? kInf : d;
+#pragma unroll
+        for (int w = 0; w < W; ++w) rMask[w * Sn + v] = m[w];
+      }
+      __syncthreads();
+      const uint32_t p0 = pt.pfx_base[t];
+      const uint32_t Pn = pt.pfx_base[t + 1] - p0;
+      const uint32_t span = ((Pn + P - 1u) / P + 3u) & ~3u;
+      const uint32_t lo = min(Pn, part * span), hi = min(Pn, lo + span);
+      auto rec = [&](uint32_t v, Rec<W>& r) {
+        r.meta = rMeta[v];
+        r.metric = rMetric[v];
+#pragma unroll
+        for (int w = 0; w < W; ++w) r.mask[w] = rMask[w * Sn + v];
+      };
+      stream_routes<W, false, OUTS3, kLdsBlock>(pt, key + size_t(t) * Sp, p0, Pn, Sp, u, s,
+                                                nflags, sv, cfg, out, rec, nullptr,
+                                                (flags & kFlagNtStores) != 0, lo, hi);
+      __syncthreads();  // the records are read before the next item reuses LDS
+    }
+  });
 }
 
 int num_cus() {
@@ -535,44 +729,64 @@ int num_cus() {
 
 }  // namespace
 
-// Scratch of the LDS images (workspace) and whether the batch qualifies:
-// nodes fit 15 bits, chunk ids 16 bits, the image + one unit's state fit LDS.
-size_t lds_image_bytes(const ogs_graph& g, int W) {
+extern int g_routeStoreNt;  // route_stream.hip
+
+// Workspace bytes of the LDS paths for this batch (lds_scratch), or 0 when
+// it does not qualify: nodes fit 15 bits, chunk ids 16 bits, the image + one
+// unit's state (and the megakernel's per-node records) fit LDS.
+size_t lds_scratch_bytes(const ogs_graph& g, int W, int nUnits) {
   if (g.max_nodes <= 0 || uint32_t(g.max_nodes) > kNodeMax || W < 1 || W > 4) return 0;
   const uint32_t cap = chunk_cap(uint32_t(g.max_nodes), uint32_t(g.max_edges));
   if (cap > 0xFFFFu || uint32_t(g.max_edges) > 0xFFFFFFu) return 0;
   const LdsImage L = lds_image(g, W);
-  if (L.block + L.state + 64u > 160u * 1024u) return 0;  // + the static counters
-  return (size_t(g.num_topos) * L.stride + 255u) & ~size_t(255);
+  const uint32_t recs = uint32_t(g.max_nodes) * uint32_t(2 + W) * 4u;
+  if (L.block + std::max(L.state, recs) + 64u > 160u * 1024u) return 0;  // + static LDS
+  return lds_scratch(g, L, nUnits).bytes;
 }
 
-// SPF of every unit into dist / nh (u32 distances, W next-hop words): image
-// build (one workgroup per topology), then one persistent 1024-thread
-// workgroup per CU over the units. Call only when lds_image_bytes() != 0.
+// Prep launch (lds_prep_kernel): images, weight partials, counters, and the
+// route keys when key != nullptr.
+hipError_t launch_lds_prep(const ogs_graph& g, const ogs_prefix_table* pt, uint32_t* key,
+                           int W, int nUnits, void* scratch, hipStream_t stream) {
+  const LdsImage L = lds_image(g, W);
+  const LdsScratch S = lds_scratch(g, L, nUnits);
+  uint8_t* base = static_cast<uint8_t*>(scratch);
+  const uint32_t T = uint32_t(g.num_topos);
+  const uint32_t Sp = pt ? uint32_t(pt->max_prefixes) : 0u;
+  const uint32_t nKB = key && Sp ? (Sp + kLdsBlock - 1u) / kLdsBlock : 0u;
+  const ogs_prefix_table ptv = pt ? *pt : ogs_prefix_table{};
+  hipLaunchKernelGGL(lds_prep_kernel, dim3(T * (1u + S.nEB + nKB)), dim3(kLdsBlock), 0, stream,
+                     g, ptv, nKB ? key : nullptr, nKB, L, base,
+                     reinterpret_cast<uint2*>(base + S.mm), S.nEB,
+                     reinterpret_cast<uint32_t*>(base + S.ctr),
+                     reinterpret_cast<uint32_t*>(base + S.ready), uint32_t(nUnits));
+  return hipGetLastError();
+}
+
+template <typename K>
+static hipError_t allow_lds(K k, uint32_t lds) {
+  if (lds <= 64u * 1024u) return hipSuccess;
+  return hipFuncSetAttribute(reinterpret_cast<const void*>(k),
+                             hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
+}
+
+// SPF of every unit into dist / nh (u32 distances, W next-hop words) after
+// launch_lds_prep: one persistent 1024-thread workgroup per CU over the
+// units. Call only when lds_scratch_bytes() != 0.
 hipError_t launch_spf_lds(const ogs_graph& g, const ogs_unit* units, int nUnits,
                           uint32_t flags, int W, uint32_t* dist, uint32_t* nh,
                           void* scratch, hipStream_t stream) {
   const LdsImage L = lds_image(g, W);
-  uint8_t* img = static_cast<uint8_t*>(scratch);
-  hipLaunchKernelGGL(lds_scan_kernel, dim3(g.num_topos), dim3(kLdsBlock), 0, stream, g, L, img);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  const uint32_t per = kBlock * kEdgesPerThread;
-  hipLaunchKernelGGL(lds_edges_kernel,
-                     dim3((uint32_t(std::max(g.max_edges, 1)) + per - 1u) / per, g.num_topos),
-                     dim3(kBlock), 0, stream, g, L, img);
-  e = hipGetLastError();
-  if (e != hipSuccess) return e;
+  const LdsScratch S = lds_scratch(g, L, nUnits);
+  const uint8_t* img = static_cast<const uint8_t*>(scratch);
+  const uint2* mm = reinterpret_cast<const uint2*>(img + S.mm);
   const uint32_t lds = L.block + L.state;
   const int grid = std::max(1, std::min(nUnits, num_cus()));
   auto go = [&](auto k) {
-    if (lds > 64u * 1024u) {
-      hipError_t a = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
-      if (a != hipSuccess) return a;
-    }
-    hipLaunchKernelGGL(k, dim3(grid), dim3(kLdsBlock), lds, stream, g, L,
-                       static_cast<const uint8_t*>(img), units, nUnits, flags, dist, nh);
+    hipError_t a = allow_lds(k, lds);
+    if (a != hipSuccess) return a;
+    hipLaunchKernelGGL(k, dim3(grid), dim3(kLdsBlock), lds, stream, g, L, img, mm, S.nEB,
+                       units, nUnits, flags, dist, nh);
     return hipGetLastError();
   };
   switch (W) {
@@ -580,6 +794,50 @@ hipError_t launch_spf_lds(const ogs_graph& g, const ogs_unit* units, int nUnits,
     case 2: return go(spf_lds_kernel<2>);
     case 3: return go(spf_lds_kernel<3>);
     case 4: return go(spf_lds_kernel<4>);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+// "lds_parts": prefix ranges per unit in the one-launch form (default 4);
+// "lds_grid": its workgroups (0 = one per CU).
+int g_ldsParts = 4;
+int g_ldsGrid = 0;
+
+// SPF + RouteDb stream in one persistent launch (spf_lds_route_kernel)
+// after launch_lds_prep with keys; dist / nh are the published SPF rows.
+hipError_t launch_spf_lds_routes(const ogs_graph& g, const ogs_prefix_table& pt,
+                                 const uint32_t* key, const ogs_unit* units, int nUnits,
+                                 uint32_t flags, int W, uint32_t* dist, uint32_t* nh,
+                                 const ogs_spf_out& out, void* scratch, hipStream_t stream) {
+  const LdsImage L = lds_image(g, W);
+  const LdsScratch S = lds_scratch(g, L, nUnits);
+  uint8_t* base = static_cast<uint8_t*>(scratch);
+  const uint2* mm = reinterpret_cast<const uint2*>(base + S.mm);
+  uint32_t* ctr = reinterpret_cast<uint32_t*>(base + S.ctr);
+  uint32_t* ready = reinterpret_cast<uint32_t*>(base + S.ready);
+  const uint32_t recs = uint32_t(g.max_nodes) * uint32_t(2 + W) * 4u;
+  const uint32_t lds = L.block + std::max(L.state, recs);
+  const int grid = std::max(1, g_ldsGrid > 0 ? g_ldsGrid : num_cus());
+  const uint32_t P = uint32_t(std::max(1, g_ldsParts));
+  if (g_routeStoreNt & 1) flags |= kFlagNtStores;
+  const bool outs3 = out.meta && out.metric && out.mask && !out.sel;
+  auto go = [&](auto k) {
+    hipError_t a = allow_lds(k, lds);
+    if (a != hipSuccess) return a;
+    hipLaunchKernelGGL(k, dim3(grid), dim3(kLdsBlock), lds, stream, g, pt, key, L,
+                       static_cast<const uint8_t*>(base), mm, S.nEB, units, nUnits, flags,
+                       dist, nh, out, ctr, ready, P);
+    return hipGetLastError();
+  };
+  switch (W * 2 + (outs3 ? 1 : 0)) {
+    case 2: return go(spf_lds_route_kernel<1, false>);
+    case 3: return go(spf_lds_route_kernel<1, true>);
+    case 4: return go(spf_lds_route_kernel<2, false>);
+    case 5: return go(spf_lds_route_kernel<2, true>);
+    case 6: return go(spf_lds_route_kernel<3, false>);
+    case 7: return go(spf_lds_route_kernel<3, true>);
+    case 8: return go(spf_lds_route_kernel<4, false>);
+    case 9: return go(spf_lds_route_kernel<4, true>);
     default: return hipErrorInvalidValue;
   }
 }

@@ -70,7 +70,9 @@ def _c3(product, names, ppn=100):
                                   dict(frontier_block=512, frontier_parts=3,
                                        frontier_parts_wide=5),
                                   dict(route_stream=4), dict(route_stream=4, frontier_parts=3,
-                                                             frontier_parts_wide=5)])
+                                                             frontier_parts_wide=5),
+                                  dict(route_stream=5), dict(route_stream=5, lds_parts=7,
+                                                             lds_grid=100)])
 def test_c3_full_every_source_matches_oracle(product, opts):
     """C3-full at bench size (2,080 sources x 208k prefixes) through
     bench.py's two-stream width-group launches: every source's digest equals
@@ -78,7 +80,8 @@ def test_c3_full_every_source_matches_oracle(product, opts):
     golden job digest bench.py asserts; with the default launch form and
     forced ones (fused: frontier_block threads per workgroup, frontier_parts
     workgroups per unit each streaming one prefix range; route_stream 4: the
-    LDS-resident SPF then the split stream)."""
+    LDS-resident SPF then the split stream; route_stream 5: both in one
+    persistent launch, at several item / grid shapes)."""
     if not os.path.exists(C3_SOURCES):
         pytest.skip("oracle C3 per-source digests not generated")
     want = json.load(open(C3_SOURCES))
@@ -88,7 +91,8 @@ def test_c3_full_every_source_matches_oracle(product, opts):
     assert set(want) == set(names)
     import openr_amd.capi as capi
     lib = capi.load()
-    defaults = dict(frontier_block=0, frontier_parts=0, frontier_parts_wide=0, route_stream=2)
+    defaults = dict(frontier_block=0, frontier_parts=0, frontier_parts_wide=0, route_stream=2,
+                    lds_parts=4, lds_grid=0)
     for k, v in opts.items():
         capi.check(lib, lib.ogs_set_option(k.encode(), v), k)
     try:

@@ -355,6 +355,8 @@ def _batch_dbs(product, kind, opts, srcs, enable_v4, brs, **options):
         return [br.canonical(u) for u in range(len(srcs))]
     finally:
         lib.ogs_set_option(b"route_stream", 2)
+        lib.ogs_set_option(b"lds_parts", 4)
+        lib.ogs_set_option(b"lds_grid", 0)
         lib.ogs_set_option(b"frontier_parts", 0)
         lib.ogs_set_option(b"frontier_parts_wide", 0)
         lib.ogs_set_option(b"spf_frontier", 1)
@@ -366,7 +368,7 @@ def _batch_dbs(product, kind, opts, srcs, enable_v4, brs, **options):
 MIX = dict(v4Permille=150, anycastPermille=120, minNhPermille=60, drainPermille=50)
 
 
-@pytest.mark.parametrize("stream,frontier", [(1, 0), (1, 1), (2, 0), (2, 1), (4, 1)])
+@pytest.mark.parametrize("stream,frontier", [(1, 0), (1, 1), (2, 0), (2, 1), (4, 1), (5, 1)])
 @pytest.mark.parametrize("enable_v4,brs", [(True, False), (False, True), (True, True)])
 def test_route_stream_fabric_prefix_mix(product, oracle, stream, frontier, enable_v4, brs):
     """Split SPF / route-stream launches vs the fused multi-source kernel on a
@@ -386,7 +388,7 @@ def test_route_stream_fabric_prefix_mix(product, oracle, stream, frontier, enabl
 
 
 @pytest.mark.parametrize("nt", [0, 1, 3])
-@pytest.mark.parametrize("stream", [1, 2, 4])
+@pytest.mark.parametrize("stream", [1, 2, 4, 5])
 def test_route_stream_store_flavours(product, oracle, nt, stream):
     """The RouteDb stream's ordinary (default) and non-temporal 16-B stores
     (route_store_nt bit 1) write the same records: fused and split forms on the
@@ -422,7 +424,7 @@ def test_frontier_seed_row(product, oracle, seed, wide):
     _cmp(a, oracle.gen_route_dbs("fabric", opts, srcs, True, False, True), "seedrow")
 
 
-@pytest.mark.parametrize("stream,frontier", [(1, 0), (1, 1), (2, 0), (2, 1), (4, 1)])
+@pytest.mark.parametrize("stream,frontier", [(1, 0), (1, 1), (2, 0), (2, 1), (4, 1), (5, 1)])
 def test_route_stream_wan_prefix_mix(product, oracle, stream, frontier):
     """700-node WAN, random metrics, overloads and the prefix mix, best-route
     selection on, through every large-topology SPF / RouteDb form."""
@@ -435,7 +437,7 @@ def test_route_stream_wan_prefix_mix(product, oracle, stream, frontier):
     _cmp(a, oracle.gen_route_dbs("wan", opts, srcs, True, False, True), "wanmix")
 
 
-@pytest.mark.parametrize("stream", [1, 2, 4])
+@pytest.mark.parametrize("stream", [1, 2, 4, 5])
 def test_route_stream_three_word_sources(product, oracle, stream):
     """FSW sources of 84 links (36 SSW + 48 RSW, the C3 shape on 4 pods x 2
     planes) keep three next-hop words: the fused kernel, the HBM split and

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Prints the last N dispatches of a rocprofv3 kernel trace (csv) as a
 timeline: start / end offsets (us) from the first of them, duration, queue,
-short kernel name. Usage: trace_timeline.py <k_kernel_trace.csv> [N]"""
+short kernel name (runtime copies / torch kernels left out). Usage: trace_timeline.py <k_kernel_trace.csv> [N]"""
 import csv
 import sys
 
@@ -9,6 +9,8 @@ import sys
 def main():
     rows = list(csv.DictReader(open(sys.argv[1])))
     n = int(sys.argv[2]) if len(sys.argv) > 2 else 12
+    rows = [r for r in rows if "rocclr" not in r["Kernel_Name"] and
+            "elementwise" not in r["Kernel_Name"] and "reduce" not in r["Kernel_Name"]]
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     rows = rows[-n:]
     t0 = int(rows[0]["Start_Timestamp"])
