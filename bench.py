@@ -391,6 +391,15 @@ def c3_launches(torch, M, capi, dev, names, ppn=100, with_sel=False):
         launches.append(dict(br=br, h=h, t=t, o=o, g=g, pt=pt, so=so, U=U, W=W,
                              flags=h["flags"], bytes=float(unit_bytes.sum()),
                              unit_bytes=unit_bytes, names=mine, rows=None))
+    # the width groups are built from the same fabric: one graph / prefix
+    # table serves all of them (ogs_spf_routes_groups) iff the arrays agree
+    same = ("node_base", "row_ptr", "edges", "node_flags", "pfx_base", "adv_off",
+            "adv_node", "adv_metrics", "adv_min_nh", "pfx_flags")
+    h0 = launches[0]["h"]
+    shared = all(np.array_equal(L["h"][k], h0[k]) for L in launches for k in same) and \
+        all(L["flags"] == launches[0]["flags"] for L in launches)
+    for L in launches:
+        L["shared"] = shared
     return launches, N
 
 
@@ -479,9 +488,31 @@ def c3_shard_projection(lib, capi, launches, main, side, world_sizes=(2, 4, 8),
     return out
 
 
+# C3 steps through ogs_spf_routes_groups (one call for every width group,
+# the engine's one-launch form under route_stream 5) when True, else one
+# ogs_spf_routes per group on two streams (--c3-launch per-group)
+C3_GROUPS = [True]
+
+
 def c3_launch_all(lib, capi, launches, main, side):
-    """One C3 step: every width group's ogs_spf_routes, the second group on
-    its own HIP stream (`side`), joined back into `main`."""
+    """One C3 step: every width group's RouteDbs -- one ogs_spf_routes_groups
+    call on `main` (the groups share the graph and prefix table: checked in
+    c3_launches), or per group, the second on its own HIP stream (`side`),
+    joined back into `main`."""
+    if C3_GROUPS[0] and all(L.get("shared") for L in launches):
+        arr = (capi.RouteGroup * len(launches))()
+        for i, L in enumerate(launches):
+            arr[i].units = L["t"]["units"].data_ptr()
+            arr[i].n_units = L["U"]
+            arr[i].nh_words = L["W"]
+            arr[i].out = L["so"]
+        L0 = launches[0]
+        rc = lib.ogs_spf_routes_groups(ctypes.byref(L0["g"]), ctypes.byref(L0["pt"]), arr,
+                                       len(launches), L0["flags"],
+                                       ctypes.c_void_p(main.cuda_stream))
+        if rc != 0:
+            capi.check(lib, rc, "ogs_spf_routes_groups")
+        return
     streams = [main, side] + [main] * max(0, len(launches) - 2)
     fork = torch.cuda.Event()
     fork.record(main)
@@ -1256,6 +1287,9 @@ def main():
                          "on this GPU (the line reports that shard)")
     ap.add_argument("--no-shard-projection", action="store_true",
                     help="C3 at N=1: skip the per-rank shard timings for N=2/4/8")
+    ap.add_argument("--c3-launch", default="groups", choices=["groups", "per-group"],
+                    help="C3 width groups through one ogs_spf_routes_groups call (default) "
+                         "or one ogs_spf_routes per group on two streams")
     ap.add_argument("--c3-order", default="wide-first", choices=["narrow-first", "wide-first"],
                     help="C3: which next-hop width group is dispatched first")
     ap.add_argument("--no-c4", action="store_true", help="skip the C4 link-failure sub-line")
@@ -1269,6 +1303,7 @@ def main():
     ap.add_argument("--launch-check", action="store_true",
                     help="only join the process group and print the rank map (no GPU)")
     args = ap.parse_args()
+    C3_GROUPS[0] = args.c3_launch == "groups"
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         raise SystemExit(launch_ranks(args))

@@ -50,8 +50,9 @@ extern "C" {
  * OGS_ABI_VERSION once at start-up. 3: ogs_spf_out.reached,
  * ogs_area_table.reached, ogs_routes_from_spf(spf_reached), u16 RibPolicy
  * statement ids, ogs_graph.rslot_ext (rows of 511+ edges). 4:
- * ogs_spf_routes_variants writes ogs_route_diff.base_desc_valid back. */
-#define OGS_ABI_VERSION 4
+ * ogs_spf_routes_variants writes ogs_route_diff.base_desc_valid back. 5:
+ * ogs_spf_routes_groups / ogs_route_group. */
+#define OGS_ABI_VERSION 5
 
 /* ---- status codes ------------------------------------------------------ */
 #define OGS_OK 0
@@ -374,6 +375,26 @@ int ogs_spf_routes(const ogs_graph* graph, const ogs_prefix_table* prefixes,
                    const ogs_unit* units /* device */, int32_t n_units,
                    uint32_t flags, int32_t nh_words, ogs_spf_out* out,
                    void* stream);
+
+/* Several unit groups over ONE graph and prefix table, each with its own
+ * next-hop width (nh_words) and outputs (out, by value, as ogs_spf_routes'
+ * *out): the same results as one ogs_spf_routes call per group (a
+ * BatchRunner's width groups, e.g. the C3 fabric's one- and three-word
+ * sources), in as few launches as the engine can -- with "route_stream" 5
+ * on a large shared topology one prep and ONE persistent launch for all
+ * groups, so the widest group's SPFs and every group's route streams share
+ * the CUs. groups: host array; groups with n_units == 0 are skipped. */
+typedef struct ogs_route_group {
+  const ogs_unit* units; /* device, n_units */
+  int32_t n_units;
+  int32_t nh_words;
+  ogs_spf_out out;
+} ogs_route_group;
+
+int ogs_spf_routes_groups(const ogs_graph* graph, const ogs_prefix_table* prefixes,
+                          const ogs_route_group* groups, int32_t n_groups, uint32_t flags,
+                          void* stream);
+
 
 /* RouteDb records of n_units units from SPF state a previous ogs_spf_routes
  * launch left in device memory (spf_dist [U*S_n] uint32, or uint64 with

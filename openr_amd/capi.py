@@ -6,7 +6,7 @@ import ctypes
 from . import LIB_PATH
 
 OGS_OK = 0
-OGS_ABI_VERSION = 4  # include/openr_gpu.h
+OGS_ABI_VERSION = 5  # include/openr_gpu.h
 OGS_F_ENABLE_V4 = 0x01
 OGS_F_V4_OVER_V6 = 0x02
 OGS_F_BEST_ROUTE_SELECTION = 0x04
@@ -21,7 +21,7 @@ EXPORTS = [
     "ogs_ksp_paths", "ogs_ksp2_paths", "ogs_set_option", "ogs_routes_multiarea",
     "ogs_spf_routes_variants", "ogs_rib_policy_apply", "ogs_route_changes_gather",
     "ogs_csr_patch", "ogs_host_alloc", "ogs_host_free", "ogs_routes_from_spf",
-    "ogs_abi_version",
+    "ogs_abi_version", "ogs_spf_routes_groups",
 ]
 
 
@@ -51,6 +51,11 @@ class SpfOut(ctypes.Structure):
                 ("reached", ctypes.c_void_p)]
 
 
+class RouteGroup(ctypes.Structure):
+    _fields_ = [("units", ctypes.c_void_p), ("n_units", ctypes.c_int32),
+                ("nh_words", ctypes.c_int32), ("out", SpfOut)]
+
+
 def load(path=None):
     lib = ctypes.CDLL(path or LIB_PATH)
     lib.ogs_version.restype = ctypes.c_char_p
@@ -63,6 +68,10 @@ def load(path=None):
         ctypes.c_int32, ctypes.c_uint32, ctypes.c_int32, ctypes.POINTER(SpfOut),
         ctypes.c_void_p]
     lib.ogs_spf_routes.restype = ctypes.c_int
+    lib.ogs_spf_routes_groups.argtypes = [
+        ctypes.POINTER(Graph), ctypes.POINTER(PrefixTable), ctypes.POINTER(RouteGroup),
+        ctypes.c_int32, ctypes.c_uint32, ctypes.c_void_p]
+    lib.ogs_spf_routes_groups.restype = ctypes.c_int
     lib.ogs_set_option.argtypes = [ctypes.c_char_p, ctypes.c_int64]
     lib.ogs_set_option.restype = ctypes.c_int
     return lib

@@ -39,6 +39,9 @@ hipError_t launch_spf_routes(const ogs_graph& g, const ogs_prefix_table* pt,
                              const ogs_unit* units, int nUnits, uint32_t flags,
                              int W, const ogs_spf_out& out, hipStream_t stream,
                              int* unsupported);
+hipError_t launch_spf_routes_groups(const ogs_graph& g, const ogs_prefix_table* pt,
+                                    const ogs_route_group* groups, int n, uint32_t flags,
+                                    hipStream_t stream, int* unsupported);
 hipError_t launch_routes_multiarea(const ogs_graph& g, const ogs_prefix_table& pt,
                                    const ogs_area_table& at,
                                    const uint32_t* units, int n,
@@ -335,6 +338,63 @@ int ogs_nh_words_for_degree(int degree) {
     if (words <= w) return w;
   }
   return words;  // sources of more than 512 links: exact width
+}
+
+// Shape checks shared by ogs_spf_routes and ogs_spf_routes_groups.
+static int check_routes_args(const ogs_graph* graph, const ogs_prefix_table* prefixes,
+                             uint32_t flags) {
+  if (!graph->node_base || !graph->row_ptr || !graph->node_flags) {
+    return fail(OGS_E_INVALID, "graph arrays are NULL");
+  }
+  if (graph->max_nodes <= 0 ||
+      uint32_t(graph->max_nodes) > OGS_MAX_NODES_PER_TOPO) {
+    return fail(OGS_E_UNSUPPORTED, "max_nodes outside (0, 2^21]");
+  }
+  if (graph->slot_node && graph->slot_stride != 64 &&
+      graph->slot_stride != 128 && graph->slot_stride != 256) {
+    return fail(OGS_E_INVALID, "slot_stride must be 64, 128 or 256");
+  }
+  if (graph->slot_node && graph->slot_stride < graph->max_nodes) {
+    return fail(OGS_E_INVALID, "slot_stride < max_nodes");
+  }
+  if (graph->slot_edges &&
+      (!graph->slot_node || (graph->slot_degree != 4 && graph->slot_degree != 8))) {
+    return fail(OGS_E_INVALID, "slot_edges needs slot_node and slot_degree 4 or 8");
+  }
+  if (prefixes && (!prefixes->pfx_base || !prefixes->adv_off ||
+                   !prefixes->adv_node || !prefixes->adv_metrics ||
+                   !prefixes->adv_min_nh || !prefixes->pfx_flags)) {
+    return fail(OGS_E_INVALID, "prefix table arrays are NULL");
+  }
+  if ((flags & OGS_F_EXACT_ORDER) && !(flags & OGS_F_WIDE_METRIC)) {
+    return fail(OGS_E_INVALID, "OGS_F_EXACT_ORDER needs OGS_F_WIDE_METRIC");
+  }
+  return OGS_OK;
+}
+
+int ogs_spf_routes_groups(const ogs_graph* graph, const ogs_prefix_table* prefixes,
+                          const ogs_route_group* groups, int32_t n_groups, uint32_t flags,
+                          void* stream) {
+  if (!graph || (!groups && n_groups > 0)) return fail(OGS_E_INVALID, "graph/groups is NULL");
+  if (n_groups < 0) return fail(OGS_E_INVALID, "n_groups < 0");
+  int live = 0;
+  for (int32_t i = 0; i < n_groups; ++i) {
+    if (groups[i].n_units < 0) return fail(OGS_E_INVALID, "n_units < 0");
+    if (groups[i].n_units == 0) continue;
+    if (!groups[i].units) return fail(OGS_E_INVALID, "group units are NULL");
+    if (groups[i].nh_words < 1) return fail(OGS_E_INVALID, "nh_words < 1");
+    ++live;
+  }
+  if (live == 0) return OGS_OK;
+  const int rc = check_routes_args(graph, prefixes, flags);
+  if (rc != OGS_OK) return rc;
+  int unsupported = 0;
+  hipError_t e = ogs::launch_spf_routes_groups(*graph, prefixes, groups, n_groups, flags,
+                                               static_cast<hipStream_t>(stream), &unsupported);
+  if (unsupported) {
+    return fail(OGS_E_UNSUPPORTED, "no SPF path for these shapes");
+  }
+  return e == hipSuccess ? OGS_OK : hipFail(e, "spf_route launch");
 }
 
 int ogs_spf_routes(const ogs_graph* graph, const ogs_prefix_table* prefixes,

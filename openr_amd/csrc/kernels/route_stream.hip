@@ -36,6 +36,7 @@
 #include "openr_gpu.h"
 #include "route_core.h"
 #include "route_stream.h"
+#include "spf_lds.h"
 #include "spf_core.h"
 
 namespace ogs {
@@ -190,16 +191,6 @@ hipError_t launch_frontier_routes(const ogs_graph& g, const ogs_prefix_table& pt
                                   int nUnits, uint32_t flags, int W,
                                   const ogs_spf_out& out, void* scratch,
                                   hipStream_t stream);
-size_t lds_scratch_bytes(const ogs_graph& g, int W, int nUnits);
-hipError_t launch_lds_prep(const ogs_graph& g, const ogs_prefix_table* pt, uint32_t* key,
-                           int W, int nUnits, void* scratch, hipStream_t stream);
-hipError_t launch_spf_lds_routes(const ogs_graph& g, const ogs_prefix_table& pt,
-                                 const uint32_t* key, const ogs_unit* units, int nUnits,
-                                 uint32_t flags, int W, uint32_t* dist, uint32_t* nh,
-                                 const ogs_spf_out& out, void* scratch, hipStream_t stream);
-hipError_t launch_spf_lds(const ogs_graph& g, const ogs_unit* units, int nUnits,
-                          uint32_t flags, int W, uint32_t* dist, uint32_t* nh,
-                          void* scratch, hipStream_t stream);
 void stream_parts(int nUnits, int W, int P, int* parts);
 
 template <int W>
@@ -320,8 +311,8 @@ bool try_ms_stream(const ogs_graph& g, const ogs_prefix_table& pt,
     if (*err != hipSuccess) return true;
     uint32_t* d = static_cast<uint32_t*>(spf.dist);
     if (g_routeStream == 5) {
-      *err = launch_spf_lds_routes(g, pt, key, units, nUnits, flags, W, d, spf.nh, out,
-                                   chunkScratch, stream);
+      const LdsRouteGroup one{units, nUnits, W, d, spf.nh, out};
+      *err = launch_spf_lds_routes(g, pt, key, &one, 1, flags, chunkScratch, stream);
       return true;
     }
     *err = launch_spf_lds(g, units, nUnits, flags, W, d, spf.nh, chunkScratch, stream);
@@ -365,4 +356,74 @@ bool try_ms_stream(const ogs_graph& g, const ogs_prefix_table& pt,
   return true;
 }
 
+
+hipError_t launch_spf_routes(const ogs_graph& g, const ogs_prefix_table* pt,
+                             const ogs_unit* units, int nUnits, uint32_t flags, int W,
+                             const ogs_spf_out& out, hipStream_t stream, int* unsupported);
+int small_unit_width();
+
+// ogs_spf_routes_groups: every group's RouteDbs over one graph / prefix
+// table. With route_stream 5 on a large shared topology whose image fits
+// LDS for the widest group: one prep launch and ONE persistent launch for
+// all groups (widest first). Otherwise one launch_spf_routes per group, in
+// order on the stream -- the same outputs either way.
+hipError_t launch_spf_routes_groups(const ogs_graph& g, const ogs_prefix_table* pt,
+                                    const ogs_route_group* groups, int n, uint32_t flags,
+                                    hipStream_t stream, int* unsupported) {
+  std::vector<LdsRouteGroup> lg;
+  int Wmax = 1, U = 0;
+  for (int i = 0; i < n; ++i) {
+    if (groups[i].n_units <= 0) continue;
+    lg.push_back(LdsRouteGroup{groups[i].units, groups[i].n_units, groups[i].nh_words,
+                               nullptr, nullptr, groups[i].out});
+    Wmax = std::max(Wmax, groups[i].nh_words);
+    U += groups[i].n_units;
+  }
+  const size_t Sp = pt ? size_t(pt->max_prefixes) : 0;
+  bool one = g_routeStream == 5 && pt && Sp > 0 && g.edge_src && g.max_nodes > 256 &&
+      !(flags & (OGS_F_EXACT_ORDER | OGS_F_WIDE_METRIC)) && small_unit_width() == -1 &&
+      !lg.empty() && lg.size() <= 4 && Wmax <= 4;
+  const size_t ldsBytes = one ? lds_scratch_bytes(g, Wmax, U) : 0;
+  if (!ldsBytes) {
+    for (const LdsRouteGroup& x : lg) {
+      const hipError_t e = launch_spf_routes(g, pt, x.units, x.n, flags, x.W, x.out, stream,
+                                             unsupported);
+      if (e != hipSuccess || *unsupported) return e;
+    }
+    return hipSuccess;
+  }
+  std::stable_sort(lg.begin(), lg.end(),
+                   [](const LdsRouteGroup& a, const LdsRouteGroup& b) { return a.W > b.W; });
+  const size_t Sn = size_t(g.max_nodes);
+  const size_t keyBytes = round256(size_t(g.num_topos) * Sp * 4);
+  size_t rows = 0;
+  for (const LdsRouteGroup& x : lg) {
+    if (!x.out.dist) rows += round256(size_t(x.n) * Sn * 4);
+    if (!x.out.nh) rows += round256(size_t(x.n) * x.W * Sn * 4);
+  }
+  void* ws = nullptr;
+  hipError_t e = workspace(keyBytes + round256(ldsBytes) + rows, stream, &ws);
+  if (e != hipSuccess) return e;
+  char* base = static_cast<char*>(ws);
+  uint32_t* key = reinterpret_cast<uint32_t*>(base);
+  void* scratch = base + keyBytes;
+  char* at = base + keyBytes + round256(ldsBytes);
+  for (LdsRouteGroup& x : lg) {
+    if (x.out.dist) {
+      x.dist = static_cast<uint32_t*>(x.out.dist);
+    } else {
+      x.dist = reinterpret_cast<uint32_t*>(at);
+      at += round256(size_t(x.n) * Sn * 4);
+    }
+    if (x.out.nh) {
+      x.nh = x.out.nh;
+    } else {
+      x.nh = reinterpret_cast<uint32_t*>(at);
+      at += round256(size_t(x.n) * x.W * Sn * 4);
+    }
+  }
+  e = launch_lds_prep(g, pt, key, Wmax, U, scratch, stream);
+  if (e != hipSuccess) return e;
+  return launch_spf_lds_routes(g, *pt, key, lg.data(), int(lg.size()), flags, scratch, stream);
+}
 }  // namespace ogs

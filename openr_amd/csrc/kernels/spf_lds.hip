@@ -33,6 +33,7 @@
 #include "openr_gpu.h"
 #include "route_core.h"
 #include "route_stream.h"
+#include "spf_lds.h"
 #include "spf_core.h"
 
 namespace ogs {
@@ -246,22 +247,73 @@ __device__ uint32_t g_ldsStamps[4 * kLdsDiagWgs * 32];
 // with fire-and-forget LDS atomics, and every chunk record is visited only
 // in the rounds its node is active (each once, on unit-weight BFS layers).
 //
-// spf_lds_body runs that solver for the units its driver hands it:
-// driver(solve) calls solve(u) for each unit index u of this workgroup (the
-// image of unit u's topology is staged on first use and kept).
-template <int W, typename Driver>
-__device__ __forceinline__ void spf_lds_body(
+// Per-workgroup staging state (the topology whose image is in LDS) and the
+// diagnostics policy of spf_lds_unit: NoDiag in product builds; the
+// OGS_STAMPS build's LdsStamps records the first unit's phase cycles.
+struct LdsWg {
+  uint32_t staged = 0xFFFFFFFFu;
+  uint32_t C = 0, uniform = 0, w0 = 0, N = 0, e0 = 0;
+};
+
+struct NoDiag {
+  __device__ void mark(uint32_t) {}
+  __device__ void rounds(uint32_t) {}
+  __device__ void queued(uint32_t) {}
+  __device__ void unit_done() {}
+};
+
+#ifdef OGS_STAMPS
+struct LdsStamps {
+  uint32_t* diag;
+  bool on, first = true;
+  uint64_t k0, tr;
+  uint32_t units = 0, q = 0;
+  __device__ LdsStamps(int W)
+      : diag(g_ldsStamps + (size_t(W - 1) * kLdsDiagWgs + blockIdx.x) * 32u),
+        on(threadIdx.x == 0u && blockIdx.x < kLdsDiagWgs),
+        k0(__builtin_amdgcn_s_memtime()),
+        tr(k0) {}
+  __device__ void mark(uint32_t slot) {  // cycles since the last mark of the first unit
+    const uint64_t now = __builtin_amdgcn_s_memtime();
+    if (on && first && slot < 32u) diag[slot] = uint32_t(now - tr);
+    tr = now;
+  }
+  __device__ void rounds(uint32_t r) {
+    if (on && first) diag[2] = r;
+  }
+  __device__ void queued(uint32_t n) { q += n; }
+  __device__ void unit_done() {
+    if (on && first) {
+      diag[1] = uint32_t(__builtin_amdgcn_s_memtime() - k0);  // staging + first unit
+      diag[5] = q;
+    }
+    first = false;
+    ++units;
+  }
+  __device__ void finish() {
+    if (on) {
+      diag[3] = units;
+      diag[4] = uint32_t(__builtin_amdgcn_s_memtime() - k0);
+    }
+  }
+};
+#endif
+
+// spf_lds_unit: the SPF of unit u (index into the launch's dist / nh rows)
+// by this workgroup, its topology's image staged on first use and kept.
+// smem: the dynamic LDS (image block, then the unit's state laid out by L,
+// whose next-hop region may be sized for a wider W than this one).
+template <int W, typename Diag>
+__device__ __forceinline__ void spf_lds_unit(
     const ogs_graph& g, const LdsImage& L, const uint8_t* __restrict__ img,
-    const uint2* __restrict__ mm, uint32_t nEB, const ogs_unit* __restrict__ units,
-    uint32_t flags, uint32_t* __restrict__ oDist, uint32_t* __restrict__ oNh,
-    Driver&& driver) {
+    const uint2* __restrict__ mm, uint32_t nEB, const ogs_unit unit, uint32_t u,
+    uint32_t flags, uint32_t* __restrict__ oDist, uint32_t* __restrict__ oNh, char* smem,
+    uint32_t* qCount, LdsWg& wg, Diag& dg) {
   constexpr uint32_t kInf = 0xFFFFFFFFu;
   constexpr uint32_t B = kLdsBlock;
   const uint32_t tid = threadIdx.x, lane = tid & 63u;
   const uint32_t Sn = uint32_t(g.max_nodes);
   const bool hop = (flags & OGS_F_HOP_METRIC) != 0u;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  __shared__ uint32_t qCount[2];
   char* blk = smem;
   const uint16_t* eimg = reinterpret_cast<const uint16_t*>(blk + L.eimg);
   const uint16_t* cnode = reinterpret_cast<const uint16_t*>(blk + L.cnode);
@@ -272,26 +324,14 @@ __device__ __forceinline__ void spf_lds_body(
   uint32_t* nh = reinterpret_cast<uint32_t*>(st + L.nh);
   uint8_t* stamp = reinterpret_cast<uint8_t*>(st + L.stamp);
   uint16_t* queue = reinterpret_cast<uint16_t*>(st + L.queue);
-
-  uint32_t staged = 0xFFFFFFFFu;
-  uint32_t C = 0, uniform = 0, w0 = 0, N = 0, e0 = 0;
-#ifdef OGS_STAMPS
-  uint32_t* diag = g_ldsStamps + (size_t(W - 1) * kLdsDiagWgs + blockIdx.x) * 32u;
-  const bool diagOn = tid == 0u && blockIdx.x < kLdsDiagWgs;
-  const uint64_t k0 = __builtin_amdgcn_s_memtime();
-  uint64_t tr = k0;
-  bool firstUnit = true;
-  uint32_t nUnitsDone = 0;
-  auto mark = [&](uint32_t slot) {  // cycles since the last mark of the first unit
-    const uint64_t now = __builtin_amdgcn_s_memtime();
-    if (diagOn && firstUnit && slot < 32u) diag[slot] = uint32_t(now - tr);
-    tr = now;
-  };
-#else
-  auto mark = [](uint32_t) {};
-#endif
-  auto solve = [&](uint32_t u) {
-    const ogs_unit unit = units[u];
+  uint32_t& staged = wg.staged;
+  uint32_t& C = wg.C;
+  uint32_t& uniform = wg.uniform;
+  uint32_t& w0 = wg.w0;
+  uint32_t& N = wg.N;
+  uint32_t& e0 = wg.e0;
+  auto mark = [&](uint32_t slot) { dg.mark(slot); };
+  {
     if (unit.topo != staged) {
       __syncthreads();  // the previous unit's state reads are done
       const uint8_t* hdr = img + size_t(unit.topo) * L.stride;
@@ -349,9 +389,6 @@ __device__ __forceinline__ void spf_lds_body(
       stamp[t] = 2;
     }
     __syncthreads();
-#ifdef OGS_STAMPS
-    uint32_t queued = 0;
-#endif
     // rounds 2.., specialised on whether the weight is one constant (no
     // per-edge weight reads at all) or read per edge from the CSR
     auto rounds = [&](auto constant, auto layered) {
@@ -432,9 +469,7 @@ __device__ __forceinline__ void spf_lds_body(
         mark(8u + 3u * (r - 2u));
         const uint32_t nq = *qc;
         if (nq == 0u) break;  // nothing stamped r: the fixpoint
-#ifdef OGS_STAMPS
-        queued += nq;
-#endif
+        dg.queued(nq);
         if (tid == 0u) qCount[(r + 1u) & 1u] = 0u;  // next round's counter
         // the queue is walked transposed: lane l of a wave takes entries
         // l * M + j (M = ceil(nq / 64)), so the lanes of one instruction
@@ -472,9 +507,7 @@ __device__ __forceinline__ void spf_lds_body(
           }
           __syncthreads();
           mark(8u + 3u * (r - 2u) + 2u);
-#ifdef OGS_STAMPS
-          if (diagOn && firstUnit) diag[2] = r;
-#endif
+          dg.rounds(r);
           continue;
         }
         // (1) distances. A push with cand < dt (dt read during this pass;
@@ -538,9 +571,7 @@ __device__ __forceinline__ void spf_lds_body(
         }
         __syncthreads();
         mark(8u + 3u * (r - 2u) + 2u);
-#ifdef OGS_STAMPS
-        if (diagOn && firstUnit) diag[2] = r;
-#endif
+        dg.rounds(r);
       }
     };
     if (constW && wc > 0u) {
@@ -550,30 +581,14 @@ __device__ __forceinline__ void spf_lds_body(
     } else {
       rounds(std::false_type{}, std::false_type{});
     }
-#ifdef OGS_STAMPS
-    if (diagOn && firstUnit) diag[5] = queued;
-#endif
     for (uint32_t v = tid; v < N; v += B) {
       oDist[size_t(u) * Sn + v] = dist[v];
 #pragma unroll
       for (int w = 0; w < W; ++w) oNh[(size_t(u) * W + w) * Sn + v] = nh[v * W + w];
     }
     __syncthreads();  // state and outputs of this unit done before the next
-#ifdef OGS_STAMPS
-    if (firstUnit) {
-      if (diagOn) diag[1] = uint32_t(__builtin_amdgcn_s_memtime() - k0);  // staging + first unit
-      firstUnit = false;
-    }
-    ++nUnitsDone;
-#endif
-  };
-  driver(solve);
-#ifdef OGS_STAMPS
-  if (diagOn) {
-    diag[3] = nUnitsDone;
-    diag[4] = uint32_t(__builtin_amdgcn_s_memtime() - k0);
+    dg.unit_done();
   }
-#endif
 }
 
 template <int W>
@@ -581,9 +596,21 @@ __global__ __launch_bounds__(kLdsBlock) void spf_lds_kernel(
     ogs_graph g, LdsImage L, const uint8_t* __restrict__ img, const uint2* __restrict__ mm,
     uint32_t nEB, const ogs_unit* __restrict__ units, int nUnits, uint32_t flags,
     uint32_t* __restrict__ oDist, uint32_t* __restrict__ oNh) {
-  spf_lds_body<W>(g, L, img, mm, nEB, units, flags, oDist, oNh, [&](auto& solve) {
-    for (int u = int(blockIdx.x); u < nUnits; u += int(gridDim.x)) solve(uint32_t(u));
-  });
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  __shared__ uint32_t qCount[2];
+  LdsWg wg;
+#ifdef OGS_STAMPS
+  LdsStamps dg(W);
+#else
+  NoDiag dg;
+#endif
+  for (int u = int(blockIdx.x); u < nUnits; u += int(gridDim.x)) {
+    spf_lds_unit<W>(g, L, img, mm, nEB, units[u], uint32_t(u), flags, oDist, oNh, smem, qCount,
+                    wg, dg);
+  }
+#ifdef OGS_STAMPS
+  dg.finish();
+#endif
 }
 
 // The unit's SPF state as published in HBM (ogs_spf_out layout), for the
@@ -599,119 +626,170 @@ struct PublishedView {
   }
 };
 
-// SPF and RouteDb stream in ONE persistent launch (route_stream 5): each
-// workgroup takes items from a device-wide counter --
-//   items [0, G): the SPF of unit i (G = the grid: every workgroup starts
-//     with one);
-//   then per unit b, P + 1 items: the SPF of unit G + b (when there is
-//     one), then the P prefix ranges of unit b's route stream.
-// So SPFs stay G units ahead of the streams, a stream item never waits for
-// an SPF that is not already taken by a running workgroup (it was handed
-// out earlier), and a shard with a few more units than CUs streams the
-// other units' rows while its last SPFs run instead of a whole SPF launch
-// waiting on them. Hand-off (MI355X_MICROARCH.md, inter-workgroup
-// visibility): the SPF's dist / nh rows are plain stores, drained by every
-// wave, then a barrier, lane 0's agent release and a relaxed agent flag
-// store; a stream item's lane 0 polls the flag (relaxed agent loads), takes
-// an agent acquire, and the workgroup reads the rows after a barrier.
-template <int W, bool OUTS3>
-__global__ __launch_bounds__(kLdsBlock) void spf_lds_route_kernel(
-    ogs_graph g, ogs_prefix_table pt, const uint32_t* __restrict__ key, LdsImage L,
-    const uint8_t* __restrict__ img, const uint2* __restrict__ mm, uint32_t nEB,
-    const ogs_unit* __restrict__ units, int nUnits, uint32_t flags,
-    uint32_t* __restrict__ oDist, uint32_t* __restrict__ oNh, ogs_spf_out out,
-    uint32_t* __restrict__ ctr, uint32_t* __restrict__ ready, uint32_t P) {
-  __shared__ uint32_t item;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
+// Unit groups of one launch of the one-launch form: each group's units
+// share a next-hop width W and output arrays (ogs_spf_routes_groups). Global
+// unit index gu = group base + local index; groups are laid out widest
+// first (their SPFs are the slowest, so they start first).
+constexpr int kMaxLdsGroups = 4;
+struct LdsGroup {
+  const ogs_unit* units;
+  uint32_t n, base, W, outs3;
+  uint32_t* dist;  // [n * Sn] published SPF rows
+  uint32_t* nh;    // [n * W * Sn]
+  ogs_spf_out out;
+};
+struct LdsGroups {
+  LdsGroup g[kMaxLdsGroups];
+  uint32_t n;
+};
+
+// One stream item: prefix range `part` (of P) of local unit u of group grp,
+// from the published SPF rows: per-node records into LDS, then the rows.
+template <int W>
+__device__ __forceinline__ void lds_stream_item(const ogs_graph& g, const ogs_prefix_table& pt,
+                                                const uint32_t* __restrict__ key,
+                                                const LdsGroup& grp, uint32_t u, uint32_t part,
+                                                uint32_t P, uint32_t flags, uint32_t* rec0) {
   constexpr uint32_t kInf = 0xFFFFFFFFu;
   const uint32_t tid = threadIdx.x;
-  const uint32_t U = uint32_t(nUnits);
-  const uint32_t G = min(U, gridDim.x);
-  const uint32_t total = G + U * (P + 1u);
   const uint32_t Sn = uint32_t(g.max_nodes), Sp = uint32_t(pt.max_prefixes);
   const RouteCfg cfg{(flags & OGS_F_ENABLE_V4) != 0, (flags & OGS_F_V4_OVER_V6) != 0,
                      (flags & OGS_F_BEST_ROUTE_SELECTION) != 0};
-  spf_lds_body<W>(g, L, img, mm, nEB, units, flags, oDist, oNh, [&](auto& solve) {
-    for (;;) {
-      if (tid == 0u) item = atomicAdd(ctr, 1u);
-      __syncthreads();
-      const uint32_t i = item;
-      __syncthreads();  // every lane has read item before lane 0 takes the next
-      if (i >= total) break;
-      uint32_t u = i, part = 0;
-      bool spf = true;
-      if (i >= G) {
-        const uint32_t j = i - G;
-        u = j / (P + 1u);
-        const uint32_t r = j - u * (P + 1u);
-        if (r == 0u) {
-          u += G;
-          if (u >= U) continue;
-        } else {
-          spf = false;
-          part = r - 1u;
-        }
-      }
-      if (spf) {
-        solve(u);  // ends with the dist / nh row stores and a barrier
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (tid == 0u) {
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          __hip_atomic_store(&ready[u], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        continue;
-      }
-      // stream item: prefix range `part` of unit u
-      if (tid == 0u) {
-        while (__hip_atomic_load(&ready[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
-          __builtin_amdgcn_s_sleep(8);
-        }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      __syncthreads();
-      const ogs_unit unit = units[u];
-      const uint32_t t = unit.topo, s = unit.src;
-      const uint32_t nb = g.node_base[t];
-      const uint32_t N = g.node_base[t + 1] - nb;
-      const uint8_t* __restrict__ nflags = g.node_flags + nb;
-      const PublishedView<W> sv{oDist + size_t(u) * Sn, oNh + size_t(u) * W * Sn, Sn};
-      // per-node records in the state region of LDS (the image stays)
-      uint32_t* rMeta = reinterpret_cast<uint32_t*>(smem + L.block);
-      uint32_t* rMetric = rMeta + Sn;
-      uint32_t* rMask = rMetric + Sn;  // [W][Sn]
-      for (uint32_t v = tid; v < N; v += kLdsBlock) {
-        const uint32_t d = sv.dist(v);
-        uint32_t m[W], cnt = 0;
+  const ogs_unit unit = grp.units[u];
+  const uint32_t t = unit.topo, s = unit.src;
+  const uint32_t nb = g.node_base[t];
+  const uint32_t N = g.node_base[t + 1] - nb;
+  const uint8_t* __restrict__ nflags = g.node_flags + nb;
+  const PublishedView<W> sv{grp.dist + size_t(u) * Sn, grp.nh + size_t(u) * W * Sn, Sn};
+  uint32_t* rMeta = rec0;
+  uint32_t* rMetric = rMeta + Sn;
+  uint32_t* rMask = rMetric + Sn;  // [W][Sn]
+  for (uint32_t v = tid; v < N; v += kLdsBlock) {
+    const uint32_t d = sv.dist(v);
+    uint32_t m[W], cnt = 0;
 #pragma unroll
-        for (int w = 0; w < W; ++w) {
-          m[w] = sv.nh(v, w);
-          cnt += __popc(m[w]);
-        }
-        rMeta[v] = node_route_meta(v, s, d != kInf, cnt, nflags[v]);
-        rMetric[v] = (v == s) ? kInf : d;
-#pragma unroll
-        for (int w = 0; w < W; ++w) rMask[w * Sn + v] = m[w];
-      }
-      __syncthreads();
-      const uint32_t p0 = pt.pfx_base[t];
-      const uint32_t Pn = pt.pfx_base[t + 1] - p0;
-      const uint32_t span = ((Pn + P - 1u) / P + 3u) & ~3u;
-      const uint32_t lo = min(Pn, part * span), hi = min(Pn, lo + span);
-      auto rec = [&](uint32_t v, Rec<W>& r) {
-        r.meta = rMeta[v];
-        r.metric = rMetric[v];
-#pragma unroll
-        for (int w = 0; w < W; ++w) r.mask[w] = rMask[w * Sn + v];
-      };
-      stream_routes<W, false, OUTS3, kLdsBlock>(pt, key + size_t(t) * Sp, p0, Pn, Sp, u, s,
-                                                nflags, sv, cfg, out, rec, nullptr,
-                                                (flags & kFlagNtStores) != 0, lo, hi);
-      __syncthreads();  // the records are read before the next item reuses LDS
+    for (int w = 0; w < W; ++w) {
+      m[w] = sv.nh(v, w);
+      cnt += __popc(m[w]);
     }
-  });
+    rMeta[v] = node_route_meta(v, s, d != kInf, cnt, nflags[v]);
+    rMetric[v] = (v == s) ? kInf : d;
+#pragma unroll
+    for (int w = 0; w < W; ++w) rMask[w * Sn + v] = m[w];
+  }
+  __syncthreads();
+  const uint32_t p0 = pt.pfx_base[t];
+  const uint32_t Pn = pt.pfx_base[t + 1] - p0;
+  const uint32_t span = ((Pn + P - 1u) / P + 3u) & ~3u;
+  const uint32_t lo = min(Pn, part * span), hi = min(Pn, lo + span);
+  auto rec = [&](uint32_t v, Rec<W>& r) {
+    r.meta = rMeta[v];
+    r.metric = rMetric[v];
+#pragma unroll
+    for (int w = 0; w < W; ++w) r.mask[w] = rMask[w * Sn + v];
+  };
+  const bool nt = (flags & kFlagNtStores) != 0;
+  if (grp.outs3) {
+    stream_routes<W, false, true, kLdsBlock>(pt, key + size_t(t) * Sp, p0, Pn, Sp, u, s, nflags,
+                                             sv, cfg, grp.out, rec, nullptr, nt, lo, hi);
+  } else {
+    stream_routes<W, false, false, kLdsBlock>(pt, key + size_t(t) * Sp, p0, Pn, Sp, u, s,
+                                              nflags, sv, cfg, grp.out, rec, nullptr, nt, lo,
+                                              hi);
+  }
+  __syncthreads();  // the records are read before the next item reuses LDS
+}
+
+// SPF and RouteDb stream in ONE persistent launch (route_stream 5): each
+// workgroup takes items from a device-wide counter --
+//   items [0, G): the SPF of unit i (G = min(units, grid): every workgroup
+//     starts with one);
+//   then per unit b, P + 1 items: the SPF of unit G + b (when there is
+//     one), then the P prefix ranges of unit b's route stream
+// (unit = global index over the groups). So SPFs stay G units ahead of the
+// streams, a stream item never waits for an SPF that is not already taken
+// by a running workgroup (it was handed out earlier), and a shard with a
+// few more units than CUs streams the other units' rows while its last
+// SPFs run instead of a whole SPF launch waiting on them. Hand-off
+// (MI355X_MICROARCH.md, inter-workgroup visibility): the SPF's dist / nh
+// rows are plain stores, drained by every wave, then a barrier, lane 0's
+// agent release and a relaxed agent flag store; a stream item's lane 0
+// polls the flag (relaxed agent loads), takes an agent acquire, and the
+// workgroup reads the rows after a barrier.
+__global__ __launch_bounds__(kLdsBlock) void spf_lds_route_kernel(
+    ogs_graph g, ogs_prefix_table pt, const uint32_t* __restrict__ key, LdsImage L,
+    const uint8_t* __restrict__ img, const uint2* __restrict__ mm, uint32_t nEB,
+    LdsGroups grps, uint32_t flags, uint32_t* __restrict__ ctr, uint32_t* __restrict__ ready,
+    uint32_t P) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  __shared__ uint32_t qCount[2];
+  __shared__ uint32_t item;
+  const uint32_t tid = threadIdx.x;
+  const LdsGroup& last = grps.g[grps.n - 1u];
+  const uint32_t U = last.base + last.n;
+  const uint32_t G = min(U, gridDim.x);
+  const uint32_t total = G + U * (P + 1u);
+  LdsWg wg;
+  NoDiag dg;
+  for (;;) {
+    if (tid == 0u) item = atomicAdd(ctr, 1u);
+    __syncthreads();
+    const uint32_t i = item;
+    __syncthreads();  // every lane has read item before lane 0 takes the next
+    if (i >= total) break;
+    uint32_t gu = i, part = 0;
+    bool spf = true;
+    if (i >= G) {
+      const uint32_t j = i - G;
+      gu = j / (P + 1u);
+      const uint32_t r = j - gu * (P + 1u);
+      if (r == 0u) {
+        gu += G;
+        if (gu >= U) continue;
+      } else {
+        spf = false;
+        part = r - 1u;
+      }
+    }
+    uint32_t gi = 0;
+    while (gi + 1u < grps.n && gu >= grps.g[gi + 1u].base) ++gi;
+    const LdsGroup& grp = grps.g[gi];
+    const uint32_t u = gu - grp.base;
+    if (spf) {
+      const ogs_unit unit = grp.units[u];
+      switch (grp.W) {
+        case 1: spf_lds_unit<1>(g, L, img, mm, nEB, unit, u, flags, grp.dist, grp.nh, smem, qCount, wg, dg); break;
+        case 2: spf_lds_unit<2>(g, L, img, mm, nEB, unit, u, flags, grp.dist, grp.nh, smem, qCount, wg, dg); break;
+        case 3: spf_lds_unit<3>(g, L, img, mm, nEB, unit, u, flags, grp.dist, grp.nh, smem, qCount, wg, dg); break;
+        default: spf_lds_unit<4>(g, L, img, mm, nEB, unit, u, flags, grp.dist, grp.nh, smem, qCount, wg, dg); break;
+      }
+      // publish: every wave's row stores drained, barrier, release, flag
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0u) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(&ready[gu], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      continue;
+    }
+    if (tid == 0u) {
+      while (__hip_atomic_load(&ready[gu], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+        __builtin_amdgcn_s_sleep(8);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    // the per-node records go to the state region (the image stays)
+    uint32_t* rec0 = reinterpret_cast<uint32_t*>(smem + L.block);
+    switch (grp.W) {
+      case 1: lds_stream_item<1>(g, pt, key, grp, u, part, P, flags, rec0); break;
+      case 2: lds_stream_item<2>(g, pt, key, grp, u, part, P, flags, rec0); break;
+      case 3: lds_stream_item<3>(g, pt, key, grp, u, part, P, flags, rec0); break;
+      default: lds_stream_item<4>(g, pt, key, grp, u, part, P, flags, rec0); break;
+    }
+  }
 }
 
 int num_cus() {
@@ -803,43 +881,42 @@ hipError_t launch_spf_lds(const ogs_graph& g, const ogs_unit* units, int nUnits,
 int g_ldsParts = 4;
 int g_ldsGrid = 0;
 
-// SPF + RouteDb stream in one persistent launch (spf_lds_route_kernel)
-// after launch_lds_prep with keys; dist / nh are the published SPF rows.
+// SPF + RouteDb stream of every group in one persistent launch
+// (spf_lds_route_kernel) after launch_lds_prep (keys, and the image laid out
+// for the widest group; nUnits = all groups' units). groups: n <= 4, widest
+// first, each with its published dist / nh rows.
 hipError_t launch_spf_lds_routes(const ogs_graph& g, const ogs_prefix_table& pt,
-                                 const uint32_t* key, const ogs_unit* units, int nUnits,
-                                 uint32_t flags, int W, uint32_t* dist, uint32_t* nh,
-                                 const ogs_spf_out& out, void* scratch, hipStream_t stream) {
-  const LdsImage L = lds_image(g, W);
-  const LdsScratch S = lds_scratch(g, L, nUnits);
+                                 const uint32_t* key, const LdsRouteGroup* groups, int n,
+                                 uint32_t flags, void* scratch, hipStream_t stream) {
+  if (n < 1 || n > kMaxLdsGroups) return hipErrorInvalidValue;
+  int Wmax = 1, U = 0;
+  LdsGroups G{};
+  G.n = uint32_t(n);
+  for (int i = 0; i < n; ++i) {
+    const LdsRouteGroup& x = groups[i];
+    if (x.W < 1 || x.W > 4) return hipErrorInvalidValue;
+    Wmax = std::max(Wmax, x.W);
+    G.g[i] = LdsGroup{x.units, uint32_t(x.n), uint32_t(U), uint32_t(x.W),
+                      (x.out.meta && x.out.metric && x.out.mask && !x.out.sel) ? 1u : 0u,
+                      x.dist, x.nh, x.out};
+    U += x.n;
+  }
+  const LdsImage L = lds_image(g, Wmax);
+  const LdsScratch S = lds_scratch(g, L, U);
   uint8_t* base = static_cast<uint8_t*>(scratch);
   const uint2* mm = reinterpret_cast<const uint2*>(base + S.mm);
   uint32_t* ctr = reinterpret_cast<uint32_t*>(base + S.ctr);
   uint32_t* ready = reinterpret_cast<uint32_t*>(base + S.ready);
-  const uint32_t recs = uint32_t(g.max_nodes) * uint32_t(2 + W) * 4u;
+  const uint32_t recs = uint32_t(g.max_nodes) * uint32_t(2 + Wmax) * 4u;
   const uint32_t lds = L.block + std::max(L.state, recs);
   const int grid = std::max(1, g_ldsGrid > 0 ? g_ldsGrid : num_cus());
   const uint32_t P = uint32_t(std::max(1, g_ldsParts));
   if (g_routeStoreNt & 1) flags |= kFlagNtStores;
-  const bool outs3 = out.meta && out.metric && out.mask && !out.sel;
-  auto go = [&](auto k) {
-    hipError_t a = allow_lds(k, lds);
-    if (a != hipSuccess) return a;
-    hipLaunchKernelGGL(k, dim3(grid), dim3(kLdsBlock), lds, stream, g, pt, key, L,
-                       static_cast<const uint8_t*>(base), mm, S.nEB, units, nUnits, flags,
-                       dist, nh, out, ctr, ready, P);
-    return hipGetLastError();
-  };
-  switch (W * 2 + (outs3 ? 1 : 0)) {
-    case 2: return go(spf_lds_route_kernel<1, false>);
-    case 3: return go(spf_lds_route_kernel<1, true>);
-    case 4: return go(spf_lds_route_kernel<2, false>);
-    case 5: return go(spf_lds_route_kernel<2, true>);
-    case 6: return go(spf_lds_route_kernel<3, false>);
-    case 7: return go(spf_lds_route_kernel<3, true>);
-    case 8: return go(spf_lds_route_kernel<4, false>);
-    case 9: return go(spf_lds_route_kernel<4, true>);
-    default: return hipErrorInvalidValue;
-  }
+  hipError_t a = allow_lds(spf_lds_route_kernel, lds);
+  if (a != hipSuccess) return a;
+  hipLaunchKernelGGL(spf_lds_route_kernel, dim3(grid), dim3(kLdsBlock), lds, stream, g, pt, key,
+                     L, static_cast<const uint8_t*>(base), mm, S.nEB, G, flags, ctr, ready, P);
+  return hipGetLastError();
 }
 
 }  // namespace ogs

@@ -56,6 +56,7 @@ def main():
     # variant (options are process-wide and would otherwise carry over)
     keys = {kv.split("=")[0] for v in a.variants for kv in filter(None, v.split(","))}
     keys.discard("lib")
+    keys.discard("c3groups")  # bench.C3_GROUPS: 1 one groups call, 0 per-group streams
     libs = {"": lib}
     if any("lib=base" in v for v in a.variants):
         libs["base"] = capi.load(os.path.join(ROOT, "openr_amd", "lib", "libopenr_gpu_base.so"))
@@ -66,11 +67,12 @@ def main():
     def apply(v):
         """Sets variant v's options; returns the library it runs through."""
         use = libs["base"] if "lib=base" in v else lib
+        bench.C3_GROUPS[0] = "c3groups=0" not in v
         for k in keys:
             use.ogs_set_option(k.encode(), DEFAULTS[k])  # the base may lack newer knobs
         for kv in filter(None, v.split(",")):
             k, x = kv.split("=")
-            if k != "lib":
+            if k not in ("lib", "c3groups"):
                 capi.check(use, use.ogs_set_option(k.encode(), int(x)), k)
         return use
 
