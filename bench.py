@@ -543,27 +543,29 @@ def c3_digest(L, threads=16):
     return shard.combine_digests(d)
 
 
+C3_CPU_REPS = 5
+
+
 def cpu_baseline_c3(N):
     """refcpu buildRouteDb(s) for a stratified sample of the 2,080 sources
     (every 130th name: 3 SSW, 2 FSW, 11 RSW) on T threads with private
-    replicas, and 2 sources (1 SSW, 1 RSW) on 1 thread; 3 reps each (one
-    source's build takes seconds on refcpu, so >= 5 reps would dominate the
-    run); extrapolated to whole-node builds/s = 1 / (mean s per source x
-    2080 / threads)."""
+    replicas, and 2 sources (1 SSW, 1 RSW) on 1 thread; 5 reps each (about
+    2 s per rep on T threads and 4 s on one); extrapolated to whole-node
+    builds/s = 1 / (mean s per source x 2080 / threads)."""
     R = oracle()
     T = cpu_threads()
     names = c3_source_names()
     out = {}
     for threads, sample in ((T, names[::130][:16]), (1, [names[0], names[-1]])):
-        secs, _ = R.cpu_baseline_sources("fabric", C3_OPTS, sample, threads, 3)
+        secs, _ = R.cpu_baseline_sources("fabric", C3_OPTS, sample, threads, C3_CPU_REPS)
         # thread-seconds per source -> whole-node builds/s at `threads`
         out[threads] = median(1.0 / (s * min(threads, len(sample)) / len(sample) * N / threads)
                               for s in secs)
     return {"value": round(out[T], 6), "unit": "builds/s", "cores": T, "kind": "port",
-            "value_1thread": round(out[1], 7), "reps": 3, "host": host_info(),
+            "value_1thread": round(out[1], 7), "reps": C3_CPU_REPS, "host": host_info(),
             "sample": f"refcpu buildRouteDb(s) of 16 stratified sources on {T} threads and "
                       "2 (1-0-0, 3-31-47) on 1 thread, private replicas, ingestion excluded, "
-                      "median of 3 reps, extrapolated to all 2,080 sources"}
+                      f"median of {C3_CPU_REPS} reps, extrapolated to all 2,080 sources"}
 
 
 def run_c3(args, torch, dist, rank, world, local_rank):
@@ -665,7 +667,7 @@ def run_c3(args, torch, dist, rank, world, local_rank):
         return line
     golden_check(line, "c3", job_digest, GOLDEN.get("c3") if ppn == 100 else None)
     if world == 1:
-        set_traffic(line, "c3", "spf_frontier_kernel")
+        set_traffic(line, "c3", ("spf_lds_route_kernel", "lds_prep_kernel"))
         if not args.no_shard_projection:
             # the 2/4/8-GPU shards, each rank's share timed alone on this GPU
             line["shard_projection"] = c3_shard_projection(lib, capi, launches, main, side)

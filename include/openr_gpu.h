@@ -287,7 +287,8 @@ int ogs_host_free(void* hptr);
  *                 wave-kernel workgroup, 4 (default), 8 or 16.
  *   "ms_group":   sources per workgroup of the multi-source kernel (0 auto,
  *                 1, 2, 4).
- *   "route_stream": RouteDb form for large shared topologies: 2 (default)
+ *   "route_stream": RouteDb form for large shared topologies: 5 (default,
+ *                 below; topologies whose LDS image does not fit take 2); 2
  *                 one launch per unit set, SPF then the unit's RouteDb write
  *                 stream from LDS; 1 an SPF launch then a route-stream launch
  *                 (dist/next-hop sets through HBM); 4 the SPF with the

@@ -157,16 +157,19 @@ hipError_t workspace(size_t bytes, hipStream_t stream, void** out) {
   return hipSuccess;
 }
 
-// "route_stream" option for large shared topologies: 2 (default) fused
-// frontier SPF + route stream, one launch; 1 SPF launch then route-stream
-// launch (dist / next-hop sets through HBM); 4 the LDS-resident SPF
-// (spf_lds.hip) then the route stream over parts; 5 both of those in one
-// persistent launch (spf_lds.hip, spf_lds_route_kernel). (0, the fused multi-source
+// "route_stream" option for large shared topologies: 5 (default) the
+// LDS-resident SPF and the route stream in one persistent launch
+// (spf_lds.hip, spf_lds_route_kernel; topologies whose image does not fit
+// LDS take form 2); 2 fused frontier SPF + route stream, one launch; 1 SPF
+// launch then route-stream launch (dist / next-hop sets through HBM); 4 the
+// LDS-resident SPF then the route stream over parts. C3 (profiles/
+// r04_lds_groups_ab.log): 5 at 1.10 / 0.57 / 0.31 / 0.17 ms for 1 / 2 / 4 / 8
+// shards vs 2 at 1.22 / 0.72 / 0.41 / 0.26. (0, the fused multi-source
 // kernel as the C3 form, and 3, the split pipelined over unit chunks on two
 // streams -- 1.40-1.64 vs 1.33 ms on C3, profiles/r03_c3_pipelined_split_
 // ab.log -- were removed in round 4; the multi-source kernel remains the
 // fallback where neither form applies.)
-int g_routeStream = 2;
+int g_routeStream = 5;
 // "route_store_nt" option, bits: 1 the RouteDb stream's 16-B stores are
 // non-temporal (else ordinary write-back stores), 2 the wave kernel's output
 // stores are. Default 2. The bare C3 store pattern drains faster with

@@ -66,8 +66,9 @@ def _c3(product, names, ppn=100):
     return launches
 
 
-@pytest.mark.parametrize("opts", [{}, dict(frontier_block=1024, frontier_parts=1),
-                                  dict(frontier_block=512, frontier_parts=3,
+@pytest.mark.parametrize("opts", [{}, dict(route_stream=2),
+                                  dict(route_stream=2, frontier_block=1024, frontier_parts=1),
+                                  dict(route_stream=2, frontier_block=512, frontier_parts=3,
                                        frontier_parts_wide=5),
                                   dict(route_stream=4), dict(route_stream=4, frontier_parts=3,
                                                              frontier_parts_wide=5),
@@ -91,7 +92,7 @@ def test_c3_full_every_source_matches_oracle(product, opts):
     assert set(want) == set(names)
     import openr_amd.capi as capi
     lib = capi.load()
-    defaults = dict(frontier_block=0, frontier_parts=0, frontier_parts_wide=0, route_stream=2,
+    defaults = dict(frontier_block=0, frontier_parts=0, frontier_parts_wide=0, route_stream=5,
                     lds_parts=4, lds_grid=0)
     for k, v in opts.items():
         capi.check(lib, lib.ogs_set_option(k.encode(), v), k)

@@ -277,7 +277,7 @@ def test_batch_runner_feature_sweep(product, oracle, seed):
     kind, opts, names = _big_topology(rng)
     srcs = rng.sample(names, min(len(names), rng.randint(1, 12)))
     v4, brs = rng.random() < 0.7, rng.random() < 0.5
-    options = dict(route_stream=rng.choice([0, 1, 2]), spf_frontier=rng.choice([0, 1]),
+    options = dict(route_stream=rng.choice([1, 2, 4, 5]), spf_frontier=rng.choice([0, 1]),
                    ms_group=rng.choice([0, 1, 2, 4]))
     lib = capi.load()
     try:
@@ -290,7 +290,7 @@ def test_batch_runner_feature_sweep(product, oracle, seed):
         br.download()
         got = [br.canonical(u) for u in range(len(srcs))]
     finally:
-        lib.ogs_set_option(b"route_stream", 2)
+        lib.ogs_set_option(b"route_stream", 5)
         lib.ogs_set_option(b"spf_frontier", 1)
         lib.ogs_set_option(b"ms_group", 0)
     _cmp(got, oracle.gen_route_dbs(kind, opts, srcs, v4, False, brs),

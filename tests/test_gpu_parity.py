@@ -354,7 +354,7 @@ def _batch_dbs(product, kind, opts, srcs, enable_v4, brs, **options):
         br.download()
         return [br.canonical(u) for u in range(len(srcs))]
     finally:
-        lib.ogs_set_option(b"route_stream", 2)
+        lib.ogs_set_option(b"route_stream", 5)
         lib.ogs_set_option(b"lds_parts", 4)
         lib.ogs_set_option(b"lds_grid", 0)
         lib.ogs_set_option(b"frontier_parts", 0)
