@@ -835,6 +835,15 @@ struct PrefixHostTable {
   std::vector<uint32_t> advOff;
   uint64_t generation{0};  // bumped by every build (compiled-policy cache key)
   void build(const PrefixState& ps);
+  // prefix indices in prefix order (PrefixState is a hashed map): computed
+  // on first use per build, for the outputs that list routes sorted (the
+  // direct thrift build of getRouteDbComputed, merged with the statics)
+  const std::vector<uint32_t>& sortedOrder() const;
+
+ private:
+  mutable std::mutex sortedMutex_;
+  mutable std::vector<uint32_t> sorted_;
+  mutable uint64_t sortedGen_{0};
 };
 
 bool wideDistancesNeeded(const FlatTopology& f);

@@ -192,6 +192,7 @@ LinkState::LinkStateChange LinkState::updateAdjacencyDatabase(
     patchFlat(name, touched, nodeFlagsChanged);
     if (ch.topologyChanged) {  // LinkState.cpp:635-638
       spfMemo_.clear();
+      spfCounted_.clear();
       kthMemo_.clear();
     }
   } else {

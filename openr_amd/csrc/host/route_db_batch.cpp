@@ -294,8 +294,12 @@ RouteDatabase RouteDbBatch::getRouteDbComputed(const std::string& node, void* st
   }
   const int W = r.W;
   const size_t Sp = r.Sp;
-  auto build = [&](size_t p0, size_t p1, std::vector<UnicastRoute>& dst) {
-    for (size_t p = p0; p < p1; ++p) {
+  // routes in prefix order (the DecisionRouteDb map's), merged with the
+  // statics below
+  const std::vector<uint32_t>& sorted = table_.sortedOrder();
+  auto build = [&](size_t i0, size_t i1, std::vector<UnicastRoute>& dst) {
+    for (size_t i = i0; i < i1; ++i) {
+      const size_t p = sorted[i];
       if (!(r.meta[p] & OGS_ROUTE_VALID)) continue;
       const std::string& prefix = table_.prefixes[p];
       const int fl = (isV4Prefix(prefix) && !solver_.v4OverV6Nexthop_) ? 1 : 0;

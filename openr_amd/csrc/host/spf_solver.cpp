@@ -544,6 +544,18 @@ void PrefixHostTable::build(const PrefixState& ps) {
   }
 }
 
+const std::vector<uint32_t>& PrefixHostTable::sortedOrder() const {
+  std::lock_guard<std::mutex> lock(sortedMutex_);
+  if (sortedGen_ != generation || sorted_.size() != prefixes.size()) {
+    sorted_.resize(prefixes.size());
+    for (uint32_t i = 0; i < uint32_t(prefixes.size()); ++i) sorted_[i] = i;
+    std::sort(sorted_.begin(), sorted_.end(),
+              [&](uint32_t a, uint32_t b) { return prefixes[a] < prefixes[b]; });
+    sortedGen_ = generation;
+  }
+  return sorted_;
+}
+
 // One prefix's route from the unit's compact records (RibUnicastEntry of
 // createRouteForPrefix, SpfSolver.cpp:160-311 + addBestPaths 595-639).
 // `meta`, `metric` and the link-slot mask words (word w at mask[w * stride])
