@@ -702,10 +702,14 @@ def run_c3(args, torch, dist, rank, world, local_rank):
     # RouteDb in one sub-table build, vs the engine's per-prefix loop and vs
     # refcpu's createRouteForPrefixOrGetStaticRoute loop (SPF memo warm, as
     # in the reference's Decision::rebuildRoutes, Decision.cpp:929-938)
-    b_ms, l_ms, same, n_chg = M.incremental_routes_bench("fabric", fab, C3_INC_SOURCE, 100)
+    b_ms, l_ms, same, n_chg, *split = M.incremental_routes_bench("fabric", fab, C3_INC_SOURCE,
+                                                                 100)
     assert same, "createRoutesForPrefixes differs from the per-prefix loop"
-    line["incremental_routes"] = {"changed_prefixes": n_chg, "batch_ms": round(b_ms, 3),
-                                  "per_prefix_loop_ms": round(l_ms, 2)}
+    line["incremental_routes"] = {
+        "changed_prefixes": n_chg, "batch_ms": round(b_ms, 3),
+        "per_prefix_loop_ms": round(l_ms, 2),
+        "batch_split_ms": dict(zip(("spf_memo", "sub_table_h2d", "launch_d2h_sync",
+                                    "materialize"), (round(x, 3) for x in split)))}
     if not args.no_cpu_baseline:
         ms = [oracle().cpu_incremental_routes("fabric", fab, C3_INC_SOURCE, 100)[0]
               for _ in range(CPU_REPS)]

@@ -611,13 +611,16 @@ DecisionRouteDb materializeRouteDb(
   if (bestRoutesCache) bestRoutesCache->clear();
   const auto meIt = f.id.find(me);
   const uint32_t rb = meIt == f.id.end() ? 0u : f.rowPtr[meIt->second];
-  // prefixes [p0, p1) into `routes` / `sel` (table order = prefix order, so
-  // appending at the end is the hint)
+  // sorted positions [i0, i1) into `routes` / `sel`: walked in prefix order
+  // (the table follows the hashed PrefixState), so appending at the end is
+  // the map's hint
+  const std::vector<uint32_t>& sorted = pt.sortedOrder();
   std::atomic<uint64_t> noRoute{0};  // decision.no_route_to_prefix (SpfSolver.cpp:221, 242)
-  auto build = [&](uint32_t p0, uint32_t p1, std::map<std::string, RibUnicastEntry>& routes,
+  auto build = [&](uint32_t i0, uint32_t i1, std::map<std::string, RibUnicastEntry>& routes,
                    std::map<std::string, RouteSelectionResult>* cache) {
     uint64_t unreachable = 0;
-    for (uint32_t p = p0; p < p1; ++p) {
+    for (uint32_t i = i0; i < i1; ++i) {
+      const uint32_t p = sorted[i];
       const uint32_t meta = r.meta[p];
       unreachable += !(meta & OGS_ROUTE_VALID) &&
           ((meta >> OGS_ROUTE_REASON_SHIFT) & 0xFu) == OGS_REASON_UNREACHABLE;
@@ -956,6 +959,7 @@ void SpfSolver::routesFromSpfMemo(const std::string& me, const LinkState& ls,
                                   const PrefixState& sub,
                                   std::map<std::string, std::optional<RibUnicastEntry>>& out) {
   Impl& I = *impl_;
+  const auto tIn = std::chrono::steady_clock::now();
   const FlatTopology& f = ls.flatOnDevice();
   const bool exact = f.hasZeroMetric || f.hasWideMetric;
   const uint32_t s = f.id.at(me);
@@ -997,6 +1001,7 @@ void SpfSolver::routesFromSpfMemo(const std::string& me, const LinkState& ls,
     I.spfDb = db;
   }
   const ResultImage S(I.spfN, 0, I.spfW, I.spfDb);
+  const auto tSpf = std::chrono::steady_clock::now();
 
   // the changed prefixes' table: one packed H2D
   HostBatch hb;
@@ -1008,6 +1013,7 @@ void SpfSolver::routesFromSpfMemo(const std::string& me, const LinkState& ls,
   T.pack(hb, desc, I.hSubTab);
   I.subTab.resize(T.end);
   ogsCheck(ogs_memcpy_h2d(I.subTab.get(), I.hSubTab.get(), T.end, nullptr), "ogs_memcpy_h2d");
+  const auto tTab = std::chrono::steady_clock::now();
   const ResultImage R(0, np, W, db);  // records only (dist / nh spans empty)
   I.subRes.resize(R.end);
   I.hSubRes.resize(R.end);
@@ -1027,6 +1033,7 @@ void SpfSolver::routesFromSpfMemo(const std::string& me, const LinkState& ls,
                           R.end - R.meta, nullptr),
            "ogs_memcpy_d2h");
   ogsCheck(ogs_stream_sync(nullptr), "ogs_stream_sync");
+  const auto tDev = std::chrono::steady_clock::now();
 
   std::vector<uint64_t> metric;
   widenSpan(I.hSubRes.at<void>(R.metric), np, wide, metric);
@@ -1052,6 +1059,14 @@ void SpfSolver::routesFromSpfMemo(const std::string& me, const LinkState& ls,
                                    v4OverV6Nexthop_, nullptr, OGS_POLICY_NONE,
                                    OGS_POLICY_NONE);
   }
+  // split of the per-prefix path (decision.gpu.inc_*_ms): SPF memo check /
+  // run, sub-table build + H2D, route launch + D2H + sync, materialisation
+  auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+  const auto tEnd = std::chrono::steady_clock::now();
+  addStatValue("decision.gpu.inc_spf_ms", ms(tIn, tSpf), StatType::AVG);
+  addStatValue("decision.gpu.inc_table_ms", ms(tSpf, tTab), StatType::AVG);
+  addStatValue("decision.gpu.inc_device_ms", ms(tTab, tDev), StatType::AVG);
+  addStatValue("decision.gpu.inc_materialize_ms", ms(tDev, tEnd), StatType::AVG);
 }
 
 // Domain tables of a multi-area buildRouteDb: the areas' CSR as one graph

@@ -1566,19 +1566,42 @@ PYBIND11_MODULE(_decision, m) {
             }
           }
           for (auto& [na, p, e] : upd) ps.updatePrefixKeyed(na.first, na.second, p, std::move(e));
-          a.createRoutesForPrefixes(me, als, ps, changed);  // warm (device sub-table)
+          // both solvers warm (device sub-table buffers allocated, as the
+          // reference's loop runs with its SPF memo warm); createRoutesForPrefixes
+          // leaves the per-prefix path's change-log cursor alone
+          a.createRoutesForPrefixes(me, als, ps, changed);
+          b.createRoutesForPrefixes(me, als, ps, changed);
+          const char* kSplit[4] = {"decision.gpu.inc_spf_ms.sum", "decision.gpu.inc_table_ms.sum",
+                                   "decision.gpu.inc_device_ms.sum",
+                                   "decision.gpu.inc_materialize_ms.sum"};
+          auto sums = [&](std::array<double, 4>& acc, double sign) {
+            const auto c = getDecisionCounters();
+            for (int i = 0; i < 4; ++i) {
+              auto it = c.find(kSplit[i]);
+              acc[i] += sign * (it == c.end() ? 0.0 : it->second);
+            }
+          };
+          std::array<double, 4> split{};
+          sums(split, -1.0);
           auto t0 = std::chrono::steady_clock::now();
           auto batch = a.createRoutesForPrefixes(me, als, ps, changed);
           auto t1 = std::chrono::steady_clock::now();
-          bool same = true;
+          sums(split, 1.0);
+          std::vector<std::optional<RibUnicastEntry>> loop;
+          loop.reserve(changed.size());
           for (const auto& p : changed) {
-            auto r = b.createRouteForPrefixOrGetStaticRoute(me, als, ps, p);
-            same &= (r.has_value() == batch[p].has_value()) && (!r || *r == *batch[p]);
+            loop.push_back(b.createRouteForPrefixOrGetStaticRoute(me, als, ps, p));
           }
           auto t2 = std::chrono::steady_clock::now();
+          bool same = true;  // compared after the timed loop
+          size_t i = 0;
+          for (const auto& p : changed) {
+            const auto& r = loop[i++];
+            same &= (r.has_value() == batch[p].has_value()) && (!r || *r == *batch[p]);
+          }
           return std::make_tuple(std::chrono::duration<double, std::milli>(t1 - t0).count(),
                                  std::chrono::duration<double, std::milli>(t2 - t1).count(),
-                                 same, changed.size());
+                                 same, changed.size(), split[0], split[1], split[2], split[3]);
         });
   m.def("gen_publication",
         [](const std::string& kind, py::dict opts) {
@@ -1811,6 +1834,7 @@ PYBIND11_MODULE(_decision, m) {
               dCold = digest::unit(me, *db);
               sums(splitWarm, -1.0);
               for (int k = 0; k < reps; ++k) {
+                db.reset();  // the previous result is released untimed, as before a cold build
                 t0 = std::chrono::steady_clock::now();
                 db = solver.buildRouteDb(me, als, ps);
                 warm.push_back(std::chrono::duration<double, std::micro>(
