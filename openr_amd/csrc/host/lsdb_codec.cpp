@@ -770,54 +770,86 @@ std::string getNodeNameFromKey(const std::string& key) {  // LsdbUtil.cpp:691-69
   return key.substr(a + 1, b == std::string::npos ? std::string::npos : b - a - 1);
 }
 
-LsdbKeyUpdate LsdbIngest::updateKeyInLsdb(const std::string& area, LinkState& areaLinkState,
-                                          PrefixState& prefixState, const std::string& key,
-                                          const std::optional<std::string_view>& rawVal,
-                                          bool inInitialization) const {
-  LsdbKeyUpdate u;
-  if (!rawVal) return u;  // TTL update (Decision.cpp:716-720)
+// The pure half of updateKeyInLsdb: decode (no state touched), so a
+// publication's values can be decoded on several threads.
+LsdbIngest::Decoded LsdbIngest::decodeKey(const std::string& key,
+                                          const std::optional<std::string_view>& rawVal) {
+  Decoded d;
+  if (!rawVal) return d;  // TTL update (Decision.cpp:716-720)
   try {
     if (key.compare(0, 4, "adj:") == 0) {
-      AdjacencyDatabase db = readAdjacencyDatabase(*rawVal);
+      d.adj = readAdjacencyDatabase(*rawVal);
+      d.kind = Decoded::kAdj;
+      return d;
+    }
+    if (key.compare(0, 7, "prefix:") == 0) {
+      std::vector<std::string> networks;
+      d.prefix = readPrefixDatabase(*rawVal, &networks);
+      if (!networks.empty()) d.network = std::move(networks.front());
+      d.kind = Decoded::kPrefix;
+    }
+  } catch (const std::exception& e) {  // Decision.cpp:781-784: log, drop the key
+    d.kind = Decoded::kError;
+    d.error = "Failed to deserialize info for key " + key + ". Exception: " + e.what();
+  }
+  return d;
+}
+
+LsdbKeyUpdate LsdbIngest::applyDecoded(const std::string& area, LinkState& areaLinkState,
+                                       PrefixState& prefixState, const std::string& key,
+                                       Decoded&& d, bool inInitialization) const {
+  LsdbKeyUpdate u;
+  if (d.kind == Decoded::kNone) return u;
+  if (d.kind == Decoded::kError) {
+    u.kind = LsdbKeyUpdate::kError;
+    u.error = std::move(d.error);
+    return u;
+  }
+  try {
+    if (d.kind == Decoded::kAdj) {
+      AdjacencyDatabase& db = d.adj;
       db.area = area;  // Decision.cpp:732
       u.kind = LsdbKeyUpdate::kAdjacency;
       u.nodeName = db.thisNodeName;
       u.linkChange = areaLinkState.updateAdjacencyDatabase(db, area, inInitialization);
       return u;
     }
-    if (key.compare(0, 7, "prefix:") == 0) {
-      std::vector<std::string> networks;
-      PrefixDatabase db = readPrefixDatabase(*rawVal, &networks);
-      u.nodeName = db.thisNodeName;
-      if (db.prefixEntries.size() != 1) {  // Decision.cpp:750-756
-        u.kind = LsdbKeyUpdate::kError;
-        u.error = "Expecting exactly one entry per prefix key, publication received from " +
-                  db.thisNodeName;
-        return u;
-      }
-      PrefixEntry& entry = db.prefixEntries.front();
-      // self-redistributed route reflection (Decision.cpp:761-769)
-      if (db.thisNodeName == myNodeName_ && !entry.area_stack.empty() &&
-          areas_.count(entry.area_stack.back())) {
-        return u;
-      }
-      // PrefixKey(node, toIPNetwork(*entry.prefix()), area) (Decision.cpp:772-773);
-      // a default IpPrefix (no prefix field) is rejected by toIPNetwork
-      const std::string& network = networks.front();
-      if (network.empty()) fail("prefix: PrefixEntry without a prefix");
-      u.kind = LsdbKeyUpdate::kPrefix;
-      u.changedPrefixes =
-          db.deletePrefix
-              ? prefixState.deletePrefix(db.thisNodeName, area, network)
-              : prefixState.updatePrefixKeyed(db.thisNodeName, area, network, std::move(entry));
+    PrefixDatabase& db = d.prefix;
+    u.nodeName = db.thisNodeName;
+    if (db.prefixEntries.size() != 1) {  // Decision.cpp:750-756
+      u.kind = LsdbKeyUpdate::kError;
+      u.error = "Expecting exactly one entry per prefix key, publication received from " +
+                db.thisNodeName;
       return u;
     }
+    PrefixEntry& entry = db.prefixEntries.front();
+    // self-redistributed route reflection (Decision.cpp:761-769)
+    if (db.thisNodeName == myNodeName_ && !entry.area_stack.empty() &&
+        areas_.count(entry.area_stack.back())) {
+      return u;
+    }
+    // PrefixKey(node, toIPNetwork(*entry.prefix()), area) (Decision.cpp:772-773);
+    // a default IpPrefix (no prefix field) is rejected by toIPNetwork
+    if (d.network.empty()) fail("prefix: PrefixEntry without a prefix");
+    u.kind = LsdbKeyUpdate::kPrefix;
+    u.changedPrefixes =
+        db.deletePrefix
+            ? prefixState.deletePrefix(db.thisNodeName, area, d.network)
+            : prefixState.updatePrefixKeyed(db.thisNodeName, area, d.network, std::move(entry));
   } catch (const std::exception& e) {  // Decision.cpp:781-784: log, drop the key
     u = LsdbKeyUpdate{};
     u.kind = LsdbKeyUpdate::kError;
     u.error = "Failed to deserialize info for key " + key + ". Exception: " + e.what();
   }
   return u;
+}
+
+LsdbKeyUpdate LsdbIngest::updateKeyInLsdb(const std::string& area, LinkState& areaLinkState,
+                                          PrefixState& prefixState, const std::string& key,
+                                          const std::optional<std::string_view>& rawVal,
+                                          bool inInitialization) const {
+  return applyDecoded(area, areaLinkState, prefixState, key, decodeKey(key, rawVal),
+                      inInitialization);
 }
 
 LsdbKeyUpdate LsdbIngest::deleteKeyFromLsdb(const std::string& area, LinkState& areaLinkState,

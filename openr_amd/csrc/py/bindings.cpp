@@ -1626,9 +1626,26 @@ PYBIND11_MODULE(_decision, m) {
             bytes += vals[i].size();
             if (i < nAdj) adjBytes += vals[i].size();
           }
-          std::vector<double> ingest, decode, keyedDecode, insert;
+          std::vector<double> ingest, decode, keyedDecode, insert, publication;
           size_t routesKept = 0;
+          std::vector<PublicationKeyVal> pub(keys.size());
+          for (size_t i = 0; i < keys.size(); ++i) pub[i] = PublicationKeyVal{keys[i], vals[i]};
           for (int r = 0; r < reps; ++r) {
+            {
+              // the whole publication through processPublication (decode on
+              // host threads, then the per-key apply in key order)
+              AreaLinkStates als;
+              PrefixState ps0;
+              LsdbIngest ing0("test_node", {g.area});
+              DecisionPendingUpdates pending("test_node");
+              auto p0 = std::chrono::steady_clock::now();
+              ing0.processPublication(g.area, als, ps0, pub, {}, pending);
+              publication.push_back(std::chrono::duration<double, std::milli>(
+                                        std::chrono::steady_clock::now() - p0).count());
+              if (ps0.prefixes().size() != keys.size() - nAdj) {
+                throw std::runtime_error("processPublication lost prefixes");
+              }
+            }
             LinkState ls(g.area, "test_node");
             PrefixState ps;
             LsdbIngest ing("test_node", {g.area});
@@ -1667,6 +1684,7 @@ PYBIND11_MODULE(_decision, m) {
             insert.push_back(std::chrono::duration<double, std::milli>(t4 - t3).count());
           }
           std::sort(keyedDecode.begin(), keyedDecode.end());
+          std::sort(publication.begin(), publication.end());
           std::sort(insert.begin(), insert.end());
           std::sort(ingest.begin(), ingest.end());
           std::sort(decode.begin(), decode.end());
@@ -1680,6 +1698,7 @@ PYBIND11_MODULE(_decision, m) {
           d["decode_ms"] = decode[decode.size() / 2];
           d["prefix_keyed_decode_ms"] = keyedDecode[keyedDecode.size() / 2];
           d["prefix_insert_ms"] = insert[insert.size() / 2];
+          d["publication_ms"] = publication[publication.size() / 2];
           return d;
         },
         py::arg("kind"), py::arg("opts"), py::arg("reps") = 3);
