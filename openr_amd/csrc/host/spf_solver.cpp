@@ -522,6 +522,15 @@ void finishPolicy(const RibPolicy* pol, uint16_t applied, uint16_t counter,
 
 }  // namespace
 
+// decision.no_route_to_prefix (SpfSolver.cpp:221 no reachable advertiser,
+// :242 empty selection, :579 no next hop): the records whose reason code is
+// one of those
+static bool noRouteReason(uint32_t meta) {
+  if (meta & OGS_ROUTE_VALID) return false;
+  const uint32_t r = (meta >> OGS_ROUTE_REASON_SHIFT) & 0xFu;
+  return r == OGS_REASON_UNREACHABLE || r == OGS_REASON_NO_NEXTHOP;
+}
+
 bool wideDistancesNeeded(const FlatTopology& f) {
   const uint64_t n = f.names.empty() ? 0 : f.names.size() - 1;
   // 32-bit kernels cap "unreachable" at 2^31 - 1 inside their loops
@@ -622,8 +631,7 @@ DecisionRouteDb materializeRouteDb(
     for (uint32_t i = i0; i < i1; ++i) {
       const uint32_t p = sorted[i];
       const uint32_t meta = r.meta[p];
-      unreachable += !(meta & OGS_ROUTE_VALID) &&
-          ((meta >> OGS_ROUTE_REASON_SHIFT) & 0xFu) == OGS_REASON_UNREACHABLE;
+      unreachable += noRouteReason(meta);
       if (cache && (meta & OGS_ROUTE_SELECTED)) {  // SpfSolver.cpp:247
         const uint32_t a0 = pt.advOff[p];
         RouteSelectionResult sel;
@@ -1041,8 +1049,10 @@ void SpfSolver::routesFromSpfMemo(const std::string& me, const LinkState& ls,
   const uint32_t* mask = I.hSubRes.at<uint32_t>(R.mask);
   const uint32_t* sel = I.hSubRes.at<uint32_t>(R.sel);
   const PrefixHostTable& st = I.subTable;
+  uint64_t noRoute = 0;
   for (uint32_t p = 0; p < np; ++p) {
     const std::string& prefix = st.prefixes[p];
+    noRoute += noRouteReason(meta[p]);
     if (meta[p] & OGS_ROUTE_SELECTED) {  // SpfSolver.cpp:247
       RouteSelectionResult rs;
       const uint32_t a0 = st.advOff[p], a1 = st.advOff[p + 1];
@@ -1059,6 +1069,7 @@ void SpfSolver::routesFromSpfMemo(const std::string& me, const LinkState& ls,
                                    v4OverV6Nexthop_, nullptr, OGS_POLICY_NONE,
                                    OGS_POLICY_NONE);
   }
+  if (noRoute) addStatValue("decision.no_route_to_prefix", double(noRoute), StatType::COUNT);
   // split of the per-prefix path (decision.gpu.inc_*_ms): SPF memo check /
   // run, sub-table build + H2D, route launch + D2H + sync, materialisation
   auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
@@ -1183,8 +1194,10 @@ DecisionRouteDb SpfSolver::materializeMultiArea(const std::string& me,
   DecisionRouteDb rdb;
   bestRoutesCache_.clear();
   const PrefixHostTable& pt = M.table;
+  uint64_t noRoute = 0;
   for (uint32_t p = 0; p < P; ++p) {
     const uint32_t m = R.meta[p];
+    noRoute += noRouteReason(m);
     const uint32_t a0 = pt.advOff[p];
     const uint32_t best = a0 + (m >> OGS_ROUTE_BEST_SHIFT);
     if (m & OGS_ROUTE_SELECTED) {  // SpfSolver.cpp:247
@@ -1224,6 +1237,9 @@ DecisionRouteDb SpfSolver::materializeMultiArea(const std::string& me,
     if (!R.applied.empty()) finishPolicy(ribPolicy_, R.applied[p], R.counter[p], e);
     rdb.unicastRoutes.emplace(e.prefix, std::move(e));
   }
+  // counted also on the probe solver of the incremental path (the
+  // reference counts it per createRouteForPrefix call)
+  if (noRoute) addStatValue("decision.no_route_to_prefix", double(noRoute), StatType::COUNT);
   for (const auto& [prefix, e] : staticUnicastRoutes_) {  // SpfSolver.cpp:343-349
     if (rdb.unicastRoutes.count(prefix)) continue;
     auto it = rdb.unicastRoutes.emplace(prefix, e).first;
@@ -1496,7 +1512,14 @@ std::optional<RibUnicastEntry> SpfSolver::createRouteForPrefixOrGetStaticRoute(
       bestRoutesCache_.erase(prefix);
     }
   }
-  if (hit->second.route) return hit->second.route;
+  if (hit->second.route) {
+    // handed out by move: Decision asks each changed prefix once per
+    // rebuild; asking it again recomputes it (a batch of just that prefix
+    // plus whatever changed since)
+    std::optional<RibUnicastEntry> r = std::move(hit->second.route);
+    incCache_.erase(hit);
+    return r;
+  }
   auto it = staticUnicastRoutes_.find(prefix);  // static routes as the fallback
   if (it != staticUnicastRoutes_.end()) return it->second;
   return std::nullopt;

@@ -88,3 +88,28 @@ def test_spf_runs_ring_four_sources(product):
     rm2 = L.getRouteMap(solver, ["1", "2", "3", "4"], als, ps)
     assert rm2 != rm
     assert M.decision_counters()["decision.spf_runs.count"] == 9
+
+
+def test_no_route_counted_on_every_path(product):
+    """decision.no_route_to_prefix (SpfSolver.cpp:221, 242, 579) is counted
+    per unroutable prefix considered on every route path, not only the
+    single-area full build: the incremental branch
+    (createRoutesForPrefixes -> one createRouteForPrefix per asked prefix)
+    and the multi-area build."""
+    M = product
+    als, ls, ps = _line(M)
+    solver = M.SpfSolver("1", True, False, False, False)
+    solver.buildRouteDb("1", als, ps)
+    M.reset_decision_counters()
+    out = solver.createRoutesForPrefixes("1", als, ps, {"fc00::4/128", "fc00::2/128"})
+    assert out["fc00::4/128"] is None and out["fc00::2/128"] is not None
+    c = M.decision_counters()
+    assert c["decision.get_route_for_prefix.count"] == 2
+    assert c["decision.no_route_to_prefix.count"] == 1
+    # a second area holding only node 1: the multi-area build
+    ls_b = als.add("area_b", "1")
+    ls_b.updateAdjacencyDatabase(L.createAdjDb("1", [], 1, area="area_b"), "area_b")
+    M.reset_decision_counters()
+    db = M.SpfSolver("1", True, False, False, False).buildRouteDb("1", als, ps)
+    assert db is not None
+    assert M.decision_counters()["decision.no_route_to_prefix.count"] == 1
