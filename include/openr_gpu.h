@@ -297,7 +297,9 @@ int ogs_host_free(void* hptr);
  *                 and the stream in one persistent launch: "lds_grid"
  *                 workgroups (0 = one per CU) take SPF and stream items
  *                 ("lds_parts" prefix ranges per unit, default 4) from a
- *                 device-wide counter, SPFs kept one grid ahead. Scratch
+ *                 device-wide counter, SPFs kept one grid ahead; route keys
+ *                 packed into 16 bits on topologies of <= 16,384 nodes
+ *                 ("lds_key16" 1, default; 0 u32 keys, A/B). Scratch
  *                 (prefix keys, dist/next-hop sets when out->dist / out->nh
  *                 are NULL) comes from a grow-only per-device workspace.
  *                 "route_store_nt", bits: 1 the RouteDb stream's 16-B stores

@@ -17,6 +17,7 @@ extern int g_msGroup;
 extern int g_routeStream;
 extern int g_ldsParts;
 extern int g_ldsGrid;
+extern int g_ldsKey16;
 extern int g_routeStoreNt;
 extern int g_spfSeedRow;
 extern int g_frontierBlock;
@@ -199,6 +200,11 @@ int ogs_set_option(const char* name, int64_t value) {
   if (std::strcmp(name, "lds_parts") == 0) {
     if (value < 1 || value > 64) return fail(OGS_E_INVALID, "lds_parts must be in [1, 64]");
     ogs::g_ldsParts = int(value);
+    return OGS_OK;
+  }
+  if (std::strcmp(name, "lds_key16") == 0) {
+    if (value != 0 && value != 1) return fail(OGS_E_INVALID, "lds_key16 must be 0 or 1");
+    ogs::g_ldsKey16 = int(value);
     return OGS_OK;
   }
   if (std::strcmp(name, "lds_grid") == 0) {

@@ -66,6 +66,18 @@ __device__ __forceinline__ uint32_t prefix_key(const ogs_prefix_table& pt, uint3
   return k;
 }
 
+// Packed 16-bit route keys (topologies of at most 16,384 nodes): node id in
+// bits 0..13, v4 bit 14, SLOW bit 15 -- the u32 key's bits 30 / 31 moved
+// down 16. Halves the stream's key reads (every unit reads the whole row).
+constexpr uint32_t kKey16MaxNodes = 1u << 14;
+__device__ __forceinline__ uint16_t key16_of(uint32_t k) {
+  return uint16_t((k & 0x3FFFu) | ((k >> 16) & 0xC000u));
+}
+__device__ __forceinline__ uint32_t key_of(uint16_t h) {
+  return (uint32_t(h) & 0x3FFFu) | ((uint32_t(h) & 0xC000u) << 16);
+}
+__device__ __forceinline__ uint32_t key_of(uint32_t k) { return k; }
+
 // one 16-B output store (route_core.h store_out: kFlagNtStores flavour)
 __device__ __forceinline__ void store4(uint32_t* p, uint32_t a, uint32_t b, uint32_t c,
                                        uint32_t d, bool nt) {
@@ -127,10 +139,10 @@ __device__ __forceinline__ bool route_changed(const Rec<W>& r, const DiffCtx& d,
 // metric and mask outputs and no sel -- the stores are then unconditional,
 // so every path leaves the same number of stores in flight and the key
 // prefetch's wait stays partial (see the loop below).
-template <int W, bool DIFF = false, bool OUTS3 = false, int B = kBlock, typename View,
-          typename RecFn>
+template <int W, bool DIFF = false, bool OUTS3 = false, int B = kBlock, typename KeyT,
+          typename View, typename RecFn>
 __device__ __forceinline__ void stream_routes(
-    const ogs_prefix_table& pt, const uint32_t* __restrict__ tkey, uint32_t p0,
+    const ogs_prefix_table& pt, const KeyT* __restrict__ tkey, uint32_t p0,
     uint32_t P, uint32_t Sp, size_t u, uint32_t s,
     const uint8_t* __restrict__ nflags, const View& sv, const RouteCfg& cfg,
     const ogs_spf_out& out, RecFn rec, const DiffCtx* diff = nullptr, bool nt = true,
@@ -222,7 +234,13 @@ __device__ __forceinline__ void stream_routes(
   uint32_t q = lo + uint32_t(tid) * 4u;
   if (q < Pv) {
     auto keyAt = [&](uint32_t x) {  // clamped: unconditional prefetch
-      return *reinterpret_cast<const uint4*>(tkey + (x < Pv ? x : Pv - 4u));
+      if constexpr (sizeof(KeyT) == 2) {  // packed keys: one 8-B load per quad
+        const uint2 h = *reinterpret_cast<const uint2*>(tkey + (x < Pv ? x : Pv - 4u));
+        return make_uint4(key_of(uint16_t(h.x)), key_of(uint16_t(h.x >> 16)),
+                          key_of(uint16_t(h.y)), key_of(uint16_t(h.y >> 16)));
+      } else {
+        return *reinterpret_cast<const uint4*>(tkey + (x < Pv ? x : Pv - 4u));
+      }
     };
     uint4 ka = keyAt(q);
     uint4 kb = keyAt(q + kStep);
@@ -240,7 +258,7 @@ __device__ __forceinline__ void stream_routes(
   }
   for (uint32_t p = Pv + tid; p < hi; p += B) {  // tail / unaligned rows
     Rec<W> r;
-    one(p, tkey[p], r);
+    one(p, key_of(tkey[p]), r);
     if (oMeta) oMeta[p] = r.meta;
     if (oMetric) oMetric[p] = r.metric;
     if (oSel) oSel[p] = r.sel;

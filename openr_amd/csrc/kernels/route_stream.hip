@@ -310,12 +310,13 @@ bool try_ms_stream(const ogs_graph& g, const ogs_prefix_table& pt,
                   : reinterpret_cast<uint32_t*>(base + keyBytes + chunkBytes + distBytes);
   if (ldsSplit) {
     // one prep launch: LDS images, weight partials, counters, route keys
-    *err = launch_lds_prep(g, &pt, key, W, nUnits, chunkScratch, stream);
+    const bool k16 = g_routeStream == 5 && lds_key16(g);  // form 4's stream reads u32 keys
+    *err = launch_lds_prep(g, &pt, key, k16, W, nUnits, chunkScratch, stream);
     if (*err != hipSuccess) return true;
     uint32_t* d = static_cast<uint32_t*>(spf.dist);
     if (g_routeStream == 5) {
       const LdsRouteGroup one{units, nUnits, W, d, spf.nh, out};
-      *err = launch_spf_lds_routes(g, pt, key, &one, 1, flags, chunkScratch, stream);
+      *err = launch_spf_lds_routes(g, pt, key, k16, &one, 1, flags, chunkScratch, stream);
       return true;
     }
     *err = launch_spf_lds(g, units, nUnits, flags, W, d, spf.nh, chunkScratch, stream);
@@ -425,8 +426,10 @@ hipError_t launch_spf_routes_groups(const ogs_graph& g, const ogs_prefix_table* 
       at += round256(size_t(x.n) * x.W * Sn * 4);
     }
   }
-  e = launch_lds_prep(g, pt, key, Wmax, U, scratch, stream);
+  const bool k16 = lds_key16(g);
+  e = launch_lds_prep(g, pt, key, k16, Wmax, U, scratch, stream);
   if (e != hipSuccess) return e;
-  return launch_spf_lds_routes(g, *pt, key, lg.data(), int(lg.size()), flags, scratch, stream);
+  return launch_spf_lds_routes(g, *pt, key, k16, lg.data(), int(lg.size()), flags, scratch,
+                               stream);
 }
 }  // namespace ogs

@@ -28,9 +28,11 @@ struct LdsRouteGroup {
 // + state fit LDS).
 size_t lds_scratch_bytes(const ogs_graph& g, int W, int nUnits);
 // Prep launch: images, weight partials, counters, route keys (key may be
-// nullptr: SPF only).
-hipError_t launch_lds_prep(const ogs_graph& g, const ogs_prefix_table* pt, uint32_t* key,
-                           int W, int nUnits, void* scratch, hipStream_t stream);
+// nullptr: SPF only; key16: packed u16 keys, route_stream.h).
+hipError_t launch_lds_prep(const ogs_graph& g, const ogs_prefix_table* pt, void* key,
+                           bool key16, int W, int nUnits, void* scratch, hipStream_t stream);
+// whether the one-launch form packs this graph's route keys into 16 bits
+bool lds_key16(const ogs_graph& g);
 // SPF of every unit into dist / nh (route_stream 4), after the prep.
 hipError_t launch_spf_lds(const ogs_graph& g, const ogs_unit* units, int nUnits,
                           uint32_t flags, int W, uint32_t* dist, uint32_t* nh,
@@ -38,7 +40,7 @@ hipError_t launch_spf_lds(const ogs_graph& g, const ogs_unit* units, int nUnits,
 // SPF + RouteDb stream of up to 4 groups (widest first) in one persistent
 // launch (route_stream 5), after the prep for the widest W and all units.
 hipError_t launch_spf_lds_routes(const ogs_graph& g, const ogs_prefix_table& pt,
-                                 const uint32_t* key, const LdsRouteGroup* groups, int n,
-                                 uint32_t flags, void* scratch, hipStream_t stream);
+                                 const void* key, bool key16, const LdsRouteGroup* groups,
+                                 int n, uint32_t flags, void* scratch, hipStream_t stream);
 
 }  // namespace ogs

@@ -108,9 +108,10 @@ __host__ LdsScratch lds_scratch(const ogs_graph& g, const LdsImage& L, int nUnit
 //  next T * nEB: 8,192 edges each -> the 2-B edge words and the block's
 //    min / max weight over up edges (uniform weights iff min == max);
 //  next T * nKB (when keys are asked for): 1,024 prefixes each -> the route
-//    keys of route_stream.h (pfx_key_kernel's).
+//    keys of route_stream.h (pfx_key_kernel's), u32 or packed u16.
 __global__ __launch_bounds__(kLdsBlock) void lds_prep_kernel(
-    ogs_graph g, ogs_prefix_table pt, uint32_t* __restrict__ key, uint32_t nKB, LdsImage L,
+    ogs_graph g, ogs_prefix_table pt, void* __restrict__ key, uint32_t key16, uint32_t nKB,
+    LdsImage L,
     uint8_t* __restrict__ img, uint2* __restrict__ mm, uint32_t nEB, uint32_t* __restrict__ ctr,
     uint32_t* __restrict__ ready, uint32_t nReady) {
   constexpr uint32_t B = kLdsBlock;
@@ -221,7 +222,14 @@ __global__ __launch_bounds__(kLdsBlock) void lds_prep_kernel(
   if (key && blk < T * nKB) {
     const uint32_t t = blk / nKB, p = (blk - t * nKB) * B + tid;
     const uint32_t Sp = uint32_t(pt.max_prefixes);
-    if (p < Sp) key[size_t(t) * Sp + p] = prefix_key(pt, t, p);
+    if (p < Sp) {
+      const uint32_t k = prefix_key(pt, t, p);
+      if (key16) {
+        static_cast<uint16_t*>(key)[size_t(t) * Sp + p] = key16_of(k);
+      } else {
+        static_cast<uint32_t*>(key)[size_t(t) * Sp + p] = k;
+      }
+    }
   }
 }
 
@@ -645,9 +653,9 @@ struct LdsGroups {
 
 // One stream item: prefix range `part` (of P) of local unit u of group grp,
 // from the published SPF rows: per-node records into LDS, then the rows.
-template <int W>
+template <int W, typename KeyT>
 __device__ __forceinline__ void lds_stream_item(const ogs_graph& g, const ogs_prefix_table& pt,
-                                                const uint32_t* __restrict__ key,
+                                                const KeyT* __restrict__ key,
                                                 const LdsGroup& grp, uint32_t u, uint32_t part,
                                                 uint32_t P, uint32_t flags, uint32_t* rec0) {
   constexpr uint32_t kInf = 0xFFFFFFFFu;
@@ -716,8 +724,9 @@ __device__ __forceinline__ void lds_stream_item(const ogs_graph& g, const ogs_pr
 // agent release and a relaxed agent flag store; a stream item's lane 0
 // polls the flag (relaxed agent loads), takes an agent acquire, and the
 // workgroup reads the rows after a barrier.
+template <typename KeyT>
 __global__ __launch_bounds__(kLdsBlock) void spf_lds_route_kernel(
-    ogs_graph g, ogs_prefix_table pt, const uint32_t* __restrict__ key, LdsImage L,
+    ogs_graph g, ogs_prefix_table pt, const KeyT* __restrict__ key, LdsImage L,
     const uint8_t* __restrict__ img, const uint2* __restrict__ mm, uint32_t nEB,
     LdsGroups grps, uint32_t flags, uint32_t* __restrict__ ctr, uint32_t* __restrict__ ready,
     uint32_t P) {
@@ -784,10 +793,10 @@ __global__ __launch_bounds__(kLdsBlock) void spf_lds_route_kernel(
     // the per-node records go to the state region (the image stays)
     uint32_t* rec0 = reinterpret_cast<uint32_t*>(smem + L.block);
     switch (grp.W) {
-      case 1: lds_stream_item<1>(g, pt, key, grp, u, part, P, flags, rec0); break;
-      case 2: lds_stream_item<2>(g, pt, key, grp, u, part, P, flags, rec0); break;
-      case 3: lds_stream_item<3>(g, pt, key, grp, u, part, P, flags, rec0); break;
-      default: lds_stream_item<4>(g, pt, key, grp, u, part, P, flags, rec0); break;
+      case 1: lds_stream_item<1, KeyT>(g, pt, key, grp, u, part, P, flags, rec0); break;
+      case 2: lds_stream_item<2, KeyT>(g, pt, key, grp, u, part, P, flags, rec0); break;
+      case 3: lds_stream_item<3, KeyT>(g, pt, key, grp, u, part, P, flags, rec0); break;
+      default: lds_stream_item<4, KeyT>(g, pt, key, grp, u, part, P, flags, rec0); break;
     }
   }
 }
@@ -824,8 +833,8 @@ size_t lds_scratch_bytes(const ogs_graph& g, int W, int nUnits) {
 
 // Prep launch (lds_prep_kernel): images, weight partials, counters, and the
 // route keys when key != nullptr.
-hipError_t launch_lds_prep(const ogs_graph& g, const ogs_prefix_table* pt, uint32_t* key,
-                           int W, int nUnits, void* scratch, hipStream_t stream) {
+hipError_t launch_lds_prep(const ogs_graph& g, const ogs_prefix_table* pt, void* key,
+                           bool key16, int W, int nUnits, void* scratch, hipStream_t stream) {
   const LdsImage L = lds_image(g, W);
   const LdsScratch S = lds_scratch(g, L, nUnits);
   uint8_t* base = static_cast<uint8_t*>(scratch);
@@ -834,7 +843,7 @@ hipError_t launch_lds_prep(const ogs_graph& g, const ogs_prefix_table* pt, uint3
   const uint32_t nKB = key && Sp ? (Sp + kLdsBlock - 1u) / kLdsBlock : 0u;
   const ogs_prefix_table ptv = pt ? *pt : ogs_prefix_table{};
   hipLaunchKernelGGL(lds_prep_kernel, dim3(T * (1u + S.nEB + nKB)), dim3(kLdsBlock), 0, stream,
-                     g, ptv, nKB ? key : nullptr, nKB, L, base,
+                     g, ptv, nKB ? key : nullptr, key16 ? 1u : 0u, nKB, L, base,
                      reinterpret_cast<uint2*>(base + S.mm), S.nEB,
                      reinterpret_cast<uint32_t*>(base + S.ctr),
                      reinterpret_cast<uint32_t*>(base + S.ready), uint32_t(nUnits));
@@ -880,14 +889,21 @@ hipError_t launch_spf_lds(const ogs_graph& g, const ogs_unit* units, int nUnits,
 // "lds_grid": its workgroups (0 = one per CU).
 int g_ldsParts = 4;
 int g_ldsGrid = 0;
+// "lds_key16": packed 16-bit route keys on topologies of <= 16,384 nodes
+// (1, default) or u32 keys (0, A/B)
+int g_ldsKey16 = 1;
+
+bool lds_key16(const ogs_graph& g) {
+  return g_ldsKey16 && g.max_nodes > 0 && uint32_t(g.max_nodes) <= kKey16MaxNodes;
+}
 
 // SPF + RouteDb stream of every group in one persistent launch
 // (spf_lds_route_kernel) after launch_lds_prep (keys, and the image laid out
 // for the widest group; nUnits = all groups' units). groups: n <= 4, widest
 // first, each with its published dist / nh rows.
 hipError_t launch_spf_lds_routes(const ogs_graph& g, const ogs_prefix_table& pt,
-                                 const uint32_t* key, const LdsRouteGroup* groups, int n,
-                                 uint32_t flags, void* scratch, hipStream_t stream) {
+                                 const void* key, bool key16, const LdsRouteGroup* groups,
+                                 int n, uint32_t flags, void* scratch, hipStream_t stream) {
   if (n < 1 || n > kMaxLdsGroups) return hipErrorInvalidValue;
   int Wmax = 1, U = 0;
   LdsGroups G{};
@@ -912,11 +928,15 @@ hipError_t launch_spf_lds_routes(const ogs_graph& g, const ogs_prefix_table& pt,
   const int grid = std::max(1, g_ldsGrid > 0 ? g_ldsGrid : num_cus());
   const uint32_t P = uint32_t(std::max(1, g_ldsParts));
   if (g_routeStoreNt & 1) flags |= kFlagNtStores;
-  hipError_t a = allow_lds(spf_lds_route_kernel, lds);
-  if (a != hipSuccess) return a;
-  hipLaunchKernelGGL(spf_lds_route_kernel, dim3(grid), dim3(kLdsBlock), lds, stream, g, pt, key,
-                     L, static_cast<const uint8_t*>(base), mm, S.nEB, G, flags, ctr, ready, P);
-  return hipGetLastError();
+  auto go = [&](auto k, auto keyp) {
+    hipError_t a = allow_lds(k, lds);
+    if (a != hipSuccess) return a;
+    hipLaunchKernelGGL(k, dim3(grid), dim3(kLdsBlock), lds, stream, g, pt, keyp, L,
+                       static_cast<const uint8_t*>(base), mm, S.nEB, G, flags, ctr, ready, P);
+    return hipGetLastError();
+  };
+  return key16 ? go(spf_lds_route_kernel<uint16_t>, static_cast<const uint16_t*>(key))
+               : go(spf_lds_route_kernel<uint32_t>, static_cast<const uint32_t*>(key));
 }
 
 }  // namespace ogs

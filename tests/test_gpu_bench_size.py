@@ -73,7 +73,8 @@ def _c3(product, names, ppn=100):
                                   dict(route_stream=4), dict(route_stream=4, frontier_parts=3,
                                                              frontier_parts_wide=5),
                                   dict(route_stream=5), dict(route_stream=5, lds_parts=7,
-                                                             lds_grid=100)])
+                                                             lds_grid=100),
+                                  dict(route_stream=5, lds_key16=0)])
 def test_c3_full_every_source_matches_oracle(product, opts):
     """C3-full at bench size (2,080 sources x 208k prefixes) through
     bench.py's two-stream width-group launches: every source's digest equals
@@ -93,7 +94,7 @@ def test_c3_full_every_source_matches_oracle(product, opts):
     import openr_amd.capi as capi
     lib = capi.load()
     defaults = dict(frontier_block=0, frontier_parts=0, frontier_parts_wide=0, route_stream=5,
-                    lds_parts=4, lds_grid=0)
+                    lds_parts=4, lds_grid=0, lds_key16=1)
     for k, v in opts.items():
         capi.check(lib, lib.ogs_set_option(k.encode(), v), k)
     try:

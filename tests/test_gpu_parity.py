@@ -357,6 +357,7 @@ def _batch_dbs(product, kind, opts, srcs, enable_v4, brs, **options):
         lib.ogs_set_option(b"route_stream", 5)
         lib.ogs_set_option(b"lds_parts", 4)
         lib.ogs_set_option(b"lds_grid", 0)
+        lib.ogs_set_option(b"lds_key16", 1)
         lib.ogs_set_option(b"frontier_parts", 0)
         lib.ogs_set_option(b"frontier_parts_wide", 0)
         lib.ogs_set_option(b"spf_frontier", 1)
@@ -437,15 +438,16 @@ def test_route_stream_wan_prefix_mix(product, oracle, stream, frontier):
     _cmp(a, oracle.gen_route_dbs("wan", opts, srcs, True, False, True), "wanmix")
 
 
-@pytest.mark.parametrize("stream", [1, 2, 4, 5])
-def test_route_stream_three_word_sources(product, oracle, stream):
+@pytest.mark.parametrize("stream,key16", [(1, 1), (2, 1), (4, 1), (5, 1), (5, 0)])
+def test_route_stream_three_word_sources(product, oracle, stream, key16):
     """FSW sources of 84 links (36 SSW + 48 RSW, the C3 shape on 4 pods x 2
     planes) keep three next-hop words: the fused kernel, the HBM split and
     the LDS-resident split, vs the oracle."""
     opts = dict(pods=4, planes=2, sswPerPlane=36, rswPerPod=48, full=True,
                 prefixesPerNode=3, nodeOverloadPermille=10, **MIX)
     srcs = [f"2-{p}-{f}" for p in range(4) for f in range(2)]
-    a = _batch_dbs(product, "fabric", opts, srcs, True, False, route_stream=stream)
+    a = _batch_dbs(product, "fabric", opts, srcs, True, False, route_stream=stream,
+                   lds_key16=key16)
     _cmp(a, oracle.gen_route_dbs("fabric", opts, srcs, True, False, False), "fsw3")
 
 
