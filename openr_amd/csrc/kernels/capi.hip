@@ -198,7 +198,7 @@ int ogs_set_option(const char* name, int64_t value) {
     return OGS_OK;
   }
   if (std::strcmp(name, "lds_parts") == 0) {
-    if (value < 1 || value > 64) return fail(OGS_E_INVALID, "lds_parts must be in [1, 64]");
+    if (value < 0 || value > 64) return fail(OGS_E_INVALID, "lds_parts must be in [0, 64]");
     ogs::g_ldsParts = int(value);
     return OGS_OK;
   }

@@ -885,9 +885,9 @@ hipError_t launch_spf_lds(const ogs_graph& g, const ogs_unit* units, int nUnits,
   }
 }
 
-// "lds_parts": prefix ranges per unit in the one-launch form (default 4);
-// "lds_grid": its workgroups (0 = one per CU).
-int g_ldsParts = 4;
+// "lds_parts": prefix ranges per unit in the one-launch form (0 = by
+// regime, default); "lds_grid": its workgroups (0 = one per CU).
+int g_ldsParts = 0;
 int g_ldsGrid = 0;
 // "lds_key16": packed 16-bit route keys on topologies of <= 16,384 nodes
 // (1, default) or u32 keys (0, A/B)
@@ -926,7 +926,12 @@ hipError_t launch_spf_lds_routes(const ogs_graph& g, const ogs_prefix_table& pt,
   const uint32_t recs = uint32_t(g.max_nodes) * uint32_t(2 + Wmax) * 4u;
   const uint32_t lds = L.block + std::max(L.state, recs);
   const int grid = std::max(1, g_ldsGrid > 0 ? g_ldsGrid : num_cus());
-  const uint32_t P = uint32_t(std::max(1, g_ldsParts));
+  // prefix ranges per unit: "lds_parts", or 0 = by regime -- 2 when every
+  // workgroup has four or more units (whole-node builds: fewer record
+  // rebuilds), 4 below that (sharded builds: more items to balance a few
+  // units per CU); profiles/r04_lds_store_parts_ab.log
+  const uint32_t P = g_ldsParts > 0 ? uint32_t(g_ldsParts)
+                                    : (uint32_t(U) >= 4u * uint32_t(grid) ? 2u : 4u);
   if (g_routeStoreNt & 1) flags |= kFlagNtStores;
   auto go = [&](auto k, auto keyp) {
     hipError_t a = allow_lds(k, lds);

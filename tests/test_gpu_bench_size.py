@@ -94,7 +94,7 @@ def test_c3_full_every_source_matches_oracle(product, opts):
     import openr_amd.capi as capi
     lib = capi.load()
     defaults = dict(frontier_block=0, frontier_parts=0, frontier_parts_wide=0, route_stream=5,
-                    lds_parts=4, lds_grid=0, lds_key16=1)
+                    lds_parts=0, lds_grid=0, lds_key16=1)
     for k, v in opts.items():
         capi.check(lib, lib.ogs_set_option(k.encode(), v), k)
     try:

@@ -355,7 +355,7 @@ def _batch_dbs(product, kind, opts, srcs, enable_v4, brs, **options):
         return [br.canonical(u) for u in range(len(srcs))]
     finally:
         lib.ogs_set_option(b"route_stream", 5)
-        lib.ogs_set_option(b"lds_parts", 4)
+        lib.ogs_set_option(b"lds_parts", 0)
         lib.ogs_set_option(b"lds_grid", 0)
         lib.ogs_set_option(b"lds_key16", 1)
         lib.ogs_set_option(b"frontier_parts", 0)
