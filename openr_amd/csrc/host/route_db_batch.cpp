@@ -149,13 +149,20 @@ void RouteDbBatch::launch(void* stream) {
       (solver_.v4OverV6Nexthop_ ? OGS_F_V4_OVER_V6 : 0u) |
       (solver_.enableBestRouteSelection_ ? OGS_F_BEST_ROUTE_SELECTION : 0u) |
       (wide_ ? OGS_F_WIDE_METRIC : 0u) | (exact_ ? OGS_F_EXACT_ORDER : 0u);
+  // every width group in one call (one prep + one persistent launch for
+  // all of them on the large-topology form, ogs_spf_routes_groups)
+  std::vector<ogs_route_group> rg;
+  rg.reserve(groups_.size());
   for (Group& G : groups_) {
     ogs_spf_out out{G.dist.get(), G.nh.as<uint32_t>(), G.meta.as<uint32_t>(),
                     G.metric.get(), G.mask.as<uint32_t>(), G.sel.as<uint32_t>(),
                     exact_ ? G.reach.as<uint32_t>() : nullptr};
-    ogsCheck(ogs_spf_routes(&g, hb_.maxPrefixes ? &pt : nullptr, G.units.as<ogs_unit>(),
-                            int32_t(G.members.size()), flags, G.W, &out, stream),
-             "ogs_spf_routes(batch)");
+    rg.push_back(ogs_route_group{G.units.as<ogs_unit>(), int32_t(G.members.size()), G.W, out});
+  }
+  ogsCheck(ogs_spf_routes_groups(&g, hb_.maxPrefixes ? &pt : nullptr, rg.data(),
+                                 int32_t(rg.size()), flags, stream),
+           "ogs_spf_routes_groups(batch)");
+  for (Group& G : groups_) {
     for (uint32_t m : G.members) ls_->noteSpf(sources_[m]);
   }
   launched_ = true;

@@ -51,3 +51,20 @@ def test_wan_sources_with_ghost(product, oracle, brs):
 def test_grid_all_sources_small_kernel_path(product, oracle):
     opts = dict(n=8, metricSeed=0xC2000042, prefixesPerNode=2)
     _check(product, oracle, "grid", opts, [str(i) for i in range(64)], True, False, groups=1)
+
+
+@pytest.mark.parametrize("brs", [False, True])
+def test_fabric_width_groups_one_launch(product, oracle, brs):
+    """A fabric past 256 nodes (72 SSW + 8 FSW + 192 RSW) with FSWs of 84
+    links (three next-hop words) and one-word SSW / RSW sources: the batch's
+    two width groups go through ogs_spf_routes_groups -- one prep and one
+    persistent launch (route_stream 5) -- with drained nodes /
+    links and the prefix mix; every served RouteDb equals the oracle's."""
+    opts = dict(pods=4, planes=2, sswPerPlane=36, rswPerPod=48, full=True, prefixesPerNode=2,
+                nodeOverloadPermille=20, adjOverloadPermille=10, v4Permille=150,
+                anycastPermille=120, minNhPermille=60, drainPermille=50)
+    names = ([f"1-{p}-{s}" for p in range(2) for s in range(36)] +
+             [f"2-{p}-{f}" for p in range(4) for f in range(2)] +
+             [f"3-{p}-{r}" for p in range(4) for r in range(48)])
+    srcs = names[::5] + [f"2-{p}-{f}" for p in range(4) for f in range(2)]
+    _check(product, oracle, "fabric", opts, sorted(set(srcs)), True, brs, groups=2)
