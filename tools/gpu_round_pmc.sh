@@ -5,7 +5,7 @@
 # each summary records the commit it measured.
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 F="--no-cpu-baseline --no-extras"
-bash tools/gpu_pmc.sh c3 --config c3 $F --steps 2 --warmup 1 || exit $?
+bash tools/gpu_pmc.sh c3 --config c3 $F --no-shard-projection --steps 2 --warmup 1 || exit $?
 bash tools/gpu_pmc.sh c2 --config c2 $F --steps 20 --warmup 3 || exit $?
 bash tools/gpu_pmc.sh c4 --config c4 $F --steps 3 --warmup 1 || exit $?
 bash tools/gpu_pmc.sh c5 --config c5 $F --steps 5 --warmup 1 || exit $?
