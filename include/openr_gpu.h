@@ -297,7 +297,8 @@ int ogs_host_free(void* hptr);
  *                 and the stream in one persistent launch: "lds_grid"
  *                 workgroups (0 = one per CU) take SPF and stream items
  *                 ("lds_parts" prefix ranges per unit; 0, default: 2 when
- *                 every workgroup has 4+ units, else 4) from a
+ *                 every workgroup has 4+ units, else 4; "lds_tail" 1,
+ *                 default: then the last grid's worth of units in 4) from a
  *                 device-wide counter, SPFs kept one grid ahead; route keys
  *                 packed into 16 bits on topologies of <= 16,384 nodes
  *                 ("lds_key16" 1, default; 0 u32 keys, A/B). Scratch

@@ -18,6 +18,7 @@ extern int g_routeStream;
 extern int g_ldsParts;
 extern int g_ldsGrid;
 extern int g_ldsKey16;
+extern int g_ldsTail;
 extern int g_routeStoreNt;
 extern int g_spfSeedRow;
 extern int g_frontierBlock;
@@ -200,6 +201,11 @@ int ogs_set_option(const char* name, int64_t value) {
   if (std::strcmp(name, "lds_parts") == 0) {
     if (value < 0 || value > 64) return fail(OGS_E_INVALID, "lds_parts must be in [0, 64]");
     ogs::g_ldsParts = int(value);
+    return OGS_OK;
+  }
+  if (std::strcmp(name, "lds_tail") == 0) {
+    if (value != 0 && value != 1) return fail(OGS_E_INVALID, "lds_tail must be 0 or 1");
+    ogs::g_ldsTail = int(value);
     return OGS_OK;
   }
   if (std::strcmp(name, "lds_key16") == 0) {

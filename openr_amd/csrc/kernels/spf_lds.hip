@@ -729,7 +729,7 @@ __global__ __launch_bounds__(kLdsBlock) void spf_lds_route_kernel(
     ogs_graph g, ogs_prefix_table pt, const KeyT* __restrict__ key, LdsImage L,
     const uint8_t* __restrict__ img, const uint2* __restrict__ mm, uint32_t nEB,
     LdsGroups grps, uint32_t flags, uint32_t* __restrict__ ctr, uint32_t* __restrict__ ready,
-    uint32_t P) {
+    uint32_t P, uint32_t P2, uint32_t U1) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ uint32_t qCount[2];
   __shared__ uint32_t item;
@@ -737,7 +737,10 @@ __global__ __launch_bounds__(kLdsBlock) void spf_lds_route_kernel(
   const LdsGroup& last = grps.g[grps.n - 1u];
   const uint32_t U = last.base + last.n;
   const uint32_t G = min(U, gridDim.x);
-  const uint32_t total = G + U * (P + 1u);
+  // units [0, U1) stream in P prefix ranges, the last U - U1 in P2 (smaller
+  // items at the end of the queue shorten the launch's tail)
+  const uint32_t headItems = U1 * (P + 1u);
+  const uint32_t total = G + headItems + (U - U1) * (P2 + 1u);
   LdsWg wg;
   NoDiag dg;
   for (;;) {
@@ -746,12 +749,20 @@ __global__ __launch_bounds__(kLdsBlock) void spf_lds_route_kernel(
     const uint32_t i = item;
     __syncthreads();  // every lane has read item before lane 0 takes the next
     if (i >= total) break;
-    uint32_t gu = i, part = 0;
+    uint32_t gu = i, part = 0, parts = P;
     bool spf = true;
     if (i >= G) {
-      const uint32_t j = i - G;
-      gu = j / (P + 1u);
-      const uint32_t r = j - gu * (P + 1u);
+      uint32_t j = i - G, r;
+      if (j < headItems) {
+        gu = j / (P + 1u);
+        r = j - gu * (P + 1u);
+      } else {
+        j -= headItems;
+        const uint32_t b = j / (P2 + 1u);
+        r = j - b * (P2 + 1u);
+        gu = U1 + b;
+        parts = P2;
+      }
       if (r == 0u) {
         gu += G;
         if (gu >= U) continue;
@@ -793,10 +804,10 @@ __global__ __launch_bounds__(kLdsBlock) void spf_lds_route_kernel(
     // the per-node records go to the state region (the image stays)
     uint32_t* rec0 = reinterpret_cast<uint32_t*>(smem + L.block);
     switch (grp.W) {
-      case 1: lds_stream_item<1, KeyT>(g, pt, key, grp, u, part, P, flags, rec0); break;
-      case 2: lds_stream_item<2, KeyT>(g, pt, key, grp, u, part, P, flags, rec0); break;
-      case 3: lds_stream_item<3, KeyT>(g, pt, key, grp, u, part, P, flags, rec0); break;
-      default: lds_stream_item<4, KeyT>(g, pt, key, grp, u, part, P, flags, rec0); break;
+      case 1: lds_stream_item<1, KeyT>(g, pt, key, grp, u, part, parts, flags, rec0); break;
+      case 2: lds_stream_item<2, KeyT>(g, pt, key, grp, u, part, parts, flags, rec0); break;
+      case 3: lds_stream_item<3, KeyT>(g, pt, key, grp, u, part, parts, flags, rec0); break;
+      default: lds_stream_item<4, KeyT>(g, pt, key, grp, u, part, parts, flags, rec0); break;
     }
   }
 }
@@ -892,6 +903,7 @@ int g_ldsGrid = 0;
 // "lds_key16": packed 16-bit route keys on topologies of <= 16,384 nodes
 // (1, default) or u32 keys (0, A/B)
 int g_ldsKey16 = 1;
+int g_ldsTail = 1;
 
 bool lds_key16(const ogs_graph& g) {
   return g_ldsKey16 && g.max_nodes > 0 && uint32_t(g.max_nodes) <= kKey16MaxNodes;
@@ -932,12 +944,18 @@ hipError_t launch_spf_lds_routes(const ogs_graph& g, const ogs_prefix_table& pt,
   // units per CU); profiles/r04_lds_store_parts_ab.log
   const uint32_t P = g_ldsParts > 0 ? uint32_t(g_ldsParts)
                                     : (uint32_t(U) >= 4u * uint32_t(grid) ? 2u : 4u);
+  // "lds_tail" (default 1): with fewer than 4 ranges per unit, the last
+  // grid's worth of units stream in 4 (the queue's final items are the
+  // launch's tail); 0 every unit in P
+  const uint32_t P2 = (g_ldsTail && P < 4u) ? 4u : P;
+  const uint32_t U1 = P2 != P ? uint32_t(U - std::min(U, grid)) : uint32_t(U);
   if (g_routeStoreNt & 1) flags |= kFlagNtStores;
   auto go = [&](auto k, auto keyp) {
     hipError_t a = allow_lds(k, lds);
     if (a != hipSuccess) return a;
     hipLaunchKernelGGL(k, dim3(grid), dim3(kLdsBlock), lds, stream, g, pt, keyp, L,
-                       static_cast<const uint8_t*>(base), mm, S.nEB, G, flags, ctr, ready, P);
+                       static_cast<const uint8_t*>(base), mm, S.nEB, G, flags, ctr, ready, P,
+                       P2, U1);
     return hipGetLastError();
   };
   return key16 ? go(spf_lds_route_kernel<uint16_t>, static_cast<const uint16_t*>(key))
