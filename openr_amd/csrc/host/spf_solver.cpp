@@ -617,7 +617,11 @@ DecisionRouteDb materializeRouteDb(
     const std::map<std::string, RibUnicastEntry>& statics,
     std::map<std::string, RouteSelectionResult>* bestRoutesCache) {
   DecisionRouteDb rdb;
-  if (bestRoutesCache) bestRoutesCache->clear();
+  // SpfSolver.cpp:98 clears the cache per build; the single-threaded build
+  // refills it from the previous build's nodes (keys and selection sets
+  // reassigned in place) instead of freeing and allocating ~20k of them
+  std::map<std::string, RouteSelectionResult> spare;
+  if (bestRoutesCache) spare.swap(*bestRoutesCache);
   const auto meIt = f.id.find(me);
   const uint32_t rb = meIt == f.id.end() ? 0u : f.rowPtr[meIt->second];
   // sorted positions [i0, i1) into `routes` / `sel`: walked in prefix order
@@ -625,6 +629,7 @@ DecisionRouteDb materializeRouteDb(
   // the map's hint
   const std::vector<uint32_t>& sorted = pt.sortedOrder();
   std::atomic<uint64_t> noRoute{0};  // decision.no_route_to_prefix (SpfSolver.cpp:221, 242)
+  bool recycle = false;  // spare nodes are reused by the single-threaded build only
   auto build = [&](uint32_t i0, uint32_t i1, std::map<std::string, RibUnicastEntry>& routes,
                    std::map<std::string, RouteSelectionResult>* cache) {
     uint64_t unreachable = 0;
@@ -634,14 +639,36 @@ DecisionRouteDb materializeRouteDb(
       unreachable += noRouteReason(meta);
       if (cache && (meta & OGS_ROUTE_SELECTED)) {  // SpfSolver.cpp:247
         const uint32_t a0 = pt.advOff[p];
-        RouteSelectionResult sel;
         const uint32_t a1 = pt.advOff[p + 1];
-        for (uint32_t a = a0; a < std::min(a1, a0 + 32); ++a) {
-          if (r.sel[p] >> (a - a0) & 1u) sel.allNodeAreas.insert(pt.advKey[a]);
+        if (recycle && !spare.empty()) {
+          auto nh = spare.extract(spare.begin());
+          nh.key() = pt.prefixes[p];
+          RouteSelectionResult& sel = nh.mapped();
+          auto& areas = sel.allNodeAreas;
+          decltype(areas.extract(areas.begin())) keep;
+          if (!areas.empty()) keep = areas.extract(areas.begin());
+          areas.clear();
+          for (uint32_t a = a0; a < std::min(a1, a0 + 32); ++a) {
+            if (!(r.sel[p] >> (a - a0) & 1u)) continue;
+            if (keep) {
+              keep.value() = pt.advKey[a];
+              areas.insert(areas.end(), std::move(keep));
+            } else {
+              areas.insert(pt.advKey[a]);
+            }
+          }
+          sel.bestNodeArea = pt.advKey[a0 + (meta >> OGS_ROUTE_BEST_SHIFT)];
+          sel.isBestNodeDrained = meta & OGS_ROUTE_DRAINED;
+          cache->insert(cache->end(), std::move(nh));
+        } else {
+          RouteSelectionResult sel;
+          for (uint32_t a = a0; a < std::min(a1, a0 + 32); ++a) {
+            if (r.sel[p] >> (a - a0) & 1u) sel.allNodeAreas.insert(pt.advKey[a]);
+          }
+          sel.bestNodeArea = pt.advKey[a0 + (meta >> OGS_ROUTE_BEST_SHIFT)];
+          sel.isBestNodeDrained = meta & OGS_ROUTE_DRAINED;
+          cache->insert_or_assign(cache->end(), pt.prefixes[p], std::move(sel));
         }
-        sel.bestNodeArea = pt.advKey[a0 + (meta >> OGS_ROUTE_BEST_SHIFT)];
-        sel.isBestNodeDrained = meta & OGS_ROUTE_DRAINED;
-        cache->insert_or_assign(cache->end(), pt.prefixes[p], std::move(sel));
       }
       if (!(meta & OGS_ROUTE_VALID)) continue;
       auto e = materializeRouteAt(f, rb, me, pt, p, meta, r.metric[p], &r.mask[p],
@@ -659,6 +686,7 @@ DecisionRouteDb materializeRouteDb(
   // on one (the routes are freed later on the caller's thread, across the
   // workers' malloc arenas).
   const size_t T = g_materializeThreads > 0 ? size_t(g_materializeThreads) : 1;
+  recycle = T <= 1;
   if (T <= 1) {
     build(0, r.P, rdb.unicastRoutes, bestRoutesCache);
   } else {
