@@ -301,7 +301,14 @@ int ogs_host_free(void* hptr);
  *                 default: then the last grid's worth of units in 4) from a
  *                 device-wide counter, SPFs kept one grid ahead; route keys
  *                 packed into 16 bits on topologies of <= 16,384 nodes
- *                 ("lds_key16" 1, default; 0 u32 keys, A/B). Scratch
+ *                 ("lds_key16" 1, default; 0 u32 keys, A/B); units streamed
+ *                 in SPF completion order ("lds_ready" 1, default; 0 unit
+ *                 order, A/B); unit-weight (BFS) SPFs stop once every node
+ *                 is reached ("lds_bfs_exit" 1, default; 0 they run the
+ *                 empty last layer, A/B); "lds_tiles" T > 0: each unit's
+ *                 rows in T tiles claimed dynamically by the workgroups on
+ *                 the unit, idle workgroups joining the unit with the most
+ *                 tiles left (0: fixed ranges). Scratch
  *                 (prefix keys, dist/next-hop sets when out->dist / out->nh
  *                 are NULL) comes from a grow-only per-device workspace.
  *                 "route_store_nt", bits: 1 the RouteDb stream's 16-B stores

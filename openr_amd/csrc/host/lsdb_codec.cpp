@@ -770,8 +770,9 @@ std::string getNodeNameFromKey(const std::string& key) {  // LsdbUtil.cpp:691-69
   return key.substr(a + 1, b == std::string::npos ? std::string::npos : b - a - 1);
 }
 
-// The pure half of updateKeyInLsdb: decode (no state touched), so a
-// publication's values can be decoded on several threads.
+// The pure half of updateKeyInLsdb: decode (no state touched). The
+// publication path calls it single-threaded, streamed key by key (decoding
+// on host threads first was measured slower, lsdb_codec.h).
 LsdbIngest::Decoded LsdbIngest::decodeKey(const std::string& key,
                                           const std::optional<std::string_view>& rawVal) {
   Decoded d;

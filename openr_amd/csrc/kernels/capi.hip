@@ -19,6 +19,9 @@ extern int g_ldsParts;
 extern int g_ldsGrid;
 extern int g_ldsKey16;
 extern int g_ldsTail;
+extern int g_ldsReady;
+extern int g_ldsBfsExit;
+extern int g_ldsTiles;
 extern int g_routeStoreNt;
 extern int g_spfSeedRow;
 extern int g_frontierBlock;
@@ -206,6 +209,21 @@ int ogs_set_option(const char* name, int64_t value) {
   if (std::strcmp(name, "lds_tail") == 0) {
     if (value != 0 && value != 1) return fail(OGS_E_INVALID, "lds_tail must be 0 or 1");
     ogs::g_ldsTail = int(value);
+    return OGS_OK;
+  }
+  if (std::strcmp(name, "lds_ready") == 0) {
+    if (value != 0 && value != 1) return fail(OGS_E_INVALID, "lds_ready must be 0 or 1");
+    ogs::g_ldsReady = int(value);
+    return OGS_OK;
+  }
+  if (std::strcmp(name, "lds_tiles") == 0) {
+    if (value < 0 || value > 256) return fail(OGS_E_INVALID, "lds_tiles must be in [0, 256]");
+    ogs::g_ldsTiles = int(value);
+    return OGS_OK;
+  }
+  if (std::strcmp(name, "lds_bfs_exit") == 0) {
+    if (value != 0 && value != 1) return fail(OGS_E_INVALID, "lds_bfs_exit must be 0 or 1");
+    ogs::g_ldsBfsExit = int(value);
     return OGS_OK;
   }
   if (std::strcmp(name, "lds_key16") == 0) {

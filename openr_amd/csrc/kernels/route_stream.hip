@@ -365,6 +365,7 @@ hipError_t launch_spf_routes(const ogs_graph& g, const ogs_prefix_table* pt,
                              const ogs_unit* units, int nUnits, uint32_t flags, int W,
                              const ogs_spf_out& out, hipStream_t stream, int* unsupported);
 int small_unit_width();
+bool use_global(const ogs_graph& g, int W, uint32_t flags);
 
 // ogs_spf_routes_groups: every group's RouteDbs over one graph / prefix
 // table. With route_stream 5 on a large shared topology whose image fits
@@ -384,9 +385,14 @@ hipError_t launch_spf_routes_groups(const ogs_graph& g, const ogs_prefix_table* 
     U += groups[i].n_units;
   }
   const size_t Sp = pt ? size_t(pt->max_prefixes) : 0;
+  // the same gating as launch_spf_routes before its large-topology forms:
+  // topologies of <= 256 nodes go to the wave / small kernels, and
+  // use_global() (deep graphs past the frontier's LDS budget, or the
+  // "spf_global" option) to the HBM-state frontier -- so a group gets the
+  // same engine here as through ogs_spf_routes
   bool one = g_routeStream == 5 && pt && Sp > 0 && g.edge_src && g.max_nodes > 256 &&
       !(flags & (OGS_F_EXACT_ORDER | OGS_F_WIDE_METRIC)) && small_unit_width() == -1 &&
-      !lg.empty() && lg.size() <= 4 && Wmax <= 4;
+      !lg.empty() && lg.size() <= 4 && Wmax <= 4 && !use_global(g, Wmax, flags);
   const size_t ldsBytes = one ? lds_scratch_bytes(g, Wmax, U) : 0;
   if (!ldsBytes) {
     for (const LdsRouteGroup& x : lg) {

@@ -387,8 +387,10 @@ __device__ __forceinline__ void frontier_spf_packed(
     const uint32_t* __restrict__ gRow, uint32_t e0, uint64_t* dn, uint8_t* stamp,
     uint64_t* tp, const DeadEdges& dead, bool seedRow, bool slotWalk, bool preload) {
   // u8 round stamps (1 B per node, so 8 C3 units fit a CU): after 256
-  // rounds a stale stamp can match again -- that node is pushed once more
-  // with its current word, a no-op for the monotone fixpoint
+  // rounds a stale stamp can match again -- a reached node is pushed once
+  // more with its current word, a no-op for the monotone fixpoint; an
+  // unreached one (dist kInf, never stamped: stamp 0 == uint8_t(256)) is
+  // skipped in relax, since kInf + w would wrap to a small candidate
   constexpr uint32_t kInf = 0xFFFFFFFFu;
   const int tid = threadIdx.x;
   for (uint32_t v = tid; v < N; v += B) {
@@ -445,6 +447,7 @@ __device__ __forceinline__ void frontier_spf_packed(
       const uint32_t v = uint32_t(ch) & OGS_EDGE_DST_MASK;
       const uint64_t xv = dn[v];
       const uint32_t dv = static_cast<uint32_t>(xv), nv = static_cast<uint32_t>(xv >> 32);
+      if (dv == kInf) return;  // a stale stamp on an unreached node
       const uint32_t b = uint32_t(ch >> 32);
       // the targets' distances first (independent LDS reads): a longer
       // candidate -- most pushes of a dense frontier -- is dropped without

@@ -45,8 +45,17 @@ constexpr uint32_t kNodeMax = 0x7FFFu;    // 15-bit neighbour ids
 constexpr uint32_t kDrained16 = 0x8000u;  // cnode: the chunk's node is hard-drained
 constexpr uint32_t kLdsChunk = 8;         // edges per chunk (one lane's push)
 constexpr int kLdsBlock = 1024;
+// launch flags of the LDS forms (above the OGS_F_* bits): the BFS rounds'
+// all-reached exit off ("lds_bfs_exit" 0, A/B), and the one-launch form's
+// streams in unit order instead of SPF completion order ("lds_ready" 0)
+constexpr uint32_t kFlagLdsNoBfsExit = 1u << 25;
+constexpr uint32_t kFlagLdsUnitOrder = 1u << 24;
 
 __host__ __device__ inline uint32_t al16(uint32_t x) { return (x + 15u) & ~15u; }
+
+// u8 round stamp of round r >= 1 in the general-weight rounds: 1..255
+// cyclic, never 0 (= not pending); stamp_of(2) == 2 (the seed round's value)
+__device__ __forceinline__ uint32_t stamp_of(uint32_t r) { return 1u + (r - 1u) % 255u; }
 
 // chunk records of one topology: sum over nodes of ceil(deg / 8) <= (E + 7 N) / 8
 __host__ __device__ inline uint32_t chunk_cap(uint32_t N, uint32_t E) {
@@ -97,7 +106,8 @@ __host__ LdsScratch lds_scratch(const ogs_graph& g, const LdsImage& L, int nUnit
   S.mm = r256(size_t(g.num_topos) * L.stride);
   S.ctr = S.mm + r256(size_t(g.num_topos) * S.nEB * 8u);
   S.ready = S.ctr + 256u;
-  S.bytes = S.ready + r256(size_t(std::max(nUnits, 1)) * 4u);
+  // ready words + the tile counters of the one-launch form, one each per unit
+  S.bytes = S.ready + r256(size_t(std::max(nUnits, 1)) * 8u);
   return S;
 }
 
@@ -124,7 +134,10 @@ __global__ __launch_bounds__(kLdsBlock) void lds_prep_kernel(
   if (blk < T) {
     const uint32_t t = blk;
     if (t == 0u) {
-      if (tid == 0u) *ctr = 0u;
+      if (tid == 0u) {
+        ctr[0] = 0u;   // work items
+        ctr[32] = 0u;  // ready-list slots (spf_lds_route_kernel)
+      }
       for (uint32_t i = tid; i < nReady; i += B) ready[i] = 0u;
     }
     const uint32_t nb = g.node_base[t];
@@ -449,9 +462,19 @@ __device__ __forceinline__ void spf_lds_unit(
         }
       };
       for (uint32_t r = 2;; ++r) {
+        // round stamps of the general-weight rounds (1..255, 0 = not pending)
+        const uint32_t stCur = stamp_of(r), stPrev = stamp_of(r - 1u), stNext = stamp_of(r + 1u);
         // (0) the queue of round r: four chunk slots per thread per step, the
         // workgroup stepping together (every lane takes part in the ballots)
         uint32_t* qc = &qCount[r & 1u];
+        // BFS layers: is any node still unreached? If none is, layer r is
+        // empty -- round r's pushes from layer r - 1 can neither reach a node
+        // nor be tight (a target at distance r * wc would be in layer r) --
+        // and the fixpoint is reached without the push pass
+        bool unreached = false;
+        if constexpr (kBfs) {
+          for (uint32_t v = tid; v < N; v += B) unreached |= dist[v] == kInf;
+        }
         for (uint32_t c0 = 0; c0 < C; c0 += 4u * B) {
           uint32_t cs[4], vs[4];
           bool act[4];
@@ -466,7 +489,16 @@ __device__ __forceinline__ void spf_lds_unit(
               act[k] = !(vs[k] & kDrained16) &&
                   uint64_t(dist[vs[k] & kNodeMax]) == uint64_t(r - 1u) * wc;
             } else {
-              act[k] = !(vs[k] & kDrained16) && stamp[vs[k]] == uint8_t(r);
+              // exact u8 stamps: st(r) cycles through 1..255 and a node
+              // still carrying last round's value (pushed then, unchanged
+              // since) is cleared here, so every live stamp is st(r) or 0
+              // -- a stale stamp never matches again after 255 rounds (it
+              // would re-queue settled nodes every round: no fixpoint exit
+              // on paths of 256+ hops), and unreached nodes are never queued
+              const uint32_t v = vs[k] & kNodeMax;
+              const uint32_t sv = stamp[v];
+              if (sv == stPrev) stamp[v] = 0;
+              act[k] = !(vs[k] & kDrained16) && sv == stCur;
             }
           }
           uint64_t m[4];
@@ -488,10 +520,17 @@ __device__ __forceinline__ void spf_lds_unit(
             at += uint32_t(__popcll(m[k]));
           }
         }
-        __syncthreads();
+        if constexpr (kBfs) {
+          unreached = __syncthreads_or(unreached);
+        } else {
+          __syncthreads();
+        }
         mark(8u + 3u * (r - 2u));
         const uint32_t nq = *qc;
         if (nq == 0u) break;  // nothing stamped r: the fixpoint
+        if constexpr (kBfs) {
+          if (!unreached && !(flags & kFlagLdsNoBfsExit)) break;
+        }
         dg.queued(nq);
         if (tid == 0u) qCount[(r + 1u) & 1u] = 0u;  // next round's counter
         // the queue is walked transposed: lane l of a wave takes entries
@@ -547,7 +586,7 @@ __device__ __forceinline__ void spf_lds_unit(
             if ((k.x[i] & kDown16) || k.cand[i] >= k.dt[i]) continue;
             const uint32_t t = k.x[i] & kNodeMax;
             atomicMin(&dist[t], k.cand[i]);
-            stamp[t] = uint8_t(r + 1u);
+            stamp[t] = uint8_t(stNext);
 #pragma unroll
             for (int w = 0; w < W; ++w) nh[t * W + w] = 0u;
           }
@@ -562,7 +601,7 @@ __device__ __forceinline__ void spf_lds_unit(
           if (q >= nq) continue;
           Chunk k;
           load(q, k);
-          if (stamp[k.v] != uint8_t(r)) continue;
+          if (stamp[k.v] != stCur) continue;
           uint32_t nv[W];
 #pragma unroll
           for (int w = 0; w < W; ++w) nv[w] = nh[k.v * W + w];
@@ -589,7 +628,7 @@ __device__ __forceinline__ void spf_lds_unit(
                 add = true;
               }
             }
-            if (add) stamp[t] = uint8_t(r + 1u);
+            if (add) stamp[t] = uint8_t(stNext);
           }
         }
         __syncthreads();
@@ -666,13 +705,19 @@ struct LdsGroups {
   uint32_t n;
 };
 
-// One stream item: prefix range `part` (of P) of local unit u of group grp,
-// from the published SPF rows: per-node records into LDS, then the rows.
+// One stream item of local unit u of group grp, from the published SPF rows:
+// per-node records into LDS, then the unit's prefix rows -- either range
+// `part` of P (fixed ranges), or, with tiles (tctr != nullptr), T tiles of
+// the unit taken one by one from its tile counter, so the workgroups on one
+// unit share its rows dynamically and any workgroup can join a unit late
+// (the launch's tail). sTile: two shared words (the next tile, double
+// buffered so one barrier per tile suffices).
 template <int W, typename KeyT>
 __device__ __forceinline__ void lds_stream_item(const ogs_graph& g, const ogs_prefix_table& pt,
                                                 const KeyT* __restrict__ key,
                                                 const LdsGroup& grp, uint32_t u, uint32_t part,
-                                                uint32_t P, uint32_t flags, uint32_t* rec0) {
+                                                uint32_t P, uint32_t flags, uint32_t* rec0,
+                                                uint32_t* tctr, uint32_t T, uint32_t* sTile) {
   constexpr uint32_t kInf = 0xFFFFFFFFu;
   const uint32_t tid = threadIdx.x;
   const uint32_t Sn = uint32_t(g.max_nodes), Sp = uint32_t(pt.max_prefixes);
@@ -687,6 +732,8 @@ __device__ __forceinline__ void lds_stream_item(const ogs_graph& g, const ogs_pr
   uint32_t* rMeta = rec0;
   uint32_t* rMetric = rMeta + Sn;
   uint32_t* rMask = rMetric + Sn;  // [W][Sn]
+  // the first tile is claimed while the records are built
+  if (tctr && tid == 0u) sTile[0] = atomicAdd(tctr, 1u);
   for (uint32_t v = tid; v < N; v += kLdsBlock) {
     const uint32_t d = sv.dist(v);
     uint32_t m[W], cnt = 0;
@@ -703,8 +750,6 @@ __device__ __forceinline__ void lds_stream_item(const ogs_graph& g, const ogs_pr
   __syncthreads();
   const uint32_t p0 = pt.pfx_base[t];
   const uint32_t Pn = pt.pfx_base[t + 1] - p0;
-  const uint32_t span = ((Pn + P - 1u) / P + 3u) & ~3u;
-  const uint32_t lo = min(Pn, part * span), hi = min(Pn, lo + span);
   auto rec = [&](uint32_t v, Rec<W>& r) {
     r.meta = rMeta[v];
     r.metric = rMetric[v];
@@ -712,13 +757,33 @@ __device__ __forceinline__ void lds_stream_item(const ogs_graph& g, const ogs_pr
     for (int w = 0; w < W; ++w) r.mask[w] = rMask[w * Sn + v];
   };
   const bool nt = (flags & kFlagNtStores) != 0;
-  if (grp.outs3) {
-    stream_routes<W, false, true, kLdsBlock>(pt, key + size_t(t) * Sp, p0, Pn, Sp, u, s, nflags,
-                                             sv, cfg, grp.out, rec, nullptr, nt, lo, hi);
+  auto stream = [&](uint32_t lo, uint32_t hi) {
+    if (grp.outs3) {
+      stream_routes<W, false, true, kLdsBlock>(pt, key + size_t(t) * Sp, p0, Pn, Sp, u, s,
+                                               nflags, sv, cfg, grp.out, rec, nullptr, nt, lo,
+                                               hi);
+    } else {
+      stream_routes<W, false, false, kLdsBlock>(pt, key + size_t(t) * Sp, p0, Pn, Sp, u, s,
+                                                nflags, sv, cfg, grp.out, rec, nullptr, nt, lo,
+                                                hi);
+    }
+  };
+  if (!tctr) {
+    const uint32_t span = ((Pn + P - 1u) / P + 3u) & ~3u;
+    const uint32_t lo = min(Pn, part * span);
+    stream(lo, min(Pn, lo + span));
   } else {
-    stream_routes<W, false, false, kLdsBlock>(pt, key + size_t(t) * Sp, p0, Pn, Sp, u, s,
-                                              nflags, sv, cfg, grp.out, rec, nullptr, nt, lo,
-                                              hi);
+    const uint32_t span = ((Pn + T - 1u) / T + 3u) & ~3u;
+    uint32_t cur = sTile[0];
+    for (uint32_t k = 1; cur < T; k ^= 1u) {
+      uint32_t nxt = 0;
+      if (tid == 0u) nxt = atomicAdd(tctr, 1u);  // the next tile, while this one streams
+      const uint32_t lo = min(Pn, cur * span);
+      stream(lo, min(Pn, lo + span));
+      if (tid == 0u) sTile[k] = nxt;
+      __syncthreads();
+      cur = sTile[k];
+    }
   }
   __syncthreads();  // the records are read before the next item reuses LDS
 }
@@ -744,29 +809,72 @@ __global__ __launch_bounds__(kLdsBlock) void spf_lds_route_kernel(
     ogs_graph g, ogs_prefix_table pt, const KeyT* __restrict__ key, LdsImage L,
     const uint8_t* __restrict__ img, const uint2* __restrict__ mm, uint32_t nEB,
     LdsGroups grps, uint32_t flags, uint32_t* __restrict__ ctr, uint32_t* __restrict__ ready,
-    uint32_t P, uint32_t P2, uint32_t U1) {
+    uint32_t P, uint32_t P2, uint32_t U1, uint32_t T) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ uint32_t qCount[2];
-  __shared__ uint32_t item;
+  __shared__ uint32_t item, slotUnit, sTile[2];
   const uint32_t tid = threadIdx.x;
   const LdsGroup& last = grps.g[grps.n - 1u];
   const uint32_t U = last.base + last.n;
   const uint32_t G = min(U, gridDim.x);
-  // units [0, U1) stream in P prefix ranges, the last U - U1 in P2 (smaller
+  // stream slots [0, U1) in P prefix ranges, the last U - U1 in P2 (smaller
   // items at the end of the queue shorten the launch's tail)
   const uint32_t headItems = U1 * (P + 1u);
   const uint32_t total = G + headItems + (U - U1) * (P2 + 1u);
+  // completion order (default): stream slot b is the b-th SPF to finish --
+  // ready[b] = its global unit + 1, appended through the counter ctr[32] --
+  // so no workgroup waits on a slow (wide) SPF while finished units still
+  // have rows to write. Unit order (kFlagLdsUnitOrder): slot b = unit b,
+  // ready[b] a flag.
+  const bool unitOrder = (flags & kFlagLdsUnitOrder) != 0u;
+  uint32_t* rctr = ctr + 32;  // its own 128-B half of the counters' line
+  // tiles (T > 0): per stream slot a tile counter after the ready words
+  uint32_t* tiles = T ? ready + U : nullptr;
   LdsWg wg;
   NoDiag dg;
   for (;;) {
     if (tid == 0u) item = atomicAdd(ctr, 1u);
     __syncthreads();
-    const uint32_t i = item;
+    uint32_t i = item;
     __syncthreads();  // every lane has read item before lane 0 takes the next
-    if (i >= total) break;
+    if (i >= total) {
+      // the queue is empty: with tiles, join the stream slot with the most
+      // tiles left (every SPF is handed out by now, so its wait ends);
+      // done when no slot has any
+      if (!T) break;
+      if (tid < 64u) {
+        uint32_t best = 0, at = 0;
+        for (uint32_t b = tid; b < U; b += 64u) {
+          const uint32_t taken =
+              __hip_atomic_load(&tiles[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          const uint32_t rem = taken < T ? T - taken : 0u;
+          if (rem > best) {
+            best = rem;
+            at = b;
+          }
+        }
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) {
+          const uint32_t ob = __shfl_xor(best, d, 64), oa = __shfl_xor(at, d, 64);
+          if (ob > best || (ob == best && oa < at)) {
+            best = ob;
+            at = oa;
+          }
+        }
+        if (tid == 0u) item = best ? at : 0xFFFFFFFFu;
+      }
+      __syncthreads();
+      const uint32_t slot = item;
+      __syncthreads();
+      if (slot == 0xFFFFFFFFu) break;
+      i = G + total + slot;  // a join of that slot (below)
+    }
     uint32_t gu = i, part = 0, parts = P;
     bool spf = true;
-    if (i >= G) {
+    if (i >= G + total) {  // join (tiles): the slot, no fixed part
+      gu = i - (G + total);
+      spf = false;
+    } else if (i >= G) {
       uint32_t j = i - G, r;
       if (j < headItems) {
         gu = j / (P + 1u);
@@ -786,11 +894,11 @@ __global__ __launch_bounds__(kLdsBlock) void spf_lds_route_kernel(
         part = r - 1u;
       }
     }
-    uint32_t gi = 0;
-    while (gi + 1u < grps.n && gu >= grps.g[gi + 1u].base) ++gi;
-    const LdsGroup& grp = grps.g[gi];
-    const uint32_t u = gu - grp.base;
     if (spf) {
+      uint32_t gi = 0;
+      while (gi + 1u < grps.n && gu >= grps.g[gi + 1u].base) ++gi;
+      const LdsGroup& grp = grps.g[gi];
+      const uint32_t u = gu - grp.base;
       const ogs_unit unit = grp.units[u];
       switch (grp.W) {
         case 1: spf_lds_unit<1>(g, L, img, mm, nEB, unit, u, flags, grp.dist, grp.nh, smem, qCount, wg, dg); break;
@@ -798,31 +906,47 @@ __global__ __launch_bounds__(kLdsBlock) void spf_lds_route_kernel(
         case 3: spf_lds_unit<3>(g, L, img, mm, nEB, unit, u, flags, grp.dist, grp.nh, smem, qCount, wg, dg); break;
         default: spf_lds_unit<4>(g, L, img, mm, nEB, unit, u, flags, grp.dist, grp.nh, smem, qCount, wg, dg); break;
       }
-      // publish: every wave's row stores drained, barrier, release, flag
+      // publish: every wave's row stores drained, barrier, release, then the
+      // flag (unit order) or the unit's slot in the ready list
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (tid == 0u) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store(&ready[gu], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (unitOrder) {
+          __hip_atomic_store(&ready[gu], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+          const uint32_t slot = atomicAdd(rctr, 1u);
+          __hip_atomic_store(&ready[slot], gu + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
       }
       continue;
     }
+    // stream slot gu: wait for its SPF (a handed-out SPF item: it finishes)
+    uint32_t* tc = T ? tiles + gu : nullptr;
     if (tid == 0u) {
-      while (__hip_atomic_load(&ready[gu], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+      uint32_t x;
+      while ((x = __hip_atomic_load(&ready[gu], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) ==
+             0u) {
         __builtin_amdgcn_s_sleep(8);
       }
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      slotUnit = unitOrder ? gu : x - 1u;
     }
     __syncthreads();
+    gu = slotUnit;
+    uint32_t gi = 0;
+    while (gi + 1u < grps.n && gu >= grps.g[gi + 1u].base) ++gi;
+    const LdsGroup& grp = grps.g[gi];
+    const uint32_t u = gu - grp.base;
     // the per-node records go to the state region (the image stays)
     uint32_t* rec0 = reinterpret_cast<uint32_t*>(smem + L.block);
     switch (grp.W) {
-      case 1: lds_stream_item<1, KeyT>(g, pt, key, grp, u, part, parts, flags, rec0); break;
-      case 2: lds_stream_item<2, KeyT>(g, pt, key, grp, u, part, parts, flags, rec0); break;
-      case 3: lds_stream_item<3, KeyT>(g, pt, key, grp, u, part, parts, flags, rec0); break;
-      default: lds_stream_item<4, KeyT>(g, pt, key, grp, u, part, parts, flags, rec0); break;
+      case 1: lds_stream_item<1, KeyT>(g, pt, key, grp, u, part, parts, flags, rec0, tc, T, sTile); break;
+      case 2: lds_stream_item<2, KeyT>(g, pt, key, grp, u, part, parts, flags, rec0, tc, T, sTile); break;
+      case 3: lds_stream_item<3, KeyT>(g, pt, key, grp, u, part, parts, flags, rec0, tc, T, sTile); break;
+      default: lds_stream_item<4, KeyT>(g, pt, key, grp, u, part, parts, flags, rec0, tc, T, sTile); break;
     }
   }
 }
@@ -872,9 +996,11 @@ hipError_t launch_lds_prep(const ogs_graph& g, const ogs_prefix_table* pt, void*
                      g, ptv, nKB ? key : nullptr, key16 ? 1u : 0u, nKB, L, base,
                      reinterpret_cast<uint2*>(base + S.mm), S.nEB,
                      reinterpret_cast<uint32_t*>(base + S.ctr),
-                     reinterpret_cast<uint32_t*>(base + S.ready), uint32_t(nUnits));
+                     reinterpret_cast<uint32_t*>(base + S.ready), 2u * uint32_t(nUnits));
   return hipGetLastError();
 }
+
+extern int g_ldsBfsExit;
 
 template <typename K>
 static hipError_t allow_lds(K k, uint32_t lds) {
@@ -895,6 +1021,7 @@ hipError_t launch_spf_lds(const ogs_graph& g, const ogs_unit* units, int nUnits,
   const uint2* mm = reinterpret_cast<const uint2*>(img + S.mm);
   const uint32_t lds = L.block + L.state;
   const int grid = std::max(1, std::min(nUnits, num_cus()));
+  if (!g_ldsBfsExit) flags |= kFlagLdsNoBfsExit;
   auto go = [&](auto k) {
     hipError_t a = allow_lds(k, lds);
     if (a != hipSuccess) return a;
@@ -919,6 +1046,15 @@ int g_ldsGrid = 0;
 // (1, default) or u32 keys (0, A/B)
 int g_ldsKey16 = 1;
 int g_ldsTail = 1;
+// "lds_ready": the one-launch form streams units in SPF completion order
+// (1, default) or unit order (0, A/B); "lds_bfs_exit": the BFS rounds stop
+// once every node is reached (1, default) or run the empty last layer (0)
+int g_ldsReady = 1;
+int g_ldsBfsExit = 1;
+// "lds_tiles": 0 fixed prefix ranges per stream item; T > 0 each unit's rows
+// in T tiles taken dynamically by the workgroups on that unit, and
+// workgroups left without items join the unit with the most tiles left
+int g_ldsTiles = 0;
 
 bool lds_key16(const ogs_graph& g) {
   return g_ldsKey16 && g.max_nodes > 0 && uint32_t(g.max_nodes) <= kKey16MaxNodes;
@@ -965,12 +1101,14 @@ hipError_t launch_spf_lds_routes(const ogs_graph& g, const ogs_prefix_table& pt,
   const uint32_t P2 = (g_ldsTail && P < 4u) ? 4u : P;
   const uint32_t U1 = P2 != P ? uint32_t(U - std::min(U, grid)) : uint32_t(U);
   if (g_routeStoreNt & 1) flags |= kFlagNtStores;
+  if (!g_ldsReady) flags |= kFlagLdsUnitOrder;
+  if (!g_ldsBfsExit) flags |= kFlagLdsNoBfsExit;
   auto go = [&](auto k, auto keyp) {
     hipError_t a = allow_lds(k, lds);
     if (a != hipSuccess) return a;
     hipLaunchKernelGGL(k, dim3(grid), dim3(kLdsBlock), lds, stream, g, pt, keyp, L,
                        static_cast<const uint8_t*>(base), mm, S.nEB, G, flags, ctr, ready, P,
-                       P2, U1);
+                       P2, U1, uint32_t(g_ldsTiles));
     return hipGetLastError();
   };
   return key16 ? go(spf_lds_route_kernel<uint16_t>, static_cast<const uint16_t*>(key))

@@ -1632,8 +1632,8 @@ PYBIND11_MODULE(_decision, m) {
           for (size_t i = 0; i < keys.size(); ++i) pub[i] = PublicationKeyVal{keys[i], vals[i]};
           for (int r = 0; r < reps; ++r) {
             {
-              // the whole publication through processPublication (decode on
-              // host threads, then the per-key apply in key order)
+              // the whole publication through processPublication (one host
+              // thread: each key decoded and applied in key order, streamed)
               AreaLinkStates als;
               PrefixState ps0;
               LsdbIngest ing0("test_node", {g.area});

@@ -1,0 +1,81 @@
+#!/bin/bash
+# One parametrised driver for GPU-box evidence runs (replaces the one-off
+# gpu_rNN*.sh wrappers). Run on the box via gpurun, from the repo root:
+#   bash tools/gpu.sh <recipe> [<recipe> ...]
+# Recipes run in order; the first failure (non-zero, timeout, fault) ends the
+# call. Each step has its own time limit; logs land in gpurun_out/<name>.log.
+#   tests[:<pytest -k expr>]  GPU test suite (or a -k subset)
+#   testfile:<path>           one test file
+#   smoke                     __graft_entry__.smoke()
+#   bench[:<args>]            python bench.py <args> (commas -> spaces)
+#   prof                      kernel trace + stats of the default bench (no cpu baseline)
+#   pmc                       round PMC passes (tools/gpu_round_pmc.sh), OGS_COMMIT=<sha>
+#   sq:<tag>:<bench args>     one SQ counter pass (wave-cycle split, LDS conflicts) over
+#                             `python3 bench.py <bench args>` (commas -> spaces)
+#   sqlds:<tag>:<bench args>  second SQ pass: LDS instruction / wait counters
+#   stamps:<as-rank>          LDS SPF phase stamps (make stamps; tools/c3_stamps.py --lds)
+#   ab:<as-rank>:<A>:<B>[:..] in-process C3 option A/B (tools/c3_opt_ab.py), variants
+#                             are name=value lists joined by '+'
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+cd /tmp && cd "$GRAFT_REPO_ROOT" || exit 1
+COMMIT=${OGS_COMMIT:-unknown}
+
+step() {  # step <name> <timeout> <cmd...>
+  local name=$1 t=$2; shift 2
+  echo "=== $name: $*"
+  timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc"; grep -v amdgpu.ids "gpurun_out/$name.log" | tail -4 | cut -c1-400
+  [ $rc -eq 0 ] || exit $rc
+}
+
+SQ1="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU"
+SQ2="SQ_WAVE_CYCLES SQ_INSTS_LDS SQ_LDS_ADDR_CONFLICT SQ_LDS_UNALIGNED_STALL SQ_INSTS_SALU SQ_INSTS_VALU SQ_WAVES SQ_BUSY_CYCLES"
+
+n=0
+for recipe in "$@"; do
+  n=$((n + 1))
+  kind=${recipe%%:*}
+  rest=${recipe#*:}
+  [ "$rest" = "$recipe" ] && rest=""
+  case $kind in
+    tests)
+      if [ -n "$rest" ]; then
+        step "pytest_$n" 900 python -u -m pytest tests -m gpu -v -p no:cacheprovider -x --timeout 200 --timeout-method thread -k "$rest"
+      else
+        step pytest_gpu 900 python -u -m pytest tests -m gpu -v -p no:cacheprovider -x --timeout 200 --timeout-method thread
+      fi ;;
+    testfile)
+      step "pytest_$n" 300 python -u -m pytest "$rest" -v -p no:cacheprovider -x --timeout 200 --timeout-method thread ;;
+    smoke)
+      step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench)
+      step "bench_$n" 900 python bench.py ${rest//,/ } ;;
+    prof)
+      step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o bench -- python3 bench.py --no-cpu-baseline --no-extras
+      grep -v "at::native" gpurun_out/prof/bench_kernel_stats.csv | cut -c1-200 | head -20 ;;
+    pmc)
+      OGS_COMMIT=$COMMIT step pmc 900 bash tools/gpu_round_pmc.sh ;;
+    sq|sqlds)
+      tag=${rest%%:*}; args=${rest#*:}
+      C=$SQ1; [ "$kind" = sqlds ] && C=$SQ2
+      # a counter pass that cannot be collected may hang past SIGTERM: KILL
+      echo "=== ${kind}_$tag"
+      timeout -s KILL 150 rocprofv3 --pmc $C --output-format csv -d "gpurun_out/${kind}_$tag" -o sq -- python3 bench.py ${args//,/ } > "gpurun_out/${kind}_$tag.log" 2>&1
+      rc=$?; echo "=== ${kind}_$tag rc=$rc"; tail -3 "gpurun_out/${kind}_$tag.log" | cut -c1-300
+      [ $rc -eq 0 ] || exit $rc ;;
+    stamps)
+      OGS_LIB=openr_amd/lib/libopenr_gpu_stamps.so step "stamps_$n" 300 python -u tools/c3_stamps.py --lds --as-rank "$rest" --opt route_stream=4 ;;
+    ab)
+      IFS=: read -r -a parts <<< "$rest"
+      rank=${parts[0]}; vs=()
+      for v in "${parts[@]:1}"; do vs+=("${v//+/,}"); done
+      step "ab_$n" 600 python -u tools/c3_opt_ab.py --pairs 4 --as-rank "$rank" "${vs[@]}"
+      grep '^{' "gpurun_out/ab_$n.log" | cut -c1-200 ;;
+    *)
+      echo "unknown recipe $recipe"; exit 2 ;;
+  esac
+done
+echo "=== all done"
