@@ -301,14 +301,14 @@ int ogs_host_free(void* hptr);
  *                 default: then the last grid's worth of units in 4) from a
  *                 device-wide counter, SPFs kept one grid ahead; route keys
  *                 packed into 16 bits on topologies of <= 16,384 nodes
- *                 ("lds_key16" 1, default; 0 u32 keys, A/B); units streamed
- *                 in SPF completion order ("lds_ready" 1, default; 0 unit
- *                 order, A/B); unit-weight (BFS) SPFs stop once every node
- *                 is reached ("lds_bfs_exit" 1, default; 0 they run the
- *                 empty last layer, A/B); "lds_tiles" T > 0: each unit's
- *                 rows in T tiles claimed dynamically by the workgroups on
- *                 the unit, idle workgroups joining the unit with the most
- *                 tiles left (0: fixed ranges). Scratch
+ *                 ("lds_key16" 1, default; 0 u32 keys, A/B); on sharded
+ *                 builds (fewer than 4 units per workgroup) the last grid's
+ *                 worth of items in "lds_tail_parts" ranges per unit (0
+ *                 auto: 2 x lds_parts) and "lds_lead" narrow units streamed
+ *                 before the widest group (-1 auto: a grid's worth of
+ *                 items; 0 none); unit-weight (BFS) SPFs stop once every
+ *                 node is reached ("lds_bfs_exit" 1, default; 0 they run
+ *                 the empty last layer, A/B). Scratch
  *                 (prefix keys, dist/next-hop sets when out->dist / out->nh
  *                 are NULL) comes from a grow-only per-device workspace.
  *                 "route_store_nt", bits: 1 the RouteDb stream's 16-B stores

@@ -337,6 +337,33 @@ class LinkState {
   void noteSpf(const std::string& node, bool useLinkMetric = true) const {
     if (spfCounted_.emplace(node, useLinkMetric).second) noteSpfRuns(1);
   }
+  // Device half of the getSpfResult memo (LinkState.cpp:705-715,
+  // LinkState.h:369-372): the SPF rows of (source id, useLinkMetric) kept on
+  // the device while the host memo's key stays valid (cleared on a topology
+  // change) and node ids are stable (no re-flatten). buildRouteDb of any
+  // source routes against them (ogs_routes_from_spf) instead of relaunching
+  // the SPF; every SPF launched into a slot counts decision.gpu.spf_launches.
+  // Rows: dist [N] (db bytes each) | nh [W][N] | reach [ceil(N/32)].
+  struct DeviceSpf {
+    DeviceBuffer rows;
+    uint32_t N{0};
+    int W{0};
+    size_t db{0}, nhOff{0}, reachOff{0};
+    bool exact{false}, valid{false};
+    void* dist() const { return rows.get(); }
+    uint32_t* nh() const { return reinterpret_cast<uint32_t*>(rows.as<char>() + nhOff); }
+    uint32_t* reach() const { return reinterpret_cast<uint32_t*>(rows.as<char>() + reachOff); }
+  };
+  // the rows of source id s, or nullptr (not computed, or of another shape)
+  DeviceSpf* findDeviceSpf(uint32_t s, bool useLinkMetric, uint32_t N, int W, size_t db,
+                           bool exact) const;
+  // an empty slot for s sized for (N, W, db); the caller launches the SPF
+  // into it and then calls commitDeviceSpf
+  DeviceSpf& newDeviceSpf(uint32_t s, bool useLinkMetric, uint32_t N, int W, size_t db,
+                          bool exact) const;
+  void commitDeviceSpf(DeviceSpf& slot, const std::string& node, bool useLinkMetric) const;
+  uint64_t deviceSpfLaunches() const { return deviceSpfLaunches_; }
+  size_t deviceSpfSlots() const { return deviceSpf_.size(); }
   // attribute-only updates patch the CSR in place (default) or, off,
   // re-flatten + re-upload it (A/B measurements)
   void setIncrementalFlatten(bool on) { incrementalFlatten_ = on; }
@@ -367,6 +394,10 @@ class LinkState {
   std::unordered_map<std::string, uint64_t> metricInc_;
   mutable std::map<std::pair<std::string, bool>, SpfResult> spfMemo_;
   mutable std::set<std::pair<std::string, bool>> spfCounted_;  // noteSpf
+  mutable std::unordered_map<uint64_t, DeviceSpf> deviceSpf_;  // key s << 1 | useLinkMetric
+  mutable size_t deviceSpfBytes_{0};
+  mutable uint64_t deviceSpfLaunches_{0};
+  void clearSpfMemos() const;
   mutable std::map<std::tuple<std::string, std::string, size_t>,
                    std::vector<Path>>
       kthMemo_;

@@ -75,14 +75,70 @@ LinkPtr LinkState::makeLink(const std::string& node, const Adjacency& adj) const
   return nullptr;
 }
 
+void LinkState::clearSpfMemos() const {  // LinkState.cpp:635-638
+  spfMemo_.clear();
+  spfCounted_.clear();
+  kthMemo_.clear();
+  deviceSpf_.clear();
+  deviceSpfBytes_ = 0;
+}
+
 void LinkState::invalidate(bool topologyChanged) {
   ++mutation_;
   flatStale_ = true;
-  if (topologyChanged) {  // LinkState.cpp:635-638
-    spfMemo_.clear();
-    spfCounted_.clear();
-    kthMemo_.clear();
+  if (topologyChanged) clearSpfMemos();
+}
+
+// device SPF rows memo ------------------------------------------------------
+namespace {
+// bytes of device SPF rows kept per LinkState before the memo starts over
+// (C3: 2,080 sources x 2,080 nodes x (4 + 4 x 3) B = 69 MB)
+size_t g_deviceSpfBudget = size_t(1) << 30;
+size_t al256(size_t x) { return (x + 255) & ~size_t(255); }
+}  // namespace
+
+LinkState::DeviceSpf* LinkState::findDeviceSpf(uint32_t s, bool useLinkMetric, uint32_t N,
+                                               int W, size_t db, bool exact) const {
+  auto it = deviceSpf_.find(uint64_t(s) << 1 | (useLinkMetric ? 1u : 0u));
+  if (it == deviceSpf_.end()) return nullptr;
+  DeviceSpf& d = it->second;
+  if (!d.valid || d.N != N || d.W != W || d.db != db || d.exact != exact) return nullptr;
+  return &d;
+}
+
+LinkState::DeviceSpf& LinkState::newDeviceSpf(uint32_t s, bool useLinkMetric, uint32_t N, int W,
+                                              size_t db, bool exact) const {
+  const uint64_t key = uint64_t(s) << 1 | (useLinkMetric ? 1u : 0u);
+  const size_t nhOff = al256(size_t(N) * db);
+  const size_t reachOff = nhOff + al256(size_t(N) * W * 4);
+  const size_t bytes = reachOff + al256((size_t(N) + 31) / 32 * 4 + 4);
+  if (auto it = deviceSpf_.find(key); it != deviceSpf_.end()) {
+    deviceSpfBytes_ -= it->second.rows.capacity();
+    deviceSpf_.erase(it);
   }
+  if (deviceSpfBytes_ + bytes > g_deviceSpfBudget) {  // over budget: start over
+    deviceSpf_.clear();
+    deviceSpfBytes_ = 0;
+  }
+  DeviceSpf& d = deviceSpf_[key];
+  d.rows.resize(bytes);
+  deviceSpfBytes_ += d.rows.capacity();
+  d.N = N;
+  d.W = W;
+  d.db = db;
+  d.nhOff = nhOff;
+  d.reachOff = reachOff;
+  d.exact = exact;
+  d.valid = false;
+  return d;
+}
+
+void LinkState::commitDeviceSpf(DeviceSpf& slot, const std::string& node,
+                                bool useLinkMetric) const {
+  slot.valid = true;
+  ++deviceSpfLaunches_;
+  addStatValue("decision.gpu.spf_launches", 1, StatType::COUNT);
+  noteSpf(node, useLinkMetric);
 }
 
 LinkState::LinkStateChange LinkState::updateAdjacencyDatabase(
@@ -190,11 +246,7 @@ LinkState::LinkStateChange LinkState::updateAdjacencyDatabase(
   }
   if (!structural && incrementalFlatten_ && flat_ && !flatStale_) {
     patchFlat(name, touched, nodeFlagsChanged);
-    if (ch.topologyChanged) {  // LinkState.cpp:635-638
-      spfMemo_.clear();
-      spfCounted_.clear();
-      kthMemo_.clear();
-    }
+    if (ch.topologyChanged) clearSpfMemos();  // LinkState.cpp:635-638
   } else {
     invalidate(ch.topologyChanged);
   }
@@ -329,6 +381,10 @@ bool LinkState::pathAInPathB(const Path& a, const Path& b) {
 // ------------------------------------------------------------ flattening --
 const FlatTopology& LinkState::flat() const {
   if (flat_ && !flatStale_) return *flat_;
+  // node ids are ranks of the current names: rows of the device SPF memo
+  // are indexed by the old ones
+  deviceSpf_.clear();
+  deviceSpfBytes_ = 0;
   auto f = std::make_unique<FlatTopology>();
   f->version = nextVersionStamp();
   f->names.reserve(adjDbs_.size());
@@ -504,7 +560,7 @@ void LinkState::uploadSlotImages(FlatTopology& m) const {
 namespace {
 // Shared scratch for single-source launches made through the API surface.
 struct SpfScratch {
-  DeviceBuffer unit, dist, nh, reach;
+  DeviceBuffer unit;
 };
 SpfScratch& scratch() {
   static SpfScratch s;
@@ -544,52 +600,60 @@ const LinkState::SpfResult& LinkState::getSpfResult(const std::string& node,
   const bool wide = exact || needsWide(f, useLinkMetric);
   const size_t db = wide ? 8 : 4;
 
-  auto& sc = scratch();
-  const ogs_unit u{0, s};
-  sc.unit.upload(&u, 1);
-  sc.dist.resize(N * db);
-  sc.nh.resize(size_t(N) * W * 4);
-  sc.reach.resize(((size_t(N) + 31) / 32) * 4 + 4);
-
-  ogs_graph g{};
-  g.num_topos = 1;
-  g.max_nodes = int32_t(N);
-  g.max_edges = int32_t(f.edges.size());
-  g.max_degree = f.maxDegree;
-  g.node_base = f.dNodeBase.as<uint32_t>();
-  g.row_ptr = f.dRow.as<uint32_t>();
-  g.edges = f.dEdges.as<uint64_t>();
-  g.node_flags = f.dFlags.as<uint8_t>();
-  g.slot_node = f.slotStride ? f.dSlot.as<uint16_t>() : nullptr;
-  g.slot_stride = f.slotStride;
-  g.slot_edges = f.slotDegree ? f.dSlotEdges.as<uint32_t>() : nullptr;
-  g.slot_degree = f.slotDegree;
-  g.edge_src = f.dEdgeSrc.as<uint32_t>();
-  ogs_spf_out out{};
-  out.dist = sc.dist.get();
-  out.nh = sc.nh.as<uint32_t>();
-  out.reached = exact ? sc.reach.as<uint32_t>() : nullptr;
-  uint32_t flags = (useLinkMetric ? 0u : OGS_F_HOP_METRIC) |
-      (wide ? OGS_F_WIDE_METRIC : 0u) | (exact ? OGS_F_EXACT_ORDER : 0u);
-  ogsCheck(ogs_spf_routes(&g, nullptr, sc.unit.as<ogs_unit>(), 1, flags, W,
-                          &out, nullptr),
-           "ogs_spf_routes");
+  // the device rows memo (shared with buildRouteDb): D2H of rows already on
+  // the device, else ONE SPF launch into a new slot
+  DeviceSpf* memo = findDeviceSpf(s, useLinkMetric, N, W, db, exact);
+  if (!memo) {
+    auto& sc = scratch();
+    const ogs_unit u{0, s};
+    sc.unit.upload(&u, 1);
+    DeviceSpf& slot = newDeviceSpf(s, useLinkMetric, N, W, db, exact);
+    ogs_graph g{};
+    g.num_topos = 1;
+    g.max_nodes = int32_t(N);
+    g.max_edges = int32_t(f.edges.size());
+    g.max_degree = f.maxDegree;
+    g.node_base = f.dNodeBase.as<uint32_t>();
+    g.row_ptr = f.dRow.as<uint32_t>();
+    g.edges = f.dEdges.as<uint64_t>();
+    g.node_flags = f.dFlags.as<uint8_t>();
+    g.slot_node = f.slotStride ? f.dSlot.as<uint16_t>() : nullptr;
+    g.slot_stride = f.slotStride;
+    g.slot_edges = f.slotDegree ? f.dSlotEdges.as<uint32_t>() : nullptr;
+    g.slot_degree = f.slotDegree;
+    g.edge_src = f.dEdgeSrc.as<uint32_t>();
+    ogs_spf_out out{};
+    out.dist = slot.dist();
+    out.nh = slot.nh();
+    out.reached = exact ? slot.reach() : nullptr;
+    uint32_t flags = (useLinkMetric ? 0u : OGS_F_HOP_METRIC) |
+        (wide ? OGS_F_WIDE_METRIC : 0u) | (exact ? OGS_F_EXACT_ORDER : 0u);
+    ogsCheck(ogs_spf_routes(&g, nullptr, sc.unit.as<ogs_unit>(), 1, flags, W,
+                            &out, nullptr),
+             "ogs_spf_routes");
+    commitDeviceSpf(slot, node, useLinkMetric);
+    memo = &slot;
+  }
   std::vector<uint64_t> dist(N);
   std::vector<uint32_t> nh(size_t(N) * W);
   if (wide) {
-    sc.dist.download(dist.data(), N);
+    ogsCheck(ogs_memcpy_d2h(dist.data(), memo->dist(), size_t(N) * 8, nullptr), "ogs_memcpy_d2h");
   } else {
     std::vector<uint32_t> d32(N);
-    sc.dist.download(d32.data(), N);
+    ogsCheck(ogs_memcpy_d2h(d32.data(), memo->dist(), size_t(N) * 4, nullptr), "ogs_memcpy_d2h");
+    ogsCheck(ogs_stream_sync(nullptr), "ogs_stream_sync");
     for (uint32_t v = 0; v < N; ++v) {
       dist[v] = d32[v] == 0xFFFFFFFFu ? ~0ull : d32[v];
     }
   }
-  sc.nh.download(nh.data(), nh.size());
+  ogsCheck(ogs_memcpy_d2h(nh.data(), memo->nh(), nh.size() * 4, nullptr), "ogs_memcpy_d2h");
   // exact order: the settled bitset decides reachability (a wrapped u64
   // distance of a settled node may be all ones, kept by the reference)
   std::vector<uint32_t> reach(exact ? (size_t(N) + 31) / 32 : 0);
-  if (exact) sc.reach.download(reach.data(), reach.size());
+  if (exact) {
+    ogsCheck(ogs_memcpy_d2h(reach.data(), memo->reach(), reach.size() * 4, nullptr),
+             "ogs_memcpy_d2h");
+  }
   ogsCheck(ogs_stream_sync(nullptr), "ogs_stream_sync");
 
   const uint32_t rb = f.rowPtr[s];

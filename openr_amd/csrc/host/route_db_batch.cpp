@@ -164,6 +164,7 @@ void RouteDbBatch::launch(void* stream) {
            "ogs_spf_routes_groups(batch)");
   for (Group& G : groups_) {
     for (uint32_t m : G.members) ls_->noteSpf(sources_[m]);
+    addStatValue("decision.gpu.spf_launches", double(G.members.size()), StatType::COUNT);
   }
   launched_ = true;
 }

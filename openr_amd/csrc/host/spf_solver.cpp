@@ -335,14 +335,6 @@ struct SpfSolver::Impl {
   DeviceBuffer unit, res;
   PinnedBuffer hRes;
   uint32_t unitSrc{~0u};
-  // SPF memo: res's dist / nh spans hold the SPF of spfSrc in spfTopo at
-  // spfVersion (ResultImage of spfN / spfW / spfDb) -- what
-  // createRoutesForPrefixes routes a changed prefix set against
-  const FlatTopology* spfTopo{nullptr};
-  uint64_t spfVersion{~0ull};
-  uint32_t spfSrc{~0u}, spfN{0};
-  int spfW{0};
-  size_t spfDb{0};
   // createRoutesForPrefixes: the changed prefixes' sub-table and records
   DeviceBuffer subTab, subRes, spfDesc;
   PinnedBuffer hSubTab, hSubRes;
@@ -897,52 +889,43 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDbSingleArea(
     I.unitSrc = s;
   }
   const ResultImage L(N, P, W, db);
-  // SPF memo (LinkState::getSpfResult, LinkState.cpp:705-715): res still
-  // holds this source's SPF of this topology version (dist / nh / reach
-  // spans depend on N, W and the distance width only) -> the route pass
-  // alone, no SPF relaunch (ogs_routes_from_spf)
-  const bool memoHit = I.spfTopo == &f && I.spfVersion == f.version && I.spfSrc == s &&
-      I.spfN == N && I.spfW == W && I.spfDb == db && I.res.capacity() >= L.end;
-  if (!memoHit) I.spfTopo = nullptr;  // res is overwritten below
   I.res.resize(L.end);
   I.hRes.resize(L.end);
 
   const ogs_graph g = singleGraph(f, devAt<uint32_t>(I.tab, I.tabImg.desc));
   const ogs_prefix_table pt = I.tabImg.view(I.tab);
   ogs_spf_out out{};
-  out.dist = devAt<void>(I.res, L.dist);
-  out.nh = devAt<uint32_t>(I.res, L.nh);
   out.meta = devAt<uint32_t>(I.res, L.meta);
   out.metric = devAt<void>(I.res, L.metric);
   out.mask = devAt<uint32_t>(I.res, L.mask);
   out.sel = devAt<uint32_t>(I.res, L.sel);
-  out.reached = exact ? devAt<uint32_t>(I.res, L.reach) : nullptr;
   const uint32_t flags = (enableV4_ ? OGS_F_ENABLE_V4 : 0u) |
       (v4OverV6Nexthop_ ? OGS_F_V4_OVER_V6 : 0u) |
       (enableBestRouteSelection_ ? OGS_F_BEST_ROUTE_SELECTION : 0u) |
       (wide ? OGS_F_WIDE_METRIC : 0u) | (exact ? OGS_F_EXACT_ORDER : 0u);
-  if (memoHit) {
+  // SPF memo (LinkState::getSpfResult, LinkState.cpp:705-715): the
+  // LinkState's device rows of this source -> the route pass alone, no SPF
+  // relaunch (ogs_routes_from_spf); else ONE fused launch writes the SPF
+  // into a new memo slot and the records into res
+  LinkState::DeviceSpf* memo = ls.findDeviceSpf(s, true, N, W, db, exact);
+  if (memo) {
     if (P) {
-      ogs_spf_out ro = out;
-      ro.dist = nullptr;
-      ro.nh = nullptr;
-      ro.reached = nullptr;
-      ogsCheck(ogs_routes_from_spf(&g, &pt, I.unit.as<ogs_unit>(), 1, out.dist, out.nh,
-                                   exact ? out.reached : nullptr, flags, W, &ro, nullptr),
+      ogsCheck(ogs_routes_from_spf(&g, &pt, I.unit.as<ogs_unit>(), 1, memo->dist(),
+                                   memo->nh(), exact ? memo->reach() : nullptr, flags, W, &out,
+                                   nullptr),
                "ogs_routes_from_spf");
     }
   } else {
+    LinkState::DeviceSpf& slot = ls.newDeviceSpf(s, true, N, W, db, exact);
+    out.dist = slot.dist();
+    out.nh = slot.nh();
+    out.reached = exact ? slot.reach() : nullptr;
     ogsCheck(ogs_spf_routes(&g, P ? &pt : nullptr, I.unit.as<ogs_unit>(), 1,
                             flags, W, &out, nullptr),
              "ogs_spf_routes");
+    ls.commitDeviceSpf(slot, me, true);
+    memo = &slot;
   }
-  ls.noteSpf(me);
-  I.spfTopo = &f;
-  I.spfVersion = f.version;
-  I.spfSrc = s;
-  I.spfN = N;
-  I.spfW = W;
-  I.spfDb = db;
   const RibPolicy* policy = (ribPolicy_ && ribPolicy_->isActive()) ? ribPolicy_ : nullptr;
   std::vector<uint16_t> applied, counter;
   if (policy && P) {
@@ -950,11 +933,21 @@ std::optional<DecisionRouteDb> SpfSolver::buildRouteDbSingleArea(
                       I.policy, nullptr);
     downloadPolicy(I.policy, P, applied, counter);
   }
-  // ONE D2H of the records (+ the SPF when node-label routes read it)
-  const size_t from = enableNodeSegmentLabel_ ? 0 : L.meta;
-  ogsCheck(ogs_memcpy_d2h(I.hRes.at<char>(from), devAt<char>(I.res, from), L.end - from,
-                          nullptr),
+  // ONE D2H of the records (+ the SPF rows when node-label routes read them)
+  ogsCheck(ogs_memcpy_d2h(I.hRes.at<char>(L.meta), devAt<char>(I.res, L.meta),
+                          L.end - L.meta, nullptr),
            "ogs_memcpy_d2h");
+  if (enableNodeSegmentLabel_) {
+    ogsCheck(ogs_memcpy_d2h(I.hRes.at<char>(L.dist), memo->dist(), L.nh - L.dist, nullptr),
+             "ogs_memcpy_d2h");
+    ogsCheck(ogs_memcpy_d2h(I.hRes.at<char>(L.nh), memo->nh(), L.reach - L.nh, nullptr),
+             "ogs_memcpy_d2h");
+    if (exact) {
+      ogsCheck(ogs_memcpy_d2h(I.hRes.at<char>(L.reach), memo->reach(), L.meta - L.reach,
+                              nullptr),
+               "ogs_memcpy_d2h");
+    }
+  }
   ogsCheck(ogs_stream_sync(nullptr), "ogs_stream_sync");
   addStatValue("decision.gpu.launch_ms", msSince(tLaunch), StatType::AVG);
   const auto tMat = std::chrono::steady_clock::now();
@@ -1013,30 +1006,23 @@ void SpfSolver::routesFromSpfMemo(const std::string& me, const LinkState& ls,
     I.unit.upload(&u, 1);
     I.unitSrc = s;
   }
-  if (!(I.spfTopo == &f && I.spfVersion == f.version && I.spfSrc == s)) {
-    // SPF only: the topology's descriptor without a prefix table (the full
-    // table is not needed to answer a few prefixes)
+  LinkState::DeviceSpf* memo = ls.findDeviceSpf(s, true, N, W, db, exact);
+  if (!memo) {
+    // SPF only into a memo slot: the topology's descriptor without a prefix
+    // table (the full table is not needed to answer a few prefixes)
     const uint32_t desc[8] = {0, N, 0, uint32_t(f.edges.size()), 0, 0, 0, 0};
     I.spfDesc.upload(desc, 8);
-    const ResultImage L(N, 0, W, db);
-    I.spfTopo = nullptr;
-    I.res.resize(L.end);
+    LinkState::DeviceSpf& slot = ls.newDeviceSpf(s, true, N, W, db, exact);
     const ogs_graph g = singleGraph(f, I.spfDesc.as<uint32_t>());
     ogs_spf_out so{};
-    so.dist = devAt<void>(I.res, L.dist);
-    so.nh = devAt<uint32_t>(I.res, L.nh);
-    so.reached = exact ? devAt<uint32_t>(I.res, L.reach) : nullptr;
+    so.dist = slot.dist();
+    so.nh = slot.nh();
+    so.reached = exact ? slot.reach() : nullptr;
     ogsCheck(ogs_spf_routes(&g, nullptr, I.unit.as<ogs_unit>(), 1, flags, W, &so, nullptr),
              "ogs_spf_routes");
-    ls.noteSpf(me);
-    I.spfTopo = &f;
-    I.spfVersion = f.version;
-    I.spfSrc = s;
-    I.spfN = N;
-    I.spfW = W;
-    I.spfDb = db;
+    ls.commitDeviceSpf(slot, me, true);
+    memo = &slot;
   }
-  const ResultImage S(I.spfN, 0, I.spfW, I.spfDb);
   const auto tSpf = std::chrono::steady_clock::now();
 
   // the changed prefixes' table: one packed H2D
@@ -1060,10 +1046,8 @@ void SpfSolver::routesFromSpfMemo(const std::string& me, const LinkState& ls,
   ro.metric = devAt<void>(I.subRes, R.metric);
   ro.mask = devAt<uint32_t>(I.subRes, R.mask);
   ro.sel = devAt<uint32_t>(I.subRes, R.sel);
-  ogsCheck(ogs_routes_from_spf(&g, &pt, I.unit.as<ogs_unit>(), 1, devAt<void>(I.res, S.dist),
-                               devAt<uint32_t>(I.res, S.nh),
-                               exact ? devAt<uint32_t>(I.res, S.reach) : nullptr, flags, W,
-                               &ro, nullptr),
+  ogsCheck(ogs_routes_from_spf(&g, &pt, I.unit.as<ogs_unit>(), 1, memo->dist(), memo->nh(),
+                               exact ? memo->reach() : nullptr, flags, W, &ro, nullptr),
            "ogs_routes_from_spf");
   ogsCheck(ogs_memcpy_d2h(I.hSubRes.at<char>(R.meta), devAt<char>(I.subRes, R.meta),
                           R.end - R.meta, nullptr),
@@ -1359,6 +1343,9 @@ void SpfSolver::enqueueMultiArea(const std::string& me, const AreaLinkStates& al
   ogsCheck(ogs_spf_routes(&g, nullptr, M.units.as<ogs_unit>(), int32_t(su.size()),
                           flags, W, &spf, stream),
            "ogs_spf_routes");
+  // one SPF per area holding `me` (SpfSolver.cpp:595-639 calls getSpfResult
+  // per area); the multi-area batch does not use the per-area row memos
+  addStatValue("decision.gpu.spf_launches", double(su.size()), StatType::COUNT);
   for (const auto& [area, ls] : als) {
     if (ls.flat().id.count(me)) ls.noteSpf(me);
   }

@@ -19,9 +19,9 @@ extern int g_ldsParts;
 extern int g_ldsGrid;
 extern int g_ldsKey16;
 extern int g_ldsTail;
-extern int g_ldsReady;
+extern int g_ldsLead;
 extern int g_ldsBfsExit;
-extern int g_ldsTiles;
+extern int g_ldsTailParts;
 extern int g_routeStoreNt;
 extern int g_spfSeedRow;
 extern int g_frontierBlock;
@@ -211,14 +211,14 @@ int ogs_set_option(const char* name, int64_t value) {
     ogs::g_ldsTail = int(value);
     return OGS_OK;
   }
-  if (std::strcmp(name, "lds_ready") == 0) {
-    if (value != 0 && value != 1) return fail(OGS_E_INVALID, "lds_ready must be 0 or 1");
-    ogs::g_ldsReady = int(value);
+  if (std::strcmp(name, "lds_lead") == 0) {
+    if (value < -1 || value > 65536) return fail(OGS_E_INVALID, "lds_lead must be in [-1, 65536]");
+    ogs::g_ldsLead = int(value);
     return OGS_OK;
   }
-  if (std::strcmp(name, "lds_tiles") == 0) {
-    if (value < 0 || value > 256) return fail(OGS_E_INVALID, "lds_tiles must be in [0, 256]");
-    ogs::g_ldsTiles = int(value);
+  if (std::strcmp(name, "lds_tail_parts") == 0) {
+    if (value < 0 || value > 64) return fail(OGS_E_INVALID, "lds_tail_parts must be in [0, 64]");
+    ogs::g_ldsTailParts = int(value);
     return OGS_OK;
   }
   if (std::strcmp(name, "lds_bfs_exit") == 0) {

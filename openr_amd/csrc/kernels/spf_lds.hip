@@ -45,11 +45,10 @@ constexpr uint32_t kNodeMax = 0x7FFFu;    // 15-bit neighbour ids
 constexpr uint32_t kDrained16 = 0x8000u;  // cnode: the chunk's node is hard-drained
 constexpr uint32_t kLdsChunk = 8;         // edges per chunk (one lane's push)
 constexpr int kLdsBlock = 1024;
-// launch flags of the LDS forms (above the OGS_F_* bits): the BFS rounds'
-// all-reached exit off ("lds_bfs_exit" 0, A/B), and the one-launch form's
-// streams in unit order instead of SPF completion order ("lds_ready" 0)
+constexpr uint32_t kLdsDiagWgsItems = 1024;  // workgroups with item stamps (OGS_STAMPS)
+// launch flag of the LDS forms (above the OGS_F_* bits): the BFS rounds'
+// all-reached exit off ("lds_bfs_exit" 0, A/B)
 constexpr uint32_t kFlagLdsNoBfsExit = 1u << 25;
-constexpr uint32_t kFlagLdsUnitOrder = 1u << 24;
 
 __host__ __device__ inline uint32_t al16(uint32_t x) { return (x + 15u) & ~15u; }
 
@@ -106,8 +105,7 @@ __host__ LdsScratch lds_scratch(const ogs_graph& g, const LdsImage& L, int nUnit
   S.mm = r256(size_t(g.num_topos) * L.stride);
   S.ctr = S.mm + r256(size_t(g.num_topos) * S.nEB * 8u);
   S.ready = S.ctr + 256u;
-  // ready words + the tile counters of the one-launch form, one each per unit
-  S.bytes = S.ready + r256(size_t(std::max(nUnits, 1)) * 8u);
+  S.bytes = S.ready + r256(size_t(std::max(nUnits, 1)) * 4u);
   return S;
 }
 
@@ -134,10 +132,7 @@ __global__ __launch_bounds__(kLdsBlock) void lds_prep_kernel(
   if (blk < T) {
     const uint32_t t = blk;
     if (t == 0u) {
-      if (tid == 0u) {
-        ctr[0] = 0u;   // work items
-        ctr[32] = 0u;  // ready-list slots (spf_lds_route_kernel)
-      }
+      if (tid == 0u) *ctr = 0u;
       for (uint32_t i = tid; i < nReady; i += B) ready[i] = 0u;
     }
     const uint32_t nb = g.node_base[t];
@@ -246,6 +241,14 @@ __global__ __launch_bounds__(kLdsBlock) void lds_prep_kernel(
   }
 }
 
+#ifdef OGS_STAMPS
+// diagnostic build: item timeline of spf_lds_route_kernel, per workgroup up
+// to kItemStamps items x 4 words {kind << 28 | unit, start, ready, end} on
+// the 100 MHz realtime clock (kind 1 SPF, 2 stream item, 3 join); read with
+// ogs_diag_item_stamps (tools/c3_timeline.py)
+constexpr uint32_t kItemStamps = 64;
+__device__ uint32_t g_itemStamps[kLdsDiagWgsItems * kItemStamps * 4];
+#endif
 #ifdef OGS_STAMPS
 // diagnostic build: per workgroup 32 words {staging, first unit's SPF
 // (incl. staging), rounds, units, kernel cycles, first unit's queue total,
@@ -705,19 +708,13 @@ struct LdsGroups {
   uint32_t n;
 };
 
-// One stream item of local unit u of group grp, from the published SPF rows:
-// per-node records into LDS, then the unit's prefix rows -- either range
-// `part` of P (fixed ranges), or, with tiles (tctr != nullptr), T tiles of
-// the unit taken one by one from its tile counter, so the workgroups on one
-// unit share its rows dynamically and any workgroup can join a unit late
-// (the launch's tail). sTile: two shared words (the next tile, double
-// buffered so one barrier per tile suffices).
+// One stream item: prefix range `part` (of P) of local unit u of group grp,
+// from the published SPF rows: per-node records into LDS, then the rows.
 template <int W, typename KeyT>
 __device__ __forceinline__ void lds_stream_item(const ogs_graph& g, const ogs_prefix_table& pt,
                                                 const KeyT* __restrict__ key,
                                                 const LdsGroup& grp, uint32_t u, uint32_t part,
-                                                uint32_t P, uint32_t flags, uint32_t* rec0,
-                                                uint32_t* tctr, uint32_t T, uint32_t* sTile) {
+                                                uint32_t P, uint32_t flags, uint32_t* rec0) {
   constexpr uint32_t kInf = 0xFFFFFFFFu;
   const uint32_t tid = threadIdx.x;
   const uint32_t Sn = uint32_t(g.max_nodes), Sp = uint32_t(pt.max_prefixes);
@@ -732,8 +729,6 @@ __device__ __forceinline__ void lds_stream_item(const ogs_graph& g, const ogs_pr
   uint32_t* rMeta = rec0;
   uint32_t* rMetric = rMeta + Sn;
   uint32_t* rMask = rMetric + Sn;  // [W][Sn]
-  // the first tile is claimed while the records are built
-  if (tctr && tid == 0u) sTile[0] = atomicAdd(tctr, 1u);
   for (uint32_t v = tid; v < N; v += kLdsBlock) {
     const uint32_t d = sv.dist(v);
     uint32_t m[W], cnt = 0;
@@ -750,6 +745,8 @@ __device__ __forceinline__ void lds_stream_item(const ogs_graph& g, const ogs_pr
   __syncthreads();
   const uint32_t p0 = pt.pfx_base[t];
   const uint32_t Pn = pt.pfx_base[t + 1] - p0;
+  const uint32_t span = ((Pn + P - 1u) / P + 3u) & ~3u;
+  const uint32_t lo = min(Pn, part * span), hi = min(Pn, lo + span);
   auto rec = [&](uint32_t v, Rec<W>& r) {
     r.meta = rMeta[v];
     r.metric = rMetric[v];
@@ -757,33 +754,13 @@ __device__ __forceinline__ void lds_stream_item(const ogs_graph& g, const ogs_pr
     for (int w = 0; w < W; ++w) r.mask[w] = rMask[w * Sn + v];
   };
   const bool nt = (flags & kFlagNtStores) != 0;
-  auto stream = [&](uint32_t lo, uint32_t hi) {
-    if (grp.outs3) {
-      stream_routes<W, false, true, kLdsBlock>(pt, key + size_t(t) * Sp, p0, Pn, Sp, u, s,
-                                               nflags, sv, cfg, grp.out, rec, nullptr, nt, lo,
-                                               hi);
-    } else {
-      stream_routes<W, false, false, kLdsBlock>(pt, key + size_t(t) * Sp, p0, Pn, Sp, u, s,
-                                                nflags, sv, cfg, grp.out, rec, nullptr, nt, lo,
-                                                hi);
-    }
-  };
-  if (!tctr) {
-    const uint32_t span = ((Pn + P - 1u) / P + 3u) & ~3u;
-    const uint32_t lo = min(Pn, part * span);
-    stream(lo, min(Pn, lo + span));
+  if (grp.outs3) {
+    stream_routes<W, false, true, kLdsBlock>(pt, key + size_t(t) * Sp, p0, Pn, Sp, u, s, nflags,
+                                             sv, cfg, grp.out, rec, nullptr, nt, lo, hi);
   } else {
-    const uint32_t span = ((Pn + T - 1u) / T + 3u) & ~3u;
-    uint32_t cur = sTile[0];
-    for (uint32_t k = 1; cur < T; k ^= 1u) {
-      uint32_t nxt = 0;
-      if (tid == 0u) nxt = atomicAdd(tctr, 1u);  // the next tile, while this one streams
-      const uint32_t lo = min(Pn, cur * span);
-      stream(lo, min(Pn, lo + span));
-      if (tid == 0u) sTile[k] = nxt;
-      __syncthreads();
-      cur = sTile[k];
-    }
+    stream_routes<W, false, false, kLdsBlock>(pt, key + size_t(t) * Sp, p0, Pn, Sp, u, s,
+                                              nflags, sv, cfg, grp.out, rec, nullptr, nt, lo,
+                                              hi);
   }
   __syncthreads();  // the records are read before the next item reuses LDS
 }
@@ -792,113 +769,106 @@ __device__ __forceinline__ void lds_stream_item(const ogs_graph& g, const ogs_pr
 // workgroup takes items from a device-wide counter --
 //   items [0, G): the SPF of unit i (G = min(units, grid): every workgroup
 //     starts with one);
-//   then per unit b, P + 1 items: the SPF of unit G + b (when there is
-//     one), then the P prefix ranges of unit b's route stream
-// (unit = global index over the groups). So SPFs stay G units ahead of the
-// streams, a stream item never waits for an SPF that is not already taken
-// by a running workgroup (it was handed out earlier), and a shard with a
-// few more units than CUs streams the other units' rows while its last
-// SPFs run instead of a whole SPF launch waiting on them. Hand-off
-// (MI355X_MICROARCH.md, inter-workgroup visibility): the SPF's dist / nh
-// rows are plain stores, drained by every wave, then a barrier, lane 0's
-// agent release and a relaxed agent flag store; a stream item's lane 0
-// polls the flag (relaxed agent loads), takes an agent acquire, and the
-// workgroup reads the rows after a barrier.
+//   then per stream slot b, P + 1 items: the SPF of unit G + b (when there
+//     is one), then the P prefix ranges of slot b's unit
+// (unit = global index over the groups, widest group first). Stream slot b
+// is unit b, except that with a lead (sharded builds: every workgroup's
+// first SPF is its only one) the first `lead` slots are narrow units, whose
+// SPFs finish first, then the Uw wide ones, then the rest: the first
+// stream items do not wait on the slow wide SPFs, and the wide units' large
+// items still come early instead of at the launch's tail. The slots' units
+// are a bijection whose SPF is always handed out earlier (Uw <= G), so a
+// stream item only ever waits for an SPF that a running workgroup holds and
+// the spin always ends; a shard with a few more units than CUs streams
+// other units' rows while its last SPFs run. The last U - U1 slots stream in
+// P2 > P ranges: small items at the end of the queue shorten the launch's
+// tail (profiles/r05_c3_timeline_*.log: a workgroup's idle tail is about
+// half an item). Hand-off (MI355X_MICROARCH.md, inter-workgroup
+// visibility): the SPF's dist / nh rows are plain stores, drained by every
+// wave, then a barrier, lane 0's agent release and a relaxed agent flag
+// store; a stream item's lane 0 polls the flag (relaxed agent loads), takes
+// an agent acquire, and the workgroup reads the rows after a barrier.
+struct LdsSchedule {
+  uint32_t P, P2, U1;  // ranges per slot: P for slots [0, U1), P2 after
+  uint32_t lead, Uw;   // slot -> unit: lead narrow units before the Uw wide
+};
+
 template <typename KeyT>
 __global__ __launch_bounds__(kLdsBlock) void spf_lds_route_kernel(
     ogs_graph g, ogs_prefix_table pt, const KeyT* __restrict__ key, LdsImage L,
     const uint8_t* __restrict__ img, const uint2* __restrict__ mm, uint32_t nEB,
     LdsGroups grps, uint32_t flags, uint32_t* __restrict__ ctr, uint32_t* __restrict__ ready,
-    uint32_t P, uint32_t P2, uint32_t U1, uint32_t T) {
+    LdsSchedule sch) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ uint32_t qCount[2];
-  __shared__ uint32_t item, slotUnit, sTile[2];
+  __shared__ uint32_t item;
   const uint32_t tid = threadIdx.x;
   const LdsGroup& last = grps.g[grps.n - 1u];
   const uint32_t U = last.base + last.n;
   const uint32_t G = min(U, gridDim.x);
-  // stream slots [0, U1) in P prefix ranges, the last U - U1 in P2 (smaller
-  // items at the end of the queue shorten the launch's tail)
+  const uint32_t P = sch.P, P2 = sch.P2, U1 = sch.U1;
   const uint32_t headItems = U1 * (P + 1u);
   const uint32_t total = G + headItems + (U - U1) * (P2 + 1u);
-  // completion order (default): stream slot b is the b-th SPF to finish --
-  // ready[b] = its global unit + 1, appended through the counter ctr[32] --
-  // so no workgroup waits on a slow (wide) SPF while finished units still
-  // have rows to write. Unit order (kFlagLdsUnitOrder): slot b = unit b,
-  // ready[b] a flag.
-  const bool unitOrder = (flags & kFlagLdsUnitOrder) != 0u;
-  uint32_t* rctr = ctr + 32;  // its own 128-B half of the counters' line
-  // tiles (T > 0): per stream slot a tile counter after the ready words
-  uint32_t* tiles = T ? ready + U : nullptr;
+  auto slotUnit = [&](uint32_t b) -> uint32_t {
+    if (b < sch.lead) return sch.Uw + b;
+    if (b < sch.lead + sch.Uw) return b - sch.lead;
+    return b;
+  };
   LdsWg wg;
   NoDiag dg;
+#ifdef OGS_STAMPS
+  uint32_t nStamp = 0;
+  uint32_t* st = g_itemStamps + size_t(blockIdx.x) * kItemStamps * 4u;
+  const bool stOn = tid == 0u && blockIdx.x < kLdsDiagWgsItems;
+  auto rt = [] { return uint32_t(__builtin_amdgcn_s_memrealtime()); };
+#define OGS_ITEM_STAMP(kind, unit, t0, t1)                                       \
+  if (stOn && nStamp < kItemStamps) {                                            \
+    st[4 * nStamp + 0] = (uint32_t(kind) << 28) | (unit);                        \
+    st[4 * nStamp + 1] = (t0);                                                   \
+    st[4 * nStamp + 2] = (t1);                                                   \
+    st[4 * nStamp + 3] = rt();                                                   \
+    ++nStamp;                                                                    \
+  }
+#else
+#define OGS_ITEM_STAMP(kind, unit, t0, t1)
+#endif
   for (;;) {
+#ifdef OGS_STAMPS
+    const uint32_t tItem = rt();
+#endif
     if (tid == 0u) item = atomicAdd(ctr, 1u);
     __syncthreads();
-    uint32_t i = item;
+    const uint32_t i = item;
     __syncthreads();  // every lane has read item before lane 0 takes the next
-    if (i >= total) {
-      // the queue is empty: with tiles, join the stream slot with the most
-      // tiles left (every SPF is handed out by now, so its wait ends);
-      // done when no slot has any
-      if (!T) break;
-      if (tid < 64u) {
-        uint32_t best = 0, at = 0;
-        for (uint32_t b = tid; b < U; b += 64u) {
-          const uint32_t taken =
-              __hip_atomic_load(&tiles[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          const uint32_t rem = taken < T ? T - taken : 0u;
-          if (rem > best) {
-            best = rem;
-            at = b;
-          }
-        }
-#pragma unroll
-        for (int d = 32; d >= 1; d >>= 1) {
-          const uint32_t ob = __shfl_xor(best, d, 64), oa = __shfl_xor(at, d, 64);
-          if (ob > best || (ob == best && oa < at)) {
-            best = ob;
-            at = oa;
-          }
-        }
-        if (tid == 0u) item = best ? at : 0xFFFFFFFFu;
-      }
-      __syncthreads();
-      const uint32_t slot = item;
-      __syncthreads();
-      if (slot == 0xFFFFFFFFu) break;
-      i = G + total + slot;  // a join of that slot (below)
-    }
+    if (i >= total) break;
     uint32_t gu = i, part = 0, parts = P;
     bool spf = true;
-    if (i >= G + total) {  // join (tiles): the slot, no fixed part
-      gu = i - (G + total);
-      spf = false;
-    } else if (i >= G) {
-      uint32_t j = i - G, r;
+    if (i >= G) {
+      uint32_t j = i - G, r, b;
       if (j < headItems) {
-        gu = j / (P + 1u);
-        r = j - gu * (P + 1u);
+        b = j / (P + 1u);
+        r = j - b * (P + 1u);
       } else {
         j -= headItems;
-        const uint32_t b = j / (P2 + 1u);
-        r = j - b * (P2 + 1u);
-        gu = U1 + b;
+        const uint32_t k = j / (P2 + 1u);
+        r = j - k * (P2 + 1u);
+        b = U1 + k;
         parts = P2;
       }
       if (r == 0u) {
-        gu += G;
+        gu = G + b;
         if (gu >= U) continue;
       } else {
         spf = false;
         part = r - 1u;
+        gu = slotUnit(b);
       }
     }
+    uint32_t gi = 0;
+    while (gi + 1u < grps.n && gu >= grps.g[gi + 1u].base) ++gi;
+    const LdsGroup& grp = grps.g[gi];
+    const uint32_t u = gu - grp.base;
     if (spf) {
-      uint32_t gi = 0;
-      while (gi + 1u < grps.n && gu >= grps.g[gi + 1u].base) ++gi;
-      const LdsGroup& grp = grps.g[gi];
-      const uint32_t u = gu - grp.base;
       const ogs_unit unit = grp.units[u];
       switch (grp.W) {
         case 1: spf_lds_unit<1>(g, L, img, mm, nEB, unit, u, flags, grp.dist, grp.nh, smem, qCount, wg, dg); break;
@@ -906,49 +876,39 @@ __global__ __launch_bounds__(kLdsBlock) void spf_lds_route_kernel(
         case 3: spf_lds_unit<3>(g, L, img, mm, nEB, unit, u, flags, grp.dist, grp.nh, smem, qCount, wg, dg); break;
         default: spf_lds_unit<4>(g, L, img, mm, nEB, unit, u, flags, grp.dist, grp.nh, smem, qCount, wg, dg); break;
       }
-      // publish: every wave's row stores drained, barrier, release, then the
-      // flag (unit order) or the unit's slot in the ready list
+      // publish: every wave's row stores drained, barrier, release, flag
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (tid == 0u) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (unitOrder) {
-          __hip_atomic_store(&ready[gu], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-          const uint32_t slot = atomicAdd(rctr, 1u);
-          __hip_atomic_store(&ready[slot], gu + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+        __hip_atomic_store(&ready[gu], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
+      OGS_ITEM_STAMP(1u, gu, tItem, tItem);
       continue;
     }
-    // stream slot gu: wait for its SPF (a handed-out SPF item: it finishes)
-    uint32_t* tc = T ? tiles + gu : nullptr;
     if (tid == 0u) {
-      uint32_t x;
-      while ((x = __hip_atomic_load(&ready[gu], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) ==
-             0u) {
+      while (__hip_atomic_load(&ready[gu], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
         __builtin_amdgcn_s_sleep(8);
       }
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      slotUnit = unitOrder ? gu : x - 1u;
     }
     __syncthreads();
-    gu = slotUnit;
-    uint32_t gi = 0;
-    while (gi + 1u < grps.n && gu >= grps.g[gi + 1u].base) ++gi;
-    const LdsGroup& grp = grps.g[gi];
-    const uint32_t u = gu - grp.base;
+#ifdef OGS_STAMPS
+    const uint32_t tReady = rt();
+#endif
     // the per-node records go to the state region (the image stays)
     uint32_t* rec0 = reinterpret_cast<uint32_t*>(smem + L.block);
     switch (grp.W) {
-      case 1: lds_stream_item<1, KeyT>(g, pt, key, grp, u, part, parts, flags, rec0, tc, T, sTile); break;
-      case 2: lds_stream_item<2, KeyT>(g, pt, key, grp, u, part, parts, flags, rec0, tc, T, sTile); break;
-      case 3: lds_stream_item<3, KeyT>(g, pt, key, grp, u, part, parts, flags, rec0, tc, T, sTile); break;
-      default: lds_stream_item<4, KeyT>(g, pt, key, grp, u, part, parts, flags, rec0, tc, T, sTile); break;
+      case 1: lds_stream_item<1, KeyT>(g, pt, key, grp, u, part, parts, flags, rec0); break;
+      case 2: lds_stream_item<2, KeyT>(g, pt, key, grp, u, part, parts, flags, rec0); break;
+      case 3: lds_stream_item<3, KeyT>(g, pt, key, grp, u, part, parts, flags, rec0); break;
+      default: lds_stream_item<4, KeyT>(g, pt, key, grp, u, part, parts, flags, rec0); break;
     }
+    OGS_ITEM_STAMP(2u, gu, tItem, tReady);
   }
+#undef OGS_ITEM_STAMP
 }
 
 int num_cus() {
@@ -996,7 +956,7 @@ hipError_t launch_lds_prep(const ogs_graph& g, const ogs_prefix_table* pt, void*
                      g, ptv, nKB ? key : nullptr, key16 ? 1u : 0u, nKB, L, base,
                      reinterpret_cast<uint2*>(base + S.mm), S.nEB,
                      reinterpret_cast<uint32_t*>(base + S.ctr),
-                     reinterpret_cast<uint32_t*>(base + S.ready), 2u * uint32_t(nUnits));
+                     reinterpret_cast<uint32_t*>(base + S.ready), uint32_t(nUnits));
   return hipGetLastError();
 }
 
@@ -1046,15 +1006,15 @@ int g_ldsGrid = 0;
 // (1, default) or u32 keys (0, A/B)
 int g_ldsKey16 = 1;
 int g_ldsTail = 1;
-// "lds_ready": the one-launch form streams units in SPF completion order
-// (1, default) or unit order (0, A/B); "lds_bfs_exit": the BFS rounds stop
-// once every node is reached (1, default) or run the empty last layer (0)
-int g_ldsReady = 1;
+// "lds_bfs_exit": the BFS rounds stop once every node is reached (1,
+// default) or run the empty last layer (0, A/B): C3 N = 8 shard 0.1695 vs
+// 0.1732 ms (profiles/r05_c3_ab_bfs_exit.log)
 int g_ldsBfsExit = 1;
-// "lds_tiles": 0 fixed prefix ranges per stream item; T > 0 each unit's rows
-// in T tiles taken dynamically by the workgroups on that unit, and
-// workgroups left without items join the unit with the most tiles left
-int g_ldsTiles = 0;
+// "lds_lead": narrow units streamed before the wide group (-1 auto: one
+// grid's worth of stream items on sharded builds, 0 none); "lds_tail_parts":
+// ranges per unit of the launch's last units (0 auto)
+int g_ldsLead = -1;
+int g_ldsTailParts = 0;
 
 bool lds_key16(const ogs_graph& g) {
   return g_ldsKey16 && g.max_nodes > 0 && uint32_t(g.max_nodes) <= kKey16MaxNodes;
@@ -1095,20 +1055,42 @@ hipError_t launch_spf_lds_routes(const ogs_graph& g, const ogs_prefix_table& pt,
   // units per CU); profiles/r04_lds_store_parts_ab.log
   const uint32_t P = g_ldsParts > 0 ? uint32_t(g_ldsParts)
                                     : (uint32_t(U) >= 4u * uint32_t(grid) ? 2u : 4u);
-  // "lds_tail" (default 1): with fewer than 4 ranges per unit, the last
-  // grid's worth of units stream in 4 (the queue's final items are the
-  // launch's tail); 0 every unit in P
-  const uint32_t P2 = (g_ldsTail && P < 4u) ? 4u : P;
-  const uint32_t U1 = P2 != P ? uint32_t(U - std::min(U, grid)) : uint32_t(U);
+  const bool sharded = uint32_t(U) < 4u * uint32_t(grid);
+  // the launch's last units stream in P2 > P ranges ("lds_tail" 1,
+  // default): whole-node builds the last grid's worth of units in 4,
+  // sharded builds the last grid's worth of ITEMS in "lds_tail_parts"
+  // (auto 8); 0 every unit in P
+  LdsSchedule sch{P, P, uint32_t(U), 0u, 0u};
+  if (g_ldsTail) {
+    if (!sharded && P < 4u) {
+      sch.P2 = 4u;
+      sch.U1 = uint32_t(U - std::min(U, grid));
+    } else if (sharded) {
+      sch.P2 = g_ldsTailParts > 0 ? uint32_t(g_ldsTailParts) : 2u * P;
+      const uint32_t tailUnits = std::min(uint32_t(U), (uint32_t(grid) + sch.P2 - 1u) / sch.P2);
+      sch.U1 = uint32_t(U) - tailUnits;
+    }
+    if (sch.P2 <= P) sch.U1 = uint32_t(U);
+  }
+  // lead ("lds_lead", -1 auto): on sharded builds with several width groups,
+  // one grid's worth of stream items of narrow units before the wide group
+  // (whose SPFs finish last); needs Uw <= G (the slot map's SPFs are then
+  // always handed out before their stream items)
+  const uint32_t Uw = n > 1 ? uint32_t(groups[0].n) : 0u;
+  const uint32_t Gl = std::min(uint32_t(U), uint32_t(grid));
+  if (Uw > 0u && Uw <= Gl) {
+    const uint32_t want = g_ldsLead >= 0 ? uint32_t(g_ldsLead)
+                                         : (sharded ? (uint32_t(grid) + P - 1u) / P : 0u);
+    sch.lead = std::min(want, uint32_t(U) - Uw);
+    sch.Uw = sch.lead ? Uw : 0u;
+  }
   if (g_routeStoreNt & 1) flags |= kFlagNtStores;
-  if (!g_ldsReady) flags |= kFlagLdsUnitOrder;
   if (!g_ldsBfsExit) flags |= kFlagLdsNoBfsExit;
   auto go = [&](auto k, auto keyp) {
     hipError_t a = allow_lds(k, lds);
     if (a != hipSuccess) return a;
     hipLaunchKernelGGL(k, dim3(grid), dim3(kLdsBlock), lds, stream, g, pt, keyp, L,
-                       static_cast<const uint8_t*>(base), mm, S.nEB, G, flags, ctr, ready, P,
-                       P2, U1, uint32_t(g_ldsTiles));
+                       static_cast<const uint8_t*>(base), mm, S.nEB, G, flags, ctr, ready, sch);
     return hipGetLastError();
   };
   return key16 ? go(spf_lds_route_kernel<uint16_t>, static_cast<const uint16_t*>(key))
@@ -1118,6 +1100,16 @@ hipError_t launch_spf_lds_routes(const ogs_graph& g, const ogs_prefix_table& pt,
 }  // namespace ogs
 
 #ifdef OGS_STAMPS
+extern "C" int ogs_diag_item_stamps(uint32_t* host, int32_t words) {
+  const size_t n = std::min<size_t>(size_t(words), size_t(ogs::kLdsDiagWgsItems) * ogs::kItemStamps * 4);
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(ogs::g_itemStamps), n * 4, 0,
+                             hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+extern "C" int ogs_diag_item_stamps_clear() {
+  void* p = nullptr;
+  if (hipGetSymbolAddress(&p, HIP_SYMBOL(ogs::g_itemStamps)) != hipSuccess) return -1;
+  return hipMemset(p, 0, sizeof(ogs::g_itemStamps)) == hipSuccess ? 0 : -1;
+}
 extern "C" int ogs_diag_lds_stamps(uint32_t* host, int32_t words) {
   const size_t n = std::min<size_t>(size_t(words), size_t(4) * ogs::kLdsDiagWgs * 32);
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(ogs::g_ldsStamps), n * 4, 0,

@@ -76,10 +76,10 @@ def _c3(product, names, ppn=100):
                                                              lds_grid=100),
                                   dict(route_stream=5, lds_key16=0),
                                   dict(route_stream=5, lds_tail=0),
-                                  dict(route_stream=5, lds_ready=0, lds_bfs_exit=0),
+                                  dict(route_stream=5, lds_lead=0, lds_bfs_exit=0),
                                   dict(route_stream=5, lds_parts=8, lds_grid=300),
-                                  dict(route_stream=5, lds_tiles=13),
-                                  dict(route_stream=5, lds_tiles=3, lds_ready=0, lds_grid=64)])
+                                  dict(route_stream=5, lds_lead=100, lds_tail_parts=16),
+                                  dict(route_stream=5, lds_tail_parts=3, lds_lead=7, lds_grid=64)])
 def test_c3_full_every_source_matches_oracle(product, opts):
     """C3-full at bench size (2,080 sources x 208k prefixes) through
     bench.py's two-stream width-group launches: every source's digest equals
@@ -99,8 +99,8 @@ def test_c3_full_every_source_matches_oracle(product, opts):
     import openr_amd.capi as capi
     lib = capi.load()
     defaults = dict(frontier_block=0, frontier_parts=0, frontier_parts_wide=0, route_stream=5,
-                    lds_parts=0, lds_grid=0, lds_key16=1, lds_tail=1, lds_ready=1,
-                    lds_bfs_exit=1, lds_tiles=0)
+                    lds_parts=0, lds_grid=0, lds_key16=1, lds_tail=1, lds_lead=-1,
+                    lds_bfs_exit=1, lds_tail_parts=0)
     for k, v in opts.items():
         capi.check(lib, lib.ogs_set_option(k.encode(), v), k)
     try:

@@ -113,3 +113,43 @@ def test_no_route_counted_on_every_path(product):
     db = M.SpfSolver("1", True, False, False, False).buildRouteDb("1", als, ps)
     assert db is not None
     assert M.decision_counters()["decision.no_route_to_prefix.count"] == 1
+
+
+def test_spf_memo_every_source(product, oracle):
+    """The getSpfResult memo holds every source's SPF until a topology change
+    (LinkState.cpp:705-715, LinkState.h:369-372), and Decision builds
+    RouteDbs for arbitrary nodes (getDecisionRouteDb, Decision.cpp:341-361):
+    alternating buildRouteDb("1"), ("2"), ("1") launches TWO device SPFs --
+    the engine's own launch counter equals decision.spf_runs -- and the
+    RouteDbs equal the oracle's. getSpfResult of a built source reads the
+    same device rows (no launch); a topology change starts over."""
+    M = product
+    als, ls, ps = _line(M)
+    oals, ols, ops = _line(oracle)
+    solver = M.SpfSolver("1", True, True, False, False)
+    osolver = oracle.SpfSolver("1", True, True, False, False)
+    M.reset_decision_counters()
+    for node in ("1", "2", "1", "2", "3", "1"):
+        got = solver.buildRouteDb(node, als, ps).canonical()
+        assert got == osolver.buildRouteDb(node, oals, ops).canonical(), node
+    c = M.decision_counters()
+    assert c["decision.spf_runs.count"] == 3
+    assert c["decision.gpu.spf_launches.count"] == 3
+    want = {k: (v[0], sorted(v[1])) for k, v in ols.getSpfResult("2").items()}
+    assert {k: (v[0], sorted(v[1])) for k, v in ls.getSpfResult("2").items()} == want
+    c = M.decision_counters()
+    assert c["decision.spf_runs.count"] == 3 and c["decision.gpu.spf_launches.count"] == 3
+    # incremental routes of a memoised source: no SPF either
+    out = solver.createRoutesForPrefixes("3", als, ps, {"fc00::1/128"})
+    assert out["fc00::1/128"] is not None
+    assert M.decision_counters()["decision.gpu.spf_launches.count"] == 3
+    # a topology change (metric 1 -> 5 on 1-2) invalidates every source
+    adjs = [L.createAdjacency("2", "if12", "if21", "fe80::2", "10.0.0.2", 5, 102)]
+    assert ls.updateAdjacencyDatabase(L.createAdjDb("1", adjs, 1), A)["topologyChanged"]
+    assert ols.updateAdjacencyDatabase(L.createAdjDb("1", adjs, 1), A)["topologyChanged"]
+    for node in ("2", "1", "2"):
+        assert (solver.buildRouteDb(node, als, ps).canonical() ==
+                osolver.buildRouteDb(node, oals, ops).canonical()), node
+    c = M.decision_counters()
+    assert c["decision.spf_runs.count"] == 5
+    assert c["decision.gpu.spf_launches.count"] == 5

@@ -27,8 +27,8 @@ def _arrays(product, names):
     return br.host_arrays()
 
 
-@pytest.mark.parametrize("route_stream,tiles", [(5, 0), (5, 5), (2, 0)])
-def test_groups_match_per_group_calls(product, route_stream, tiles):
+@pytest.mark.parametrize("route_stream,lead", [(5, -1), (5, 3), (2, -1)])
+def test_groups_match_per_group_calls(product, route_stream, lead):
     import torch
 
     import openr_amd.capi as capi
@@ -75,7 +75,7 @@ def test_groups_match_per_group_calls(product, route_stream, tiles):
     stream = torch.cuda.current_stream()
     try:
         capi.check(lib, lib.ogs_set_option(b"route_stream", route_stream), "route_stream")
-        capi.check(lib, lib.ogs_set_option(b"lds_tiles", tiles), "lds_tiles")
+        capi.check(lib, lib.ogs_set_option(b"lds_lead", lead), "lds_lead")
         units = [u.contiguous().view(-1).to(dev) for u, _, _ in specs]
         grouped = [outs(len(u) // 2, W, rows) for u, (_, W, rows) in zip(units, specs)]
         arr = (capi.RouteGroup * 3)()
@@ -100,7 +100,7 @@ def test_groups_match_per_group_calls(product, route_stream, tiles):
         torch.cuda.synchronize()
     finally:
         lib.ogs_set_option(b"route_stream", 5)
-        lib.ogs_set_option(b"lds_tiles", 0)
+        lib.ogs_set_option(b"lds_tail_parts", 0)
     for i, ((o, _), s) in enumerate(zip(grouped, single)):
         for k in o:
             assert torch.equal(o[k], s[k]), f"group {i} (W={specs[i][1]}) array {k} differs"

@@ -74,8 +74,8 @@ def _oracle(oracle, uniform=False):
 
 @pytest.mark.parametrize("uniform", [False, True])
 @pytest.mark.parametrize("options", [dict(route_stream=5), dict(route_stream=4),
-                                     dict(route_stream=5, lds_bfs_exit=0, lds_ready=0),
-                                     dict(route_stream=5, lds_tiles=7),
+                                     dict(route_stream=5, lds_bfs_exit=0, lds_tail_parts=9),
+                                     dict(route_stream=5, lds_parts=3, lds_lead=2),
                                      dict(route_stream=2, spf_queue=0),
                                      dict(route_stream=1, spf_queue=0)])
 def test_deep_line_with_island_batch(product, oracle, options, uniform):
@@ -101,8 +101,8 @@ def test_deep_line_with_island_batch(product, oracle, options, uniform):
         lib.ogs_set_option(b"route_stream", 5)
         lib.ogs_set_option(b"spf_queue", -1)
         lib.ogs_set_option(b"lds_bfs_exit", 1)
-        lib.ogs_set_option(b"lds_ready", 1)
-        lib.ogs_set_option(b"lds_tiles", 0)
+        lib.ogs_set_option(b"lds_lead", -1)
+        lib.ogs_set_option(b"lds_tail_parts", 0)
     want = _oracle(oracle, uniform)
     # the island's anycast member is unreachable from the line: the line's
     # end must be the prefix's only route source

@@ -14,6 +14,7 @@
 #                             `python3 bench.py <bench args>` (commas -> spaces)
 #   sqlds:<tag>:<bench args>  second SQ pass: LDS instruction / wait counters
 #   stamps:<as-rank>          LDS SPF phase stamps (make stamps; tools/c3_stamps.py --lds)
+#   timeline:<as-rank>[:o=v+..] C3 one-launch item timeline (tools/c3_timeline.py)
 #   ab:<as-rank>:<A>:<B>[:..] in-process C3 option A/B (tools/c3_opt_ab.py), variants
 #                             are name=value lists joined by '+'
 set -o pipefail
@@ -68,6 +69,8 @@ for recipe in "$@"; do
       [ $rc -eq 0 ] || exit $rc ;;
     stamps)
       OGS_LIB=openr_amd/lib/libopenr_gpu_stamps.so step "stamps_$n" 300 python -u tools/c3_stamps.py --lds --as-rank "$rest" --opt route_stream=4 ;;
+    timeline)
+      OGS_LIB=openr_amd/lib/libopenr_gpu_stamps.so step "timeline_$n" 300 python -u tools/c3_timeline.py --as-rank "${rest%%:*}" $(for o in $(echo "${rest#*:}" | tr '+' ' '); do [ "$o" != "${rest%%:*}" ] && echo "--opt $o"; done) ;;
     ab)
       IFS=: read -r -a parts <<< "$rest"
       rank=${parts[0]}; vs=()
