@@ -335,11 +335,12 @@ def finish_g1(out, digest, args):
 
 
 # ----------------------------------------------------------------- C3 ---
-def c3_launches(torch, M, capi, dev, names, ppn=100, with_sel=False):
+def c3_launches(torch, M, capi, dev, names, ppn=100, with_sel=False, opts=None):
     """Host build + device upload of the C3 launches for the sources
     `names`: grouped by next-hop bitset width (SSW+RSW: 1 word, FSW: 3 words
-    -> 4) so each launch writes masks of its own width."""
-    opts = dict(C3_OPTS, prefixesPerNode=ppn)
+    -> 4) so each launch writes masks of its own width. `opts`: another
+    fabric of the same naming (C3-ref, tests/test_gpu_bench_size.py)."""
+    opts = dict(opts or C3_OPTS, prefixesPerNode=ppn)
     N = len(c3_source_names())
     launches = []
     fsw = [n for n in names if n.startswith("2-")]
@@ -1058,7 +1059,12 @@ def run_c5(args, torch, dist, rank, world, local_rank):
 
 
 # --------------------------------------------------------------- main ---
+DIST_BACKEND = [None]  # the process group the per-rank records went through
+
+
 def finish(line):
+    line["collectives"] = {"backend": DIST_BACKEND[0], "use": "per-rank record all-gather + "
+                           "MAX elapsed only (no data-path exchange)"}
     print(json.dumps(line), flush=True)
     if DIGEST_FAILURES:
         for f in DIGEST_FAILURES:
@@ -1306,6 +1312,10 @@ def main():
                     help="C5: HIP streams (RouteDb+policy || KSP2)")
     ap.add_argument("--opt", action="append", default=[],
                     help="engine option name=value (ogs_set_option), for A/B runs")
+    ap.add_argument("--dist", default="auto", choices=["auto", "nccl", "none"],
+                    help="process group: auto (default) RCCL ('nccl') at every world size, "
+                         "so the N=1 line takes the N>1 collective path too (gloo when "
+                         "ranks share a device); nccl the same; none only at N=1: no group")
     ap.add_argument("--launch-check", action="store_true",
                     help="only join the process group and print the rank map (no GPU)")
     args = ap.parse_args()
@@ -1345,12 +1355,27 @@ def main():
         raise SystemExit(2)
     torch.cuda.set_device(local_rank)
     dist = None
-    if world > 1:
+    if world > 1 and args.dist == "none":
+        print("bench.py: --dist none needs a single rank", file=sys.stderr)
+        raise SystemExit(2)
+    if world > 1 or args.dist != "none":
+        # RCCL carries the per-rank records (shard.reduce_stats / reduce_xor)
+        # at every world size: the N=1 line runs the same collective code as
+        # N=8 (tests/test_gpu_rccl.py). A single rank without a launcher
+        # rendezvous on 127.0.0.1 itself.
         import torch.distributed as dist
+        init = {}
+        if "MASTER_ADDR" not in os.environ:
+            import socket
+            with socket.socket() as sk:
+                sk.bind(("127.0.0.1", 0))
+                init = dict(init_method=f"tcp://127.0.0.1:{sk.getsockname()[1]}",
+                            rank=rank, world_size=world)
         if share:
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", **init)
         else:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank), **init)
+        DIST_BACKEND[0] = dist.get_backend()
 
     import openr_amd
     import openr_amd.capi as capi

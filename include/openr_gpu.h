@@ -305,10 +305,12 @@ int ogs_host_free(void* hptr);
  *                 builds (fewer than 4 units per workgroup) the last grid's
  *                 worth of items in "lds_tail_parts" ranges per unit (0
  *                 auto: 2 x lds_parts) and "lds_lead" narrow units streamed
- *                 before the widest group (-1 auto: a grid's worth of
- *                 items; 0 none); unit-weight (BFS) SPFs stop once every
+ *                 before the widest group (0, default: none; -1 a grid's
+ *                 worth of items); unit-weight (BFS) SPFs stop once every
  *                 node is reached ("lds_bfs_exit" 1, default; 0 they run
- *                 the empty last layer, A/B). Scratch
+ *                 the empty last layer, A/B) and pull a layer when 4 x the
+ *                 unreached nodes' chunk records <= "lds_pull" x the
+ *                 frontier's (6, default; 0 push only, A/B). Scratch
  *                 (prefix keys, dist/next-hop sets when out->dist / out->nh
  *                 are NULL) comes from a grow-only per-device workspace.
  *                 "route_store_nt", bits: 1 the RouteDb stream's 16-B stores

@@ -421,33 +421,84 @@ class LinkState {
 // vector (one allocation for the one or few advertisers a prefix has, where
 // a node-based map allocates per entry). Iterates as pairs, like a map.
 class PrefixEntryList {
+  // sorted by (node, area); most prefixes have ONE advertisement, kept inline
+  // (no heap block per prefix: the C3 publication's 208k keys), more move to
+  // a vector
  public:
   using value_type = std::pair<NodeAndArea, std::shared_ptr<PrefixEntry>>;
-  using const_iterator = std::vector<value_type>::const_iterator;
-  using iterator = std::vector<value_type>::iterator;
-  const_iterator begin() const { return v_.begin(); }
-  const_iterator end() const { return v_.end(); }
-  iterator begin() { return v_.begin(); }
-  iterator end() { return v_.end(); }
-  size_t size() const { return v_.size(); }
-  bool empty() const { return v_.empty(); }
+  using const_iterator = const value_type*;
+  using iterator = value_type*;
+  PrefixEntryList() = default;
+  PrefixEntryList(const PrefixEntryList& o) { *this = o; }
+  PrefixEntryList(PrefixEntryList&& o) noexcept { *this = std::move(o); }
+  PrefixEntryList& operator=(const PrefixEntryList& o) {
+    if (this != &o) {
+      one_ = o.one_;
+      many_ = o.many_;
+      n_ = o.n_;
+      heap_ = o.heap_;
+    }
+    return *this;
+  }
+  PrefixEntryList& operator=(PrefixEntryList&& o) noexcept {
+    one_ = std::move(o.one_);
+    many_ = std::move(o.many_);
+    n_ = o.n_;
+    heap_ = o.heap_;
+    o.n_ = 0;
+    o.heap_ = false;
+    return *this;
+  }
+  const_iterator begin() const { return data(); }
+  const_iterator end() const { return data() + n_; }
+  iterator begin() { return data(); }
+  iterator end() { return data() + n_; }
+  size_t size() const { return n_; }
+  bool empty() const { return n_ == 0; }
   // the entry of `k` (inserted empty when absent) and whether it was new
   std::pair<iterator, bool> try_emplace(const NodeAndArea& k) {
-    auto it = std::lower_bound(v_.begin(), v_.end(), k,
-                               [](const value_type& a, const NodeAndArea& b) { return a.first < b; });
-    if (it != v_.end() && it->first == k) return {it, false};
-    return {v_.insert(it, value_type(k, nullptr)), true};
+    iterator it = find(k);
+    if (it != end() && it->first == k) return {it, false};
+    if (!heap_ && n_ == 0) {
+      one_ = value_type(k, nullptr);
+      n_ = 1;
+      return {&one_, true};
+    }
+    if (!heap_) {  // the second advertisement: both to the vector
+      many_.reserve(4);
+      many_.push_back(std::move(one_));
+      one_ = value_type();
+      heap_ = true;
+    }
+    const size_t at = size_t(it - many_.data());
+    many_.insert(many_.begin() + at, value_type(k, nullptr));
+    ++n_;
+    return {many_.data() + at, true};
   }
   size_t erase(const NodeAndArea& k) {
-    auto it = std::lower_bound(v_.begin(), v_.end(), k,
-                               [](const value_type& a, const NodeAndArea& b) { return a.first < b; });
-    if (it == v_.end() || it->first != k) return 0;
-    v_.erase(it);
+    iterator it = find(k);
+    if (it == end() || it->first != k) return 0;
+    if (!heap_) {
+      one_ = value_type();
+      n_ = 0;
+      return 1;
+    }
+    many_.erase(many_.begin() + (it - many_.data()));
+    --n_;
     return 1;
   }
 
  private:
-  std::vector<value_type> v_;
+  value_type* data() { return heap_ ? many_.data() : &one_; }
+  const value_type* data() const { return heap_ ? many_.data() : &one_; }
+  iterator find(const NodeAndArea& k) {
+    return std::lower_bound(begin(), end(), k,
+                            [](const value_type& a, const NodeAndArea& b) { return a.first < b; });
+  }
+  value_type one_;
+  std::vector<value_type> many_;
+  uint32_t n_{0};
+  bool heap_{false};
 };
 
 class PrefixState {
@@ -466,6 +517,15 @@ class PrefixState {
   // entry; the entry itself is stored as advertised (host bits kept).
   std::set<std::string> updatePrefixKeyed(const std::string& node, const std::string& area,
                                           const std::string& network, PrefixEntry entry);
+  // the same update without the changed-set allocation (the ingestion hot
+  // path): the table's key of `network` when it changed, else nullptr;
+  // `network` is moved into the table on first sight
+  const std::string* updatePrefixInPlace(const std::string& node, const std::string& area,
+                                         std::string&& network, PrefixEntry&& entry);
+  // true when (node, area)'s entry of `prefix` existed and was removed
+  bool deletePrefixInPlace(const std::string& node, const std::string& area,
+                           const std::string& prefix, std::string* network = nullptr);
+  void reserve(size_t prefixes) { prefixes_.reserve(prefixes); }
   // `prefix` is the key's network as given (PrefixKey does not mask);
   // compared by value, so the text is normalised first
   std::set<std::string> deletePrefix(const std::string& node,

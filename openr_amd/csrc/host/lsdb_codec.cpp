@@ -12,6 +12,8 @@
 // (key << 4 | value) when non-empty.
 #include "lsdb_codec.h"
 
+#include <algorithm>
+
 #include <arpa/inet.h>
 
 #include <cstring>
@@ -833,10 +835,16 @@ LsdbKeyUpdate LsdbIngest::applyDecoded(const std::string& area, LinkState& areaL
     // a default IpPrefix (no prefix field) is rejected by toIPNetwork
     if (d.network.empty()) fail("prefix: PrefixEntry without a prefix");
     u.kind = LsdbKeyUpdate::kPrefix;
-    u.changedPrefixes =
-        db.deletePrefix
-            ? prefixState.deletePrefix(db.thisNodeName, area, d.network)
-            : prefixState.updatePrefixKeyed(db.thisNodeName, area, d.network, std::move(entry));
+    if (db.deletePrefix) {
+      std::string net;
+      if (prefixState.deletePrefixInPlace(db.thisNodeName, area, d.network, &net)) {
+        u.changedPrefixes.push_back(std::move(net));
+      }
+    } else {
+      const std::string* net = prefixState.updatePrefixInPlace(
+          db.thisNodeName, area, std::move(d.network), std::move(entry));
+      if (net) u.changedPrefixes.push_back(*net);
+    }
   } catch (const std::exception& e) {  // Decision.cpp:781-784: log, drop the key
     u = LsdbKeyUpdate{};
     u.kind = LsdbKeyUpdate::kError;
@@ -872,7 +880,10 @@ LsdbKeyUpdate LsdbIngest::deleteKeyFromLsdb(const std::string& area, LinkState& 
     }
     u.kind = LsdbKeyUpdate::kPrefix;
     u.nodeName = pk->first;
-    u.changedPrefixes = prefixState.deletePrefix(pk->first, area, pk->second);
+    std::string net;
+    if (prefixState.deletePrefixInPlace(pk->first, area, pk->second, &net)) {
+      u.changedPrefixes.push_back(std::move(net));
+    }
   }
   return u;
 }
@@ -897,14 +908,41 @@ void LsdbIngest::processPublication(const std::string& area, AreaLinkStates& are
   for (const auto& [a, _] : areaLinkStates) areas_.insert(a);
   LinkState& ls = it->second;
   if (keyVals.empty() && expiredKeys.empty()) return;
-  std::map<std::string_view, const PublicationKeyVal*> ordered;
-  for (const auto& kv : keyVals) ordered[kv.key] = &kv;
-  for (const auto& [key, kv] : ordered) {
+  // keys in std::map order (the thrift map's, Decision.cpp:821-846): a
+  // sorted index (already sorted publications skip the sort); a repeated
+  // key keeps its last value, as the map assignment would
+  std::vector<const PublicationKeyVal*> ordered;
+  ordered.reserve(keyVals.size());
+  for (const auto& kv : keyVals) ordered.push_back(&kv);
+  auto less = [](const PublicationKeyVal* a, const PublicationKeyVal* b) { return a->key < b->key; };
+  if (!std::is_sorted(ordered.begin(), ordered.end(), less)) {
+    std::stable_sort(ordered.begin(), ordered.end(), less);
+  }
+  size_t prefixKeys = 0;
+  for (const auto& kv : keyVals) prefixKeys += kv.key.compare(0, 7, "prefix:") == 0;
+  prefixState.reserve(prefixState.prefixes().size() + prefixKeys);
+  // the prefix changes are gathered and merged into the pending set once
+  std::vector<std::string> changed;
+  uint32_t prefixUpdates = 0;
+  auto take = [&](LsdbKeyUpdate&& u) {
+    if (u.kind == LsdbKeyUpdate::kPrefix) {
+      for (auto& n : u.changedPrefixes) changed.push_back(std::move(n));
+      ++prefixUpdates;
+    } else {
+      pending.apply(u);
+    }
+  };
+  for (size_t i = 0; i < ordered.size(); ++i) {
+    if (i + 1 < ordered.size() && ordered[i + 1]->key == ordered[i]->key) continue;
+    const PublicationKeyVal* kv = ordered[i];
     std::optional<std::string_view> v;
     if (kv->value) v = *kv->value;
-    pending.apply(updateKeyInLsdb(area, ls, prefixState, kv->key, v, inInitialization));
+    take(updateKeyInLsdb(area, ls, prefixState, kv->key, v, inInitialization));
   }
-  for (const auto& key : expiredKeys) pending.apply(deleteKeyFromLsdb(area, ls, prefixState, key));
+  for (const auto& key : expiredKeys) take(deleteKeyFromLsdb(area, ls, prefixState, key));
+  std::sort(changed.begin(), changed.end());
+  changed.erase(std::unique(changed.begin(), changed.end()), changed.end());
+  pending.applyPrefixStateChanges(std::move(changed), prefixUpdates);
 }
 
 }  // namespace openr_amd

@@ -82,7 +82,7 @@ struct LsdbKeyUpdate {
   Kind kind{kSkipped};
   std::string nodeName;
   LinkState::LinkStateChange linkChange;
-  std::set<std::string> changedPrefixes;
+  std::vector<std::string> changedPrefixes;  // 0 or 1 network per prefix key
   std::string error;
 };
 
@@ -97,10 +97,19 @@ class DecisionPendingUpdates {
                          (c.linkAttributesChanged && nodeName == myNodeName_);
     ++count_;
   }
-  void applyPrefixStateChange(const std::set<std::string>& change) {
+  template <typename Range>
+  void applyPrefixStateChange(const Range& change) {
     updatedPrefixes_.insert(change.begin(), change.end());
     ++count_;
   }
+  // a publication's prefix changes at once: sorted, unique networks merged
+  // with hinted inserts (linear into an empty set), `keys` prefix keys
+  void applyPrefixStateChanges(std::vector<std::string>&& sortedUnique, uint32_t keys) {
+    auto hint = updatedPrefixes_.end();
+    for (auto& n : sortedUnique) hint = std::next(updatedPrefixes_.insert(hint, std::move(n)));
+    count_ += keys;
+  }
+  void countKeys(uint32_t n) { count_ += n; }
   void apply(const LsdbKeyUpdate& u);  // routes kAdjacency / kPrefix results
   void setNeedsFullRebuild() { needsFullRebuild_ = true; }
   bool needsFullRebuild() const { return needsFullRebuild_; }

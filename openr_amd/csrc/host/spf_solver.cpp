@@ -83,18 +83,29 @@ void PrefixState::logChange(const std::string& network) {
   changeLog_.push_back(network);
 }
 
+const std::string* PrefixState::updatePrefixInPlace(const std::string& node,
+                                                    const std::string& area,
+                                                    std::string&& network, PrefixEntry&& entry) {
+  // PrefixState.cpp:15-38
+  auto mapIt = prefixes_.find(network);
+  if (mapIt == prefixes_.end()) mapIt = prefixes_.try_emplace(std::move(network)).first;
+  auto& entries = mapIt->second;
+  auto [it, inserted] = entries.try_emplace(NodeAndArea(node, area));
+  if (!inserted && *it->second == entry) return nullptr;
+  it->second = std::make_shared<PrefixEntry>(std::move(entry));
+  version_ = nextVersionStamp();
+  logChange(mapIt->first);
+  return &mapIt->first;
+}
+
 std::set<std::string> PrefixState::updatePrefixKeyed(const std::string& node,
                                                      const std::string& area,
                                                      const std::string& network,
                                                      PrefixEntry entry) {
-  std::set<std::string> changed;  // PrefixState.cpp:15-38
-  auto& entries = prefixes_[network];
-  auto [it, inserted] = entries.try_emplace(NodeAndArea(node, area));
-  if (!inserted && *it->second == entry) return changed;
-  changed.insert(network);
-  it->second = std::make_shared<PrefixEntry>(std::move(entry));
-  version_ = nextVersionStamp();
-  logChange(network);
+  std::set<std::string> changed;
+  std::string key = network;
+  if (updatePrefixInPlace(node, area, std::move(key), std::move(entry))) changed.insert(network);
+
   return changed;
 }
 
@@ -111,17 +122,24 @@ std::set<std::string> PrefixState::updatePrefix(const std::string& node,
   return updatePrefixKeyed(node, area, network, std::move(entry));
 }
 
+bool PrefixState::deletePrefixInPlace(const std::string& node, const std::string& area,
+                                      const std::string& prefix, std::string* network) {
+  // PrefixState.cpp:40-57
+  auto it = prefixes_.find(prefixNetworkKey(prefix, /*applyMask=*/false));
+  if (it == prefixes_.end() || !it->second.erase(std::make_pair(node, area))) return false;
+  if (network) *network = it->first;
+  logChange(it->first);
+  if (it->second.empty()) prefixes_.erase(it);
+  version_ = nextVersionStamp();
+  return true;
+}
+
 std::set<std::string> PrefixState::deletePrefix(const std::string& node,
                                                 const std::string& area,
                                                 const std::string& prefix) {
-  std::set<std::string> changed;  // PrefixState.cpp:40-57
-  auto it = prefixes_.find(prefixNetworkKey(prefix, /*applyMask=*/false));
-  if (it != prefixes_.end() && it->second.erase(std::make_pair(node, area))) {
-    changed.insert(it->first);
-    logChange(it->first);
-    if (it->second.empty()) prefixes_.erase(it);
-    version_ = nextVersionStamp();
-  }
+  std::set<std::string> changed;
+  std::string network;
+  if (deletePrefixInPlace(node, area, prefix, &network)) changed.insert(std::move(network));
   return changed;
 }
 

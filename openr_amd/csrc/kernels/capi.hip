@@ -21,6 +21,7 @@ extern int g_ldsKey16;
 extern int g_ldsTail;
 extern int g_ldsLead;
 extern int g_ldsBfsExit;
+extern int g_ldsPull;
 extern int g_ldsTailParts;
 extern int g_routeStoreNt;
 extern int g_spfSeedRow;
@@ -219,6 +220,11 @@ int ogs_set_option(const char* name, int64_t value) {
   if (std::strcmp(name, "lds_tail_parts") == 0) {
     if (value < 0 || value > 64) return fail(OGS_E_INVALID, "lds_tail_parts must be in [0, 64]");
     ogs::g_ldsTailParts = int(value);
+    return OGS_OK;
+  }
+  if (std::strcmp(name, "lds_pull") == 0) {
+    if (value < 0 || value > 15) return fail(OGS_E_INVALID, "lds_pull must be in [0, 15]");
+    ogs::g_ldsPull = int(value);
     return OGS_OK;
   }
   if (std::strcmp(name, "lds_bfs_exit") == 0) {

@@ -49,6 +49,9 @@ constexpr uint32_t kLdsDiagWgsItems = 1024;  // workgroups with item stamps (OGS
 // launch flag of the LDS forms (above the OGS_F_* bits): the BFS rounds'
 // all-reached exit off ("lds_bfs_exit" 0, A/B)
 constexpr uint32_t kFlagLdsNoBfsExit = 1u << 25;
+// bits 20..23: the BFS rounds' pull ratio ("lds_pull"): a round pulls when
+// 4 x (chunk records of unreached nodes) <= ratio x (the frontier's)
+constexpr uint32_t kFlagLdsPullShift = 20;
 
 __host__ __device__ inline uint32_t al16(uint32_t x) { return (x + 15u) & ~15u; }
 
@@ -90,7 +93,7 @@ __host__ LdsImage lds_image(const ogs_graph& g, int W) {
 }
 
 // Scratch of the LDS paths, one call: images [num_topos * stride] | weight
-// min / max partials uint2[num_topos * nEB] (one per prep edge block) | work
+// min / max / asymmetry partials uint4[num_topos * nEB] (one per prep edge block) | work
 // counter (u32, 256-B line) | unit ready flags u32[nUnits] (megakernel).
 constexpr uint32_t kPrepEdges = kLdsBlock * 8;  // edges per prep edge block
 struct LdsScratch {
@@ -103,7 +106,7 @@ __host__ LdsScratch lds_scratch(const ogs_graph& g, const LdsImage& L, int nUnit
   LdsScratch S{};
   S.nEB = (uint32_t(std::max(g.max_edges, 1)) + kPrepEdges - 1u) / kPrepEdges;
   S.mm = r256(size_t(g.num_topos) * L.stride);
-  S.ctr = S.mm + r256(size_t(g.num_topos) * S.nEB * 8u);
+  S.ctr = S.mm + r256(size_t(g.num_topos) * S.nEB * 16u);
   S.ready = S.ctr + 256u;
   S.bytes = S.ready + r256(size_t(std::max(nUnits, 1)) * 4u);
   return S;
@@ -120,11 +123,12 @@ __host__ LdsScratch lds_scratch(const ogs_graph& g, const LdsImage& L, int nUnit
 __global__ __launch_bounds__(kLdsBlock) void lds_prep_kernel(
     ogs_graph g, ogs_prefix_table pt, void* __restrict__ key, uint32_t key16, uint32_t nKB,
     LdsImage L,
-    uint8_t* __restrict__ img, uint2* __restrict__ mm, uint32_t nEB, uint32_t* __restrict__ ctr,
+    uint8_t* __restrict__ img, uint4* __restrict__ mm, uint32_t nEB, uint32_t* __restrict__ ctr,
     uint32_t* __restrict__ ready, uint32_t nReady) {
   constexpr uint32_t B = kLdsBlock;
   __shared__ uint32_t wsum[B / 64];
   __shared__ uint32_t whi[B / 64];
+  __shared__ uint32_t wasym[B / 64];
   __shared__ uint32_t base;
   const uint32_t T = uint32_t(g.num_topos), tid = threadIdx.x;
   const int lane = int(tid & 63u), wave = int(tid >> 6);
@@ -196,17 +200,47 @@ __global__ __launch_bounds__(kLdsBlock) void lds_prep_kernel(
       x[k] = e < E ? edges[e] : uint64_t(OGS_EDGE_DOWN);
     }
     uint32_t lo = 0xFFFFFFFFu, hi = 0u;
+    // symmetry (the BFS pull's precondition): each edge u -> v has its
+    // reverse v -> u (rslot, or rslot_ext past 511) in the same up / down
+    // state; unknown (no edge_src, saturated slot without rslot_ext) = asym
+    bool asym = g.edge_src == nullptr;
 #pragma unroll
     for (uint32_t k = 0; k < 8; ++k) {
       const uint32_t e = e00 + k * B;
       const uint32_t w = static_cast<uint32_t>(x[k]);
       const bool down = (w & OGS_EDGE_DOWN) != 0u;
-      if (e < E) eimg[e] = uint16_t(edge_dst(w) | (down ? kDown16 : 0u));
+      if (e < E) {
+        eimg[e] = uint16_t(edge_dst(w) | (down ? kDown16 : 0u));
+        if (!asym) {
+          uint32_t rs = (w >> OGS_EDGE_RSLOT_SHIFT) & OGS_EDGE_RSLOT_MASK;
+          if (rs == OGS_EDGE_RSLOT_MASK) {
+            if (g.rslot_ext) {
+              rs = g.rslot_ext[e0 + e];
+            } else {
+              asym = true;
+            }
+          }
+          const uint32_t v = edge_dst(w);
+          if (!asym && v < N) {
+            const uint32_t rb = g.row_ptr[nb + v] - e0, re = g.row_ptr[nb + v + 1] - e0;
+            if (rb + rs >= re) {
+              asym = true;
+            } else {
+              const uint32_t rw = static_cast<uint32_t>(edges[rb + rs]);
+              asym = edge_dst(rw) != g.edge_src[e0 + e] ||
+                  ((rw & OGS_EDGE_DOWN) != 0u) != down;
+            }
+          } else {
+            asym = true;
+          }
+        }
+      }
       if (!down) {
         lo = min(lo, static_cast<uint32_t>(x[k] >> 32));
         hi = max(hi, static_cast<uint32_t>(x[k] >> 32));
       }
     }
+    const uint32_t anyAsym = __ballot(asym) != 0ull ? 1u : 0u;
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) {
       lo = min(lo, __shfl_xor(lo, d, 64));
@@ -215,14 +249,17 @@ __global__ __launch_bounds__(kLdsBlock) void lds_prep_kernel(
     if (lane == 0) {
       wsum[wave] = lo;
       whi[wave] = hi;
+      wasym[wave] = anyAsym;
     }
     __syncthreads();
     if (tid == 0) {
+      uint32_t as = wasym[0];
       for (uint32_t w = 1; w < B / 64u; ++w) {
         lo = min(lo, wsum[w]);
         hi = max(hi, whi[w]);
+        as |= wasym[w];
       }
-      mm[size_t(t) * nEB + eb] = make_uint2(lo, hi);
+      mm[size_t(t) * nEB + eb] = make_uint4(lo, hi, as, 0u);
     }
     return;
   }
@@ -277,6 +314,7 @@ __device__ uint32_t g_ldsStamps[4 * kLdsDiagWgs * 32];
 struct LdsWg {
   uint32_t staged = 0xFFFFFFFFu;
   uint32_t C = 0, uniform = 0, w0 = 0, N = 0, e0 = 0;
+  uint32_t sym = 0;  // every edge's reverse present, same up / down state
 };
 
 struct NoDiag {
@@ -330,7 +368,7 @@ struct LdsStamps {
 template <int W, typename Diag>
 __device__ __forceinline__ void spf_lds_unit(
     const ogs_graph& g, const LdsImage& L, const uint8_t* __restrict__ img,
-    const uint2* __restrict__ mm, uint32_t nEB, const ogs_unit unit, uint32_t u,
+    const uint4* __restrict__ mm, uint32_t nEB, const ogs_unit unit, uint32_t u,
     uint32_t flags, uint32_t* __restrict__ oDist, uint32_t* __restrict__ oNh, char* smem,
     uint32_t* qCount, LdsWg& wg, Diag& dg) {
   constexpr uint32_t kInf = 0xFFFFFFFFu;
@@ -380,14 +418,16 @@ __device__ __forceinline__ void spf_lds_unit(
       const uint32_t* h = reinterpret_cast<const uint32_t*>(hdr);
       C = h[0];
       // weight min / max of the up edges, from the prep blocks' partials
-      uint32_t lo = 0xFFFFFFFFu, hi = 0u;
+      uint32_t lo = 0xFFFFFFFFu, hi = 0u, asym = 0u;
       for (uint32_t b = 0; b < nEB; ++b) {
-        const uint2 x = mm[size_t(unit.topo) * nEB + b];
+        const uint4 x = mm[size_t(unit.topo) * nEB + b];
         lo = min(lo, x.x);
         hi = max(hi, x.y);
+        asym |= x.z;
       }
       uniform = lo == hi ? 1u : 0u;  // every up edge of this weight
       w0 = lo;
+      wg.sym = asym ? 0u : 1u;
       const uint32_t nb = g.node_base[unit.topo];
       N = g.node_base[unit.topo + 1] - nb;
       e0 = g.row_ptr[nb];
@@ -403,13 +443,17 @@ __device__ __forceinline__ void spf_lds_unit(
     };
     const uint32_t s = unit.src;
     const uint32_t sb = row[s], se = row[s + 1];
+    const uint32_t sym = wg.sym;
+    // BFS layers (one constant weight > 0) keep no round stamps: stamp[v]
+    // holds v's hard-drained bit instead (the node pass and the pull read it)
+    const bool bfs = constW && wc > 0u;
     for (uint32_t v = tid; v < N; v += B) {
       dist[v] = (v == s) ? 0u : kInf;
-      stamp[v] = 0;
+      stamp[v] = bfs && row[v + 1] > row[v] && (cnode[first[v]] & kDrained16) ? 1 : 0;
 #pragma unroll
       for (int w = 0; w < W; ++w) nh[v * W + w] = 0u;
     }
-    if (tid < 2u) qCount[tid] = 0u;
+    if (tid < 6u) qCount[tid] = 0u;
     __syncthreads();
     // round 1: the source's row (slot j = j-th edge of the row; the source
     // relaxes even when drained, LinkState.cpp:741-752)
@@ -425,7 +469,7 @@ __device__ __forceinline__ void spf_lds_unit(
       const uint32_t t = x & kNodeMax;
       if (weight(sb + j) != dist[t]) continue;
       atomicOr(&nh[t * W + (j >> 5)], 1u << (j & 31u));
-      stamp[t] = 2;
+      if (!bfs) stamp[t] = 2;
     }
     __syncthreads();
     // rounds 2.., specialised on whether the weight is one constant (no
@@ -465,92 +509,125 @@ __device__ __forceinline__ void spf_lds_unit(
         }
       };
       for (uint32_t r = 2;; ++r) {
-        // round stamps of the general-weight rounds (1..255, 0 = not pending)
-        const uint32_t stCur = stamp_of(r), stPrev = stamp_of(r - 1u), stNext = stamp_of(r + 1u);
-        // (0) the queue of round r: four chunk slots per thread per step, the
-        // workgroup stepping together (every lane takes part in the ballots)
-        uint32_t* qc = &qCount[r & 1u];
-        // BFS layers: is any node still unreached? If none is, layer r is
-        // empty -- round r's pushes from layer r - 1 can neither reach a node
-        // nor be tight (a target at distance r * wc would be in layer r) --
-        // and the fixpoint is reached without the push pass
-        bool unreached = false;
-        if constexpr (kBfs) {
-          for (uint32_t v = tid; v < N; v += B) unreached |= dist[v] == kInf;
-        }
-        for (uint32_t c0 = 0; c0 < C; c0 += 4u * B) {
-          uint32_t cs[4], vs[4];
-          bool act[4];
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            cs[k] = c0 + uint32_t(k) * B + tid;
-            vs[k] = cs[k] < C ? cnode[cs[k]] : kDrained16;
-          }
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            if constexpr (kBfs) {  // layer r - 1
-              act[k] = !(vs[k] & kDrained16) &&
-                  uint64_t(dist[vs[k] & kNodeMax]) == uint64_t(r - 1u) * wc;
-            } else {
-              // exact u8 stamps: st(r) cycles through 1..255 and a node
-              // still carrying last round's value (pushed then, unchanged
-              // since) is cleared here, so every live stamp is st(r) or 0
-              // -- a stale stamp never matches again after 255 rounds (it
-              // would re-queue settled nodes every round: no fixpoint exit
-              // on paths of 256+ hops), and unreached nodes are never queued
-              const uint32_t v = vs[k] & kNodeMax;
-              const uint32_t sv = stamp[v];
-              if (sv == stPrev) stamp[v] = 0;
-              act[k] = !(vs[k] & kDrained16) && sv == stCur;
-            }
-          }
-          uint64_t m[4];
-          uint32_t tot = 0;
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            m[k] = __ballot(act[k]);
-            tot += uint32_t(__popcll(m[k]));
-          }
-          if (tot == 0u) continue;  // wave-uniform
-          uint32_t at = 0;
-          if (lane == 0u) at = atomicAdd(qc, tot);
-          at = __shfl(at, 0, 64);
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const uint32_t lo = static_cast<uint32_t>(m[k]), hi = static_cast<uint32_t>(m[k] >> 32);
-            const uint32_t before = __builtin_amdgcn_mbcnt_hi(hi, __builtin_amdgcn_mbcnt_lo(lo, 0u));
-            if (act[k]) queue[at + before] = uint16_t(cs[k]);
-            at += uint32_t(__popcll(m[k]));
-          }
-        }
-        if constexpr (kBfs) {
-          unreached = __syncthreads_or(unreached);
-        } else {
-          __syncthreads();
-        }
-        mark(8u + 3u * (r - 2u));
-        const uint32_t nq = *qc;
-        if (nq == 0u) break;  // nothing stamped r: the fixpoint
-        if constexpr (kBfs) {
-          if (!unreached && !(flags & kFlagLdsNoBfsExit)) break;
-        }
-        dg.queued(nq);
-        if (tid == 0u) qCount[(r + 1u) & 1u] = 0u;  // next round's counter
         // the queue is walked transposed: lane l of a wave takes entries
         // l * M + j (M = ceil(nq / 64)), so the lanes of one instruction
         // hold chunks of nodes far apart in the queue (other pods / planes)
         // instead of neighbours pushing into the same targets -- same-address
         // LDS atomics within one instruction serialise
-        const uint32_t M = (nq + 63u) >> 6;
-        auto entry = [&](uint32_t i) { return (i & 63u) * M + (i >> 6); };
+        uint32_t* qc = &qCount[r & 1u];
         if constexpr (kBfs) {
-          // one constant weight wc > 0: the rounds are BFS layers. The nodes
-          // queued in round r are layer r - 1, final with complete next hops;
-          // a target is either unreached (dt = kInf: it joins layer r, every
-          // lane that finds it so stores the same distance) or already at
-          // cand (layer r, tight) or nearer (not tight). One pass: distances
-          // by plain stores, next hops by fire-and-forget atomicOr; layer
-          // membership is the distance itself (no stamps).
+          // one constant weight wc > 0: the rounds are BFS layers; layer
+          // r - 1 (distance (r - 1) wc) is final with complete next hops.
+          // (0) the queue of the frontier's chunk records (four per thread
+          // per step, the workgroup stepping together: every lane takes part
+          // in the ballots), whether any node is still unreached, and how
+          // many chunk records the unreached nodes own (the pull's work; the
+          // push's is the queue)
+          const uint64_t lay = uint64_t(r - 1u) * wc;
+          uint32_t* cost = &qCount[2u + 2u * (r & 1u)];  // unreached chunk records
+          bool unreached = false;
+          for (uint32_t v = tid; v < N; v += B) unreached |= dist[v] == kInf;
+          uint32_t unrCh = 0;  // wave-uniform
+          for (uint32_t c0 = 0; c0 < C; c0 += 4u * B) {
+            uint32_t cs[4], vs[4], dk[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              cs[k] = c0 + uint32_t(k) * B + tid;
+              vs[k] = cs[k] < C ? cnode[cs[k]] : kDrained16;
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) dk[k] = cs[k] < C ? dist[vs[k] & kNodeMax] : 0u;
+            uint64_t m[4];
+            uint32_t tot = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              unrCh += uint32_t(__popcll(__ballot(dk[k] == kInf)));
+              m[k] = __ballot(!(vs[k] & kDrained16) && uint64_t(dk[k]) == lay);
+              tot += uint32_t(__popcll(m[k]));
+            }
+            if (tot == 0u) continue;  // wave-uniform
+            uint32_t at = 0;
+            if (lane == 0u) at = atomicAdd(qc, tot);
+            at = __shfl(at, 0, 64);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              const uint32_t lo = static_cast<uint32_t>(m[k]), hi = static_cast<uint32_t>(m[k] >> 32);
+              const uint32_t before = __builtin_amdgcn_mbcnt_hi(hi, __builtin_amdgcn_mbcnt_lo(lo, 0u));
+              if ((m[k] >> lane) & 1u) queue[at + before] = uint16_t(cs[k]);
+              at += uint32_t(__popcll(m[k]));
+            }
+          }
+          if (lane == 0u && unrCh) atomicAdd(cost, unrCh);
+          unreached = __syncthreads_or(unreached);
+          mark(8u + 3u * (r - 2u));
+          const uint32_t nq = *qc;
+          const uint32_t pullT = *cost;
+          // no frontier: the fixpoint; nothing unreached: layer r is empty
+          // -- round r's pushes can neither reach a node nor be tight
+          if (nq == 0u) break;
+          if (!unreached && !(flags & kFlagLdsNoBfsExit)) break;
+          dg.queued(nq);
+          if (tid == 0u) {  // next round's counters
+            const uint32_t o = (r + 1u) & 1u;
+            qCount[o] = 0u;
+            qCount[2u + 2u * o] = 0u;
+          }
+          const uint32_t ratio = (flags >> kFlagLdsPullShift) & 0xFu;
+          if (sym && ratio && 4u * uint64_t(pullT) <= uint64_t(ratio) * nq) {
+            // pull (direction-optimising BFS): fewer chunk records (edges / 8)
+            // of unreached nodes than of the frontier. Each unreached node
+            // scans its own row -- with every edge's reverse present and of
+            // the same up / down state (sym, checked by the prep) and one
+            // weight, v -> u up means u -> v relaxes -- and ORs the next hops
+            // of its neighbours in layer r - 1 that are not drained (the
+            // source is layer 0, never such a neighbour): no LDS atomics,
+            // one store per reached node
+            const uint32_t cand = uint32_t(lay) + wc;
+            for (uint32_t v = tid; v < N; v += B) {
+              if (dist[v] != kInf) continue;
+              const uint32_t b = row[v], e = row[v + 1];
+              uint32_t acc[W];
+#pragma unroll
+              for (int w = 0; w < W; ++w) acc[w] = 0u;
+              bool found = false;
+              for (uint32_t j0 = b; j0 < e; j0 += kLdsChunk) {
+                uint32_t x[kLdsChunk], du[kLdsChunk], dr[kLdsChunk];
+#pragma unroll
+                for (uint32_t i = 0; i < kLdsChunk; ++i) {
+                  x[i] = j0 + i < e ? eimg[j0 + i] : kDown16;
+                }
+#pragma unroll
+                for (uint32_t i = 0; i < kLdsChunk; ++i) {
+                  du[i] = dist[x[i] & kNodeMax];
+                  dr[i] = stamp[x[i] & kNodeMax];
+                }
+#pragma unroll
+                for (uint32_t i = 0; i < kLdsChunk; ++i) {
+                  if ((x[i] & kDown16) || dr[i] || uint64_t(du[i]) != lay) continue;
+                  found = true;
+#pragma unroll
+                  for (int w = 0; w < W; ++w) acc[w] |= nh[(x[i] & kNodeMax) * W + w];
+                }
+              }
+              if (found) {
+                dist[v] = cand;
+#pragma unroll
+                for (int w = 0; w < W; ++w) nh[v * W + w] = acc[w];
+              }
+            }
+            __syncthreads();
+            mark(8u + 3u * (r - 2u) + 2u);
+            dg.rounds(r);
+            continue;
+          }
+          // push: the nodes queued are layer r - 1; a target is either
+          // unreached (dt = kInf: it joins layer r, every lane that finds it
+          // so stores the same distance) or already at cand (layer r, tight)
+          // or nearer (not tight). One pass: distances by plain stores, next
+          // hops by fire-and-forget atomicOr; layer membership is the
+          // distance itself
+          const uint32_t M = (nq + 63u) >> 6;
+          auto entry = [&](uint32_t i) { return (i & 63u) * M + (i >> 6); };
           for (uint32_t i = tid; i < 64u * M; i += B) {
             const uint32_t q = entry(i);
             if (q >= nq) continue;
@@ -575,6 +652,58 @@ __device__ __forceinline__ void spf_lds_unit(
           dg.rounds(r);
           continue;
         }
+        // general weights. Round stamps: 1..255, 0 = not pending
+        const uint32_t stCur = stamp_of(r), stPrev = stamp_of(r - 1u), stNext = stamp_of(r + 1u);
+        // (0) the queue of round r: four chunk slots per thread per step, the
+        // workgroup stepping together (every lane takes part in the ballots)
+        for (uint32_t c0 = 0; c0 < C; c0 += 4u * B) {
+          uint32_t cs[4], vs[4];
+          bool act[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            cs[k] = c0 + uint32_t(k) * B + tid;
+            vs[k] = cs[k] < C ? cnode[cs[k]] : kDrained16;
+          }
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            // exact u8 stamps: st(r) cycles through 1..255 and a node still
+            // carrying last round's value (pushed then, unchanged since) is
+            // cleared here, so every live stamp is st(r) or 0 -- a stale
+            // stamp never matches again after 255 rounds (it would re-queue
+            // settled nodes every round: no fixpoint exit on paths of 256+
+            // hops), and unreached nodes are never queued
+            const uint32_t v = vs[k] & kNodeMax;
+            const uint32_t sv = stamp[v];
+            if (sv == stPrev) stamp[v] = 0;
+            act[k] = !(vs[k] & kDrained16) && sv == stCur;
+          }
+          uint64_t m[4];
+          uint32_t tot = 0;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            m[k] = __ballot(act[k]);
+            tot += uint32_t(__popcll(m[k]));
+          }
+          if (tot == 0u) continue;  // wave-uniform
+          uint32_t at = 0;
+          if (lane == 0u) at = atomicAdd(qc, tot);
+          at = __shfl(at, 0, 64);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const uint32_t lo = static_cast<uint32_t>(m[k]), hi = static_cast<uint32_t>(m[k] >> 32);
+            const uint32_t before = __builtin_amdgcn_mbcnt_hi(hi, __builtin_amdgcn_mbcnt_lo(lo, 0u));
+            if (act[k]) queue[at + before] = uint16_t(cs[k]);
+            at += uint32_t(__popcll(m[k]));
+          }
+        }
+        __syncthreads();
+        mark(8u + 3u * (r - 2u));
+        const uint32_t nq = *qc;
+        if (nq == 0u) break;  // nothing stamped r: the fixpoint
+        dg.queued(nq);
+        if (tid == 0u) qCount[(r + 1u) & 1u] = 0u;  // next round's counter
+        const uint32_t M = (nq + 63u) >> 6;
+        auto entry = [&](uint32_t i) { return (i & 63u) * M + (i >> 6); };
         // (1) distances. A push with cand < dt (dt read during this pass;
         // distances only fall) lowers its target whatever else lands there,
         // so it restarts the target's next hops without the atomic's return
@@ -658,11 +787,11 @@ __device__ __forceinline__ void spf_lds_unit(
 
 template <int W>
 __global__ __launch_bounds__(kLdsBlock) void spf_lds_kernel(
-    ogs_graph g, LdsImage L, const uint8_t* __restrict__ img, const uint2* __restrict__ mm,
+    ogs_graph g, LdsImage L, const uint8_t* __restrict__ img, const uint4* __restrict__ mm,
     uint32_t nEB, const ogs_unit* __restrict__ units, int nUnits, uint32_t flags,
     uint32_t* __restrict__ oDist, uint32_t* __restrict__ oNh) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  __shared__ uint32_t qCount[2];
+  __shared__ uint32_t qCount[6];
   LdsWg wg;
 #ifdef OGS_STAMPS
   LdsStamps dg(W);
@@ -796,11 +925,11 @@ struct LdsSchedule {
 template <typename KeyT>
 __global__ __launch_bounds__(kLdsBlock) void spf_lds_route_kernel(
     ogs_graph g, ogs_prefix_table pt, const KeyT* __restrict__ key, LdsImage L,
-    const uint8_t* __restrict__ img, const uint2* __restrict__ mm, uint32_t nEB,
+    const uint8_t* __restrict__ img, const uint4* __restrict__ mm, uint32_t nEB,
     LdsGroups grps, uint32_t flags, uint32_t* __restrict__ ctr, uint32_t* __restrict__ ready,
     LdsSchedule sch) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  __shared__ uint32_t qCount[2];
+  __shared__ uint32_t qCount[6];
   __shared__ uint32_t item;
   const uint32_t tid = threadIdx.x;
   const LdsGroup& last = grps.g[grps.n - 1u];
@@ -954,13 +1083,14 @@ hipError_t launch_lds_prep(const ogs_graph& g, const ogs_prefix_table* pt, void*
   const ogs_prefix_table ptv = pt ? *pt : ogs_prefix_table{};
   hipLaunchKernelGGL(lds_prep_kernel, dim3(T * (1u + S.nEB + nKB)), dim3(kLdsBlock), 0, stream,
                      g, ptv, nKB ? key : nullptr, key16 ? 1u : 0u, nKB, L, base,
-                     reinterpret_cast<uint2*>(base + S.mm), S.nEB,
+                     reinterpret_cast<uint4*>(base + S.mm), S.nEB,
                      reinterpret_cast<uint32_t*>(base + S.ctr),
                      reinterpret_cast<uint32_t*>(base + S.ready), uint32_t(nUnits));
   return hipGetLastError();
 }
 
 extern int g_ldsBfsExit;
+extern int g_ldsPull;
 
 template <typename K>
 static hipError_t allow_lds(K k, uint32_t lds) {
@@ -978,10 +1108,11 @@ hipError_t launch_spf_lds(const ogs_graph& g, const ogs_unit* units, int nUnits,
   const LdsImage L = lds_image(g, W);
   const LdsScratch S = lds_scratch(g, L, nUnits);
   const uint8_t* img = static_cast<const uint8_t*>(scratch);
-  const uint2* mm = reinterpret_cast<const uint2*>(img + S.mm);
+  const uint4* mm = reinterpret_cast<const uint4*>(img + S.mm);
   const uint32_t lds = L.block + L.state;
   const int grid = std::max(1, std::min(nUnits, num_cus()));
   if (!g_ldsBfsExit) flags |= kFlagLdsNoBfsExit;
+  flags |= uint32_t(g_ldsPull & 0xF) << kFlagLdsPullShift;
   auto go = [&](auto k) {
     hipError_t a = allow_lds(k, lds);
     if (a != hipSuccess) return a;
@@ -1010,10 +1141,15 @@ int g_ldsTail = 1;
 // default) or run the empty last layer (0, A/B): C3 N = 8 shard 0.1695 vs
 // 0.1732 ms (profiles/r05_c3_ab_bfs_exit.log)
 int g_ldsBfsExit = 1;
-// "lds_lead": narrow units streamed before the wide group (-1 auto: one
-// grid's worth of stream items on sharded builds, 0 none); "lds_tail_parts":
-// ranges per unit of the launch's last units (0 auto)
-int g_ldsLead = -1;
+// "lds_pull": BFS rounds pull when 4 x (chunk records of the unreached
+// nodes) <= lds_pull x (the frontier's); 0 always push (A/B)
+int g_ldsPull = 6;
+// "lds_lead": narrow units streamed before the wide group (0, default:
+// none; -1 one grid's worth of stream items on sharded builds; measured at
+// the N = 8 shard 0.1752 vs 0.1711 ms without, N = 4 0.3031 vs 0.3074 with
+// the tail change alone: profiles/r05_c3_lead_tail_ab_n*.log);
+// "lds_tail_parts": ranges per unit of the launch's last units (0 auto)
+int g_ldsLead = 0;
 int g_ldsTailParts = 0;
 
 bool lds_key16(const ogs_graph& g) {
@@ -1043,7 +1179,7 @@ hipError_t launch_spf_lds_routes(const ogs_graph& g, const ogs_prefix_table& pt,
   const LdsImage L = lds_image(g, Wmax);
   const LdsScratch S = lds_scratch(g, L, U);
   uint8_t* base = static_cast<uint8_t*>(scratch);
-  const uint2* mm = reinterpret_cast<const uint2*>(base + S.mm);
+  const uint4* mm = reinterpret_cast<const uint4*>(base + S.mm);
   uint32_t* ctr = reinterpret_cast<uint32_t*>(base + S.ctr);
   uint32_t* ready = reinterpret_cast<uint32_t*>(base + S.ready);
   const uint32_t recs = uint32_t(g.max_nodes) * uint32_t(2 + Wmax) * 4u;
@@ -1072,9 +1208,9 @@ hipError_t launch_spf_lds_routes(const ogs_graph& g, const ogs_prefix_table& pt,
     }
     if (sch.P2 <= P) sch.U1 = uint32_t(U);
   }
-  // lead ("lds_lead", -1 auto): on sharded builds with several width groups,
-  // one grid's worth of stream items of narrow units before the wide group
-  // (whose SPFs finish last); needs Uw <= G (the slot map's SPFs are then
+  // lead ("lds_lead"; -1: on sharded builds with several width groups, one
+  // grid's worth of stream items of narrow units before the wide group,
+  // whose SPFs finish last); needs Uw <= G (the slot map's SPFs are then
   // always handed out before their stream items)
   const uint32_t Uw = n > 1 ? uint32_t(groups[0].n) : 0u;
   const uint32_t Gl = std::min(uint32_t(U), uint32_t(grid));
@@ -1086,6 +1222,7 @@ hipError_t launch_spf_lds_routes(const ogs_graph& g, const ogs_prefix_table& pt,
   }
   if (g_routeStoreNt & 1) flags |= kFlagNtStores;
   if (!g_ldsBfsExit) flags |= kFlagLdsNoBfsExit;
+  flags |= uint32_t(g_ldsPull & 0xF) << kFlagLdsPullShift;
   auto go = [&](auto k, auto keyp) {
     hipError_t a = allow_lds(k, lds);
     if (a != hipSuccess) return a;

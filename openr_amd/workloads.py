@@ -27,6 +27,21 @@ C3_OPTS = dict(pods=32, planes=8, sswPerPlane=36, rswPerPod=48, full=True,
                prefixesPerNode=100)
 
 
+# C3-ref: the reference benchmark's own fabric (RoutingBenchmarkUtils.cpp:
+# 298-473), including its quirk at :316-327 -- each SSW keeps only its link
+# to the pod-0 FSW of its plane, so pods 1..31 have no link to the spine
+# (each is an island of 8 FSWs + 48 RSWs): the parity case for unreachable
+# nodes at bench size (tests/test_gpu_bench_size.py)
+C3REF_OPTS = dict(pods=32, planes=8, sswPerPlane=36, rswPerPod=48, full=False,
+                  prefixesPerNode=100)
+
+
+def c3ref_sample_names():
+    """64 stratified C3-ref sources: every 33rd of the 2,080 names (SSWs,
+    pod-0 and island FSWs, pod-0 and island RSWs)."""
+    return c3_source_names()[::33][:64]
+
+
 def c3_source_names(pods=32, planes=8, ssw=36, rsw=48):
     """Node names of topogen::fabric: SSW "1-plane-i", FSW "2-pod-plane",
     RSW "3-pod-i"."""

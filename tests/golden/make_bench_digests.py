@@ -9,7 +9,7 @@ XOR over routes of a hash of the RibUnicastEntry fields) and
 openr_amd/shard.py (C4 change lists, C5 KSP2 path lines). Every value here
 comes from oracle/refcpu (test infrastructure), never from the engine.
 
-  python tests/golden/make_bench_digests.py [c1] [c2] [c3] [c4] [c5] [g1] [--threads T]
+  python tests/golden/make_bench_digests.py [c1] [c2] [c3] [c3ref] [c4] [c5] [g1] [--threads T]
 
 C3 takes long (2,080 oracle buildRouteDb over 208k prefixes each, ~1.5 h on
 8 cores): it is resumable, per-source digests accumulate in
@@ -31,10 +31,11 @@ from openr_amd import shard  # noqa: E402  (pure Python: digest helpers)
 from openr_amd.workloads import (C1_OPTS, C1_SOURCE, C2_OPTS, C2_SOURCE, C2_TOPOS, C3_OPTS, C4_OPTS,  # noqa: E402
                                  C4_SOURCE, C4_VARIANTS, C4_SEED, C4_DUAL_PERMILLE,
                                  C5_OPTS, C5_SOURCE, G1_OPTS, G1_SOURCES, c3_source_names,
-                                 c5_policy)
+                                 c5_policy, C3REF_OPTS, c3ref_sample_names)
 
 OUT = os.path.join(HERE, "bench_digests.json")
 C3_PART = os.path.join(HERE, "c3_source_digests.json")
+C3REF_PART = os.path.join(HERE, "c3ref_source_digests.json")
 
 
 def load(path):
@@ -86,6 +87,15 @@ def gen_c3(out, threads, chunk):
     out["c3"] = f"{shard.combine_digests(int(part[n], 16) for n in names):016x}"
 
 
+def gen_c3ref(out, threads):
+    """C3-ref (the reference's own benchmark fabric, full=False): the
+    oracle's per-source digests of 64 stratified sources."""
+    names = c3ref_sample_names()
+    ds = R.gen_route_digests("fabric", C3REF_OPTS, names, True, False, False, threads)
+    save(C3REF_PART, {n: f"{d:016x}" for n, d in zip(names, ds)})
+    out["c3ref_sample"] = f"{shard.combine_digests(ds):016x}"
+
+
 def gen_c4(out, threads):
     ch = R.variant_changes("wan", C4_OPTS, C4_SOURCE, C4_VARIANTS, C4_SEED, C4_DUAL_PERMILLE,
                            threads)
@@ -125,6 +135,8 @@ def main():
             gen_c2(out, a.threads)
         elif c == "c3":
             gen_c3(out, a.threads, a.chunk)
+        elif c == "c3ref":
+            gen_c3ref(out, a.threads)
         elif c == "c4":
             gen_c4(out, a.threads)
         elif c == "c5":

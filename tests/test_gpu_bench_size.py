@@ -79,7 +79,9 @@ def _c3(product, names, ppn=100):
                                   dict(route_stream=5, lds_lead=0, lds_bfs_exit=0),
                                   dict(route_stream=5, lds_parts=8, lds_grid=300),
                                   dict(route_stream=5, lds_lead=100, lds_tail_parts=16),
-                                  dict(route_stream=5, lds_tail_parts=3, lds_lead=7, lds_grid=64)])
+                                  dict(route_stream=5, lds_tail_parts=3, lds_lead=7, lds_grid=64),
+                                  dict(route_stream=5, lds_pull=0),
+                                  dict(route_stream=5, lds_pull=15, lds_lead=-1)])
 def test_c3_full_every_source_matches_oracle(product, opts):
     """C3-full at bench size (2,080 sources x 208k prefixes) through
     bench.py's two-stream width-group launches: every source's digest equals
@@ -99,8 +101,8 @@ def test_c3_full_every_source_matches_oracle(product, opts):
     import openr_amd.capi as capi
     lib = capi.load()
     defaults = dict(frontier_block=0, frontier_parts=0, frontier_parts_wide=0, route_stream=5,
-                    lds_parts=0, lds_grid=0, lds_key16=1, lds_tail=1, lds_lead=-1,
-                    lds_bfs_exit=1, lds_tail_parts=0)
+                    lds_parts=0, lds_grid=0, lds_key16=1, lds_tail=1, lds_lead=0,
+                    lds_bfs_exit=1, lds_tail_parts=0, lds_pull=6)
     for k, v in opts.items():
         capi.check(lib, lib.ogs_set_option(k.encode(), v), k)
     try:
@@ -278,3 +280,48 @@ def test_c1_exact_workload_canonical_text(product, oracle, sr):
                                 True, sr, False)
     assert got == want
     assert got[0] == got[1] == got[3] and got[0] != b"NONE"
+
+
+def test_c3ref_reference_fabric_at_bench_size(product, oracle):
+    """C3-ref: the reference benchmark's own fabric (RoutingBenchmarkUtils.cpp
+    :298-473 with the quirk at :316-327 -- every SSW keeps only its pod-0 FSW,
+    so pods 1..31 are islands cut off from the spine) at bench size (2,080
+    nodes, 208k prefixes), through bench.py's default one-launch form: 64
+    stratified sources' digests equal the oracle's golden per-source digests
+    (tests/golden/c3ref_source_digests.json), and 12 more mixing spine,
+    pod-0 and island sources equal a LIVE oracle run. Exercises the
+    persistent kernel's unreachable nodes (BFS layers that never reach the
+    islands, no all-reached exit) at the LDS form's size."""
+    from openr_amd.workloads import C3REF_OPTS, c3ref_sample_names
+    path = os.path.join(HERE, "golden", "c3ref_source_digests.json")
+    want = json.load(open(path))
+    names = c3ref_sample_names()
+    assert set(names) == set(want)
+    live = ["1-0-0", "1-6-30", "2-0-0", "2-0-7", "2-1-0", "2-17-4", "2-31-7", "3-0-0",
+            "3-0-47", "3-1-0", "3-20-20", "3-31-47"]
+    got = {}
+    for pick in (names, live):
+        launches = _c3_opts(product, pick, C3REF_OPTS)
+        for L in launches:
+            o = L["o"]
+            d = L["br"].records_digests([], o["meta"].cpu().numpy(), o["metric"].cpu().numpy(),
+                                        o["mask"].cpu().numpy(), L["W"], 16)
+            got.update(zip(L["names"], d))
+    bad = [n for n in names if _h(got[n]) != want[n]]
+    assert not bad, f"{len(bad)} sampled sources differ from the oracle, e.g. {bad[:8]}"
+    ref = oracle.gen_route_digests("fabric", C3REF_OPTS, live, True, False, False, 16)
+    assert [got[n] for n in live] == list(ref)
+
+
+def _c3_opts(product, names, opts):
+    import torch
+    import bench
+    import openr_amd.capi as capi
+    lib = capi.load()
+    dev = torch.device("cuda", 0)
+    launches, _ = bench.c3_launches(torch, product, capi, dev, names, opts=opts)
+    main = torch.cuda.current_stream(dev)
+    side = torch.cuda.Stream(dev)
+    bench.c3_launch_all(lib, capi, launches, main, side)
+    torch.cuda.synchronize(dev)
+    return launches

@@ -27,7 +27,7 @@ def _arrays(product, names):
     return br.host_arrays()
 
 
-@pytest.mark.parametrize("route_stream,lead", [(5, -1), (5, 3), (2, -1)])
+@pytest.mark.parametrize("route_stream,lead", [(5, 0), (5, -1), (5, 3), (2, 0)])
 def test_groups_match_per_group_calls(product, route_stream, lead):
     import torch
 

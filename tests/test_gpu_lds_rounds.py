@@ -76,6 +76,7 @@ def _oracle(oracle, uniform=False):
 @pytest.mark.parametrize("options", [dict(route_stream=5), dict(route_stream=4),
                                      dict(route_stream=5, lds_bfs_exit=0, lds_tail_parts=9),
                                      dict(route_stream=5, lds_parts=3, lds_lead=2),
+                                     dict(route_stream=5, lds_pull=0), dict(route_stream=5, lds_pull=15),
                                      dict(route_stream=2, spf_queue=0),
                                      dict(route_stream=1, spf_queue=0)])
 def test_deep_line_with_island_batch(product, oracle, options, uniform):
@@ -101,8 +102,9 @@ def test_deep_line_with_island_batch(product, oracle, options, uniform):
         lib.ogs_set_option(b"route_stream", 5)
         lib.ogs_set_option(b"spf_queue", -1)
         lib.ogs_set_option(b"lds_bfs_exit", 1)
-        lib.ogs_set_option(b"lds_lead", -1)
+        lib.ogs_set_option(b"lds_lead", 0)
         lib.ogs_set_option(b"lds_tail_parts", 0)
+        lib.ogs_set_option(b"lds_pull", 6)
     want = _oracle(oracle, uniform)
     # the island's anycast member is unreachable from the line: the line's
     # end must be the prefix's only route source
@@ -118,3 +120,28 @@ def test_deep_line_with_island_single_builds(product, oracle):
         db = product.SpfSolver(s, True, False).buildRouteDb(s, als, ps)
         got.append(b"NONE" if db is None else db.canonical())
     _cmp(got, _oracle(oracle), "deep line single")
+
+
+@pytest.mark.parametrize("pull", [0, 4, 15])
+@pytest.mark.parametrize("kind", ["fabric", "fabric3"])
+def test_bfs_pull_rounds(product, oracle, pull, kind):
+    """Unit-weight (BFS) rounds of the LDS form pull a layer when the
+    unreached nodes' edges are few against the frontier's (lds_pull; 0 push
+    only): fabrics with hard-drained nodes (never relay), overloaded
+    adjacencies (down links) and the prefix mix, one- and three-word sources,
+    vs the oracle. Reference: LinkState.cpp:720-820 (a drained node settles
+    but does not relax its links; down links are not used)."""
+    from test_gpu_parity import MIX, _batch_dbs
+    if kind == "fabric":
+        opts = dict(pods=8, planes=4, sswPerPlane=16, rswPerPod=32, full=True,
+                    prefixesPerNode=2, nodeOverloadPermille=30, adjOverloadPermille=20, **MIX)
+        names = ([f"1-{p}-{s}" for p in range(4) for s in range(16)] +
+                 [f"2-{p}-{f}" for p in range(8) for f in range(4)] +
+                 [f"3-{p}-{r}" for p in range(8) for r in range(32)])
+        srcs = names[::3]
+    else:
+        opts = dict(pods=4, planes=2, sswPerPlane=36, rswPerPod=48, full=True,
+                    prefixesPerNode=2, nodeOverloadPermille=30, adjOverloadPermille=20, **MIX)
+        srcs = [f"2-{p}-{f}" for p in range(4) for f in range(2)]
+    a = _batch_dbs(product, "fabric", opts, srcs, True, True, route_stream=5, lds_pull=pull)
+    _cmp(a, oracle.gen_route_dbs("fabric", opts, srcs, True, False, True), f"pull {pull} {kind}")

@@ -27,7 +27,8 @@ DEFAULTS = {"frontier_block": 0, "frontier_parts": 0, "route_stream": 5,
             "spf_packed_scan": 1, "spf_seed_row": 1, "frontier_parts_wide": 0,
             "route_store_nt": 2, "spf_lane_walk": -1, "spf_preload": 1,
             "lds_parts": 0, "lds_grid": 0, "lds_key16": 1, "lds_tail": 1,
-            "lds_bfs_exit": 1, "lds_lead": -1, "lds_tail_parts": 0}
+            "lds_bfs_exit": 1, "lds_lead": 0, "lds_tail_parts": 0,
+            "lds_pull": 6}
 
 
 def main():
