@@ -464,13 +464,13 @@ class PrefixEntryList {
       n_ = 1;
       return {&one_, true};
     }
+    const size_t at = size_t(it - begin());  // before the storage moves
     if (!heap_) {  // the second advertisement: both to the vector
       many_.reserve(4);
       many_.push_back(std::move(one_));
       one_ = value_type();
       heap_ = true;
     }
-    const size_t at = size_t(it - many_.data());
     many_.insert(many_.begin() + at, value_type(k, nullptr));
     ++n_;
     return {many_.data() + at, true};

@@ -116,3 +116,32 @@ def test_slot_edge_image_matches_csr(n):
                 assert bool(x & 0x400) == bool(lo & (1 << 21))
                 assert (x >> 11) & 7 == (lo >> 22) & 0x1FF
                 assert x >> 16 == w
+
+
+def test_prefix_state_many_advertisers_vs_oracle(host_module, oracle):
+    """PrefixState (PrefixState.cpp:15-57) keeps each prefix's entries sorted
+    by (node, area) -- one advertisement inline, more in a vector: random
+    update / re-advertise / delete sequences with up to 6 advertisers per
+    prefix over 2 areas, the product's change sets and final table equal the
+    oracle's after every step (host only)."""
+    import random
+    import lsdb as L
+    rng = random.Random(5)
+    ps, ops = host_module.PrefixState(), oracle.PrefixState()
+    nodes, areas = [f"n{i}" for i in range(6)], ["a", "b"]
+    prefixes = [f"fc00::{i:x}/128" for i in range(5)] + ["10.0.0.0/8"]
+    for step in range(600):
+        node, area, pfx = rng.choice(nodes), rng.choice(areas), rng.choice(prefixes)
+        if rng.random() < 0.3:
+            got = ps.deletePrefix(node, area, pfx)
+            want = ops.deletePrefix(node, area, pfx)
+        else:
+            e = L.createPrefixEntry(pfx)
+            e["metrics"]["path_preference"] = rng.choice([100, 200])
+            got = ps.updatePrefix(node, area, e)
+            want = ops.updatePrefix(node, area, e)
+        assert set(got) == set(want), step
+        a, b = ps.prefixes(), ops.prefixes()
+        assert set(a) == set(b), step
+        for p in a:
+            assert list(a[p]) == list(b[p]), (step, p)
