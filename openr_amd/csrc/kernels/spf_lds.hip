@@ -525,8 +525,13 @@ __device__ __forceinline__ void spf_lds_unit(
           // push's is the queue)
           const uint64_t lay = uint64_t(r - 1u) * wc;
           uint32_t* cost = &qCount[2u + 2u * (r & 1u)];  // unreached chunk records
+          // "any node unreached": on symmetric graphs every node with an
+          // in-edge owns a chunk record, so the chunk count below decides it
+          // (no separate node scan, a plain barrier); otherwise scan the nodes
           bool unreached = false;
-          for (uint32_t v = tid; v < N; v += B) unreached |= dist[v] == kInf;
+          if (!sym) {
+            for (uint32_t v = tid; v < N; v += B) unreached |= dist[v] == kInf;
+          }
           uint32_t unrCh = 0;  // wave-uniform
           for (uint32_t c0 = 0; c0 < C; c0 += 4u * B) {
             uint32_t cs[4], vs[4], dk[4];
@@ -558,10 +563,15 @@ __device__ __forceinline__ void spf_lds_unit(
             }
           }
           if (lane == 0u && unrCh) atomicAdd(cost, unrCh);
-          unreached = __syncthreads_or(unreached);
+          if (sym) {
+            __syncthreads();
+          } else {
+            unreached = __syncthreads_or(unreached);
+          }
           mark(8u + 3u * (r - 2u));
           const uint32_t nq = *qc;
           const uint32_t pullT = *cost;
+          if (sym) unreached = pullT != 0u;
           // no frontier: the fixpoint; nothing unreached: layer r is empty
           // -- round r's pushes can neither reach a node nor be tight
           if (nq == 0u) break;
@@ -583,36 +593,78 @@ __device__ __forceinline__ void spf_lds_unit(
             // source is layer 0, never such a neighbour): no LDS atomics,
             // one store per reached node
             const uint32_t cand = uint32_t(lay) + wc;
+            // one chunk (<= 8 edges) of an unreached node: OR the next hops
+            // of its tight, not drained neighbours into acc
+            auto pullChunk = [&](uint32_t j0, uint32_t e, uint32_t (&acc)[W]) {
+              uint32_t x[kLdsChunk], du[kLdsChunk], dr[kLdsChunk];
+#pragma unroll
+              for (uint32_t i = 0; i < kLdsChunk; ++i) x[i] = j0 + i < e ? eimg[j0 + i] : kDown16;
+#pragma unroll
+              for (uint32_t i = 0; i < kLdsChunk; ++i) {
+                du[i] = dist[x[i] & kNodeMax];
+                dr[i] = stamp[x[i] & kNodeMax];
+              }
+              // branch-free: every neighbour's words are read (padding lanes
+              // read node 0) and masked, so the 8 x W reads issue together
+              bool found = false;
+              uint32_t nb[kLdsChunk][W];
+#pragma unroll
+              for (uint32_t i = 0; i < kLdsChunk; ++i) {
+#pragma unroll
+                for (int w = 0; w < W; ++w) nb[i][w] = nh[(x[i] & kNodeMax) * W + w];
+              }
+#pragma unroll
+              for (uint32_t i = 0; i < kLdsChunk; ++i) {
+                const bool t = !(x[i] & kDown16) && !dr[i] && uint64_t(du[i]) == lay;
+                found |= t;
+#pragma unroll
+                for (int w = 0; w < W; ++w) acc[w] |= t ? nb[i][w] : 0u;
+              }
+              return found;
+            };
+            // (a) per unreached node its first chunk; further chunks of
+            // long rows go to a list (the queue array: the frontier queue is
+            // not used by a pull) for (b), one thread per chunk. Writes here
+            // only touch nodes unreached at the pass start (distance kInf),
+            // which no read in this pass can take for layer r - 1
+            uint32_t* oc = &qCount[3u + 2u * (r & 1u)];  // the list's count
+            if (tid == 0u) *oc = 0u;
+            __syncthreads();
             for (uint32_t v = tid; v < N; v += B) {
               if (dist[v] != kInf) continue;
               const uint32_t b = row[v], e = row[v + 1];
               uint32_t acc[W];
 #pragma unroll
               for (int w = 0; w < W; ++w) acc[w] = 0u;
-              bool found = false;
-              for (uint32_t j0 = b; j0 < e; j0 += kLdsChunk) {
-                uint32_t x[kLdsChunk], du[kLdsChunk], dr[kLdsChunk];
-#pragma unroll
-                for (uint32_t i = 0; i < kLdsChunk; ++i) {
-                  x[i] = j0 + i < e ? eimg[j0 + i] : kDown16;
-                }
-#pragma unroll
-                for (uint32_t i = 0; i < kLdsChunk; ++i) {
-                  du[i] = dist[x[i] & kNodeMax];
-                  dr[i] = stamp[x[i] & kNodeMax];
-                }
-#pragma unroll
-                for (uint32_t i = 0; i < kLdsChunk; ++i) {
-                  if ((x[i] & kDown16) || dr[i] || uint64_t(du[i]) != lay) continue;
-                  found = true;
-#pragma unroll
-                  for (int w = 0; w < W; ++w) acc[w] |= nh[(x[i] & kNodeMax) * W + w];
-                }
+              const bool found = b < e && pullChunk(b, min(e, b + kLdsChunk), acc);
+              if (e > b + kLdsChunk) {
+                const uint32_t f = first[v], n = (e - b + kLdsChunk - 1u) / kLdsChunk;
+                const uint32_t at = atomicAdd(oc, n - 1u);
+                for (uint32_t k = 1; k < n; ++k) queue[at + k - 1u] = uint16_t(f + k);
               }
               if (found) {
                 dist[v] = cand;
 #pragma unroll
                 for (int w = 0; w < W; ++w) nh[v * W + w] = acc[w];
+              }
+            }
+            __syncthreads();
+            // (b) the listed chunks: distance by plain stores (every finder
+            // stores the same), next hops by atomicOr
+            const uint32_t no = *oc;
+            for (uint32_t i = tid; i < no; i += B) {
+              const uint32_t c = queue[i];
+              const uint32_t v = cnode[c] & kNodeMax;
+              const uint32_t b = row[v] + kLdsChunk * (c - first[v]);
+              uint32_t acc[W];
+#pragma unroll
+              for (int w = 0; w < W; ++w) acc[w] = 0u;
+              if (pullChunk(b, min(row[v + 1], b + kLdsChunk), acc)) {
+                dist[v] = cand;
+#pragma unroll
+                for (int w = 0; w < W; ++w) {
+                  if (acc[w]) atomicOr(&nh[v * W + w], acc[w]);
+                }
               }
             }
             __syncthreads();
