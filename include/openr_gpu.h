@@ -51,8 +51,9 @@ extern "C" {
  * ogs_area_table.reached, ogs_routes_from_spf(spf_reached), u16 RibPolicy
  * statement ids, ogs_graph.rslot_ext (rows of 511+ edges). 4:
  * ogs_spf_routes_variants writes ogs_route_diff.base_desc_valid back. 5:
- * ogs_spf_routes_groups / ogs_route_group. */
-#define OGS_ABI_VERSION 5
+ * ogs_spf_routes_groups / ogs_route_group. 6: execution contexts
+ * (ogs_ctx_create / ogs_ctx_set_option / ogs_ctx_* compute calls). */
+#define OGS_ABI_VERSION 6
 
 /* ---- status codes ------------------------------------------------------ */
 #define OGS_OK 0
@@ -276,7 +277,8 @@ int ogs_stream_sync(void* stream);
 int ogs_host_alloc(void** hptr, size_t bytes);
 int ogs_host_free(void* hptr);
 
-/* Tuning knobs (process-wide; for A/B measurement):
+/* Tuning knobs of the DEFAULT context (the one the plain entry points use;
+ * ogs_ctx_set_option sets a context's own copy; for A/B measurement):
  *   "unit_width": small-topology kernel choice: -1 automatic (default),
  *                 0 generic kernel only, 1 packed wave-per-unit kernel,
  *                 2 split-state kernel at its automatic unit width,
@@ -614,6 +616,56 @@ int ogs_routes_multiarea(const ogs_graph* graph,
                          const void* spf_dist, const uint32_t* spf_nh,
                          uint32_t flags, int32_t nh_words, ogs_spf_out* out,
                          void* stream);
+
+/* ---- execution contexts (ABI 6) ----------------------------------------- *
+ * A context holds a device, its own copy of the tuning knobs (initialised
+ * from the default context's at creation) and its own launch scratch (the
+ * grow-only device workspace of the large-topology paths). The ogs_ctx_*
+ * calls below take the same arguments as the plain entry points and run
+ * them on the context's device with its knobs and scratch, so host threads
+ * that each use their own context (and their own streams) never share
+ * scratch or settings. A context is thread-compatible, not thread-safe: one
+ * host thread at a time ("explicit stream/device handle;
+ * thread-compatible, one context per host thread"). The plain entry points
+ * keep using the process default context (scratch per (device, stream);
+ * concurrent calls on ONE stream from several threads share it, so give
+ * each thread its own context). Reference call sites: Decision's one
+ * SpfSolver per Decision thread (Decision.cpp:912-913). */
+typedef struct ogs_ctx ogs_ctx;
+int ogs_ctx_create(int32_t device, ogs_ctx** out);
+int ogs_ctx_destroy(ogs_ctx* ctx); /* waits for the device, frees the scratch */
+int ogs_ctx_set_option(ogs_ctx* ctx, const char* name, int64_t value);
+int ogs_ctx_spf_routes(ogs_ctx* ctx, const ogs_graph* graph, const ogs_prefix_table* prefixes,
+                       const ogs_unit* units, int32_t n_units, uint32_t flags,
+                       int32_t nh_words, ogs_spf_out* out, void* stream);
+int ogs_ctx_spf_routes_groups(ogs_ctx* ctx, const ogs_graph* graph,
+                              const ogs_prefix_table* prefixes, const ogs_route_group* groups,
+                              int32_t n_groups, uint32_t flags, void* stream);
+int ogs_ctx_routes_from_spf(ogs_ctx* ctx, const ogs_graph* graph,
+                            const ogs_prefix_table* prefixes, const ogs_unit* units,
+                            int32_t n_units, const void* spf_dist, const uint32_t* spf_nh,
+                            const uint32_t* spf_reached, uint32_t flags, int32_t nh_words,
+                            ogs_spf_out* out, void* stream);
+int ogs_ctx_spf_routes_variants(ogs_ctx* ctx, const ogs_graph* graph,
+                                const ogs_prefix_table* prefixes, const ogs_unit* units,
+                                int32_t n_units, const ogs_unit_mods* mods,
+                                ogs_route_diff* diff, uint32_t flags, int32_t nh_words,
+                                ogs_spf_out* out, void* stream);
+int ogs_ctx_ksp_paths(ogs_ctx* ctx, const ogs_graph* graph, const ogs_path_unit* units,
+                      int32_t n_units, const uint32_t* masks, uint32_t mask_words,
+                      uint32_t flags, ogs_path_out* out, void* stream);
+int ogs_ctx_ksp2_paths(ogs_ctx* ctx, const ogs_graph* graph, const ogs_unit* sources,
+                       int32_t n_sources, const ogs_path_unit* units, int32_t n_units,
+                       uint32_t flags, ogs_path_out* k1, ogs_path_out* k2, void* stream);
+int ogs_ctx_routes_multiarea(ogs_ctx* ctx, const ogs_graph* graph,
+                             const ogs_prefix_table* prefixes, const ogs_area_table* areas,
+                             const uint32_t* units, int32_t n_units, const uint32_t* spf_row,
+                             const void* spf_dist, const uint32_t* spf_nh, uint32_t flags,
+                             int32_t nh_words, ogs_spf_out* out, void* stream);
+int ogs_ctx_rib_policy_apply(ogs_ctx* ctx, const ogs_prefix_table* prefixes,
+                             const ogs_rib_policy* policy, int32_t num_areas, int32_t n_units,
+                             int32_t nh_words, const uint32_t* meta, uint32_t* mask,
+                             uint16_t* applied, uint16_t* counter, void* stream);
 
 #ifdef __cplusplus
 }

@@ -6,7 +6,7 @@ import ctypes
 from . import LIB_PATH
 
 OGS_OK = 0
-OGS_ABI_VERSION = 5  # include/openr_gpu.h
+OGS_ABI_VERSION = 6  # include/openr_gpu.h
 OGS_F_ENABLE_V4 = 0x01
 OGS_F_V4_OVER_V6 = 0x02
 OGS_F_BEST_ROUTE_SELECTION = 0x04
@@ -22,6 +22,10 @@ EXPORTS = [
     "ogs_spf_routes_variants", "ogs_rib_policy_apply", "ogs_route_changes_gather",
     "ogs_csr_patch", "ogs_host_alloc", "ogs_host_free", "ogs_routes_from_spf",
     "ogs_abi_version", "ogs_spf_routes_groups",
+    "ogs_ctx_create", "ogs_ctx_destroy", "ogs_ctx_set_option", "ogs_ctx_spf_routes",
+    "ogs_ctx_spf_routes_groups", "ogs_ctx_routes_from_spf", "ogs_ctx_spf_routes_variants",
+    "ogs_ctx_ksp_paths", "ogs_ctx_ksp2_paths", "ogs_ctx_routes_multiarea",
+    "ogs_ctx_rib_policy_apply",
 ]
 
 
@@ -74,6 +78,18 @@ def load(path=None):
     lib.ogs_spf_routes_groups.restype = ctypes.c_int
     lib.ogs_set_option.argtypes = [ctypes.c_char_p, ctypes.c_int64]
     lib.ogs_set_option.restype = ctypes.c_int
+    # execution contexts (ABI 6): opaque handles
+    lib.ogs_ctx_create.argtypes = [ctypes.c_int32, ctypes.POINTER(ctypes.c_void_p)]
+    lib.ogs_ctx_create.restype = ctypes.c_int
+    lib.ogs_ctx_destroy.argtypes = [ctypes.c_void_p]
+    lib.ogs_ctx_destroy.restype = ctypes.c_int
+    lib.ogs_ctx_set_option.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int64]
+    lib.ogs_ctx_set_option.restype = ctypes.c_int
+    lib.ogs_ctx_spf_routes.argtypes = [ctypes.c_void_p] + lib.ogs_spf_routes.argtypes
+    lib.ogs_ctx_spf_routes.restype = ctypes.c_int
+    lib.ogs_ctx_spf_routes_groups.argtypes = ([ctypes.c_void_p] +
+                                             lib.ogs_spf_routes_groups.argtypes)
+    lib.ogs_ctx_spf_routes_groups.restype = ctypes.c_int
     return lib
 
 

@@ -3,44 +3,13 @@
 
 #include <cstdio>
 #include <cstring>
+#include <new>
 #include <string>
 
 #include "openr_gpu.h"
+#include "engine.h"
 
 namespace ogs {
-extern int g_unitWidth;
-extern int g_waveWgLds;
-extern int g_waveUpb;
-extern int g_waveOpt;
-extern int g_kspWaveTrace;
-extern int g_msGroup;
-extern int g_routeStream;
-extern int g_ldsParts;
-extern int g_ldsGrid;
-extern int g_ldsKey16;
-extern int g_ldsTail;
-extern int g_ldsLead;
-extern int g_ldsBfsExit;
-extern int g_ldsPull;
-extern int g_ldsTailParts;
-extern int g_routeStoreNt;
-extern int g_spfSeedRow;
-extern int g_frontierBlock;
-extern int g_frontierParts;
-extern int g_frontierPartsWide;
-extern int g_spfLaneWalk;
-extern int g_spfPreload;
-extern int g_spfPackedScan;
-extern int g_spfFrontier;
-extern int g_spfGlobal;
-extern int g_spfGlobalSync;
-extern int g_spfGlobalLds;
-extern int g_spfQueue;
-extern int g_spfNinfo;
-extern int g_kspQueue;
-extern int g_kspStage;
-extern int g_kspHbm;
-extern int g_c4Desc;
 hipError_t launch_spf_routes(const ogs_graph& g, const ogs_prefix_table* pt,
                              const ogs_unit* units, int nUnits, uint32_t flags,
                              int W, const ogs_spf_out& out, hipStream_t stream,
@@ -178,191 +147,232 @@ int ogs_stream_sync(void* stream) {
   return e == hipSuccess ? OGS_OK : hipFail(e, "hipStreamSynchronize");
 }
 
-int ogs_set_option(const char* name, int64_t value) {
+}  // extern "C"
+
+// one knob of `o` (the default context's, or a context's own)
+static int set_option(ogs::EngineOptions& o, const char* name, int64_t value) {
   if (!name) return fail(OGS_E_INVALID, "option name is NULL");
   if (std::strcmp(name, "unit_width") == 0) {
     if (value != -1 && value != 0 && value != 1 && value != 2 && value != 3 &&
         value != 64 && value != 128 && value != 256) {
       return fail(OGS_E_INVALID, "unit_width must be -1, 0, 1, 2, 3, 64, 128 or 256");
     }
-    ogs::g_unitWidth = int(value);
+    o.unitWidth = int(value);
     return OGS_OK;
   }
   if (std::strcmp(name, "ms_group") == 0) {
     if (value != 0 && value != 1 && value != 2 && value != 4) {
       return fail(OGS_E_INVALID, "ms_group must be 0, 1, 2 or 4");
     }
-    ogs::g_msGroup = int(value);
+    o.msGroup = int(value);
     return OGS_OK;
   }
   if (std::strcmp(name, "route_stream") == 0) {
     if (value != 1 && value != 2 && value != 4 && value != 5) {
       return fail(OGS_E_INVALID, "route_stream must be 1, 2, 4 or 5");
     }
-    ogs::g_routeStream = int(value);
+    o.routeStream = int(value);
     return OGS_OK;
   }
   if (std::strcmp(name, "lds_parts") == 0) {
     if (value < 0 || value > 64) return fail(OGS_E_INVALID, "lds_parts must be in [0, 64]");
-    ogs::g_ldsParts = int(value);
+    o.ldsParts = int(value);
     return OGS_OK;
   }
   if (std::strcmp(name, "lds_tail") == 0) {
     if (value != 0 && value != 1) return fail(OGS_E_INVALID, "lds_tail must be 0 or 1");
-    ogs::g_ldsTail = int(value);
+    o.ldsTail = int(value);
     return OGS_OK;
   }
   if (std::strcmp(name, "lds_lead") == 0) {
     if (value < -1 || value > 65536) return fail(OGS_E_INVALID, "lds_lead must be in [-1, 65536]");
-    ogs::g_ldsLead = int(value);
+    o.ldsLead = int(value);
     return OGS_OK;
   }
   if (std::strcmp(name, "lds_tail_parts") == 0) {
     if (value < 0 || value > 64) return fail(OGS_E_INVALID, "lds_tail_parts must be in [0, 64]");
-    ogs::g_ldsTailParts = int(value);
+    o.ldsTailParts = int(value);
     return OGS_OK;
   }
   if (std::strcmp(name, "lds_pull") == 0) {
     if (value < 0 || value > 15) return fail(OGS_E_INVALID, "lds_pull must be in [0, 15]");
-    ogs::g_ldsPull = int(value);
+    o.ldsPull = int(value);
     return OGS_OK;
   }
   if (std::strcmp(name, "lds_bfs_exit") == 0) {
     if (value != 0 && value != 1) return fail(OGS_E_INVALID, "lds_bfs_exit must be 0 or 1");
-    ogs::g_ldsBfsExit = int(value);
+    o.ldsBfsExit = int(value);
     return OGS_OK;
   }
   if (std::strcmp(name, "lds_key16") == 0) {
     if (value != 0 && value != 1) return fail(OGS_E_INVALID, "lds_key16 must be 0 or 1");
-    ogs::g_ldsKey16 = int(value);
+    o.ldsKey16 = int(value);
     return OGS_OK;
   }
   if (std::strcmp(name, "lds_grid") == 0) {
     if (value < 0 || value > 4096) return fail(OGS_E_INVALID, "lds_grid must be in [0, 4096]");
-    ogs::g_ldsGrid = int(value);
+    o.ldsGrid = int(value);
     return OGS_OK;
   }
   if (std::strcmp(name, "spf_packed_scan") == 0) {
     if (value != 0 && value != 1) return fail(OGS_E_INVALID, "spf_packed_scan must be 0 or 1");
-    ogs::g_spfPackedScan = int(value);
+    o.spfPackedScan = int(value);
     return OGS_OK;
   }
   if (std::strcmp(name, "route_store_nt") == 0) {
     if (value < 0 || value > 3) return fail(OGS_E_INVALID, "route_store_nt must be in [0, 3]");
-    ogs::g_routeStoreNt = int(value);
+    o.routeStoreNt = int(value);
     return OGS_OK;
   }
   if (std::strcmp(name, "frontier_block") == 0) {
     if (value != 0 && value != 256 && value != 512 && value != 1024) {
       return fail(OGS_E_INVALID, "frontier_block must be 0, 256, 512 or 1024");
     }
-    ogs::g_frontierBlock = int(value);
+    o.frontierBlock = int(value);
     return OGS_OK;
   }
   if (std::strcmp(name, "frontier_parts") == 0) {
     if (value < 0 || value > 16) return fail(OGS_E_INVALID, "frontier_parts must be in [0, 16]");
-    ogs::g_frontierParts = int(value);
+    o.frontierParts = int(value);
     return OGS_OK;
   }
   if (std::strcmp(name, "spf_lane_walk") == 0) {
     if (value < -1 || value > 1) return fail(OGS_E_INVALID, "spf_lane_walk must be -1, 0 or 1");
-    ogs::g_spfLaneWalk = int(value);
+    o.spfLaneWalk = int(value);
     return OGS_OK;
   }
   if (std::strcmp(name, "spf_preload") == 0) {
     if (value != 0 && value != 1) return fail(OGS_E_INVALID, "spf_preload must be 0 or 1");
-    ogs::g_spfPreload = int(value);
+    o.spfPreload = int(value);
     return OGS_OK;
   }
   if (std::strcmp(name, "frontier_parts_wide") == 0) {
     if (value < 0 || value > 16) {
       return fail(OGS_E_INVALID, "frontier_parts_wide must be in [0, 16]");
     }
-    ogs::g_frontierPartsWide = int(value);
+    o.frontierPartsWide = int(value);
     return OGS_OK;
   }
   if (std::strcmp(name, "spf_seed_row") == 0) {
     if (value != 0 && value != 1) return fail(OGS_E_INVALID, "spf_seed_row must be 0 or 1");
-    ogs::g_spfSeedRow = int(value);
+    o.spfSeedRow = int(value);
     return OGS_OK;
   }
   if (std::strcmp(name, "spf_frontier") == 0) {
     if (value != 0 && value != 1) {
       return fail(OGS_E_INVALID, "spf_frontier must be 0 or 1");
     }
-    ogs::g_spfFrontier = int(value);
+    o.spfFrontier = int(value);
     return OGS_OK;
   }
   if (std::strcmp(name, "spf_global") == 0) {
     if (value != 0 && value != 1) return fail(OGS_E_INVALID, "spf_global must be 0 or 1");
-    ogs::g_spfGlobal = int(value);
+    o.spfGlobal = int(value);
     return OGS_OK;
   }
   if (std::strcmp(name, "ksp_queue") == 0) {
     if (value != 0 && value != 1) return fail(OGS_E_INVALID, "ksp_queue must be 0 or 1");
-    ogs::g_kspQueue = int(value);
+    o.kspQueue = int(value);
     return OGS_OK;
   }
   if (std::strcmp(name, "spf_global_sync") == 0) {
     if (value != 0 && value != 1) return fail(OGS_E_INVALID, "spf_global_sync must be 0 or 1");
-    ogs::g_spfGlobalSync = int(value);
+    o.spfGlobalSync = int(value);
     return OGS_OK;
   }
   if (std::strcmp(name, "spf_global_lds") == 0) {
     if (value < 0 || value > 3) return fail(OGS_E_INVALID, "spf_global_lds must be 0..3");
-    ogs::g_spfGlobalLds = int(value);
+    o.spfGlobalLds = int(value);
     return OGS_OK;
   }
   if (std::strcmp(name, "c4_desc") == 0) {
     if (value != 0 && value != 1) return fail(OGS_E_INVALID, "c4_desc must be 0 or 1");
-    ogs::g_c4Desc = int(value);
+    o.c4Desc = int(value);
     return OGS_OK;
   }
   if (std::strcmp(name, "ksp_hbm") == 0) {
     if (value != 0 && value != 1) return fail(OGS_E_INVALID, "ksp_hbm must be 0 or 1");
-    ogs::g_kspHbm = int(value);
+    o.kspHbm = int(value);
     return OGS_OK;
   }
   if (std::strcmp(name, "ksp_stage") == 0) {
     if (value < -1 || value > 2) return fail(OGS_E_INVALID, "ksp_stage must be -1, 0, 1 or 2");
-    ogs::g_kspStage = int(value);
+    o.kspStage = int(value);
     return OGS_OK;
   }
   if (std::strcmp(name, "spf_ninfo") == 0) {
     if (value < -1 || value > 1) return fail(OGS_E_INVALID, "spf_ninfo must be -1, 0 or 1");
-    ogs::g_spfNinfo = int(value);
+    o.spfNinfo = int(value);
     return OGS_OK;
   }
   if (std::strcmp(name, "spf_queue") == 0) {
     if (value != -1 && value != 0) return fail(OGS_E_INVALID, "spf_queue must be -1 or 0");
-    ogs::g_spfQueue = int(value);
+    o.spfQueue = int(value);
     return OGS_OK;
   }
   if (std::strcmp(name, "wave_upb") == 0) {
     if (value != 4 && value != 8 && value != 16) {
       return fail(OGS_E_INVALID, "wave_upb must be 4, 8 or 16");
     }
-    ogs::g_waveUpb = int(value);
+    o.waveUpb = int(value);
     return OGS_OK;
   }
   if (std::strcmp(name, "ksp_wave_trace") == 0) {
     if (value != 0 && value != 1) return fail(OGS_E_INVALID, "ksp_wave_trace must be 0 or 1");
-    ogs::g_kspWaveTrace = int(value);
+    o.kspWaveTrace = int(value);
     return OGS_OK;
   }
   if (std::strcmp(name, "wave_opt") == 0) {
     if (value < 0 || value > 3) return fail(OGS_E_INVALID, "wave_opt must be in [0, 3]");
-    ogs::g_waveOpt = int(value);
+    o.waveOpt = int(value);
     return OGS_OK;
   }
   if (std::strcmp(name, "wave_wg_lds") == 0) {
     if (value < 0 || value > 160 * 1024) {
       return fail(OGS_E_INVALID, "wave_wg_lds must be in [0, 163840]");
     }
-    ogs::g_waveWgLds = int(value);
+    o.waveWgLds = int(value);
     return OGS_OK;
   }
   return fail(OGS_E_INVALID, std::string("unknown option ") + name);
+}
+
+extern "C" {
+
+int ogs_set_option(const char* name, int64_t value) {
+  return set_option(ogs::default_options(), name, value);
+}
+
+// ---- contexts (ABI 6) ------------------------------------------------------
+struct ogs_ctx {
+  ogs::EngineContext e;
+};
+
+int ogs_ctx_create(int32_t device, ogs_ctx** out) {
+  if (!out) return fail(OGS_E_INVALID, "out is NULL");
+  *out = nullptr;
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess || n <= 0) return fail(OGS_E_NODEVICE, "no HIP device visible");
+  if (device < 0 || device >= n) return fail(OGS_E_INVALID, "device out of range");
+  ogs_ctx* c = new (std::nothrow) ogs_ctx;
+  if (!c) return fail(OGS_E_NOMEM, "context allocation");
+  c->e.device = device;
+  c->e.opts = ogs::default_options();  // starts from the process defaults
+  *out = c;
+  return OGS_OK;
+}
+
+int ogs_ctx_destroy(ogs_ctx* ctx) {
+  if (!ctx) return OGS_OK;
+  (void)hipSetDevice(ctx->e.device);
+  delete ctx;  // frees its scratch (hipFree waits for the device)
+  return OGS_OK;
+}
+
+int ogs_ctx_set_option(ogs_ctx* ctx, const char* name, int64_t value) {
+  if (!ctx) return fail(OGS_E_INVALID, "ctx is NULL");
+  return set_option(ctx->e.opts, name, value);
 }
 
 // any width from ceil(degree/32) up is valid for a call; this is the
@@ -707,6 +717,79 @@ int ogs_routes_multiarea(const ogs_graph* graph,
       *graph, *prefixes, *areas, units, n_units, spf_row, spf_dist, spf_nh,
       flags, nh_words, *out, static_cast<hipStream_t>(stream));
   return e == hipSuccess ? OGS_OK : hipFail(e, "multi-area route launch");
+}
+
+
+// Context forms of the compute entry points: the call runs with the
+// context's device, options and scratch (engine.h), then the thread's
+// previous binding is restored. Same arguments and status as the plain
+// entry point.
+#define OGS_CTX_CALL(ctx, call)                                  \
+  do {                                                           \
+    if (!(ctx)) return fail(OGS_E_INVALID, "ctx is NULL");       \
+    ogs::BoundContext bound_(&(ctx)->e);                         \
+    return (call);                                               \
+  } while (0)
+
+int ogs_ctx_spf_routes(ogs_ctx* ctx, const ogs_graph* graph, const ogs_prefix_table* prefixes,
+                       const ogs_unit* units, int32_t n_units, uint32_t flags,
+                       int32_t nh_words, ogs_spf_out* out, void* stream) {
+  OGS_CTX_CALL(ctx, ogs_spf_routes(graph, prefixes, units, n_units, flags, nh_words, out,
+                                   stream));
+}
+
+int ogs_ctx_spf_routes_groups(ogs_ctx* ctx, const ogs_graph* graph,
+                              const ogs_prefix_table* prefixes, const ogs_route_group* groups,
+                              int32_t n_groups, uint32_t flags, void* stream) {
+  OGS_CTX_CALL(ctx, ogs_spf_routes_groups(graph, prefixes, groups, n_groups, flags, stream));
+}
+
+int ogs_ctx_routes_from_spf(ogs_ctx* ctx, const ogs_graph* graph,
+                            const ogs_prefix_table* prefixes, const ogs_unit* units,
+                            int32_t n_units, const void* spf_dist, const uint32_t* spf_nh,
+                            const uint32_t* spf_reached, uint32_t flags, int32_t nh_words,
+                            ogs_spf_out* out, void* stream) {
+  OGS_CTX_CALL(ctx, ogs_routes_from_spf(graph, prefixes, units, n_units, spf_dist, spf_nh,
+                                        spf_reached, flags, nh_words, out, stream));
+}
+
+int ogs_ctx_spf_routes_variants(ogs_ctx* ctx, const ogs_graph* graph,
+                                const ogs_prefix_table* prefixes, const ogs_unit* units,
+                                int32_t n_units, const ogs_unit_mods* mods,
+                                ogs_route_diff* diff, uint32_t flags, int32_t nh_words,
+                                ogs_spf_out* out, void* stream) {
+  OGS_CTX_CALL(ctx, ogs_spf_routes_variants(graph, prefixes, units, n_units, mods, diff, flags,
+                                            nh_words, out, stream));
+}
+
+int ogs_ctx_ksp_paths(ogs_ctx* ctx, const ogs_graph* graph, const ogs_path_unit* units,
+                      int32_t n_units, const uint32_t* masks, uint32_t mask_words,
+                      uint32_t flags, ogs_path_out* out, void* stream) {
+  OGS_CTX_CALL(ctx, ogs_ksp_paths(graph, units, n_units, masks, mask_words, flags, out, stream));
+}
+
+int ogs_ctx_ksp2_paths(ogs_ctx* ctx, const ogs_graph* graph, const ogs_unit* sources,
+                       int32_t n_sources, const ogs_path_unit* units, int32_t n_units,
+                       uint32_t flags, ogs_path_out* k1, ogs_path_out* k2, void* stream) {
+  OGS_CTX_CALL(ctx, ogs_ksp2_paths(graph, sources, n_sources, units, n_units, flags, k1, k2,
+                                   stream));
+}
+
+int ogs_ctx_routes_multiarea(ogs_ctx* ctx, const ogs_graph* graph,
+                             const ogs_prefix_table* prefixes, const ogs_area_table* areas,
+                             const uint32_t* units, int32_t n_units, const uint32_t* spf_row,
+                             const void* spf_dist, const uint32_t* spf_nh, uint32_t flags,
+                             int32_t nh_words, ogs_spf_out* out, void* stream) {
+  OGS_CTX_CALL(ctx, ogs_routes_multiarea(graph, prefixes, areas, units, n_units, spf_row,
+                                         spf_dist, spf_nh, flags, nh_words, out, stream));
+}
+
+int ogs_ctx_rib_policy_apply(ogs_ctx* ctx, const ogs_prefix_table* prefixes,
+                             const ogs_rib_policy* policy, int32_t num_areas, int32_t n_units,
+                             int32_t nh_words, const uint32_t* meta, uint32_t* mask,
+                             uint16_t* applied, uint16_t* counter, void* stream) {
+  OGS_CTX_CALL(ctx, ogs_rib_policy_apply(prefixes, policy, num_areas, n_units, nh_words, meta,
+                                         mask, applied, counter, stream));
 }
 
 }  // extern "C"

@@ -23,6 +23,7 @@
 
 #include "openr_gpu.h"
 #include "spf_core.h"
+#include "engine.h"
 
 namespace ogs {
 
@@ -281,7 +282,7 @@ __device__ uint32_t trace_paths_wave(const UnitCsr& csr, const uint32_t* dist, u
 
 // "ksp_wave_trace" option: 1 (default) the traces of 32-bit-distance units
 // run on a whole wavefront (trace_paths_wave), 0 on lane 0 (A/B)
-int g_kspWaveTrace = 1;
+// EngineOptions::kspWaveTrace (engine.h), default 1
 // (An early stop of the k = 2 SPF once every distance lowered in a round
 // exceeds the destination's saved nothing on C5 -- 0.49 vs 0.49 ms of KSP2
 // kernels per job, profiles/r03_c5_ksp_stop_ab.log: the launch lasts as
@@ -361,7 +362,7 @@ hipError_t ksp_launch(const ogs_graph& g, const ogs_path_unit* units,
     if (e != hipSuccess) return e;
   }
   hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), bytes, stream, g, units,
-                     nUnits, masks, maskWords, out, lds, g_kspWaveTrace);
+                     nUnits, masks, maskWords, out, lds, opts().kspWaveTrace);
   return hipGetLastError();
 }
 
@@ -388,7 +389,7 @@ hipError_t ksp_launch(const ogs_graph& g, const ogs_path_unit* units,
 constexpr int kKspHbmBlock = 1024;
 constexpr uint32_t kRankNew = 0xFFFFFFFFu;   // never inserted
 constexpr uint32_t kRankOpen = 0xFFFFFFFEu;  // in the open list
-int g_kspHbm = 0;  // "ksp_hbm" option: 1 = every KSP unit on the HBM path
+// EngineOptions::kspHbm (engine.h), default 0  // "ksp_hbm" option: 1 = every KSP unit on the HBM path
 
 hipError_t workspace(size_t bytes, hipStream_t stream, void** out);
 
@@ -892,7 +893,7 @@ hipError_t ksp_dispatch(const ogs_graph& g, const ogs_path_unit* units,
                         const ogs_path_out& out, hipStream_t stream,
                         int* unsupported) {
   const uint64_t N = g.max_nodes, E = g.max_edges;
-  if (g_kspHbm) {
+  if (opts().kspHbm) {
     return launch_ksp_hbm<D, false, false, MASKED>(g, nullptr, 0, units, nUnits, masks,
                                                    maskWords, out, out, stream);
   }
@@ -1244,7 +1245,7 @@ hipError_t ksp2_launch(const ogs_graph& g, const ogs_unit* sources,
   hipLaunchKernelGGL(k2, dim3((nUnits + upb - 1) / upb), dim3(kBlock), bytes,
                      stream, g, sources, nSources,
                      static_cast<const D*>(srcDist), units, nUnits, o1, o2, lds,
-                     g_kspWaveTrace);
+                     opts().kspWaveTrace);
   return hipGetLastError();
 }
 
@@ -1254,8 +1255,8 @@ hipError_t workspace(size_t bytes, hipStream_t stream, void** out);
 // 0 with the pull fixpoint. "ksp_stage": -1 (default) auto -- the edges in
 // LDS only when three units still fit a CU, else the row offsets only --;
 // 0 nothing staged, 1 row offsets, 2 rows + edges whenever they fit.
-int g_kspQueue = 1;
-int g_kspStage = -1;
+// EngineOptions::kspQueue (engine.h), default 1
+// EngineOptions::kspStage (engine.h), default -1
 
 template <typename D>
 hipError_t ksp2_dispatch(const ogs_graph& g, const ogs_unit* sources,
@@ -1264,7 +1265,7 @@ hipError_t ksp2_dispatch(const ogs_graph& g, const ogs_unit* sources,
                          hipStream_t stream, int* unsupported) {
   const uint64_t N = g.max_nodes, E = g.max_edges;
   constexpr uint64_t kBudget = 160 * 1024;
-  if (g_kspHbm) {
+  if (opts().kspHbm) {
     return launch_ksp_hbm<D, false, true, false>(g, sources, nSources, units, nUnits,
                                                  nullptr, 0, o1, o2, stream);
   }
@@ -1277,8 +1278,8 @@ hipError_t ksp2_dispatch(const ogs_graph& g, const ogs_unit* sources,
     return ksp2_launch<D, 64, 2, false>(g, sources, nSources, d, units, nUnits,
                                         o1, o2, uint32_t(tiny), stream);
   }
-  const bool q = g_kspQueue != 0 && N <= 65535;
-  int st = g_kspStage;
+  const bool q = opts().kspQueue != 0 && N <= 65535;
+  int st = opts().kspStage;
   if (st < 0) st = ksp2_lds_bytes<D>(N, E, 2, q) * 3 <= kBudget ? 2 : 1;
   while (st > 0 && ksp2_lds_bytes<D>(N, E, st, q) > kBudget) --st;
   const uint64_t b = ksp2_lds_bytes<D>(N, E, st, q);

@@ -21,7 +21,6 @@ namespace ogs {
 // set per kernel family from the "route_store_nt" option bits):
 // non-temporal stores, or ordinary write-back ones.
 constexpr uint32_t kFlagNtStores = 1u << 28;
-extern int g_routeStoreNt;
 
 template <typename T>
 __device__ __forceinline__ void store_out(T* p, T v, bool nt) {

@@ -38,6 +38,7 @@
 #include "route_stream.h"
 #include "spf_lds.h"
 #include "spf_core.h"
+#include "engine.h"
 
 namespace ogs {
 
@@ -124,39 +125,6 @@ __global__ __launch_bounds__(kBlock) void route_stream_kernel(
   }
 }
 
-// ---- per-(device, stream) workspace (grow-only; freed at process exit) ----
-// Calls on one stream run in order, so its scratch is reused safely; calls
-// on different streams (e.g. two unit groups overlapped) get separate ones.
-namespace {
-struct Workspace {
-  void* ptr = nullptr;
-  size_t bytes = 0;
-};
-std::mutex g_wsMutex;
-std::map<std::pair<int, hipStream_t>, Workspace> g_ws;
-}  // namespace
-
-hipError_t workspace(size_t bytes, hipStream_t stream, void** out) {
-  int dev = 0;
-  hipError_t e = hipGetDevice(&dev);
-  if (e != hipSuccess) return e;
-  std::lock_guard<std::mutex> lock(g_wsMutex);
-  Workspace& w = g_ws[{dev, stream}];
-  if (w.bytes < bytes) {
-    if (w.ptr) {
-      e = hipFree(w.ptr);  // implicit device sync: no launch still reads it
-      if (e != hipSuccess) return e;
-      w.ptr = nullptr;
-      w.bytes = 0;
-    }
-    e = hipMalloc(&w.ptr, bytes);
-    if (e != hipSuccess) return e;
-    w.bytes = bytes;
-  }
-  *out = w.ptr;
-  return hipSuccess;
-}
-
 // "route_stream" option for large shared topologies: 5 (default) the
 // LDS-resident SPF and the route stream in one persistent launch
 // (spf_lds.hip, spf_lds_route_kernel; topologies whose image does not fit
@@ -169,7 +137,7 @@ hipError_t workspace(size_t bytes, hipStream_t stream, void** out) {
 // streams -- 1.40-1.64 vs 1.33 ms on C3, profiles/r03_c3_pipelined_split_
 // ab.log -- were removed in round 4; the multi-source kernel remains the
 // fallback where neither form applies.)
-int g_routeStream = 5;
+// EngineOptions::routeStream (engine.h), default 5
 // "route_store_nt" option, bits: 1 the RouteDb stream's 16-B stores are
 // non-temporal (else ordinary write-back stores), 2 the wave kernel's output
 // stores are. Default 2. The bare C3 store pattern drains faster with
@@ -177,7 +145,7 @@ int g_routeStream = 5;
 // gains 0.5-2 % from them (1.278 vs 1.283 ms mean of 5, 1.282-1.295 vs
 // 1.303-1.325 ms), the C2 wave kernel loses 3 % (10.9 vs 10.6 us):
 // profiles/r03_store_pattern.log, r03_store_nt_ab.log.
-int g_routeStoreNt = 2;
+// EngineOptions::routeStoreNt (engine.h), default 2
 
 bool try_ms(const ogs_graph& g, const ogs_prefix_table& pt, int hasPrefixes,
             const ogs_unit* units, int nUnits, uint32_t flags, int W,
@@ -210,7 +178,7 @@ hipError_t launch_route_stream(const ogs_graph& g, const ogs_prefix_table& pt,
                                        int(lds));
     if (e != hipSuccess) return e;
   }
-  if (g_routeStoreNt & 1) flags |= kFlagNtStores;
+  if (opts().routeStoreNt & 1) flags |= kFlagNtStores;
   hipLaunchKernelGGL(k, dim3(unsigned(nUnits) * unsigned(parts)), dim3(kBlock), lds, stream, g,
                      pt, key, units, flags, dist, nh, out, uint32_t(parts));
   return hipGetLastError();
@@ -288,10 +256,10 @@ bool try_ms_stream(const ogs_graph& g, const ogs_prefix_table& pt,
   const bool frontier = frontier_fits(g, flags, W);
   // route_stream 4: SPF with the topology in LDS (spf_lds.hip), then the
   // stream over `parts` workgroups per unit; 5: both in one persistent launch
-  const bool ldsForm = (g_routeStream == 4 || g_routeStream == 5) && Sp > 0;
+  const bool ldsForm = (opts().routeStream == 4 || opts().routeStream == 5) && Sp > 0;
   const size_t ldsBytes = ldsForm ? lds_scratch_bytes(g, W, nUnits) : 0;
   const bool ldsSplit = ldsBytes != 0;
-  const bool fused = (g_routeStream == 2 || (ldsForm && !ldsSplit)) && frontier;
+  const bool fused = (opts().routeStream == 2 || (ldsForm && !ldsSplit)) && frontier;
   // three-word sets (65..96 links: C3 FSWs) through the frontier forms only
   if (W == 3 && !fused && !ldsSplit) return false;
   const size_t keyBytes = round256(size_t(g.num_topos) * Sp * 4);
@@ -310,11 +278,11 @@ bool try_ms_stream(const ogs_graph& g, const ogs_prefix_table& pt,
                   : reinterpret_cast<uint32_t*>(base + keyBytes + chunkBytes + distBytes);
   if (ldsSplit) {
     // one prep launch: LDS images, weight partials, counters, route keys
-    const bool k16 = g_routeStream == 5 && lds_key16(g);  // form 4's stream reads u32 keys
+    const bool k16 = opts().routeStream == 5 && lds_key16(g);  // form 4's stream reads u32 keys
     *err = launch_lds_prep(g, &pt, key, k16, W, nUnits, chunkScratch, stream);
     if (*err != hipSuccess) return true;
     uint32_t* d = static_cast<uint32_t*>(spf.dist);
-    if (g_routeStream == 5) {
+    if (opts().routeStream == 5) {
       const LdsRouteGroup one{units, nUnits, W, d, spf.nh, out};
       *err = launch_spf_lds_routes(g, pt, key, k16, &one, 1, flags, chunkScratch, stream);
       return true;
@@ -390,7 +358,7 @@ hipError_t launch_spf_routes_groups(const ogs_graph& g, const ogs_prefix_table* 
   // use_global() (deep graphs past the frontier's LDS budget, or the
   // "spf_global" option) to the HBM-state frontier -- so a group gets the
   // same engine here as through ogs_spf_routes
-  bool one = g_routeStream == 5 && pt && Sp > 0 && g.edge_src && g.max_nodes > 256 &&
+  bool one = opts().routeStream == 5 && pt && Sp > 0 && g.edge_src && g.max_nodes > 256 &&
       !(flags & (OGS_F_EXACT_ORDER | OGS_F_WIDE_METRIC)) && small_unit_width() == -1 &&
       !lg.empty() && lg.size() <= 4 && Wmax <= 4 && !use_global(g, Wmax, flags);
   const size_t ldsBytes = one ? lds_scratch_bytes(g, Wmax, U) : 0;

@@ -37,6 +37,7 @@
 #include "route_core.h"
 #include "route_stream.h"
 #include "spf_core.h"
+#include "engine.h"
 
 namespace ogs {
 
@@ -786,8 +787,8 @@ constexpr uint32_t kFlagScanRound1 = 1u << 27;
 // preloaded target distances in the packed relax (A/B).
 constexpr uint32_t kFlagSlotWalk = 1u << 29;
 constexpr uint32_t kFlagNoPreload = 1u << 26;
-int g_spfLaneWalk = -1;
-int g_spfPreload = 1;
+// EngineOptions::spfLaneWalk (engine.h), default -1
+// EngineOptions::spfPreload (engine.h), default 1
 
 #ifdef OGS_STAMPS
 // diagnostic build (make stamps): 8 phase clocks per workgroup of the last
@@ -970,26 +971,26 @@ __global__ __launch_bounds__(B) void spf_frontier_kernel(
 
 // "spf_seed_row" option: 1 (default) round 1 of the chunk-scan forms relaxes
 // the source's row directly, 0 it scans every chunk record (A/B)
-int g_spfSeedRow = 1;
+// EngineOptions::spfSeedRow (engine.h), default 1
 
 
 // "spf_packed_scan" option: 1 (default) chunk-scan units with one-word
 // next-hop sets relax packed {dist, nh} words in one phase
 // (frontier_spf_packed), 0 the two-phase chunk scan (A/B)
-int g_spfPackedScan = 1;
+// EngineOptions::spfPackedScan (engine.h), default 1
 
 // "spf_queue" option: -1 (default) the queue form for sparse topologies
 // (max degree <= 16, <= 65,535 nodes; one-phase packed words when the
 // next-hop sets fit one word), 0 always the chunk scan (A/B, tests).
-int g_spfQueue = -1;
+// EngineOptions::spfQueue (engine.h), default -1
 
 // "spf_ninfo" option: 1 (default) the queue forms keep row begin | drained
 // per node in LDS, 0 read them from the CSR (L2) -- 4 B/node less LDS, more
 // units per CU --, -1 the CSR form whenever that raises the units per CU.
-int g_spfNinfo = 1;
+// EngineOptions::spfNinfo (engine.h), default 1
 
 bool ninfo_in_lds(uint32_t Sn, int W) {
-  if (g_spfNinfo >= 0) return g_spfNinfo != 0;
+  if (opts().spfNinfo >= 0) return opts().spfNinfo != 0;
   constexpr uint32_t kCu = 160u * 1024u;
   return kCu / frontier_lds_bytes(Sn, W, true, true) >=
       kCu / frontier_lds_bytes(Sn, W, true, false);
@@ -997,7 +998,7 @@ bool ninfo_in_lds(uint32_t Sn, int W) {
 
 // 0 chunk scan, 1 two-phase queue, 2 packed one-phase queue
 int queue_mode(const ogs_graph& g, int W) {
-  if (g_spfQueue == 0 || g.max_nodes > 65535) return 0;
+  if (opts().spfQueue == 0 || g.max_nodes > 65535) return 0;
   if (frontier_lds_bytes(uint32_t(g.max_nodes), W, true) > 160u * 1024u) return 0;
   if (g.max_degree > 16) return 0;
   return W != 1 ? 1 : 2;
@@ -1017,10 +1018,10 @@ hipError_t launch_frontier_q(const ogs_graph& g, const ogs_prefix_table& pt,
   uint32_t lds =
       frontier_lds_bytes(uint32_t(g.max_nodes), W, !scan, ninfo, QMODE == 4);
   if (!ninfo) flags |= kFlagNinfoGlobal;
-  if (!g_spfSeedRow) flags |= kFlagScanRound1;
-  if (g_spfLaneWalk == 0 || (g_spfLaneWalk < 0 && B < 512)) flags |= kFlagSlotWalk;
-  if (!g_spfPreload) flags |= kFlagNoPreload;
-  if (g_routeStoreNt & 1) flags |= kFlagNtStores;
+  if (!opts().spfSeedRow) flags |= kFlagScanRound1;
+  if (opts().spfLaneWalk == 0 || (opts().spfLaneWalk < 0 && B < 512)) flags |= kFlagSlotWalk;
+  if (!opts().spfPreload) flags |= kFlagNoPreload;
+  if (opts().routeStoreNt & 1) flags |= kFlagNtStores;
   auto k = spf_frontier_kernel<W, ROUTES, MODS, DIFF, QMODE, OUTS3, B>;
   if (lds > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
@@ -1047,9 +1048,9 @@ hipError_t launch_frontier_q(const ogs_graph& g, const ogs_prefix_table& pt,
 // Options "frontier_block" (0 auto, 256 / 512 / 1024), "frontier_parts"
 // (workgroups per one-word unit, 0 auto) and "frontier_parts_wide" (per
 // unit of wider next-hop sets, 0 auto) override the choice.
-int g_frontierBlock = 0;
-int g_frontierParts = 0;
-int g_frontierPartsWide = 0;
+// EngineOptions::frontierBlock (engine.h), default 0
+// EngineOptions::frontierParts (engine.h), default 0
+// EngineOptions::frontierPartsWide (engine.h), default 0
 
 namespace {
 int num_cus() {
@@ -1075,7 +1076,7 @@ int num_cus() {
 // keep one workgroup per unit ("frontier_parts" / "frontier_parts_wide"
 // override, as for the fused launches).
 void stream_parts(int nUnits, int W, int P, int* parts) {
-  int k = W > 1 ? g_frontierPartsWide : g_frontierParts;
+  int k = W > 1 ? opts().frontierPartsWide : opts().frontierParts;
   if (!k) {
     const double unitBytes = double(P) * (8 + 4 * W);
     k = nUnits >= 2 * num_cus()
@@ -1088,7 +1089,7 @@ void stream_parts(int nUnits, int W, int P, int* parts) {
 void stream_geometry(int nUnits, int W, int* block, int* parts) {
   // the launch's streamed bytes per CU, in one-word units (12 B per prefix)
   const double load = double(nUnits) * (8 + 4 * W) / 12.0 / num_cus();
-  int b = g_frontierBlock, k = W > 1 ? g_frontierPartsWide : g_frontierParts;
+  int b = opts().frontierBlock, k = W > 1 ? opts().frontierPartsWide : opts().frontierParts;
   // Tuned on the C3 shards (profiles/r04_geometry_ab.log), where the one-
   // word group (load 7.1 / 3.6 / 1.8 / 0.9 at N = 1 / 2 / 4 / 8) runs beside
   // the three-word group (1.7 / 0.8 / 0.4 / 0.2) on a second stream: each
@@ -1113,7 +1114,7 @@ hipError_t launch_frontier(const ogs_graph& g, const ogs_prefix_table& pt,
   const int qm = queue_mode(g, W);
   // chunk scan with one-word next-hop sets: the one-phase packed form
   constexpr int kScanMode = W == 1 ? 4 : 0;
-  const bool packedScan = W == 1 && g_spfPackedScan && qm == 0;
+  const bool packedScan = W == 1 && opts().spfPackedScan && qm == 0;
   // the all-sources RouteDb stream writes exactly meta / metric / mask:
   // unconditional stores (stream_routes OUTS3), geometry by stream_geometry
   if constexpr (ROUTES && !MODS && !DIFF) {
@@ -1160,10 +1161,10 @@ hipError_t launch_frontier(const ogs_graph& g, const ogs_prefix_table& pt,
 
 // "spf_frontier" option: 1 (default) large topologies use this kernel for
 // their SPF, 0 the multi-source edge sweep (spf_route_ms.hip).
-int g_spfFrontier = 1;
+// EngineOptions::spfFrontier (engine.h), default 1
 
 bool frontier_fits(const ogs_graph& g, uint32_t flags, int W) {
-  if (!g_spfFrontier || (flags & OGS_F_WIDE_METRIC)) return false;
+  if (!opts().spfFrontier || (flags & OGS_F_WIDE_METRIC)) return false;
   if (g.max_nodes > 30000 || g.max_degree > OGS_MAX_DEGREE) return false;  // u16 stamps
   return frontier_lds_bytes(uint32_t(g.max_nodes), W) <= 160u * 1024u;
 }
@@ -1321,12 +1322,12 @@ __global__ __launch_bounds__(64) void tight_desc_kernel(ogs_graph g,
 
 // "c4_desc" option: 1 (default) the repair's A from precomputed descendant
 // rows where the topology has <= kDescMaxN nodes, 0 the growth rounds (A/B)
-int g_c4Desc = 1;
+// EngineOptions::c4Desc (engine.h), default 1
 
 // scratch the descendant rows need (0: not used for this graph)
 size_t desc_scratch_bytes(const ogs_graph& g) {
   const uint32_t Sn = uint32_t(g.max_nodes);
-  if (!g_c4Desc || Sn > kDescMaxN) return 0;
+  if (!opts().c4Desc || Sn > kDescMaxN) return 0;
   return size_t(Sn) * ((Sn + 31u) / 32u) * 4u;
 }
 
@@ -1567,7 +1568,7 @@ bool launch_variants_repair(const ogs_graph& g, const ogs_prefix_table& pt,
     if (cached) diff->base_desc_valid = 1;  // the caller's cache now holds them
   }
   hipLaunchKernelGGL(k, dim3(n), dim3(kBlock), lds, stream, g, pt, key, units,
-                     flags | ((g_routeStoreNt & 1) ? kFlagNtStores : 0u),
+                     flags | ((opts().routeStoreNt & 1) ? kFlagNtStores : 0u),
                      static_cast<uint32_t*>(out.dist), out.nh, out, *mods, *diff, desc);
   *err = hipGetLastError();
   return true;

@@ -31,6 +31,7 @@
 #include "route_core.h"
 #include "route_global.h"
 #include "spf_core.h"
+#include "engine.h"
 
 namespace ogs {
 
@@ -859,16 +860,16 @@ hipError_t workspace(size_t bytes, hipStream_t stream, void** out);
 
 // "spf_global" option: 0 (default) the global path only where the LDS paths
 // cannot hold a unit, 1 every ogs_spf_routes call (A/B, parity tests).
-int g_spfGlobal = 0;
+// EngineOptions::spfGlobal (engine.h), default 0
 // "spf_global_sync": 1 (default) rounds end with drained stores + barrier
 // and state is read through sc1 loads; 0 agent-scope fences per round (A/B)
-int g_spfGlobalSync = 1;
+// EngineOptions::spfGlobalSync (engine.h), default 1
 // "spf_global_lds": 1 (default) the best LDS form that fits -- one-phase
 // packed {dist, nh} words (spf_global_lds3_kernel, W = 1, u32), else
 // distances and next-hop words in two phases (spf_global_lds2_kernel), else
 // distances only (spf_global_lds_kernel); 3 the two-phase form, 2 distances
 // only, 0 always the all-HBM form (A/B)
-int g_spfGlobalLds = 1;
+// EngineOptions::spfGlobalLds (engine.h), default 1
 
 // Does the LDS-resident workgroup path fit a unit of this graph? (the last
 // fallback of spf_route.hip: dist + next-hop words, CSR read from L2)
@@ -882,7 +883,7 @@ bool lds_unit_fits(const ogs_graph& g, int W, uint32_t flags) {
 uint32_t frontier_lds_bytes(uint32_t Sn, int W, bool queue, bool ninfo, bool stamp8);
 
 bool use_global(const ogs_graph& g, int W, uint32_t flags) {
-  if (g_spfGlobal == 1 || !lds_unit_fits(g, W, flags)) return true;
+  if (opts().spfGlobal == 1 || !lds_unit_fits(g, W, flags)) return true;
   // past the frontier kernel's LDS budget the remaining LDS paths sweep
   // every edge every round; on such graphs (large sparse / deep: WAN areas
   // of 16k+ nodes) the HBM frontier wins -- G1, 20,000-node WAN x 64
@@ -912,7 +913,7 @@ hipError_t launch_global_w(const ogs_graph& g, const ogs_prefix_table* pt,
   const uint32_t lds2 = global_lds2_bytes(uint32_t(Sn), sizeof(D), W);
   const uint32_t lds3 = global_lds3_bytes(uint32_t(Sn));
   if constexpr (W == 1 && sizeof(D) == 4) {
-    if (g_spfGlobalLds == 1 && g_spfGlobalSync && lds3 <= 160u * 1024u) {
+    if (opts().spfGlobalLds == 1 && opts().spfGlobalSync && lds3 <= 160u * 1024u) {
       auto k = spf_global_lds3_kernel;
       if (lds3 > 64u * 1024u) {
         e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
@@ -926,7 +927,7 @@ hipError_t launch_global_w(const ogs_graph& g, const ogs_prefix_table* pt,
       return launch_route_global<D, W>(g, *pt, units, nUnits, flags, dist, nh, out, stream);
     }
   }
-  if ((g_spfGlobalLds == 1 || g_spfGlobalLds == 3) && g_spfGlobalSync && lds2 <= 160u * 1024u) {
+  if ((opts().spfGlobalLds == 1 || opts().spfGlobalLds == 3) && opts().spfGlobalSync && lds2 <= 160u * 1024u) {
     auto k = spf_global_lds2_kernel<D, W>;
     if (lds2 > 64u * 1024u) {
       e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
@@ -935,7 +936,7 @@ hipError_t launch_global_w(const ogs_graph& g, const ogs_prefix_table* pt,
     }
     hipLaunchKernelGGL(k, dim3(nUnits), dim3(kGBlock), lds2, stream, g, units, flags, dist, nh,
                        scratch);
-  } else if ((g_spfGlobalLds == 1 || g_spfGlobalLds == 2) && g_spfGlobalSync &&
+  } else if ((opts().spfGlobalLds == 1 || opts().spfGlobalLds == 2) && opts().spfGlobalSync &&
              lds <= 160u * 1024u) {
     auto k = spf_global_lds_kernel<D, W>;
     if (lds > 64u * 1024u) {
@@ -945,7 +946,7 @@ hipError_t launch_global_w(const ogs_graph& g, const ogs_prefix_table* pt,
     }
     hipLaunchKernelGGL(k, dim3(nUnits), dim3(kGBlock), lds, stream, g, units, flags, dist, nh,
                        scratch);
-  } else if (g_spfGlobalSync) {
+  } else if (opts().spfGlobalSync) {
     hipLaunchKernelGGL((spf_global_kernel<D, W, true>), dim3(nUnits), dim3(kGBlock), 0, stream,
                        g, units, flags, dist, nh, scratch);
   } else {

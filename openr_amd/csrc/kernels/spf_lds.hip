@@ -35,6 +35,7 @@
 #include "route_stream.h"
 #include "spf_lds.h"
 #include "spf_core.h"
+#include "engine.h"
 
 namespace ogs {
 
@@ -1107,8 +1108,6 @@ int num_cus() {
 
 }  // namespace
 
-extern int g_routeStoreNt;  // route_stream.hip
-
 // Workspace bytes of the LDS paths for this batch (lds_scratch), or 0 when
 // it does not qualify: nodes fit 15 bits, chunk ids 16 bits, the image + one
 // unit's state (and the megakernel's per-node records) fit LDS.
@@ -1141,9 +1140,6 @@ hipError_t launch_lds_prep(const ogs_graph& g, const ogs_prefix_table* pt, void*
   return hipGetLastError();
 }
 
-extern int g_ldsBfsExit;
-extern int g_ldsPull;
-
 template <typename K>
 static hipError_t allow_lds(K k, uint32_t lds) {
   if (lds <= 64u * 1024u) return hipSuccess;
@@ -1163,8 +1159,8 @@ hipError_t launch_spf_lds(const ogs_graph& g, const ogs_unit* units, int nUnits,
   const uint4* mm = reinterpret_cast<const uint4*>(img + S.mm);
   const uint32_t lds = L.block + L.state;
   const int grid = std::max(1, std::min(nUnits, num_cus()));
-  if (!g_ldsBfsExit) flags |= kFlagLdsNoBfsExit;
-  flags |= uint32_t(g_ldsPull & 0xF) << kFlagLdsPullShift;
+  if (!opts().ldsBfsExit) flags |= kFlagLdsNoBfsExit;
+  flags |= uint32_t(opts().ldsPull & 0xF) << kFlagLdsPullShift;
   auto go = [&](auto k) {
     hipError_t a = allow_lds(k, lds);
     if (a != hipSuccess) return a;
@@ -1183,29 +1179,29 @@ hipError_t launch_spf_lds(const ogs_graph& g, const ogs_unit* units, int nUnits,
 
 // "lds_parts": prefix ranges per unit in the one-launch form (0 = by
 // regime, default); "lds_grid": its workgroups (0 = one per CU).
-int g_ldsParts = 0;
-int g_ldsGrid = 0;
+// EngineOptions::ldsParts (engine.h), default 0
+// EngineOptions::ldsGrid (engine.h), default 0
 // "lds_key16": packed 16-bit route keys on topologies of <= 16,384 nodes
 // (1, default) or u32 keys (0, A/B)
-int g_ldsKey16 = 1;
-int g_ldsTail = 1;
+// EngineOptions::ldsKey16 (engine.h), default 1
+// EngineOptions::ldsTail (engine.h), default 1
 // "lds_bfs_exit": the BFS rounds stop once every node is reached (1,
 // default) or run the empty last layer (0, A/B): C3 N = 8 shard 0.1695 vs
 // 0.1732 ms (profiles/r05_c3_ab_bfs_exit.log)
-int g_ldsBfsExit = 1;
+// EngineOptions::ldsBfsExit (engine.h), default 1
 // "lds_pull": BFS rounds pull when 4 x (chunk records of the unreached
 // nodes) <= lds_pull x (the frontier's); 0 always push (A/B)
-int g_ldsPull = 6;
+// EngineOptions::ldsPull (engine.h), default 6
 // "lds_lead": narrow units streamed before the wide group (0, default:
 // none; -1 one grid's worth of stream items on sharded builds; measured at
 // the N = 8 shard 0.1752 vs 0.1711 ms without, N = 4 0.3031 vs 0.3074 with
 // the tail change alone: profiles/r05_c3_lead_tail_ab_n*.log);
 // "lds_tail_parts": ranges per unit of the launch's last units (0 auto)
-int g_ldsLead = 0;
-int g_ldsTailParts = 0;
+// EngineOptions::ldsLead (engine.h), default 0
+// EngineOptions::ldsTailParts (engine.h), default 0
 
 bool lds_key16(const ogs_graph& g) {
-  return g_ldsKey16 && g.max_nodes > 0 && uint32_t(g.max_nodes) <= kKey16MaxNodes;
+  return opts().ldsKey16 && g.max_nodes > 0 && uint32_t(g.max_nodes) <= kKey16MaxNodes;
 }
 
 // SPF + RouteDb stream of every group in one persistent launch
@@ -1236,12 +1232,12 @@ hipError_t launch_spf_lds_routes(const ogs_graph& g, const ogs_prefix_table& pt,
   uint32_t* ready = reinterpret_cast<uint32_t*>(base + S.ready);
   const uint32_t recs = uint32_t(g.max_nodes) * uint32_t(2 + Wmax) * 4u;
   const uint32_t lds = L.block + std::max(L.state, recs);
-  const int grid = std::max(1, g_ldsGrid > 0 ? g_ldsGrid : num_cus());
+  const int grid = std::max(1, opts().ldsGrid > 0 ? opts().ldsGrid : num_cus());
   // prefix ranges per unit: "lds_parts", or 0 = by regime -- 2 when every
   // workgroup has four or more units (whole-node builds: fewer record
   // rebuilds), 4 below that (sharded builds: more items to balance a few
   // units per CU); profiles/r04_lds_store_parts_ab.log
-  const uint32_t P = g_ldsParts > 0 ? uint32_t(g_ldsParts)
+  const uint32_t P = opts().ldsParts > 0 ? uint32_t(opts().ldsParts)
                                     : (uint32_t(U) >= 4u * uint32_t(grid) ? 2u : 4u);
   const bool sharded = uint32_t(U) < 4u * uint32_t(grid);
   // the launch's last units stream in P2 > P ranges ("lds_tail" 1,
@@ -1249,12 +1245,12 @@ hipError_t launch_spf_lds_routes(const ogs_graph& g, const ogs_prefix_table& pt,
   // sharded builds the last grid's worth of ITEMS in "lds_tail_parts"
   // (auto 8); 0 every unit in P
   LdsSchedule sch{P, P, uint32_t(U), 0u, 0u};
-  if (g_ldsTail) {
+  if (opts().ldsTail) {
     if (!sharded && P < 4u) {
       sch.P2 = 4u;
       sch.U1 = uint32_t(U - std::min(U, grid));
     } else if (sharded) {
-      sch.P2 = g_ldsTailParts > 0 ? uint32_t(g_ldsTailParts) : 2u * P;
+      sch.P2 = opts().ldsTailParts > 0 ? uint32_t(opts().ldsTailParts) : 2u * P;
       const uint32_t tailUnits = std::min(uint32_t(U), (uint32_t(grid) + sch.P2 - 1u) / sch.P2);
       sch.U1 = uint32_t(U) - tailUnits;
     }
@@ -1267,14 +1263,14 @@ hipError_t launch_spf_lds_routes(const ogs_graph& g, const ogs_prefix_table& pt,
   const uint32_t Uw = n > 1 ? uint32_t(groups[0].n) : 0u;
   const uint32_t Gl = std::min(uint32_t(U), uint32_t(grid));
   if (Uw > 0u && Uw <= Gl) {
-    const uint32_t want = g_ldsLead >= 0 ? uint32_t(g_ldsLead)
+    const uint32_t want = opts().ldsLead >= 0 ? uint32_t(opts().ldsLead)
                                          : (sharded ? (uint32_t(grid) + P - 1u) / P : 0u);
     sch.lead = std::min(want, uint32_t(U) - Uw);
     sch.Uw = sch.lead ? Uw : 0u;
   }
-  if (g_routeStoreNt & 1) flags |= kFlagNtStores;
-  if (!g_ldsBfsExit) flags |= kFlagLdsNoBfsExit;
-  flags |= uint32_t(g_ldsPull & 0xF) << kFlagLdsPullShift;
+  if (opts().routeStoreNt & 1) flags |= kFlagNtStores;
+  if (!opts().ldsBfsExit) flags |= kFlagLdsNoBfsExit;
+  flags |= uint32_t(opts().ldsPull & 0xF) << kFlagLdsPullShift;
   auto go = [&](auto k, auto keyp) {
     hipError_t a = allow_lds(k, lds);
     if (a != hipSuccess) return a;

@@ -36,6 +36,7 @@
 #include "openr_gpu.h"
 #include "route_core.h"
 #include "spf_core.h"
+#include "engine.h"
 
 namespace ogs {
 
@@ -217,11 +218,8 @@ bool try_ms(const ogs_graph& g, const ogs_prefix_table& pt, int hasPrefixes,
 // unit_width option / OGS_UNIT_WIDTH env: -1 automatic, 0 generic kernel
 // only, 1 wave kernel, 2 small kernel (automatic width), 3 multi-source
 // edge-parallel kernel, 64/128/256 small kernel at that unit width.
-int g_unitWidth = [] {
-  const char* e = getenv("OGS_UNIT_WIDTH");
-  return e ? atoi(e) : -1;
-}();
-int small_unit_width() { return g_unitWidth; }
+// EngineOptions::unitWidth (engine.h), default $OGS_UNIT_WIDTH or -1
+int small_unit_width() { return opts().unitWidth; }
 
 bool use_global(const ogs_graph& g, int W, uint32_t flags);
 hipError_t launch_spf_routes_exact(const ogs_graph& g, const ogs_prefix_table* pt,

@@ -31,6 +31,7 @@
 #include "openr_gpu.h"
 #include "route_core.h"
 #include "spf_core.h"
+#include "engine.h"
 
 namespace ogs {
 
@@ -292,7 +293,7 @@ hipError_t launch_ms(const ogs_graph& g, const ogs_prefix_table& pt,
 }
 
 // "ms_group" option: 0 automatic, else force G (1, 2 or 4) when it fits.
-int g_msGroup = 0;
+// EngineOptions::msGroup (engine.h), default 0
 
 template <int W>
 bool try_ms_w(const ogs_graph& g, const ogs_prefix_table& pt, int hasPrefixes,
@@ -302,9 +303,9 @@ bool try_ms_w(const ogs_graph& g, const ogs_prefix_table& pt, int hasPrefixes,
   constexpr uint32_t kMax = 160 * 1024;
   const int N = g.max_nodes;
   for (int G : {4, 2, 1}) {
-    if (g_msGroup && G != g_msGroup) continue;
+    if (opts().msGroup && G != opts().msGroup) continue;
     const uint32_t b = ms_lds_bytes(N, G, W);
-    if (b > (G == 1 || g_msGroup ? kMax : kBudget)) continue;
+    if (b > (G == 1 || opts().msGroup ? kMax : kBudget)) continue;
     switch (G) {
       case 4: *err = launch_ms<4, W>(g, pt, hasPrefixes, units, nUnits, flags, out, stream); return true;
       case 2: *err = launch_ms<2, W>(g, pt, hasPrefixes, units, nUnits, flags, out, stream); return true;

@@ -33,6 +33,7 @@
 #include "openr_gpu.h"
 #include "route_core.h"
 #include "spf_core.h"
+#include "engine.h"
 
 namespace ogs {
 
@@ -838,9 +839,9 @@ __global__ __launch_bounds__(64 * UPB) void spf_route_wave_kernel(
 // ---- two units per wavefront: 16-bit packed words ---------------------------
 // "wave_wg_lds" option: minimum LDS bytes per workgroup (occupancy probe for
 // A/B measurements; 0 = just what the units need)
-int g_waveWgLds = 0;
+// EngineOptions::waveWgLds (engine.h), default 0
 // "wave_upb" option: units (wavefronts) per workgroup, 4, 8 or 16
-int g_waveUpb = 4;
+// EngineOptions::waveUpb (engine.h), default 4
 // "wave_opt" option: OGS_WAVE_OPT_* bits (A/B of the register paths); the
 // ds_bpermute SPF measured no faster than the LDS words (latency-bound
 // rounds), so only the register route path is on by default. (Two units per
@@ -848,7 +849,7 @@ int g_waveUpb = 4;
 // vs 10.0 us per launch, profiles/r03_ab_wave_pair.log: every wave is
 // resident from the start, so a launch lasts one wave's dependent chain --
 // and was removed in round 4.)
-int g_waveOpt = OGS_WAVE_OPT_REG_ROUTES;
+// EngineOptions::waveOpt (engine.h), default OGS_WAVE_OPT_REG_ROUTES
 
 template <int NPL, int MAXD, int UPB>
 hipError_t launch_wave_upb(const ogs_graph& g, const ogs_prefix_table& pt,
@@ -857,7 +858,7 @@ hipError_t launch_wave_upb(const ogs_graph& g, const ogs_prefix_table& pt,
                            uint32_t maxA, hipStream_t stream) {
   const int grid = (nUnits + UPB - 1) / UPB;
   size_t bytes = size_t(lds) * UPB;
-  if (bytes < size_t(g_waveWgLds)) bytes = size_t(g_waveWgLds);
+  if (bytes < size_t(opts().waveWgLds)) bytes = size_t(opts().waveWgLds);
   auto k = spf_route_wave_kernel<NPL, MAXD, UPB>;
   if (bytes > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute(
@@ -865,9 +866,9 @@ hipError_t launch_wave_upb(const ogs_graph& g, const ogs_prefix_table& pt,
         hipFuncAttributeMaxDynamicSharedMemorySize, int(bytes));
     if (e != hipSuccess) return e;
   }
-  if (g_routeStoreNt & 2) flags |= kFlagNtStores;
+  if (opts().routeStoreNt & 2) flags |= kFlagNtStores;
   hipLaunchKernelGGL(k, dim3(grid), dim3(64 * UPB), bytes, stream, g, pt,
-                     hasPrefixes, units, nUnits, flags, out, lds, maxA, uint32_t(g_waveOpt));
+                     hasPrefixes, units, nUnits, flags, out, lds, maxA, uint32_t(opts().waveOpt));
   return hipGetLastError();
 }
 
@@ -876,11 +877,11 @@ hipError_t launch_wave(const ogs_graph& g, const ogs_prefix_table& pt,
                        int hasPrefixes, const ogs_unit* units, int nUnits,
                        uint32_t flags, const ogs_spf_out& out, uint32_t lds,
                        uint32_t maxA, hipStream_t stream) {
-  if (g_waveUpb == 16 && uint64_t(lds) * 16 <= 160 * 1024) {
+  if (opts().waveUpb == 16 && uint64_t(lds) * 16 <= 160 * 1024) {
     return launch_wave_upb<NPL, MAXD, 16>(g, pt, hasPrefixes, units, nUnits, flags,
                                           out, lds, maxA, stream);
   }
-  if (g_waveUpb == 8 && uint64_t(lds) * 8 <= 160 * 1024) {
+  if (opts().waveUpb == 8 && uint64_t(lds) * 8 <= 160 * 1024) {
     return launch_wave_upb<NPL, MAXD, 8>(g, pt, hasPrefixes, units, nUnits, flags,
                                          out, lds, maxA, stream);
   }

@@ -85,6 +85,18 @@ int main(void) {
     printf("node %d: dist %u nh 0x%x\n", v, dist[v], nh[v]);
     bad |= dist[v] != want_dist[v] || nh[v] != want_nh[v];
   }
+  /* the same SPF through an execution context (ABI 6) with its own knobs */
+  ogs_ctx* ctx = NULL;
+  CHECK(ogs_ctx_create(0, &ctx));
+  CHECK(ogs_ctx_set_option(ctx, "unit_width", 0)); /* the generic kernel, this context only */
+  CHECK(ogs_memset(d_dist, 0xFF, sizeof dist, NULL));
+  CHECK(ogs_ctx_spf_routes(ctx, &g, NULL, (const ogs_unit*)d_unit, 1, 0, 1, &out, NULL));
+  CHECK(ogs_memcpy_d2h(dist, d_dist, sizeof dist, NULL));
+  CHECK(ogs_memcpy_d2h(nh, d_nh, sizeof nh, NULL));
+  CHECK(ogs_stream_sync(NULL));
+  CHECK(ogs_ctx_destroy(ctx));
+  for (int v = 0; v < 4; ++v) bad |= dist[v] != want_dist[v] || nh[v] != want_nh[v];
+  printf("context: %s\n", bad ? "MISMATCH" : "ok");
   ogs_free(d_nb);
   ogs_free(d_row);
   ogs_free(d_edges);
