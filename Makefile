@@ -59,8 +59,31 @@ $(STAMPS): $(SOBJ)
 	@mkdir -p openr_amd/lib
 	$(HIPCC) --offload-arch=$(ARCH) -shared $(SOBJ) -o $@
 
+# CPU sanitizer build (AddressSanitizer + UBSan) of the drop-in's host code
+# (tests/asan/host_asan.cpp over a host-only C-ABI stub, no device) and of
+# the oracle (build/asan/_refcpu, driven by tools/asan_oracle.py with libasan
+# preloaded); `make asan` runs both and keeps the log in profiles/
+SAN := -fsanitize=address,undefined -fno-sanitize-recover=undefined -fno-omit-frame-pointer -g -O1
+ASAN_BIN := build/asan/host_asan
+ASAN_REF := build/asan/_refcpu$(EXT)
+ASAN_LOG ?= profiles/r05_asan.log
+$(ASAN_BIN): $(HOST) $(HOST_H) tests/asan/host_asan.cpp tests/asan/ogs_stub.cpp
+	@mkdir -p build/asan
+	$(CXX) -std=c++17 $(SAN) -Wall -Wno-unused-function -Iinclude -Iopenr_amd/csrc/host \
+	  $(HOST) tests/asan/host_asan.cpp tests/asan/ogs_stub.cpp -o $@ -lpthread
+$(ASAN_REF): oracle/refcpu/refcpu.cpp oracle/refcpu/refcpu.h oracle/refcpu/bindings.cpp openr_amd/csrc/gen/topogen.h
+	@mkdir -p build/asan
+	$(CXX) -std=c++17 $(SAN) -fPIC -shared -I$(PY_INC) -I$(PYBIND_INC) \
+	  oracle/refcpu/refcpu.cpp oracle/refcpu/bindings.cpp -o $@ -lpthread
+asan: $(ASAN_BIN) $(ASAN_REF)
+	{ echo "== host_asan (drop-in host code, ASan+UBSan)"; \
+	  ASAN_OPTIONS=detect_leaks=1:abort_on_error=1 ./$(ASAN_BIN) && \
+	  echo "== oracle (refcpu, ASan+UBSan, KATs + generated RouteDbs)" && \
+	  LD_PRELOAD=$$($(CXX) -print-file-name=libasan.so):$$($(CXX) -print-file-name=libubsan.so) \
+	  ASAN_OPTIONS=detect_leaks=0:abort_on_error=1 python3 tools/asan_oracle.py; } 2>&1 | tee $(ASAN_LOG)
+
 clean:
 	rm -f $(LIB) $(MOD) $(STAMPS) $(CCONS) $(KOBJ) $(SOBJ)
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle clean stamps
+.PHONY: all oracle clean stamps asan

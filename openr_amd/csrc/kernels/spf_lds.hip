@@ -651,16 +651,12 @@ __device__ __forceinline__ void spf_lds_unit(
             }
             __syncthreads();
             // (b) the listed chunks: distance by plain stores (every finder
-            // stores the same), next hops by atomicOr. Walked transposed (as
-            // the push queue): a row's chunks are listed together and their
-            // neighbours are 8 ids apart -- consecutive lanes on them would
-            // hit 4 of the 32 LDS banks
+            // stores the same), next hops by atomicOr. (Walked in list order:
+            // the transposed walk of the push queue measured 1.8x slower here,
+            // profiles/r05_lds_stamps_n8_pulltransposed.log)
             const uint32_t no = *oc;
-            const uint32_t Mo = (no + 63u) >> 6;
-            for (uint32_t i = tid; i < 64u * Mo; i += B) {
-              const uint32_t q = (i & 63u) * Mo + (i >> 6);
-              if (q >= no) continue;
-              const uint32_t c = queue[q];
+            for (uint32_t i = tid; i < no; i += B) {
+              const uint32_t c = queue[i];
               const uint32_t v = cnode[c] & kNodeMax;
               const uint32_t b = row[v] + kLdsChunk * (c - first[v]);
               uint32_t acc[W];
