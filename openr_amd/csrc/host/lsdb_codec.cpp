@@ -294,8 +294,16 @@ std::string readIpPrefix(Reader& r, std::string* network) {  // Network.thrift:5
     else if (id == 2 && t == CT_I16) len = r.zz16();
     else r.skip(t, 2);
   }
-  if (network) *network = ipPrefixToNetworkString(addr, len);
-  return ipPrefixToString(addr, len);
+  std::string text = ipPrefixToString(addr, len);  // validates size and length
+  if (network) {
+    // no host bits set (the usual advertisement): the network prints the same
+    bool masked = true;
+    for (int bit = len; bit < int(addr.size()) * 8 && masked; ++bit) {
+      masked = !(uint8_t(addr[size_t(bit >> 3)]) & (0x80u >> (bit & 7)));
+    }
+    *network = masked ? text : ipPrefixToNetworkString(addr, len);
+  }
+  return text;
 }
 
 void readMetrics(Reader& r, PrefixMetrics& m) {  // Types.thrift:287-317
@@ -921,12 +929,11 @@ void LsdbIngest::processPublication(const std::string& area, AreaLinkStates& are
   size_t prefixKeys = 0;
   for (const auto& kv : keyVals) prefixKeys += kv.key.compare(0, 7, "prefix:") == 0;
   prefixState.reserve(prefixState.prefixes().size() + prefixKeys);
-  // the prefix changes are gathered and merged into the pending set once
-  std::vector<std::string> changed;
+  pending.reserveUpdatedPrefixes(prefixKeys);
   uint32_t prefixUpdates = 0;
   auto take = [&](LsdbKeyUpdate&& u) {
     if (u.kind == LsdbKeyUpdate::kPrefix) {
-      for (auto& n : u.changedPrefixes) changed.push_back(std::move(n));
+      for (const auto& n : u.changedPrefixes) pending.addUpdatedPrefix(n);
       ++prefixUpdates;
     } else {
       pending.apply(u);
@@ -940,9 +947,7 @@ void LsdbIngest::processPublication(const std::string& area, AreaLinkStates& are
     take(updateKeyInLsdb(area, ls, prefixState, kv->key, v, inInitialization));
   }
   for (const auto& key : expiredKeys) take(deleteKeyFromLsdb(area, ls, prefixState, key));
-  std::sort(changed.begin(), changed.end());
-  changed.erase(std::unique(changed.begin(), changed.end()), changed.end());
-  pending.applyPrefixStateChanges(std::move(changed), prefixUpdates);
+  pending.countKeys(prefixUpdates);
 }
 
 }  // namespace openr_amd

@@ -28,6 +28,7 @@
 #include <stdexcept>
 #include <string>
 #include <string_view>
+#include <unordered_set>
 #include <vector>
 
 #include "decision.h"
@@ -102,19 +103,15 @@ class DecisionPendingUpdates {
     updatedPrefixes_.insert(change.begin(), change.end());
     ++count_;
   }
-  // a publication's prefix changes at once: sorted, unique networks merged
-  // with hinted inserts (linear into an empty set), `keys` prefix keys
-  void applyPrefixStateChanges(std::vector<std::string>&& sortedUnique, uint32_t keys) {
-    auto hint = updatedPrefixes_.end();
-    for (auto& n : sortedUnique) hint = std::next(updatedPrefixes_.insert(hint, std::move(n)));
-    count_ += keys;
-  }
+  // one changed network of a publication's prefix key (counted with countKeys)
+  void addUpdatedPrefix(const std::string& network) { updatedPrefixes_.insert(network); }
+  void reserveUpdatedPrefixes(size_t n) { updatedPrefixes_.reserve(updatedPrefixes_.size() + n); }
   void countKeys(uint32_t n) { count_ += n; }
   void apply(const LsdbKeyUpdate& u);  // routes kAdjacency / kPrefix results
   void setNeedsFullRebuild() { needsFullRebuild_ = true; }
   bool needsFullRebuild() const { return needsFullRebuild_; }
   bool needsRouteUpdate() const { return needsFullRebuild_ || !updatedPrefixes_.empty(); }
-  const std::set<std::string>& updatedPrefixes() const { return updatedPrefixes_; }
+  const std::unordered_set<std::string>& updatedPrefixes() const { return updatedPrefixes_; }
   uint32_t getCount() const { return count_; }
   void reset() {
     count_ = 0;
@@ -126,7 +123,7 @@ class DecisionPendingUpdates {
   std::string myNodeName_;
   uint32_t count_{0};
   bool needsFullRebuild_{false};
-  std::set<std::string> updatedPrefixes_;
+  std::unordered_set<std::string> updatedPrefixes_;  // Decision.h:104 (unordered)
 };
 
 // One KvStore publication's key/values (rawVal nullopt = TTL-only Value).

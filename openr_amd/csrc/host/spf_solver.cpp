@@ -87,8 +87,8 @@ const std::string* PrefixState::updatePrefixInPlace(const std::string& node,
                                                     const std::string& area,
                                                     std::string&& network, PrefixEntry&& entry) {
   // PrefixState.cpp:15-38
-  auto mapIt = prefixes_.find(network);
-  if (mapIt == prefixes_.end()) mapIt = prefixes_.try_emplace(std::move(network)).first;
+  // one lookup: the key moves in only when inserted
+  auto mapIt = prefixes_.try_emplace(std::move(network)).first;
   auto& entries = mapIt->second;
   auto [it, inserted] = entries.try_emplace(NodeAndArea(node, area));
   if (!inserted && *it->second == entry) return nullptr;

@@ -277,16 +277,17 @@ bool try_ms_stream(const ogs_graph& g, const ogs_prefix_table& pt,
   spf.nh = out.nh ? out.nh
                   : reinterpret_cast<uint32_t*>(base + keyBytes + chunkBytes + distBytes);
   if (ldsSplit) {
-    // one prep launch: LDS images, weight partials, counters, route keys
-    const bool k16 = opts().routeStream == 5 && lds_key16(g);  // form 4's stream reads u32 keys
-    *err = launch_lds_prep(g, &pt, key, k16, W, nUnits, chunkScratch, stream);
-    if (*err != hipSuccess) return true;
     uint32_t* d = static_cast<uint32_t*>(spf.dist);
-    if (opts().routeStream == 5) {
+    if (opts().routeStream == 5) {  // the prep is part of that launch (or its own, A/B)
       const LdsRouteGroup one{units, nUnits, W, d, spf.nh, out};
-      *err = launch_spf_lds_routes(g, pt, key, k16, &one, 1, flags, chunkScratch, stream);
+      *err = launch_spf_lds_routes(g, pt, key, lds_key16(g), &one, 1, flags, chunkScratch,
+                                   stream);
       return true;
     }
+    // form 4: one prep launch (LDS images, weight partials, counters, u32
+    // route keys), the SPF launch, the stream launch
+    *err = launch_lds_prep(g, &pt, key, false, W, nUnits, chunkScratch, stream);
+    if (*err != hipSuccess) return true;
     *err = launch_spf_lds(g, units, nUnits, flags, W, d, spf.nh, chunkScratch, stream);
     if (*err != hipSuccess) return true;
     int parts = 1;
@@ -337,8 +338,8 @@ bool use_global(const ogs_graph& g, int W, uint32_t flags);
 
 // ogs_spf_routes_groups: every group's RouteDbs over one graph / prefix
 // table. With route_stream 5 on a large shared topology whose image fits
-// LDS for the widest group: one prep launch and ONE persistent launch for
-// all groups (widest first). Otherwise one launch_spf_routes per group, in
+// LDS for the widest group: ONE persistent launch for all groups (widest
+// first), the prep as its first items. Otherwise one launch_spf_routes per group, in
 // order on the stream -- the same outputs either way.
 hipError_t launch_spf_routes_groups(const ogs_graph& g, const ogs_prefix_table* pt,
                                     const ogs_route_group* groups, int n, uint32_t flags,
@@ -400,10 +401,7 @@ hipError_t launch_spf_routes_groups(const ogs_graph& g, const ogs_prefix_table* 
       at += round256(size_t(x.n) * x.W * Sn * 4);
     }
   }
-  const bool k16 = lds_key16(g);
-  e = launch_lds_prep(g, pt, key, k16, Wmax, U, scratch, stream);
-  if (e != hipSuccess) return e;
-  return launch_spf_lds_routes(g, *pt, key, k16, lg.data(), int(lg.size()), flags, scratch,
-                               stream);
+  return launch_spf_lds_routes(g, *pt, key, lds_key16(g), lg.data(), int(lg.size()), flags,
+                               scratch, stream);
 }
 }  // namespace ogs

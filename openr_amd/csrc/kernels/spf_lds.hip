@@ -27,6 +27,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <mutex>
 #include <cstdint>
 #include <type_traits>
 
@@ -96,7 +97,9 @@ __host__ LdsImage lds_image(const ogs_graph& g, int W) {
 // Scratch of the LDS paths, one call: images [num_topos * stride] | weight
 // min / max / asymmetry partials uint4[num_topos * nEB] (one per prep edge block) | work
 // counter (u32, 256-B line) | unit ready flags u32[nUnits] (megakernel).
-constexpr uint32_t kPrepEdges = kLdsBlock * 8;  // edges per prep edge block
+constexpr uint32_t kPrepEdgesPerThread = 2;
+constexpr uint32_t kPrepEdges = kLdsBlock * kPrepEdgesPerThread;  // edges per prep edge block
+constexpr uint32_t kPrepKeys = kLdsBlock;  // route keys per prep key block
 struct LdsScratch {
   size_t mm, ctr, ready, bytes;
   uint32_t nEB;
@@ -117,15 +120,20 @@ __host__ LdsScratch lds_scratch(const ogs_graph& g, const LdsImage& L, int nUnit
 //  blocks [0, T): topology t's row offsets, chunk -> node table (with the
 //    node's drained bit) and header {chunks}; block 0 also zeroes the work
 //    counter and the ready flags;
-//  next T * nEB: 8,192 edges each -> the 2-B edge words and the block's
+//  next T * nEB: 2,048 edges each -> the 2-B edge words and the block's
 //    min / max weight over up edges (uniform weights iff min == max);
 //  next T * nKB (when keys are asked for): 1,024 prefixes each -> the route
 //    keys of route_stream.h (pfx_key_kernel's), u32 or packed u16.
-__global__ __launch_bounds__(kLdsBlock) void lds_prep_kernel(
-    ogs_graph g, ogs_prefix_table pt, void* __restrict__ key, uint32_t key16, uint32_t nKB,
-    LdsImage L,
-    uint8_t* __restrict__ img, uint4* __restrict__ mm, uint32_t nEB, uint32_t* __restrict__ ctr,
-    uint32_t* __restrict__ ready, uint32_t nReady) {
+// One prep block `blk` (a 1024-thread workgroup): the body of both the
+// separate prep launch (lds_prep_kernel, blk = blockIdx.x) and the prep items
+// at the head of the one-launch form's queue (spf_lds_route_kernel). `ctr` /
+// `ready` (zeroed by block 0) are nullptr in the one-launch form, whose
+// counters are epoch-based.
+__device__ __forceinline__ void lds_prep_block(
+    const ogs_graph& g, const ogs_prefix_table& pt, void* __restrict__ key, uint32_t key16,
+    uint32_t nKB, const LdsImage& L, uint8_t* __restrict__ img, uint4* __restrict__ mm,
+    uint32_t nEB, uint32_t* __restrict__ ctr, uint32_t* __restrict__ ready, uint32_t nReady,
+    uint32_t blk) {
   constexpr uint32_t B = kLdsBlock;
   __shared__ uint32_t wsum[B / 64];
   __shared__ uint32_t whi[B / 64];
@@ -133,10 +141,9 @@ __global__ __launch_bounds__(kLdsBlock) void lds_prep_kernel(
   __shared__ uint32_t base;
   const uint32_t T = uint32_t(g.num_topos), tid = threadIdx.x;
   const int lane = int(tid & 63u), wave = int(tid >> 6);
-  uint32_t blk = blockIdx.x;
   if (blk < T) {
     const uint32_t t = blk;
-    if (t == 0u) {
+    if (t == 0u && ctr) {
       if (tid == 0u) *ctr = 0u;
       for (uint32_t i = tid; i < nReady; i += B) ready[i] = 0u;
     }
@@ -194,51 +201,63 @@ __global__ __launch_bounds__(kLdsBlock) void lds_prep_kernel(
     uint16_t* __restrict__ eimg = reinterpret_cast<uint16_t*>(img + size_t(t) * L.stride + 16 + L.eimg);
     const uint64_t* __restrict__ edges = g.edges + e0;
     const uint32_t e00 = eb * kPrepEdges + tid;
-    uint64_t x[8];
+    uint64_t x[kPrepEdgesPerThread];
 #pragma unroll
-    for (uint32_t k = 0; k < 8; ++k) {
+    for (uint32_t k = 0; k < kPrepEdgesPerThread; ++k) {
       const uint32_t e = e00 + k * B;
       x[k] = e < E ? edges[e] : uint64_t(OGS_EDGE_DOWN);
     }
     uint32_t lo = 0xFFFFFFFFu, hi = 0u;
     // symmetry (the BFS pull's precondition): each edge u -> v has its
     // reverse v -> u (rslot, or rslot_ext past 511) in the same up / down
-    // state; unknown (no edge_src, saturated slot without rslot_ext) = asym
+    // state; unknown (no edge_src, saturated slot without rslot_ext) = asym.
+    // A thread's edges are checked independently, so each dependent step
+    // (slot -> reverse row -> reverse edge) issues its loads for all of them
+    // at once.
     bool asym = g.edge_src == nullptr;
+    uint32_t rs[kPrepEdgesPerThread], src[kPrepEdgesPerThread];
 #pragma unroll
-    for (uint32_t k = 0; k < 8; ++k) {
+    for (uint32_t k = 0; k < kPrepEdgesPerThread; ++k) {
       const uint32_t e = e00 + k * B;
       const uint32_t w = static_cast<uint32_t>(x[k]);
       const bool down = (w & OGS_EDGE_DOWN) != 0u;
-      if (e < E) {
-        eimg[e] = uint16_t(edge_dst(w) | (down ? kDown16 : 0u));
-        if (!asym) {
-          uint32_t rs = (w >> OGS_EDGE_RSLOT_SHIFT) & OGS_EDGE_RSLOT_MASK;
-          if (rs == OGS_EDGE_RSLOT_MASK) {
-            if (g.rslot_ext) {
-              rs = g.rslot_ext[e0 + e];
-            } else {
-              asym = true;
-            }
-          }
-          const uint32_t v = edge_dst(w);
-          if (!asym && v < N) {
-            const uint32_t rb = g.row_ptr[nb + v] - e0, re = g.row_ptr[nb + v + 1] - e0;
-            if (rb + rs >= re) {
-              asym = true;
-            } else {
-              const uint32_t rw = static_cast<uint32_t>(edges[rb + rs]);
-              asym = edge_dst(rw) != g.edge_src[e0 + e] ||
-                  ((rw & OGS_EDGE_DOWN) != 0u) != down;
-            }
-          } else {
-            asym = true;
-          }
-        }
-      }
+      if (e < E) eimg[e] = uint16_t(edge_dst(w) | (down ? kDown16 : 0u));
       if (!down) {
         lo = min(lo, static_cast<uint32_t>(x[k] >> 32));
         hi = max(hi, static_cast<uint32_t>(x[k] >> 32));
+      }
+      rs[k] = (w >> OGS_EDGE_RSLOT_SHIFT) & OGS_EDGE_RSLOT_MASK;
+      src[k] = 0u;
+      if (!asym && e < E) {
+        src[k] = g.edge_src[e0 + e];
+        if (rs[k] == OGS_EDGE_RSLOT_MASK && g.rslot_ext) rs[k] = g.rslot_ext[e0 + e];
+      }
+    }
+    if (!asym) {
+      uint32_t rb[kPrepEdgesPerThread], re[kPrepEdgesPerThread];
+#pragma unroll
+      for (uint32_t k = 0; k < kPrepEdgesPerThread; ++k) {
+        const uint32_t v = edge_dst(static_cast<uint32_t>(x[k]));
+        rb[k] = re[k] = 0u;
+        if (e00 + k * B < E && v < N) {
+          rb[k] = g.row_ptr[nb + v] - e0;
+          re[k] = g.row_ptr[nb + v + 1] - e0;
+        }
+      }
+#pragma unroll
+      for (uint32_t k = 0; k < kPrepEdgesPerThread; ++k) {
+        const uint32_t e = e00 + k * B;
+        if (e >= E) continue;
+        const uint32_t w = static_cast<uint32_t>(x[k]);
+        // rs still saturated: past 511 with no rslot_ext; rb == re: v >= N
+        bool bad = rs[k] == OGS_EDGE_RSLOT_MASK && !g.rslot_ext;
+        bad = bad || rb[k] + rs[k] >= re[k];
+        if (!bad) {
+          const uint32_t rw = static_cast<uint32_t>(edges[rb[k] + rs[k]]);
+          bad = edge_dst(rw) != src[k] ||
+              ((rw & OGS_EDGE_DOWN) != 0u) != ((w & OGS_EDGE_DOWN) != 0u);
+        }
+        asym = asym || bad;
       }
     }
     const uint32_t anyAsym = __ballot(asym) != 0ull ? 1u : 0u;
@@ -266,17 +285,29 @@ __global__ __launch_bounds__(kLdsBlock) void lds_prep_kernel(
   }
   blk -= T * nEB;
   if (key && blk < T * nKB) {
-    const uint32_t t = blk / nKB, p = (blk - t * nKB) * B + tid;
+    const uint32_t t = blk / nKB, p0 = (blk - t * nKB) * kPrepKeys + tid;
     const uint32_t Sp = uint32_t(pt.max_prefixes);
-    if (p < Sp) {
-      const uint32_t k = prefix_key(pt, t, p);
-      if (key16) {
-        static_cast<uint16_t*>(key)[size_t(t) * Sp + p] = key16_of(k);
-      } else {
-        static_cast<uint32_t*>(key)[size_t(t) * Sp + p] = k;
+#pragma unroll
+    for (uint32_t j = 0; j < kPrepKeys / B; ++j) {
+      const uint32_t p = p0 + j * B;
+      if (p < Sp) {
+        const uint32_t k = prefix_key(pt, t, p);
+        if (key16) {
+          static_cast<uint16_t*>(key)[size_t(t) * Sp + p] = key16_of(k);
+        } else {
+          static_cast<uint32_t*>(key)[size_t(t) * Sp + p] = k;
+        }
       }
     }
   }
+}
+
+__global__ __launch_bounds__(kLdsBlock) void lds_prep_kernel(
+    ogs_graph g, ogs_prefix_table pt, void* __restrict__ key, uint32_t key16, uint32_t nKB,
+    LdsImage L,
+    uint8_t* __restrict__ img, uint4* __restrict__ mm, uint32_t nEB, uint32_t* __restrict__ ctr,
+    uint32_t* __restrict__ ready, uint32_t nReady) {
+  lds_prep_block(g, pt, key, key16, nKB, L, img, mm, nEB, ctr, ready, nReady, blockIdx.x);
 }
 
 #ifdef OGS_STAMPS
@@ -977,12 +1008,29 @@ struct LdsSchedule {
   uint32_t lead, Uw;   // slot -> unit: lead narrow units before the Uw wide
 };
 
+// The prep work as the first items of the same launch ("lds_fused_prep" 1,
+// default): items [0, nImg) build the topologies' LDS images and weight
+// partials (lds_prep_block's topology and edge blocks), [nImg, nPrep) the
+// route keys; an SPF item waits for every image item, a stream item for
+// every key item (both handed out before it, so the waits end). Counters
+// are monotonic with host-tracked bases (engine.h LdsCounters): ctr[0]
+// items, ctr[64] image items done, ctr[128] key items done (each on its own
+// 256-B line: the pollers do not share the item counter's); ready[u] holds
+// the launch's epoch once unit u's SPF is published. nPrep = 0: a separate
+// prep launch ran (it zeroed ctr and ready; bases 0).
+struct LdsPrep {
+  void* key;
+  uint32_t key16, nKB, nEB;
+  uint32_t nPrep, nImg;
+  uint32_t itemBase, imgBase, keyBase, epoch;
+};
+
 template <typename KeyT>
 __global__ __launch_bounds__(kLdsBlock) void spf_lds_route_kernel(
     ogs_graph g, ogs_prefix_table pt, const KeyT* __restrict__ key, LdsImage L,
-    const uint8_t* __restrict__ img, const uint4* __restrict__ mm, uint32_t nEB,
+    uint8_t* __restrict__ img, uint4* __restrict__ mm, uint32_t nEB,
     LdsGroups grps, uint32_t flags, uint32_t* __restrict__ ctr, uint32_t* __restrict__ ready,
-    LdsSchedule sch) {
+    LdsSchedule sch, LdsPrep pp) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ uint32_t qCount[6];
   __shared__ uint32_t item;
@@ -992,7 +1040,8 @@ __global__ __launch_bounds__(kLdsBlock) void spf_lds_route_kernel(
   const uint32_t G = min(U, gridDim.x);
   const uint32_t P = sch.P, P2 = sch.P2, U1 = sch.U1;
   const uint32_t headItems = U1 * (P + 1u);
-  const uint32_t total = G + headItems + (U - U1) * (P2 + 1u);
+  const uint32_t total = pp.nPrep + G + headItems + (U - U1) * (P2 + 1u);
+  bool imgOk = pp.nPrep == 0u, keysOk = pp.nPrep == 0u;  // workgroup-uniform
   auto slotUnit = [&](uint32_t b) -> uint32_t {
     if (b < sch.lead) return sch.Uw + b;
     if (b < sch.lead + sch.Uw) return b - sch.lead;
@@ -1020,11 +1069,28 @@ __global__ __launch_bounds__(kLdsBlock) void spf_lds_route_kernel(
 #ifdef OGS_STAMPS
     const uint32_t tItem = rt();
 #endif
-    if (tid == 0u) item = atomicAdd(ctr, 1u);
+    if (tid == 0u) item = atomicAdd(ctr, 1u) - pp.itemBase;
     __syncthreads();
-    const uint32_t i = item;
+    const uint32_t i0 = item;
     __syncthreads();  // every lane has read item before lane 0 takes the next
-    if (i >= total) break;
+    if (i0 >= total) break;
+    if (i0 < pp.nPrep) {  // a prep item: build, drain, release, count
+      lds_prep_block(g, pt, pp.key, pp.key16, pp.nKB, L, img, mm, pp.nEB, nullptr, nullptr, 0u,
+                     i0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+#ifdef OGS_STAMPS
+      const uint32_t tBody = rt();
+#endif
+      if (tid == 0u) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        atomicAdd(ctr + (i0 < pp.nImg ? 64 : 128), 1u);
+      }
+      OGS_ITEM_STAMP(4u, i0, tItem, tBody);
+      continue;
+    }
+    const uint32_t i = i0 - pp.nPrep;
     uint32_t gu = i, part = 0, parts = P;
     bool spf = true;
     if (i >= G) {
@@ -1053,6 +1119,24 @@ __global__ __launch_bounds__(kLdsBlock) void spf_lds_route_kernel(
     const LdsGroup& grp = grps.g[gi];
     const uint32_t u = gu - grp.base;
     if (spf) {
+#ifdef OGS_STAMPS
+      uint32_t tImg = tItem;
+#endif
+      if (!imgOk) {  // the images and weight partials are built
+        if (tid == 0u) {
+          while (__hip_atomic_load(ctr + 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) -
+                     pp.imgBase < pp.nImg) {
+            __builtin_amdgcn_s_sleep(4);
+          }
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __syncthreads();
+        imgOk = true;
+#ifdef OGS_STAMPS
+        tImg = rt();
+#endif
+      }
       const ogs_unit unit = grp.units[u];
       switch (grp.W) {
         case 1: spf_lds_unit<1>(g, L, img, mm, nEB, unit, u, flags, grp.dist, grp.nh, smem, qCount, wg, dg); break;
@@ -1066,19 +1150,27 @@ __global__ __launch_bounds__(kLdsBlock) void spf_lds_route_kernel(
       if (tid == 0u) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store(&ready[gu], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&ready[gu], pp.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
-      OGS_ITEM_STAMP(1u, gu, tItem, tItem);
+      OGS_ITEM_STAMP(1u, gu, tItem, tImg);
       continue;
     }
     if (tid == 0u) {
-      while (__hip_atomic_load(&ready[gu], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+      if (!keysOk) {  // the route keys are built
+        while (__hip_atomic_load(ctr + 128, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) -
+                   pp.keyBase < pp.nPrep - pp.nImg) {
+          __builtin_amdgcn_s_sleep(4);
+        }
+      }
+      while (__hip_atomic_load(&ready[gu], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) !=
+             pp.epoch) {
         __builtin_amdgcn_s_sleep(8);
       }
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
+    keysOk = true;
 #ifdef OGS_STAMPS
     const uint32_t tReady = rt();
 #endif
@@ -1119,7 +1211,7 @@ size_t lds_scratch_bytes(const ogs_graph& g, int W, int nUnits) {
   if (cap > 0xFFFFu || uint32_t(g.max_edges) > 0xFFFFFFu) return 0;
   const LdsImage L = lds_image(g, W);
   const uint32_t recs = uint32_t(g.max_nodes) * uint32_t(2 + W) * 4u;
-  if (L.block + std::max(L.state, recs) + 64u > 160u * 1024u) return 0;  // + static LDS
+  if (L.block + std::max(L.state, recs) + 512u > 160u * 1024u) return 0;  // + static LDS
   return lds_scratch(g, L, nUnits).bytes;
 }
 
@@ -1132,7 +1224,7 @@ hipError_t launch_lds_prep(const ogs_graph& g, const ogs_prefix_table* pt, void*
   uint8_t* base = static_cast<uint8_t*>(scratch);
   const uint32_t T = uint32_t(g.num_topos);
   const uint32_t Sp = pt ? uint32_t(pt->max_prefixes) : 0u;
-  const uint32_t nKB = key && Sp ? (Sp + kLdsBlock - 1u) / kLdsBlock : 0u;
+  const uint32_t nKB = key && Sp ? (Sp + kPrepKeys - 1u) / kPrepKeys : 0u;
   const ogs_prefix_table ptv = pt ? *pt : ogs_prefix_table{};
   hipLaunchKernelGGL(lds_prep_kernel, dim3(T * (1u + S.nEB + nKB)), dim3(kLdsBlock), 0, stream,
                      g, ptv, nKB ? key : nullptr, key16 ? 1u : 0u, nKB, L, base,
@@ -1199,6 +1291,9 @@ hipError_t launch_spf_lds(const ogs_graph& g, const ogs_unit* units, int nUnits,
 // the N = 8 shard 0.1752 vs 0.1711 ms without, N = 4 0.3031 vs 0.3074 with
 // the tail change alone: profiles/r05_c3_lead_tail_ab_n*.log);
 // "lds_tail_parts": ranges per unit of the launch's last units (0 auto)
+// "lds_fused_prep": the prep as the first items of the one-launch form (1,
+// default) or its own launch before it (0, A/B)
+// EngineOptions::ldsFusedPrep (engine.h), default 1
 // EngineOptions::ldsLead (engine.h), default 0
 // EngineOptions::ldsTailParts (engine.h), default 0
 
@@ -1207,9 +1302,10 @@ bool lds_key16(const ogs_graph& g) {
 }
 
 // SPF + RouteDb stream of every group in one persistent launch
-// (spf_lds_route_kernel) after launch_lds_prep (keys, and the image laid out
-// for the widest group; nUnits = all groups' units). groups: n <= 4, widest
-// first, each with its published dist / nh rows.
+// (spf_lds_route_kernel) whose first items are the prep (keys, and the image
+// laid out for the widest group; "lds_fused_prep" 0: a launch_lds_prep
+// before it). groups: n <= 4, widest first, each with its published dist /
+// nh rows. key16: lds_key16(g).
 hipError_t launch_spf_lds_routes(const ogs_graph& g, const ogs_prefix_table& pt,
                                  const void* key, bool key16, const LdsRouteGroup* groups,
                                  int n, uint32_t flags, void* scratch, hipStream_t stream) {
@@ -1229,9 +1325,29 @@ hipError_t launch_spf_lds_routes(const ogs_graph& g, const ogs_prefix_table& pt,
   const LdsImage L = lds_image(g, Wmax);
   const LdsScratch S = lds_scratch(g, L, U);
   uint8_t* base = static_cast<uint8_t*>(scratch);
-  const uint4* mm = reinterpret_cast<const uint4*>(base + S.mm);
+  uint4* mm = reinterpret_cast<uint4*>(base + S.mm);
   uint32_t* ctr = reinterpret_cast<uint32_t*>(base + S.ctr);
   uint32_t* ready = reinterpret_cast<uint32_t*>(base + S.ready);
+  const uint32_t T = uint32_t(g.num_topos);
+  const uint32_t Sp = uint32_t(pt.max_prefixes);
+  const uint32_t nKB = Sp ? (Sp + kPrepKeys - 1u) / kPrepKeys : 0u;
+  LdsPrep pp{const_cast<void*>(key), key16 ? 1u : 0u, nKB, S.nEB, 0u, 0u, 0u, 0u, 0u, 1u};
+  std::unique_lock<std::mutex> counterLock;
+  LdsCounters* lc = nullptr;
+  if (opts().ldsFusedPrep) {
+    // the prep as the launch's first items, counters with host bases
+    hipError_t e = lds_counters(stream, size_t(U), &lc, &counterLock);
+    if (e != hipSuccess) return e;
+    ctr = lc->dev;
+    ready = lc->dev + kLdsCounterWords;
+    pp.nImg = T * (1u + S.nEB);
+    pp.nPrep = pp.nImg + T * nKB;
+  } else {
+    // a separate prep launch (it zeroes ctr / ready in the scratch)
+    hipError_t e = launch_lds_prep(g, &pt, const_cast<void*>(key), key16, Wmax, U, scratch,
+                                   stream);
+    if (e != hipSuccess) return e;
+  }
   const uint32_t recs = uint32_t(g.max_nodes) * uint32_t(2 + Wmax) * 4u;
   const uint32_t lds = L.block + std::max(L.state, recs);
   const int grid = std::max(1, opts().ldsGrid > 0 ? opts().ldsGrid : num_cus());
@@ -1273,11 +1389,24 @@ hipError_t launch_spf_lds_routes(const ogs_graph& g, const ogs_prefix_table& pt,
   if (opts().routeStoreNt & 1) flags |= kFlagNtStores;
   if (!opts().ldsBfsExit) flags |= kFlagLdsNoBfsExit;
   flags |= uint32_t(opts().ldsPull & 0xF) << kFlagLdsPullShift;
+  if (lc) {  // bases: what the launches before this one added (all in stream order)
+    const uint32_t G0 = std::min(uint32_t(U), uint32_t(grid));
+    const uint32_t items = pp.nPrep + G0 + sch.U1 * (sch.P + 1u) +
+        (uint32_t(U) - sch.U1) * (sch.P2 + 1u);
+    pp.itemBase = lc->items;
+    pp.imgBase = lc->img;
+    pp.keyBase = lc->keys;
+    pp.epoch = ++lc->epoch;
+    if (pp.epoch == 0u) pp.epoch = ++lc->epoch;  // 0 = never published
+    lc->items += items + uint32_t(grid);  // every workgroup's last fetch fails
+    lc->img += pp.nImg;
+    lc->keys += pp.nPrep - pp.nImg;
+  }
   auto go = [&](auto k, auto keyp) {
     hipError_t a = allow_lds(k, lds);
     if (a != hipSuccess) return a;
-    hipLaunchKernelGGL(k, dim3(grid), dim3(kLdsBlock), lds, stream, g, pt, keyp, L,
-                       static_cast<const uint8_t*>(base), mm, S.nEB, G, flags, ctr, ready, sch);
+    hipLaunchKernelGGL(k, dim3(grid), dim3(kLdsBlock), lds, stream, g, pt, keyp, L, base, mm,
+                       S.nEB, G, flags, ctr, ready, sch, pp);
     return hipGetLastError();
   };
   return key16 ? go(spf_lds_route_kernel<uint16_t>, static_cast<const uint16_t*>(key))
