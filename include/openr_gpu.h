@@ -312,10 +312,7 @@ int ogs_host_free(void* hptr);
  *                 node is reached ("lds_bfs_exit" 1, default; 0 they run
  *                 the empty last layer, A/B) and pull a layer when 4 x the
  *                 unreached nodes' chunk records <= "lds_pull" x the
- *                 frontier's (6, default; 0 push only, A/B). The images,
- *                 weight partials and route keys are built by the same
- *                 launch's first items ("lds_fused_prep" 1, default; 0 a
- *                 prep launch before it, A/B). Scratch
+ *                 frontier's (6, default; 0 push only, A/B). Scratch
  *                 (prefix keys, dist/next-hop sets when out->dist / out->nh
  *                 are NULL) comes from a grow-only per-device workspace.
  *                 "route_store_nt", bits: 1 the RouteDb stream's 16-B stores

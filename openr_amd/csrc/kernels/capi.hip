@@ -194,11 +194,6 @@ static int set_option(ogs::EngineOptions& o, const char* name, int64_t value) {
     o.ldsTailParts = int(value);
     return OGS_OK;
   }
-  if (std::strcmp(name, "lds_fused_prep") == 0) {
-    if (value != 0 && value != 1) return fail(OGS_E_INVALID, "lds_fused_prep must be 0 or 1");
-    o.ldsFusedPrep = int(value);
-    return OGS_OK;
-  }
   if (std::strcmp(name, "lds_pull") == 0) {
     if (value < 0 || value > 15) return fail(OGS_E_INVALID, "lds_pull must be in [0, 15]");
     o.ldsPull = int(value);

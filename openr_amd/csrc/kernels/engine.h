@@ -48,7 +48,6 @@ struct EngineOptions {
   int ldsPull = 6;
   int ldsLead = 0;
   int ldsTailParts = 0;
-  int ldsFusedPrep = 1;  // the LDS form's prep as the launch's first items (0: own launch)
   int msGroup = 0;
   int waveWgLds = 0;
   int waveUpb = 4;
@@ -64,24 +63,10 @@ struct Workspace {
   size_t bytes = 0;
 };
 
-// Work counters of the one-launch LDS form (spf_lds_route_kernel): a device
-// line of monotonic counters {items, image items done, key items done} and
-// per-unit ready words holding the launch's epoch, never reset on the
-// device -- the host advances the bases by exactly what each launch adds, so
-// no launch needs a zeroing kernel in front of it. One per (context, stream):
-// launches on one stream run in the order their bases were taken.
-constexpr uint32_t kLdsCounterWords = 192;  // three 256-B counter lines
-struct LdsCounters {
-  uint32_t* dev = nullptr;  // [kLdsCounterWords] counter lines, then ready words
-  size_t readyWords = 0;
-  uint32_t items = 0, img = 0, keys = 0, epoch = 0;
-};
-
 struct EngineContext {
   int device = 0;
   EngineOptions opts;
   std::map<hipStream_t, Workspace> ws;  // grow-only scratch per stream
-  std::map<hipStream_t, LdsCounters> lds;
   ~EngineContext();
 };
 
@@ -103,13 +88,6 @@ inline const EngineOptions& opts() {
 // to another host thread stays valid (calls on ONE stream from several
 // threads still share the buffer: give each thread its own context).
 hipError_t workspace(size_t bytes, hipStream_t stream, void** out);
-
-// The LDS form's counters for launches on `stream` with at least `units`
-// ready words (zeroed on allocation), and the lock that must be held from
-// taking the bases to the launch (the default context's are shared by host
-// threads; a context's lock is empty).
-hipError_t lds_counters(hipStream_t stream, size_t units, LdsCounters** out,
-                        std::unique_lock<std::mutex>* lock);
 
 // RAII: binds `ctx` (and its device) to the calling thread for one call
 class BoundContext {

@@ -31,51 +31,6 @@ EngineContext::~EngineContext() {
   for (auto& [s, w] : ws) {
     if (w.ptr) (void)hipFree(w.ptr);  // device sync: no launch still reads it
   }
-  for (auto& [s, c] : lds) {
-    if (c.dev) (void)hipFree(c.dev);
-  }
-}
-
-namespace {
-std::mutex g_ldsMutex;
-std::map<std::pair<int, hipStream_t>, LdsCounters> g_lds;
-
-hipError_t ensure_counters(LdsCounters& c, size_t units) {
-  if (c.dev && c.readyWords >= units) return hipSuccess;
-  // grown: a fresh zeroed block (the old one is dropped only after the
-  // device has finished with it: hipFree synchronises)
-  const size_t words = std::max<size_t>(units, 2 * c.readyWords);
-  uint32_t* p = nullptr;
-  hipError_t e = hipMalloc(&p, (kLdsCounterWords + words) * 4);
-  if (e != hipSuccess) return e;
-  e = hipMemset(p, 0, (kLdsCounterWords + words) * 4);
-  if (e != hipSuccess) return e;
-  if (c.dev) (void)hipFree(c.dev);
-  c = LdsCounters{};
-  c.dev = p;
-  c.readyWords = words;
-  return hipSuccess;
-}
-}  // namespace
-
-hipError_t lds_counters(hipStream_t stream, size_t units, LdsCounters** out,
-                        std::unique_lock<std::mutex>* lock) {
-  if (EngineContext* c = t_ctx) {
-    LdsCounters& l = c->lds[stream];
-    hipError_t e = ensure_counters(l, units);
-    if (e != hipSuccess) return e;
-    *out = &l;
-    return hipSuccess;
-  }
-  int dev = 0;
-  hipError_t e = hipGetDevice(&dev);
-  if (e != hipSuccess) return e;
-  *lock = std::unique_lock<std::mutex>(g_ldsMutex);
-  LdsCounters& l = g_lds[{dev, stream}];
-  e = ensure_counters(l, units);
-  if (e != hipSuccess) return e;
-  *out = &l;
-  return hipSuccess;
 }
 
 hipError_t workspace(size_t bytes, hipStream_t stream, void** out) {

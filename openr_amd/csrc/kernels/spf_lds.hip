@@ -129,6 +129,21 @@ __host__ LdsScratch lds_scratch(const ogs_graph& g, const LdsImage& L, int nUnit
 // at the head of the one-launch form's queue (spf_lds_route_kernel). `ctr` /
 // `ready` (zeroed by block 0) are nullptr in the one-launch form, whose
 // counters are epoch-based.
+// Topology t's offsets: from topo_desc in one load when the caller passes
+// it, else node_base / row_ptr (a dependent pair)
+struct TopoSpan {
+  uint32_t nb, N, e0, E;
+};
+__device__ __forceinline__ TopoSpan topo_span(const ogs_graph& g, uint32_t t) {
+  if (g.topo_desc) {
+    const uint4 d = *reinterpret_cast<const uint4*>(g.topo_desc + size_t(t) * 8u);
+    return TopoSpan{d.x, d.y, d.z, d.w};
+  }
+  const uint32_t nb = g.node_base[t], N = g.node_base[t + 1] - nb;
+  const uint32_t e0 = g.row_ptr[nb];
+  return TopoSpan{nb, N, e0, g.row_ptr[nb + N] - e0};
+}
+
 __device__ __forceinline__ void lds_prep_block(
     const ogs_graph& g, const ogs_prefix_table& pt, void* __restrict__ key, uint32_t key16,
     uint32_t nKB, const LdsImage& L, uint8_t* __restrict__ img, uint4* __restrict__ mm,
@@ -147,22 +162,42 @@ __device__ __forceinline__ void lds_prep_block(
       if (tid == 0u) *ctr = 0u;
       for (uint32_t i = tid; i < nReady; i += B) ready[i] = 0u;
     }
-    const uint32_t nb = g.node_base[t];
-    const uint32_t N = g.node_base[t + 1] - nb;
+    const TopoSpan sp = topo_span(g, t);
+    const uint32_t nb = sp.nb, N = sp.N, e0 = sp.e0;
     const uint32_t* __restrict__ gRow = g.row_ptr + nb;
-    const uint32_t e0 = gRow[0];
     uint8_t* hdr = img + size_t(t) * L.stride;
     uint8_t* b8 = hdr + 16;
     uint16_t* __restrict__ cnode = reinterpret_cast<uint16_t*>(b8 + L.cnode);
     uint32_t* __restrict__ row = reinterpret_cast<uint32_t*>(b8 + L.row);
     uint16_t* __restrict__ first = reinterpret_cast<uint16_t*>(b8 + L.first);
+    // the first kPre tiles' degrees and drained bits in one round of loads
+    // (C3's 2,080 nodes are three tiles), later tiles per tile
+    constexpr uint32_t kPre = 4;
+    uint32_t deg0[kPre], tag0[kPre];
+#pragma unroll
+    for (uint32_t k = 0; k < kPre; ++k) {
+      const uint32_t v = k * B + tid;
+      deg0[k] = v < N ? gRow[v + 1] - gRow[v] : 0u;
+      tag0[k] = v < N && (g.node_flags[nb + v] & OGS_NODE_OVERLOADED) ? kDrained16 : 0u;
+    }
     if (tid == 0) base = 0u;
     for (uint32_t v = tid; v <= N; v += B) row[v] = gRow[v] - e0;
     __syncthreads();
     // chunk ids: exclusive scan of ceil(deg / 8) over the nodes, tile by tile
-    for (uint32_t t0 = 0; t0 < N; t0 += B) {
+    uint32_t ti = 0;
+    for (uint32_t t0 = 0; t0 < N; t0 += B, ++ti) {
       const uint32_t v = t0 + tid;
-      const uint32_t deg = v < N ? gRow[v + 1] - gRow[v] : 0u;
+      uint32_t deg = 0u, tag = 0u;
+      if (ti < kPre) {
+#pragma unroll
+        for (uint32_t k = 0; k < kPre; ++k) {
+          deg = ti == k ? deg0[k] : deg;
+          tag = ti == k ? tag0[k] : tag;
+        }
+      } else if (v < N) {
+        deg = gRow[v + 1] - gRow[v];
+        tag = (g.node_flags[nb + v] & OGS_NODE_OVERLOADED) ? kDrained16 : 0u;
+      }
       const uint32_t n = (deg + kLdsChunk - 1u) / kLdsChunk;
       uint32_t inc = n;
 #pragma unroll
@@ -179,25 +214,24 @@ __device__ __forceinline__ void lds_prep_block(
       const uint32_t at = off + inc - n;
       if (v < N) {
         first[v] = uint16_t(at);
-        const uint32_t tag = (g.node_flags[nb + v] & OGS_NODE_OVERLOADED) ? kDrained16 : 0u;
         for (uint32_t k = 0; k < n; ++k) cnode[at + k] = uint16_t(v | tag);
       }
       __syncthreads();
     }
     if (tid == 0) {
       uint32_t* h = reinterpret_cast<uint32_t*>(hdr);
-      h[0] = base;
-      h[1] = h[2] = h[3] = 0u;
+      h[0] = base;  // chunk records
+      h[1] = N;
+      h[2] = e0;
+      h[3] = 0u;
     }
     return;
   }
   blk -= T;
   if (blk < T * nEB) {
     const uint32_t t = blk / nEB, eb = blk - t * nEB;
-    const uint32_t nb = g.node_base[t];
-    const uint32_t N = g.node_base[t + 1] - nb;
-    const uint32_t e0 = g.row_ptr[nb];
-    const uint32_t E = g.row_ptr[nb + N] - e0;
+    const TopoSpan sp = topo_span(g, t);
+    const uint32_t nb = sp.nb, N = sp.N, e0 = sp.e0, E = sp.E;
     uint16_t* __restrict__ eimg = reinterpret_cast<uint16_t*>(img + size_t(t) * L.stride + 16 + L.eimg);
     const uint64_t* __restrict__ edges = g.edges + e0;
     const uint32_t e00 = eb * kPrepEdges + tid;
@@ -393,6 +427,53 @@ struct LdsStamps {
 };
 #endif
 
+// lds_stage: topology t's image (built by the prep launch) into this
+// workgroup's LDS, with its header {chunk records, nodes, first edge} and
+// the edge blocks' weight / symmetry partials -- every load of it issued in
+// one round (eight 16-B loads in flight per lane: C3's 113 KB image is one
+// batch), no dependent global load after the copy.
+__device__ __forceinline__ void lds_stage(const ogs_graph& g, const LdsImage& L,
+                                          const uint8_t* __restrict__ img,
+                                          const uint4* __restrict__ mm, uint32_t nEB, uint32_t t,
+                                          char* blk, LdsWg& wg) {
+  constexpr uint32_t B = kLdsBlock;
+  const uint32_t tid = threadIdx.x;
+  __syncthreads();  // the previous unit's state reads are done
+  const uint8_t* hdr = img + size_t(t) * L.stride;
+  const uint4* src = reinterpret_cast<const uint4*>(hdr + 16);
+  uint4* dst = reinterpret_cast<uint4*>(blk);
+  const uint4 h = *reinterpret_cast<const uint4*>(hdr);
+  uint32_t lo = 0xFFFFFFFFu, hi = 0u, asym = 0u;
+  for (uint32_t b = 0; b < nEB; ++b) {
+    const uint4 x = mm[size_t(t) * nEB + b];
+    lo = min(lo, x.x);
+    hi = max(hi, x.y);
+    asym |= x.z;
+  }
+  const uint32_t n16 = L.block / 16u;
+  for (uint32_t i0 = 0; i0 < n16; i0 += 8u * B) {
+    uint4 x[8];
+#pragma unroll
+    for (uint32_t k = 0; k < 8u; ++k) {
+      const uint32_t i = i0 + k * B + tid;
+      x[k] = i < n16 ? src[i] : make_uint4(0u, 0u, 0u, 0u);
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < 8u; ++k) {
+      const uint32_t i = i0 + k * B + tid;
+      if (i < n16) dst[i] = x[k];
+    }
+  }
+  wg.C = h.x;
+  wg.N = h.y;
+  wg.e0 = h.z;
+  wg.uniform = lo == hi ? 1u : 0u;  // every up edge of this weight
+  wg.w0 = lo;
+  wg.sym = asym ? 0u : 1u;
+  wg.staged = t;
+  __syncthreads();
+}
+
 // spf_lds_unit: the SPF of unit u (index into the launch's dist / nh rows)
 // by this workgroup, its topology's image staged on first use and kept.
 // smem: the dynamic LDS (image block, then the unit's state laid out by L,
@@ -426,46 +507,7 @@ __device__ __forceinline__ void spf_lds_unit(
   uint32_t& e0 = wg.e0;
   auto mark = [&](uint32_t slot) { dg.mark(slot); };
   {
-    if (unit.topo != staged) {
-      __syncthreads();  // the previous unit's state reads are done
-      const uint8_t* hdr = img + size_t(unit.topo) * L.stride;
-      const uint4* src = reinterpret_cast<const uint4*>(hdr + 16);
-      uint4* dst = reinterpret_cast<uint4*>(blk);
-      // eight 16-B loads in flight per lane before their LDS stores (one
-      // L2 round trip for C3's 113 KB image instead of one per 16 KB)
-      const uint32_t n16 = L.block / 16u;
-      for (uint32_t i0 = 0; i0 < n16; i0 += 8u * B) {
-        uint4 x[8];
-#pragma unroll
-        for (uint32_t k = 0; k < 8u; ++k) {
-          const uint32_t i = i0 + k * B + tid;
-          x[k] = i < n16 ? src[i] : make_uint4(0u, 0u, 0u, 0u);
-        }
-#pragma unroll
-        for (uint32_t k = 0; k < 8u; ++k) {
-          const uint32_t i = i0 + k * B + tid;
-          if (i < n16) dst[i] = x[k];
-        }
-      }
-      const uint32_t* h = reinterpret_cast<const uint32_t*>(hdr);
-      C = h[0];
-      // weight min / max of the up edges, from the prep blocks' partials
-      uint32_t lo = 0xFFFFFFFFu, hi = 0u, asym = 0u;
-      for (uint32_t b = 0; b < nEB; ++b) {
-        const uint4 x = mm[size_t(unit.topo) * nEB + b];
-        lo = min(lo, x.x);
-        hi = max(hi, x.y);
-        asym |= x.z;
-      }
-      uniform = lo == hi ? 1u : 0u;  // every up edge of this weight
-      w0 = lo;
-      wg.sym = asym ? 0u : 1u;
-      const uint32_t nb = g.node_base[unit.topo];
-      N = g.node_base[unit.topo + 1] - nb;
-      e0 = g.row_ptr[nb];
-      staged = unit.topo;
-      __syncthreads();
-    }
+    if (unit.topo != staged) lds_stage(g, L, img, mm, nEB, unit.topo, blk, wg);
     mark(0);  // staging (the first unit only)
     const uint64_t* __restrict__ edges = g.edges + e0;
     const uint32_t wc = hop ? 1u : w0;  // the weight when it is one constant
@@ -1008,29 +1050,12 @@ struct LdsSchedule {
   uint32_t lead, Uw;   // slot -> unit: lead narrow units before the Uw wide
 };
 
-// The prep work as the first items of the same launch ("lds_fused_prep" 1,
-// default): items [0, nImg) build the topologies' LDS images and weight
-// partials (lds_prep_block's topology and edge blocks), [nImg, nPrep) the
-// route keys; an SPF item waits for every image item, a stream item for
-// every key item (both handed out before it, so the waits end). Counters
-// are monotonic with host-tracked bases (engine.h LdsCounters): ctr[0]
-// items, ctr[64] image items done, ctr[128] key items done (each on its own
-// 256-B line: the pollers do not share the item counter's); ready[u] holds
-// the launch's epoch once unit u's SPF is published. nPrep = 0: a separate
-// prep launch ran (it zeroed ctr and ready; bases 0).
-struct LdsPrep {
-  void* key;
-  uint32_t key16, nKB, nEB;
-  uint32_t nPrep, nImg;
-  uint32_t itemBase, imgBase, keyBase, epoch;
-};
-
 template <typename KeyT>
 __global__ __launch_bounds__(kLdsBlock) void spf_lds_route_kernel(
     ogs_graph g, ogs_prefix_table pt, const KeyT* __restrict__ key, LdsImage L,
-    uint8_t* __restrict__ img, uint4* __restrict__ mm, uint32_t nEB,
+    const uint8_t* __restrict__ img, const uint4* __restrict__ mm, uint32_t nEB,
     LdsGroups grps, uint32_t flags, uint32_t* __restrict__ ctr, uint32_t* __restrict__ ready,
-    LdsSchedule sch, LdsPrep pp) {
+    LdsSchedule sch) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ uint32_t qCount[6];
   __shared__ uint32_t item;
@@ -1040,8 +1065,7 @@ __global__ __launch_bounds__(kLdsBlock) void spf_lds_route_kernel(
   const uint32_t G = min(U, gridDim.x);
   const uint32_t P = sch.P, P2 = sch.P2, U1 = sch.U1;
   const uint32_t headItems = U1 * (P + 1u);
-  const uint32_t total = pp.nPrep + G + headItems + (U - U1) * (P2 + 1u);
-  bool imgOk = pp.nPrep == 0u, keysOk = pp.nPrep == 0u;  // workgroup-uniform
+  const uint32_t total = G + headItems + (U - U1) * (P2 + 1u);
   auto slotUnit = [&](uint32_t b) -> uint32_t {
     if (b < sch.lead) return sch.Uw + b;
     if (b < sch.lead + sch.Uw) return b - sch.lead;
@@ -1065,32 +1089,25 @@ __global__ __launch_bounds__(kLdsBlock) void spf_lds_route_kernel(
 #else
 #define OGS_ITEM_STAMP(kind, unit, t0, t1)
 #endif
+  // one topology (every unit's): its image is staged while the first item
+  // is fetched, the counter's round trip hidden behind the image loads
+  bool preStage = g.num_topos == 1;
   for (;;) {
 #ifdef OGS_STAMPS
     const uint32_t tItem = rt();
 #endif
-    if (tid == 0u) item = atomicAdd(ctr, 1u) - pp.itemBase;
+    uint32_t fetched = 0u;
+    if (tid == 0u) fetched = atomicAdd(ctr, 1u);
+    if (preStage) {
+      lds_stage(g, L, img, mm, nEB, 0u, smem, wg);
+      preStage = false;
+    }
+    if (tid == 0u) item = fetched;
     __syncthreads();
     const uint32_t i0 = item;
     __syncthreads();  // every lane has read item before lane 0 takes the next
     if (i0 >= total) break;
-    if (i0 < pp.nPrep) {  // a prep item: build, drain, release, count
-      lds_prep_block(g, pt, pp.key, pp.key16, pp.nKB, L, img, mm, pp.nEB, nullptr, nullptr, 0u,
-                     i0);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-#ifdef OGS_STAMPS
-      const uint32_t tBody = rt();
-#endif
-      if (tid == 0u) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        atomicAdd(ctr + (i0 < pp.nImg ? 64 : 128), 1u);
-      }
-      OGS_ITEM_STAMP(4u, i0, tItem, tBody);
-      continue;
-    }
-    const uint32_t i = i0 - pp.nPrep;
+    const uint32_t i = i0;
     uint32_t gu = i, part = 0, parts = P;
     bool spf = true;
     if (i >= G) {
@@ -1119,24 +1136,6 @@ __global__ __launch_bounds__(kLdsBlock) void spf_lds_route_kernel(
     const LdsGroup& grp = grps.g[gi];
     const uint32_t u = gu - grp.base;
     if (spf) {
-#ifdef OGS_STAMPS
-      uint32_t tImg = tItem;
-#endif
-      if (!imgOk) {  // the images and weight partials are built
-        if (tid == 0u) {
-          while (__hip_atomic_load(ctr + 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) -
-                     pp.imgBase < pp.nImg) {
-            __builtin_amdgcn_s_sleep(4);
-          }
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        __syncthreads();
-        imgOk = true;
-#ifdef OGS_STAMPS
-        tImg = rt();
-#endif
-      }
       const ogs_unit unit = grp.units[u];
       switch (grp.W) {
         case 1: spf_lds_unit<1>(g, L, img, mm, nEB, unit, u, flags, grp.dist, grp.nh, smem, qCount, wg, dg); break;
@@ -1150,27 +1149,19 @@ __global__ __launch_bounds__(kLdsBlock) void spf_lds_route_kernel(
       if (tid == 0u) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store(&ready[gu], pp.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&ready[gu], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
-      OGS_ITEM_STAMP(1u, gu, tItem, tImg);
+      OGS_ITEM_STAMP(1u, gu, tItem, tItem);
       continue;
     }
     if (tid == 0u) {
-      if (!keysOk) {  // the route keys are built
-        while (__hip_atomic_load(ctr + 128, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) -
-                   pp.keyBase < pp.nPrep - pp.nImg) {
-          __builtin_amdgcn_s_sleep(4);
-        }
-      }
-      while (__hip_atomic_load(&ready[gu], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) !=
-             pp.epoch) {
+      while (__hip_atomic_load(&ready[gu], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
         __builtin_amdgcn_s_sleep(8);
       }
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
-    keysOk = true;
 #ifdef OGS_STAMPS
     const uint32_t tReady = rt();
 #endif
@@ -1291,9 +1282,6 @@ hipError_t launch_spf_lds(const ogs_graph& g, const ogs_unit* units, int nUnits,
 // the N = 8 shard 0.1752 vs 0.1711 ms without, N = 4 0.3031 vs 0.3074 with
 // the tail change alone: profiles/r05_c3_lead_tail_ab_n*.log);
 // "lds_tail_parts": ranges per unit of the launch's last units (0 auto)
-// "lds_fused_prep": the prep as the first items of the one-launch form (1,
-// default) or its own launch before it (0, A/B)
-// EngineOptions::ldsFusedPrep (engine.h), default 1
 // EngineOptions::ldsLead (engine.h), default 0
 // EngineOptions::ldsTailParts (engine.h), default 0
 
@@ -1302,10 +1290,9 @@ bool lds_key16(const ogs_graph& g) {
 }
 
 // SPF + RouteDb stream of every group in one persistent launch
-// (spf_lds_route_kernel) whose first items are the prep (keys, and the image
-// laid out for the widest group; "lds_fused_prep" 0: a launch_lds_prep
-// before it). groups: n <= 4, widest first, each with its published dist /
-// nh rows. key16: lds_key16(g).
+// (spf_lds_route_kernel) after launch_lds_prep (keys, and the image laid out
+// for the widest group; nUnits = all groups' units). groups: n <= 4, widest
+// first, each with its published dist / nh rows. key16: lds_key16(g).
 hipError_t launch_spf_lds_routes(const ogs_graph& g, const ogs_prefix_table& pt,
                                  const void* key, bool key16, const LdsRouteGroup* groups,
                                  int n, uint32_t flags, void* scratch, hipStream_t stream) {
@@ -1325,29 +1312,12 @@ hipError_t launch_spf_lds_routes(const ogs_graph& g, const ogs_prefix_table& pt,
   const LdsImage L = lds_image(g, Wmax);
   const LdsScratch S = lds_scratch(g, L, U);
   uint8_t* base = static_cast<uint8_t*>(scratch);
-  uint4* mm = reinterpret_cast<uint4*>(base + S.mm);
+  const uint4* mm = reinterpret_cast<const uint4*>(base + S.mm);
   uint32_t* ctr = reinterpret_cast<uint32_t*>(base + S.ctr);
   uint32_t* ready = reinterpret_cast<uint32_t*>(base + S.ready);
-  const uint32_t T = uint32_t(g.num_topos);
-  const uint32_t Sp = uint32_t(pt.max_prefixes);
-  const uint32_t nKB = Sp ? (Sp + kPrepKeys - 1u) / kPrepKeys : 0u;
-  LdsPrep pp{const_cast<void*>(key), key16 ? 1u : 0u, nKB, S.nEB, 0u, 0u, 0u, 0u, 0u, 1u};
-  std::unique_lock<std::mutex> counterLock;
-  LdsCounters* lc = nullptr;
-  if (opts().ldsFusedPrep) {
-    // the prep as the launch's first items, counters with host bases
-    hipError_t e = lds_counters(stream, size_t(U), &lc, &counterLock);
-    if (e != hipSuccess) return e;
-    ctr = lc->dev;
-    ready = lc->dev + kLdsCounterWords;
-    pp.nImg = T * (1u + S.nEB);
-    pp.nPrep = pp.nImg + T * nKB;
-  } else {
-    // a separate prep launch (it zeroes ctr / ready in the scratch)
-    hipError_t e = launch_lds_prep(g, &pt, const_cast<void*>(key), key16, Wmax, U, scratch,
-                                   stream);
-    if (e != hipSuccess) return e;
-  }
+  // the prep launch: images, weight partials, zeroed counters, route keys
+  hipError_t e = launch_lds_prep(g, &pt, const_cast<void*>(key), key16, Wmax, U, scratch, stream);
+  if (e != hipSuccess) return e;
   const uint32_t recs = uint32_t(g.max_nodes) * uint32_t(2 + Wmax) * 4u;
   const uint32_t lds = L.block + std::max(L.state, recs);
   const int grid = std::max(1, opts().ldsGrid > 0 ? opts().ldsGrid : num_cus());
@@ -1389,24 +1359,11 @@ hipError_t launch_spf_lds_routes(const ogs_graph& g, const ogs_prefix_table& pt,
   if (opts().routeStoreNt & 1) flags |= kFlagNtStores;
   if (!opts().ldsBfsExit) flags |= kFlagLdsNoBfsExit;
   flags |= uint32_t(opts().ldsPull & 0xF) << kFlagLdsPullShift;
-  if (lc) {  // bases: what the launches before this one added (all in stream order)
-    const uint32_t G0 = std::min(uint32_t(U), uint32_t(grid));
-    const uint32_t items = pp.nPrep + G0 + sch.U1 * (sch.P + 1u) +
-        (uint32_t(U) - sch.U1) * (sch.P2 + 1u);
-    pp.itemBase = lc->items;
-    pp.imgBase = lc->img;
-    pp.keyBase = lc->keys;
-    pp.epoch = ++lc->epoch;
-    if (pp.epoch == 0u) pp.epoch = ++lc->epoch;  // 0 = never published
-    lc->items += items + uint32_t(grid);  // every workgroup's last fetch fails
-    lc->img += pp.nImg;
-    lc->keys += pp.nPrep - pp.nImg;
-  }
   auto go = [&](auto k, auto keyp) {
     hipError_t a = allow_lds(k, lds);
     if (a != hipSuccess) return a;
-    hipLaunchKernelGGL(k, dim3(grid), dim3(kLdsBlock), lds, stream, g, pt, keyp, L, base, mm,
-                       S.nEB, G, flags, ctr, ready, sch, pp);
+    hipLaunchKernelGGL(k, dim3(grid), dim3(kLdsBlock), lds, stream, g, pt, keyp, L,
+                       static_cast<const uint8_t*>(base), mm, S.nEB, G, flags, ctr, ready, sch);
     return hipGetLastError();
   };
   return key16 ? go(spf_lds_route_kernel<uint16_t>, static_cast<const uint16_t*>(key))

@@ -81,8 +81,7 @@ def _c3(product, names, ppn=100):
                                   dict(route_stream=5, lds_lead=100, lds_tail_parts=16),
                                   dict(route_stream=5, lds_tail_parts=3, lds_lead=7, lds_grid=64),
                                   dict(route_stream=5, lds_pull=0),
-                                  dict(route_stream=5, lds_pull=15, lds_lead=-1),
-                                  dict(route_stream=5, lds_fused_prep=0)])
+                                  dict(route_stream=5, lds_pull=15, lds_lead=-1)])
 def test_c3_full_every_source_matches_oracle(product, opts):
     """C3-full at bench size (2,080 sources x 208k prefixes) through
     bench.py's two-stream width-group launches: every source's digest equals
@@ -103,7 +102,7 @@ def test_c3_full_every_source_matches_oracle(product, opts):
     lib = capi.load()
     defaults = dict(frontier_block=0, frontier_parts=0, frontier_parts_wide=0, route_stream=5,
                     lds_parts=0, lds_grid=0, lds_key16=1, lds_tail=1, lds_lead=0,
-                    lds_bfs_exit=1, lds_tail_parts=0, lds_pull=6, lds_fused_prep=1)
+                    lds_bfs_exit=1, lds_tail_parts=0, lds_pull=6)
     for k, v in opts.items():
         capi.check(lib, lib.ogs_set_option(k.encode(), v), k)
     try:

@@ -77,7 +77,6 @@ def _oracle(oracle, uniform=False):
                                      dict(route_stream=5, lds_bfs_exit=0, lds_tail_parts=9),
                                      dict(route_stream=5, lds_parts=3, lds_lead=2),
                                      dict(route_stream=5, lds_pull=0), dict(route_stream=5, lds_pull=15),
-                                     dict(route_stream=5, lds_fused_prep=0),
                                      dict(route_stream=2, spf_queue=0),
                                      dict(route_stream=1, spf_queue=0)])
 def test_deep_line_with_island_batch(product, oracle, options, uniform):
@@ -106,7 +105,6 @@ def test_deep_line_with_island_batch(product, oracle, options, uniform):
         lib.ogs_set_option(b"lds_lead", 0)
         lib.ogs_set_option(b"lds_tail_parts", 0)
         lib.ogs_set_option(b"lds_pull", 6)
-        lib.ogs_set_option(b"lds_fused_prep", 1)
     want = _oracle(oracle, uniform)
     # the island's anycast member is unreachable from the line: the line's
     # end must be the prefix's only route source

@@ -363,7 +363,6 @@ def _batch_dbs(product, kind, opts, srcs, enable_v4, brs, **options):
         lib.ogs_set_option(b"lds_bfs_exit", 1)
         lib.ogs_set_option(b"lds_tail_parts", 0)
         lib.ogs_set_option(b"lds_pull", 6)
-        lib.ogs_set_option(b"lds_fused_prep", 1)
         lib.ogs_set_option(b"frontier_parts", 0)
         lib.ogs_set_option(b"frontier_parts_wide", 0)
         lib.ogs_set_option(b"spf_frontier", 1)

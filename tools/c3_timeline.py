@@ -1,11 +1,10 @@
 """Item timeline of the C3 one-launch form (spf_lds_route_kernel) from the
 diagnostic build (`make stamps`, OGS_LIB=openr_amd/lib/libopenr_gpu_stamps.so):
-per workgroup every item {SPF | stream | join | prep, unit, start, ready, end}
-on the 100 MHz realtime clock. Prints where one launch's time goes: the prep
-items (lds_fused_prep 1), SPFs' wait for the images, the SPF head (launch
-start -> a workgroup's first stream item), stream items' wait for their SPF,
-busy stream time, and each workgroup's idle tail (its last item's end -> the
-launch's end). Usage:
+per workgroup every item {SPF | stream | join, unit, start, ready, end} on the
+100 MHz realtime clock. Prints where one launch's time goes: the SPF head
+(launch start -> a workgroup's first stream item), stream items' wait for
+their SPF (the first one's too), busy stream time per width group, and each
+workgroup's idle tail (its last item's end -> the launch's end). Usage:
   python tools/c3_timeline.py [--as-rank r/N] [--opt name=value ...]"""
 import argparse
 import ctypes
@@ -17,7 +16,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-KINDS = {1: "spf", 2: "stream", 3: "join", 4: "prep"}
+KINDS = {1: "spf", 2: "stream", 3: "join"}
 
 
 def main():
@@ -58,8 +57,7 @@ def main():
         t1 = max(raw[w, :, 3].max() for w in wgs)
         us = lambda x: x / 100.0  # noqa: E731
         head, waits, busy, idle, spf_t, n_items = [], [], [], [], [], []
-        first_wait, img_wait, prep_end, prep_body, prep_rel = [], [], [], [], []
-        prep_items = {}
+        first_wait = []
         item_us = {k: [] for k in KINDS.values()}
         uw = launches[0]["U"] if len(launches) > 1 else 0  # wide group first
         by_group = {"stream wide": [], "stream narrow": [], "spf wide": [], "spf narrow": []}
@@ -71,18 +69,10 @@ def main():
                 item_us[KINDS[int(k)]].append(us(row[3] - row[1]))
                 unit = int(row[0]) & 0x0FFFFFFF
                 grp = "wide" if unit < uw else "narrow"
-                if int(k) in (1, 2, 3):
-                    by_group[("spf " if int(k) == 1 else "stream ") + grp].append(
-                        us(row[3] - (row[2] if int(k) != 1 else row[1])))
+                by_group[("spf " if int(k) == 1 else "stream ") + grp].append(
+                    us(row[3] - (row[2] if int(k) != 1 else row[1])))
             sp = it[kinds == 1]
             spf_t.append(us((sp[:, 3] - sp[:, 1]).sum()) if len(sp) else 0.0)
-            img_wait.extend(us(sp[:, 2] - sp[:, 1]))
-            pr = it[kinds == 4]
-            prep_end.extend(us(pr[:, 3] - t0))
-            prep_body.extend(us(pr[:, 2] - pr[:, 1]))
-            prep_rel.extend(us(pr[:, 3] - pr[:, 2]))
-            for row in pr:
-                prep_items[int(row[0]) & 0x0FFFFFFF] = (us(row[1] - t0), us(row[2] - row[1]))
             st = it[(kinds == 2) | (kinds == 3)]
             head.append(us(st[:, 1].min() - t0) if len(st) else us(t1 - t0))
             waits.append(us((st[:, 2] - st[:, 1]).sum()) if len(st) else 0.0)
@@ -94,18 +84,11 @@ def main():
         pct = lambda x, q: float(np.percentile(x, q))  # noqa: E731
         print(f"rep {rep}: launch {us(t1 - t0):.1f} us over {len(wgs)} workgroups, "
               f"items/wg med {np.median(n_items):.0f} max {max(n_items)}")
-        rows = [("spf time", spf_t), ("spf image wait", img_wait)]
-        if prep_end:
-            rows += [("prep item end", prep_end), ("prep body", prep_body),
-                     ("prep release", prep_rel)]
-        for name, x in rows + [("first stream start", head),
+        for name, x in [("spf time", spf_t), ("first stream start", head),
                         ("first item wait", first_wait),
                         ("stream wait", waits), ("stream busy", busy), ("tail idle", idle)]:
             print(f"   {name:18s} mean {np.mean(x):6.1f}  p10 {pct(x, 10):6.1f}  "
                   f"med {pct(x, 50):6.1f}  p90 {pct(x, 90):6.1f}  max {max(x):6.1f} us")
-        if prep_items:
-            print("   prep items (index: start, body us): " + ", ".join(
-                f"{i}: {a:.1f} {b:.1f}" for i, (a, b) in sorted(prep_items.items())[:20]))
         for k, x in by_group.items():
             if x:
                 print(f"   {k:14s} n={len(x):5d}  med {np.median(x):6.1f}  "
