@@ -17,6 +17,11 @@
 #   timeline:<as-rank>[:o=v+..] C3 one-launch item timeline (tools/c3_timeline.py)
 #   ab:<as-rank>:<A>:<B>[:..] in-process C3 option A/B (tools/c3_opt_ab.py), variants
 #                             are name=value lists joined by '+'
+#   benchab:<config>:<A>:<B>[:..] any bench.py config, variants interleaved twice, each
+#                             a '+'-joined list of engine options name=value (--opt),
+#                             bench flags --name=value written name=value with a
+#                             leading '-' (e.g. -c5-streams=2), or lib=base
+#                             (openr_amd/lib/libopenr_gpu_base.so, tools/build_ab_base.sh)
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -77,6 +82,27 @@ for recipe in "$@"; do
       for v in "${parts[@]:1}"; do vs+=("${v//+/,}"); done
       step "ab_$n" 600 python -u tools/c3_opt_ab.py --pairs 4 --as-rank "$rank" "${vs[@]}"
       grep '^{' "gpurun_out/ab_$n.log" | cut -c1-200 ;;
+    benchab)
+      IFS=: read -r -a parts <<< "$rest"
+      cfg=${parts[0]}
+      for rep in 1 2; do
+        vi=0
+        for v in "${parts[@]:1}"; do
+          vi=$((vi + 1)); args=(); lib=""
+          for kv in ${v//+/ }; do
+            case $kv in
+              lib=base) lib=openr_amd/lib/libopenr_gpu_base.so ;;
+              -*) args+=("-${kv%%=*}" "${kv#*=}") ;;
+              *) args+=(--opt "$kv") ;;
+            esac
+          done
+          log="gpurun_out/benchab_${n}_${cfg}_${vi}_$rep.log"
+          OGS_LIB=$lib timeout -k 10 300 python3 bench.py --config "$cfg" --steps 10 --warmup 2 \
+            --no-cpu-baseline "${args[@]}" > "$log" 2>&1
+          rc=$?; [ $rc -eq 0 ] || { tail -5 "$log"; exit $rc; }
+          echo "$cfg [$v] rep $rep: $(grep '^{' "$log" | tail -1 | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["unit"], d["ms_per_step"], "ms", {k: v for k, v in d.items() if k.endswith("digest") or k == "golden"})')"
+        done
+      done ;;
     *)
       echo "unknown recipe $recipe"; exit 2 ;;
   esac

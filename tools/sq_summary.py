@@ -1,4 +1,4 @@
-"""SQ counter pass summary (tools/gpu_sq.sh, tools/gpu_c2_evidence.sh): per
+"""SQ counter pass summary (tools/gpu.sh sq / sqlds recipes): per
 kernel the average per dispatch of each counter plus the derived wave-cycle
 split. Usage: python3 tools/sq_summary.py <counter_collection.csv> <match>
 <out.json> [commit]"""
