@@ -1292,6 +1292,9 @@ def main():
     ap.add_argument("--no-g1", action="store_true",
                     help="skip the 20,000-node WAN sub-line (global-state SPF path)")
     ap.add_argument("--no-c2", action="store_true", help="skip the C2 topology-batch sub-line")
+    ap.add_argument("--host-lines-last", action="store_true",
+                    help="run the C1 / G1 single-source host builds after the C3 line and its "
+                         "host sub-lines (A/B of the heap state they leave; default: before)")
     ap.add_argument("--c2-steps", type=int, default=50)
     ap.add_argument("--c2-warmup", type=int, default=5)
     ap.add_argument("--as-rank", default=None, metavar="r/N",
@@ -1397,6 +1400,24 @@ def main():
             raise SystemExit(1)
         return
 
+    # the single-source host builds (C1, G1: the drop-in's materialisation of
+    # std::map / std::string routes) run first by default: after the C3 host
+    # sub-lines (hundreds of MB of route maps built and freed) the same G1
+    # build measures 17-21 ms instead of 11 (heap state, not the build;
+    # profiles/r05_g1_heap_ab.log, --host-lines-last)
+    host = {}
+
+    def host_lines():
+        if rank != 0:
+            return
+        if not args.no_c1:
+            host["c1_single_source"] = run_c1(args, rank)
+        if not args.no_g1:
+            log("g1 large WAN ...")
+            host["g1_large_wan"] = run_g1(args, rank)
+
+    if not args.host_lines_last:
+        host_lines()
     # headline: the north-star config, C3 fabric all-sources (whole-node
     # builds/s), sources sharded over the ranks; sub-lines after it
     line = run_c3(args, torch, dist, rank, world, local_rank)
@@ -1405,12 +1426,10 @@ def main():
         if rank == 0:
             line["c2_topology_batch"] = {k: c2[k] for k in SUB_KEYS["c2_topology_batch"]
                                          if k in c2}
+    if args.host_lines_last:
+        host_lines()
     if rank == 0:
-        if not args.no_c1:
-            line["c1_single_source"] = run_c1(args, rank)
-        if not args.no_g1:
-            log("g1 large WAN ...")
-            line["g1_large_wan"] = run_g1(args, rank)
+        line.update(host)
     if not args.no_c4:
         c4 = run_c4(args, torch, dist, rank, world, local_rank)
         if rank == 0:
