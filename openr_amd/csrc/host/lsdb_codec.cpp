@@ -700,8 +700,10 @@ AdjacencyDatabase readAdjacencyDatabase(std::string_view bytes) {  // Types.thri
   return db;
 }
 
-PrefixDatabase readPrefixDatabase(std::string_view bytes,
-                                  std::vector<std::string>* networks) {  // Types.thrift:415-430
+namespace {
+// networks: every entry's toIPNetwork text; first: the first entry's only
+PrefixDatabase readPrefixDb(std::string_view bytes, std::vector<std::string>* networks,
+                            std::string* first) {  // Types.thrift:415-430
   Reader r(bytes);
   if (networks) networks->clear();
   PrefixDatabase db;
@@ -722,7 +724,8 @@ PrefixDatabase readPrefixDatabase(std::string_view bytes,
           db.prefixEntries.reserve(n);
           if (networks) networks->resize(db.prefixEntries.size() + n);
           for (uint32_t i = 0; i < n; ++i) {
-            std::string* net = networks ? &(*networks)[db.prefixEntries.size()] : nullptr;
+            std::string* net = networks ? &(*networks)[db.prefixEntries.size()]
+                               : (first && db.prefixEntries.empty()) ? first : nullptr;
             db.prefixEntries.push_back(readPrefixEntry(r, net));
           }
           continue;
@@ -742,6 +745,11 @@ PrefixDatabase readPrefixDatabase(std::string_view bytes,
     r.skip(t, 0);
   }
   return db;
+}
+}  // namespace
+
+PrefixDatabase readPrefixDatabase(std::string_view bytes, std::vector<std::string>* networks) {
+  return readPrefixDb(bytes, networks, nullptr);
 }
 
 std::string writeAdjacencyDatabase(const AdjacencyDatabase& db) {
@@ -794,9 +802,7 @@ LsdbIngest::Decoded LsdbIngest::decodeKey(const std::string& key,
       return d;
     }
     if (key.compare(0, 7, "prefix:") == 0) {
-      std::vector<std::string> networks;
-      d.prefix = readPrefixDatabase(*rawVal, &networks);
-      if (!networks.empty()) d.network = std::move(networks.front());
+      d.prefix = readPrefixDb(*rawVal, nullptr, &d.network);  // the first entry's network
       d.kind = Decoded::kPrefix;
     }
   } catch (const std::exception& e) {  // Decision.cpp:781-784: log, drop the key
@@ -808,7 +814,8 @@ LsdbIngest::Decoded LsdbIngest::decodeKey(const std::string& key,
 
 LsdbKeyUpdate LsdbIngest::applyDecoded(const std::string& area, LinkState& areaLinkState,
                                        PrefixState& prefixState, const std::string& key,
-                                       Decoded&& d, bool inInitialization) const {
+                                       Decoded&& d, bool inInitialization,
+                                       DecisionPendingUpdates* direct) const {
   LsdbKeyUpdate u;
   if (d.kind == Decoded::kNone) return u;
   if (d.kind == Decoded::kError) {
@@ -843,15 +850,21 @@ LsdbKeyUpdate LsdbIngest::applyDecoded(const std::string& area, LinkState& areaL
     // a default IpPrefix (no prefix field) is rejected by toIPNetwork
     if (d.network.empty()) fail("prefix: PrefixEntry without a prefix");
     u.kind = LsdbKeyUpdate::kPrefix;
+    // direct: the changed network goes straight into the pending set (the
+    // publication path; no per-key vector or copy)
     if (db.deletePrefix) {
       std::string net;
       if (prefixState.deletePrefixInPlace(db.thisNodeName, area, d.network, &net)) {
-        u.changedPrefixes.push_back(std::move(net));
+        if (direct) direct->addUpdatedPrefix(net);
+        else u.changedPrefixes.push_back(std::move(net));
       }
     } else {
       const std::string* net = prefixState.updatePrefixInPlace(
           db.thisNodeName, area, std::move(d.network), std::move(entry));
-      if (net) u.changedPrefixes.push_back(*net);
+      if (net) {
+        if (direct) direct->addUpdatedPrefix(*net);
+        else u.changedPrefixes.push_back(*net);
+      }
     }
   } catch (const std::exception& e) {  // Decision.cpp:781-784: log, drop the key
     u = LsdbKeyUpdate{};
@@ -944,7 +957,8 @@ void LsdbIngest::processPublication(const std::string& area, AreaLinkStates& are
     const PublicationKeyVal* kv = ordered[i];
     std::optional<std::string_view> v;
     if (kv->value) v = *kv->value;
-    take(updateKeyInLsdb(area, ls, prefixState, kv->key, v, inInitialization));
+    take(applyDecoded(area, ls, prefixState, kv->key, decodeKey(kv->key, v), inInitialization,
+                      &pending));
   }
   for (const auto& key : expiredKeys) take(deleteKeyFromLsdb(area, ls, prefixState, key));
   pending.countKeys(prefixUpdates);

@@ -166,9 +166,12 @@ class LsdbIngest {
   };
   static Decoded decodeKey(const std::string& key,
                            const std::optional<std::string_view>& rawVal);
+  // direct != nullptr: a prefix key's changed network is added to it
+  // instead of returned in changedPrefixes (processPublication)
   LsdbKeyUpdate applyDecoded(const std::string& area, LinkState& areaLinkState,
                              PrefixState& prefixState, const std::string& key, Decoded&& d,
-                             bool inInitialization = false) const;
+                             bool inInitialization = false,
+                             DecisionPendingUpdates* direct = nullptr) const;
 
   // Decision::processPublication (Decision.cpp:821-846): the area's LinkState
   // is created on first sight, keyVals are applied in key order (thrift
