@@ -566,7 +566,9 @@ def cpu_baseline_c3(N):
             "value_1thread": round(out[1], 7), "reps": C3_CPU_REPS, "host": host_info(),
             "sample": f"refcpu buildRouteDb(s) of 16 stratified sources on {T} threads and "
                       "2 (1-0-0, 3-31-47) on 1 thread, private replicas, ingestion excluded, "
-                      f"median of {C3_CPU_REPS} reps, extrapolated to all 2,080 sources"}
+                      f"median of {C3_CPU_REPS} reps, extrapolated to all 2,080 sources",
+            "note": "value and value_1thread come from different source samples (degree "
+                    "mixes): their ratio is not a thread-scaling measurement"}
 
 
 def run_c3(args, torch, dist, rank, world, local_rank):
