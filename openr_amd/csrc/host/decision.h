@@ -82,11 +82,18 @@ struct Adjacency {  // Types.thrift:145-215
   bool adjOnlyUsedByOtherNode{false};
 };
 
+struct PerfEvent {  // Types.thrift:80-84
+  std::string nodeName, eventDescr;
+  int64_t unixTs{0};
+};
+using PerfEvents = std::vector<PerfEvent>;  // thrift::PerfEvents.events (Types.thrift:86-95)
+
 struct AdjacencyDatabase {  // Types.thrift:223-270
   std::string thisNodeName;
   bool isOverloaded{false};
   std::vector<Adjacency> adjacencies;
   int32_t nodeLabel{0};
+  std::optional<PerfEvents> perfEvents;
   std::string area;
   int32_t nodeMetricIncrementVal{0};
 };
@@ -589,6 +596,7 @@ struct DecisionRouteUpdate {  // RouteUpdate.h:28-110
   std::vector<std::string> unicastRoutesToDelete;
   std::map<int32_t, RibMplsEntry> mplsRoutesToUpdate;
   std::vector<int32_t> mplsRoutesToDelete;
+  std::optional<PerfEvents> perfEvents;  // the batch's (Decision.cpp:954-955)
 };
 
 // thrift::UnicastRoute / MplsRoute / RouteDatabase (Network.thrift,

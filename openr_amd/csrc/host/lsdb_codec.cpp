@@ -13,6 +13,7 @@
 #include "lsdb_codec.h"
 
 #include <algorithm>
+#include <chrono>
 
 #include <arpa/inet.h>
 
@@ -688,6 +689,13 @@ AdjacencyDatabase readAdjacencyDatabase(std::string_view bytes) {  // Types.thri
       case 4:
         if (t == CT_I32) { db.nodeLabel = r.zz32(); continue; }
         break;
+      case 5:
+        if (t == CT_STRUCT) {
+          db.perfEvents.emplace();
+          readPerfEvents(r, *db.perfEvents);
+          continue;
+        }
+        break;
       case 6:
         if (t == CT_BINARY) { db.area = r.bytes(); continue; }
         break;
@@ -695,7 +703,7 @@ AdjacencyDatabase readAdjacencyDatabase(std::string_view bytes) {  // Types.thri
         if (t == CT_I32) { db.nodeMetricIncrementVal = r.zz32(); continue; }
         break;
     }
-    r.skip(t, 0);  // perfEvents (5) is not kept by the route path
+    r.skip(t, 0);
   }
   return db;
 }
@@ -762,6 +770,7 @@ std::string writeAdjacencyDatabase(const AdjacencyDatabase& db) {
   w.listHeader(CT_STRUCT, db.adjacencies.size());
   for (const auto& a : db.adjacencies) writeAdjacency(w, a);
   w.field(l, 4, CT_I32); w.zz(db.nodeLabel);
+  if (db.perfEvents) { w.field(l, 5, CT_STRUCT); writePerfEvents(w, *db.perfEvents); }
   w.field(l, 6, CT_BINARY); w.bytes(db.area);
   w.field(l, 7, CT_I32); w.zz(db.nodeMetricIncrementVal);
   w.stop();
@@ -779,6 +788,55 @@ std::string writePrefixDatabase(const PrefixDatabase& db) {
   w.boolField(l, 5, db.deletePrefix);
   w.stop();
   return std::move(w.out);
+}
+
+int64_t getUnixTimeStampMs() {  // Util: system clock, ms since the epoch
+  return std::chrono::duration_cast<std::chrono::milliseconds>(
+             std::chrono::system_clock::now().time_since_epoch())
+      .count();
+}
+
+void addPerfEvent(PerfEvents& events, const std::string& nodeName,
+                  const std::string& descr) {  // LsdbUtil.cpp:52-59
+  events.push_back(PerfEvent{nodeName, descr, getUnixTimeStampMs()});
+}
+
+std::vector<std::string> sprintPerfEvents(const PerfEvents& events) {  // LsdbUtil.cpp:61-82
+  std::vector<std::string> out;
+  if (events.empty()) return out;
+  int64_t recent = events.front().unixTs;
+  for (const auto& e : events) {
+    const int64_t d = e.unixTs - recent;
+    recent = e.unixTs;
+    out.push_back("node: " + e.nodeName + ", event: " + e.eventDescr + ", duration: " +
+                  std::to_string(d) + "ms, unix-timestamp: " + std::to_string(e.unixTs));
+  }
+  return out;
+}
+
+int64_t getTotalPerfEventsDuration(const PerfEvents& events) {  // LsdbUtil.cpp:84-93
+  if (events.empty()) return 0;
+  return events.back().unixTs - events.front().unixTs;
+}
+
+std::optional<int64_t> getDurationBetweenPerfEvents(const PerfEvents& events,
+                                                    const std::string& first,
+                                                    const std::string& second,
+                                                    std::string* error) {  // LsdbUtil.cpp:95-128
+  auto fail = [&](std::string m) -> std::optional<int64_t> {
+    if (error) *error = std::move(m);
+    return std::nullopt;
+  };
+  auto it = std::find_if(events.begin(), events.end(),
+                         [&](const PerfEvent& e) { return e.eventDescr == first; });
+  if (it == events.end()) return fail("Could not find first event: " + first);
+  const int64_t t1 = it->unixTs;
+  it = std::find_if(it + 1, events.end(),
+                    [&](const PerfEvent& e) { return e.eventDescr == second; });
+  if (it == events.end()) return fail("Could not find second event: " + second);
+  const int64_t t2 = it->unixTs;
+  if (t2 < t1) return fail("Negative duration between first and second event");
+  return t2 - t1;
 }
 
 std::string getNodeNameFromKey(const std::string& key) {  // LsdbUtil.cpp:691-698
@@ -829,6 +887,7 @@ LsdbKeyUpdate LsdbIngest::applyDecoded(const std::string& area, LinkState& areaL
       db.area = area;  // Decision.cpp:732
       u.kind = LsdbKeyUpdate::kAdjacency;
       u.nodeName = db.thisNodeName;
+      u.perfEvents = std::move(db.perfEvents);  // Decision.cpp:739
       u.linkChange = areaLinkState.updateAdjacencyDatabase(db, area, inInitialization);
       return u;
     }
@@ -850,6 +909,10 @@ LsdbKeyUpdate LsdbIngest::applyDecoded(const std::string& area, LinkState& areaL
     // a default IpPrefix (no prefix field) is rejected by toIPNetwork
     if (d.network.empty()) fail("prefix: PrefixEntry without a prefix");
     u.kind = LsdbKeyUpdate::kPrefix;
+    // the key's count and perf events (Decision.cpp:775-780): straight into
+    // `direct` on the publication path, else with the update
+    if (direct) direct->notePrefixKey(db.perfEvents);
+    else u.perfEvents = std::move(db.perfEvents);
     // direct: the changed network goes straight into the pending set (the
     // publication path; no per-key vector or copy)
     if (db.deletePrefix) {
@@ -910,8 +973,11 @@ LsdbKeyUpdate LsdbIngest::deleteKeyFromLsdb(const std::string& area, LinkState& 
 }
 
 void DecisionPendingUpdates::apply(const LsdbKeyUpdate& u) {
-  if (u.kind == LsdbKeyUpdate::kAdjacency) applyLinkStateChange(u.nodeName, u.linkChange);
-  else if (u.kind == LsdbKeyUpdate::kPrefix) applyPrefixStateChange(u.changedPrefixes);
+  if (u.kind == LsdbKeyUpdate::kAdjacency) {
+    applyLinkStateChange(u.nodeName, u.linkChange, u.perfEvents);
+  } else if (u.kind == LsdbKeyUpdate::kPrefix) {
+    applyPrefixStateChange(u.changedPrefixes, u.perfEvents);
+  }
 }
 
 void LsdbIngest::processPublication(const std::string& area, AreaLinkStates& areaLinkStates,
@@ -943,14 +1009,10 @@ void LsdbIngest::processPublication(const std::string& area, AreaLinkStates& are
   for (const auto& kv : keyVals) prefixKeys += kv.key.compare(0, 7, "prefix:") == 0;
   prefixState.reserve(prefixState.prefixes().size() + prefixKeys);
   pending.reserveUpdatedPrefixes(prefixKeys);
-  uint32_t prefixUpdates = 0;
+  // the publication's prefix keys note themselves into `pending`
+  // (applyDecoded's direct path); adjacency keys apply here
   auto take = [&](LsdbKeyUpdate&& u) {
-    if (u.kind == LsdbKeyUpdate::kPrefix) {
-      for (const auto& n : u.changedPrefixes) pending.addUpdatedPrefix(n);
-      ++prefixUpdates;
-    } else {
-      pending.apply(u);
-    }
+    if (u.kind != LsdbKeyUpdate::kPrefix) pending.apply(u);
   };
   for (size_t i = 0; i < ordered.size(); ++i) {
     if (i + 1 < ordered.size() && ordered[i + 1]->key == ordered[i]->key) continue;
@@ -960,8 +1022,7 @@ void LsdbIngest::processPublication(const std::string& area, AreaLinkStates& are
     take(applyDecoded(area, ls, prefixState, kv->key, decodeKey(kv->key, v), inInitialization,
                       &pending));
   }
-  for (const auto& key : expiredKeys) take(deleteKeyFromLsdb(area, ls, prefixState, key));
-  pending.countKeys(prefixUpdates);
+  for (const auto& key : expiredKeys) pending.apply(deleteKeyFromLsdb(area, ls, prefixState, key));
 }
 
 }  // namespace openr_amd

@@ -39,11 +39,6 @@ struct LsdbDecodeError : std::runtime_error {
   using std::runtime_error::runtime_error;
 };
 
-struct PerfEvent {  // Types.thrift:80-84
-  std::string nodeName, eventDescr;
-  int64_t unixTs{0};
-};
-
 struct PrefixDatabase {  // Types.thrift:415-430
   std::string thisNodeName;
   std::vector<PrefixEntry> prefixEntries;
@@ -66,6 +61,20 @@ std::string stringToBinaryAddress(const std::string& text);
 std::string ipPrefixToNetworkString(std::string_view raw, int16_t len);  // masked
 std::string ipPrefixToString(std::string_view raw, int16_t len);         // as advertised
 
+// PerfEvents helpers (LsdbUtil.cpp:40-128): an event stamped now (unix ms)
+// appended; the events as "node: n, event: e, duration: dms, unix-timestamp:
+// t" lines; last - first timestamp; the time from the first event named
+// `first` to the next one named `second` after it (nullopt and `error` set
+// when either is missing or the duration is negative)
+int64_t getUnixTimeStampMs();
+void addPerfEvent(PerfEvents& events, const std::string& nodeName, const std::string& descr);
+std::vector<std::string> sprintPerfEvents(const PerfEvents& events);
+int64_t getTotalPerfEventsDuration(const PerfEvents& events);
+std::optional<int64_t> getDurationBetweenPerfEvents(const PerfEvents& events,
+                                                    const std::string& first,
+                                                    const std::string& second,
+                                                    std::string* error = nullptr);
+
 // getNodeNameFromKey (LsdbUtil.cpp:691-698): the text
 // between the first and second ':' of "adj:<node>" / "prefix:<node>:<...>".
 std::string getNodeNameFromKey(const std::string& key);
@@ -84,44 +93,74 @@ struct LsdbKeyUpdate {
   std::string nodeName;
   LinkState::LinkStateChange linkChange;
   std::vector<std::string> changedPrefixes;  // 0 or 1 network per prefix key
+  std::optional<PerfEvents> perfEvents;      // the database's (Decision.cpp:739, 779)
   std::string error;
 };
 
-// DecisionPendingUpdates (Decision.h:40-105, Decision.cpp:35-60) without the
-// perf-event bookkeeping: what the next rebuildRoutes must do.
+// DecisionPendingUpdates (Decision.h:40-105, Decision.cpp:35-95): what the
+// next rebuildRoutes must do, and the batch's perf events -- the OLDEST
+// update's list (debounced batches are measured from their first event),
+// with "DECISION_RECEIVED" appended when a list is taken on.
 class DecisionPendingUpdates {
  public:
   explicit DecisionPendingUpdates(std::string myNodeName) : myNodeName_(std::move(myNodeName)) {}
-  void applyLinkStateChange(const std::string& nodeName, const LinkState::LinkStateChange& c) {
+  void applyLinkStateChange(const std::string& nodeName, const LinkState::LinkStateChange& c,
+                            const std::optional<PerfEvents>& perfEvents = std::nullopt) {
     // a full rebuild only when link attributes change locally
     needsFullRebuild_ |= c.topologyChanged || c.nodeLabelChanged ||
                          (c.linkAttributesChanged && nodeName == myNodeName_);
-    ++count_;
+    addUpdate(perfEvents);
   }
   template <typename Range>
-  void applyPrefixStateChange(const Range& change) {
+  void applyPrefixStateChange(const Range& change,
+                              const std::optional<PerfEvents>& perfEvents = std::nullopt) {
     updatedPrefixes_.insert(change.begin(), change.end());
-    ++count_;
+    addUpdate(perfEvents);
   }
-  // one changed network of a publication's prefix key (counted with countKeys)
+  // one changed network of a publication's prefix key (counted with
+  // notePrefixKey)
   void addUpdatedPrefix(const std::string& network) { updatedPrefixes_.insert(network); }
   void reserveUpdatedPrefixes(size_t n) { updatedPrefixes_.reserve(updatedPrefixes_.size() + n); }
-  void countKeys(uint32_t n) { count_ += n; }
+  // a processed prefix key: applyPrefixStateChange's count and perf events
+  void notePrefixKey(const std::optional<PerfEvents>& perfEvents) { addUpdate(perfEvents); }
   void apply(const LsdbKeyUpdate& u);  // routes kAdjacency / kPrefix results
   void setNeedsFullRebuild() { needsFullRebuild_ = true; }
   bool needsFullRebuild() const { return needsFullRebuild_; }
   bool needsRouteUpdate() const { return needsFullRebuild_ || !updatedPrefixes_.empty(); }
   const std::unordered_set<std::string>& updatedPrefixes() const { return updatedPrefixes_; }
   uint32_t getCount() const { return count_; }
+  // Decision.cpp:62-75
+  void addEvent(const std::string& descr) {
+    if (perfEvents_) addPerfEvent(*perfEvents_, myNodeName_, descr);
+  }
+  const std::optional<PerfEvents>& perfEvents() const { return perfEvents_; }
+  std::optional<PerfEvents> moveOutEvents() {
+    std::optional<PerfEvents> e = std::move(perfEvents_);
+    perfEvents_ = std::nullopt;
+    return e;
+  }
   void reset() {
     count_ = 0;
+    perfEvents_ = std::nullopt;
     needsFullRebuild_ = false;
     updatedPrefixes_.clear();
   }
 
  private:
+  // Decision.cpp:77-95: the update's list replaces the batch's when the
+  // batch has none or the update's first event is older
+  void addUpdate(const std::optional<PerfEvents>& perfEvents) {
+    ++count_;
+    if (!perfEvents_ ||
+        (perfEvents && !perfEvents->empty() && !perfEvents_->empty() &&
+         perfEvents_->front().unixTs > perfEvents->front().unixTs)) {
+      perfEvents_ = perfEvents ? *perfEvents : PerfEvents{};
+      addPerfEvent(*perfEvents_, myNodeName_, "DECISION_RECEIVED");
+    }
+  }
   std::string myNodeName_;
   uint32_t count_{0};
+  std::optional<PerfEvents> perfEvents_;
   bool needsFullRebuild_{false};
   std::unordered_set<std::string> updatedPrefixes_;  // Decision.h:104 (unordered)
 };

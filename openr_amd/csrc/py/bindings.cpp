@@ -49,6 +49,24 @@ Adjacency toAdj(const py::dict& d) {
   return a;
 }
 
+// perf events as [(nodeName, eventDescr, unixTs), ...] (None: absent)
+std::optional<PerfEvents> toPerfEvents(const py::handle& h) {
+  if (h.is_none()) return std::nullopt;
+  PerfEvents evs;
+  for (auto x : h) {
+    py::tuple t = x.cast<py::tuple>();
+    evs.push_back(PerfEvent{t[0].cast<std::string>(), t[1].cast<std::string>(),
+                            t[2].cast<int64_t>()});
+  }
+  return evs;
+}
+py::object fromPerfEvents(const std::optional<PerfEvents>& evs) {
+  if (!evs) return py::none();
+  py::list out;
+  for (const auto& e : *evs) out.append(py::make_tuple(e.nodeName, e.eventDescr, e.unixTs));
+  return out;
+}
+
 AdjacencyDatabase toAdjDb(const py::dict& d) {
   AdjacencyDatabase db;
   db.thisNodeName = get<std::string>(d, "thisNodeName", "");
@@ -59,6 +77,7 @@ AdjacencyDatabase toAdjDb(const py::dict& d) {
   if (d.contains("adjacencies")) {
     for (auto h : d["adjacencies"]) db.adjacencies.push_back(toAdj(h.cast<py::dict>()));
   }
+  if (d.contains("perfEvents")) db.perfEvents = toPerfEvents(d["perfEvents"]);
   return db;
 }
 
@@ -195,6 +214,7 @@ py::dict fromAdjDb(const AdjacencyDatabase& db) {
   d["nodeLabel"] = db.nodeLabel;
   d["area"] = db.area;
   d["nodeMetricIncrementVal"] = db.nodeMetricIncrementVal;
+  d["perfEvents"] = fromPerfEvents(db.perfEvents);
   py::list adjs;
   for (const auto& a : db.adjacencies) {
     py::dict x;
@@ -258,6 +278,7 @@ py::dict fromKeyUpdate(const LsdbKeyUpdate& u) {
   d["linkChange"] = u.kind == LsdbKeyUpdate::kAdjacency ? py::object(fromChange(u.linkChange))
                                                          : py::object(py::none());
   d["changedPrefixes"] = u.changedPrefixes;
+  d["perfEvents"] = fromPerfEvents(u.perfEvents);
   d["error"] = u.error;
   return d;
 }
@@ -1156,7 +1177,41 @@ PYBIND11_MODULE(_decision, m) {
       .def("needsRouteUpdate", &DecisionPendingUpdates::needsRouteUpdate)
       .def("updatedPrefixes", &DecisionPendingUpdates::updatedPrefixes)
       .def("getCount", &DecisionPendingUpdates::getCount)
-      .def("reset", &DecisionPendingUpdates::reset);
+      .def("reset", &DecisionPendingUpdates::reset)
+      .def("applyLinkStateChange",
+           [](DecisionPendingUpdates& p, const std::string& node, py::dict change,
+              py::object perf) {
+             LinkState::LinkStateChange c;
+             c.topologyChanged = get<bool>(change, "topologyChanged", false);
+             c.linkAttributesChanged = get<bool>(change, "linkAttributesChanged", false);
+             c.nodeLabelChanged = get<bool>(change, "nodeLabelChanged", false);
+             p.applyLinkStateChange(node, c, toPerfEvents(perf));
+           },
+           py::arg("nodeName"), py::arg("change"), py::arg("perfEvents") = py::none())
+      .def("applyPrefixStateChange",
+           [](DecisionPendingUpdates& p, const std::vector<std::string>& change,
+              py::object perf) { p.applyPrefixStateChange(change, toPerfEvents(perf)); },
+           py::arg("change"), py::arg("perfEvents") = py::none())
+      .def("addEvent", &DecisionPendingUpdates::addEvent)
+      .def("perfEvents",
+           [](const DecisionPendingUpdates& p) { return fromPerfEvents(p.perfEvents()); })
+      .def("moveOutEvents",
+           [](DecisionPendingUpdates& p) { return fromPerfEvents(p.moveOutEvents()); });
+  m.def("addPerfEvent", [](py::list evs, const std::string& node, const std::string& descr) {
+    PerfEvents e = *toPerfEvents(evs);
+    addPerfEvent(e, node, descr);
+    return fromPerfEvents(e);
+  });
+  m.def("sprintPerfEvents", [](py::list evs) { return sprintPerfEvents(*toPerfEvents(evs)); });
+  m.def("getTotalPerfEventsDuration",
+        [](py::list evs) { return getTotalPerfEventsDuration(*toPerfEvents(evs)); });
+  m.def("getDurationBetweenPerfEvents",
+        [](py::list evs, const std::string& a, const std::string& b) -> py::object {
+          std::string err;
+          auto d = getDurationBetweenPerfEvents(*toPerfEvents(evs), a, b, &err);
+          if (!d) return py::make_tuple(py::none(), err);
+          return py::make_tuple(*d, py::none());
+        });
 
   py::class_<LsdbIngest>(m, "LsdbIngest")
       .def(py::init<std::string, std::set<std::string>>(), py::arg("myNodeName"),
