@@ -697,6 +697,9 @@ def run_c3(args, torch, dist, rank, world, local_rank):
         "decode_ms": round(pub["decode_ms"], 2),
         "prefix_keyed_decode_ms": round(pub["prefix_keyed_decode_ms"], 2),
         "prefix_insert_ms": round(pub["prefix_insert_ms"], 2),
+        # the whole publication through processPublication (key order, the
+        # pending update set and perf events included)
+        "process_publication_ms": round(pub["publication_ms"], 2),
         "keys_per_s": round(keys / pub["ingest_ms"] * 1e3, 1),
         "decode_MB_per_s": round(pub["bytes"] / pub["decode_ms"] / 1e3, 1),
         "note": "LsdbIngest (C++ drop-in), 1 host thread, median of 3; rank 0, "

@@ -1628,6 +1628,11 @@ PYBIND11_MODULE(_decision, m) {
           size_t routesKept = 0;
           std::vector<PublicationKeyVal> pub(keys.size());
           for (size_t i = 0; i < keys.size(); ++i) pub[i] = PublicationKeyVal{keys[i], vals[i]};
+          // in key order, as Decision receives it (thrift::Publication's
+          // keyVals is a std::map, Decision.cpp:821-846); processPublication
+          // sorts an unsorted vector itself
+          std::sort(pub.begin(), pub.end(), [](const PublicationKeyVal& a,
+                                               const PublicationKeyVal& b) { return a.key < b.key; });
           for (int r = 0; r < reps; ++r) {
             {
               // the whole publication through processPublication (one host
