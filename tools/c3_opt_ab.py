@@ -28,10 +28,7 @@ DEFAULTS = {"frontier_block": 0, "frontier_parts": 0, "route_stream": 5,
             "route_store_nt": 2, "spf_lane_walk": -1, "spf_preload": 1,
             "lds_parts": 0, "lds_grid": 0, "lds_key16": 1, "lds_tail": 1,
             "lds_bfs_exit": 1, "lds_lead": 0, "lds_tail_parts": 0,
-            "lds_pull": 6,
-            # lib=base comparisons with a build that still had the option
-            # (round 5's prep-as-first-items form, measured slower, removed)
-            "lds_fused_prep": 0}
+            "lds_pull": 6}
 
 
 def main():
