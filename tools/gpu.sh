@@ -22,6 +22,7 @@
 #                             bench flags --name=value written name=value with a
 #                             leading '-' (e.g. -c5-streams=2), or lib=base
 #                             (openr_amd/lib/libopenr_gpu_base.so, tools/build_ab_base.sh)
+#                             or an OGS_* environment variable (OGS_SLOT_BANKS=0)
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -88,16 +89,17 @@ for recipe in "$@"; do
       for rep in 1 2; do
         vi=0
         for v in "${parts[@]:1}"; do
-          vi=$((vi + 1)); args=(); lib=""
+          vi=$((vi + 1)); args=(); lib=""; envs=()
           for kv in ${v//+/ }; do
             case $kv in
               lib=base) lib=openr_amd/lib/libopenr_gpu_base.so ;;
+              OGS_*=*) envs+=("$kv") ;;
               -*) args+=("-${kv%%=*}" "${kv#*=}") ;;
               *) args+=(--opt "$kv") ;;
             esac
           done
           log="gpurun_out/benchab_${n}_${cfg}_${vi}_$rep.log"
-          OGS_LIB=$lib timeout -k 10 300 python3 bench.py --config "$cfg" --steps 10 --warmup 2 \
+          env "${envs[@]}" OGS_LIB=$lib timeout -k 10 300 python3 bench.py --config "$cfg" --steps 10 --warmup 2 \
             --no-cpu-baseline "${args[@]}" > "$log" 2>&1
           rc=$?; [ $rc -eq 0 ] || { tail -5 "$log"; exit $rc; }
           echo "$cfg [$v] rep $rep: $(grep '^{' "$log" | tail -1 | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["unit"], d["ms_per_step"], "ms", {k: v for k, v in d.items() if k.endswith("digest") or k == "golden"})')"
