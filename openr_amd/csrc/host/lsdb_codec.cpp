@@ -516,10 +516,9 @@ char* formatV4(const unsigned char* b, char* o) {
 // ties) of >= 2 zero words becomes "::", and ::a.b.c.d / ::ffff:a.b.c.d
 // print the embedded IPv4 address (glibc resolv/inet_ntop.c inet_ntop6 --
 // the form folly::IPAddressV6::str() returns).
-std::string formatAddress(const unsigned char* raw, int family) {
-  char buf[48];
-  char* o = buf;
-  if (family == AF_INET) return std::string(buf, formatV4(raw, o));
+// (into `o`, at most 45 chars; returns the end)
+char* formatAddressTo(const unsigned char* raw, int family, char* o) {
+  if (family == AF_INET) return formatV4(raw, o);
   unsigned w[8];
   for (int i = 0; i < 8; ++i) w[i] = unsigned(raw[2 * i]) << 8 | raw[2 * i + 1];
   int bestBase = -1, bestLen = 0, curBase = -1, curLen = 0;
@@ -542,8 +541,7 @@ std::string formatAddress(const unsigned char* raw, int family) {
     }
     if (i) *o++ = ':';
     if (i == 6 && bestBase == 0 && (bestLen == 6 || (bestLen == 5 && w[5] == 0xffff))) {
-      o = formatV4(raw + 12, o);
-      return std::string(buf, o);
+      return formatV4(raw + 12, o);
     }
     unsigned v = w[i];
     bool lead = true;
@@ -553,6 +551,22 @@ std::string formatAddress(const unsigned char* raw, int family) {
     }
   }
   if (bestBase >= 0 && bestBase + bestLen == 8) *o++ = ':';
+  return o;
+}
+
+std::string formatAddress(const unsigned char* raw, int family) {
+  char buf[48];
+  return std::string(buf, formatAddressTo(raw, family, buf));
+}
+
+// "<addr>/<len>" in one string construction (len in 0..128)
+std::string formatPrefix(const unsigned char* raw, int family, int len) {
+  char buf[64];
+  char* o = formatAddressTo(raw, family, buf);
+  *o++ = '/';
+  if (len >= 100) *o++ = char('0' + len / 100);
+  if (len >= 10) *o++ = char('0' + len / 10 % 10);
+  *o++ = char('0' + len % 10);
   return std::string(buf, o);
 }
 
@@ -623,8 +637,8 @@ std::string ipPrefixToString(std::string_view raw, int16_t len) {
   if (raw.size() != 4 && raw.size() != 16) fail("prefix: address must be 4 or 16 bytes");
   int bits = int(raw.size()) * 8;
   if (len < 0 || len > bits) fail("prefix: length out of range");
-  return formatAddress(reinterpret_cast<const unsigned char*>(raw.data()),
-                       raw.size() == 16 ? AF_INET6 : AF_INET) + "/" + std::to_string(len);
+  return formatPrefix(reinterpret_cast<const unsigned char*>(raw.data()),
+                      raw.size() == 16 ? AF_INET6 : AF_INET, len);
 }
 
 // "<addr>/<len>" text -> toIPNetwork(prefix, applyMask) printed as
@@ -646,7 +660,7 @@ std::string prefixNetworkKey(const std::string& text, bool applyMask) {
   if (len > bits) throw std::invalid_argument("Invalid IPAddress: " + text);
   if (applyMask)
     for (int bit = len; bit < bits; ++bit) buf[bit >> 3] &= uint8_t(~(0x80u >> (bit & 7)));
-  return formatAddress(buf, fam) + "/" + std::to_string(len);
+  return formatPrefix(buf, fam, len);
 }
 
 // toIPNetwork(prefix, applyMask=true) (NetworkUtil.h:196-208) printed as
@@ -658,7 +672,7 @@ std::string ipPrefixToNetworkString(std::string_view raw, int16_t len) {
   unsigned char buf[16];
   std::memcpy(buf, raw.data(), raw.size());
   for (int bit = len; bit < bits; ++bit) buf[bit >> 3] &= uint8_t(~(0x80u >> (bit & 7)));
-  return formatAddress(buf, raw.size() == 16 ? AF_INET6 : AF_INET) + "/" + std::to_string(len);
+  return formatPrefix(buf, raw.size() == 16 ? AF_INET6 : AF_INET, len);
 }
 
 AdjacencyDatabase readAdjacencyDatabase(std::string_view bytes) {  // Types.thrift:223-270
