@@ -119,7 +119,10 @@ class DecisionPendingUpdates {
   }
   // one changed network of a publication's prefix key (counted with
   // notePrefixKey)
-  void addUpdatedPrefix(const std::string& network) { updatedPrefixes_.insert(network); }
+  void addUpdatedPrefix(const std::string& network) {
+    growHashTable(updatedPrefixes_);
+    updatedPrefixes_.insert(network);
+  }
   void reserveUpdatedPrefixes(size_t n) { updatedPrefixes_.reserve(updatedPrefixes_.size() + n); }
   // a processed prefix key: applyPrefixStateChange's count and perf events
   void notePrefixKey(const std::optional<PerfEvents>& perfEvents) { addUpdate(perfEvents); }

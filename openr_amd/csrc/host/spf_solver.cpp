@@ -88,6 +88,7 @@ const std::string* PrefixState::updatePrefixInPlace(const std::string& node,
                                                     std::string&& network, PrefixEntry&& entry) {
   // PrefixState.cpp:15-38
   // one lookup: the key moves in only when inserted
+  growHashTable(prefixes_);
   auto mapIt = prefixes_.try_emplace(std::move(network)).first;
   auto& entries = mapIt->second;
   auto [it, inserted] = entries.try_emplace(NodeAndArea(node, area));
