@@ -16,6 +16,7 @@
 #pragma once
 
 #include <algorithm>
+#include <cstdlib>
 #include <chrono>
 #include <cstdint>
 #include <limits>
@@ -424,11 +425,20 @@ class LinkState {
 // node through a cache miss, and a bulk ingest (the C3 publication: 208k
 // prefix keys, no count known up front) then pays ~1.1 relinks per entry
 // instead of ~2. Past 1M entries the library's policy applies.
+// OGS_HASH_GROWTH=<k> sets the factor (<= 2: the library's policy).
+inline int hashGrowthFactor() {
+  static const int k = [] {
+    const char* e = std::getenv("OGS_HASH_GROWTH");
+    return e ? std::atoi(e) : 8;
+  }();
+  return k;
+}
 template <typename Table>
 inline void growHashTable(Table& t) {
-  if (t.size() + 1 > size_t(double(t.bucket_count()) * t.max_load_factor()) &&
+  const int k = hashGrowthFactor();
+  if (k > 2 && t.size() + 1 > size_t(double(t.bucket_count()) * t.max_load_factor()) &&
       t.size() < (size_t(1) << 20)) {
-    t.reserve(std::max<size_t>(64, t.size() * 8));
+    t.reserve(std::max<size_t>(64, t.size() * size_t(k)));
   }
 }
 
