@@ -1045,6 +1045,9 @@ def run_c5(args, torch, dist, rank, world, local_rank):
         "ksp2_dests_per_s": round(total_units * steps / tmax, 1),
         "route_kernels_ms": round(route_ms, 4), "ksp2_kernels_ms": round(ksp_ms, 4),
         "job_kernel_ms": round(job_ms, 4),
+        # (route + KSP2 kernel time) / job time: 2.0 = perfect two-stream
+        # overlap of equal parts, 1.0 = the parts run back to back
+        "overlap": round((route_ms + ksp_ms) / job_ms, 3) if job_ms > 0 else None,
         "route_digest": f"{routes_job:016x}", "path_digest": f"{paths_job:016x}",
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
@@ -1052,7 +1055,8 @@ def run_c5(args, torch, dist, rank, world, local_rank):
                      "kernel": "ksp_base_kernel + ksp2_kernel (one launch pair over the "
                                "source's areas)"},
     }
-    log(f"c5 timed: {job_ms:.4f} ms/job")
+    log(f"c5 timed: {job_ms:.4f} ms/job (route {route_ms:.4f} + ksp2 {ksp_ms:.4f} ms, "
+        f"overlap {line['overlap']})")
     golden_check(line, "c5_routes", routes_job, GOLDEN.get("c5_routes"))
     golden_check(line, "c5_paths", paths_job, GOLDEN.get("c5_paths"))
     if world == 1:
@@ -1065,6 +1069,49 @@ def run_c5(args, torch, dist, rank, world, local_rank):
 
 # --------------------------------------------------------------- main ---
 DIST_BACKEND = [None]  # the process group the per-rank records went through
+
+
+PERF_FLOOR_PATH = os.path.join(ROOT, "tests", "golden", "perf_floor.json")
+
+
+def _dig(d, path):
+    for k in path:
+        if not isinstance(d, dict) or k not in d:
+            return None
+        d = d[k]
+    return d if isinstance(d, (int, float)) else None
+
+
+def perf_summary(line):
+    """Every sub-line figure as ONE compact stderr line (the driver's record
+    keeps the stderr tail, not the sub-lines), then a PERF-REGRESSION line per
+    figure past its committed floor (tests/golden/perf_floor.json: the best
+    driver / builder figures with a tolerance). The result goes into
+    line["perf_check"]; a regression is reported, it does not fail the run."""
+    floor = {}
+    if os.path.exists(PERF_FLOOR_PATH):
+        with open(PERF_FLOOR_PATH) as f:
+            floor = {k: v for k, v in json.load(f).items() if not k.startswith("_")}
+    figs, bad = [], []
+    for name, spec in floor.items():
+        got = _dig(line, spec["path"])
+        if got is None:
+            continue
+        figs.append(f"{name}={got:g}")
+        lim, worse = (spec["max"], got > spec["max"]) if "max" in spec else \
+            (spec["min"], got < spec["min"])
+        if worse:
+            bad.append((name, got, lim, "max" if "max" in spec else "min"))
+    gold = line.get("golden", {})
+    ok = sum(1 for v in gold.values() if v == "match")
+    figs.append(f"golden={ok}/{len(gold)}")
+    log("SUMMARY " + " ".join(figs))
+    for name, got, lim, kind in bad:
+        print(f"PERF-REGRESSION: {name} = {got:g} (floor {kind} {lim:g}, "
+              f"tests/golden/perf_floor.json)", file=sys.stderr, flush=True)
+    line["perf_check"] = {"floor": os.path.relpath(PERF_FLOOR_PATH, ROOT),
+                          "checked": len(figs) - 1,
+                          "regressions": [f"{n}={g:g} vs {k} {lim:g}" for n, g, lim, k in bad]}
 
 
 def finish(line):
@@ -1245,6 +1292,7 @@ SUB_KEYS = {
                               "config", "steps"),
     "c5_multiarea_ksp2_ucmp": ("value", "unit", "ms_per_step", "ksp2_dests_per_s",
                                "route_kernels_ms", "ksp2_kernels_ms", "job_kernel_ms",
+                               "overlap",
                                "route_digest", "path_digest", "golden", "roofline",
                                "config", "steps", "cpu_baseline"),
 }
@@ -1460,6 +1508,7 @@ def main():
         for k, v in ((line.get("g1_large_wan") or {}).get("single_source") or {}).get(
                 "golden", {}).items():
             line["golden"][k] = v
+        perf_summary(line)
         finish(line)
     elif DIGEST_FAILURES:
         raise SystemExit(1)

@@ -90,6 +90,24 @@ def load(path=None):
     lib.ogs_ctx_spf_routes_groups.argtypes = ([ctypes.c_void_p] +
                                              lib.ogs_spf_routes_groups.argtypes)
     lib.ogs_ctx_spf_routes_groups.restype = ctypes.c_int
+    # the remaining compute entry points: structs this module does not model
+    # (ogs_path_unit, ogs_unit_mods, ogs_area_table, ogs_rib_policy, ...)
+    # pass as c_void_p, so 64-bit handles and device pointers never go
+    # through ctypes' default int conversion
+    P, I32, U32 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_uint32
+    plain = {
+        "ogs_routes_from_spf": [P, P, P, I32, P, P, P, U32, I32, P, P],
+        "ogs_spf_routes_variants": [P, P, P, I32, P, P, U32, I32, P, P],
+        "ogs_ksp_paths": [P, P, I32, P, U32, U32, P, P],
+        "ogs_ksp2_paths": [P, P, I32, P, I32, U32, P, P, P],
+        "ogs_routes_multiarea": [P, P, P, P, I32, P, P, P, U32, I32, P, P],
+        "ogs_rib_policy_apply": [P, P, I32, I32, I32, P, P, P, P, P],
+    }
+    for name, args in plain.items():
+        for fn, a in ((name, args), ("ogs_ctx_" + name[4:], [P] + args)):
+            f = getattr(lib, fn)
+            f.argtypes = a
+            f.restype = ctypes.c_int
     return lib
 
 

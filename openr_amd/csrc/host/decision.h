@@ -15,6 +15,7 @@
 // missing device or an input outside the GPU engine's domain throws.
 #pragma once
 
+#include <atomic>
 #include <algorithm>
 #include <cstdlib>
 #include <chrono>
@@ -424,21 +425,25 @@ class LinkState {
 // the library's 2x while it is under 1M entries: every rehash relinks each
 // node through a cache miss, and a bulk ingest (the C3 publication: 208k
 // prefix keys, no count known up front) then pays ~1.1 relinks per entry
-// instead of ~2. Past 1M entries the library's policy applies.
-// OGS_HASH_GROWTH=<k> sets the factor (<= 2: the library's policy).
-inline int hashGrowthFactor() {
-  static const int k = [] {
-    const char* e = std::getenv("OGS_HASH_GROWTH");
-    return e ? std::atoi(e) : 8;
-  }();
+// instead of ~2. Past 1M entries the library's policy applies, and one
+// reserve never asks for more than 2M buckets (16 MB of bucket pointers), so
+// a table just under 1M entries holds at most twice the library's buckets.
+// setHashGrowthFactor(k) sets the factor process-wide (<= 2: the library's
+// policy; for A/B runs).
+inline std::atomic<int>& hashGrowthFactorRef() {
+  static std::atomic<int> k{8};
   return k;
 }
+inline void setHashGrowthFactor(int k) { hashGrowthFactorRef().store(k); }
+inline int hashGrowthFactor() { return hashGrowthFactorRef().load(std::memory_order_relaxed); }
 template <typename Table>
 inline void growHashTable(Table& t) {
   const int k = hashGrowthFactor();
+  constexpr size_t kMaxEntries = size_t(1) << 20, kMaxBuckets = size_t(1) << 21;
   if (k > 2 && t.size() + 1 > size_t(double(t.bucket_count()) * t.max_load_factor()) &&
-      t.size() < (size_t(1) << 20)) {
-    t.reserve(std::max<size_t>(64, t.size() * size_t(k)));
+      t.size() < kMaxEntries) {
+    const size_t want = std::max<size_t>(64, t.size() * size_t(k));
+    t.reserve(std::max(std::min(want, kMaxBuckets), 2 * t.size()));
   }
 }
 
@@ -471,6 +476,7 @@ class PrefixEntryList {
     return *this;
   }
   PrefixEntryList& operator=(PrefixEntryList&& o) noexcept {
+    if (this == &o) return *this;
     one_ = std::move(o.one_);
     many_ = std::move(o.many_);
     n_ = o.n_;

@@ -923,10 +923,6 @@ LsdbKeyUpdate LsdbIngest::applyDecoded(const std::string& area, LinkState& areaL
     // a default IpPrefix (no prefix field) is rejected by toIPNetwork
     if (d.network.empty()) fail("prefix: PrefixEntry without a prefix");
     u.kind = LsdbKeyUpdate::kPrefix;
-    // the key's count and perf events (Decision.cpp:775-780): straight into
-    // `direct` on the publication path, else with the update
-    if (direct) direct->notePrefixKey(db.perfEvents);
-    else u.perfEvents = std::move(db.perfEvents);
     // direct: the changed network goes straight into the pending set (the
     // publication path; no per-key vector or copy)
     if (db.deletePrefix) {
@@ -943,6 +939,12 @@ LsdbKeyUpdate LsdbIngest::applyDecoded(const std::string& area, LinkState& areaL
         else u.changedPrefixes.push_back(*net);
       }
     }
+    // the key's count and perf events (Decision.cpp:775-780): only once the
+    // update above did not throw, as applyPrefixStateChange runs after
+    // updatePrefix / deletePrefix; straight into `direct` on the publication
+    // path, else with the update
+    if (direct) direct->notePrefixKey(db.perfEvents);
+    else u.perfEvents = std::move(db.perfEvents);
   } catch (const std::exception& e) {  // Decision.cpp:781-784: log, drop the key
     u = LsdbKeyUpdate{};
     u.kind = LsdbKeyUpdate::kError;

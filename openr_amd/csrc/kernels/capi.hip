@@ -365,7 +365,7 @@ int ogs_ctx_create(int32_t device, ogs_ctx** out) {
 
 int ogs_ctx_destroy(ogs_ctx* ctx) {
   if (!ctx) return OGS_OK;
-  (void)hipSetDevice(ctx->e.device);
+  ogs::DeviceGuard dev(ctx->e.device);  // the caller's device comes back
   delete ctx;  // frees its scratch (hipFree waits for the device)
   return OGS_OK;
 }
@@ -722,8 +722,8 @@ int ogs_routes_multiarea(const ogs_graph* graph,
 
 // Context forms of the compute entry points: the call runs with the
 // context's device, options and scratch (engine.h), then the thread's
-// previous binding is restored. Same arguments and status as the plain
-// entry point.
+// previous context binding and its previous HIP device are restored
+// (BoundContext). Same arguments and status as the plain entry point.
 #define OGS_CTX_CALL(ctx, call)                                  \
   do {                                                           \
     if (!(ctx)) return fail(OGS_E_INVALID, "ctx is NULL");       \

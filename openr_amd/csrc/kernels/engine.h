@@ -89,12 +89,33 @@ inline const EngineOptions& opts() {
 // threads still share the buffer: give each thread its own context).
 hipError_t workspace(size_t bytes, hipStream_t stream, void** out);
 
-// RAII: binds `ctx` (and its device) to the calling thread for one call
+// RAII: sets the calling thread's HIP device to `device` for one scope and
+// restores the thread's previous device on exit (only when it was changed)
+class DeviceGuard {
+ public:
+  explicit DeviceGuard(int device) {
+    if (device < 0 || hipGetDevice(&prev_) != hipSuccess) return;
+    if (prev_ != device && hipSetDevice(device) == hipSuccess) set_ = true;
+  }
+  ~DeviceGuard() {
+    if (set_) (void)hipSetDevice(prev_);
+  }
+  DeviceGuard(const DeviceGuard&) = delete;
+  DeviceGuard& operator=(const DeviceGuard&) = delete;
+
+ private:
+  int prev_ = -1;
+  bool set_ = false;
+};
+
+// RAII: binds `ctx` (and its device) to the calling thread for one call; the
+// thread's previous context binding AND its previous HIP device come back on
+// exit, so a thread on device 1 calling a device-0 context stays on device 1
 class BoundContext {
  public:
-  explicit BoundContext(EngineContext* ctx) : prev_(bound_context()) {
+  explicit BoundContext(EngineContext* ctx)
+      : prev_(bound_context()), dev_(ctx ? ctx->device : -1) {
     bind_context(ctx);
-    if (ctx) (void)hipSetDevice(ctx->device);
   }
   ~BoundContext() { bind_context(prev_); }
   BoundContext(const BoundContext&) = delete;
@@ -102,6 +123,7 @@ class BoundContext {
 
  private:
   EngineContext* prev_;
+  DeviceGuard dev_;
 };
 
 }  // namespace ogs

@@ -1045,6 +1045,9 @@ PYBIND11_MODULE(_decision, m) {
   // fb303-style Decision counters (stats.cpp)
   m.def("decision_counters", []() { return getDecisionCounters(); });
   m.def("reset_decision_counters", []() { resetDecisionCounters(); });
+  // growHashTable's factor (decision.h), process-wide; for A/B runs
+  m.def("set_hash_growth_factor", [](int k) { setHashGrowthFactor(k); });
+  m.def("hash_growth_factor", []() { return hashGrowthFactor(); });
 
   py::class_<LinkState>(m, "LinkState")
       .def(py::init<const std::string&, const std::string&>())

@@ -184,3 +184,132 @@ def test_two_threads_own_contexts(product):
     finally:
         lib.ogs_ctx_destroy(ctx_a)
         lib.ogs_ctx_destroy(ctx_b)
+
+
+def _c3_shard_job(product, capi, torch, dev, rank=0, world=8):
+    """The C3 fabric (2,080 nodes x 208k prefixes) restricted to the sources
+    of one N-rank shard (bench.py's interleave), every width group through
+    ONE ogs_ctx_spf_routes_groups call; the XOR of its per-source digests
+    must equal the oracle's golden per-source digests of those sources."""
+    import bench
+    from openr_amd import shard
+    from openr_amd.workloads import c3_source_names
+    mine = shard.interleave(c3_source_names(), rank, world)
+    launches, _ = bench.c3_launches(torch, product, capi, dev, mine)
+    assert all(L["shared"] for L in launches)
+    want = bench.c3_golden_shard(mine)
+    arr = (capi.RouteGroup * len(launches))()
+    for i, L in enumerate(launches):
+        arr[i].units = L["t"]["units"].data_ptr()
+        arr[i].n_units = L["U"]
+        arr[i].nh_words = L["W"]
+        arr[i].out = L["so"]
+    L0 = launches[0]
+
+    def run(lib, ctx, stream):
+        for L in launches:
+            for k in ("meta", "metric", "mask"):
+                L["o"][k].zero_()
+        rc = lib.ogs_ctx_spf_routes_groups(ctx, ctypes.byref(L0["g"]), ctypes.byref(L0["pt"]),
+                                           arr, len(launches), L0["flags"],
+                                           ctypes.c_void_p(stream.cuda_stream))
+        capi.check(lib, rc, "ogs_ctx_spf_routes_groups")
+        stream.synchronize()
+        return f"{shard.combine_digests(bench.c3_digest(L) for L in launches):016x}"
+    return run, want, (launches, arr)
+
+
+def test_two_threads_default_lds_form(product, oracle):
+    """Both threads on the DEFAULT one-launch LDS form (route_stream 5: the
+    persistent SPF + route-stream kernel with its device-wide item counter
+    and release / acquire ready flags in per-context scratch), each on its
+    own context and HIP stream, at the same time:
+      A: the C3-size fabric's N=8 rank-0 shard (260 sources, 208k prefixes)
+         -- equals the oracle's golden per-source digests every time;
+      B: the 352-node fabric's two width groups -- every source's digest
+         equals a live oracle buildRouteDb every time.
+    Each context call leaves the calling thread's HIP device as it was."""
+    import torch
+
+    import openr_amd.capi as capi
+    lib = capi.load()
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    c3_run, c3_want, keep_a = _c3_shard_job(product, capi, torch, dev)
+    assert c3_want is not None, "golden C3 per-source digests missing"
+    fab_run, keep_b = _fabric_job(product, capi, torch, dev)
+    names = ([f"1-{p}-{s}" for p in range(4) for s in range(16)] +
+             [f"2-{p}-{f}" for p in range(8) for f in range(4)] +
+             [f"3-{p}-{r}" for p in range(8) for r in range(32)])
+    fsw = [n for n in names if n.startswith("2-")][::2]
+    rest = [n for n in names if not n.startswith("2-")][::3]
+    fab_names = fsw + rest
+    fab_want = list(oracle.gen_route_digests("fabric", FABRIC, fab_names, True, False, False, 8))
+    _, o_b, specs = keep_b
+    br_b = product.BatchRunner(True, False, False)
+    br_b.add_generated("fabric", FABRIC, fab_names)
+    def fab_digests(got):
+        out, row = [], 0
+        for g, (u, W) in zip(got, specs):
+            U = len(u) // 2
+            out += list(br_b.records_digests([], g["meta"].numpy(), g["metric"].numpy(),
+                                             g["mask"].numpy(), W, 4,
+                                             list(range(row, row + U))))
+            row += U
+        return out
+
+    ctx_a, ctx_b = ctypes.c_void_p(), ctypes.c_void_p()
+    capi.check(lib, lib.ogs_ctx_create(0, ctypes.byref(ctx_a)), "ogs_ctx_create")
+    capi.check(lib, lib.ogs_ctx_create(0, ctypes.byref(ctx_b)), "ogs_ctx_create")
+    try:
+        errors, results = [], {"a": [], "b": []}
+        reps = 6
+
+        def worker(key, run, ctx):
+            try:
+                torch.cuda.set_device(dev)
+                s = torch.cuda.Stream(dev)
+                for _ in range(reps):
+                    before = torch.cuda.current_device()
+                    results[key].append(run(lib, ctx, s))
+                    assert torch.cuda.current_device() == before, "ctx call moved the device"
+            except Exception as e:  # noqa: BLE001
+                errors.append((key, repr(e)))
+
+        ts = [threading.Thread(target=worker, args=("a", c3_run, ctx_a)),
+              threading.Thread(target=worker, args=("b", fab_run, ctx_b))]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(timeout=240)
+        assert not any(t.is_alive() for t in ts), "a context thread hung"
+        assert not errors, errors
+        assert results["a"] == [c3_want] * reps
+        assert len(results["b"]) == reps
+        for got in results["b"]:
+            d = fab_digests(got)
+            assert d == fab_want, [n for n, x, y in zip(fab_names, d, fab_want) if x != y][:8]
+    finally:
+        lib.ogs_ctx_destroy(ctx_a)
+        lib.ogs_ctx_destroy(ctx_b)
+
+
+def test_ctx_calls_restore_callers_device():
+    """BoundContext / ogs_ctx_destroy restore the calling thread's HIP
+    device: a thread on device 1 that destroys (or calls) a device-0
+    context is still on device 1 afterwards. With one visible device the
+    call on the same device must leave it unchanged."""
+    import torch
+
+    import openr_amd.capi as capi
+    lib = capi.load()
+    n = torch.cuda.device_count()
+    cur = 1 if n >= 2 else 0
+    torch.cuda.set_device(cur)
+    ctx = ctypes.c_void_p()
+    capi.check(lib, lib.ogs_ctx_create(0, ctypes.byref(ctx)), "ogs_ctx_create")
+    capi.check(lib, lib.ogs_ctx_set_option(ctx, b"route_stream", 5), "ctx option")
+    assert torch.cuda.current_device() == cur
+    capi.check(lib, lib.ogs_ctx_destroy(ctx), "ogs_ctx_destroy")
+    assert torch.cuda.current_device() == cur
+    torch.cuda.set_device(0)
