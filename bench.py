@@ -601,7 +601,7 @@ def run_c3(args, torch, dist, rank, world, local_rank):
         # first so it is not the lone tail after the 1-word group
         launches = launches[::-1]
     main = torch.cuda.current_stream(dev)
-    side = torch.cuda.Stream(dev) if args.c3_streams > 1 else main
+    side = side_stream(torch, dev) if args.c3_streams > 1 else main
 
     for _ in range(warmup):
         c3_launch_all(lib, capi, launches, main, side)
@@ -964,7 +964,7 @@ def run_c5(args, torch, dist, rank, world, local_rank):
     sptr = stream.cuda_stream
     # the RouteDb (+ policy) and the KSP2 batch are independent: with
     # --c5-streams 2 the KSP2 launches run on a second HIP stream, overlapped
-    side = torch.cuda.Stream(dev) if args.c5_streams > 1 else stream
+    side = side_stream(torch, dev) if args.c5_streams > 1 else stream
 
     def job():
         fork = torch.cuda.Event()
@@ -1069,6 +1069,23 @@ def run_c5(args, torch, dist, rank, world, local_rank):
 
 # --------------------------------------------------------------- main ---
 DIST_BACKEND = [None]  # the process group the per-rank records went through
+# The second HIP stream of the C3 / C5 steps. A HIP stream is bound to one of
+# the process's GPU_MAX_HW_QUEUES (4) hardware queues at its FIRST dispatch,
+# and RCCL's communicator init dispatches on its own streams. When the
+# launch stream and the side stream were first used after that, both landed
+# on the same hardware queue (kernel trace: null stream and side stream on
+# queue 4, RCCL's streams on 2 and 4; without the group queues 1 and 2) and
+# the C5 job's two streams ran back to back: 0.69 vs 0.47 ms per job
+# (profiles/r06_c5_queue_trace.log). main() therefore dispatches once on both
+# streams BEFORE the process group exists (--early-streams 1).
+SIDE = {}
+
+
+def side_stream(torch, dev, priority=0):
+    key = (dev.index, priority)
+    if key not in SIDE:
+        SIDE[key] = torch.cuda.Stream(dev, priority=priority)
+    return SIDE[key]
 
 
 PERF_FLOOR_PATH = os.path.join(ROOT, "tests", "golden", "perf_floor.json")
@@ -1372,6 +1389,10 @@ def main():
                     help="process group: auto (default) RCCL ('nccl') at every world size, "
                          "so the N=1 line takes the N>1 collective path too (gloo when "
                          "ranks share a device); nccl the same; none only at N=1: no group")
+    ap.add_argument("--early-streams", type=int, default=1, choices=[0, 1],
+                    help="first dispatch on the launch and side streams before the process "
+                         "group (1, default: their own hardware queues) or when first used "
+                         "(0: after RCCL's streams; A/B)")
     ap.add_argument("--launch-check", action="store_true",
                     help="only join the process group and print the rank map (no GPU)")
     args = ap.parse_args()
@@ -1410,6 +1431,14 @@ def main():
         print(f"bench.py: rank {rank} needs GPU {local_rank}, {ndev} visible", file=sys.stderr)
         raise SystemExit(2)
     torch.cuda.set_device(local_rank)
+    if args.early_streams:
+        # the launch stream and the side stream take their hardware queues
+        # (first dispatch) before RCCL's streams exist (see SIDE)
+        d0 = torch.device("cuda", local_rank)
+        for st in (torch.cuda.current_stream(d0), side_stream(torch, d0)):
+            with torch.cuda.stream(st):
+                torch.zeros(1, device=d0)
+        torch.cuda.synchronize(d0)
     dist = None
     if world > 1 and args.dist == "none":
         print("bench.py: --dist none needs a single rank", file=sys.stderr)

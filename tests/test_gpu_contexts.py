@@ -113,9 +113,10 @@ def _fabric_job(product, capi, torch, dev):
                                  oo["mask"].data_ptr(), None)
 
     def run(lib, ctx, stream):
-        for oo in o:
-            for v in oo.values():
-                v.zero_()
+        with torch.cuda.stream(stream):  # ordered before the launch on `stream`
+            for oo in o:
+                for v in oo.values():
+                    v.zero_()
         if ctx is None:
             rc = lib.ogs_spf_routes_groups(ctypes.byref(g), ctypes.byref(pt), arr, 2, h["flags"],
                                            ctypes.c_void_p(stream.cuda_stream))
@@ -207,9 +208,10 @@ def _c3_shard_job(product, capi, torch, dev, rank=0, world=8):
     L0 = launches[0]
 
     def run(lib, ctx, stream):
-        for L in launches:
-            for k in ("meta", "metric", "mask"):
-                L["o"][k].zero_()
+        with torch.cuda.stream(stream):  # ordered before the launch on `stream`
+            for L in launches:
+                for k in ("meta", "metric", "mask"):
+                    L["o"][k].zero_()
         rc = lib.ogs_ctx_spf_routes_groups(ctx, ctypes.byref(L0["g"]), ctypes.byref(L0["pt"]),
                                            arr, len(launches), L0["flags"],
                                            ctypes.c_void_p(stream.cuda_stream))
@@ -246,16 +248,20 @@ def test_two_threads_default_lds_form(product, oracle):
     fab_names = fsw + rest
     fab_want = list(oracle.gen_route_digests("fabric", FABRIC, fab_names, True, False, False, 8))
     _, o_b, specs = keep_b
-    br_b = product.BatchRunner(True, False, False)
-    br_b.add_generated("fabric", FABRIC, fab_names)
+    # one digest runner per width group (records_digests takes the runner's
+    # own next-hop width): FSWs (W = 2), then SSW / RSW (W = 1)
+    runners = []
+    for grp, (u, W) in zip((fsw, rest), specs):
+        r = product.BatchRunner(True, False, False)
+        r.add_generated("fabric", FABRIC, grp)
+        assert r.nh_words() == W
+        runners.append(r)
+
     def fab_digests(got):
-        out, row = [], 0
-        for g, (u, W) in zip(got, specs):
-            U = len(u) // 2
-            out += list(br_b.records_digests([], g["meta"].numpy(), g["metric"].numpy(),
-                                             g["mask"].numpy(), W, 4,
-                                             list(range(row, row + U))))
-            row += U
+        out = []
+        for g, (u, W), r in zip(got, specs, runners):
+            out += list(r.records_digests([], g["meta"].numpy(), g["metric"].numpy(),
+                                          g["mask"].numpy(), W, 4))
         return out
 
     ctx_a, ctx_b = ctypes.c_void_p(), ctypes.c_void_p()

@@ -10,6 +10,7 @@
 #   bench[:<args>]            python bench.py <args> (commas -> spaces)
 #   prof                      kernel trace + stats of the default bench (no cpu baseline)
 #   pmc                       round PMC passes (tools/gpu_round_pmc.sh), OGS_COMMIT=<sha>
+#   c2scale[:<args>]          C2 kernel time vs batch size in one process (tools/c2_scaling.py)
 #   sq:<tag>:<bench args>     one SQ counter pass (wave-cycle split, LDS conflicts) over
 #                             `python3 bench.py <bench args>` (commas -> spaces)
 #   sqlds:<tag>:<bench args>  second SQ pass: LDS instruction / wait counters
@@ -22,6 +23,8 @@
 #                             bench flags --name=value written name=value with a
 #                             leading '-' (e.g. -c5-streams=2), or lib=base
 #                             (openr_amd/lib/libopenr_gpu_base.so, tools/build_ab_base.sh)
+#                             or tree=<dir> (another built tree's bench.py, e.g. ab/r04:
+#                             a git worktree of an older commit, built, copied in)
 #                             or an OGS_* environment variable (OGS_SLOT_BANKS=0)
 set -o pipefail
 mkdir -p gpurun_out
@@ -89,22 +92,25 @@ for recipe in "$@"; do
       for rep in 1 2; do
         vi=0
         for v in "${parts[@]:1}"; do
-          vi=$((vi + 1)); args=(); lib=""; envs=()
+          vi=$((vi + 1)); args=(); lib=""; envs=(); tree=.
           for kv in ${v//+/ }; do
             case $kv in
               lib=base) lib=openr_amd/lib/libopenr_gpu_base.so ;;
+              tree=*) tree=${kv#tree=} ;;
               OGS_*=*) envs+=("$kv") ;;
               -*) args+=("-${kv%%=*}" "${kv#*=}") ;;
               *) args+=(--opt "$kv") ;;
             esac
           done
           log="gpurun_out/benchab_${n}_${cfg}_${vi}_$rep.log"
-          env "${envs[@]}" OGS_LIB=$lib timeout -k 10 300 python3 bench.py --config "$cfg" --steps 10 --warmup 2 \
+          env "${envs[@]}" OGS_LIB=$lib timeout -k 10 300 python3 "$tree/bench.py" --config "$cfg" --steps 10 --warmup 2 \
             --no-cpu-baseline "${args[@]}" > "$log" 2>&1
           rc=$?; [ $rc -eq 0 ] || { tail -5 "$log"; exit $rc; }
           echo "$cfg [$v] rep $rep: $(grep '^{' "$log" | tail -1 | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["unit"], d["ms_per_step"], "ms", {k: v for k, v in d.items() if k.endswith("digest") or k == "golden"})')"
         done
       done ;;
+    c2scale)
+      step "c2scale_$n" 300 python -u tools/c2_scaling.py ${rest//,/ } ;;
     *)
       echo "unknown recipe $recipe"; exit 2 ;;
   esac
