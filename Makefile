@@ -30,9 +30,12 @@ $(CCONS): tests/c_consumer/spf_square.c include/openr_gpu.h $(LIB)
 # one object per kernel translation unit (parallel make), then one link
 KOBJ := $(patsubst openr_amd/csrc/kernels/%.hip,build/kernels/%.o,$(KERNELS))
 
+# each object leaves its kernels' resource report (VGPRs, scratch, occupancy)
+# in build/kernels/<tu>.ru; tools/kernel_resources.py lists the spills
 build/kernels/%.o: openr_amd/csrc/kernels/%.hip $(KERNEL_H) include/openr_gpu.h
 	@mkdir -p build/kernels
-	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Iinclude -c $< -o $@
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Iinclude -c $< -o $@ \
+	  -Rpass-analysis=kernel-resource-usage 2> $@.ru || { cat $@.ru; rm -f $@; false; }
 
 $(LIB): $(KOBJ)
 	@mkdir -p openr_amd/lib

@@ -1050,7 +1050,14 @@ struct LdsSchedule {
   uint32_t lead, Uw;   // slot -> unit: lead narrow units before the Uw wide
 };
 
-template <typename KeyT>
+// WMAX: the widest next-hop width the launch's groups use (3 or 4). The
+// kernel runs at 1024 threads per workgroup, so every wave has 128 VGPRs;
+// with the W = 4 SPF / stream paths compiled in, the kernel spilled 44 B per
+// lane to scratch (and 60 B at 8f3cd6b), which cost the whole-node C3 build
+// 1.134 vs 1.088 ms and 62 MB of scratch reads per build
+// (profiles/r06_c3_bisect.log); a launch whose groups are at most 3 words
+// wide takes the WMAX = 3 form, which has no W = 4 path and no spills.
+template <typename KeyT, int WMAX>
 __global__ __launch_bounds__(kLdsBlock) void spf_lds_route_kernel(
     ogs_graph g, ogs_prefix_table pt, const KeyT* __restrict__ key, LdsImage L,
     const uint8_t* __restrict__ img, const uint4* __restrict__ mm, uint32_t nEB,
@@ -1141,7 +1148,11 @@ __global__ __launch_bounds__(kLdsBlock) void spf_lds_route_kernel(
         case 1: spf_lds_unit<1>(g, L, img, mm, nEB, unit, u, flags, grp.dist, grp.nh, smem, qCount, wg, dg); break;
         case 2: spf_lds_unit<2>(g, L, img, mm, nEB, unit, u, flags, grp.dist, grp.nh, smem, qCount, wg, dg); break;
         case 3: spf_lds_unit<3>(g, L, img, mm, nEB, unit, u, flags, grp.dist, grp.nh, smem, qCount, wg, dg); break;
-        default: spf_lds_unit<4>(g, L, img, mm, nEB, unit, u, flags, grp.dist, grp.nh, smem, qCount, wg, dg); break;
+        default:
+          if constexpr (WMAX >= 4) {
+            spf_lds_unit<4>(g, L, img, mm, nEB, unit, u, flags, grp.dist, grp.nh, smem, qCount, wg, dg);
+          }
+          break;
       }
       // publish: every wave's row stores drained, barrier, release, flag
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1171,7 +1182,9 @@ __global__ __launch_bounds__(kLdsBlock) void spf_lds_route_kernel(
       case 1: lds_stream_item<1, KeyT>(g, pt, key, grp, u, part, parts, flags, rec0); break;
       case 2: lds_stream_item<2, KeyT>(g, pt, key, grp, u, part, parts, flags, rec0); break;
       case 3: lds_stream_item<3, KeyT>(g, pt, key, grp, u, part, parts, flags, rec0); break;
-      default: lds_stream_item<4, KeyT>(g, pt, key, grp, u, part, parts, flags, rec0); break;
+      default:
+        if constexpr (WMAX >= 4) lds_stream_item<4, KeyT>(g, pt, key, grp, u, part, parts, flags, rec0);
+        break;
     }
     OGS_ITEM_STAMP(2u, gu, tItem, tReady);
   }
@@ -1366,8 +1379,13 @@ hipError_t launch_spf_lds_routes(const ogs_graph& g, const ogs_prefix_table& pt,
                        static_cast<const uint8_t*>(base), mm, S.nEB, G, flags, ctr, ready, sch);
     return hipGetLastError();
   };
-  return key16 ? go(spf_lds_route_kernel<uint16_t>, static_cast<const uint16_t*>(key))
-               : go(spf_lds_route_kernel<uint32_t>, static_cast<const uint32_t*>(key));
+  // the widest group picks the form (WMAX 3: no W = 4 path, no spills)
+  if (Wmax <= 3) {
+    return key16 ? go(spf_lds_route_kernel<uint16_t, 3>, static_cast<const uint16_t*>(key))
+                 : go(spf_lds_route_kernel<uint32_t, 3>, static_cast<const uint32_t*>(key));
+  }
+  return key16 ? go(spf_lds_route_kernel<uint16_t, 4>, static_cast<const uint16_t*>(key))
+               : go(spf_lds_route_kernel<uint32_t, 4>, static_cast<const uint32_t*>(key));
 }
 
 }  // namespace ogs
