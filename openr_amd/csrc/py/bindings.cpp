@@ -1828,49 +1828,56 @@ PYBIND11_MODULE(_decision, m) {
           std::vector<double> cold, warm;
           size_t routes = 0;
           uint64_t dCold = 0, dWarm = 0;  // route_digest.h unit(me, db)
-          // the drop-in's split timers (decision.gpu.*_ms) summed over the
-          // timed cold builds and over the warm ones, separately
+          // the drop-in's split timers (decision.gpu.*_ms) of EACH timed
+          // build (counter deltas around it), so a caller can report the
+          // split of the same rep as its total
           const char* kSplit[3] = {"decision.gpu.prepare_ms.sum", "decision.gpu.launch_ms.sum",
                                    "decision.gpu.materialize_ms.sum"};
-          auto sums = [&](std::array<double, 3>& acc, double sign) {
+          auto snap = [&]() {
+            std::array<double, 3> a{};
             const auto c = getDecisionCounters();
             for (int i = 0; i < 3; ++i) {
               auto it = c.find(kSplit[i]);
-              acc[i] += sign * (it == c.end() ? 0.0 : it->second);
+              a[i] = it == c.end() ? 0.0 : it->second;
             }
+            return a;
           };
-          std::array<double, 3> splitCold{}, splitWarm{};
+          auto delta = [](const std::array<double, 3>& a, const std::array<double, 3>& b) {
+            return std::array<double, 3>{b[0] - a[0], b[1] - a[1], b[2] - a[2]};
+          };
+          std::vector<std::array<double, 3>> splitCold, splitWarm;
           for (int r = 0; r < reps + 1; ++r) {
             AreaLinkStates als;
             auto& ls = als.emplace(g.area, LinkState(g.area, "test_node")).first->second;
             PrefixState ps;
             loadLsdb(g, ls, ps);
             SpfSolver solver("test_node", true, false, false);
-            if (r) sums(splitCold, -1.0);
+            const auto c0 = snap();
             auto t0 = std::chrono::steady_clock::now();
             auto db = solver.buildRouteDb(me, als, ps);
             const double us = std::chrono::duration<double, std::micro>(
                                   std::chrono::steady_clock::now() - t0).count();
-            if (r) sums(splitCold, 1.0);
+            const auto c1 = snap();
             if (!db) throw std::runtime_error("no RouteDb for " + me);
             routes = db->unicastRoutes.size();
-            if (r) cold.push_back(us);  // rep 0 warms code objects / workspace
+            if (r) {  // rep 0 warms code objects / workspace
+              cold.push_back(us);
+              splitCold.push_back(delta(c0, c1));
+            }
             if (r == reps) {
               dCold = digest::unit(me, *db);
-              sums(splitWarm, -1.0);
               for (int k = 0; k < reps; ++k) {
                 db.reset();  // the previous result is released untimed, as before a cold build
+                const auto w0 = snap();
                 t0 = std::chrono::steady_clock::now();
                 db = solver.buildRouteDb(me, als, ps);
                 warm.push_back(std::chrono::duration<double, std::micro>(
                                    std::chrono::steady_clock::now() - t0).count());
+                splitWarm.push_back(delta(w0, snap()));
               }
-              sums(splitWarm, 1.0);
               dWarm = digest::unit(me, *db);
             }
           }
-          for (auto& x : splitCold) x /= std::max(reps, 1);
-          for (auto& x : splitWarm) x /= std::max(reps, 1);
           return std::make_tuple(cold, warm, routes, dCold, dWarm, splitCold, splitWarm);
         },
         py::arg("kind"), py::arg("opts"), py::arg("me"), py::arg("reps"));

@@ -73,6 +73,7 @@ for recipe in "$@"; do
       C=$SQ1; [ "$kind" = sqlds ] && C=$SQ2
       # a counter pass that cannot be collected may hang past SIGTERM: KILL
       echo "=== ${kind}_$tag"
+      mkdir -p "gpurun_out/${kind}_$tag" && echo "$COMMIT" > "gpurun_out/${kind}_$tag/commit.txt"
       timeout -s KILL 150 rocprofv3 --pmc $C --output-format csv -d "gpurun_out/${kind}_$tag" -o sq -- python3 bench.py ${args//,/ } > "gpurun_out/${kind}_$tag.log" 2>&1
       rc=$?; echo "=== ${kind}_$tag rc=$rc"; tail -3 "gpurun_out/${kind}_$tag.log" | cut -c1-300
       [ $rc -eq 0 ] || exit $rc ;;
