@@ -275,8 +275,9 @@ def run_g1(args, rank):
     out["roofline"] = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                        "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                        "traffic": None, "bytes_alg_per_unit": round(bpu, 1),
-                       "kernel": "spf_global*_kernel + route_global_kernel (one launch; "
-                                 "latency bound: frontier rounds of one workgroup per unit)"}
+                       "kernel": "spf_global_lds3_kernel with the route pass fused in (one "
+                                 "launch; latency bound: frontier rounds of one workgroup per "
+                                 "unit)"}
     set_traffic(out, "g1", ("spf_global", "route_global_kernel"))
     # Decision's own call on this area: ONE buildRouteDb(myNode) through the
     # drop-in (Decision.cpp:912-913 -> SpfSolver.cpp:313-453), cold (fresh

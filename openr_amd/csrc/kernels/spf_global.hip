@@ -754,9 +754,16 @@ __global__ __launch_bounds__(kGBlock) void spf_global_lds2_kernel(
 // rounds); the least fixpoint is the same (spf_core.h).
 uint32_t global_lds3_bytes(uint32_t Sn) { return Sn * 8u + 4u * ((Sn + 31u) / 32u); }
 
+// With a prefix table (pt.max_prefixes > 0) the unit's RouteDb is written by
+// the same workgroup after its last round (route_one against the packed LDS
+// words, one thread per prefix, coalesced record stores), as
+// route_global_kernel would from the HBM rows: the launch no longer reads
+// its own dist / next-hop rows back (G1: 64 x 20k x 8 B of the 44 MB the PMC
+// counted per launch pair, profiles/r05_pmc_g1.json).
 __global__ __launch_bounds__(kGBlock) void spf_global_lds3_kernel(
     ogs_graph g, const ogs_unit* __restrict__ units, uint32_t flags,
-    uint32_t* __restrict__ oDist, uint32_t* __restrict__ oNh, uint32_t* __restrict__ scratch) {
+    uint32_t* __restrict__ oDist, uint32_t* __restrict__ oNh, uint32_t* __restrict__ scratch,
+    ogs_prefix_table pt, ogs_spf_out out) {
   constexpr uint32_t kInf = 0xFFFFFFFFu;
   const int tid = threadIdx.x;
   const uint32_t u0 = blockIdx.x;
@@ -854,6 +861,24 @@ __global__ __launch_bounds__(kGBlock) void spf_global_lds3_kernel(
     oD[v] = static_cast<uint32_t>(x);
     oN[v] = static_cast<uint32_t>(x >> 32);
   }
+  // ---- the unit's RouteDb from the final LDS words (every thread left the
+  // last round through its barrier: dn is final) --------------------------
+  const uint32_t Sp = uint32_t(pt.max_prefixes);
+  if (Sp == 0u) return;
+  const uint32_t p0 = pt.pfx_base[unit.topo];
+  const uint32_t P = pt.pfx_base[unit.topo + 1] - p0;
+  const RouteCfg cfg{(flags & OGS_F_ENABLE_V4) != 0, (flags & OGS_F_V4_OVER_V6) != 0,
+                     (flags & OGS_F_BEST_ROUTE_SELECTION) != 0};
+  const PackedView sv{dn};
+  for (uint32_t p = tid; p < Sp; p += kGBlock) {
+    const size_t rec = size_t(u0) * Sp + p;
+    uint32_t meta = 0, metric = kInf, selBits = 0, mask[1] = {0u};
+    if (p < P) route_one<uint32_t, 1>(pt, p0 + p, s, nflags, sv, cfg, meta, metric, mask, selBits);
+    if (out.meta) out.meta[rec] = meta;
+    if (out.metric) static_cast<uint32_t*>(out.metric)[rec] = metric;
+    if (out.sel) out.sel[rec] = selBits;
+    if (out.mask) out.mask[rec] = mask[0];
+  }
 }
 
 hipError_t workspace(size_t bytes, hipStream_t stream, void** out);
@@ -920,11 +945,11 @@ hipError_t launch_global_w(const ogs_graph& g, const ogs_prefix_table* pt,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, int(lds3));
         if (e != hipSuccess) return e;
       }
+      // the route pass runs inside the launch (no separate route kernel)
+      const ogs_prefix_table ptv = pt ? *pt : ogs_prefix_table{};
       hipLaunchKernelGGL(k, dim3(nUnits), dim3(kGBlock), lds3, stream, g, units, flags,
-                         reinterpret_cast<uint32_t*>(dist), nh, scratch);
-      e = hipGetLastError();
-      if (e != hipSuccess || !pt || pt->max_prefixes == 0) return e;
-      return launch_route_global<D, W>(g, *pt, units, nUnits, flags, dist, nh, out, stream);
+                         reinterpret_cast<uint32_t*>(dist), nh, scratch, ptv, out);
+      return hipGetLastError();
     }
   }
   if ((opts().spfGlobalLds == 1 || opts().spfGlobalLds == 3) && opts().spfGlobalSync && lds2 <= 160u * 1024u) {
