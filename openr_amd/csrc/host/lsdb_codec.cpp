@@ -724,11 +724,16 @@ AdjacencyDatabase readAdjacencyDatabase(std::string_view bytes) {  // Types.thri
 
 namespace {
 // networks: every entry's toIPNetwork text; first: the first entry's only
-PrefixDatabase readPrefixDb(std::string_view bytes, std::vector<std::string>* networks,
-                            std::string* first) {  // Types.thrift:415-430
+// into `db`, reusing its entry vector's storage (the ingestion loop decodes
+// every key into one scratch database: no vector allocation per key)
+void readPrefixDbInto(PrefixDatabase& db, std::string_view bytes,
+                      std::vector<std::string>* networks, std::string* first) {
   Reader r(bytes);
   if (networks) networks->clear();
-  PrefixDatabase db;
+  db.thisNodeName.clear();
+  db.prefixEntries.clear();
+  db.perfEvents.reset();
+  db.deletePrefix = false;
   int16_t last = 0, id;
   uint8_t t;
   while (r.field(last, id, t)) {
@@ -766,6 +771,12 @@ PrefixDatabase readPrefixDb(std::string_view bytes, std::vector<std::string>* ne
     }
     r.skip(t, 0);
   }
+}
+
+PrefixDatabase readPrefixDb(std::string_view bytes, std::vector<std::string>* networks,
+                            std::string* first) {  // Types.thrift:415-430
+  PrefixDatabase db;
+  readPrefixDbInto(db, bytes, networks, first);
   return db;
 }
 }  // namespace
@@ -866,22 +877,30 @@ std::string getNodeNameFromKey(const std::string& key) {  // LsdbUtil.cpp:691-69
 LsdbIngest::Decoded LsdbIngest::decodeKey(const std::string& key,
                                           const std::optional<std::string_view>& rawVal) {
   Decoded d;
-  if (!rawVal) return d;  // TTL update (Decision.cpp:716-720)
+  decodeKeyInto(d, key, rawVal);
+  return d;
+}
+
+void LsdbIngest::decodeKeyInto(Decoded& d, const std::string& key,
+                               const std::optional<std::string_view>& rawVal) {
+  d.kind = Decoded::kNone;
+  d.network.clear();
+  d.error.clear();
+  if (!rawVal) return;  // TTL update (Decision.cpp:716-720)
   try {
     if (key.compare(0, 4, "adj:") == 0) {
       d.adj = readAdjacencyDatabase(*rawVal);
       d.kind = Decoded::kAdj;
-      return d;
+      return;
     }
     if (key.compare(0, 7, "prefix:") == 0) {
-      d.prefix = readPrefixDb(*rawVal, nullptr, &d.network);  // the first entry's network
+      readPrefixDbInto(d.prefix, *rawVal, nullptr, &d.network);  // the first entry's network
       d.kind = Decoded::kPrefix;
     }
   } catch (const std::exception& e) {  // Decision.cpp:781-784: log, drop the key
     d.kind = Decoded::kError;
     d.error = "Failed to deserialize info for key " + key + ". Exception: " + e.what();
   }
-  return d;
 }
 
 LsdbKeyUpdate LsdbIngest::applyDecoded(const std::string& area, LinkState& areaLinkState,
@@ -957,7 +976,12 @@ LsdbKeyUpdate LsdbIngest::updateKeyInLsdb(const std::string& area, LinkState& ar
                                           PrefixState& prefixState, const std::string& key,
                                           const std::optional<std::string_view>& rawVal,
                                           bool inInitialization) const {
-  return applyDecoded(area, areaLinkState, prefixState, key, decodeKey(key, rawVal),
+  // one decode scratch per ingesting thread: its containers keep their
+  // storage from key to key (applyDecoded moves the entry and the network
+  // out; decodeKeyInto resets every field it reads)
+  thread_local Decoded scratch;
+  decodeKeyInto(scratch, key, rawVal);
+  return applyDecoded(area, areaLinkState, prefixState, key, std::move(scratch),
                       inInitialization);
 }
 
@@ -1030,12 +1054,14 @@ void LsdbIngest::processPublication(const std::string& area, AreaLinkStates& are
   auto take = [&](LsdbKeyUpdate&& u) {
     if (u.kind != LsdbKeyUpdate::kPrefix) pending.apply(u);
   };
+  Decoded scratch;  // reused key to key (decodeKeyInto)
   for (size_t i = 0; i < ordered.size(); ++i) {
     if (i + 1 < ordered.size() && ordered[i + 1]->key == ordered[i]->key) continue;
     const PublicationKeyVal* kv = ordered[i];
     std::optional<std::string_view> v;
     if (kv->value) v = *kv->value;
-    take(applyDecoded(area, ls, prefixState, kv->key, decodeKey(kv->key, v), inInitialization,
+    decodeKeyInto(scratch, kv->key, v);
+    take(applyDecoded(area, ls, prefixState, kv->key, std::move(scratch), inInitialization,
                       &pending));
   }
   for (const auto& key : expiredKeys) pending.apply(deleteKeyFromLsdb(area, ls, prefixState, key));

@@ -79,6 +79,28 @@ std::optional<int64_t> getDurationBetweenPerfEvents(const PerfEvents& events,
 // between the first and second ':' of "adj:<node>" / "prefix:<node>:<...>".
 std::string getNodeNameFromKey(const std::string& key);
 
+// The changed networks of one key: 0 or 1 (a prefix key names one entry,
+// Decision.cpp:750-756), held inline -- a contiguous range of at most one
+// string, so a key's update allocates no container (f4 ingestion).
+class ChangedNetworks {
+ public:
+  using const_iterator = const std::string*;
+  void push_back(std::string s) {
+    if (n_) throw std::logic_error("ChangedNetworks: one network per prefix key");
+    one_ = std::move(s);
+    n_ = 1;
+  }
+  const_iterator begin() const { return &one_; }
+  const_iterator end() const { return &one_ + n_; }
+  size_t size() const { return n_; }
+  bool empty() const { return n_ == 0; }
+  const std::string& operator[](size_t i) const { return (&one_)[i]; }
+
+ private:
+  std::string one_;
+  size_t n_{0};
+};
+
 // Outcome of one key, mirroring what Decision::updateKeyInLsdb feeds into
 // pendingUpdates_ (applyLinkStateChange / applyPrefixStateChange).
 struct LsdbKeyUpdate {
@@ -92,7 +114,7 @@ struct LsdbKeyUpdate {
   Kind kind{kSkipped};
   std::string nodeName;
   LinkState::LinkStateChange linkChange;
-  std::vector<std::string> changedPrefixes;  // 0 or 1 network per prefix key
+  ChangedNetworks changedPrefixes;  // 0 or 1 network per prefix key
   std::optional<PerfEvents> perfEvents;      // the database's (Decision.cpp:739, 779)
   std::string error;
 };
@@ -208,6 +230,9 @@ class LsdbIngest {
   };
   static Decoded decodeKey(const std::string& key,
                            const std::optional<std::string_view>& rawVal);
+  // the same into `d`, reusing its containers' storage (every field reset)
+  static void decodeKeyInto(Decoded& d, const std::string& key,
+                            const std::optional<std::string_view>& rawVal);
   // direct != nullptr: a prefix key's changed network is added to it
   // instead of returned in changedPrefixes (processPublication)
   LsdbKeyUpdate applyDecoded(const std::string& area, LinkState& areaLinkState,

@@ -277,7 +277,8 @@ py::dict fromKeyUpdate(const LsdbKeyUpdate& u) {
   d["nodeName"] = u.nodeName;
   d["linkChange"] = u.kind == LsdbKeyUpdate::kAdjacency ? py::object(fromChange(u.linkChange))
                                                          : py::object(py::none());
-  d["changedPrefixes"] = u.changedPrefixes;
+  d["changedPrefixes"] = std::vector<std::string>(u.changedPrefixes.begin(),
+                                                  u.changedPrefixes.end());
   d["perfEvents"] = fromPerfEvents(u.perfEvents);
   d["error"] = u.error;
   return d;

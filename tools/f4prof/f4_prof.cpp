@@ -63,8 +63,28 @@ int main(int argc, char** argv) {
       ta = ms(t0, t1);
       tq = ms(t1, t2);
     }
-    std::printf("rep %d: processPublication %.1f ms | per-key: adj %.1f ms + prefix %.1f ms = %.1f\n",
-                r, tp, ta, tq, ta + tq);
+    // the prefix keys' decode alone, then the apply of the decoded keys
+    double td, tapp;
+    {
+      LinkState ls(g.area, "test_node");
+      PrefixState ps;
+      LsdbIngest ing("test_node", {g.area});
+      std::vector<LsdbIngest::Decoded> dec;
+      dec.reserve(keys.size() - nAdj);
+      auto t0 = std::chrono::steady_clock::now();
+      for (size_t i = nAdj; i < keys.size(); ++i) {
+        dec.push_back(LsdbIngest::decodeKey(keys[i], std::string_view(vals[i])));
+      }
+      auto t1 = std::chrono::steady_clock::now();
+      for (size_t i = nAdj; i < keys.size(); ++i) {
+        ing.applyDecoded(g.area, ls, ps, keys[i], std::move(dec[i - nAdj]));
+      }
+      auto t2 = std::chrono::steady_clock::now();
+      td = ms(t0, t1);
+      tapp = ms(t1, t2);
+    }
+    std::printf("rep %d: processPublication %.1f ms | per-key: adj %.1f ms + prefix %.1f ms = %.1f"
+                " | prefix decode %.1f + apply %.1f\n", r, tp, ta, tq, ta + tq, td, tapp);
   }
   return 0;
 }
