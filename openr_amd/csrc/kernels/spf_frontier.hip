@@ -1379,8 +1379,13 @@ __global__ __launch_bounds__(kBlock) void spf_variant_repair_kernel(
   if (tid < 2) cnt[tid] = 0u;
   __syncthreads();
   // ---- seeds: heads of the failed edges that are tight in the base --------
-  if (tid < kMaxDead && dead.e[tid] != OGS_NODE_NONE) {
-    const uint32_t e = dead.e[tid];
+  // (the seed's edge straight from the list: indexing `dead` by tid would put
+  // the array in scratch memory, and every edge test of the rounds with it)
+  const uint32_t seedEdge = (tid < kMaxDead && tid < mods.dead_per_unit)
+      ? mods.dead_edges[size_t(u0) * mods.dead_per_unit + tid]
+      : OGS_NODE_NONE;
+  if (seedEdge != OGS_NODE_NONE) {
+    const uint32_t e = seedEdge;
     const uint32_t u = g.edge_src[e0 + e];
     const uint64_t x = edges[e];
     const uint32_t lo = static_cast<uint32_t>(x);
