@@ -317,6 +317,11 @@ static int set_option(ogs::EngineOptions& o, const char* name, int64_t value) {
     o.waveUpb = int(value);
     return OGS_OK;
   }
+  if (std::strcmp(name, "ksp_prune") == 0) {
+    if (value != 0 && value != 1) return fail(OGS_E_INVALID, "ksp_prune must be 0 or 1");
+    o.kspPrune = int(value);
+    return OGS_OK;
+  }
   if (std::strcmp(name, "ksp_wave_trace") == 0) {
     if (value != 0 && value != 1) return fail(OGS_E_INVALID, "ksp_wave_trace must be 0 or 1");
     o.kspWaveTrace = int(value);

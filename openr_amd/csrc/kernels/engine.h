@@ -24,6 +24,7 @@ struct EngineOptions {
   int kspHbm = 0;
   int kspQueue = 1;
   int kspStage = -1;
+  int kspPrune = 1;
   int routeStream = 5;
   int routeStoreNt = 2;
   int spfLaneWalk = -1;

@@ -205,14 +205,15 @@ __device__ uint32_t trace_paths_wave(const UnitCsr& csr, const uint32_t* dist, u
         lastKey = pack(dist[edge_dst(llo)], edge_dst(llo), csr_rslot(csr, f.edge, llo));
       }
       uint64_t best = kNone;
-      uint32_t be = 0xFFFFFFFFu;
+      uint32_t be = 0xFFFFFFFFu, blo = 0u;
       const uint32_t rEnd = csr.rowp[v + 1];
       for (uint32_t eb = csr.rowp[v]; eb < rEnd; eb += 64) {
         const uint32_t e = eb + uint32_t(lane);
         uint64_t key = kNone;
+        uint32_t lo = 0u;
         if (e < rEnd) {
           const uint64_t ed = csr.edg[e];
-          const uint32_t lo = static_cast<uint32_t>(ed);
+          lo = static_cast<uint32_t>(ed);
           const uint32_t u = edge_dst(lo);
           bool ok = !(lo & OGS_EDGE_DOWN) && !((lo & OGS_EDGE_DST_OVERLOADED) && u != s);
           if constexpr (MASKED) {
@@ -229,20 +230,35 @@ __device__ uint32_t trace_paths_wave(const UnitCsr& csr, const uint32_t* dist, u
             }
           }
         }
-        const uint64_t m = wave_min_u64(key);
+        // the window's best candidate: with one candidate lane (a unique
+        // tight predecessor, the common case) its key directly, else the
+        // wave-wide min; the winner's edge word comes back through
+        // v_readlane (uniform lane), not a reload of the CSR
+        const uint64_t cand = __ballot(key != kNone);
+        if (cand == 0ull) continue;  // uniform
+        int wl;
+        uint64_t m;
+        if ((cand & (cand - 1ull)) == 0ull) {
+          wl = int(__builtin_ctzll(cand));
+          m = (uint64_t(uint32_t(__builtin_amdgcn_readlane(int(key >> 32), wl))) << 32) |
+              uint32_t(__builtin_amdgcn_readlane(int(uint32_t(key)), wl));
+        } else {
+          m = wave_min_u64(key);
+          wl = int(__builtin_ctzll(__ballot(key == m)));
+        }
         if (m < best) {
-          const uint64_t who = __ballot(key == m);
           best = m;
-          be = __shfl(e, int(__builtin_ctzll(who)));
+          be = uint32_t(__builtin_amdgcn_readlane(int(e), wl));
+          blo = uint32_t(__builtin_amdgcn_readlane(int(lo), wl));
         }
       }
       if (best == kNone) {  // exhausted: this recursion level fails
         --sp;
         continue;
       }
-      const uint32_t bu = edge_dst(static_cast<uint32_t>(csr.edg[be]));  // the chosen pred
+      const uint32_t bu = edge_dst(blo);  // the chosen pred
       if (lane == 0) stack[sp].edge = be;  // resume key (+ path edge on success)
-      const uint32_t l = link_id(csr, be, static_cast<uint32_t>(csr.edg[be]));
+      const uint32_t l = link_id(csr, be, blo);
       const bool seen = (visited[l >> 5] >> (l & 31u)) & 1u;
       lane_sync();
       if (seen) continue;  // already used
@@ -961,11 +977,23 @@ hipError_t launch_ksp(const ogs_graph& g, const ogs_path_unit* units,
 // queue_spf, workgroup units only): round r walks the nodes changed in round
 // r - 1 and pushes dist + w over their usable, unmasked links; one barrier
 // per round. Same least fixpoint as spf_fixpoint (spf_core.h).
+//
+// prune (the masked rerun of ksp2_kernel: the k = 2 trace of destination
+// `prune` only reads distances below dist(prune)): a push whose candidate is
+// not below the current dist(prune) is dropped. Link metrics are >= 1 on
+// this path (zero / negative metrics take the exact-order HBM form), so a
+// node u with d(u) >= d(t) is never a predecessor on a shortest path to t
+// (d(u) + w > d(t) >= d(v) for every v the trace visits), and every node
+// with d(u) < d(t) keeps its exact distance: each relaxation along its
+// shortest path has a candidate < d(t) <= dist(prune) at all times. Nodes at
+// or past d(t) may keep larger (or no) distances; the trace's tight test
+// rejects them either way. OGS_NODE_NONE: no pruning (the base SPF).
 template <typename D, bool MASKED>
 __device__ void queue_dist(uint32_t N, uint32_t s, const UnitCsr& c,
                            const uint8_t* __restrict__ nflags, D* dist,
                            uint32_t* stamp, uint16_t* q0, uint16_t* q1,
-                           uint32_t* qcnt, const uint32_t* ignore) {
+                           uint32_t* qcnt, const uint32_t* ignore,
+                           uint32_t prune = OGS_NODE_NONE) {
   constexpr D kInf = DistInf<D>::value;
   const int tid = threadIdx.x;
   for (uint32_t v = tid; v < N; v += kBlock) {
@@ -988,6 +1016,8 @@ __device__ void queue_dist(uint32_t N, uint32_t s, const UnitCsr& c,
       const uint32_t v = cur[i];
       if (v != s && (nflags[v] & OGS_NODE_OVERLOADED)) continue;
       const D dv = dist[v];
+      const D ub = prune != OGS_NODE_NONE ? dist[prune] : kInf;
+      if (dv >= ub) continue;  // every push of v would be pruned
       const uint32_t rEnd = c.rowp[v + 1];
       for (uint32_t eb = c.rowp[v]; eb < rEnd; eb += 8) {
         uint64_t xs[8];
@@ -1006,7 +1036,7 @@ __device__ void queue_dist(uint32_t N, uint32_t s, const UnitCsr& c,
           }
           const uint32_t t = edge_dst(lo);
           const D cand = dv + static_cast<D>(ed >> 32);
-          if (cand < dist[t] && cand < atomicMin(&dist[t], cand)) {
+          if (cand < ub && cand < dist[t] && cand < atomicMin(&dist[t], cand)) {
             if (atomicMax(&stamp[t], r + 1) < r + 1) {
               nxt[atomicAdd(&qcnt[(r + 1) % 3], 1u)] = uint16_t(t);
             }
@@ -1125,11 +1155,12 @@ __device__ __forceinline__ uint32_t unit_bcast(uint32_t x) {
 // The unit's SPF into l.dist: queue form (workgroup units) or the pull
 // fixpoint (spf_core.h).
 template <typename D, int UT, bool QUEUE, bool MASKED>
-__device__ __forceinline__ void ksp_spf(const KspLds<D>& l, uint32_t s, int lane) {
+__device__ __forceinline__ void ksp_spf(const KspLds<D>& l, uint32_t s, int lane,
+                                        uint32_t prune = OGS_NODE_NONE) {
   if constexpr (QUEUE) {
     static_assert(UT == kBlock, "queue form: one workgroup per unit");
     queue_dist<D, MASKED>(l.N, s, l.csr, l.nflags, l.dist, l.stamp, l.q0, l.q1,
-                          l.qcnt, l.mask);
+                          l.qcnt, l.mask, prune);
   } else {
     spf_fixpoint<D, 1, UT, false, MASKED>(l.N, s, lane, l.csr, false, l.dist,
                                           nullptr, MASKED ? l.mask : nullptr);
@@ -1184,7 +1215,8 @@ __global__ __launch_bounds__(kBlock) void ksp2_kernel(
   Scope::sync();
   const uint32_t s = unit.src, t = unit.dest;
   uint32_t c1 = 0;
-  const bool wt = sizeof(D) == 4 && waveTrace;
+  const bool prune = (waveTrace & 2) != 0;  // "ksp_prune"
+  const bool wt = sizeof(D) == 4 && (waveTrace & 1);
   if (wt && lane < 64) {
     if constexpr (sizeof(D) == 4) {
       c1 = trace_paths_wave<false>(l.csr, l.dist, s, t, l.visited, l.stack, nullptr, o1,
@@ -1205,7 +1237,8 @@ __global__ __launch_bounds__(kBlock) void ksp2_kernel(
     return;
   }
   for (uint32_t i = lane; i < l.linkWords; i += UT) l.visited[i] = 0u;
-  ksp_spf<D, UT, QUEUE, true>(l, s, lane);
+  // the masked rerun only needs the distances below d(t) ("ksp_prune")
+  ksp_spf<D, UT, QUEUE, true>(l, s, lane, prune ? t : OGS_NODE_NONE);
   if constexpr (sizeof(D) == 4) {
     if (wt) {
       if (lane >= 64) return;
@@ -1245,7 +1278,7 @@ hipError_t ksp2_launch(const ogs_graph& g, const ogs_unit* sources,
   hipLaunchKernelGGL(k2, dim3((nUnits + upb - 1) / upb), dim3(kBlock), bytes,
                      stream, g, sources, nSources,
                      static_cast<const D*>(srcDist), units, nUnits, o1, o2, lds,
-                     opts().kspWaveTrace);
+                     (opts().kspWaveTrace ? 1 : 0) | (opts().kspPrune ? 2 : 0));
   return hipGetLastError();
 }
 
@@ -1256,6 +1289,9 @@ hipError_t workspace(size_t bytes, hipStream_t stream, void** out);
 // LDS only when three units still fit a CU, else the row offsets only --;
 // 0 nothing staged, 1 row offsets, 2 rows + edges whenever they fit.
 // EngineOptions::kspQueue (engine.h), default 1
+// "ksp_prune": 1 (default) the masked rerun of the queue form drops pushes
+// at or past the destination's current distance (queue_dist); 0 full SPF
+// EngineOptions::kspPrune (engine.h), default 1
 // EngineOptions::kspStage (engine.h), default -1
 
 template <typename D>

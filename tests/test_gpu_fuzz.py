@@ -208,7 +208,8 @@ def test_link_failure_variants_feature_sweep(product, oracle, seed, desc):
                     assert vr.updated_canonical(v) == canon, f"variant {v} {links[v]}: {label}"
 
 
-KSP_PATHS = [[], [(b"ksp_hbm", 1, 0)], [(b"ksp_wave_trace", 0, 1)], [(b"ksp_queue", 0, 1)]]
+KSP_PATHS = [[], [(b"ksp_hbm", 1, 0)], [(b"ksp_wave_trace", 0, 1)], [(b"ksp_queue", 0, 1)],
+             [(b"ksp_prune", 0, 1)]]
 
 
 @pytest.mark.parametrize("seed", range(64))
@@ -217,7 +218,8 @@ def test_ksp2_feature_sweep(product, oracle, seed):
     random grids: metric sets with zeros / negatives / large values, parallel
     links (engine and oracle share the canonical link order),
     hard-drained nodes, k = 1..3 single calls and the k = 1, 2 batch, through
-    the default, HBM-state, lane-0-trace and queue KSP paths."""
+    the default, HBM-state, lane-0-trace, pull-fixpoint and unpruned (full
+    masked rerun) KSP paths."""
     import test_gpu_ksp_domains as K
     rng = random.Random(0xF05B + seed)
     n = rng.randint(2, 8)
