@@ -69,7 +69,7 @@ $(STAMPS): $(SOBJ)
 SAN := -fsanitize=address,undefined -fno-sanitize-recover=undefined -fno-omit-frame-pointer -g -O1
 ASAN_BIN := build/asan/host_asan
 ASAN_REF := build/asan/_refcpu$(EXT)
-ASAN_LOG ?= profiles/r05_asan.log
+ASAN_LOG ?= profiles/r06_asan.log
 $(ASAN_BIN): $(HOST) $(HOST_H) tests/asan/host_asan.cpp tests/asan/ogs_stub.cpp
 	@mkdir -p build/asan
 	$(CXX) -std=c++17 $(SAN) -Wall -Wno-unused-function -Iinclude -Iopenr_amd/csrc/host \
