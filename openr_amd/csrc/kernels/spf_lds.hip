@@ -986,18 +986,34 @@ __device__ __forceinline__ void lds_stream_item(const ogs_graph& g, const ogs_pr
   uint32_t* rMeta = rec0;
   uint32_t* rMetric = rMeta + Sn;
   uint32_t* rMask = rMetric + Sn;  // [W][Sn]
-  for (uint32_t v = tid; v < N; v += kLdsBlock) {
-    const uint32_t d = sv.dist(v);
-    uint32_t m[W], cnt = 0;
+  // the records of K nodes per thread per batch: every row load of the batch
+  // is issued before the first record is built (one L2 round trip per batch
+  // of K x 1024 nodes instead of one per 1024)
+  constexpr int K = 3;
+  for (uint32_t v0 = tid; v0 < N; v0 += K * kLdsBlock) {
+    uint32_t d[K], m[K][W];
+    uint8_t nf[K];
 #pragma unroll
-    for (int w = 0; w < W; ++w) {
-      m[w] = sv.nh(v, w);
-      cnt += __popc(m[w]);
+    for (int k = 0; k < K; ++k) {
+      const uint32_t v = v0 + uint32_t(k) * kLdsBlock;
+      const uint32_t vc = v < N ? v : v0;  // clamped: unconditional loads
+      d[k] = sv.dist(vc);
+      nf[k] = nflags[vc];
+#pragma unroll
+      for (int w = 0; w < W; ++w) m[k][w] = sv.nh(vc, w);
     }
-    rMeta[v] = node_route_meta(v, s, d != kInf, cnt, nflags[v]);
-    rMetric[v] = (v == s) ? kInf : d;
 #pragma unroll
-    for (int w = 0; w < W; ++w) rMask[w * Sn + v] = m[w];
+    for (int k = 0; k < K; ++k) {
+      const uint32_t v = v0 + uint32_t(k) * kLdsBlock;
+      if (v >= N) break;
+      uint32_t cnt = 0;
+#pragma unroll
+      for (int w = 0; w < W; ++w) cnt += __popc(m[k][w]);
+      rMeta[v] = node_route_meta(v, s, d[k] != kInf, cnt, nf[k]);
+      rMetric[v] = (v == s) ? kInf : d[k];
+#pragma unroll
+      for (int w = 0; w < W; ++w) rMask[w * Sn + v] = m[k][w];
+    }
   }
   __syncthreads();
   const uint32_t p0 = pt.pfx_base[t];
