@@ -981,6 +981,10 @@ __device__ __forceinline__ void lds_stream_item(const ogs_graph& g, const ogs_pr
   const uint32_t t = unit.topo, s = unit.src;
   const uint32_t nb = g.node_base[t];
   const uint32_t N = g.node_base[t + 1] - nb;
+  // the prefix range's bounds load with the node range (one round), not
+  // after the records' barrier
+  const uint32_t p0 = pt.pfx_base[t];
+  const uint32_t Pn = pt.pfx_base[t + 1] - p0;
   const uint8_t* __restrict__ nflags = g.node_flags + nb;
   const PublishedView<W> sv{grp.dist + size_t(u) * Sn, grp.nh + size_t(u) * W * Sn, Sn};
   uint32_t* rMeta = rec0;
@@ -1016,8 +1020,6 @@ __device__ __forceinline__ void lds_stream_item(const ogs_graph& g, const ogs_pr
     }
   }
   __syncthreads();
-  const uint32_t p0 = pt.pfx_base[t];
-  const uint32_t Pn = pt.pfx_base[t + 1] - p0;
   const uint32_t span = ((Pn + P - 1u) / P + 3u) & ~3u;
   const uint32_t lo = min(Pn, part * span), hi = min(Pn, lo + span);
   auto rec = [&](uint32_t v, Rec<W>& r) {
