@@ -360,10 +360,17 @@ int ogs_host_free(void* hptr);
  *   "spf_global_lds": 1 (default) global-path distances and next-hop words
  *                 in LDS where both fit, else distances only; 2 distances
  *                 only; 0 all state in HBM (A/B).
+ *   "spf_global_eimg": 1 the one-phase global kernel relaxes from a per-call
+ *                 edge image {edge, weight, target row} and queues {node,
+ *                 row} entries (no node-flag / row-offset loads per round);
+ *                 0 (default) CSR rows and node-id lists.
  *   "ksp_hbm":    1 every KSP unit on the HBM-state path (A/B, tests); 0
  *                 (default) only units past LDS and OGS_F_EXACT_ORDER units.
  *                 "ksp_wave_trace": 1 (default) path traces of 32-bit
  *                 distance units run on a whole wavefront, 0 on one lane.
+ *                 "ksp_prune": 1 (default) the KSP2 masked rerun skips and
+ *                 does not queue nodes at or past the destination's current
+ *                 distance (exact for metrics >= 1); 0 the full rerun (A/B).
  *   "c4_desc":    1 (default) the link-failure repair (OGS_F_INCREMENTAL)
  *                 seeds its affected set from precomputed descendant rows of
  *                 the base tight DAG (S_n <= 16384), 0 by growth rounds.
