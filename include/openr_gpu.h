@@ -360,10 +360,6 @@ int ogs_host_free(void* hptr);
  *   "spf_global_lds": 1 (default) global-path distances and next-hop words
  *                 in LDS where both fit, else distances only; 2 distances
  *                 only; 0 all state in HBM (A/B).
- *   "spf_global_eimg": 1 the one-phase global kernel relaxes from a per-call
- *                 edge image {edge, weight, target row} and queues {node,
- *                 row} entries (no node-flag / row-offset loads per round);
- *                 0 (default) CSR rows and node-id lists.
  *   "ksp_hbm":    1 every KSP unit on the HBM-state path (A/B, tests); 0
  *                 (default) only units past LDS and OGS_F_EXACT_ORDER units.
  *                 "ksp_wave_trace": 1 (default) path traces of 32-bit
