@@ -733,6 +733,9 @@ int ogs_routes_multiarea(const ogs_graph* graph,
   do {                                                           \
     if (!(ctx)) return fail(OGS_E_INVALID, "ctx is NULL");       \
     ogs::BoundContext bound_(&(ctx)->e);                         \
+    if (!bound_.ok()) {                                          \
+      return fail(OGS_E_HIP, "cannot switch to the ctx's device"); \
+    }                                                            \
     return (call);                                               \
   } while (0)
 

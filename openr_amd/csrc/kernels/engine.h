@@ -95,18 +95,29 @@ hipError_t workspace(size_t bytes, hipStream_t stream, void** out);
 class DeviceGuard {
  public:
   explicit DeviceGuard(int device) {
-    if (device < 0 || hipGetDevice(&prev_) != hipSuccess) return;
-    if (prev_ != device && hipSetDevice(device) == hipSuccess) set_ = true;
+    if (device < 0) return;
+    if (hipGetDevice(&prev_) != hipSuccess) {
+      ok_ = false;
+      return;
+    }
+    if (prev_ == device) return;
+    set_ = hipSetDevice(device) == hipSuccess;
+    ok_ = set_;
   }
   ~DeviceGuard() {
     if (set_) (void)hipSetDevice(prev_);
   }
+  // false when the thread could not be switched to the device: the call
+  // must not run (it would use the caller's device with the context's
+  // pointers)
+  bool ok() const { return ok_; }
   DeviceGuard(const DeviceGuard&) = delete;
   DeviceGuard& operator=(const DeviceGuard&) = delete;
 
  private:
   int prev_ = -1;
   bool set_ = false;
+  bool ok_ = true;
 };
 
 // RAII: binds `ctx` (and its device) to the calling thread for one call; the
@@ -119,6 +130,7 @@ class BoundContext {
     bind_context(ctx);
   }
   ~BoundContext() { bind_context(prev_); }
+  bool ok() const { return dev_.ok(); }
   BoundContext(const BoundContext&) = delete;
   BoundContext& operator=(const BoundContext&) = delete;
 
